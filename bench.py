@@ -1,0 +1,273 @@
+#!/usr/bin/env python3
+"""Headline benchmark: device-resident Zarr v3 chunk decode on MI355X.
+
+Workload (BASELINE.json configs[2], the single-GPU config the metric is quoted on):
+  uint32 array 1x4096x4096x1536 (96 GiB decoded), chunk (= shard) 1x1024x1024x1024,
+  codecs [sharding_indexed{chunk_shape [1,32,32,32], codecs [bytes(big)],
+          index_codecs [bytes(little), crc32c], index_location end}].
+One step = one full-array core.Array.read (M/core/Array.java:378-441) of all 32 shards /
+786,432 in-bounds inner chunks: index CRC + index parse + byte swap + scatter, inputs
+already resident in HBM.  Synthetic data v(g) = lo32(splitmix64(g ^ 0x5A5A2026)) is written
+on the device and encoded by the product's own write path (zh_array_write); after warmup
+the decoded array is verified element-by-element on the device against the generator.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--config c3|c4|c2]
+
+N>1 (launched by torch.distributed.run): every rank decodes its own full-size array on its
+own GPU (weak scaling, no data-path collective: shards are independent objects); the
+barrier and max-over-ranks timing use torch.distributed (gloo, CPU tensors).
+"""
+import argparse
+import ctypes as C
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "zarr-java_amd"))
+
+SEED = 0x5A5A2026
+GiB = 1 << 30
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+
+CONFIGS = {
+    # name: (description, sharded, transpose order)
+    "c2": ("bytes(big) only, chunk 1x1024x1024x1024", False, None),
+    "c3": ("sharding 1x32x32x32 + bytes(big), index [bytes(little), crc32c] at end", True, None),
+    "c4": ("c3 + transpose [0,3,2,1] inside the shard", True, [0, 3, 2, 1]),
+}
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def dist_env():
+    ws = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    return ws, rank, local
+
+
+class Dist:
+    """Barrier / max over ranks.  torch.distributed (gloo on CPU tensors) only when N>1;
+    torch is imported before libzarrhip so both share one HIP runtime."""
+
+    def __init__(self, ws):
+        self.ws = ws
+        if ws > 1:
+            import torch
+            import torch.distributed as dist
+            dist.init_process_group("gloo")
+            self.torch, self.dist = torch, dist
+
+    def barrier(self):
+        if self.ws > 1:
+            self.dist.barrier()
+
+    def max(self, v):
+        if self.ws == 1:
+            return v
+        t = self.torch.tensor([float(v)], dtype=self.torch.float64)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+        return float(t.item())
+
+    def close(self):
+        if self.ws > 1:
+            self.dist.destroy_process_group()
+
+
+def build_meta(A, cfg):
+    _, sharded, order = CONFIGS[cfg]
+    return A.make_meta([1, 4096, 4096, 1536], [1, 1024, 1024, 1024], 4,
+                       endian=A.ZH_ENDIAN_BIG, sharded=sharded,
+                       inner_chunk_shape=[1, 32, 32, 32] if sharded else None,
+                       transpose_order=order, index_endian=A.ZH_ENDIAN_LITTLE,
+                       index_crc32c=True, index_location=A.ZH_INDEX_END)
+
+
+def chunk_capacities(meta, coords):
+    """Exact encoded sizes for synthetic data (every in-bounds inner chunk is non-fill;
+    inner chunks wholly in the boundary padding are elided as all-fill)."""
+    n = meta.ndim
+    sharded = meta.chain.sharded
+    inner = [meta.chain.inner_chunk_shape[d] if sharded else meta.chunk_shape[d] for d in range(n)]
+    inner_bytes = 4
+    for d in range(n):
+        inner_bytes *= inner[d]
+    isz = 0
+    if sharded:
+        ncps = 1
+        for d in range(n):
+            ncps *= meta.chunk_shape[d] // inner[d]
+        isz = 16 * ncps + 4
+    caps = []
+    for c in coords:
+        valid = 1
+        for d in range(n):
+            lo = c[d] * meta.chunk_shape[d]
+            hi = min(lo + meta.chunk_shape[d], meta.shape[d])
+            valid *= -(-(hi - lo) // inner[d])
+        caps.append(valid * inner_bytes + isz)
+    return caps
+
+
+def cpu_baseline(dev, A, meta, shard_ptr, shard_nbytes, budget_s=12.0):
+    """The C oracle (restated reference path, oracle/zh_oracle.c) on this host's cores over a
+    bounded sample of the same workload: region reads [1,1024,1024,64] inside shard (0,0,0,0)
+    (copied D2H), repeated until ~budget_s of CPU work."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+    try:
+        cores = min(16, len(os.sched_getaffinity(0)))
+    except AttributeError:
+        cores = min(16, os.cpu_count() or 1)
+    host = (C.c_char * shard_nbytes)()
+    dev.memcpy(C.addressof(host), shard_ptr, shard_nbytes, 1, None, True)
+    srcs = (A.zh_chunk_src * 1)()
+    srcs[0].data = C.addressof(host)
+    srcs[0].nbytes = shard_nbytes
+    shape = [1, 1024, 1024, 64]
+    nbytes_out = 1024 * 1024 * 64 * 4
+    out = (C.c_char * nbytes_out)()
+    total_bytes, total_t, reps = 0, 0.0, 0
+    z = 0
+    while total_t < budget_s and reps < 64:
+        off = [0, 0, 0, z]
+        t0 = time.perf_counter()
+        O.array_read_into(meta, srcs, 1, off, shape, C.addressof(out), nthreads=cores)
+        total_t += time.perf_counter() - t0
+        total_bytes += nbytes_out
+        reps += 1
+        z = (z + 64) % 1024
+    return {"value": round(total_bytes / total_t / GiB, 4), "unit": "GiB/s",
+            "cores": cores, "kind": "port",
+            "sample": f"{reps} x Array.read [1,1024,1024,64] (256 MiB each) from one "
+                      f"device-encoded shard, C oracle (oracle/zh_oracle.c, OpenMP over inner "
+                      f"chunks), {total_t:.1f} s"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-budget", type=float, default=12.0)
+    args = ap.parse_args()
+
+    ws, rank, local = dist_env()
+    if args.gpus != ws and ws > 1:
+        log(f"warning: --gpus {args.gpus} but WORLD_SIZE {ws}")
+    dist = Dist(ws)
+
+    from zarrhip import _abi as A
+    from zarrhip._lib import DeviceContext, lib
+
+    dev = DeviceContext(local)
+    info = dev.info()
+    meta = build_meta(A, args.config)
+    n = meta.ndim
+    shape = [meta.shape[d] for d in range(n)]
+    L = lib()
+    ncoords = L.zh_compute_chunk_coords(n, (C.c_int64 * 8)(*shape),
+                                        (C.c_int32 * 8)(*[meta.chunk_shape[d] for d in range(n)]),
+                                        (C.c_int64 * 8)(*([0] * n)), (C.c_int64 * 8)(*shape),
+                                        None, 0)
+    cbuf = (C.c_int64 * (ncoords * n))()
+    L.zh_compute_chunk_coords(n, (C.c_int64 * 8)(*shape),
+                              (C.c_int32 * 8)(*[meta.chunk_shape[d] for d in range(n)]),
+                              (C.c_int64 * 8)(*([0] * n)), (C.c_int64 * 8)(*shape), cbuf, ncoords)
+    coords = [tuple(cbuf[i * n + d] for d in range(n)) for i in range(ncoords)]
+    caps = chunk_capacities(meta, coords)
+    nel = 1
+    for s in shape:
+        nel *= s
+    out_bytes = nel * 4
+
+    # device buffers: decoded region (also the encode source) + one slab for all shards
+    t0 = time.perf_counter()
+    out = dev.malloc(out_bytes)
+    offs, tot = [], 0
+    for cap in caps:
+        offs.append(tot)
+        tot += (cap + 255) // 256 * 256
+    shard_slab = dev.malloc(tot)
+    dev.synth_fill(out, nel, 4, 0, SEED)
+    dev.sync()
+    t1 = time.perf_counter()
+    sizes = dev.array_write(meta, out, [0] * n, shape,
+                            [(shard_slab + o, c) for o, c in zip(offs, caps)])
+    t2 = time.perf_counter()
+    assert all(s == c for s, c in zip(sizes, caps)), (sizes[:4], caps[:4])
+    log(f"[rank {rank}] {info['name']} {info['arch']} cus={info['cu_count']}: synth "
+        f"{t1 - t0:.2f}s, device encode {t2 - t1:.2f}s ({sum(sizes) / GiB:.2f} GiB in "
+        f"{len(sizes)} shards)")
+
+    flags = A.ZH_SRC_DEVICE | A.ZH_OUT_DEVICE
+    plan = dev.plan(meta, [(shard_slab + o, s) for o, s in zip(offs, sizes)], [0] * n, shape,
+                    flags)
+    st = plan.stats()
+    dev.memset(out, 0, out_bytes)
+    for _ in range(max(1, args.warmup)):
+        plan.execute(out)
+    plan.wait()
+    bad = dev.synth_verify(out, shape, [0] * n, shape, 4, SEED)
+    if bad:
+        raise SystemExit(f"decode verification FAILED: {bad} mismatching elements")
+    log(f"[rank {rank}] verified {nel} decoded elements bit-exact vs generator")
+
+    plan.set_timing(True)
+    dist.barrier()
+    dev.sync()
+    t_start = time.perf_counter()
+    for _ in range(args.steps):
+        plan.execute(out)
+    plan.wait()
+    t_end = time.perf_counter()
+    dist.barrier()
+    elapsed = dist.max(t_end - t_start)
+    kt = plan.kernel_time()
+    scatter_ms = kt["scatter_ms"] / max(1, kt["launches"])
+    index_ms = kt["index_ms"] / max(1, kt["launches"])
+
+    ms_per_step = elapsed * 1000.0 / args.steps
+    value = ws * args.steps * out_bytes / elapsed / GiB
+    traffic_alg = st["in_bytes"] + st["out_bytes"]
+    achieved = traffic_alg / (scatter_ms / 1000.0) / 1e9
+    roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                "kernel": "scatter_kernel<4,false,%s>" % ("true" if meta.chain.has_transpose else
+                                                          "false"),
+                "kernel_ms": round(scatter_ms, 3), "index_kernels_ms": round(index_ms, 4),
+                "alg_bytes_per_launch": traffic_alg}
+    cpu = None
+    if rank == 0 and ws == 1 and not args.no_cpu_baseline and meta.chain.sharded:
+        cpu = cpu_baseline(dev, A, meta, shard_slab + offs[0], sizes[0], args.cpu_budget)
+
+    line = {
+        "metric": "GiB/s device-resident chunk decode (sharding+bytes+transpose), uint32 1024³",
+        "value": round(value, 2), "unit": "GiB/s", "n_gpus": ws, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "u32", "data": "synthetic",
+        "config": {"workload": f"{args.config}: Array.read of the full 1x4096x4096x1536 uint32 "
+                               f"array, {CONFIGS[args.config][0]}",
+                   "array_shape": shape, "chunk_shape": [1, 1024, 1024, 1024],
+                   "inner_chunk_shape": [1, 32, 32, 32] if meta.chain.sharded else None,
+                   "shards": st["shards"], "inner_chunks": st["items"],
+                   "decoded_bytes_per_gpu": out_bytes, "parallelism": f"shard-parallel x{ws}"},
+        "roofline": roofline,
+        "cpu_baseline": cpu,
+    }
+    plan.close()
+    dev.free(shard_slab)
+    dev.free(out)
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    dist.close()
+
+
+if __name__ == "__main__":
+    main()

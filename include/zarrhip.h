@@ -1,0 +1,228 @@
+/*
+ * zarrhip.h — C-ABI of the MI355X-native Zarr v3 chunk codec path.
+ *
+ * This is the drop-in boundary that zarr-java's JNI shim binds.
+ * Every entry point is `extern "C"`, takes plain pointers and sizes, and returns an
+ * `int` status (ZH_OK = 0).  No torch / HIP types appear in any signature: streams
+ * and device buffers travel as `void*`.
+ *
+ * Reference interfaces replaced (zarr-java snapshot 2026-08-07,
+ * M/ = src/main/java/dev/zarr/zarrjava/):
+ *   zh_array_read               core.Array.read(long[],long[],boolean)       M/core/Array.java:378-441
+ *   zh_plan_* (prepared read)   same, split into plan (host) + execute (device)
+ *   zh_sharding_decode          ShardingIndexedCodec.decode(ByteBuffer)      M/v3/codec/core/ShardingIndexedCodec.java:98-103
+ *   zh_sharding_decode_partial  ShardingIndexedCodec.decodePartial(...)      M/v3/codec/core/ShardingIndexedCodec.java:245-255
+ *   zh_array_write              core.Array.write + writeChunk + ShardingIndexedCodec.encode
+ *                                                                            M/core/Array.java:83-156, ShardingIndexedCodec.java:105-168
+ *   zh_shard_index_size         ShardingIndexedCodec.getShardIndexSize       ShardingIndexedCodec.java:176-181
+ *   zh_crc32c                   utils.CRC32C.update/getValue                 M/utils/CRC32C.java:119-125,137-139
+ *   zh_compute_chunk_coords     IndexingUtils.computeChunkCoords             M/utils/IndexingUtils.java:16-51
+ *   zh_compute_projection       IndexingUtils.computeProjection (5-arg)      M/utils/IndexingUtils.java:65-117
+ *   zh_is_permutation           Utils.isPermutation                          M/utils/Utils.java:91-100
+ *   zh_inverse_permutation      Utils.inversePermutation                     M/utils/Utils.java:102-109
+ *
+ * Status → Java exception mapping used by the JNI shim:
+ *   ZH_EINVAL  → IllegalArgumentException      (rank mismatches, Array.java:380-385)
+ *   ZH_EDATA   → dev.zarr.zarrjava.ZarrException (message text reproduces the reference's)
+ *   ZH_EUNSUPPORTED → caller falls back to the Java codec (chain not device-supported)
+ *   ZH_EARITH  → ArithmeticException            (IndexingUtils overflow checks)
+ *   ZH_EHIP / ZH_ENOMEM → RuntimeException
+ */
+#ifndef ZARRHIP_H
+#define ZARRHIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define ZH_MAX_DIMS 8
+
+enum zh_status {
+  ZH_OK = 0,
+  ZH_EINVAL = 1,
+  ZH_EDATA = 2,
+  ZH_EUNSUPPORTED = 3,
+  ZH_EHIP = 4,
+  ZH_ENOMEM = 5,
+  ZH_EARITH = 6
+};
+
+enum zh_endian { ZH_ENDIAN_LITTLE = 0, ZH_ENDIAN_BIG = 1 };
+enum zh_index_location { ZH_INDEX_END = 0, ZH_INDEX_START = 1 };
+
+/* call flags */
+#define ZH_SRC_DEVICE 0x1u /* chunk/shard byte sources are device pointers            */
+#define ZH_OUT_DEVICE 0x2u /* output buffer is a device pointer                      */
+
+/*
+ * Codec chain the device path executes.  Mirrors the JSON `codecs` list of a v3 array
+ * (v3/ArrayMetadata.java) restricted to the device-supported chains:
+ *   sharded = 0 :  [transpose?, bytes]                          (BASELINE config 2)
+ *   sharded = 1 :  [sharding_indexed{ codecs=[transpose?, bytes],
+ *                                     index_codecs=[bytes, crc32c?],
+ *                                     index_location }]          (configs 3, 4, 5)
+ * Anything else (blosc/gzip/zstd inside the chain, nested sharding, array-level codecs
+ * next to sharding) is rejected with ZH_EUNSUPPORTED so the caller keeps the Java path.
+ */
+typedef struct zh_codec_chain {
+  int32_t sharded;                          /* 1: outer codec is sharding_indexed              */
+  int32_t inner_chunk_shape[ZH_MAX_DIMS];   /* sharding configuration.chunk_shape              */
+  int32_t has_transpose;                    /* transpose codec present in the (inner) chain    */
+  int32_t transpose_order[ZH_MAX_DIMS];     /* TransposeCodec.Configuration.order              */
+  int32_t endian;                           /* bytes codec endian (ignored for 1-byte types)   */
+  int32_t index_endian;                     /* index_codecs bytes endian                       */
+  int32_t index_has_crc32c;                 /* index_codecs contains crc32c                    */
+  int32_t index_location;                   /* ZH_INDEX_END (default) / ZH_INDEX_START          */
+} zh_codec_chain;
+
+/* CoreArrayMetadata (M/core/ArrayMetadata.java:154-187) + the codec chain. */
+typedef struct zh_array_meta {
+  int32_t ndim;
+  int32_t dtype_size;                 /* DataType.getByteCount(): 1, 2, 4 or 8             */
+  int32_t dtype_is_bool;              /* bool decodes as b != 0 (core BytesCodec.java:24-33) */
+  int32_t reserved0;
+  int64_t shape[ZH_MAX_DIMS];         /* array shape                                       */
+  int32_t chunk_shape[ZH_MAX_DIMS];   /* regular chunk grid shape (= shard shape)          */
+  uint8_t fill_value[8];              /* parsed fill value, element bytes little-endian     */
+  zh_codec_chain chain;
+} zh_array_meta;
+
+/* One stored chunk (or shard) object.  data == NULL means the key does not exist in the
+ * store (StoreHandle.exists() == false, M/core/Array.java:419-421). */
+typedef struct zh_chunk_src {
+  const void* data;
+  int64_t nbytes;
+} zh_chunk_src;
+
+/* Destination of one encoded chunk object for zh_array_write. */
+typedef struct zh_chunk_dst {
+  void* data;          /* device buffer for the encoded bytes                         */
+  int64_t capacity;    /* bytes available                                            */
+  int64_t nbytes;      /* out: encoded size; 0 = chunk is all fill → delete key      */
+} zh_chunk_dst;
+
+typedef struct zh_ctx zh_ctx;
+typedef struct zh_plan zh_plan;
+
+/* ---- context -------------------------------------------------------------------- */
+int zh_ctx_create(int device, zh_ctx** out);
+void zh_ctx_destroy(zh_ctx* ctx);
+int zh_ctx_device(const zh_ctx* ctx);
+/* The context's default stream (a hipStream_t).  Calls with stream == NULL use it. */
+void* zh_ctx_stream(zh_ctx* ctx);
+const char* zh_version(void);
+
+/* ---- host-side metadata helpers (no device needed) ------------------------------- */
+/* Validates the chain against the reference rules (CodecPipeline ctor, sharding
+ * divisibility ArrayMetadata.java:285-306, TransposeCodec.decode :35-41,
+ * v3 BytesCodec.getByteOrder :43-48).  Returns ZH_EUNSUPPORTED for valid-but-not-
+ * device-supported chains. */
+int zh_validate_meta(const zh_array_meta* meta, char* err, size_t errlen);
+/* 16 * prod(chunks per shard) (+4 with crc32c).  -1 for unsharded metas. */
+int64_t zh_shard_index_size(const zh_array_meta* meta);
+/* CRC32C.update over n bytes starting from a previous getValue() (0 for a fresh CRC32C). */
+uint32_t zh_crc32c(uint32_t crc, const void* data, size_t n);
+/* IndexingUtils.computeChunkCoords: writes up to max_coords rows of ndim int64 into
+ * coords_out (may be NULL) in C order; returns the number of chunks, or -1 (ZH_EARITH
+ * condition: more than Integer.MAX_VALUE chunks). */
+int64_t zh_compute_chunk_coords(int ndim, const int64_t* array_shape, const int32_t* chunk_shape,
+                                const int64_t* sel_offset, const int64_t* sel_shape,
+                                int64_t* coords_out, int64_t max_coords);
+/* IndexingUtils.computeProjection (5-arg).  Returns ZH_OK or ZH_EARITH. */
+int zh_compute_projection(int ndim, const int64_t* chunk_coords, const int64_t* array_shape,
+                          const int32_t* chunk_shape, const int64_t* sel_offset,
+                          const int64_t* sel_shape, int32_t* chunk_offset_out,
+                          int32_t* out_offset_out, int32_t* shape_out);
+int zh_is_permutation(int n, const int32_t* order);
+int zh_inverse_permutation(int n, const int32_t* order, int32_t* inverse_out);
+
+/* ---- decode (the hot path) ------------------------------------------------------ */
+/*
+ * Prepared region read: the host half of core.Array.read (domain check, chunk
+ * enumeration, projection, per-shard inner-chunk boxes) runs once in zh_plan_create;
+ * zh_plan_execute only enqueues device work on `stream` (no allocation, no sync:
+ * hipGraph-capturable); zh_plan_wait synchronises and reports deferred device errors
+ * (CRC mismatch, corrupt index) with the reference's messages.
+ *   chunks[i] belongs to the i-th chunk coordinate of
+ *   computeChunkCoords(meta->shape, meta->chunk_shape, offset, shape) (C order).
+ *   out = C-order buffer of prod(shape) elements.
+ */
+int zh_plan_create(zh_ctx* ctx, const zh_array_meta* meta, const zh_chunk_src* chunks,
+                   int64_t nchunks, const int64_t* offset, const int64_t* shape, uint32_t flags,
+                   zh_plan** out, char* err, size_t errlen);
+int zh_plan_execute(zh_plan* plan, void* out, void* stream);
+int zh_plan_wait(zh_plan* plan, char* err, size_t errlen);
+void zh_plan_destroy(zh_plan* plan);
+/* Plan statistics: bytes of encoded input read, output bytes written, number of
+ * inner-chunk work items, shards touched. */
+int zh_plan_stats(const zh_plan* plan, int64_t* in_bytes, int64_t* out_bytes,
+                  int64_t* items, int64_t* nshards);
+/* Per-kernel timing (HIP events around the scatter kernel on the launch stream).
+ * enable=1 starts recording; zh_plan_kernel_time synchronises and returns the summed
+ * scatter-kernel milliseconds and launch count since the last call. */
+int zh_plan_set_timing(zh_plan* plan, int enable);
+int zh_plan_kernel_time(zh_plan* plan, double* scatter_ms, int64_t* launches,
+                        double* index_ms);
+
+/* One-shot synchronous region read: plan + execute + wait. */
+int zh_array_read(zh_ctx* ctx, const zh_array_meta* meta, const zh_chunk_src* chunks,
+                  int64_t nchunks, const int64_t* offset, const int64_t* shape, void* out,
+                  uint32_t flags, void* stream, char* err, size_t errlen);
+/* ShardingIndexedCodec.decode: whole shard → chunk_shape elements. */
+int zh_sharding_decode(zh_ctx* ctx, const zh_array_meta* meta, const void* shard, int64_t nbytes,
+                       void* out, uint32_t flags, void* stream, char* err, size_t errlen);
+/* ShardingIndexedCodec.decodePartial: shard-local offset/shape → shape elements. */
+int zh_sharding_decode_partial(zh_ctx* ctx, const zh_array_meta* meta, const void* shard,
+                               int64_t nbytes, const int64_t* offset, const int32_t* shape,
+                               void* out, uint32_t flags, void* stream, char* err,
+                               size_t errlen);
+
+/* ---- encode (write path) ---------------------------------------------------------- */
+/*
+ * Device encode of every chunk intersecting [offset, offset+shape), which must cover
+ * whole chunks (clipped only by the array boundary); src is that region in C order on
+ * the device.  Inner chunks that are all fill_value become (-1,-1) index entries and
+ * are laid out in C order (deterministic; the reference's order is not — SURVEY Q7).
+ * A chunk that is entirely fill reports nbytes = 0 (writeChunk deletes it).
+ * dsts[i] follows computeChunkCoords order.  zh_array_encoded_bound gives the worst-
+ * case encoded size of one chunk.
+ */
+int64_t zh_array_encoded_bound(const zh_array_meta* meta);
+int zh_array_write(zh_ctx* ctx, const zh_array_meta* meta, const void* src,
+                   const int64_t* offset, const int64_t* shape, zh_chunk_dst* dsts,
+                   int64_t nchunks, void* stream, char* err, size_t errlen);
+
+/* ---- device memory / stream / event plumbing for callers without their own ---------- */
+int zh_device_malloc(zh_ctx* ctx, size_t bytes, void** out);
+int zh_device_free(zh_ctx* ctx, void* ptr);
+int zh_host_malloc_pinned(zh_ctx* ctx, size_t bytes, void** out);
+int zh_host_free_pinned(zh_ctx* ctx, void* ptr);
+/* kind: 0 H2D, 1 D2H, 2 D2D; asynchronous on stream */
+int zh_memcpy_async(zh_ctx* ctx, void* dst, const void* src, size_t bytes, int kind, void* stream);
+int zh_memset_async(zh_ctx* ctx, void* dst, int value, size_t bytes, void* stream);
+int zh_stream_synchronize(zh_ctx* ctx, void* stream);
+int zh_event_create(zh_ctx* ctx, void** ev);
+int zh_event_destroy(zh_ctx* ctx, void* ev);
+int zh_event_record(zh_ctx* ctx, void* ev, void* stream);
+int zh_event_elapsed_ms(zh_ctx* ctx, void* start, void* stop, float* ms);
+int zh_device_info(zh_ctx* ctx, char* name, size_t namelen, int64_t* total_mem,
+                   int* cu_count, char* arch, size_t archlen);
+
+/* ---- synthetic data (bench / property tests) -------------------------------------- */
+/* dst[i] = low dtype_size bytes of splitmix64((first + i) ^ seed), i in [0, n). */
+int zh_synth_fill(zh_ctx* ctx, void* dst, int64_t n, int dtype_size, int64_t first,
+                  uint64_t seed, void* stream);
+/* Counts elements of the C-order region [offset, offset+shape) of an array of
+ * array_shape whose value differs from the synth value at their global index. */
+int zh_synth_verify(zh_ctx* ctx, const void* region, int ndim, const int64_t* array_shape,
+                    const int64_t* offset, const int64_t* shape, int dtype_size,
+                    uint64_t seed, uint64_t* mismatches, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* ZARRHIP_H */

@@ -1,0 +1,209 @@
+"""HIP path vs the CPU oracle (bit-exact), through the C-ABI.  Mirrors the reference's
+own tests: ZarrV3Test testEndianness / testTransposeCodec / testShardingReadWrite /
+testUnalignedArrayAccess / testLargerChunkSizeThanArraySize, ParallelWriteTest shapes,
+and the ZarrPythonTests codec configurations (parse_codecs.py:104-116)."""
+import itertools
+
+import numpy as np
+import pytest
+
+import oracle as O
+from helpers import (chunk_coords, device_read, device_write, encode_oracle, load_reference_fixture,
+                     rand_array, shape_of)
+from zarrhip import _abi as A
+from zarrhip._lib import ZhError
+
+pytestmark = pytest.mark.gpu
+
+
+def roundtrip(dev, meta, arr, regions):
+    shards = encode_oracle(meta, arr)
+    n = meta.ndim
+    for off, shp in regions:
+        srcs = [shards[i] for i in range(len(shards))]
+        coords_all = chunk_coords(meta, [0] * n, shape_of(meta))
+        sel = chunk_coords(meta, off, shp)
+        pos = {c: i for i, c in enumerate(coords_all)}
+        src_sel = [srcs[pos[c]] for c in sel]
+        want = np.frombuffer(O.array_read(meta, src_sel, off, shp),
+                             dtype=arr.dtype).reshape(shp)
+        got = device_read(dev, meta, src_sel, off, shp)
+        np.testing.assert_array_equal(got, want)
+        sl = tuple(slice(o, o + s) for o, s in zip(off, shp))
+        np.testing.assert_array_equal(got, arr[sl])
+    return shards
+
+
+def test_reference_fixtures_decode_to_arange(dev):
+    for loc in ("start", "end"):
+        _, meta, srcs = load_reference_fixture(loc)
+        got = device_read(dev, meta, srcs, [0, 0, 0], [16, 16, 16])
+        np.testing.assert_array_equal(got.astype(np.int64).ravel(), np.arange(4096))
+        got2 = device_read(dev, meta, srcs, [3, 5, 1], [9, 7, 14])
+        np.testing.assert_array_equal(got2.astype(np.int64),
+                                      np.arange(4096).reshape(16, 16, 16)[3:12, 5:12, 1:15])
+
+
+@pytest.mark.parametrize("dsize", [1, 2, 4, 8])
+@pytest.mark.parametrize("endian", [A.ZH_ENDIAN_LITTLE, A.ZH_ENDIAN_BIG])
+def test_unsharded_bytes(dev, dsize, endian):
+    shape = [16, 16, 16]
+    meta = A.make_meta(shape, [2, 4, 8], dsize, endian=endian)
+    arr = rand_array(shape, dsize, seed=dsize + endian)
+    roundtrip(dev, meta, arr, [([0, 0, 0], shape), ([1, 3, 5], [10, 9, 11])])
+
+
+@pytest.mark.parametrize("dsize", [1, 2, 4, 8])
+@pytest.mark.parametrize("endian", [A.ZH_ENDIAN_LITTLE, A.ZH_ENDIAN_BIG])
+@pytest.mark.parametrize("loc", [A.ZH_INDEX_END, A.ZH_INDEX_START])
+def test_sharded(dev, dsize, endian, loc):
+    shape = [16, 16, 16]
+    meta = A.make_meta(shape, [8, 8, 8], dsize, endian=endian, sharded=True,
+                       inner_chunk_shape=[2, 4, 8], index_location=loc)
+    arr = rand_array(shape, dsize, seed=3 * dsize + endian, fill_frac=0.0)
+    roundtrip(dev, meta, arr, [([0, 0, 0], shape), ([1, 3, 5], [10, 9, 11]), ([8, 8, 8], [8, 8, 8])])
+
+
+@pytest.mark.parametrize("order", list(itertools.permutations(range(4))))
+def test_sharded_transpose_all_orders(dev, order):
+    shape = [2, 24, 20, 36]
+    meta = A.make_meta(shape, [2, 16, 8, 32], 4, endian=A.ZH_ENDIAN_BIG, sharded=True,
+                       inner_chunk_shape=[1, 8, 4, 16], transpose_order=list(order))
+    arr = rand_array(shape, 4, seed=sum(o * 10 ** i for i, o in enumerate(order)))
+    roundtrip(dev, meta, arr, [([0, 0, 0, 0], shape), ([1, 3, 2, 5], [1, 17, 15, 30])])
+
+
+@pytest.mark.parametrize("order", [[2, 1, 0], [1, 2, 0], [0, 2, 1], [1, 0, 2]])
+@pytest.mark.parametrize("dsize", [1, 2, 8])
+def test_unsharded_transpose(dev, order, dsize):
+    shape = [40, 33, 70]
+    meta = A.make_meta(shape, [32, 32, 64], dsize, endian=A.ZH_ENDIAN_BIG,
+                       transpose_order=order)
+    arr = rand_array(shape, dsize, seed=7)
+    roundtrip(dev, meta, arr, [([0, 0, 0], shape), ([5, 1, 9], [30, 31, 60])])
+
+
+def test_large_tiles_transpose_c4_shape(dev):
+    """BASELINE config 4 shapes at reduced extent: inner 1x32x32x32, order [0,3,2,1]."""
+    shape = [1, 128, 96, 80]
+    meta = A.make_meta(shape, [1, 64, 64, 64], 4, endian=A.ZH_ENDIAN_BIG, sharded=True,
+                       inner_chunk_shape=[1, 32, 32, 32], transpose_order=[0, 3, 2, 1])
+    arr = rand_array(shape, 4, seed=11)
+    roundtrip(dev, meta, arr, [([0, 0, 0, 0], shape), ([0, 7, 33, 5], [1, 100, 60, 70])])
+
+
+def test_missing_inner_chunks_are_zero_and_missing_shards_fill(dev):
+    """Q1: a missing inner chunk reads 0 even with a non-zero fill; a missing shard reads
+    fill_value (ShardingIndexedCodec.java:189,219-221; Array.java:400-402,419-421)."""
+    shape = [16, 16]
+    fill = np.uint32(7)
+    meta = A.make_meta(shape, [8, 8], 4, fill=int(fill).to_bytes(4, "little"), sharded=True,
+                       inner_chunk_shape=[4, 4])
+    arr = rand_array(shape, 4, seed=5)
+    arr[0:4, 0:4] = fill      # all-fill inner chunk → (-1,-1) in the index
+    arr[8:16, 8:16] = fill    # all-fill shard → deleted
+    shards = encode_oracle(meta, arr)
+    assert shards[3] is None
+    got = device_read(dev, meta, shards, [0, 0], shape)
+    want = np.frombuffer(O.array_read(meta, shards, [0, 0], shape), dtype=np.uint32).reshape(shape)
+    np.testing.assert_array_equal(got, want)
+    assert (got[0:4, 0:4] == 0).all()          # Q1
+    assert (got[8:16, 8:16] == fill).all()
+
+
+def test_boundary_chunks_larger_than_array(dev):
+    """testLargerChunkSizeThanArraySize / boundary shards with padding."""
+    shape = [10, 21, 13]
+    meta = A.make_meta(shape, [16, 16, 16], 2, endian=A.ZH_ENDIAN_BIG, sharded=True,
+                       inner_chunk_shape=[4, 8, 4], transpose_order=[1, 2, 0])
+    arr = rand_array(shape, 2, seed=13)
+    roundtrip(dev, meta, arr, [([0, 0, 0], shape), ([9, 20, 12], [1, 1, 1]), ([2, 3, 4], [8, 18, 9])])
+
+
+def test_bool(dev):
+    shape = [9, 17]
+    meta = A.make_meta(shape, [4, 8], 1, is_bool=True, sharded=True, inner_chunk_shape=[2, 4])
+    arr = (rand_array(shape, 1, seed=3) % 2).astype(np.uint8)
+    roundtrip(dev, meta, arr, [([0, 0], shape)])
+
+
+def test_crc_mismatch_message(dev):
+    shape = [8, 8]
+    meta = A.make_meta(shape, [8, 8], 4, sharded=True, inner_chunk_shape=[4, 4])
+    arr = rand_array(shape, 4, seed=1)
+    shards = encode_oracle(meta, arr)
+    bad = bytearray(shards[0])
+    bad[-10] ^= 0x40  # flip an index byte (inside the crc'd range)
+    with pytest.raises(O.OracleError) as eo:
+        O.array_read(meta, [bytes(bad)], [0, 0], shape)
+    with pytest.raises(ZhError) as ed:
+        device_read(dev, meta, [bytes(bad)], [0, 0], shape)
+    assert str(ed.value) == str(eo.value)
+    assert str(ed.value).startswith("The checksum of the sharding index is invalid. Stored: ")
+
+
+def test_corrupt_offset_rejected(dev):
+    shape = [8, 8]
+    meta = A.make_meta(shape, [8, 8], 4, sharded=True, inner_chunk_shape=[4, 4],
+                       index_crc32c=False)
+    arr = rand_array(shape, 4, seed=1)
+    shards = encode_oracle(meta, arr)
+    bad = bytearray(shards[0])
+    isz = 16 * 4
+    ib = len(bad) - isz
+    bad[ib + 16: ib + 24] = (10 ** 9).to_bytes(8, "little")  # entry 1 offset far out of range
+    with pytest.raises(ZhError) as ed:
+        device_read(dev, meta, [bytes(bad)], [0, 0], shape)
+    with pytest.raises(O.OracleError) as eo:
+        O.array_read(meta, [bytes(bad)], [0, 0], shape)
+    assert str(ed.value) == str(eo.value) == "Could not load byte data for chunk [0, 1]"
+
+
+def test_domain_error(dev):
+    meta = A.make_meta([8, 8], [4, 4], 4)
+    with pytest.raises(ZhError) as ed:
+        device_read(dev, meta, [None], [6, 6], [4, 4])
+    assert str(ed.value) == "Requested data is outside of the array's domain."
+
+
+@pytest.mark.parametrize("sharded", [False, True])
+@pytest.mark.parametrize("order", [None, [2, 0, 1]])
+@pytest.mark.parametrize("loc", [A.ZH_INDEX_END, A.ZH_INDEX_START])
+def test_device_encode_matches_oracle_bytes(dev, sharded, order, loc):
+    shape = [20, 24, 40]
+    meta = A.make_meta(shape, [8, 16, 32], 4, endian=A.ZH_ENDIAN_BIG, sharded=sharded,
+                       inner_chunk_shape=[4, 8, 16] if sharded else None, transpose_order=order,
+                       index_location=loc, fill=(3).to_bytes(4, "little"))
+    arr = rand_array(shape, 4, seed=17, fill_frac=0.0)
+    arr[0:8, 0:16, 0:32] = 3     # a whole chunk of fill → deleted
+    arr[8:12, 0:8, 0:16] = 3     # an inner chunk of fill → (-1,-1)
+    want = encode_oracle(meta, arr)
+    got = device_write(dev, meta, arr)
+    assert len(got) == len(want)
+    for g, w in zip(got, want):
+        assert g == w
+
+
+def test_single_full_chunk_and_partial_decode_api(dev):
+    """Array.java:392-395 single-full-chunk shortcut and ShardingIndexedCodec.decode /
+    decodePartial through their own C-ABI entry points."""
+    import ctypes as C
+    shape = [32, 32]
+    meta = A.make_meta(shape, [16, 16], 4, sharded=True, inner_chunk_shape=[4, 8],
+                       endian=A.ZH_ENDIAN_BIG)
+    arr = rand_array(shape, 4, seed=21)
+    shards = encode_oracle(meta, arr)
+    got = device_read(dev, meta, [shards[3]], [16, 16], [16, 16])
+    np.testing.assert_array_equal(got, arr[16:, 16:])
+    from zarrhip._lib import lib, i64arr, i32arr
+    L = lib()
+    sb = (C.c_char * len(shards[1])).from_buffer_copy(shards[1])
+    out = (C.c_char * (16 * 16 * 4))()
+    err = C.create_string_buffer(512)
+    assert L.zh_sharding_decode(dev.h, C.byref(meta), sb, len(shards[1]), out, 0, None, err, 512) == 0
+    np.testing.assert_array_equal(np.frombuffer(bytes(out), np.uint32).reshape(16, 16), arr[:16, 16:])
+    out2 = (C.c_char * (5 * 7 * 4))()
+    assert L.zh_sharding_decode_partial(dev.h, C.byref(meta), sb, len(shards[1]), i64arr([3, 4]),
+                                        i32arr([5, 7]), out2, 0, None, err, 512) == 0
+    np.testing.assert_array_equal(np.frombuffer(bytes(out2), np.uint32).reshape(5, 7),
+                                  arr[3:8, 20:27])

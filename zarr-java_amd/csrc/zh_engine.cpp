@@ -1,0 +1,1044 @@
+// zh_engine.cpp — host side of the MI355X Zarr v3 chunk codec path and its C-ABI
+// (include/zarrhip.h).
+//
+// The planner restates the host half of core.Array.read (M/core/Array.java:378-441):
+// domain check, chunk enumeration (IndexingUtils.computeChunkCoords :16-51), outer
+// projection (computeProjection :65-117) and, per shard, the inner-chunk box that
+// ShardingIndexedCodec.decodeInternal (:206-208) iterates.  Everything per element —
+// index CRC, index parse, endian swap, transpose, scatter — runs on the GPU in
+// zh_kernels.hip.  There is no CPU fallback: if the device is unusable every entry point
+// fails with ZH_EHIP.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <array>
+#include <cstdarg>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "zh_internal.h"
+
+using namespace zh;
+
+namespace {
+
+constexpr int64_t kIntMax = 2147483647LL;
+
+void set_err(char* err, size_t errlen, const char* fmt, ...) {
+  if (!err || errlen == 0) return;
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(err, errlen, fmt, ap);
+  va_end(ap);
+}
+
+#define ZH_HIP(call)                                                                       \
+  do {                                                                                     \
+    hipError_t e_ = (call);                                                                \
+    if (e_ != hipSuccess) {                                                                \
+      set_err(err, errlen, "HIP error %s at %s:%d (%s)", hipGetErrorName(e_), __FILE__,     \
+              __LINE__, hipGetErrorString(e_));                                            \
+      return ZH_EHIP;                                                                      \
+    }                                                                                      \
+  } while (0)
+
+std::string fmt_ints(const int64_t* v, int n) {  // java.util.Arrays.toString
+  std::string s = "[";
+  for (int i = 0; i < n; i++) {
+    if (i) s += ", ";
+    s += std::to_string((long long)v[i]);
+  }
+  return s + "]";
+}
+std::string fmt_ints32(const int32_t* v, int n) {
+  std::vector<int64_t> t(v, v + n);
+  return fmt_ints(t.data(), n);
+}
+
+// ---- CRC-32C (host; slicing-by-8 over the reference's table, CRC32C.java:14-80) ----
+struct CrcTables {
+  uint32_t t[8][256];
+  CrcTables() {
+    for (uint32_t i = 0; i < 256; i++) {
+      uint32_t c = i;
+      for (int k = 0; k < 8; k++) c = (c & 1) ? (c >> 1) ^ 0x82F63B78u : (c >> 1);
+      t[0][i] = c;
+    }
+    for (int k = 1; k < 8; k++)
+      for (int i = 0; i < 256; i++) t[k][i] = (t[k - 1][i] >> 8) ^ t[0][t[k - 1][i] & 0xFF];
+  }
+};
+const CrcTables& crc_tables() {
+  static CrcTables T;
+  return T;
+}
+
+uint32_t crc32c_host(uint32_t crc, const uint8_t* p, size_t n) {
+  const auto& T = crc_tables().t;
+  uint32_t c = crc ^ 0xFFFFFFFFu;
+  size_t i = 0;
+  for (; i + 8 <= n; i += 8) {
+    uint64_t w;
+    memcpy(&w, p + i, 8);
+    uint32_t lo = (uint32_t)w ^ c, hi = (uint32_t)(w >> 32);
+    c = T[7][lo & 0xFF] ^ T[6][(lo >> 8) & 0xFF] ^ T[5][(lo >> 16) & 0xFF] ^ T[4][lo >> 24] ^
+        T[3][hi & 0xFF] ^ T[2][(hi >> 8) & 0xFF] ^ T[1][(hi >> 16) & 0xFF] ^ T[0][hi >> 24];
+  }
+  for (; i < n; i++) c = T[0][(c ^ p[i]) & 0xFF] ^ (c >> 8);
+  return c ^ 0xFFFFFFFFu;
+}
+
+// ---- IndexingUtils (M/utils/IndexingUtils.java) ----
+int64_t chunk_coords(int n, const int32_t* chunk, const int64_t* off, const int64_t* shp,
+                     int64_t* start, int64_t* count) {
+  int64_t num = 1;
+  for (int d = 0; d < n; d++) {  // :22-28 (int casts reproduced)
+    int64_t s = (int64_t)(int32_t)(off[d] / chunk[d]);
+    int64_t e = (int64_t)(int32_t)((off[d] + shp[d] - 1) / chunk[d]);
+    start[d] = s;
+    count[d] = e - s + 1;
+    num *= count[d];
+  }
+  return num;
+}
+
+int projection(int n, const int64_t* cc, const int64_t* ashape, const int32_t* chunk,
+               const int64_t* soff, const int64_t* sshape, int32_t* co, int32_t* oo,
+               int32_t* ps) {
+  for (int d = 0; d < n; d++) {
+    const int64_t dim_off = (int64_t)chunk[d] * cc[d];
+    const int64_t dim_limit = std::min(ashape[d], (cc[d] + 1) * (int64_t)chunk[d]);
+    if (soff[d] < dim_off) {
+      co[d] = 0;
+      int64_t v = dim_off - soff[d];
+      if (v > kIntMax) return ZH_EARITH;
+      oo[d] = (int32_t)v;
+    } else {
+      int64_t v = soff[d] - dim_off;
+      if (v > kIntMax) return ZH_EARITH;
+      co[d] = (int32_t)v;
+      oo[d] = 0;
+    }
+    if (soff[d] + sshape[d] > dim_limit) {
+      ps[d] = chunk[d] - co[d];
+    } else {
+      int64_t v = soff[d] + sshape[d] - dim_off - co[d];
+      if (v > kIntMax || v < 0) return ZH_EARITH;
+      ps[d] = (int32_t)v;
+    }
+  }
+  return ZH_OK;
+}
+
+bool is_perm(int n, const int32_t* o) {
+  if (n <= 0 || n > kMaxDims) return false;
+  bool seen[kMaxDims] = {false};
+  for (int i = 0; i < n; i++) {
+    if (o[i] < 0 || o[i] >= n || seen[o[i]]) return false;
+    seen[o[i]] = true;
+  }
+  return true;
+}
+
+uint32_t next_pow2_shift(uint64_t v) {
+  uint32_t s = 0;
+  while ((1ull << s) < v) s++;
+  return s;
+}
+
+int env_int(const char* name, int def) {
+  const char* v = getenv(name);
+  return v && *v ? atoi(v) : def;
+}
+
+}  // namespace
+
+// =====================================================================================
+// context
+// =====================================================================================
+struct zh_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  int cu_count = 256;
+  std::mutex mu;
+};
+
+struct zh_plan {
+  zh_ctx* ctx = nullptr;
+  zh_array_meta meta{};
+  uint32_t flags = 0;
+  int64_t nshards = 0;
+  int64_t n_items = 0;          // inner-chunk items (without pieces)
+  int64_t in_bytes = 0, out_bytes = 0;
+  std::vector<int64_t> coords;  // chunk coords (for messages)
+  // device state
+  DevShard* d_shards = nullptr;
+  uint64_t* d_status = nullptr;
+  CrcJob* d_crc_jobs = nullptr;
+  uint32_t* d_crc_partials = nullptr;
+  int64_t n_crc_jobs = 0, n_crc_spans = 0;
+  uint8_t* d_input = nullptr;   // staged host sources
+  std::vector<std::pair<int64_t, const void*>> h2d;  // (offset in d_input, host ptr)
+  std::vector<int64_t> h2d_len;
+  uint8_t* d_out = nullptr;     // staging when the output is host memory
+  ScatterArgs args{};
+  int tile_mode = 0;
+  int grid = 0;
+  hipStream_t last_stream = nullptr;
+  // timing
+  bool timing = false;
+  std::vector<hipEvent_t> ev_pool;
+  std::vector<std::array<hipEvent_t, 3>> ev_pending;
+};
+
+extern "C" {
+
+const char* zh_version(void) { return "zarrhip 0.1.0 (gfx950)"; }
+
+int zh_ctx_create(int device, zh_ctx** out) {
+  char* err = nullptr;
+  size_t errlen = 0;
+  if (!out) return ZH_EINVAL;
+  *out = nullptr;
+  int ndev = 0;
+  ZH_HIP(hipGetDeviceCount(&ndev));
+  if (device < 0 || device >= ndev) return ZH_EINVAL;
+  ZH_HIP(hipSetDevice(device));
+  zh_ctx* c = new zh_ctx();
+  c->device = device;
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, device) == hipSuccess) c->cu_count = prop.multiProcessorCount;
+  if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+    delete c;
+    return ZH_EHIP;
+  }
+  *out = c;
+  return ZH_OK;
+}
+
+void zh_ctx_destroy(zh_ctx* c) {
+  if (!c) return;
+  (void)hipSetDevice(c->device);
+  if (c->stream) (void)hipStreamDestroy(c->stream);
+  delete c;
+}
+
+int zh_ctx_device(const zh_ctx* c) { return c ? c->device : -1; }
+void* zh_ctx_stream(zh_ctx* c) { return c ? (void*)c->stream : nullptr; }
+
+// =====================================================================================
+// host helpers
+// =====================================================================================
+uint32_t zh_crc32c(uint32_t crc, const void* data, size_t n) {
+  return crc32c_host(crc, (const uint8_t*)data, n);
+}
+
+int64_t zh_compute_chunk_coords(int ndim, const int64_t* array_shape, const int32_t* chunk_shape,
+                                const int64_t* sel_offset, const int64_t* sel_shape,
+                                int64_t* coords_out, int64_t max_coords) {
+  (void)array_shape;
+  if (ndim <= 0 || ndim > kMaxDims) return -1;
+  int64_t start[kMaxDims], count[kMaxDims];
+  int64_t num = chunk_coords(ndim, chunk_shape, sel_offset, sel_shape, start, count);
+  if (num > kIntMax) return -1;  // :30-32
+  if (coords_out) {
+    int64_t cur[kMaxDims] = {0};
+    for (int64_t i = 0; i < num && i < max_coords; i++) {
+      for (int d = 0; d < ndim; d++) coords_out[i * ndim + d] = start[d] + cur[d];
+      for (int d = ndim - 1; d >= 0; d--) {
+        if (++cur[d] < count[d]) break;
+        cur[d] = 0;
+      }
+    }
+  }
+  return num;
+}
+
+int zh_compute_projection(int ndim, const int64_t* chunk_coords, const int64_t* array_shape,
+                          const int32_t* chunk_shape, const int64_t* sel_offset,
+                          const int64_t* sel_shape, int32_t* chunk_offset_out,
+                          int32_t* out_offset_out, int32_t* shape_out) {
+  if (ndim <= 0 || ndim > kMaxDims) return ZH_EINVAL;
+  return projection(ndim, chunk_coords, array_shape, chunk_shape, sel_offset, sel_shape,
+                    chunk_offset_out, out_offset_out, shape_out);
+}
+
+int zh_is_permutation(int n, const int32_t* order) { return is_perm(n, order) ? 1 : 0; }
+
+int zh_inverse_permutation(int n, const int32_t* order, int32_t* inverse_out) {
+  if (!is_perm(n, order)) return ZH_EINVAL;
+  for (int i = 0; i < n; i++) inverse_out[order[i]] = i;
+  return ZH_OK;
+}
+
+int64_t zh_shard_index_size(const zh_array_meta* m) {
+  if (!m || !m->chain.sharded) return -1;
+  int64_t n = 1;
+  for (int d = 0; d < m->ndim; d++) n *= m->chunk_shape[d] / m->chain.inner_chunk_shape[d];
+  return 16 * n + (m->chain.index_has_crc32c ? 4 : 0);  // ShardingIndexedCodec.java:176-181
+}
+
+int zh_validate_meta(const zh_array_meta* m, char* err, size_t errlen) {
+  if (!m) return ZH_EINVAL;
+  const int n = m->ndim;
+  if (n <= 0 || n > kMaxDims) {
+    set_err(err, errlen, "ndim %d not supported (1..%d)", n, kMaxDims);
+    return ZH_EUNSUPPORTED;
+  }
+  if (m->dtype_size != 1 && m->dtype_size != 2 && m->dtype_size != 4 && m->dtype_size != 8) {
+    set_err(err, errlen, "dtype size %d not supported", m->dtype_size);
+    return ZH_EUNSUPPORTED;
+  }
+  for (int d = 0; d < n; d++) {
+    if (m->shape[d] < 0 || m->chunk_shape[d] <= 0) {
+      set_err(err, errlen, "invalid shape/chunk shape at dimension %d", d);
+      return ZH_EINVAL;
+    }
+  }
+  const zh_codec_chain& c = m->chain;
+  const int32_t* inner = c.sharded ? c.inner_chunk_shape : m->chunk_shape;
+  if (c.sharded) {  // v3/ArrayMetadata.java:102-116
+    for (int d = 0; d < n; d++) {
+      if (inner[d] <= 0 || m->chunk_shape[d] % inner[d] != 0) {
+        set_err(err, errlen,
+                "Sharding inner chunk shape %s does not evenly divide the outer chunk size %s",
+                fmt_ints32(inner, n).c_str(), fmt_ints32(m->chunk_shape, n).c_str());
+        return ZH_EDATA;
+      }
+    }
+    if (c.index_location != ZH_INDEX_START && c.index_location != ZH_INDEX_END) {
+      set_err(err, errlen, "Only index_location \"start\" or \"end\" are supported.");
+      return ZH_EDATA;  // ShardingIndexedCodec.java:288-293
+    }
+  }
+  if (c.has_transpose && !is_perm(n, c.transpose_order)) {
+    set_err(err, errlen, "Order is no permutation array");  // TransposeCodec.java:36-38
+    return ZH_EDATA;
+  }
+  int64_t nel = 1;
+  for (int d = 0; d < n; d++) nel *= inner[d];
+  if (nel >= kIntMax) {  // ucar.ma2.Array / Java int limits: one inner chunk < 2^31 elements
+    set_err(err, errlen, "inner chunk of %lld elements exceeds the 2^31 element limit",
+            (long long)nel);
+    return ZH_EUNSUPPORTED;
+  }
+  return ZH_OK;
+}
+
+}  // extern "C"
+
+// =====================================================================================
+// planning
+// =====================================================================================
+namespace {
+
+void fill_common_args(const zh_array_meta* m, const int64_t* region_shape, bool encode,
+                      ScatterArgs& a, int& tile_mode) {
+  const int n = m->ndim;
+  const zh_codec_chain& c = m->chain;
+  const int32_t* inner = c.sharded ? c.inner_chunk_shape : m->chunk_shape;
+  int32_t order[kMaxDims];
+  for (int d = 0; d < n; d++) order[d] = c.has_transpose ? c.transpose_order[d] : d;
+  memset(&a, 0, sizeof(a));
+  a.ndim = n;
+  a.swap = (m->dtype_size > 1 && c.endian == ZH_ENDIAN_BIG) ? 1 : 0;
+  a.is_bool = m->dtype_is_bool ? 1 : 0;
+  a.index_be = c.index_endian == ZH_ENDIAN_BIG ? 1 : 0;
+  a.sharded = c.sharded ? 1 : 0;
+  // payload: C-order over P[j] = inner[order[j]] (TransposeCodec.java:70-71)
+  int64_t st = 1;
+  for (int j = n - 1; j >= 0; j--) {
+    a.pstride[order[j]] = st;
+    st *= inner[order[j]];
+  }
+  st = 1;
+  for (int d = n - 1; d >= 0; d--) {
+    a.rstride[d] = st;
+    st *= region_shape[d];
+  }
+  st = 1;
+  for (int d = n - 1; d >= 0; d--) {
+    a.cps_stride[d] = st;
+    st *= c.sharded ? (m->chunk_shape[d] / inner[d]) : 1;
+  }
+  int64_t nel = 1;
+  for (int d = 0; d < n; d++) {
+    a.inner[d] = inner[d];
+    a.inner_div[d] = make_fastdiv((uint32_t)inner[d]);
+    nel *= inner[d];
+  }
+  for (int d = n; d < kMaxDims; d++) {
+    a.inner[d] = 1;
+    a.inner_div[d] = make_fastdiv(1);
+  }
+  a.inner_nbytes = nel * m->dtype_size;
+  uint64_t f = 0;
+  for (int i = 0; i < 8; i++) f |= (uint64_t)m->fill_value[i] << (8 * i);
+  a.fill = f;
+  if (encode) {
+    a.fs = n - 1;
+    a.fd = order[n - 1];
+  } else {
+    a.fs = order[n - 1];
+    a.fd = n - 1;
+  }
+  tile_mode = a.fs != a.fd;
+  const int64_t piece_kb = std::max(1, env_int("ZH_PIECE_KB", 128));
+  const uint64_t pieces = (uint64_t)((a.inner_nbytes + piece_kb * 1024 - 1) / (piece_kb * 1024));
+  a.piece_shift = (int32_t)next_pow2_shift(std::max<uint64_t>(1, pieces));
+}
+
+int grid_for(const zh_ctx* ctx, int64_t total_items) {
+  const int per_cu = std::max(1, env_int("ZH_BLOCKS_PER_CU", 16));
+  int64_t g = (int64_t)ctx->cu_count * per_cu;
+  return (int)std::max<int64_t>(1, std::min<int64_t>(g, total_items));
+}
+
+template <typename T>
+int dev_alloc(T** p, size_t count, char* err, size_t errlen) {
+  *p = nullptr;
+  if (count == 0) return ZH_OK;
+  hipError_t e = hipMalloc((void**)p, count * sizeof(T));
+  if (e != hipSuccess) {
+    set_err(err, errlen, "hipMalloc(%zu bytes) failed: %s", count * sizeof(T),
+            hipGetErrorString(e));
+    return e == hipErrorOutOfMemory ? ZH_ENOMEM : ZH_EHIP;
+  }
+  return ZH_OK;
+}
+
+void plan_free(zh_plan* p) {
+  if (!p) return;
+  (void)hipSetDevice(p->ctx->device);
+  (void)hipFree(p->d_shards);
+  (void)hipFree(p->d_status);
+  (void)hipFree(p->d_crc_jobs);
+  (void)hipFree(p->d_crc_partials);
+  (void)hipFree(p->d_input);
+  (void)hipFree(p->d_out);
+  for (auto& e : p->ev_pending)
+    for (auto ev : e) p->ev_pool.push_back(ev);
+  for (auto ev : p->ev_pool) (void)hipEventDestroy(ev);
+  delete p;
+}
+
+}  // namespace
+
+extern "C" {
+
+int zh_plan_create(zh_ctx* ctx, const zh_array_meta* m, const zh_chunk_src* chunks,
+                   int64_t nchunks, const int64_t* offset, const int64_t* shape, uint32_t flags,
+                   zh_plan** out, char* err, size_t errlen) {
+  if (!ctx || !m || !offset || !shape || !out) return ZH_EINVAL;
+  *out = nullptr;
+  int st = zh_validate_meta(m, err, errlen);
+  if (st != ZH_OK) return st;
+  const int n = m->ndim;
+  for (int d = 0; d < n; d++) {  // M/core/Array.java:386-390
+    if (offset[d] < 0 || offset[d] + shape[d] > m->shape[d]) {
+      set_err(err, errlen, "Requested data is outside of the array's domain.");
+      return ZH_EDATA;
+    }
+    if (shape[d] <= 0) {
+      set_err(err, errlen, "empty selection at dimension %d", d);
+      return ZH_EINVAL;
+    }
+  }
+  int64_t cstart[kMaxDims], ccount[kMaxDims];
+  const int64_t ncoords = chunk_coords(n, m->chunk_shape, offset, shape, cstart, ccount);
+  if (ncoords > kIntMax) {
+    set_err(err, errlen, "Number of chunks exceeds Integer.MAX_VALUE");
+    return ZH_EARITH;
+  }
+  if (ncoords != nchunks || (nchunks > 0 && !chunks)) {
+    set_err(err, errlen, "expected %lld chunk sources (computeChunkCoords order), got %lld",
+            (long long)ncoords, (long long)nchunks);
+    return ZH_EINVAL;
+  }
+  (void)hipSetDevice(ctx->device);
+  zh_plan* p = new zh_plan();
+  p->ctx = ctx;
+  p->meta = *m;
+  p->flags = flags;
+  p->nshards = ncoords;
+  fill_common_args(m, shape, false, p->args, p->tile_mode);
+  const zh_codec_chain& c = m->chain;
+  const int32_t* inner = c.sharded ? c.inner_chunk_shape : m->chunk_shape;
+  const int64_t isz = zh_shard_index_size(m);
+  std::vector<DevShard> hs(ncoords);
+  std::vector<CrcJob> jobs;
+  p->coords.resize(ncoords * n);
+  int64_t cur[kMaxDims] = {0};
+  int64_t items = 0, staged = 0, in_bytes = 0;
+  std::vector<int64_t> stage_off(ncoords, -1);
+  for (int64_t i = 0; i < ncoords; i++) {
+    int64_t cc[kMaxDims];
+    for (int d = 0; d < n; d++) cc[d] = p->coords[i * n + d] = cstart[d] + cur[d];
+    for (int d = n - 1; d >= 0; d--) {
+      if (++cur[d] < ccount[d]) break;
+      cur[d] = 0;
+    }
+    int32_t co[kMaxDims], oo[kMaxDims], ps[kMaxDims];
+    if (projection(n, cc, m->shape, m->chunk_shape, offset, shape, co, oo, ps) != ZH_OK) {
+      set_err(err, errlen, "projection exceeds Integer.MAX_VALUE");
+      plan_free(p);
+      return ZH_EARITH;
+    }
+    DevShard& S = hs[i];
+    memset(&S, 0, sizeof(S));
+    S.data = (const uint8_t*)chunks[i].data;
+    S.nbytes = chunks[i].nbytes;
+    S.item_begin = items;
+    int64_t ob = 0, nit = 1;
+    for (int d = 0; d < n; d++) {
+      ob += (int64_t)oo[d] * p->args.rstride[d];
+      S.part_lo[d] = co[d];
+      S.part_hi[d] = co[d] + ps[d];
+      // inner-chunk box of the part (ShardingIndexedCodec.java:206-208)
+      const int32_t b0 = co[d] / inner[d], b1 = (co[d] + ps[d] - 1) / inner[d];
+      S.box_start[d] = b0;
+      S.box_count[d] = b1 - b0 + 1;
+      nit *= S.box_count[d];
+    }
+    for (int d = n; d < kMaxDims; d++) {
+      S.box_count[d] = 1;
+      S.part_hi[d] = 1;
+    }
+    S.out_base = ob;
+    items += nit;
+    if (S.data) {
+      if (c.sharded) {
+        if (S.nbytes < isz) {
+          set_err(err, errlen, "Shard %s of %lld bytes is smaller than its index (%lld bytes).",
+                  fmt_ints(cc, n).c_str(), (long long)S.nbytes, (long long)isz);
+          plan_free(p);
+          return ZH_EDATA;
+        }
+        S.index_off = c.index_location == ZH_INDEX_START ? 0 : S.nbytes - isz;
+      } else if (S.nbytes != p->args.inner_nbytes) {  // Q12 (knowing divergence)
+        set_err(err, errlen,
+                "unexpected inner chunk byte length: %lld (expected %lld) for chunk %s",
+                (long long)S.nbytes, (long long)p->args.inner_nbytes, fmt_ints(cc, n).c_str());
+        plan_free(p);
+        return ZH_EDATA;
+      }
+      in_bytes += S.nbytes;
+      if (!(flags & ZH_SRC_DEVICE)) {
+        stage_off[i] = staged;
+        staged += (S.nbytes + 255) & ~(int64_t)255;
+      }
+    }
+  }
+  p->n_items = items;
+  p->in_bytes = in_bytes;
+  int64_t onel = 1;
+  for (int d = 0; d < n; d++) onel *= shape[d];
+  p->out_bytes = onel * m->dtype_size;
+  // stage host sources
+  if (staged > 0) {
+    st = dev_alloc(&p->d_input, (size_t)staged, err, errlen);
+    if (st != ZH_OK) {
+      plan_free(p);
+      return st;
+    }
+    for (int64_t i = 0; i < ncoords; i++) {
+      if (stage_off[i] < 0) continue;
+      p->h2d.push_back({stage_off[i], hs[i].data});
+      p->h2d_len.push_back(hs[i].nbytes);
+      hs[i].data = p->d_input + stage_off[i];
+    }
+  }
+  // CRC jobs over the device copies of the indexes
+  if (c.sharded && c.index_has_crc32c) {
+    int64_t spans = 0;
+    for (int64_t i = 0; i < ncoords; i++) {
+      if (!hs[i].data) continue;
+      CrcJob J;
+      J.base = hs[i].data + hs[i].index_off;
+      J.len = isz - 4;
+      J.span_begin = spans;
+      J.shard = (int32_t)i;
+      J.pad = 0;
+      spans += (J.len + kCrcSpan - 1) / kCrcSpan;
+      jobs.push_back(J);
+    }
+    p->n_crc_jobs = (int64_t)jobs.size();
+    p->n_crc_spans = spans;
+  }
+  if ((st = dev_alloc(&p->d_shards, hs.size(), err, errlen)) != ZH_OK ||
+      (st = dev_alloc(&p->d_status, (size_t)ncoords * kStWords, err, errlen)) != ZH_OK ||
+      (st = dev_alloc(&p->d_crc_jobs, jobs.size(), err, errlen)) != ZH_OK ||
+      (st = dev_alloc(&p->d_crc_partials, (size_t)p->n_crc_spans, err, errlen)) != ZH_OK) {
+    plan_free(p);
+    return st;
+  }
+  if (!(flags & ZH_OUT_DEVICE)) {
+    if ((st = dev_alloc(&p->d_out, (size_t)p->out_bytes, err, errlen)) != ZH_OK) {
+      plan_free(p);
+      return st;
+    }
+  }
+  hipError_t e = hipMemcpy(p->d_shards, hs.data(), hs.size() * sizeof(DevShard),
+                           hipMemcpyHostToDevice);
+  if (e == hipSuccess && !jobs.empty())
+    e = hipMemcpy(p->d_crc_jobs, jobs.data(), jobs.size() * sizeof(CrcJob), hipMemcpyHostToDevice);
+  if (e != hipSuccess) {
+    set_err(err, errlen, "plan upload failed: %s", hipGetErrorString(e));
+    plan_free(p);
+    return ZH_EHIP;
+  }
+  p->args.shards = p->d_shards;
+  p->args.nshards = ncoords;
+  p->args.total_items = items << p->args.piece_shift;
+  p->args.status = p->d_status;
+  p->grid = grid_for(ctx, p->args.total_items);
+  *out = p;
+  return ZH_OK;
+}
+
+int zh_plan_execute(zh_plan* p, void* out, void* stream_v) {
+  if (!p || !out) return ZH_EINVAL;
+  char* err = nullptr;
+  size_t errlen = 0;
+  hipStream_t s = stream_v ? (hipStream_t)stream_v : p->ctx->stream;
+  (void)hipSetDevice(p->ctx->device);
+  for (size_t k = 0; k < p->h2d.size(); k++)
+    ZH_HIP(hipMemcpyAsync(p->d_input + p->h2d[k].first, p->h2d[k].second, (size_t)p->h2d_len[k],
+                          hipMemcpyHostToDevice, s));
+  ZH_HIP(hipMemsetAsync(p->d_status, 0, (size_t)p->nshards * kStWords * sizeof(uint64_t), s));
+  std::array<hipEvent_t, 3> ev{};
+  if (p->timing) {
+    for (int k = 0; k < 3; k++) {
+      if (p->ev_pool.empty()) {
+        hipEvent_t e;
+        ZH_HIP(hipEventCreate(&e));
+        p->ev_pool.push_back(e);
+      }
+      ev[k] = p->ev_pool.back();
+      p->ev_pool.pop_back();
+    }
+    ZH_HIP(hipEventRecord(ev[0], s));
+  }
+  ZH_HIP(launch_crc(p->d_crc_jobs, p->n_crc_jobs, p->n_crc_spans, p->d_crc_partials, p->d_status,
+                    s));
+  if (p->timing) ZH_HIP(hipEventRecord(ev[1], s));
+  ScatterArgs a = p->args;
+  a.region = (p->flags & ZH_OUT_DEVICE) ? (uint8_t*)out : p->d_out;
+  ZH_HIP(launch_scatter(a, p->meta.dtype_size, p->tile_mode, 0, p->grid, s));
+  if (p->timing) {
+    ZH_HIP(hipEventRecord(ev[2], s));
+    p->ev_pending.push_back(ev);
+  }
+  if (!(p->flags & ZH_OUT_DEVICE))
+    ZH_HIP(hipMemcpyAsync(out, p->d_out, (size_t)p->out_bytes, hipMemcpyDeviceToHost, s));
+  p->last_stream = s;
+  return ZH_OK;
+}
+
+int zh_plan_wait(zh_plan* p, char* err, size_t errlen) {
+  if (!p) return ZH_EINVAL;
+  (void)hipSetDevice(p->ctx->device);
+  if (p->last_stream) ZH_HIP(hipStreamSynchronize(p->last_stream));
+  std::vector<uint64_t> stv((size_t)p->nshards * kStWords);
+  if (!stv.empty())
+    ZH_HIP(hipMemcpy(stv.data(), p->d_status, stv.size() * sizeof(uint64_t),
+                     hipMemcpyDeviceToHost));
+  const int n = p->meta.ndim;
+  for (int64_t i = 0; i < p->nshards; i++) {
+    const uint64_t* w = &stv[i * kStWords];
+    if (!w[kStFlags]) continue;
+    if (w[kStFlags] & kFlagCrc) {  // Crc32cCodec.java:39-44 (signed ints)
+      set_err(err, errlen, "The checksum of the sharding index is invalid. Stored: %d Computed: %d",
+              (int32_t)(uint32_t)w[kStCrcStored], (int32_t)(uint32_t)w[kStCrcComputed]);
+      return ZH_EDATA;
+    }
+    const uint64_t key = w[kStBadChunk];
+    const uint32_t lin = 0xFFFFFFFFu - (uint32_t)(key >> 8);
+    const uint32_t kind = (uint32_t)(key & 0xFF);
+    int64_t ic[kMaxDims];
+    uint32_t r = lin;
+    for (int d = n - 1; d >= 0; d--) {
+      const int32_t cps = p->meta.chunk_shape[d] / p->meta.chain.inner_chunk_shape[d];
+      ic[d] = r % cps;
+      r /= cps;
+    }
+    if (kind == kFlagRange)  // ShardingIndexedCodec.java:227-230
+      set_err(err, errlen, "Could not load byte data for chunk %s", fmt_ints(ic, n).c_str());
+    else
+      set_err(err, errlen, "unexpected inner chunk byte length for chunk %s",
+              fmt_ints(ic, n).c_str());
+    return ZH_EDATA;
+  }
+  return ZH_OK;
+}
+
+void zh_plan_destroy(zh_plan* p) { plan_free(p); }
+
+int zh_plan_stats(const zh_plan* p, int64_t* in_bytes, int64_t* out_bytes, int64_t* items,
+                  int64_t* nshards) {
+  if (!p) return ZH_EINVAL;
+  if (in_bytes) *in_bytes = p->in_bytes;
+  if (out_bytes) *out_bytes = p->out_bytes;
+  if (items) *items = p->n_items;
+  if (nshards) *nshards = p->nshards;
+  return ZH_OK;
+}
+
+int zh_plan_set_timing(zh_plan* p, int enable) {
+  if (!p) return ZH_EINVAL;
+  p->timing = enable != 0;
+  return ZH_OK;
+}
+
+int zh_plan_kernel_time(zh_plan* p, double* scatter_ms, int64_t* launches, double* index_ms) {
+  if (!p) return ZH_EINVAL;
+  char* err = nullptr;
+  size_t errlen = 0;
+  (void)hipSetDevice(p->ctx->device);
+  double sc = 0, ix = 0;
+  for (auto& e : p->ev_pending) {
+    ZH_HIP(hipEventSynchronize(e[2]));
+    float a = 0, b = 0;
+    ZH_HIP(hipEventElapsedTime(&a, e[0], e[1]));
+    ZH_HIP(hipEventElapsedTime(&b, e[1], e[2]));
+    ix += a;
+    sc += b;
+  }
+  if (scatter_ms) *scatter_ms = sc;
+  if (index_ms) *index_ms = ix;
+  if (launches) *launches = (int64_t)p->ev_pending.size();
+  for (auto& e : p->ev_pending)
+    for (auto ev : e) p->ev_pool.push_back(ev);
+  p->ev_pending.clear();
+  return ZH_OK;
+}
+
+int zh_array_read(zh_ctx* ctx, const zh_array_meta* meta, const zh_chunk_src* chunks,
+                  int64_t nchunks, const int64_t* offset, const int64_t* shape, void* out,
+                  uint32_t flags, void* stream, char* err, size_t errlen) {
+  if (!ctx) return ZH_EINVAL;
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  zh_plan* p = nullptr;
+  int st = zh_plan_create(ctx, meta, chunks, nchunks, offset, shape, flags, &p, err, errlen);
+  if (st != ZH_OK) return st;
+  st = zh_plan_execute(p, out, stream);
+  if (st != ZH_OK) {
+    set_err(err, errlen, "kernel launch failed");
+    plan_free(p);
+    return st;
+  }
+  st = zh_plan_wait(p, err, errlen);
+  plan_free(p);
+  return st;
+}
+
+// ShardingIndexedCodec.decode / decodePartial: one shard viewed as a one-chunk array.
+int zh_sharding_decode_partial(zh_ctx* ctx, const zh_array_meta* meta, const void* shard,
+                               int64_t nbytes, const int64_t* offset, const int32_t* shape,
+                               void* out, uint32_t flags, void* stream, char* err,
+                               size_t errlen) {
+  if (!meta || !shard || !offset || !shape) return ZH_EINVAL;
+  if (!meta->chain.sharded) {
+    set_err(err, errlen, "meta does not describe a sharding_indexed chain");
+    return ZH_EINVAL;
+  }
+  zh_array_meta sm = *meta;
+  for (int d = 0; d < meta->ndim; d++) sm.shape[d] = meta->chunk_shape[d];
+  int64_t shp[kMaxDims];
+  for (int d = 0; d < meta->ndim; d++) shp[d] = shape[d];
+  zh_chunk_src src{shard, nbytes};
+  return zh_array_read(ctx, &sm, &src, 1, offset, shp, out, flags, stream, err, errlen);
+}
+
+int zh_sharding_decode(zh_ctx* ctx, const zh_array_meta* meta, const void* shard, int64_t nbytes,
+                       void* out, uint32_t flags, void* stream, char* err, size_t errlen) {
+  if (!meta) return ZH_EINVAL;
+  int64_t off[kMaxDims] = {0};
+  return zh_sharding_decode_partial(ctx, meta, shard, nbytes, off, meta->chunk_shape, out, flags,
+                                    stream, err, errlen);
+}
+
+// =====================================================================================
+// write path
+// =====================================================================================
+int64_t zh_array_encoded_bound(const zh_array_meta* m) {
+  if (!m) return -1;
+  int64_t nel = 1;
+  for (int d = 0; d < m->ndim; d++) nel *= m->chunk_shape[d];
+  return nel * m->dtype_size + (m->chain.sharded ? zh_shard_index_size(m) : 0);
+}
+
+int zh_array_write(zh_ctx* ctx, const zh_array_meta* m, const void* src, const int64_t* offset,
+                   const int64_t* shape, zh_chunk_dst* dsts, int64_t nchunks, void* stream_v,
+                   char* err, size_t errlen) {
+  if (!ctx || !m || !src || !offset || !shape) return ZH_EINVAL;
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  int st = zh_validate_meta(m, err, errlen);
+  if (st != ZH_OK) return st;
+  const int n = m->ndim;
+  for (int d = 0; d < n; d++) {
+    if (offset[d] < 0 || offset[d] + shape[d] > m->shape[d]) {
+      set_err(err, errlen, "Requested data is outside of the array's domain.");
+      return ZH_EDATA;
+    }
+    const int64_t e = offset[d] + shape[d];
+    if (shape[d] <= 0 || offset[d] % m->chunk_shape[d] != 0 ||
+        (e % m->chunk_shape[d] != 0 && e != m->shape[d])) {
+      set_err(err, errlen, "region does not cover whole chunks (host read-modify-write needed)");
+      return ZH_EUNSUPPORTED;
+    }
+  }
+  int64_t cstart[kMaxDims], ccount[kMaxDims];
+  const int64_t ncoords = chunk_coords(n, m->chunk_shape, offset, shape, cstart, ccount);
+  if (ncoords != nchunks || !dsts) {
+    set_err(err, errlen, "expected %lld chunk destinations", (long long)ncoords);
+    return ZH_EINVAL;
+  }
+  (void)hipSetDevice(ctx->device);
+  hipStream_t s = stream_v ? (hipStream_t)stream_v : ctx->stream;
+  ScatterArgs a;
+  int tile_mode = 0;
+  fill_common_args(m, shape, true, a, tile_mode);
+  const zh_codec_chain& c = m->chain;
+  const int32_t* inner = c.sharded ? c.inner_chunk_shape : m->chunk_shape;
+  std::vector<DevShard> hs(ncoords);
+  int64_t cur[kMaxDims] = {0};
+  int64_t items = 0;
+  int64_t cps_total = 1;
+  for (int d = 0; d < n; d++) cps_total *= m->chunk_shape[d] / inner[d];
+  for (int64_t i = 0; i < ncoords; i++) {
+    int64_t cc[kMaxDims];
+    for (int d = 0; d < n; d++) cc[d] = cstart[d] + cur[d];
+    for (int d = n - 1; d >= 0; d--) {
+      if (++cur[d] < ccount[d]) break;
+      cur[d] = 0;
+    }
+    int32_t co[kMaxDims], oo[kMaxDims], ps[kMaxDims];
+    projection(n, cc, m->shape, m->chunk_shape, offset, shape, co, oo, ps);
+    DevShard& S = hs[i];
+    memset(&S, 0, sizeof(S));
+    S.wdata = (uint8_t*)dsts[i].data;
+    S.item_begin = items;
+    int64_t ob = 0;
+    for (int d = 0; d < n; d++) {
+      ob += (int64_t)oo[d] * a.rstride[d];
+      S.part_lo[d] = co[d];
+      S.part_hi[d] = co[d] + ps[d];
+      S.box_start[d] = 0;
+      S.box_count[d] = m->chunk_shape[d] / inner[d];
+    }
+    for (int d = n; d < kMaxDims; d++) {
+      S.box_count[d] = 1;
+      S.part_hi[d] = 1;
+    }
+    S.out_base = ob;
+    items += c.sharded ? cps_total : 1;
+  }
+  const int64_t pitems = items << a.piece_shift;
+  DevShard* d_shards = nullptr;
+  uint8_t* d_flags = nullptr;
+  int64_t* d_off = nullptr;
+  auto cleanup = [&]() {
+    (void)hipFree(d_shards);
+    (void)hipFree(d_flags);
+    (void)hipFree(d_off);
+  };
+  if ((st = dev_alloc(&d_shards, hs.size(), err, errlen)) != ZH_OK ||
+      (st = dev_alloc(&d_flags, (size_t)pitems, err, errlen)) != ZH_OK ||
+      (st = dev_alloc(&d_off, (size_t)items, err, errlen)) != ZH_OK) {
+    cleanup();
+    return st;
+  }
+#define ZH_HIPC(call)                                                                      \
+  do {                                                                                     \
+    hipError_t e_ = (call);                                                                \
+    if (e_ != hipSuccess) {                                                                \
+      set_err(err, errlen, "HIP error %s (%s)", hipGetErrorName(e_), hipGetErrorString(e_)); \
+      cleanup();                                                                           \
+      return ZH_EHIP;                                                                      \
+    }                                                                                      \
+  } while (0)
+  ZH_HIPC(hipMemcpy(d_shards, hs.data(), hs.size() * sizeof(DevShard), hipMemcpyHostToDevice));
+  a.shards = d_shards;
+  a.nshards = ncoords;
+  a.total_items = pitems;
+  a.region = (uint8_t*)src;
+  a.flags = d_flags;
+  a.item_off = nullptr;
+  const int grid = grid_for(ctx, pitems);
+  ZH_HIPC(launch_flags(a, m->dtype_size, grid, s));
+  std::vector<uint8_t> hflags((size_t)pitems);
+  ZH_HIPC(hipMemcpyAsync(hflags.data(), d_flags, (size_t)pitems, hipMemcpyDeviceToHost, s));
+  ZH_HIPC(hipStreamSynchronize(s));
+  // layout: C-order over the non-fill inner chunks (deterministic)
+  const int64_t isz = c.sharded ? zh_shard_index_size(m) : 0;
+  const int start = c.sharded && c.index_location == ZH_INDEX_START;
+  const int big = c.index_endian == ZH_ENDIAN_BIG;
+  std::vector<int64_t> hoff((size_t)items, -1);
+  std::vector<std::vector<uint8_t>> indexes(ncoords);
+  const int64_t np = 1ll << a.piece_shift;
+  for (int64_t i = 0; i < ncoords; i++) {
+    const int64_t nit = c.sharded ? cps_total : 1;
+    const int64_t b = hs[i].item_begin;
+    int64_t payload = 0, nonfill = 0;
+    std::vector<uint8_t>& idx = indexes[i];
+    if (c.sharded) idx.assign((size_t)isz, 0);
+    for (int64_t k = 0; k < nit; k++) {
+      bool any = false;
+      for (int64_t q = 0; q < np; q++) any |= hflags[(size_t)(((b + k) << a.piece_shift) + q)] != 0;
+      uint64_t eo = ~0ull, en = ~0ull;
+      if (any) {
+        hoff[b + k] = (start ? isz : 0) + payload;
+        eo = (uint64_t)hoff[b + k];
+        en = (uint64_t)a.inner_nbytes;
+        payload += a.inner_nbytes;
+        nonfill++;
+      }
+      if (c.sharded) {
+        for (int byte = 0; byte < 8; byte++) {
+          const int sh = big ? 56 - 8 * byte : 8 * byte;
+          idx[16 * k + byte] = (uint8_t)(eo >> sh);
+          idx[16 * k + 8 + byte] = (uint8_t)(en >> sh);
+        }
+      }
+    }
+    if (nonfill == 0) {  // all fill → writeChunk deletes the key (M/core/Array.java:150-151)
+      dsts[i].nbytes = 0;
+      continue;
+    }
+    const int64_t total = payload + isz;
+    if (total > dsts[i].capacity || !dsts[i].data) {
+      set_err(err, errlen, "chunk destination %lld too small: need %lld bytes, have %lld",
+              (long long)i, (long long)total, (long long)dsts[i].capacity);
+      cleanup();
+      return ZH_EINVAL;
+    }
+    dsts[i].nbytes = total;
+    if (c.sharded) {
+      if (c.index_has_crc32c) {  // Crc32cCodec.encode :50-60
+        const uint32_t crc = crc32c_host(0, idx.data(), (size_t)(isz - 4));
+        for (int byte = 0; byte < 4; byte++) idx[isz - 4 + byte] = (uint8_t)(crc >> (8 * byte));
+      }
+      uint8_t* dst = (uint8_t*)dsts[i].data + (start ? 0 : payload);
+      ZH_HIPC(hipMemcpyAsync(dst, idx.data(), (size_t)isz, hipMemcpyHostToDevice, s));
+    }
+  }
+  ZH_HIPC(hipMemcpyAsync(d_off, hoff.data(), (size_t)items * sizeof(int64_t),
+                         hipMemcpyHostToDevice, s));
+  a.item_off = d_off;
+  a.flags = nullptr;
+  ZH_HIPC(launch_scatter(a, m->dtype_size, tile_mode, 1, grid, s));
+  ZH_HIPC(hipStreamSynchronize(s));
+  cleanup();
+#undef ZH_HIPC
+  return ZH_OK;
+}
+
+// =====================================================================================
+// plumbing
+// =====================================================================================
+int zh_device_malloc(zh_ctx* ctx, size_t bytes, void** out) {
+  if (!ctx || !out) return ZH_EINVAL;
+  (void)hipSetDevice(ctx->device);
+  hipError_t e = hipMalloc(out, bytes);
+  return e == hipSuccess ? ZH_OK : (e == hipErrorOutOfMemory ? ZH_ENOMEM : ZH_EHIP);
+}
+int zh_device_free(zh_ctx* ctx, void* ptr) {
+  if (!ctx) return ZH_EINVAL;
+  (void)hipSetDevice(ctx->device);
+  return hipFree(ptr) == hipSuccess ? ZH_OK : ZH_EHIP;
+}
+int zh_host_malloc_pinned(zh_ctx* ctx, size_t bytes, void** out) {
+  if (!ctx || !out) return ZH_EINVAL;
+  (void)hipSetDevice(ctx->device);
+  return hipHostMalloc(out, bytes, hipHostMallocDefault) == hipSuccess ? ZH_OK : ZH_ENOMEM;
+}
+int zh_host_free_pinned(zh_ctx* ctx, void* ptr) {
+  if (!ctx) return ZH_EINVAL;
+  return hipHostFree(ptr) == hipSuccess ? ZH_OK : ZH_EHIP;
+}
+int zh_memcpy_async(zh_ctx* ctx, void* dst, const void* src, size_t bytes, int kind,
+                    void* stream) {
+  if (!ctx) return ZH_EINVAL;
+  (void)hipSetDevice(ctx->device);
+  hipMemcpyKind k = kind == 0 ? hipMemcpyHostToDevice
+                              : (kind == 1 ? hipMemcpyDeviceToHost : hipMemcpyDeviceToDevice);
+  hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
+  return hipMemcpyAsync(dst, src, bytes, k, s) == hipSuccess ? ZH_OK : ZH_EHIP;
+}
+int zh_memset_async(zh_ctx* ctx, void* dst, int value, size_t bytes, void* stream) {
+  if (!ctx) return ZH_EINVAL;
+  (void)hipSetDevice(ctx->device);
+  hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
+  return hipMemsetAsync(dst, value, bytes, s) == hipSuccess ? ZH_OK : ZH_EHIP;
+}
+int zh_stream_synchronize(zh_ctx* ctx, void* stream) {
+  if (!ctx) return ZH_EINVAL;
+  (void)hipSetDevice(ctx->device);
+  hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
+  return hipStreamSynchronize(s) == hipSuccess ? ZH_OK : ZH_EHIP;
+}
+int zh_event_create(zh_ctx* ctx, void** ev) {
+  if (!ctx || !ev) return ZH_EINVAL;
+  (void)hipSetDevice(ctx->device);
+  return hipEventCreate((hipEvent_t*)ev) == hipSuccess ? ZH_OK : ZH_EHIP;
+}
+int zh_event_destroy(zh_ctx* ctx, void* ev) {
+  if (!ctx) return ZH_EINVAL;
+  return hipEventDestroy((hipEvent_t)ev) == hipSuccess ? ZH_OK : ZH_EHIP;
+}
+int zh_event_record(zh_ctx* ctx, void* ev, void* stream) {
+  if (!ctx) return ZH_EINVAL;
+  hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
+  return hipEventRecord((hipEvent_t)ev, s) == hipSuccess ? ZH_OK : ZH_EHIP;
+}
+int zh_event_elapsed_ms(zh_ctx* ctx, void* start, void* stop, float* ms) {
+  if (!ctx || !ms) return ZH_EINVAL;
+  if (hipEventSynchronize((hipEvent_t)stop) != hipSuccess) return ZH_EHIP;
+  return hipEventElapsedTime(ms, (hipEvent_t)start, (hipEvent_t)stop) == hipSuccess ? ZH_OK
+                                                                                    : ZH_EHIP;
+}
+int zh_device_info(zh_ctx* ctx, char* name, size_t namelen, int64_t* total_mem, int* cu_count,
+                   char* arch, size_t archlen) {
+  if (!ctx) return ZH_EINVAL;
+  hipDeviceProp_t p;
+  if (hipGetDeviceProperties(&p, ctx->device) != hipSuccess) return ZH_EHIP;
+  if (name && namelen) snprintf(name, namelen, "%s", p.name);
+  if (arch && archlen) snprintf(arch, archlen, "%s", p.gcnArchName);
+  if (total_mem) *total_mem = (int64_t)p.totalGlobalMem;
+  if (cu_count) *cu_count = p.multiProcessorCount;
+  return ZH_OK;
+}
+
+int zh_synth_fill(zh_ctx* ctx, void* dst, int64_t n, int dtype_size, int64_t first,
+                  uint64_t seed, void* stream) {
+  if (!ctx || !dst) return ZH_EINVAL;
+  (void)hipSetDevice(ctx->device);
+  hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
+  return launch_synth_fill(dst, n, dtype_size, first, seed, s) == hipSuccess ? ZH_OK : ZH_EHIP;
+}
+
+int zh_synth_verify(zh_ctx* ctx, const void* region, int ndim, const int64_t* array_shape,
+                    const int64_t* offset, const int64_t* shape, int dtype_size, uint64_t seed,
+                    uint64_t* mismatches, void* stream) {
+  if (!ctx || !region || !mismatches || ndim <= 0 || ndim > kMaxDims) return ZH_EINVAL;
+  (void)hipSetDevice(ctx->device);
+  hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
+  unsigned long long* d = nullptr;
+  if (hipMalloc((void**)&d, sizeof(*d)) != hipSuccess) return ZH_ENOMEM;
+  int rc = ZH_OK;
+  if (hipMemsetAsync(d, 0, sizeof(*d), s) != hipSuccess ||
+      launch_synth_verify(region, ndim, array_shape, offset, shape, dtype_size, seed, d, s) !=
+          hipSuccess ||
+      hipMemcpyAsync(mismatches, d, sizeof(*d), hipMemcpyDeviceToHost, s) != hipSuccess ||
+      hipStreamSynchronize(s) != hipSuccess)
+    rc = ZH_EHIP;
+  (void)hipFree(d);
+  return rc;
+}
+
+}  // extern "C"

@@ -1,0 +1,105 @@
+// zh_internal.h — structures shared by the host planner (zh_engine.cpp) and the HIP
+// kernels (zh_kernels.hip).  Not part of the public ABI.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/zarrhip.h"
+
+namespace zh {
+
+constexpr int kMaxDims = ZH_MAX_DIMS;
+constexpr int kBlock = 256;            // threads per workgroup (4 waves of 64)
+constexpr int kTileTPB = 4;            // 32x32 transpose tiles per workgroup iteration
+constexpr int kCrcSpan = 64 * 1024;    // index bytes hashed per CRC workgroup
+constexpr int kCrcLane = kCrcSpan / kBlock;  // 256 bytes per lane
+
+// Per-shard status words (device, uint64 each), read back by zh_plan_wait.
+enum : uint32_t { kStFlags = 0, kStCrcStored = 1, kStCrcComputed = 2, kStBadChunk = 3,
+                  kStWords = 4 };
+enum : uint32_t { kFlagCrc = 1u, kFlagRange = 2u, kFlagLength = 4u };
+
+// Exact floor(n / d) for 0 <= n < 2^31, 1 <= d < 2^31 (Granlund–Montgomery round-up
+// method with N = 31): q = (n * m) >> s.
+struct FastDiv {
+  uint64_t m;
+  uint32_t s;
+  uint32_t d;
+};
+
+__host__ __device__ inline FastDiv make_fastdiv(uint32_t d) {
+  uint32_t l = 0;
+  while ((1ull << l) < (uint64_t)d) l++;
+  FastDiv f;
+  f.d = d;
+  f.s = 31 + l;
+  f.m = ((1ull << (31 + l)) / d) + 1;
+  return f;
+}
+
+__host__ __device__ inline uint32_t fdiv(uint32_t n, const FastDiv& f) {
+  return (uint32_t)(((uint64_t)n * f.m) >> f.s);
+}
+
+// One stored chunk object (a shard when sharded) touched by a region.
+struct DevShard {
+  const uint8_t* data;      // decode: encoded bytes (nullptr: key missing → fill_value)
+  uint8_t* wdata;           // encode: destination buffer
+  int64_t nbytes;           // decode: object size
+  int64_t index_off;        // decode (sharded): byte offset of the index entries
+  int64_t item_begin;       // prefix sum of inner-chunk items before this shard
+  int64_t out_base;         // element offset of part_lo inside the region buffer
+  int32_t box_start[kMaxDims];  // first inner-chunk coordinate of the box
+  int32_t box_count[kMaxDims];  // inner chunks per dim in the box
+  int32_t part_lo[kMaxDims];    // requested part of the shard (shard-local coords)
+  int32_t part_hi[kMaxDims];
+};
+
+// Uniform launch arguments of the decode/encode scatter kernels.
+struct ScatterArgs {
+  const DevShard* shards;
+  int64_t nshards;
+  int64_t total_items;      // (inner chunks) << piece_shift
+  uint8_t* region;          // decode: output region; encode: source region (C order)
+  uint64_t* status;         // decode: kStWords u64 per shard
+  const int64_t* item_off;  // encode: payload byte offset per inner-chunk item (-1 = skip)
+  uint8_t* flags;           // encode flag pass: 1 = item has a non-fill element
+  int32_t ndim;
+  int32_t swap;             // byte-swap elements (big-endian bytes codec, dtype > 1 byte)
+  int32_t is_bool;          // normalise bool bytes to 0/1
+  int32_t piece_shift;      // items per inner chunk = 1 << piece_shift
+  int32_t fs;               // src-fast dim (decoded-dim index)
+  int32_t fd;               // dst-fast dim
+  int32_t index_be;         // shard index stored big-endian
+  int32_t sharded;
+  int32_t inner[kMaxDims];      // decoded inner chunk shape
+  int64_t pstride[kMaxDims];    // payload element stride of each decoded dim
+  int64_t rstride[kMaxDims];    // region element stride of each dim
+  int64_t cps_stride[kMaxDims]; // index entry stride of each inner-chunk coordinate
+  int64_t inner_nbytes;
+  uint64_t fill;                // fill_value bytes (little-endian), replicated as needed
+  FastDiv inner_div[kMaxDims];  // divisors for unclipped extents
+};
+
+struct CrcJob {
+  const uint8_t* base;      // first index byte (device)
+  int64_t len;              // bytes under the CRC (16 * entries)
+  int64_t span_begin;       // prefix sum of spans
+  int32_t shard;            // status slot
+  int32_t pad;
+};
+
+// Kernel launchers (zh_kernels.hip).
+hipError_t launch_crc(const CrcJob* jobs, int64_t njobs, int64_t nspans, uint32_t* partials,
+                      uint64_t* status, hipStream_t stream);
+hipError_t launch_scatter(const ScatterArgs& a, int dsize, int tile_mode, int encode, int grid,
+                          hipStream_t stream);
+hipError_t launch_flags(const ScatterArgs& a, int dsize, int grid, hipStream_t stream);
+hipError_t launch_synth_fill(void* dst, int64_t n, int dsize, int64_t first, uint64_t seed,
+                             hipStream_t stream);
+hipError_t launch_synth_verify(const void* region, int ndim, const int64_t* array_shape,
+                               const int64_t* offset, const int64_t* shape, int dsize,
+                               uint64_t seed, unsigned long long* d_count, hipStream_t stream);
+
+}  // namespace zh

@@ -1,0 +1,893 @@
+// zh_kernels.hip — hand-written CDNA4 (gfx950) kernels of the Zarr v3 chunk codec path.
+//
+//   crc_partial / crc_finalize   sharding index CRC-32C (Crc32cCodec.decode,
+//                                M/v3/codec/core/Crc32cCodec.java:24-48; CRC32C.java:119-125):
+//                                per-lane slicing-by-8 segment CRCs combined in GF(2)
+//   scatter<DS,ENC,TILE>         the per-inner-chunk codec chain + region scatter
+//                                (ShardingIndexedCodec.decodeInternal :183-243, BytesCodec.decode,
+//                                TransposeCodec.decode, MultiArrayUtils.copyRegion) and, with
+//                                ENC, the inverse (ShardingIndexedCodec.encode payload writes)
+//   flags                        encode pre-pass: inner chunk all fill_value? (:129-133)
+//   synth_fill / synth_verify    synthetic data for the bench and full-size property tests
+//
+// Everything is byte movement: HBM-bound.  The scatter kernel streams each inner chunk
+// with 16-byte per-lane loads/stores (1 KiB per wave instruction); the transpose variant
+// stages 32x32-element tiles through padded LDS so that both the read (payload-fast
+// axis) and the write (region-fast axis) are whole 128-byte rows.
+#include <hip/hip_runtime.h>
+
+#include "zh_internal.h"
+
+namespace zh {
+
+// ---------------------------------------------------------------------------------
+// element helpers
+// ---------------------------------------------------------------------------------
+template <int DS> struct ElemT;
+template <> struct ElemT<1> { using T = uint8_t; };
+template <> struct ElemT<2> { using T = uint16_t; };
+template <> struct ElemT<4> { using T = uint32_t; };
+template <> struct ElemT<8> { using T = uint64_t; };
+
+template <int DS>
+__device__ __forceinline__ typename ElemT<DS>::T xform1(typename ElemT<DS>::T v, int swap,
+                                                         int is_bool) {
+  if constexpr (DS == 1) {
+    (void)swap;
+    return is_bool ? (uint8_t)(v != 0) : v;
+  } else if constexpr (DS == 2) {
+    (void)is_bool;
+    return swap ? (uint16_t)((v >> 8) | (v << 8)) : v;
+  } else if constexpr (DS == 4) {
+    (void)is_bool;
+    return swap ? __builtin_bswap32(v) : v;
+  } else {
+    (void)is_bool;
+    return swap ? __builtin_bswap64(v) : v;
+  }
+}
+
+__device__ __forceinline__ uint32_t bool_bytes(uint32_t x) {
+  // per byte: 1 if non-zero, else 0
+  uint32_t t = ((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x;
+  return (t >> 7) & 0x01010101u;
+}
+
+template <int DS>
+__device__ __forceinline__ uint4 xform16(uint4 v, int swap, int is_bool) {
+  if constexpr (DS == 1) {
+    (void)swap;
+    if (is_bool) {
+      v.x = bool_bytes(v.x);
+      v.y = bool_bytes(v.y);
+      v.z = bool_bytes(v.z);
+      v.w = bool_bytes(v.w);
+    }
+    return v;
+  } else if constexpr (DS == 2) {
+    (void)is_bool;
+    if (swap) {
+      v.x = ((v.x & 0x00FF00FFu) << 8) | ((v.x >> 8) & 0x00FF00FFu);
+      v.y = ((v.y & 0x00FF00FFu) << 8) | ((v.y >> 8) & 0x00FF00FFu);
+      v.z = ((v.z & 0x00FF00FFu) << 8) | ((v.z >> 8) & 0x00FF00FFu);
+      v.w = ((v.w & 0x00FF00FFu) << 8) | ((v.w >> 8) & 0x00FF00FFu);
+    }
+    return v;
+  } else if constexpr (DS == 4) {
+    (void)is_bool;
+    if (swap) {
+      v.x = __builtin_bswap32(v.x);
+      v.y = __builtin_bswap32(v.y);
+      v.z = __builtin_bswap32(v.z);
+      v.w = __builtin_bswap32(v.w);
+    }
+    return v;
+  } else {
+    (void)is_bool;
+    if (swap) {
+      uint4 r;
+      r.x = __builtin_bswap32(v.y);
+      r.y = __builtin_bswap32(v.x);
+      r.z = __builtin_bswap32(v.w);
+      r.w = __builtin_bswap32(v.z);
+      return r;
+    }
+    return v;
+  }
+}
+
+template <int DS>
+__device__ __forceinline__ uint4 fill16(uint64_t f) {
+  uint32_t lo = (uint32_t)f, hi = (uint32_t)(f >> 32);
+  uint32_t w;
+  if constexpr (DS == 1) {
+    w = (lo & 0xFFu) * 0x01010101u;
+  } else if constexpr (DS == 2) {
+    w = (lo & 0xFFFFu) * 0x00010001u;
+  } else {
+    w = lo;
+  }
+  if constexpr (DS == 8) return make_uint4(lo, hi, lo, hi);
+  return make_uint4(w, w, w, w);
+}
+
+__device__ __forceinline__ uint4 ld16(const uint8_t* p) {
+  return *reinterpret_cast<const uint4*>(p);
+}
+__device__ __forceinline__ void st16(uint8_t* p, uint4 v) { *reinterpret_cast<uint4*>(p) = v; }
+
+template <int DS>
+__device__ __forceinline__ typename ElemT<DS>::T ld1(const uint8_t* p) {
+  return *reinterpret_cast<const typename ElemT<DS>::T*>(p);
+}
+template <int DS>
+__device__ __forceinline__ void st1(uint8_t* p, typename ElemT<DS>::T v) {
+  *reinterpret_cast<typename ElemT<DS>::T*>(p) = v;
+}
+
+__device__ __forceinline__ uint64_t ld_u64_unaligned(const uint8_t* p, int big) {
+  uint64_t v = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) v |= (uint64_t)p[i] << (8 * i);
+  return big ? __builtin_bswap64(v) : v;
+}
+
+// ---------------------------------------------------------------------------------
+// per-item geometry (all values are wave-uniform).  Every per-dimension loop runs over
+// the compile-time bound kMaxDims with a uniform `d < n` guard, so the arrays below
+// are indexed by constants after unrolling and live in (scalar) registers, not scratch.
+// ---------------------------------------------------------------------------------
+enum ItemMode : int { kCopy = 0, kFill = 1, kSkip = 2 };
+
+struct Item {
+  const uint8_t* sbase;   // source bytes (payload for decode, region for encode)
+  uint8_t* dbase;         // destination bytes
+  int64_t s0, d0;         // element offsets of the box origin
+  int32_t e[kMaxDims];    // box extents (elements written)
+  int32_t v[kMaxDims];    // loadable extents (encode: array-domain clip; decode: == e)
+  FastDiv ediv[kMaxDims]; // divisors for e[]
+  uint64_t fill;          // constant for kFill
+  int mode;
+  uint32_t piece;
+};
+
+__device__ __forceinline__ int64_t find_shard(const ScatterArgs& a, int64_t citem) {
+  int64_t lo = 0, hi = a.nshards - 1;
+  while (lo < hi) {
+    int64_t mid = (lo + hi + 1) >> 1;
+    if (a.shards[mid].item_begin <= citem) lo = mid;
+    else hi = mid - 1;
+  }
+  return lo;
+}
+
+// Builds the geometry of work item `item` (returns the shard slot).
+template <bool ENC>
+__device__ __forceinline__ int64_t make_item(const ScatterArgs& a, int64_t item, Item& it) {
+  const int n = a.ndim;
+  const int64_t citem = item >> a.piece_shift;
+  it.piece = (uint32_t)(item & ((1ll << a.piece_shift) - 1));
+  const int64_t s = find_shard(a, citem);
+  const DevShard& S = a.shards[s];
+  // inner-chunk coordinates: C-order unravel of the item inside the shard's box
+  // (IndexingUtils.computeChunkCoords order, M/utils/IndexingUtils.java:36-49)
+  uint32_t j = (uint32_t)(citem - S.item_begin);
+  int32_t ic[kMaxDims];
+#pragma unroll
+  for (int d = kMaxDims - 1; d >= 0; --d) {
+    ic[d] = 0;
+    if (d < n) {
+      const uint32_t c = (uint32_t)S.box_count[d];
+      const uint32_t q = j / c;
+      ic[d] = S.box_start[d] + (int32_t)(j - q * c);
+      j = q;
+    }
+  }
+  it.mode = kCopy;
+  it.fill = 0;
+  if constexpr (!ENC) {
+    if (S.data == nullptr) {
+      // missing shard: region keeps fill_value (M/core/Array.java:400-402, 419-421)
+      it.mode = kFill;
+      it.fill = a.fill;
+      it.sbase = nullptr;
+    } else if (a.sharded) {
+      int64_t lin = 0;
+#pragma unroll
+      for (int d = 0; d < kMaxDims; d++)
+        if (d < n) lin += (int64_t)ic[d] * a.cps_stride[d];
+      const uint8_t* ent = S.data + S.index_off + 16 * lin;
+      const uint64_t off = ld_u64_unaligned(ent, a.index_be);
+      const uint64_t nb = ld_u64_unaligned(ent + 8, a.index_be);
+      if (off == ~0ull || nb == ~0ull) {
+        // missing inner chunk: the zero-initialised part array shows through (Q1,
+        // ShardingIndexedCodec.java:189, 219-221)
+        it.mode = kFill;
+        it.fill = 0;
+        it.sbase = nullptr;
+      } else {
+        const uint64_t total = (uint64_t)S.nbytes;
+        const bool range_ok = off <= total && nb <= total - off;
+        if (!range_ok || nb != (uint64_t)a.inner_nbytes) {
+          if (threadIdx.x == 0 && it.piece == 0) {
+            const uint32_t kind = range_ok ? kFlagLength : kFlagRange;
+            const uint64_t key = ((uint64_t)(0xFFFFFFFFu - (uint32_t)lin) << 8) | kind;
+            atomicOr((unsigned long long*)(a.status + s * kStWords + kStFlags),
+                     (unsigned long long)kind);
+            atomicMax((unsigned long long*)(a.status + s * kStWords + kStBadChunk),
+                      (unsigned long long)key);
+          }
+          it.mode = kSkip;
+          return s;
+        }
+        it.sbase = S.data + off;
+      }
+    } else {
+      it.sbase = S.data;  // object size validated on the host
+    }
+    it.dbase = a.region;
+    int64_t s0 = 0, d0 = S.out_base;
+#pragma unroll
+    for (int d = 0; d < kMaxDims; d++) {
+      it.e[d] = 1;
+      it.v[d] = 1;
+      it.ediv[d] = a.inner_div[0];
+      if (d < n) {
+        const int32_t io = ic[d] * a.inner[d];
+        const int32_t lo = max(io, S.part_lo[d]) - io;
+        const int32_t hi = min(io + a.inner[d], S.part_hi[d]) - io;
+        it.e[d] = hi - lo;
+        it.v[d] = hi - lo;
+        s0 += (int64_t)lo * a.pstride[d];
+        d0 += (int64_t)(io + lo - S.part_lo[d]) * a.rstride[d];
+        it.ediv[d] = (hi - lo == a.inner[d]) ? a.inner_div[d] : make_fastdiv((uint32_t)(hi - lo));
+      }
+    }
+    it.s0 = s0;
+    it.d0 = d0;
+  } else {
+    const int64_t off = a.item_off ? a.item_off[citem] : 0;
+    if (off < 0) {
+      it.mode = kSkip;
+      return s;
+    }
+    it.sbase = a.region;
+    it.dbase = S.wdata + off;
+    int64_t s0 = S.out_base;
+    bool empty = false;
+#pragma unroll
+    for (int d = 0; d < kMaxDims; d++) {
+      it.e[d] = 1;
+      it.v[d] = 1;
+      it.ediv[d] = a.inner_div[0];
+      if (d < n) {
+        const int32_t io = ic[d] * a.inner[d];
+        const int32_t vhi = min(io + a.inner[d], S.part_hi[d]) - io;
+        it.e[d] = a.inner[d];
+        it.v[d] = vhi;
+        empty |= vhi <= 0;
+        s0 += (int64_t)(io - S.part_lo[d]) * a.rstride[d];
+        it.ediv[d] = a.inner_div[d];
+      }
+    }
+    it.s0 = s0;
+    it.d0 = 0;
+    // an inner chunk entirely in the boundary padding is all fill: never encoded
+    if (empty) it.mode = kSkip;
+  }
+  return s;
+}
+
+// ---------------------------------------------------------------------------------
+// row pass: rows along dim F, unit-stride on both sides (on the destination only for
+// constant fills).  VEC: 16-byte granules; otherwise single elements with
+// loadable-extent checks.  CHECK: compare against fill_value instead of storing.
+// ---------------------------------------------------------------------------------
+template <int DS, bool VEC, bool CHECK>
+__device__ __forceinline__ bool row_pass(const ScatterArgs& a, const Item& it, int F,
+                                         const int64_t* sstr, const int64_t* dstr,
+                                         uint32_t nrows, const int32_t* ext,
+                                         const FastDiv* ediv) {
+  using T = typename ElemT<DS>::T;
+  constexpr int U = 4;
+  const int n = a.ndim;
+  const bool fill = it.mode == kFill;
+  int32_t eF = 1;
+#pragma unroll
+  for (int d = 0; d < kMaxDims; d++)
+    if (d == F) eF = ext[d];
+  const uint32_t gpr = VEC ? (uint32_t)(eF * DS / 16) : (uint32_t)eF;
+  if (gpr == 0 || nrows == 0) return false;
+  const FastDiv gdiv = make_fastdiv(gpr);
+  const uint32_t pieces = 1u << a.piece_shift;
+  const uint32_t r0 = (uint32_t)(((uint64_t)nrows * it.piece) / pieces);
+  const uint32_t r1 = (uint32_t)(((uint64_t)nrows * (it.piece + 1)) / pieces);
+  const uint32_t total = (r1 - r0) * gpr;
+  const uint4 fv = fill16<DS>(CHECK ? a.fill : it.fill);
+  int64_t sF = 1, dF = 1;
+#pragma unroll
+  for (int d = 0; d < kMaxDims; d++)
+    if (d == F) {
+      sF = sstr[d];
+      dF = dstr[d];
+    }
+  bool diff = false;
+  for (uint32_t base = threadIdx.x; base < total; base += kBlock * U) {
+    uint4 vv[U];
+    T sv[U];
+    int64_t doff[U];
+    bool ok[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const uint32_t g = base + u * kBlock;
+      ok[u] = g < total;
+      vv[u] = make_uint4(0, 0, 0, 0);
+      sv[u] = 0;
+      doff[u] = 0;
+      if (!ok[u]) continue;
+      uint32_t r = fdiv(g, gdiv);
+      const uint32_t c = g - r * gpr;
+      r += r0;
+      int64_t so = it.s0, dof = it.d0;
+      bool valid = true;
+#pragma unroll
+      for (int d = kMaxDims - 1; d >= 0; --d) {
+        if (d >= n || d == F || ext[d] <= 1) continue;
+        const uint32_t q = fdiv(r, ediv[d]);
+        const uint32_t m = r - q * (uint32_t)ext[d];
+        so += (int64_t)m * sstr[d];
+        dof += (int64_t)m * dstr[d];
+        valid &= (int32_t)m < it.v[d];
+        r = q;
+      }
+      if constexpr (VEC) {
+        doff[u] = dof * DS + (int64_t)c * 16;
+        if (!fill) vv[u] = ld16(it.sbase + so * DS + (int64_t)c * 16);
+      } else {
+        doff[u] = (dof + (int64_t)c * dF) * DS;
+        bool vF = false;
+#pragma unroll
+        for (int d = 0; d < kMaxDims; d++)
+          if (d == F) vF = (int32_t)c < it.v[d];
+        valid &= vF;
+        if (!fill) sv[u] = valid ? ld1<DS>(it.sbase + (so + (int64_t)c * sF) * DS) : (T)a.fill;
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      if (!ok[u]) continue;
+      if constexpr (CHECK) {
+        if constexpr (VEC) {
+          diff |= (vv[u].x != fv.x) | (vv[u].y != fv.y) | (vv[u].z != fv.z) | (vv[u].w != fv.w);
+        } else {
+          diff |= sv[u] != (T)a.fill;
+        }
+      } else if constexpr (VEC) {
+        st16(it.dbase + doff[u], fill ? fv : xform16<DS>(vv[u], a.swap, a.is_bool));
+      } else {
+        st1<DS>(it.dbase + doff[u], fill ? (T)it.fill : xform1<DS>(sv[u], a.swap, a.is_bool));
+      }
+    }
+  }
+  return diff;
+}
+
+// Can the whole item move in 16-byte granules along F?
+template <int DS>
+__device__ __forceinline__ bool vec_ok(const ScatterArgs& a, const Item& it, int F,
+                                       const int64_t* sstr, const int64_t* dstr,
+                                       const int32_t* ext, bool need_src) {
+  const int n = a.ndim;
+  bool ok = !(((uintptr_t)(it.dbase + it.d0 * DS)) & 15);
+  if (need_src) ok &= !(((uintptr_t)(it.sbase + it.s0 * DS)) & 15);
+#pragma unroll
+  for (int d = 0; d < kMaxDims; d++) {
+    if (d >= n) continue;
+    if (d == F) {
+      ok &= !((ext[d] * DS) & 15);
+      if (need_src) ok &= it.v[d] == ext[d];
+      continue;
+    }
+    if (ext[d] > 1) {
+      ok &= !((dstr[d] * DS) & 15);
+      if (need_src) ok &= !((sstr[d] * DS) & 15);
+    }
+    if (need_src) ok &= it.v[d] == ext[d];
+  }
+  return ok;
+}
+
+// ---------------------------------------------------------------------------------
+// tile pass: transpose between the src-fast dim fs and the dst-fast dim fd through
+// 32x32-element LDS tiles (row pitch 33 elements: conflict-free on both sides).
+// ---------------------------------------------------------------------------------
+template <int DS>
+__device__ __forceinline__ void tile_pass(const ScatterArgs& a, const Item& it,
+                                          const int64_t* sstr, const int64_t* dstr,
+                                          typename ElemT<DS>::T (*tile)[32][33]) {
+  using T = typename ElemT<DS>::T;
+  const int n = a.ndim, fs = a.fs, fd = a.fd;
+  const int tid = threadIdx.x, l = tid >> 3, g = tid & 7;
+  int32_t efs = 1, efd = 1, vfs = 1, vfd = 1;
+  int64_t ss_fs = 1, ss_fd = 1, ds_fs = 1, ds_fd = 1;
+  uint32_t nb = 1;
+  bool vec = DS == 4 && !(((uintptr_t)(it.sbase + it.s0 * DS)) & 15) &&
+             !(((uintptr_t)(it.dbase + it.d0 * DS)) & 15);
+#pragma unroll
+  for (int d = 0; d < kMaxDims; d++) {
+    if (d >= n) continue;
+    if (d == fs) {
+      efs = it.e[d];
+      vfs = it.v[d];
+      ss_fs = sstr[d];
+      ds_fs = dstr[d];
+    }
+    if (d == fd) {
+      efd = it.e[d];
+      vfd = it.v[d];
+      ss_fd = sstr[d];
+      ds_fd = dstr[d];
+    }
+    if (d != fs && d != fd) nb *= (uint32_t)it.e[d];
+    if (d != fs && (sstr[d] & 3)) vec = false;
+    if (d != fd && (dstr[d] & 3)) vec = false;
+    if (it.v[d] != it.e[d]) vec = false;
+  }
+  const uint32_t ts = (uint32_t)(efs + 31) >> 5, td = (uint32_t)(efd + 31) >> 5;
+  const uint32_t units = nb * ts * td;
+  const uint32_t pieces = 1u << a.piece_shift;
+  const uint32_t u0 = (uint32_t)(((uint64_t)units * it.piece) / pieces);
+  const uint32_t u1 = (uint32_t)(((uint64_t)units * (it.piece + 1)) / pieces);
+  const FastDiv tddiv = make_fastdiv(td), tsdiv = make_fastdiv(ts);
+  for (uint32_t ub = u0; ub < u1; ub += kTileTPB) {
+    int64_t so_t[kTileTPB], do_t[kTileTPB];
+    uint32_t xs0[kTileTPB], xd0[kTileTPB];
+    bool bval[kTileTPB], live[kTileTPB];
+#pragma unroll
+    for (int t = 0; t < kTileTPB; t++) {
+      const uint32_t unit = ub + t;
+      live[t] = unit < u1;
+      const uint32_t q1 = fdiv(unit, tddiv);
+      const uint32_t ud = unit - q1 * td;
+      uint32_t b = fdiv(q1, tsdiv);
+      const uint32_t us = q1 - b * ts;
+      int64_t so = it.s0 + (int64_t)(us * 32) * ss_fs + (int64_t)(ud * 32) * ss_fd;
+      int64_t dof = it.d0 + (int64_t)(us * 32) * ds_fs + (int64_t)(ud * 32) * ds_fd;
+      bool bv = true;
+#pragma unroll
+      for (int d = kMaxDims - 1; d >= 0; --d) {
+        if (d >= n || d == fs || d == fd || it.e[d] <= 1) continue;
+        const uint32_t q = fdiv(b, it.ediv[d]);
+        const uint32_t m = b - q * (uint32_t)it.e[d];
+        so += (int64_t)m * sstr[d];
+        dof += (int64_t)m * dstr[d];
+        bv &= (int32_t)m < it.v[d];
+        b = q;
+      }
+      so_t[t] = so;
+      do_t[t] = dof;
+      xs0[t] = us * 32;
+      xd0[t] = ud * 32;
+      bval[t] = bv;
+    }
+    // load phase: lane (l, g) reads 4 consecutive fs-elements of fd-row l
+#pragma unroll
+    for (int t = 0; t < kTileTPB; t++) {
+      if (!live[t]) continue;
+      const bool full = xs0[t] + 32 <= (uint32_t)efs && xd0[t] + 32 <= (uint32_t)efd;
+      if (vec && full) {
+        const uint4 x = ld16(it.sbase + (so_t[t] + (int64_t)l * ss_fd + g * 4) * 4);
+        T* row = &tile[t][l][g * 4];
+        row[0] = (T)xform1<4>(x.x, a.swap, 0);
+        row[1] = (T)xform1<4>(x.y, a.swap, 0);
+        row[2] = (T)xform1<4>(x.z, a.swap, 0);
+        row[3] = (T)xform1<4>(x.w, a.swap, 0);
+      } else {
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+          const uint32_t xs = xs0[t] + g * 4 + k, xd = xd0[t] + l;
+          if (xs < (uint32_t)efs && xd < (uint32_t)efd) {
+            const bool ld = bval[t] && (int32_t)xs < vfs && (int32_t)xd < vfd;
+            const T x = ld ? ld1<DS>(it.sbase + (so_t[t] + (int64_t)l * ss_fd +
+                                                 (int64_t)(g * 4 + k) * ss_fs) * DS)
+                           : (T)a.fill;
+            tile[t][l][g * 4 + k] = xform1<DS>(x, a.swap, a.is_bool);
+          }
+        }
+      }
+    }
+    __syncthreads();
+    // store phase: lane (l = fs-row, g) writes 4 consecutive fd-elements of fs-row l
+#pragma unroll
+    for (int t = 0; t < kTileTPB; t++) {
+      if (!live[t]) continue;
+      const bool full = xs0[t] + 32 <= (uint32_t)efs && xd0[t] + 32 <= (uint32_t)efd;
+      if (vec && full) {
+        uint4 y;
+        y.x = (uint32_t)tile[t][g * 4 + 0][l];
+        y.y = (uint32_t)tile[t][g * 4 + 1][l];
+        y.z = (uint32_t)tile[t][g * 4 + 2][l];
+        y.w = (uint32_t)tile[t][g * 4 + 3][l];
+        st16(it.dbase + (do_t[t] + (int64_t)l * ds_fs + g * 4) * 4, y);
+      } else {
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+          const uint32_t xs = xs0[t] + l, xd = xd0[t] + g * 4 + k;
+          if (xs < (uint32_t)efs && xd < (uint32_t)efd)
+            st1<DS>(it.dbase + (do_t[t] + (int64_t)l * ds_fs + (int64_t)(g * 4 + k) * ds_fd) * DS,
+                    tile[t][g * 4 + k][l]);
+        }
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// ---------------------------------------------------------------------------------
+// scatter kernel: one workgroup per work item (grid-stride over items)
+// ---------------------------------------------------------------------------------
+template <int DS, bool ENC, bool TILE>
+__global__ __launch_bounds__(kBlock) void scatter_kernel(ScatterArgs a) {
+  using T = typename ElemT<DS>::T;
+  const int64_t* sstr = ENC ? a.rstride : a.pstride;
+  const int64_t* dstr = ENC ? a.pstride : a.rstride;
+  for (int64_t item = blockIdx.x; item < a.total_items; item += gridDim.x) {
+    Item it;
+    make_item<ENC>(a, item, it);
+    if (it.mode == kSkip) continue;
+    const int n = a.ndim;
+    if (it.mode == kFill || !TILE) {
+      // decode fills: constant rows along the destination-fast dim; copies: rows along
+      // the dim that is unit-stride on both sides
+      const int F = it.mode == kFill ? a.fd : a.fs;
+      uint32_t nrows = 1;
+#pragma unroll
+      for (int d = 0; d < kMaxDims; d++)
+        if (d < n && d != F) nrows *= (uint32_t)it.e[d];
+      const bool need_src = it.mode != kFill;
+      if (vec_ok<DS>(a, it, F, sstr, dstr, it.e, need_src))
+        row_pass<DS, true, false>(a, it, F, sstr, dstr, nrows, it.e, it.ediv);
+      else
+        row_pass<DS, false, false>(a, it, F, sstr, dstr, nrows, it.e, it.ediv);
+      continue;
+    }
+    if constexpr (TILE) {
+      __shared__ T tile[kTileTPB][32][33];
+      tile_pass<DS>(a, it, sstr, dstr, tile);
+    }
+  }
+}
+
+// encode pre-pass: does the loadable part of an inner chunk differ from fill_value?
+// (ShardingIndexedCodec.encode :129-133 / writeChunk M/core/Array.java:150-151)
+template <int DS>
+__global__ __launch_bounds__(kBlock) void flags_kernel(ScatterArgs a) {
+  const int64_t* sstr = a.rstride;
+  for (int64_t item = blockIdx.x; item < a.total_items; item += gridDim.x) {
+    Item it;
+    make_item<true>(a, item, it);
+    bool diff = false;
+    if (it.mode == kCopy) {
+      const int n = a.ndim, F = n - 1;
+      int32_t ext[kMaxDims];
+      FastDiv ediv[kMaxDims];
+      uint32_t nrows = 1;
+      bool vec = !(((uintptr_t)(it.sbase + it.s0 * DS)) & 15);
+#pragma unroll
+      for (int d = 0; d < kMaxDims; d++) {
+        ext[d] = it.v[d];
+        ediv[d] = it.ediv[d];
+        if (d >= n) continue;
+        if (ext[d] != a.inner[d]) ediv[d] = make_fastdiv((uint32_t)ext[d]);
+        if (d != F) {
+          nrows *= (uint32_t)ext[d];
+          if (ext[d] > 1 && ((sstr[d] * DS) & 15)) vec = false;
+        } else if ((ext[d] * DS) & 15) {
+          vec = false;
+        }
+      }
+      if (vec)
+        diff = row_pass<DS, true, true>(a, it, F, sstr, sstr, nrows, ext, ediv);
+      else
+        diff = row_pass<DS, false, true>(a, it, F, sstr, sstr, nrows, ext, ediv);
+    }
+    const int any = __syncthreads_or(diff ? 1 : 0);
+    if (threadIdx.x == 0) a.flags[item] = any ? 1 : 0;
+  }
+}
+
+// ---------------------------------------------------------------------------------
+// CRC-32C of the shard index
+// ---------------------------------------------------------------------------------
+__constant__ uint32_t c_x2n[32] = {
+    0x40000000u, 0x20000000u, 0x08000000u, 0x00800000u, 0x00008000u, 0x82F63B78u, 0x6EA2D55Cu,
+    0x18B8EA18u, 0x510AC59Au, 0xB82BE955u, 0xB8FDB1E7u, 0x88E56F72u, 0x74C360A4u, 0xE4172B16u,
+    0x0D65762Au, 0x35D73A62u, 0x28461564u, 0xBF455269u, 0xE2EA32DCu, 0xFE7740E6u, 0xF946610Bu,
+    0x3C204F8Fu, 0x538586E3u, 0x59726915u, 0x734D5309u, 0xBC1AC763u, 0x7D0722CCu, 0xD289CABEu,
+    0xE94CA9BCu, 0x05B74F3Fu, 0xA51E1F42u, 0x40000000u};
+
+constexpr uint32_t kPoly = 0x82F63B78u;
+
+// a(x) * b(x) mod P (reflected bit order)
+__device__ __forceinline__ uint32_t multmodp(uint32_t a, uint32_t b) {
+  uint32_t m = 1u << 31, p = 0;
+  for (;;) {
+    if (a & m) {
+      p ^= b;
+      if ((a & (m - 1)) == 0) break;
+    }
+    m >>= 1;
+    b = (b & 1) ? (b >> 1) ^ kPoly : b >> 1;
+  }
+  return p;
+}
+
+__device__ __forceinline__ uint32_t x2nmodp(uint64_t n, unsigned k) {
+  uint32_t p = 1u << 31;
+  while (n) {
+    if (n & 1) p = multmodp(c_x2n[k & 31], p);
+    n >>= 1;
+    k++;
+  }
+  return p;
+}
+
+// crc(A || B) from crc(A), crc(B), |B|
+__device__ __forceinline__ uint32_t crc_combine(uint32_t c1, uint32_t c2, uint64_t len2) {
+  return multmodp(x2nmodp(len2, 3), c1) ^ c2;
+}
+
+__global__ __launch_bounds__(kBlock) void crc_partial_kernel(const CrcJob* jobs, int64_t njobs,
+                                                              uint32_t* partials) {
+  __shared__ uint32_t T[8][256];
+  __shared__ uint32_t red[kBlock];
+  const int tid = threadIdx.x;
+  {
+    uint32_t c = (uint32_t)tid;
+#pragma unroll
+    for (int k = 0; k < 8; k++) c = (c & 1) ? (c >> 1) ^ kPoly : c >> 1;
+    T[0][tid] = c;
+  }
+  __syncthreads();
+  for (int k = 1; k < 8; k++) {
+    const uint32_t p = T[k - 1][tid];
+    T[k][tid] = (p >> 8) ^ T[0][p & 0xFFu];
+    __syncthreads();
+  }
+  const int64_t span = blockIdx.x;
+  int64_t lo = 0, hi = njobs - 1;
+  while (lo < hi) {
+    int64_t mid = (lo + hi + 1) >> 1;
+    if (jobs[mid].span_begin <= span) lo = mid;
+    else hi = mid - 1;
+  }
+  const CrcJob J = jobs[lo];
+  const int64_t sb = (span - J.span_begin) * kCrcSpan;
+  const int64_t slen = min((int64_t)kCrcSpan, J.len - sb);
+  const int64_t lb = (int64_t)tid * kCrcLane;
+  const int64_t llen = max((int64_t)0, min((int64_t)kCrcLane, slen - lb));
+  const uint8_t* p = J.base + sb + lb;
+  uint32_t c = 0xFFFFFFFFu;
+  int64_t i = 0;
+  if ((((uintptr_t)p) & 7) == 0) {
+    for (; i + 8 <= llen; i += 8) {
+      const uint64_t w = *reinterpret_cast<const uint64_t*>(p + i);
+      const uint32_t lo32 = (uint32_t)w ^ c, hi32 = (uint32_t)(w >> 32);
+      c = T[7][lo32 & 0xFFu] ^ T[6][(lo32 >> 8) & 0xFFu] ^ T[5][(lo32 >> 16) & 0xFFu] ^
+          T[4][lo32 >> 24] ^ T[3][hi32 & 0xFFu] ^ T[2][(hi32 >> 8) & 0xFFu] ^
+          T[1][(hi32 >> 16) & 0xFFu] ^ T[0][hi32 >> 24];
+    }
+  }
+  for (; i < llen; i++) c = T[0][(c ^ p[i]) & 0xFFu] ^ (c >> 8);
+  red[tid] = c ^ 0xFFFFFFFFu;  // standard CRC of this lane's segment (empty: 0)
+  __syncthreads();
+#pragma unroll 1
+  for (int k = 0; k < 8; k++) {
+    const int stride = 1 << k;
+    if ((tid & ((stride << 1) - 1)) == 0) {
+      const int64_t rstart = (int64_t)(tid + stride) * kCrcLane;
+      const int64_t rlen = max((int64_t)0, min((int64_t)kCrcLane << k, slen - rstart));
+      if (rlen > 0) red[tid] = crc_combine(red[tid], red[tid + stride], (uint64_t)rlen);
+    }
+    __syncthreads();
+  }
+  if (tid == 0) partials[span] = red[0];
+}
+
+__global__ void crc_finalize_kernel(const CrcJob* jobs, int64_t njobs, const uint32_t* partials,
+                                    uint64_t* status) {
+  const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= njobs) return;
+  const CrcJob J = jobs[j];
+  uint32_t c = 0;
+  const int64_t nspans = (J.len + kCrcSpan - 1) / kCrcSpan;
+  for (int64_t k = 0; k < nspans; k++) {
+    const int64_t slen = min((int64_t)kCrcSpan, J.len - k * kCrcSpan);
+    c = crc_combine(c, partials[J.span_begin + k], (uint64_t)slen);
+  }
+  const uint8_t* s = J.base + J.len;  // stored little-endian (Crc32cCodec.java:121,130)
+  const uint32_t stored =
+      (uint32_t)s[0] | ((uint32_t)s[1] << 8) | ((uint32_t)s[2] << 16) | ((uint32_t)s[3] << 24);
+  uint64_t* st = status + (int64_t)J.shard * kStWords;
+  st[kStCrcStored] = stored;
+  st[kStCrcComputed] = c;
+  if (c != stored) atomicOr((unsigned long long*)(st + kStFlags), (unsigned long long)kFlagCrc);
+}
+
+// ---------------------------------------------------------------------------------
+// synthetic data
+// ---------------------------------------------------------------------------------
+__device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
+  uint64_t z = x + 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+template <int DS>
+__global__ __launch_bounds__(kBlock) void synth_fill_kernel(uint8_t* dst, int64_t n, int64_t first,
+                                                             uint64_t seed) {
+  using T = typename ElemT<DS>::T;
+  const int64_t stride = (int64_t)gridDim.x * kBlock;
+  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i * 4 < n; i += stride) {
+    const int64_t e0 = i * 4;
+    if (e0 + 4 <= n && !(((uintptr_t)(dst + e0 * DS)) & (4 * DS - 1)) && DS == 4) {
+      uint4 v;
+      v.x = (uint32_t)splitmix64((uint64_t)(first + e0 + 0) ^ seed);
+      v.y = (uint32_t)splitmix64((uint64_t)(first + e0 + 1) ^ seed);
+      v.z = (uint32_t)splitmix64((uint64_t)(first + e0 + 2) ^ seed);
+      v.w = (uint32_t)splitmix64((uint64_t)(first + e0 + 3) ^ seed);
+      st16(dst + e0 * DS, v);
+    } else {
+      for (int k = 0; k < 4 && e0 + k < n; k++)
+        st1<DS>(dst + (e0 + k) * DS, (T)splitmix64((uint64_t)(first + e0 + k) ^ seed));
+    }
+  }
+}
+
+struct VerifyArgs {
+  const uint8_t* region;
+  int32_t ndim;
+  int64_t rows;               // prod(shape[0..n-2])
+  int64_t rowlen;             // shape[n-1]
+  int64_t shape[kMaxDims];
+  int64_t offset[kMaxDims];
+  int64_t astride[kMaxDims];  // array C-order strides
+  uint64_t seed;
+  unsigned long long* count;
+};
+
+template <int DS>
+__global__ __launch_bounds__(kBlock) void synth_verify_kernel(VerifyArgs a) {
+  using T = typename ElemT<DS>::T;
+  __shared__ unsigned long long wsum[kBlock / 64];
+  unsigned long long bad = 0;
+  const int n = a.ndim;
+  for (int64_t r = blockIdx.x; r < a.rows; r += gridDim.x) {
+    // global index of the row start
+    int64_t rr = r, g = 0;
+    for (int d = n - 2; d >= 0; --d) {
+      const int64_t m = rr % a.shape[d];
+      rr /= a.shape[d];
+      g += (a.offset[d] + m) * a.astride[d];
+    }
+    g += a.offset[n - 1];
+    const uint8_t* row = a.region + r * a.rowlen * DS;
+    for (int64_t c = threadIdx.x; c < a.rowlen; c += kBlock) {
+      const T want = (T)splitmix64((uint64_t)(g + c) ^ a.seed);
+      bad += ld1<DS>(row + c * DS) != want;
+    }
+  }
+  for (int o = 32; o > 0; o >>= 1) bad += __shfl_down(bad, o, 64);
+  if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = bad;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned long long s = 0;
+    for (int w = 0; w < kBlock / 64; w++) s += wsum[w];
+    if (s) atomicAdd(a.count, s);
+  }
+}
+
+// ---------------------------------------------------------------------------------
+// launchers
+// ---------------------------------------------------------------------------------
+hipError_t launch_crc(const CrcJob* jobs, int64_t njobs, int64_t nspans, uint32_t* partials,
+                      uint64_t* status, hipStream_t stream) {
+  if (njobs == 0) return hipSuccess;
+  hipLaunchKernelGGL(crc_partial_kernel, dim3((unsigned)nspans), dim3(kBlock), 0, stream, jobs,
+                     njobs, partials);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(crc_finalize_kernel, dim3((unsigned)((njobs + 63) / 64)), dim3(64), 0,
+                     stream, jobs, njobs, (const uint32_t*)partials, status);
+  return hipGetLastError();
+}
+
+template <int DS>
+static void launch_scatter_ds(const ScatterArgs& a, int tile, int enc, int grid,
+                              hipStream_t s) {
+  if (enc) {
+    if (tile)
+      hipLaunchKernelGGL((scatter_kernel<DS, true, true>), dim3(grid), dim3(kBlock), 0, s, a);
+    else
+      hipLaunchKernelGGL((scatter_kernel<DS, true, false>), dim3(grid), dim3(kBlock), 0, s, a);
+  } else {
+    if (tile)
+      hipLaunchKernelGGL((scatter_kernel<DS, false, true>), dim3(grid), dim3(kBlock), 0, s, a);
+    else
+      hipLaunchKernelGGL((scatter_kernel<DS, false, false>), dim3(grid), dim3(kBlock), 0, s, a);
+  }
+}
+
+hipError_t launch_scatter(const ScatterArgs& a, int dsize, int tile_mode, int encode, int grid,
+                          hipStream_t stream) {
+  if (a.total_items == 0) return hipSuccess;
+  switch (dsize) {
+    case 1: launch_scatter_ds<1>(a, tile_mode, encode, grid, stream); break;
+    case 2: launch_scatter_ds<2>(a, tile_mode, encode, grid, stream); break;
+    case 4: launch_scatter_ds<4>(a, tile_mode, encode, grid, stream); break;
+    case 8: launch_scatter_ds<8>(a, tile_mode, encode, grid, stream); break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+hipError_t launch_flags(const ScatterArgs& a, int dsize, int grid, hipStream_t stream) {
+  if (a.total_items == 0) return hipSuccess;
+  switch (dsize) {
+    case 1: hipLaunchKernelGGL(flags_kernel<1>, dim3(grid), dim3(kBlock), 0, stream, a); break;
+    case 2: hipLaunchKernelGGL(flags_kernel<2>, dim3(grid), dim3(kBlock), 0, stream, a); break;
+    case 4: hipLaunchKernelGGL(flags_kernel<4>, dim3(grid), dim3(kBlock), 0, stream, a); break;
+    case 8: hipLaunchKernelGGL(flags_kernel<8>, dim3(grid), dim3(kBlock), 0, stream, a); break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+hipError_t launch_synth_fill(void* dst, int64_t n, int dsize, int64_t first, uint64_t seed,
+                             hipStream_t stream) {
+  if (n <= 0) return hipSuccess;
+  int64_t vecs = (n + 3) / 4;
+  int grid = (int)std::min<int64_t>((vecs + kBlock - 1) / kBlock, 65536);
+  uint8_t* p = (uint8_t*)dst;
+  switch (dsize) {
+    case 1: hipLaunchKernelGGL(synth_fill_kernel<1>, dim3(grid), dim3(kBlock), 0, stream, p, n, first, seed); break;
+    case 2: hipLaunchKernelGGL(synth_fill_kernel<2>, dim3(grid), dim3(kBlock), 0, stream, p, n, first, seed); break;
+    case 4: hipLaunchKernelGGL(synth_fill_kernel<4>, dim3(grid), dim3(kBlock), 0, stream, p, n, first, seed); break;
+    case 8: hipLaunchKernelGGL(synth_fill_kernel<8>, dim3(grid), dim3(kBlock), 0, stream, p, n, first, seed); break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+hipError_t launch_synth_verify(const void* region, int ndim, const int64_t* array_shape,
+                               const int64_t* offset, const int64_t* shape, int dsize,
+                               uint64_t seed, unsigned long long* d_count, hipStream_t stream) {
+  VerifyArgs a;
+  a.region = (const uint8_t*)region;
+  a.ndim = ndim;
+  a.seed = seed;
+  a.count = d_count;
+  int64_t st = 1;
+  for (int d = ndim - 1; d >= 0; --d) {
+    a.astride[d] = st;
+    st *= array_shape[d];
+    a.shape[d] = shape[d];
+    a.offset[d] = offset[d];
+  }
+  a.rows = 1;
+  for (int d = 0; d < ndim - 1; d++) a.rows *= shape[d];
+  a.rowlen = shape[ndim - 1];
+  if (a.rows <= 0 || a.rowlen <= 0) return hipSuccess;
+  int grid = (int)std::min<int64_t>(a.rows, 65536);
+  switch (dsize) {
+    case 1: hipLaunchKernelGGL(synth_verify_kernel<1>, dim3(grid), dim3(kBlock), 0, stream, a); break;
+    case 2: hipLaunchKernelGGL(synth_verify_kernel<2>, dim3(grid), dim3(kBlock), 0, stream, a); break;
+    case 4: hipLaunchKernelGGL(synth_verify_kernel<4>, dim3(grid), dim3(kBlock), 0, stream, a); break;
+    case 8: hipLaunchKernelGGL(synth_verify_kernel<8>, dim3(grid), dim3(kBlock), 0, stream, a); break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+}  // namespace zh

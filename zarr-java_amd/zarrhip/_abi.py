@@ -1,0 +1,85 @@
+"""ctypes mirror of include/zarrhip.h (types and constants only; no library load)."""
+import ctypes as C
+
+ZH_MAX_DIMS = 8
+
+ZH_OK = 0
+ZH_EINVAL = 1
+ZH_EDATA = 2
+ZH_EUNSUPPORTED = 3
+ZH_EHIP = 4
+ZH_ENOMEM = 5
+ZH_EARITH = 6
+
+ZH_ENDIAN_LITTLE = 0
+ZH_ENDIAN_BIG = 1
+ZH_INDEX_END = 0
+ZH_INDEX_START = 1
+
+ZH_SRC_DEVICE = 0x1
+ZH_OUT_DEVICE = 0x2
+
+
+class zh_codec_chain(C.Structure):
+    _fields_ = [
+        ("sharded", C.c_int32),
+        ("inner_chunk_shape", C.c_int32 * ZH_MAX_DIMS),
+        ("has_transpose", C.c_int32),
+        ("transpose_order", C.c_int32 * ZH_MAX_DIMS),
+        ("endian", C.c_int32),
+        ("index_endian", C.c_int32),
+        ("index_has_crc32c", C.c_int32),
+        ("index_location", C.c_int32),
+    ]
+
+
+class zh_array_meta(C.Structure):
+    _fields_ = [
+        ("ndim", C.c_int32),
+        ("dtype_size", C.c_int32),
+        ("dtype_is_bool", C.c_int32),
+        ("reserved0", C.c_int32),
+        ("shape", C.c_int64 * ZH_MAX_DIMS),
+        ("chunk_shape", C.c_int32 * ZH_MAX_DIMS),
+        ("fill_value", C.c_uint8 * 8),
+        ("chain", zh_codec_chain),
+    ]
+
+
+class zh_chunk_src(C.Structure):
+    _fields_ = [("data", C.c_void_p), ("nbytes", C.c_int64)]
+
+
+class zh_chunk_dst(C.Structure):
+    _fields_ = [("data", C.c_void_p), ("capacity", C.c_int64), ("nbytes", C.c_int64)]
+
+
+def make_meta(shape, chunk_shape, dtype_size, *, fill=b"\0" * 8, is_bool=False, sharded=False,
+              inner_chunk_shape=None, transpose_order=None, endian=ZH_ENDIAN_LITTLE,
+              index_endian=ZH_ENDIAN_LITTLE, index_crc32c=True, index_location=ZH_INDEX_END):
+    """Build a zh_array_meta from Python values.  `fill` is the element's bytes (LE)."""
+    m = zh_array_meta()
+    n = len(shape)
+    m.ndim = n
+    m.dtype_size = dtype_size
+    m.dtype_is_bool = 1 if is_bool else 0
+    for d in range(n):
+        m.shape[d] = int(shape[d])
+        m.chunk_shape[d] = int(chunk_shape[d])
+    fb = bytes(fill)[:8].ljust(8, b"\0")
+    for i in range(8):
+        m.fill_value[i] = fb[i]
+    ch = m.chain
+    ch.sharded = 1 if sharded else 0
+    if sharded:
+        for d in range(n):
+            ch.inner_chunk_shape[d] = int(inner_chunk_shape[d])
+    if transpose_order is not None:
+        ch.has_transpose = 1
+        for d in range(n):
+            ch.transpose_order[d] = int(transpose_order[d])
+    ch.endian = endian
+    ch.index_endian = index_endian
+    ch.index_has_crc32c = 1 if index_crc32c else 0
+    ch.index_location = index_location
+    return m

@@ -1,0 +1,291 @@
+"""Loader for libzarrhip.so (the HIP path).  There is no CPU fallback: if the library or
+the GPU is missing, the product raises instead of silently computing on the host."""
+import ctypes as C
+import os
+
+from . import _abi as A
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libzarrhip.so")
+
+_lib = None
+
+P = C.c_void_p
+I32 = C.c_int32
+I64 = C.c_int64
+U32 = C.c_uint32
+U64 = C.c_uint64
+SZ = C.c_size_t
+CH = C.c_char_p
+PI64 = C.POINTER(C.c_int64)
+PI32 = C.POINTER(C.c_int32)
+PMETA = C.POINTER(A.zh_array_meta)
+
+_SIGS = {
+    "zh_version": (CH, []),
+    "zh_ctx_create": (C.c_int, [C.c_int, C.POINTER(P)]),
+    "zh_ctx_destroy": (None, [P]),
+    "zh_ctx_device": (C.c_int, [P]),
+    "zh_ctx_stream": (P, [P]),
+    "zh_validate_meta": (C.c_int, [PMETA, CH, SZ]),
+    "zh_shard_index_size": (I64, [PMETA]),
+    "zh_crc32c": (U32, [U32, P, SZ]),
+    "zh_compute_chunk_coords": (I64, [C.c_int, PI64, PI32, PI64, PI64, PI64, I64]),
+    "zh_compute_projection": (C.c_int, [C.c_int, PI64, PI64, PI32, PI64, PI64, PI32, PI32, PI32]),
+    "zh_is_permutation": (C.c_int, [C.c_int, PI32]),
+    "zh_inverse_permutation": (C.c_int, [C.c_int, PI32, PI32]),
+    "zh_plan_create": (C.c_int, [P, PMETA, C.POINTER(A.zh_chunk_src), I64, PI64, PI64, U32,
+                                 C.POINTER(P), CH, SZ]),
+    "zh_plan_execute": (C.c_int, [P, P, P]),
+    "zh_plan_wait": (C.c_int, [P, CH, SZ]),
+    "zh_plan_destroy": (None, [P]),
+    "zh_plan_stats": (C.c_int, [P, PI64, PI64, PI64, PI64]),
+    "zh_plan_set_timing": (C.c_int, [P, C.c_int]),
+    "zh_plan_kernel_time": (C.c_int, [P, C.POINTER(C.c_double), PI64, C.POINTER(C.c_double)]),
+    "zh_array_read": (C.c_int, [P, PMETA, C.POINTER(A.zh_chunk_src), I64, PI64, PI64, P, U32, P,
+                                CH, SZ]),
+    "zh_sharding_decode": (C.c_int, [P, PMETA, P, I64, P, U32, P, CH, SZ]),
+    "zh_sharding_decode_partial": (C.c_int, [P, PMETA, P, I64, PI64, PI32, P, U32, P, CH, SZ]),
+    "zh_array_encoded_bound": (I64, [PMETA]),
+    "zh_array_write": (C.c_int, [P, PMETA, P, PI64, PI64, C.POINTER(A.zh_chunk_dst), I64, P, CH,
+                                 SZ]),
+    "zh_device_malloc": (C.c_int, [P, SZ, C.POINTER(P)]),
+    "zh_device_free": (C.c_int, [P, P]),
+    "zh_host_malloc_pinned": (C.c_int, [P, SZ, C.POINTER(P)]),
+    "zh_host_free_pinned": (C.c_int, [P, P]),
+    "zh_memcpy_async": (C.c_int, [P, P, P, SZ, C.c_int, P]),
+    "zh_memset_async": (C.c_int, [P, P, C.c_int, SZ, P]),
+    "zh_stream_synchronize": (C.c_int, [P, P]),
+    "zh_event_create": (C.c_int, [P, C.POINTER(P)]),
+    "zh_event_destroy": (C.c_int, [P, P]),
+    "zh_event_record": (C.c_int, [P, P, P]),
+    "zh_event_elapsed_ms": (C.c_int, [P, P, P, C.POINTER(C.c_float)]),
+    "zh_device_info": (C.c_int, [P, CH, SZ, PI64, C.POINTER(C.c_int), CH, SZ]),
+    "zh_synth_fill": (C.c_int, [P, P, I64, C.c_int, I64, U64, P]),
+    "zh_synth_verify": (C.c_int, [P, P, C.c_int, PI64, PI64, PI64, C.c_int, U64,
+                                  C.POINTER(U64), P]),
+}
+
+
+def lib():
+    """The loaded libzarrhip.so (raises ImportError when it has not been built)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(
+                f"libzarrhip.so not found at {LIB_PATH}: build it with "
+                "`make -C zarr-java_amd` (the HIP path has no CPU fallback)")
+        L = C.CDLL(LIB_PATH)
+        for name, (res, args) in _SIGS.items():
+            f = getattr(L, name)
+            f.restype = res
+            f.argtypes = args
+        _lib = L
+    return _lib
+
+
+def declared_symbols():
+    return list(_SIGS)
+
+
+def i64arr(vals):
+    return (C.c_int64 * max(1, len(vals)))(*[int(v) for v in vals])
+
+
+def i32arr(vals):
+    return (C.c_int32 * max(1, len(vals)))(*[int(v) for v in vals])
+
+
+class ZhError(RuntimeError):
+    def __init__(self, status, message):
+        super().__init__(message)
+        self.status = status
+
+
+def check(status, err=None):
+    if status != A.ZH_OK:
+        msg = err.value.decode(errors="replace") if err is not None else ""
+        raise ZhError(status, msg or f"zarrhip status {status}")
+
+
+class DeviceContext:
+    """One GPU (a zh_ctx): device memory, streams and the decode/encode entry points."""
+
+    def __init__(self, device=0):
+        self.L = lib()
+        h = P()
+        st = self.L.zh_ctx_create(int(device), C.byref(h))
+        if st != A.ZH_OK:
+            raise ZhError(st, f"zh_ctx_create(device={device}) failed (status {st}); "
+                              "is a GPU visible?")
+        self.h = h
+        self.device = device
+
+    def close(self):
+        if self.h:
+            self.L.zh_ctx_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # -- memory ---------------------------------------------------------------------
+    def malloc(self, nbytes):
+        p = P()
+        st = self.L.zh_device_malloc(self.h, int(nbytes), C.byref(p))
+        if st != A.ZH_OK:
+            raise ZhError(st, f"device malloc of {nbytes} bytes failed")
+        return p.value
+
+    def free(self, ptr):
+        if ptr:
+            self.L.zh_device_free(self.h, P(ptr))
+
+    def malloc_pinned(self, nbytes):
+        p = P()
+        check(self.L.zh_host_malloc_pinned(self.h, int(nbytes), C.byref(p)))
+        return p.value
+
+    def free_pinned(self, ptr):
+        if ptr:
+            self.L.zh_host_free_pinned(self.h, P(ptr))
+
+    def memcpy(self, dst, src, nbytes, kind, stream=None, sync=True):
+        check(self.L.zh_memcpy_async(self.h, P(dst), P(src), int(nbytes), int(kind), P(stream)))
+        if sync:
+            self.sync(stream)
+
+    def h2d(self, dst, host_bytes, stream=None):
+        buf = (C.c_char * len(host_bytes)).from_buffer_copy(host_bytes) \
+            if not isinstance(host_bytes, C.Array) else host_bytes
+        self.memcpy(dst, C.addressof(buf), len(host_bytes), 0, stream, True)
+
+    def d2h(self, src, nbytes, stream=None):
+        buf = (C.c_char * int(nbytes))()
+        self.memcpy(C.addressof(buf), src, nbytes, 1, stream, True)
+        return bytes(buf)
+
+    def memset(self, dst, value, nbytes, stream=None):
+        check(self.L.zh_memset_async(self.h, P(dst), int(value), int(nbytes), P(stream)))
+
+    def sync(self, stream=None):
+        check(self.L.zh_stream_synchronize(self.h, P(stream)))
+
+    def info(self):
+        name = C.create_string_buffer(256)
+        arch = C.create_string_buffer(64)
+        mem = C.c_int64()
+        cus = C.c_int()
+        check(self.L.zh_device_info(self.h, name, 256, C.byref(mem), C.byref(cus), arch, 64))
+        return {"name": name.value.decode(), "arch": arch.value.decode(),
+                "total_mem": mem.value, "cu_count": cus.value}
+
+    # -- events ---------------------------------------------------------------------
+    def event(self):
+        e = P()
+        check(self.L.zh_event_create(self.h, C.byref(e)))
+        return e.value
+
+    def record(self, ev, stream=None):
+        check(self.L.zh_event_record(self.h, P(ev), P(stream)))
+
+    def elapsed_ms(self, a, b):
+        ms = C.c_float()
+        check(self.L.zh_event_elapsed_ms(self.h, P(a), P(b), C.byref(ms)))
+        return ms.value
+
+    # -- synthetic data ---------------------------------------------------------------
+    def synth_fill(self, dst, n, dtype_size, first=0, seed=0x5A5A2026, stream=None):
+        check(self.L.zh_synth_fill(self.h, P(dst), int(n), int(dtype_size), int(first),
+                                   int(seed), P(stream)))
+
+    def synth_verify(self, region, array_shape, offset, shape, dtype_size, seed=0x5A5A2026,
+                     stream=None):
+        mm = C.c_uint64()
+        n = len(array_shape)
+        check(self.L.zh_synth_verify(self.h, P(region), n, i64arr(array_shape), i64arr(offset),
+                                     i64arr(shape), int(dtype_size), int(seed), C.byref(mm),
+                                     P(stream)))
+        return mm.value
+
+    # -- codec path -------------------------------------------------------------------
+    def array_read(self, meta, sources, offset, shape, out, flags, stream=None):
+        """zh_array_read.  sources: list of (pointer or None, nbytes)."""
+        srcs = (A.zh_chunk_src * max(1, len(sources)))()
+        for i, (ptr, nb) in enumerate(sources):
+            srcs[i].data = ptr
+            srcs[i].nbytes = int(nb)
+        err = C.create_string_buffer(1024)
+        st = self.L.zh_array_read(self.h, C.byref(meta), srcs, len(sources), i64arr(offset),
+                                  i64arr(shape), P(out), int(flags), P(stream), err, 1024)
+        check(st, err)
+
+    def plan(self, meta, sources, offset, shape, flags):
+        return Plan(self, meta, sources, offset, shape, flags)
+
+    def array_write(self, meta, src, offset, shape, dsts, stream=None):
+        """zh_array_write.  dsts: list of (device pointer, capacity) → list of nbytes."""
+        arr = (A.zh_chunk_dst * max(1, len(dsts)))()
+        for i, (ptr, cap) in enumerate(dsts):
+            arr[i].data = ptr
+            arr[i].capacity = int(cap)
+            arr[i].nbytes = 0
+        err = C.create_string_buffer(1024)
+        st = self.L.zh_array_write(self.h, C.byref(meta), P(src), i64arr(offset), i64arr(shape),
+                                   arr, len(dsts), P(stream), err, 1024)
+        check(st, err)
+        return [arr[i].nbytes for i in range(len(dsts))]
+
+
+class Plan:
+    """A prepared region read (zh_plan): plan once, execute many times."""
+
+    def __init__(self, ctx, meta, sources, offset, shape, flags):
+        self.ctx = ctx
+        self.L = ctx.L
+        self._meta = meta
+        srcs = (A.zh_chunk_src * max(1, len(sources)))()
+        for i, (ptr, nb) in enumerate(sources):
+            srcs[i].data = ptr
+            srcs[i].nbytes = int(nb)
+        self._srcs = srcs
+        h = P()
+        err = C.create_string_buffer(1024)
+        st = self.L.zh_plan_create(ctx.h, C.byref(meta), srcs, len(sources), i64arr(offset),
+                                   i64arr(shape), int(flags), C.byref(h), err, 1024)
+        check(st, err)
+        self.h = h
+
+    def execute(self, out, stream=None):
+        check(self.L.zh_plan_execute(self.h, P(out), P(stream)))
+
+    def wait(self):
+        err = C.create_string_buffer(1024)
+        check(self.L.zh_plan_wait(self.h, err, 1024), err)
+
+    def stats(self):
+        a, b, c, d = C.c_int64(), C.c_int64(), C.c_int64(), C.c_int64()
+        check(self.L.zh_plan_stats(self.h, C.byref(a), C.byref(b), C.byref(c), C.byref(d)))
+        return {"in_bytes": a.value, "out_bytes": b.value, "items": c.value, "shards": d.value}
+
+    def set_timing(self, on=True):
+        check(self.L.zh_plan_set_timing(self.h, 1 if on else 0))
+
+    def kernel_time(self):
+        sc, ix, n = C.c_double(), C.c_double(), C.c_int64()
+        check(self.L.zh_plan_kernel_time(self.h, C.byref(sc), C.byref(n), C.byref(ix)))
+        return {"scatter_ms": sc.value, "index_ms": ix.value, "launches": n.value}
+
+    def close(self):
+        if self.h:
+            self.L.zh_plan_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
