@@ -113,6 +113,18 @@ def chunk_capacities(meta, coords):
     return caps
 
 
+def pmc_traffic(config):
+    """HBM bytes per launch of the scatter kernel from the newest committed PMC summary for
+    this config (profiles/rNN/<config>_summary.json, made by profiles/pmc_summary.py from
+    separate FETCH_SIZE / WRITE_SIZE rocprofv3 passes, FETCH_SIZE x2 per the gfx950 note)."""
+    import glob
+    cands = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", f"{config}_summary.json")))
+    if not cands:
+        return None, None
+    d = json.load(open(cands[-1]))
+    return int(d["pmc"]["traffic_bytes_per_launch"]), os.path.relpath(cands[-1], ROOT)
+
+
 def cpu_baseline(dev, A, meta, shard_ptr, shard_nbytes, budget_s=12.0):
     """The C oracle (restated reference path, oracle/zh_oracle.c) on this host's cores over a
     bounded sample of the same workload: region reads [1,1024,1024,64] inside shard (0,0,0,0)
@@ -237,8 +249,10 @@ def main():
     value = ws * args.steps * out_bytes / elapsed / GiB
     traffic_alg = st["in_bytes"] + st["out_bytes"]
     achieved = traffic_alg / (scatter_ms / 1000.0) / 1e9
+    traffic, traffic_src = pmc_traffic(args.config)
     roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
-                "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                "traffic_source": traffic_src,
                 "kernel": "scatter_kernel<4,false,%s>" % ("true" if meta.chain.has_transpose else
                                                           "false"),
                 "kernel_ms": round(scatter_ms, 3), "index_kernels_ms": round(index_ms, 4),

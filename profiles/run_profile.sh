@@ -1,0 +1,27 @@
+#!/bin/bash
+# Profiling recipe (run on the GPU box from the repo root):
+#   kernel trace + stats of the headline bench, then separate PMC passes for HBM bytes
+#   (FETCH_SIZE and WRITE_SIZE cannot share a pass on gfx950), plus the c4/c2 configs.
+set -u
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+TAG=${1:-r01}
+OUT=$R/gpurun_out/$TAG
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+cd /tmp || exit 1
+step() {  # name, timeout, cmd...
+  local name=$1 t=$2; shift 2
+  echo "== $name: $*" >&2
+  timeout -k 10 "$t" "$@" > "$OUT/$name.out" 2> "$OUT/$name.err"
+  local rc=$?
+  echo "== $name rc=$rc" >&2
+  if [ $rc -ne 0 ]; then exit $rc; fi
+}
+step trace_c3 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace_c3" -o run -- \
+  python3 "$R/bench.py" --steps 5 --warmup 2 --no-cpu-baseline
+step pmc_fetch_c3 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch_c3" -o run -- \
+  python3 "$R/bench.py" --steps 2 --warmup 1 --no-cpu-baseline
+step pmc_write_c3 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write_c3" -o run -- \
+  python3 "$R/bench.py" --steps 2 --warmup 1 --no-cpu-baseline
+step bench_c4 300 python3 "$R/bench.py" --config c4 --steps 5 --warmup 2 --no-cpu-baseline
+step bench_c2 300 python3 "$R/bench.py" --config c2 --steps 5 --warmup 2 --no-cpu-baseline

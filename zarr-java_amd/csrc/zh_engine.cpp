@@ -526,7 +526,15 @@ int zh_plan_create(zh_ctx* ctx, const zh_array_meta* m, const zh_chunk_src* chun
         plan_free(p);
         return ZH_EDATA;
       }
-      in_bytes += S.nbytes;
+      // algorithmic input bytes: referenced inner chunks + the index for a
+      // shard; only the in-bounds part of an unsharded chunk
+      if (c.sharded) {
+        in_bytes += nit * p->args.inner_nbytes + isz;
+      } else {
+        int64_t pb = m->dtype_size;
+        for (int d = 0; d < n; d++) pb *= ps[d];
+        in_bytes += pb;
+      }
       if (!(flags & ZH_SRC_DEVICE)) {
         stage_off[i] = staged;
         staged += (S.nbytes + 255) & ~(int64_t)255;
