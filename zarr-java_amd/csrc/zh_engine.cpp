@@ -186,8 +186,12 @@ struct zh_plan {
   std::vector<int64_t> h2d_len;
   uint8_t* d_out = nullptr;     // staging when the output is host memory
   ScatterArgs args{};
+  ItemDesc* d_desc = nullptr;   // per inner-chunk descriptors (resolve kernel)
+  uint32_t* d_slow = nullptr;   // [count, list...] of items for the generic kernel
+  uint32_t* d_fast_tab = nullptr;
   int tile_mode = 0;
   int grid = 0;
+  int slow_grid = 0;
   hipStream_t last_stream = nullptr;
   // timing
   bool timing = false;
@@ -376,6 +380,7 @@ void fill_common_args(const zh_array_meta* m, const int64_t* region_shape, bool 
     a.inner_div[d] = make_fastdiv(1);
   }
   a.inner_nbytes = nel * m->dtype_size;
+  a.dsize = m->dtype_size;
   uint64_t f = 0;
   for (int i = 0; i < 8; i++) f |= (uint64_t)m->fill_value[i] << (8 * i);
   a.fill = f;
@@ -387,13 +392,104 @@ void fill_common_args(const zh_array_meta* m, const int64_t* region_shape, bool 
     a.fd = n - 1;
   }
   tile_mode = a.fs != a.fd;
+  a.tile = tile_mode;
   const int64_t piece_kb = std::max(1, env_int("ZH_PIECE_KB", 128));
   const uint64_t pieces = (uint64_t)((a.inner_nbytes + piece_kb * 1024 - 1) / (piece_kb * 1024));
   a.piece_shift = (int32_t)next_pow2_shift(std::max<uint64_t>(1, pieces));
 }
 
+// Chooses the decode fast path for unclipped inner chunks and fills its launch-uniform
+// parameters: rows along the unit-stride dim mapped by shift/mask arithmetic (power-of-two
+// row extents, <= 3 row dims) or by a (src, dst) offset table, or 32x32 transpose tiles
+// from a table.  Returns the table (empty when the mode needs none).
+std::vector<uint32_t> setup_fast(const zh_array_meta* m, ScatterArgs& a, int tile_mode) {
+  const int n = m->ndim, ds = m->dtype_size;
+  const int64_t kMaxEntries = 4096;
+  std::vector<uint32_t> tab;
+  auto fits = [](int64_t v) { return v >= 0 && v < (1ll << 32); };
+  a.fast_mode = kFastNone;
+  a.fast_n = 0;
+  a.rm_n = 0;
+  if (!tile_mode) {
+    const int F = a.fs;
+    const int64_t rowb = (int64_t)a.inner[F] * ds;
+    if (rowb % 16) return {};
+    const int64_t vpr = rowb / 16;
+    if (vpr > kBlock || (vpr & (vpr - 1))) return {};
+    int64_t rows = 1;
+    std::vector<int> rdims;  // innermost first
+    for (int d = n - 1; d >= 0; d--) {
+      if (d == F) continue;
+      rows *= a.inner[d];
+      if (a.inner[d] > 1) {
+        if ((a.pstride[d] * ds) % 16 || (a.rstride[d] * ds) % 16) return {};
+        rdims.push_back(d);
+      }
+    }
+    a.fast_vpr_shift = (int32_t)next_pow2_shift((uint64_t)vpr);
+    a.fast_rows = (int32_t)rows;
+    bool pow2 = rdims.size() <= 3;
+    for (int d : rdims) pow2 &= (a.inner[d] & (a.inner[d] - 1)) == 0;
+    if (pow2 && rows < (1ll << 31)) {
+      a.fast_mode = kFastRowArith;
+      a.rm_n = (int32_t)rdims.size();
+      for (size_t i = 0; i < rdims.size(); i++) {
+        a.rm_shift[i] = (int32_t)next_pow2_shift((uint64_t)a.inner[rdims[i]]);
+        a.rm_sstr[i] = a.pstride[rdims[i]];
+        a.rm_dstr[i] = a.rstride[rdims[i]];
+      }
+      return {};
+    }
+    if (rows > kMaxEntries) return {};
+    for (int64_t r = 0; r < rows; r++) {
+      int64_t rr = r, so = 0, dof = 0;
+      for (int d = n - 1; d >= 0; d--) {
+        if (d == F) continue;
+        const int64_t mm = rr % a.inner[d];
+        rr /= a.inner[d];
+        so += mm * a.pstride[d];
+        dof += mm * a.rstride[d];
+      }
+      if (!fits(so) || !fits(dof)) return {};
+      tab.push_back((uint32_t)so);
+      tab.push_back((uint32_t)dof);
+    }
+    a.fast_mode = kFastRowTable;
+    a.fast_n = (int32_t)rows;
+    return tab;
+  }
+  const int fs = a.fs, fd = a.fd;
+  if (ds != 4 || a.inner[fs] % 32 || a.inner[fd] % 32) return {};
+  if (a.pstride[fd] % 4 || a.rstride[fs] % 4) return {};
+  const int64_t ts = a.inner[fs] / 32, td = a.inner[fd] / 32;
+  int64_t nb = 1;
+  for (int d = 0; d < n; d++)
+    if (d != fs && d != fd) nb *= a.inner[d];
+  if (nb * ts * td > kMaxEntries) return {};
+  for (int64_t u = 0; u < nb * ts * td; u++) {
+    const int64_t ud = u % td, us = (u / td) % ts;
+    int64_t b = u / (td * ts);
+    int64_t so = us * 32 * a.pstride[fs] + ud * 32 * a.pstride[fd];
+    int64_t dof = us * 32 * a.rstride[fs] + ud * 32 * a.rstride[fd];
+    for (int d = n - 1; d >= 0; d--) {
+      if (d == fs || d == fd) continue;
+      const int64_t mm = b % a.inner[d];
+      b /= a.inner[d];
+      so += mm * a.pstride[d];
+      dof += mm * a.rstride[d];
+    }
+    if (!fits(so) || !fits(dof) || so % 4 || dof % 4) return {};
+    tab.push_back((uint32_t)so);
+    tab.push_back((uint32_t)dof);
+  }
+  a.fast_mode = kFastTileTable;
+  a.fast_n = (int32_t)(nb * ts * td);
+  a.fast_rows = a.fast_n;
+  return tab;
+}
+
 int grid_for(const zh_ctx* ctx, int64_t total_items) {
-  const int per_cu = std::max(1, env_int("ZH_BLOCKS_PER_CU", 16));
+  const int per_cu = std::max(1, env_int("ZH_BLOCKS_PER_CU", 32));
   int64_t g = (int64_t)ctx->cu_count * per_cu;
   return (int)std::max<int64_t>(1, std::min<int64_t>(g, total_items));
 }
@@ -420,6 +516,9 @@ void plan_free(zh_plan* p) {
   (void)hipFree(p->d_crc_partials);
   (void)hipFree(p->d_input);
   (void)hipFree(p->d_out);
+  (void)hipFree(p->d_desc);
+  (void)hipFree(p->d_slow);
+  (void)hipFree(p->d_fast_tab);
   for (auto& e : p->ev_pending)
     for (auto ev : e) p->ev_pool.push_back(ev);
   for (auto ev : p->ev_pool) (void)hipEventDestroy(ev);
@@ -599,11 +698,30 @@ int zh_plan_create(zh_ctx* ctx, const zh_array_meta* m, const zh_chunk_src* chun
     plan_free(p);
     return ZH_EHIP;
   }
+  std::vector<uint32_t> tab = setup_fast(m, p->args, p->tile_mode);
+  if ((st = dev_alloc(&p->d_desc, (size_t)items, err, errlen)) != ZH_OK ||
+      (st = dev_alloc(&p->d_slow, (size_t)items + 4, err, errlen)) != ZH_OK ||
+      (st = dev_alloc(&p->d_fast_tab, tab.size(), err, errlen)) != ZH_OK) {
+    plan_free(p);
+    return st;
+  }
+  if (!tab.empty() &&
+      hipMemcpy(p->d_fast_tab, tab.data(), tab.size() * 4, hipMemcpyHostToDevice) != hipSuccess) {
+    set_err(err, errlen, "plan upload failed");
+    plan_free(p);
+    return ZH_EHIP;
+  }
+  p->args.desc = p->d_desc;
+  p->args.fast_tab = p->d_fast_tab;
+  p->args.n_citems = items;
+  p->args.slow_count = p->d_slow;
+  p->args.slow_list = p->d_slow + 4;
   p->args.shards = p->d_shards;
   p->args.nshards = ncoords;
   p->args.total_items = items << p->args.piece_shift;
   p->args.status = p->d_status;
   p->grid = grid_for(ctx, p->args.total_items);
+  p->slow_grid = p->grid;
   *out = p;
   return ZH_OK;
 }
@@ -618,6 +736,7 @@ int zh_plan_execute(zh_plan* p, void* out, void* stream_v) {
     ZH_HIP(hipMemcpyAsync(p->d_input + p->h2d[k].first, p->h2d[k].second, (size_t)p->h2d_len[k],
                           hipMemcpyHostToDevice, s));
   ZH_HIP(hipMemsetAsync(p->d_status, 0, (size_t)p->nshards * kStWords * sizeof(uint64_t), s));
+  ZH_HIP(hipMemsetAsync(p->d_slow, 0, sizeof(uint32_t), s));
   std::array<hipEvent_t, 3> ev{};
   if (p->timing) {
     for (int k = 0; k < 3; k++) {
@@ -633,10 +752,12 @@ int zh_plan_execute(zh_plan* p, void* out, void* stream_v) {
   }
   ZH_HIP(launch_crc(p->d_crc_jobs, p->n_crc_jobs, p->n_crc_spans, p->d_crc_partials, p->d_status,
                     s));
-  if (p->timing) ZH_HIP(hipEventRecord(ev[1], s));
   ScatterArgs a = p->args;
   a.region = (p->flags & ZH_OUT_DEVICE) ? (uint8_t*)out : p->d_out;
+  ZH_HIP(launch_resolve(a, s));
+  if (p->timing) ZH_HIP(hipEventRecord(ev[1], s));
   ZH_HIP(launch_scatter(a, p->meta.dtype_size, p->tile_mode, 0, p->grid, s));
+  ZH_HIP(launch_decode_slow(a, p->slow_grid, s));
   if (p->timing) {
     ZH_HIP(hipEventRecord(ev[2], s));
     p->ev_pending.push_back(ev);

@@ -56,6 +56,19 @@ struct DevShard {
   int32_t part_hi[kMaxDims];
 };
 
+// Per-inner-chunk work descriptor written by the resolve kernel (index parse) and read
+// by the scatter kernel, one item ahead of use.
+enum : int32_t { kFastNone = 0, kFastRowArith = 1, kFastRowTable = 2, kFastTileTable = 3 };
+enum : uint32_t { kDescFullCopy = 0, kDescFullFill = 1, kDescClip = 2, kDescSkip = 3,
+                  kDescModeMask = 0xFF, kDescFast = 0x100 };
+struct ItemDesc {
+  uint64_t src;   // absolute address of the inner chunk's bytes (kDescFullCopy)
+  int64_t d0;     // destination element offset of the inner chunk origin
+  uint64_t fill;  // kDescFullFill value (fill_value for a missing shard, 0 for Q1)
+  uint32_t kind;
+  uint32_t shard;
+};
+
 // Uniform launch arguments of the decode/encode scatter kernels.
 struct ScatterArgs {
   const DevShard* shards;
@@ -80,6 +93,22 @@ struct ScatterArgs {
   int64_t inner_nbytes;
   uint64_t fill;                // fill_value bytes (little-endian), replicated as needed
   FastDiv inner_div[kMaxDims];  // divisors for unclipped extents
+  // decode fast path for unclipped inner chunks
+  ItemDesc* desc;               // per inner chunk (resolve kernel output)
+  int32_t fast_mode;            // kFastNone / kFastRowArith / kFastRowTable / kFastTileTable
+  int32_t fast_vpr_shift;       // row modes: log2(16-byte vectors per row)
+  int32_t fast_rows;            // row modes: rows (tile mode: 32x32 units) per inner chunk
+  const uint32_t* fast_tab;     // (src, dst) element offsets per row / tile unit
+  int32_t fast_n;               // table entries (0: no table)
+  int32_t rm_n;                 // kFastRowArith: row dims (innermost first)
+  int32_t rm_shift[3];          //   log2 extent of each row dim
+  int64_t rm_sstr[3];           //   payload element stride of each row dim
+  int64_t rm_dstr[3];           //   region element stride of each row dim
+  int64_t n_citems;             // inner-chunk items (without pieces)
+  uint32_t* slow_list;          // inner chunks that need the generic path (resolve output)
+  uint32_t* slow_count;
+  int32_t dsize;
+  int32_t tile;
 };
 
 struct CrcJob {
@@ -93,8 +122,10 @@ struct CrcJob {
 // Kernel launchers (zh_kernels.hip).
 hipError_t launch_crc(const CrcJob* jobs, int64_t njobs, int64_t nspans, uint32_t* partials,
                       uint64_t* status, hipStream_t stream);
+hipError_t launch_resolve(const ScatterArgs& a, hipStream_t stream);
 hipError_t launch_scatter(const ScatterArgs& a, int dsize, int tile_mode, int encode, int grid,
                           hipStream_t stream);
+hipError_t launch_decode_slow(const ScatterArgs& a, int grid, hipStream_t stream);
 hipError_t launch_flags(const ScatterArgs& a, int dsize, int grid, hipStream_t stream);
 hipError_t launch_synth_fill(void* dst, int64_t n, int dsize, int64_t first, uint64_t seed,
                              hipStream_t stream);

@@ -3,10 +3,12 @@
 //   crc_partial / crc_finalize   sharding index CRC-32C (Crc32cCodec.decode,
 //                                M/v3/codec/core/Crc32cCodec.java:24-48; CRC32C.java:119-125):
 //                                per-lane slicing-by-8 segment CRCs combined in GF(2)
-//   scatter<DS,ENC,TILE>         the per-inner-chunk codec chain + region scatter
+//   resolve                      index parse: one 32-byte descriptor per inner chunk
+//                                (ShardingIndexedCodec.java:206-230)
+//   decode<DS,TILE>              the per-inner-chunk codec chain + region scatter
 //                                (ShardingIndexedCodec.decodeInternal :183-243, BytesCodec.decode,
-//                                TransposeCodec.decode, MultiArrayUtils.copyRegion) and, with
-//                                ENC, the inverse (ShardingIndexedCodec.encode payload writes)
+//                                TransposeCodec.decode, MultiArrayUtils.copyRegion)
+//   encode<DS,TILE>              the inverse (ShardingIndexedCodec.encode payload writes)
 //   flags                        encode pre-pass: inner chunk all fill_value? (:129-133)
 //   synth_fill / synth_verify    synthetic data for the bench and full-size property tests
 //
@@ -15,6 +17,9 @@
 // stages 32x32-element tiles through padded LDS so that both the read (payload-fast
 // axis) and the write (region-fast axis) are whole 128-byte rows.
 #include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdlib>
 
 #include "zh_internal.h"
 
@@ -524,34 +529,412 @@ __device__ __forceinline__ void tile_pass(const ScatterArgs& a, const Item& it,
 }
 
 // ---------------------------------------------------------------------------------
-// scatter kernel: one workgroup per work item (grid-stride over items)
+// resolve kernel (index parse): one thread per inner chunk → ItemDesc.  Validates the
+// index entry (ShardingIndexedCodec.java:215-230) and classifies the item so that the
+// scatter kernel's per-item work is a single 32-byte descriptor load, issued one item
+// ahead.
 // ---------------------------------------------------------------------------------
-template <int DS, bool ENC, bool TILE>
-__global__ __launch_bounds__(kBlock) void scatter_kernel(ScatterArgs a) {
+__device__ __forceinline__ ItemDesc resolve_one(const ScatterArgs& a, int64_t citem) {
+  ItemDesc D;
+  D.src = 0;
+  D.d0 = 0;
+  D.fill = 0;
+  D.kind = kDescSkip;
+  const int n = a.ndim;
+  const int64_t s = find_shard(a, citem);
+  const DevShard& S = a.shards[s];
+  D.shard = (uint32_t)s;
+  uint32_t j = (uint32_t)(citem - S.item_begin);
+  int32_t ic[kMaxDims];
+#pragma unroll
+  for (int d = kMaxDims - 1; d >= 0; --d) {
+    ic[d] = 0;
+    if (d < n) {
+      const uint32_t c = (uint32_t)S.box_count[d];
+      const uint32_t q = j / c;
+      ic[d] = S.box_start[d] + (int32_t)(j - q * c);
+      j = q;
+    }
+  }
+  bool full = true;
+  int64_t d0 = S.out_base, lin = 0;
+#pragma unroll
+  for (int d = 0; d < kMaxDims; d++) {
+    if (d >= n) continue;
+    const int32_t io = ic[d] * a.inner[d];
+    const int32_t lo = max(io, S.part_lo[d]) - io;
+    const int32_t hi = min(io + a.inner[d], S.part_hi[d]) - io;
+    full &= lo == 0 && hi == a.inner[d];
+    d0 += (int64_t)(io + lo - S.part_lo[d]) * a.rstride[d];
+    lin += (int64_t)ic[d] * a.cps_stride[d];
+  }
+  D.d0 = d0;
+  if (S.data == nullptr) {  // missing shard → fill_value (Array.java:400-402, 419-421)
+    D.kind = full ? kDescFullFill : kDescClip;
+    D.fill = a.fill;
+    return D;
+  }
+  const uint8_t* src = S.data;
+  if (a.sharded) {
+    const uint8_t* ent = S.data + S.index_off + 16 * lin;
+    const uint64_t off = ld_u64_unaligned(ent, a.index_be);
+    const uint64_t nb = ld_u64_unaligned(ent + 8, a.index_be);
+    if (off == ~0ull || nb == ~0ull) {  // Q1: zero-initialised part array
+      D.kind = full ? kDescFullFill : kDescClip;
+      D.fill = 0;
+      return D;
+    }
+    const uint64_t total = (uint64_t)S.nbytes;
+    const bool range_ok = off <= total && nb <= total - off;
+    if (!range_ok || nb != (uint64_t)a.inner_nbytes) {
+      const uint32_t kind = range_ok ? kFlagLength : kFlagRange;
+      const uint64_t key = ((uint64_t)(0xFFFFFFFFu - (uint32_t)lin) << 8) | kind;
+      atomicOr((unsigned long long*)(a.status + s * kStWords + kStFlags), (unsigned long long)kind);
+      atomicMax((unsigned long long*)(a.status + s * kStWords + kStBadChunk),
+                (unsigned long long)key);
+      D.kind = kDescSkip;
+      return D;
+    }
+    src = S.data + off;
+  }
+  D.src = (uint64_t)(uintptr_t)src;
+  D.kind = full ? kDescFullCopy : kDescClip;
+  return D;
+}
+
+// Can the fast kernel take this item?  (table present, 16-byte aligned ends; the tile
+// table path moves uint32 copies only)
+__device__ __forceinline__ bool is_fast(const ScatterArgs& a, const ItemDesc& D) {
+  const uint32_t mode = D.kind & kDescModeMask;
+  if (a.fast_mode == kFastNone || (mode != kDescFullCopy && mode != kDescFullFill)) return false;
+  if ((((uintptr_t)a.region) + (uint64_t)D.d0 * a.dsize) & 15) return false;
+  if (mode == kDescFullCopy && (D.src & 15)) return false;
+  if (a.tile && (a.dsize != 4 || mode != kDescFullCopy)) return false;
+  return true;
+}
+
+__global__ __launch_bounds__(kBlock) void resolve_kernel(ScatterArgs a) {
+  const int64_t stride = (int64_t)gridDim.x * kBlock;
+  for (int64_t c = (int64_t)blockIdx.x * kBlock + threadIdx.x; c < a.n_citems; c += stride) {
+    ItemDesc D = resolve_one(a, c);
+    if ((D.kind & kDescModeMask) != kDescSkip) {
+      if (is_fast(a, D)) {
+        D.kind |= kDescFast;
+      } else {
+        const uint32_t slot = atomicAdd(a.slow_count, 1u);
+        a.slow_list[slot] = (uint32_t)c;
+      }
+    }
+    a.desc[c] = D;
+  }
+}
+
+// descriptor load into scalar registers (vector load + readfirstlane: tracked by vmcnt,
+// so the one-item-ahead prefetch never forces an early lgkmcnt wait)
+__device__ __forceinline__ uint32_t rfl(uint32_t v) {
+  // readfirstlane is int-typed: keep it unsigned so 64-bit assembly never sign-extends
+  return (uint32_t)__builtin_amdgcn_readfirstlane((int)v);
+}
+
+__device__ __forceinline__ ItemDesc ld_desc(const ItemDesc* p) {
+  const uint4* q = reinterpret_cast<const uint4*>(p);
+  const uint4 x = q[0], y = q[1];
+  ItemDesc D;
+  D.src = ((uint64_t)rfl(x.y) << 32) | (uint64_t)rfl(x.x);
+  D.d0 = (int64_t)(((uint64_t)rfl(x.w) << 32) | (uint64_t)rfl(x.z));
+  D.fill = ((uint64_t)rfl(y.y) << 32) | (uint64_t)rfl(y.x);
+  D.kind = rfl(y.z);
+  D.shard = rfl(y.w);
+  return D;
+}
+
+// Unclipped item as an Item (geometry is the launch-uniform inner chunk).
+__device__ __forceinline__ void full_item(const ScatterArgs& a, const ItemDesc& D, uint32_t piece,
+                                          Item& it) {
+  it.sbase = (const uint8_t*)(uintptr_t)D.src;
+  it.dbase = a.region;
+  it.s0 = 0;
+  it.d0 = D.d0;
+  it.fill = D.fill;
+  it.mode = (D.kind & kDescModeMask) == kDescFullFill ? kFill : kCopy;
+  it.piece = piece;
+#pragma unroll
+  for (int d = 0; d < kMaxDims; d++) {
+    it.e[d] = a.inner[d];
+    it.v[d] = a.inner[d];
+    it.ediv[d] = a.inner_div[d];
+  }
+}
+
+// Fast tile path (uint32): full 32x32 tiles whose origins come from the LDS table; the next
+// group's global loads are issued before the current group's LDS reads and stores.
+template <int TPB>
+__device__ __forceinline__ void fast_tiles(const ScatterArgs& a, const uint2* tab,
+                                           const uint8_t* src, uint8_t* dst, uint32_t piece,
+                                           uint32_t (*tile)[32][33]) {
+  const int tid = threadIdx.x, l = tid >> 3, g = tid & 7;
+  const int64_t s_fd = a.pstride[a.fd], d_fs = a.rstride[a.fs];
+  const uint32_t units = (uint32_t)a.fast_n, pieces = 1u << a.piece_shift;
+  const uint32_t u0 = (uint32_t)(((uint64_t)units * piece) / pieces);
+  const uint32_t u1 = (uint32_t)(((uint64_t)units * (piece + 1)) / pieces);
+  uint4 x[TPB];
+#pragma unroll
+  for (int t = 0; t < TPB; t++)
+    if (u0 + t < u1) x[t] = ld16(src + ((size_t)tab[u0 + t].x + (size_t)l * s_fd + g * 4) * 4);
+  for (uint32_t ub = u0; ub < u1; ub += TPB) {
+#pragma unroll
+    for (int t = 0; t < TPB; t++) {
+      if (ub + t < u1) {
+        uint32_t* row = &tile[t][l][g * 4];
+        row[0] = xform1<4>(x[t].x, a.swap, 0);
+        row[1] = xform1<4>(x[t].y, a.swap, 0);
+        row[2] = xform1<4>(x[t].z, a.swap, 0);
+        row[3] = xform1<4>(x[t].w, a.swap, 0);
+      }
+    }
+    __syncthreads();
+    const uint32_t nb = ub + TPB;
+#pragma unroll
+    for (int t = 0; t < TPB; t++)
+      if (nb + t < u1) x[t] = ld16(src + ((size_t)tab[nb + t].x + (size_t)l * s_fd + g * 4) * 4);
+#pragma unroll
+    for (int t = 0; t < TPB; t++) {
+      if (ub + t < u1) {
+        uint4 y;
+        y.x = tile[t][g * 4 + 0][l];
+        y.y = tile[t][g * 4 + 1][l];
+        y.z = tile[t][g * 4 + 2][l];
+        y.w = tile[t][g * 4 + 3][l];
+        st16(dst + ((size_t)tab[ub + t].y + (size_t)l * d_fs + g * 4) * 4, y);
+      }
+    }
+    __syncthreads();
+  }
+}
+
+constexpr int kFastTPB = 4;
+
+template <int DS, bool TILE>
+__device__ __forceinline__ void generic_item(const ScatterArgs& a, Item& it,
+                                             typename ElemT<DS>::T (*tile)[32][33]) {
+  const int64_t* sstr = a.pstride;
+  const int64_t* dstr = a.rstride;
+  const int n = a.ndim;
+  if (it.mode == kFill || !TILE) {
+    const int F = it.mode == kFill ? a.fd : a.fs;
+    uint32_t nrows = 1;
+#pragma unroll
+    for (int d = 0; d < kMaxDims; d++)
+      if (d < n && d != F) nrows *= (uint32_t)it.e[d];
+    const bool need_src = it.mode != kFill;
+    if (vec_ok<DS>(a, it, F, sstr, dstr, it.e, need_src))
+      row_pass<DS, true, false>(a, it, F, sstr, dstr, nrows, it.e, it.ediv);
+    else
+      row_pass<DS, false, false>(a, it, F, sstr, dstr, nrows, it.e, it.ediv);
+  } else {
+    tile_pass<DS>(a, it, sstr, dstr, tile);
+  }
+}
+
+// Row offsets (payload, region) of row r of an unclipped inner chunk.
+__device__ __forceinline__ void row_offsets(const ScatterArgs& a, const uint2* tab, uint32_t r,
+                                            uint64_t& so, uint64_t& dof) {
+  if (a.fast_mode == kFastRowTable) {
+    const uint2 t = tab[r];
+    so = t.x;
+    dof = t.y;
+    return;
+  }
+  so = 0;
+  dof = 0;
+#pragma unroll
+  for (int i = 0; i < 3; i++) {
+    if (i < a.rm_n) {
+      const uint32_t m = i + 1 < a.rm_n ? (r & ((1u << a.rm_shift[i]) - 1)) : r;
+      so += (uint64_t)m * (uint64_t)a.rm_sstr[i];
+      dof += (uint64_t)m * (uint64_t)a.rm_dstr[i];
+      r >>= a.rm_shift[i];
+    }
+  }
+}
+
+// decode, fast row kernel: unclipped aligned items whose rows (along the unit-stride dim)
+// are whole 16-byte vectors.  Each lane owns one 16-byte column; the block walks
+// (item, row batch) steps uniformly, and the loads of step k+1 are issued before the
+// stores of step k, across item boundaries (vmcnt counts stores, so un-pipelined code
+// would wait for the previous stores before every batch of loads).
+template <int DS, int U>
+__global__ __launch_bounds__(kBlock) void decode_rows_kernel(ScatterArgs a) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  uint2* tab = reinterpret_cast<uint2*>(smem);
+  for (int i = threadIdx.x; i < a.fast_n; i += kBlock)
+    tab[i] = reinterpret_cast<const uint2*>(a.fast_tab)[i];
+  __syncthreads();
+  const int vs = a.fast_vpr_shift;
+  const uint32_t col = (threadIdx.x & ((1u << vs) - 1)) * 16;
+  const uint32_t lr = threadIdx.x >> vs;
+  const uint32_t rstep = kBlock >> vs;
+  const uint32_t nrows = (uint32_t)a.fast_rows, pieces = 1u << a.piece_shift;
+  const uint32_t pmask = pieces - 1;
+  const int64_t total = a.total_items;
+
+  // block-uniform walk over this block's fast items
+  int64_t item = blockIdx.x;
+  ItemDesc D, Dn;
+  if (item >= total) return;
+  D = ld_desc(a.desc + (item >> a.piece_shift));
+  Dn = D;
+  if (item + gridDim.x < total) Dn = ld_desc(a.desc + ((item + gridDim.x) >> a.piece_shift));
+  // seek to a fast item (item, D, Dn advance together)
+  auto seek = [&]() -> bool {
+    while (item < total && !(D.kind & kDescFast)) {
+      item += gridDim.x;
+      D = Dn;
+      if (item + gridDim.x < total) Dn = ld_desc(a.desc + ((item + gridDim.x) >> a.piece_shift));
+    }
+    return item < total;
+  };
+  if (!seek()) return;
+
+  // current step
+  const uint8_t* src;
+  uint8_t* dst;
+  bool fill;
+  uint4 fv;
+  uint32_t rbase, r1;
+  auto start_item = [&]() {
+    const uint32_t piece = (uint32_t)item & pmask;
+    rbase = (uint32_t)(((uint64_t)nrows * piece) / pieces);
+    r1 = (uint32_t)(((uint64_t)nrows * (piece + 1)) / pieces);
+    src = (const uint8_t*)(uintptr_t)D.src + col;
+    dst = a.region + D.d0 * DS + col;
+    fill = (D.kind & kDescModeMask) == kDescFullFill;
+    fv = fill16<DS>(D.fill);
+  };
+  start_item();
+
+  uint4 va[U];
+  uint64_t da[U];
+  auto load_step = [&](uint4* v, uint64_t* dd) {
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const uint32_t r = rbase + lr + u * rstep;
+      dd[u] = ~0ull;
+      v[u] = fv;
+      if (r < r1) {
+        uint64_t so, dof;
+        row_offsets(a, tab, r, so, dof);
+        dd[u] = dof * DS;
+        if (!fill) v[u] = ld16(src + so * DS);
+      }
+    }
+  };
+  load_step(va, da);
+  const uint8_t* dst_a = dst;
+  bool fill_a = fill;
+  uint4 fv_a = fv;
+  for (;;) {
+    // advance one step (uniform)
+    rbase += rstep * U;
+    bool more = true;
+    if (rbase >= r1) {
+      item += gridDim.x;
+      D = Dn;
+      if (item + gridDim.x < total) Dn = ld_desc(a.desc + ((item + gridDim.x) >> a.piece_shift));
+      more = seek();
+      if (more) start_item();
+    }
+    uint4 vb[U];
+    uint64_t db[U];
+    if (more) load_step(vb, db);
+#pragma unroll
+    for (int u = 0; u < U; u++)
+      if (da[u] != ~0ull)
+        st16(const_cast<uint8_t*>(dst_a) + da[u],
+             fill_a ? fv_a : xform16<DS>(va[u], a.swap, a.is_bool));
+    if (!more) break;
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      va[u] = vb[u];
+      da[u] = db[u];
+    }
+    dst_a = dst;
+    fill_a = fill;
+    fv_a = fv;
+  }
+}
+
+// decode, fast tile kernel: unclipped aligned uint32 copies through 32x32 LDS tiles whose
+// origins come from the LDS table
+__global__ __launch_bounds__(kBlock) void decode_tiles_kernel(ScatterArgs a) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  uint2* tab = reinterpret_cast<uint2*>(smem);
+  uint32_t(*tile)[32][33] =
+      reinterpret_cast<uint32_t(*)[32][33]>(smem + (((size_t)a.fast_n * 8 + 15) & ~(size_t)15));
+  for (int i = threadIdx.x; i < a.fast_n; i += kBlock)
+    tab[i] = reinterpret_cast<const uint2*>(a.fast_tab)[i];
+  __syncthreads();
+  const int64_t total = a.total_items;
+  const uint32_t pmask = (1u << a.piece_shift) - 1;
+  int64_t item = blockIdx.x;
+  if (item >= total) return;
+  ItemDesc D = ld_desc(a.desc + (item >> a.piece_shift));
+  for (; item < total; item += gridDim.x) {
+    const int64_t nxt = item + gridDim.x;
+    ItemDesc Dn = D;
+    if (nxt < total) Dn = ld_desc(a.desc + (nxt >> a.piece_shift));
+    if (D.kind & kDescFast)
+      fast_tiles<kFastTPB>(a, tab, (const uint8_t*)(uintptr_t)D.src, a.region + D.d0 * 4,
+                           (uint32_t)item & pmask, tile);
+    D = Dn;
+  }
+}
+
+// decode, slow kernel: the items the resolve kernel listed (clipped by the region,
+// misaligned, or without a fast table), through the generic strided paths
+template <int DS, bool TILE>
+__global__ __launch_bounds__(kBlock) void decode_slow_kernel(ScatterArgs a) {
   using T = typename ElemT<DS>::T;
-  const int64_t* sstr = ENC ? a.rstride : a.pstride;
-  const int64_t* dstr = ENC ? a.pstride : a.rstride;
+  __shared__ T tile[TILE ? kTileTPB : 1][32][33];
+  const int64_t total = (int64_t)(*a.slow_count) << a.piece_shift;
+  const uint32_t pmask = (1u << a.piece_shift) - 1;
+  for (int64_t k = blockIdx.x; k < total; k += gridDim.x) {
+    const uint32_t citem = a.slow_list[k >> a.piece_shift];
+    const uint32_t piece = (uint32_t)k & pmask;
+    const ItemDesc D = ld_desc(a.desc + citem);
+    Item it;
+    if ((D.kind & kDescModeMask) == kDescClip) {
+      make_item<false>(a, ((int64_t)citem << a.piece_shift) | piece, it);
+      if (it.mode == kSkip) continue;
+    } else {
+      full_item(a, D, piece, it);
+    }
+    generic_item<DS, TILE>(a, it, tile);
+  }
+}
+
+// encode: the same geometry with source = region and destination = shard payload
+template <int DS, bool TILE>
+__global__ __launch_bounds__(kBlock) void encode_kernel(ScatterArgs a) {
+  using T = typename ElemT<DS>::T;
+  const int64_t* sstr = a.rstride;
+  const int64_t* dstr = a.pstride;
   for (int64_t item = blockIdx.x; item < a.total_items; item += gridDim.x) {
     Item it;
-    make_item<ENC>(a, item, it);
+    make_item<true>(a, item, it);
     if (it.mode == kSkip) continue;
     const int n = a.ndim;
-    if (it.mode == kFill || !TILE) {
-      // decode fills: constant rows along the destination-fast dim; copies: rows along
-      // the dim that is unit-stride on both sides
-      const int F = it.mode == kFill ? a.fd : a.fs;
+    if constexpr (!TILE) {
+      const int F = a.fs;  // == a.fd
       uint32_t nrows = 1;
 #pragma unroll
       for (int d = 0; d < kMaxDims; d++)
         if (d < n && d != F) nrows *= (uint32_t)it.e[d];
-      const bool need_src = it.mode != kFill;
-      if (vec_ok<DS>(a, it, F, sstr, dstr, it.e, need_src))
+      if (vec_ok<DS>(a, it, F, sstr, dstr, it.e, true))
         row_pass<DS, true, false>(a, it, F, sstr, dstr, nrows, it.e, it.ediv);
       else
         row_pass<DS, false, false>(a, it, F, sstr, dstr, nrows, it.e, it.ediv);
-      continue;
-    }
-    if constexpr (TILE) {
+    } else {
       __shared__ T tile[kTileTPB][32][33];
       tile_pass<DS>(a, it, sstr, dstr, tile);
     }
@@ -803,19 +1186,40 @@ hipError_t launch_crc(const CrcJob* jobs, int64_t njobs, int64_t nspans, uint32_
   return hipGetLastError();
 }
 
+hipError_t launch_resolve(const ScatterArgs& a, hipStream_t stream) {
+  if (a.n_citems == 0) return hipSuccess;
+  const int grid = (int)std::min<int64_t>((a.n_citems + kBlock - 1) / kBlock, 8192);
+  hipLaunchKernelGGL(resolve_kernel, dim3(grid), dim3(kBlock), 0, stream, a);
+  return hipGetLastError();
+}
+
 template <int DS>
 static void launch_scatter_ds(const ScatterArgs& a, int tile, int enc, int grid,
                               hipStream_t s) {
   if (enc) {
     if (tile)
-      hipLaunchKernelGGL((scatter_kernel<DS, true, true>), dim3(grid), dim3(kBlock), 0, s, a);
+      hipLaunchKernelGGL((encode_kernel<DS, true>), dim3(grid), dim3(kBlock), 0, s, a);
     else
-      hipLaunchKernelGGL((scatter_kernel<DS, true, false>), dim3(grid), dim3(kBlock), 0, s, a);
+      hipLaunchKernelGGL((encode_kernel<DS, false>), dim3(grid), dim3(kBlock), 0, s, a);
   } else {
-    if (tile)
-      hipLaunchKernelGGL((scatter_kernel<DS, false, true>), dim3(grid), dim3(kBlock), 0, s, a);
-    else
-      hipLaunchKernelGGL((scatter_kernel<DS, false, false>), dim3(grid), dim3(kBlock), 0, s, a);
+    size_t lds = ((size_t)a.fast_n * 8 + 15) & ~(size_t)15;
+    if (a.fast_mode == kFastTileTable) {
+      if (DS == 4) {
+        lds += (size_t)kFastTPB * 32 * 33 * 4;
+        hipLaunchKernelGGL(decode_tiles_kernel, dim3(grid), dim3(kBlock), lds, s, a);
+      }
+    } else if (a.fast_mode != kFastNone) {
+      static const int u = [] {
+        const char* e = getenv("ZH_FAST_U");
+        return e && atoi(e) == 8 ? 8 : (e && atoi(e) == 2 ? 2 : 4);
+      }();
+      if (u == 8)
+        hipLaunchKernelGGL((decode_rows_kernel<DS, 8>), dim3(grid), dim3(kBlock), lds, s, a);
+      else if (u == 2)
+        hipLaunchKernelGGL((decode_rows_kernel<DS, 2>), dim3(grid), dim3(kBlock), lds, s, a);
+      else
+        hipLaunchKernelGGL((decode_rows_kernel<DS, 4>), dim3(grid), dim3(kBlock), lds, s, a);
+    }
   }
 }
 
@@ -827,6 +1231,25 @@ hipError_t launch_scatter(const ScatterArgs& a, int dsize, int tile_mode, int en
     case 2: launch_scatter_ds<2>(a, tile_mode, encode, grid, stream); break;
     case 4: launch_scatter_ds<4>(a, tile_mode, encode, grid, stream); break;
     case 8: launch_scatter_ds<8>(a, tile_mode, encode, grid, stream); break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+template <int DS>
+static void launch_slow_ds(const ScatterArgs& a, int grid, hipStream_t s) {
+  if (a.tile)
+    hipLaunchKernelGGL((decode_slow_kernel<DS, true>), dim3(grid), dim3(kBlock), 0, s, a);
+  else
+    hipLaunchKernelGGL((decode_slow_kernel<DS, false>), dim3(grid), dim3(kBlock), 0, s, a);
+}
+
+hipError_t launch_decode_slow(const ScatterArgs& a, int grid, hipStream_t stream) {
+  switch (a.dsize) {
+    case 1: launch_slow_ds<1>(a, grid, stream); break;
+    case 2: launch_slow_ds<2>(a, grid, stream); break;
+    case 4: launch_slow_ds<4>(a, grid, stream); break;
+    case 8: launch_slow_ds<8>(a, grid, stream); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();
