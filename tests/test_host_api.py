@@ -1,0 +1,153 @@
+"""Host mirror of zarr-java's v3 surface (no GPU): metadata JSON, fill values, codec
+builder/registry/pipeline validation, chunk keys, store range reads.  Mirrors
+ZarrV3Test.testCheckInvalidCodecConfiguration / testCheckShardingBounds /
+testArrayMetadataBuilder / parseFillValue cases and StoreTest range semantics."""
+import json
+import os
+
+import pytest
+
+import zarrhip as z
+from helpers import GOLDEN
+
+
+def meta_with(codecs_fn, shape=(4, 4), chunk=(2, 2), dt=z.DataType.UINT32):
+    return (z.ArrayMetadataBuilder().withShape(*shape).withDataType(dt).withChunkShape(*chunk)
+            .withCodecs(codecs_fn).build())
+
+
+@pytest.mark.parametrize("fn", [
+    lambda c: c.withBytes("LITTLE").withBytes("LITTLE"),
+    lambda c: c.withBlosc().withBytes("LITTLE"),
+    lambda c: c.withBytes("LITTLE").withTranspose([1, 0]),
+    lambda c: c.withTranspose([1, 0]).withBytes("LITTLE").withTranspose([1, 0]),
+])
+def test_invalid_codec_configuration(fn):
+    m = meta_with(fn)
+    with pytest.raises(z.ZarrException):
+        z.device_chain(m.codecs, 2, 4)
+
+
+def test_pipeline_messages():
+    with pytest.raises(z.ZarrException, match=r"Exactly 1 ArrayBytesCodec is required. Found 2."):
+        z.device_chain(meta_with(lambda c: c.withBytes().withBytes()).codecs, 2, 4)
+
+
+@pytest.mark.parametrize("shard", [[3, 3], [4, 3], [5, 2]])
+def test_sharding_bounds(shard):
+    with pytest.raises(z.ZarrException, match="does not evenly divide"):
+        (z.ArrayMetadataBuilder().withShape(10, 10).withDataType(z.DataType.UINT32)
+         .withChunkShape(*shard)
+         .withCodecs(lambda c: c.withSharding([2, 2], lambda c1: c1.withBytes("LITTLE"))).build())
+
+
+@pytest.mark.parametrize("chunk", [[1], [1, 1, 1]])
+def test_invalid_chunk_dimensions(chunk):
+    with pytest.raises(z.ZarrException):
+        z.ArrayMetadataBuilder().withShape(4, 4).withDataType(z.DataType.UINT32) \
+            .withChunkShape(*chunk).build()
+
+
+def test_metadata_builder_baseline_shape():
+    """testArrayMetadataBuilder (ZarrV3Test.java:360-384): the BASELINE shape."""
+    m = (z.ArrayMetadataBuilder().withShape(1, 4096, 4096, 1536).withDataType(z.DataType.UINT32)
+         .withChunkShape(1, 1024, 1024, 1024).withFillValue(0)
+         .withCodecs(lambda c: c.withSharding([1, 32, 32, 32])).build())
+    j = m.to_json()
+    assert j["shape"] == [1, 4096, 4096, 1536]
+    sh = j["codecs"][0]
+    assert sh["name"] == "sharding_indexed"
+    assert sh["configuration"]["chunk_shape"] == [1, 32, 32, 32]
+    assert sh["configuration"]["index_codecs"] == [
+        {"name": "bytes", "configuration": {"endian": "little"}}, {"name": "crc32c"}]
+    assert sh["configuration"]["index_location"] == "end"
+    back = z.ArrayMetadata.from_json(json.loads(m.dumps()))
+    assert back.to_json() == j
+
+
+@pytest.mark.parametrize("fill,dt,val", [
+    ("0x00010203", z.DataType.UINT32, 50462976),   # ZarrV3Test.java:389
+    (0, z.DataType.UINT8, 0), (-1, z.DataType.UINT32, 0xFFFFFFFF), (4294967295, z.DataType.INT32, -1),
+    (True, z.DataType.BOOL, 1), ("0b00000001", z.DataType.UINT8, 1),
+])
+def test_fill_values(fill, dt, val):
+    b = z.parse_fill_value(fill, dt)
+    signed = dt.value_name.startswith("int")
+    assert int.from_bytes(b, "little", signed=signed) == val
+
+
+def test_fill_value_nan_float():
+    import math
+    import struct
+    assert math.isnan(struct.unpack("<f", z.parse_fill_value("NaN", z.DataType.FLOAT32))[0])
+    with pytest.raises(z.ZarrException):
+        z.parse_fill_value("NaN", z.DataType.INT32)
+
+
+def test_fixture_metadata_roundtrip():
+    for loc in ("start", "end"):
+        j = json.load(open(os.path.join(GOLDEN, "sharding_index_location", loc, "zarr.json")))
+        m = z.ArrayMetadata.from_json(j)
+        assert m.shape == [16, 16, 16] and m.chunk_shape == [16, 8, 8]
+        sh = m.codecs[0]
+        assert sh.index_location == loc and sh.chunk_shape == [8, 4, 8]
+        dc = z.device_chain(m.codecs, 3, 4)
+        assert dc.chain["transpose_order"] == [2, 1, 0] and dc.chain["index_crc32c"]
+        assert [type(c).__name__ for c in dc.inner_host_bb] == ["BloscCodec"]
+        out = m.to_json()
+        for k in ("shape", "data_type", "chunk_grid", "codecs", "fill_value"):
+            assert out[k] == j[k]
+
+
+def test_chunk_key_encoding():
+    assert z.ChunkKeyEncoding("default", "/").encode_chunk_key([0, 3, 1]) == ["c", "0", "3", "1"]
+    assert z.ChunkKeyEncoding("default", ".").encode_chunk_key([0, 3, 1]) == ["c.0.3.1"]
+    assert z.ChunkKeyEncoding("v2", ".").encode_chunk_key([0, 3, 1]) == ["0.3.1"]
+    assert z.ChunkKeyEncoding("v2", "/").encode_chunk_key([2, 1]) == ["2", "1"]
+
+
+def test_registry_add_type_replaces():
+    class MySharding(z.ShardingIndexedCodec):
+        pass
+    old = z.CodecRegistry.map["sharding_indexed"]
+    try:
+        z.CodecRegistry.addType("sharding_indexed", MySharding)
+        c = z.CodecRegistry.codec_from_json({"name": "sharding_indexed", "configuration": {
+            "chunk_shape": [2], "codecs": [{"name": "bytes", "configuration": {"endian": "little"}}],
+            "index_codecs": [{"name": "bytes", "configuration": {"endian": "little"}}]}})
+        assert type(c) is MySharding
+    finally:
+        z.CodecRegistry.addType("sharding_indexed", old)
+
+
+def test_unsupported_chains_are_flagged():
+    m = meta_with(lambda c: c.withSharding([1, 1], lambda c1: c1.withSharding([1, 1])))
+    with pytest.raises(z.UnsupportedChainError):
+        z.device_chain(m.codecs, 2, 4)
+    m = meta_with(lambda c: c.withTranspose([1, 0]).withSharding([1, 1]))
+    with pytest.raises(z.ZarrException):
+        z.device_chain(m.codecs, 2, 4)
+
+
+def test_bytes_without_configuration_multibyte():
+    m = meta_with(lambda c: c.withBytes("LITTLE"))
+    m.codecs[0] = z.BytesCodec(None)
+    with pytest.raises(z.ZarrException, match="BytesCodec configuration is required"):
+        z.device_chain(m.codecs, 2, 4)
+    assert z.device_chain(m.codecs, 2, 1).chain["endian"] == 1  # 1-byte types ignore endian
+
+
+@pytest.mark.parametrize("store_cls", ["fs", "mem"])
+def test_store_range_reads(tmp_path, store_cls):
+    """StoreTest.java:83-107: read(5,15) and read(size-10) semantics."""
+    s = z.FilesystemStore(tmp_path) if store_cls == "fs" else z.MemoryStore()
+    h = s.resolve("a", "b")
+    assert h.read() is None and not h.exists()
+    data = bytes(range(100))
+    h.set(data)
+    assert h.exists() and h.read() == data
+    assert h.read(5, 15) == data[5:15]
+    assert h.read(len(data) - 10) == data[-10:]
+    assert h.read(-10) == data[-10:]
+    h.delete()
+    assert not h.exists()

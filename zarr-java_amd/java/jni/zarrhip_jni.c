@@ -1,0 +1,162 @@
+/*
+ * zarrhip_jni.c — thin JNI shim from zarr-java to the zarrhip C-ABI (include/zarrhip.h).
+ * Built only where a JDK exists (needs $JAVA_HOME/include/jni.h); see INTEGRATION.md.
+ *
+ * Every native method assembles a zh_array_meta from Java primitives, pins the Java
+ * arrays for the duration of the call (GetPrimitiveArrayCritical: no JNI calls while
+ * pinned), and maps zh_status to the reference's exceptions:
+ *   ZH_EDATA → dev.zarr.zarrjava.ZarrException, ZH_EINVAL → IllegalArgumentException,
+ *   ZH_EARITH → ArithmeticException, ZH_EUNSUPPORTED → returned as 3 (Java falls back to
+ *   the reference codec), anything else → RuntimeException.
+ */
+#include <jni.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "zarrhip.h"
+
+static int throw_status(JNIEnv* env, int st, const char* msg) {
+  const char* cls = "java/lang/RuntimeException";
+  if (st == ZH_EDATA) cls = "dev/zarr/zarrjava/ZarrException";
+  else if (st == ZH_EINVAL) cls = "java/lang/IllegalArgumentException";
+  else if (st == ZH_EARITH) cls = "java/lang/ArithmeticException";
+  jclass c = (*env)->FindClass(env, cls);
+  if (c) (*env)->ThrowNew(env, c, msg && *msg ? msg : "zarrhip error");
+  return st;
+}
+
+JNIEXPORT jlong JNICALL Java_dev_zarr_zarrjava_hip_ZarrHip_ctxCreate(JNIEnv* env, jclass cls,
+                                                                    jint device) {
+  (void)cls;
+  zh_ctx* ctx = NULL;
+  int st = zh_ctx_create(device, &ctx);
+  if (st != ZH_OK) {
+    throw_status(env, ZH_EHIP, "zh_ctx_create failed: no usable MI355X device");
+    return 0;
+  }
+  return (jlong)(intptr_t)ctx;
+}
+
+JNIEXPORT void JNICALL Java_dev_zarr_zarrjava_hip_ZarrHip_ctxDestroy(JNIEnv* env, jclass cls,
+                                                                    jlong ctx) {
+  (void)env;
+  (void)cls;
+  zh_ctx_destroy((zh_ctx*)(intptr_t)ctx);
+}
+
+/* meta: int[] {ndim, dtypeSize, isBool, sharded, hasTranspose, endian, indexEndian,
+ *              indexCrc32c, indexLocation}; shape long[ndim]; chunkShape/innerShape/order
+ *              int[ndim]; fill byte[dtypeSize] (little-endian element bytes). */
+static int build_meta(JNIEnv* env, jintArray jm, jlongArray jshape, jintArray jchunk,
+                      jintArray jinner, jintArray jorder, jbyteArray jfill, zh_array_meta* m) {
+  memset(m, 0, sizeof(*m));
+  jint mi[9];
+  (*env)->GetIntArrayRegion(env, jm, 0, 9, mi);
+  m->ndim = mi[0];
+  if (m->ndim <= 0 || m->ndim > ZH_MAX_DIMS) return ZH_EUNSUPPORTED;
+  m->dtype_size = mi[1];
+  m->dtype_is_bool = mi[2];
+  m->chain.sharded = mi[3];
+  m->chain.has_transpose = mi[4];
+  m->chain.endian = mi[5];
+  m->chain.index_endian = mi[6];
+  m->chain.index_has_crc32c = mi[7];
+  m->chain.index_location = mi[8];
+  jlong sh[ZH_MAX_DIMS];
+  jint ch[ZH_MAX_DIMS];
+  (*env)->GetLongArrayRegion(env, jshape, 0, m->ndim, sh);
+  (*env)->GetIntArrayRegion(env, jchunk, 0, m->ndim, ch);
+  for (int d = 0; d < m->ndim; d++) {
+    m->shape[d] = sh[d];
+    m->chunk_shape[d] = ch[d];
+  }
+  if (m->chain.sharded) (*env)->GetIntArrayRegion(env, jinner, 0, m->ndim, m->chain.inner_chunk_shape);
+  if (m->chain.has_transpose) (*env)->GetIntArrayRegion(env, jorder, 0, m->ndim, m->chain.transpose_order);
+  if (jfill) {
+    jsize n = (*env)->GetArrayLength(env, jfill);
+    (*env)->GetByteArrayRegion(env, jfill, 0, n < 8 ? n : 8, (jbyte*)m->fill_value);
+  }
+  return ZH_OK;
+}
+
+/* core.Array.read replacement: chunks[i] = bytes of the i-th chunk of
+ * computeChunkCoords(shape, chunkShape, offset, regionShape) or null (missing key);
+ * out = the primitive array behind the result ucar.ma2.Array (C order).
+ * Returns 0 on success, 3 (ZH_EUNSUPPORTED) to request the Java fallback. */
+JNIEXPORT jint JNICALL Java_dev_zarr_zarrjava_hip_ZarrHip_arrayRead(
+    JNIEnv* env, jclass cls, jlong ctx, jintArray jm, jlongArray jshape, jintArray jchunk,
+    jintArray jinner, jintArray jorder, jbyteArray jfill, jobjectArray jchunks,
+    jlongArray joffset, jlongArray jregion, jobject out) {
+  (void)cls;
+  zh_array_meta m;
+  int st = build_meta(env, jm, jshape, jchunk, jinner, jorder, jfill, &m);
+  if (st != ZH_OK) return st;
+  char err[1024] = {0};
+  st = zh_validate_meta(&m, err, sizeof err);
+  if (st == ZH_EUNSUPPORTED) return st;
+  if (st != ZH_OK) return throw_status(env, st, err);
+  jsize n = (*env)->GetArrayLength(env, jchunks);
+  zh_chunk_src* srcs = (zh_chunk_src*)calloc((size_t)(n > 0 ? n : 1), sizeof(zh_chunk_src));
+  jbyteArray* arrs = (jbyteArray*)calloc((size_t)(n > 0 ? n : 1), sizeof(jbyteArray));
+  /* copy chunk bytes out of the heap (several may be large: no long critical sections) */
+  void** copies = (void**)calloc((size_t)(n > 0 ? n : 1), sizeof(void*));
+  for (jsize i = 0; i < n; i++) {
+    arrs[i] = (jbyteArray)(*env)->GetObjectArrayElement(env, jchunks, i);
+    if (!arrs[i]) continue;
+    jsize len = (*env)->GetArrayLength(env, arrs[i]);
+    copies[i] = malloc((size_t)(len > 0 ? len : 1));
+    (*env)->GetByteArrayRegion(env, arrs[i], 0, len, (jbyte*)copies[i]);
+    srcs[i].data = copies[i];
+    srcs[i].nbytes = len;
+    (*env)->DeleteLocalRef(env, arrs[i]);
+  }
+  jlong off[ZH_MAX_DIMS], reg[ZH_MAX_DIMS];
+  (*env)->GetLongArrayRegion(env, joffset, 0, m.ndim, off);
+  (*env)->GetLongArrayRegion(env, jregion, 0, m.ndim, reg);
+  int64_t o64[ZH_MAX_DIMS], r64[ZH_MAX_DIMS];
+  for (int d = 0; d < m.ndim; d++) {
+    o64[d] = off[d];
+    r64[d] = reg[d];
+  }
+  void* dst = (*env)->GetPrimitiveArrayCritical(env, (jarray)out, NULL);
+  st = zh_array_read((zh_ctx*)(intptr_t)ctx, &m, srcs, n, o64, r64, dst, 0, NULL, err,
+                     sizeof err);
+  (*env)->ReleasePrimitiveArrayCritical(env, (jarray)out, dst, 0);
+  for (jsize i = 0; i < n; i++) free(copies[i]);
+  free(copies);
+  free(arrs);
+  free(srcs);
+  if (st == ZH_EUNSUPPORTED) return st;
+  if (st != ZH_OK) return throw_status(env, st, err);
+  return 0;
+}
+
+/* ShardingIndexedCodec.decode / decodePartial replacement for one shard's bytes. */
+JNIEXPORT jint JNICALL Java_dev_zarr_zarrjava_hip_ZarrHip_shardDecodePartial(
+    JNIEnv* env, jclass cls, jlong ctx, jintArray jm, jlongArray jshape, jintArray jchunk,
+    jintArray jinner, jintArray jorder, jbyteArray jfill, jbyteArray shard, jlongArray joffset,
+    jintArray jpart, jobject out) {
+  (void)cls;
+  zh_array_meta m;
+  int st = build_meta(env, jm, jshape, jchunk, jinner, jorder, jfill, &m);
+  if (st != ZH_OK) return st;
+  char err[1024] = {0};
+  jlong off[ZH_MAX_DIMS];
+  jint part[ZH_MAX_DIMS];
+  (*env)->GetLongArrayRegion(env, joffset, 0, m.ndim, off);
+  (*env)->GetIntArrayRegion(env, jpart, 0, m.ndim, part);
+  int64_t o64[ZH_MAX_DIMS];
+  for (int d = 0; d < m.ndim; d++) o64[d] = off[d];
+  jsize len = (*env)->GetArrayLength(env, shard);
+  void* src = malloc((size_t)(len > 0 ? len : 1));
+  (*env)->GetByteArrayRegion(env, shard, 0, len, (jbyte*)src);
+  void* dst = (*env)->GetPrimitiveArrayCritical(env, (jarray)out, NULL);
+  st = zh_sharding_decode_partial((zh_ctx*)(intptr_t)ctx, &m, src, len, o64, part, dst, 0, NULL,
+                                  err, sizeof err);
+  (*env)->ReleasePrimitiveArrayCritical(env, (jarray)out, dst, 0);
+  free(src);
+  if (st == ZH_EUNSUPPORTED) return st;
+  if (st != ZH_OK) return throw_status(env, st, err);
+  return 0;
+}

@@ -1,0 +1,85 @@
+package dev.zarr.zarrjava.hip;
+
+import dev.zarr.zarrjava.core.ArrayMetadata.CoreArrayMetadata;
+import dev.zarr.zarrjava.v3.codec.Codec;
+import dev.zarr.zarrjava.v3.codec.core.BytesCodec;
+import dev.zarr.zarrjava.v3.codec.core.Crc32cCodec;
+import dev.zarr.zarrjava.v3.codec.core.ShardingIndexedCodec;
+import dev.zarr.zarrjava.v3.codec.core.TransposeCodec;
+
+import java.nio.ByteBuffer;
+import java.nio.ByteOrder;
+
+/**
+ * Recognises the device-supported codec chains (zarrhip.h zh_codec_chain) and packs the
+ * zh_array_meta fields the JNI shim expects.  Anything else → null (use the reference).
+ */
+final class DeviceChain {
+    final int[] meta = new int[9];  // ndim, dtypeSize, isBool, sharded, hasTranspose, endian,
+                                    // indexEndian, indexCrc32c, indexLocation
+    final long[] shape;
+    final int[] chunkShape;
+    int[] innerShape;
+    int[] order;
+    final byte[] fill;
+
+    private DeviceChain(CoreArrayMetadata m) {
+        shape = m.shape.clone();
+        chunkShape = m.chunkShape.clone();
+        meta[0] = m.ndim();
+        meta[1] = m.dataType.getByteCount();
+        meta[2] = "bool".equals(m.dataType.toString().toLowerCase()) ? 1 : 0;
+        fill = fillBytes(m);
+    }
+
+    static byte[] fillBytes(CoreArrayMetadata m) {
+        int n = m.dataType.getByteCount();
+        ByteBuffer b = ByteBuffer.allocate(8).order(ByteOrder.LITTLE_ENDIAN);
+        Object f = m.parsedFillValue;
+        if (f instanceof Boolean) b.put((byte) (((Boolean) f) ? 1 : 0));
+        else if (f instanceof Byte) b.put((Byte) f);
+        else if (f instanceof Short) b.putShort((Short) f);
+        else if (f instanceof Integer) b.putInt((Integer) f);
+        else if (f instanceof Long) b.putLong((Long) f);
+        else if (f instanceof Float) b.putFloat((Float) f);
+        else if (f instanceof Double) b.putDouble((Double) f);
+        byte[] out = new byte[n];
+        System.arraycopy(b.array(), 0, out, 0, n);
+        return out;
+    }
+
+    private static boolean innerChain(DeviceChain d, Codec[] codecs) {
+        int i = 0;
+        if (i < codecs.length && codecs[i] instanceof TransposeCodec) {
+            d.meta[4] = 1;
+            d.order = ((TransposeCodec) codecs[i]).configuration.order.clone();
+            i++;
+        }
+        if (i >= codecs.length || !(codecs[i] instanceof BytesCodec)) return false;
+        BytesCodec bc = (BytesCodec) codecs[i];
+        d.meta[5] = bc.configuration != null
+                && bc.configuration.endian == BytesCodec.Endian.BIG ? 1 : 0;
+        return i + 1 == codecs.length;  // byte-to-byte codecs stay on the Java path
+    }
+
+    /** Chain of a v3 array's codec list, or null when not device-supported. */
+    static DeviceChain of(Codec[] codecs, CoreArrayMetadata m) {
+        DeviceChain d = new DeviceChain(m);
+        if (codecs.length == 1 && codecs[0] instanceof ShardingIndexedCodec) {
+            ShardingIndexedCodec.Configuration c = ((ShardingIndexedCodec) codecs[0]).configuration;
+            d.meta[3] = 1;
+            d.innerShape = c.chunkShape.clone();
+            if (!innerChain(d, c.codecs)) return null;
+            Codec[] ic = c.indexCodecs;
+            if (ic.length < 1 || ic.length > 2 || !(ic[0] instanceof BytesCodec)) return null;
+            if (ic.length == 2 && !(ic[1] instanceof Crc32cCodec)) return null;
+            BytesCodec ib = (BytesCodec) ic[0];
+            d.meta[6] = ib.configuration != null
+                    && ib.configuration.endian == BytesCodec.Endian.BIG ? 1 : 0;
+            d.meta[7] = ic.length == 2 ? 1 : 0;
+            d.meta[8] = "start".equals(c.indexLocation) ? 1 : 0;
+            return d;
+        }
+        return innerChain(d, codecs) ? d : null;
+    }
+}

@@ -1,0 +1,75 @@
+package dev.zarr.zarrjava.hip;
+
+import com.fasterxml.jackson.annotation.JsonCreator;
+import com.fasterxml.jackson.annotation.JsonProperty;
+import dev.zarr.zarrjava.ZarrException;
+import dev.zarr.zarrjava.core.ArrayMetadata.CoreArrayMetadata;
+import dev.zarr.zarrjava.store.StoreHandle;
+import dev.zarr.zarrjava.v3.codec.Codec;
+import dev.zarr.zarrjava.v3.codec.core.ShardingIndexedCodec;
+import ucar.ma2.Array;
+
+import javax.annotation.Nonnull;
+import java.nio.ByteBuffer;
+import java.util.Arrays;
+
+/**
+ * Drop-in `sharding_indexed` codec whose decode runs on the MI355X.  Registered with
+ * {@code CodecRegistry.addType("sharding_indexed", HipShardingIndexedCodec.class)}; it
+ * extends the reference codec so `instanceof ShardingIndexedCodec` discovery
+ * (v3/ArrayMetadata.java) and CodecPipeline.supportsPartialDecode keep working, and falls
+ * back to {@code super} for chains the device does not run.
+ */
+public class HipShardingIndexedCodec extends ShardingIndexedCodec {
+    private DeviceChain chain;
+
+    @JsonCreator(mode = JsonCreator.Mode.PROPERTIES)
+    public HipShardingIndexedCodec(
+            @Nonnull @JsonProperty(value = "configuration", required = true)
+            Configuration configuration) throws ZarrException {
+        super(configuration);
+    }
+
+    @Override
+    public void setCoreArrayMetadata(CoreArrayMetadata arrayMetadata) throws ZarrException {
+        super.setCoreArrayMetadata(arrayMetadata);
+        chain = ZarrHip.available() ? DeviceChain.of(new Codec[]{this}, arrayMetadata) : null;
+    }
+
+    private Array device(byte[] shard, long[] offset, int[] shape) throws ZarrException {
+        Array out = Array.factory(arrayMetadata.dataType.getMA2DataType(), shape);
+        int st = ZarrHip.shardDecodePartial(ZarrHip.ctx(), chain.meta, chain.shape,
+                chain.chunkShape, chain.innerShape, chain.order, chain.fill, shard, offset, shape,
+                out.getStorage());
+        return st == 0 ? out : null;
+    }
+
+    @Override
+    public Array decode(ByteBuffer shardBytes) throws ZarrException {
+        if (chain != null) {
+            byte[] b = new byte[shardBytes.remaining()];
+            shardBytes.duplicate().get(b);
+            Array a = device(b, new long[arrayMetadata.ndim()], arrayMetadata.chunkShape);
+            if (a != null) return a;
+        }
+        return super.decode(shardBytes);
+    }
+
+    @Override
+    public Array decodePartial(StoreHandle chunkHandle, long[] offset, int[] shape)
+            throws ZarrException {
+        if (chain != null) {
+            ByteBuffer bytes = chunkHandle.read();
+            if (bytes == null) {
+                return Arrays.equals(shape, arrayMetadata.chunkShape)
+                        ? arrayMetadata.allocateFillValueChunk()
+                        : super.decodePartial(chunkHandle, offset, shape);
+            }
+            byte[] b = new byte[bytes.remaining()];
+            bytes.duplicate().get(b);
+            Array a = device(b, offset, shape);
+            if (a != null) return a;
+        }
+        return super.decodePartial(chunkHandle, offset, shape);
+    }
+}

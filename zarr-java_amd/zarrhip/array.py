@@ -1,0 +1,296 @@
+"""v3 Array — the read/write surface of dev.zarr.zarrjava.v3.Array / core.Array, with the
+chunk codec work done by the HIP path through the C-ABI (libzarrhip.so).
+
+  Array.open / create        M/v3/Array.java:41-50, 142-154
+  read(offset, shape)        M/core/Array.java:378-441   → zh_array_read (one call, all chunks)
+  readChunk(coords)          M/core/Array.java:167-182
+  write(offset, data)        M/core/Array.java:83-133    → zh_array_write (whole chunks)
+  access()                   M/core/Array.java:483-536   (ArrayAccessor)
+
+Byte-to-byte compressors stay on the host (north star): their frames are decoded here and
+the raw chunk bytes are handed to the device.
+"""
+import ctypes as C
+import json
+import os
+import struct
+import threading
+
+import numpy as np
+
+from . import _abi as A
+from . import _lib
+from .codecs import device_chain, host_bb_decode, host_bb_encode
+from .errors import ZarrException, raise_for
+from .metadata import ZARR_JSON, ArrayMetadata
+
+_ctx = None
+_ctx_lock = threading.Lock()
+
+
+def device():
+    """The process-wide DeviceContext (GPU ZH_DEVICE, default LOCAL_RANK or 0)."""
+    global _ctx
+    with _ctx_lock:
+        if _ctx is None:
+            dev = int(os.environ.get("ZH_DEVICE", os.environ.get("LOCAL_RANK", "0")))
+            _ctx = _lib.DeviceContext(dev)
+        return _ctx
+
+
+def _host_buf(b):
+    return (C.c_char * max(1, len(b))).from_buffer_copy(bytes(b) if len(b) else b"\0")
+
+
+class Array:
+    def __init__(self, store_handle, metadata):
+        self.storeHandle = store_handle
+        self.metadata = metadata
+        self.chain = device_chain(metadata.codecs, metadata.ndim,
+                                  metadata.data_type.getByteCount())
+        self.zmeta = metadata.to_zh_meta(self.chain)
+        err = C.create_string_buffer(512)
+        st = _lib.lib().zh_validate_meta(C.byref(self.zmeta), err, 512)
+        if st != A.ZH_OK:
+            raise_for(_lib.ZhError(st, err.value.decode()))
+
+    # ---------------------------------------------------------------- open / create
+    @classmethod
+    def open(cls, store_handle):
+        raw = store_handle.resolve(ZARR_JSON).read()
+        if raw is None:
+            raise ZarrException(f"No Zarr array found at {store_handle!r}")
+        return cls(store_handle, ArrayMetadata.from_json(json.loads(raw)))
+
+    @classmethod
+    def create(cls, store_handle, metadata, exist_ok=False):
+        h = store_handle.resolve(ZARR_JSON)
+        if not exist_ok and h.exists():
+            raise ZarrException(f"Trying to create a new array in {store_handle!r}. But "
+                                f"{ZARR_JSON} already exists.")
+        h.set(metadata.dumps().encode())
+        return cls(store_handle, metadata)
+
+    # ---------------------------------------------------------------- helpers
+    @property
+    def ndim(self):
+        return self.metadata.ndim
+
+    def _chunk_coords(self, offset, shape):
+        n = self.ndim
+        L = _lib.lib()
+        args = (n, _lib.i64arr(self.metadata.shape), _lib.i32arr(self.metadata.chunk_shape),
+                _lib.i64arr(offset), _lib.i64arr(shape))
+        num = L.zh_compute_chunk_coords(*args, None, 0)
+        if num < 0:
+            raise ArithmeticError("Number of chunks exceeds Integer.MAX_VALUE")
+        out = (C.c_int64 * max(1, num * n))()
+        L.zh_compute_chunk_coords(*args, out, num)
+        return [tuple(out[i * n:(i + 1) * n]) for i in range(num)]
+
+    def _handle(self, coords):
+        return self.storeHandle.resolve(*self.metadata.chunk_key_encoding.encode_chunk_key(coords))
+
+    def _check_region(self, offset, shape):
+        n = self.ndim
+        if len(offset) != n:
+            raise ValueError(f"'offset' needs to have rank '{n}'.")
+        if len(shape) != n:
+            raise ValueError(f"'shape' needs to have rank '{n}'.")
+        for d in range(n):  # M/core/Array.java:386-390
+            if offset[d] < 0 or offset[d] + shape[d] > self.metadata.shape[d]:
+                raise ZarrException("Requested data is outside of the array's domain.")
+
+    def _n_inner(self):
+        inner = self.chain.chain["inner_chunk_shape"]
+        n = 1
+        for c, i in zip(self.metadata.chunk_shape, inner):
+            n *= c // i
+        return n
+
+    def _unwrap_inner(self, shard):
+        """Host hand-off for inner byte-to-byte codecs: verify/parse the index with the
+        index codecs, decode every inner chunk's frame on the host and rebuild a raw shard
+        (same index location/endianness) for the device."""
+        ch = self.chain.chain
+        n_in = self._n_inner()
+        crc = ch["index_crc32c"]
+        isz = 16 * n_in + (4 if crc else 0)
+        start = ch["index_location"] == A.ZH_INDEX_START
+        idx = shard[:isz] if start else shard[len(shard) - isz:]
+        body = self.chain.index_codecs[1].decode(idx) if crc else idx
+        big = ch["index_endian"] == A.ZH_ENDIAN_BIG
+        fmt = ">QQ" if big else "<QQ"
+        ents = [struct.unpack(fmt, body[16 * k:16 * k + 16]) for k in range(n_in)]
+        payload = []
+        pos = isz if start else 0
+        new = []
+        for off, nb in ents:
+            if off == 2 ** 64 - 1 or nb == 2 ** 64 - 1:
+                new.append((off, nb))
+                continue
+            raw = host_bb_decode(self.chain.inner_host_bb, shard[off:off + nb])
+            new.append((pos, len(raw)))
+            payload.append(raw)
+            pos += len(raw)
+        ib = b"".join(struct.pack(fmt, *e) for e in new)
+        if crc:
+            ib = self.chain.index_codecs[1].encode(ib)
+        pb = b"".join(payload)
+        return ib + pb if start else pb + ib
+
+    def _wrap_inner(self, shard):
+        """Inverse of _unwrap_inner for the write path."""
+        ch = self.chain.chain
+        n_in = self._n_inner()
+        crc = ch["index_crc32c"]
+        isz = 16 * n_in + (4 if crc else 0)
+        start = ch["index_location"] == A.ZH_INDEX_START
+        idx = shard[:isz] if start else shard[len(shard) - isz:]
+        body = idx[:16 * n_in]
+        fmt = ">QQ" if ch["index_endian"] == A.ZH_ENDIAN_BIG else "<QQ"
+        pos = isz if start else 0
+        payload, new = [], []
+        for k in range(n_in):
+            off, nb = struct.unpack(fmt, body[16 * k:16 * k + 16])
+            if off == 2 ** 64 - 1:
+                new.append((off, nb))
+                continue
+            enc = host_bb_encode(self.chain.inner_host_bb, shard[off:off + nb])
+            new.append((pos, len(enc)))
+            payload.append(enc)
+            pos += len(enc)
+        ib = b"".join(struct.pack(fmt, *e) for e in new)
+        if crc:
+            ib = self.chain.index_codecs[1].encode(ib)
+        pb = b"".join(payload)
+        return ib + pb if start else pb + ib
+
+    def _load_source(self, coords):
+        b = self._handle(coords).read()
+        if b is None:
+            return None
+        if self.chain.host_bb:
+            b = host_bb_decode(self.chain.host_bb, b)
+        elif self.chain.inner_host_bb:
+            b = self._unwrap_inner(b)
+        return b
+
+    # ---------------------------------------------------------------- read
+    def read(self, offset=None, shape=None, parallel=True):
+        """core.Array.read → numpy array (C order, the array's dtype)."""
+        n = self.ndim
+        offset = [0] * n if offset is None else [int(o) for o in offset]
+        shape = list(self.metadata.shape) if shape is None else [int(s) for s in shape]
+        self._check_region(offset, shape)
+        dt = self.metadata.data_type.numpy
+        if any(s == 0 for s in shape):
+            return np.zeros(shape, dtype=dt)
+        coords = self._chunk_coords(offset, shape)
+        sources = [self._load_source(c) for c in coords]
+        bufs = [(_host_buf(s) if s is not None else None) for s in sources]
+        srcs = [((C.addressof(b), len(s)) if s is not None else (None, 0))
+                for b, s in zip(bufs, sources)]
+        out = np.empty(shape, dtype=dt)
+        try:
+            device().array_read(self.zmeta, srcs, offset, shape, out.ctypes.data, 0)
+        except _lib.ZhError as e:
+            raise_for(e)
+        return out
+
+    def readChunk(self, coords):
+        """core.Array.readChunk (M/core/Array.java:167-182)."""
+        cs = self.metadata.chunk_shape
+        for d, c in enumerate(coords):
+            if c < 0 or c * cs[d] >= self.metadata.shape[d]:
+                raise ZarrException("Attempting to read data outside of the array's domain.")
+        src = self._load_source(tuple(coords))
+        out = np.empty(cs, dtype=self.metadata.data_type.numpy)
+        if src is None:
+            out.view(np.uint8).reshape(-1)[:] = np.frombuffer(
+                self.metadata.fill_bytes * int(np.prod(cs)), np.uint8)
+            return out
+        # one chunk viewed as a one-chunk array: ShardingIndexedCodec.decode / bytes decode
+        m = A.zh_array_meta.from_buffer_copy(self.zmeta)
+        for d in range(self.ndim):
+            m.shape[d] = cs[d]
+        b = _host_buf(src)
+        try:
+            device().array_read(m, [(C.addressof(b), len(src))], [0] * self.ndim, cs,
+                                out.ctypes.data, 0)
+        except _lib.ZhError as e:
+            raise_for(e)
+        return out
+
+    # ---------------------------------------------------------------- write
+    def write(self, offset, data):
+        """core.Array.write: whole-chunk regions are encoded on the device in one call;
+        partial chunks are read-modify-written (decode → patch → encode)."""
+        data = np.ascontiguousarray(data, dtype=self.metadata.data_type.numpy)
+        n = self.ndim
+        offset = [0] * n if offset is None else [int(o) for o in offset]
+        shape = list(data.shape)
+        self._check_region(offset, shape)
+        cs, ash = self.metadata.chunk_shape, self.metadata.shape
+        lo = [(o // c) * c for o, c in zip(offset, cs)]
+        hi = [min(-(-(o + s) // c) * c, a) for o, s, c, a in zip(offset, shape, cs, ash)]
+        if lo != offset or hi != [o + s for o, s in zip(offset, shape)]:
+            ext = [h - l for l, h in zip(lo, hi)]
+            region = self.read(lo, ext)
+            sl = tuple(slice(o - l, o - l + s) for o, l, s in zip(offset, lo, shape))
+            region[sl] = data
+            data, offset, shape = region, lo, ext
+        coords = self._chunk_coords(offset, shape)
+        dev = device()
+        L = _lib.lib()
+        cap = L.zh_array_encoded_bound(C.byref(self.zmeta))
+        src = dev.malloc(max(1, data.nbytes))
+        bufs = []
+        try:
+            dev.memcpy(src, data.ctypes.data, data.nbytes, 0)
+            bufs = [dev.malloc(cap) for _ in coords]
+            try:
+                sizes = dev.array_write(self.zmeta, src, offset, shape, [(b, cap) for b in bufs])
+            except _lib.ZhError as e:
+                raise_for(e)
+            for c, b, sz in zip(coords, bufs, sizes):
+                h = self._handle(c)
+                if sz == 0:
+                    h.delete()  # all fill → writeChunk deletes the key (Array.java:150-151)
+                    continue
+                enc = dev.d2h(b, sz)
+                if self.chain.host_bb:
+                    enc = host_bb_encode(self.chain.host_bb, enc)
+                elif self.chain.inner_host_bb:
+                    enc = self._wrap_inner(enc)
+                h.set(enc)
+        finally:
+            for b in bufs:
+                dev.free(b)
+            dev.free(src)
+
+    def access(self):
+        return ArrayAccessor(self)
+
+
+class ArrayAccessor:
+    """core.Array.ArrayAccessor (M/core/Array.java:483-536)."""
+
+    def __init__(self, array):
+        self.array = array
+        self.offset = None
+        self.shape = None
+
+    def withOffset(self, *offset):
+        self.offset = list(offset)
+        return self
+
+    def withShape(self, *shape):
+        self.shape = list(shape)
+        return self
+
+    def read(self):
+        return self.array.read(self.offset, self.shape)
+
+    def write(self, data):
+        self.array.write(self.offset, data)

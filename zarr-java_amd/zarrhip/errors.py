@@ -1,0 +1,26 @@
+"""dev.zarr.zarrjava.ZarrException (M/ZarrException.java:3-11) and the C-ABI status map."""
+
+
+class ZarrException(Exception):
+    """Data / format errors; message text follows the reference where one exists."""
+
+
+class UnsupportedChainError(ZarrException):
+    """The codec chain is valid but not device-supported (ZH_EUNSUPPORTED): the Java
+    integration keeps the reference codec for it."""
+
+
+def raise_for(err):
+    """Map a _lib.ZhError to the reference's exception types."""
+    from . import _abi as A
+    st = getattr(err, "status", None)
+    msg = str(err)
+    if st == A.ZH_EDATA:
+        raise ZarrException(msg) from None
+    if st == A.ZH_EUNSUPPORTED:
+        raise UnsupportedChainError(msg) from None
+    if st == A.ZH_EINVAL:
+        raise ValueError(msg) from None
+    if st == A.ZH_EARITH:
+        raise ArithmeticError(msg) from None
+    raise RuntimeError(msg) from None
