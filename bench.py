@@ -78,9 +78,9 @@ class Dist:
             self.dist.destroy_process_group()
 
 
-def build_meta(A, cfg):
+def build_meta(A, cfg, ydiv=1):
     _, sharded, order = CONFIGS[cfg]
-    return A.make_meta([1, 4096, 4096, 1536], [1, 1024, 1024, 1024], 4,
+    return A.make_meta([1, 4096 // ydiv, 4096, 1536], [1, 1024, 1024, 1024], 4,
                        endian=A.ZH_ENDIAN_BIG, sharded=sharded,
                        inner_chunk_shape=[1, 32, 32, 32] if sharded else None,
                        transpose_order=order, index_endian=A.ZH_ENDIAN_LITTLE,
@@ -123,6 +123,80 @@ def pmc_traffic(config):
         return None, None
     d = json.load(open(cands[-1]))
     return int(d["pmc"]["traffic_bytes_per_launch"]), os.path.relpath(cands[-1], ROOT)
+
+
+def host_inclusive(dev, A, meta, coords, offs, sizes, shard_slab, n_shards=4, reps=2):
+    """Host-resident bytes in, host-resident decoded array out: the readChunk /
+    ShardingIndexedCodec.decode(ByteBuffer) of `n_shards` interior shards (4 GiB each way)
+    from pinned host memory, pipelined over three streams (H2D | decode | D2H) with two
+    device slots, so PCIe traffic in both directions overlaps the decode."""
+    n = meta.ndim
+    cs = [meta.chunk_shape[d] for d in range(n)]
+    sel = [i for i, c in enumerate(coords)
+           if all((c[d] + 1) * cs[d] <= meta.shape[d] for d in range(n))][:n_shards]
+    in_sz = [sizes[i] for i in sel]
+    out_sz = 4
+    for c in cs:
+        out_sz *= c
+    hin = dev.malloc_pinned(sum(in_sz))
+    hout = dev.malloc_pinned(out_sz * len(sel))
+    pos, p = [], 0
+    for k, i in enumerate(sel):  # stage the encoded shards into pinned host memory
+        pos.append(p)
+        dev.memcpy(hin + p, shard_slab + offs[i], in_sz[k], 1, None, True)
+        p += in_sz[k]
+    smeta = A.zh_array_meta.from_buffer_copy(meta)
+    for d in range(n):
+        smeta.shape[d] = cs[d]
+    din = [dev.malloc(max(in_sz)) for _ in range(2)]
+    dout = [dev.malloc(out_sz) for _ in range(2)]
+    flags = A.ZH_SRC_DEVICE | A.ZH_OUT_DEVICE
+    plans = [dev.plan(smeta, [(din[j], in_sz[0])], [0] * n, cs, flags) for j in range(2)]
+    s_in, s_dec, s_out = dev.stream(), dev.stream(), dev.stream()
+    times = []
+    for _ in range(reps):
+        ev = [[dev.event() for _ in range(3)] for _ in sel]
+        dev.sync()
+        t0 = time.perf_counter()
+        for k in range(len(sel)):
+            j = k & 1
+            if k >= 2:
+                dev.wait_event(s_in, ev[k - 2][1])       # slot j's input consumed
+            dev.memcpy(din[j], hin + pos[k], in_sz[k], 0, s_in, False)
+            dev.record(ev[k][0], s_in)
+            dev.wait_event(s_dec, ev[k][0])
+            if k >= 2:
+                dev.wait_event(s_dec, ev[k - 2][2])      # slot j's output drained
+            plans[j].execute(dout[j], s_dec)
+            dev.record(ev[k][1], s_dec)
+            dev.wait_event(s_out, ev[k][1])
+            dev.memcpy(hout + k * out_sz, dout[j], out_sz, 1, s_out, False)
+            dev.record(ev[k][2], s_out)
+        for s in (s_in, s_dec, s_out):
+            dev.sync(s)
+        times.append(time.perf_counter() - t0)
+        for pl in plans:
+            pl.wait()
+    t = min(times)
+    res = {"value": round(len(sel) * out_sz / t / GiB, 2), "unit": "GiB/s",
+           "h2d_bytes": sum(in_sz), "d2h_bytes": out_sz * len(sel), "seconds": round(t, 4),
+           "workload": f"readChunk of {len(sel)} interior shards (4 GiB in + 4 GiB out each) "
+                       "from pinned host memory, H2D | decode | D2H pipelined on 3 streams"}
+    # a decoded shard must equal the generator's values of its region
+    chk = dev.malloc(out_sz)
+    dev.memcpy(chk, hout + (len(sel) - 1) * out_sz, out_sz, 0, None, True)
+    c = coords[sel[-1]]
+    res["verify_mismatches"] = dev.synth_verify(chk, [meta.shape[d] for d in range(n)],
+                                                [c[d] * cs[d] for d in range(n)], cs, 4, SEED)
+    for pl in plans:
+        pl.close()
+    for x in din + dout + [chk]:
+        dev.free(x)
+    dev.free_pinned(hin)
+    dev.free_pinned(hout)
+    for s in (s_in, s_dec, s_out):
+        dev.stream_destroy(s)
+    return res
 
 
 def cpu_baseline(dev, A, meta, shard_ptr, shard_nbytes, budget_s=12.0):
@@ -168,6 +242,10 @@ def main():
     ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
+    ap.add_argument("--ydiv", type=int, default=1,
+                    help="rehearsal only: divide the array's y extent (not a bench config)")
+    ap.add_argument("--host-inclusive", action="store_true",
+                    help="also measure pinned H2D + decode + D2H (adds 'host_inclusive')")
     args = ap.parse_args()
 
     ws, rank, local = dist_env()
@@ -178,9 +256,9 @@ def main():
     from zarrhip import _abi as A
     from zarrhip._lib import DeviceContext, lib
 
-    dev = DeviceContext(local)
+    dev = DeviceContext(int(os.environ.get("ZH_DEVICE", local)))
     info = dev.info()
-    meta = build_meta(A, args.config)
+    meta = build_meta(A, args.config, args.ydiv)
     n = meta.ndim
     shape = [meta.shape[d] for d in range(n)]
     L = lib()
@@ -249,14 +327,18 @@ def main():
     value = ws * args.steps * out_bytes / elapsed / GiB
     traffic_alg = st["in_bytes"] + st["out_bytes"]
     achieved = traffic_alg / (scatter_ms / 1000.0) / 1e9
-    traffic, traffic_src = pmc_traffic(args.config)
+    traffic, traffic_src = pmc_traffic(args.config) if args.ydiv == 1 else (None, None)
     roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                 "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                 "traffic_source": traffic_src,
-                "kernel": "scatter_kernel<4,false,%s>" % ("true" if meta.chain.has_transpose else
-                                                          "false"),
+                "kernel": ("decode_tiles_kernel" if meta.chain.has_transpose
+                           else "decode_rows_kernel<4,4>"),
                 "kernel_ms": round(scatter_ms, 3), "index_kernels_ms": round(index_ms, 4),
                 "alg_bytes_per_launch": traffic_alg}
+    hinc = None
+    if args.host_inclusive and meta.chain.sharded:
+        hinc = host_inclusive(dev, A, meta, coords, offs, sizes, shard_slab)
+        log(f"[rank {rank}] host-inclusive: {hinc}")
     cpu = None
     if rank == 0 and ws == 1 and not args.no_cpu_baseline and meta.chain.sharded:
         cpu = cpu_baseline(dev, A, meta, shard_slab + offs[0], sizes[0], args.cpu_budget)
@@ -266,7 +348,7 @@ def main():
         "value": round(value, 2), "unit": "GiB/s", "n_gpus": ws, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3), "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "u32", "data": "synthetic",
-        "config": {"workload": f"{args.config}: Array.read of the full 1x4096x4096x1536 uint32 "
+        "config": {"workload": f"{args.config}: Array.read of the full {'x'.join(map(str, shape))} uint32 "
                                f"array, {CONFIGS[args.config][0]}",
                    "array_shape": shape, "chunk_shape": [1, 1024, 1024, 1024],
                    "inner_chunk_shape": [1, 32, 32, 32] if meta.chain.sharded else None,
@@ -275,6 +357,8 @@ def main():
         "roofline": roofline,
         "cpu_baseline": cpu,
     }
+    if hinc is not None:
+        line["host_inclusive"] = hinc
     plan.close()
     dev.free(shard_slab)
     dev.free(out)

@@ -204,6 +204,13 @@ int zh_host_free_pinned(zh_ctx* ctx, void* ptr);
 int zh_memcpy_async(zh_ctx* ctx, void* dst, const void* src, size_t bytes, int kind, void* stream);
 int zh_memset_async(zh_ctx* ctx, void* dst, int value, size_t bytes, void* stream);
 int zh_stream_synchronize(zh_ctx* ctx, void* stream);
+int zh_stream_create(zh_ctx* ctx, void** stream);
+int zh_stream_destroy(zh_ctx* ctx, void* stream);
+/* make `stream` wait for `ev` (recorded on another stream) */
+int zh_stream_wait_event(zh_ctx* ctx, void* stream, void* ev);
+/* pitched copy of `height` rows of `width` bytes; kind as zh_memcpy_async */
+int zh_memcpy2d_async(zh_ctx* ctx, void* dst, size_t dpitch, const void* src, size_t spitch,
+                      size_t width, size_t height, int kind, void* stream);
 int zh_event_create(zh_ctx* ctx, void** ev);
 int zh_event_destroy(zh_ctx* ctx, void* ev);
 int zh_event_record(zh_ctx* ctx, void* ev, void* stream);

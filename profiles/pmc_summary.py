@@ -23,27 +23,34 @@ def kernel_rows(path, match):
 
 
 def main(src, config, out):
-    decode = lambda n: "scatter_kernel" in n and "false," in n.split("<")[1].split(",")[1] + ","
+    def decode(n):  # every decode kernel of one step: fast rows/tiles + the generic list
+        return any(k in n for k in ("decode_rows_kernel", "decode_tiles_kernel",
+                                     "decode_slow_kernel"))
+
+    def fast(n):
+        return "decode_rows_kernel" in n or "decode_tiles_kernel" in n
     fetch = kernel_rows(os.path.join(src, f"pmc_fetch_{config}", "run_counter_collection.csv"),
                         decode)
     write = kernel_rows(os.path.join(src, f"pmc_write_{config}", "run_counter_collection.csv"),
                         decode)
     stats = list(csv.DictReader(open(os.path.join(src, f"trace_{config}",
                                                   "run_kernel_stats.csv"))))
-    f_kib = [float(r["Counter_Value"]) for r in fetch]
-    w_kib = [float(r["Counter_Value"]) for r in write]
-    fetch_b = 2 * 1024 * sum(f_kib) / len(f_kib)
-    write_b = 1024 * sum(w_kib) / len(w_kib)
-    dec = [s for s in stats if "scatter_kernel<4, false" in s["Name"]][0]
+    launches = sum(1 for r in fetch if fast(r["Kernel_Name"]))
+    f_kib = sum(float(r["Counter_Value"]) for r in fetch) / launches
+    w_kib = sum(float(r["Counter_Value"]) for r in write) / launches
+    fetch_b = 2 * 1024 * f_kib
+    write_b = 1024 * w_kib
+    decs = [s for s in stats if decode(s["Name"])]
+    calls = max(int(s["Calls"]) for s in decs)
     res = {
         "config": config,
-        "kernel": dec["Name"],
-        "kernel_trace": {"calls": int(dec["Calls"]), "avg_ns": float(dec["AverageNs"]),
-                         "min_ns": float(dec["MinNs"]), "max_ns": float(dec["MaxNs"])},
-        "pmc": {"FETCH_SIZE_KiB_raw": sum(f_kib) / len(f_kib),
-                "WRITE_SIZE_KiB_raw": sum(w_kib) / len(w_kib),
+        "kernel": " + ".join(s["Name"] for s in decs),
+        "kernel_trace": {"calls": calls,
+                         "avg_ns": sum(float(s["TotalDurationNs"]) for s in decs) / calls,
+                         "per_kernel": {s["Name"]: float(s["AverageNs"]) for s in decs}},
+        "pmc": {"FETCH_SIZE_KiB_raw": f_kib, "WRITE_SIZE_KiB_raw": w_kib,
                 "fetch_bytes_corrected_x2": fetch_b, "write_bytes": write_b,
-                "traffic_bytes_per_launch": fetch_b + write_b, "launches": len(f_kib)},
+                "traffic_bytes_per_launch": fetch_b + write_b, "launches": launches},
         "all_kernels": [{"name": s["Name"], "calls": int(s["Calls"]),
                          "avg_ns": float(s["AverageNs"])} for s in stats],
     }

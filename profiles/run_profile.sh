@@ -23,5 +23,11 @@ step pmc_fetch_c3 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pm
   python3 "$R/bench.py" --steps 2 --warmup 1 --no-cpu-baseline
 step pmc_write_c3 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write_c3" -o run -- \
   python3 "$R/bench.py" --steps 2 --warmup 1 --no-cpu-baseline
-step bench_c4 300 python3 "$R/bench.py" --config c4 --steps 5 --warmup 2 --no-cpu-baseline
-step bench_c2 300 python3 "$R/bench.py" --config c2 --steps 5 --warmup 2 --no-cpu-baseline
+for cfg in c4 c2; do
+  step trace_$cfg 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace_$cfg" -o run -- \
+    python3 "$R/bench.py" --config $cfg --steps 5 --warmup 2 --no-cpu-baseline
+  step pmc_fetch_$cfg 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch_$cfg" -o run -- \
+    python3 "$R/bench.py" --config $cfg --steps 2 --warmup 1 --no-cpu-baseline
+  step pmc_write_$cfg 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write_$cfg" -o run -- \
+    python3 "$R/bench.py" --config $cfg --steps 2 --warmup 1 --no-cpu-baseline
+done

@@ -1111,6 +1111,33 @@ int zh_stream_synchronize(zh_ctx* ctx, void* stream) {
   hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
   return hipStreamSynchronize(s) == hipSuccess ? ZH_OK : ZH_EHIP;
 }
+int zh_stream_create(zh_ctx* ctx, void** stream) {
+  if (!ctx || !stream) return ZH_EINVAL;
+  (void)hipSetDevice(ctx->device);
+  return hipStreamCreateWithFlags((hipStream_t*)stream, hipStreamNonBlocking) == hipSuccess
+             ? ZH_OK
+             : ZH_EHIP;
+}
+int zh_stream_destroy(zh_ctx* ctx, void* stream) {
+  if (!ctx || !stream) return ZH_EINVAL;
+  (void)hipSetDevice(ctx->device);
+  return hipStreamDestroy((hipStream_t)stream) == hipSuccess ? ZH_OK : ZH_EHIP;
+}
+int zh_stream_wait_event(zh_ctx* ctx, void* stream, void* ev) {
+  if (!ctx || !ev) return ZH_EINVAL;
+  hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
+  return hipStreamWaitEvent(s, (hipEvent_t)ev, 0) == hipSuccess ? ZH_OK : ZH_EHIP;
+}
+int zh_memcpy2d_async(zh_ctx* ctx, void* dst, size_t dpitch, const void* src, size_t spitch,
+                      size_t width, size_t height, int kind, void* stream) {
+  if (!ctx) return ZH_EINVAL;
+  (void)hipSetDevice(ctx->device);
+  hipMemcpyKind k = kind == 0 ? hipMemcpyHostToDevice
+                              : (kind == 1 ? hipMemcpyDeviceToHost : hipMemcpyDeviceToDevice);
+  hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
+  return hipMemcpy2DAsync(dst, dpitch, src, spitch, width, height, k, s) == hipSuccess ? ZH_OK
+                                                                                      : ZH_EHIP;
+}
 int zh_event_create(zh_ctx* ctx, void** ev) {
   if (!ctx || !ev) return ZH_EINVAL;
   (void)hipSetDevice(ctx->device);

@@ -56,6 +56,10 @@ _SIGS = {
     "zh_memcpy_async": (C.c_int, [P, P, P, SZ, C.c_int, P]),
     "zh_memset_async": (C.c_int, [P, P, C.c_int, SZ, P]),
     "zh_stream_synchronize": (C.c_int, [P, P]),
+    "zh_stream_create": (C.c_int, [P, C.POINTER(P)]),
+    "zh_stream_destroy": (C.c_int, [P, P]),
+    "zh_stream_wait_event": (C.c_int, [P, P, P]),
+    "zh_memcpy2d_async": (C.c_int, [P, P, SZ, P, SZ, SZ, SZ, C.c_int, P]),
     "zh_event_create": (C.c_int, [P, C.POINTER(P)]),
     "zh_event_destroy": (C.c_int, [P, P]),
     "zh_event_record": (C.c_int, [P, P, P]),
@@ -182,6 +186,22 @@ class DeviceContext:
         check(self.L.zh_device_info(self.h, name, 256, C.byref(mem), C.byref(cus), arch, 64))
         return {"name": name.value.decode(), "arch": arch.value.decode(),
                 "total_mem": mem.value, "cu_count": cus.value}
+
+    def stream(self):
+        s = P()
+        check(self.L.zh_stream_create(self.h, C.byref(s)))
+        return s.value
+
+    def stream_destroy(self, s):
+        if s:
+            self.L.zh_stream_destroy(self.h, P(s))
+
+    def wait_event(self, stream, ev):
+        check(self.L.zh_stream_wait_event(self.h, P(stream), P(ev)))
+
+    def memcpy2d(self, dst, dpitch, src, spitch, width, height, kind, stream=None):
+        check(self.L.zh_memcpy2d_async(self.h, P(dst), int(dpitch), P(src), int(spitch),
+                                       int(width), int(height), int(kind), P(stream)))
 
     # -- events ---------------------------------------------------------------------
     def event(self):
