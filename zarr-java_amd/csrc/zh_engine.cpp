@@ -489,7 +489,7 @@ std::vector<uint32_t> setup_fast(const zh_array_meta* m, ScatterArgs& a, int til
 }
 
 int grid_for(const zh_ctx* ctx, int64_t total_items) {
-  const int per_cu = std::max(1, env_int("ZH_BLOCKS_PER_CU", 32));
+  const int per_cu = std::max(1, env_int("ZH_BLOCKS_PER_CU", 256));
   int64_t g = (int64_t)ctx->cu_count * per_cu;
   return (int)std::max<int64_t>(1, std::min<int64_t>(g, total_items));
 }
@@ -721,6 +721,9 @@ int zh_plan_create(zh_ctx* ctx, const zh_array_meta* m, const zh_chunk_src* chun
   p->args.total_items = items << p->args.piece_shift;
   p->args.status = p->d_status;
   p->grid = grid_for(ctx, p->args.total_items);
+  // non-temporal loads + stores: +4 % on the row path, +1 % on the tile path (interleaved
+  // A/B in one process, profiles/r01/experiments/tune_*.json)
+  p->args.nt = env_int("ZH_NT", 3) & 3;
   p->slow_grid = p->grid;
   *out = p;
   return ZH_OK;

@@ -109,6 +109,7 @@ struct ScatterArgs {
   uint32_t* slow_count;
   int32_t dsize;
   int32_t tile;
+  int32_t nt;                   // fast kernels: bit 0 non-temporal loads, bit 1 stores
 };
 
 struct CrcJob {
