@@ -20,6 +20,7 @@ def main():
     rounds = int(sys.argv[2]) if len(sys.argv) > 2 else 5
     grids = [int(g) for g in os.environ.get("TUNE_GRIDS", "32,64,128,192,256,384,512").split(",")]
     nts = [int(x) for x in os.environ.get("TUNE_NT", "0,3").split(",")]
+    variants = [int(x) for x in os.environ.get("TUNE_VARIANTS", "0").split(",")]
     dev = DeviceContext(0)
     meta = bench.build_meta(A, cfg)
     n = meta.ndim
@@ -47,10 +48,12 @@ def main():
     plans = {}
     for g in grids:
         for nt in nts:
-            os.environ["ZH_BLOCKS_PER_CU"] = str(g)
-            os.environ["ZH_NT"] = str(nt)
-            plans[(g, nt)] = dev.plan(meta, [(slab + o, s) for o, s in zip(offs, sizes)],
-                                      [0] * n, shape, A.ZH_SRC_DEVICE | A.ZH_OUT_DEVICE)
+            for v in variants:
+                os.environ["ZH_BLOCKS_PER_CU"] = str(g)
+                os.environ["ZH_NT"] = str(nt)
+                os.environ["ZH_TILE_VARIANT"] = str(v)
+                plans[(g, nt, v)] = dev.plan(meta, [(slab + o, s) for o, s in zip(offs, sizes)],
+                                             [0] * n, shape, A.ZH_SRC_DEVICE | A.ZH_OUT_DEVICE)
     res = {k: [] for k in plans}
     for k, p in plans.items():  # warm every variant once
         p.execute(out)
@@ -64,11 +67,16 @@ def main():
             p.wait()
             res[k].append((time.perf_counter() - t0) / 3 * 1e3)
         print(f"round {r} done", file=sys.stderr, flush=True)
-    bad = dev.synth_verify(out, shape, [0] * n, shape, 4, bench.SEED)
+    bad = {}
+    for k, p in plans.items():  # every variant must decode bit-exactly
+        dev.memset(out, 0, nel * 4)
+        p.execute(out)
+        p.wait()
+        bad[str(k)] = dev.synth_verify(out, shape, [0] * n, shape, 4, bench.SEED)
     rows = []
-    for (g, nt), v in sorted(res.items()):
+    for (g, nt, var), v in sorted(res.items()):
         med = statistics.median(v)
-        rows.append({"blocks_per_cu": g, "nt": nt, "median_ms": round(med, 3),
+        rows.append({"blocks_per_cu": g, "nt": nt, "tile_variant": var, "median_ms": round(med, 3),
                      "min_ms": round(min(v), 3), "GiB/s": round(nel * 4 / med * 1e3 / 2**30, 1)})
     print(json.dumps({"config": cfg, "rounds": rounds, "verify_mismatches": bad, "results": rows}))
 

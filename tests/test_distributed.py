@@ -1,0 +1,88 @@
+"""Multi-process (world_size 2, gloo on CPU) coverage of the N>1 paths: bench.py's
+barrier / max-over-ranks harness and zarrhip.parallel's slab partition + gather.  The
+per-rank decode here is the oracle (test infrastructure); on GPUs it is the HIP path."""
+import os
+import socket
+
+import numpy as np
+import pytest
+
+from zarrhip import parallel as P
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+@pytest.mark.parametrize("shape,world,align", [([1, 4096, 4096, 1536], 8, 32),
+                                               ([1, 4096, 4096, 1536], 2, 32),
+                                               ([100, 7], 3, 1), ([1, 1, 64, 5], 4, 16),
+                                               ([50], 4, 32)])
+def test_slab_partition_covers_region(shape, world, align):
+    off = [0] * len(shape)
+    parts = P.slab_partition(off, shape, world, align)
+    ax = P.slab_axis(shape, world)
+    assert len(parts) == world
+    pos = off[ax]
+    for o, s in parts:
+        assert o[ax] == pos
+        for d in range(len(shape)):
+            if d != ax:
+                assert o[d] == off[d] and s[d] == shape[d]
+        pos += s[ax]
+    assert pos == off[ax] + shape[ax]
+    if shape == [1, 4096, 4096, 1536] and world == 8:
+        assert [s[1] for _, s in parts] == [512] * 8  # 512-row slabs
+
+
+def _worker(rank, world, port, tmp):
+    import sys
+    for p in (os.path.join(ROOT, "zarr-java_amd"), os.path.join(ROOT, "oracle"), ROOT,
+              os.path.join(ROOT, "tests")):
+        sys.path.insert(0, p)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    import torch.distributed as dist
+    import bench
+    import oracle as O
+    from helpers import encode_oracle, rand_array
+    from zarrhip import _abi as A
+    from zarrhip import parallel as PP
+    d = bench.Dist(world)  # init_process_group("gloo") from the env, as under torchrun
+    d.barrier()
+    mx = d.max(float(rank + 1))
+    shape = [1, 24, 20, 12]
+    meta = A.make_meta(shape, [1, 8, 8, 8], 4, endian=A.ZH_ENDIAN_BIG, sharded=True,
+                       inner_chunk_shape=[1, 4, 4, 4], transpose_order=[0, 3, 2, 1])
+    arr = rand_array(shape, 4, seed=99)
+    shards = encode_oracle(meta, arr)
+    allc = O.compute_chunk_coords(shape, [1, 8, 8, 8], [0] * 4, shape)
+    pos = {c: i for i, c in enumerate(allc)}
+
+    def decode(off, shp):
+        sel = O.compute_chunk_coords(shape, [1, 8, 8, 8], off, shp)
+        raw = O.array_read(meta, [shards[pos[c]] for c in sel], off, shp)
+        return np.frombuffer(raw, np.uint32).reshape(shp)
+
+    full = PP.distributed_read(decode, [0] * 4, shape, dist, root=0, align=4)
+    if rank == 0:
+        np.save(os.path.join(tmp, "full.npy"), full)
+        np.save(os.path.join(tmp, "want.npy"), arr)
+    with open(os.path.join(tmp, f"max{rank}.txt"), "w") as f:
+        f.write(str(mx))
+    d.close()
+
+
+def test_two_rank_gloo_partition_gather_and_bench_harness(tmp_path):
+    import torch.multiprocessing as mp
+    world = 2
+    mp.spawn(_worker, args=(world, free_port(), str(tmp_path)), nprocs=world, join=True)
+    np.testing.assert_array_equal(np.load(tmp_path / "full.npy"), np.load(tmp_path / "want.npy"))
+    for r in range(world):
+        assert float(open(tmp_path / f"max{r}.txt").read()) == 2.0

@@ -738,6 +738,78 @@ __device__ __forceinline__ void fast_tiles(const ScatterArgs& a, const uint2* ta
 
 constexpr int kFastTPB = 4;
 
+// Wave-level tile path: every wave owns UPW LDS tiles and walks its own units (stride
+// = waves per block), so there is no workgroup barrier; LDS ordering within a wave is
+// program order (one in-order DS queue per wave) plus the wave fences below.
+template <int UPW, int NT>
+__device__ __forceinline__ void wave_tiles(const ScatterArgs& a, const uint2* tab,
+                                           const uint8_t* src, uint8_t* dst, uint32_t piece,
+                                           uint32_t (*tile)[32][33]) {
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int r8 = lane >> 3, g = lane & 7;
+  constexpr int kWaves = kBlock / 64;
+  const int64_t s_fd = a.pstride[a.fd], d_fs = a.rstride[a.fs];
+  const uint32_t units = (uint32_t)a.fast_n, pieces = 1u << a.piece_shift;
+  const uint32_t u0 = (uint32_t)(((uint64_t)units * piece) / pieces);
+  const uint32_t u1 = (uint32_t)(((uint64_t)units * (piece + 1)) / pieces);
+  uint32_t(*mine)[32][33] = tile + wave * UPW;
+  uint4 x[UPW][4];
+  auto load = [&](uint32_t ub) {
+#pragma unroll
+    for (int t = 0; t < UPW; t++) {
+      const uint32_t u = ub + t * kWaves;
+      if (u < u1) {
+        const uint8_t* base = src + ((size_t)tab[u].x + g * 4) * 4;
+#pragma unroll
+        for (int k = 0; k < 4; k++)
+          x[t][k] = ld16s<(NT & 1) != 0>(base + (size_t)(r8 + 8 * k) * s_fd * 4);
+      }
+    }
+  };
+  uint32_t ub = u0 + wave;
+  if (ub < u1) load(ub);
+  for (; ub < u1; ub += UPW * kWaves) {
+#pragma unroll
+    for (int t = 0; t < UPW; t++) {
+      if (ub + t * kWaves < u1) {
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+          uint32_t* row = &mine[t][r8 + 8 * k][g * 4];
+          row[0] = xform1<4>(x[t][k].x, a.swap, 0);
+          row[1] = xform1<4>(x[t][k].y, a.swap, 0);
+          row[2] = xform1<4>(x[t][k].z, a.swap, 0);
+          row[3] = xform1<4>(x[t][k].w, a.swap, 0);
+        }
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const uint32_t nb = ub + UPW * kWaves;
+    if (nb < u1) load(nb);
+#pragma unroll
+    for (int t = 0; t < UPW; t++) {
+      const uint32_t u = ub + t * kWaves;
+      if (u < u1) {
+        uint8_t* base = dst + ((size_t)tab[u].y + g * 4) * 4;
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+          const int rr = r8 + 8 * k;
+          uint4 y;
+          y.x = mine[t][g * 4 + 0][rr];
+          y.y = mine[t][g * 4 + 1][rr];
+          y.z = mine[t][g * 4 + 2][rr];
+          y.w = mine[t][g * 4 + 3][rr];
+          st16s<(NT & 2) != 0>(base + (size_t)rr * d_fs * 4, y);
+        }
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  }
+}
+
 template <int DS, bool TILE>
 __device__ __forceinline__ void generic_item(const ScatterArgs& a, Item& it,
                                              typename ElemT<DS>::T (*tile)[32][33]) {
@@ -890,7 +962,7 @@ __global__ __launch_bounds__(kBlock) void decode_rows_kernel(ScatterArgs a) {
 
 // decode, fast tile kernel: unclipped aligned uint32 copies through 32x32 LDS tiles whose
 // origins come from the LDS table
-template <int NT>
+template <int NT, int VARIANT>
 __global__ __launch_bounds__(kBlock) void decode_tiles_kernel(ScatterArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   uint2* tab = reinterpret_cast<uint2*>(smem);
@@ -908,9 +980,14 @@ __global__ __launch_bounds__(kBlock) void decode_tiles_kernel(ScatterArgs a) {
     const int64_t nxt = item + gridDim.x;
     ItemDesc Dn = D;
     if (nxt < total) Dn = ld_desc(a.desc + (nxt >> a.piece_shift));
-    if (D.kind & kDescFast)
-      fast_tiles<kFastTPB, NT>(a, tab, (const uint8_t*)(uintptr_t)D.src, a.region + D.d0 * 4,
-                           (uint32_t)item & pmask, tile);
+    if (D.kind & kDescFast) {
+      const uint8_t* src = (const uint8_t*)(uintptr_t)D.src;
+      uint8_t* dst = a.region + D.d0 * 4;
+      if constexpr (VARIANT == 0)
+        fast_tiles<kFastTPB, NT>(a, tab, src, dst, (uint32_t)item & pmask, tile);
+      else
+        wave_tiles<VARIANT, NT>(a, tab, src, dst, (uint32_t)item & pmask, tile);
+    }
     D = Dn;
   }
 }
@@ -1231,12 +1308,19 @@ static void launch_scatter_ds(const ScatterArgs& a, int tile, int enc, int grid,
     const int nt = a.nt & 3;  // streaming cache policy (per plan)
     if (a.fast_mode == kFastTileTable) {
       if (DS == 4) {
-        lds += (size_t)kFastTPB * 32 * 33 * 4;
-        switch (nt) {
-          case 0: hipLaunchKernelGGL(decode_tiles_kernel<0>, dim3(grid), dim3(kBlock), lds, s, a); break;
-          case 1: hipLaunchKernelGGL(decode_tiles_kernel<1>, dim3(grid), dim3(kBlock), lds, s, a); break;
-          case 2: hipLaunchKernelGGL(decode_tiles_kernel<2>, dim3(grid), dim3(kBlock), lds, s, a); break;
-          default: hipLaunchKernelGGL(decode_tiles_kernel<3>, dim3(grid), dim3(kBlock), lds, s, a); break;
+        const int v = a.tile_variant;
+        const int ntiles = v == 0 ? kFastTPB : (kBlock / 64) * v;
+        lds += (size_t)ntiles * 32 * 33 * 4;
+        const bool ntx = nt == 3;
+        if (v == 1) {
+          if (ntx) hipLaunchKernelGGL((decode_tiles_kernel<3, 1>), dim3(grid), dim3(kBlock), lds, s, a);
+          else hipLaunchKernelGGL((decode_tiles_kernel<0, 1>), dim3(grid), dim3(kBlock), lds, s, a);
+        } else if (v == 2) {
+          if (ntx) hipLaunchKernelGGL((decode_tiles_kernel<3, 2>), dim3(grid), dim3(kBlock), lds, s, a);
+          else hipLaunchKernelGGL((decode_tiles_kernel<0, 2>), dim3(grid), dim3(kBlock), lds, s, a);
+        } else {
+          if (ntx) hipLaunchKernelGGL((decode_tiles_kernel<3, 0>), dim3(grid), dim3(kBlock), lds, s, a);
+          else hipLaunchKernelGGL((decode_tiles_kernel<0, 0>), dim3(grid), dim3(kBlock), lds, s, a);
         }
       }
     } else if (a.fast_mode != kFastNone) {
