@@ -724,7 +724,7 @@ int zh_plan_create(zh_ctx* ctx, const zh_array_meta* m, const zh_chunk_src* chun
   // non-temporal loads + stores: +4 % on the row path, +1 % on the tile path (interleaved
   // A/B in one process, profiles/r01/experiments/tune_*.json)
   p->args.nt = env_int("ZH_NT", 3) & 3;
-  p->args.tile_variant = std::min(2, std::max(0, env_int("ZH_TILE_VARIANT", 0)));
+  p->args.tile_variant = std::min(1, std::max(0, env_int("ZH_TILE_VARIANT", 1)));
   p->slow_grid = p->grid;
   *out = p;
   return ZH_OK;

@@ -110,7 +110,7 @@ struct ScatterArgs {
   int32_t dsize;
   int32_t tile;
   int32_t nt;                   // fast kernels: bit 0 non-temporal loads, bit 1 stores
-  int32_t tile_variant;         // tile fast path: 0 block-synchronous, 1/2 wave-level (units/wave)
+  int32_t tile_variant;         // tile fast path: 0 row-per-tile loads, 1 row-interleaved groups
 };
 
 struct CrcJob {

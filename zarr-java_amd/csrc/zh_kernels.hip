@@ -738,75 +738,65 @@ __device__ __forceinline__ void fast_tiles(const ScatterArgs& a, const uint2* ta
 
 constexpr int kFastTPB = 4;
 
-// Wave-level tile path: every wave owns UPW LDS tiles and walks its own units (stride
-// = waves per block), so there is no workgroup barrier; LDS ordering within a wave is
-// program order (one in-order DS queue per wave) plus the wave fences below.
-template <int UPW, int NT>
-__device__ __forceinline__ void wave_tiles(const ScatterArgs& a, const uint2* tab,
-                                           const uint8_t* src, uint8_t* dst, uint32_t piece,
-                                           uint32_t (*tile)[32][33]) {
+// Row-interleaved tile path: a group of 8 tile units whose source rows are adjacent (the
+// table's unit order puts batch-adjacent tiles next to each other, e.g. C4's x-neighbours)
+// is moved so that one wave instruction covers the SAME row of all 8 tiles: lane (t, g)
+// reads 16 bytes of row l of tile t, i.e. 1 KiB of contiguous payload per instruction
+// (instead of 8 rows 4 KiB apart).  Tile pitch 1057 words (≡ 1 mod 32): lanes (t, g) hit
+// banks t + 4g + j on both the write and the transposed read.
+constexpr int kTG = 8;           // tiles per group
+constexpr int kTilePitch = 1057; // words per LDS tile (32 x 33 + 1)
+
+template <int NT>
+__device__ __forceinline__ void fast_tiles_rows(const ScatterArgs& a, const uint2* tab,
+                                                const uint8_t* src, uint8_t* dst,
+                                                uint32_t piece, uint32_t* lds) {
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int r8 = lane >> 3, g = lane & 7;
-  constexpr int kWaves = kBlock / 64;
+  const int t = lane >> 3, g = lane & 7;
   const int64_t s_fd = a.pstride[a.fd], d_fs = a.rstride[a.fs];
   const uint32_t units = (uint32_t)a.fast_n, pieces = 1u << a.piece_shift;
   const uint32_t u0 = (uint32_t)(((uint64_t)units * piece) / pieces);
   const uint32_t u1 = (uint32_t)(((uint64_t)units * (piece + 1)) / pieces);
-  uint32_t(*mine)[32][33] = tile + wave * UPW;
-  uint4 x[UPW][4];
+  uint32_t* mine = lds + t * kTilePitch;
+  uint4 x[8];
   auto load = [&](uint32_t ub) {
+    const uint32_t u = ub + t;
+    if (u < u1) {
+      const uint8_t* base = src + ((size_t)tab[u].x + g * 4) * 4;
 #pragma unroll
-    for (int t = 0; t < UPW; t++) {
-      const uint32_t u = ub + t * kWaves;
-      if (u < u1) {
-        const uint8_t* base = src + ((size_t)tab[u].x + g * 4) * 4;
-#pragma unroll
-        for (int k = 0; k < 4; k++)
-          x[t][k] = ld16s<(NT & 1) != 0>(base + (size_t)(r8 + 8 * k) * s_fd * 4);
-      }
+      for (int k = 0; k < 8; k++)
+        x[k] = ld16s<(NT & 1) != 0>(base + (size_t)(wave * 8 + k) * s_fd * 4);
     }
   };
-  uint32_t ub = u0 + wave;
-  if (ub < u1) load(ub);
-  for (; ub < u1; ub += UPW * kWaves) {
+  if (u0 < u1) load(u0);
+  for (uint32_t ub = u0; ub < u1; ub += kTG) {
+    const bool live = ub + t < u1;
+    if (live) {
 #pragma unroll
-    for (int t = 0; t < UPW; t++) {
-      if (ub + t * kWaves < u1) {
-#pragma unroll
-        for (int k = 0; k < 4; k++) {
-          uint32_t* row = &mine[t][r8 + 8 * k][g * 4];
-          row[0] = xform1<4>(x[t][k].x, a.swap, 0);
-          row[1] = xform1<4>(x[t][k].y, a.swap, 0);
-          row[2] = xform1<4>(x[t][k].z, a.swap, 0);
-          row[3] = xform1<4>(x[t][k].w, a.swap, 0);
-        }
+      for (int k = 0; k < 8; k++) {
+        uint32_t* row = mine + (wave * 8 + k) * 33 + g * 4;
+        row[0] = xform1<4>(x[k].x, a.swap, 0);
+        row[1] = xform1<4>(x[k].y, a.swap, 0);
+        row[2] = xform1<4>(x[k].z, a.swap, 0);
+        row[3] = xform1<4>(x[k].w, a.swap, 0);
       }
     }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    const uint32_t nb = ub + UPW * kWaves;
-    if (nb < u1) load(nb);
+    __syncthreads();
+    if (ub + kTG < u1) load(ub + kTG);
+    if (live) {
+      uint8_t* base = dst + ((size_t)tab[ub + t].y + g * 4) * 4;
 #pragma unroll
-    for (int t = 0; t < UPW; t++) {
-      const uint32_t u = ub + t * kWaves;
-      if (u < u1) {
-        uint8_t* base = dst + ((size_t)tab[u].y + g * 4) * 4;
-#pragma unroll
-        for (int k = 0; k < 4; k++) {
-          const int rr = r8 + 8 * k;
-          uint4 y;
-          y.x = mine[t][g * 4 + 0][rr];
-          y.y = mine[t][g * 4 + 1][rr];
-          y.z = mine[t][g * 4 + 2][rr];
-          y.w = mine[t][g * 4 + 3][rr];
-          st16s<(NT & 2) != 0>(base + (size_t)rr * d_fs * 4, y);
-        }
+      for (int k = 0; k < 8; k++) {
+        const int r = wave * 8 + k;
+        uint4 y;
+        y.x = mine[(g * 4 + 0) * 33 + r];
+        y.y = mine[(g * 4 + 1) * 33 + r];
+        y.z = mine[(g * 4 + 2) * 33 + r];
+        y.w = mine[(g * 4 + 3) * 33 + r];
+        st16s<(NT & 2) != 0>(base + (size_t)r * d_fs * 4, y);
       }
     }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    __syncthreads();
   }
 }
 
@@ -986,7 +976,8 @@ __global__ __launch_bounds__(kBlock) void decode_tiles_kernel(ScatterArgs a) {
       if constexpr (VARIANT == 0)
         fast_tiles<kFastTPB, NT>(a, tab, src, dst, (uint32_t)item & pmask, tile);
       else
-        wave_tiles<VARIANT, NT>(a, tab, src, dst, (uint32_t)item & pmask, tile);
+        fast_tiles_rows<NT>(a, tab, src, dst, (uint32_t)item & pmask,
+                            reinterpret_cast<uint32_t*>(tile));
     }
     D = Dn;
   }
@@ -1309,15 +1300,11 @@ static void launch_scatter_ds(const ScatterArgs& a, int tile, int enc, int grid,
     if (a.fast_mode == kFastTileTable) {
       if (DS == 4) {
         const int v = a.tile_variant;
-        const int ntiles = v == 0 ? kFastTPB : (kBlock / 64) * v;
-        lds += (size_t)ntiles * 32 * 33 * 4;
+        lds += v == 0 ? (size_t)kFastTPB * 32 * 33 * 4 : (size_t)kTG * kTilePitch * 4;
         const bool ntx = nt == 3;
         if (v == 1) {
           if (ntx) hipLaunchKernelGGL((decode_tiles_kernel<3, 1>), dim3(grid), dim3(kBlock), lds, s, a);
           else hipLaunchKernelGGL((decode_tiles_kernel<0, 1>), dim3(grid), dim3(kBlock), lds, s, a);
-        } else if (v == 2) {
-          if (ntx) hipLaunchKernelGGL((decode_tiles_kernel<3, 2>), dim3(grid), dim3(kBlock), lds, s, a);
-          else hipLaunchKernelGGL((decode_tiles_kernel<0, 2>), dim3(grid), dim3(kBlock), lds, s, a);
         } else {
           if (ntx) hipLaunchKernelGGL((decode_tiles_kernel<3, 0>), dim3(grid), dim3(kBlock), lds, s, a);
           else hipLaunchKernelGGL((decode_tiles_kernel<0, 0>), dim3(grid), dim3(kBlock), lds, s, a);
