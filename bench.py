@@ -54,8 +54,10 @@ class Dist:
     """Barrier / max over ranks.  torch.distributed (gloo on CPU tensors) only when N>1;
     torch is imported before libzarrhip so both share one HIP runtime."""
 
-    def __init__(self, ws):
+    def __init__(self, ws, need_torch=False):
         self.ws = ws
+        if need_torch or ws > 1:
+            import torch  # noqa: F401  (load torch's HIP runtime first)
         if ws > 1:
             import torch
             import torch.distributed as dist
@@ -234,6 +236,124 @@ def cpu_baseline(dev, A, meta, shard_ptr, shard_nbytes, budget_s=12.0):
                       f"chunks), {total_t:.1f} s"}
 
 
+def run_strong(args, dist, dev, A, L, meta, rank, ws, local):
+    """Strong scaling: ONE full array split into per-rank y-slabs (512 rows at
+    N=8, aligned to inner chunks); each rank holds only the shards its slab touches
+    (encoded on its own GPU), decodes its slab, and optionally gathers the assembled region
+    to rank 0 (RCCL over xGMI via torch.distributed 'nccl', or 'gloo' through the host)."""
+    import ctypes as C
+    sys.path.insert(0, os.path.join(ROOT, "zarr-java_amd"))
+    from zarrhip.parallel import slab_partition
+    from zarrhip._lib import i32arr, i64arr
+    n = meta.ndim
+    shape = [meta.shape[d] for d in range(n)]
+    cs = [meta.chunk_shape[d] for d in range(n)]
+    inner_y = meta.chain.inner_chunk_shape[1] if meta.chain.sharded else 1
+    so, ss = slab_partition([0] * n, shape, ws, align=inner_y)[rank]
+    lo = [(so[d] // cs[d]) * cs[d] for d in range(n)]
+    hi = [min(-(-(so[d] + ss[d]) // cs[d]) * cs[d], shape[d]) for d in range(n)]
+    ext = [h - l for l, h in zip(lo, hi)]
+    for d in range(2, n):
+        assert lo[d] == 0 and ext[d] == shape[d]
+
+    def coords_of(off, shp):
+        num = L.zh_compute_chunk_coords(n, i64arr(shape), i32arr(cs), i64arr(off), i64arr(shp),
+                                        None, 0)
+        buf = (C.c_int64 * (num * n))()
+        L.zh_compute_chunk_coords(n, i64arr(shape), i32arr(cs), i64arr(off), i64arr(shp), buf, num)
+        return [tuple(buf[i * n + d] for d in range(n)) for i in range(num)]
+    cover = coords_of(lo, ext)
+    caps = chunk_capacities(meta, cover)
+    nel_cover = 1
+    for e in ext:
+        nel_cover *= e
+    first = lo[1] * shape[2] * shape[3] if n == 4 else 0
+    src = dev.malloc(nel_cover * 4)
+    dev.synth_fill(src, nel_cover, 4, first, SEED)
+    offs, tot = [], 0
+    for c in caps:
+        offs.append(tot)
+        tot += (c + 255) // 256 * 256
+    slab_buf = dev.malloc(tot)
+    sizes = dev.array_write(meta, src, lo, ext, [(slab_buf + o, c) for o, c in zip(offs, caps)])
+    dev.free(src)
+    where = {c: (slab_buf + o, s) for c, o, s in zip(cover, offs, sizes)}
+    mine = coords_of(so, ss)
+    nel = 1
+    for s in ss:
+        nel *= s
+    out_bytes = nel * 4
+    backend = args.gather_backend if ws > 1 else None
+    if backend == "nccl":
+        import torch
+        out_t = torch.empty(out_bytes, dtype=torch.uint8, device=f"cuda:{local}")
+        out = out_t.data_ptr()
+    else:
+        out = dev.malloc(out_bytes)
+    plan = dev.plan(meta, [where[c] for c in mine], so, ss, A.ZH_SRC_DEVICE | A.ZH_OUT_DEVICE)
+    for _ in range(max(1, args.warmup)):
+        plan.execute(out)
+    plan.wait()
+    bad = dev.synth_verify(out, shape, so, ss, 4, SEED)
+    if bad:
+        raise SystemExit(f"[rank {rank}] slab verification FAILED: {bad} mismatches")
+    plan.set_timing(True)
+    dist.barrier()
+    dev.sync()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        plan.execute(out)
+    plan.wait()
+    t_dec = dist.max(time.perf_counter() - t0)
+    kt = plan.kernel_time()
+    gather = None
+    if backend is not None:
+        import torch
+        import torch.distributed as tdist
+        grp = tdist.new_group(backend=backend)
+        if backend == "nccl":
+            send = out_t
+            recv = [torch.empty_like(out_t) for _ in range(ws)] if rank == 0 else None
+        else:
+            host = (C.c_char * out_bytes)()
+            dev.memcpy(C.addressof(host), out, out_bytes, 1, None, True)
+            send = torch.frombuffer(host, dtype=torch.uint8)
+            recv = [torch.empty(out_bytes, dtype=torch.uint8) for _ in range(ws)] if rank == 0 \
+                else None
+        dist.barrier()
+        t1 = time.perf_counter()
+        tdist.gather(send, recv, dst=0, group=grp)
+        if backend == "nccl":
+            torch.cuda.synchronize(local)
+        t_g = dist.max(time.perf_counter() - t1)
+        if rank == 0 and backend == "nccl":  # every gathered slab must be the generator's
+            tot_bad = 0
+            parts = slab_partition([0] * n, shape, ws, align=inner_y)
+            for r in range(ws):
+                tot_bad += dev.synth_verify(recv[r].data_ptr(), shape, parts[r][0], parts[r][1],
+                                            4, SEED)
+            if tot_bad:
+                raise SystemExit(f"gathered region verification FAILED: {tot_bad}")
+        full = 1
+        for s in shape:
+            full *= s
+        gather = {"backend": backend, "gather_ms": round(t_g * 1e3, 3),
+                  "value_incl_one_decode": round(full * 4 / (t_dec / args.steps + t_g) / GiB, 2),
+                  "unit": "GiB/s"}
+    full = 1
+    for s in shape:
+        full *= s
+    res = {"mode": "strong", "slab_offset": so, "slab_shape": ss,
+           "decode_ms_per_step": round(t_dec * 1e3 / args.steps, 3),
+           "value": round(full * 4 * args.steps / t_dec / GiB, 2),
+           "scatter_ms": round(kt["scatter_ms"] / max(1, kt["launches"]), 3), "gather": gather}
+    plan.close()
+    if backend != "nccl":
+        dev.free(out)
+    dev.free(slab_buf)
+    return res
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -242,6 +362,10 @@ def main():
     ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
+    ap.add_argument("--mode", default="weak", choices=["weak", "strong"],
+                    help="weak: one full array per GPU (the metric); strong: one array split "
+                         "into per-GPU slabs, plus a gather to rank 0")
+    ap.add_argument("--gather-backend", default="nccl", choices=["nccl", "gloo", "none"])
     ap.add_argument("--ydiv", type=int, default=1,
                     help="rehearsal only: divide the array's y extent (not a bench config)")
     ap.add_argument("--host-inclusive", action="store_true",
@@ -251,7 +375,7 @@ def main():
     ws, rank, local = dist_env()
     if args.gpus != ws and ws > 1:
         log(f"warning: --gpus {args.gpus} but WORLD_SIZE {ws}")
-    dist = Dist(ws)
+    dist = Dist(ws, need_torch=args.mode == "strong")
 
     from zarrhip import _abi as A
     from zarrhip._lib import DeviceContext, lib
@@ -259,6 +383,27 @@ def main():
     dev = DeviceContext(int(os.environ.get("ZH_DEVICE", local)))
     info = dev.info()
     meta = build_meta(A, args.config, args.ydiv)
+    if args.mode == "strong":
+        if args.gather_backend == "none":
+            args.gather_backend = None
+        res = run_strong(args, dist, dev, A, lib(), meta, rank, ws, local)
+        log(f"[rank {rank}] strong: {res}")
+        if rank == 0:
+            n = meta.ndim
+            print(json.dumps({
+                "metric": "GiB/s device-resident chunk decode (sharding+bytes+transpose), "
+                          "uint32 1024³ — strong scaling (one array split over GPUs)",
+                "value": res["value"], "unit": "GiB/s", "n_gpus": ws, "steps": args.steps,
+                "warmup": args.warmup, "ms_per_step": res["decode_ms_per_step"],
+                "higher_is_better": True, "scaling": "strong", "vs_baseline": None,
+                "dtype": "u32", "data": "synthetic",
+                "config": {"workload": f"{args.config}: Array.read of "
+                                       f"{'x'.join(str(meta.shape[d]) for d in range(n))} "
+                                       f"uint32 split into {ws} y-slabs",
+                           "parallelism": f"slab-parallel x{ws}"},
+                "strong": res}), flush=True)
+        dist.close()
+        return
     n = meta.ndim
     shape = [meta.shape[d] for d in range(n)]
     L = lib()
