@@ -174,3 +174,42 @@ def test_array_read_matches_oracle_with_missing_shards(tmp_path):
             for c in O.compute_chunk_coords([12, 12], [6, 6], [0, 0], [12, 12])]
     want = np.frombuffer(O.array_read(a.zmeta, srcs, [0, 0], [12, 12]), np.uint32).reshape(12, 12)
     np.testing.assert_array_equal(got, want)
+
+
+@pytest.mark.parametrize("loc", ["start", "end"])
+@pytest.mark.parametrize("inner_bb", [False, True])
+def test_partial_shard_staging_reads_only_referenced_chunks(tmp_path, loc, inner_bb):
+    """Sub-shard reads fetch the index + referenced inner chunks only (the reference's
+    StoreHandleDataProvider path, ShardingIndexedCodec.java:333-357), with identical
+    results."""
+    shape = [64, 64, 32]
+    fn = (lambda c1: c1.withBytes("BIG").withGzip()) if inner_bb else (lambda c1: c1.withBytes("BIG"))
+    m = (z.ArrayMetadataBuilder().withShape(*shape).withDataType(z.DataType.UINT32)
+         .withChunkShape(64, 64, 32).withFillValue(0)
+         .withCodecs(lambda c: c.withSharding([8, 8, 8], fn, loc)).build())
+    a = z.Array.create(z.FilesystemStore(tmp_path).resolve("s"), m)
+    data = np.arange(np.prod(shape), dtype=np.uint32).reshape(shape)
+    a.write(None, data)
+    b = z.Array.open(z.FilesystemStore(tmp_path).resolve("s"))
+    got = b.read([5, 9, 3], [10, 12, 6])
+    np.testing.assert_array_equal(got, data[5:15, 9:21, 3:9])
+    shard_bytes = os.path.getsize(os.path.join(tmp_path, "s", "c", "0", "0", "0"))
+    assert b.staged_bytes < shard_bytes / 4
+    b.staged_bytes = 0
+    np.testing.assert_array_equal(b.read(), data)
+    assert b.staged_bytes == shard_bytes
+
+
+def test_partial_staging_crc_error_message(tmp_path):
+    m = (z.ArrayMetadataBuilder().withShape(16, 16).withDataType(z.DataType.UINT32)
+         .withChunkShape(16, 16).withCodecs(lambda c: c.withSharding([4, 4])).build())
+    a = z.Array.create(z.FilesystemStore(tmp_path).resolve("k"), m)
+    a.write(None, np.arange(256, dtype=np.uint32).reshape(16, 16))
+    p = os.path.join(tmp_path, "k", "c", "0", "0")
+    raw = bytearray(open(p, "rb").read())
+    raw[-8] ^= 0x10
+    open(p, "wb").write(bytes(raw))
+    with pytest.raises(z.ZarrException, match="The checksum of the sharding index is invalid"):
+        a.read([1, 1], [3, 3])       # partial path: host CRC check
+    with pytest.raises(z.ZarrException, match="The checksum of the sharding index is invalid"):
+        a.read()                     # full-shard path: device CRC check

@@ -46,6 +46,7 @@ class Array:
     def __init__(self, store_handle, metadata):
         self.storeHandle = store_handle
         self.metadata = metadata
+        self.staged_bytes = 0  # encoded bytes read from the store and handed to the device
         self.chain = device_chain(metadata.codecs, metadata.ndim,
                                   metadata.data_type.getByteCount())
         self.zmeta = metadata.to_zh_meta(self.chain)
@@ -166,10 +167,82 @@ class Array:
         pb = b"".join(payload)
         return ib + pb if start else pb + ib
 
-    def _load_source(self, coords):
-        b = self._handle(coords).read()
+    def _stage_partial(self, h, part_lo, part_hi):
+        """StoreHandleDataProvider semantics (ShardingIndexedCodec.java:333-357): read the
+        index with one range read, verify its crc32c on the host (same message as the
+        device), then read only the inner chunks the part references (adjacent ranges
+        coalesced) and rebuild a compact raw shard for the device: referenced chunks only,
+        their host byte-to-byte codecs already undone, a fresh index (+crc)."""
+        ch = self.chain.chain
+        inner = ch["inner_chunk_shape"]
+        n_in = self._n_inner()
+        crc = ch["index_crc32c"]
+        isz = 16 * n_in + (4 if crc else 0)
+        start = ch["index_location"] == A.ZH_INDEX_START
+        idx = h.read(0, isz) if start else h.read(-isz)
+        if idx is None:
+            return None
+        if len(idx) < isz:
+            raise ZarrException(f"Shard {h!r} is smaller than its index ({isz} bytes).")
+        body = self.chain.index_codecs[1].decode(idx) if crc else idx
+        fmt = ">QQ" if ch["index_endian"] == A.ZH_ENDIAN_BIG else "<QQ"
+        cps = [c // i for c, i in zip(self.metadata.chunk_shape, inner)]
+        b0 = [lo // i for lo, i in zip(part_lo, inner)]
+        b1 = [(hi - 1) // i for hi, i in zip(part_hi, inner)]
+        refs = []
+        for ic in np.ndindex(*[e - s + 1 for s, e in zip(b0, b1)]):
+            lin = 0
+            for d, c in enumerate(ic):
+                lin = lin * cps[d] + b0[d] + c
+            off, nb = struct.unpack(fmt, body[16 * lin:16 * lin + 16])
+            if off == 2 ** 64 - 1 or nb == 2 ** 64 - 1:
+                continue
+            refs.append((off, nb, lin))
+        refs.sort()
+        data = {}
+        i = 0
+        while i < len(refs):  # coalesce adjacent ranges into one store read
+            j = i
+            while j + 1 < len(refs) and refs[j + 1][0] == refs[j][0] + refs[j][1]:
+                j += 1
+            s0, s1 = refs[i][0], refs[j][0] + refs[j][1]
+            blob = h.read(s0, s1)
+            if blob is None or len(blob) < s1 - s0:
+                raise ZarrException(f"Could not load byte data for chunk range [{s0}, {s1})")
+            for off, nb, lin in refs[i:j + 1]:
+                raw = blob[off - s0:off - s0 + nb]
+                if self.chain.inner_host_bb:
+                    raw = host_bb_decode(self.chain.inner_host_bb, raw)
+                data[lin] = raw
+            self.staged_bytes += s1 - s0
+            i = j + 1
+        self.staged_bytes += isz
+        ents = [(2 ** 64 - 1, 2 ** 64 - 1)] * n_in
+        payload, pos = [], isz if start else 0
+        for lin in sorted(data):
+            ents[lin] = (pos, len(data[lin]))
+            payload.append(data[lin])
+            pos += len(data[lin])
+        ib = b"".join(struct.pack(fmt, *e) for e in ents)
+        if crc:
+            ib = self.chain.index_codecs[1].encode(ib)
+        pb = b"".join(payload)
+        return ib + pb if start else pb + ib
+
+    def _load_source(self, coords, part_lo=None, part_hi=None):
+        h = self._handle(coords)
+        ch = self.chain.chain
+        if ch["sharded"] and part_lo is not None:
+            full = all(lo == 0 and hi == c for lo, hi, c in
+                       zip(part_lo, part_hi, self.metadata.chunk_shape))
+            if not full:  # sub-shard part: stage only what it references
+                if not h.exists():
+                    return None
+                return self._stage_partial(h, part_lo, part_hi)
+        b = h.read()
         if b is None:
             return None
+        self.staged_bytes += len(b)
         if self.chain.host_bb:
             b = host_bb_decode(self.chain.host_bb, b)
         elif self.chain.inner_host_bb:
@@ -187,7 +260,12 @@ class Array:
         if any(s == 0 for s in shape):
             return np.zeros(shape, dtype=dt)
         coords = self._chunk_coords(offset, shape)
-        sources = [self._load_source(c) for c in coords]
+        sources = []
+        for c in coords:
+            lo = [max(o, ci * cs) - ci * cs for o, ci, cs in zip(offset, c, self.metadata.chunk_shape)]
+            hi = [min(o + s, (ci + 1) * cs) - ci * cs
+                  for o, s, ci, cs in zip(offset, shape, c, self.metadata.chunk_shape)]
+            sources.append(self._load_source(c, lo, hi))
         bufs = [(_host_buf(s) if s is not None else None) for s in sources]
         srcs = [((C.addressof(b), len(s)) if s is not None else (None, 0))
                 for b, s in zip(bufs, sources)]
