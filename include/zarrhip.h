@@ -76,6 +76,15 @@ typedef struct zh_codec_chain {
   int32_t index_endian;                     /* index_codecs bytes endian                       */
   int32_t index_has_crc32c;                 /* index_codecs contains crc32c                    */
   int32_t index_location;                   /* ZH_INDEX_END (default) / ZH_INDEX_START          */
+  /* Nested sharding (ZarrPythonTests.java:177-179, ZarrV3Test.java:197-200): the sharding
+   * codec's inner codecs are [sharding_indexed{nested_chunk_shape, codecs [transpose?,
+   * bytes], index_codecs [bytes(nested_index_endian), crc32c?], nested_index_location}].
+   * Each inner chunk is then itself a shard; transpose/endian above apply to its leaves. */
+  int32_t nested;
+  int32_t nested_chunk_shape[ZH_MAX_DIMS];
+  int32_t nested_index_endian;
+  int32_t nested_index_has_crc32c;
+  int32_t nested_index_location;
 } zh_codec_chain;
 
 /* CoreArrayMetadata (M/core/ArrayMetadata.java:154-187) + the codec chain. */
@@ -197,6 +206,13 @@ int zh_array_write(zh_ctx* ctx, const zh_array_meta* meta, const void* src,
 
 /* ---- device memory / stream / event plumbing for callers without their own ---------- */
 int zh_device_malloc(zh_ctx* ctx, size_t bytes, void** out);
+/* Allocation flags for zh_device_malloc_ex.  ZH_MALLOC_CONTIGUOUS asks for physically
+ * contiguous HBM (hipDeviceMallocContiguous): the scattered row/tile writes of the decode
+ * kernels are sensitive to the allocation's physical fragmentation (TLB reach), while plain
+ * copies are not (DESIGN.md "Placement").  Falls back to hipMalloc unless ZH_MALLOC_REQUIRE. */
+#define ZH_MALLOC_CONTIGUOUS 0x1u
+#define ZH_MALLOC_REQUIRE 0x2u
+int zh_device_malloc_ex(zh_ctx* ctx, size_t bytes, unsigned flags, void** out);
 int zh_device_free(zh_ctx* ctx, void* ptr);
 int zh_host_malloc_pinned(zh_ctx* ctx, size_t bytes, void** out);
 int zh_host_free_pinned(zh_ctx* ctx, void* ptr);

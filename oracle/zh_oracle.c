@@ -250,7 +250,7 @@ static int inner_decode(const zh_array_meta* m, const int32_t* chunk_shape, cons
   enc.data = b;
   enc.ndim = n;
   enc.dsize = ds;
-  int32_t order[ZH_MAX_DIMS], inv[ZH_MAX_DIMS];
+  int32_t order[ZH_MAX_DIMS] = {0}, inv[ZH_MAX_DIMS] = {0};
   for (int d = 0; d < n; d++) order[d] = ch->has_transpose ? ch->transpose_order[d] : d;
   if (ch->has_transpose) {
     if (!zo_is_permutation(n, order)) {                       /* :36-38 */
@@ -281,6 +281,28 @@ static int64_t shard_index_size(const zh_array_meta* m) {
   for (int d = 0; d < m->ndim; d++) n *= m->chunk_shape[d] / m->chain.inner_chunk_shape[d];
   return 16 * n + (m->chain.index_has_crc32c ? 4 : 0);
 }
+
+/* Nested sharding: the inner codec pipeline of the outer ShardingIndexedCodec is itself
+ * [sharding_indexed{...}] (ZarrPythonTests.java:177-179).  Its CoreArrayMetadata is the
+ * outer codec's inner-chunk metadata (ShardingIndexedCodec.java:44-55 builds codecPipeline
+ * with chunkShape = inner chunk shape), so the level-2 codec sees a "shard" whose shape is
+ * the level-1 inner chunk. */
+static void nested_meta(const zh_array_meta* m, zh_array_meta* m2) {
+  *m2 = *m;
+  for (int d = 0; d < m->ndim; d++) {
+    m2->chunk_shape[d] = m->chain.inner_chunk_shape[d];
+    m2->shape[d] = m->chain.inner_chunk_shape[d];
+    m2->chain.inner_chunk_shape[d] = m->chain.nested_chunk_shape[d];
+  }
+  m2->chain.index_endian = m->chain.nested_index_endian;
+  m2->chain.index_has_crc32c = m->chain.nested_index_has_crc32c;
+  m2->chain.index_location = m->chain.nested_index_location;
+  m2->chain.nested = 0;
+}
+
+static int sharding_decode_internal(const zh_array_meta* m, const uint8_t* shard, int64_t nbytes,
+                                    const int64_t* offset, const int32_t* shape, uint8_t* out,
+                                    int nthreads, char* err, size_t errlen);
 
 static uint64_t load_u64(const uint8_t* p, int big) {
   uint64_t v = 0;
@@ -343,8 +365,28 @@ static int decode_one_inner(inner_job_t* J, int64_t k, char* err, size_t errlen)
   }
   uint8_t* buf = NULL;
   nd_t arr;
-  int st = inner_decode(m, inner, J->shard + off, len, &buf, &arr, err, errlen); /* :231 */
-  if (st != ZH_OK) return st;
+  int st;
+  if (m->chain.nested) {  /* codecPipeline.decode → the level-2 ShardingIndexedCodec.decode
+                           * (:97-103): decodeInternal over the whole sub-shard buffer */
+    zh_array_meta m2;
+    nested_meta(m, &m2);
+    int64_t nel1 = 1, zoff[ZH_MAX_DIMS] = {0};
+    for (int d = 0; d < n; d++) nel1 *= inner[d];
+    buf = (uint8_t*)malloc(nel1 * m->dtype_size > 0 ? nel1 * m->dtype_size : 1);
+    st = sharding_decode_internal(&m2, J->shard + off, len, zoff, inner, buf, 1, err, errlen);
+    if (st != ZH_OK) {
+      free(buf);
+      return st;
+    }
+    arr.data = buf;
+    arr.ndim = n;
+    arr.dsize = m->dtype_size;
+    for (int d = 0; d < n; d++) arr.shape[d] = inner[d];
+    nd_c_order(&arr);
+  } else {
+    st = inner_decode(m, inner, J->shard + off, len, &buf, &arr, err, errlen); /* :231 */
+    if (st != ZH_OK) return st;
+  }
   int64_t so[ZH_MAX_DIMS], dof[ZH_MAX_DIMS], sh[ZH_MAX_DIMS];
   for (int d = 0; d < n; d++) {
     so[d] = co[d];
@@ -582,7 +624,7 @@ static int sharding_encode(const zh_array_meta* m, const nd_t* chunk, uint8_t** 
                            int64_t* out_n) {
   int n = m->ndim, ds = m->dtype_size;
   const int32_t* inner = m->chain.inner_chunk_shape;
-  int64_t cps[ZH_MAX_DIMS], shard_shape[ZH_MAX_DIMS], zero[ZH_MAX_DIMS] = {0};
+  int64_t cps[ZH_MAX_DIMS] = {0}, shard_shape[ZH_MAX_DIMS] = {0}, zero[ZH_MAX_DIMS] = {0};
   int64_t ninner = 1, inner_nel = 1;
   for (int d = 0; d < n; d++) {
     cps[d] = m->chunk_shape[d] / inner[d];
@@ -594,6 +636,8 @@ static int sharding_encode(const zh_array_meta* m, const nd_t* chunk, uint8_t** 
   int64_t* coords = (int64_t*)malloc(sizeof(int64_t) * n * ninner);
   zo_compute_chunk_coords(n, shard_shape, inner, zero, shard_shape, coords, ninner);
   int64_t* offs = (int64_t*)malloc(sizeof(int64_t) * ninner);
+  int64_t* lens = (int64_t*)malloc(sizeof(int64_t) * ninner);
+  uint8_t** subs = (uint8_t**)calloc((size_t)ninner, sizeof(uint8_t*)); /* nested payloads */
   int64_t payload = 0;
   for (int64_t k = 0; k < ninner; k++) {                              /* :116-152 */
     int64_t o[ZH_MAX_DIMS], sh[ZH_MAX_DIMS];
@@ -603,9 +647,23 @@ static int sharding_encode(const zh_array_meta* m, const nd_t* chunk, uint8_t** 
     }
     if (all_equal(chunk, o, sh, m->fill_value)) {                    /* :129-133 */
       offs[k] = -1;
+      lens[k] = 0;
     } else {
       offs[k] = payload;                                              /* :137-143 */
-      payload += inner_nel * ds;
+      lens[k] = inner_nel * ds;
+      if (m->chain.nested) {  /* codecPipeline.encode(chunkArray) = level-2 sharding encode */
+        zh_array_meta m2;
+        nested_meta(m, &m2);
+        nd_t view = *chunk;
+        int64_t eo = 0;
+        for (int d = 0; d < n; d++) {
+          eo += o[d] * chunk->stride[d];
+          view.shape[d] = inner[d];
+        }
+        view.data = chunk->data + eo * ds;
+        sharding_encode(&m2, &view, &subs[k], &lens[k]);
+      }
+      payload += lens[k];
     }
   }
   int64_t total = payload + isz;                                      /* :153-156 */
@@ -621,9 +679,14 @@ static int sharding_encode(const zh_array_meta* m, const nd_t* chunk, uint8_t** 
       store_u64(idx + 16 * k, (uint64_t)-1, big);
       store_u64(idx + 16 * k + 8, (uint64_t)-1, big);
     } else {
-      inner_encode(m, chunk, o, inner, pay + offs[k]);
+      if (subs[k]) {
+        memcpy(pay + offs[k], subs[k], (size_t)lens[k]);
+        free(subs[k]);
+      } else {
+        inner_encode(m, chunk, o, inner, pay + offs[k]);
+      }
       store_u64(idx + 16 * k, (uint64_t)(offs[k] + (start ? isz : 0)), big); /* :140-143 */
-      store_u64(idx + 16 * k + 8, (uint64_t)(inner_nel * ds), big);
+      store_u64(idx + 16 * k + 8, (uint64_t)lens[k], big);
     }
   }
   if (m->chain.index_has_crc32c) {                                    /* Crc32cCodec.encode :50-60 */
@@ -632,6 +695,8 @@ static int sharding_encode(const zh_array_meta* m, const nd_t* chunk, uint8_t** 
   }
   free(coords);
   free(offs);
+  free(lens);
+  free(subs);
   *out = buf;
   *out_n = total;
   return ZH_OK;

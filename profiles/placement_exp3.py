@@ -18,7 +18,8 @@ cfg = sys.argv[1] if len(sys.argv) > 1 else "c4"
 dev = DeviceContext(0)
 GB = 26 << 30
 NB = 7
-bufs = [dev.malloc(GB) for _ in range(NB)]
+FLAGS = int(sys.argv[2], 0) if len(sys.argv) > 2 else 0  # A.ZH_MALLOC_* (3 = contiguous, required)
+bufs = [dev.malloc(GB, FLAGS) for _ in range(NB)]
 e0, e1 = dev.event(), dev.event()
 
 
@@ -84,5 +85,5 @@ print(json.dumps({
     "decode_GiBps": {k: gib(v) for k, v in res.items()},
     "memset_GBps": {k: round(nb / statistics.median(v) / 1e6, 1) for k, v in ms.items()},
     "copy_GBps": {k: round(2 * nb / statistics.median(v) / 1e6, 1) for k, v in cp.items()},
-    "addresses": [hex(b) for b in bufs],
+    "addresses": [hex(b) for b in bufs], "malloc_flags": FLAGS,
 }))

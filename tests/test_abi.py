@@ -29,7 +29,7 @@ def test_header_symbols_exported():
 
 
 def test_struct_layout():
-    assert C.sizeof(A.zh_codec_chain) == 4 * (1 + 8 + 1 + 8 + 4)
+    assert C.sizeof(A.zh_codec_chain) == 4 * (1 + 8 + 1 + 8 + 4 + 1 + 8 + 3)
     assert C.sizeof(A.zh_array_meta) == 16 + 64 + 32 + 8 + C.sizeof(A.zh_codec_chain)
     assert C.sizeof(A.zh_chunk_src) == 16 and C.sizeof(A.zh_chunk_dst) == 24
 

@@ -213,3 +213,26 @@ def test_partial_staging_crc_error_message(tmp_path):
         a.read([1, 1], [3, 3])       # partial path: host CRC check
     with pytest.raises(z.ZarrException, match="The checksum of the sharding index is invalid"):
         a.read()                     # full-shard path: device CRC check
+
+
+@pytest.mark.parametrize("dt", [z.DataType.INT32, z.DataType.UINT8, z.DataType.FLOAT64])
+def test_sharding_nested_python_config(tmp_path, dt):
+    """ZarrPythonTests "sharding_nested" (ZarrPythonTests.java:146-151,177-179): 16^3,
+    chunk [2,4,8], sharding [2,2,4] → sharding [2,1,2] → bytes(little); write + read back,
+    plus sub-shard reads (partial staging of a nested shard)."""
+    m = (z.ArrayMetadataBuilder().withShape(16, 16, 16).withDataType(dt).withChunkShape(2, 4, 8)
+         .withFillValue(0).withCodecs(lambda c: c.withSharding(
+             [2, 2, 4], lambda c1: c1.withSharding([2, 1, 2], lambda c2: c2.withBytes("LITTLE"))))
+         .build())
+    a = z.Array.create(z.FilesystemStore(tmp_path).resolve("n"), m)
+    data = make_testdata(dt)
+    a.write(None, data)
+    b = z.Array.open(z.FilesystemStore(tmp_path).resolve("n"))
+    np.testing.assert_array_equal(b.read(), data)
+    np.testing.assert_array_equal(b.read([1, 3, 5], [9, 7, 6]), data[1:10, 3:10, 5:11])
+    # the stored shard bytes equal the oracle's encoding of the same chunk
+    coords = (0, 1, 1)
+    raw = open(os.path.join(tmp_path, "n", "c", *map(str, coords)), "rb").read()
+    want = O.array_write(b.zmeta, data.tobytes(), [0, 0, 0], [16, 16, 16])
+    idx = O.compute_chunk_coords([16, 16, 16], [2, 4, 8], [0, 0, 0], [16, 16, 16]).index(coords)
+    assert raw == want[idx]

@@ -121,8 +121,13 @@ def test_registry_add_type_replaces():
 
 
 def test_unsupported_chains_are_flagged():
-    m = meta_with(lambda c: c.withSharding([1, 1], lambda c1: c1.withSharding([1, 1])))
-    with pytest.raises(z.UnsupportedChainError):
+    m = meta_with(lambda c: c.withSharding([4, 4], lambda c1: c1.withSharding(
+        [2, 2], lambda c2: c2.withSharding([1, 1]))), shape=(8, 8), chunk=(8, 8))
+    with pytest.raises(z.UnsupportedChainError):  # three sharding levels
+        z.device_chain(m.codecs, 2, 4)
+    m = meta_with(lambda c: c.withSharding([4, 4], lambda c1: c1.withSharding(
+        [2, 2], lambda c2: c2.withBytes("LITTLE").withGzip())), shape=(8, 8), chunk=(8, 8))
+    with pytest.raises(z.UnsupportedChainError):  # nested + leaf byte-to-byte codecs
         z.device_chain(m.codecs, 2, 4)
     m = meta_with(lambda c: c.withTranspose([1, 0]).withSharding([1, 1]))
     with pytest.raises(z.ZarrException):
@@ -181,3 +186,19 @@ def test_partial_staging_compacts_shard(loc, gz):
     off, shp = lo, [h - l for l, h in zip(lo, hi)]
     got = np.frombuffer(O.array_read(a.zmeta, [compact], off, shp), np.uint32).reshape(shp)
     np.testing.assert_array_equal(got, data[3:13, 5:11, 2:9])
+
+
+def test_nested_sharding_chain_mapping():
+    """ZarrPythonTests 'sharding_nested' (ZarrPythonTests.java:177-179): outer [2,2,4], level-2
+    [2,1,2] over bytes(little); both index chains [bytes(little), crc32c] at the end."""
+    from zarrhip import _abi as A
+    m = (z.ArrayMetadataBuilder().withShape(16, 16, 16).withDataType(z.DataType.INT32)
+         .withChunkShape(8, 8, 8).withCodecs(lambda c: c.withSharding(
+             [2, 2, 4], lambda c1: c1.withSharding([2, 1, 2], lambda c2: c2.withBytes("LITTLE"))))
+         .build())
+    ch = z.device_chain(m.codecs, 3, 4).chain
+    assert ch["inner_chunk_shape"] == [2, 2, 4] and ch["nested_chunk_shape"] == [2, 1, 2]
+    zm = m.to_zh_meta(z.device_chain(m.codecs, 3, 4))
+    assert zm.chain.nested == 1 and list(zm.chain.nested_chunk_shape)[:3] == [2, 1, 2]
+    assert zm.chain.nested_index_has_crc32c == 1
+    assert zm.chain.nested_index_location == A.ZH_INDEX_END

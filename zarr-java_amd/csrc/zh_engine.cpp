@@ -189,6 +189,9 @@ struct zh_plan {
   ItemDesc* d_desc = nullptr;   // per inner-chunk descriptors (resolve kernel)
   uint32_t* d_slow = nullptr;   // [count, list...] of items for the generic kernel
   uint32_t* d_fast_tab = nullptr;
+  uint8_t* d_flat = nullptr;    // nested sharding: flattened leaf indexes
+  NestArgs nest{};
+  int nest_grid = 0;
   int tile_mode = 0;
   int grid = 0;
   int slow_grid = 0;
@@ -318,6 +321,23 @@ int zh_validate_meta(const zh_array_meta* m, char* err, size_t errlen) {
       set_err(err, errlen, "Only index_location \"start\" or \"end\" are supported.");
       return ZH_EDATA;  // ShardingIndexedCodec.java:288-293
     }
+    if (c.nested) {  // the level-2 codec validates against its own "shard" (the inner chunk)
+      for (int d = 0; d < n; d++) {
+        if (c.nested_chunk_shape[d] <= 0 || inner[d] % c.nested_chunk_shape[d] != 0) {
+          set_err(err, errlen,
+                  "Sharding inner chunk shape %s does not evenly divide the outer chunk size %s",
+                  fmt_ints32(c.nested_chunk_shape, n).c_str(), fmt_ints32(inner, n).c_str());
+          return ZH_EDATA;
+        }
+      }
+      if (c.nested_index_location != ZH_INDEX_START && c.nested_index_location != ZH_INDEX_END) {
+        set_err(err, errlen, "Only index_location \"start\" or \"end\" are supported.");
+        return ZH_EDATA;
+      }
+    }
+  } else if (c.nested) {
+    set_err(err, errlen, "nested sharding requires an outer sharding codec");
+    return ZH_EINVAL;
   }
   if (c.has_transpose && !is_perm(n, c.transpose_order)) {
     set_err(err, errlen, "Order is no permutation array");  // TransposeCodec.java:36-38
@@ -340,11 +360,19 @@ int zh_validate_meta(const zh_array_meta* m, char* err, size_t errlen) {
 // =====================================================================================
 namespace {
 
+// Shape of the chunks the scatter kernels move: the chunk (unsharded), the inner chunk
+// (sharded) or the leaf of the level-2 shard (nested: the flattened leaf grid).
+const int32_t* leaf_shape(const zh_array_meta* m) {
+  const zh_codec_chain& c = m->chain;
+  if (!c.sharded) return m->chunk_shape;
+  return c.nested ? c.nested_chunk_shape : c.inner_chunk_shape;
+}
+
 void fill_common_args(const zh_array_meta* m, const int64_t* region_shape, bool encode,
                       ScatterArgs& a, int& tile_mode) {
   const int n = m->ndim;
   const zh_codec_chain& c = m->chain;
-  const int32_t* inner = c.sharded ? c.inner_chunk_shape : m->chunk_shape;
+  const int32_t* inner = leaf_shape(m);
   int32_t order[kMaxDims];
   for (int d = 0; d < n; d++) order[d] = c.has_transpose ? c.transpose_order[d] : d;
   memset(&a, 0, sizeof(a));
@@ -519,6 +547,7 @@ void plan_free(zh_plan* p) {
   (void)hipFree(p->d_desc);
   (void)hipFree(p->d_slow);
   (void)hipFree(p->d_fast_tab);
+  (void)hipFree(p->d_flat);
   for (auto& e : p->ev_pending)
     for (auto ev : e) p->ev_pool.push_back(ev);
   for (auto ev : p->ev_pool) (void)hipEventDestroy(ev);
@@ -566,8 +595,18 @@ int zh_plan_create(zh_ctx* ctx, const zh_array_meta* m, const zh_chunk_src* chun
   p->nshards = ncoords;
   fill_common_args(m, shape, false, p->args, p->tile_mode);
   const zh_codec_chain& c = m->chain;
-  const int32_t* inner = c.sharded ? c.inner_chunk_shape : m->chunk_shape;
+  const int32_t* inner = leaf_shape(m);
   const int64_t isz = zh_shard_index_size(m);
+  // nested sharding: level-1 cells and the flattened leaf index per shard
+  const bool nested = c.sharded && c.nested;
+  int64_t cps_leaf = 1, cps2 = 1;
+  for (int d = 0; d < n; d++) {
+    cps_leaf *= m->chunk_shape[d] / inner[d];
+    if (nested) cps2 *= c.inner_chunk_shape[d] / c.nested_chunk_shape[d];
+  }
+  const int64_t sub_isz = nested ? 16 * cps2 + (c.nested_index_has_crc32c ? 4 : 0) : 0;
+  int64_t l1_items = 0, flat_bytes = 0;
+  std::vector<int64_t> flat_off(ncoords, -1);
   std::vector<DevShard> hs(ncoords);
   std::vector<CrcJob> jobs;
   p->coords.resize(ncoords * n);
@@ -608,6 +647,7 @@ int zh_plan_create(zh_ctx* ctx, const zh_array_meta* m, const zh_chunk_src* chun
       S.part_hi[d] = 1;
     }
     S.out_base = ob;
+    S.l1_begin = l1_items;
     items += nit;
     if (S.data) {
       if (c.sharded) {
@@ -624,6 +664,21 @@ int zh_plan_create(zh_ctx* ctx, const zh_array_meta* m, const zh_chunk_src* chun
                 (long long)S.nbytes, (long long)p->args.inner_nbytes, fmt_ints(cc, n).c_str());
         plan_free(p);
         return ZH_EDATA;
+      }
+      if (nested) {
+        int64_t ncell = 1;
+        S.l1_begin = l1_items;
+        for (int d = 0; d < n; d++) {
+          const int32_t i1 = c.inner_chunk_shape[d];
+          S.l1_box_start[d] = co[d] / i1;
+          S.l1_box_count[d] = (co[d] + ps[d] - 1) / i1 - S.l1_box_start[d] + 1;
+          ncell *= S.l1_box_count[d];
+        }
+        for (int d = n; d < kMaxDims; d++) S.l1_box_count[d] = 1;
+        l1_items += ncell;
+        flat_off[i] = flat_bytes;
+        flat_bytes += 16 * cps_leaf;
+        in_bytes += ncell * sub_isz;  // the referenced sub-shard indexes
       }
       // algorithmic input bytes: referenced inner chunks + the index for a
       // shard; only the in-bounds part of an unsharded chunk
@@ -658,6 +713,35 @@ int zh_plan_create(zh_ctx* ctx, const zh_array_meta* m, const zh_chunk_src* chun
       p->h2d_len.push_back(hs[i].nbytes);
       hs[i].data = p->d_input + stage_off[i];
     }
+  }
+  if (nested && flat_bytes > 0) {
+    st = dev_alloc(&p->d_flat, (size_t)flat_bytes, err, errlen);
+    if (st != ZH_OK) {
+      plan_free(p);
+      return st;
+    }
+    for (int64_t i = 0; i < ncoords; i++)
+      if (flat_off[i] >= 0) hs[i].flat = p->d_flat + flat_off[i];
+    NestArgs& N = p->nest;
+    N.nshards = ncoords;
+    N.n_l1 = l1_items;
+    N.ndim = n;
+    N.index_be = c.index_endian == ZH_ENDIAN_BIG;
+    N.sub_be = c.nested_index_endian == ZH_ENDIAN_BIG;
+    N.sub_crc = c.nested_index_has_crc32c ? 1 : 0;
+    N.sub_start = c.nested_index_location == ZH_INDEX_START;
+    N.sub_isz = sub_isz;
+    N.cps2 = cps2;
+    N.leaf_nbytes = p->args.inner_nbytes;
+    int64_t s1 = 1, sf = 1;
+    for (int d = n - 1; d >= 0; d--) {
+      N.cps1_stride[d] = s1;
+      s1 *= m->chunk_shape[d] / c.inner_chunk_shape[d];
+      N.flat_stride[d] = sf;
+      sf *= m->chunk_shape[d] / inner[d];
+      N.r[d] = c.inner_chunk_shape[d] / inner[d];
+    }
+    p->nest_grid = (int)std::min<int64_t>(l1_items, (int64_t)ctx->cu_count * 16);
   }
   // CRC jobs over the device copies of the indexes
   if (c.sharded && c.index_has_crc32c) {
@@ -720,6 +804,8 @@ int zh_plan_create(zh_ctx* ctx, const zh_array_meta* m, const zh_chunk_src* chun
   p->args.nshards = ncoords;
   p->args.total_items = items << p->args.piece_shift;
   p->args.status = p->d_status;
+  p->nest.shards = p->d_shards;
+  p->nest.status = p->d_status;
   p->grid = grid_for(ctx, p->args.total_items);
   // non-temporal loads + stores: +4 % on the row path, +1 % on the tile path (interleaved
   // A/B in one process, profiles/r01/experiments/tune_*.json)
@@ -756,6 +842,7 @@ int zh_plan_execute(zh_plan* p, void* out, void* stream_v) {
   }
   ZH_HIP(launch_crc(p->d_crc_jobs, p->n_crc_jobs, p->n_crc_spans, p->d_crc_partials, p->d_status,
                     s));
+  if (p->d_flat) ZH_HIP(launch_nested_index(p->nest, p->nest_grid, s));
   ScatterArgs a = p->args;
   a.region = (p->flags & ZH_OUT_DEVICE) ? (uint8_t*)out : p->d_out;
   ZH_HIP(launch_resolve(a, s));
@@ -791,11 +878,17 @@ int zh_plan_wait(zh_plan* p, char* err, size_t errlen) {
     }
     const uint64_t key = w[kStBadChunk];
     const uint32_t lin = 0xFFFFFFFFu - (uint32_t)(key >> 8);
-    const uint32_t kind = (uint32_t)(key & 0xFF);
+    const uint32_t level = (uint32_t)(key & (kFlagL1 | kFlagLeaf));
+    const uint32_t kind = (uint32_t)(key & (kFlagRange | kFlagLength));
+    // chunk coordinates in the grid of the codec that read the entry: the outer shard's
+    // inner-chunk grid, or (nested, kFlagLeaf) the sub-shard's leaf grid
+    const zh_codec_chain& ch = p->meta.chain;
     int64_t ic[kMaxDims];
     uint32_t r = lin;
     for (int d = n - 1; d >= 0; d--) {
-      const int32_t cps = p->meta.chunk_shape[d] / p->meta.chain.inner_chunk_shape[d];
+      int32_t cps = p->meta.chunk_shape[d] / leaf_shape(&p->meta)[d];
+      if (level & kFlagL1) cps = p->meta.chunk_shape[d] / ch.inner_chunk_shape[d];
+      if (level & kFlagLeaf) cps = ch.inner_chunk_shape[d] / ch.nested_chunk_shape[d];
       ic[d] = r % cps;
       r /= cps;
     }
@@ -902,7 +995,16 @@ int64_t zh_array_encoded_bound(const zh_array_meta* m) {
   if (!m) return -1;
   int64_t nel = 1;
   for (int d = 0; d < m->ndim; d++) nel *= m->chunk_shape[d];
-  return nel * m->dtype_size + (m->chain.sharded ? zh_shard_index_size(m) : 0);
+  int64_t bound = nel * m->dtype_size + (m->chain.sharded ? zh_shard_index_size(m) : 0);
+  if (m->chain.sharded && m->chain.nested) {  // + one sub-shard index per level-1 cell
+    int64_t ncell = 1, cps2 = 1;
+    for (int d = 0; d < m->ndim; d++) {
+      ncell *= m->chunk_shape[d] / m->chain.inner_chunk_shape[d];
+      cps2 *= m->chain.inner_chunk_shape[d] / m->chain.nested_chunk_shape[d];
+    }
+    bound += ncell * (16 * cps2 + (m->chain.nested_index_has_crc32c ? 4 : 0));
+  }
+  return bound;
 }
 
 int zh_array_write(zh_ctx* ctx, const zh_array_meta* m, const void* src, const int64_t* offset,
@@ -937,7 +1039,7 @@ int zh_array_write(zh_ctx* ctx, const zh_array_meta* m, const void* src, const i
   int tile_mode = 0;
   fill_common_args(m, shape, true, a, tile_mode);
   const zh_codec_chain& c = m->chain;
-  const int32_t* inner = c.sharded ? c.inner_chunk_shape : m->chunk_shape;
+  const int32_t* inner = leaf_shape(m);
   std::vector<DevShard> hs(ncoords);
   int64_t cur[kMaxDims] = {0};
   int64_t items = 0;
@@ -1013,14 +1115,99 @@ int zh_array_write(zh_ctx* ctx, const zh_array_meta* m, const void* src, const i
   const int big = c.index_endian == ZH_ENDIAN_BIG;
   std::vector<int64_t> hoff((size_t)items, -1);
   std::vector<std::vector<uint8_t>> indexes(ncoords);
+  struct SubIndex {  // nested: a sub-shard index, kept alive until the stream syncs
+    int64_t shard, pos;
+    std::vector<uint8_t> bytes;
+  };
+  std::vector<SubIndex> sub_indexes;
   const int64_t np = 1ll << a.piece_shift;
+  auto put_entry = [](uint8_t* e, uint64_t eo, uint64_t en, bool be) {
+    for (int byte = 0; byte < 8; byte++) {
+      const int sh = be ? 56 - 8 * byte : 8 * byte;
+      e[byte] = (uint8_t)(eo >> sh);
+      e[8 + byte] = (uint8_t)(en >> sh);
+    }
+  };
   for (int64_t i = 0; i < ncoords; i++) {
     const int64_t nit = c.sharded ? cps_total : 1;
     const int64_t b = hs[i].item_begin;
     int64_t payload = 0, nonfill = 0;
     std::vector<uint8_t>& idx = indexes[i];
     if (c.sharded) idx.assign((size_t)isz, 0);
-    for (int64_t k = 0; k < nit; k++) {
+    auto leaf_any = [&](int64_t k) {
+      bool any = false;
+      for (int64_t q = 0; q < np; q++) any |= hflags[(size_t)(((b + k) << a.piece_shift) + q)] != 0;
+      return any;
+    };
+    if (c.sharded && c.nested) {
+      // level-1 cells in C order, each a sub-shard (ShardingIndexedCodec.encode of the level-2
+      // codec, :105-168): its non-fill leaves in C order + its own index (+crc32c); an
+      // all-fill cell is elided at level 1 (-1, -1)
+      int64_t g1[kMaxDims], r[kMaxDims], fstr[kMaxDims], ncell = 1, cps2 = 1;
+      for (int d = 0; d < n; d++) {
+        g1[d] = m->chunk_shape[d] / c.inner_chunk_shape[d];
+        r[d] = c.inner_chunk_shape[d] / inner[d];
+        ncell *= g1[d];
+        cps2 *= r[d];
+      }
+      int64_t sf = 1;
+      for (int d = n - 1; d >= 0; d--) {
+        fstr[d] = sf;
+        sf *= m->chunk_shape[d] / inner[d];
+      }
+      const int64_t sub_isz = 16 * cps2 + (c.nested_index_has_crc32c ? 4 : 0);
+      const bool sub_start = c.nested_index_location == ZH_INDEX_START;
+      const bool sub_be = c.nested_index_endian == ZH_ENDIAN_BIG;
+      int64_t pos = start ? isz : 0;
+      std::vector<int64_t> ks((size_t)cps2);
+      for (int64_t cell = 0; cell < ncell; cell++) {
+        int64_t c1[kMaxDims], q = cell;
+        for (int d = n - 1; d >= 0; d--) {
+          c1[d] = q % g1[d];
+          q /= g1[d];
+        }
+        bool any_cell = false;
+        for (int64_t k2 = 0; k2 < cps2; k2++) {
+          int64_t f = 0, t = k2;
+          for (int d = n - 1; d >= 0; d--) {
+            f += (c1[d] * r[d] + t % r[d]) * fstr[d];
+            t /= r[d];
+          }
+          ks[(size_t)k2] = f;
+          any_cell |= leaf_any(f);
+        }
+        if (!any_cell) {
+          put_entry(&idx[16 * cell], ~0ull, ~0ull, big);
+          continue;
+        }
+        const int64_t sub_pos = pos;
+        int64_t leaf_pos = pos + (sub_start ? sub_isz : 0);
+        std::vector<uint8_t> sidx((size_t)sub_isz, 0);
+        for (int64_t k2 = 0; k2 < cps2; k2++) {
+          const int64_t f = ks[(size_t)k2];
+          if (leaf_any(f)) {
+            hoff[b + f] = leaf_pos;
+            put_entry(&sidx[16 * k2], (uint64_t)(leaf_pos - sub_pos), (uint64_t)a.inner_nbytes,
+                      sub_be);
+            leaf_pos += a.inner_nbytes;
+            nonfill++;
+          } else {
+            put_entry(&sidx[16 * k2], ~0ull, ~0ull, sub_be);
+          }
+        }
+        if (c.nested_index_has_crc32c) {
+          const uint32_t crc = crc32c_host(0, sidx.data(), (size_t)(sub_isz - 4));
+          for (int byte = 0; byte < 4; byte++) sidx[sub_isz - 4 + byte] = (uint8_t)(crc >> (8 * byte));
+        }
+        const int64_t sidx_pos = sub_start ? sub_pos : leaf_pos;
+        const int64_t sub_len = leaf_pos - sub_pos + (sub_start ? 0 : sub_isz);
+        put_entry(&idx[16 * cell], (uint64_t)sub_pos, (uint64_t)sub_len, big);
+        sub_indexes.push_back({i, sidx_pos, std::move(sidx)});
+        pos = sub_pos + sub_len;
+      }
+      payload = pos - (start ? isz : 0);
+    }
+    for (int64_t k = 0; k < nit && !(c.sharded && c.nested); k++) {
       bool any = false;
       for (int64_t q = 0; q < np; q++) any |= hflags[(size_t)(((b + k) << a.piece_shift) + q)] != 0;
       uint64_t eo = ~0ull, en = ~0ull;
@@ -1051,6 +1238,12 @@ int zh_array_write(zh_ctx* ctx, const zh_array_meta* m, const void* src, const i
       return ZH_EINVAL;
     }
     dsts[i].nbytes = total;
+    if (c.sharded && c.nested) {
+      for (auto& si : sub_indexes)
+        if (si.shard == i)
+          ZH_HIPC(hipMemcpyAsync((uint8_t*)dsts[i].data + si.pos, si.bytes.data(), si.bytes.size(),
+                                 hipMemcpyHostToDevice, s));
+    }
     if (c.sharded) {
       if (c.index_has_crc32c) {  // Crc32cCodec.encode :50-60
         const uint32_t crc = crc32c_host(0, idx.data(), (size_t)(isz - 4));
@@ -1078,6 +1271,17 @@ int zh_device_malloc(zh_ctx* ctx, size_t bytes, void** out) {
   if (!ctx || !out) return ZH_EINVAL;
   (void)hipSetDevice(ctx->device);
   hipError_t e = hipMalloc(out, bytes);
+  return e == hipSuccess ? ZH_OK : (e == hipErrorOutOfMemory ? ZH_ENOMEM : ZH_EHIP);
+}
+int zh_device_malloc_ex(zh_ctx* ctx, size_t bytes, unsigned flags, void** out) {
+  if (!ctx || !out) return ZH_EINVAL;
+  (void)hipSetDevice(ctx->device);
+  hipError_t e = hipErrorOutOfMemory;
+  if (flags & ZH_MALLOC_CONTIGUOUS) {
+    e = hipExtMallocWithFlags(out, bytes, hipDeviceMallocContiguous);
+    if (e != hipSuccess) (void)hipGetLastError();
+  }
+  if (e != hipSuccess && !(flags & ZH_MALLOC_REQUIRE)) e = hipMalloc(out, bytes);
   return e == hipSuccess ? ZH_OK : (e == hipErrorOutOfMemory ? ZH_ENOMEM : ZH_EHIP);
 }
 int zh_device_free(zh_ctx* ctx, void* ptr) {

@@ -54,6 +54,13 @@ struct DevShard {
   int32_t box_count[kMaxDims];  // inner chunks per dim in the box
   int32_t part_lo[kMaxDims];    // requested part of the shard (shard-local coords)
   int32_t part_hi[kMaxDims];
+  // nested sharding: flattened leaf index (16 B LE entries over the shard's leaf grid,
+  // written by nested_index_kernel; nullptr for single-level sharding) and the box of
+  // level-1 cells the part references
+  uint8_t* flat;
+  int64_t l1_begin;             // prefix sum of referenced level-1 cells before this shard
+  int32_t l1_box_start[kMaxDims];
+  int32_t l1_box_count[kMaxDims];
 };
 
 // Per-inner-chunk work descriptor written by the resolve kernel (index parse) and read
@@ -113,6 +120,30 @@ struct ScatterArgs {
   int32_t tile_variant;         // tile fast path: 0 row-per-tile loads, 1 row-interleaved groups
 };
 
+// Nested sharding pre-pass (nested_index_kernel): one workgroup per referenced level-1 cell
+// resolves the outer entry, CRC-checks the cell's sub-shard index and writes its leaves'
+// absolute (offset, nbytes) into DevShard::flat, so that the single-level resolve/scatter
+// kernels run unchanged with leaf = inner chunk.
+enum : uint32_t { kFlagL1 = 8, kFlagLeaf = 16 };  // error-key level bits (status kStBadChunk)
+struct NestArgs {
+  const DevShard* shards;
+  int64_t nshards;
+  int64_t n_l1;                   // referenced level-1 cells (all shards)
+  uint64_t* status;
+  int32_t ndim;
+  int32_t index_be;               // outer index endianness
+  int32_t sub_be;                 // sub-shard index endianness
+  int32_t sub_crc;                // sub-shard index has crc32c
+  int32_t sub_start;              // sub-shard index at the start
+  int32_t pad;
+  int64_t sub_isz;                // encoded sub-shard index size (16 * cps2 [+ 4])
+  int64_t cps2;                   // leaves per level-1 cell
+  int64_t leaf_nbytes;
+  int64_t cps1_stride[kMaxDims];  // outer index entry stride per level-1 coordinate
+  int64_t flat_stride[kMaxDims];  // flat index entry stride per leaf coordinate
+  int32_t r[kMaxDims];            // leaves per level-1 cell along each dim
+};
+
 struct CrcJob {
   const uint8_t* base;      // first index byte (device)
   int64_t len;              // bytes under the CRC (16 * entries)
@@ -125,6 +156,7 @@ struct CrcJob {
 hipError_t launch_crc(const CrcJob* jobs, int64_t njobs, int64_t nspans, uint32_t* partials,
                       uint64_t* status, hipStream_t stream);
 hipError_t launch_resolve(const ScatterArgs& a, hipStream_t stream);
+hipError_t launch_nested_index(const NestArgs& a, int grid, hipStream_t stream);
 hipError_t launch_scatter(const ScatterArgs& a, int dsize, int tile_mode, int encode, int grid,
                           hipStream_t stream);
 hipError_t launch_decode_slow(const ScatterArgs& a, int grid, hipStream_t stream);

@@ -188,6 +188,21 @@ __device__ __forceinline__ int64_t find_shard(const ScatterArgs& a, int64_t cite
   return lo;
 }
 
+// Index entry `lin` of shard S: the stored index (index_codecs endianness) or, for nested
+// sharding, the flattened little-endian leaf index written by nested_index_kernel.
+__device__ __forceinline__ void index_entry(const ScatterArgs& a, const DevShard& S, int64_t lin,
+                                            uint64_t& off, uint64_t& nb) {
+  if (S.flat) {
+    const uint64_t* e = reinterpret_cast<const uint64_t*>(S.flat) + 2 * lin;
+    off = e[0];
+    nb = e[1];
+    return;
+  }
+  const uint8_t* ent = S.data + S.index_off + 16 * lin;
+  off = ld_u64_unaligned(ent, a.index_be);
+  nb = ld_u64_unaligned(ent + 8, a.index_be);
+}
+
 // Builds the geometry of work item `item` (returns the shard slot).
 template <bool ENC>
 __device__ __forceinline__ int64_t make_item(const ScatterArgs& a, int64_t item, Item& it) {
@@ -223,9 +238,8 @@ __device__ __forceinline__ int64_t make_item(const ScatterArgs& a, int64_t item,
 #pragma unroll
       for (int d = 0; d < kMaxDims; d++)
         if (d < n) lin += (int64_t)ic[d] * a.cps_stride[d];
-      const uint8_t* ent = S.data + S.index_off + 16 * lin;
-      const uint64_t off = ld_u64_unaligned(ent, a.index_be);
-      const uint64_t nb = ld_u64_unaligned(ent + 8, a.index_be);
+      uint64_t off, nb;
+      index_entry(a, S, lin, off, nb);
       if (off == ~0ull || nb == ~0ull) {
         // missing inner chunk: the zero-initialised part array shows through (Q1,
         // ShardingIndexedCodec.java:189, 219-221)
@@ -598,9 +612,8 @@ __device__ __forceinline__ ItemDesc resolve_one(const ScatterArgs& a, int64_t ci
   }
   const uint8_t* src = S.data;
   if (a.sharded) {
-    const uint8_t* ent = S.data + S.index_off + 16 * lin;
-    const uint64_t off = ld_u64_unaligned(ent, a.index_be);
-    const uint64_t nb = ld_u64_unaligned(ent + 8, a.index_be);
+    uint64_t off, nb;
+    index_entry(a, S, lin, off, nb);
     if (off == ~0ull || nb == ~0ull) {  // Q1: zero-initialised part array
       D.kind = full ? kDescFullFill : kDescClip;
       D.fill = 0;
@@ -1185,9 +1198,145 @@ __global__ void crc_finalize_kernel(const CrcJob* jobs, int64_t njobs, const uin
   const uint32_t stored =
       (uint32_t)s[0] | ((uint32_t)s[1] << 8) | ((uint32_t)s[2] << 16) | ((uint32_t)s[3] << 24);
   uint64_t* st = status + (int64_t)J.shard * kStWords;
-  st[kStCrcStored] = stored;
-  st[kStCrcComputed] = c;
-  if (c != stored) atomicOr((unsigned long long*)(st + kStFlags), (unsigned long long)kFlagCrc);
+  if (c != stored) {  // bit 32 marks the pair as set (nested sub-shard checks come later)
+    st[kStCrcStored] = (1ull << 32) | stored;
+    st[kStCrcComputed] = c;
+    atomicOr((unsigned long long*)(st + kStFlags), (unsigned long long)kFlagCrc);
+  }
+}
+
+// ---------------------------------------------------------------------------------
+// nested sharding: flatten the two-level index (ShardingIndexedCodec.decodeInternal :183-243
+// applied twice — the outer codec's inner pipeline is the level-2 sharding codec, whose
+// decode(ByteBuffer) :97-103 reads its own index from the sub-shard bytes)
+// ---------------------------------------------------------------------------------
+__device__ __forceinline__ void nest_error(const NestArgs& a, int64_t s, uint32_t lin,
+                                           uint32_t kind) {
+  const uint64_t key = ((uint64_t)(0xFFFFFFFFu - lin) << 8) | kind;
+  atomicOr((unsigned long long*)(a.status + s * kStWords + kStFlags),
+           (unsigned long long)(kind & (kFlagRange | kFlagLength)));
+  atomicMax((unsigned long long*)(a.status + s * kStWords + kStBadChunk), (unsigned long long)key);
+}
+
+// CRC-32C of p[0, len) by the whole workgroup (kBlock lanes, kCrcLane-byte segments per
+// lane, kCrcSpan bytes per round); result valid in every lane.
+__device__ uint32_t block_crc(const uint8_t* p, int64_t len, const uint32_t (*T)[256],
+                              uint32_t* red) {
+  const int tid = threadIdx.x;
+  uint32_t total = 0;
+  for (int64_t sb = 0; sb < len; sb += kCrcSpan) {
+    const int64_t slen = min((int64_t)kCrcSpan, len - sb);
+    const int64_t lb = (int64_t)tid * kCrcLane;
+    const int64_t llen = max((int64_t)0, min((int64_t)kCrcLane, slen - lb));
+    const uint8_t* q = p + sb + lb;
+    uint32_t c = 0xFFFFFFFFu;
+    for (int64_t i = 0; i < llen; i++) c = T[0][(c ^ q[i]) & 0xFFu] ^ (c >> 8);
+    red[tid] = c ^ 0xFFFFFFFFu;
+    __syncthreads();
+#pragma unroll 1
+    for (int k = 0; k < 8; k++) {
+      const int stride = 1 << k;
+      if ((tid & ((stride << 1) - 1)) == 0) {
+        const int64_t rstart = (int64_t)(tid + stride) * kCrcLane;
+        const int64_t rlen = max((int64_t)0, min((int64_t)kCrcLane << k, slen - rstart));
+        if (rlen > 0) red[tid] = crc_combine(red[tid], red[tid + stride], (uint64_t)rlen);
+      }
+      __syncthreads();
+    }
+    total = crc_combine(total, red[0], (uint64_t)slen);
+    __syncthreads();
+  }
+  return total;
+}
+
+__global__ __launch_bounds__(kBlock) void nested_index_kernel(NestArgs a) {
+  __shared__ uint32_t T[1][256];
+  __shared__ uint32_t red[kBlock];
+  const int tid = threadIdx.x;
+  {
+    uint32_t c = (uint32_t)tid;
+#pragma unroll
+    for (int k = 0; k < 8; k++) c = (c & 1) ? (c >> 1) ^ kPoly : c >> 1;
+    T[0][tid] = c;
+  }
+  __syncthreads();
+  const int n = a.ndim;
+  for (int64_t it = blockIdx.x; it < a.n_l1; it += gridDim.x) {
+    int64_t lo = 0, hi = a.nshards - 1;  // shard of this level-1 cell (uniform)
+    while (lo < hi) {
+      const int64_t mid = (lo + hi + 1) >> 1;
+      if (a.shards[mid].l1_begin <= it) lo = mid;
+      else hi = mid - 1;
+    }
+    const DevShard& S = a.shards[lo];
+    if (S.data == nullptr || S.flat == nullptr) continue;
+    int64_t j = it - S.l1_begin, lin1 = 0, fbase = 0;
+    int32_t c1[kMaxDims];
+#pragma unroll
+    for (int d = kMaxDims - 1; d >= 0; --d) {
+      c1[d] = 0;
+      if (d < n) {
+        const int64_t cnt = S.l1_box_count[d];
+        c1[d] = S.l1_box_start[d] + (int32_t)(j % cnt);
+        j /= cnt;
+        lin1 += (int64_t)c1[d] * a.cps1_stride[d];
+        fbase += (int64_t)c1[d] * a.r[d] * a.flat_stride[d];
+      }
+    }
+    const uint8_t* ent = S.data + S.index_off + 16 * lin1;
+    const uint64_t off1 = ld_u64_unaligned(ent, a.index_be);
+    const uint64_t nb1 = ld_u64_unaligned(ent + 8, a.index_be);
+    const uint64_t total = (uint64_t)S.nbytes;
+    bool ok = !(off1 == ~0ull || nb1 == ~0ull);  // missing sub-shard: zeros (Q1)
+    if (ok && !(off1 <= total && nb1 <= total - off1 && nb1 >= (uint64_t)a.sub_isz)) {
+      if (tid == 0) nest_error(a, lo, (uint32_t)lin1, kFlagRange | kFlagL1);
+      ok = false;
+    }
+    const uint8_t* sub = S.data + off1;
+    const uint8_t* ib = ok ? (a.sub_start ? sub : sub + nb1 - a.sub_isz) : nullptr;
+    if (ok && a.sub_crc) {  // Crc32cCodec.decode on the sub-shard index (:24-48)
+      const int64_t len = a.sub_isz - 4;
+      const uint32_t c = block_crc(ib, len, T, red);
+      const uint8_t* s = ib + len;
+      const uint32_t stored =
+          (uint32_t)s[0] | ((uint32_t)s[1] << 8) | ((uint32_t)s[2] << 16) | ((uint32_t)s[3] << 24);
+      if (c != stored && tid == 0) {
+        uint64_t* st = a.status + lo * kStWords;
+        // first reporter wins the (stored, computed) pair; bit 32 marks the word as set
+        if (atomicCAS((unsigned long long*)(st + kStCrcStored), 0ull,
+                      (unsigned long long)((1ull << 32) | stored)) == 0ull)
+          st[kStCrcComputed] = c;
+        atomicOr((unsigned long long*)(st + kStFlags), (unsigned long long)kFlagCrc);
+      }
+    }
+    uint64_t* flat = reinterpret_cast<uint64_t*>(S.flat);
+    for (int64_t k2 = tid; k2 < a.cps2; k2 += kBlock) {
+      int64_t q = k2, f = fbase;
+#pragma unroll
+      for (int d = kMaxDims - 1; d >= 0; --d)
+        if (d < n) {
+          f += (q % a.r[d]) * a.flat_stride[d];
+          q /= a.r[d];
+        }
+      uint64_t eo = ~0ull, en = ~0ull;
+      if (ok) {
+        const uint64_t off2 = ld_u64_unaligned(ib + 16 * k2, a.sub_be);
+        const uint64_t nb2 = ld_u64_unaligned(ib + 16 * k2 + 8, a.sub_be);
+        if (!(off2 == ~0ull || nb2 == ~0ull)) {
+          if (!(off2 <= nb1 && nb2 <= nb1 - off2)) {
+            nest_error(a, lo, (uint32_t)k2, kFlagRange | kFlagLeaf);
+          } else if (nb2 != (uint64_t)a.leaf_nbytes) {
+            nest_error(a, lo, (uint32_t)k2, kFlagLength | kFlagLeaf);
+          } else {
+            eo = off1 + off2;
+            en = nb2;
+          }
+        }
+      }
+      flat[2 * f] = eo;
+      flat[2 * f + 1] = en;
+    }
+  }
 }
 
 // ---------------------------------------------------------------------------------
@@ -1267,6 +1416,12 @@ __global__ __launch_bounds__(kBlock) void synth_verify_kernel(VerifyArgs a) {
 // ---------------------------------------------------------------------------------
 // launchers
 // ---------------------------------------------------------------------------------
+hipError_t launch_nested_index(const NestArgs& a, int grid, hipStream_t stream) {
+  if (a.n_l1 <= 0) return hipSuccess;
+  hipLaunchKernelGGL(nested_index_kernel, dim3((unsigned)grid), dim3(kBlock), 0, stream, a);
+  return hipGetLastError();
+}
+
 hipError_t launch_crc(const CrcJob* jobs, int64_t njobs, int64_t nspans, uint32_t* partials,
                       uint64_t* status, hipStream_t stream) {
   if (njobs == 0) return hipSuccess;

@@ -17,6 +17,8 @@ ZH_INDEX_END = 0
 ZH_INDEX_START = 1
 
 ZH_SRC_DEVICE = 0x1
+ZH_MALLOC_CONTIGUOUS = 0x1
+ZH_MALLOC_REQUIRE = 0x2
 ZH_OUT_DEVICE = 0x2
 
 
@@ -30,6 +32,11 @@ class zh_codec_chain(C.Structure):
         ("index_endian", C.c_int32),
         ("index_has_crc32c", C.c_int32),
         ("index_location", C.c_int32),
+        ("nested", C.c_int32),
+        ("nested_chunk_shape", C.c_int32 * ZH_MAX_DIMS),
+        ("nested_index_endian", C.c_int32),
+        ("nested_index_has_crc32c", C.c_int32),
+        ("nested_index_location", C.c_int32),
     ]
 
 
@@ -56,7 +63,9 @@ class zh_chunk_dst(C.Structure):
 
 def make_meta(shape, chunk_shape, dtype_size, *, fill=b"\0" * 8, is_bool=False, sharded=False,
               inner_chunk_shape=None, transpose_order=None, endian=ZH_ENDIAN_LITTLE,
-              index_endian=ZH_ENDIAN_LITTLE, index_crc32c=True, index_location=ZH_INDEX_END):
+              index_endian=ZH_ENDIAN_LITTLE, index_crc32c=True, index_location=ZH_INDEX_END,
+              nested_chunk_shape=None, nested_index_endian=ZH_ENDIAN_LITTLE,
+              nested_index_crc32c=True, nested_index_location=ZH_INDEX_END):
     """Build a zh_array_meta from Python values.  `fill` is the element's bytes (LE)."""
     m = zh_array_meta()
     n = len(shape)
@@ -82,4 +91,11 @@ def make_meta(shape, chunk_shape, dtype_size, *, fill=b"\0" * 8, is_bool=False, 
     ch.index_endian = index_endian
     ch.index_has_crc32c = 1 if index_crc32c else 0
     ch.index_location = index_location
+    if nested_chunk_shape is not None:
+        ch.nested = 1
+        for d in range(n):
+            ch.nested_chunk_shape[d] = int(nested_chunk_shape[d])
+        ch.nested_index_endian = nested_index_endian
+        ch.nested_index_has_crc32c = 1 if nested_index_crc32c else 0
+        ch.nested_index_location = nested_index_location
     return m

@@ -50,6 +50,7 @@ _SIGS = {
     "zh_array_write": (C.c_int, [P, PMETA, P, PI64, PI64, C.POINTER(A.zh_chunk_dst), I64, P, CH,
                                  SZ]),
     "zh_device_malloc": (C.c_int, [P, SZ, C.POINTER(P)]),
+    "zh_device_malloc_ex": (C.c_int, [P, SZ, C.c_uint, C.POINTER(P)]),
     "zh_device_free": (C.c_int, [P, P]),
     "zh_host_malloc_pinned": (C.c_int, [P, SZ, C.POINTER(P)]),
     "zh_host_free_pinned": (C.c_int, [P, P]),
@@ -137,9 +138,12 @@ class DeviceContext:
             pass
 
     # -- memory ---------------------------------------------------------------------
-    def malloc(self, nbytes):
+    def malloc(self, nbytes, flags=None):
+        """Device allocation; `flags` (A.ZH_MALLOC_*) defaults to ZH_MALLOC env (else 0)."""
         p = P()
-        st = self.L.zh_device_malloc(self.h, int(nbytes), C.byref(p))
+        if flags is None:
+            flags = int(os.environ.get("ZH_MALLOC", "0"), 0)
+        st = self.L.zh_device_malloc_ex(self.h, int(nbytes), int(flags), C.byref(p))
         if st != A.ZH_OK:
             raise ZhError(st, f"device malloc of {nbytes} bytes failed")
         return p.value

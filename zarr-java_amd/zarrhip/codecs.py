@@ -340,12 +340,20 @@ def _split_inner(codecs, ndim, dsize):
     if len(aa) > 1 or any(not isinstance(c, TransposeCodec) for c in aa):
         raise UnsupportedChainError("only a single transpose array→array codec is device-supported")
     if not isinstance(ab, BytesCodec):
-        raise UnsupportedChainError("nested sharding is not device-supported")
+        raise UnsupportedChainError("only bytes (or one nested sharding level) is device-supported")
     order = None
     if aa:
         aa[0].validate(ndim)
         order = aa[0].order
     return order, ab.byte_order(dsize), bb
+
+
+def _index_chain(sh):
+    ic = sh.index_codecs
+    if not ic or not isinstance(ic[0], BytesCodec) or \
+            any(not isinstance(c, Crc32cCodec) for c in ic[1:]) or len(ic) > 2:
+        raise UnsupportedChainError("index codecs must be [bytes, crc32c?]")
+    return ic
 
 
 def device_chain(codecs, ndim, dsize):
@@ -357,16 +365,33 @@ def device_chain(codecs, ndim, dsize):
             # array-level codecs next to sharding disable partial decode
             # (CodecPipeline.supportsPartialDecode :82-84)
             raise UnsupportedChainError("sharding_indexed must be the only array-level codec")
-        order, endian, inner_bb = _split_inner(ab.codecs, ndim, dsize)
-        ic = ab.index_codecs
-        if not ic or not isinstance(ic[0], BytesCodec) or \
-                any(not isinstance(c, Crc32cCodec) for c in ic[1:]) or len(ic) > 2:
-            raise UnsupportedChainError("index codecs must be [bytes, crc32c?]")
+        ic = _index_chain(ab)
+        nested = None
+        validate_pipeline(ab.codecs)
+        inner_ab = [c for c in ab.codecs if c.kind == "ab"][0]
+        if isinstance(inner_ab, ShardingIndexedCodec):
+            # nested sharding (ZarrPythonTests.java:177-179): the inner pipeline is exactly
+            # [sharding_indexed{...}] whose own inner pipeline is [transpose?, bytes]
+            if len(ab.codecs) != 1:
+                raise UnsupportedChainError("nested sharding must be the only inner codec")
+            nested = inner_ab
+            order, endian, inner_bb = _split_inner(nested.codecs, ndim, dsize)
+            if inner_bb:
+                raise UnsupportedChainError("nested sharding with byte-to-byte leaf codecs")
+        else:
+            order, endian, inner_bb = _split_inner(ab.codecs, ndim, dsize)
         chain = dict(sharded=True, inner_chunk_shape=ab.chunk_shape, transpose_order=order,
                      endian=endian, index_endian=ic[0].byte_order(8),
                      index_crc32c=len(ic) == 2,
                      index_location=A.ZH_INDEX_START if ab.index_location == "start"
                      else A.ZH_INDEX_END)
+        if nested is not None:
+            nic = _index_chain(nested)
+            chain.update(nested_chunk_shape=nested.chunk_shape,
+                         nested_index_endian=nic[0].byte_order(8),
+                         nested_index_crc32c=len(nic) == 2,
+                         nested_index_location=A.ZH_INDEX_START
+                         if nested.index_location == "start" else A.ZH_INDEX_END)
         return DeviceChain(chain, [], inner_bb, ic)
     order, endian, bb = _split_inner(codecs, ndim, dsize)
     chain = dict(sharded=False, transpose_order=order, endian=endian)

@@ -157,7 +157,11 @@ class ArrayMetadata:
                            transpose_order=ch["transpose_order"], endian=ch["endian"],
                            index_endian=ch.get("index_endian", A.ZH_ENDIAN_LITTLE),
                            index_crc32c=ch.get("index_crc32c", False),
-                           index_location=ch.get("index_location", A.ZH_INDEX_END))
+                           index_location=ch.get("index_location", A.ZH_INDEX_END),
+                           nested_chunk_shape=ch.get("nested_chunk_shape"),
+                           nested_index_endian=ch.get("nested_index_endian", A.ZH_ENDIAN_LITTLE),
+                           nested_index_crc32c=ch.get("nested_index_crc32c", True),
+                           nested_index_location=ch.get("nested_index_location", A.ZH_INDEX_END))
 
 
 def calculate_default_chunks(shape):
