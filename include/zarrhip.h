@@ -85,6 +85,10 @@ typedef struct zh_codec_chain {
   int32_t nested_index_endian;
   int32_t nested_index_has_crc32c;
   int32_t nested_index_location;
+  /* The chunk codecs end with crc32c ([transpose?, bytes, crc32c]; ZarrPythonTests "crc32c",
+   * ZarrPythonTests.java:180-182): each stored (inner/leaf) chunk is its payload followed by
+   * the payload's CRC-32C, little-endian (Crc32cCodec.java:24-60), verified on the device. */
+  int32_t inner_crc32c;
 } zh_codec_chain;
 
 /* CoreArrayMetadata (M/core/ArrayMetadata.java:154-187) + the codec chain. */
@@ -205,6 +209,9 @@ int zh_array_write(zh_ctx* ctx, const zh_array_meta* meta, const void* src,
                    int64_t nchunks, void* stream, char* err, size_t errlen);
 
 /* ---- device memory / stream / event plumbing for callers without their own ---------- */
+/* sizeof of the public structs, for binding-side layout checks (ctypes / JNI mirrors):
+ * out[0..3] = zh_codec_chain, zh_array_meta, zh_chunk_src, zh_chunk_dst.  Returns 4. */
+int zh_abi_sizes(int64_t* out, int n);
 int zh_device_malloc(zh_ctx* ctx, size_t bytes, void** out);
 /* Allocation flags for zh_device_malloc_ex.  ZH_MALLOC_CONTIGUOUS asks for physically
  * contiguous HBM (hipDeviceMallocContiguous): the scattered row/tile writes of the decode

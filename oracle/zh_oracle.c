@@ -234,9 +234,28 @@ static int inner_decode(const zh_array_meta* m, const int32_t* chunk_shape, cons
   int n = m->ndim, ds = m->dtype_size;
   int64_t nel = 1;
   for (int d = 0; d < n; d++) nel *= chunk_shape[d];
+  if (ch->inner_crc32c) { /* Crc32cCodec.decode (Crc32cCodec.java:24-48), last BB codec */
+    if (nbytes < 4) {
+      set_err(err, errlen, "unexpected inner chunk byte length: %lld (expected %lld)",
+              (long long)nbytes, (long long)(nel * ds + 4));
+      return ZH_EDATA;
+    }
+    nbytes -= 4;
+    int32_t computed = (int32_t)zo_crc32c(0, bytes, nbytes);
+    const uint8_t* s = bytes + nbytes;
+    int32_t stored = (int32_t)((uint32_t)s[0] | ((uint32_t)s[1] << 8) | ((uint32_t)s[2] << 16) |
+                               ((uint32_t)s[3] << 24));
+    if (computed != stored) {
+      set_err(err, errlen,
+              "The checksum of the sharding index is invalid. Stored: %d Computed: %d", stored,
+              computed);
+      return ZH_EDATA;
+    }
+  }
   if (nbytes != nel * ds) { /* Q12, see header */
     set_err(err, errlen, "unexpected inner chunk byte length: %lld (expected %lld)",
-            (long long)nbytes, (long long)(nel * ds));
+            (long long)(nbytes + (ch->inner_crc32c ? 4 : 0)),
+            (long long)(nel * ds + (ch->inner_crc32c ? 4 : 0)));
     return ZH_EDATA;
   }
   uint8_t* b = (uint8_t*)malloc(nel * ds > 0 ? nel * ds : 1);
@@ -617,6 +636,10 @@ static void inner_encode(const zh_array_meta* m, const nd_t* src, const int64_t*
       idx[d] = 0;
     }
   }
+  if (m->chain.inner_crc32c) { /* Crc32cCodec.encode (Crc32cCodec.java:50-60) */
+    uint32_t c = zo_crc32c(0, dst, (size_t)(total * ds));
+    for (int i = 0; i < 4; i++) dst[total * ds + i] = (uint8_t)(c >> (8 * i));
+  }
 }
 
 /* ShardingIndexedCodec.encode — ShardingIndexedCodec.java:105-168, C-order layout (Q7) */
@@ -650,7 +673,7 @@ static int sharding_encode(const zh_array_meta* m, const nd_t* chunk, uint8_t** 
       lens[k] = 0;
     } else {
       offs[k] = payload;                                              /* :137-143 */
-      lens[k] = inner_nel * ds;
+      lens[k] = inner_nel * ds + (m->chain.inner_crc32c ? 4 : 0);
       if (m->chain.nested) {  /* codecPipeline.encode(chunkArray) = level-2 sharding encode */
         zh_array_meta m2;
         nested_meta(m, &m2);
@@ -767,10 +790,11 @@ int zo_array_write(const zh_array_meta* m, const void* src_v, const int64_t* off
       out_bufs[i] = b;
       out_sizes[i] = nb;
     } else {
-      uint8_t* b = (uint8_t*)malloc(cnel * ds);
+      const int64_t extra = m->chain.inner_crc32c ? 4 : 0;
+      uint8_t* b = (uint8_t*)malloc(cnel * ds + extra);
       inner_encode(m, &ch, zero, m->chunk_shape, b);
       out_bufs[i] = b;
-      out_sizes[i] = cnel * ds;
+      out_sizes[i] = cnel * ds + extra;
     }
   }
   free(cbuf);

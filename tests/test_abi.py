@@ -28,9 +28,16 @@ def test_header_symbols_exported():
     assert sorted(declared_symbols()) == syms
 
 
+def test_struct_layout_matches_compiler():
+    out = (C.c_int64 * 4)()
+    assert lib().zh_abi_sizes(out, 4) == 4
+    assert list(out) == [C.sizeof(A.zh_codec_chain), C.sizeof(A.zh_array_meta),
+                         C.sizeof(A.zh_chunk_src), C.sizeof(A.zh_chunk_dst)]
+
+
 def test_struct_layout():
-    assert C.sizeof(A.zh_codec_chain) == 4 * (1 + 8 + 1 + 8 + 4 + 1 + 8 + 3)
-    assert C.sizeof(A.zh_array_meta) == 16 + 64 + 32 + 8 + C.sizeof(A.zh_codec_chain)
+    assert C.sizeof(A.zh_codec_chain) == 4 * (1 + 8 + 1 + 8 + 4 + 1 + 8 + 3 + 1)
+    assert C.sizeof(A.zh_array_meta) == (16 + 64 + 32 + 8 + C.sizeof(A.zh_codec_chain) + 7) // 8 * 8
     assert C.sizeof(A.zh_chunk_src) == 16 and C.sizeof(A.zh_chunk_dst) == 24
 
 

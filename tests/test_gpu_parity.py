@@ -207,3 +207,58 @@ def test_single_full_chunk_and_partial_decode_api(dev):
                                         i32arr([5, 7]), out2, 0, None, err, 512) == 0
     np.testing.assert_array_equal(np.frombuffer(bytes(out2), np.uint32).reshape(5, 7),
                                   arr[3:8, 20:27])
+
+
+@pytest.mark.parametrize("mode", ["unsharded", "sharded", "sharded_transpose", "nested"])
+@pytest.mark.parametrize("dsize", [1, 4, 8])
+def test_chunk_crc32c_decode_encode(dev, mode, dsize):
+    """[transpose?, bytes, crc32c] chunk codecs on the device (data-CRC pass after resolve,
+    CRC store pass after encode) vs the oracle: decoded values, encoded bytes, and regions."""
+    shape = [24, 40, 36]
+    kw = dict(endian=A.ZH_ENDIAN_BIG, inner_crc32c=True)
+    if mode != "unsharded":
+        kw.update(sharded=True, inner_chunk_shape=[8, 8, 12])
+    if mode == "sharded_transpose":
+        kw.update(transpose_order=[2, 0, 1])
+    if mode == "nested":
+        kw.update(nested_chunk_shape=[4, 8, 6])
+    meta = A.make_meta(shape, [16, 16, 24], dsize, **kw)
+    arr = rand_array(shape, dsize, seed=23)
+    arr[0:8, 0:8, 0:12] = 0
+    want = encode_oracle(meta, arr)
+    got = device_write(dev, meta, arr)
+    assert got == want
+    roundtrip(dev, meta, arr, [([0, 0, 0], shape), ([3, 5, 7], [17, 30, 20]), ([20, 1, 30], [4, 9, 6])])
+
+
+@pytest.mark.parametrize("sharded", [False, True])
+def test_chunk_crc32c_mismatch_message(dev, sharded):
+    shape = [16, 16]
+    meta = A.make_meta(shape, [16, 16], 4, sharded=sharded,
+                       inner_chunk_shape=[8, 8] if sharded else None, inner_crc32c=True)
+    arr = rand_array(shape, 4, seed=2)
+    b = bytearray(encode_oracle(meta, arr)[0])
+    b[100] ^= 0x08
+    with pytest.raises(O.OracleError) as eo:
+        O.array_read(meta, [bytes(b)], [0, 0], shape)
+    with pytest.raises(ZhError) as ed:
+        device_read(dev, meta, [bytes(b)], [0, 0], shape)
+    assert str(ed.value) == str(eo.value)
+
+
+def test_chunk_crc32c_missing_and_clipped(dev):
+    """Missing shards/inner chunks under a clipped region carry no source: the data-CRC pass
+    must skip them (Q1 zeros, fill for a missing shard)."""
+    shape = [20, 20]
+    meta = A.make_meta(shape, [16, 16], 4, sharded=True, inner_chunk_shape=[8, 8],
+                       inner_crc32c=True, fill=(9).to_bytes(4, "little"))
+    arr = rand_array(shape, 4, seed=4)
+    arr[0:8, 8:16] = 9            # an elided inner chunk
+    shards = encode_oracle(meta, arr)
+    shards[1] = None              # a missing shard
+    off, shp = [3, 3], [15, 16]
+    sel = chunk_coords(meta, off, shp)
+    pos = {c: i for i, c in enumerate(chunk_coords(meta, [0, 0], shape))}
+    srcs = [shards[pos[c]] for c in sel]
+    want = np.frombuffer(O.array_read(meta, srcs, off, shp), np.uint32).reshape(shp)
+    np.testing.assert_array_equal(device_read(dev, meta, srcs, off, shp), want)

@@ -190,6 +190,9 @@ struct zh_plan {
   uint32_t* d_slow = nullptr;   // [count, list...] of items for the generic kernel
   uint32_t* d_fast_tab = nullptr;
   uint8_t* d_flat = nullptr;    // nested sharding: flattened leaf indexes
+  uint32_t* d_dcrc = nullptr;   // inner crc32c: span partials per chunk
+  DataCrcArgs dcrc{};
+  int dcrc_grid = 0;
   NestArgs nest{};
   int nest_grid = 0;
   int tile_mode = 0;
@@ -408,6 +411,7 @@ void fill_common_args(const zh_array_meta* m, const int64_t* region_shape, bool 
     a.inner_div[d] = make_fastdiv(1);
   }
   a.inner_nbytes = nel * m->dtype_size;
+  a.crc_extra = c.inner_crc32c ? 4 : 0;
   a.dsize = m->dtype_size;
   uint64_t f = 0;
   for (int i = 0; i < 8; i++) f |= (uint64_t)m->fill_value[i] << (8 * i);
@@ -548,6 +552,7 @@ void plan_free(zh_plan* p) {
   (void)hipFree(p->d_slow);
   (void)hipFree(p->d_fast_tab);
   (void)hipFree(p->d_flat);
+  (void)hipFree(p->d_dcrc);
   for (auto& e : p->ev_pending)
     for (auto ev : e) p->ev_pool.push_back(ev);
   for (auto ev : p->ev_pool) (void)hipEventDestroy(ev);
@@ -658,10 +663,11 @@ int zh_plan_create(zh_ctx* ctx, const zh_array_meta* m, const zh_chunk_src* chun
           return ZH_EDATA;
         }
         S.index_off = c.index_location == ZH_INDEX_START ? 0 : S.nbytes - isz;
-      } else if (S.nbytes != p->args.inner_nbytes) {  // Q12 (knowing divergence)
+      } else if (S.nbytes != p->args.inner_nbytes + p->args.crc_extra) {  // Q12 (knowing divergence)
         set_err(err, errlen,
                 "unexpected inner chunk byte length: %lld (expected %lld) for chunk %s",
-                (long long)S.nbytes, (long long)p->args.inner_nbytes, fmt_ints(cc, n).c_str());
+                (long long)S.nbytes, (long long)(p->args.inner_nbytes + p->args.crc_extra),
+                fmt_ints(cc, n).c_str());
         plan_free(p);
         return ZH_EDATA;
       }
@@ -683,7 +689,7 @@ int zh_plan_create(zh_ctx* ctx, const zh_array_meta* m, const zh_chunk_src* chun
       // algorithmic input bytes: referenced inner chunks + the index for a
       // shard; only the in-bounds part of an unsharded chunk
       if (c.sharded) {
-        in_bytes += nit * p->args.inner_nbytes + isz;
+        in_bytes += nit * (p->args.inner_nbytes + p->args.crc_extra) + isz;
       } else {
         int64_t pb = m->dtype_size;
         for (int d = 0; d < n; d++) pb *= ps[d];
@@ -732,7 +738,7 @@ int zh_plan_create(zh_ctx* ctx, const zh_array_meta* m, const zh_chunk_src* chun
     N.sub_start = c.nested_index_location == ZH_INDEX_START;
     N.sub_isz = sub_isz;
     N.cps2 = cps2;
-    N.leaf_nbytes = p->args.inner_nbytes;
+    N.leaf_nbytes = p->args.inner_nbytes + p->args.crc_extra;
     int64_t s1 = 1, sf = 1;
     for (int d = n - 1; d >= 0; d--) {
       N.cps1_stride[d] = s1;
@@ -795,6 +801,22 @@ int zh_plan_create(zh_ctx* ctx, const zh_array_meta* m, const zh_chunk_src* chun
     plan_free(p);
     return ZH_EHIP;
   }
+  if (c.inner_crc32c && items > 0) {
+    const int64_t nspan = (p->args.inner_nbytes + kCrcSpan - 1) / kCrcSpan;
+    if ((st = dev_alloc(&p->d_dcrc, (size_t)(items * nspan), err, errlen)) != ZH_OK) {
+      plan_free(p);
+      return st;
+    }
+    DataCrcArgs& D = p->dcrc;
+    D.desc = p->d_desc;
+    D.n_items = items;
+    D.len = p->args.inner_nbytes;
+    D.nspan = (int32_t)nspan;
+    D.store = 0;
+    D.partials = p->d_dcrc;
+    D.status = p->d_status;
+    p->dcrc_grid = (int)std::min<int64_t>(items * nspan, (int64_t)ctx->cu_count * 32);
+  }
   p->args.desc = p->d_desc;
   p->args.fast_tab = p->d_fast_tab;
   p->args.n_citems = items;
@@ -846,6 +868,7 @@ int zh_plan_execute(zh_plan* p, void* out, void* stream_v) {
   ScatterArgs a = p->args;
   a.region = (p->flags & ZH_OUT_DEVICE) ? (uint8_t*)out : p->d_out;
   ZH_HIP(launch_resolve(a, s));
+  if (p->d_dcrc) ZH_HIP(launch_data_crc(p->dcrc, p->dcrc_grid, s));
   if (p->timing) ZH_HIP(hipEventRecord(ev[1], s));
   ZH_HIP(launch_scatter(a, p->meta.dtype_size, p->tile_mode, 0, p->grid, s));
   ZH_HIP(launch_decode_slow(a, p->slow_grid, s));
@@ -996,6 +1019,12 @@ int64_t zh_array_encoded_bound(const zh_array_meta* m) {
   int64_t nel = 1;
   for (int d = 0; d < m->ndim; d++) nel *= m->chunk_shape[d];
   int64_t bound = nel * m->dtype_size + (m->chain.sharded ? zh_shard_index_size(m) : 0);
+  if (m->chain.inner_crc32c) {  // + 4 per (inner/leaf) chunk
+    int64_t nch = 1;
+    const int32_t* leaf = leaf_shape(m);
+    for (int d = 0; d < m->ndim; d++) nch *= m->chunk_shape[d] / leaf[d];
+    bound += 4 * nch;
+  }
   if (m->chain.sharded && m->chain.nested) {  // + one sub-shard index per level-1 cell
     int64_t ncell = 1, cps2 = 1;
     for (int d = 0; d < m->ndim; d++) {
@@ -1187,9 +1216,9 @@ int zh_array_write(zh_ctx* ctx, const zh_array_meta* m, const void* src, const i
           const int64_t f = ks[(size_t)k2];
           if (leaf_any(f)) {
             hoff[b + f] = leaf_pos;
-            put_entry(&sidx[16 * k2], (uint64_t)(leaf_pos - sub_pos), (uint64_t)a.inner_nbytes,
-                      sub_be);
-            leaf_pos += a.inner_nbytes;
+            put_entry(&sidx[16 * k2], (uint64_t)(leaf_pos - sub_pos),
+                      (uint64_t)(a.inner_nbytes + a.crc_extra), sub_be);
+            leaf_pos += a.inner_nbytes + a.crc_extra;
             nonfill++;
           } else {
             put_entry(&sidx[16 * k2], ~0ull, ~0ull, sub_be);
@@ -1214,8 +1243,8 @@ int zh_array_write(zh_ctx* ctx, const zh_array_meta* m, const void* src, const i
       if (any) {
         hoff[b + k] = (start ? isz : 0) + payload;
         eo = (uint64_t)hoff[b + k];
-        en = (uint64_t)a.inner_nbytes;
-        payload += a.inner_nbytes;
+        en = (uint64_t)(a.inner_nbytes + a.crc_extra);
+        payload += a.inner_nbytes + a.crc_extra;
         nonfill++;
       }
       if (c.sharded) {
@@ -1258,6 +1287,46 @@ int zh_array_write(zh_ctx* ctx, const zh_array_meta* m, const void* src, const i
   a.item_off = d_off;
   a.flags = nullptr;
   ZH_HIPC(launch_scatter(a, m->dtype_size, tile_mode, 1, grid, s));
+  if (c.inner_crc32c) {  // Crc32cCodec.encode (:50-60) of every written payload, on the device
+    std::vector<ItemDesc> wd((size_t)items);
+    for (int64_t i = 0; i < ncoords; i++) {
+      const int64_t nit = c.sharded ? cps_total : 1;
+      for (int64_t k = 0; k < nit; k++) {
+        ItemDesc& D = wd[(size_t)(hs[i].item_begin + k)];
+        memset(&D, 0, sizeof(D));
+        D.kind = kDescSkip;
+        const int64_t o = hoff[(size_t)(hs[i].item_begin + k)];
+        if (o < 0 || dsts[i].nbytes == 0) continue;
+        D.kind = kDescFullCopy;
+        D.src = (uint64_t)(uintptr_t)((uint8_t*)dsts[i].data + o);
+        D.shard = (uint32_t)i;
+      }
+    }
+    const int64_t nspan = (a.inner_nbytes + kCrcSpan - 1) / kCrcSpan;
+    ItemDesc* d_wd = nullptr;
+    uint32_t* d_part = nullptr;
+    if ((st = dev_alloc(&d_wd, wd.size(), err, errlen)) != ZH_OK ||
+        (st = dev_alloc(&d_part, (size_t)(items * nspan), err, errlen)) != ZH_OK) {
+      (void)hipFree(d_wd);
+      cleanup();
+      return st;
+    }
+    DataCrcArgs D{};
+    D.desc = d_wd;
+    D.n_items = items;
+    D.len = a.inner_nbytes;
+    D.nspan = (int32_t)nspan;
+    D.store = 1;
+    D.partials = d_part;
+    hipError_t e1 = hipMemcpyAsync(d_wd, wd.data(), wd.size() * sizeof(ItemDesc),
+                                   hipMemcpyHostToDevice, s);
+    if (e1 == hipSuccess)
+      e1 = launch_data_crc(D, (int)std::min<int64_t>(items * nspan, (int64_t)ctx->cu_count * 32), s);
+    if (e1 == hipSuccess) e1 = hipStreamSynchronize(s);
+    (void)hipFree(d_wd);
+    (void)hipFree(d_part);
+    ZH_HIPC(e1);
+  }
   ZH_HIPC(hipStreamSynchronize(s));
   cleanup();
 #undef ZH_HIPC
@@ -1267,6 +1336,12 @@ int zh_array_write(zh_ctx* ctx, const zh_array_meta* m, const void* src, const i
 // =====================================================================================
 // plumbing
 // =====================================================================================
+int zh_abi_sizes(int64_t* out, int n) {
+  const int64_t s[4] = {(int64_t)sizeof(zh_codec_chain), (int64_t)sizeof(zh_array_meta),
+                        (int64_t)sizeof(zh_chunk_src), (int64_t)sizeof(zh_chunk_dst)};
+  for (int i = 0; i < n && i < 4 && out; i++) out[i] = s[i];
+  return 4;
+}
 int zh_device_malloc(zh_ctx* ctx, size_t bytes, void** out) {
   if (!ctx || !out) return ZH_EINVAL;
   (void)hipSetDevice(ctx->device);

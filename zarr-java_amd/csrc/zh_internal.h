@@ -118,6 +118,20 @@ struct ScatterArgs {
   int32_t tile;
   int32_t nt;                   // fast kernels: bit 0 non-temporal loads, bit 1 stores
   int32_t tile_variant;         // tile fast path: 0 row-per-tile loads, 1 row-interleaved groups
+  int32_t crc_extra;            // 4 when each stored chunk carries a trailing crc32c, else 0
+};
+
+// Chunk-payload CRC-32C pass (inner crc32c codec): one workgroup per (item, 64 KiB span) of
+// every resolved chunk, then one lane per item combines the spans and verifies the stored
+// value (decode) or writes it after the payload (encode, store = 1).
+struct DataCrcArgs {
+  const ItemDesc* desc;         // src = payload address; kinds other than copy/clip skipped
+  int64_t n_items;
+  int64_t len;                  // payload bytes per chunk
+  int32_t nspan;                // ceil(len / kCrcSpan)
+  int32_t store;
+  uint32_t* partials;           // n_items * nspan
+  uint64_t* status;             // decode: kStWords per shard
 };
 
 // Nested sharding pre-pass (nested_index_kernel): one workgroup per referenced level-1 cell
@@ -157,6 +171,7 @@ hipError_t launch_crc(const CrcJob* jobs, int64_t njobs, int64_t nspans, uint32_
                       uint64_t* status, hipStream_t stream);
 hipError_t launch_resolve(const ScatterArgs& a, hipStream_t stream);
 hipError_t launch_nested_index(const NestArgs& a, int grid, hipStream_t stream);
+hipError_t launch_data_crc(const DataCrcArgs& a, int grid, hipStream_t stream);
 hipError_t launch_scatter(const ScatterArgs& a, int dsize, int tile_mode, int encode, int grid,
                           hipStream_t stream);
 hipError_t launch_decode_slow(const ScatterArgs& a, int grid, hipStream_t stream);

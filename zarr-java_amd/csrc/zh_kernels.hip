@@ -249,7 +249,7 @@ __device__ __forceinline__ int64_t make_item(const ScatterArgs& a, int64_t item,
       } else {
         const uint64_t total = (uint64_t)S.nbytes;
         const bool range_ok = off <= total && nb <= total - off;
-        if (!range_ok || nb != (uint64_t)a.inner_nbytes) {
+        if (!range_ok || nb != (uint64_t)(a.inner_nbytes + a.crc_extra)) {
           if (threadIdx.x == 0 && it.piece == 0) {
             const uint32_t kind = range_ok ? kFlagLength : kFlagRange;
             const uint64_t key = ((uint64_t)(0xFFFFFFFFu - (uint32_t)lin) << 8) | kind;
@@ -621,7 +621,7 @@ __device__ __forceinline__ ItemDesc resolve_one(const ScatterArgs& a, int64_t ci
     }
     const uint64_t total = (uint64_t)S.nbytes;
     const bool range_ok = off <= total && nb <= total - off;
-    if (!range_ok || nb != (uint64_t)a.inner_nbytes) {
+    if (!range_ok || nb != (uint64_t)(a.inner_nbytes + a.crc_extra)) {
       const uint32_t kind = range_ok ? kFlagLength : kFlagRange;
       const uint64_t key = ((uint64_t)(0xFFFFFFFFu - (uint32_t)lin) << 8) | kind;
       atomicOr((unsigned long long*)(a.status + s * kStWords + kStFlags), (unsigned long long)kind);
@@ -1126,10 +1126,8 @@ __device__ __forceinline__ uint32_t crc_combine(uint32_t c1, uint32_t c2, uint64
   return multmodp(x2nmodp(len2, 3), c1) ^ c2;
 }
 
-__global__ __launch_bounds__(kBlock) void crc_partial_kernel(const CrcJob* jobs, int64_t njobs,
-                                                              uint32_t* partials) {
-  __shared__ uint32_t T[8][256];
-  __shared__ uint32_t red[kBlock];
+// slicing-by-8 tables of the reflected Castagnoli polynomial (CRC32C.java:14-80), per block
+__device__ __forceinline__ void init_crc_tables(uint32_t (*T)[256]) {
   const int tid = threadIdx.x;
   {
     uint32_t c = (uint32_t)tid;
@@ -1143,19 +1141,17 @@ __global__ __launch_bounds__(kBlock) void crc_partial_kernel(const CrcJob* jobs,
     T[k][tid] = (p >> 8) ^ T[0][p & 0xFFu];
     __syncthreads();
   }
-  const int64_t span = blockIdx.x;
-  int64_t lo = 0, hi = njobs - 1;
-  while (lo < hi) {
-    int64_t mid = (lo + hi + 1) >> 1;
-    if (jobs[mid].span_begin <= span) lo = mid;
-    else hi = mid - 1;
-  }
-  const CrcJob J = jobs[lo];
-  const int64_t sb = (span - J.span_begin) * kCrcSpan;
-  const int64_t slen = min((int64_t)kCrcSpan, J.len - sb);
+}
+
+// Standard CRC-32C of base[0, slen), slen <= kCrcSpan, by the whole workgroup: kCrcLane-byte
+// lane segments (slicing-by-8), combined pairwise in GF(2).  Uniform call; every lane
+// returns the result.
+__device__ uint32_t span_crc8(const uint8_t* base, int64_t slen, const uint32_t (*T)[256],
+                              uint32_t* red) {
+  const int tid = threadIdx.x;
   const int64_t lb = (int64_t)tid * kCrcLane;
   const int64_t llen = max((int64_t)0, min((int64_t)kCrcLane, slen - lb));
-  const uint8_t* p = J.base + sb + lb;
+  const uint8_t* p = base + lb;
   uint32_t c = 0xFFFFFFFFu;
   int64_t i = 0;
   if ((((uintptr_t)p) & 7) == 0) {
@@ -1180,7 +1176,80 @@ __global__ __launch_bounds__(kBlock) void crc_partial_kernel(const CrcJob* jobs,
     }
     __syncthreads();
   }
-  if (tid == 0) partials[span] = red[0];
+  const uint32_t r = red[0];
+  __syncthreads();
+  return r;
+}
+
+__global__ __launch_bounds__(kBlock) void crc_partial_kernel(const CrcJob* jobs, int64_t njobs,
+                                                              uint32_t* partials) {
+  __shared__ uint32_t T[8][256];
+  __shared__ uint32_t red[kBlock];
+  init_crc_tables(T);
+  const int64_t span = blockIdx.x;
+  int64_t lo = 0, hi = njobs - 1;
+  while (lo < hi) {
+    int64_t mid = (lo + hi + 1) >> 1;
+    if (jobs[mid].span_begin <= span) lo = mid;
+    else hi = mid - 1;
+  }
+  const CrcJob J = jobs[lo];
+  const int64_t sb = (span - J.span_begin) * kCrcSpan;
+  const int64_t slen = min((int64_t)kCrcSpan, J.len - sb);
+  const uint32_t c = span_crc8(J.base + sb, slen, T, red);
+  if (threadIdx.x == 0) partials[span] = c;
+}
+
+// inner crc32c codec: partial CRCs of every resolved chunk payload
+__global__ __launch_bounds__(kBlock) void data_crc_partial_kernel(DataCrcArgs a) {
+  __shared__ uint32_t T[8][256];
+  __shared__ uint32_t red[kBlock];
+  init_crc_tables(T);
+  const int64_t total = a.n_items * a.nspan;
+  for (int64_t b = blockIdx.x; b < total; b += gridDim.x) {
+    const int64_t item = b / a.nspan;
+    const int64_t span = b - item * a.nspan;
+    const ItemDesc D = ld_desc(a.desc + item);
+    const uint32_t mode = D.kind & kDescModeMask;
+    // missing shards / inner chunks are clip or fill descriptors without a source
+    if ((mode != kDescFullCopy && mode != kDescClip) || D.src == 0) continue;  // uniform
+    const int64_t sb = span * kCrcSpan;
+    const uint32_t c = span_crc8((const uint8_t*)(uintptr_t)D.src + sb,
+                                 min((int64_t)kCrcSpan, a.len - sb), T, red);
+    if (threadIdx.x == 0) a.partials[b] = c;
+  }
+}
+
+// combine the spans; decode: compare with the stored little-endian value (mismatch →
+// Crc32cCodec.java:39-44 via the shard's status); encode: write it after the payload
+__global__ void data_crc_finalize_kernel(DataCrcArgs a) {
+  const int64_t item = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (item >= a.n_items) return;
+  const ItemDesc D = a.desc[item];
+  const uint32_t mode = D.kind & kDescModeMask;
+  if ((mode != kDescFullCopy && mode != kDescClip) || D.src == 0) return;
+  uint32_t c = 0;
+  for (int64_t k = 0; k < a.nspan; k++) {
+    const int64_t slen = min((int64_t)kCrcSpan, a.len - k * kCrcSpan);
+    c = crc_combine(c, a.partials[item * a.nspan + k], (uint64_t)slen);
+  }
+  uint8_t* s = (uint8_t*)(uintptr_t)D.src + a.len;
+  if (a.store) {
+    s[0] = (uint8_t)c;
+    s[1] = (uint8_t)(c >> 8);
+    s[2] = (uint8_t)(c >> 16);
+    s[3] = (uint8_t)(c >> 24);
+    return;
+  }
+  const uint32_t stored =
+      (uint32_t)s[0] | ((uint32_t)s[1] << 8) | ((uint32_t)s[2] << 16) | ((uint32_t)s[3] << 24);
+  if (c != stored) {
+    uint64_t* st = a.status + (int64_t)D.shard * kStWords;
+    if (atomicCAS((unsigned long long*)(st + kStCrcStored), 0ull,
+                  (unsigned long long)((1ull << 32) | stored)) == 0ull)
+      st[kStCrcComputed] = c;
+    atomicOr((unsigned long long*)(st + kStFlags), (unsigned long long)kFlagCrc);
+  }
 }
 
 __global__ void crc_finalize_kernel(const CrcJob* jobs, int64_t njobs, const uint32_t* partials,
@@ -1419,6 +1488,14 @@ __global__ __launch_bounds__(kBlock) void synth_verify_kernel(VerifyArgs a) {
 hipError_t launch_nested_index(const NestArgs& a, int grid, hipStream_t stream) {
   if (a.n_l1 <= 0) return hipSuccess;
   hipLaunchKernelGGL(nested_index_kernel, dim3((unsigned)grid), dim3(kBlock), 0, stream, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_data_crc(const DataCrcArgs& a, int grid, hipStream_t stream) {
+  if (a.n_items <= 0) return hipSuccess;
+  hipLaunchKernelGGL(data_crc_partial_kernel, dim3((unsigned)grid), dim3(kBlock), 0, stream, a);
+  hipLaunchKernelGGL(data_crc_finalize_kernel, dim3((unsigned)((a.n_items + 255) / 256)),
+                     dim3(256), 0, stream, a);
   return hipGetLastError();
 }
 

@@ -37,6 +37,7 @@ class zh_codec_chain(C.Structure):
         ("nested_index_endian", C.c_int32),
         ("nested_index_has_crc32c", C.c_int32),
         ("nested_index_location", C.c_int32),
+        ("inner_crc32c", C.c_int32),
     ]
 
 
@@ -65,7 +66,8 @@ def make_meta(shape, chunk_shape, dtype_size, *, fill=b"\0" * 8, is_bool=False, 
               inner_chunk_shape=None, transpose_order=None, endian=ZH_ENDIAN_LITTLE,
               index_endian=ZH_ENDIAN_LITTLE, index_crc32c=True, index_location=ZH_INDEX_END,
               nested_chunk_shape=None, nested_index_endian=ZH_ENDIAN_LITTLE,
-              nested_index_crc32c=True, nested_index_location=ZH_INDEX_END):
+              nested_index_crc32c=True, nested_index_location=ZH_INDEX_END,
+              inner_crc32c=False):
     """Build a zh_array_meta from Python values.  `fill` is the element's bytes (LE)."""
     m = zh_array_meta()
     n = len(shape)
@@ -91,6 +93,7 @@ def make_meta(shape, chunk_shape, dtype_size, *, fill=b"\0" * 8, is_bool=False, 
     ch.index_endian = index_endian
     ch.index_has_crc32c = 1 if index_crc32c else 0
     ch.index_location = index_location
+    ch.inner_crc32c = 1 if inner_crc32c else 0
     if nested_chunk_shape is not None:
         ch.nested = 1
         for d in range(n):

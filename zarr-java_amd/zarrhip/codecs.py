@@ -348,6 +348,14 @@ def _split_inner(codecs, ndim, dsize):
     return order, ab.byte_order(dsize), bb
 
 
+def _take_crc(bb):
+    """A trailing-only [crc32c] byte-to-byte chain runs on the device (zh_codec_chain
+    .inner_crc32c); anything else stays a host byte-to-byte stage."""
+    if len(bb) == 1 and isinstance(bb[0], Crc32cCodec):
+        return [], True
+    return bb, False
+
+
 def _index_chain(sh):
     ic = sh.index_codecs
     if not ic or not isinstance(ic[0], BytesCodec) or \
@@ -376,12 +384,14 @@ def device_chain(codecs, ndim, dsize):
                 raise UnsupportedChainError("nested sharding must be the only inner codec")
             nested = inner_ab
             order, endian, inner_bb = _split_inner(nested.codecs, ndim, dsize)
+            inner_bb, crc = _take_crc(inner_bb)
             if inner_bb:
                 raise UnsupportedChainError("nested sharding with byte-to-byte leaf codecs")
         else:
             order, endian, inner_bb = _split_inner(ab.codecs, ndim, dsize)
+            inner_bb, crc = _take_crc(inner_bb)
         chain = dict(sharded=True, inner_chunk_shape=ab.chunk_shape, transpose_order=order,
-                     endian=endian, index_endian=ic[0].byte_order(8),
+                     endian=endian, inner_crc32c=crc, index_endian=ic[0].byte_order(8),
                      index_crc32c=len(ic) == 2,
                      index_location=A.ZH_INDEX_START if ab.index_location == "start"
                      else A.ZH_INDEX_END)
@@ -394,7 +404,8 @@ def device_chain(codecs, ndim, dsize):
                          if nested.index_location == "start" else A.ZH_INDEX_END)
         return DeviceChain(chain, [], inner_bb, ic)
     order, endian, bb = _split_inner(codecs, ndim, dsize)
-    chain = dict(sharded=False, transpose_order=order, endian=endian)
+    bb, crc = _take_crc(bb)
+    chain = dict(sharded=False, transpose_order=order, endian=endian, inner_crc32c=crc)
     return DeviceChain(chain, bb, [])
 
 

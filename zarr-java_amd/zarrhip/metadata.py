@@ -161,7 +161,8 @@ class ArrayMetadata:
                            nested_chunk_shape=ch.get("nested_chunk_shape"),
                            nested_index_endian=ch.get("nested_index_endian", A.ZH_ENDIAN_LITTLE),
                            nested_index_crc32c=ch.get("nested_index_crc32c", True),
-                           nested_index_location=ch.get("nested_index_location", A.ZH_INDEX_END))
+                           nested_index_location=ch.get("nested_index_location", A.ZH_INDEX_END),
+                           inner_crc32c=ch.get("inner_crc32c", False))
 
 
 def calculate_default_chunks(shape):
