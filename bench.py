@@ -32,10 +32,16 @@ GiB = 1 << 30
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 
 CONFIGS = {
-    # name: (description, sharded, transpose order)
+    # name: (description, sharded, transpose order[, extra make_meta keywords])
     "c2": ("bytes(big) only, chunk 1x1024x1024x1024", False, None),
     "c3": ("sharding 1x32x32x32 + bytes(big), index [bytes(little), crc32c] at end", True, None),
     "c4": ("c3 + transpose [0,3,2,1] inside the shard", True, [0, 3, 2, 1]),
+    # §8(f) rank-2 workloads (not the headline): same array and shards
+    "c3crc": ("c3 with inner codecs [bytes(big), crc32c] (per-chunk checksum verified)", True,
+              None, dict(inner_crc32c=True)),
+    "c3nest": ("nested sharding: shard 1x1024^3 -> 1x256x256x256 sub-shards -> 1x32x32x32 "
+               "leaves, bytes(big); both indexes [bytes(little), crc32c] at end", True, None,
+               dict(nested=True)),
 }
 
 
@@ -81,10 +87,15 @@ class Dist:
 
 
 def build_meta(A, cfg, ydiv=1):
-    _, sharded, order = CONFIGS[cfg]
+    _, sharded, order = CONFIGS[cfg][:3]
+    extra = dict(CONFIGS[cfg][3]) if len(CONFIGS[cfg]) > 3 else {}
+    inner = [1, 32, 32, 32]
+    if extra.pop("nested", False):
+        inner = [1, 256, 256, 256]
+        extra["nested_chunk_shape"] = [1, 32, 32, 32]
     return A.make_meta([1, 4096 // ydiv, 4096, 1536], [1, 1024, 1024, 1024], 4,
-                       endian=A.ZH_ENDIAN_BIG, sharded=sharded,
-                       inner_chunk_shape=[1, 32, 32, 32] if sharded else None,
+                       endian=A.ZH_ENDIAN_BIG, sharded=sharded, **extra,
+                       inner_chunk_shape=inner if sharded else None,
                        transpose_order=order, index_endian=A.ZH_ENDIAN_LITTLE,
                        index_crc32c=True, index_location=A.ZH_INDEX_END)
 
@@ -93,25 +104,31 @@ def chunk_capacities(meta, coords):
     """Exact encoded sizes for synthetic data (every in-bounds inner chunk is non-fill;
     inner chunks wholly in the boundary padding are elided as all-fill)."""
     n = meta.ndim
-    sharded = meta.chain.sharded
-    inner = [meta.chain.inner_chunk_shape[d] if sharded else meta.chunk_shape[d] for d in range(n)]
-    inner_bytes = 4
-    for d in range(n):
-        inner_bytes *= inner[d]
-    isz = 0
+    ch = meta.chain
+    sharded = ch.sharded
+    l1 = [ch.inner_chunk_shape[d] if sharded else meta.chunk_shape[d] for d in range(n)]
+    leaf = [ch.nested_chunk_shape[d] for d in range(n)] if ch.nested else l1
+    def prod(v):
+        r = 1
+        for x in v:
+            r *= x
+        return r
+
+    leaf_bytes = 4 * prod(leaf) + (4 if ch.inner_crc32c else 0)
+    isz = sub_isz = 0
     if sharded:
-        ncps = 1
-        for d in range(n):
-            ncps *= meta.chunk_shape[d] // inner[d]
-        isz = 16 * ncps + 4
+        isz = 16 * prod([meta.chunk_shape[d] // l1[d] for d in range(n)]) + 4
+    if ch.nested:
+        sub_isz = 16 * prod([l1[d] // leaf[d] for d in range(n)]) + 4
     caps = []
     for c in coords:
-        valid = 1
+        valid = cells = 1
         for d in range(n):
             lo = c[d] * meta.chunk_shape[d]
             hi = min(lo + meta.chunk_shape[d], meta.shape[d])
-            valid *= -(-(hi - lo) // inner[d])
-        caps.append(valid * inner_bytes + isz)
+            valid *= -(-(hi - lo) // leaf[d])
+            cells *= -(-(hi - lo) // l1[d])
+        caps.append(valid * leaf_bytes + isz + (cells * sub_isz if ch.nested else 0))
     return caps
 
 

@@ -420,7 +420,9 @@ __device__ __forceinline__ bool vec_ok(const ScatterArgs& a, const Item& it, int
                                        const int32_t* ext, bool need_src) {
   const int n = a.ndim;
   bool ok = !(((uintptr_t)(it.dbase + it.d0 * DS)) & 15);
-  if (need_src) ok &= !(((uintptr_t)(it.sbase + it.s0 * DS)) & 15);
+  // sources need dword alignment only: a chunk after a 4-byte crc32c or a sub-shard index
+  // sits at 4 mod 16, and dwordx4 loads from dword-aligned addresses are legal on gfx950
+  if (need_src) ok &= !(((uintptr_t)(it.sbase + it.s0 * DS)) & 3);
 #pragma unroll
   for (int d = 0; d < kMaxDims; d++) {
     if (d >= n) continue;
@@ -452,7 +454,7 @@ __device__ __forceinline__ void tile_pass(const ScatterArgs& a, const Item& it,
   int32_t efs = 1, efd = 1, vfs = 1, vfd = 1;
   int64_t ss_fs = 1, ss_fd = 1, ds_fs = 1, ds_fd = 1;
   uint32_t nb = 1;
-  bool vec = DS == 4 && !(((uintptr_t)(it.sbase + it.s0 * DS)) & 15) &&
+  bool vec = DS == 4 && !(((uintptr_t)(it.sbase + it.s0 * DS)) & 3) &&
              !(((uintptr_t)(it.dbase + it.d0 * DS)) & 15);
 #pragma unroll
   for (int d = 0; d < kMaxDims; d++) {
@@ -643,7 +645,7 @@ __device__ __forceinline__ bool is_fast(const ScatterArgs& a, const ItemDesc& D)
   const uint32_t mode = D.kind & kDescModeMask;
   if (a.fast_mode == kFastNone || (mode != kDescFullCopy && mode != kDescFullFill)) return false;
   if ((((uintptr_t)a.region) + (uint64_t)D.d0 * a.dsize) & 15) return false;
-  if (mode == kDescFullCopy && (D.src & 15)) return false;
+  if (mode == kDescFullCopy && (D.src & 3)) return false;  // dword-aligned sources suffice
   if (a.tile && (a.dsize != 4 || mode != kDescFullCopy)) return false;
   return true;
 }
@@ -1200,39 +1202,107 @@ __global__ __launch_bounds__(kBlock) void crc_partial_kernel(const CrcJob* jobs,
   if (threadIdx.x == 0) partials[span] = c;
 }
 
-// inner crc32c codec: partial CRCs of every resolved chunk payload
+// inner crc32c codec: CRC-32C of every resolved chunk payload, coalesced.  A workgroup
+// takes one 64 KiB span of one chunk; lane l reads the 16-byte vectors l, l+256, ... (each
+// wave load is 1 KiB contiguous) and keeps the raw register of its vectors as if the other
+// lanes' bytes were zeros: acc = upd16(shift_4080(acc), v), with the constant zero-shift by
+// four table lookups.  Each lane then shifts acc to the span end and the lanes XOR together
+// (CRC linearity over GF(2)); the partial is the raw (init 0, no xorout) span register.
+__device__ __forceinline__ uint32_t crc_upd16(uint32_t c, v4u v, const uint32_t (*T)[256]) {
+  uint32_t lo = v.x ^ c, hi = v.y;
+  c = T[7][lo & 0xFFu] ^ T[6][(lo >> 8) & 0xFFu] ^ T[5][(lo >> 16) & 0xFFu] ^ T[4][lo >> 24] ^
+      T[3][hi & 0xFFu] ^ T[2][(hi >> 8) & 0xFFu] ^ T[1][(hi >> 16) & 0xFFu] ^ T[0][hi >> 24];
+  lo = v.z ^ c;
+  hi = v.w;
+  return T[7][lo & 0xFFu] ^ T[6][(lo >> 8) & 0xFFu] ^ T[5][(lo >> 16) & 0xFFu] ^ T[4][lo >> 24] ^
+         T[3][hi & 0xFFu] ^ T[2][(hi >> 8) & 0xFFu] ^ T[1][(hi >> 16) & 0xFFu] ^ T[0][hi >> 24];
+}
+
+__device__ __forceinline__ uint32_t crc_shift_tab(uint32_t c, const uint32_t (*S)[256]) {
+  return S[0][c & 0xFFu] ^ S[1][(c >> 8) & 0xFFu] ^ S[2][(c >> 16) & 0xFFu] ^ S[3][c >> 24];
+}
+
+constexpr int kDcBatch = 8;  // vectors in flight per lane
+
 __global__ __launch_bounds__(kBlock) void data_crc_partial_kernel(DataCrcArgs a) {
   __shared__ uint32_t T[8][256];
-  __shared__ uint32_t red[kBlock];
+  __shared__ uint32_t S[4][256];
+  __shared__ uint32_t wred[kBlock / 64];
   init_crc_tables(T);
+  const int tid = threadIdx.x;
+  {
+    const uint32_t k4080 = x2nmodp(4080, 3);  // x^(8*4080): the other lanes' 255 vectors
+#pragma unroll
+    for (int b = 0; b < 4; b++) S[b][tid] = multmodp(k4080, (uint32_t)tid << (8 * b));
+  }
+  // full span: this lane's last vector ends 4080 - 16*tid bytes before the span end
+  const uint32_t kfull = x2nmodp((uint64_t)(4080 - 16 * tid), 3);
+  __syncthreads();
   const int64_t total = a.n_items * a.nspan;
-  for (int64_t b = blockIdx.x; b < total; b += gridDim.x) {
-    const int64_t item = b / a.nspan;
-    const int64_t span = b - item * a.nspan;
+  for (int64_t blk = blockIdx.x; blk < total; blk += gridDim.x) {
+    const int64_t item = blk / a.nspan;
+    const int64_t span = blk - item * a.nspan;
     const ItemDesc D = ld_desc(a.desc + item);
     const uint32_t mode = D.kind & kDescModeMask;
     // missing shards / inner chunks are clip or fill descriptors without a source
     if ((mode != kDescFullCopy && mode != kDescClip) || D.src == 0) continue;  // uniform
-    const int64_t sb = span * kCrcSpan;
-    const uint32_t c = span_crc8((const uint8_t*)(uintptr_t)D.src + sb,
-                                 min((int64_t)kCrcSpan, a.len - sb), T, red);
-    if (threadIdx.x == 0) a.partials[b] = c;
+    const uint8_t* base = (const uint8_t*)(uintptr_t)D.src + span * kCrcSpan;
+    const int64_t slen = min((int64_t)kCrcSpan, a.len - span * kCrcSpan);
+    const int nblk = (int)(slen >> 4);
+    uint32_t acc = 0;
+    int nb = 0;
+    for (int j0 = 0; j0 < nblk; j0 += kBlock * kDcBatch) {
+      v4u v[kDcBatch];
+#pragma unroll
+      for (int u = 0; u < kDcBatch; u++) {
+        const int j = j0 + tid + u * kBlock;
+        if (j < nblk) v[u] = __builtin_nontemporal_load(reinterpret_cast<const v4u*>(base + 16 * (int64_t)j));
+      }
+#pragma unroll
+      for (int u = 0; u < kDcBatch; u++) {
+        if (j0 + tid + u * kBlock < nblk) {
+          acc = crc_upd16(crc_shift_tab(acc, S), v[u], T);
+          nb++;
+        }
+      }
+    }
+    uint32_t contrib = 0;
+    if (nb > 0) {
+      const int64_t e = 16 * (int64_t)(tid + kBlock * (nb - 1)) + 16;
+      const uint32_t k = slen == kCrcSpan ? kfull : x2nmodp((uint64_t)(slen - e), 3);
+      contrib = multmodp(k, acc);
+    }
+    if (tid == 0) {  // tail bytes (payload length not a multiple of 16) end the span
+      uint32_t t = 0;
+      for (int64_t i = (int64_t)nblk * 16; i < slen; i++) t = T[0][(t ^ base[i]) & 0xFFu] ^ (t >> 8);
+      contrib ^= t;
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) contrib ^= (uint32_t)__shfl_xor((int)contrib, o, 64);
+    if ((tid & 63) == 0) wred[tid >> 6] = contrib;
+    __syncthreads();
+    if (tid == 0) a.partials[blk] = wred[0] ^ wred[1] ^ wred[2] ^ wred[3];
+    __syncthreads();
   }
 }
 
-// combine the spans; decode: compare with the stored little-endian value (mismatch →
-// Crc32cCodec.java:39-44 via the shard's status); encode: write it after the payload
+// combine the raw span registers into the standard CRC; decode: compare with the stored
+// little-endian value (mismatch → Crc32cCodec.java:39-44 via the shard's status); encode:
+// write it after the payload (Crc32cCodec.java:50-60)
 __global__ void data_crc_finalize_kernel(DataCrcArgs a) {
   const int64_t item = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (item >= a.n_items) return;
   const ItemDesc D = a.desc[item];
   const uint32_t mode = D.kind & kDescModeMask;
   if ((mode != kDescFullCopy && mode != kDescClip) || D.src == 0) return;
-  uint32_t c = 0;
+  uint32_t raw = 0;
+  const uint32_t kspan = x2nmodp((uint64_t)kCrcSpan, 3);
   for (int64_t k = 0; k < a.nspan; k++) {
     const int64_t slen = min((int64_t)kCrcSpan, a.len - k * kCrcSpan);
-    c = crc_combine(c, a.partials[item * a.nspan + k], (uint64_t)slen);
+    raw = multmodp(slen == kCrcSpan ? kspan : x2nmodp((uint64_t)slen, 3), raw) ^
+          a.partials[item * a.nspan + k];
   }
+  const uint32_t c = multmodp(x2nmodp((uint64_t)a.len, 3), 0xFFFFFFFFu) ^ raw ^ 0xFFFFFFFFu;
   uint8_t* s = (uint8_t*)(uintptr_t)D.src + a.len;
   if (a.store) {
     s[0] = (uint8_t)c;
