@@ -46,13 +46,16 @@ JNIEXPORT void JNICALL Java_dev_zarr_zarrjava_hip_ZarrHip_ctxDestroy(JNIEnv* env
 }
 
 /* meta: int[] {ndim, dtypeSize, isBool, sharded, hasTranspose, endian, indexEndian,
- *              indexCrc32c, indexLocation}; shape long[ndim]; chunkShape/innerShape/order
- *              int[ndim]; fill byte[dtypeSize] (little-endian element bytes). */
+ *              indexCrc32c, indexLocation[, nested, nestedIndexEndian, nestedIndexCrc32c,
+ *              nestedIndexLocation, innerCrc32c]}; shape long[ndim]; chunkShape/order int[ndim];
+ *              innerShape int[ndim] (nested: int[2*ndim], inner then leaf shape);
+ *              fill byte[dtypeSize] (little-endian element bytes). */
 static int build_meta(JNIEnv* env, jintArray jm, jlongArray jshape, jintArray jchunk,
                       jintArray jinner, jintArray jorder, jbyteArray jfill, zh_array_meta* m) {
   memset(m, 0, sizeof(*m));
-  jint mi[9];
-  (*env)->GetIntArrayRegion(env, jm, 0, 9, mi);
+  jint mi[14] = {0};
+  jsize nm = (*env)->GetArrayLength(env, jm);
+  (*env)->GetIntArrayRegion(env, jm, 0, nm < 14 ? nm : 14, mi);
   m->ndim = mi[0];
   if (m->ndim <= 0 || m->ndim > ZH_MAX_DIMS) return ZH_EUNSUPPORTED;
   m->dtype_size = mi[1];
@@ -63,6 +66,11 @@ static int build_meta(JNIEnv* env, jintArray jm, jlongArray jshape, jintArray jc
   m->chain.index_endian = mi[6];
   m->chain.index_has_crc32c = mi[7];
   m->chain.index_location = mi[8];
+  m->chain.nested = mi[9];
+  m->chain.nested_index_endian = mi[10];
+  m->chain.nested_index_has_crc32c = mi[11];
+  m->chain.nested_index_location = mi[12];
+  m->chain.inner_crc32c = mi[13];
   jlong sh[ZH_MAX_DIMS];
   jint ch[ZH_MAX_DIMS];
   (*env)->GetLongArrayRegion(env, jshape, 0, m->ndim, sh);
@@ -72,6 +80,8 @@ static int build_meta(JNIEnv* env, jintArray jm, jlongArray jshape, jintArray jc
     m->chunk_shape[d] = ch[d];
   }
   if (m->chain.sharded) (*env)->GetIntArrayRegion(env, jinner, 0, m->ndim, m->chain.inner_chunk_shape);
+  if (m->chain.sharded && m->chain.nested)
+    (*env)->GetIntArrayRegion(env, jinner, m->ndim, m->ndim, m->chain.nested_chunk_shape);
   if (m->chain.has_transpose) (*env)->GetIntArrayRegion(env, jorder, 0, m->ndim, m->chain.transpose_order);
   if (jfill) {
     jsize n = (*env)->GetArrayLength(env, jfill);

@@ -15,8 +15,11 @@ import java.nio.ByteOrder;
  * zh_array_meta fields the JNI shim expects.  Anything else → null (use the reference).
  */
 final class DeviceChain {
-    final int[] meta = new int[9];  // ndim, dtypeSize, isBool, sharded, hasTranspose, endian,
-                                    // indexEndian, indexCrc32c, indexLocation
+    final int[] meta = new int[14]; // ndim, dtypeSize, isBool, sharded, hasTranspose, endian,
+                                    // indexEndian, indexCrc32c, indexLocation, nested,
+                                    // nestedIndexEndian, nestedIndexCrc32c,
+                                    // nestedIndexLocation, innerCrc32c
+    // sharded: the inner chunk shape; nested: inner chunk shape followed by the leaf shape
     final long[] shape;
     final int[] chunkShape;
     int[] innerShape;
@@ -59,7 +62,21 @@ final class DeviceChain {
         BytesCodec bc = (BytesCodec) codecs[i];
         d.meta[5] = bc.configuration != null
                 && bc.configuration.endian == BytesCodec.Endian.BIG ? 1 : 0;
-        return i + 1 == codecs.length;  // byte-to-byte codecs stay on the Java path
+        i++;
+        if (i < codecs.length && codecs[i] instanceof Crc32cCodec) {  // verified on the device
+            d.meta[13] = 1;
+            i++;
+        }
+        return i == codecs.length;  // other byte-to-byte codecs stay on the Java path
+    }
+
+    /** index_codecs [bytes, crc32c?] → {endian, crc}, or null. */
+    private static int[] indexChain(Codec[] ic) {
+        if (ic.length < 1 || ic.length > 2 || !(ic[0] instanceof BytesCodec)) return null;
+        if (ic.length == 2 && !(ic[1] instanceof Crc32cCodec)) return null;
+        BytesCodec ib = (BytesCodec) ic[0];
+        int be = ib.configuration != null && ib.configuration.endian == BytesCodec.Endian.BIG ? 1 : 0;
+        return new int[]{be, ic.length == 2 ? 1 : 0};
     }
 
     /** Chain of a v3 array's codec list, or null when not device-supported. */
@@ -69,14 +86,29 @@ final class DeviceChain {
             ShardingIndexedCodec.Configuration c = ((ShardingIndexedCodec) codecs[0]).configuration;
             d.meta[3] = 1;
             d.innerShape = c.chunkShape.clone();
-            if (!innerChain(d, c.codecs)) return null;
-            Codec[] ic = c.indexCodecs;
-            if (ic.length < 1 || ic.length > 2 || !(ic[0] instanceof BytesCodec)) return null;
-            if (ic.length == 2 && !(ic[1] instanceof Crc32cCodec)) return null;
-            BytesCodec ib = (BytesCodec) ic[0];
-            d.meta[6] = ib.configuration != null
-                    && ib.configuration.endian == BytesCodec.Endian.BIG ? 1 : 0;
-            d.meta[7] = ic.length == 2 ? 1 : 0;
+            if (c.codecs.length == 1 && c.codecs[0] instanceof ShardingIndexedCodec) {
+                // nested sharding (ZarrPythonTests.java:177-179): one level is flattened on
+                // the device; deeper nesting stays on the Java path
+                ShardingIndexedCodec.Configuration nc =
+                        ((ShardingIndexedCodec) c.codecs[0]).configuration;
+                int n = c.chunkShape.length;
+                d.innerShape = new int[2 * n];
+                System.arraycopy(c.chunkShape, 0, d.innerShape, 0, n);
+                System.arraycopy(nc.chunkShape, 0, d.innerShape, n, n);
+                int[] nix = indexChain(nc.indexCodecs);
+                if (nix == null) return null;
+                d.meta[9] = 1;
+                d.meta[10] = nix[0];
+                d.meta[11] = nix[1];
+                d.meta[12] = "start".equals(nc.indexLocation) ? 1 : 0;
+                if (!innerChain(d, nc.codecs)) return null;
+            } else if (!innerChain(d, c.codecs)) {
+                return null;
+            }
+            int[] ix = indexChain(c.indexCodecs);
+            if (ix == null) return null;
+            d.meta[6] = ix[0];
+            d.meta[7] = ix[1];
             d.meta[8] = "start".equals(c.indexLocation) ? 1 : 0;
             return d;
         }
