@@ -1,17 +1,19 @@
 #!/usr/bin/env python3
 """Headline benchmark: device-resident Zarr v3 chunk decode on MI355X.
 
-Workload (BASELINE.json configs[2], the single-GPU config the metric is quoted on):
+Workload (default c4 = BASELINE.json configs[3], the chain the metric names:
+"sharding+bytes+transpose", 32^3 sharding, 1 GPU):
   uint32 array 1x4096x4096x1536 (96 GiB decoded), chunk (= shard) 1x1024x1024x1024,
-  codecs [sharding_indexed{chunk_shape [1,32,32,32], codecs [bytes(big)],
-          index_codecs [bytes(little), crc32c], index_location end}].
-One step = one full-array core.Array.read (M/core/Array.java:378-441) of all 32 shards /
-786,432 in-bounds inner chunks: index CRC + index parse + byte swap + scatter, inputs
-already resident in HBM.  Synthetic data v(g) = lo32(splitmix64(g ^ 0x5A5A2026)) is written
+  codecs [sharding_indexed{chunk_shape [1,32,32,32], codecs [transpose [0,3,2,1],
+          bytes(big)], index_codecs [bytes(little), crc32c], index_location end}].
+c3 (configs[2], no transpose) and c2 (configs[1], unsharded bytes) are the other
+single-GPU configs.  One step = one full-array core.Array.read (M/core/Array.java:378-441)
+of all 32 shards / 786,432 in-bounds inner chunks: index CRC + index parse + byte swap
+(+ transpose) + scatter, inputs already resident in HBM.  Synthetic data v(g) = lo32(splitmix64(g ^ 0x5A5A2026)) is written
 on the device and encoded by the product's own write path (zh_array_write); after warmup
 the decoded array is verified element-by-element on the device against the generator.
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--config c3|c4|c2]
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--config c4|c3|c2|c3crc|c3nest]
 
 N>1 (launched by torch.distributed.run): every rank decodes its own full-size array on its
 own GPU (weak scaling, no data-path collective: shards are independent objects); the
@@ -376,7 +378,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
+    ap.add_argument("--config", default="c4", choices=sorted(CONFIGS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
     ap.add_argument("--mode", default="weak", choices=["weak", "strong"],
