@@ -236,3 +236,28 @@ def test_sharding_nested_python_config(tmp_path, dt):
     want = O.array_write(b.zmeta, data.tobytes(), [0, 0, 0], [16, 16, 16])
     idx = O.compute_chunk_coords([16, 16, 16], [2, 4, 8], [0, 0, 0], [16, 16, 16]).index(coords)
     assert raw == want[idx]
+
+
+@pytest.mark.parametrize("shape,chunk,fn", [
+    # ReshapeCodecTest.testReshapeCodecReadWriteSingleChunk (zstd → gzip: no zstd here)
+    ([4, 5, 6, 3], [4, 5, 6, 3], lambda c: c.withReshape([[0, 1], [2], 3]).withGzip()),
+    # testReshapeCodecReadWriteMultipleChunks
+    ([8, 6, 4], [4, 3, 4], lambda c: c.withReshape([[0, 1], [2]]).withBytes("LITTLE")),
+    # testReshapeCombinedWithTranspose
+    ([4, 4, 4], [4, 4, 4], lambda c: c.withTranspose([2, 1, 0]).withReshape([[0, 1], [2]])
+     .withBytes("LITTLE")),
+    # merge then transpose (folded into a chunk-dim permutation), big-endian, inside shards
+    ([8, 12, 10], [8, 12, 10], lambda c: c.withSharding([4, 6, 5], lambda c1: c1.withReshape(
+        [[0, 1], [2]]).withTranspose([1, 0]).withBytes("BIG"))),
+])
+def test_reshape_read_write(tmp_path, shape, chunk, fn):
+    m = (z.ArrayMetadataBuilder().withShape(*shape).withDataType(z.DataType.UINT32)
+         .withChunkShape(*chunk).withFillValue(0).withCodecs(fn).build())
+    a = z.Array.create(z.FilesystemStore(tmp_path).resolve("r"), m)
+    data = np.arange(int(np.prod(shape)), dtype=np.uint32).reshape(shape)
+    a.write(None, data)
+    b = z.Array.open(z.FilesystemStore(tmp_path).resolve("r"))
+    np.testing.assert_array_equal(b.read(), data)
+    off = [1] * len(shape)
+    shp = [s - 2 for s in shape]
+    np.testing.assert_array_equal(b.read(off, shp), data[tuple(slice(1, s - 1) for s in shape)])

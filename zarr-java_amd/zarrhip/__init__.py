@@ -6,6 +6,7 @@ compute fallback in this package.
 """
 from .array import Array, ArrayAccessor, device
 from .codecs import (BloscCodec, BytesCodec, CodecBuilder, CodecRegistry, Crc32cCodec, GzipCodec,
+                     ReshapeCodec,
                      ShardingIndexedCodec, TransposeCodec, ZstdCodec, device_chain)
 from .dtypes import DataType
 from .errors import UnsupportedChainError, ZarrException
@@ -13,6 +14,7 @@ from .metadata import ArrayMetadata, ArrayMetadataBuilder, ChunkKeyEncoding, par
 from .store import FilesystemStore, MemoryStore, StoreHandle
 
 __all__ = ["Array", "ArrayAccessor", "ArrayMetadata", "ArrayMetadataBuilder", "BloscCodec",
+           "ReshapeCodec",
            "BytesCodec", "ChunkKeyEncoding", "CodecBuilder", "CodecRegistry", "Crc32cCodec",
            "DataType", "FilesystemStore", "GzipCodec", "MemoryStore", "ShardingIndexedCodec",
            "StoreHandle", "TransposeCodec", "UnsupportedChainError", "ZarrException",

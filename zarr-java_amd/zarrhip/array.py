@@ -48,7 +48,7 @@ class Array:
         self.metadata = metadata
         self.staged_bytes = 0  # encoded bytes read from the store and handed to the device
         self.chain = device_chain(metadata.codecs, metadata.ndim,
-                                  metadata.data_type.getByteCount())
+                                  metadata.data_type.getByteCount(), metadata.chunk_shape)
         self.zmeta = metadata.to_zh_meta(self.chain)
         err = C.create_string_buffer(512)
         st = _lib.lib().zh_validate_meta(C.byref(self.zmeta), err, 512)

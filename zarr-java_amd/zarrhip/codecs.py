@@ -86,6 +86,128 @@ class TransposeCodec(Codec):
         return cls(cfg["order"])
 
 
+class ReshapeCodec(Codec):
+    """ReshapeCodec (M/v3/codec/core/ReshapeCodec.java): a ravel-preserving array→array
+    reshape.  Each `shape` entry is a positive size, a list of input dims (their product), or
+    -1 (once).  Validation and messages follow resolveOutputShape (:148-168) and its steps."""
+    name, kind = "reshape", "aa"
+
+    def __init__(self, shape):
+        self.shape = [list(s) if isinstance(s, (list, tuple)) else s for s in shape]
+
+    def to_json(self):
+        return {"name": "reshape", "configuration": {"shape": [
+            list(s) if isinstance(s, list) else s for s in self.shape]}}
+
+    @classmethod
+    def from_json(cls, cfg, registry):
+        return cls(cfg["shape"])
+
+    def resolve(self, input_shape):
+        """→ (output shape, input dims per output entry or None)."""
+        ndim, n = len(input_shape), len(self.shape)
+        if n == 0:
+            raise ZarrException("reshape codec: 'shape' must not be empty.")
+        out, dims_per, minus, flat = [0] * n, [None] * n, -1, []
+        for i, e in enumerate(self.shape):  # parseConfiguredShape :187-235
+            if isinstance(e, list):
+                prod = 1
+                for d in e:
+                    if not isinstance(d, int):
+                        raise ZarrException("reshape codec: 'shape' entries must be integers or "
+                                            f"arrays of integers, but got {d}.")
+                    if d < 0 or d >= ndim:
+                        raise ZarrException(f"reshape codec: input dimension {d} is out of range "
+                                            f"for an input array with {ndim} dimensions.")
+                    prod *= input_shape[d]
+                    flat.append(d)
+                dims_per[i] = list(e)
+                out[i] = prod
+            elif isinstance(e, int):
+                if e == -1:
+                    if minus != -1:
+                        raise ZarrException("reshape codec: 'shape' may contain -1 at most once.")
+                    minus = i
+                    out[i] = -1
+                elif e <= 0:
+                    raise ZarrException("reshape codec: 'shape' entries must be a positive integer, "
+                                        f"-1, or an array of input dimensions, but got {e}.")
+                else:
+                    out[i] = e
+            else:
+                raise ZarrException("reshape codec: 'shape' entries must be integers or arrays of "
+                                    f"integers, but got {e}.")
+        for j in range(1, len(flat)):  # checkNoReordering :241-249
+            if flat[j] <= flat[j - 1]:
+                raise ZarrException("reshape codec: the flattened list of input dimensions must be "
+                                    f"strictly increasing, but got [{', '.join(map(str, flat))}].")
+        total = 1
+        for s in input_shape:
+            total *= s
+        if minus != -1:  # resolveInferredDimension :254-267
+            known = 1
+            for i, s in enumerate(out):
+                if i != minus:
+                    known *= s
+            if known == 0 or total % known != 0:
+                raise ZarrException("reshape codec: cannot infer the -1 dimension because "
+                                    "prod(output shape) would not equal prod(input shape) "
+                                    f"({total}).")
+            out[minus] = total // known
+        prod_out = 1
+        for s in out:
+            prod_out *= s
+        if prod_out != total:  # checkElementCountPreserved :272-283
+            raise ZarrException(f"reshape codec: prod(output shape)={prod_out} does not equal "
+                                f"prod(input shape)={total}.")
+        for i, dims in enumerate(dims_per):  # checkMergesAligned :291-322
+            if not dims:
+                continue
+            op = 1
+            for j in range(i):
+                op *= out[j]
+            os_ = 1
+            for j in range(i + 1, n):
+                os_ *= out[j]
+            ip = 1
+            for d in range(dims[0]):
+                ip *= input_shape[d]
+            is_ = 1
+            for d in range(dims[-1] + 1, ndim):
+                is_ *= input_shape[d]
+            if op != ip or os_ != is_:
+                raise ZarrException(
+                    f"reshape codec: output dimension {i} specified by input dimensions "
+                    f"[{', '.join(map(str, dims))}] does not align with the raveled input array "
+                    f"(prefix {op} vs {ip}, suffix {os_} vs {is_}).")
+        for i, s in enumerate(out):  # toIntShape :328-337
+            if s > 2 ** 31 - 1:
+                raise ZarrException(f"reshape codec: output dimension {i} exceeds "
+                                    "Integer.MAX_VALUE.")
+        return out, dims_per
+
+    def resolve_array_metadata(self, shape, chunk_shape):
+        """resolveArrayMetadata (:99-142): the output chunk shape and the output grid shape
+        (a merged output dim multiplies the input chunk counts; a split input dim keeps its
+        count on the outermost output dim)."""
+        out, _ = self.resolve(chunk_shape)
+        mult = [1] * len(out)
+        ostart = [1]
+        for s in out:
+            ostart.append(ostart[-1] * s)
+        istart = 1
+        for d, c in enumerate(chunk_shape):
+            nchunks = shape[d] // c
+            target = len(out) - 1
+            for i in range(len(out)):
+                if ostart[i] <= istart < ostart[i + 1]:
+                    target = i
+                    break
+            mult[target] *= nchunks
+            istart *= c
+        return [m * s for m, s in zip(mult, out)], out
+
+
 class Crc32cCodec(Codec):
     """Crc32cCodec (M/v3/codec/core/Crc32cCodec.java:24-60)."""
     name, kind = "crc32c", "bb"
@@ -242,8 +364,8 @@ class CodecRegistry:
         return cls.map[name].from_json(j.get("configuration"), cls)
 
 
-for _c in (TransposeCodec, BytesCodec, BloscCodec, GzipCodec, ZstdCodec, Crc32cCodec,
-           ShardingIndexedCodec):
+for _c in (TransposeCodec, ReshapeCodec, BytesCodec, BloscCodec, GzipCodec, ZstdCodec,
+           Crc32cCodec, ShardingIndexedCodec):
     CodecRegistry.addType(_c.name, _c)
 
 
@@ -256,6 +378,10 @@ class CodecBuilder:
 
     def withTranspose(self, order):
         self.codecs.append(TransposeCodec(order))
+        return self
+
+    def withReshape(self, shape):
+        self.codecs.append(ReshapeCodec(shape))
         return self
 
     def withBytes(self, endian="LITTLE"):
@@ -332,19 +458,79 @@ class DeviceChain:
         self.index_codecs = index_codecs
 
 
-def _split_inner(codecs, ndim, dsize):
+def _aa_order(aa, ndim, chunk_shape):
+    """Fold the array→array codecs (transpose, reshape) into one permutation of the chunk's
+    own dims: the order in which the payload's C-order traverses them (zh_codec_chain
+    .transpose_order), or None for the identity.
+
+    A reshape preserves the ravel (ReshapeCodec.java:62-88), so it never moves bytes; it only
+    regroups the current dims.  A later transpose is expressible as a chunk-dim permutation
+    when every current dim is a whole group of chunk dims (merges, unit dims) — splits followed
+    by a transpose are not, and stay unsupported."""
+    seq = list(range(ndim))                      # payload traversal order of the chunk dims
+    groups = [[d] for d in range(ndim)]          # current dims as groups of chunk dims
+    shape = list(chunk_shape) if chunk_shape is not None else None
+    for c in aa:
+        if isinstance(c, TransposeCodec):
+            c.validate(len(groups) if groups is not None else len(shape))
+            if list(c.order) == list(range(len(c.order))):
+                continue
+            if groups is None:
+                raise UnsupportedChainError("transpose after a dimension-splitting reshape")
+            groups = [groups[o] for o in c.order]
+            if shape is not None:
+                shape = [shape[o] for o in c.order]
+            seq = [d for g in groups for d in g]
+        elif isinstance(c, ReshapeCodec):
+            if shape is None:
+                raise UnsupportedChainError("reshape needs the chunk shape")
+            out, _ = c.resolve(shape)
+            groups = _regroup(groups, shape, out)
+            shape = out
+        else:
+            raise UnsupportedChainError(f"array→array codec '{c.name}' is not device-supported")
+    return None if seq == list(range(ndim)) else seq
+
+
+def _regroup(groups, cur, out):
+    """Groups of chunk dims behind each output dim of a ravel-preserving reshape cur → out,
+    or None when some output dim splits a current dim (or groups is already None)."""
+    if groups is None:
+        return None
+    res, j = [], 0
+    for s in out:
+        if s == 1:
+            res.append([])
+            continue
+        g, prod = [], 1
+        while j < len(cur) and prod < s:
+            g += groups[j]
+            prod *= cur[j]
+            j += 1
+        if prod != s:
+            return None
+        res.append(g)
+    tail = []
+    while j < len(cur):   # trailing unit dims: size 1, so their position is free
+        if cur[j] != 1:
+            return None
+        tail += groups[j]
+        j += 1
+    if tail:
+        if not res:
+            res.append([])
+        res[-1] = res[-1] + tail
+    return res
+
+
+def _split_inner(codecs, ndim, dsize, chunk_shape=None):
     validate_pipeline(codecs)
     aa = [c for c in codecs if c.kind == "aa"]
     ab = [c for c in codecs if c.kind == "ab"][0]
     bb = [c for c in codecs if c.kind == "bb"]
-    if len(aa) > 1 or any(not isinstance(c, TransposeCodec) for c in aa):
-        raise UnsupportedChainError("only a single transpose array→array codec is device-supported")
     if not isinstance(ab, BytesCodec):
         raise UnsupportedChainError("only bytes (or one nested sharding level) is device-supported")
-    order = None
-    if aa:
-        aa[0].validate(ndim)
-        order = aa[0].order
+    order = _aa_order(aa, ndim, chunk_shape)
     return order, ab.byte_order(dsize), bb
 
 
@@ -364,8 +550,9 @@ def _index_chain(sh):
     return ic
 
 
-def device_chain(codecs, ndim, dsize):
-    """Map a v3 codec list onto the device path (raises UnsupportedChainError otherwise)."""
+def device_chain(codecs, ndim, dsize, chunk_shape=None):
+    """Map a v3 codec list onto the device path (raises UnsupportedChainError otherwise).
+    `chunk_shape` (the array's chunk shape) is needed to resolve reshape codecs."""
     validate_pipeline(codecs)
     ab = [c for c in codecs if c.kind == "ab"][0]
     if isinstance(ab, ShardingIndexedCodec):
@@ -383,12 +570,12 @@ def device_chain(codecs, ndim, dsize):
             if len(ab.codecs) != 1:
                 raise UnsupportedChainError("nested sharding must be the only inner codec")
             nested = inner_ab
-            order, endian, inner_bb = _split_inner(nested.codecs, ndim, dsize)
+            order, endian, inner_bb = _split_inner(nested.codecs, ndim, dsize, nested.chunk_shape)
             inner_bb, crc = _take_crc(inner_bb)
             if inner_bb:
                 raise UnsupportedChainError("nested sharding with byte-to-byte leaf codecs")
         else:
-            order, endian, inner_bb = _split_inner(ab.codecs, ndim, dsize)
+            order, endian, inner_bb = _split_inner(ab.codecs, ndim, dsize, ab.chunk_shape)
             inner_bb, crc = _take_crc(inner_bb)
         chain = dict(sharded=True, inner_chunk_shape=ab.chunk_shape, transpose_order=order,
                      endian=endian, inner_crc32c=crc, index_endian=ic[0].byte_order(8),
@@ -403,7 +590,7 @@ def device_chain(codecs, ndim, dsize):
                          nested_index_location=A.ZH_INDEX_START
                          if nested.index_location == "start" else A.ZH_INDEX_END)
         return DeviceChain(chain, [], inner_bb, ic)
-    order, endian, bb = _split_inner(codecs, ndim, dsize)
+    order, endian, bb = _split_inner(codecs, ndim, dsize, chunk_shape)
     bb, crc = _take_crc(bb)
     chain = dict(sharded=False, transpose_order=order, endian=endian, inner_crc32c=crc)
     return DeviceChain(chain, bb, [])
