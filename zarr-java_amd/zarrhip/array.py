@@ -56,19 +56,22 @@ class Array:
             raise_for(_lib.ZhError(st, err.value.decode()))
 
     # ---------------------------------------------------------------- open / create
+    META_FILE = ZARR_JSON          # v2.Array: ".zarray"
+    METADATA = ArrayMetadata
+
     @classmethod
     def open(cls, store_handle):
-        raw = store_handle.resolve(ZARR_JSON).read()
+        raw = store_handle.resolve(cls.META_FILE).read()
         if raw is None:
             raise ZarrException(f"No Zarr array found at {store_handle!r}")
-        return cls(store_handle, ArrayMetadata.from_json(json.loads(raw)))
+        return cls(store_handle, cls.METADATA.from_json(json.loads(raw)))
 
     @classmethod
     def create(cls, store_handle, metadata, exist_ok=False):
-        h = store_handle.resolve(ZARR_JSON)
+        h = store_handle.resolve(cls.META_FILE)
         if not exist_ok and h.exists():
             raise ZarrException(f"Trying to create a new array in {store_handle!r}. But "
-                                f"{ZARR_JSON} already exists.")
+                                f"{cls.META_FILE} already exists.")
         h.set(metadata.dumps().encode())
         return cls(store_handle, metadata)
 
@@ -331,12 +334,21 @@ class Array:
                 sizes = dev.array_write(self.zmeta, src, offset, shape, [(b, cap) for b in bufs])
             except _lib.ZhError as e:
                 raise_for(e)
+            keep_fill = getattr(self.metadata, "fill_value", 0) is None and \
+                not self.chain.chain["sharded"]
             for c, b, sz in zip(coords, bufs, sizes):
                 h = self._handle(c)
-                if sz == 0:
+                if sz == 0 and not keep_fill:
                     h.delete()  # all fill → writeChunk deletes the key (Array.java:150-151)
                     continue
-                enc = dev.d2h(b, sz)
+                if sz == 0:
+                    # no fill value (v2 "fill_value": null): writeChunk never deletes
+                    # (Array.java:150 tests parsedFillValue != null) — store the zero chunk
+                    enc = bytes(int(np.prod(cs)) * self.metadata.data_type.getByteCount())
+                    if self.chain.chain.get("inner_crc32c"):
+                        enc += struct.pack("<I", L.zh_crc32c(0, enc, len(enc)))
+                else:
+                    enc = dev.d2h(b, sz)
                 if self.chain.host_bb:
                     enc = host_bb_encode(self.chain.host_bb, enc)
                 elif self.chain.inner_host_bb:

@@ -150,19 +150,24 @@ class ArrayMetadata:
 
     def to_zh_meta(self, device_chain):
         """zh_array_meta for the C-ABI."""
-        ch = device_chain.chain
-        return A.make_meta(self.shape, self.chunk_shape, self.data_type.getByteCount(),
-                           fill=self.fill_bytes, is_bool=self.data_type == DataType.BOOL,
-                           sharded=ch["sharded"], inner_chunk_shape=ch.get("inner_chunk_shape"),
-                           transpose_order=ch["transpose_order"], endian=ch["endian"],
-                           index_endian=ch.get("index_endian", A.ZH_ENDIAN_LITTLE),
-                           index_crc32c=ch.get("index_crc32c", False),
-                           index_location=ch.get("index_location", A.ZH_INDEX_END),
-                           nested_chunk_shape=ch.get("nested_chunk_shape"),
-                           nested_index_endian=ch.get("nested_index_endian", A.ZH_ENDIAN_LITTLE),
-                           nested_index_crc32c=ch.get("nested_index_crc32c", True),
-                           nested_index_location=ch.get("nested_index_location", A.ZH_INDEX_END),
-                           inner_crc32c=ch.get("inner_crc32c", False))
+        return zh_meta_for(self, device_chain, self.data_type == DataType.BOOL)
+
+
+def zh_meta_for(md, device_chain, is_bool):
+    """zh_array_meta of an array's metadata (v3 or v2) and its device chain."""
+    ch = device_chain.chain
+    return A.make_meta(md.shape, md.chunk_shape, md.data_type.getByteCount(),
+                       fill=md.fill_bytes, is_bool=is_bool,
+                       sharded=ch["sharded"], inner_chunk_shape=ch.get("inner_chunk_shape"),
+                       transpose_order=ch["transpose_order"], endian=ch["endian"],
+                       index_endian=ch.get("index_endian", A.ZH_ENDIAN_LITTLE),
+                       index_crc32c=ch.get("index_crc32c", False),
+                       index_location=ch.get("index_location", A.ZH_INDEX_END),
+                       nested_chunk_shape=ch.get("nested_chunk_shape"),
+                       nested_index_endian=ch.get("nested_index_endian", A.ZH_ENDIAN_LITTLE),
+                       nested_index_crc32c=ch.get("nested_index_crc32c", True),
+                       nested_index_location=ch.get("nested_index_location", A.ZH_INDEX_END),
+                       inner_crc32c=ch.get("inner_crc32c", False))
 
 
 def calculate_default_chunks(shape):
