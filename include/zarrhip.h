@@ -241,6 +241,15 @@ int zh_event_elapsed_ms(zh_ctx* ctx, void* start, void* stop, float* ms);
 int zh_device_info(zh_ctx* ctx, char* name, size_t namelen, int64_t* total_mem,
                    int* cu_count, char* arch, size_t archlen);
 
+/* ---- host byte-to-byte stage: blosc1 frames ----------------------------------------
+ * Replaces the blosc-java call inside BloscCodec.decode (M/v3/codec/core/BloscCodec.java,
+ * M/v2/codec/core/BloscCodec.java) for hosts without the blosc library: BloscLZ, LZ4/LZ4HC
+ * and zlib payloads, byte shuffle, split and unsplit blocks, memcpyed frames.  dst == NULL
+ * only reports the decompressed size in *nbytes_out.  Bit shuffle, snappy and zstd payloads
+ * → ZH_EUNSUPPORTED. */
+int zh_blosc_decompress(const void* src, size_t srclen, void* dst, size_t dstcap,
+                        size_t* nbytes_out, char* err, size_t errlen);
+
 /* ---- synthetic data (bench / property tests) -------------------------------------- */
 /* dst[i] = low dtype_size bytes of splitmix64((first + i) ^ seed), i in [0, n). */
 int zh_synth_fill(zh_ctx* ctx, void* dst, int64_t n, int dtype_size, int64_t first,

@@ -1,0 +1,75 @@
+"""Host blosc1 decompression (zh_blosc_decompress, zarr-java_amd/csrc/zh_blosc.cpp): pinned by
+the reference's v2_sample fixtures (BloscLZ split + shuffle, LZ4 unsplit + shuffle, memcpyed)
+and round-tripped through the test-side encoders in spec_blosc.py over every decoder path."""
+import os
+import struct
+
+import numpy as np
+import pytest
+
+import spec_blosc as sb
+import zarrhip as z
+from helpers import GOLDEN
+from zarrhip.codecs import BloscCodec
+
+ARANGE_CHUNK = np.add.outer(np.add.outer(np.arange(2) * 256, np.arange(4) * 16), np.arange(8))
+
+
+@pytest.mark.parametrize("name,dt", [("subgroup/array", "<i4"), ("double", "<f8")])
+def test_reference_fixtures_decode(name, dt):
+    raw = open(os.path.join(GOLDEN, "v2_sample", *name.split("/"), "0.0.0"), "rb").read()
+    got = np.frombuffer(BloscCodec().decode(raw), dt).reshape(2, 4, 8)
+    np.testing.assert_array_equal(got, ARANGE_CHUNK.astype(dt))
+
+
+def test_reference_fixture_memcpyed():
+    raw = open(os.path.join(GOLDEN, "v2_sample", "bool", "0.0.0"), "rb").read()
+    assert BloscCodec().decode(raw) == raw[16:16 + 64]
+
+
+def _payloads():
+    rng = np.random.default_rng(7)
+    yield "arange_i4", np.arange(5000, dtype="<i4").tobytes()
+    yield "runs", bytes([7]) * 3000 + bytes(range(256)) * 3 + bytes(1000)
+    yield "random", rng.integers(0, 256, 4099, dtype=np.uint8).tobytes()
+    yield "text", (b"the quick brown fox jumps over the lazy dog " * 200)[:7777]
+    far = rng.integers(0, 256, 9000, dtype=np.uint8).tobytes()
+    yield "far", far + bytes(50) + far[:4000]   # BloscLZ matches beyond 8191 bytes
+
+
+@pytest.mark.parametrize("comp", ["lz4", "blosclz", "zlib"])
+@pytest.mark.parametrize("ts,bs,split", [(4, 2048, None), (4, 4096, True), (8, 1024, False),
+                                         (1, 65536, None), (2, 16384, True)])
+@pytest.mark.parametrize("shuffle", [True, False])
+def test_roundtrip(comp, ts, bs, split, shuffle):
+    for name, data in _payloads():
+        f = sb.frame(data, ts, bs, comp, shuffle, split)
+        assert BloscCodec().decode(f) == data, name
+
+
+def test_codec_edge_cases():
+    assert BloscCodec().decode(sb.frame(b"", 4, 256, "lz4")) == b""
+    # a long literal run and long match extensions in one LZ4 stream
+    data = bytes(range(256)) * 2 + bytes(5000)
+    assert BloscCodec().decode(sb.frame(data, 1, 1 << 16, "lz4", False)) == data
+    # memcpyed frames as the product writes them
+    c = BloscCodec("lz4", 5, "shuffle", 4)
+    assert c.decode(c.encode(b"abcdefgh" * 9)) == b"abcdefgh" * 9
+
+
+def test_corrupt_frames_raise():
+    good = sb.frame(np.arange(3000, dtype="<i4").tobytes(), 4, 4096, "lz4")
+    for bad in (good[:10], good[:40], good[:-7], good[:16] + b"\xff" * (len(good) - 16)):
+        with pytest.raises(z.ZarrException):
+            BloscCodec().decode(bad)
+
+
+def test_unsupported_flags():
+    f = bytearray(sb.frame(bytes(4096), 4, 4096, "lz4"))
+    f[2] |= 0x04  # bit shuffle
+    with pytest.raises(z.UnsupportedChainError):
+        BloscCodec().decode(bytes(f))
+    f = bytearray(sb.frame(bytes(4096), 4, 4096, "lz4"))
+    f[2] = (f[2] & 0x1F) | (4 << 5)  # zstd payload
+    with pytest.raises(z.UnsupportedChainError):
+        BloscCodec().decode(bytes(f))

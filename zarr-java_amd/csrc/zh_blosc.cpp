@@ -1,0 +1,225 @@
+// zh_blosc.cpp — host decompression of blosc1 frames (the `blosc` codec of v3 and v2
+// arrays, M/v3/codec/core/BloscCodec.java / M/v2/codec/core/BloscCodec.java, which call the
+// blosc-java JNI library).  Compressors stay on the host (north star); this restates the
+// blosc1 frame and its BloscLZ / LZ4 / zlib payloads so that the raw chunk bytes can be
+// handed to the device, without the blosc library (absent from this image).
+//
+// Frame (16-byte header, little-endian): version, versionlz, flags, typesize, nbytes,
+// blocksize, cbytes; then one int32 start offset per block.  flags: 0x01 byte shuffle,
+// 0x02 memcpyed (raw bytes follow the header), 0x04 bit shuffle (unsupported here), 0x10
+// blocks not split into typesize streams, bits 5-7 compressor (0 BloscLZ, 1 LZ4/LZ4HC,
+// 3 zlib).  A split block is typesize streams of blocksize/typesize bytes; each stream is
+// int32 csize + payload (csize == stream size: stored raw).  The last (short) block is never
+// split.  Pinned by the reference's v2_sample fixtures (BloscLZ split + shuffle, LZ4
+// unsplit + shuffle, memcpyed), tests/test_blosc.py.
+#include <zlib.h>
+
+#include <cstdint>
+#include <cstring>
+#include <vector>
+
+#include "../../include/zarrhip.h"
+
+namespace {
+
+void set_err(char* err, size_t errlen, const char* msg) {
+  if (err && errlen) {
+    strncpy(err, msg, errlen - 1);
+    err[errlen - 1] = 0;
+  }
+}
+
+uint32_t rd32(const uint8_t* p) {
+  return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
+}
+
+// LZ4 block format: token (literal length << 4 | match length - 4), 255-continued lengths,
+// literals, 16-bit LE offset, overlapping match copy.  Returns bytes written or -1.
+int64_t lz4_block(const uint8_t* s, size_t n, uint8_t* d, size_t cap) {
+  size_t i = 0, o = 0;
+  while (i < n) {
+    const uint8_t tok = s[i++];
+    size_t lit = tok >> 4;
+    if (lit == 15) {
+      uint8_t b;
+      do {
+        if (i >= n) return -1;
+        b = s[i++];
+        lit += b;
+      } while (b == 255);
+    }
+    if (lit > n - i || lit > cap - o) return -1;
+    memcpy(d + o, s + i, lit);
+    i += lit;
+    o += lit;
+    if (i >= n) break;  // the last sequence has literals only
+    if (n - i < 2) return -1;
+    const size_t off = (size_t)s[i] | ((size_t)s[i + 1] << 8);
+    i += 2;
+    size_t ml = tok & 15;
+    if (ml == 15) {
+      uint8_t b;
+      do {
+        if (i >= n) return -1;
+        b = s[i++];
+        ml += b;
+      } while (b == 255);
+    }
+    ml += 4;
+    if (off == 0 || off > o || ml > cap - o) return -1;
+    for (size_t k = 0; k < ml; k++, o++) d[o] = d[o - off];
+  }
+  return (int64_t)o;
+}
+
+// BloscLZ (FastLZ-derived): ctrl < 32 → ctrl+1 literals; else match of (ctrl >> 5) + 2
+// bytes (7 → 255-continued), distance ((ctrl & 31) << 8) + next byte + 1, with the 16-bit
+// far form (+8191) when that byte is 255 and the high part is 31.
+int64_t blosclz_block(const uint8_t* s, size_t n, uint8_t* d, size_t cap) {
+  constexpr size_t kMaxDistance = 8191;
+  if (n == 0) return 0;
+  size_t ip = 0, o = 0;
+  uint32_t ctrl = s[ip++] & 31u;
+  for (;;) {
+    if (ctrl >= 32) {
+      size_t len = (ctrl >> 5) - 1;
+      size_t dist = (size_t)(ctrl & 31) << 8;
+      if (len == 6) {
+        uint8_t c;
+        do {
+          if (ip >= n) return -1;
+          c = s[ip++];
+          len += c;
+        } while (c == 255);
+      }
+      if (ip >= n) return -1;
+      const uint8_t code = s[ip++];
+      if (code == 255 && dist == (31u << 8)) {
+        if (n - ip < 2) return -1;
+        dist = (((size_t)s[ip] << 8) | s[ip + 1]) + kMaxDistance;
+        ip += 2;
+      } else {
+        dist += code;
+      }
+      len += 3;
+      if (dist + 1 > o || len > cap - o) return -1;
+      for (size_t k = 0; k < len; k++, o++) d[o] = d[o - dist - 1];
+    } else {
+      const size_t lit = ctrl + 1;
+      if (lit > n - ip || lit > cap - o) return -1;
+      memcpy(d + o, s + ip, lit);
+      ip += lit;
+      o += lit;
+    }
+    if (ip >= n) break;
+    ctrl = s[ip++];
+  }
+  return (int64_t)o;
+}
+
+int64_t zlib_block(const uint8_t* s, size_t n, uint8_t* d, size_t cap) {
+  uLongf dl = (uLongf)cap;
+  if (uncompress(d, &dl, s, (uLong)n) != Z_OK) return -1;
+  return (int64_t)dl;
+}
+
+}  // namespace
+
+extern "C" {
+
+int zh_blosc_decompress(const void* src_v, size_t srclen, void* dst_v, size_t dstcap,
+                        size_t* nbytes_out, char* err, size_t errlen) {
+  const uint8_t* src = (const uint8_t*)src_v;
+  uint8_t* dst = (uint8_t*)dst_v;
+  if (!src || srclen < 16) {
+    set_err(err, errlen, "blosc frame shorter than its 16-byte header");
+    return ZH_EDATA;
+  }
+  const uint8_t flags = src[2], ts = src[3];
+  const size_t nbytes = rd32(src + 4), bsize = rd32(src + 8), cbytes = rd32(src + 12);
+  if (nbytes_out) *nbytes_out = nbytes;
+  if (!dst) return ZH_OK;  // size query
+  if (nbytes > dstcap) {
+    set_err(err, errlen, "blosc destination too small");
+    return ZH_EINVAL;
+  }
+  if (cbytes > srclen) {
+    set_err(err, errlen, "blosc frame truncated");
+    return ZH_EDATA;
+  }
+  if (flags & 0x02) {  // memcpyed
+    if (16 + nbytes > srclen) {
+      set_err(err, errlen, "blosc frame truncated");
+      return ZH_EDATA;
+    }
+    memcpy(dst, src + 16, nbytes);
+    return ZH_OK;
+  }
+  if (flags & 0x04) {
+    set_err(err, errlen, "blosc bit-shuffled frames are not supported");
+    return ZH_EUNSUPPORTED;
+  }
+  const int comp = flags >> 5;
+  if (comp != 0 && comp != 1 && comp != 3) {
+    set_err(err, errlen, "blosc compressor (snappy/zstd) not available on this host");
+    return ZH_EUNSUPPORTED;
+  }
+  if (nbytes == 0) return ZH_OK;
+  if (bsize == 0 || ts == 0) {
+    set_err(err, errlen, "corrupt blosc header");
+    return ZH_EDATA;
+  }
+  const size_t nblocks = (nbytes + bsize - 1) / bsize;
+  if (16 + 4 * nblocks > srclen) {
+    set_err(err, errlen, "blosc frame truncated");
+    return ZH_EDATA;
+  }
+  std::vector<uint8_t> tmp(bsize);
+  for (size_t k = 0; k < nblocks; k++) {
+    const size_t bs = k + 1 < nblocks ? bsize : nbytes - k * bsize;
+    const bool leftover = bs < bsize;
+    const size_t nsplit = ((flags & 0x10) || leftover) ? 1 : ts;
+    const size_t neb = bs / nsplit;
+    size_t p = rd32(src + 16 + 4 * k);
+    uint8_t* blk = (flags & 0x01) && ts > 1 ? tmp.data() : dst + k * bsize;
+    for (size_t sidx = 0; sidx < nsplit; sidx++) {
+      if (p + 4 > srclen) {
+        set_err(err, errlen, "blosc frame truncated");
+        return ZH_EDATA;
+      }
+      const size_t cs = rd32(src + p);
+      p += 4;
+      if (cs > srclen - p) {
+        set_err(err, errlen, "blosc frame truncated");
+        return ZH_EDATA;
+      }
+      uint8_t* out = blk + sidx * neb;
+      int64_t got;
+      if (cs == neb) {
+        memcpy(out, src + p, neb);
+        got = (int64_t)neb;
+      } else if (comp == 0) {
+        got = blosclz_block(src + p, cs, out, neb);
+      } else if (comp == 1) {
+        got = lz4_block(src + p, cs, out, neb);
+      } else {
+        got = zlib_block(src + p, cs, out, neb);
+      }
+      if (got != (int64_t)neb) {
+        set_err(err, errlen, "corrupt blosc block");
+        return ZH_EDATA;
+      }
+      p += cs;
+    }
+    if (blk == tmp.data()) {  // byte unshuffle: stream j holds byte j of every element
+      uint8_t* d = dst + k * bsize;
+      const size_t ne = bs / ts;
+      for (size_t e = 0; e < ne; e++)
+        for (size_t j = 0; j < ts; j++) d[e * ts + j] = tmp[j * ne + e];
+      memcpy(d + ne * ts, tmp.data() + ne * ts, bs - ne * ts);
+    }
+  }
+  return ZH_OK;
+}
+
+}  // extern "C"

@@ -257,9 +257,9 @@ class GzipCodec(Codec):
 
 
 class BloscCodec(Codec):
-    """BloscCodec (M/v3/codec/core/BloscCodec.java) — host only.  Without the blosc
-    library only MEMCPYED frames (flags & 0x02: raw bytes after the 16-byte header) can be
-    decoded; other frames raise UnsupportedChainError."""
+    """BloscCodec (M/v3/codec/core/BloscCodec.java) — host only.  Frames are decoded by
+    zh_blosc_decompress (BloscLZ / LZ4 / zlib payloads, byte shuffle; bit shuffle, snappy and
+    zstd raise UnsupportedChainError); encode writes MEMCPYED frames (no compressor here)."""
     name, kind = "blosc", "bb"
 
     def __init__(self, cname="zstd", clevel=5, shuffle="noshuffle", typesize=None, blocksize=0):
@@ -267,15 +267,22 @@ class BloscCodec(Codec):
                     "blocksize": blocksize}
 
     def decode(self, b):
+        import ctypes as C
+        from . import _abi as A
+        from ._lib import lib
         b = bytes(b)
-        if len(b) < 16:
-            raise ZarrException("blosc frame too short")
-        flags = b[2]
-        nbytes = struct.unpack("<I", b[4:8])[0]
-        if flags & 0x02:
-            return b[16:16 + nbytes]
-        raise UnsupportedChainError("blosc frames other than MEMCPYED need the host blosc "
-                                    "library, which is not available here")
+        L = lib()
+        n = C.c_size_t()
+        err = C.create_string_buffer(256)
+        st = L.zh_blosc_decompress(b, len(b), None, 0, C.byref(n), err, 256)
+        if st == A.ZH_OK:
+            out = (C.c_char * max(1, n.value))()
+            st = L.zh_blosc_decompress(b, len(b), out, n.value, C.byref(n), err, 256)
+        if st == A.ZH_EUNSUPPORTED:
+            raise UnsupportedChainError(err.value.decode())
+        if st != A.ZH_OK:
+            raise ZarrException(f"Error in decoding blosc: {err.value.decode()}")
+        return bytes(out)[:n.value]
 
     def encode(self, b):
         b = bytes(b)
