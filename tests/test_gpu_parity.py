@@ -262,3 +262,36 @@ def test_chunk_crc32c_missing_and_clipped(dev):
     srcs = [shards[pos[c]] for c in sel]
     want = np.frombuffer(O.array_read(meta, srcs, off, shp), np.uint32).reshape(shp)
     np.testing.assert_array_equal(device_read(dev, meta, srcs, off, shp), want)
+
+
+@pytest.mark.parametrize("piece_kb", [128, 16, 4])
+@pytest.mark.parametrize("fuse", ["1", "0"])
+def test_chunk_crc32c_fused_row_kernel(dev, monkeypatch, piece_kb, fuse):
+    """Chunk CRC fused into decode_rows_kernel (rows sequential in the payload, pieces of
+    whole 4 KiB rounds): 64 KiB inner chunks in 1, 4 or 16 pieces, with elided chunks,
+    a missing shard, a clipped region (slow items keep the standalone CRC pass), and a
+    corrupted payload caught inside a fused item — vs the oracle and its message."""
+    monkeypatch.setenv("ZH_PIECE_KB", str(piece_kb))
+    monkeypatch.setenv("ZH_CRC_FUSE", fuse)
+    shape = [64, 64, 96]
+    meta = A.make_meta(shape, [32, 64, 64], 4, endian=A.ZH_ENDIAN_BIG, sharded=True,
+                       inner_chunk_shape=[16, 32, 32], inner_crc32c=True)
+    arr = rand_array(shape, 4, seed=29)
+    arr[0:16, 0:32, 0:32] = 0
+    shards = encode_oracle(meta, arr)
+    shards[3] = None
+    roundtrip_srcs = shards
+    for off, shp in [([0, 0, 0], shape), ([5, 3, 7], [50, 60, 80])]:
+        sel = chunk_coords(meta, off, shp)
+        pos = {c: i for i, c in enumerate(chunk_coords(meta, [0, 0, 0], shape))}
+        srcs = [roundtrip_srcs[pos[c]] for c in sel]
+        want = np.frombuffer(O.array_read(meta, srcs, off, shp), np.uint32).reshape(shp)
+        np.testing.assert_array_equal(device_read(dev, meta, srcs, off, shp), want)
+    bad = bytearray(shards[0])
+    bad[70000] ^= 0x20    # inside the second inner chunk's payload (a full, fast item)
+    srcs = [bytes(bad)] + shards[1:]
+    with pytest.raises(O.OracleError) as eo:
+        O.array_read(meta, srcs, [0, 0, 0], shape)
+    with pytest.raises(ZhError) as ed:
+        device_read(dev, meta, srcs, [0, 0, 0], shape)
+    assert str(ed.value) == str(eo.value)

@@ -802,7 +802,27 @@ int zh_plan_create(zh_ctx* ctx, const zh_array_meta* m, const zh_chunk_src* chun
     return ZH_EHIP;
   }
   if (c.inner_crc32c && items > 0) {
-    const int64_t nspan = (p->args.inner_nbytes + kCrcSpan - 1) / kCrcSpan;
+    // Fuse the chunk CRC into the row kernel when its lanes read each piece's payload in
+    // the CRC pass's order: rows sequential in the payload (pstride[F] == 1, row dims in
+    // C order) and equal pieces of whole 4 KiB rounds (256 lanes x 16 B).
+    ScatterArgs& g = p->args;
+    const int64_t pieces = 1ll << g.piece_shift;
+    bool fuse = !p->tile_mode && env_int("ZH_CRC_FUSE", 1) != 0 &&
+                (g.fast_mode == kFastRowArith || g.fast_mode == kFastRowTable);
+    if (fuse) {
+      const int F = g.fs;
+      int64_t stv = g.inner[F];
+      fuse = g.pstride[F] == 1;
+      for (int d = n - 1; d >= 0; d--) {
+        if (d == F) continue;
+        if (g.inner[d] > 1 && g.pstride[d] != stv) fuse = false;
+        stv *= g.inner[d];
+      }
+      fuse = fuse && g.inner_nbytes % pieces == 0 && (g.inner_nbytes / pieces) % 4096 == 0 &&
+             g.fast_rows % pieces == 0;
+    }
+    const int64_t span = fuse ? g.inner_nbytes / pieces : (int64_t)kCrcSpan;
+    const int64_t nspan = (g.inner_nbytes + span - 1) / span;
     if ((st = dev_alloc(&p->d_dcrc, (size_t)(items * nspan), err, errlen)) != ZH_OK) {
       plan_free(p);
       return st;
@@ -810,11 +830,15 @@ int zh_plan_create(zh_ctx* ctx, const zh_array_meta* m, const zh_chunk_src* chun
     DataCrcArgs& D = p->dcrc;
     D.desc = p->d_desc;
     D.n_items = items;
-    D.len = p->args.inner_nbytes;
+    D.len = g.inner_nbytes;
+    D.span = span;
     D.nspan = (int32_t)nspan;
     D.store = 0;
+    D.skip_fast = fuse ? 1 : 0;
     D.partials = p->d_dcrc;
     D.status = p->d_status;
+    g.crc_fused = fuse ? 1 : 0;
+    g.crc_partials = p->d_dcrc;
     p->dcrc_grid = (int)std::min<int64_t>(items * nspan, (int64_t)ctx->cu_count * 32);
   }
   p->args.desc = p->d_desc;
@@ -867,11 +891,14 @@ int zh_plan_execute(zh_plan* p, void* out, void* stream_v) {
   if (p->d_flat) ZH_HIP(launch_nested_index(p->nest, p->nest_grid, s));
   ScatterArgs a = p->args;
   a.region = (p->flags & ZH_OUT_DEVICE) ? (uint8_t*)out : p->d_out;
+  if (p->d_dcrc && p->args.crc_fused)  // the row kernel XOR-accumulates per-piece partials
+    ZH_HIP(hipMemsetAsync(p->d_dcrc, 0, (size_t)p->dcrc.n_items * p->dcrc.nspan * 4, s));
   ZH_HIP(launch_resolve(a, s));
-  if (p->d_dcrc) ZH_HIP(launch_data_crc(p->dcrc, p->dcrc_grid, s));
+  if (p->d_dcrc) ZH_HIP(launch_data_crc_partial(p->dcrc, p->dcrc_grid, s));
   if (p->timing) ZH_HIP(hipEventRecord(ev[1], s));
   ZH_HIP(launch_scatter(a, p->meta.dtype_size, p->tile_mode, 0, p->grid, s));
   ZH_HIP(launch_decode_slow(a, p->slow_grid, s));
+  if (p->d_dcrc) ZH_HIP(launch_data_crc_finalize(p->dcrc, s));
   if (p->timing) {
     ZH_HIP(hipEventRecord(ev[2], s));
     p->ev_pending.push_back(ev);
@@ -1315,6 +1342,7 @@ int zh_array_write(zh_ctx* ctx, const zh_array_meta* m, const void* src, const i
     D.desc = d_wd;
     D.n_items = items;
     D.len = a.inner_nbytes;
+    D.span = kCrcSpan;
     D.nspan = (int32_t)nspan;
     D.store = 1;
     D.partials = d_part;

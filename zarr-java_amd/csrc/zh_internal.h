@@ -119,6 +119,8 @@ struct ScatterArgs {
   int32_t nt;                   // fast kernels: bit 0 non-temporal loads, bit 1 stores
   int32_t tile_variant;         // tile fast path: 0 row-per-tile loads, 1 row-interleaved groups
   int32_t crc_extra;            // 4 when each stored chunk carries a trailing crc32c, else 0
+  int32_t crc_fused;            // row kernel also computes the chunk CRC (per-piece partials)
+  uint32_t* crc_partials;       // raw CRC register per (chunk, piece) = per item, XOR-accumulated
 };
 
 // Chunk-payload CRC-32C pass (inner crc32c codec): one workgroup per (item, 64 KiB span) of
@@ -128,8 +130,11 @@ struct DataCrcArgs {
   const ItemDesc* desc;         // src = payload address; kinds other than copy/clip skipped
   int64_t n_items;
   int64_t len;                  // payload bytes per chunk
-  int32_t nspan;                // ceil(len / kCrcSpan)
+  int64_t span;                 // bytes per partial (kCrcSpan, or the row kernel's piece)
+  int32_t nspan;                // ceil(len / span)
   int32_t store;
+  int32_t skip_fast;            // partial pass skips kDescFast items (their CRC is fused)
+  int32_t pad;
   uint32_t* partials;           // n_items * nspan
   uint64_t* status;             // decode: kStWords per shard
 };
@@ -172,6 +177,8 @@ hipError_t launch_crc(const CrcJob* jobs, int64_t njobs, int64_t nspans, uint32_
 hipError_t launch_resolve(const ScatterArgs& a, hipStream_t stream);
 hipError_t launch_nested_index(const NestArgs& a, int grid, hipStream_t stream);
 hipError_t launch_data_crc(const DataCrcArgs& a, int grid, hipStream_t stream);
+hipError_t launch_data_crc_partial(const DataCrcArgs& a, int grid, hipStream_t stream);
+hipError_t launch_data_crc_finalize(const DataCrcArgs& a, hipStream_t stream);
 hipError_t launch_scatter(const ScatterArgs& a, int dsize, int tile_mode, int encode, int grid,
                           hipStream_t stream);
 hipError_t launch_decode_slow(const ScatterArgs& a, int grid, hipStream_t stream);

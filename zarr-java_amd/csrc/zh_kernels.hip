@@ -837,6 +837,85 @@ __device__ __forceinline__ void generic_item(const ScatterArgs& a, Item& it,
   }
 }
 
+// ---------------------------------------------------------------------------------
+// CRC-32C helpers (CRC32C.java:14-80, 119-125): GF(2) shift/combine, slicing tables,
+// and the lane-interleaved update used by the chunk-CRC pass and the fused row kernel
+// ---------------------------------------------------------------------------------
+__constant__ uint32_t c_x2n[32] = {
+    0x40000000u, 0x20000000u, 0x08000000u, 0x00800000u, 0x00008000u, 0x82F63B78u, 0x6EA2D55Cu,
+    0x18B8EA18u, 0x510AC59Au, 0xB82BE955u, 0xB8FDB1E7u, 0x88E56F72u, 0x74C360A4u, 0xE4172B16u,
+    0x0D65762Au, 0x35D73A62u, 0x28461564u, 0xBF455269u, 0xE2EA32DCu, 0xFE7740E6u, 0xF946610Bu,
+    0x3C204F8Fu, 0x538586E3u, 0x59726915u, 0x734D5309u, 0xBC1AC763u, 0x7D0722CCu, 0xD289CABEu,
+    0xE94CA9BCu, 0x05B74F3Fu, 0xA51E1F42u, 0x40000000u};
+
+constexpr uint32_t kPoly = 0x82F63B78u;
+
+// a(x) * b(x) mod P (reflected bit order)
+__device__ __forceinline__ uint32_t multmodp(uint32_t a, uint32_t b) {
+  uint32_t m = 1u << 31, p = 0;
+  for (;;) {
+    if (a & m) {
+      p ^= b;
+      if ((a & (m - 1)) == 0) break;
+    }
+    m >>= 1;
+    b = (b & 1) ? (b >> 1) ^ kPoly : b >> 1;
+  }
+  return p;
+}
+
+__device__ __forceinline__ uint32_t x2nmodp(uint64_t n, unsigned k) {
+  uint32_t p = 1u << 31;
+  while (n) {
+    if (n & 1) p = multmodp(c_x2n[k & 31], p);
+    n >>= 1;
+    k++;
+  }
+  return p;
+}
+
+// crc(A || B) from crc(A), crc(B), |B|
+__device__ __forceinline__ uint32_t crc_combine(uint32_t c1, uint32_t c2, uint64_t len2) {
+  return multmodp(x2nmodp(len2, 3), c1) ^ c2;
+}
+
+// slicing-by-8 tables of the reflected Castagnoli polynomial (CRC32C.java:14-80), per block
+__device__ __forceinline__ void init_crc_tables(uint32_t (*T)[256]) {
+  const int tid = threadIdx.x;
+  {
+    uint32_t c = (uint32_t)tid;
+#pragma unroll
+    for (int k = 0; k < 8; k++) c = (c & 1) ? (c >> 1) ^ kPoly : c >> 1;
+    T[0][tid] = c;
+  }
+  __syncthreads();
+  for (int k = 1; k < 8; k++) {
+    const uint32_t p = T[k - 1][tid];
+    T[k][tid] = (p >> 8) ^ T[0][p & 0xFFu];
+    __syncthreads();
+  }
+}
+
+// inner crc32c codec: CRC-32C of every resolved chunk payload, coalesced.  A workgroup
+// takes one 64 KiB span of one chunk; lane l reads the 16-byte vectors l, l+256, ... (each
+// wave load is 1 KiB contiguous) and keeps the raw register of its vectors as if the other
+// lanes' bytes were zeros: acc = upd16(shift_4080(acc), v), with the constant zero-shift by
+// four table lookups.  Each lane then shifts acc to the span end and the lanes XOR together
+// (CRC linearity over GF(2)); the partial is the raw (init 0, no xorout) span register.
+__device__ __forceinline__ uint32_t crc_upd16(uint32_t c, v4u v, const uint32_t (*T)[256]) {
+  uint32_t lo = v.x ^ c, hi = v.y;
+  c = T[7][lo & 0xFFu] ^ T[6][(lo >> 8) & 0xFFu] ^ T[5][(lo >> 16) & 0xFFu] ^ T[4][lo >> 24] ^
+      T[3][hi & 0xFFu] ^ T[2][(hi >> 8) & 0xFFu] ^ T[1][(hi >> 16) & 0xFFu] ^ T[0][hi >> 24];
+  lo = v.z ^ c;
+  hi = v.w;
+  return T[7][lo & 0xFFu] ^ T[6][(lo >> 8) & 0xFFu] ^ T[5][(lo >> 16) & 0xFFu] ^ T[4][lo >> 24] ^
+         T[3][hi & 0xFFu] ^ T[2][(hi >> 8) & 0xFFu] ^ T[1][(hi >> 16) & 0xFFu] ^ T[0][hi >> 24];
+}
+
+__device__ __forceinline__ uint32_t crc_shift_tab(uint32_t c, const uint32_t (*S)[256]) {
+  return S[0][c & 0xFFu] ^ S[1][(c >> 8) & 0xFFu] ^ S[2][(c >> 16) & 0xFFu] ^ S[3][c >> 24];
+}
+
 // Row offsets (payload, region) of row r of an unclipped inner chunk.
 __device__ __forceinline__ void row_offsets(const ScatterArgs& a, const uint2* tab, uint32_t r,
                                             uint64_t& so, uint64_t& dof) {
@@ -864,12 +943,25 @@ __device__ __forceinline__ void row_offsets(const ScatterArgs& a, const uint2* t
 // (item, row batch) steps uniformly, and the loads of step k+1 are issued before the
 // stores of step k, across item boundaries (vmcnt counts stores, so un-pipelined code
 // would wait for the previous stores before every batch of loads).
-template <int DS, int U, int NT>
+template <int DS, int U, int NT, bool CRC = false>
 __global__ __launch_bounds__(kBlock) void decode_rows_kernel(ScatterArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   uint2* tab = reinterpret_cast<uint2*>(smem);
   for (int i = threadIdx.x; i < a.fast_n; i += kBlock)
     tab[i] = reinterpret_cast<const uint2*>(a.fast_tab)[i];
+  // fused chunk CRC (inner crc32c): the lanes' loads of a piece are the payload vectors
+  // tid + 256·m in order (rows sequential in the payload, host-checked), which is exactly
+  // the chunk-CRC pass's lane pattern — the raw CRC needs no second read of the payload
+  uint32_t(*T)[256] = reinterpret_cast<uint32_t(*)[256]>(smem + (((size_t)a.fast_n * 8 + 15) & ~(size_t)15));
+  uint32_t(*S)[256] = T + 8;
+  uint32_t kfull = 0, acc = 0;
+  if constexpr (CRC) {
+    init_crc_tables(T);
+    const uint32_t k4080 = x2nmodp(4080, 3);
+#pragma unroll
+    for (int b = 0; b < 4; b++) S[b][threadIdx.x] = multmodp(k4080, (uint32_t)threadIdx.x << (8 * b));
+    kfull = x2nmodp((uint64_t)(4080 - 16 * threadIdx.x), 3);
+  }
   __syncthreads();
   const int vs = a.fast_vpr_shift;
   const uint32_t col = (threadIdx.x & ((1u << vs) - 1)) * 16;
@@ -934,11 +1026,13 @@ __global__ __launch_bounds__(kBlock) void decode_rows_kernel(ScatterArgs a) {
   const uint8_t* dst_a = dst;
   bool fill_a = fill;
   uint4 fv_a = fv;
+  int64_t item_a = item;
   for (;;) {
     // advance one step (uniform)
     rbase += rstep * U;
     bool more = true;
-    if (rbase >= r1) {
+    const bool piece_end = rbase >= r1;
+    if (piece_end) {
       item += gridDim.x;
       D = Dn;
       if (item + gridDim.x < total) Dn = ld_desc(a.desc + ((item + gridDim.x) >> a.piece_shift));
@@ -953,6 +1047,23 @@ __global__ __launch_bounds__(kBlock) void decode_rows_kernel(ScatterArgs a) {
       if (da[u] != ~0ull)
         st16s<(NT & 2) != 0>(const_cast<uint8_t*>(dst_a) + da[u],
                              fill_a ? fv_a : xform16<DS>(va[u], a.swap, a.is_bool));
+    if constexpr (CRC) {
+      if (!fill_a) {
+#pragma unroll
+        for (int u = 0; u < U; u++)
+          if (da[u] != ~0ull) {
+            const v4u w = {va[u].x, va[u].y, va[u].z, va[u].w};
+            acc = crc_upd16(crc_shift_tab(acc, S), w, T);
+          }
+        if (piece_end) {  // uniform: shift every lane to the piece end, XOR the wave
+          uint32_t c = multmodp(kfull, acc);
+#pragma unroll
+          for (int o = 32; o > 0; o >>= 1) c ^= (uint32_t)__shfl_xor((int)c, o, 64);
+          if ((threadIdx.x & 63) == 0) atomicXor(a.crc_partials + item_a, c);
+          acc = 0;
+        }
+      }
+    }
     if (!more) break;
 #pragma unroll
     for (int u = 0; u < U; u++) {
@@ -962,6 +1073,7 @@ __global__ __launch_bounds__(kBlock) void decode_rows_kernel(ScatterArgs a) {
     dst_a = dst;
     fill_a = fill;
     fv_a = fv;
+    item_a = item;
   }
 }
 
@@ -1088,63 +1200,8 @@ __global__ __launch_bounds__(kBlock) void flags_kernel(ScatterArgs a) {
 }
 
 // ---------------------------------------------------------------------------------
-// CRC-32C of the shard index
+// CRC-32C of the shard index (helpers: "CRC-32C helpers" above the row kernel)
 // ---------------------------------------------------------------------------------
-__constant__ uint32_t c_x2n[32] = {
-    0x40000000u, 0x20000000u, 0x08000000u, 0x00800000u, 0x00008000u, 0x82F63B78u, 0x6EA2D55Cu,
-    0x18B8EA18u, 0x510AC59Au, 0xB82BE955u, 0xB8FDB1E7u, 0x88E56F72u, 0x74C360A4u, 0xE4172B16u,
-    0x0D65762Au, 0x35D73A62u, 0x28461564u, 0xBF455269u, 0xE2EA32DCu, 0xFE7740E6u, 0xF946610Bu,
-    0x3C204F8Fu, 0x538586E3u, 0x59726915u, 0x734D5309u, 0xBC1AC763u, 0x7D0722CCu, 0xD289CABEu,
-    0xE94CA9BCu, 0x05B74F3Fu, 0xA51E1F42u, 0x40000000u};
-
-constexpr uint32_t kPoly = 0x82F63B78u;
-
-// a(x) * b(x) mod P (reflected bit order)
-__device__ __forceinline__ uint32_t multmodp(uint32_t a, uint32_t b) {
-  uint32_t m = 1u << 31, p = 0;
-  for (;;) {
-    if (a & m) {
-      p ^= b;
-      if ((a & (m - 1)) == 0) break;
-    }
-    m >>= 1;
-    b = (b & 1) ? (b >> 1) ^ kPoly : b >> 1;
-  }
-  return p;
-}
-
-__device__ __forceinline__ uint32_t x2nmodp(uint64_t n, unsigned k) {
-  uint32_t p = 1u << 31;
-  while (n) {
-    if (n & 1) p = multmodp(c_x2n[k & 31], p);
-    n >>= 1;
-    k++;
-  }
-  return p;
-}
-
-// crc(A || B) from crc(A), crc(B), |B|
-__device__ __forceinline__ uint32_t crc_combine(uint32_t c1, uint32_t c2, uint64_t len2) {
-  return multmodp(x2nmodp(len2, 3), c1) ^ c2;
-}
-
-// slicing-by-8 tables of the reflected Castagnoli polynomial (CRC32C.java:14-80), per block
-__device__ __forceinline__ void init_crc_tables(uint32_t (*T)[256]) {
-  const int tid = threadIdx.x;
-  {
-    uint32_t c = (uint32_t)tid;
-#pragma unroll
-    for (int k = 0; k < 8; k++) c = (c & 1) ? (c >> 1) ^ kPoly : c >> 1;
-    T[0][tid] = c;
-  }
-  __syncthreads();
-  for (int k = 1; k < 8; k++) {
-    const uint32_t p = T[k - 1][tid];
-    T[k][tid] = (p >> 8) ^ T[0][p & 0xFFu];
-    __syncthreads();
-  }
-}
-
 // Standard CRC-32C of base[0, slen), slen <= kCrcSpan, by the whole workgroup: kCrcLane-byte
 // lane segments (slicing-by-8), combined pairwise in GF(2).  Uniform call; every lane
 // returns the result.
@@ -1202,25 +1259,7 @@ __global__ __launch_bounds__(kBlock) void crc_partial_kernel(const CrcJob* jobs,
   if (threadIdx.x == 0) partials[span] = c;
 }
 
-// inner crc32c codec: CRC-32C of every resolved chunk payload, coalesced.  A workgroup
-// takes one 64 KiB span of one chunk; lane l reads the 16-byte vectors l, l+256, ... (each
-// wave load is 1 KiB contiguous) and keeps the raw register of its vectors as if the other
-// lanes' bytes were zeros: acc = upd16(shift_4080(acc), v), with the constant zero-shift by
-// four table lookups.  Each lane then shifts acc to the span end and the lanes XOR together
-// (CRC linearity over GF(2)); the partial is the raw (init 0, no xorout) span register.
-__device__ __forceinline__ uint32_t crc_upd16(uint32_t c, v4u v, const uint32_t (*T)[256]) {
-  uint32_t lo = v.x ^ c, hi = v.y;
-  c = T[7][lo & 0xFFu] ^ T[6][(lo >> 8) & 0xFFu] ^ T[5][(lo >> 16) & 0xFFu] ^ T[4][lo >> 24] ^
-      T[3][hi & 0xFFu] ^ T[2][(hi >> 8) & 0xFFu] ^ T[1][(hi >> 16) & 0xFFu] ^ T[0][hi >> 24];
-  lo = v.z ^ c;
-  hi = v.w;
-  return T[7][lo & 0xFFu] ^ T[6][(lo >> 8) & 0xFFu] ^ T[5][(lo >> 16) & 0xFFu] ^ T[4][lo >> 24] ^
-         T[3][hi & 0xFFu] ^ T[2][(hi >> 8) & 0xFFu] ^ T[1][(hi >> 16) & 0xFFu] ^ T[0][hi >> 24];
-}
-
-__device__ __forceinline__ uint32_t crc_shift_tab(uint32_t c, const uint32_t (*S)[256]) {
-  return S[0][c & 0xFFu] ^ S[1][(c >> 8) & 0xFFu] ^ S[2][(c >> 16) & 0xFFu] ^ S[3][c >> 24];
-}
+// (crc_upd16 / crc_shift_tab: see "CRC-32C helpers" above the row kernel)
 
 constexpr int kDcBatch = 8;  // vectors in flight per lane
 
@@ -1235,7 +1274,8 @@ __global__ __launch_bounds__(kBlock) void data_crc_partial_kernel(DataCrcArgs a)
 #pragma unroll
     for (int b = 0; b < 4; b++) S[b][tid] = multmodp(k4080, (uint32_t)tid << (8 * b));
   }
-  // full span: this lane's last vector ends 4080 - 16*tid bytes before the span end
+  // a span of whole 4 KiB rounds: this lane's last vector ends 4080 - 16*tid bytes before
+  // the span end
   const uint32_t kfull = x2nmodp((uint64_t)(4080 - 16 * tid), 3);
   __syncthreads();
   const int64_t total = a.n_items * a.nspan;
@@ -1246,8 +1286,9 @@ __global__ __launch_bounds__(kBlock) void data_crc_partial_kernel(DataCrcArgs a)
     const uint32_t mode = D.kind & kDescModeMask;
     // missing shards / inner chunks are clip or fill descriptors without a source
     if ((mode != kDescFullCopy && mode != kDescClip) || D.src == 0) continue;  // uniform
-    const uint8_t* base = (const uint8_t*)(uintptr_t)D.src + span * kCrcSpan;
-    const int64_t slen = min((int64_t)kCrcSpan, a.len - span * kCrcSpan);
+    if (a.skip_fast && (D.kind & kDescFast)) continue;  // fused into the row kernel
+    const uint8_t* base = (const uint8_t*)(uintptr_t)D.src + span * a.span;
+    const int64_t slen = min(a.span, a.len - span * a.span);
     const int nblk = (int)(slen >> 4);
     uint32_t acc = 0;
     int nb = 0;
@@ -1269,7 +1310,7 @@ __global__ __launch_bounds__(kBlock) void data_crc_partial_kernel(DataCrcArgs a)
     uint32_t contrib = 0;
     if (nb > 0) {
       const int64_t e = 16 * (int64_t)(tid + kBlock * (nb - 1)) + 16;
-      const uint32_t k = slen == kCrcSpan ? kfull : x2nmodp((uint64_t)(slen - e), 3);
+      const uint32_t k = (slen & 4095) == 0 ? kfull : x2nmodp((uint64_t)(slen - e), 3);
       contrib = multmodp(k, acc);
     }
     if (tid == 0) {  // tail bytes (payload length not a multiple of 16) end the span
@@ -1296,10 +1337,10 @@ __global__ void data_crc_finalize_kernel(DataCrcArgs a) {
   const uint32_t mode = D.kind & kDescModeMask;
   if ((mode != kDescFullCopy && mode != kDescClip) || D.src == 0) return;
   uint32_t raw = 0;
-  const uint32_t kspan = x2nmodp((uint64_t)kCrcSpan, 3);
+  const uint32_t kspan = x2nmodp((uint64_t)a.span, 3);
   for (int64_t k = 0; k < a.nspan; k++) {
-    const int64_t slen = min((int64_t)kCrcSpan, a.len - k * kCrcSpan);
-    raw = multmodp(slen == kCrcSpan ? kspan : x2nmodp((uint64_t)slen, 3), raw) ^
+    const int64_t slen = min(a.span, a.len - k * a.span);
+    raw = multmodp(slen == a.span ? kspan : x2nmodp((uint64_t)slen, 3), raw) ^
           a.partials[item * a.nspan + k];
   }
   const uint32_t c = multmodp(x2nmodp((uint64_t)a.len, 3), 0xFFFFFFFFu) ^ raw ^ 0xFFFFFFFFu;
@@ -1561,12 +1602,22 @@ hipError_t launch_nested_index(const NestArgs& a, int grid, hipStream_t stream) 
   return hipGetLastError();
 }
 
-hipError_t launch_data_crc(const DataCrcArgs& a, int grid, hipStream_t stream) {
+hipError_t launch_data_crc_partial(const DataCrcArgs& a, int grid, hipStream_t stream) {
   if (a.n_items <= 0) return hipSuccess;
   hipLaunchKernelGGL(data_crc_partial_kernel, dim3((unsigned)grid), dim3(kBlock), 0, stream, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_data_crc_finalize(const DataCrcArgs& a, hipStream_t stream) {
+  if (a.n_items <= 0) return hipSuccess;
   hipLaunchKernelGGL(data_crc_finalize_kernel, dim3((unsigned)((a.n_items + 255) / 256)),
                      dim3(256), 0, stream, a);
   return hipGetLastError();
+}
+
+hipError_t launch_data_crc(const DataCrcArgs& a, int grid, hipStream_t stream) {
+  hipError_t e = launch_data_crc_partial(a, grid, stream);
+  return e == hipSuccess ? launch_data_crc_finalize(a, stream) : e;
 }
 
 hipError_t launch_crc(const CrcJob* jobs, int64_t njobs, int64_t nspans, uint32_t* partials,
@@ -1611,6 +1662,12 @@ static void launch_scatter_ds(const ScatterArgs& a, int tile, int enc, int grid,
           if (ntx) hipLaunchKernelGGL((decode_tiles_kernel<3, 0>), dim3(grid), dim3(kBlock), lds, s, a);
           else hipLaunchKernelGGL((decode_tiles_kernel<0, 0>), dim3(grid), dim3(kBlock), lds, s, a);
         }
+      }
+    } else if (a.fast_mode != kFastNone && a.crc_fused) {
+      lds += 12 * 256 * 4;  // slicing tables T[8][256] + zero-shift tables S[4][256]
+      switch (nt) {
+        case 0: hipLaunchKernelGGL((decode_rows_kernel<DS, 4, 0, true>), dim3(grid), dim3(kBlock), lds, s, a); break;
+        default: hipLaunchKernelGGL((decode_rows_kernel<DS, 4, 3, true>), dim3(grid), dim3(kBlock), lds, s, a); break;
       }
     } else if (a.fast_mode != kFastNone) {
       switch (nt) {
