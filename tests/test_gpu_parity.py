@@ -295,3 +295,19 @@ def test_chunk_crc32c_fused_row_kernel(dev, monkeypatch, piece_kb, fuse):
     with pytest.raises(ZhError) as ed:
         device_read(dev, meta, srcs, [0, 0, 0], shape)
     assert str(ed.value) == str(eo.value)
+
+
+@pytest.mark.parametrize("mode", ["rows", "tiles", "rows_crc"])
+def test_item_permutation_order(dev, monkeypatch, mode):
+    """ZH_ITEM_PERM=1 (fast kernels walk items in a coprime-stride order): same bytes."""
+    monkeypatch.setenv("ZH_ITEM_PERM", "1")
+    monkeypatch.setenv("ZH_PIECE_KB", "16")
+    shape = [64, 64, 96]
+    kw = dict(endian=A.ZH_ENDIAN_BIG, sharded=True, inner_chunk_shape=[16, 32, 32])
+    if mode == "tiles":
+        kw["transpose_order"] = [2, 1, 0]
+    if mode == "rows_crc":
+        kw["inner_crc32c"] = True
+    meta = A.make_meta(shape, [32, 64, 64], 4, **kw)
+    arr = rand_array(shape, 4, seed=31)
+    roundtrip(dev, meta, arr, [([0, 0, 0], shape), ([3, 2, 1], [60, 61, 90])])

@@ -857,6 +857,24 @@ int zh_plan_create(zh_ctx* ctx, const zh_array_meta* m, const zh_chunk_src* chun
   // A/B in one process, profiles/r01/experiments/tune_*.json)
   p->args.nt = env_int("ZH_NT", 3) & 3;
   p->args.tile_variant = std::min(1, std::max(0, env_int("ZH_TILE_VARIANT", 1)));
+  // Visit items in a golden-ratio stride order: +3.6 % on the tile path (c4) on every normal
+  // allocation, neutral on the row path (interleaved A/B, profiles/placement_perm.py), so
+  // on by default for tiles.  ZH_ITEM_PERM=0/1 overrides.
+  p->args.item_mul = 0;
+  if (env_int("ZH_ITEM_PERM", p->tile_mode ? 1 : 0) && p->args.total_items > 1) {
+    const uint64_t t = (uint64_t)p->args.total_items;
+    uint64_t m = ((uint64_t)((double)t * 0.6180339887498949)) | 1;
+    auto gcd = [](uint64_t x, uint64_t y) {
+      while (y) {
+        const uint64_t r = x % y;
+        x = y;
+        y = r;
+      }
+      return x;
+    };
+    while (gcd(m, t) != 1) m += 2;
+    p->args.item_mul = m % t;
+  }
   p->slow_grid = p->grid;
   *out = p;
   return ZH_OK;

@@ -119,6 +119,9 @@ struct ScatterArgs {
   int32_t nt;                   // fast kernels: bit 0 non-temporal loads, bit 1 stores
   int32_t tile_variant;         // tile fast path: 0 row-per-tile loads, 1 row-interleaved groups
   int32_t crc_extra;            // 4 when each stored chunk carries a trailing crc32c, else 0
+  uint64_t item_mul;            // fast kernels visit items in the order (i * item_mul) mod
+                                // total_items (coprime; 0 = identity): decorrelates the
+                                // addresses written concurrently (DESIGN §4 placement)
   int32_t crc_fused;            // row kernel also computes the chunk CRC (per-piece partials)
   uint32_t* crc_partials;       // raw CRC register per (chunk, piece) = per item, XOR-accumulated
 };

@@ -938,6 +938,11 @@ __device__ __forceinline__ void row_offsets(const ScatterArgs& a, const uint2* t
   }
 }
 
+// Work order of the fast kernels: item i of the grid-stride walk is work item pitem(i).
+__device__ __forceinline__ int64_t pitem(const ScatterArgs& a, int64_t i) {
+  return a.item_mul ? (int64_t)(((uint64_t)i * a.item_mul) % (uint64_t)a.total_items) : i;
+}
+
 // decode, fast row kernel: unclipped aligned items whose rows (along the unit-stride dim)
 // are whole 16-byte vectors.  Each lane owns one 16-byte column; the block walks
 // (item, row batch) steps uniformly, and the loads of step k+1 are issued before the
@@ -975,15 +980,15 @@ __global__ __launch_bounds__(kBlock) void decode_rows_kernel(ScatterArgs a) {
   int64_t item = blockIdx.x;
   ItemDesc D, Dn;
   if (item >= total) return;
-  D = ld_desc(a.desc + (item >> a.piece_shift));
+  D = ld_desc(a.desc + (pitem(a, item) >> a.piece_shift));
   Dn = D;
-  if (item + gridDim.x < total) Dn = ld_desc(a.desc + ((item + gridDim.x) >> a.piece_shift));
+  if (item + gridDim.x < total) Dn = ld_desc(a.desc + (pitem(a, item + gridDim.x) >> a.piece_shift));
   // seek to a fast item (item, D, Dn advance together)
   auto seek = [&]() -> bool {
     while (item < total && !(D.kind & kDescFast)) {
       item += gridDim.x;
       D = Dn;
-      if (item + gridDim.x < total) Dn = ld_desc(a.desc + ((item + gridDim.x) >> a.piece_shift));
+      if (item + gridDim.x < total) Dn = ld_desc(a.desc + (pitem(a, item + gridDim.x) >> a.piece_shift));
     }
     return item < total;
   };
@@ -996,7 +1001,7 @@ __global__ __launch_bounds__(kBlock) void decode_rows_kernel(ScatterArgs a) {
   uint4 fv;
   uint32_t rbase, r1;
   auto start_item = [&]() {
-    const uint32_t piece = (uint32_t)item & pmask;
+    const uint32_t piece = (uint32_t)pitem(a, item) & pmask;
     rbase = (uint32_t)(((uint64_t)nrows * piece) / pieces);
     r1 = (uint32_t)(((uint64_t)nrows * (piece + 1)) / pieces);
     src = (const uint8_t*)(uintptr_t)D.src + col;
@@ -1035,7 +1040,7 @@ __global__ __launch_bounds__(kBlock) void decode_rows_kernel(ScatterArgs a) {
     if (piece_end) {
       item += gridDim.x;
       D = Dn;
-      if (item + gridDim.x < total) Dn = ld_desc(a.desc + ((item + gridDim.x) >> a.piece_shift));
+      if (item + gridDim.x < total) Dn = ld_desc(a.desc + (pitem(a, item + gridDim.x) >> a.piece_shift));
       more = seek();
       if (more) start_item();
     }
@@ -1059,7 +1064,7 @@ __global__ __launch_bounds__(kBlock) void decode_rows_kernel(ScatterArgs a) {
           uint32_t c = multmodp(kfull, acc);
 #pragma unroll
           for (int o = 32; o > 0; o >>= 1) c ^= (uint32_t)__shfl_xor((int)c, o, 64);
-          if ((threadIdx.x & 63) == 0) atomicXor(a.crc_partials + item_a, c);
+          if ((threadIdx.x & 63) == 0) atomicXor(a.crc_partials + pitem(a, item_a), c);
           acc = 0;
         }
       }
@@ -1092,18 +1097,18 @@ __global__ __launch_bounds__(kBlock) void decode_tiles_kernel(ScatterArgs a) {
   const uint32_t pmask = (1u << a.piece_shift) - 1;
   int64_t item = blockIdx.x;
   if (item >= total) return;
-  ItemDesc D = ld_desc(a.desc + (item >> a.piece_shift));
+  ItemDesc D = ld_desc(a.desc + (pitem(a, item) >> a.piece_shift));
   for (; item < total; item += gridDim.x) {
     const int64_t nxt = item + gridDim.x;
     ItemDesc Dn = D;
-    if (nxt < total) Dn = ld_desc(a.desc + (nxt >> a.piece_shift));
+    if (nxt < total) Dn = ld_desc(a.desc + (pitem(a, nxt) >> a.piece_shift));
     if (D.kind & kDescFast) {
       const uint8_t* src = (const uint8_t*)(uintptr_t)D.src;
       uint8_t* dst = a.region + D.d0 * 4;
       if constexpr (VARIANT == 0)
-        fast_tiles<kFastTPB, NT>(a, tab, src, dst, (uint32_t)item & pmask, tile);
+        fast_tiles<kFastTPB, NT>(a, tab, src, dst, (uint32_t)pitem(a, item) & pmask, tile);
       else
-        fast_tiles_rows<NT>(a, tab, src, dst, (uint32_t)item & pmask,
+        fast_tiles_rows<NT>(a, tab, src, dst, (uint32_t)pitem(a, item) & pmask,
                             reinterpret_cast<uint32_t*>(tile));
     }
     D = Dn;
