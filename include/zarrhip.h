@@ -219,6 +219,10 @@ int zh_device_malloc(zh_ctx* ctx, size_t bytes, void** out);
  * copies are not (DESIGN.md "Placement").  Falls back to hipMalloc unless ZH_MALLOC_REQUIRE. */
 #define ZH_MALLOC_CONTIGUOUS 0x1u
 #define ZH_MALLOC_REQUIRE 0x2u
+/* Physical chunks (hipMemCreate, ZH_SCATTER_MB MiB each, default 2) mapped into one virtual
+ * range in a coprime-stride order, so that virtually adjacent chunks are not physically
+ * adjacent (DESIGN.md "Placement").  Freed by zh_device_free. */
+#define ZH_MALLOC_SCATTER 0x4u
 int zh_device_malloc_ex(zh_ctx* ctx, size_t bytes, unsigned flags, void** out);
 int zh_device_free(zh_ctx* ctx, void* ptr);
 int zh_host_malloc_pinned(zh_ctx* ctx, size_t bytes, void** out);

@@ -1,0 +1,68 @@
+#!/usr/bin/env python3
+"""Larger sample for placement_vmm: 12 GiB outputs (1/8 of the array), 16 output buffers:
+4 plain hipMalloc, 4 ZH_MALLOC_SCATTER at 2 MiB, 4 at 64 MiB, 4 at 256 MiB chunks.  One slab,
+interleaved rounds, kernel time by HIP events, every output verified.  argv[1] = config."""
+import json
+import os
+import statistics
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import bench  # noqa: E402
+from zarrhip import _abi as A  # noqa: E402
+from zarrhip._lib import DeviceContext, lib, i64arr, i32arr  # noqa: E402
+import ctypes as C  # noqa: E402
+
+cfg = sys.argv[1] if len(sys.argv) > 1 else "c4"
+dev = DeviceContext(0)
+meta = bench.build_meta(A, cfg, 8)
+n = meta.ndim
+shape = [meta.shape[d] for d in range(n)]
+cs = [meta.chunk_shape[d] for d in range(n)]
+nel = 1
+for s in shape:
+    nel *= s
+nb = nel * 4
+src = dev.malloc(nb, 0)
+L = lib()
+num = L.zh_compute_chunk_coords(n, i64arr(shape), i32arr(cs), i64arr([0] * n), i64arr(shape), None, 0)
+cb = (C.c_int64 * (num * n))()
+L.zh_compute_chunk_coords(n, i64arr(shape), i32arr(cs), i64arr([0] * n), i64arr(shape), cb, num)
+coords = [tuple(cb[i * n + d] for d in range(n)) for i in range(num)]
+caps = bench.chunk_capacities(meta, coords)
+offs, tot = [], 0
+for c in caps:
+    offs.append(tot)
+    tot += (c + 255) // 256 * 256
+slab = dev.malloc(tot, 0)
+outs = {}
+for rep in range(4):
+    for mode, flags, mb in (("plain", 0, 2), ("s2", 6, 2), ("s64", 6, 64), ("s256", 6, 256)):
+        os.environ["ZH_SCATTER_MB"] = str(mb)
+        outs[f"{mode}_{rep}"] = dev.malloc(nb, flags)
+dev.synth_fill(src, nel, 4, 0, bench.SEED)
+sizes = dev.array_write(meta, src, [0] * n, shape, [(slab + o, c) for o, c in zip(offs, caps)])
+plan = dev.plan(meta, [(slab + o, s) for o, s in zip(offs, sizes)], [0] * n, shape,
+                A.ZH_SRC_DEVICE | A.ZH_OUT_DEVICE)
+plan.set_timing(True)
+
+
+def dec(out):
+    plan.execute(out)
+    plan.wait()
+    plan.kernel_time()
+    plan.execute(out)
+    plan.wait()
+    return plan.kernel_time()["scatter_ms"]
+
+
+res = {k: [] for k in outs}
+for r in range(3):
+    for k, o in outs.items():
+        res[k].append(dec(o))
+g = {k: round(nb / statistics.median(v) * 1e3 / 2**30, 1) for k, v in res.items()}
+print(json.dumps({"config": cfg, "GiBps": g,
+                  "bad_verify": sum(dev.synth_verify(o, shape, [0] * n, shape, 4, bench.SEED)
+                                    for o in outs.values())}))
+for o in outs.values():
+    dev.free(o)

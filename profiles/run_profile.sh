@@ -18,11 +18,11 @@ step() {  # name, timeout, cmd...
   if [ $rc -ne 0 ]; then exit $rc; fi
 }
 step trace_c3 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace_c3" -o run -- \
-  python3 "$R/bench.py" --steps 5 --warmup 2 --no-cpu-baseline
+  python3 "$R/bench.py" --config c3 --steps 5 --warmup 2 --no-cpu-baseline
 step pmc_fetch_c3 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch_c3" -o run -- \
-  python3 "$R/bench.py" --steps 2 --warmup 1 --no-cpu-baseline
+  python3 "$R/bench.py" --config c3 --steps 2 --warmup 1 --no-cpu-baseline
 step pmc_write_c3 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write_c3" -o run -- \
-  python3 "$R/bench.py" --steps 2 --warmup 1 --no-cpu-baseline
+  python3 "$R/bench.py" --config c3 --steps 2 --warmup 1 --no-cpu-baseline
 for cfg in c4 c2; do
   step trace_$cfg 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace_$cfg" -o run -- \
     python3 "$R/bench.py" --config $cfg --steps 5 --warmup 2 --no-cpu-baseline

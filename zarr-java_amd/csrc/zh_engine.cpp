@@ -16,6 +16,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <map>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -1382,6 +1383,102 @@ int zh_array_write(zh_ctx* ctx, const zh_array_meta* m, const void* src, const i
 // =====================================================================================
 // plumbing
 // =====================================================================================
+}  // extern "C"
+
+namespace {
+// ZH_MALLOC_SCATTER allocations: VA base → (size, physical chunk handles)
+struct ScatterAlloc {
+  size_t size = 0;
+  std::vector<hipMemGenericAllocationHandle_t> handles;
+};
+std::mutex g_scatter_mu;
+std::map<void*, ScatterAlloc> g_scatter;
+
+int scatter_malloc(int device, size_t bytes, void** out) {
+  hipMemAllocationProp prop = {};
+  prop.type = hipMemAllocationTypePinned;
+  prop.location.type = hipMemLocationTypeDevice;
+  prop.location.id = device;
+  size_t gran = 0;
+  if (hipMemGetAllocationGranularity(&gran, &prop, hipMemAllocationGranularityRecommended) !=
+          hipSuccess || gran == 0)
+    return ZH_EHIP;
+  size_t chunk = (size_t)std::max(1, env_int("ZH_SCATTER_MB", 2)) << 20;
+  chunk = (chunk + gran - 1) / gran * gran;
+  const size_t n = std::max<size_t>(1, (bytes + chunk - 1) / chunk);
+  ScatterAlloc A;
+  A.size = n * chunk;
+  void* base = nullptr;
+  auto undo = [&]() {
+    for (auto h : A.handles) (void)hipMemRelease(h);
+    if (base) (void)hipMemAddressFree(base, A.size);
+    (void)hipGetLastError();
+  };
+  for (size_t i = 0; i < n; i++) {
+    hipMemGenericAllocationHandle_t h;
+    if (hipMemCreate(&h, chunk, &prop, 0) != hipSuccess) {
+      undo();
+      return ZH_ENOMEM;
+    }
+    A.handles.push_back(h);
+  }
+  if (hipMemAddressReserve(&base, A.size, chunk, nullptr, 0) != hipSuccess) {
+    base = nullptr;
+    undo();
+    return ZH_ENOMEM;
+  }
+  // virtual slot i ← physical chunk (i * m) mod n, m coprime with n (golden-ratio stride)
+  uint64_t m = ((uint64_t)((double)n * 0.6180339887498949)) | 1;
+  auto gcd = [](uint64_t x, uint64_t y) {
+    while (y) {
+      const uint64_t r = x % y;
+      x = y;
+      y = r;
+    }
+    return x;
+  };
+  while (n > 1 && gcd(m, n) != 1) m += 2;
+  for (size_t i = 0; i < n; i++) {
+    const size_t src = n > 1 ? (size_t)(((uint64_t)i * m) % n) : 0;
+    if (hipMemMap((uint8_t*)base + i * chunk, chunk, 0, A.handles[src], 0) != hipSuccess) {
+      for (size_t k = 0; k < i; k++) (void)hipMemUnmap((uint8_t*)base + k * chunk, chunk);
+      undo();
+      return ZH_EHIP;
+    }
+  }
+  hipMemAccessDesc acc = {};
+  acc.location = prop.location;
+  acc.flags = hipMemAccessFlagsProtReadWrite;
+  if (hipMemSetAccess(base, A.size, &acc, 1) != hipSuccess) {
+    (void)hipMemUnmap(base, A.size);
+    undo();
+    return ZH_EHIP;
+  }
+  std::lock_guard<std::mutex> lk(g_scatter_mu);
+  g_scatter[base] = std::move(A);
+  *out = base;
+  return ZH_OK;
+}
+
+bool scatter_free(void* ptr) {
+  ScatterAlloc A;
+  {
+    std::lock_guard<std::mutex> lk(g_scatter_mu);
+    auto it = g_scatter.find(ptr);
+    if (it == g_scatter.end()) return false;
+    A = std::move(it->second);
+    g_scatter.erase(it);
+  }
+  (void)hipDeviceSynchronize();
+  (void)hipMemUnmap(ptr, A.size);
+  for (auto h : A.handles) (void)hipMemRelease(h);
+  (void)hipMemAddressFree(ptr, A.size);
+  return true;
+}
+}  // namespace
+
+extern "C" {
+
 int zh_abi_sizes(int64_t* out, int n) {
   const int64_t s[4] = {(int64_t)sizeof(zh_codec_chain), (int64_t)sizeof(zh_array_meta),
                         (int64_t)sizeof(zh_chunk_src), (int64_t)sizeof(zh_chunk_dst)};
@@ -1398,6 +1495,10 @@ int zh_device_malloc_ex(zh_ctx* ctx, size_t bytes, unsigned flags, void** out) {
   if (!ctx || !out) return ZH_EINVAL;
   (void)hipSetDevice(ctx->device);
   hipError_t e = hipErrorOutOfMemory;
+  if (flags & ZH_MALLOC_SCATTER) {
+    const int st = scatter_malloc(ctx->device, bytes, out);
+    if (st == ZH_OK || (flags & ZH_MALLOC_REQUIRE)) return st;
+  }
   if (flags & ZH_MALLOC_CONTIGUOUS) {
     e = hipExtMallocWithFlags(out, bytes, hipDeviceMallocContiguous);
     if (e != hipSuccess) (void)hipGetLastError();
@@ -1408,6 +1509,7 @@ int zh_device_malloc_ex(zh_ctx* ctx, size_t bytes, unsigned flags, void** out) {
 int zh_device_free(zh_ctx* ctx, void* ptr) {
   if (!ctx) return ZH_EINVAL;
   (void)hipSetDevice(ctx->device);
+  if (scatter_free(ptr)) return ZH_OK;
   return hipFree(ptr) == hipSuccess ? ZH_OK : ZH_EHIP;
 }
 int zh_host_malloc_pinned(zh_ctx* ctx, size_t bytes, void** out) {

@@ -19,6 +19,7 @@ ZH_INDEX_START = 1
 ZH_SRC_DEVICE = 0x1
 ZH_MALLOC_CONTIGUOUS = 0x1
 ZH_MALLOC_REQUIRE = 0x2
+ZH_MALLOC_SCATTER = 0x4
 ZH_OUT_DEVICE = 0x2
 
 
