@@ -176,6 +176,10 @@ int zh_plan_stats(const zh_plan* plan, int64_t* in_bytes, int64_t* out_bytes,
 /* Per-kernel timing (HIP events around the scatter kernel on the launch stream).
  * enable=1 starts recording; zh_plan_kernel_time synchronises and returns the summed
  * scatter-kernel milliseconds and launch count since the last call. */
+/* Bytes the plan copies host→device per execute (0 for device sources).  With host sources a
+ * sub-shard part stages only its index + referenced inner chunks (StoreHandleDataProvider
+ * semantics, ShardingIndexedCodec.java:333-357). */
+int64_t zh_plan_staged_bytes(const zh_plan* plan);
 int zh_plan_set_timing(zh_plan* plan, int enable);
 int zh_plan_kernel_time(zh_plan* plan, double* scatter_ms, int64_t* launches,
                         double* index_ms);

@@ -311,3 +311,94 @@ def test_item_permutation_order(dev, monkeypatch, mode):
     meta = A.make_meta(shape, [32, 64, 64], 4, **kw)
     arr = rand_array(shape, 4, seed=31)
     roundtrip(dev, meta, arr, [([0, 0, 0], shape), ([3, 2, 1], [60, 61, 90])])
+
+
+def _plan_read_host(dev, meta, srcs, off, shp):
+    """zh_plan over HOST shard buffers (the mmap-style C-ABI use) → (array, staged bytes)."""
+    import ctypes as C
+    keep = [(C.c_char * max(1, len(s))).from_buffer_copy(s) if s is not None else None for s in srcs]
+    plan = dev.plan(meta, [(C.addressof(k), len(s)) if s is not None else (None, 0)
+                           for k, s in zip(keep, srcs)], off, shp, 0)
+    try:
+        staged = plan.staged_bytes()
+        out = (C.c_char * (int(np.prod(shp)) * meta.dtype_size))()
+        plan.execute(C.addressof(out))
+        plan.wait()
+        return np.frombuffer(bytes(out), np.uint32).reshape(shp), staged
+    finally:
+        plan.close()
+
+
+def _shard_meta(**kw):
+    return A.make_meta([64, 64, 64], [64, 64, 64], 4, endian=A.ZH_ENDIAN_BIG, sharded=True,
+                       inner_chunk_shape=[8, 8, 8], **kw)
+
+
+@pytest.mark.parametrize("loc", [A.ZH_INDEX_END, A.ZH_INDEX_START])
+@pytest.mark.parametrize("ibe", [False, True])
+def test_compact_staging_of_host_shards(dev, loc, ibe):
+    """Host sources, sub-shard part: the planner stages the index + referenced inner chunks
+    only (coalesced), rewriting the index; results equal the oracle's."""
+    meta = _shard_meta(index_location=loc, index_endian=A.ZH_ENDIAN_BIG if ibe else A.ZH_ENDIAN_LITTLE)
+    arr = rand_array([64, 64, 64], 4, seed=41)
+    arr[8:16, 8:16, 8:16] = 0   # one elided inner chunk inside the part
+    shard = encode_oracle(meta, arr)[0]
+    for off, shp in [([5, 5, 5], [10, 10, 10]), ([0, 0, 0], [8, 64, 64]), ([60, 3, 0], [4, 9, 64]),
+                     ([0, 0, 0], [64, 64, 32])]:
+        want = np.frombuffer(O.array_read(meta, [shard], off, shp), np.uint32).reshape(shp)
+        got, staged = _plan_read_host(dev, meta, [shard], off, shp)
+        np.testing.assert_array_equal(got, want)
+        assert staged < 0.6 * len(shard)
+    got, staged = _plan_read_host(dev, meta, [shard], [0, 0, 0], [64, 64, 64])
+    assert staged == len(shard)          # whole-shard reads keep one copy
+    np.testing.assert_array_equal(got, arr)
+
+
+def _reorder_shard(shard, meta, perm_seed):
+    """Same shard, inner chunks stored in a shuffled order (index-driven decode, Q7)."""
+    import struct
+    n_in = 512
+    isz = 16 * n_in + 4
+    idx = shard[-isz:-4]
+    ents = [struct.unpack("<QQ", idx[16 * k:16 * k + 16]) for k in range(n_in)]
+    order = np.random.default_rng(perm_seed).permutation(n_in)
+    payload, new = b"", [None] * n_in
+    for k in order:
+        off, nb = ents[k]
+        if off == 2 ** 64 - 1:
+            new[k] = (off, nb)
+            continue
+        new[k] = (len(payload), nb)
+        payload += shard[off:off + nb]
+    ib = b"".join(struct.pack("<QQ", *e) for e in new)
+    return payload + ib + struct.pack("<I", O.crc32c(ib))
+
+
+def test_compact_staging_shuffled_layout(dev):
+    meta = _shard_meta()
+    arr = rand_array([64, 64, 64], 4, seed=43)
+    shard = _reorder_shard(encode_oracle(meta, arr)[0], meta, 5)
+    for off, shp in [([9, 17, 33], [20, 30, 11]), ([0, 0, 0], [64, 8, 8])]:
+        want = np.frombuffer(O.array_read(meta, [shard], off, shp), np.uint32).reshape(shp)
+        got, staged = _plan_read_host(dev, meta, [shard], off, shp)
+        np.testing.assert_array_equal(got, want)
+        np.testing.assert_array_equal(got, arr[tuple(slice(o, o + s) for o, s in zip(off, shp))])
+        assert staged < len(shard) / 2
+
+
+def test_compact_staging_errors_match_oracle(dev):
+    meta = _shard_meta()
+    arr = rand_array([64, 64, 64], 4, seed=47)
+    shard = encode_oracle(meta, arr)[0]
+    off, shp = [1, 1, 1], [6, 6, 6]
+    bad = bytearray(shard)
+    bad[-20] ^= 0x01                      # index CRC
+    bad_off = bytearray(shard)            # entry (0,0,0) offset beyond the shard
+    bad_off[-(16 * 512 + 4):-(16 * 512 + 4) + 8] = (10 ** 9).to_bytes(8, "little")
+    bad_off[-4:] = O.crc32c(bytes(bad_off[-(16 * 512 + 4):-4])).to_bytes(4, "little")
+    for b in (bad, bad_off):
+        with pytest.raises(O.OracleError) as eo:
+            O.array_read(meta, [bytes(b)], off, shp)
+        with pytest.raises(ZhError) as ed:
+            _plan_read_host(dev, meta, [bytes(b)], off, shp)
+        assert str(ed.value) == str(eo.value)

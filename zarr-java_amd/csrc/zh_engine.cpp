@@ -185,6 +185,7 @@ struct zh_plan {
   uint8_t* d_input = nullptr;   // staged host sources
   std::vector<std::pair<int64_t, const void*>> h2d;  // (offset in d_input, host ptr)
   std::vector<int64_t> h2d_len;
+  std::vector<std::vector<uint8_t>> h_index;  // rewritten indexes of compact-staged shards
   uint8_t* d_out = nullptr;     // staging when the output is host memory
   ScatterArgs args{};
   ItemDesc* d_desc = nullptr;   // per inner-chunk descriptors (resolve kernel)
@@ -540,6 +541,112 @@ int dev_alloc(T** p, size_t count, char* err, size_t errlen) {
   return ZH_OK;
 }
 
+uint64_t ld_u64_host(const uint8_t* p, bool be) {
+  uint64_t v = 0;
+  for (int i = 0; i < 8; i++) v |= (uint64_t)p[i] << (be ? 56 - 8 * i : 8 * i);
+  return v;
+}
+
+// Host sources, single-level sharding: StoreHandleDataProvider semantics
+// (ShardingIndexedCodec.java:333-357) inside the planner.  Read the index from host memory,
+// verify its crc32c here (Crc32cCodec.java:39-44), validate the part's entries with the
+// device's messages, and plan a compact
+// device copy: a rewritten index (same endianness, entries outside the part missing) followed
+// by the referenced payloads, copied as coalesced ranges.  *compact_size = -1 keeps the
+// whole-shard copy (parts referencing over 90 % of the shard).
+struct StageRange {
+  int64_t shard, src, dst, len;  // host shard offset → offset in the compact stage
+};
+
+int compact_stage(zh_plan* p, const zh_array_meta* m, const DevShard& S, int64_t si, int64_t isz,
+                  std::vector<char>& host_checked, std::vector<StageRange>& ranges,
+                  int64_t* compact_size, char* err, size_t errlen) {
+  *compact_size = -1;
+  if (!env_int("ZH_COMPACT", 1)) return ZH_OK;  // A/B switch: whole-shard staging
+  const int n = m->ndim;
+  const ScatterArgs& g = p->args;
+  const bool be = g.index_be != 0;
+  const uint8_t* shard = (const uint8_t*)S.data;
+  const uint8_t* idx = shard + S.index_off;
+  // entries of the part's inner-chunk box, C order (the resolve kernel's enumeration)
+  int64_t nit = 1;
+  for (int d = 0; d < n; d++) nit *= S.box_count[d];
+  struct Ent {
+    uint64_t off, nb;
+    int64_t lin;
+  };
+  std::vector<Ent> ents;
+  int64_t ref_bytes = isz;
+  const uint64_t want = (uint64_t)(g.inner_nbytes + g.crc_extra);
+  int64_t ic[kMaxDims];
+  for (int64_t j = 0; j < nit; j++) {
+    int64_t q = j, lin = 0;
+    for (int d = n - 1; d >= 0; d--) {
+      ic[d] = S.box_start[d] + q % S.box_count[d];
+      q /= S.box_count[d];
+    }
+    for (int d = 0; d < n; d++) lin += ic[d] * g.cps_stride[d];
+    const uint64_t off = ld_u64_host(idx + 16 * lin, be), nb = ld_u64_host(idx + 16 * lin + 8, be);
+    if (off == ~0ull || nb == ~0ull) continue;  // Q1
+    ents.push_back({off, nb, lin});
+    ref_bytes += (int64_t)std::min<uint64_t>(nb, (uint64_t)S.nbytes);
+  }
+  // H2D is bandwidth-bound: compacting pays whenever it skips a tenth of the shard
+  if (10 * ref_bytes > 9 * S.nbytes) return ZH_OK;
+  // from here the host owns the checks the device would have made on this shard
+  if (m->chain.index_has_crc32c) {  // Crc32cCodec.decode (:24-48)
+    const uint32_t computed = crc32c_host(0, idx, (size_t)(isz - 4));
+    const uint8_t* s = idx + isz - 4;
+    const uint32_t stored = (uint32_t)s[0] | ((uint32_t)s[1] << 8) | ((uint32_t)s[2] << 16) |
+                            ((uint32_t)s[3] << 24);
+    if (computed != stored) {
+      set_err(err, errlen, "The checksum of the sharding index is invalid. Stored: %d Computed: %d",
+              (int32_t)stored, (int32_t)computed);
+      return ZH_EDATA;
+    }
+  }
+  for (const Ent& e : ents) {  // first failure in C order = the device's smallest-lin report
+    const uint64_t total = (uint64_t)S.nbytes;
+    const bool range_ok = e.off <= total && e.nb <= total - e.off;
+    if (range_ok && e.nb == want) continue;
+    int64_t q = e.lin;
+    for (int d = n - 1; d >= 0; d--) {
+      const int64_t cps = m->chunk_shape[d] / m->chain.inner_chunk_shape[d];
+      ic[d] = q % cps;
+      q /= cps;
+    }
+    if (!range_ok)  // ShardingIndexedCodec.java:227-230
+      set_err(err, errlen, "Could not load byte data for chunk %s", fmt_ints(ic, n).c_str());
+    else
+      set_err(err, errlen, "unexpected inner chunk byte length for chunk %s", fmt_ints(ic, n).c_str());
+    return ZH_EDATA;
+  }
+  // compact layout: [index][payloads in source order]; adjacent sources → one copy
+  std::sort(ents.begin(), ents.end(), [](const Ent& x, const Ent& y) { return x.off < y.off; });
+  std::vector<uint8_t> nidx((size_t)isz, 0xFF);  // entries outside the part: missing
+  int64_t pos = isz;
+  for (size_t k = 0; k < ents.size(); k++) {
+    const Ent& e = ents[k];
+    uint8_t* d = nidx.data() + 16 * e.lin;
+    for (int b = 0; b < 8; b++) {
+      const int sh = be ? 56 - 8 * b : 8 * b;
+      d[b] = (uint8_t)((uint64_t)pos >> sh);
+      d[8 + b] = (uint8_t)(e.nb >> sh);
+    }
+    if (!ranges.empty() && ranges.back().shard == si &&
+        ranges.back().src + ranges.back().len == (int64_t)e.off &&
+        ranges.back().dst + ranges.back().len == pos)
+      ranges.back().len += (int64_t)e.nb;
+    else
+      ranges.push_back({si, (int64_t)e.off, pos, (int64_t)e.nb});
+    pos += (int64_t)e.nb;
+  }
+  p->h_index.push_back(std::move(nidx));
+  host_checked[si] = 1;
+  *compact_size = pos;
+  return ZH_OK;
+}
+
 void plan_free(zh_plan* p) {
   if (!p) return;
   (void)hipSetDevice(p->ctx->device);
@@ -619,6 +726,8 @@ int zh_plan_create(zh_ctx* ctx, const zh_array_meta* m, const zh_chunk_src* chun
   int64_t cur[kMaxDims] = {0};
   int64_t items = 0, staged = 0, in_bytes = 0;
   std::vector<int64_t> stage_off(ncoords, -1);
+  std::vector<char> host_checked(ncoords, 0);  // index CRC verified on the host (compact)
+  std::vector<StageRange> compact_ranges;
   for (int64_t i = 0; i < ncoords; i++) {
     int64_t cc[kMaxDims];
     for (int d = 0; d < n; d++) cc[d] = p->coords[i * n + d] = cstart[d] + cur[d];
@@ -697,8 +806,17 @@ int zh_plan_create(zh_ctx* ctx, const zh_array_meta* m, const zh_chunk_src* chun
         in_bytes += pb;
       }
       if (!(flags & ZH_SRC_DEVICE)) {
+        int64_t compact = -1;
+        if (c.sharded && !nested) {
+          st = compact_stage(p, m, S, i, isz, host_checked, compact_ranges, &compact, err,
+                             errlen);
+          if (st != ZH_OK) {
+            plan_free(p);
+            return st;
+          }
+        }
         stage_off[i] = staged;
-        staged += (S.nbytes + 255) & ~(int64_t)255;
+        staged += ((compact >= 0 ? compact : S.nbytes) + 255) & ~(int64_t)255;
       }
     }
   }
@@ -714,10 +832,26 @@ int zh_plan_create(zh_ctx* ctx, const zh_array_meta* m, const zh_chunk_src* chun
       plan_free(p);
       return st;
     }
+    size_t rk = 0, ik = 0;
     for (int64_t i = 0; i < ncoords; i++) {
       if (stage_off[i] < 0) continue;
-      p->h2d.push_back({stage_off[i], hs[i].data});
-      p->h2d_len.push_back(hs[i].nbytes);
+      if (host_checked[i]) {  // compact shard: rewritten index + the referenced ranges
+        p->h2d.push_back({stage_off[i], p->h_index[ik].data()});
+        p->h2d_len.push_back((int64_t)p->h_index[ik].size());
+        ik++;
+        int64_t total = isz;
+        for (; rk < compact_ranges.size() && compact_ranges[rk].shard == i; rk++) {
+          const StageRange& R = compact_ranges[rk];
+          p->h2d.push_back({stage_off[i] + R.dst, (const uint8_t*)hs[i].data + R.src});
+          p->h2d_len.push_back(R.len);
+          total = std::max(total, R.dst + R.len);
+        }
+        hs[i].nbytes = total;
+        hs[i].index_off = 0;
+      } else {
+        p->h2d.push_back({stage_off[i], hs[i].data});
+        p->h2d_len.push_back(hs[i].nbytes);
+      }
       hs[i].data = p->d_input + stage_off[i];
     }
   }
@@ -754,7 +888,7 @@ int zh_plan_create(zh_ctx* ctx, const zh_array_meta* m, const zh_chunk_src* chun
   if (c.sharded && c.index_has_crc32c) {
     int64_t spans = 0;
     for (int64_t i = 0; i < ncoords; i++) {
-      if (!hs[i].data) continue;
+      if (!hs[i].data || host_checked[i]) continue;
       CrcJob J;
       J.base = hs[i].data + hs[i].index_off;
       J.len = isz - 4;
@@ -981,6 +1115,13 @@ int zh_plan_stats(const zh_plan* p, int64_t* in_bytes, int64_t* out_bytes, int64
   if (items) *items = p->n_items;
   if (nshards) *nshards = p->nshards;
   return ZH_OK;
+}
+
+int64_t zh_plan_staged_bytes(const zh_plan* p) {
+  if (!p) return -1;
+  int64_t t = 0;
+  for (int64_t l : p->h2d_len) t += l;
+  return t;
 }
 
 int zh_plan_set_timing(zh_plan* p, int enable) {

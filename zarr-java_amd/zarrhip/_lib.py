@@ -50,6 +50,7 @@ _SIGS = {
     "zh_array_write": (C.c_int, [P, PMETA, P, PI64, PI64, C.POINTER(A.zh_chunk_dst), I64, P, CH,
                                  SZ]),
     "zh_abi_sizes": (C.c_int, [C.POINTER(C.c_int64), C.c_int]),
+    "zh_plan_staged_bytes": (C.c_int64, [P]),
     "zh_blosc_decompress": (C.c_int, [P, SZ, P, SZ, C.POINTER(SZ), C.c_char_p, SZ]),
     "zh_device_malloc": (C.c_int, [P, SZ, C.POINTER(P)]),
     "zh_device_malloc_ex": (C.c_int, [P, SZ, C.c_uint, C.POINTER(P)]),
@@ -299,6 +300,9 @@ class Plan:
 
     def set_timing(self, on=True):
         check(self.L.zh_plan_set_timing(self.h, 1 if on else 0))
+
+    def staged_bytes(self):
+        return int(self.L.zh_plan_staged_bytes(self.h))
 
     def kernel_time(self):
         sc, ix, n = C.c_double(), C.c_double(), C.c_int64()
