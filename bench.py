@@ -13,7 +13,7 @@ of all 32 shards / 786,432 in-bounds inner chunks: index CRC + index parse + byt
 on the device and encoded by the product's own write path (zh_array_write); after warmup
 the decoded array is verified element-by-element on the device against the generator.
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--config c4|c3|c2|c3crc|c3nest]
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--config c4|c3|c2|c3crc|c4crc|c3nest]
 
 N>1 (launched by torch.distributed.run): every rank decodes its own full-size array on its
 own GPU (weak scaling, no data-path collective: shards are independent objects); the
@@ -41,6 +41,8 @@ CONFIGS = {
     # §8(f) rank-2 workloads (not the headline): same array and shards
     "c3crc": ("c3 with inner codecs [bytes(big), crc32c] (per-chunk checksum verified)", True,
               None, dict(inner_crc32c=True)),
+    "c4crc": ("c4 with inner codecs [transpose [0,3,2,1], bytes(big), crc32c] (per-chunk "
+              "checksum verified)", True, [0, 3, 2, 1], dict(inner_crc32c=True)),
     "c3nest": ("nested sharding: shard 1x1024^3 -> 1x256x256x256 sub-shards -> 1x32x32x32 "
                "leaves, bytes(big); both indexes [bytes(little), crc32c] at end", True, None,
                dict(nested=True)),

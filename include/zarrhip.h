@@ -61,11 +61,13 @@ enum zh_index_location { ZH_INDEX_END = 0, ZH_INDEX_START = 1 };
  * Codec chain the device path executes.  Mirrors the JSON `codecs` list of a v3 array
  * (v3/ArrayMetadata.java) restricted to the device-supported chains:
  *   sharded = 0 :  [transpose?, bytes]                          (BASELINE config 2)
- *   sharded = 1 :  [sharding_indexed{ codecs=[transpose?, bytes],
+ *   sharded = 1 :  [sharding_indexed{ codecs=[transpose?, bytes, crc32c?],
  *                                     index_codecs=[bytes, crc32c?],
  *                                     index_location }]          (configs 3, 4, 5)
- * Anything else (blosc/gzip/zstd inside the chain, nested sharding, array-level codecs
- * next to sharding) is rejected with ZH_EUNSUPPORTED so the caller keeps the Java path.
+ *   plus one nested sharding_indexed level as the sole inner codec (nested* fields) and a
+ *   trailing chunk crc32c (inner_crc32c).  Anything else (blosc/gzip/zstd inside the chain,
+ *   array-level codecs next to sharding) is rejected with ZH_EUNSUPPORTED so the caller
+ *   keeps the Java path (host byte-to-byte stages: INTEGRATION.md §3).
  */
 typedef struct zh_codec_chain {
   int32_t sharded;                          /* 1: outer codec is sharding_indexed              */
@@ -231,6 +233,10 @@ int zh_device_malloc_ex(zh_ctx* ctx, size_t bytes, unsigned flags, void** out);
 int zh_device_free(zh_ctx* ctx, void* ptr);
 int zh_host_malloc_pinned(zh_ctx* ctx, size_t bytes, void** out);
 int zh_host_free_pinned(zh_ctx* ctx, void* ptr);
+/* Page-lock caller-owned host memory (hipHostRegister), e.g. one rank's slice of a region
+ * buffer shared by the processes of a multi-GPU read, so that its D2H runs at pinned rate. */
+int zh_host_register(zh_ctx* ctx, void* ptr, size_t bytes);
+int zh_host_unregister(zh_ctx* ctx, void* ptr);
 /* kind: 0 H2D, 1 D2H, 2 D2D; asynchronous on stream */
 int zh_memcpy_async(zh_ctx* ctx, void* dst, const void* src, size_t bytes, int kind, void* stream);
 int zh_memset_async(zh_ctx* ctx, void* dst, int value, size_t bytes, void* stream);

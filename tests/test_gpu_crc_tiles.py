@@ -1,0 +1,78 @@
+"""Chunk crc32c fused into the transpose tile kernel (decode_tiles_kernel<..., CRC=true>):
+[transpose, bytes(big), crc32c] inner chains whose unclipped uint32 chunks take the 32x32
+LDS-tile fast path.  Bit-exact against the oracle (decoded values, mismatch message) across
+piece splits and transpose orders, with an elided inner chunk, a missing shard and a clipped
+region (slow items keep the standalone CRC pass)."""
+import numpy as np
+import pytest
+
+import oracle as O
+from helpers import chunk_coords, device_read, encode_oracle, rand_array
+from zarrhip import _abi as A
+from zarrhip._lib import ZhError
+
+pytestmark = pytest.mark.gpu
+
+SHAPE = [64, 64, 96]
+CHUNK = 32 * 32 * 32 * 4 + 4  # stored inner chunk: payload + crc32c
+
+
+def _meta(order):
+    return A.make_meta(SHAPE, [32, 64, 64], 4, endian=A.ZH_ENDIAN_BIG, sharded=True,
+                       inner_chunk_shape=[32, 32, 32], transpose_order=order, inner_crc32c=True)
+
+
+def _read_both(dev, meta, shards, off, shp):
+    sel = chunk_coords(meta, off, shp)
+    pos = {c: i for i, c in enumerate(chunk_coords(meta, [0, 0, 0], SHAPE))}
+    srcs = [shards[pos[c]] for c in sel]
+    want = np.frombuffer(O.array_read(meta, srcs, off, shp), np.uint32).reshape(shp)
+    return device_read(dev, meta, srcs, off, shp), want
+
+
+def _corrupt_matches_oracle(dev, meta, shards, k, pos):
+    bad = bytearray(shards[k])
+    bad[pos] ^= 0x20
+    srcs = list(shards)
+    srcs[k] = bytes(bad)
+    with pytest.raises(O.OracleError) as eo:
+        O.array_read(meta, srcs, [0, 0, 0], SHAPE)
+    with pytest.raises(ZhError) as ed:
+        device_read(dev, meta, srcs, [0, 0, 0], SHAPE)
+    assert str(ed.value) == str(eo.value)
+
+
+@pytest.mark.parametrize("order", [[0, 2, 1], [2, 0, 1], [1, 2, 0], [2, 1, 0]])
+@pytest.mark.parametrize("piece_kb", [128, 16, 4])
+@pytest.mark.parametrize("fuse", ["1", "0"])
+def test_chunk_crc32c_fused_tile_kernel(dev, monkeypatch, order, piece_kb, fuse):
+    monkeypatch.setenv("ZH_PIECE_KB", str(piece_kb))
+    monkeypatch.setenv("ZH_CRC_FUSE", fuse)
+    meta = _meta(order)
+    arr = rand_array(SHAPE, 4, seed=41)
+    arr[0:32, 0:32, 0:32] = 0     # an elided inner chunk (Q1 zeros)
+    shards = encode_oracle(meta, arr)
+    shards[3] = None              # a missing shard (fill)
+    for off, shp in [([0, 0, 0], SHAPE), ([5, 3, 7], [50, 60, 80])]:
+        got, want = _read_both(dev, meta, shards, off, shp)
+        np.testing.assert_array_equal(got, want)
+    _corrupt_matches_oracle(dev, meta, shards, 0, 70000)  # first stored chunk: a fast item
+
+
+@pytest.mark.parametrize("variant", ["0", "1"])
+@pytest.mark.parametrize("perm", ["0", "1"])
+def test_tile_crc_variants_and_item_order(dev, monkeypatch, variant, perm):
+    """Row-per-tile variant (ZH_TILE_VARIANT=0: the CRC stays a separate pass) and the
+    golden-ratio item order on/off give the same bytes; corruption of the last payload byte
+    of a shard's last inner chunk is caught."""
+    monkeypatch.setenv("ZH_TILE_VARIANT", variant)
+    monkeypatch.setenv("ZH_ITEM_PERM", perm)
+    monkeypatch.setenv("ZH_PIECE_KB", "32")
+    meta = _meta([2, 1, 0])
+    arr = rand_array(SHAPE, 4, seed=43)
+    shards = encode_oracle(meta, arr)
+    got, want = _read_both(dev, meta, shards, [0, 0, 0], SHAPE)
+    np.testing.assert_array_equal(got, want)
+    np.testing.assert_array_equal(got, arr)
+    # shard (1,0,0) holds 4 inner chunks; flip a bit of the 4th one's last payload byte
+    _corrupt_matches_oracle(dev, meta, shards, 2, 3 * CHUNK + CHUNK - 5)

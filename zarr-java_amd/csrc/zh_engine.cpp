@@ -93,6 +93,30 @@ uint32_t crc32c_host(uint32_t crc, const uint8_t* p, size_t n) {
   return c ^ 0xFFFFFFFFu;
 }
 
+// GF(2) arithmetic mod the reflected CRC-32C polynomial (the device's multmodp/x2nmodp):
+// a(x)·b(x) mod P, and x^(8n) mod P = the shift of a raw CRC register past n zero bytes.
+uint32_t gf2_mulmod(uint32_t a, uint32_t b) {
+  uint32_t m = 1u << 31, p = 0;
+  for (;;) {
+    if (a & m) {
+      p ^= b;
+      if ((a & (m - 1)) == 0) break;
+    }
+    m >>= 1;
+    b = (b & 1) ? (b >> 1) ^ 0x82F63B78u : b >> 1;
+  }
+  return p;
+}
+uint32_t gf2_xpow8n(uint64_t n) {
+  uint32_t p = 1u << 31, sq = 1u << 23;  // x^0, x^8 (reflected)
+  while (n) {
+    if (n & 1) p = gf2_mulmod(sq, p);
+    sq = gf2_mulmod(sq, sq);
+    n >>= 1;
+  }
+  return p;
+}
+
 // ---- IndexingUtils (M/utils/IndexingUtils.java) ----
 int64_t chunk_coords(int n, const int32_t* chunk, const int64_t* off, const int64_t* shp,
                      int64_t* start, int64_t* count) {
@@ -924,6 +948,24 @@ int zh_plan_create(zh_ctx* ctx, const zh_array_meta* m, const zh_chunk_src* chun
     return ZH_EHIP;
   }
   std::vector<uint32_t> tab = setup_fast(m, p->args, p->tile_mode);
+  p->args.tile_variant = std::min(1, std::max(0, env_int("ZH_TILE_VARIANT", 1)));
+  // Chunk CRC fused into the row-interleaved tile kernel: every payload byte of a fast item
+  // is loaded exactly once by some lane, and each lane's share is shifted to the payload end
+  // by K[u] = x^(8(L − E_u)) (E_u = end of unit u's last row, appended to the table) and a
+  // lane constant.  Dynamic LDS (table, 8 tiles, CRC tables, K) stays within 64 KiB.
+  const bool tile_crc =
+      c.inner_crc32c && items > 0 && p->tile_mode && p->args.fast_mode == kFastTileTable &&
+      p->args.tile_variant == 1 && env_int("ZH_CRC_FUSE", 1) != 0 &&
+      ((int64_t)p->args.fast_n * 8 + 15) / 16 * 16 + 8 * 1057 * 4 + 12 * 256 * 4 +
+              (int64_t)p->args.fast_n * 4 <= 65536;
+  if (tile_crc) {
+    const ScatterArgs& g = p->args;
+    const int64_t L = g.inner_nbytes, s_fd = g.pstride[g.fd];
+    for (int32_t u = 0; u < g.fast_n; u++) {
+      const int64_t end = 4 * (int64_t)tab[2 * (size_t)u] + 4 * 31 * s_fd + 128;
+      tab.push_back(gf2_xpow8n((uint64_t)(L - end)));
+    }
+  }
   if ((st = dev_alloc(&p->d_desc, (size_t)items, err, errlen)) != ZH_OK ||
       (st = dev_alloc(&p->d_slow, (size_t)items + 4, err, errlen)) != ZH_OK ||
       (st = dev_alloc(&p->d_fast_tab, tab.size(), err, errlen)) != ZH_OK) {
@@ -939,7 +981,8 @@ int zh_plan_create(zh_ctx* ctx, const zh_array_meta* m, const zh_chunk_src* chun
   if (c.inner_crc32c && items > 0) {
     // Fuse the chunk CRC into the row kernel when its lanes read each piece's payload in
     // the CRC pass's order: rows sequential in the payload (pstride[F] == 1, row dims in
-    // C order) and equal pieces of whole 4 KiB rounds (256 lanes x 16 B).
+    // C order) and equal pieces of whole 4 KiB rounds (256 lanes x 16 B); or into the tile
+    // kernel (tile_crc above: one partial per chunk).
     ScatterArgs& g = p->args;
     const int64_t pieces = 1ll << g.piece_shift;
     bool fuse = !p->tile_mode && env_int("ZH_CRC_FUSE", 1) != 0 &&
@@ -956,7 +999,9 @@ int zh_plan_create(zh_ctx* ctx, const zh_array_meta* m, const zh_chunk_src* chun
       fuse = fuse && g.inner_nbytes % pieces == 0 && (g.inner_nbytes / pieces) % 4096 == 0 &&
              g.fast_rows % pieces == 0;
     }
-    const int64_t span = fuse ? g.inner_nbytes / pieces : (int64_t)kCrcSpan;
+    const int64_t span = tile_crc ? g.inner_nbytes
+                                  : (fuse ? g.inner_nbytes / pieces : (int64_t)kCrcSpan);
+    fuse = fuse || tile_crc;
     const int64_t nspan = (g.inner_nbytes + span - 1) / span;
     if ((st = dev_alloc(&p->d_dcrc, (size_t)(items * nspan), err, errlen)) != ZH_OK) {
       plan_free(p);
@@ -991,7 +1036,6 @@ int zh_plan_create(zh_ctx* ctx, const zh_array_meta* m, const zh_chunk_src* chun
   // non-temporal loads + stores: +4 % on the row path, +1 % on the tile path (interleaved
   // A/B in one process, profiles/r01/experiments/tune_*.json)
   p->args.nt = env_int("ZH_NT", 3) & 3;
-  p->args.tile_variant = std::min(1, std::max(0, env_int("ZH_TILE_VARIANT", 1)));
   // Visit items in a golden-ratio stride order: +3.6 % on the tile path (c4) on every normal
   // allocation, neutral on the row path (interleaved A/B, profiles/placement_perm.py), so
   // on by default for tiles.  ZH_ITEM_PERM=0/1 overrides.
@@ -1661,6 +1705,16 @@ int zh_host_malloc_pinned(zh_ctx* ctx, size_t bytes, void** out) {
 int zh_host_free_pinned(zh_ctx* ctx, void* ptr) {
   if (!ctx) return ZH_EINVAL;
   return hipHostFree(ptr) == hipSuccess ? ZH_OK : ZH_EHIP;
+}
+int zh_host_register(zh_ctx* ctx, void* ptr, size_t bytes) {
+  if (!ctx || !ptr) return ZH_EINVAL;
+  (void)hipSetDevice(ctx->device);
+  return hipHostRegister(ptr, bytes, hipHostRegisterDefault) == hipSuccess ? ZH_OK : ZH_EHIP;
+}
+int zh_host_unregister(zh_ctx* ctx, void* ptr) {
+  if (!ctx || !ptr) return ZH_EINVAL;
+  (void)hipSetDevice(ctx->device);
+  return hipHostUnregister(ptr) == hipSuccess ? ZH_OK : ZH_EHIP;
 }
 int zh_memcpy_async(zh_ctx* ctx, void* dst, const void* src, size_t bytes, int kind,
                     void* stream) {

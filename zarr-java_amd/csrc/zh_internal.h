@@ -122,8 +122,11 @@ struct ScatterArgs {
   uint64_t item_mul;            // fast kernels visit items in the order (i * item_mul) mod
                                 // total_items (coprime; 0 = identity): decorrelates the
                                 // addresses written concurrently (DESIGN §4 placement)
-  int32_t crc_fused;            // row kernel also computes the chunk CRC (per-piece partials)
-  uint32_t* crc_partials;       // raw CRC register per (chunk, piece) = per item, XOR-accumulated
+  int32_t crc_fused;            // the fast kernel also computes the chunk CRC: row kernel per
+                                // piece; tile kernel per chunk (shares shifted to the payload
+                                // end, per-unit shifts after the (src, dst) pairs of fast_tab)
+  uint32_t* crc_partials;       // raw CRC registers, XOR-accumulated: per item (rows) or per
+                                // chunk (tiles)
 };
 
 // Chunk-payload CRC-32C pass (inner crc32c codec): one workgroup per (item, 64 KiB span) of

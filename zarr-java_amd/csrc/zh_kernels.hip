@@ -762,59 +762,6 @@ constexpr int kFastTPB = 4;
 constexpr int kTG = 8;           // tiles per group
 constexpr int kTilePitch = 1057; // words per LDS tile (32 x 33 + 1)
 
-template <int NT>
-__device__ __forceinline__ void fast_tiles_rows(const ScatterArgs& a, const uint2* tab,
-                                                const uint8_t* src, uint8_t* dst,
-                                                uint32_t piece, uint32_t* lds) {
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int t = lane >> 3, g = lane & 7;
-  const int64_t s_fd = a.pstride[a.fd], d_fs = a.rstride[a.fs];
-  const uint32_t units = (uint32_t)a.fast_n, pieces = 1u << a.piece_shift;
-  const uint32_t u0 = (uint32_t)(((uint64_t)units * piece) / pieces);
-  const uint32_t u1 = (uint32_t)(((uint64_t)units * (piece + 1)) / pieces);
-  uint32_t* mine = lds + t * kTilePitch;
-  uint4 x[8];
-  auto load = [&](uint32_t ub) {
-    const uint32_t u = ub + t;
-    if (u < u1) {
-      const uint8_t* base = src + ((size_t)tab[u].x + g * 4) * 4;
-#pragma unroll
-      for (int k = 0; k < 8; k++)
-        x[k] = ld16s<(NT & 1) != 0>(base + (size_t)(wave * 8 + k) * s_fd * 4);
-    }
-  };
-  if (u0 < u1) load(u0);
-  for (uint32_t ub = u0; ub < u1; ub += kTG) {
-    const bool live = ub + t < u1;
-    if (live) {
-#pragma unroll
-      for (int k = 0; k < 8; k++) {
-        uint32_t* row = mine + (wave * 8 + k) * 33 + g * 4;
-        row[0] = xform1<4>(x[k].x, a.swap, 0);
-        row[1] = xform1<4>(x[k].y, a.swap, 0);
-        row[2] = xform1<4>(x[k].z, a.swap, 0);
-        row[3] = xform1<4>(x[k].w, a.swap, 0);
-      }
-    }
-    __syncthreads();
-    if (ub + kTG < u1) load(ub + kTG);
-    if (live) {
-      uint8_t* base = dst + ((size_t)tab[ub + t].y + g * 4) * 4;
-#pragma unroll
-      for (int k = 0; k < 8; k++) {
-        const int r = wave * 8 + k;
-        uint4 y;
-        y.x = mine[(g * 4 + 0) * 33 + r];
-        y.y = mine[(g * 4 + 1) * 33 + r];
-        y.z = mine[(g * 4 + 2) * 33 + r];
-        y.w = mine[(g * 4 + 3) * 33 + r];
-        st16s<(NT & 2) != 0>(base + (size_t)r * d_fs * 4, y);
-      }
-    }
-    __syncthreads();
-  }
-}
-
 template <int DS, bool TILE>
 __device__ __forceinline__ void generic_item(const ScatterArgs& a, Item& it,
                                              typename ElemT<DS>::T (*tile)[32][33]) {
@@ -1082,16 +1029,119 @@ __global__ __launch_bounds__(kBlock) void decode_rows_kernel(ScatterArgs a) {
   }
 }
 
+// Row-interleaved tile path (see kTG above).  With CRC (inner crc32c fused): lane (w, t, g)
+// holds the payload vectors at bytes P_k = 4·tab[u].x + 4·(8w + k)·s_fd + 16g, k = 0..7,
+// a constant gap G = 4·s_fd − 16 apart, so its raw register over [v0, G zeros, v1, …, v7]
+// is acc = upd16(shift_G(acc), v_k).  Shifted to the payload end it contributes
+// acc · x^(8(L − P_7 − 16)) to the chunk's raw CRC (CRC is linear over GF(2)), and
+// L − P_7 − 16 = (L − E_u) + B_lane, E_u = the end of unit u's last payload row.  The host
+// table gives K[u] = x^(8(L − E_u)); the caller applies the lane constant x^(8·B_lane) once
+// per piece.  Returns the lane's share (zero without CRC).
+template <int NT, bool CRC>
+__device__ __forceinline__ uint32_t fast_tiles_rows(const ScatterArgs& a, const uint2* tab,
+                                                    const uint8_t* src, uint8_t* dst,
+                                                    uint32_t piece, uint32_t* lds,
+                                                    const uint32_t (*T)[256],
+                                                    const uint32_t (*S)[256],
+                                                    const uint32_t* K) {
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int t = lane >> 3, g = lane & 7;
+  const int64_t s_fd = a.pstride[a.fd], d_fs = a.rstride[a.fs];
+  const uint32_t units = (uint32_t)a.fast_n, pieces = 1u << a.piece_shift;
+  const uint32_t u0 = (uint32_t)(((uint64_t)units * piece) / pieces);
+  const uint32_t u1 = (uint32_t)(((uint64_t)units * (piece + 1)) / pieces);
+  uint32_t* mine = lds + t * kTilePitch;
+  uint32_t share = 0;
+  uint4 x[8];
+  auto load = [&](uint32_t ub) {
+    const uint32_t u = ub + t;
+    if (u < u1) {
+      const uint8_t* base = src + ((size_t)tab[u].x + g * 4) * 4;
+#pragma unroll
+      for (int k = 0; k < 8; k++)
+        x[k] = ld16s<(NT & 1) != 0>(base + (size_t)(wave * 8 + k) * s_fd * 4);
+    }
+  };
+  if (u0 < u1) load(u0);
+  for (uint32_t ub = u0; ub < u1; ub += kTG) {
+    const bool live = ub + t < u1;
+    if (live) {
+#pragma unroll
+      for (int k = 0; k < 8; k++) {
+        uint32_t* row = mine + (wave * 8 + k) * 33 + g * 4;
+        row[0] = xform1<4>(x[k].x, a.swap, 0);
+        row[1] = xform1<4>(x[k].y, a.swap, 0);
+        row[2] = xform1<4>(x[k].z, a.swap, 0);
+        row[3] = xform1<4>(x[k].w, a.swap, 0);
+      }
+    }
+    __syncthreads();
+    uint4 xc[8];  // raw payload vectors of this group, kept for the CRC
+    if constexpr (CRC) {
+#pragma unroll
+      for (int k = 0; k < 8; k++) xc[k] = x[k];
+    }
+    if (ub + kTG < u1) load(ub + kTG);
+    if (live) {
+      uint8_t* base = dst + ((size_t)tab[ub + t].y + g * 4) * 4;
+#pragma unroll
+      for (int k = 0; k < 8; k++) {
+        const int r = wave * 8 + k;
+        uint4 y;
+        y.x = mine[(g * 4 + 0) * 33 + r];
+        y.y = mine[(g * 4 + 1) * 33 + r];
+        y.z = mine[(g * 4 + 2) * 33 + r];
+        y.w = mine[(g * 4 + 3) * 33 + r];
+        st16s<(NT & 2) != 0>(base + (size_t)r * d_fs * 4, y);
+      }
+    }
+    if constexpr (CRC) {
+      if (live) {
+        uint32_t acc = 0;
+#pragma unroll
+        for (int k = 0; k < 8; k++) {
+          const v4u w = {xc[k].x, xc[k].y, xc[k].z, xc[k].w};
+          acc = crc_upd16(k ? crc_shift_tab(acc, S) : acc, w, T);
+        }
+        share ^= multmodp(K[ub + t], acc);
+      }
+    }
+    __syncthreads();
+  }
+  return share;
+}
+
 // decode, fast tile kernel: unclipped aligned uint32 copies through 32x32 LDS tiles whose
-// origins come from the LDS table
-template <int NT, int VARIANT>
+// origins come from the LDS table.  CRC: the chunk CRC is fused (row-interleaved variant);
+// each wave XORs its lanes' shares, already shifted to the payload end, into the chunk's
+// partial, which data_crc_finalize_kernel compares with the stored value.
+template <int NT, int VARIANT, bool CRC = false>
 __global__ __launch_bounds__(kBlock) void decode_tiles_kernel(ScatterArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   uint2* tab = reinterpret_cast<uint2*>(smem);
-  uint32_t(*tile)[32][33] =
-      reinterpret_cast<uint32_t(*)[32][33]>(smem + (((size_t)a.fast_n * 8 + 15) & ~(size_t)15));
+  uint8_t* after_tab = smem + (((size_t)a.fast_n * 8 + 15) & ~(size_t)15);
+  uint32_t(*tile)[32][33] = reinterpret_cast<uint32_t(*)[32][33]>(after_tab);
   for (int i = threadIdx.x; i < a.fast_n; i += kBlock)
     tab[i] = reinterpret_cast<const uint2*>(a.fast_tab)[i];
+  uint32_t(*T)[256] = nullptr;
+  uint32_t(*S)[256] = nullptr;
+  uint32_t* K = nullptr;
+  uint32_t kb = 0;
+  if constexpr (CRC) {
+    // slicing tables, the zero-shift by the row gap G, the per-unit end shifts (host table
+    // after the (src, dst) pairs) and this lane's constant x^(8·B_lane)
+    T = reinterpret_cast<uint32_t(*)[256]>(after_tab + (size_t)kTG * kTilePitch * 4);
+    S = T + 8;
+    K = reinterpret_cast<uint32_t*>(S + 4);
+    init_crc_tables(T);
+    const int64_t s_fd = a.pstride[a.fd];
+    const uint32_t kg = x2nmodp((uint64_t)(4 * s_fd - 16), 3);
+#pragma unroll
+    for (int b = 0; b < 4; b++) S[b][threadIdx.x] = multmodp(kg, (uint32_t)threadIdx.x << (8 * b));
+    for (int i = threadIdx.x; i < a.fast_n; i += kBlock) K[i] = a.fast_tab[2 * a.fast_n + i];
+    const int w = threadIdx.x >> 6, g = threadIdx.x & 7;
+    kb = x2nmodp((uint64_t)(4 * (24 - 8 * w) * s_fd + 112 - 16 * g), 3);
+  }
   __syncthreads();
   const int64_t total = a.total_items;
   const uint32_t pmask = (1u << a.piece_shift) - 1;
@@ -1105,11 +1155,19 @@ __global__ __launch_bounds__(kBlock) void decode_tiles_kernel(ScatterArgs a) {
     if (D.kind & kDescFast) {
       const uint8_t* src = (const uint8_t*)(uintptr_t)D.src;
       uint8_t* dst = a.region + D.d0 * 4;
-      if constexpr (VARIANT == 0)
+      if constexpr (VARIANT == 0) {
         fast_tiles<kFastTPB, NT>(a, tab, src, dst, (uint32_t)pitem(a, item) & pmask, tile);
-      else
-        fast_tiles_rows<NT>(a, tab, src, dst, (uint32_t)pitem(a, item) & pmask,
-                            reinterpret_cast<uint32_t*>(tile));
+      } else {
+        const int64_t pi = pitem(a, item);
+        const uint32_t share = fast_tiles_rows<NT, CRC>(a, tab, src, dst, (uint32_t)pi & pmask,
+                                                        reinterpret_cast<uint32_t*>(tile), T, S, K);
+        if constexpr (CRC) {
+          uint32_t c = multmodp(kb, share);
+#pragma unroll
+          for (int o = 32; o > 0; o >>= 1) c ^= (uint32_t)__shfl_xor((int)c, o, 64);
+          if ((threadIdx.x & 63) == 0) atomicXor(a.crc_partials + (pi >> a.piece_shift), c);
+        }
+      }
     }
     D = Dn;
   }
@@ -1660,7 +1718,11 @@ static void launch_scatter_ds(const ScatterArgs& a, int tile, int enc, int grid,
         const int v = a.tile_variant;
         lds += v == 0 ? (size_t)kFastTPB * 32 * 33 * 4 : (size_t)kTG * kTilePitch * 4;
         const bool ntx = nt == 3;
-        if (v == 1) {
+        if (v == 1 && a.crc_fused) {
+          lds += 12 * 256 * 4 + (size_t)a.fast_n * 4;  // T[8][256] + S[4][256] + K[fast_n]
+          if (ntx) hipLaunchKernelGGL((decode_tiles_kernel<3, 1, true>), dim3(grid), dim3(kBlock), lds, s, a);
+          else hipLaunchKernelGGL((decode_tiles_kernel<0, 1, true>), dim3(grid), dim3(kBlock), lds, s, a);
+        } else if (v == 1) {
           if (ntx) hipLaunchKernelGGL((decode_tiles_kernel<3, 1>), dim3(grid), dim3(kBlock), lds, s, a);
           else hipLaunchKernelGGL((decode_tiles_kernel<0, 1>), dim3(grid), dim3(kBlock), lds, s, a);
         } else {

@@ -57,6 +57,8 @@ _SIGS = {
     "zh_device_free": (C.c_int, [P, P]),
     "zh_host_malloc_pinned": (C.c_int, [P, SZ, C.POINTER(P)]),
     "zh_host_free_pinned": (C.c_int, [P, P]),
+    "zh_host_register": (C.c_int, [P, P, SZ]),
+    "zh_host_unregister": (C.c_int, [P, P]),
     "zh_memcpy_async": (C.c_int, [P, P, P, SZ, C.c_int, P]),
     "zh_memset_async": (C.c_int, [P, P, C.c_int, SZ, P]),
     "zh_stream_synchronize": (C.c_int, [P, P]),
@@ -163,6 +165,13 @@ class DeviceContext:
     def free_pinned(self, ptr):
         if ptr:
             self.L.zh_host_free_pinned(self.h, P(ptr))
+
+    def host_register(self, ptr, nbytes):
+        check(self.L.zh_host_register(self.h, P(ptr), int(nbytes)))
+
+    def host_unregister(self, ptr):
+        if ptr:
+            self.L.zh_host_unregister(self.h, P(ptr))
 
     def memcpy(self, dst, src, nbytes, kind, stream=None, sync=True):
         check(self.L.zh_memcpy_async(self.h, P(dst), P(src), int(nbytes), int(kind), P(stream)))
