@@ -257,6 +257,86 @@ def cpu_baseline(dev, A, meta, shard_ptr, shard_nbytes, budget_s=12.0):
                       f"chunks), {total_t:.1f} s"}
 
 
+def host_terminated(args, dist, dev, plan, out, out_bytes, shape, so, ss, rank, ws):
+    """Host-terminated multi-GPU read (no gather): each rank decodes its slab and
+    copies it D2H into ITS slice of one host buffer that holds the whole region (POSIX shared
+    memory mapped by every rank; the slabs are contiguous in C order), so N GPUs drive N PCIe
+    links at once.  Each rank page-locks only its own slice (zh_host_register).  Falls back
+    to a private pinned slab per rank when /dev/shm cannot hold the region.  Timed: barrier,
+    K x (decode + D2H) on the plan's stream, sync, max over ranks; D2H alone timed likewise."""
+    import mmap
+    from zarrhip.parallel import slab_byte_offset
+    full = 4
+    for s in shape:
+        full *= s
+    off = slab_byte_offset(shape, so, 4)
+    name = f"/dev/shm/zh_region_{os.environ.get('MASTER_PORT', 'solo')}_{os.getuid()}"
+    try:
+        vfs = os.statvfs("/dev/shm")
+        shared = vfs.f_bavail * vfs.f_frsize >= full + (1 << 30)
+    except OSError:
+        shared = False
+    mm = cbuf = None
+    reg = 0
+    if shared:
+        if rank == 0:
+            fd = os.open(name, os.O_RDWR | os.O_CREAT | os.O_TRUNC, 0o600)
+            os.ftruncate(fd, full)
+            os.close(fd)
+        dist.barrier()
+        fd = os.open(name, os.O_RDWR)
+        mm = mmap.mmap(fd, full, mmap.MAP_SHARED, mmap.PROT_READ | mmap.PROT_WRITE)
+        os.close(fd)
+        cbuf = C.c_char.from_buffer(mm)
+        base = C.addressof(cbuf)
+        dst = base + off
+        reg = dst & ~4095
+        dev.host_register(reg, ((dst + out_bytes + 4095) & ~4095) - reg)
+        kind = "one region buffer in /dev/shm shared by the ranks; each pins its slice"
+    else:
+        dst = dev.malloc_pinned(out_bytes)
+        kind = "private pinned slab per rank (/dev/shm too small for the region)"
+    for _ in range(max(1, args.warmup)):
+        plan.execute(out)
+        dev.memcpy(dst, out, out_bytes, 1, None, False)
+    plan.wait()
+    dist.barrier()
+    dev.sync()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        plan.execute(out)
+        dev.memcpy(dst, out, out_bytes, 1, None, False)
+    plan.wait()
+    dev.sync()
+    t = dist.max(time.perf_counter() - t0)
+    dist.barrier()
+    t1 = time.perf_counter()
+    for _ in range(args.steps):
+        dev.memcpy(dst, out, out_bytes, 1, None, False)
+    dev.sync()
+    t_copy = dist.max(time.perf_counter() - t1)
+    # the host slice must hold this rank's slab of the generator's array
+    dev.memset(out, 0, out_bytes)
+    dev.memcpy(out, dst, out_bytes, 0, None, True)
+    bad = dist.max(dev.synth_verify(out, shape, so, ss, 4, SEED))
+    if shared:
+        dev.host_unregister(reg)
+        del cbuf
+        mm.close()
+        dist.barrier()
+        if rank == 0:
+            os.unlink(name)
+    else:
+        dev.free_pinned(dst)
+    if bad:
+        raise SystemExit(f"[rank {rank}] host-terminated slab verification FAILED: {bad}")
+    return {"buffer": kind, "ms_per_step": round(t * 1e3 / args.steps, 3),
+            "value": round(full * args.steps / t / GiB, 2), "unit": "GiB/s",
+            "d2h_only_ms_per_step": round(t_copy * 1e3 / args.steps, 3),
+            "d2h_GBps_per_rank": round(out_bytes * args.steps / t_copy / 1e9, 2),
+            "region_bytes": full, "verify_mismatches": int(bad)}
+
+
 def run_strong(args, dist, dev, A, L, meta, rank, ws, local):
     """Strong scaling: ONE full array split into per-rank y-slabs (512 rows at
     N=8, aligned to inner chunks); each rank holds only the shards its slab touches
@@ -327,6 +407,9 @@ def run_strong(args, dist, dev, A, L, meta, rank, ws, local):
     plan.wait()
     t_dec = dist.max(time.perf_counter() - t0)
     kt = plan.kernel_time()
+    host_out = None
+    if args.host_out:
+        host_out = host_terminated(args, dist, dev, plan, out, out_bytes, shape, so, ss, rank, ws)
     gather = None
     if backend is not None:
         import torch
@@ -367,7 +450,8 @@ def run_strong(args, dist, dev, A, L, meta, rank, ws, local):
     res = {"mode": "strong", "slab_offset": so, "slab_shape": ss,
            "decode_ms_per_step": round(t_dec * 1e3 / args.steps, 3),
            "value": round(full * 4 * args.steps / t_dec / GiB, 2),
-           "scatter_ms": round(kt["scatter_ms"] / max(1, kt["launches"]), 3), "gather": gather}
+           "scatter_ms": round(kt["scatter_ms"] / max(1, kt["launches"]), 3), "gather": gather,
+           "host_out": host_out}
     plan.close()
     if backend != "nccl":
         dev.free(out)
@@ -387,6 +471,9 @@ def main():
                     help="weak: one full array per GPU (the metric); strong: one array split "
                          "into per-GPU slabs, plus a gather to rank 0")
     ap.add_argument("--gather-backend", default="nccl", choices=["nccl", "gloo", "none"])
+    ap.add_argument("--host-out", action="store_true",
+                    help="strong mode: also time decode + D2H of each slab into its slice of "
+                         "one host buffer (the host-terminated read, no gather)")
     ap.add_argument("--ydiv", type=int, default=1,
                     help="rehearsal only: divide the array's y extent (not a bench config)")
     ap.add_argument("--host-inclusive", action="store_true",

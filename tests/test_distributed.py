@@ -39,6 +39,13 @@ def test_slab_partition_covers_region(shape, world, align):
     assert pos == off[ax] + shape[ax]
     if shape == [1, 4096, 4096, 1536] and world == 8:
         assert [s[1] for _, s in parts] == [512] * 8  # 512-row slabs
+    # host-terminated read: each slab's slice of the region buffer starts where the
+    # previous one ends (contiguous C-order slabs tile the buffer)
+    pos_b = 0
+    for o, s in parts:
+        assert P.slab_byte_offset(shape, o, 4) == pos_b
+        pos_b += 4 * int(np.prod(s))
+    assert pos_b == 4 * int(np.prod(shape))
 
 
 def _worker(rank, world, port, tmp):

@@ -47,6 +47,16 @@ def slab_partition(offset, shape, world, align=1):
     return out
 
 
+def slab_byte_offset(shape, slab_offset, itemsize):
+    """Byte offset of a slab's first element in the C-order region buffer of `shape`: where
+    a rank's slice starts in a host-terminated read's shared region buffer."""
+    off, st = 0, 1
+    for d in range(len(shape) - 1, -1, -1):
+        off += int(slab_offset[d]) * st
+        st *= int(shape[d])
+    return off * itemsize
+
+
 def assemble(slabs, shape, axis):
     """Concatenate per-rank slabs (in rank order) into the full region."""
     parts = [np.asarray(s) for s in slabs if np.asarray(s).size]
