@@ -1,7 +1,8 @@
 #!/bin/bash
 # Profiling recipe (run on the GPU box from the repo root):
-#   kernel trace + stats of the headline bench, then separate PMC passes for HBM bytes
-#   (FETCH_SIZE and WRITE_SIZE cannot share a pass on gfx950), plus the c4/c2 configs.
+#   per config: kernel trace + stats of the bench, then separate PMC passes for HBM bytes
+#   (FETCH_SIZE and WRITE_SIZE cannot share a pass on gfx950).
+#   usage: profiles/run_profile.sh [tag] ; CONFIGS="c3 c4 c2" by default
 set -u
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 TAG=${1:-r01}
@@ -17,13 +18,7 @@ step() {  # name, timeout, cmd...
   echo "== $name rc=$rc" >&2
   if [ $rc -ne 0 ]; then exit $rc; fi
 }
-step trace_c3 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace_c3" -o run -- \
-  python3 "$R/bench.py" --config c3 --steps 5 --warmup 2 --no-cpu-baseline
-step pmc_fetch_c3 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch_c3" -o run -- \
-  python3 "$R/bench.py" --config c3 --steps 2 --warmup 1 --no-cpu-baseline
-step pmc_write_c3 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write_c3" -o run -- \
-  python3 "$R/bench.py" --config c3 --steps 2 --warmup 1 --no-cpu-baseline
-for cfg in c4 c2; do
+for cfg in ${CONFIGS:-c3 c4 c2}; do
   step trace_$cfg 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace_$cfg" -o run -- \
     python3 "$R/bench.py" --config $cfg --steps 5 --warmup 2 --no-cpu-baseline
   step pmc_fetch_$cfg 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch_$cfg" -o run -- \

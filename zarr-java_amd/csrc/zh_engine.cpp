@@ -523,7 +523,9 @@ std::vector<uint32_t> setup_fast(const zh_array_meta* m, ScatterArgs& a, int til
   int64_t nb = 1;
   for (int d = 0; d < n; d++)
     if (d != fs && d != fd) nb *= a.inner[d];
-  if (nb * ts * td > kMaxEntries) return {};
+  // the tile kernels keep the table next to 8 LDS tiles (33.8 KB): stay within 64 KiB of
+  // dynamic LDS (larger inner chunks take the generic kernel)
+  if (nb * ts * td > kMaxEntries - 256) return {};
   for (int64_t u = 0; u < nb * ts * td; u++) {
     const int64_t ud = u % td, us = (u / td) % ts;
     int64_t b = u / (td * ts);

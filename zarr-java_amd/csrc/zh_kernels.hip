@@ -1433,9 +1433,11 @@ __global__ void crc_finalize_kernel(const CrcJob* jobs, int64_t njobs, const uin
   const CrcJob J = jobs[j];
   uint32_t c = 0;
   const int64_t nspans = (J.len + kCrcSpan - 1) / kCrcSpan;
+  const uint32_t kspan = x2nmodp((uint64_t)kCrcSpan, 3);  // shift past one full span
   for (int64_t k = 0; k < nspans; k++) {
     const int64_t slen = min((int64_t)kCrcSpan, J.len - k * kCrcSpan);
-    c = crc_combine(c, partials[J.span_begin + k], (uint64_t)slen);
+    const uint32_t p = partials[J.span_begin + k];
+    c = slen == kCrcSpan ? multmodp(kspan, c) ^ p : crc_combine(c, p, (uint64_t)slen);
   }
   const uint8_t* s = J.base + J.len;  // stored little-endian (Crc32cCodec.java:121,130)
   const uint32_t stored =
