@@ -190,6 +190,32 @@ int zh_plan_kernel_time(zh_plan* plan, double* scatter_ms, int64_t* launches,
 int zh_array_read(zh_ctx* ctx, const zh_array_meta* meta, const zh_chunk_src* chunks,
                   int64_t nchunks, const int64_t* offset, const int64_t* shape, void* out,
                   uint32_t flags, void* stream, char* err, size_t errlen);
+/*
+ * Multi-GPU region read in ONE process: the single-JVM form of SURVEY §8(b)'s
+ * zh_decode_region_multi (one zarr-java Array.read spread over the GPUs of a node).
+ *   The region splits into `ndev` contiguous C-order slabs along its first axis of extent
+ *   >= ndev (all earlier axes must have extent 1; otherwise ctxs[root] decodes it whole),
+ *   with boundaries on inner-chunk multiples (zh_slab_partition).  Slab r is planned on
+ *   ctxs[r] over the chunks it touches and decoded there; all devices work concurrently,
+ *   one host thread each.  chunks[] follows computeChunkCoords of the WHOLE region, as in
+ *   zh_array_read; flags as there:
+ *     no ZH_OUT_DEVICE : host-terminated — slab r is copied D2H straight into its slice of
+ *                        the host buffer `out`, each device over its own PCIe link (pin
+ *                        `out` with zh_host_register for the full rate);
+ *     ZH_OUT_DEVICE    : `out` is a buffer on ctxs[root]'s device; the other devices decode
+ *                        into their own HBM and copy their slab to the root's slice over
+ *                        xGMI (hipMemcpyPeerAsync).
+ *   Errors: the first failing slab in C order, with zh_array_read's messages.
+ * zh_slab_partition writes nslabs rows of ndim int64 offsets / shapes (ZH_EINVAL when the
+ * region cannot be split into nslabs contiguous slabs).
+ */
+int zh_array_read_multi(zh_ctx* const* ctxs, int ndev, int root, const zh_array_meta* meta,
+                        const zh_chunk_src* chunks, int64_t nchunks, const int64_t* offset,
+                        const int64_t* shape, void* out, uint32_t flags, char* err,
+                        size_t errlen);
+int zh_slab_partition(int ndim, const int64_t* offset, const int64_t* shape, int nslabs,
+                      int64_t align, int64_t* slab_off, int64_t* slab_shape);
+
 /* ShardingIndexedCodec.decode: whole shard → chunk_shape elements. */
 int zh_sharding_decode(zh_ctx* ctx, const zh_array_meta* meta, const void* shard, int64_t nbytes,
                        void* out, uint32_t flags, void* stream, char* err, size_t errlen);

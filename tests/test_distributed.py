@@ -93,3 +93,23 @@ def test_two_rank_gloo_partition_gather_and_bench_harness(tmp_path):
     np.testing.assert_array_equal(np.load(tmp_path / "full.npy"), np.load(tmp_path / "want.npy"))
     for r in range(world):
         assert float(open(tmp_path / f"max{r}.txt").read()) == 2.0
+
+
+@pytest.mark.parametrize("seed", range(12))
+def test_c_slab_partition_matches_python(seed):
+    """zh_slab_partition (the C-ABI multi-GPU read's split) == zarrhip.parallel.slab_partition."""
+    from zarrhip._lib import ZhError, slab_partition
+    rng = np.random.default_rng(seed)
+    n = int(rng.integers(1, 5))
+    lead = int(rng.integers(0, n))
+    shape = [1] * lead + [int(rng.integers(1, 300)) for _ in range(n - lead)]
+    off = [int(rng.integers(0, 50)) for _ in range(n)]
+    world = int(rng.integers(1, 9))
+    align = int(rng.choice([1, 4, 16, 32]))
+    try:
+        want = P.slab_partition(off, shape, world, align)
+    except ValueError:
+        with pytest.raises(ZhError):
+            slab_partition(off, shape, world, align)
+        return
+    assert slab_partition(off, shape, world, align) == want

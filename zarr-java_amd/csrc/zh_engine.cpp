@@ -19,6 +19,7 @@
 #include <map>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "zh_internal.h"
@@ -1216,6 +1217,155 @@ int zh_array_read(zh_ctx* ctx, const zh_array_meta* meta, const zh_chunk_src* ch
   st = zh_plan_wait(p, err, errlen);
   plan_free(p);
   return st;
+}
+
+// Multi-GPU region read inside one process: contiguous C-order slabs, one
+// per device, decoded concurrently (one host thread per device, each on its context), then
+// delivered to the caller's host buffer (each device over its own PCIe link) or to the
+// root device's buffer over xGMI.
+int zh_slab_partition(int ndim, const int64_t* offset, const int64_t* shape, int nslabs,
+                      int64_t align, int64_t* slab_off, int64_t* slab_shape) {
+  if (ndim <= 0 || ndim > kMaxDims || nslabs <= 0 || !offset || !shape || !slab_off ||
+      !slab_shape)
+    return ZH_EINVAL;
+  int ax = -1;  // first axis long enough; all earlier axes must have extent 1
+  for (int d = 0; d < ndim; d++) {
+    if (shape[d] >= nslabs) {
+      ax = d;
+      break;
+    }
+    if (shape[d] != 1) break;
+  }
+  if (ax < 0) return ZH_EINVAL;
+  const int64_t lo = offset[ax], ext = shape[ax];
+  const bool units_ok = align > 1 && ext % align == 0 && ext / align >= nslabs;
+  for (int r = 0; r < nslabs; r++) {
+    auto bound = [&](int k) {
+      return units_ok ? lo + (ext / align * k / nslabs) * align : lo + ext * k / nslabs;
+    };
+    for (int d = 0; d < ndim; d++) {
+      slab_off[r * ndim + d] = offset[d];
+      slab_shape[r * ndim + d] = shape[d];
+    }
+    slab_off[r * ndim + ax] = bound(r);
+    slab_shape[r * ndim + ax] = bound(r + 1) - bound(r);
+  }
+  return ZH_OK;
+}
+
+int zh_array_read_multi(zh_ctx* const* ctxs, int ndev, int root, const zh_array_meta* meta,
+                        const zh_chunk_src* chunks, int64_t nchunks, const int64_t* offset,
+                        const int64_t* shape, void* out, uint32_t flags, char* err,
+                        size_t errlen) {
+  if (!ctxs || ndev <= 0 || root < 0 || root >= ndev || !meta || !offset || !shape || !out)
+    return ZH_EINVAL;
+  for (int k = 0; k < ndev; k++)
+    if (!ctxs[k]) return ZH_EINVAL;
+  int st = zh_validate_meta(meta, err, errlen);
+  if (st != ZH_OK) return st;
+  const int n = meta->ndim;
+  for (int d = 0; d < n; d++) {  // M/core/Array.java:386-390
+    if (offset[d] < 0 || shape[d] <= 0 || offset[d] + shape[d] > meta->shape[d]) {
+      set_err(err, errlen, "Requested data is outside of the array's domain.");
+      return ZH_EDATA;
+    }
+  }
+  int64_t cstart[kMaxDims], ccount[kMaxDims];
+  const int64_t ncoords = chunk_coords(n, meta->chunk_shape, offset, shape, cstart, ccount);
+  if (ncoords != nchunks || !chunks) {
+    set_err(err, errlen, "expected %lld chunk sources (computeChunkCoords order), got %lld",
+            (long long)ncoords, (long long)nchunks);
+    return ZH_EINVAL;
+  }
+  // slabs aligned to inner (leaf) chunks along the split axis, so no item is cut in two
+  int ax = -1;
+  for (int d = 0; d < n; d++) {
+    if (shape[d] >= ndev) {
+      ax = d;
+      break;
+    }
+    if (shape[d] != 1) break;
+  }
+  const int nslab = ax < 0 ? 1 : ndev;
+  std::vector<int64_t> so((size_t)nslab * n), ss((size_t)nslab * n);
+  if (ax < 0) {  // not splittable: the root decodes it all
+    std::copy(offset, offset + n, so.begin());
+    std::copy(shape, shape + n, ss.begin());
+  } else {
+    zh_slab_partition(n, offset, shape, nslab, leaf_shape(meta)[ax], so.data(), ss.data());
+  }
+  const bool out_dev = (flags & ZH_OUT_DEVICE) != 0;
+  int64_t rstride[kMaxDims], cstride[kMaxDims], s1 = 1, s2 = 1;
+  for (int d = n - 1; d >= 0; d--) {
+    rstride[d] = s1;
+    s1 *= shape[d];
+    cstride[d] = s2;
+    s2 *= ccount[d];
+  }
+  std::vector<int> status(nslab, ZH_OK);
+  std::vector<std::string> msgs(nslab);
+  auto work = [&](int r) {
+    const int64_t* o = &so[(size_t)r * n];
+    const int64_t* s = &ss[(size_t)r * n];
+    int64_t nel = 1, base = 0;
+    for (int d = 0; d < n; d++) {
+      nel *= s[d];
+      base += (o[d] - offset[d]) * rstride[d];
+    }
+    if (nel == 0) return;
+    zh_ctx* ctx = ctxs[ax < 0 ? root : r];
+    char e[1024] = {0};
+    int rc = ZH_OK;
+    // this slab's chunks, picked out of the caller's (full region) list
+    int64_t st0[kMaxDims], cnt[kMaxDims];
+    const int64_t m = chunk_coords(n, meta->chunk_shape, o, s, st0, cnt);
+    std::vector<zh_chunk_src> sub((size_t)m);
+    int64_t cur[kMaxDims] = {0};
+    for (int64_t i = 0; i < m; i++) {
+      int64_t lin = 0;
+      for (int d = 0; d < n; d++) lin += (st0[d] + cur[d] - cstart[d]) * cstride[d];
+      sub[(size_t)i] = chunks[lin];
+      for (int d = n - 1; d >= 0; d--) {
+        if (++cur[d] < cnt[d]) break;
+        cur[d] = 0;
+      }
+    }
+    uint8_t* dst = (uint8_t*)out + base * meta->dtype_size;
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    (void)hipSetDevice(ctx->device);
+    const int rdev = ctxs[root]->device;
+    const bool peer = out_dev && ctx != ctxs[root];
+    void* local = nullptr;
+    if (peer && hipMalloc(&local, (size_t)(nel * meta->dtype_size)) != hipSuccess) {
+      status[r] = ZH_ENOMEM;
+      msgs[r] = "hipMalloc of a slab buffer failed";
+      return;
+    }
+    zh_plan* p = nullptr;
+    uint32_t pf = (flags & ZH_SRC_DEVICE) | (out_dev ? ZH_OUT_DEVICE : 0u);
+    rc = zh_plan_create(ctx, meta, sub.data(), m, o, s, pf, &p, e, sizeof(e));
+    if (rc == ZH_OK) rc = zh_plan_execute(p, peer ? local : (void*)dst, nullptr);
+    if (rc == ZH_OK && peer &&
+        hipMemcpyPeerAsync(dst, rdev, local, ctx->device, (size_t)(nel * meta->dtype_size),
+                           ctx->stream) != hipSuccess) {
+      rc = ZH_EHIP;
+      snprintf(e, sizeof(e), "slab copy to device %d failed", rdev);
+    }
+    if (rc == ZH_OK) rc = zh_plan_wait(p, e, sizeof(e));
+    if (p) plan_free(p);
+    if (local) (void)hipFree(local);
+    status[r] = rc;
+    msgs[r] = e;
+  };
+  std::vector<std::thread> th;
+  for (int r = 0; r < nslab; r++) th.emplace_back(work, r);
+  for (auto& t : th) t.join();
+  for (int r = 0; r < nslab; r++)  // first failing slab in C order
+    if (status[r] != ZH_OK) {
+      set_err(err, errlen, "%s", msgs[r].c_str());
+      return status[r];
+    }
+  return ZH_OK;
 }
 
 // ShardingIndexedCodec.decode / decodePartial: one shard viewed as a one-chunk array.

@@ -94,11 +94,10 @@ static int build_meta(JNIEnv* env, jintArray jm, jlongArray jshape, jintArray jc
  * computeChunkCoords(shape, chunkShape, offset, regionShape) or null (missing key);
  * out = the primitive array behind the result ucar.ma2.Array (C order).
  * Returns 0 on success, 3 (ZH_EUNSUPPORTED) to request the Java fallback. */
-JNIEXPORT jint JNICALL Java_dev_zarr_zarrjava_hip_ZarrHip_arrayRead(
-    JNIEnv* env, jclass cls, jlong ctx, jintArray jm, jlongArray jshape, jintArray jchunk,
-    jintArray jinner, jintArray jorder, jbyteArray jfill, jobjectArray jchunks,
-    jlongArray joffset, jlongArray jregion, jobject out) {
-  (void)cls;
+static jint array_read_common(JNIEnv* env, zh_ctx* const* ctxs, int nctx, jintArray jm,
+                              jlongArray jshape, jintArray jchunk, jintArray jinner,
+                              jintArray jorder, jbyteArray jfill, jobjectArray jchunks,
+                              jlongArray joffset, jlongArray jregion, jobject out) {
   zh_array_meta m;
   int st = build_meta(env, jm, jshape, jchunk, jinner, jorder, jfill, &m);
   if (st != ZH_OK) return st;
@@ -130,8 +129,10 @@ JNIEXPORT jint JNICALL Java_dev_zarr_zarrjava_hip_ZarrHip_arrayRead(
     r64[d] = reg[d];
   }
   void* dst = (*env)->GetPrimitiveArrayCritical(env, (jarray)out, NULL);
-  st = zh_array_read((zh_ctx*)(intptr_t)ctx, &m, srcs, n, o64, r64, dst, 0, NULL, err,
-                     sizeof err);
+  if (nctx == 1)
+    st = zh_array_read(ctxs[0], &m, srcs, n, o64, r64, dst, 0, NULL, err, sizeof err);
+  else  /* one slab per device, each D2H'd straight into its slice of the Java array */
+    st = zh_array_read_multi(ctxs, nctx, 0, &m, srcs, n, o64, r64, dst, 0, err, sizeof err);
   (*env)->ReleasePrimitiveArrayCritical(env, (jarray)out, dst, 0);
   for (jsize i = 0; i < n; i++) free(copies[i]);
   free(copies);
@@ -140,6 +141,32 @@ JNIEXPORT jint JNICALL Java_dev_zarr_zarrjava_hip_ZarrHip_arrayRead(
   if (st == ZH_EUNSUPPORTED) return st;
   if (st != ZH_OK) return throw_status(env, st, err);
   return 0;
+}
+
+JNIEXPORT jint JNICALL Java_dev_zarr_zarrjava_hip_ZarrHip_arrayRead(
+    JNIEnv* env, jclass cls, jlong ctx, jintArray jm, jlongArray jshape, jintArray jchunk,
+    jintArray jinner, jintArray jorder, jbyteArray jfill, jobjectArray jchunks,
+    jlongArray joffset, jlongArray jregion, jobject out) {
+  (void)cls;
+  zh_ctx* c = (zh_ctx*)(intptr_t)ctx;
+  return array_read_common(env, &c, 1, jm, jshape, jchunk, jinner, jorder, jfill, jchunks,
+                           joffset, jregion, out);
+}
+
+/* The same read spread over several devices (zh_array_read_multi, host-terminated). */
+JNIEXPORT jint JNICALL Java_dev_zarr_zarrjava_hip_ZarrHip_arrayReadMulti(
+    JNIEnv* env, jclass cls, jlongArray jctxs, jintArray jm, jlongArray jshape,
+    jintArray jchunk, jintArray jinner, jintArray jorder, jbyteArray jfill,
+    jobjectArray jchunks, jlongArray joffset, jlongArray jregion, jobject out) {
+  (void)cls;
+  jsize k = (*env)->GetArrayLength(env, jctxs);
+  if (k <= 0 || k > 64) return throw_status(env, ZH_EINVAL, "bad device context list");
+  jlong raw[64];
+  zh_ctx* ctxs[64];
+  (*env)->GetLongArrayRegion(env, jctxs, 0, k, raw);
+  for (jsize i = 0; i < k; i++) ctxs[i] = (zh_ctx*)(intptr_t)raw[i];
+  return array_read_common(env, ctxs, (int)k, jm, jshape, jchunk, jinner, jorder, jfill,
+                           jchunks, joffset, jregion, out);
 }
 
 /* ShardingIndexedCodec.decode / decodePartial replacement for one shard's bytes. */

@@ -54,9 +54,14 @@ public class HipArray extends Array {
         }
         ucar.ma2.Array out = ucar.ma2.Array.factory(md.dataType().getMA2DataType(),
                 Utils.toIntArray(shape));
-        int st = ZarrHip.arrayRead(ZarrHip.ctx(), chain.meta, chain.shape, chain.chunkShape,
-                chain.innerShape, chain.order, chain.fill, chunks, offset, shape,
-                out.getStorage());
+        long[] ctxs = ZarrHip.ctxs();
+        int st = ctxs.length > 1
+                ? ZarrHip.arrayReadMulti(ctxs, chain.meta, chain.shape, chain.chunkShape,
+                        chain.innerShape, chain.order, chain.fill, chunks, offset, shape,
+                        out.getStorage())
+                : ZarrHip.arrayRead(ctxs[0], chain.meta, chain.shape, chain.chunkShape,
+                        chain.innerShape, chain.order, chain.fill, chunks, offset, shape,
+                        out.getStorage());
         return st == 0 ? out : super.read(offset, shape, parallel);
     }
 }

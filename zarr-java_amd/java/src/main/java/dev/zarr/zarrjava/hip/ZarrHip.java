@@ -5,28 +5,42 @@ package dev.zarr.zarrjava.hip;
  * forwards to the zarrhip C-ABI (include/zarrhip.h).  A status of 3 (ZH_EUNSUPPORTED)
  * means "codec chain not device-supported": callers fall back to the reference codec.
  * Data errors surface as dev.zarr.zarrjava.ZarrException with the reference's messages.
+ *
+ * Devices: ZH_DEVICES="0,1,...,7" spreads every region read over those GPUs
+ * (zh_array_read_multi: one slab per device, each copied straight into its slice of the
+ * result); otherwise ZH_DEVICE (default 0) is the one device.
  */
 public final class ZarrHip {
     public static final int UNSUPPORTED = 3;
 
     private static final boolean AVAILABLE;
-    private static final long CTX;
+    private static final long[] CTXS;
 
     static {
-        boolean ok = false;
-        long ctx = 0;
+        long[] ctxs = new long[0];
         if (!"1".equals(System.getenv("ZH_DISABLE"))) {
             try {
                 System.loadLibrary("zarrhip_jni");
-                String dev = System.getenv("ZH_DEVICE");
-                ctx = ctxCreate(dev == null ? 0 : Integer.parseInt(dev));
-                ok = ctx != 0;
+                String list = System.getenv("ZH_DEVICES");
+                if (list == null) {
+                    String dev = System.getenv("ZH_DEVICE");
+                    list = dev == null ? "0" : dev;
+                }
+                String[] ids = list.split(",");
+                ctxs = new long[ids.length];
+                for (int i = 0; i < ids.length; i++) {
+                    ctxs[i] = ctxCreate(Integer.parseInt(ids[i].trim()));
+                    if (ctxs[i] == 0) {
+                        ctxs = new long[0];
+                        break;
+                    }
+                }
             } catch (Throwable t) {
-                ok = false;
+                ctxs = new long[0];
             }
         }
-        AVAILABLE = ok;
-        CTX = ctx;
+        AVAILABLE = ctxs.length > 0;
+        CTXS = ctxs;
     }
 
     private ZarrHip() {
@@ -37,7 +51,11 @@ public final class ZarrHip {
     }
 
     static long ctx() {
-        return CTX;
+        return CTXS[0];
+    }
+
+    static long[] ctxs() {
+        return CTXS;
     }
 
     static native long ctxCreate(int device);
@@ -48,6 +66,11 @@ public final class ZarrHip {
     static native int arrayRead(long ctx, int[] meta, long[] shape, int[] chunkShape,
                                 int[] innerShape, int[] order, byte[] fill, byte[][] chunks,
                                 long[] offset, long[] regionShape, Object out);
+
+    /** The same read split into one slab per device context (zh_array_read_multi). */
+    static native int arrayReadMulti(long[] ctxs, int[] meta, long[] shape, int[] chunkShape,
+                                     int[] innerShape, int[] order, byte[] fill, byte[][] chunks,
+                                     long[] offset, long[] regionShape, Object out);
 
     /** ShardingIndexedCodec.decodePartial over one shard's bytes. */
     static native int shardDecodePartial(long ctx, int[] meta, long[] shape, int[] chunkShape,

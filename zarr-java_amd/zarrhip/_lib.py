@@ -44,6 +44,10 @@ _SIGS = {
     "zh_plan_kernel_time": (C.c_int, [P, C.POINTER(C.c_double), PI64, C.POINTER(C.c_double)]),
     "zh_array_read": (C.c_int, [P, PMETA, C.POINTER(A.zh_chunk_src), I64, PI64, PI64, P, U32, P,
                                 CH, SZ]),
+    "zh_array_read_multi": (C.c_int, [C.POINTER(P), C.c_int, C.c_int, PMETA,
+                                      C.POINTER(A.zh_chunk_src), I64, PI64, PI64, P, U32, CH,
+                                      SZ]),
+    "zh_slab_partition": (C.c_int, [C.c_int, PI64, PI64, C.c_int, I64, PI64, PI64]),
     "zh_sharding_decode": (C.c_int, [P, PMETA, P, I64, P, U32, P, CH, SZ]),
     "zh_sharding_decode_partial": (C.c_int, [P, PMETA, P, I64, PI64, PI32, P, U32, P, CH, SZ]),
     "zh_array_encoded_bound": (I64, [PMETA]),
@@ -274,6 +278,31 @@ class DeviceContext:
                                    arr, len(dsts), P(stream), err, 1024)
         check(st, err)
         return [arr[i].nbytes for i in range(len(dsts))]
+
+
+def array_read_multi(ctxs, meta, sources, offset, shape, out, flags, root=0):
+    """zh_array_read_multi: one region read split into per-device slabs (one DeviceContext
+    per slab), delivered to a host buffer or to a buffer on ctxs[root]'s device."""
+    L = lib()
+    hs = (P * len(ctxs))(*[c.h for c in ctxs])
+    srcs = (A.zh_chunk_src * max(1, len(sources)))()
+    for i, (ptr, nb) in enumerate(sources):
+        srcs[i].data = ptr
+        srcs[i].nbytes = int(nb)
+    err = C.create_string_buffer(1024)
+    st = L.zh_array_read_multi(hs, len(ctxs), int(root), C.byref(meta), srcs, len(sources),
+                               i64arr(offset), i64arr(shape), P(out), int(flags), err, 1024)
+    check(st, err)
+
+
+def slab_partition(offset, shape, nslabs, align=1):
+    """zh_slab_partition → [(slab_offset, slab_shape)] (the C twin of parallel.slab_partition)."""
+    n = len(shape)
+    so = (C.c_int64 * (n * nslabs))()
+    ss = (C.c_int64 * (n * nslabs))()
+    check(lib().zh_slab_partition(n, i64arr(offset), i64arr(shape), int(nslabs), int(align),
+                                  so, ss))
+    return [(list(so[r * n:(r + 1) * n]), list(ss[r * n:(r + 1) * n])) for r in range(nslabs)]
 
 
 class Plan:
