@@ -261,3 +261,18 @@ def test_reshape_read_write(tmp_path, shape, chunk, fn):
     off = [1] * len(shape)
     shp = [s - 2 for s in shape]
     np.testing.assert_array_equal(b.read(off, shp), data[tuple(slice(1, s - 1) for s in shape)])
+
+
+@pytest.mark.parametrize("spec", ["0,0", "0,0,0"])
+def test_read_spread_over_devices(tmp_path, monkeypatch, spec):
+    """ZH_DEVICES: Array.read runs zh_array_read_multi (one slab per listed device, here
+    repeated device 0) and returns what the single-device read returns."""
+    ref = z.Array.open(z.FilesystemStore(GOLDEN).resolve("sharding_index_location", "end"))
+    content = ref.read()
+    dst = z.Array.create(z.FilesystemStore(tmp_path).resolve("multi"), ref.metadata)
+    dst.write(None, content)
+    arr = z.Array.open(z.FilesystemStore(tmp_path).resolve("multi"))
+    one = arr.read([1, 2, 3], [14, 13, 12])
+    monkeypatch.setenv("ZH_DEVICES", spec)
+    np.testing.assert_array_equal(arr.read(), content)
+    np.testing.assert_array_equal(arr.read([1, 2, 3], [14, 13, 12]), one)

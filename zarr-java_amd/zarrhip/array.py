@@ -2,7 +2,8 @@
 chunk codec work done by the HIP path through the C-ABI (libzarrhip.so).
 
   Array.open / create        M/v3/Array.java:41-50, 142-154
-  read(offset, shape)        M/core/Array.java:378-441   → zh_array_read (one call, all chunks)
+  read(offset, shape)        M/core/Array.java:378-441   → zh_array_read (one call, all chunks;
+                                                          zh_array_read_multi over ZH_DEVICES)
   readChunk(coords)          M/core/Array.java:167-182
   write(offset, data)        M/core/Array.java:83-133    → zh_array_write (whole chunks)
   access()                   M/core/Array.java:483-536   (ArrayAccessor)
@@ -36,6 +37,22 @@ def device():
             dev = int(os.environ.get("ZH_DEVICE", os.environ.get("LOCAL_RANK", "0")))
             _ctx = _lib.DeviceContext(dev)
         return _ctx
+
+
+_multi = {}
+
+
+def devices():
+    """DeviceContexts of ZH_DEVICES="0,1,..." (one per listed GPU, a GPU may repeat), or
+    [device()]: Array.read spreads a region over them (zh_array_read_multi)."""
+    spec = os.environ.get("ZH_DEVICES", "")
+    ids = [int(x) for x in spec.split(",") if x.strip()]
+    if len(ids) <= 1:
+        return [device()]
+    with _ctx_lock:
+        if spec not in _multi:
+            _multi[spec] = [_lib.DeviceContext(i) for i in ids]
+        return _multi[spec]
 
 
 def _host_buf(b):
@@ -273,8 +290,12 @@ class Array:
         srcs = [((C.addressof(b), len(s)) if s is not None else (None, 0))
                 for b, s in zip(bufs, sources)]
         out = np.empty(shape, dtype=dt)
+        devs = devices()
         try:
-            device().array_read(self.zmeta, srcs, offset, shape, out.ctypes.data, 0)
+            if len(devs) > 1:  # one slab per device, each D2H'd into its slice of `out`
+                _lib.array_read_multi(devs, self.zmeta, srcs, offset, shape, out.ctypes.data, 0)
+            else:
+                devs[0].array_read(self.zmeta, srcs, offset, shape, out.ctypes.data, 0)
         except _lib.ZhError as e:
             raise_for(e)
         return out
