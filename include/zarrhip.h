@@ -183,6 +183,10 @@ int zh_plan_stats(const zh_plan* plan, int64_t* in_bytes, int64_t* out_bytes,
  * semantics, ShardingIndexedCodec.java:333-357). */
 int64_t zh_plan_staged_bytes(const zh_plan* plan);
 int zh_plan_set_timing(zh_plan* plan, int enable);
+/* enable=1: zh_plan_execute replays the plan as one hipGraph (captured on the first execute
+ * for a given (out, stream); device sources and device output only, timing off).  For small
+ * repeated reads this replaces ~8 enqueues with one graph launch. */
+int zh_plan_set_graph(zh_plan* plan, int enable);
 int zh_plan_kernel_time(zh_plan* plan, double* scatter_ms, int64_t* launches,
                         double* index_ms);
 

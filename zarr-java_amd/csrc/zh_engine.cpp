@@ -226,6 +226,11 @@ struct zh_plan {
   int grid = 0;
   int slow_grid = 0;
   hipStream_t last_stream = nullptr;
+  // hipGraph replay of execute (zh_plan_set_graph)
+  bool use_graph = false;
+  hipGraphExec_t graph_exec = nullptr;
+  void* graph_out = nullptr;
+  hipStream_t graph_stream = nullptr;
   // timing
   bool timing = false;
   std::vector<hipEvent_t> ev_pool;
@@ -691,6 +696,7 @@ void plan_free(zh_plan* p) {
   for (auto& e : p->ev_pending)
     for (auto ev : e) p->ev_pool.push_back(ev);
   for (auto ev : p->ev_pool) (void)hipEventDestroy(ev);
+  if (p->graph_exec) (void)hipGraphExecDestroy(p->graph_exec);
   delete p;
 }
 
@@ -1062,12 +1068,10 @@ int zh_plan_create(zh_ctx* ctx, const zh_array_meta* m, const zh_chunk_src* chun
   return ZH_OK;
 }
 
-int zh_plan_execute(zh_plan* p, void* out, void* stream_v) {
-  if (!p || !out) return ZH_EINVAL;
+// Enqueues one execution of the plan on stream s (also the body a hipGraph captures).
+static int plan_enqueue(zh_plan* p, void* out, hipStream_t s) {
   char* err = nullptr;
   size_t errlen = 0;
-  hipStream_t s = stream_v ? (hipStream_t)stream_v : p->ctx->stream;
-  (void)hipSetDevice(p->ctx->device);
   for (size_t k = 0; k < p->h2d.size(); k++)
     ZH_HIP(hipMemcpyAsync(p->d_input + p->h2d[k].first, p->h2d[k].second, (size_t)p->h2d_len[k],
                           hipMemcpyHostToDevice, s));
@@ -1105,7 +1109,61 @@ int zh_plan_execute(zh_plan* p, void* out, void* stream_v) {
   }
   if (!(p->flags & ZH_OUT_DEVICE))
     ZH_HIP(hipMemcpyAsync(out, p->d_out, (size_t)p->out_bytes, hipMemcpyDeviceToHost, s));
-  p->last_stream = s;
+  return ZH_OK;
+}
+
+static void plan_drop_graph(zh_plan* p) {
+  if (p->graph_exec) (void)hipGraphExecDestroy(p->graph_exec);
+  p->graph_exec = nullptr;
+  p->graph_out = nullptr;
+  p->graph_stream = nullptr;
+}
+
+int zh_plan_execute(zh_plan* p, void* out, void* stream_v) {
+  if (!p || !out) return ZH_EINVAL;
+  char* err = nullptr;
+  size_t errlen = 0;
+  hipStream_t s = stream_v ? (hipStream_t)stream_v : p->ctx->stream;
+  (void)hipSetDevice(p->ctx->device);
+  // hipGraph replay (zh_plan_set_graph): device-resident plans without timing events; the
+  // graph is captured on the first execute for this (out, stream) and then relaunched as
+  // one unit, so a small read pays one launch instead of ~8 enqueues
+  if (p->use_graph && !p->timing && p->h2d.empty() && (p->flags & ZH_OUT_DEVICE)) {
+    if (!p->graph_exec || p->graph_out != out || p->graph_stream != s) {
+      plan_drop_graph(p);
+      ZH_HIP(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
+      const int st = plan_enqueue(p, out, s);
+      hipGraph_t g = nullptr;
+      const hipError_t e = hipStreamEndCapture(s, &g);
+      if (st != ZH_OK || e != hipSuccess) {
+        if (g) (void)hipGraphDestroy(g);
+        return st != ZH_OK ? st : ZH_EHIP;
+      }
+      const hipError_t ei = hipGraphInstantiate(&p->graph_exec, g, nullptr, nullptr, 0);
+      (void)hipGraphDestroy(g);
+      if (ei != hipSuccess) {
+        p->graph_exec = nullptr;
+        return ZH_EHIP;
+      }
+      p->graph_out = out;
+      p->graph_stream = s;
+    }
+    ZH_HIP(hipGraphLaunch(p->graph_exec, s));
+    p->last_stream = s;
+    return ZH_OK;
+  }
+  const int st = plan_enqueue(p, out, s);
+  if (st == ZH_OK) p->last_stream = s;
+  return st;
+}
+
+int zh_plan_set_graph(zh_plan* p, int enable) {
+  if (!p) return ZH_EINVAL;
+  p->use_graph = enable != 0;
+  if (!p->use_graph) {
+    (void)hipSetDevice(p->ctx->device);
+    plan_drop_graph(p);
+  }
   return ZH_OK;
 }
 

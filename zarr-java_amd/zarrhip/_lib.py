@@ -41,6 +41,7 @@ _SIGS = {
     "zh_plan_destroy": (None, [P]),
     "zh_plan_stats": (C.c_int, [P, PI64, PI64, PI64, PI64]),
     "zh_plan_set_timing": (C.c_int, [P, C.c_int]),
+    "zh_plan_set_graph": (C.c_int, [P, C.c_int]),
     "zh_plan_kernel_time": (C.c_int, [P, C.POINTER(C.c_double), PI64, C.POINTER(C.c_double)]),
     "zh_array_read": (C.c_int, [P, PMETA, C.POINTER(A.zh_chunk_src), I64, PI64, PI64, P, U32, P,
                                 CH, SZ]),
@@ -338,6 +339,9 @@ class Plan:
 
     def set_timing(self, on=True):
         check(self.L.zh_plan_set_timing(self.h, 1 if on else 0))
+
+    def set_graph(self, on=True):
+        check(self.L.zh_plan_set_graph(self.h, 1 if on else 0))
 
     def staged_bytes(self):
         return int(self.L.zh_plan_staged_bytes(self.h))
