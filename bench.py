@@ -473,6 +473,56 @@ def run_strong(args, dist, dev, A, L, meta, rank, ws, local):
     return res
 
 
+def run_write(args, dist, dev, A, meta, shape, region, out_bytes, shard_slab, offs, caps, rank,
+              ws):
+    """Write path: zh_array_write of the full array = core.Array.write
+    + ShardingIndexedCodec.encode of every shard (all-fill flags pass, C-order layout, index +
+    crc32c, payload encode) from the device-resident region into device shard buffers.  The
+    call synchronises internally (the layout needs the flags), so it is timed by wall clock;
+    the written shards are verified by decoding them and checking every element."""
+    n = len(shape)
+    dsts = [(shard_slab + o, c) for o, c in zip(offs, caps)]
+    for _ in range(max(1, args.warmup)):
+        sizes = dev.array_write(meta, region, [0] * n, shape, dsts)
+    dist.barrier()
+    dev.sync()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        sizes = dev.array_write(meta, region, [0] * n, shape, dsts)
+    dev.sync()
+    elapsed = dist.max(time.perf_counter() - t0)
+    in_bytes = sum(sizes)
+    plan = dev.plan(meta, [(shard_slab + o, s) for o, s in zip(offs, sizes)], [0] * n, shape,
+                    A.ZH_SRC_DEVICE | A.ZH_OUT_DEVICE)
+    dev.memset(region, 0, out_bytes)
+    plan.execute(region)
+    plan.wait()
+    plan.close()
+    bad = dev.synth_verify(region, shape, [0] * n, shape, 4, SEED)
+    if bad:
+        raise SystemExit(f"write round trip FAILED: {bad} mismatching elements")
+    log(f"[rank {rank}] write path verified: decode of the written shards == generator")
+    ms = elapsed * 1000.0 / args.steps
+    achieved = (in_bytes + out_bytes) / (ms / 1000.0) / 1e9
+    if rank == 0:
+        print(json.dumps({
+            "metric": "GiB/s device-resident chunk encode (sharding+bytes+transpose), "
+                      "uint32 1024³ — write path",
+            "value": round(ws * args.steps * out_bytes / elapsed / GiB, 2), "unit": "GiB/s",
+            "n_gpus": ws, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(ms, 3), "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "u32", "data": "synthetic",
+            "config": {"workload": f"{args.config}: Array.write of the full "
+                                   f"{'x'.join(map(str, shape))} uint32 array, "
+                                   f"{CONFIGS[args.config][0]}",
+                       "encoded_bytes": in_bytes, "decoded_bytes_per_gpu": out_bytes,
+                       "parallelism": f"shard-parallel x{ws}"},
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                         "traffic": None, "kernel": "zh_array_write (whole call, wall clock)",
+                         "alg_bytes_per_launch": in_bytes + out_bytes}}), flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -480,6 +530,9 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="c4", choices=sorted(CONFIGS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--op", default="read", choices=["read", "write"],
+                    help="read: the decode path (the metric); write: zh_array_write, the "
+                         "encode path (SURVEY §8(f) rank 1)")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
     ap.add_argument("--mode", default="weak", choices=["weak", "strong"],
                     help="weak: one full array per GPU (the metric); strong: one array split "
@@ -563,6 +616,13 @@ def main():
         f"{t1 - t0:.2f}s, device encode {t2 - t1:.2f}s ({sum(sizes) / GiB:.2f} GiB in "
         f"{len(sizes)} shards)")
 
+    if args.op == "write":
+        run_write(args, dist, dev, A, meta, shape, out, out_bytes, shard_slab, offs, caps, rank,
+                  ws)
+        dev.free(shard_slab)
+        dev.free(out)
+        dist.close()
+        return
     flags = A.ZH_SRC_DEVICE | A.ZH_OUT_DEVICE
     plan = dev.plan(meta, [(shard_slab + o, s) for o, s in zip(offs, sizes)], [0] * n, shape,
                     flags)

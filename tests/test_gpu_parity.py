@@ -184,6 +184,51 @@ def test_device_encode_matches_oracle_bytes(dev, sharded, order, loc):
         assert g == w
 
 
+@pytest.mark.parametrize("dsize", [1, 2, 4, 8])
+@pytest.mark.parametrize("mode", ["unsharded", "sharded", "transpose_rows", "transpose_tiles",
+                                  "crc32c"])
+@pytest.mark.parametrize("loc", [A.ZH_INDEX_END, A.ZH_INDEX_START])
+def test_device_encode_one_pass(dev, monkeypatch, dsize, mode, loc):
+    """The one-pass write path (no all-fill chunk, so the speculative C-order layout holds):
+    fast kernels on the encode view + the generic kernel for clipped chunks + device index and
+    index crc32c.  Bytes equal the oracle's and the flags → layout → encode path's."""
+    if mode == "unsharded" and loc == A.ZH_INDEX_START:
+        pytest.skip("no index")
+    shape = [40, 48, 72]          # boundary chunks on every axis
+    kw = dict(endian=A.ZH_ENDIAN_BIG, index_location=loc,
+              index_endian=A.ZH_ENDIAN_BIG if loc == A.ZH_INDEX_START else A.ZH_ENDIAN_LITTLE)
+    if mode != "unsharded":
+        kw.update(sharded=True, inner_chunk_shape=[8, 16, 32])
+    if mode == "transpose_rows":
+        kw.update(transpose_order=[1, 0, 2])      # keeps the last axis: row kernel
+    if mode == "transpose_tiles":
+        kw.update(transpose_order=[0, 2, 1])      # moves the last axis: tile kernel (u32)
+    if mode == "crc32c":
+        kw.update(inner_crc32c=True)
+    meta = A.make_meta(shape, [16, 32, 64], dsize, fill=(7).to_bytes(dsize, "little"), **kw)
+    arr = rand_array(shape, dsize, seed=31 + dsize)
+    arr[arr == 7] = 8              # no element equals fill_value: nothing is elided
+    want = encode_oracle(meta, arr)
+    got = device_write(dev, meta, arr)
+    assert [len(g) if g else 0 for g in got] == [len(w) if w else 0 for w in want]
+    assert got == want
+    monkeypatch.setenv("ZH_ENC_FAST", "0")
+    assert device_write(dev, meta, arr) == want
+
+
+def test_device_encode_one_pass_fallback(dev):
+    """A late all-fill inner chunk (seen only after the one-pass kernels ran) sends the write
+    back through flags → layout → encode; the bytes still equal the oracle's."""
+    shape = [32, 64]
+    meta = A.make_meta(shape, [32, 64], 4, sharded=True, inner_chunk_shape=[8, 16],
+                       endian=A.ZH_ENDIAN_BIG)
+    arr = rand_array(shape, 4, seed=5)
+    arr[arr == 0] = 1
+    arr[24:32, 48:64] = 0          # the last inner chunk is all fill → (-1, -1)
+    want = encode_oracle(meta, arr)
+    assert device_write(dev, meta, arr) == want
+
+
 def test_single_full_chunk_and_partial_decode_api(dev):
     """Array.java:392-395 single-full-chunk shortcut and ShardingIndexedCodec.decode /
     decodePartial through their own C-ABI entry points."""

@@ -1477,6 +1477,228 @@ int64_t zh_array_encoded_bound(const zh_array_meta* m) {
   return bound;
 }
 
+// Crc32cCodec.encode (:50-60) of every written chunk payload (inner crc32c), on the device:
+// the data-CRC pass in store mode over descriptors of the kept chunks.
+static int store_chunk_crcs(zh_ctx* ctx, const ScatterArgs& a, const std::vector<DevShard>& hs,
+                            const std::vector<int64_t>& hoff, const zh_chunk_dst* dsts,
+                            int64_t ncoords, int64_t nit, int64_t items, hipStream_t s,
+                            char* err, size_t errlen) {
+  std::vector<ItemDesc> wd((size_t)items);
+  for (int64_t i = 0; i < ncoords; i++) {
+    for (int64_t k = 0; k < nit; k++) {
+      ItemDesc& D = wd[(size_t)(hs[i].item_begin + k)];
+      memset(&D, 0, sizeof(D));
+      D.kind = kDescSkip;
+      const int64_t o = hoff[(size_t)(hs[i].item_begin + k)];
+      if (o < 0 || dsts[i].nbytes == 0) continue;
+      D.kind = kDescFullCopy;
+      D.src = (uint64_t)(uintptr_t)((uint8_t*)dsts[i].data + o);
+      D.shard = (uint32_t)i;
+    }
+  }
+  const int64_t nspan = (a.inner_nbytes + kCrcSpan - 1) / kCrcSpan;
+  ItemDesc* d_wd = nullptr;
+  uint32_t* d_part = nullptr;
+  int st;
+  if ((st = dev_alloc(&d_wd, wd.size(), err, errlen)) != ZH_OK ||
+      (st = dev_alloc(&d_part, (size_t)(items * nspan), err, errlen)) != ZH_OK) {
+    (void)hipFree(d_wd);
+    return st;
+  }
+  DataCrcArgs D{};
+  D.desc = d_wd;
+  D.n_items = items;
+  D.len = a.inner_nbytes;
+  D.span = kCrcSpan;
+  D.nspan = (int32_t)nspan;
+  D.store = 1;
+  D.partials = d_part;
+  hipError_t e1 = hipMemcpyAsync(d_wd, wd.data(), wd.size() * sizeof(ItemDesc),
+                                 hipMemcpyHostToDevice, s);
+  if (e1 == hipSuccess)
+    e1 = launch_data_crc(D, (int)std::min<int64_t>(items * nspan, (int64_t)ctx->cu_count * 32), s);
+  if (e1 == hipSuccess) e1 = hipStreamSynchronize(s);
+  (void)hipFree(d_wd);
+  (void)hipFree(d_part);
+  if (e1 != hipSuccess) {
+    set_err(err, errlen, "HIP error %s (%s)", hipGetErrorName(e1), hipGetErrorString(e1));
+    return ZH_EHIP;
+  }
+  return ZH_OK;
+}
+
+constexpr int kWriteFallback = -1;
+
+// zh_array_write in one pass over the region (single-level chains): the layout assumes every
+// in-bounds inner chunk is kept (C order), the fast decode kernels run on an encode view
+// (source = region, destination = payloads) and test each piece against fill_value on the
+// way, the generic kernel takes the clipped/misaligned chunks, and the index (+ crc32c) is
+// written on the device.  If some in-bounds chunk turns out to be all fill_value the layout
+// was wrong: returns kWriteFallback and the caller runs flags → layout → encode.
+static int array_write_fast(zh_ctx* ctx, const zh_array_meta* m, ScatterArgs a,
+                            std::vector<DevShard>& hs, int64_t items, int64_t cps_total,
+                            int tile_mode, zh_chunk_dst* dsts, hipStream_t s, char* err,
+                            size_t errlen) {
+  const zh_codec_chain& c = m->chain;
+  const int n = m->ndim;
+  const int64_t ncoords = (int64_t)hs.size();
+  const int64_t nit = c.sharded ? cps_total : 1;
+  const int64_t cn = a.inner_nbytes + a.crc_extra;  // stored bytes per inner chunk
+  const int64_t isz = c.sharded ? zh_shard_index_size(m) : 0;
+  const bool start = c.sharded && c.index_location == ZH_INDEX_START;
+  const int32_t* inner = leaf_shape(m);
+  std::vector<int64_t> hoff((size_t)items, -1);
+  for (int64_t i = 0; i < ncoords; i++) {
+    DevShard& S = hs[i];
+    int64_t pos = start ? isz : 0, ic[kMaxDims] = {0};
+    for (int64_t k = 0; k < nit; k++) {
+      bool in = true;
+      for (int d = 0; d < n; d++) in &= ic[d] * inner[d] < S.part_hi[d];
+      if (in) {
+        hoff[(size_t)(S.item_begin + k)] = pos;
+        pos += cn;
+      }
+      for (int d = n - 1; d >= 0; d--) {
+        if (++ic[d] < S.box_count[d]) break;
+        ic[d] = 0;
+      }
+    }
+    const int64_t payload = pos - (start ? isz : 0);
+    const int64_t total = payload + isz;
+    if (total > dsts[i].capacity || !dsts[i].data) {
+      set_err(err, errlen, "chunk destination %lld too small: need %lld bytes, have %lld",
+              (long long)i, (long long)total, (long long)dsts[i].capacity);
+      return ZH_EINVAL;
+    }
+    dsts[i].nbytes = total;
+    S.index_off = c.sharded ? (start ? 0 : payload) : -1;
+  }
+  const int64_t pitems = items << a.piece_shift;
+  DevShard* d_shards = nullptr;
+  uint8_t* d_flags = nullptr;
+  int64_t* d_off = nullptr;
+  ItemDesc* d_desc = nullptr;
+  uint32_t* d_slow = nullptr;
+  uint32_t* d_tab = nullptr;
+  CrcJob* d_jobs = nullptr;
+  uint32_t* d_part = nullptr;
+  auto cleanup = [&]() {
+    (void)hipFree(d_shards);
+    (void)hipFree(d_flags);
+    (void)hipFree(d_off);
+    (void)hipFree(d_desc);
+    (void)hipFree(d_slow);
+    (void)hipFree(d_tab);
+    (void)hipFree(d_jobs);
+    (void)hipFree(d_part);
+  };
+  // the encode view: source strides = region, destination strides = payload, destination
+  // addresses relative to the lowest shard buffer
+  ScatterArgs v = a;
+  for (int d = 0; d < kMaxDims; d++) std::swap(v.pstride[d], v.rstride[d]);
+  std::vector<uint32_t> tab = setup_fast(m, v, tile_mode);
+  uint8_t* vbase = nullptr;
+  for (int64_t i = 0; i < ncoords; i++)
+    if (!vbase || (uint8_t*)dsts[i].data < vbase) vbase = (uint8_t*)dsts[i].data;
+  int st;
+  if ((st = dev_alloc(&d_shards, hs.size(), err, errlen)) != ZH_OK ||
+      (st = dev_alloc(&d_flags, (size_t)pitems, err, errlen)) != ZH_OK ||
+      (st = dev_alloc(&d_off, (size_t)items, err, errlen)) != ZH_OK ||
+      (st = dev_alloc(&d_desc, (size_t)items, err, errlen)) != ZH_OK ||
+      (st = dev_alloc(&d_slow, (size_t)items + 4, err, errlen)) != ZH_OK ||
+      (st = dev_alloc(&d_tab, tab.size(), err, errlen)) != ZH_OK) {
+    cleanup();
+    return st;
+  }
+#define ZH_HIPF(call)                                                                      \
+  do {                                                                                     \
+    hipError_t e_ = (call);                                                                \
+    if (e_ != hipSuccess) {                                                                \
+      set_err(err, errlen, "HIP error %s (%s)", hipGetErrorName(e_), hipGetErrorString(e_)); \
+      cleanup();                                                                           \
+      return ZH_EHIP;                                                                      \
+    }                                                                                      \
+  } while (0)
+  ZH_HIPF(hipMemcpyAsync(d_shards, hs.data(), hs.size() * sizeof(DevShard), hipMemcpyHostToDevice,
+                         s));
+  ZH_HIPF(hipMemcpyAsync(d_off, hoff.data(), (size_t)items * sizeof(int64_t),
+                         hipMemcpyHostToDevice, s));
+  if (!tab.empty())
+    ZH_HIPF(hipMemcpyAsync(d_tab, tab.data(), tab.size() * 4, hipMemcpyHostToDevice, s));
+  ZH_HIPF(hipMemsetAsync(d_flags, 0, (size_t)pitems, s));
+  ZH_HIPF(hipMemsetAsync(d_slow, 0, sizeof(uint32_t), s));
+  a.shards = d_shards;
+  a.nshards = ncoords;
+  a.n_citems = items;
+  a.total_items = pitems;
+  a.item_off = d_off;
+  a.flags = d_flags;
+  a.desc = d_desc;
+  a.slow_count = d_slow;
+  a.slow_list = d_slow + 4;
+  ZH_HIPF(launch_encode_resolve(a, vbase, v.fast_mode != kFastNone ? 1 : 0, s));
+  v.shards = d_shards;
+  v.nshards = ncoords;
+  v.n_citems = items;
+  v.total_items = pitems;
+  v.region = vbase;
+  v.flags = d_flags;
+  v.desc = d_desc;
+  v.fast_tab = d_tab;
+  v.item_mul = 0;
+  const int grid = grid_for(ctx, pitems);
+  ZH_HIPF(launch_encode_fast(v, grid, s));
+  ZH_HIPF(launch_encode_slow(a, grid, s));
+  std::vector<uint8_t> hflags((size_t)pitems);
+  ZH_HIPF(hipMemcpyAsync(hflags.data(), d_flags, (size_t)pitems, hipMemcpyDeviceToHost, s));
+  ZH_HIPF(hipStreamSynchronize(s));
+  const int64_t np = 1ll << a.piece_shift;
+  for (int64_t k = 0; k < items; k++) {
+    if (hoff[(size_t)k] < 0) continue;
+    bool any = false;
+    for (int64_t q = 0; q < np; q++) any |= hflags[(size_t)((k << a.piece_shift) + q)] != 0;
+    if (!any) {  // an all-fill chunk is elided by the reference: this layout is wrong
+      cleanup();
+      return kWriteFallback;
+    }
+  }
+  if (c.sharded) {
+    ZH_HIPF(launch_index_write(a, cn, s));
+    if (c.index_has_crc32c) {  // Crc32cCodec.encode of each index, stored on the device
+      std::vector<CrcJob> jobs((size_t)ncoords);
+      int64_t spans = 0;
+      for (int64_t i = 0; i < ncoords; i++) {
+        CrcJob& J = jobs[(size_t)i];
+        J.base = (const uint8_t*)dsts[i].data + hs[i].index_off;
+        J.len = isz - 4;
+        J.span_begin = spans;
+        J.shard = (int32_t)i;
+        J.pad = 0;
+        spans += (J.len + kCrcSpan - 1) / kCrcSpan;
+      }
+      if ((st = dev_alloc(&d_jobs, jobs.size(), err, errlen)) != ZH_OK ||
+          (st = dev_alloc(&d_part, (size_t)spans, err, errlen)) != ZH_OK) {
+        cleanup();
+        return st;
+      }
+      ZH_HIPF(hipMemcpyAsync(d_jobs, jobs.data(), jobs.size() * sizeof(CrcJob),
+                             hipMemcpyHostToDevice, s));
+      ZH_HIPF(launch_crc(d_jobs, ncoords, spans, d_part, nullptr, s));
+    }
+  }
+  ZH_HIPF(hipStreamSynchronize(s));
+  if (c.inner_crc32c) {
+    st = store_chunk_crcs(ctx, a, hs, hoff, dsts, ncoords, nit, items, s, err, errlen);
+    if (st != ZH_OK) {
+      cleanup();
+      return st;
+    }
+  }
+  cleanup();
+#undef ZH_HIPF
+  return ZH_OK;
+}
+
 int zh_array_write(zh_ctx* ctx, const zh_array_meta* m, const void* src, const int64_t* offset,
                    const int64_t* shape, zh_chunk_dst* dsts, int64_t nchunks, void* stream_v,
                    char* err, size_t errlen) {
@@ -1542,6 +1764,15 @@ int zh_array_write(zh_ctx* ctx, const zh_array_meta* m, const void* src, const i
     }
     S.out_base = ob;
     items += c.sharded ? cps_total : 1;
+  }
+  if (!c.nested && env_int("ZH_ENC_FAST", 1) != 0) {
+    a.region = (uint8_t*)src;
+    st = array_write_fast(ctx, m, a, hs, items, cps_total, tile_mode, dsts, s, err, errlen);
+    if (st != kWriteFallback) return st;
+    for (int64_t i = 0; i < ncoords; i++) {
+      hs[i].index_off = 0;
+      dsts[i].nbytes = 0;
+    }
   }
   const int64_t pitems = items << a.piece_shift;
   DevShard* d_shards = nullptr;
@@ -1729,45 +1960,12 @@ int zh_array_write(zh_ctx* ctx, const zh_array_meta* m, const void* src, const i
   a.flags = nullptr;
   ZH_HIPC(launch_scatter(a, m->dtype_size, tile_mode, 1, grid, s));
   if (c.inner_crc32c) {  // Crc32cCodec.encode (:50-60) of every written payload, on the device
-    std::vector<ItemDesc> wd((size_t)items);
-    for (int64_t i = 0; i < ncoords; i++) {
-      const int64_t nit = c.sharded ? cps_total : 1;
-      for (int64_t k = 0; k < nit; k++) {
-        ItemDesc& D = wd[(size_t)(hs[i].item_begin + k)];
-        memset(&D, 0, sizeof(D));
-        D.kind = kDescSkip;
-        const int64_t o = hoff[(size_t)(hs[i].item_begin + k)];
-        if (o < 0 || dsts[i].nbytes == 0) continue;
-        D.kind = kDescFullCopy;
-        D.src = (uint64_t)(uintptr_t)((uint8_t*)dsts[i].data + o);
-        D.shard = (uint32_t)i;
-      }
-    }
-    const int64_t nspan = (a.inner_nbytes + kCrcSpan - 1) / kCrcSpan;
-    ItemDesc* d_wd = nullptr;
-    uint32_t* d_part = nullptr;
-    if ((st = dev_alloc(&d_wd, wd.size(), err, errlen)) != ZH_OK ||
-        (st = dev_alloc(&d_part, (size_t)(items * nspan), err, errlen)) != ZH_OK) {
-      (void)hipFree(d_wd);
+    st = store_chunk_crcs(ctx, a, hs, hoff, dsts, ncoords, c.sharded ? cps_total : 1, items, s,
+                          err, errlen);
+    if (st != ZH_OK) {
       cleanup();
       return st;
     }
-    DataCrcArgs D{};
-    D.desc = d_wd;
-    D.n_items = items;
-    D.len = a.inner_nbytes;
-    D.span = kCrcSpan;
-    D.nspan = (int32_t)nspan;
-    D.store = 1;
-    D.partials = d_part;
-    hipError_t e1 = hipMemcpyAsync(d_wd, wd.data(), wd.size() * sizeof(ItemDesc),
-                                   hipMemcpyHostToDevice, s);
-    if (e1 == hipSuccess)
-      e1 = launch_data_crc(D, (int)std::min<int64_t>(items * nspan, (int64_t)ctx->cu_count * 32), s);
-    if (e1 == hipSuccess) e1 = hipStreamSynchronize(s);
-    (void)hipFree(d_wd);
-    (void)hipFree(d_part);
-    ZH_HIPC(e1);
   }
   ZH_HIPC(hipStreamSynchronize(s));
   cleanup();

@@ -895,7 +895,11 @@ __device__ __forceinline__ int64_t pitem(const ScatterArgs& a, int64_t i) {
 // (item, row batch) steps uniformly, and the loads of step k+1 are issued before the
 // stores of step k, across item boundaries (vmcnt counts stores, so un-pipelined code
 // would wait for the previous stores before every batch of loads).
-template <int DS, int U, int NT, bool CRC = false>
+//
+// FLAGS (write path, encode view: source = region, destination = payload): also record
+// whether each piece holds an element that differs from fill_value (the all-fill elision
+// test of ShardingIndexedCodec.encode :129-133) in a.flags[piece], from the loaded vectors.
+template <int DS, int U, int NT, bool CRC = false, bool FLAGS = false>
 __global__ __launch_bounds__(kBlock) void decode_rows_kernel(ScatterArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   uint2* tab = reinterpret_cast<uint2*>(smem);
@@ -960,6 +964,8 @@ __global__ __launch_bounds__(kBlock) void decode_rows_kernel(ScatterArgs a) {
 
   uint4 va[U];
   uint64_t da[U];
+  bool differs = false;
+  const uint4 ffill = fill16<DS>(a.fill);
   auto load_step = [&](uint4* v, uint64_t* dd) {
 #pragma unroll
     for (int u = 0; u < U; u++) {
@@ -999,6 +1005,17 @@ __global__ __launch_bounds__(kBlock) void decode_rows_kernel(ScatterArgs a) {
       if (da[u] != ~0ull)
         st16s<(NT & 2) != 0>(const_cast<uint8_t*>(dst_a) + da[u],
                              fill_a ? fv_a : xform16<DS>(va[u], a.swap, a.is_bool));
+    if constexpr (FLAGS) {
+#pragma unroll
+      for (int u = 0; u < U; u++)
+        if (da[u] != ~0ull)
+          differs |= (va[u].x != ffill.x) | (va[u].y != ffill.y) | (va[u].z != ffill.z) |
+                      (va[u].w != ffill.w);
+      if (piece_end) {  // uniform: one flag byte per piece, set by any wave that saw data
+        if (__ballot(differs) != 0 && (threadIdx.x & 63) == 0) a.flags[pitem(a, item_a)] = 1;
+        differs = false;
+      }
+    }
     if constexpr (CRC) {
       if (!fill_a) {
 #pragma unroll
@@ -1037,13 +1054,13 @@ __global__ __launch_bounds__(kBlock) void decode_rows_kernel(ScatterArgs a) {
 // L − P_7 − 16 = (L − E_u) + B_lane, E_u = the end of unit u's last payload row.  The host
 // table gives K[u] = x^(8(L − E_u)); the caller applies the lane constant x^(8·B_lane) once
 // per piece.  Returns the lane's share (zero without CRC).
-template <int NT, bool CRC>
+template <int NT, bool CRC, bool FLAGS = false>
 __device__ __forceinline__ uint32_t fast_tiles_rows(const ScatterArgs& a, const uint2* tab,
                                                     const uint8_t* src, uint8_t* dst,
                                                     uint32_t piece, uint32_t* lds,
                                                     const uint32_t (*T)[256],
                                                     const uint32_t (*S)[256],
-                                                    const uint32_t* K) {
+                                                    const uint32_t* K, bool& differs) {
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int t = lane >> 3, g = lane & 7;
   const int64_t s_fd = a.pstride[a.fd], d_fs = a.rstride[a.fs];
@@ -1065,6 +1082,14 @@ __device__ __forceinline__ uint32_t fast_tiles_rows(const ScatterArgs& a, const 
   if (u0 < u1) load(u0);
   for (uint32_t ub = u0; ub < u1; ub += kTG) {
     const bool live = ub + t < u1;
+    if constexpr (FLAGS) {  // write path: any element != fill_value (uint32 tiles)
+      if (live) {
+        const uint32_t f = (uint32_t)a.fill;
+#pragma unroll
+        for (int k = 0; k < 8; k++)
+          differs |= (x[k].x != f) | (x[k].y != f) | (x[k].z != f) | (x[k].w != f);
+      }
+    }
     if (live) {
 #pragma unroll
       for (int k = 0; k < 8; k++) {
@@ -1115,7 +1140,7 @@ __device__ __forceinline__ uint32_t fast_tiles_rows(const ScatterArgs& a, const 
 // origins come from the LDS table.  CRC: the chunk CRC is fused (row-interleaved variant);
 // each wave XORs its lanes' shares, already shifted to the payload end, into the chunk's
 // partial, which data_crc_finalize_kernel compares with the stored value.
-template <int NT, int VARIANT, bool CRC = false>
+template <int NT, int VARIANT, bool CRC = false, bool FLAGS = false>
 __global__ __launch_bounds__(kBlock) void decode_tiles_kernel(ScatterArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   uint2* tab = reinterpret_cast<uint2*>(smem);
@@ -1159,8 +1184,13 @@ __global__ __launch_bounds__(kBlock) void decode_tiles_kernel(ScatterArgs a) {
         fast_tiles<kFastTPB, NT>(a, tab, src, dst, (uint32_t)pitem(a, item) & pmask, tile);
       } else {
         const int64_t pi = pitem(a, item);
-        const uint32_t share = fast_tiles_rows<NT, CRC>(a, tab, src, dst, (uint32_t)pi & pmask,
-                                                        reinterpret_cast<uint32_t*>(tile), T, S, K);
+        bool differs = false;
+        const uint32_t share = fast_tiles_rows<NT, CRC, FLAGS>(
+            a, tab, src, dst, (uint32_t)pi & pmask, reinterpret_cast<uint32_t*>(tile), T, S, K,
+            differs);
+        if constexpr (FLAGS) {
+          if (__ballot(differs) != 0 && (threadIdx.x & 63) == 0) a.flags[pi] = 1;
+        }
         if constexpr (CRC) {
           uint32_t c = multmodp(kb, share);
 #pragma unroll
@@ -1196,69 +1226,165 @@ __global__ __launch_bounds__(kBlock) void decode_slow_kernel(ScatterArgs a) {
   }
 }
 
+// encode one (piece of an) item through the generic paths: source = region, destination =
+// shard payload, boundary padding written as fill_value
+template <int DS, bool TILE>
+__device__ __forceinline__ void encode_item(const ScatterArgs& a, Item& it,
+                                            typename ElemT<DS>::T (*tile)[32][33]) {
+  const int64_t* sstr = a.rstride;
+  const int64_t* dstr = a.pstride;
+  const int n = a.ndim;
+  if constexpr (!TILE) {
+    const int F = a.fs;  // == a.fd
+    uint32_t nrows = 1;
+#pragma unroll
+    for (int d = 0; d < kMaxDims; d++)
+      if (d < n && d != F) nrows *= (uint32_t)it.e[d];
+    if (vec_ok<DS>(a, it, F, sstr, dstr, it.e, true))
+      row_pass<DS, true, false>(a, it, F, sstr, dstr, nrows, it.e, it.ediv);
+    else
+      row_pass<DS, false, false>(a, it, F, sstr, dstr, nrows, it.e, it.ediv);
+  } else {
+    tile_pass<DS>(a, it, sstr, dstr, tile);
+  }
+}
+
 // encode: the same geometry with source = region and destination = shard payload
 template <int DS, bool TILE>
 __global__ __launch_bounds__(kBlock) void encode_kernel(ScatterArgs a) {
   using T = typename ElemT<DS>::T;
-  const int64_t* sstr = a.rstride;
-  const int64_t* dstr = a.pstride;
+  __shared__ T tile[TILE ? kTileTPB : 1][32][33];
   for (int64_t item = blockIdx.x; item < a.total_items; item += gridDim.x) {
     Item it;
     make_item<true>(a, item, it);
     if (it.mode == kSkip) continue;
-    const int n = a.ndim;
-    if constexpr (!TILE) {
-      const int F = a.fs;  // == a.fd
-      uint32_t nrows = 1;
+    encode_item<DS, TILE>(a, it, tile);
+  }
+}
+
+// Does this thread's share of the loadable part of an (encode) item differ from fill_value?
+template <int DS>
+__device__ __forceinline__ bool flag_item(const ScatterArgs& a, const Item& it) {
+  const int64_t* sstr = a.rstride;
+  const int n = a.ndim, F = n - 1;
+  int32_t ext[kMaxDims];
+  FastDiv ediv[kMaxDims];
+  uint32_t nrows = 1;
+  bool vec = !(((uintptr_t)(it.sbase + it.s0 * DS)) & 15);
 #pragma unroll
-      for (int d = 0; d < kMaxDims; d++)
-        if (d < n && d != F) nrows *= (uint32_t)it.e[d];
-      if (vec_ok<DS>(a, it, F, sstr, dstr, it.e, true))
-        row_pass<DS, true, false>(a, it, F, sstr, dstr, nrows, it.e, it.ediv);
-      else
-        row_pass<DS, false, false>(a, it, F, sstr, dstr, nrows, it.e, it.ediv);
-    } else {
-      __shared__ T tile[kTileTPB][32][33];
-      tile_pass<DS>(a, it, sstr, dstr, tile);
+  for (int d = 0; d < kMaxDims; d++) {
+    ext[d] = it.v[d];
+    ediv[d] = it.ediv[d];
+    if (d >= n) continue;
+    if (ext[d] != a.inner[d]) ediv[d] = make_fastdiv((uint32_t)ext[d]);
+    if (d != F) {
+      nrows *= (uint32_t)ext[d];
+      if (ext[d] > 1 && ((sstr[d] * DS) & 15)) vec = false;
+    } else if ((ext[d] * DS) & 15) {
+      vec = false;
     }
   }
+  if (vec) return row_pass<DS, true, true>(a, it, F, sstr, sstr, nrows, ext, ediv);
+  return row_pass<DS, false, true>(a, it, F, sstr, sstr, nrows, ext, ediv);
 }
 
 // encode pre-pass: does the loadable part of an inner chunk differ from fill_value?
 // (ShardingIndexedCodec.encode :129-133 / writeChunk M/core/Array.java:150-151)
 template <int DS>
 __global__ __launch_bounds__(kBlock) void flags_kernel(ScatterArgs a) {
-  const int64_t* sstr = a.rstride;
   for (int64_t item = blockIdx.x; item < a.total_items; item += gridDim.x) {
     Item it;
     make_item<true>(a, item, it);
-    bool diff = false;
-    if (it.mode == kCopy) {
-      const int n = a.ndim, F = n - 1;
-      int32_t ext[kMaxDims];
-      FastDiv ediv[kMaxDims];
-      uint32_t nrows = 1;
-      bool vec = !(((uintptr_t)(it.sbase + it.s0 * DS)) & 15);
-#pragma unroll
-      for (int d = 0; d < kMaxDims; d++) {
-        ext[d] = it.v[d];
-        ediv[d] = it.ediv[d];
-        if (d >= n) continue;
-        if (ext[d] != a.inner[d]) ediv[d] = make_fastdiv((uint32_t)ext[d]);
-        if (d != F) {
-          nrows *= (uint32_t)ext[d];
-          if (ext[d] > 1 && ((sstr[d] * DS) & 15)) vec = false;
-        } else if ((ext[d] * DS) & 15) {
-          vec = false;
-        }
-      }
-      if (vec)
-        diff = row_pass<DS, true, true>(a, it, F, sstr, sstr, nrows, ext, ediv);
-      else
-        diff = row_pass<DS, false, true>(a, it, F, sstr, sstr, nrows, ext, ediv);
-    }
+    const bool diff = it.mode == kCopy && flag_item<DS>(a, it);
     const int any = __syncthreads_or(diff ? 1 : 0);
     if (threadIdx.x == 0) a.flags[item] = any ? 1 : 0;
+  }
+}
+
+// ---------------------------------------------------------------------------------
+// write path, one pass (zh_array_write fast path): the layout assumes every in-bounds
+// inner chunk is kept, the fast decode kernels run on an "encode view" (source = region,
+// destination = payloads) and record the all-fill test per piece; the host falls back to
+// flags → layout → encode when some chunk turns out to be all fill_value.
+// ---------------------------------------------------------------------------------
+// per inner chunk: the encode-view descriptor (src = the chunk's origin in the region,
+// d0 = its payload position relative to vbase, in elements) or a slow-list entry (clipped by
+// the array boundary, misaligned); chunks wholly in the boundary padding are skipped
+__global__ __launch_bounds__(kBlock) void encode_resolve_kernel(ScatterArgs a,
+                                                                const uint8_t* vbase,
+                                                                int vfast) {
+  const int64_t stride = (int64_t)gridDim.x * kBlock;
+  for (int64_t c = (int64_t)blockIdx.x * kBlock + threadIdx.x; c < a.n_citems; c += stride) {
+    Item it;
+    make_item<true>(a, c << a.piece_shift, it);
+    ItemDesc D;
+    D.src = 0;
+    D.d0 = 0;
+    D.fill = 0;
+    D.shard = 0;
+    D.kind = kDescSkip;
+    if (it.mode != kSkip) {
+      bool full = true;
+#pragma unroll
+      for (int d = 0; d < kMaxDims; d++)
+        if (d < a.ndim) full &= it.v[d] == it.e[d];
+      const uint64_t saddr = (uint64_t)(uintptr_t)(it.sbase + it.s0 * a.dsize);
+      const int64_t doff = it.dbase - vbase;
+      D.src = saddr;
+      D.d0 = doff / a.dsize;
+      D.kind = kDescFullCopy;
+      const bool fast = vfast && full && (saddr & 3) == 0 &&
+                        (((uintptr_t)it.dbase) & 15) == 0 && doff >= 0 && doff % a.dsize == 0 &&
+                        (!a.tile || a.dsize == 4);
+      if (fast) {
+        D.kind |= kDescFast;
+      } else {
+        const uint32_t slot = atomicAdd(a.slow_count, 1u);
+        a.slow_list[slot] = (uint32_t)c;
+      }
+    }
+    a.desc[c] = D;
+  }
+}
+
+// the slow-list chunks: generic encode + the all-fill test of each piece
+template <int DS, bool TILE>
+__global__ __launch_bounds__(kBlock) void encode_slow_kernel(ScatterArgs a) {
+  using T = typename ElemT<DS>::T;
+  __shared__ T tile[TILE ? kTileTPB : 1][32][33];
+  const int64_t total = (int64_t)(*a.slow_count) << a.piece_shift;
+  const uint32_t pmask = (1u << a.piece_shift) - 1;
+  for (int64_t k = blockIdx.x; k < total; k += gridDim.x) {
+    const int64_t item = ((int64_t)a.slow_list[k >> a.piece_shift] << a.piece_shift) |
+                         ((uint32_t)k & pmask);
+    Item it;
+    make_item<true>(a, item, it);
+    if (it.mode == kSkip) continue;
+    const bool diff = flag_item<DS>(a, it);
+    const int any = __syncthreads_or(diff ? 1 : 0);
+    if (threadIdx.x == 0 && any) a.flags[item] = 1;
+    encode_item<DS, TILE>(a, it, tile);
+  }
+}
+
+// index entries of every written shard (ShardingIndexedCodec.encode :135-160): (offset,
+// nbytes) of a kept chunk or (-1, -1), in the index codecs' byte order, at S.index_off of
+// the shard's buffer (index_off < 0: shard not written)
+__global__ __launch_bounds__(kBlock) void index_write_kernel(ScatterArgs a, int64_t chunk_nbytes) {
+  const int64_t stride = (int64_t)gridDim.x * kBlock;
+  for (int64_t c = (int64_t)blockIdx.x * kBlock + threadIdx.x; c < a.n_citems; c += stride) {
+    const DevShard& S = a.shards[find_shard(a, c)];
+    if (S.index_off < 0) continue;
+    const int64_t off = a.item_off[c];
+    const uint64_t eo = off >= 0 ? (uint64_t)off : ~0ull;
+    const uint64_t en = off >= 0 ? (uint64_t)chunk_nbytes : ~0ull;
+    uint8_t* e = S.wdata + S.index_off + 16 * (c - S.item_begin);
+#pragma unroll
+    for (int b = 0; b < 8; b++) {
+      const int sh = a.index_be ? 56 - 8 * b : 8 * b;
+      e[b] = (uint8_t)(eo >> sh);
+      e[8 + b] = (uint8_t)(en >> sh);
+    }
   }
 }
 
@@ -1448,6 +1574,14 @@ __global__ void crc_finalize_kernel(const CrcJob* jobs, int64_t njobs, const uin
     c = slen == kCrcSpan ? multmodp(kspan, c) ^ p : crc_combine(c, p, (uint64_t)slen);
   }
   const uint8_t* s = J.base + J.len;  // stored little-endian (Crc32cCodec.java:121,130)
+  if (!status) {  // write path: store it after the index (Crc32cCodec.encode :50-60)
+    uint8_t* w = const_cast<uint8_t*>(s);
+    w[0] = (uint8_t)c;
+    w[1] = (uint8_t)(c >> 8);
+    w[2] = (uint8_t)(c >> 16);
+    w[3] = (uint8_t)(c >> 24);
+    return;
+  }
   const uint32_t stored =
       (uint32_t)s[0] | ((uint32_t)s[1] << 8) | ((uint32_t)s[2] << 16) | ((uint32_t)s[3] << 24);
   uint64_t* st = status + (int64_t)J.shard * kStWords;
@@ -1773,6 +1907,65 @@ hipError_t launch_decode_slow(const ScatterArgs& a, int grid, hipStream_t stream
     case 8: launch_slow_ds<8>(a, grid, stream); break;
     default: return hipErrorInvalidValue;
   }
+  return hipGetLastError();
+}
+
+template <int DS>
+static void launch_encode_fast_ds(const ScatterArgs& v, int grid, hipStream_t s) {
+  const size_t lds = ((size_t)v.fast_n * 8 + 15) & ~(size_t)15;
+  if (v.fast_mode == kFastTileTable) {
+    if constexpr (DS == 4)
+      hipLaunchKernelGGL((decode_tiles_kernel<3, 1, false, true>), dim3(grid), dim3(kBlock),
+                         lds + (size_t)kTG * kTilePitch * 4, s, v);
+  } else if (v.fast_mode != kFastNone) {
+    hipLaunchKernelGGL((decode_rows_kernel<DS, 4, 3, false, true>), dim3(grid), dim3(kBlock), lds,
+                       s, v);
+  }
+}
+
+hipError_t launch_encode_fast(const ScatterArgs& view, int grid, hipStream_t stream) {
+  if (view.total_items == 0 || view.fast_mode == kFastNone) return hipSuccess;
+  switch (view.dsize) {
+    case 1: launch_encode_fast_ds<1>(view, grid, stream); break;
+    case 2: launch_encode_fast_ds<2>(view, grid, stream); break;
+    case 4: launch_encode_fast_ds<4>(view, grid, stream); break;
+    case 8: launch_encode_fast_ds<8>(view, grid, stream); break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+hipError_t launch_encode_resolve(const ScatterArgs& a, const uint8_t* vbase, int vfast,
+                                 hipStream_t stream) {
+  if (a.n_citems == 0) return hipSuccess;
+  const int grid = (int)std::min<int64_t>((a.n_citems + kBlock - 1) / kBlock, 8192);
+  hipLaunchKernelGGL(encode_resolve_kernel, dim3(grid), dim3(kBlock), 0, stream, a, vbase, vfast);
+  return hipGetLastError();
+}
+
+template <int DS>
+static void launch_encode_slow_ds(const ScatterArgs& a, int grid, hipStream_t s) {
+  if (a.tile)
+    hipLaunchKernelGGL((encode_slow_kernel<DS, true>), dim3(grid), dim3(kBlock), 0, s, a);
+  else
+    hipLaunchKernelGGL((encode_slow_kernel<DS, false>), dim3(grid), dim3(kBlock), 0, s, a);
+}
+
+hipError_t launch_encode_slow(const ScatterArgs& a, int grid, hipStream_t stream) {
+  switch (a.dsize) {
+    case 1: launch_encode_slow_ds<1>(a, grid, stream); break;
+    case 2: launch_encode_slow_ds<2>(a, grid, stream); break;
+    case 4: launch_encode_slow_ds<4>(a, grid, stream); break;
+    case 8: launch_encode_slow_ds<8>(a, grid, stream); break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+hipError_t launch_index_write(const ScatterArgs& a, int64_t chunk_nbytes, hipStream_t stream) {
+  if (a.n_citems == 0) return hipSuccess;
+  const int grid = (int)std::min<int64_t>((a.n_citems + kBlock - 1) / kBlock, 8192);
+  hipLaunchKernelGGL(index_write_kernel, dim3(grid), dim3(kBlock), 0, stream, a, chunk_nbytes);
   return hipGetLastError();
 }
 
