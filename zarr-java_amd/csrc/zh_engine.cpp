@@ -191,6 +191,9 @@ struct zh_ctx {
   hipStream_t stream = nullptr;
   int cu_count = 256;
   std::mutex mu;
+  // write-path scratch (grow-only, under mu; zh_array_write synchronises before it returns)
+  uint8_t* wscratch = nullptr;
+  size_t wscratch_cap = 0;
 };
 
 struct zh_plan {
@@ -266,6 +269,7 @@ void zh_ctx_destroy(zh_ctx* c) {
   if (!c) return;
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamDestroy(c->stream);
+  if (c->wscratch) (void)hipFree(c->wscratch);
   delete c;
 }
 
@@ -552,6 +556,24 @@ std::vector<uint32_t> setup_fast(const zh_array_meta* m, ScatterArgs& a, int til
   a.fast_n = (int32_t)(nb * ts * td);
   a.fast_rows = a.fast_n;
   return tab;
+}
+
+// Multiplier of the golden-ratio visit order of the fast kernels (item i → i·m mod t, m odd
+// and coprime to t); 0 = natural order.
+uint64_t golden_item_mul(int64_t total) {
+  if (total <= 1) return 0;
+  const uint64_t t = (uint64_t)total;
+  uint64_t m = ((uint64_t)((double)t * 0.6180339887498949)) | 1;
+  auto gcd = [](uint64_t x, uint64_t y) {
+    while (y) {
+      const uint64_t r = x % y;
+      x = y;
+      y = r;
+    }
+    return x;
+  };
+  while (gcd(m, t) != 1) m += 2;
+  return m % t;
 }
 
 int grid_for(const zh_ctx* ctx, int64_t total_items) {
@@ -1048,21 +1070,8 @@ int zh_plan_create(zh_ctx* ctx, const zh_array_meta* m, const zh_chunk_src* chun
   // Visit items in a golden-ratio stride order: +3.6 % on the tile path (c4) on every normal
   // allocation, neutral on the row path (interleaved A/B, profiles/placement_perm.py), so
   // on by default for tiles.  ZH_ITEM_PERM=0/1 overrides.
-  p->args.item_mul = 0;
-  if (env_int("ZH_ITEM_PERM", p->tile_mode ? 1 : 0) && p->args.total_items > 1) {
-    const uint64_t t = (uint64_t)p->args.total_items;
-    uint64_t m = ((uint64_t)((double)t * 0.6180339887498949)) | 1;
-    auto gcd = [](uint64_t x, uint64_t y) {
-      while (y) {
-        const uint64_t r = x % y;
-        x = y;
-        y = r;
-      }
-      return x;
-    };
-    while (gcd(m, t) != 1) m += 2;
-    p->args.item_mul = m % t;
-  }
+  p->args.item_mul =
+      env_int("ZH_ITEM_PERM", p->tile_mode ? 1 : 0) ? golden_item_mul(p->args.total_items) : 0;
   p->slow_grid = p->grid;
   *out = p;
   return ZH_OK;
@@ -1530,40 +1539,30 @@ static int store_chunk_crcs(zh_ctx* ctx, const ScatterArgs& a, const std::vector
 constexpr int kWriteFallback = -1;
 
 // zh_array_write in one pass over the region (single-level chains): the layout assumes every
-// in-bounds inner chunk is kept (C order), the fast decode kernels run on an encode view
-// (source = region, destination = payloads) and test each piece against fill_value on the
-// way, the generic kernel takes the clipped/misaligned chunks, and the index (+ crc32c) is
-// written on the device.  If some in-bounds chunk turns out to be all fill_value the layout
-// was wrong: returns kWriteFallback and the caller runs flags → layout → encode.
+// in-bounds inner chunk is kept, in C order, so each chunk's payload offset is
+// its rank in the shard's in-bounds box — computed on the device by the resolve kernel.  The
+// fast decode kernels run on an encode view (source = region, destination = payloads) and
+// test each piece against fill_value on the way, the generic kernel takes the clipped or
+// misaligned chunks, and one finish kernel writes the index entries, builds the chunk-CRC
+// descriptors and counts kept chunks that turned out all fill_value.  Index crc32c and
+// chunk crc32c are stored on the device; the call synchronises once.  A non-zero count means
+// the layout was wrong (the reference elides such a chunk): returns kWriteFallback and the
+// caller runs flags → layout → encode.  Scratch tables live in the context (grow-only).
 static int array_write_fast(zh_ctx* ctx, const zh_array_meta* m, ScatterArgs a,
-                            std::vector<DevShard>& hs, int64_t items, int64_t cps_total,
-                            int tile_mode, zh_chunk_dst* dsts, hipStream_t s, char* err,
-                            size_t errlen) {
+                            std::vector<DevShard>& hs, int64_t items, int tile_mode,
+                            zh_chunk_dst* dsts, hipStream_t s, char* err, size_t errlen) {
   const zh_codec_chain& c = m->chain;
   const int n = m->ndim;
   const int64_t ncoords = (int64_t)hs.size();
-  const int64_t nit = c.sharded ? cps_total : 1;
   const int64_t cn = a.inner_nbytes + a.crc_extra;  // stored bytes per inner chunk
   const int64_t isz = c.sharded ? zh_shard_index_size(m) : 0;
   const bool start = c.sharded && c.index_location == ZH_INDEX_START;
   const int32_t* inner = leaf_shape(m);
-  std::vector<int64_t> hoff((size_t)items, -1);
   for (int64_t i = 0; i < ncoords; i++) {
     DevShard& S = hs[i];
-    int64_t pos = start ? isz : 0, ic[kMaxDims] = {0};
-    for (int64_t k = 0; k < nit; k++) {
-      bool in = true;
-      for (int d = 0; d < n; d++) in &= ic[d] * inner[d] < S.part_hi[d];
-      if (in) {
-        hoff[(size_t)(S.item_begin + k)] = pos;
-        pos += cn;
-      }
-      for (int d = n - 1; d >= 0; d--) {
-        if (++ic[d] < S.box_count[d]) break;
-        ic[d] = 0;
-      }
-    }
-    const int64_t payload = pos - (start ? isz : 0);
+    int64_t kept = 1;  // in-bounds inner chunks of the shard (all kept under this layout)
+    for (int d = 0; d < n; d++) kept *= (S.part_hi[d] + inner[d] - 1) / inner[d];
+    const int64_t payload = kept * cn;
     const int64_t total = payload + isz;
     if (total > dsts[i].capacity || !dsts[i].data) {
       set_err(err, errlen, "chunk destination %lld too small: need %lld bytes, have %lld",
@@ -1574,24 +1573,6 @@ static int array_write_fast(zh_ctx* ctx, const zh_array_meta* m, ScatterArgs a,
     S.index_off = c.sharded ? (start ? 0 : payload) : -1;
   }
   const int64_t pitems = items << a.piece_shift;
-  DevShard* d_shards = nullptr;
-  uint8_t* d_flags = nullptr;
-  int64_t* d_off = nullptr;
-  ItemDesc* d_desc = nullptr;
-  uint32_t* d_slow = nullptr;
-  uint32_t* d_tab = nullptr;
-  CrcJob* d_jobs = nullptr;
-  uint32_t* d_part = nullptr;
-  auto cleanup = [&]() {
-    (void)hipFree(d_shards);
-    (void)hipFree(d_flags);
-    (void)hipFree(d_off);
-    (void)hipFree(d_desc);
-    (void)hipFree(d_slow);
-    (void)hipFree(d_tab);
-    (void)hipFree(d_jobs);
-    (void)hipFree(d_part);
-  };
   // the encode view: source strides = region, destination strides = payload, destination
   // addresses relative to the lowest shard buffer
   ScatterArgs v = a;
@@ -1600,103 +1581,117 @@ static int array_write_fast(zh_ctx* ctx, const zh_array_meta* m, ScatterArgs a,
   uint8_t* vbase = nullptr;
   for (int64_t i = 0; i < ncoords; i++)
     if (!vbase || (uint8_t*)dsts[i].data < vbase) vbase = (uint8_t*)dsts[i].data;
-  int st;
-  if ((st = dev_alloc(&d_shards, hs.size(), err, errlen)) != ZH_OK ||
-      (st = dev_alloc(&d_flags, (size_t)pitems, err, errlen)) != ZH_OK ||
-      (st = dev_alloc(&d_off, (size_t)items, err, errlen)) != ZH_OK ||
-      (st = dev_alloc(&d_desc, (size_t)items, err, errlen)) != ZH_OK ||
-      (st = dev_alloc(&d_slow, (size_t)items + 4, err, errlen)) != ZH_OK ||
-      (st = dev_alloc(&d_tab, tab.size(), err, errlen)) != ZH_OK) {
-    cleanup();
-    return st;
+  std::vector<CrcJob> jobs;
+  int64_t spans = 0;
+  if (c.sharded && c.index_has_crc32c) {  // Crc32cCodec.encode of each index (:50-60)
+    jobs.resize((size_t)ncoords);
+    for (int64_t i = 0; i < ncoords; i++) {
+      CrcJob& J = jobs[(size_t)i];
+      J.base = (const uint8_t*)dsts[i].data + hs[i].index_off;
+      J.len = isz - 4;
+      J.span_begin = spans;
+      J.shard = (int32_t)i;
+      J.pad = 0;
+      spans += (J.len + kCrcSpan - 1) / kCrcSpan;
+    }
   }
+  const int64_t nspan = c.inner_crc32c ? (a.inner_nbytes + kCrcSpan - 1) / kCrcSpan : 0;
+  // scratch carve-up (256-B aligned sub-buffers)
+  size_t off = 0;
+  auto carve = [&](size_t bytes) {
+    const size_t o = off;
+    off += (bytes + 255) & ~(size_t)255;
+    return o;
+  };
+  const size_t o_shards = carve(hs.size() * sizeof(DevShard));
+  const size_t o_flags = carve((size_t)pitems);
+  const size_t o_off = carve((size_t)items * sizeof(int64_t));
+  const size_t o_desc = carve((size_t)items * sizeof(ItemDesc));
+  const size_t o_slow = carve(((size_t)items + 4) * sizeof(uint32_t));
+  const size_t o_tab = carve(tab.size() * sizeof(uint32_t));
+  const size_t o_jobs = carve(jobs.size() * sizeof(CrcJob));
+  const size_t o_part = carve((size_t)spans * sizeof(uint32_t));
+  const size_t o_cdesc = carve(c.inner_crc32c ? (size_t)items * sizeof(ItemDesc) : 0);
+  const size_t o_cpart = carve((size_t)(items * nspan) * sizeof(uint32_t));
+  const size_t o_cnt = carve(sizeof(uint32_t));
+  if (off > ctx->wscratch_cap) {
+    (void)hipFree(ctx->wscratch);
+    ctx->wscratch = nullptr;
+    ctx->wscratch_cap = 0;
+    const size_t cap = off + off / 4;
+    int st = dev_alloc(&ctx->wscratch, cap, err, errlen);
+    if (st != ZH_OK) return st;
+    ctx->wscratch_cap = cap;
+  }
+  uint8_t* W = ctx->wscratch;
+  DevShard* d_shards = (DevShard*)(W + o_shards);
+  uint8_t* d_flags = W + o_flags;
+  int64_t* d_off = (int64_t*)(W + o_off);
+  uint32_t* d_slow = (uint32_t*)(W + o_slow);
+  uint32_t* d_cnt = (uint32_t*)(W + o_cnt);
+  ItemDesc* d_cdesc = c.inner_crc32c ? (ItemDesc*)(W + o_cdesc) : nullptr;
 #define ZH_HIPF(call)                                                                      \
   do {                                                                                     \
     hipError_t e_ = (call);                                                                \
     if (e_ != hipSuccess) {                                                                \
       set_err(err, errlen, "HIP error %s (%s)", hipGetErrorName(e_), hipGetErrorString(e_)); \
-      cleanup();                                                                           \
       return ZH_EHIP;                                                                      \
     }                                                                                      \
   } while (0)
   ZH_HIPF(hipMemcpyAsync(d_shards, hs.data(), hs.size() * sizeof(DevShard), hipMemcpyHostToDevice,
                          s));
-  ZH_HIPF(hipMemcpyAsync(d_off, hoff.data(), (size_t)items * sizeof(int64_t),
-                         hipMemcpyHostToDevice, s));
   if (!tab.empty())
-    ZH_HIPF(hipMemcpyAsync(d_tab, tab.data(), tab.size() * 4, hipMemcpyHostToDevice, s));
+    ZH_HIPF(hipMemcpyAsync(W + o_tab, tab.data(), tab.size() * 4, hipMemcpyHostToDevice, s));
+  if (!jobs.empty())
+    ZH_HIPF(hipMemcpyAsync(W + o_jobs, jobs.data(), jobs.size() * sizeof(CrcJob),
+                           hipMemcpyHostToDevice, s));
   ZH_HIPF(hipMemsetAsync(d_flags, 0, (size_t)pitems, s));
   ZH_HIPF(hipMemsetAsync(d_slow, 0, sizeof(uint32_t), s));
+  ZH_HIPF(hipMemsetAsync(d_cnt, 0, sizeof(uint32_t), s));
   a.shards = d_shards;
   a.nshards = ncoords;
   a.n_citems = items;
   a.total_items = pitems;
   a.item_off = d_off;
   a.flags = d_flags;
-  a.desc = d_desc;
+  a.desc = (ItemDesc*)(W + o_desc);
   a.slow_count = d_slow;
   a.slow_list = d_slow + 4;
-  ZH_HIPF(launch_encode_resolve(a, vbase, v.fast_mode != kFastNone ? 1 : 0, s));
+  ZH_HIPF(launch_encode_resolve(a, d_off, start ? isz : 0, cn, vbase,
+                                v.fast_mode != kFastNone ? 1 : 0, s));
   v.shards = d_shards;
   v.nshards = ncoords;
   v.n_citems = items;
   v.total_items = pitems;
   v.region = vbase;
   v.flags = d_flags;
-  v.desc = d_desc;
-  v.fast_tab = d_tab;
-  v.item_mul = 0;
+  v.desc = a.desc;
+  v.fast_tab = (uint32_t*)(W + o_tab);
+  v.item_mul = tile_mode && env_int("ZH_ITEM_PERM", 1) ? golden_item_mul(pitems) : 0;
   const int grid = grid_for(ctx, pitems);
   ZH_HIPF(launch_encode_fast(v, grid, s));
   ZH_HIPF(launch_encode_slow(a, grid, s));
-  std::vector<uint8_t> hflags((size_t)pitems);
-  ZH_HIPF(hipMemcpyAsync(hflags.data(), d_flags, (size_t)pitems, hipMemcpyDeviceToHost, s));
+  ZH_HIPF(launch_encode_finish(a, cn, d_cnt, d_cdesc, s));
+  if (!jobs.empty())
+    ZH_HIPF(launch_crc((const CrcJob*)(W + o_jobs), ncoords, spans, (uint32_t*)(W + o_part),
+                       nullptr, s));
+  if (c.inner_crc32c) {  // Crc32cCodec.encode (:50-60) of every kept chunk payload
+    DataCrcArgs D{};
+    D.desc = d_cdesc;
+    D.n_items = items;
+    D.len = a.inner_nbytes;
+    D.span = kCrcSpan;
+    D.nspan = (int32_t)nspan;
+    D.store = 1;
+    D.partials = (uint32_t*)(W + o_cpart);
+    ZH_HIPF(launch_data_crc(D, (int)std::min<int64_t>(items * nspan, (int64_t)ctx->cu_count * 32),
+                            s));
+  }
+  uint32_t bad = 0;
+  ZH_HIPF(hipMemcpyAsync(&bad, d_cnt, sizeof(bad), hipMemcpyDeviceToHost, s));
   ZH_HIPF(hipStreamSynchronize(s));
-  const int64_t np = 1ll << a.piece_shift;
-  for (int64_t k = 0; k < items; k++) {
-    if (hoff[(size_t)k] < 0) continue;
-    bool any = false;
-    for (int64_t q = 0; q < np; q++) any |= hflags[(size_t)((k << a.piece_shift) + q)] != 0;
-    if (!any) {  // an all-fill chunk is elided by the reference: this layout is wrong
-      cleanup();
-      return kWriteFallback;
-    }
-  }
-  if (c.sharded) {
-    ZH_HIPF(launch_index_write(a, cn, s));
-    if (c.index_has_crc32c) {  // Crc32cCodec.encode of each index, stored on the device
-      std::vector<CrcJob> jobs((size_t)ncoords);
-      int64_t spans = 0;
-      for (int64_t i = 0; i < ncoords; i++) {
-        CrcJob& J = jobs[(size_t)i];
-        J.base = (const uint8_t*)dsts[i].data + hs[i].index_off;
-        J.len = isz - 4;
-        J.span_begin = spans;
-        J.shard = (int32_t)i;
-        J.pad = 0;
-        spans += (J.len + kCrcSpan - 1) / kCrcSpan;
-      }
-      if ((st = dev_alloc(&d_jobs, jobs.size(), err, errlen)) != ZH_OK ||
-          (st = dev_alloc(&d_part, (size_t)spans, err, errlen)) != ZH_OK) {
-        cleanup();
-        return st;
-      }
-      ZH_HIPF(hipMemcpyAsync(d_jobs, jobs.data(), jobs.size() * sizeof(CrcJob),
-                             hipMemcpyHostToDevice, s));
-      ZH_HIPF(launch_crc(d_jobs, ncoords, spans, d_part, nullptr, s));
-    }
-  }
-  ZH_HIPF(hipStreamSynchronize(s));
-  if (c.inner_crc32c) {
-    st = store_chunk_crcs(ctx, a, hs, hoff, dsts, ncoords, nit, items, s, err, errlen);
-    if (st != ZH_OK) {
-      cleanup();
-      return st;
-    }
-  }
-  cleanup();
 #undef ZH_HIPF
-  return ZH_OK;
+  return bad ? kWriteFallback : ZH_OK;
 }
 
 int zh_array_write(zh_ctx* ctx, const zh_array_meta* m, const void* src, const int64_t* offset,
@@ -1767,7 +1762,7 @@ int zh_array_write(zh_ctx* ctx, const zh_array_meta* m, const void* src, const i
   }
   if (!c.nested && env_int("ZH_ENC_FAST", 1) != 0) {
     a.region = (uint8_t*)src;
-    st = array_write_fast(ctx, m, a, hs, items, cps_total, tile_mode, dsts, s, err, errlen);
+    st = array_write_fast(ctx, m, a, hs, items, tile_mode, dsts, s, err, errlen);
     if (st != kWriteFallback) return st;
     for (int64_t i = 0; i < ncoords; i++) {
       hs[i].index_off = 0;

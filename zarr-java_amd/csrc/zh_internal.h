@@ -189,14 +189,17 @@ hipError_t launch_scatter(const ScatterArgs& a, int dsize, int tile_mode, int en
                           hipStream_t stream);
 hipError_t launch_decode_slow(const ScatterArgs& a, int grid, hipStream_t stream);
 hipError_t launch_flags(const ScatterArgs& a, int dsize, int grid, hipStream_t stream);
-// write path, one pass: encode-view descriptors + slow list, the fast kernels with the
-// all-fill test, the slow list through the generic encode, index entries on the device;
-// launch_crc with status == nullptr stores the index crc32c instead of checking it
-hipError_t launch_encode_resolve(const ScatterArgs& a, const uint8_t* vbase, int vfast,
+// write path, one pass: payload offsets + encode-view descriptors + slow list, the fast
+// kernels with the all-fill test, the slow list through the generic encode, then the finish
+// kernel (all-fill count, index entries, chunk-CRC descriptors); launch_crc with
+// status == nullptr stores the index crc32c instead of checking it
+hipError_t launch_encode_resolve(const ScatterArgs& a, int64_t* item_off, int64_t base_off,
+                                 int64_t cn, const uint8_t* vbase, int vfast,
                                  hipStream_t stream);
 hipError_t launch_encode_fast(const ScatterArgs& view, int grid, hipStream_t stream);
 hipError_t launch_encode_slow(const ScatterArgs& a, int grid, hipStream_t stream);
-hipError_t launch_index_write(const ScatterArgs& a, int64_t chunk_nbytes, hipStream_t stream);
+hipError_t launch_encode_finish(const ScatterArgs& a, int64_t chunk_nbytes, uint32_t* bad,
+                                ItemDesc* crc_desc, hipStream_t stream);
 hipError_t launch_synth_fill(void* dst, int64_t n, int dsize, int64_t first, uint64_t seed,
                              hipStream_t stream);
 hipError_t launch_synth_verify(const void* region, int ndim, const int64_t* array_shape,

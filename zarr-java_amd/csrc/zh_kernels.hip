@@ -323,8 +323,12 @@ __device__ __forceinline__ int64_t make_item(const ScatterArgs& a, int64_t item,
 // row pass: rows along dim F, unit-stride on both sides (on the destination only for
 // constant fills).  VEC: 16-byte granules; otherwise single elements with
 // loadable-extent checks.  CHECK: compare against fill_value instead of storing.
+// CLIP (encode, VEC only): the item is clipped by the array domain at a 16-byte granule
+// boundary of F and/or in whole rows; granules outside the loadable extents store the
+// encoded fill_value (boundary padding) instead of loading.  FLAG (encode, storing): also
+// return whether a loaded element differs from fill_value (one read for test + encode).
 // ---------------------------------------------------------------------------------
-template <int DS, bool VEC, bool CHECK>
+template <int DS, bool VEC, bool CHECK, bool CLIP = false, bool FLAG = false>
 __device__ __forceinline__ bool row_pass(const ScatterArgs& a, const Item& it, int F,
                                          const int64_t* sstr, const int64_t* dstr,
                                          uint32_t nrows, const int32_t* ext,
@@ -345,12 +349,15 @@ __device__ __forceinline__ bool row_pass(const ScatterArgs& a, const Item& it, i
   const uint32_t r1 = (uint32_t)(((uint64_t)nrows * (it.piece + 1)) / pieces);
   const uint32_t total = (r1 - r0) * gpr;
   const uint4 fv = fill16<DS>(CHECK ? a.fill : it.fill);
+  const uint4 pad = fill16<DS>(a.fill);  // CLIP: raw fill_value granule (encoded on store)
   int64_t sF = 1, dF = 1;
+  uint32_t vgF = 0;  // CLIP: loadable granules along F
 #pragma unroll
   for (int d = 0; d < kMaxDims; d++)
     if (d == F) {
       sF = sstr[d];
       dF = dstr[d];
+      vgF = (uint32_t)(it.v[d] * DS / 16);
     }
   bool diff = false;
   for (uint32_t base = threadIdx.x; base < total; base += kBlock * U) {
@@ -383,7 +390,12 @@ __device__ __forceinline__ bool row_pass(const ScatterArgs& a, const Item& it, i
       }
       if constexpr (VEC) {
         doff[u] = dof * DS + (int64_t)c * 16;
-        if (!fill) vv[u] = ld16(it.sbase + so * DS + (int64_t)c * 16);
+        if constexpr (CLIP) {
+          valid &= c < vgF;
+          vv[u] = valid ? ld16(it.sbase + so * DS + (int64_t)c * 16) : pad;
+        } else if (!fill) {
+          vv[u] = ld16(it.sbase + so * DS + (int64_t)c * 16);
+        }
       } else {
         doff[u] = (dof + (int64_t)c * dF) * DS;
         bool vF = false;
@@ -405,8 +417,11 @@ __device__ __forceinline__ bool row_pass(const ScatterArgs& a, const Item& it, i
         }
       } else if constexpr (VEC) {
         st16(it.dbase + doff[u], fill ? fv : xform16<DS>(vv[u], a.swap, a.is_bool));
+        if constexpr (FLAG)
+          diff |= (vv[u].x != pad.x) | (vv[u].y != pad.y) | (vv[u].z != pad.z) | (vv[u].w != pad.w);
       } else {
         st1<DS>(it.dbase + doff[u], fill ? (T)it.fill : xform1<DS>(sv[u], a.swap, a.is_bool));
+        if constexpr (FLAG) diff |= sv[u] != (T)a.fill;
       }
     }
   }
@@ -436,6 +451,26 @@ __device__ __forceinline__ bool vec_ok(const ScatterArgs& a, const Item& it, int
       if (need_src) ok &= !((sstr[d] * DS) & 15);
     }
     if (need_src) ok &= it.v[d] == ext[d];
+  }
+  return ok;
+}
+
+// Encode: can a domain-clipped item move in 16-byte granules along F (row_pass CLIP)?  The
+// loadable extent along F must end on a granule boundary; clipped rows are padded whole.
+template <int DS>
+__device__ __forceinline__ bool vec_clip_ok(const ScatterArgs& a, const Item& it, int F,
+                                            const int64_t* sstr, const int64_t* dstr) {
+  const int n = a.ndim;
+  bool ok = !(((uintptr_t)(it.dbase + it.d0 * DS)) & 15) &&
+            !(((uintptr_t)(it.sbase + it.s0 * DS)) & 3);
+#pragma unroll
+  for (int d = 0; d < kMaxDims; d++) {
+    if (d >= n) continue;
+    if (d == F) {
+      ok &= !((it.e[d] * DS) & 15) && !((it.v[d] * DS) & 15);
+    } else if (it.e[d] > 1) {
+      ok &= !((dstr[d] * DS) & 15) && !((sstr[d] * DS) & 15);
+    }
   }
   return ok;
 }
@@ -1227,9 +1262,10 @@ __global__ __launch_bounds__(kBlock) void decode_slow_kernel(ScatterArgs a) {
 }
 
 // encode one (piece of an) item through the generic paths: source = region, destination =
-// shard payload, boundary padding written as fill_value
-template <int DS, bool TILE>
-__device__ __forceinline__ void encode_item(const ScatterArgs& a, Item& it,
+// shard payload, boundary padding written as fill_value.  FLAG (row paths): returns this
+// thread's share of the all-fill test from the same loads.
+template <int DS, bool TILE, bool FLAG = false>
+__device__ __forceinline__ bool encode_item(const ScatterArgs& a, Item& it,
                                             typename ElemT<DS>::T (*tile)[32][33]) {
   const int64_t* sstr = a.rstride;
   const int64_t* dstr = a.pstride;
@@ -1237,15 +1273,20 @@ __device__ __forceinline__ void encode_item(const ScatterArgs& a, Item& it,
   if constexpr (!TILE) {
     const int F = a.fs;  // == a.fd
     uint32_t nrows = 1;
+    bool clipped = false;
 #pragma unroll
-    for (int d = 0; d < kMaxDims; d++)
+    for (int d = 0; d < kMaxDims; d++) {
       if (d < n && d != F) nrows *= (uint32_t)it.e[d];
-    if (vec_ok<DS>(a, it, F, sstr, dstr, it.e, true))
-      row_pass<DS, true, false>(a, it, F, sstr, dstr, nrows, it.e, it.ediv);
-    else
-      row_pass<DS, false, false>(a, it, F, sstr, dstr, nrows, it.e, it.ediv);
+      if (d < n) clipped |= it.v[d] != it.e[d];
+    }
+    if (!clipped && vec_ok<DS>(a, it, F, sstr, dstr, it.e, true))
+      return row_pass<DS, true, false, false, FLAG>(a, it, F, sstr, dstr, nrows, it.e, it.ediv);
+    if (clipped && vec_clip_ok<DS>(a, it, F, sstr, dstr))
+      return row_pass<DS, true, false, true, FLAG>(a, it, F, sstr, dstr, nrows, it.e, it.ediv);
+    return row_pass<DS, false, false, false, FLAG>(a, it, F, sstr, dstr, nrows, it.e, it.ediv);
   } else {
     tile_pass<DS>(a, it, sstr, dstr, tile);
+    return false;
   }
 }
 
@@ -1307,14 +1348,37 @@ __global__ __launch_bounds__(kBlock) void flags_kernel(ScatterArgs a) {
 // destination = payloads) and record the all-fill test per piece; the host falls back to
 // flags → layout → encode when some chunk turns out to be all fill_value.
 // ---------------------------------------------------------------------------------
-// per inner chunk: the encode-view descriptor (src = the chunk's origin in the region,
-// d0 = its payload position relative to vbase, in elements) or a slow-list entry (clipped by
-// the array boundary, misaligned); chunks wholly in the boundary padding are skipped
-__global__ __launch_bounds__(kBlock) void encode_resolve_kernel(ScatterArgs a,
+// per inner chunk: its payload offset under the one-pass layout (every in-bounds inner chunk
+// kept, C order: the chunk's rank in the shard's in-bounds box × stored chunk bytes, after the
+// index when it is at the start; -1 for chunks wholly in the boundary padding), then the
+// encode-view descriptor (src = the chunk's origin in the region, d0 = its payload position
+// relative to vbase, in elements) or a slow-list entry (clipped by the array boundary,
+// misaligned)
+__global__ __launch_bounds__(kBlock) void encode_resolve_kernel(ScatterArgs a, int64_t* item_off,
+                                                                int64_t base_off, int64_t cn,
                                                                 const uint8_t* vbase,
                                                                 int vfast) {
   const int64_t stride = (int64_t)gridDim.x * kBlock;
   for (int64_t c = (int64_t)blockIdx.x * kBlock + threadIdx.x; c < a.n_citems; c += stride) {
+    {
+      const DevShard& S = a.shards[find_shard(a, c)];
+      uint32_t j = (uint32_t)(c - S.item_begin);
+      int64_t rank = 0, mul = 1;
+      bool in = true;
+#pragma unroll
+      for (int d = kMaxDims - 1; d >= 0; --d) {
+        if (d >= a.ndim) continue;
+        const uint32_t bc = (uint32_t)S.box_count[d];
+        const uint32_t q = j / bc;
+        const int64_t icd = (int64_t)(j - q * bc);
+        j = q;
+        const int64_t cnt = (S.part_hi[d] + a.inner[d] - 1) / a.inner[d];
+        in &= icd < cnt;
+        rank += icd * mul;
+        mul *= cnt;
+      }
+      item_off[c] = in ? base_off + rank * cn : -1;
+    }
     Item it;
     make_item<true>(a, c << a.piece_shift, it);
     ItemDesc D;
@@ -1360,22 +1424,42 @@ __global__ __launch_bounds__(kBlock) void encode_slow_kernel(ScatterArgs a) {
     Item it;
     make_item<true>(a, item, it);
     if (it.mode == kSkip) continue;
-    const bool diff = flag_item<DS>(a, it);
+    // row paths test the loaded vectors on the way; the tile path reads the piece twice
+    const bool diff = TILE ? flag_item<DS>(a, it) : encode_item<DS, false, true>(a, it, tile);
+    if constexpr (TILE) encode_item<DS, TILE>(a, it, tile);
     const int any = __syncthreads_or(diff ? 1 : 0);
     if (threadIdx.x == 0 && any) a.flags[item] = 1;
-    encode_item<DS, TILE>(a, it, tile);
   }
 }
 
-// index entries of every written shard (ShardingIndexedCodec.encode :135-160): (offset,
-// nbytes) of a kept chunk or (-1, -1), in the index codecs' byte order, at S.index_off of
-// the shard's buffer (index_off < 0: shard not written)
-__global__ __launch_bounds__(kBlock) void index_write_kernel(ScatterArgs a, int64_t chunk_nbytes) {
+// after the one-pass encode, per inner chunk: count a kept chunk none of whose pieces holds a
+// non-fill element (the layout assumed it kept; the reference elides it, :129-133 → the host
+// falls back), build its chunk-CRC store descriptor (inner crc32c), and write the index entry
+// (ShardingIndexedCodec.encode :135-160): (offset, nbytes) or (-1, -1), in the index codecs'
+// byte order, at S.index_off of the shard's buffer
+__global__ __launch_bounds__(kBlock) void encode_finish_kernel(ScatterArgs a, int64_t chunk_nbytes,
+                                                               uint32_t* bad, ItemDesc* crc_desc) {
   const int64_t stride = (int64_t)gridDim.x * kBlock;
+  const int64_t np = 1ll << a.piece_shift;
   for (int64_t c = (int64_t)blockIdx.x * kBlock + threadIdx.x; c < a.n_citems; c += stride) {
-    const DevShard& S = a.shards[find_shard(a, c)];
-    if (S.index_off < 0) continue;
+    const int64_t s = find_shard(a, c);
+    const DevShard& S = a.shards[s];
     const int64_t off = a.item_off[c];
+    if (off >= 0) {
+      bool any = false;
+      for (int64_t q = 0; q < np; q++) any |= a.flags[(c << a.piece_shift) + q] != 0;
+      if (!any) atomicAdd(bad, 1u);
+    }
+    if (crc_desc) {
+      ItemDesc D;
+      D.src = off >= 0 ? (uint64_t)(uintptr_t)(S.wdata + off) : 0;
+      D.d0 = 0;
+      D.fill = 0;
+      D.kind = off >= 0 ? kDescFullCopy : kDescSkip;
+      D.shard = (uint32_t)s;
+      crc_desc[c] = D;
+    }
+    if (!a.sharded || S.index_off < 0) continue;
     const uint64_t eo = off >= 0 ? (uint64_t)off : ~0ull;
     const uint64_t en = off >= 0 ? (uint64_t)chunk_nbytes : ~0ull;
     uint8_t* e = S.wdata + S.index_off + 16 * (c - S.item_begin);
@@ -1935,11 +2019,13 @@ hipError_t launch_encode_fast(const ScatterArgs& view, int grid, hipStream_t str
   return hipGetLastError();
 }
 
-hipError_t launch_encode_resolve(const ScatterArgs& a, const uint8_t* vbase, int vfast,
+hipError_t launch_encode_resolve(const ScatterArgs& a, int64_t* item_off, int64_t base_off,
+                                 int64_t cn, const uint8_t* vbase, int vfast,
                                  hipStream_t stream) {
   if (a.n_citems == 0) return hipSuccess;
   const int grid = (int)std::min<int64_t>((a.n_citems + kBlock - 1) / kBlock, 8192);
-  hipLaunchKernelGGL(encode_resolve_kernel, dim3(grid), dim3(kBlock), 0, stream, a, vbase, vfast);
+  hipLaunchKernelGGL(encode_resolve_kernel, dim3(grid), dim3(kBlock), 0, stream, a, item_off,
+                     base_off, cn, vbase, vfast);
   return hipGetLastError();
 }
 
@@ -1962,10 +2048,12 @@ hipError_t launch_encode_slow(const ScatterArgs& a, int grid, hipStream_t stream
   return hipGetLastError();
 }
 
-hipError_t launch_index_write(const ScatterArgs& a, int64_t chunk_nbytes, hipStream_t stream) {
+hipError_t launch_encode_finish(const ScatterArgs& a, int64_t chunk_nbytes, uint32_t* bad,
+                                ItemDesc* crc_desc, hipStream_t stream) {
   if (a.n_citems == 0) return hipSuccess;
   const int grid = (int)std::min<int64_t>((a.n_citems + kBlock - 1) / kBlock, 8192);
-  hipLaunchKernelGGL(index_write_kernel, dim3(grid), dim3(kBlock), 0, stream, a, chunk_nbytes);
+  hipLaunchKernelGGL(encode_finish_kernel, dim3(grid), dim3(kBlock), 0, stream, a, chunk_nbytes,
+                     bad, crc_desc);
   return hipGetLastError();
 }
 
