@@ -67,6 +67,8 @@ def device_write(dev, meta, arr):
     coords = chunk_coords(meta, [0] * n, shape)
     cap = lib().zh_array_encoded_bound(C.byref(meta))
     bufs = [dev.malloc(cap) for _ in coords]
+    for b in bufs:  # poison: every byte of the result must be written by the encode
+        dev.memset(b, 0xA5, cap)
     sizes = dev.array_write(meta, src, [0] * n, shape, [(b, cap) for b in bufs])
     out = []
     for b, sz in zip(bufs, sizes):

@@ -216,6 +216,23 @@ def test_device_encode_one_pass(dev, monkeypatch, dsize, mode, loc):
     assert device_write(dev, meta, arr) == want
 
 
+@pytest.mark.parametrize("dsize", [1, 2, 4, 8])
+@pytest.mark.parametrize("order", [None, [1, 0, 2]])
+def test_device_encode_grouped_rows(dev, dsize, order):
+    """One-pass write with chunk rows of 1 KiB along the last axis split into inner chunks of
+    64-128 B rows (many inner chunks adjacent along the region's unit-stride axis); boundary
+    shards exercise the slow list beside the fast kernel."""
+    last = 1024 // dsize
+    inner_last = (64 if dsize <= 2 else 128) // dsize
+    shape = [20, 24, last + last // 2 + inner_last // 2]
+    meta = A.make_meta(shape, [8, 16, last], dsize, endian=A.ZH_ENDIAN_BIG, sharded=True,
+                       inner_chunk_shape=[4, 8, inner_last], transpose_order=order)
+    arr = rand_array(shape, dsize, seed=41 + dsize)
+    arr[arr == 0] = 1
+    want = encode_oracle(meta, arr)
+    assert device_write(dev, meta, arr) == want
+
+
 def test_device_encode_one_pass_fallback(dev):
     """A late all-fill inner chunk (seen only after the one-pass kernels ran) sends the write
     back through flags → layout → encode; the bytes still equal the oracle's."""

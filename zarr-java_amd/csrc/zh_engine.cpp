@@ -1604,7 +1604,7 @@ static int array_write_fast(zh_ctx* ctx, const zh_array_meta* m, ScatterArgs a,
     return o;
   };
   const size_t o_shards = carve(hs.size() * sizeof(DevShard));
-  const size_t o_flags = carve((size_t)pitems);
+  const size_t o_flags = carve((size_t)items);  // one all-fill flag per inner chunk
   const size_t o_off = carve((size_t)items * sizeof(int64_t));
   const size_t o_desc = carve((size_t)items * sizeof(ItemDesc));
   const size_t o_slow = carve(((size_t)items + 4) * sizeof(uint32_t));
@@ -1645,7 +1645,7 @@ static int array_write_fast(zh_ctx* ctx, const zh_array_meta* m, ScatterArgs a,
   if (!jobs.empty())
     ZH_HIPF(hipMemcpyAsync(W + o_jobs, jobs.data(), jobs.size() * sizeof(CrcJob),
                            hipMemcpyHostToDevice, s));
-  ZH_HIPF(hipMemsetAsync(d_flags, 0, (size_t)pitems, s));
+  ZH_HIPF(hipMemsetAsync(d_flags, 0, (size_t)items, s));
   ZH_HIPF(hipMemsetAsync(d_slow, 0, sizeof(uint32_t), s));
   ZH_HIPF(hipMemsetAsync(d_cnt, 0, sizeof(uint32_t), s));
   a.shards = d_shards;
@@ -1667,9 +1667,12 @@ static int array_write_fast(zh_ctx* ctx, const zh_array_meta* m, ScatterArgs a,
   v.flags = d_flags;
   v.desc = a.desc;
   v.fast_tab = (uint32_t*)(W + o_tab);
-  v.item_mul = tile_mode && env_int("ZH_ITEM_PERM", 1) ? golden_item_mul(pitems) : 0;
+  // golden-ratio visit order and (uint32 rows) 8 rows in flight per lane: +2.4 % on c3, the
+  // order +4 % on c4 (interleaved A/B, profiles/tune_write.py → profiles/r01/experiments/)
+  v.item_mul = env_int("ZH_ITEM_PERM", 1) ? golden_item_mul(pitems) : 0;
+  v.nt = env_int("ZH_ENC_NT", 3) & 3;
   const int grid = grid_for(ctx, pitems);
-  ZH_HIPF(launch_encode_fast(v, grid, s));
+  ZH_HIPF(launch_encode_fast(v, grid, env_int("ZH_ENC_DEEP", 1), s));
   ZH_HIPF(launch_encode_slow(a, grid, s));
   ZH_HIPF(launch_encode_finish(a, cn, d_cnt, d_cdesc, s));
   if (!jobs.empty())

@@ -196,7 +196,7 @@ hipError_t launch_flags(const ScatterArgs& a, int dsize, int grid, hipStream_t s
 hipError_t launch_encode_resolve(const ScatterArgs& a, int64_t* item_off, int64_t base_off,
                                  int64_t cn, const uint8_t* vbase, int vfast,
                                  hipStream_t stream);
-hipError_t launch_encode_fast(const ScatterArgs& view, int grid, hipStream_t stream);
+hipError_t launch_encode_fast(const ScatterArgs& view, int grid, int deep, hipStream_t stream);
 hipError_t launch_encode_slow(const ScatterArgs& a, int grid, hipStream_t stream);
 hipError_t launch_encode_finish(const ScatterArgs& a, int64_t chunk_nbytes, uint32_t* bad,
                                 ItemDesc* crc_desc, hipStream_t stream);

@@ -1047,7 +1047,8 @@ __global__ __launch_bounds__(kBlock) void decode_rows_kernel(ScatterArgs a) {
           differs |= (va[u].x != ffill.x) | (va[u].y != ffill.y) | (va[u].z != ffill.z) |
                       (va[u].w != ffill.w);
       if (piece_end) {  // uniform: one flag byte per piece, set by any wave that saw data
-        if (__ballot(differs) != 0 && (threadIdx.x & 63) == 0) a.flags[pitem(a, item_a)] = 1;
+        if (__ballot(differs) != 0 && (threadIdx.x & 63) == 0)
+          a.flags[pitem(a, item_a) >> a.piece_shift] = 1;
         differs = false;
       }
     }
@@ -1224,7 +1225,7 @@ __global__ __launch_bounds__(kBlock) void decode_tiles_kernel(ScatterArgs a) {
             a, tab, src, dst, (uint32_t)pi & pmask, reinterpret_cast<uint32_t*>(tile), T, S, K,
             differs);
         if constexpr (FLAGS) {
-          if (__ballot(differs) != 0 && (threadIdx.x & 63) == 0) a.flags[pi] = 1;
+          if (__ballot(differs) != 0 && (threadIdx.x & 63) == 0) a.flags[pi >> a.piece_shift] = 1;
         }
         if constexpr (CRC) {
           uint32_t c = multmodp(kb, share);
@@ -1428,7 +1429,7 @@ __global__ __launch_bounds__(kBlock) void encode_slow_kernel(ScatterArgs a) {
     const bool diff = TILE ? flag_item<DS>(a, it) : encode_item<DS, false, true>(a, it, tile);
     if constexpr (TILE) encode_item<DS, TILE>(a, it, tile);
     const int any = __syncthreads_or(diff ? 1 : 0);
-    if (threadIdx.x == 0 && any) a.flags[item] = 1;
+    if (threadIdx.x == 0 && any) a.flags[item >> a.piece_shift] = 1;
   }
 }
 
@@ -1440,16 +1441,11 @@ __global__ __launch_bounds__(kBlock) void encode_slow_kernel(ScatterArgs a) {
 __global__ __launch_bounds__(kBlock) void encode_finish_kernel(ScatterArgs a, int64_t chunk_nbytes,
                                                                uint32_t* bad, ItemDesc* crc_desc) {
   const int64_t stride = (int64_t)gridDim.x * kBlock;
-  const int64_t np = 1ll << a.piece_shift;
   for (int64_t c = (int64_t)blockIdx.x * kBlock + threadIdx.x; c < a.n_citems; c += stride) {
     const int64_t s = find_shard(a, c);
     const DevShard& S = a.shards[s];
     const int64_t off = a.item_off[c];
-    if (off >= 0) {
-      bool any = false;
-      for (int64_t q = 0; q < np; q++) any |= a.flags[(c << a.piece_shift) + q] != 0;
-      if (!any) atomicAdd(bad, 1u);
-    }
+    if (off >= 0 && a.flags[c] == 0) atomicAdd(bad, 1u);
     if (crc_desc) {
       ItemDesc D;
       D.src = off >= 0 ? (uint64_t)(uintptr_t)(S.wdata + off) : 0;
@@ -1994,26 +1990,50 @@ hipError_t launch_decode_slow(const ScatterArgs& a, int grid, hipStream_t stream
   return hipGetLastError();
 }
 
+// the encode view through the fast kernels (FLAGS); v.nt picks the cache policy and
+// `deep` 8 rows in flight per lane instead of 4 (uint32 rows; tuning, ZH_ENC_NT/ZH_ENC_DEEP)
 template <int DS>
-static void launch_encode_fast_ds(const ScatterArgs& v, int grid, hipStream_t s) {
+static void launch_encode_fast_ds(const ScatterArgs& v, int grid, int deep, hipStream_t s) {
   const size_t lds = ((size_t)v.fast_n * 8 + 15) & ~(size_t)15;
   if (v.fast_mode == kFastTileTable) {
-    if constexpr (DS == 4)
-      hipLaunchKernelGGL((decode_tiles_kernel<3, 1, false, true>), dim3(grid), dim3(kBlock),
-                         lds + (size_t)kTG * kTilePitch * 4, s, v);
+    if constexpr (DS == 4) {
+      const size_t l = lds + (size_t)kTG * kTilePitch * 4;
+      switch (v.nt) {
+        case 0: hipLaunchKernelGGL((decode_tiles_kernel<0, 1, false, true>), dim3(grid), dim3(kBlock), l, s, v); break;
+        case 1: hipLaunchKernelGGL((decode_tiles_kernel<1, 1, false, true>), dim3(grid), dim3(kBlock), l, s, v); break;
+        case 2: hipLaunchKernelGGL((decode_tiles_kernel<2, 1, false, true>), dim3(grid), dim3(kBlock), l, s, v); break;
+        default: hipLaunchKernelGGL((decode_tiles_kernel<3, 1, false, true>), dim3(grid), dim3(kBlock), l, s, v); break;
+      }
+    }
   } else if (v.fast_mode != kFastNone) {
+    if constexpr (DS == 4) {
+      if (deep) {
+        switch (v.nt) {
+          case 0: hipLaunchKernelGGL((decode_rows_kernel<DS, 8, 0, false, true>), dim3(grid), dim3(kBlock), lds, s, v); return;
+          case 1: hipLaunchKernelGGL((decode_rows_kernel<DS, 8, 1, false, true>), dim3(grid), dim3(kBlock), lds, s, v); return;
+          case 2: hipLaunchKernelGGL((decode_rows_kernel<DS, 8, 2, false, true>), dim3(grid), dim3(kBlock), lds, s, v); return;
+          default: hipLaunchKernelGGL((decode_rows_kernel<DS, 8, 3, false, true>), dim3(grid), dim3(kBlock), lds, s, v); return;
+        }
+      }
+      switch (v.nt) {
+        case 0: hipLaunchKernelGGL((decode_rows_kernel<DS, 4, 0, false, true>), dim3(grid), dim3(kBlock), lds, s, v); return;
+        case 1: hipLaunchKernelGGL((decode_rows_kernel<DS, 4, 1, false, true>), dim3(grid), dim3(kBlock), lds, s, v); return;
+        case 2: hipLaunchKernelGGL((decode_rows_kernel<DS, 4, 2, false, true>), dim3(grid), dim3(kBlock), lds, s, v); return;
+        default: break;
+      }
+    }
     hipLaunchKernelGGL((decode_rows_kernel<DS, 4, 3, false, true>), dim3(grid), dim3(kBlock), lds,
                        s, v);
   }
 }
 
-hipError_t launch_encode_fast(const ScatterArgs& view, int grid, hipStream_t stream) {
+hipError_t launch_encode_fast(const ScatterArgs& view, int grid, int deep, hipStream_t stream) {
   if (view.total_items == 0 || view.fast_mode == kFastNone) return hipSuccess;
   switch (view.dsize) {
-    case 1: launch_encode_fast_ds<1>(view, grid, stream); break;
-    case 2: launch_encode_fast_ds<2>(view, grid, stream); break;
-    case 4: launch_encode_fast_ds<4>(view, grid, stream); break;
-    case 8: launch_encode_fast_ds<8>(view, grid, stream); break;
+    case 1: launch_encode_fast_ds<1>(view, grid, deep, stream); break;
+    case 2: launch_encode_fast_ds<2>(view, grid, deep, stream); break;
+    case 4: launch_encode_fast_ds<4>(view, grid, deep, stream); break;
+    case 8: launch_encode_fast_ds<8>(view, grid, deep, stream); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();
