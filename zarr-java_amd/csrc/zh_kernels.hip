@@ -428,13 +428,15 @@ __device__ __forceinline__ bool row_pass(const ScatterArgs& a, const Item& it, i
   return diff;
 }
 
-// Can the whole item move in 16-byte granules along F?
-template <int DS>
+// Can the whole item move in 16-byte granules along F?  ENC: the destination is a shard
+// payload, which may sit at 4 mod 16 (after a chunk's crc32c or a sub-shard index):
+// dwordx4 stores, like loads, need dword alignment only in gfx9's unaligned mode.
+template <int DS, bool ENC = false>
 __device__ __forceinline__ bool vec_ok(const ScatterArgs& a, const Item& it, int F,
                                        const int64_t* sstr, const int64_t* dstr,
                                        const int32_t* ext, bool need_src) {
   const int n = a.ndim;
-  bool ok = !(((uintptr_t)(it.dbase + it.d0 * DS)) & 15);
+  bool ok = !(((uintptr_t)(it.dbase + it.d0 * DS)) & (ENC ? 3 : 15));
   // sources need dword alignment only: a chunk after a 4-byte crc32c or a sub-shard index
   // sits at 4 mod 16, and dwordx4 loads from dword-aligned addresses are legal on gfx950
   if (need_src) ok &= !(((uintptr_t)(it.sbase + it.s0 * DS)) & 3);
@@ -461,7 +463,7 @@ template <int DS>
 __device__ __forceinline__ bool vec_clip_ok(const ScatterArgs& a, const Item& it, int F,
                                             const int64_t* sstr, const int64_t* dstr) {
   const int n = a.ndim;
-  bool ok = !(((uintptr_t)(it.dbase + it.d0 * DS)) & 15) &&
+  bool ok = !(((uintptr_t)(it.dbase + it.d0 * DS)) & 3) &&
             !(((uintptr_t)(it.sbase + it.s0 * DS)) & 3);
 #pragma unroll
   for (int d = 0; d < kMaxDims; d++) {
@@ -1280,7 +1282,7 @@ __device__ __forceinline__ bool encode_item(const ScatterArgs& a, Item& it,
       if (d < n && d != F) nrows *= (uint32_t)it.e[d];
       if (d < n) clipped |= it.v[d] != it.e[d];
     }
-    if (!clipped && vec_ok<DS>(a, it, F, sstr, dstr, it.e, true))
+    if (!clipped && vec_ok<DS, true>(a, it, F, sstr, dstr, it.e, true))
       return row_pass<DS, true, false, false, FLAG>(a, it, F, sstr, dstr, nrows, it.e, it.ediv);
     if (clipped && vec_clip_ok<DS>(a, it, F, sstr, dstr))
       return row_pass<DS, true, false, true, FLAG>(a, it, F, sstr, dstr, nrows, it.e, it.ediv);
@@ -1399,7 +1401,7 @@ __global__ __launch_bounds__(kBlock) void encode_resolve_kernel(ScatterArgs a, i
       D.d0 = doff / a.dsize;
       D.kind = kDescFullCopy;
       const bool fast = vfast && full && (saddr & 3) == 0 &&
-                        (((uintptr_t)it.dbase) & 15) == 0 && doff >= 0 && doff % a.dsize == 0 &&
+                        (((uintptr_t)it.dbase) & 3) == 0 && doff >= 0 && doff % a.dsize == 0 &&
                         (!a.tile || a.dsize == 4);
       if (fast) {
         D.kind |= kDescFast;
