@@ -1595,7 +1595,26 @@ static int array_write_fast(zh_ctx* ctx, const zh_array_meta* m, ScatterArgs a,
       spans += (J.len + kCrcSpan - 1) / kCrcSpan;
     }
   }
-  const int64_t nspan = c.inner_crc32c ? (a.inner_nbytes + kCrcSpan - 1) / kCrcSpan : 0;
+  // chunk crc32c fused into the row encode when its lanes store each piece's payload in the
+  // CRC pass's order (the decode rule, plan creation above: rows sequential in the payload,
+  // equal pieces of whole 4 KiB rounds); otherwise a separate pass over the written payloads
+  bool crc_fuse = false;
+  const int64_t pieces = 1ll << a.piece_shift;
+  if (c.inner_crc32c && !tile_mode && env_int("ZH_CRC_FUSE", 1) != 0 &&
+      (v.fast_mode == kFastRowArith || v.fast_mode == kFastRowTable)) {
+    const int F = a.fs;
+    int64_t stv = a.inner[F];
+    crc_fuse = a.pstride[F] == 1;
+    for (int d = n - 1; d >= 0; d--) {
+      if (d == F) continue;
+      if (a.inner[d] > 1 && a.pstride[d] != stv) crc_fuse = false;
+      stv *= a.inner[d];
+    }
+    crc_fuse = crc_fuse && a.inner_nbytes % pieces == 0 &&
+               (a.inner_nbytes / pieces) % 4096 == 0 && v.fast_rows % pieces == 0;
+  }
+  const int64_t cspan = crc_fuse ? a.inner_nbytes / pieces : (int64_t)kCrcSpan;
+  const int64_t nspan = c.inner_crc32c ? (a.inner_nbytes + cspan - 1) / cspan : 0;
   // scratch carve-up (256-B aligned sub-buffers)
   size_t off = 0;
   auto carve = [&](size_t bytes) {
@@ -1670,6 +1689,10 @@ static int array_write_fast(zh_ctx* ctx, const zh_array_meta* m, ScatterArgs a,
   // golden-ratio visit order and (uint32 rows) 8 rows in flight per lane: +2.4 % on c3, the
   // order +4 % on c4 (interleaved A/B, profiles/tune_write.py → profiles/r01/experiments/)
   v.item_mul = env_int("ZH_ITEM_PERM", 1) ? golden_item_mul(pitems) : 0;
+  v.crc_fused = crc_fuse ? 1 : 0;
+  v.crc_partials = (uint32_t*)(W + o_cpart);
+  if (crc_fuse)
+    ZH_HIPF(hipMemsetAsync(W + o_cpart, 0, (size_t)(items * nspan) * sizeof(uint32_t), s));
   v.nt = env_int("ZH_ENC_NT", 3) & 3;
   const int grid = grid_for(ctx, pitems);
   ZH_HIPF(launch_encode_fast(v, grid, env_int("ZH_ENC_DEEP", 1), s));
@@ -1683,9 +1706,10 @@ static int array_write_fast(zh_ctx* ctx, const zh_array_meta* m, ScatterArgs a,
     D.desc = d_cdesc;
     D.n_items = items;
     D.len = a.inner_nbytes;
-    D.span = kCrcSpan;
+    D.span = cspan;
     D.nspan = (int32_t)nspan;
     D.store = 1;
+    D.skip_fast = crc_fuse ? 1 : 0;
     D.partials = (uint32_t*)(W + o_cpart);
     ZH_HIPF(launch_data_crc(D, (int)std::min<int64_t>(items * nspan, (int64_t)ctx->cu_count * 32),
                             s));

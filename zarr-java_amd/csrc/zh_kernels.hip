@@ -1059,7 +1059,9 @@ __global__ __launch_bounds__(kBlock) void decode_rows_kernel(ScatterArgs a) {
 #pragma unroll
         for (int u = 0; u < U; u++)
           if (da[u] != ~0ull) {
-            const v4u w = {va[u].x, va[u].y, va[u].z, va[u].w};
+            // decode: the loaded payload vector; encode view (FLAGS): the stored one
+            const uint4 cv = FLAGS ? xform16<DS>(va[u], a.swap, a.is_bool) : va[u];
+            const v4u w = {cv.x, cv.y, cv.z, cv.w};
             acc = crc_upd16(crc_shift_tab(acc, S), w, T);
           }
         if (piece_end) {  // uniform: shift every lane to the piece end, XOR the wave
@@ -1453,7 +1455,8 @@ __global__ __launch_bounds__(kBlock) void encode_finish_kernel(ScatterArgs a, in
       D.src = off >= 0 ? (uint64_t)(uintptr_t)(S.wdata + off) : 0;
       D.d0 = 0;
       D.fill = 0;
-      D.kind = off >= 0 ? kDescFullCopy : kDescSkip;
+      // the fast bit tells the CRC pass which chunks the row kernel already hashed
+      D.kind = off >= 0 ? kDescFullCopy | (a.desc[c].kind & kDescFast) : kDescSkip;
       D.shard = (uint32_t)s;
       crc_desc[c] = D;
     }
@@ -2007,6 +2010,13 @@ static void launch_encode_fast_ds(const ScatterArgs& v, int grid, int deep, hipS
         default: hipLaunchKernelGGL((decode_tiles_kernel<3, 1, false, true>), dim3(grid), dim3(kBlock), l, s, v); break;
       }
     }
+  } else if (v.fast_mode != kFastNone && v.crc_fused) {
+    // chunk crc32c of the stored payload, fused (rows sequential in the payload)
+    const size_t l = lds + 12 * 256 * 4;
+    if (deep)
+      hipLaunchKernelGGL((decode_rows_kernel<DS, 8, 3, true, true>), dim3(grid), dim3(kBlock), l, s, v);
+    else
+      hipLaunchKernelGGL((decode_rows_kernel<DS, 4, 3, true, true>), dim3(grid), dim3(kBlock), l, s, v);
   } else if (v.fast_mode != kFastNone) {
     if constexpr (DS == 4) {
       if (deep) {
