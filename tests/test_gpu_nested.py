@@ -88,6 +88,26 @@ def test_nested_encode_matches_oracle_bytes(dev, case):
     assert got == want
 
 
+@pytest.mark.parametrize("case", CASES, ids=lambda c: f"{c['chunk']}-{c['l1']}-{c['l2']}")
+@pytest.mark.parametrize("variant", ["plain", "transpose", "crc32c"])
+def test_nested_encode_one_pass(dev, monkeypatch, case, variant):
+    """The one-pass write on nested chains (no leaf is all fill_value, so the speculative
+    layout holds): cell table, outer index and its crc32c on the host; leaf offsets, sub-index
+    entries and sub-index crc32c on the device.  Boundary shards elide padding-only cells and
+    leaves.  Bytes equal the oracle's and the flags → layout → encode fallback's."""
+    m = _meta(case, order=[1, 0] + list(range(2, len(case["shape"])))
+              if variant == "transpose" else None)
+    if variant == "crc32c":
+        m.chain.inner_crc32c = 1
+    shape = shape_of(m)
+    arr = rand_array(shape, 4, seed=13)
+    arr[arr == 0] = 1
+    want = encode_oracle(m, arr)
+    assert device_write(dev, m, arr) == want
+    monkeypatch.setenv("ZH_ENC_FAST", "0")
+    assert device_write(dev, m, arr) == want
+
+
 def test_nested_sub_index_crc_message(dev):
     m = nested_meta([8, 8], [8, 8], [4, 4], [2, 2])
     data = np.arange(64, dtype=np.uint32).reshape(8, 8) + 1

@@ -1558,11 +1558,86 @@ static int array_write_fast(zh_ctx* ctx, const zh_array_meta* m, ScatterArgs a,
   const int64_t isz = c.sharded ? zh_shard_index_size(m) : 0;
   const bool start = c.sharded && c.index_location == ZH_INDEX_START;
   const int32_t* inner = leaf_shape(m);
+  // nested sharding: each level-1 cell with an in-bounds leaf is a sub-shard in C order —
+  // its in-bounds leaves in C order + its own index (ShardingIndexedCodec.encode of the
+  // level-2 codec, :105-168) — and a cell without one is (-1, -1) at level 1.  The cell table
+  // and the outer index (+ crc32c) are built here; leaf entries and sub-index CRCs on the
+  // device.
+  EncNest nz{};
+  std::vector<int64_t> cells;
+  std::vector<std::vector<uint8_t>> outer;
+  std::vector<CrcJob> jobs;
+  int64_t spans = 0;
+  auto add_job = [&](const uint8_t* base, int64_t len, int64_t shard) {
+    CrcJob J;
+    J.base = base;
+    J.len = len;
+    J.span_begin = spans;
+    J.shard = (int32_t)shard;
+    J.pad = 0;
+    jobs.push_back(J);
+    spans += (len + kCrcSpan - 1) / kCrcSpan;
+  };
+  int64_t cps2 = 1;
+  if (c.nested) {
+    nz.ncell = 1;
+    for (int d = 0; d < kMaxDims; d++) {
+      nz.r[d] = d < n ? c.inner_chunk_shape[d] / inner[d] : 1;
+      nz.g1[d] = d < n ? m->chunk_shape[d] / c.inner_chunk_shape[d] : 1;
+      nz.ncell *= nz.g1[d];
+      cps2 *= nz.r[d];
+    }
+    nz.sub_isz = 16 * cps2 + (c.nested_index_has_crc32c ? 4 : 0);
+    nz.sub_start = c.nested_index_location == ZH_INDEX_START;
+    nz.sub_be = c.nested_index_endian == ZH_ENDIAN_BIG;
+    cells.assign((size_t)(2 * nz.ncell * ncoords), -1);
+    outer.resize((size_t)ncoords);
+  }
   for (int64_t i = 0; i < ncoords; i++) {
     DevShard& S = hs[i];
-    int64_t kept = 1;  // in-bounds inner chunks of the shard (all kept under this layout)
-    for (int d = 0; d < n; d++) kept *= (S.part_hi[d] + inner[d] - 1) / inner[d];
-    const int64_t payload = kept * cn;
+    int64_t payload;
+    if (c.nested) {
+      std::vector<uint8_t>& idx = outer[(size_t)i];
+      idx.assign((size_t)isz, 0);
+      const bool be = c.index_endian == ZH_ENDIAN_BIG;
+      int64_t pos = start ? isz : 0;
+      for (int64_t cell = 0; cell < nz.ncell; cell++) {
+        int64_t q = cell, nk = 1;
+        for (int d = n - 1; d >= 0; d--) {
+          const int64_t c1 = q % nz.g1[d];
+          q /= nz.g1[d];
+          const int64_t lo = c1 * c.inner_chunk_shape[d];
+          nk *= std::max<int64_t>(0, std::min<int64_t>(nz.r[d], (S.part_hi[d] - lo + inner[d] - 1) /
+                                                                     inner[d]));
+        }
+        uint64_t eo = ~0ull, en = ~0ull;
+        if (nk > 0) {
+          const int64_t len = nk * cn + nz.sub_isz;
+          const int64_t sidx = nz.sub_start ? pos : pos + nk * cn;
+          cells[(size_t)(2 * (i * nz.ncell + cell))] = pos;
+          cells[(size_t)(2 * (i * nz.ncell + cell) + 1)] = sidx;
+          if (c.nested_index_has_crc32c)
+            add_job((const uint8_t*)dsts[i].data + sidx, 16 * cps2, i);
+          eo = (uint64_t)pos;
+          en = (uint64_t)len;
+          pos += len;
+        }
+        for (int b = 0; b < 8; b++) {
+          const int sh = be ? 56 - 8 * b : 8 * b;
+          idx[(size_t)(16 * cell + b)] = (uint8_t)(eo >> sh);
+          idx[(size_t)(16 * cell + 8 + b)] = (uint8_t)(en >> sh);
+        }
+      }
+      if (c.index_has_crc32c) {  // Crc32cCodec.encode :50-60
+        const uint32_t crc = crc32c_host(0, idx.data(), (size_t)(isz - 4));
+        for (int b = 0; b < 4; b++) idx[(size_t)(isz - 4 + b)] = (uint8_t)(crc >> (8 * b));
+      }
+      payload = pos - (start ? isz : 0);
+    } else {
+      int64_t kept = 1;  // in-bounds inner chunks of the shard (all kept under this layout)
+      for (int d = 0; d < n; d++) kept *= (S.part_hi[d] + inner[d] - 1) / inner[d];
+      payload = kept * cn;
+    }
     const int64_t total = payload + isz;
     if (total > dsts[i].capacity || !dsts[i].data) {
       set_err(err, errlen, "chunk destination %lld too small: need %lld bytes, have %lld",
@@ -1570,7 +1645,7 @@ static int array_write_fast(zh_ctx* ctx, const zh_array_meta* m, ScatterArgs a,
       return ZH_EINVAL;
     }
     dsts[i].nbytes = total;
-    S.index_off = c.sharded ? (start ? 0 : payload) : -1;
+    S.index_off = c.sharded && !c.nested ? (start ? 0 : payload) : -1;
   }
   const int64_t pitems = items << a.piece_shift;
   // the encode view: source strides = region, destination strides = payload, destination
@@ -1581,20 +1656,9 @@ static int array_write_fast(zh_ctx* ctx, const zh_array_meta* m, ScatterArgs a,
   uint8_t* vbase = nullptr;
   for (int64_t i = 0; i < ncoords; i++)
     if (!vbase || (uint8_t*)dsts[i].data < vbase) vbase = (uint8_t*)dsts[i].data;
-  std::vector<CrcJob> jobs;
-  int64_t spans = 0;
-  if (c.sharded && c.index_has_crc32c) {  // Crc32cCodec.encode of each index (:50-60)
-    jobs.resize((size_t)ncoords);
-    for (int64_t i = 0; i < ncoords; i++) {
-      CrcJob& J = jobs[(size_t)i];
-      J.base = (const uint8_t*)dsts[i].data + hs[i].index_off;
-      J.len = isz - 4;
-      J.span_begin = spans;
-      J.shard = (int32_t)i;
-      J.pad = 0;
-      spans += (J.len + kCrcSpan - 1) / kCrcSpan;
-    }
-  }
+  if (c.sharded && !c.nested && c.index_has_crc32c)  // Crc32cCodec.encode of each index
+    for (int64_t i = 0; i < ncoords; i++)
+      add_job((const uint8_t*)dsts[i].data + hs[i].index_off, isz - 4, i);
   // chunk crc32c fused into the row encode when its lanes store each piece's payload in the
   // CRC pass's order (the decode rule, plan creation above: rows sequential in the payload,
   // equal pieces of whole 4 KiB rounds); otherwise a separate pass over the written payloads
@@ -1633,6 +1697,7 @@ static int array_write_fast(zh_ctx* ctx, const zh_array_meta* m, ScatterArgs a,
   const size_t o_cdesc = carve(c.inner_crc32c ? (size_t)items * sizeof(ItemDesc) : 0);
   const size_t o_cpart = carve((size_t)(items * nspan) * sizeof(uint32_t));
   const size_t o_cnt = carve(sizeof(uint32_t));
+  const size_t o_cells = carve(cells.size() * sizeof(int64_t));
   if (off > ctx->wscratch_cap) {
     (void)hipFree(ctx->wscratch);
     ctx->wscratch = nullptr;
@@ -1667,6 +1732,14 @@ static int array_write_fast(zh_ctx* ctx, const zh_array_meta* m, ScatterArgs a,
   ZH_HIPF(hipMemsetAsync(d_flags, 0, (size_t)items, s));
   ZH_HIPF(hipMemsetAsync(d_slow, 0, sizeof(uint32_t), s));
   ZH_HIPF(hipMemsetAsync(d_cnt, 0, sizeof(uint32_t), s));
+  if (c.nested) {
+    ZH_HIPF(hipMemcpyAsync(W + o_cells, cells.data(), cells.size() * sizeof(int64_t),
+                           hipMemcpyHostToDevice, s));
+    nz.cell = (const int64_t*)(W + o_cells);
+    for (int64_t i = 0; i < ncoords; i++)  // the outer index (entries + crc32c), host-built
+      ZH_HIPF(hipMemcpyAsync((uint8_t*)dsts[i].data + (start ? 0 : dsts[i].nbytes - isz),
+                             outer[(size_t)i].data(), (size_t)isz, hipMemcpyHostToDevice, s));
+  }
   a.shards = d_shards;
   a.nshards = ncoords;
   a.n_citems = items;
@@ -1676,7 +1749,7 @@ static int array_write_fast(zh_ctx* ctx, const zh_array_meta* m, ScatterArgs a,
   a.desc = (ItemDesc*)(W + o_desc);
   a.slow_count = d_slow;
   a.slow_list = d_slow + 4;
-  ZH_HIPF(launch_encode_resolve(a, d_off, start ? isz : 0, cn, vbase,
+  ZH_HIPF(launch_encode_resolve(a, nz, d_off, start ? isz : 0, cn, vbase,
                                 v.fast_mode != kFastNone ? 1 : 0, s));
   v.shards = d_shards;
   v.nshards = ncoords;
@@ -1697,10 +1770,10 @@ static int array_write_fast(zh_ctx* ctx, const zh_array_meta* m, ScatterArgs a,
   const int grid = grid_for(ctx, pitems);
   ZH_HIPF(launch_encode_fast(v, grid, env_int("ZH_ENC_DEEP", 1), s));
   ZH_HIPF(launch_encode_slow(a, grid, s));
-  ZH_HIPF(launch_encode_finish(a, cn, d_cnt, d_cdesc, s));
+  ZH_HIPF(launch_encode_finish(a, nz, cn, d_cnt, d_cdesc, s));
   if (!jobs.empty())
-    ZH_HIPF(launch_crc((const CrcJob*)(W + o_jobs), ncoords, spans, (uint32_t*)(W + o_part),
-                       nullptr, s));
+    ZH_HIPF(launch_crc((const CrcJob*)(W + o_jobs), (int64_t)jobs.size(), spans,
+                       (uint32_t*)(W + o_part), nullptr, s));
   if (c.inner_crc32c) {  // Crc32cCodec.encode (:50-60) of every kept chunk payload
     DataCrcArgs D{};
     D.desc = d_cdesc;
@@ -1787,7 +1860,7 @@ int zh_array_write(zh_ctx* ctx, const zh_array_meta* m, const void* src, const i
     S.out_base = ob;
     items += c.sharded ? cps_total : 1;
   }
-  if (!c.nested && env_int("ZH_ENC_FAST", 1) != 0) {
+  if (env_int("ZH_ENC_FAST", 1) != 0) {
     a.region = (uint8_t*)src;
     st = array_write_fast(ctx, m, a, hs, items, tile_mode, dsts, s, err, errlen);
     if (st != kWriteFallback) return st;

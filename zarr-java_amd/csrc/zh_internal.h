@@ -193,13 +193,24 @@ hipError_t launch_flags(const ScatterArgs& a, int dsize, int grid, hipStream_t s
 // kernels with the all-fill test, the slow list through the generic encode, then the finish
 // kernel (all-fill count, index entries, chunk-CRC descriptors); launch_crc with
 // status == nullptr stores the index crc32c instead of checking it
-hipError_t launch_encode_resolve(const ScatterArgs& a, int64_t* item_off, int64_t base_off,
-                                 int64_t cn, const uint8_t* vbase, int vfast,
+// nested sharding on the one-pass write: per (shard, level-1 cell) {cell offset in the shard
+// (-1: no in-bounds leaf, elided at level 1), sub-shard index offset}, and the cell geometry
+struct EncNest {
+  const int64_t* cell;          // 2 per (shard, cell); nullptr: single-level chain
+  int64_t ncell;                // level-1 cells per shard
+  int64_t sub_isz;              // sub-shard index bytes (16 per leaf, +4 with crc32c)
+  int32_t r[kMaxDims];          // leaves per cell per dim
+  int32_t g1[kMaxDims];         // cells per shard per dim
+  int32_t sub_start;            // sub-shard index before the leaves
+  int32_t sub_be;               // sub-shard index big-endian
+};
+hipError_t launch_encode_resolve(const ScatterArgs& a, const EncNest& nz, int64_t* item_off,
+                                 int64_t base_off, int64_t cn, const uint8_t* vbase, int vfast,
                                  hipStream_t stream);
 hipError_t launch_encode_fast(const ScatterArgs& view, int grid, int deep, hipStream_t stream);
 hipError_t launch_encode_slow(const ScatterArgs& a, int grid, hipStream_t stream);
-hipError_t launch_encode_finish(const ScatterArgs& a, int64_t chunk_nbytes, uint32_t* bad,
-                                ItemDesc* crc_desc, hipStream_t stream);
+hipError_t launch_encode_finish(const ScatterArgs& a, const EncNest& nz, int64_t chunk_nbytes,
+                                uint32_t* bad, ItemDesc* crc_desc, hipStream_t stream);
 hipError_t launch_synth_fill(void* dst, int64_t n, int dsize, int64_t first, uint64_t seed,
                              hipStream_t stream);
 hipError_t launch_synth_verify(const void* region, int ndim, const int64_t* array_shape,

@@ -1359,13 +1359,50 @@ __global__ __launch_bounds__(kBlock) void flags_kernel(ScatterArgs a) {
 // encode-view descriptor (src = the chunk's origin in the region, d0 = its payload position
 // relative to vbase, in elements) or a slow-list entry (clipped by the array boundary,
 // misaligned)
-__global__ __launch_bounds__(kBlock) void encode_resolve_kernel(ScatterArgs a, int64_t* item_off,
+// Nested sharding: a leaf's cell (C order over the shard's cells), its position in the cell
+// (C order over the cell's leaf grid) and its rank in the cell's in-bounds leaf box.
+__device__ __forceinline__ void nest_coords(const ScatterArgs& a, const EncNest& nz,
+                                            const DevShard& S, int64_t c, int64_t& cell,
+                                            int64_t& k2, int64_t& rank, bool& in) {
+  uint32_t j = (uint32_t)(c - S.item_begin);
+  int64_t mc = 1, mk = 1, mr = 1;
+  cell = k2 = rank = 0;
+  in = true;
+#pragma unroll
+  for (int d = kMaxDims - 1; d >= 0; --d) {
+    if (d >= a.ndim) continue;
+    const uint32_t bc = (uint32_t)S.box_count[d];
+    const uint32_t q = j / bc;
+    const int32_t lc = (int32_t)(j - q * bc);
+    j = q;
+    const int32_t c1 = lc / nz.r[d], w = lc - c1 * nz.r[d];
+    const int32_t cnt = min(nz.r[d], (S.part_hi[d] - c1 * nz.r[d] * a.inner[d] + a.inner[d] - 1) /
+                                         a.inner[d]);
+    in &= w < cnt;
+    cell += c1 * mc;
+    mc *= nz.g1[d];
+    k2 += w * mk;
+    mk *= nz.r[d];
+    rank += w * mr;
+    mr *= max(cnt, 1);
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void encode_resolve_kernel(ScatterArgs a, EncNest nz,
+                                                                int64_t* item_off,
                                                                 int64_t base_off, int64_t cn,
                                                                 const uint8_t* vbase,
                                                                 int vfast) {
   const int64_t stride = (int64_t)gridDim.x * kBlock;
   for (int64_t c = (int64_t)blockIdx.x * kBlock + threadIdx.x; c < a.n_citems; c += stride) {
-    {
+    if (nz.cell) {  // nested: the cell's offset + the sub-index (at the start) + the rank
+      const int64_t s = find_shard(a, c);
+      int64_t cell, k2, rank;
+      bool in;
+      nest_coords(a, nz, a.shards[s], c, cell, k2, rank, in);
+      const int64_t co = nz.cell[2 * (s * nz.ncell + cell)];
+      item_off[c] = in && co >= 0 ? co + (nz.sub_start ? nz.sub_isz : 0) + rank * cn : -1;
+    } else {
       const DevShard& S = a.shards[find_shard(a, c)];
       uint32_t j = (uint32_t)(c - S.item_begin);
       int64_t rank = 0, mul = 1;
@@ -1442,7 +1479,8 @@ __global__ __launch_bounds__(kBlock) void encode_slow_kernel(ScatterArgs a) {
 // falls back), build its chunk-CRC store descriptor (inner crc32c), and write the index entry
 // (ShardingIndexedCodec.encode :135-160): (offset, nbytes) or (-1, -1), in the index codecs'
 // byte order, at S.index_off of the shard's buffer
-__global__ __launch_bounds__(kBlock) void encode_finish_kernel(ScatterArgs a, int64_t chunk_nbytes,
+__global__ __launch_bounds__(kBlock) void encode_finish_kernel(ScatterArgs a, EncNest nz,
+                                                               int64_t chunk_nbytes,
                                                                uint32_t* bad, ItemDesc* crc_desc) {
   const int64_t stride = (int64_t)gridDim.x * kBlock;
   for (int64_t c = (int64_t)blockIdx.x * kBlock + threadIdx.x; c < a.n_citems; c += stride) {
@@ -1460,13 +1498,27 @@ __global__ __launch_bounds__(kBlock) void encode_finish_kernel(ScatterArgs a, in
       D.shard = (uint32_t)s;
       crc_desc[c] = D;
     }
-    if (!a.sharded || S.index_off < 0) continue;
-    const uint64_t eo = off >= 0 ? (uint64_t)off : ~0ull;
+    uint64_t eo = off >= 0 ? (uint64_t)off : ~0ull;
     const uint64_t en = off >= 0 ? (uint64_t)chunk_nbytes : ~0ull;
-    uint8_t* e = S.wdata + S.index_off + 16 * (c - S.item_begin);
+    uint8_t* e;
+    int be;
+    if (nz.cell) {  // nested: the leaf's entry in its cell's sub-shard index, offset relative
+      int64_t cell, k2, rank;  // to the cell (ShardingIndexedCodec.encode of the sub-shard)
+      bool in;
+      nest_coords(a, nz, S, c, cell, k2, rank, in);
+      const int64_t* ci = nz.cell + 2 * (s * nz.ncell + cell);
+      if (ci[0] < 0) continue;  // elided cell: no sub-index (the host wrote (-1, -1) above it)
+      if (off >= 0) eo = (uint64_t)(off - ci[0]);
+      e = S.wdata + ci[1] + 16 * k2;
+      be = nz.sub_be;
+    } else {
+      if (!a.sharded || S.index_off < 0) continue;
+      e = S.wdata + S.index_off + 16 * (c - S.item_begin);
+      be = a.index_be;
+    }
 #pragma unroll
     for (int b = 0; b < 8; b++) {
-      const int sh = a.index_be ? 56 - 8 * b : 8 * b;
+      const int sh = be ? 56 - 8 * b : 8 * b;
       e[b] = (uint8_t)(eo >> sh);
       e[8 + b] = (uint8_t)(en >> sh);
     }
@@ -2051,12 +2103,12 @@ hipError_t launch_encode_fast(const ScatterArgs& view, int grid, int deep, hipSt
   return hipGetLastError();
 }
 
-hipError_t launch_encode_resolve(const ScatterArgs& a, int64_t* item_off, int64_t base_off,
-                                 int64_t cn, const uint8_t* vbase, int vfast,
+hipError_t launch_encode_resolve(const ScatterArgs& a, const EncNest& nz, int64_t* item_off,
+                                 int64_t base_off, int64_t cn, const uint8_t* vbase, int vfast,
                                  hipStream_t stream) {
   if (a.n_citems == 0) return hipSuccess;
   const int grid = (int)std::min<int64_t>((a.n_citems + kBlock - 1) / kBlock, 8192);
-  hipLaunchKernelGGL(encode_resolve_kernel, dim3(grid), dim3(kBlock), 0, stream, a, item_off,
+  hipLaunchKernelGGL(encode_resolve_kernel, dim3(grid), dim3(kBlock), 0, stream, a, nz, item_off,
                      base_off, cn, vbase, vfast);
   return hipGetLastError();
 }
@@ -2080,12 +2132,12 @@ hipError_t launch_encode_slow(const ScatterArgs& a, int grid, hipStream_t stream
   return hipGetLastError();
 }
 
-hipError_t launch_encode_finish(const ScatterArgs& a, int64_t chunk_nbytes, uint32_t* bad,
-                                ItemDesc* crc_desc, hipStream_t stream) {
+hipError_t launch_encode_finish(const ScatterArgs& a, const EncNest& nz, int64_t chunk_nbytes,
+                                uint32_t* bad, ItemDesc* crc_desc, hipStream_t stream) {
   if (a.n_citems == 0) return hipSuccess;
   const int grid = (int)std::min<int64_t>((a.n_citems + kBlock - 1) / kBlock, 8192);
-  hipLaunchKernelGGL(encode_finish_kernel, dim3(grid), dim3(kBlock), 0, stream, a, chunk_nbytes,
-                     bad, crc_desc);
+  hipLaunchKernelGGL(encode_finish_kernel, dim3(grid), dim3(kBlock), 0, stream, a, nz,
+                     chunk_nbytes, bad, crc_desc);
   return hipGetLastError();
 }
 
