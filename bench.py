@@ -476,12 +476,22 @@ def run_strong(args, dist, dev, A, L, meta, rank, ws, local):
 def run_write(args, dist, dev, A, meta, shape, region, out_bytes, shard_slab, offs, caps, rank,
               ws):
     """Write path: zh_array_write of the full array = core.Array.write
-    + ShardingIndexedCodec.encode of every shard (all-fill flags pass, C-order layout, index +
-    crc32c, payload encode) from the device-resident region into device shard buffers.  The
-    call synchronises internally (the layout needs the flags), so it is timed by wall clock;
-    the written shards are verified by decoding them and checking every element."""
+    + ShardingIndexedCodec.encode of every shard (one pass: speculative C-order layout with
+    the all-fill test fused, index + crc32c on the device) from the device-resident region
+    into device shard buffers.  The call synchronises internally, so it is timed by wall
+    clock; the written shards are verified by decoding them and checking every element.
+    --sparse zeroes (= fill_value) the first row of inner chunks along y, so that 1/128 of the
+    chunks are elided and every call takes the second pass (the reference's layout)."""
     n = len(shape)
     dsts = [(shard_slab + o, c) for o, c in zip(offs, caps)]
+    zbytes = 0
+    if args.sparse:
+        ch = meta.chain
+        leaf = (ch.nested_chunk_shape if ch.nested else ch.inner_chunk_shape) if ch.sharded \
+            else meta.chunk_shape
+        zy = int(leaf[1])
+        zbytes = zy * shape[2] * shape[3] * 4
+        dev.memset(region, 0, zbytes)
     for _ in range(max(1, args.warmup)):
         sizes = dev.array_write(meta, region, [0] * n, shape, dsts)
     dist.barrier()
@@ -492,13 +502,23 @@ def run_write(args, dist, dev, A, meta, shape, region, out_bytes, shard_slab, of
     dev.sync()
     elapsed = dist.max(time.perf_counter() - t0)
     in_bytes = sum(sizes)
-    plan = dev.plan(meta, [(shard_slab + o, s) for o, s in zip(offs, sizes)], [0] * n, shape,
-                    A.ZH_SRC_DEVICE | A.ZH_OUT_DEVICE)
+    # a deleted (all fill_value) chunk is a missing key: the read fills it
+    plan = dev.plan(meta, [(shard_slab + o, s) if s else (None, 0) for o, s in zip(offs, sizes)],
+                    [0] * n, shape, A.ZH_SRC_DEVICE | A.ZH_OUT_DEVICE)
     dev.memset(region, 0, out_bytes)
     plan.execute(region)
     plan.wait()
     plan.close()
-    bad = dev.synth_verify(region, shape, [0] * n, shape, 4, SEED)
+    if zbytes:
+        rest = [shape[0], shape[1] - zy] + list(shape[2:])
+        bad = dev.synth_verify(region + zbytes, shape, [0, zy] + [0] * (n - 2), rest, 4, SEED)
+        import numpy as np
+        step = 1 << 30
+        for o in range(0, zbytes, step):
+            blk = np.frombuffer(dev.d2h(region + o, min(step, zbytes - o)), np.uint8)
+            bad += int(np.count_nonzero(blk))
+    else:
+        bad = dev.synth_verify(region, shape, [0] * n, shape, 4, SEED)
     if bad:
         raise SystemExit(f"write round trip FAILED: {bad} mismatching elements")
     log(f"[rank {rank}] write path verified: decode of the written shards == generator")
@@ -513,6 +533,7 @@ def run_write(args, dist, dev, A, meta, shape, region, out_bytes, shard_slab, of
             "ms_per_step": round(ms, 3), "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None, "dtype": "u32", "data": "synthetic",
             "config": {"workload": f"{args.config}: Array.write of the full "
+                                   f"{'sparse (first y-row of inner chunks = fill_value) ' if zbytes else ''}"
                                    f"{'x'.join(map(str, shape))} uint32 array, "
                                    f"{CONFIGS[args.config][0]}",
                        "encoded_bytes": in_bytes, "decoded_bytes_per_gpu": out_bytes,
@@ -533,6 +554,9 @@ def main():
     ap.add_argument("--op", default="read", choices=["read", "write"],
                     help="read: the decode path (the metric); write: zh_array_write, the "
                          "encode path (SURVEY §8(f) rank 1)")
+    ap.add_argument("--sparse", action="store_true",
+                    help="--op write: elide 1/128 of the inner chunks (all fill_value), so the "
+                         "write takes its second pass")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
     ap.add_argument("--mode", default="weak", choices=["weak", "strong"],
                     help="weak: one full array per GPU (the metric); strong: one array split "

@@ -1548,9 +1548,16 @@ constexpr int kWriteFallback = -1;
 // chunk crc32c are stored on the device; the call synchronises once.  A non-zero count means
 // the layout was wrong (the reference elides such a chunk): returns kWriteFallback and the
 // caller runs flags → layout → encode.  Scratch tables live in the context (grow-only).
+//
+// keep != nullptr (the second pass after a fallback): keep[item] = the chunk holds a
+// non-fill element, from the first pass's flags (flags_out).  The layout is then the
+// reference's: kept chunks only, in C order, a shard (or nested cell) with none elided; the
+// host computes the offsets and the same kernels run once more.
 static int array_write_fast(zh_ctx* ctx, const zh_array_meta* m, ScatterArgs a,
                             std::vector<DevShard>& hs, int64_t items, int tile_mode,
-                            zh_chunk_dst* dsts, hipStream_t s, char* err, size_t errlen) {
+                            zh_chunk_dst* dsts, const uint8_t* keep,
+                            std::vector<uint8_t>* flags_out, hipStream_t s, char* err,
+                            size_t errlen) {
   const zh_codec_chain& c = m->chain;
   const int n = m->ndim;
   const int64_t ncoords = (int64_t)hs.size();
@@ -1579,6 +1586,10 @@ static int array_write_fast(zh_ctx* ctx, const zh_array_meta* m, ScatterArgs a,
     spans += (len + kCrcSpan - 1) / kCrcSpan;
   };
   int64_t cps2 = 1;
+  std::vector<int64_t> hoff;  // keep mode: payload offset per item (-1: elided)
+  if (keep) hoff.assign((size_t)items, -1);
+  int64_t cps_total = 1;
+  for (int d = 0; d < n; d++) cps_total *= m->chunk_shape[d] / inner[d];
   if (c.nested) {
     nz.ncell = 1;
     for (int d = 0; d < kMaxDims; d++) {
@@ -1602,13 +1613,27 @@ static int array_write_fast(zh_ctx* ctx, const zh_array_meta* m, ScatterArgs a,
       const bool be = c.index_endian == ZH_ENDIAN_BIG;
       int64_t pos = start ? isz : 0;
       for (int64_t cell = 0; cell < nz.ncell; cell++) {
-        int64_t q = cell, nk = 1;
+        int64_t q = cell, nk = 1, c1v[kMaxDims] = {0};
         for (int d = n - 1; d >= 0; d--) {
           const int64_t c1 = q % nz.g1[d];
           q /= nz.g1[d];
+          c1v[d] = c1;
           const int64_t lo = c1 * c.inner_chunk_shape[d];
           nk *= std::max<int64_t>(0, std::min<int64_t>(nz.r[d], (S.part_hi[d] - lo + inner[d] - 1) /
                                                                      inner[d]));
+        }
+        if (keep) {  // the cell's kept leaves, C order over its leaf grid
+          nk = 0;
+          const int64_t lpos = pos + (nz.sub_start ? nz.sub_isz : 0);
+          for (int64_t k2 = 0; k2 < cps2; k2++) {
+            int64_t f = 0, tq = k2, fs = 1;
+            for (int d = n - 1; d >= 0; d--) {
+              f += (c1v[d] * nz.r[d] + tq % nz.r[d]) * fs;
+              tq /= nz.r[d];
+              fs *= S.box_count[d];
+            }
+            if (keep[S.item_begin + f]) hoff[(size_t)(S.item_begin + f)] = lpos + cn * nk++;
+          }
         }
         uint64_t eo = ~0ull, en = ~0ull;
         if (nk > 0) {
@@ -1633,10 +1658,21 @@ static int array_write_fast(zh_ctx* ctx, const zh_array_meta* m, ScatterArgs a,
         for (int b = 0; b < 4; b++) idx[(size_t)(isz - 4 + b)] = (uint8_t)(crc >> (8 * b));
       }
       payload = pos - (start ? isz : 0);
+    } else if (keep) {
+      const int64_t nit = c.sharded ? cps_total : 1;
+      int64_t kept = 0;
+      for (int64_t k = 0; k < nit; k++)
+        if (keep[S.item_begin + k]) hoff[(size_t)(S.item_begin + k)] = (start ? isz : 0) + cn * kept++;
+      payload = kept * cn;
     } else {
       int64_t kept = 1;  // in-bounds inner chunks of the shard (all kept under this layout)
       for (int d = 0; d < n; d++) kept *= (S.part_hi[d] + inner[d] - 1) / inner[d];
       payload = kept * cn;
+    }
+    if (keep && payload == 0) {  // all fill: writeChunk deletes the key (Array.java:150-151)
+      dsts[i].nbytes = 0;
+      S.index_off = -1;
+      continue;
     }
     const int64_t total = payload + isz;
     if (total > dsts[i].capacity || !dsts[i].data) {
@@ -1658,7 +1694,7 @@ static int array_write_fast(zh_ctx* ctx, const zh_array_meta* m, ScatterArgs a,
     if (!vbase || (uint8_t*)dsts[i].data < vbase) vbase = (uint8_t*)dsts[i].data;
   if (c.sharded && !c.nested && c.index_has_crc32c)  // Crc32cCodec.encode of each index
     for (int64_t i = 0; i < ncoords; i++)
-      add_job((const uint8_t*)dsts[i].data + hs[i].index_off, isz - 4, i);
+      if (hs[i].index_off >= 0) add_job((const uint8_t*)dsts[i].data + hs[i].index_off, isz - 4, i);
   // chunk crc32c fused into the row encode when its lanes store each piece's payload in the
   // CRC pass's order (the decode rule, plan creation above: rows sequential in the payload,
   // equal pieces of whole 4 KiB rounds); otherwise a separate pass over the written payloads
@@ -1737,8 +1773,9 @@ static int array_write_fast(zh_ctx* ctx, const zh_array_meta* m, ScatterArgs a,
                            hipMemcpyHostToDevice, s));
     nz.cell = (const int64_t*)(W + o_cells);
     for (int64_t i = 0; i < ncoords; i++)  // the outer index (entries + crc32c), host-built
-      ZH_HIPF(hipMemcpyAsync((uint8_t*)dsts[i].data + (start ? 0 : dsts[i].nbytes - isz),
-                             outer[(size_t)i].data(), (size_t)isz, hipMemcpyHostToDevice, s));
+      if (dsts[i].nbytes)
+        ZH_HIPF(hipMemcpyAsync((uint8_t*)dsts[i].data + (start ? 0 : dsts[i].nbytes - isz),
+                               outer[(size_t)i].data(), (size_t)isz, hipMemcpyHostToDevice, s));
   }
   a.shards = d_shards;
   a.nshards = ncoords;
@@ -1749,7 +1786,10 @@ static int array_write_fast(zh_ctx* ctx, const zh_array_meta* m, ScatterArgs a,
   a.desc = (ItemDesc*)(W + o_desc);
   a.slow_count = d_slow;
   a.slow_list = d_slow + 4;
-  ZH_HIPF(launch_encode_resolve(a, nz, d_off, start ? isz : 0, cn, vbase,
+  if (keep)
+    ZH_HIPF(hipMemcpyAsync(d_off, hoff.data(), hoff.size() * sizeof(int64_t),
+                           hipMemcpyHostToDevice, s));
+  ZH_HIPF(launch_encode_resolve(a, nz, keep ? nullptr : d_off, start ? isz : 0, cn, vbase,
                                 v.fast_mode != kFastNone ? 1 : 0, s));
   v.shards = d_shards;
   v.nshards = ncoords;
@@ -1790,7 +1830,15 @@ static int array_write_fast(zh_ctx* ctx, const zh_array_meta* m, ScatterArgs a,
   uint32_t bad = 0;
   ZH_HIPF(hipMemcpyAsync(&bad, d_cnt, sizeof(bad), hipMemcpyDeviceToHost, s));
   ZH_HIPF(hipStreamSynchronize(s));
+  if (bad && !keep && flags_out) {  // the speculative layout was wrong: hand the flags back
+    flags_out->resize((size_t)items);
+    ZH_HIPF(hipMemcpy(flags_out->data(), d_flags, (size_t)items, hipMemcpyDeviceToHost));
+  }
 #undef ZH_HIPF
+  if (bad && keep) {
+    set_err(err, errlen, "internal error: kept chunk without data on the second write pass");
+    return ZH_EHIP;
+  }
   return bad ? kWriteFallback : ZH_OK;
 }
 
@@ -1862,13 +1910,48 @@ int zh_array_write(zh_ctx* ctx, const zh_array_meta* m, const void* src, const i
   }
   if (env_int("ZH_ENC_FAST", 1) != 0) {
     a.region = (uint8_t*)src;
-    st = array_write_fast(ctx, m, a, hs, items, tile_mode, dsts, s, err, errlen);
+    std::vector<uint8_t> flags;
+    st = array_write_fast(ctx, m, a, hs, items, tile_mode, dsts, nullptr, &flags, s, err, errlen);
     if (st != kWriteFallback) return st;
+    // second pass with the layout the first pass's all-fill flags give (the reference's),
+    // over the shards that hold an elided inner chunk only: in every other shard the
+    // speculative layout was the true one and the first pass's bytes are final
+    const int32_t* leaf = leaf_shape(m);
+    std::vector<DevShard> hs2;
+    std::vector<zh_chunk_dst> d2;
+    std::vector<int64_t> which;
+    std::vector<uint8_t> keep2;
     for (int64_t i = 0; i < ncoords; i++) {
-      hs[i].index_off = 0;
-      dsts[i].nbytes = 0;
+      const int64_t b = hs[i].item_begin;
+      const int64_t nit = c.sharded ? cps_total : 1;
+      bool dirty = false;
+      int64_t ic[kMaxDims] = {0};
+      for (int64_t k = 0; k < nit && !dirty; k++) {  // an in-bounds chunk without data?
+        bool in = true;
+        for (int d = 0; d < n; d++) in &= ic[d] * leaf[d] < hs[i].part_hi[d];
+        dirty = in && !flags[(size_t)(b + k)];
+        for (int d = n - 1; d >= 0; d--) {
+          if (++ic[d] < hs[i].box_count[d]) break;
+          ic[d] = 0;
+        }
+      }
+      if (!dirty) continue;
+      DevShard S = hs[i];
+      S.index_off = 0;
+      S.item_begin = (int64_t)keep2.size();
+      hs2.push_back(S);
+      zh_chunk_dst D = dsts[i];
+      D.nbytes = 0;
+      d2.push_back(D);
+      which.push_back(i);
+      keep2.insert(keep2.end(), flags.begin() + b, flags.begin() + b + nit);
     }
+    st = array_write_fast(ctx, m, a, hs2, (int64_t)keep2.size(), tile_mode, d2.data(),
+                          keep2.data(), nullptr, s, err, errlen);
+    for (size_t j = 0; j < which.size(); j++) dsts[which[j]].nbytes = d2[j].nbytes;
+    return st;
   }
+  // ZH_ENC_FAST=0: the independent flags → host layout → encode path (kept as a cross-check)
   const int64_t pitems = items << a.piece_shift;
   DevShard* d_shards = nullptr;
   uint8_t* d_flags = nullptr;

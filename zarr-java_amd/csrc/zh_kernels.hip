@@ -1355,7 +1355,8 @@ __global__ __launch_bounds__(kBlock) void flags_kernel(ScatterArgs a) {
 // ---------------------------------------------------------------------------------
 // per inner chunk: its payload offset under the one-pass layout (every in-bounds inner chunk
 // kept, C order: the chunk's rank in the shard's in-bounds box × stored chunk bytes, after the
-// index when it is at the start; -1 for chunks wholly in the boundary padding), then the
+// index when it is at the start; -1 for chunks wholly in the boundary padding; item_off ==
+// nullptr: a.item_off was uploaded by the host), then the
 // encode-view descriptor (src = the chunk's origin in the region, d0 = its payload position
 // relative to vbase, in elements) or a slow-list entry (clipped by the array boundary,
 // misaligned)
@@ -1395,7 +1396,8 @@ __global__ __launch_bounds__(kBlock) void encode_resolve_kernel(ScatterArgs a, E
                                                                 int vfast) {
   const int64_t stride = (int64_t)gridDim.x * kBlock;
   for (int64_t c = (int64_t)blockIdx.x * kBlock + threadIdx.x; c < a.n_citems; c += stride) {
-    if (nz.cell) {  // nested: the cell's offset + the sub-index (at the start) + the rank
+    if (!item_off) {  // offsets uploaded by the host (second pass after a fallback)
+    } else if (nz.cell) {  // nested: the cell's offset + the sub-index (at the start) + the rank
       const int64_t s = find_shard(a, c);
       int64_t cell, k2, rank;
       bool in;
