@@ -142,6 +142,30 @@ def test_crc_mismatch_message(dev):
     assert str(ed.value).startswith("The checksum of the sharding index is invalid. Stored: ")
 
 
+@pytest.mark.parametrize("loc", [A.ZH_INDEX_END, A.ZH_INDEX_START])
+def test_index_crc_multi_span_unaligned(dev, loc):
+    """Index CRC over several 4 KiB spans, the index at a byte offset that is not a multiple
+    of 4 (3-byte inner chunks, index at the end) or at 0 (start): decode equals the oracle,
+    and a flipped byte in the third span gives the reference's checksum message."""
+    shape = [41, 63]
+    meta = A.make_meta(shape, [41, 63], 1, sharded=True, inner_chunk_shape=[1, 3],
+                       index_location=loc)
+    arr = rand_array(shape, 1, seed=8)
+    arr[arr == 0] = 1
+    shards = encode_oracle(meta, arr)
+    got = device_read(dev, meta, shards, [0, 0], shape)
+    np.testing.assert_array_equal(got, arr)
+    isz = 16 * 41 * 21
+    bad = bytearray(shards[0])
+    ib = 0 if loc == A.ZH_INDEX_START else len(bad) - isz - 4
+    bad[ib + 2 * 4096 + 77] ^= 0x10
+    with pytest.raises(O.OracleError) as eo:
+        O.array_read(meta, [bytes(bad)], [0, 0], shape)
+    with pytest.raises(ZhError) as ed:
+        device_read(dev, meta, [bytes(bad)], [0, 0], shape)
+    assert str(ed.value) == str(eo.value)
+
+
 def test_corrupt_offset_rejected(dev):
     shape = [8, 8]
     meta = A.make_meta(shape, [8, 8], 4, sharded=True, inner_chunk_shape=[4, 4],

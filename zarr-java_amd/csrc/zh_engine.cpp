@@ -210,6 +210,7 @@ struct zh_plan {
   CrcJob* d_crc_jobs = nullptr;
   uint32_t* d_crc_partials = nullptr;
   int64_t n_crc_jobs = 0, n_crc_spans = 0;
+  int crc_shift = 0;            // index-CRC span = kIdxSpan << crc_shift
   uint8_t* d_input = nullptr;   // staged host sources
   std::vector<std::pair<int64_t, const void*>> h2d;  // (offset in d_input, host ptr)
   std::vector<int64_t> h2d_len;
@@ -574,6 +575,23 @@ uint64_t golden_item_mul(int64_t total) {
   };
   while (gcd(m, t) != 1) m += 2;
   return m % t;
+}
+
+// Index-CRC spans: 4 KiB per workgroup when the indexes are few (a small read: a 512 KiB
+// index in 128 workgroups instead of 8, the span CRC no longer latency-bound), 64 KiB when
+// there are enough spans to fill the chip anyway (each workgroup also loads 12 KiB of tables).
+// Sets every job's span_begin; returns the span count, *shift = log2(span / kIdxSpan).
+int64_t assign_crc_spans(std::vector<CrcJob>& jobs, int cu_count, int* shift) {
+  int64_t small = 0;
+  for (const CrcJob& J : jobs) small += (J.len + kIdxSpan - 1) / kIdxSpan;
+  *shift = small >= 4 * (int64_t)cu_count ? 4 : 0;
+  const int64_t span = (int64_t)kIdxSpan << *shift;
+  int64_t spans = 0;
+  for (CrcJob& J : jobs) {
+    J.span_begin = spans;
+    spans += (J.len + span - 1) / span;
+  }
+  return spans;
 }
 
 int grid_for(const zh_ctx* ctx, int64_t total_items) {
@@ -941,27 +959,32 @@ int zh_plan_create(zh_ctx* ctx, const zh_array_meta* m, const zh_chunk_src* chun
   }
   // CRC jobs over the device copies of the indexes
   if (c.sharded && c.index_has_crc32c) {
-    int64_t spans = 0;
     for (int64_t i = 0; i < ncoords; i++) {
       if (!hs[i].data || host_checked[i]) continue;
       CrcJob J;
       J.base = hs[i].data + hs[i].index_off;
       J.len = isz - 4;
-      J.span_begin = spans;
+      J.span_begin = 0;
       J.shard = (int32_t)i;
       J.pad = 0;
-      spans += (J.len + kCrcSpan - 1) / kCrcSpan;
       jobs.push_back(J);
     }
     p->n_crc_jobs = (int64_t)jobs.size();
-    p->n_crc_spans = spans;
+    p->n_crc_spans = assign_crc_spans(jobs, ctx->cu_count, &p->crc_shift);
   }
   if ((st = dev_alloc(&p->d_shards, hs.size(), err, errlen)) != ZH_OK ||
       (st = dev_alloc(&p->d_status, (size_t)ncoords * kStWords, err, errlen)) != ZH_OK ||
       (st = dev_alloc(&p->d_crc_jobs, jobs.size(), err, errlen)) != ZH_OK ||
-      (st = dev_alloc(&p->d_crc_partials, (size_t)p->n_crc_spans, err, errlen)) != ZH_OK) {
+      (st = dev_alloc(&p->d_crc_partials, (size_t)(p->n_crc_spans + p->n_crc_jobs), err,
+                      errlen)) != ZH_OK) {
     plan_free(p);
     return st;
+  }
+  if (p->n_crc_jobs &&  // the index CRC kernel's per-job completion counters start at zero
+      hipMemset(p->d_crc_partials, 0, (size_t)(p->n_crc_spans + p->n_crc_jobs) * 4) != hipSuccess) {
+    set_err(err, errlen, "plan upload failed");
+    plan_free(p);
+    return ZH_EHIP;
   }
   if (!(flags & ZH_OUT_DEVICE)) {
     if ((st = dev_alloc(&p->d_out, (size_t)p->out_bytes, err, errlen)) != ZH_OK) {
@@ -978,6 +1001,14 @@ int zh_plan_create(zh_ctx* ctx, const zh_array_meta* m, const zh_chunk_src* chun
     plan_free(p);
     return ZH_EHIP;
   }
+  // Small reads: split inner chunks into more pieces until the launch covers the chip (a
+  // 64^3 read touches 27 inner chunks: one workgroup each left the other CUs idle and the
+  // clipped ones ran 43 us).  Pieces stay whole 4 KiB CRC rounds, at most 256 per chunk.
+  if (env_int("ZH_SMALL_SPLIT", 1) != 0)
+    while ((items << p->args.piece_shift) < 2 * (int64_t)ctx->cu_count &&
+           p->args.piece_shift < 8 && (p->args.inner_nbytes >> (p->args.piece_shift + 1)) >= 4096 &&
+           (p->args.inner_nbytes >> (p->args.piece_shift + 1)) % 4096 == 0)
+      p->args.piece_shift++;
   std::vector<uint32_t> tab = setup_fast(m, p->args, p->tile_mode);
   p->args.tile_variant = std::min(1, std::max(0, env_int("ZH_TILE_VARIANT", 1)));
   // Chunk CRC fused into the row-interleaved tile kernel: every payload byte of a fast item
@@ -1099,8 +1130,8 @@ static int plan_enqueue(zh_plan* p, void* out, hipStream_t s) {
     }
     ZH_HIP(hipEventRecord(ev[0], s));
   }
-  ZH_HIP(launch_crc(p->d_crc_jobs, p->n_crc_jobs, p->n_crc_spans, p->d_crc_partials, p->d_status,
-                    s));
+  ZH_HIP(launch_crc(p->d_crc_jobs, p->n_crc_jobs, p->n_crc_spans, p->crc_shift, p->d_crc_partials,
+                    p->d_status, s));
   if (p->d_flat) ZH_HIP(launch_nested_index(p->nest, p->nest_grid, s));
   ScatterArgs a = p->args;
   a.region = (p->flags & ZH_OUT_DEVICE) ? (uint8_t*)out : p->d_out;
@@ -1579,11 +1610,10 @@ static int array_write_fast(zh_ctx* ctx, const zh_array_meta* m, ScatterArgs a,
     CrcJob J;
     J.base = base;
     J.len = len;
-    J.span_begin = spans;
+    J.span_begin = 0;
     J.shard = (int32_t)shard;
     J.pad = 0;
     jobs.push_back(J);
-    spans += (len + kCrcSpan - 1) / kCrcSpan;
   };
   int64_t cps2 = 1;
   std::vector<int64_t> hoff;  // keep mode: payload offset per item (-1: elided)
@@ -1695,6 +1725,8 @@ static int array_write_fast(zh_ctx* ctx, const zh_array_meta* m, ScatterArgs a,
   if (c.sharded && !c.nested && c.index_has_crc32c)  // Crc32cCodec.encode of each index
     for (int64_t i = 0; i < ncoords; i++)
       if (hs[i].index_off >= 0) add_job((const uint8_t*)dsts[i].data + hs[i].index_off, isz - 4, i);
+  int crc_shift = 0;
+  spans = assign_crc_spans(jobs, ctx->cu_count, &crc_shift);
   // chunk crc32c fused into the row encode when its lanes store each piece's payload in the
   // CRC pass's order (the decode rule, plan creation above: rows sequential in the payload,
   // equal pieces of whole 4 KiB rounds); otherwise a separate pass over the written payloads
@@ -1729,7 +1761,7 @@ static int array_write_fast(zh_ctx* ctx, const zh_array_meta* m, ScatterArgs a,
   const size_t o_slow = carve(((size_t)items + 4) * sizeof(uint32_t));
   const size_t o_tab = carve(tab.size() * sizeof(uint32_t));
   const size_t o_jobs = carve(jobs.size() * sizeof(CrcJob));
-  const size_t o_part = carve((size_t)spans * sizeof(uint32_t));
+  const size_t o_part = carve((size_t)(spans + (int64_t)jobs.size()) * sizeof(uint32_t));
   const size_t o_cdesc = carve(c.inner_crc32c ? (size_t)items * sizeof(ItemDesc) : 0);
   const size_t o_cpart = carve((size_t)(items * nspan) * sizeof(uint32_t));
   const size_t o_cnt = carve(sizeof(uint32_t));
@@ -1811,8 +1843,11 @@ static int array_write_fast(zh_ctx* ctx, const zh_array_meta* m, ScatterArgs a,
   ZH_HIPF(launch_encode_fast(v, grid, env_int("ZH_ENC_DEEP", 1), s));
   ZH_HIPF(launch_encode_slow(a, grid, s));
   ZH_HIPF(launch_encode_finish(a, nz, cn, d_cnt, d_cdesc, s));
+  if (!jobs.empty()) {
+    ZH_HIPF(hipMemsetAsync(W + o_part + spans * 4, 0, jobs.size() * 4, s));  // job counters
+  }
   if (!jobs.empty())
-    ZH_HIPF(launch_crc((const CrcJob*)(W + o_jobs), (int64_t)jobs.size(), spans,
+    ZH_HIPF(launch_crc((const CrcJob*)(W + o_jobs), (int64_t)jobs.size(), spans, crc_shift,
                        (uint32_t*)(W + o_part), nullptr, s));
   if (c.inner_crc32c) {  // Crc32cCodec.encode (:50-60) of every kept chunk payload
     DataCrcArgs D{};

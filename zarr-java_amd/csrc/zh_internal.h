@@ -12,7 +12,9 @@ namespace zh {
 constexpr int kMaxDims = ZH_MAX_DIMS;
 constexpr int kBlock = 256;            // threads per workgroup (4 waves of 64)
 constexpr int kTileTPB = 4;            // 32x32 transpose tiles per workgroup iteration
-constexpr int kCrcSpan = 64 * 1024;    // index bytes hashed per CRC workgroup
+constexpr int kCrcSpan = 64 * 1024;    // chunk payload bytes per data-CRC partial
+constexpr int kIdxSpan = 4096;         // index bytes per index-CRC workgroup (one 16-B vector
+                                       // per lane: a 512 KiB index is 128 workgroups)
 constexpr int kCrcLane = kCrcSpan / kBlock;  // 256 bytes per lane
 
 // Per-shard status words (device, uint64 each), read back by zh_plan_wait.
@@ -178,8 +180,11 @@ struct CrcJob {
 };
 
 // Kernel launchers (zh_kernels.hip).
-hipError_t launch_crc(const CrcJob* jobs, int64_t njobs, int64_t nspans, uint32_t* partials,
-                      uint64_t* status, hipStream_t stream);
+// index crc32c of every job in one launch, spans of kIdxSpan << span_shift bytes (job
+// span_begin set by assign_crc_spans); partials holds nspans span registers followed by njobs
+// completion counters, zero before the first launch (the kernel resets them)
+hipError_t launch_crc(const CrcJob* jobs, int64_t njobs, int64_t nspans, int span_shift,
+                      uint32_t* partials, uint64_t* status, hipStream_t stream);
 hipError_t launch_resolve(const ScatterArgs& a, hipStream_t stream);
 hipError_t launch_nested_index(const NestArgs& a, int grid, hipStream_t stream);
 hipError_t launch_data_crc(const DataCrcArgs& a, int grid, hipStream_t stream);

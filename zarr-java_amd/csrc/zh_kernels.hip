@@ -863,21 +863,69 @@ __device__ __forceinline__ uint32_t crc_combine(uint32_t c1, uint32_t c2, uint64
   return multmodp(x2nmodp(len2, 3), c1) ^ c2;
 }
 
-// slicing-by-8 tables of the reflected Castagnoli polynomial (CRC32C.java:14-80), per block
+// Compile-time CRC-32C constants (reflected Castagnoli polynomial, CRC32C.java:14-80):
+// slicing-by-8 tables T, the zero-shift tables S of the lane-interleaved update
+// (x^(8·4080)·b·x^(8k) for byte b at position k: the other 255 lanes' vectors of a 4 KiB
+// round), the per-lane shift kfull[t] = x^(8·(4080 − 16t)) from a lane's last vector to the
+// round's end, and x^(8·kCrcSpan).  Built by constexpr evaluation, read by every CRC kernel
+// (before: every workgroup rebuilt them in LDS with 8 dependent rounds and x^n loops).
+struct CrcTabs {
+  uint32_t T[8][256];
+  uint32_t S[4][256];
+  uint32_t kfull[256];
+  uint32_t kspan;
+  uint32_t kidx[256];  // x^(8·kIdxSpan·j): span j of an index shifted past j later spans
+};
+
+constexpr uint32_t cx_mult(uint32_t a, uint32_t b) {  // a(x)·b(x) mod P, reflected
+  uint32_t p = 0;
+  for (int i = 0; i < 32; i++) {
+    if (a & (1u << (31 - i))) p ^= b;
+    b = (b & 1) ? (b >> 1) ^ kPoly : b >> 1;
+  }
+  return p;
+}
+
+constexpr uint32_t cx_xpow8n(uint64_t n) {  // x^(8n) mod P
+  uint32_t r = 1u << 31, b = 1u << 23;
+  while (n) {
+    if (n & 1) r = cx_mult(b, r);
+    b = cx_mult(b, b);
+    n >>= 1;
+  }
+  return r;
+}
+
+constexpr CrcTabs make_crc_tabs() {
+  CrcTabs t{};
+  for (uint32_t i = 0; i < 256; i++) {
+    uint32_t c = i;
+    for (int k = 0; k < 8; k++) c = (c & 1) ? (c >> 1) ^ kPoly : c >> 1;
+    t.T[0][i] = c;
+  }
+  for (int k = 1; k < 8; k++)
+    for (int i = 0; i < 256; i++) t.T[k][i] = (t.T[k - 1][i] >> 8) ^ t.T[0][t.T[k - 1][i] & 0xFFu];
+  const uint32_t k4080 = cx_xpow8n(4080);
+  for (int b = 0; b < 4; b++)
+    for (uint32_t i = 0; i < 256; i++) t.S[b][i] = cx_mult(k4080, i << (8 * b));
+  const uint32_t x128 = cx_xpow8n(16);
+  t.kfull[255] = 1u << 31;
+  for (int i = 254; i >= 0; i--) t.kfull[i] = cx_mult(x128, t.kfull[i + 1]);
+  t.kspan = cx_xpow8n(kCrcSpan);
+  const uint32_t ki = cx_xpow8n(kIdxSpan);
+  t.kidx[0] = 1u << 31;
+  for (int j = 1; j < 256; j++) t.kidx[j] = cx_mult(ki, t.kidx[j - 1]);
+  return t;
+}
+
+__device__ const CrcTabs g_crc = make_crc_tabs();
+
+// slicing-by-8 tables into LDS (a copy of the compile-time table), per block
 __device__ __forceinline__ void init_crc_tables(uint32_t (*T)[256]) {
   const int tid = threadIdx.x;
-  {
-    uint32_t c = (uint32_t)tid;
 #pragma unroll
-    for (int k = 0; k < 8; k++) c = (c & 1) ? (c >> 1) ^ kPoly : c >> 1;
-    T[0][tid] = c;
-  }
+  for (int k = 0; k < 8; k++) T[k][tid] = g_crc.T[k][tid];
   __syncthreads();
-  for (int k = 1; k < 8; k++) {
-    const uint32_t p = T[k - 1][tid];
-    T[k][tid] = (p >> 8) ^ T[0][p & 0xFFu];
-    __syncthreads();
-  }
 }
 
 // inner crc32c codec: CRC-32C of every resolved chunk payload, coalesced.  A workgroup
@@ -949,11 +997,10 @@ __global__ __launch_bounds__(kBlock) void decode_rows_kernel(ScatterArgs a) {
   uint32_t(*S)[256] = T + 8;
   uint32_t kfull = 0, acc = 0;
   if constexpr (CRC) {
-    init_crc_tables(T);
-    const uint32_t k4080 = x2nmodp(4080, 3);
 #pragma unroll
-    for (int b = 0; b < 4; b++) S[b][threadIdx.x] = multmodp(k4080, (uint32_t)threadIdx.x << (8 * b));
-    kfull = x2nmodp((uint64_t)(4080 - 16 * threadIdx.x), 3);
+    for (int b = 0; b < 4; b++) S[b][threadIdx.x] = g_crc.S[b][threadIdx.x];
+    init_crc_tables(T);
+    kfull = g_crc.kfull[threadIdx.x];
   }
   __syncthreads();
   const int vs = a.fast_vpr_shift;
@@ -1549,37 +1596,29 @@ __device__ uint32_t lanes_to_span_crc(uint32_t c, int64_t lb, int64_t llen, int6
   return r;
 }
 
-// Standard CRC-32C of base[0, slen), slen <= kCrcSpan, by the whole workgroup: each lane
-// takes the raw register (init 0, no final xor) of its kCrcLane-byte segment
-// (slicing-by-8), shifts it past the zero bytes to the span end with one GF(2) multiply and
-// the lanes XOR together (CRC is linear over GF(2)); the init/xorout terms are added once.
-// (A pairwise combine tree cost 8 dependent x^n computations: 59 us per 512 KiB index.)
-// Uniform call; every lane returns the result.
-__device__ uint32_t span_crc8(const uint8_t* base, int64_t slen, const uint32_t (*T)[256],
-                              uint32_t* red) {
-  const int tid = threadIdx.x;
-  const int64_t lb = (int64_t)tid * kCrcLane;
-  const int64_t llen = max((int64_t)0, min((int64_t)kCrcLane, slen - lb));
-  const uint8_t* p = base + lb;
-  uint32_t c = 0;
-  int64_t i = 0;
-  if ((((uintptr_t)p) & 7) == 0) {
-    for (; i + 8 <= llen; i += 8) {
-      const uint64_t w = *reinterpret_cast<const uint64_t*>(p + i);
-      const uint32_t lo32 = (uint32_t)w ^ c, hi32 = (uint32_t)(w >> 32);
-      c = T[7][lo32 & 0xFFu] ^ T[6][(lo32 >> 8) & 0xFFu] ^ T[5][(lo32 >> 16) & 0xFFu] ^
-          T[4][lo32 >> 24] ^ T[3][hi32 & 0xFFu] ^ T[2][(hi32 >> 8) & 0xFFu] ^
-          T[1][(hi32 >> 16) & 0xFFu] ^ T[0][hi32 >> 24];
-    }
-  }
-  for (; i < llen; i++) c = T[0][(c ^ p[i]) & 0xFFu] ^ (c >> 8);
-  return lanes_to_span_crc(c, lb, llen, slen, red);
-}
 
-__global__ __launch_bounds__(kBlock) void crc_partial_kernel(const CrcJob* jobs, int64_t njobs,
-                                                              uint32_t* partials) {
+// Index CRC, one workgroup per 4 KiB span of a job (a shard index, or a sub-shard index on
+// the write path), finished in the same launch: each span's raw register (init 0, no xorout)
+// goes to partials[span]; the job's last workgroup to finish (a self-resetting counter per
+// job, after partials[nspans + job]) shifts every span's register to the job end in parallel
+// (one lane per span, x^(8·4096·j) from a table), XORs them, adds the init/xorout terms, and
+// compares
+// with the stored little-endian crc32c (decode: Crc32cCodec.decode :24-48, status) or stores
+// it (status == nullptr: Crc32cCodec.encode :50-60).  A dword-aligned span is read as
+// coalesced 16-byte vectors (lane l: vectors l, l+256, ...) with the lane-interleaved update;
+// otherwise with a per-lane slicing-by-8 byte loop.
+__global__ __launch_bounds__(kBlock) void crc_index_kernel(const CrcJob* jobs, int64_t njobs,
+                                                           int64_t nspans, int sshift,
+                                                           uint32_t* partials,
+                                                           uint64_t* status) {
+  const int64_t SPAN = (int64_t)kIdxSpan << sshift;
   __shared__ uint32_t T[8][256];
+  __shared__ uint32_t S[4][256];
   __shared__ uint32_t red[kBlock];
+  __shared__ int last;
+  const int tid = threadIdx.x;
+#pragma unroll
+  for (int b = 0; b < 4; b++) S[b][tid] = g_crc.S[b][tid];
   init_crc_tables(T);
   const int64_t span = blockIdx.x;
   int64_t lo = 0, hi = njobs - 1;
@@ -1589,10 +1628,108 @@ __global__ __launch_bounds__(kBlock) void crc_partial_kernel(const CrcJob* jobs,
     else hi = mid - 1;
   }
   const CrcJob J = jobs[lo];
-  const int64_t sb = (span - J.span_begin) * kCrcSpan;
-  const int64_t slen = min((int64_t)kCrcSpan, J.len - sb);
-  const uint32_t c = span_crc8(J.base + sb, slen, T, red);
-  if (threadIdx.x == 0) partials[span] = c;
+  const int64_t sb = (span - J.span_begin) * SPAN;
+  const int64_t slen = min(SPAN, J.len - sb);
+  const uint8_t* base = J.base + sb;
+  uint32_t raw;
+  if ((((uintptr_t)base) & 3) == 0) {
+    const int nblk = (int)(slen >> 4);
+    uint32_t acc = 0;
+    int nb = 0;
+    for (int j0 = 0; j0 < nblk; j0 += kBlock * 4) {
+      v4u v[4];
+#pragma unroll
+      for (int u = 0; u < 4; u++) {
+        const int j = j0 + tid + u * kBlock;
+        if (j < nblk) v[u] = *reinterpret_cast<const v4u*>(base + 16 * (int64_t)j);
+      }
+#pragma unroll
+      for (int u = 0; u < 4; u++)
+        if (j0 + tid + u * kBlock < nblk) {
+          acc = crc_upd16(crc_shift_tab(acc, S), v[u], T);
+          nb++;
+        }
+    }
+    uint32_t contrib = 0;
+    if (nb > 0) {
+      const int64_t e = 16 * (int64_t)(tid + kBlock * (nb - 1)) + 16;
+      contrib = multmodp((slen & 4095) == 0 ? g_crc.kfull[tid] : x2nmodp((uint64_t)(slen - e), 3),
+                         acc);
+    }
+    if (tid == 0) {  // tail bytes (span length not a multiple of 16) end the span
+      uint32_t t = 0;
+      for (int64_t i = (int64_t)nblk * 16; i < slen; i++) t = T[0][(t ^ base[i]) & 0xFFu] ^ (t >> 8);
+      contrib ^= t;
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) contrib ^= (uint32_t)__shfl_xor((int)contrib, o, 64);
+    if ((tid & 63) == 0) red[tid >> 6] = contrib;
+    __syncthreads();
+    raw = red[0] ^ red[1] ^ red[2] ^ red[3];
+  } else {
+    const int64_t kLane = SPAN / kBlock;  // bytes per lane
+    const int64_t lb = (int64_t)tid * kLane;
+    const int64_t llen = max((int64_t)0, min((int64_t)kLane, slen - lb));
+    uint32_t c = 0;
+    for (int64_t i = 0; i < llen; i++) c = T[0][(c ^ base[lb + i]) & 0xFFu] ^ (c >> 8);
+    uint32_t v = llen > 0 ? multmodp(x2nmodp((uint64_t)(slen - lb - llen), 3), c) : 0u;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v ^= (uint32_t)__shfl_xor((int)v, o, 64);
+    if ((tid & 63) == 0) red[tid >> 6] = v;
+    __syncthreads();
+    raw = red[0] ^ red[1] ^ red[2] ^ red[3];
+  }
+  uint32_t* counter = partials + nspans + lo;
+  const int64_t njs = (J.len + SPAN - 1) / SPAN;
+  if (tid == 0) {
+    partials[span] = raw;
+    __threadfence();
+    last = atomicAdd(counter, 1u) == (uint32_t)(njs - 1);
+  }
+  __syncthreads();
+  if (!last) return;  // uniform
+  __threadfence();
+  // span k ends at min((k+1)·SPAN, len); the bytes after it are (njs−1−k)·SPAN when the last
+  // span is full, else (njs−2−k)·SPAN + tail (the last span itself: 0)
+  const int64_t tail = J.len - (njs - 1) * SPAN;
+  const uint32_t xtail = tail == SPAN ? g_crc.kidx[1 << sshift] : x2nmodp((uint64_t)tail, 3);
+  uint32_t r = 0;
+  for (int64_t k = tid; k < njs; k += kBlock) {
+    const uint32_t pk = __hip_atomic_load(partials + J.span_begin + k, __ATOMIC_RELAXED,
+                                          __HIP_MEMORY_SCOPE_AGENT);
+    const int64_t j = (njs - 2 - k) << sshift;  // 4 KiB units of the full spans after span k
+    uint32_t sh;
+    if (k == njs - 1) sh = 1u << 31;
+    else if (j < 256) sh = multmodp(g_crc.kidx[j], xtail);
+    else sh = x2nmodp((uint64_t)(J.len - (k + 1) * SPAN), 3);
+    r ^= multmodp(sh, pk);
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) r ^= (uint32_t)__shfl_xor((int)r, o, 64);
+  __syncthreads();
+  if ((tid & 63) == 0) red[tid >> 6] = r;
+  __syncthreads();
+  if (tid != 0) return;
+  *counter = 0;  // ready for the next launch
+  r = red[0] ^ red[1] ^ red[2] ^ red[3];
+  const uint32_t c = multmodp(x2nmodp((uint64_t)J.len, 3), 0xFFFFFFFFu) ^ r ^ 0xFFFFFFFFu;
+  const uint8_t* sp = J.base + J.len;  // stored little-endian (Crc32cCodec.java:121,130)
+  if (!status) {  // write path: store it after the index (Crc32cCodec.encode :50-60)
+    uint8_t* w = const_cast<uint8_t*>(sp);
+    w[0] = (uint8_t)c;
+    w[1] = (uint8_t)(c >> 8);
+    w[2] = (uint8_t)(c >> 16);
+    w[3] = (uint8_t)(c >> 24);
+    return;
+  }
+  const uint32_t stored =
+      (uint32_t)sp[0] | ((uint32_t)sp[1] << 8) | ((uint32_t)sp[2] << 16) | ((uint32_t)sp[3] << 24);
+  uint64_t* st = status + (int64_t)J.shard * kStWords;
+  if (c != stored) {  // bit 32 marks the pair as set (nested sub-shard checks come later)
+    st[kStCrcStored] = (1ull << 32) | stored;
+    st[kStCrcComputed] = c;
+    atomicOr((unsigned long long*)(st + kStFlags), (unsigned long long)kFlagCrc);
+  }
 }
 
 // (crc_upd16 / crc_shift_tab: see "CRC-32C helpers" above the row kernel)
@@ -1603,17 +1740,13 @@ __global__ __launch_bounds__(kBlock) void data_crc_partial_kernel(DataCrcArgs a)
   __shared__ uint32_t T[8][256];
   __shared__ uint32_t S[4][256];
   __shared__ uint32_t wred[kBlock / 64];
-  init_crc_tables(T);
   const int tid = threadIdx.x;
-  {
-    const uint32_t k4080 = x2nmodp(4080, 3);  // x^(8*4080): the other lanes' 255 vectors
 #pragma unroll
-    for (int b = 0; b < 4; b++) S[b][tid] = multmodp(k4080, (uint32_t)tid << (8 * b));
-  }
+  for (int b = 0; b < 4; b++) S[b][tid] = g_crc.S[b][tid];  // the other lanes' 255 vectors
+  init_crc_tables(T);
   // a span of whole 4 KiB rounds: this lane's last vector ends 4080 - 16*tid bytes before
   // the span end
-  const uint32_t kfull = x2nmodp((uint64_t)(4080 - 16 * tid), 3);
-  __syncthreads();
+  const uint32_t kfull = g_crc.kfull[tid];
   const int64_t total = a.n_items * a.nspan;
   for (int64_t blk = blockIdx.x; blk < total; blk += gridDim.x) {
     const int64_t item = blk / a.nspan;
@@ -1699,37 +1832,6 @@ __global__ void data_crc_finalize_kernel(DataCrcArgs a) {
   }
 }
 
-__global__ void crc_finalize_kernel(const CrcJob* jobs, int64_t njobs, const uint32_t* partials,
-                                    uint64_t* status) {
-  const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (j >= njobs) return;
-  const CrcJob J = jobs[j];
-  uint32_t c = 0;
-  const int64_t nspans = (J.len + kCrcSpan - 1) / kCrcSpan;
-  const uint32_t kspan = x2nmodp((uint64_t)kCrcSpan, 3);  // shift past one full span
-  for (int64_t k = 0; k < nspans; k++) {
-    const int64_t slen = min((int64_t)kCrcSpan, J.len - k * kCrcSpan);
-    const uint32_t p = partials[J.span_begin + k];
-    c = slen == kCrcSpan ? multmodp(kspan, c) ^ p : crc_combine(c, p, (uint64_t)slen);
-  }
-  const uint8_t* s = J.base + J.len;  // stored little-endian (Crc32cCodec.java:121,130)
-  if (!status) {  // write path: store it after the index (Crc32cCodec.encode :50-60)
-    uint8_t* w = const_cast<uint8_t*>(s);
-    w[0] = (uint8_t)c;
-    w[1] = (uint8_t)(c >> 8);
-    w[2] = (uint8_t)(c >> 16);
-    w[3] = (uint8_t)(c >> 24);
-    return;
-  }
-  const uint32_t stored =
-      (uint32_t)s[0] | ((uint32_t)s[1] << 8) | ((uint32_t)s[2] << 16) | ((uint32_t)s[3] << 24);
-  uint64_t* st = status + (int64_t)J.shard * kStWords;
-  if (c != stored) {  // bit 32 marks the pair as set (nested sub-shard checks come later)
-    st[kStCrcStored] = (1ull << 32) | stored;
-    st[kStCrcComputed] = c;
-    atomicOr((unsigned long long*)(st + kStFlags), (unsigned long long)kFlagCrc);
-  }
-}
 
 // ---------------------------------------------------------------------------------
 // nested sharding: flatten the two-level index (ShardingIndexedCodec.decodeInternal :183-243
@@ -1953,15 +2055,11 @@ hipError_t launch_data_crc(const DataCrcArgs& a, int grid, hipStream_t stream) {
   return e == hipSuccess ? launch_data_crc_finalize(a, stream) : e;
 }
 
-hipError_t launch_crc(const CrcJob* jobs, int64_t njobs, int64_t nspans, uint32_t* partials,
-                      uint64_t* status, hipStream_t stream) {
+hipError_t launch_crc(const CrcJob* jobs, int64_t njobs, int64_t nspans, int span_shift,
+                      uint32_t* partials, uint64_t* status, hipStream_t stream) {
   if (njobs == 0) return hipSuccess;
-  hipLaunchKernelGGL(crc_partial_kernel, dim3((unsigned)nspans), dim3(kBlock), 0, stream, jobs,
-                     njobs, partials);
-  hipError_t e = hipGetLastError();
-  if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(crc_finalize_kernel, dim3((unsigned)((njobs + 63) / 64)), dim3(64), 0,
-                     stream, jobs, njobs, (const uint32_t*)partials, status);
+  hipLaunchKernelGGL(crc_index_kernel, dim3((unsigned)nspans), dim3(kBlock), 0, stream, jobs,
+                     njobs, nspans, span_shift, partials, status);
   return hipGetLastError();
 }
 
