@@ -205,6 +205,7 @@ struct zh_plan {
   int64_t in_bytes = 0, out_bytes = 0;
   std::vector<int64_t> coords;  // chunk coords (for messages)
   // device state
+  uint8_t* d_tables = nullptr;   // one allocation holding the tables below
   DevShard* d_shards = nullptr;
   uint64_t* d_status = nullptr;
   CrcJob* d_crc_jobs = nullptr;
@@ -722,15 +723,9 @@ int compact_stage(zh_plan* p, const zh_array_meta* m, const DevShard& S, int64_t
 void plan_free(zh_plan* p) {
   if (!p) return;
   (void)hipSetDevice(p->ctx->device);
-  (void)hipFree(p->d_shards);
-  (void)hipFree(p->d_status);
-  (void)hipFree(p->d_crc_jobs);
-  (void)hipFree(p->d_crc_partials);
+  (void)hipFree(p->d_tables);  // shards, status, CRC jobs/partials, descriptors, slow list, table
   (void)hipFree(p->d_input);
   (void)hipFree(p->d_out);
-  (void)hipFree(p->d_desc);
-  (void)hipFree(p->d_slow);
-  (void)hipFree(p->d_fast_tab);
   (void)hipFree(p->d_flat);
   (void)hipFree(p->d_dcrc);
   for (auto& e : p->ev_pending)
@@ -972,34 +967,11 @@ int zh_plan_create(zh_ctx* ctx, const zh_array_meta* m, const zh_chunk_src* chun
     p->n_crc_jobs = (int64_t)jobs.size();
     p->n_crc_spans = assign_crc_spans(jobs, ctx->cu_count, &p->crc_shift);
   }
-  if ((st = dev_alloc(&p->d_shards, hs.size(), err, errlen)) != ZH_OK ||
-      (st = dev_alloc(&p->d_status, (size_t)ncoords * kStWords, err, errlen)) != ZH_OK ||
-      (st = dev_alloc(&p->d_crc_jobs, jobs.size(), err, errlen)) != ZH_OK ||
-      (st = dev_alloc(&p->d_crc_partials, (size_t)(p->n_crc_spans + p->n_crc_jobs), err,
-                      errlen)) != ZH_OK) {
-    plan_free(p);
-    return st;
-  }
-  if (p->n_crc_jobs &&  // the index CRC kernel's per-job completion counters start at zero
-      hipMemset(p->d_crc_partials, 0, (size_t)(p->n_crc_spans + p->n_crc_jobs) * 4) != hipSuccess) {
-    set_err(err, errlen, "plan upload failed");
-    plan_free(p);
-    return ZH_EHIP;
-  }
   if (!(flags & ZH_OUT_DEVICE)) {
     if ((st = dev_alloc(&p->d_out, (size_t)p->out_bytes, err, errlen)) != ZH_OK) {
       plan_free(p);
       return st;
     }
-  }
-  hipError_t e = hipMemcpy(p->d_shards, hs.data(), hs.size() * sizeof(DevShard),
-                           hipMemcpyHostToDevice);
-  if (e == hipSuccess && !jobs.empty())
-    e = hipMemcpy(p->d_crc_jobs, jobs.data(), jobs.size() * sizeof(CrcJob), hipMemcpyHostToDevice);
-  if (e != hipSuccess) {
-    set_err(err, errlen, "plan upload failed: %s", hipGetErrorString(e));
-    plan_free(p);
-    return ZH_EHIP;
   }
   // Small reads: split inner chunks into more pieces until the launch covers the chip (a
   // 64^3 read touches 27 inner chunks: one workgroup each left the other CUs idle and the
@@ -1028,17 +1000,45 @@ int zh_plan_create(zh_ctx* ctx, const zh_array_meta* m, const zh_chunk_src* chun
       tab.push_back(gf2_xpow8n((uint64_t)(L - end)));
     }
   }
-  if ((st = dev_alloc(&p->d_desc, (size_t)items, err, errlen)) != ZH_OK ||
-      (st = dev_alloc(&p->d_slow, (size_t)items + 4, err, errlen)) != ZH_OK ||
-      (st = dev_alloc(&p->d_fast_tab, tab.size(), err, errlen)) != ZH_OK) {
-    plan_free(p);
-    return st;
-  }
-  if (!tab.empty() &&
-      hipMemcpy(p->d_fast_tab, tab.data(), tab.size() * 4, hipMemcpyHostToDevice) != hipSuccess) {
-    set_err(err, errlen, "plan upload failed");
-    plan_free(p);
-    return ZH_EHIP;
+  // All plan tables in one allocation, the uploaded ones (shards, CRC jobs, zeroed CRC
+  // partials + completion counters, fast-path table) as one prefix in one copy: a one-shot
+  // small read paid ~15-20 us per synchronous upload and per allocation.
+  {
+    size_t off = 0;
+    auto carve = [&](size_t bytes) {
+      const size_t o = off;
+      off += (bytes + 255) & ~(size_t)255;
+      return o;
+    };
+    const size_t o_shards = carve(hs.size() * sizeof(DevShard));
+    const size_t o_jobs = carve(jobs.size() * sizeof(CrcJob));
+    const size_t o_part = carve((size_t)(p->n_crc_spans + p->n_crc_jobs) * 4);
+    const size_t o_tab = carve(tab.size() * 4);
+    const size_t up = off;  // uploaded prefix
+    const size_t o_status = carve((size_t)ncoords * kStWords * 8);
+    const size_t o_desc = carve((size_t)items * sizeof(ItemDesc));
+    const size_t o_slow = carve(((size_t)items + 4) * 4);
+    if ((st = dev_alloc(&p->d_tables, off, err, errlen)) != ZH_OK) {
+      plan_free(p);
+      return st;
+    }
+    std::vector<uint8_t> blob(up, 0);
+    memcpy(blob.data() + o_shards, hs.data(), hs.size() * sizeof(DevShard));
+    if (!jobs.empty()) memcpy(blob.data() + o_jobs, jobs.data(), jobs.size() * sizeof(CrcJob));
+    if (!tab.empty()) memcpy(blob.data() + o_tab, tab.data(), tab.size() * 4);
+    uint8_t* T = p->d_tables;
+    p->d_shards = (DevShard*)(T + o_shards);
+    p->d_crc_jobs = jobs.empty() ? nullptr : (CrcJob*)(T + o_jobs);
+    p->d_crc_partials = (uint32_t*)(T + o_part);
+    p->d_fast_tab = tab.empty() ? nullptr : (uint32_t*)(T + o_tab);
+    p->d_status = (uint64_t*)(T + o_status);
+    p->d_desc = (ItemDesc*)(T + o_desc);
+    p->d_slow = (uint32_t*)(T + o_slow);
+    if (hipMemcpy(T, blob.data(), up, hipMemcpyHostToDevice) != hipSuccess) {
+      set_err(err, errlen, "plan upload failed");
+      plan_free(p);
+      return ZH_EHIP;
+    }
   }
   if (c.inner_crc32c && items > 0) {
     // Fuse the chunk CRC into the row kernel when its lanes read each piece's payload in
