@@ -257,6 +257,26 @@ def test_device_encode_grouped_rows(dev, dsize, order):
     assert device_write(dev, meta, arr) == want
 
 
+@pytest.mark.parametrize("order", [[0, 3, 2, 1], [0, 1, 3, 2]])
+def test_tile_encode_chunk_crc_fused(dev, monkeypatch, order):
+    """c4crc-shaped chain at small extent: [transpose, bytes(big), crc32c] with 32x32 tiles,
+    the chunk CRC fused into the tile encode (stored vectors, per-unit end shifts from the
+    payload side of the table), boundary chunks through the slow list + CRC pass; equals the
+    oracle and the unfused pass, and decodes back."""
+    shape = [1, 64, 80, 96]
+    meta = A.make_meta(shape, [1, 64, 64, 64], 4, endian=A.ZH_ENDIAN_BIG, sharded=True,
+                       inner_chunk_shape=[1, 32, 32, 32], transpose_order=order,
+                       inner_crc32c=True)
+    arr = rand_array(shape, 4, seed=51)
+    arr[arr == 0] = 1
+    want = encode_oracle(meta, arr)
+    assert device_write(dev, meta, arr) == want
+    monkeypatch.setenv("ZH_CRC_FUSE", "0")
+    assert device_write(dev, meta, arr) == want
+    monkeypatch.delenv("ZH_CRC_FUSE")
+    roundtrip(dev, meta, arr, [([0, 0, 0, 0], shape), ([0, 5, 7, 9], [1, 50, 60, 80])])
+
+
 def test_device_encode_one_pass_fallback(dev):
     """A late all-fill inner chunk (seen only after the one-pass kernels ran) sends the write
     back through flags → layout → encode; the bytes still equal the oracle's."""

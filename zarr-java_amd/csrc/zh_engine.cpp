@@ -1745,7 +1745,23 @@ static int array_write_fast(zh_ctx* ctx, const zh_array_meta* m, ScatterArgs a,
     crc_fuse = crc_fuse && a.inner_nbytes % pieces == 0 &&
                (a.inner_nbytes / pieces) % 4096 == 0 && v.fast_rows % pieces == 0;
   }
-  const int64_t cspan = crc_fuse ? a.inner_nbytes / pieces : (int64_t)kCrcSpan;
+  // ... or into the tile encode (its stores have the decode loads' geometry: per-unit end
+  // shifts from the payload side of the table, appended to it; one partial per chunk)
+  const bool tile_crc =
+      c.inner_crc32c && tile_mode && v.fast_mode == kFastTileTable &&
+      env_int("ZH_CRC_FUSE", 1) != 0 &&
+      ((int64_t)v.fast_n * 8 + 15) / 16 * 16 + 8 * 1057 * 4 + 12 * 256 * 4 +
+              (int64_t)v.fast_n * 4 <= 65536;
+  if (tile_crc) {
+    const int64_t L = a.inner_nbytes, d_fs = v.rstride[v.fs];
+    for (int32_t u = 0; u < v.fast_n; u++) {
+      const int64_t end = 4 * (int64_t)tab[2 * (size_t)u + 1] + 4 * 31 * d_fs + 128;
+      tab.push_back(gf2_xpow8n((uint64_t)(L - end)));
+    }
+  }
+  const int64_t cspan = tile_crc ? a.inner_nbytes
+                                 : (crc_fuse ? a.inner_nbytes / pieces : (int64_t)kCrcSpan);
+  crc_fuse = crc_fuse || tile_crc;
   const int64_t nspan = c.inner_crc32c ? (a.inner_nbytes + cspan - 1) / cspan : 0;
   // scratch carve-up (256-B aligned sub-buffers)
   size_t off = 0;

@@ -1188,12 +1188,13 @@ __device__ __forceinline__ uint32_t fast_tiles_rows(const ScatterArgs& a, const 
       }
     }
     __syncthreads();
-    uint4 xc[8];  // raw payload vectors of this group, kept for the CRC
-    if constexpr (CRC) {
+    uint4 xc[8];  // raw payload vectors of this group, kept for the CRC (decode)
+    if constexpr (CRC && !FLAGS) {
 #pragma unroll
       for (int k = 0; k < 8; k++) xc[k] = x[k];
     }
     if (ub + kTG < u1) load(ub + kTG);
+    uint32_t eacc = 0;  // encode view: raw register of the stored (payload) vectors
     if (live) {
       uint8_t* base = dst + ((size_t)tab[ub + t].y + g * 4) * 4;
 #pragma unroll
@@ -1205,15 +1206,21 @@ __device__ __forceinline__ uint32_t fast_tiles_rows(const ScatterArgs& a, const 
         y.z = mine[(g * 4 + 2) * 33 + r];
         y.w = mine[(g * 4 + 3) * 33 + r];
         st16s<(NT & 2) != 0>(base + (size_t)r * d_fs * 4, y);
+        if constexpr (CRC && FLAGS) {  // the stored rows have the decode loads' geometry
+          const v4u w = {y.x, y.y, y.z, y.w};
+          eacc = crc_upd16(k ? crc_shift_tab(eacc, S) : eacc, w, T);
+        }
       }
     }
     if constexpr (CRC) {
       if (live) {
-        uint32_t acc = 0;
+        uint32_t acc = eacc;
+        if constexpr (!FLAGS) {
 #pragma unroll
-        for (int k = 0; k < 8; k++) {
-          const v4u w = {xc[k].x, xc[k].y, xc[k].z, xc[k].w};
-          acc = crc_upd16(k ? crc_shift_tab(acc, S) : acc, w, T);
+          for (int k = 0; k < 8; k++) {
+            const v4u w = {xc[k].x, xc[k].y, xc[k].z, xc[k].w};
+            acc = crc_upd16(k ? crc_shift_tab(acc, S) : acc, w, T);
+          }
         }
         share ^= multmodp(K[ub + t], acc);
       }
@@ -1246,7 +1253,9 @@ __global__ __launch_bounds__(kBlock) void decode_tiles_kernel(ScatterArgs a) {
     S = T + 8;
     K = reinterpret_cast<uint32_t*>(S + 4);
     init_crc_tables(T);
-    const int64_t s_fd = a.pstride[a.fd];
+    // payload row stride of the lane's vectors: the loaded rows (decode) or, on the encode
+    // view, the stored rows (the same lane/row geometry on the destination side)
+    const int64_t s_fd = FLAGS ? a.rstride[a.fs] : a.pstride[a.fd];
     const uint32_t kg = x2nmodp((uint64_t)(4 * s_fd - 16), 3);
 #pragma unroll
     for (int b = 0; b < 4; b++) S[b][threadIdx.x] = multmodp(kg, (uint32_t)threadIdx.x << (8 * b));
@@ -2155,6 +2164,11 @@ static void launch_encode_fast_ds(const ScatterArgs& v, int grid, int deep, hipS
   if (v.fast_mode == kFastTileTable) {
     if constexpr (DS == 4) {
       const size_t l = lds + (size_t)kTG * kTilePitch * 4;
+      if (v.crc_fused) {  // chunk crc32c of the stored payload: tables + per-unit shifts
+        hipLaunchKernelGGL((decode_tiles_kernel<3, 1, true, true>), dim3(grid), dim3(kBlock),
+                           l + 12 * 256 * 4 + (size_t)v.fast_n * 4, s, v);
+        return;
+      }
       switch (v.nt) {
         case 0: hipLaunchKernelGGL((decode_tiles_kernel<0, 1, false, true>), dim3(grid), dim3(kBlock), l, s, v); break;
         case 1: hipLaunchKernelGGL((decode_tiles_kernel<1, 1, false, true>), dim3(grid), dim3(kBlock), l, s, v); break;
