@@ -148,11 +148,17 @@ def pmc_traffic(config):
     return int(d["pmc"]["traffic_bytes_per_launch"]), os.path.relpath(cands[-1], ROOT)
 
 
-def host_inclusive(dev, A, meta, coords, offs, sizes, shard_slab, n_shards=4, reps=2):
+def host_inclusive(dev, A, meta, coords, offs, sizes, shard_slab, n_shards=4, reps=2, slabs=8,
+                   nslots=3):
     """Host-resident bytes in, host-resident decoded array out: the readChunk /
     ShardingIndexedCodec.decode(ByteBuffer) of `n_shards` interior shards (4 GiB each way)
-    from pinned host memory, pipelined over three streams (H2D | decode | D2H) with two
-    device slots, so PCIe traffic in both directions overlaps the decode."""
+    from pinned host memory, pipelined over three streams (H2D | decode | D2H) so PCIe traffic
+    in both directions overlaps the decode.  Each shard moves as `slabs` y-slabs: a slab's
+    inner chunks are one contiguous byte range of the C-order payload, so a unit is that
+    range + the index, copied into a device slot that mirrors the shard's address range (the
+    decode touches only the index and the referenced chunks), and its decoded rows are one
+    contiguous part of the shard's output.  32 units of 512 MiB instead of 4 of 4 GiB cut
+    the pipeline's fill and drain from a quarter of the run to 1/32."""
     n = meta.ndim
     cs = [meta.chunk_shape[d] for d in range(n)]
     sel = [i for i, c in enumerate(coords)
@@ -161,6 +167,19 @@ def host_inclusive(dev, A, meta, coords, offs, sizes, shard_slab, n_shards=4, re
     out_sz = 4
     for c in cs:
         out_sz *= c
+    ch = meta.chain
+    inner = [ch.inner_chunk_shape[d] for d in range(n)]
+    cps = 1
+    for d in range(n):
+        cps *= cs[d] // inner[d]
+    isz = 16 * cps + 4
+    cn = 4
+    for d in range(n):
+        cn *= inner[d]
+    ys = cs[1] // slabs                    # decoded rows per slab (dim 0 is 1)
+    slab_chunks = cps // slabs             # inner chunks per slab: contiguous in C order
+    slab_in, slab_out = slab_chunks * cn, out_sz // slabs
+    assert cs[0] == 1 and ys % inner[1] == 0 and all(s == in_sz[0] for s in in_sz)
     hin = dev.malloc_pinned(sum(in_sz))
     hout = dev.malloc_pinned(out_sz * len(sel))
     pos, p = [], 0
@@ -171,48 +190,60 @@ def host_inclusive(dev, A, meta, coords, offs, sizes, shard_slab, n_shards=4, re
     smeta = A.zh_array_meta.from_buffer_copy(meta)
     for d in range(n):
         smeta.shape[d] = cs[d]
-    din = [dev.malloc(max(in_sz)) for _ in range(2)]
-    dout = [dev.malloc(out_sz) for _ in range(2)]
+    din = [dev.malloc(in_sz[0]) for _ in range(nslots)]
+    dout = [dev.malloc(slab_out) for _ in range(nslots)]
     flags = A.ZH_SRC_DEVICE | A.ZH_OUT_DEVICE
-    plans = [dev.plan(smeta, [(din[j], in_sz[0])], [0] * n, cs, flags) for j in range(2)]
+    plans = [[dev.plan(smeta, [(din[j], in_sz[0])], [0, ys * q] + [0] * (n - 2),
+                       [1, ys] + cs[2:], flags) for q in range(slabs)] for j in range(nslots)]
     s_in, s_dec, s_out = dev.stream(), dev.stream(), dev.stream()
+    units = [(k, q) for k in range(len(sel)) for q in range(slabs)]
     times = []
     for _ in range(reps):
-        ev = [[dev.event() for _ in range(3)] for _ in sel]
+        ev = [[dev.event() for _ in range(3)] for _ in units]
         dev.sync()
         t0 = time.perf_counter()
-        for k in range(len(sel)):
-            j = k & 1
-            if k >= 2:
-                dev.wait_event(s_in, ev[k - 2][1])       # slot j's input consumed
-            dev.memcpy(din[j], hin + pos[k], in_sz[k], 0, s_in, False)
-            dev.record(ev[k][0], s_in)
-            dev.wait_event(s_dec, ev[k][0])
-            if k >= 2:
-                dev.wait_event(s_dec, ev[k - 2][2])      # slot j's output drained
-            plans[j].execute(dout[j], s_dec)
-            dev.record(ev[k][1], s_dec)
-            dev.wait_event(s_out, ev[k][1])
-            dev.memcpy(hout + k * out_sz, dout[j], out_sz, 1, s_out, False)
-            dev.record(ev[k][2], s_out)
+        for u, (k, q) in enumerate(units):
+            j = u % nslots
+            if u >= nslots:
+                dev.wait_event(s_in, ev[u - nslots][1])       # slot j's input consumed
+            ioff = in_sz[k] - isz                             # index at the end
+            dev.memcpy(din[j] + q * slab_in, hin + pos[k] + q * slab_in, slab_in, 0, s_in, False)
+            dev.memcpy(din[j] + ioff, hin + pos[k] + ioff, isz, 0, s_in, False)
+            dev.record(ev[u][0], s_in)
+            dev.wait_event(s_dec, ev[u][0])
+            if u >= nslots:
+                dev.wait_event(s_dec, ev[u - nslots][2])      # slot j's output drained
+            plans[j][q].execute(dout[j], s_dec)
+            dev.record(ev[u][1], s_dec)
+            dev.wait_event(s_out, ev[u][1])
+            dev.memcpy(hout + k * out_sz + q * slab_out, dout[j], slab_out, 1, s_out, False)
+            dev.record(ev[u][2], s_out)
         for s in (s_in, s_dec, s_out):
             dev.sync(s)
         times.append(time.perf_counter() - t0)
-        for pl in plans:
-            pl.wait()
+        for row in plans:
+            for pl in row:
+                pl.wait()
     t = min(times)
     res = {"value": round(len(sel) * out_sz / t / GiB, 2), "unit": "GiB/s",
-           "h2d_bytes": sum(in_sz), "d2h_bytes": out_sz * len(sel), "seconds": round(t, 4),
+           "h2d_bytes": len(units) * (slab_in + isz), "d2h_bytes": out_sz * len(sel),
+           "seconds": round(t, 4),
            "workload": f"readChunk of {len(sel)} interior shards (4 GiB in + 4 GiB out each) "
-                       "from pinned host memory, H2D | decode | D2H pipelined on 3 streams"}
-    # a decoded shard must equal the generator's values of its region
+                       f"from pinned host memory as {len(units)} y-slab units (chunk range + "
+                       f"index in, slab out), H2D | decode | D2H pipelined on 3 streams, "
+                       f"{nslots} device slots"}
+    # every decoded shard must equal the generator's values of its region
     chk = dev.malloc(out_sz)
-    dev.memcpy(chk, hout + (len(sel) - 1) * out_sz, out_sz, 0, None, True)
-    c = coords[sel[-1]]
-    res["verify_mismatches"] = dev.synth_verify(chk, [meta.shape[d] for d in range(n)],
-                                                [c[d] * cs[d] for d in range(n)], cs, 4, SEED)
-    for pl in plans:
-        pl.close()
+    bad = 0
+    for k, i in enumerate(sel):
+        dev.memcpy(chk, hout + k * out_sz, out_sz, 0, None, True)
+        c = coords[i]
+        bad += dev.synth_verify(chk, [meta.shape[d] for d in range(n)],
+                                [c[d] * cs[d] for d in range(n)], cs, 4, SEED)
+    res["verify_mismatches"] = bad
+    for row in plans:
+        for pl in row:
+            pl.close()
     for x in din + dout + [chk]:
         dev.free(x)
     dev.free_pinned(hin)
