@@ -128,6 +128,10 @@ void zh_ctx_destroy(zh_ctx* ctx);
 int zh_ctx_device(const zh_ctx* ctx);
 /* The context's default stream (a hipStream_t).  Calls with stream == NULL use it. */
 void* zh_ctx_stream(zh_ctx* ctx);
+/* Device blocks of finished plans are kept by the context (at most 8 GiB, blocks up to
+ * 4 GiB) and reused by later plans: fresh device memory pays for its first touch.  Returns
+ * them to the runtime; returns the bytes released.  No reference counterpart. */
+int64_t zh_ctx_release_cache(zh_ctx* ctx);
 const char* zh_version(void);
 
 /* ---- host-side metadata helpers (no device needed) ------------------------------- */

@@ -2,7 +2,8 @@
 """One-shot small-read latency: zh_array_read (plan + execute + teardown in one call, the
 way HipArray.read binds it) of a 1x64x64x64 region (BASELINE configs[0]'s read shape) from a
 device-resident c4-format shard (1x1024^3 uint32, inner 32^3 + transpose [0,3,2,1], index +
-crc32c), into device memory and into host memory; beside it the reused plan (execute + wait).
+crc32c), into device memory and into pinned and pageable host memory; beside it the reused
+plan (execute + wait), and the rate of a 2 GiB half-shard read into pinned / pageable memory.
 Median of 200 after 20 warmups; every result checked against the generator.
 usage: oneshot_latency.py [reps]"""
 import ctypes as C
@@ -54,6 +55,27 @@ res["zh_array_read one-shot, pinned host out"] = timed(
     lambda: dev.array_read(meta, [(shard, size)], off, shp, hout, A.ZH_SRC_DEVICE))
 dev.memcpy(dout, hout, nb, 0, None, True)
 assert dev.synth_verify(dout, shape, off, shp, 4, bench.SEED) == 0
+pageable = (C.c_char * nb)()  # e.g. the Java int[] behind GetPrimitiveArrayCritical
+res["zh_array_read one-shot, pageable host out"] = timed(
+    lambda: dev.array_read(meta, [(shard, size)], off, shp, C.addressof(pageable), A.ZH_SRC_DEVICE))
+dev.memcpy(dout, C.addressof(pageable), nb, 0, None, True)
+assert dev.synth_verify(dout, shape, off, shp, 4, bench.SEED) == 0
+# a large read: a 1x512x1024x1024 half shard (2 GiB) into pinned and pageable host memory
+boff, bshp = [0, 256, 0, 0], [1, 512, 1024, 1024]
+bnb = 512 * 1024 * 1024 * 4
+bpin = dev.malloc_pinned(bnb)
+bpage = (C.c_char * bnb)()
+for tag, dst in (("pinned", bpin), ("pageable", C.addressof(bpage))):
+    ts = []
+    for i in range(4):
+        t0 = time.perf_counter()
+        dev.array_read(meta, [(shard, size)], boff, bshp, dst, A.ZH_SRC_DEVICE)
+        if i:
+            ts.append(time.perf_counter() - t0)
+    res[f"zh_array_read 2 GiB half shard, {tag} host out (GiB/s)"] = \
+        round(bnb / statistics.median(ts) / 2**30, 2)
+dev.free_pinned(bpin)
+del bpage
 plan = dev.plan(meta, [(shard, size)], off, shp, A.ZH_SRC_DEVICE | A.ZH_OUT_DEVICE)
 
 

@@ -508,3 +508,21 @@ def test_compact_staging_errors_match_oracle(dev):
         with pytest.raises(ZhError) as ed:
             _plan_read_host(dev, meta, [bytes(b)], off, shp)
         assert str(ed.value) == str(eo.value)
+
+
+def test_plan_block_cache_reuse_and_release(dev):
+    """Finished plans hand their device blocks to the context, later plans reuse them (no
+    stale data leaks into results: every read below is checked), and zh_ctx_release_cache
+    returns them to the runtime."""
+    shape = [24, 40, 36]
+    meta = A.make_meta(shape, [16, 16, 24], 4, endian=A.ZH_ENDIAN_BIG, sharded=True,
+                       inner_chunk_shape=[8, 8, 12])
+    arr = rand_array(shape, 4, seed=61)
+    shards = encode_oracle(meta, arr)
+    for off, shp in [([0, 0, 0], shape), ([3, 5, 7], [17, 30, 20]), ([0, 0, 0], shape)]:
+        got = device_read(dev, meta, shards, off, shp)
+        np.testing.assert_array_equal(got, arr[tuple(slice(o, o + s) for o, s in zip(off, shp))])
+    assert dev.release_cache() > 0
+    assert dev.release_cache() == 0
+    got = device_read(dev, meta, shards, [0, 0, 0], shape)
+    np.testing.assert_array_equal(got, arr)

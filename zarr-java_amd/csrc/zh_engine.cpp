@@ -194,7 +194,63 @@ struct zh_ctx {
   // write-path scratch (grow-only, under mu; zh_array_write synchronises before it returns)
   uint8_t* wscratch = nullptr;
   size_t wscratch_cap = 0;
+  // device blocks released by finished plans, reused by later plans of this context: fresh
+  // device memory pays for its first touch (a 2 GiB staging buffer cost ~30 ms in page
+  // setup on every one-shot host-output read) and small allocations pay per call
+  std::mutex cache_mu;
+  std::multimap<size_t, void*> cache;  // block bytes → block
+  size_t cache_bytes = 0;
 };
+
+namespace {
+constexpr size_t kCacheMaxBlock = (size_t)4 << 30;   // larger blocks go back to the runtime
+constexpr size_t kCacheMaxTotal = (size_t)8 << 30;
+
+size_t cache_round(size_t bytes) {  // 64 KiB granules below 64 MiB, 2 MiB above
+  const size_t g = bytes < ((size_t)64 << 20) ? ((size_t)64 << 10) : ((size_t)2 << 20);
+  return (bytes + g - 1) / g * g;
+}
+
+// a device block of at least `bytes` (returned size in *got): a cached block of up to 1.25x
+// the request, else hipMalloc
+hipError_t ctx_alloc(zh_ctx* ctx, size_t bytes, void** p, size_t* got) {
+  const size_t want = cache_round(bytes);
+  {
+    std::lock_guard<std::mutex> lk(ctx->cache_mu);
+    auto it = ctx->cache.lower_bound(want);
+    if (it != ctx->cache.end() && it->first <= want + want / 4) {
+      *p = it->second;
+      *got = it->first;
+      ctx->cache_bytes -= it->first;
+      ctx->cache.erase(it);
+      return hipSuccess;
+    }
+  }
+  *got = want;
+  hipError_t e = hipMalloc(p, want);
+  if (e == hipErrorOutOfMemory) {  // give the cached blocks back and try once more
+    std::lock_guard<std::mutex> lk(ctx->cache_mu);
+    for (auto& kv : ctx->cache) (void)hipFree(kv.second);
+    ctx->cache.clear();
+    ctx->cache_bytes = 0;
+    e = hipMalloc(p, want);
+  }
+  return e;
+}
+
+void ctx_release(zh_ctx* ctx, void* p, size_t bytes) {
+  if (!p) return;
+  if (bytes <= kCacheMaxBlock) {
+    std::lock_guard<std::mutex> lk(ctx->cache_mu);
+    if (ctx->cache_bytes + bytes <= kCacheMaxTotal) {
+      ctx->cache.emplace(bytes, p);
+      ctx->cache_bytes += bytes;
+      return;
+    }
+  }
+  (void)hipFree(p);
+}
+}  // namespace
 
 struct zh_plan {
   zh_ctx* ctx = nullptr;
@@ -205,6 +261,7 @@ struct zh_plan {
   int64_t in_bytes = 0, out_bytes = 0;
   std::vector<int64_t> coords;  // chunk coords (for messages)
   // device state
+  std::vector<std::pair<void*, size_t>> blocks;  // context-cache blocks owned by the plan
   uint8_t* d_tables = nullptr;   // one allocation holding the tables below
   DevShard* d_shards = nullptr;
   uint64_t* d_status = nullptr;
@@ -272,11 +329,23 @@ void zh_ctx_destroy(zh_ctx* c) {
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   if (c->wscratch) (void)hipFree(c->wscratch);
+  for (auto& kv : c->cache) (void)hipFree(kv.second);
   delete c;
 }
 
 int zh_ctx_device(const zh_ctx* c) { return c ? c->device : -1; }
 void* zh_ctx_stream(zh_ctx* c) { return c ? (void*)c->stream : nullptr; }
+
+int64_t zh_ctx_release_cache(zh_ctx* c) {
+  if (!c) return 0;
+  (void)hipSetDevice(c->device);
+  std::lock_guard<std::mutex> lk(c->cache_mu);
+  const int64_t n = (int64_t)c->cache_bytes;
+  for (auto& kv : c->cache) (void)hipFree(kv.second);
+  c->cache.clear();
+  c->cache_bytes = 0;
+  return n;
+}
 
 // =====================================================================================
 // host helpers
@@ -614,6 +683,24 @@ int dev_alloc(T** p, size_t count, char* err, size_t errlen) {
   return ZH_OK;
 }
 
+// a plan buffer from the context's block cache (released by plan_free)
+template <typename T>
+int plan_alloc(zh_plan* p, T** ptr, size_t count, char* err, size_t errlen) {
+  *ptr = nullptr;
+  if (count == 0) return ZH_OK;
+  void* q = nullptr;
+  size_t got = 0;
+  hipError_t e = ctx_alloc(p->ctx, count * sizeof(T), &q, &got);
+  if (e != hipSuccess) {
+    set_err(err, errlen, "hipMalloc(%zu bytes) failed: %s", count * sizeof(T),
+            hipGetErrorString(e));
+    return e == hipErrorOutOfMemory ? ZH_ENOMEM : ZH_EHIP;
+  }
+  p->blocks.emplace_back(q, got);
+  *ptr = (T*)q;
+  return ZH_OK;
+}
+
 uint64_t ld_u64_host(const uint8_t* p, bool be) {
   uint64_t v = 0;
   for (int i = 0; i < 8; i++) v |= (uint64_t)p[i] << (be ? 56 - 8 * i : 8 * i);
@@ -723,11 +810,12 @@ int compact_stage(zh_plan* p, const zh_array_meta* m, const DevShard& S, int64_t
 void plan_free(zh_plan* p) {
   if (!p) return;
   (void)hipSetDevice(p->ctx->device);
-  (void)hipFree(p->d_tables);  // shards, status, CRC jobs/partials, descriptors, slow list, table
-  (void)hipFree(p->d_input);
-  (void)hipFree(p->d_out);
-  (void)hipFree(p->d_flat);
-  (void)hipFree(p->d_dcrc);
+  // the blocks go back to the context's cache: the plan's last work on them must be done
+  if (!p->blocks.empty()) {
+    if (p->last_stream) (void)hipStreamSynchronize(p->last_stream);
+    if (p->graph_stream) (void)hipStreamSynchronize(p->graph_stream);
+  }
+  for (auto& b : p->blocks) ctx_release(p->ctx, b.first, b.second);
   for (auto& e : p->ev_pending)
     for (auto ev : e) p->ev_pool.push_back(ev);
   for (auto ev : p->ev_pool) (void)hipEventDestroy(ev);
@@ -895,7 +983,7 @@ int zh_plan_create(zh_ctx* ctx, const zh_array_meta* m, const zh_chunk_src* chun
   p->out_bytes = onel * m->dtype_size;
   // stage host sources
   if (staged > 0) {
-    st = dev_alloc(&p->d_input, (size_t)staged, err, errlen);
+    st = plan_alloc(p, &p->d_input, (size_t)staged, err, errlen);
     if (st != ZH_OK) {
       plan_free(p);
       return st;
@@ -924,7 +1012,7 @@ int zh_plan_create(zh_ctx* ctx, const zh_array_meta* m, const zh_chunk_src* chun
     }
   }
   if (nested && flat_bytes > 0) {
-    st = dev_alloc(&p->d_flat, (size_t)flat_bytes, err, errlen);
+    st = plan_alloc(p, &p->d_flat, (size_t)flat_bytes, err, errlen);
     if (st != ZH_OK) {
       plan_free(p);
       return st;
@@ -968,7 +1056,7 @@ int zh_plan_create(zh_ctx* ctx, const zh_array_meta* m, const zh_chunk_src* chun
     p->n_crc_spans = assign_crc_spans(jobs, ctx->cu_count, &p->crc_shift);
   }
   if (!(flags & ZH_OUT_DEVICE)) {
-    if ((st = dev_alloc(&p->d_out, (size_t)p->out_bytes, err, errlen)) != ZH_OK) {
+    if ((st = plan_alloc(p, &p->d_out, (size_t)p->out_bytes, err, errlen)) != ZH_OK) {
       plan_free(p);
       return st;
     }
@@ -1018,7 +1106,7 @@ int zh_plan_create(zh_ctx* ctx, const zh_array_meta* m, const zh_chunk_src* chun
     const size_t o_status = carve((size_t)ncoords * kStWords * 8);
     const size_t o_desc = carve((size_t)items * sizeof(ItemDesc));
     const size_t o_slow = carve(((size_t)items + 4) * 4);
-    if ((st = dev_alloc(&p->d_tables, off, err, errlen)) != ZH_OK) {
+    if ((st = plan_alloc(p, &p->d_tables, off, err, errlen)) != ZH_OK) {
       plan_free(p);
       return st;
     }
@@ -1065,7 +1153,7 @@ int zh_plan_create(zh_ctx* ctx, const zh_array_meta* m, const zh_chunk_src* chun
                                   : (fuse ? g.inner_nbytes / pieces : (int64_t)kCrcSpan);
     fuse = fuse || tile_crc;
     const int64_t nspan = (g.inner_nbytes + span - 1) / span;
-    if ((st = dev_alloc(&p->d_dcrc, (size_t)(items * nspan), err, errlen)) != ZH_OK) {
+    if ((st = plan_alloc(p, &p->d_dcrc, (size_t)(items * nspan), err, errlen)) != ZH_OK) {
       plan_free(p);
       return st;
     }

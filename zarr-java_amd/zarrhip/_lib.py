@@ -27,6 +27,7 @@ _SIGS = {
     "zh_ctx_destroy": (None, [P]),
     "zh_ctx_device": (C.c_int, [P]),
     "zh_ctx_stream": (P, [P]),
+    "zh_ctx_release_cache": (I64, [P]),
     "zh_validate_meta": (C.c_int, [PMETA, CH, SZ]),
     "zh_shard_index_size": (I64, [PMETA]),
     "zh_crc32c": (U32, [U32, P, SZ]),
@@ -140,6 +141,10 @@ class DeviceContext:
         if self.h:
             self.L.zh_ctx_destroy(self.h)
             self.h = None
+
+    def release_cache(self):
+        """zh_ctx_release_cache: hand the finished plans' cached device blocks back."""
+        return self.L.zh_ctx_release_cache(self.h)
 
     def __del__(self):
         try:
