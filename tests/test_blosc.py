@@ -73,3 +73,33 @@ def test_unsupported_flags():
     f[2] = (f[2] & 0x1F) | (4 << 5)  # zstd payload
     with pytest.raises(z.UnsupportedChainError):
         BloscCodec().decode(bytes(f))
+
+
+@pytest.mark.parametrize("comp", ["lz4", "blosclz", "zlib"])
+@pytest.mark.parametrize("split", [True, False])
+def test_mutated_frames_never_crash(comp, split):
+    """Untrusted frames: random byte flips, truncations and header-field overwrites of valid
+    frames either decode or raise the codec's error; the C++ decoder must never read or write
+    out of bounds (run under tools/run_host_asan.sh, the host ASan + UBSan build)."""
+    rng = np.random.default_rng(100 + len(comp) + split)
+    data = (np.arange(6000, dtype="<i4") % 97).tobytes()
+    good = sb.frame(data, 4, 4096, comp, True, split)
+    for i in range(300):
+        b = bytearray(good)
+        kind = i % 4
+        if kind == 0:      # flip a few payload bytes
+            for _ in range(int(rng.integers(1, 6))):
+                b[int(rng.integers(16, len(b)))] ^= int(rng.integers(1, 256))
+        elif kind == 1:    # truncate
+            b = b[:int(rng.integers(0, len(b)))]
+        elif kind == 2:    # overwrite a header field (sizes, block size, compressed size)
+            o = int(rng.choice([4, 8, 12]))
+            b[o:o + 4] = struct.pack("<I", int(rng.integers(0, 1 << 32)))
+        else:              # corrupt a block start offset
+            if len(b) >= 20:
+                b[16:20] = struct.pack("<I", int(rng.integers(0, 1 << 32)))
+        try:
+            out = BloscCodec().decode(bytes(b))
+            assert isinstance(out, (bytes, bytearray))
+        except (z.ZarrException, z.UnsupportedChainError):
+            pass

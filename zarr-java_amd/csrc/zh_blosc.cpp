@@ -137,21 +137,38 @@ int zh_blosc_decompress(const void* src_v, size_t srclen, void* dst_v, size_t ds
   }
   const uint8_t flags = src[2], ts = src[3];
   const size_t nbytes = rd32(src + 4), bsize = rd32(src + 8), cbytes = rd32(src + 12);
+  // The header is validated before the size query answers: callers allocate nbytes, and a
+  // corrupt frame must not make them allocate gigabytes first.
+  if (cbytes > srclen) {
+    set_err(err, errlen, "blosc frame truncated");
+    return ZH_EDATA;
+  }
+  const bool memcpyed = (flags & 0x02) != 0;
+  if (memcpyed && 16 + nbytes > srclen) {
+    set_err(err, errlen, "blosc frame truncated");
+    return ZH_EDATA;
+  }
+  size_t nblocks = 0;
+  if (!memcpyed && nbytes > 0) {
+    // no codec here expands a stream by more than ~1032x (deflate), so a larger nbytes is a
+    // corrupt header
+    if (bsize == 0 || ts == 0 || nbytes > 2048 * (size_t)cbytes + 65536) {
+      set_err(err, errlen, "corrupt blosc header");
+      return ZH_EDATA;
+    }
+    nblocks = (nbytes + bsize - 1) / bsize;
+    if (16 + 4 * nblocks > srclen) {
+      set_err(err, errlen, "blosc frame truncated");
+      return ZH_EDATA;
+    }
+  }
   if (nbytes_out) *nbytes_out = nbytes;
   if (!dst) return ZH_OK;  // size query
   if (nbytes > dstcap) {
     set_err(err, errlen, "blosc destination too small");
     return ZH_EINVAL;
   }
-  if (cbytes > srclen) {
-    set_err(err, errlen, "blosc frame truncated");
-    return ZH_EDATA;
-  }
-  if (flags & 0x02) {  // memcpyed
-    if (16 + nbytes > srclen) {
-      set_err(err, errlen, "blosc frame truncated");
-      return ZH_EDATA;
-    }
+  if (memcpyed) {
     memcpy(dst, src + 16, nbytes);
     return ZH_OK;
   }
@@ -165,16 +182,7 @@ int zh_blosc_decompress(const void* src_v, size_t srclen, void* dst_v, size_t ds
     return ZH_EUNSUPPORTED;
   }
   if (nbytes == 0) return ZH_OK;
-  if (bsize == 0 || ts == 0) {
-    set_err(err, errlen, "corrupt blosc header");
-    return ZH_EDATA;
-  }
-  const size_t nblocks = (nbytes + bsize - 1) / bsize;
-  if (16 + 4 * nblocks > srclen) {
-    set_err(err, errlen, "blosc frame truncated");
-    return ZH_EDATA;
-  }
-  std::vector<uint8_t> tmp(bsize);
+  std::vector<uint8_t> tmp(std::min(bsize, nbytes));  // one (shuffled) block
   for (size_t k = 0; k < nblocks; k++) {
     const size_t bs = k + 1 < nblocks ? bsize : nbytes - k * bsize;
     const bool leftover = bs < bsize;

@@ -6,7 +6,8 @@ import os
 from . import _abi as A
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libzarrhip.so")
+# ZH_LIB_PATH: another build of the same library (the host-sanitizer build, make asan)
+LIB_PATH = os.environ.get("ZH_LIB_PATH") or os.path.join(_HERE, "libzarrhip.so")
 
 _lib = None
 
