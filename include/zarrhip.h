@@ -247,6 +247,16 @@ int64_t zh_array_encoded_bound(const zh_array_meta* meta);
 int zh_array_write(zh_ctx* ctx, const zh_array_meta* meta, const void* src,
                    const int64_t* offset, const int64_t* shape, zh_chunk_dst* dsts,
                    int64_t nchunks, void* stream, char* err, size_t errlen);
+/* zh_array_write for host buffers (the JNI write path: the region is a Java array, the
+ * encoded chunks become byte[]s): src_host holds the region in C order; the encoded chunk i
+ * is copied to outs[i] (capacities[i] bytes available) and its size stored in nbytes[i]
+ * (0 = chunk is all fill → delete the key).  A capacity below the encoded size → ZH_EINVAL
+ * naming the size needed; zh_array_encoded_bound always suffices.  Staging goes through the
+ * context's block cache. */
+int zh_array_write_host(zh_ctx* ctx, const zh_array_meta* meta, const void* src_host,
+                        const int64_t* offset, const int64_t* shape, void* const* outs,
+                        const int64_t* capacities, int64_t* nbytes, int64_t nchunks, char* err,
+                        size_t errlen);
 
 /* ---- device memory / stream / event plumbing for callers without their own ---------- */
 /* sizeof of the public structs, for binding-side layout checks (ctypes / JNI mirrors):

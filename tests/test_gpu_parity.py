@@ -526,3 +526,24 @@ def test_plan_block_cache_reuse_and_release(dev):
     assert dev.release_cache() == 0
     got = device_read(dev, meta, shards, [0, 0, 0], shape)
     np.testing.assert_array_equal(got, arr)
+
+
+@pytest.mark.parametrize("mode", ["sharded_transpose", "unsharded", "nested_crc"])
+def test_array_write_host_buffers(dev, mode):
+    """zh_array_write_host (the JNI write path: Java array in, byte[] chunks out) equals the
+    oracle's encode, with elided inner chunks, a deleted all-fill chunk and boundary chunks."""
+    shape = [20, 24, 40]
+    kw = dict(endian=A.ZH_ENDIAN_BIG)
+    if mode == "sharded_transpose":
+        kw.update(sharded=True, inner_chunk_shape=[4, 8, 16], transpose_order=[2, 0, 1])
+    if mode == "nested_crc":
+        kw.update(sharded=True, inner_chunk_shape=[4, 8, 16], nested_chunk_shape=[2, 4, 8],
+                  inner_crc32c=True)
+    meta = A.make_meta(shape, [8, 16, 32], 4, **kw)
+    arr = rand_array(shape, 4, seed=71)
+    arr[arr == 0] = 1
+    arr[0:8, 0:16, 0:32] = 0      # a whole chunk of fill → deleted
+    arr[8:12, 0:8, 0:16] = 0      # an inner chunk of fill → (-1, -1)
+    want = encode_oracle(meta, arr)
+    got = dev.array_write_host(meta, arr.tobytes(), [0, 0, 0], shape, len(want))
+    assert got == want

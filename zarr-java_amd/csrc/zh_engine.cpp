@@ -2290,6 +2290,56 @@ int zh_array_write(zh_ctx* ctx, const zh_array_meta* m, const void* src, const i
   return ZH_OK;
 }
 
+int zh_array_write_host(zh_ctx* ctx, const zh_array_meta* m, const void* src_host,
+                        const int64_t* offset, const int64_t* shape, void* const* outs,
+                        const int64_t* capacities, int64_t* nbytes, int64_t nchunks, char* err,
+                        size_t errlen) {
+  if (!ctx || !m || !src_host || !offset || !shape || (nchunks > 0 && (!outs || !capacities ||
+                                                                         !nbytes)))
+    return ZH_EINVAL;
+  int st = zh_validate_meta(m, err, errlen);
+  if (st != ZH_OK) return st;
+  (void)hipSetDevice(ctx->device);
+  int64_t rbytes = m->dtype_size;
+  for (int d = 0; d < m->ndim; d++) rbytes *= shape[d];
+  const int64_t bound = zh_array_encoded_bound(m);
+  void* dsrc = nullptr;
+  void* ddst = nullptr;
+  size_t gsrc = 0, gdst = 0;
+  hipError_t e = ctx_alloc(ctx, (size_t)std::max<int64_t>(1, rbytes), &dsrc, &gsrc);
+  if (e == hipSuccess)
+    e = ctx_alloc(ctx, (size_t)std::max<int64_t>(1, bound * nchunks), &ddst, &gdst);
+  if (e == hipSuccess) e = hipMemcpy(dsrc, src_host, (size_t)rbytes, hipMemcpyHostToDevice);
+  std::vector<zh_chunk_dst> dsts((size_t)std::max<int64_t>(1, nchunks));
+  if (e == hipSuccess) {
+    for (int64_t i = 0; i < nchunks; i++) {
+      dsts[(size_t)i].data = (uint8_t*)ddst + i * bound;
+      dsts[(size_t)i].capacity = bound;
+      dsts[(size_t)i].nbytes = 0;
+    }
+    st = zh_array_write(ctx, m, dsrc, offset, shape, dsts.data(), nchunks, nullptr, err, errlen);
+    for (int64_t i = 0; st == ZH_OK && i < nchunks; i++) {
+      nbytes[i] = dsts[(size_t)i].nbytes;
+      if (nbytes[i] == 0) continue;
+      if (nbytes[i] > capacities[i] || !outs[i]) {
+        set_err(err, errlen, "chunk destination %lld too small: need %lld bytes, have %lld",
+                (long long)i, (long long)nbytes[i], (long long)capacities[i]);
+        st = ZH_EINVAL;
+        break;
+      }
+      e = hipMemcpy(outs[i], dsts[(size_t)i].data, (size_t)nbytes[i], hipMemcpyDeviceToHost);
+      if (e != hipSuccess) break;
+    }
+  }
+  if (dsrc) ctx_release(ctx, dsrc, gsrc);
+  if (ddst) ctx_release(ctx, ddst, gdst);
+  if (e != hipSuccess) {
+    set_err(err, errlen, "HIP error %s (%s)", hipGetErrorName(e), hipGetErrorString(e));
+    return e == hipErrorOutOfMemory ? ZH_ENOMEM : ZH_EHIP;
+  }
+  return st;
+}
+
 // =====================================================================================
 // plumbing
 // =====================================================================================

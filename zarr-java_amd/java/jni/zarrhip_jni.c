@@ -197,3 +197,90 @@ JNIEXPORT jint JNICALL Java_dev_zarr_zarrjava_hip_ZarrHip_shardDecodePartial(
   if (st != ZH_OK) return throw_status(env, st, err);
   return 0;
 }
+
+/* core.Array.write replacement for a region of whole chunks (clipped only by the array
+ * boundary): data = the primitive array of the region in C order (ucar storage copied to
+ * 1-D); returns byte[][] in computeChunkCoords order, null = chunk all fill_value (the
+ * caller deletes the key, Array.java:150-151), or null when the chain or region is not
+ * device-supported (the caller keeps core.Array.write). */
+JNIEXPORT jobjectArray JNICALL Java_dev_zarr_zarrjava_hip_ZarrHip_arrayWrite(
+    JNIEnv* env, jclass cls, jlong ctx, jintArray jm, jlongArray jshape, jintArray jchunk,
+    jintArray jinner, jintArray jorder, jbyteArray jfill, jlongArray joffset,
+    jlongArray jregion, jobject data) {
+  (void)cls;
+  zh_array_meta m;
+  int st = build_meta(env, jm, jshape, jchunk, jinner, jorder, jfill, &m);
+  if (st != ZH_OK) return NULL;
+  char err[1024] = {0};
+  st = zh_validate_meta(&m, err, sizeof err);
+  if (st == ZH_EUNSUPPORTED) return NULL;
+  if (st != ZH_OK) {
+    throw_status(env, st, err);
+    return NULL;
+  }
+  jlong off[ZH_MAX_DIMS], reg[ZH_MAX_DIMS];
+  (*env)->GetLongArrayRegion(env, joffset, 0, m.ndim, off);
+  (*env)->GetLongArrayRegion(env, jregion, 0, m.ndim, reg);
+  int64_t o64[ZH_MAX_DIMS], r64[ZH_MAX_DIMS], sh64[ZH_MAX_DIMS];
+  int32_t cs32[ZH_MAX_DIMS];
+  for (int d = 0; d < m.ndim; d++) {
+    o64[d] = off[d];
+    r64[d] = reg[d];
+    sh64[d] = m.shape[d];
+    cs32[d] = m.chunk_shape[d];
+  }
+  const int64_t n = zh_compute_chunk_coords(m.ndim, sh64, cs32, o64, r64, NULL, 0);
+  if (n < 0) {
+    throw_status(env, ZH_EINVAL, "chunk coordinates out of range");
+    return NULL;
+  }
+  const int64_t bound = zh_array_encoded_bound(&m);
+  void** outs = (void**)calloc((size_t)(n > 0 ? n : 1), sizeof(void*));
+  int64_t* caps = (int64_t*)calloc((size_t)(n > 0 ? n : 1), sizeof(int64_t));
+  int64_t* sizes = (int64_t*)calloc((size_t)(n > 0 ? n : 1), sizeof(int64_t));
+  int ok = outs && caps && sizes;
+  for (int64_t i = 0; ok && i < n; i++) {
+    outs[i] = malloc((size_t)(bound > 0 ? bound : 1));
+    caps[i] = bound;
+    ok = outs[i] != NULL;
+  }
+  jobjectArray res = NULL;
+  if (!ok) {
+    throw_status(env, ZH_ENOMEM, "out of host memory for the encoded chunks");
+  } else {
+    /* copy the region out of the heap: the call stages it to the device (no long critical
+     * section around device work) */
+    jsize nel = (*env)->GetArrayLength(env, (jarray)data);
+    const size_t rbytes = (size_t)nel * (size_t)m.dtype_size;
+    void* src = malloc(rbytes > 0 ? rbytes : 1);
+    void* pin = (*env)->GetPrimitiveArrayCritical(env, (jarray)data, NULL);
+    if (src && pin) memcpy(src, pin, rbytes);
+    if (pin) (*env)->ReleasePrimitiveArrayCritical(env, (jarray)data, pin, JNI_ABORT);
+    st = src ? zh_array_write_host((zh_ctx*)(intptr_t)ctx, &m, src, o64, r64, outs, caps, sizes,
+                                   n, err, sizeof err)
+             : ZH_ENOMEM;
+    free(src);
+    if (st == ZH_OK) {
+      jclass bcls = (*env)->FindClass(env, "[B");
+      res = bcls ? (*env)->NewObjectArray(env, (jsize)n, bcls, NULL) : NULL;
+      for (int64_t i = 0; res && i < n; i++) {
+        if (sizes[i] == 0) continue;  /* all fill: null → delete the key */
+        jbyteArray b = (*env)->NewByteArray(env, (jsize)sizes[i]);
+        if (!b) {
+          res = NULL;
+          break;
+        }
+        (*env)->SetByteArrayRegion(env, b, 0, (jsize)sizes[i], (const jbyte*)outs[i]);
+        (*env)->SetObjectArrayElement(env, res, (jsize)i, b);
+        (*env)->DeleteLocalRef(env, b);
+      }
+    } else if (st != ZH_EUNSUPPORTED) {
+      throw_status(env, st, err);
+    }
+  }
+  for (int64_t i = 0; outs && i < n; i++) free(outs[i]);
+  free(outs);
+  free(caps);
+  free(sizes);
+  return res;
+}

@@ -64,4 +64,45 @@ public class HipArray extends Array {
                         out.getStorage());
         return st == 0 ? out : super.read(offset, shape, parallel);
     }
+
+    /**
+     * core.Array.write (M/core/Array.java:83-133) + writeChunk (:143-156) in one device call
+     * when the region covers whole chunks (clipped only by the array boundary): every chunk is
+     * encoded on the device (ShardingIndexedCodec.encode incl. the all-fill elision) and then
+     * stored, or deleted when it is all fill_value.  Regions that cut chunks need the
+     * read-modify-write of core.Array.write and take {@code super.write}.
+     */
+    @Override
+    public void write(long[] offset, ucar.ma2.Array array, boolean parallel) {
+        ArrayMetadata md = metadata();
+        if (chain == null || offset.length != md.ndim() || array.getRank() != md.ndim()) {
+            super.write(offset, array, parallel);
+            return;
+        }
+        long[] shape = Utils.toLongArray(array.getShape());
+        int[] cs = md.chunkShape();
+        for (int d = 0; d < md.ndim(); d++) {
+            long end = offset[d] + shape[d];
+            if (offset[d] % cs[d] != 0 || (end % cs[d] != 0 && end != md.shape[d])) {
+                super.write(offset, array, parallel);
+                return;
+            }
+        }
+        byte[][] enc = ZarrHip.arrayWrite(ZarrHip.ctx(), chain.meta, chain.shape,
+                chain.chunkShape, chain.innerShape, chain.order, chain.fill, offset, shape,
+                array.copyTo1DJavaArray());
+        if (enc == null) {
+            super.write(offset, array, parallel);
+            return;
+        }
+        long[][] coords = IndexingUtils.computeChunkCoords(md.shape, cs, offset, shape);
+        for (int i = 0; i < coords.length; i++) {
+            StoreHandle h = storeHandle.resolve(md.chunkKeyEncoding().encodeChunkKey(coords[i]));
+            if (enc[i] == null) {
+                h.delete();
+            } else {
+                h.set(ByteBuffer.wrap(enc[i]));
+            }
+        }
+    }
 }

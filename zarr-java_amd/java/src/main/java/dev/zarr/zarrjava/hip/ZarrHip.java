@@ -72,6 +72,15 @@ public final class ZarrHip {
                                      int[] innerShape, int[] order, byte[] fill, byte[][] chunks,
                                      long[] offset, long[] regionShape, Object out);
 
+    /**
+     * core.Array.write of a region of whole chunks (clipped only by the array boundary):
+     * the encoded chunk objects in computeChunkCoords order, null entries for chunks that are
+     * all fill_value (delete the key); null when the chain or region is not device-supported.
+     */
+    static native byte[][] arrayWrite(long ctx, int[] meta, long[] shape, int[] chunkShape,
+                                      int[] innerShape, int[] order, byte[] fill, long[] offset,
+                                      long[] regionShape, Object data);
+
     /** ShardingIndexedCodec.decodePartial over one shard's bytes. */
     static native int shardDecodePartial(long ctx, int[] meta, long[] shape, int[] chunkShape,
                                          int[] innerShape, int[] order, byte[] fill, byte[] shard,

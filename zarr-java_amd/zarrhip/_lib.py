@@ -56,6 +56,8 @@ _SIGS = {
     "zh_array_encoded_bound": (I64, [PMETA]),
     "zh_array_write": (C.c_int, [P, PMETA, P, PI64, PI64, C.POINTER(A.zh_chunk_dst), I64, P, CH,
                                  SZ]),
+    "zh_array_write_host": (C.c_int, [P, PMETA, P, PI64, PI64, C.POINTER(P), PI64, PI64, I64, CH,
+                                      SZ]),
     "zh_abi_sizes": (C.c_int, [C.POINTER(C.c_int64), C.c_int]),
     "zh_plan_staged_bytes": (C.c_int64, [P]),
     "zh_blosc_decompress": (C.c_int, [P, SZ, P, SZ, C.POINTER(SZ), C.c_char_p, SZ]),
@@ -272,6 +274,21 @@ class DeviceContext:
 
     def plan(self, meta, sources, offset, shape, flags):
         return Plan(self, meta, sources, offset, shape, flags)
+
+    def array_write_host(self, meta, data, offset, shape, nchunks):
+        """zh_array_write_host: region bytes (host) → list of encoded chunk bytes (None =
+        all fill, delete the key), staged through the device inside the call."""
+        bound = self.L.zh_array_encoded_bound(C.byref(meta))
+        bufs = [(C.c_char * max(1, bound))() for _ in range(nchunks)]
+        outs = (P * max(1, nchunks))(*[C.addressof(b) for b in bufs])
+        caps = (C.c_int64 * max(1, nchunks))(*([bound] * nchunks))
+        sizes = (C.c_int64 * max(1, nchunks))()
+        src = (C.c_char * max(1, len(data))).from_buffer_copy(data if len(data) else b"\0")
+        err = C.create_string_buffer(1024)
+        st = self.L.zh_array_write_host(self.h, C.byref(meta), src, i64arr(offset), i64arr(shape),
+                                        outs, caps, sizes, nchunks, err, 1024)
+        check(st, err)
+        return [bytes(b)[:sizes[i]] if sizes[i] else None for i, b in enumerate(bufs)]
 
     def array_write(self, meta, src, offset, shape, dsts, stream=None):
         """zh_array_write.  dsts: list of (device pointer, capacity) → list of nbytes."""
