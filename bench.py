@@ -71,7 +71,17 @@ class Dist:
         if ws > 1:
             import torch
             import torch.distributed as dist
-            dist.init_process_group("gloo")
+            # gloo prints its connection lines on stdout: keep stdout for the one JSON line
+            sys.stdout.flush()
+            saved = os.dup(1)
+            os.dup2(2, 1)
+            try:
+                dist.init_process_group("gloo")
+                dist.barrier()
+            finally:
+                sys.stdout.flush()
+                os.dup2(saved, 1)
+                os.close(saved)
             self.torch, self.dist = torch, dist
 
     def barrier(self):
