@@ -547,3 +547,26 @@ def test_array_write_host_buffers(dev, mode):
     want = encode_oracle(meta, arr)
     got = dev.array_write_host(meta, arr.tobytes(), [0, 0, 0], shape, len(want))
     assert got == want
+
+
+@pytest.mark.parametrize("case", [
+    dict(shape=[1000], chunk=[256], inner=[64], order=None),
+    dict(shape=[5, 6, 7, 8, 9], chunk=[4, 4, 4, 8, 8], inner=[2, 2, 4, 4, 8], order=[4, 0, 3, 1, 2]),
+    dict(shape=[3, 2, 5, 2, 3, 4, 2, 6], chunk=[2, 2, 4, 2, 2, 4, 2, 4],
+         inner=[1, 2, 2, 1, 2, 4, 1, 4], order=[7, 6, 5, 4, 3, 2, 1, 0]),
+    dict(shape=[3, 2, 5, 2, 3, 4, 2, 6], chunk=[2, 2, 4, 2, 2, 4, 2, 4],
+         inner=[1, 2, 2, 1, 2, 4, 1, 4], order=None),
+], ids=["1d", "5d_transpose", "8d_reverse", "8d"])
+@pytest.mark.parametrize("dsize", [1, 4])
+def test_rank_1_to_8(dev, case, dsize):
+    """Ranks 1, 5 and 8 (ZH_MAX_DIMS): sharded chains with and without transpose, whole and
+    unaligned regions decoded bit-exactly, and the device encode equal to the oracle's."""
+    shape, n = case["shape"], len(case["shape"])
+    meta = A.make_meta(shape, case["chunk"], dsize, endian=A.ZH_ENDIAN_BIG, sharded=True,
+                       inner_chunk_shape=case["inner"], transpose_order=case["order"])
+    arr = rand_array(shape, dsize, seed=81 + n)
+    arr[arr == 0] = 1
+    off = [min(1, s - 1) for s in shape]
+    shp = [s - o - (1 if s - o > 2 else 0) for s, o in zip(shape, off)]
+    roundtrip(dev, meta, arr, [([0] * n, shape), (off, shp)])
+    assert device_write(dev, meta, arr) == encode_oracle(meta, arr)
