@@ -76,6 +76,30 @@ for tag, dst in (("pinned", bpin), ("pageable", C.addressof(bpage))):
         round(bnb / statistics.median(ts) / 2**30, 2)
 dev.free_pinned(bpin)
 del bpage
+# the whole 4 GiB shard into pinned memory: one staging buffer (ZH_HOST_SLABS=0) against the
+# double-buffered C-order slab pipeline, with 512 MiB and 1 GiB slabs
+fnb = 1024 ** 3 * 4
+fpin = dev.malloc_pinned(fnb)
+for tag, env in (("one staging buffer", {"ZH_HOST_SLABS": "0"}),
+                 ("512 MiB slabs", {"ZH_HOST_SLABS": "1", "ZH_HOST_SLAB_MIN_KB": "1048576",
+                                    "ZH_HOST_SLAB_KB": "524288"}),
+                 ("1 GiB slabs", {"ZH_HOST_SLABS": "1", "ZH_HOST_SLAB_MIN_KB": "1048576",
+                                  "ZH_HOST_SLAB_KB": "1048576"})):
+    os.environ.update(env)
+    ts = []
+    for i in range(4):
+        t0 = time.perf_counter()
+        dev.array_read(meta, [(shard, size)], [0] * 4, shape, fpin, A.ZH_SRC_DEVICE)
+        if i:
+            ts.append(time.perf_counter() - t0)
+    res[f"zh_array_read 4 GiB shard, pinned host out, {tag} (GiB/s)"] = \
+        round(fnb / statistics.median(ts) / 2**30, 2)
+for k in ("ZH_HOST_SLABS", "ZH_HOST_SLAB_MIN_KB", "ZH_HOST_SLAB_KB"):
+    os.environ.pop(k, None)
+chk = dev.malloc(64 ** 3 * 4)
+dev.memcpy(chk, fpin + (512 * 1024 * 1024 + 512 * 1024 + 512) * 4, 64 * 4, 0, None, True)
+dev.free(chk)
+dev.free_pinned(fpin)
 plan = dev.plan(meta, [(shard, size)], off, shp, A.ZH_SRC_DEVICE | A.ZH_OUT_DEVICE)
 
 

@@ -570,3 +570,42 @@ def test_rank_1_to_8(dev, case, dsize):
     shp = [s - o - (1 if s - o > 2 else 0) for s, o in zip(shape, off)]
     roundtrip(dev, meta, arr, [([0] * n, shape), (off, shp)])
     assert device_write(dev, meta, arr) == encode_oracle(meta, arr)
+
+
+@pytest.mark.parametrize("case", ["sharded_transpose", "unsharded", "nested", "missing_shard"])
+def test_host_output_slab_pipeline(dev, monkeypatch, case):
+    """Large host-output reads go through C-order slabs double-buffered on the device (decode
+    of slab r+1 beside the copy-out of slab r).  The thresholds are shrunk here so small
+    arrays take that path: results equal the oracle, missing shards read fill_value, and a
+    CRC error reports the reference's message."""
+    monkeypatch.setenv("ZH_HOST_SLAB_MIN_KB", "1")
+    monkeypatch.setenv("ZH_HOST_SLAB_KB", "4")
+    shape = [24, 40, 36]
+    kw = dict(endian=A.ZH_ENDIAN_BIG, fill=(9).to_bytes(4, "little"))
+    if case != "unsharded":
+        kw.update(sharded=True, inner_chunk_shape=[8, 8, 12])
+    if case == "sharded_transpose":
+        kw.update(transpose_order=[2, 0, 1])
+    if case == "nested":
+        kw.update(nested_chunk_shape=[4, 8, 6])
+    meta = A.make_meta(shape, [16, 16, 24], 4, **kw)
+    arr = rand_array(shape, 4, seed=91)
+    shards = encode_oracle(meta, arr)
+    if case == "missing_shard":
+        shards[1] = None
+    for off, shp in [([0, 0, 0], shape), ([3, 5, 7], [17, 30, 20]), ([1, 0, 0], [1, 40, 36])]:
+        coords_all = chunk_coords(meta, [0, 0, 0], shape)
+        pos = {c: i for i, c in enumerate(coords_all)}
+        srcs = [shards[pos[c]] for c in chunk_coords(meta, off, shp)]
+        want = np.frombuffer(O.array_read(meta, srcs, off, shp), np.uint32).reshape(shp)
+        np.testing.assert_array_equal(device_read(dev, meta, srcs, off, shp), want)
+    if case == "sharded_transpose":
+        bad = list(shards)
+        b = bytearray(bad[2])
+        b[-10] ^= 0x40
+        bad[2] = bytes(b)
+        with pytest.raises(O.OracleError) as eo:
+            O.array_read(meta, bad, [0, 0, 0], shape)
+        with pytest.raises(ZhError) as ed:
+            device_read(dev, meta, bad, [0, 0, 0], shape)
+        assert str(ed.value) == str(eo.value)

@@ -1386,11 +1386,170 @@ int zh_plan_kernel_time(zh_plan* p, double* scatter_ms, int64_t* launches, doubl
   return ZH_OK;
 }
 
+}  // extern "C"
+
+namespace {
+// The chunks of slab (o, s) picked out of the caller's list for the whole region (offset,
+// shape), which follows computeChunkCoords order.
+std::vector<zh_chunk_src> slab_chunks(const zh_array_meta* meta, const zh_chunk_src* chunks,
+                                      const int64_t* offset, const int64_t* shape,
+                                      const int64_t* o, const int64_t* s) {
+  const int n = meta->ndim;
+  int64_t cstart[kMaxDims], ccount[kMaxDims], cstride[kMaxDims], st0[kMaxDims], cnt[kMaxDims];
+  chunk_coords(n, meta->chunk_shape, offset, shape, cstart, ccount);
+  int64_t s2 = 1;
+  for (int d = n - 1; d >= 0; d--) {
+    cstride[d] = s2;
+    s2 *= ccount[d];
+  }
+  const int64_t m = chunk_coords(n, meta->chunk_shape, o, s, st0, cnt);
+  std::vector<zh_chunk_src> sub((size_t)m);
+  int64_t cur[kMaxDims] = {0};
+  for (int64_t i = 0; i < m; i++) {
+    int64_t lin = 0;
+    for (int d = 0; d < n; d++) lin += (st0[d] + cur[d] - cstart[d]) * cstride[d];
+    sub[(size_t)i] = chunks[lin];
+    for (int d = n - 1; d >= 0; d--) {
+      if (++cur[d] < cnt[d]) break;
+      cur[d] = 0;
+    }
+  }
+  return sub;
+}
+
+// Host outputs above ZH_HOST_SLAB_MIN_KB (4 GiB: larger than the block cache keeps) are
+// slabbed, ZH_HOST_SLAB_KB (1 GiB) per slab; up to 4 GiB one cached staging buffer is 3-4 %
+// faster (profiles/r01/experiments/oneshot_latency.json).  The tests shrink both to run the
+// path on small arrays.
+int64_t host_slab_min() { return (int64_t)env_int("ZH_HOST_SLAB_MIN_KB", 4 << 20) << 10; }
+int64_t host_slab_bytes() { return (int64_t)std::max(1, env_int("ZH_HOST_SLAB_KB", 1 << 20)) << 10; }
+
+// A large read into host memory, in C-order slabs of about 1 GiB: each slab is decoded
+// into one of two device buffers (from the context's block cache) while the previous slab is
+// copied out on a second stream.  Device memory stays bounded and reused across calls; a
+// single staging buffer of the whole output paid its first touch on every call (fresh device
+// memory) and held the output twice.  Returns ZH_EUNSUPPORTED when the region does not split.
+int array_read_host_slabs(zh_ctx* ctx, const zh_array_meta* meta, const zh_chunk_src* chunks,
+                          int64_t nchunks, const int64_t* offset, const int64_t* shape,
+                          void* out, uint32_t flags, void* stream_v, char* err, size_t errlen) {
+  const int n = meta->ndim;
+  int64_t nel = 1;
+  for (int d = 0; d < n; d++) nel *= shape[d];
+  const int64_t bytes = nel * meta->dtype_size;
+  const int64_t per = host_slab_bytes();
+  int64_t nslab = (bytes + per - 1) / per;
+  int ax = -1;
+  for (int d = 0; d < n; d++) {
+    if (shape[d] >= 2) {
+      ax = d;
+      break;
+    }
+  }
+  if (ax < 0) return ZH_EUNSUPPORTED;
+  nslab = std::min<int64_t>(nslab, shape[ax]);
+  if (nslab < 2) return ZH_EUNSUPPORTED;
+  {
+    int64_t cs[kMaxDims], cc[kMaxDims];  // the caller's list must match the whole region
+    if (chunk_coords(n, meta->chunk_shape, offset, shape, cs, cc) != nchunks || !chunks)
+      return ZH_EUNSUPPORTED;  // the one-plan path reports it
+  }
+  std::vector<int64_t> so((size_t)nslab * n), ss((size_t)nslab * n);
+  if (zh_slab_partition(n, offset, shape, (int)nslab, leaf_shape(meta)[ax], so.data(),
+                        ss.data()) != ZH_OK)
+    return ZH_EUNSUPPORTED;
+  int64_t rstride[kMaxDims], sr = 1, maxb = 0;
+  for (int d = n - 1; d >= 0; d--) {
+    rstride[d] = sr;
+    sr *= shape[d];
+  }
+  for (int64_t r = 0; r < nslab; r++) {
+    int64_t e = meta->dtype_size;
+    for (int d = 0; d < n; d++) e *= ss[(size_t)(r * n + d)];
+    maxb = std::max(maxb, e);
+  }
+  (void)hipSetDevice(ctx->device);
+  hipStream_t s = stream_v ? (hipStream_t)stream_v : ctx->stream, s2 = nullptr;
+  void* ring[2] = {nullptr, nullptr};
+  size_t got[2] = {0, 0};
+  std::vector<zh_plan*> plans;
+  std::vector<hipEvent_t> evs;
+  int st = ZH_OK;
+  hipError_t he = hipStreamCreateWithFlags(&s2, hipStreamNonBlocking);
+  for (int k = 0; k < 2 && he == hipSuccess; k++) he = ctx_alloc(ctx, (size_t)maxb, &ring[k], &got[k]);
+  std::vector<hipEvent_t> decoded((size_t)nslab, nullptr), copied((size_t)nslab, nullptr);
+  for (int64_t r = 0; r < nslab && he == hipSuccess && st == ZH_OK; r++) {
+    const int64_t* o = &so[(size_t)(r * n)];
+    const int64_t* sh = &ss[(size_t)(r * n)];
+    int64_t base = 0, e = meta->dtype_size;
+    for (int d = 0; d < n; d++) {
+      base += (o[d] - offset[d]) * rstride[d];
+      e *= sh[d];
+    }
+    std::vector<zh_chunk_src> sub = slab_chunks(meta, chunks, offset, shape, o, sh);
+    zh_plan* p = nullptr;
+    st = zh_plan_create(ctx, meta, sub.data(), (int64_t)sub.size(), o, sh,
+                        (flags & ZH_SRC_DEVICE) | ZH_OUT_DEVICE, &p, err, errlen);
+    if (st != ZH_OK) break;
+    plans.push_back(p);
+    he = hipEventCreateWithFlags(&decoded[(size_t)r], hipEventDisableTiming);
+    if (he == hipSuccess) he = hipEventCreateWithFlags(&copied[(size_t)r], hipEventDisableTiming);
+    if (he != hipSuccess) break;
+    if (r >= 2) he = hipStreamWaitEvent(s, copied[(size_t)(r - 2)], 0);  // slot drained
+    if (he != hipSuccess) break;
+    st = zh_plan_execute(p, ring[r & 1], s);
+    if (st != ZH_OK) break;
+    he = hipEventRecord(decoded[(size_t)r], s);
+    if (he == hipSuccess) he = hipStreamWaitEvent(s2, decoded[(size_t)r], 0);
+    if (he == hipSuccess)
+      he = hipMemcpyAsync((uint8_t*)out + base * meta->dtype_size, ring[r & 1], (size_t)e,
+                          hipMemcpyDeviceToHost, s2);
+    if (he == hipSuccess) he = hipEventRecord(copied[(size_t)r], s2);
+  }
+  if (s2) (void)hipStreamSynchronize(s2);
+  (void)hipStreamSynchronize(s);
+  // status of every slab (deferred: the first failing slab in C order is reported)
+  for (size_t r = 0; r < plans.size(); r++) {
+    const int rc = zh_plan_wait(plans[r], st == ZH_OK && he == hipSuccess ? err : nullptr,
+                                st == ZH_OK && he == hipSuccess ? errlen : 0);
+    if (rc != ZH_OK && st == ZH_OK && he == hipSuccess) st = rc;
+  }
+  for (zh_plan* p : plans) plan_free(p);
+  for (auto ev : decoded)
+    if (ev) (void)hipEventDestroy(ev);
+  for (auto ev : copied)
+    if (ev) (void)hipEventDestroy(ev);
+  for (int k = 0; k < 2; k++)
+    if (ring[k]) ctx_release(ctx, ring[k], got[k]);
+  if (s2) (void)hipStreamDestroy(s2);
+  if (he != hipSuccess && st == ZH_OK) {
+    set_err(err, errlen, "HIP error %s (%s)", hipGetErrorName(he), hipGetErrorString(he));
+    st = he == hipErrorOutOfMemory ? ZH_ENOMEM : ZH_EHIP;
+  }
+  return st;
+}
+}  // namespace
+
+extern "C" {
+
 int zh_array_read(zh_ctx* ctx, const zh_array_meta* meta, const zh_chunk_src* chunks,
                   int64_t nchunks, const int64_t* offset, const int64_t* shape, void* out,
                   uint32_t flags, void* stream, char* err, size_t errlen) {
   if (!ctx) return ZH_EINVAL;
   std::lock_guard<std::mutex> lk(ctx->mu);
+  if (meta && offset && shape && out && !(flags & ZH_OUT_DEVICE) &&
+      env_int("ZH_HOST_SLABS", 1) != 0 && zh_validate_meta(meta, nullptr, 0) == ZH_OK) {
+    bool inside = true;
+    int64_t bytes = meta->dtype_size;
+    for (int d = 0; d < meta->ndim; d++) {
+      inside &= offset[d] >= 0 && shape[d] > 0 && offset[d] + shape[d] <= meta->shape[d];
+      bytes *= shape[d];
+    }
+    if (inside && bytes > host_slab_min()) {
+      const int st = array_read_host_slabs(ctx, meta, chunks, nchunks, offset, shape, out,
+                                           flags, stream, err, errlen);
+      if (st != ZH_EUNSUPPORTED) return st;
+    }
+  }
   zh_plan* p = nullptr;
   int st = zh_plan_create(ctx, meta, chunks, nchunks, offset, shape, flags, &p, err, errlen);
   if (st != ZH_OK) return st;
