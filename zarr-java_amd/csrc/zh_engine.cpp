@@ -262,6 +262,7 @@ struct zh_plan {
   std::vector<int64_t> coords;  // chunk coords (for messages)
   // device state
   std::vector<std::pair<void*, size_t>> blocks;  // context-cache blocks owned by the plan
+  hipEvent_t done_ev = nullptr;  // recorded after every execute (plan_free waits on it)
   uint8_t* d_tables = nullptr;   // one allocation holding the tables below
   DevShard* d_shards = nullptr;
   uint64_t* d_status = nullptr;
@@ -811,9 +812,9 @@ void plan_free(zh_plan* p) {
   if (!p) return;
   (void)hipSetDevice(p->ctx->device);
   // the blocks go back to the context's cache: the plan's last work on them must be done
-  if (!p->blocks.empty()) {
-    if (p->last_stream) (void)hipStreamSynchronize(p->last_stream);
-    if (p->graph_stream) (void)hipStreamSynchronize(p->graph_stream);
+  if (p->done_ev) {
+    (void)hipEventSynchronize(p->done_ev);
+    (void)hipEventDestroy(p->done_ev);
   }
   for (auto& b : p->blocks) ctx_release(p->ctx, b.first, b.second);
   for (auto& e : p->ev_pending)
@@ -1247,6 +1248,22 @@ static void plan_drop_graph(zh_plan* p) {
   p->graph_stream = nullptr;
 }
 
+}  // extern "C"
+
+namespace {
+// Records the end of the plan's latest execution: plan_free waits on this event before its
+// device blocks go back to the context's cache (an event outlives a caller's stream).
+int plan_mark_done(zh_plan* p, hipStream_t s) {
+  if (!p->done_ev && hipEventCreateWithFlags(&p->done_ev, hipEventDisableTiming) != hipSuccess) {
+    p->done_ev = nullptr;
+    return ZH_EHIP;
+  }
+  return hipEventRecord(p->done_ev, s) == hipSuccess ? ZH_OK : ZH_EHIP;
+}
+}  // namespace
+
+extern "C" {
+
 int zh_plan_execute(zh_plan* p, void* out, void* stream_v) {
   if (!p || !out) return ZH_EINVAL;
   char* err = nullptr;
@@ -1278,11 +1295,11 @@ int zh_plan_execute(zh_plan* p, void* out, void* stream_v) {
     }
     ZH_HIP(hipGraphLaunch(p->graph_exec, s));
     p->last_stream = s;
-    return ZH_OK;
+    return plan_mark_done(p, s);
   }
   const int st = plan_enqueue(p, out, s);
   if (st == ZH_OK) p->last_stream = s;
-  return st;
+  return st == ZH_OK ? plan_mark_done(p, s) : st;
 }
 
 int zh_plan_set_graph(zh_plan* p, int enable) {
