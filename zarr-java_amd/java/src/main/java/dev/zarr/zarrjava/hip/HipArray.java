@@ -42,10 +42,24 @@ public class HipArray extends Array {
                 throw new ZarrException("Requested data is outside of the array's domain.");
             }
         }
-        long[][] coords = IndexingUtils.computeChunkCoords(md.shape, md.chunkShape(), offset, shape);
+        int[] cs = md.chunkShape();
+        long[][] coords = IndexingUtils.computeChunkCoords(md.shape, cs, offset, shape);
         byte[][] chunks = new byte[coords.length][];
         for (int i = 0; i < coords.length; i++) {
             StoreHandle h = storeHandle.resolve(md.chunkKeyEncoding().encodeChunkKey(coords[i]));
+            if (chain.meta[3] == 1) {  // the part of this shard the region covers
+                long[] lo = new long[cs.length], hi = new long[cs.length];
+                for (int d = 0; d < cs.length; d++) {
+                    long c0 = coords[i][d] * cs[d];
+                    lo[d] = Math.max(offset[d], c0) - c0;
+                    hi[d] = Math.min(offset[d] + shape[d], c0 + cs[d]) - c0;
+                }
+                if (!ShardStaging.whole(chain, lo, hi)) {
+                    // sub-shard part: the index + the referenced inner chunks only
+                    chunks[i] = ShardStaging.compact(h, chain, lo, hi);
+                    continue;
+                }
+            }
             ByteBuffer b = h.read();
             if (b != null) {
                 chunks[i] = new byte[b.remaining()];

@@ -59,6 +59,17 @@ public class HipShardingIndexedCodec extends ShardingIndexedCodec {
     public Array decodePartial(StoreHandle chunkHandle, long[] offset, int[] shape)
             throws ZarrException {
         if (chain != null) {
+            long[] hi = new long[offset.length];
+            for (int d = 0; d < offset.length; d++) hi[d] = offset[d] + shape[d];
+            if (!ShardStaging.whole(chain, offset, hi)) {
+                // the index + the referenced inner chunks only (StoreHandleDataProvider)
+                byte[] compact = ShardStaging.compact(chunkHandle, chain, offset, hi);
+                if (compact != null) {
+                    Array a = device(compact, offset, shape);
+                    if (a != null) return a;
+                }
+                return super.decodePartial(chunkHandle, offset, shape);
+            }
             ByteBuffer bytes = chunkHandle.read();
             if (bytes == null) {
                 return Arrays.equals(shape, arrayMetadata.chunkShape)

@@ -1,0 +1,148 @@
+package dev.zarr.zarrjava.hip;
+
+import dev.zarr.zarrjava.ZarrException;
+import dev.zarr.zarrjava.store.StoreHandle;
+import dev.zarr.zarrjava.utils.CRC32C;
+
+import java.io.ByteArrayOutputStream;
+import java.nio.ByteBuffer;
+import java.nio.ByteOrder;
+import java.util.ArrayList;
+import java.util.Arrays;
+import java.util.List;
+
+/**
+ * Sub-shard reads with the reference's StoreHandleDataProvider semantics
+ * (M/v3/codec/core/ShardingIndexedCodec.java:333-357): one range read for the index (suffix
+ * or prefix), its crc32c verified here with the reference's message (Crc32cCodec.java:39-44),
+ * then range reads of only the inner chunks the part references, adjacent ranges coalesced.
+ * The result is a compact shard for the device: the referenced chunks only, under a fresh
+ * index (+ crc32c).  For a nested chain the "inner chunks" are the level-1 sub-shards, kept
+ * whole (their own indexes are relative to their start).  Java twin of
+ * zarrhip.Array._stage_partial (zarr-java_amd/zarrhip/array.py).
+ */
+final class ShardStaging {
+    private ShardStaging() {
+    }
+
+    private static byte[] bytes(ByteBuffer b) {
+        byte[] out = new byte[b.remaining()];
+        b.duplicate().get(out);
+        return out;
+    }
+
+    /**
+     * The compact shard for the part [partLo, partHi) (shard-local coordinates) of the shard
+     * at {@code h}, or null when the shard key is missing (the caller fills the part).
+     */
+    static byte[] compact(StoreHandle h, DeviceChain chain, long[] partLo, long[] partHi)
+            throws ZarrException {
+        final int n = chain.meta[0];
+        final boolean be = chain.meta[6] == 1, crc = chain.meta[7] == 1, start = chain.meta[8] == 1;
+        final int[] inner = Arrays.copyOf(chain.innerShape, n);
+        final int[] cps = new int[n];
+        int nIn = 1;
+        for (int d = 0; d < n; d++) {
+            cps[d] = chain.chunkShape[d] / inner[d];
+            nIn *= cps[d];
+        }
+        final long isz = 16L * nIn + (crc ? 4 : 0);
+        if (!h.exists()) return null;
+        ByteBuffer ib = start ? h.read(0, isz) : h.read(-isz);
+        if (ib == null) return null;
+        byte[] idx = bytes(ib);
+        if (idx.length < isz) {
+            throw new ZarrException("Shard " + h + " is smaller than its index (" + isz + " bytes).");
+        }
+        if (crc) {
+            CRC32C c = new CRC32C();
+            c.update(idx, 0, 16 * nIn);
+            int computed = (int) c.getValue();
+            int stored = ByteBuffer.wrap(idx, 16 * nIn, 4).order(ByteOrder.LITTLE_ENDIAN).getInt();
+            if (computed != stored) {
+                throw new ZarrException("The checksum of the sharding index is invalid. Stored: "
+                        + stored + " Computed: " + computed);
+            }
+        }
+        ByteBuffer entries = ByteBuffer.wrap(idx, 0, 16 * nIn)
+                .order(be ? ByteOrder.BIG_ENDIAN : ByteOrder.LITTLE_ENDIAN);
+        // inner chunks of the part, C order over their box
+        int[] b0 = new int[n], cnt = new int[n];
+        int total = 1;
+        for (int d = 0; d < n; d++) {
+            b0[d] = (int) (partLo[d] / inner[d]);
+            cnt[d] = (int) ((partHi[d] - 1) / inner[d]) - b0[d] + 1;
+            total *= cnt[d];
+        }
+        List<long[]> refs = new ArrayList<>();  // {offset, nbytes, linear index}
+        int[] cur = new int[n];
+        for (int k = 0; k < total; k++) {
+            int lin = 0;
+            for (int d = 0; d < n; d++) lin = lin * cps[d] + b0[d] + cur[d];
+            long off = entries.getLong(16 * lin), nb = entries.getLong(16 * lin + 8);
+            if (off != -1 && nb != -1) refs.add(new long[]{off, nb, lin});
+            for (int d = n - 1; d >= 0; d--) {
+                if (++cur[d] < cnt[d]) break;
+                cur[d] = 0;
+            }
+        }
+        refs.sort((x, y) -> Long.compare(x[0], y[0]));
+        byte[][] data = new byte[nIn][];
+        for (int i = 0; i < refs.size(); ) {  // coalesce adjacent ranges into one store read
+            int j = i;
+            while (j + 1 < refs.size() && refs.get(j + 1)[0] == refs.get(j)[0] + refs.get(j)[1]) j++;
+            long s0 = refs.get(i)[0], s1 = refs.get(j)[0] + refs.get(j)[1];
+            ByteBuffer blob = h.read(s0, s1);
+            if (blob == null || blob.remaining() < s1 - s0) {
+                throw new ZarrException("Could not load byte data for chunk range [" + s0 + ", "
+                        + s1 + ")");
+            }
+            byte[] bb = bytes(blob);
+            for (int k = i; k <= j; k++) {
+                long[] r = refs.get(k);
+                data[(int) r[2]] = Arrays.copyOfRange(bb, (int) (r[0] - s0), (int) (r[0] - s0 + r[1]));
+            }
+            i = j + 1;
+        }
+        ByteBuffer ni = ByteBuffer.allocate((int) isz)
+                .order(be ? ByteOrder.BIG_ENDIAN : ByteOrder.LITTLE_ENDIAN);
+        ByteArrayOutputStream payload = new ByteArrayOutputStream();
+        long pos = start ? isz : 0;
+        for (int lin = 0; lin < nIn; lin++) {
+            if (data[lin] == null) {
+                ni.putLong(16 * lin, -1L);
+                ni.putLong(16 * lin + 8, -1L);
+                continue;
+            }
+            ni.putLong(16 * lin, pos);
+            ni.putLong(16 * lin + 8, data[lin].length);
+            payload.write(data[lin], 0, data[lin].length);
+            pos += data[lin].length;
+        }
+        byte[] nib = ni.array();
+        if (crc) {
+            CRC32C c = new CRC32C();
+            c.update(nib, 0, 16 * nIn);
+            ByteBuffer.wrap(nib, 16 * nIn, 4).order(ByteOrder.LITTLE_ENDIAN)
+                    .putInt((int) c.getValue());
+        }
+        byte[] pb = payload.toByteArray();
+        byte[] out = new byte[nib.length + pb.length];
+        if (start) {
+            System.arraycopy(nib, 0, out, 0, nib.length);
+            System.arraycopy(pb, 0, out, nib.length, pb.length);
+        } else {
+            System.arraycopy(pb, 0, out, 0, pb.length);
+            System.arraycopy(nib, 0, out, pb.length, nib.length);
+        }
+        return out;
+    }
+
+    /** True when [partLo, partHi) is the whole shard. */
+    static boolean whole(DeviceChain chain, long[] partLo, long[] partHi) {
+        for (int d = 0; d < chain.meta[0]; d++) {
+            if (partLo[d] != 0 || partHi[d] != chain.chunkShape[d]) return false;
+        }
+        return true;
+    }
+}
