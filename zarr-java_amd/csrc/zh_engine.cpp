@@ -1186,7 +1186,7 @@ int zh_plan_create(zh_ctx* ctx, const zh_array_meta* m, const zh_chunk_src* chun
   p->grid = grid_for(ctx, p->args.total_items);
   // non-temporal loads + stores: +4 % on the row path, +1 % on the tile path (interleaved
   // A/B in one process, profiles/r01/experiments/tune_*.json)
-  p->args.nt = env_int("ZH_NT", 3) & 3;
+  p->args.nt = env_int("ZH_NT", 3) & 7;  // bit 2: 8 rows in flight per lane (rows)
   // Visit items in a golden-ratio stride order: +3.6 % on the tile path (c4) on every normal
   // allocation, neutral on the row path (interleaved A/B, profiles/placement_perm.py), so
   // on by default for tiles.  ZH_ITEM_PERM=0/1 overrides.

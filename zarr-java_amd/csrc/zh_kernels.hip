@@ -2113,6 +2113,9 @@ static void launch_scatter_ds(const ScatterArgs& a, int tile, int enc, int grid,
         case 0: hipLaunchKernelGGL((decode_rows_kernel<DS, 4, 0, true>), dim3(grid), dim3(kBlock), lds, s, a); break;
         default: hipLaunchKernelGGL((decode_rows_kernel<DS, 4, 3, true>), dim3(grid), dim3(kBlock), lds, s, a); break;
       }
+    } else if (a.fast_mode != kFastNone && (a.nt & 4) && nt == 3) {
+      // 8 rows in flight per lane (ZH_NT bit 2; A/B switch)
+      hipLaunchKernelGGL((decode_rows_kernel<DS, 8, 3>), dim3(grid), dim3(kBlock), lds, s, a);
     } else if (a.fast_mode != kFastNone) {
       switch (nt) {
         case 0: hipLaunchKernelGGL((decode_rows_kernel<DS, 4, 0>), dim3(grid), dim3(kBlock), lds, s, a); break;
