@@ -638,3 +638,30 @@ def test_device_encode_subregion_offset(dev, sharded):
         dev.free(b)
     dev.free(src)
     assert got == want
+
+
+@pytest.mark.parametrize("loc", [A.ZH_INDEX_END, A.ZH_INDEX_START])
+def test_truncated_shards_raise(dev, loc):
+    """Fault injection: a shard cut inside its index is rejected by both paths
+    (the reference's readSuffix would throw on the short buffer; no message to match); a
+    shard whose payload is cut leaves index entries past the end, which both report with
+    the reference's "Could not load byte data for chunk [..]"."""
+    shape = [16, 16]
+    meta = A.make_meta(shape, [16, 16], 4, sharded=True, inner_chunk_shape=[8, 8],
+                       index_location=loc)
+    arr = rand_array(shape, 4, seed=111)
+    good = encode_oracle(meta, arr)[0]
+    isz = 16 * 4 + 4
+    cut = good[:isz - 3] if loc == A.ZH_INDEX_START else good[-(isz - 3):]
+    with pytest.raises(O.OracleError):
+        O.array_read(meta, [cut], [0, 0], shape)
+    with pytest.raises(ZhError):
+        device_read(dev, meta, [cut], [0, 0], shape)
+    if loc == A.ZH_INDEX_END:
+        short = good[:100] + good[-isz:]          # payload cut: entries point past the end
+        with pytest.raises(O.OracleError) as eo:
+            O.array_read(meta, [short], [0, 0], shape)
+        with pytest.raises(ZhError) as ed:
+            device_read(dev, meta, [short], [0, 0], shape)
+        assert str(ed.value) == str(eo.value)
+        assert str(ed.value).startswith("Could not load byte data for chunk")
