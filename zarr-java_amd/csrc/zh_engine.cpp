@@ -1581,6 +1581,33 @@ int zh_array_read(zh_ctx* ctx, const zh_array_meta* meta, const zh_chunk_src* ch
   return st;
 }
 
+}  // extern "C"
+
+namespace {
+// Peer access from device `from` to device `to` (once per pair per process), so that the
+// slab copies to the root device go device to device over xGMI.  Same device, or a pair
+// without peer support: nothing to do (hipMemcpyPeerAsync still works, staged).
+void enable_peer(int from, int to) {
+  if (from == to) return;
+  static std::mutex mu;
+  static std::vector<std::pair<int, int>> done;
+  std::lock_guard<std::mutex> lk(mu);
+  for (auto& p : done)
+    if (p.first == from && p.second == to) return;
+  done.emplace_back(from, to);
+  int can = 0;
+  if (hipDeviceCanAccessPeer(&can, from, to) != hipSuccess || !can) return;
+  int cur = 0;
+  (void)hipGetDevice(&cur);
+  (void)hipSetDevice(from);
+  const hipError_t e = hipDeviceEnablePeerAccess(to, 0);
+  if (e == hipErrorPeerAccessAlreadyEnabled) (void)hipGetLastError();
+  (void)hipSetDevice(cur);
+}
+}  // namespace
+
+extern "C" {
+
 // Multi-GPU region read inside one process: contiguous C-order slabs, one
 // per device, decoded concurrently (one host thread per device, each on its context), then
 // delivered to the caller's host buffer (each device over its own PCIe link) or to the
@@ -1697,6 +1724,7 @@ int zh_array_read_multi(zh_ctx* const* ctxs, int ndev, int root, const zh_array_
     (void)hipSetDevice(ctx->device);
     const int rdev = ctxs[root]->device;
     const bool peer = out_dev && ctx != ctxs[root];
+    if (peer) enable_peer(ctx->device, rdev);  // xGMI copies straight into the root's buffer
     void* local = nullptr;
     if (peer && hipMalloc(&local, (size_t)(nel * meta->dtype_size)) != hipSuccess) {
       status[r] = ZH_ENOMEM;
