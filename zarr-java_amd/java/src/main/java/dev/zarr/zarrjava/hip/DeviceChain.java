@@ -1,6 +1,8 @@
 package dev.zarr.zarrjava.hip;
 
+import dev.zarr.zarrjava.ZarrException;
 import dev.zarr.zarrjava.core.ArrayMetadata.CoreArrayMetadata;
+import dev.zarr.zarrjava.core.codec.BytesBytesCodec;
 import dev.zarr.zarrjava.v3.codec.Codec;
 import dev.zarr.zarrjava.v3.codec.core.BytesCodec;
 import dev.zarr.zarrjava.v3.codec.core.Crc32cCodec;
@@ -25,6 +27,10 @@ final class DeviceChain {
     int[] innerShape;
     int[] order;
     final byte[] fill;
+    // byte-to-byte codecs after `bytes` that run on the host (zstd, gzip, blosc, and a crc32c
+    // that is not the only one), decoded per chunk before the bytes reach the device; null
+    // when the device takes the chunk bytes as stored
+    BytesBytesCodec[] innerHost;
 
     private DeviceChain(CoreArrayMetadata m) {
         shape = m.shape.clone();
@@ -63,11 +69,30 @@ final class DeviceChain {
         d.meta[5] = bc.configuration != null
                 && bc.configuration.endian == BytesCodec.Endian.BIG ? 1 : 0;
         i++;
-        if (i < codecs.length && codecs[i] instanceof Crc32cCodec) {  // verified on the device
+        if (i == codecs.length - 1 && codecs[i] instanceof Crc32cCodec) {  // verified on the device
             d.meta[13] = 1;
-            i++;
+            return true;
         }
-        return i == codecs.length;  // other byte-to-byte codecs stay on the Java path
+        if (i == codecs.length) return true;
+        // the host decompression hand-off (north star: blosc/gzip/zstd stay on the host): the
+        // remaining byte-to-byte codecs are undone per chunk with the reference's own codec
+        // objects, and the device gets the raw `bytes` payload
+        BytesBytesCodec[] host = new BytesBytesCodec[codecs.length - i];
+        for (int k = i; k < codecs.length; k++) {
+            if (!(codecs[k] instanceof BytesBytesCodec)) return false;
+            host[k - i] = (BytesBytesCodec) codecs[k];
+        }
+        d.innerHost = host;
+        return true;
+    }
+
+    /** The raw `bytes` payload of one stored chunk: the host stages decoded in reverse order. */
+    byte[] hostDecode(byte[] stored) throws ZarrException {
+        ByteBuffer b = ByteBuffer.wrap(stored);
+        for (int k = innerHost.length - 1; k >= 0; k--) b = innerHost[k].decode(b);
+        byte[] out = new byte[b.remaining()];
+        b.duplicate().get(out);
+        return out;
     }
 
     /** index_codecs [bytes, crc32c?] → {endian, crc}, or null. */
@@ -101,7 +126,7 @@ final class DeviceChain {
                 d.meta[10] = nix[0];
                 d.meta[11] = nix[1];
                 d.meta[12] = "start".equals(nc.indexLocation) ? 1 : 0;
-                if (!innerChain(d, nc.codecs)) return null;
+                if (!innerChain(d, nc.codecs) || d.innerHost != null) return null;
             } else if (!innerChain(d, c.codecs)) {
                 return null;
             }

@@ -64,6 +64,8 @@ public class HipArray extends Array {
             if (b != null) {
                 chunks[i] = new byte[b.remaining()];
                 b.duplicate().get(chunks[i]);
+                // unsharded chain with host stages (e.g. [bytes, zstd]): raw payload for the device
+                if (chain.innerHost != null) chunks[i] = chain.hostDecode(chunks[i]);
             }
         }
         ucar.ma2.Array out = ucar.ma2.Array.factory(md.dataType().getMA2DataType(),

@@ -46,7 +46,7 @@ public class HipShardingIndexedCodec extends ShardingIndexedCodec {
 
     @Override
     public Array decode(ByteBuffer shardBytes) throws ZarrException {
-        if (chain != null) {
+        if (chain != null && chain.innerHost == null) {  // host stages: decodePartial stages them
             byte[] b = new byte[shardBytes.remaining()];
             shardBytes.duplicate().get(b);
             Array a = device(b, new long[arrayMetadata.ndim()], arrayMetadata.chunkShape);

@@ -18,7 +18,9 @@ import java.util.List;
  * then range reads of only the inner chunks the part references, adjacent ranges coalesced.
  * The result is a compact shard for the device: the referenced chunks only, under a fresh
  * index (+ crc32c).  For a nested chain the "inner chunks" are the level-1 sub-shards, kept
- * whole (their own indexes are relative to their start).  Java twin of
+ * whole (their own indexes are relative to their start).  With host stages in the chain
+ * (DeviceChain.innerHost: zstd, gzip, blosc ...) every referenced chunk is decoded through
+ * them here, so the compact shard holds raw `bytes` payloads.  Java twin of
  * zarrhip.Array._stage_partial (zarr-java_amd/zarrhip/array.py).
  */
 final class ShardStaging {
@@ -100,7 +102,8 @@ final class ShardStaging {
             byte[] bb = bytes(blob);
             for (int k = i; k <= j; k++) {
                 long[] r = refs.get(k);
-                data[(int) r[2]] = Arrays.copyOfRange(bb, (int) (r[0] - s0), (int) (r[0] - s0 + r[1]));
+                byte[] raw = Arrays.copyOfRange(bb, (int) (r[0] - s0), (int) (r[0] - s0 + r[1]));
+                data[(int) r[2]] = chain.innerHost != null ? chain.hostDecode(raw) : raw;
             }
             i = j + 1;
         }
@@ -138,8 +141,12 @@ final class ShardStaging {
         return out;
     }
 
-    /** True when [partLo, partHi) is the whole shard. */
+    /**
+     * True when [partLo, partHi) is the whole shard and the stored bytes can go to the device
+     * as they are (no host stages to undo).
+     */
     static boolean whole(DeviceChain chain, long[] partLo, long[] partHi) {
+        if (chain.innerHost != null) return false;
         for (int d = 0; d < chain.meta[0]; d++) {
             if (partLo[d] != 0 || partHi[d] != chain.chunkShape[d]) return false;
         }
