@@ -9,7 +9,7 @@ cd "$R" || exit 1
 chk() { local rc=$1 name=$2; echo "$name rc=$rc"; if [ "$rc" -ne 0 ]; then tail -5 "$OUT/$name.err" 2>/dev/null; exit "$rc"; fi; }
 timeout -k 10 600 python3 -m pytest tests -m gpu -q > "$OUT/gpu_tests.log" 2>&1; rc=$?
 tail -2 "$OUT/gpu_tests.log"; chk $rc gpu_tests
-timeout -k 10 500 python3 bench.py --host-inclusive > "$OUT/bench_c3.json" 2> "$OUT/bench_c3.err"; chk $? bench_c3
+timeout -k 10 500 python3 bench.py --config c3 --host-inclusive > "$OUT/bench_c3.json" 2> "$OUT/bench_c3.err"; chk $? bench_c3
 timeout -k 10 300 python3 bench.py --config c4 --no-cpu-baseline > "$OUT/bench_c4.json" 2> "$OUT/bench_c4.err"; chk $? bench_c4
 timeout -k 10 300 python3 bench.py --config c2 --no-cpu-baseline > "$OUT/bench_c2.json" 2> "$OUT/bench_c2.err"; chk $? bench_c2
 timeout -k 10 300 python3 bench.py --mode strong --steps 5 > "$OUT/bench_strong1.json" 2> "$OUT/bench_strong1.err"; chk $? bench_strong1
