@@ -9,20 +9,33 @@ Workload (default c4 = BASELINE.json configs[3], the chain the metric names:
 c3 (configs[2], no transpose) and c2 (configs[1], unsharded bytes) are the other
 single-GPU configs.  One step = one full-array core.Array.read (M/core/Array.java:378-441)
 of all 32 shards / 786,432 in-bounds inner chunks: index CRC + index parse + byte swap
-(+ transpose) + scatter, inputs already resident in HBM.  Synthetic data v(g) = lo32(splitmix64(g ^ 0x5A5A2026)) is written
-on the device and encoded by the product's own write path (zh_array_write); after warmup
-the decoded array is verified element-by-element on the device against the generator.
+(+ transpose) + scatter, inputs already resident in HBM.  Synthetic data v(g) =
+lo32(splitmix64(g ^ 0x5A5A2026)) is written on the device and encoded by the product's own
+write path (zh_array_write); after warmup the decoded array is verified element-by-element
+on the device against the generator.
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--config c4|c3|c2|c3crc|c4crc|c3nest]
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--config c4|c3|c2|...]
 
-N>1 (launched by torch.distributed.run): every rank decodes its own full-size array on its
-own GPU (weak scaling, no data-path collective: shards are independent objects); the
-barrier and max-over-ranks timing use torch.distributed (gloo, CPU tensors).
+N=1 prints the headline line (weak scaling of one full array per GPU, which at N=1 is the
+single-GPU number), plus `extra_configs` (c3, c2 and c4 little-endian timed in the same
+process), a one-shot `zh_array_read` time and the CPU baseline.
+
+N>1 (BASELINE.json configs[4]): ONE full array partitioned across the GPUs in
+contiguous y-slabs (512 rows at N=8, aligned to inner chunks), strong scaling.  Each rank
+holds the shards its slab touches, decodes its slab (value = decode-only aggregate GiB/s =
+array bytes / max-over-ranks time), then the root assembles the whole region over RCCL
+(grouped send/recv into one buffer on the root, re-verified there: `gather`), and every rank
+copies its slab into its slice of one host region buffer (`host_terminated`).  Launched by
+torch.distributed.run (one process per GPU), or, when WORLD_SIZE is unset, bench.py launches
+the N ranks itself before anything touches the GPU.  --mode weak keeps the older
+one-array-per-GPU run.
 """
 import argparse
 import ctypes as C
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -32,12 +45,15 @@ sys.path.insert(0, os.path.join(ROOT, "zarr-java_amd"))
 SEED = 0x5A5A2026
 GiB = 1 << 30
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+METRIC = "GiB/s device-resident chunk decode (sharding+bytes+transpose), uint32 1024³"
 
 CONFIGS = {
     # name: (description, sharded, transpose order[, extra make_meta keywords])
     "c2": ("bytes(big) only, chunk 1x1024x1024x1024", False, None),
     "c3": ("sharding 1x32x32x32 + bytes(big), index [bytes(little), crc32c] at end", True, None),
     "c4": ("c3 + transpose [0,3,2,1] inside the shard", True, [0, 3, 2, 1]),
+    "c4le": ("c4 with bytes(little) inner codec (the endian-neutral copy, §8(d))", True,
+             [0, 3, 2, 1], dict(little=True)),
     # §8(f) rank-2 workloads (not the headline): same array and shards
     "c3crc": ("c3 with inner codecs [bytes(big), crc32c] (per-chunk checksum verified)", True,
               None, dict(inner_crc32c=True)),
@@ -58,6 +74,23 @@ def dist_env():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     return ws, rank, local
+
+
+def self_launch(nproc):
+    """`--gpus N` without a launcher: start N ranks under torch.distributed.run as CHILD
+    processes (this process has touched neither torch nor HIP, and it is not replaced by an
+    exec) and return their exit status.  Rank 0's stdout is the one JSON line."""
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={nproc}", "--master-addr", "127.0.0.1", "--master-port", str(port),
+           os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("OMP_NUM_THREADS", "1")
+    log(f"[launcher] {nproc} ranks: {' '.join(cmd[1:6])} ...")
+    return subprocess.call(cmd, env=env)
 
 
 class Dist:
@@ -107,8 +140,9 @@ def build_meta(A, cfg, ydiv=1):
     if extra.pop("nested", False):
         inner = [1, 256, 256, 256]
         extra["nested_chunk_shape"] = [1, 32, 32, 32]
+    endian = A.ZH_ENDIAN_LITTLE if extra.pop("little", False) else A.ZH_ENDIAN_BIG
     return A.make_meta([1, 4096 // ydiv, 4096, 1536], [1, 1024, 1024, 1024], 4,
-                       endian=A.ZH_ENDIAN_BIG, sharded=sharded, **extra,
+                       endian=endian, sharded=sharded, **extra,
                        inner_chunk_shape=inner if sharded else None,
                        transpose_order=order, index_endian=A.ZH_ENDIAN_LITTLE,
                        index_crc32c=True, index_location=A.ZH_INDEX_END)
@@ -122,6 +156,7 @@ def chunk_capacities(meta, coords):
     sharded = ch.sharded
     l1 = [ch.inner_chunk_shape[d] if sharded else meta.chunk_shape[d] for d in range(n)]
     leaf = [ch.nested_chunk_shape[d] for d in range(n)] if ch.nested else l1
+
     def prod(v):
         r = 1
         for x in v:
@@ -146,6 +181,28 @@ def chunk_capacities(meta, coords):
     return caps
 
 
+def all_coords(L, meta, off=None, shp=None):
+    n = meta.ndim
+    shape = [meta.shape[d] for d in range(n)]
+    off = [0] * n if off is None else off
+    shp = shape if shp is None else shp
+    cs = (C.c_int32 * 8)(*[meta.chunk_shape[d] for d in range(n)])
+    num = L.zh_compute_chunk_coords(n, (C.c_int64 * 8)(*shape), cs, (C.c_int64 * 8)(*off),
+                                    (C.c_int64 * 8)(*shp), None, 0)
+    buf = (C.c_int64 * (num * n))()
+    L.zh_compute_chunk_coords(n, (C.c_int64 * 8)(*shape), cs, (C.c_int64 * 8)(*off),
+                              (C.c_int64 * 8)(*shp), buf, num)
+    return [tuple(buf[i * n + d] for d in range(n)) for i in range(num)]
+
+
+def slab_layout(caps):
+    offs, tot = [], 0
+    for cap in caps:
+        offs.append(tot)
+        tot += (cap + 255) // 256 * 256
+    return offs, tot
+
+
 def pmc_traffic(config):
     """HBM bytes per launch of the scatter kernel from the newest committed PMC summary for
     this config (profiles/rNN/<config>_summary.json, made by profiles/pmc_summary.py from
@@ -158,6 +215,27 @@ def pmc_traffic(config):
     return int(d["pmc"]["traffic_bytes_per_launch"]), os.path.relpath(cands[-1], ROOT)
 
 
+def kernel_name(meta):
+    return "decode_tiles_kernel" if meta.chain.has_transpose else "decode_rows_kernel<4,4>"
+
+
+def roofline_of(plan, st, config=None):
+    kt = plan.kernel_time()
+    scatter_ms = kt["scatter_ms"] / max(1, kt["launches"])
+    index_ms = kt["index_ms"] / max(1, kt["launches"])
+    alg = st["in_bytes"] + st["out_bytes"]
+    achieved = alg / (scatter_ms / 1000.0) / 1e9
+    traffic, src = pmc_traffic(config) if config else (None, None)
+    return {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+            "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+            "traffic_source": src, "kernel": kernel_name(plan._meta),
+            "kernel_ms": round(scatter_ms, 3), "index_kernels_ms": round(index_ms, 4),
+            "alg_bytes_per_launch": alg}
+
+
+# ------------------------------------------------------------------------------------------
+# host-inclusive readChunk pipeline
+# ------------------------------------------------------------------------------------------
 def host_inclusive(dev, A, meta, coords, offs, sizes, shard_slab, n_shards=4, reps=2, slabs=8,
                    nslots=3):
     """Host-resident bytes in, host-resident decoded array out: the readChunk /
@@ -263,62 +341,164 @@ def host_inclusive(dev, A, meta, coords, offs, sizes, shard_slab, n_shards=4, re
     return res
 
 
-def cpu_baseline(dev, A, meta, shard_ptr, shard_nbytes, budget_s=12.0):
-    """The C oracle (restated reference path, oracle/zh_oracle.c) on this host's cores over a
-    bounded sample of the same workload: region reads [1,1024,1024,64] inside shard (0,0,0,0)
-    (copied D2H), repeated until ~budget_s of CPU work."""
+# ------------------------------------------------------------------------------------------
+# CPU baseline
+# ------------------------------------------------------------------------------------------
+def host_cpu_info():
+    """Threads this process may use (affinity ∩ cgroup CPU quota), nproc and the CPU model."""
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except AttributeError:
+        aff = os.cpu_count() or 1
+    quota = None
+    for path in ("/sys/fs/cgroup/cpu.max",):
+        try:
+            q, per = open(path).read().split()[:2]
+            if q != "max":
+                quota = max(1, -(-int(q) // int(per)))
+        except (OSError, ValueError):
+            pass
+    model = None
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    usable = min(aff, quota) if quota else aff
+    return {"threads": usable, "nproc": os.cpu_count(), "affinity": aff, "cgroup_quota": quota,
+            "omp_num_threads": os.environ.get("OMP_NUM_THREADS"), "cpu_model": model}
+
+
+def _store_dir(need_bytes):
+    for d in ("/dev/shm", os.environ.get("TMPDIR", "/tmp")):
+        try:
+            v = os.statvfs(d)
+            if v.f_bavail * v.f_frsize >= need_bytes + (2 << 30):
+                return d
+        except OSError:
+            pass
+    return None
+
+
+def cpu_baseline(dev, A, L, meta, shard_ptr, shard_nbytes, budget_s=12.0):
+    """The C oracle (the restated reference path, oracle/zh_oracle.c) on this host's cores,
+    over BASELINE.md §3's workload: Array.read of [1,1024,1024,512] regions (2 GiB out each),
+    each inside one shard, from a FilesystemStore on tmpfs, so each goes through the partial
+    path — suffix read of the index, then one open + range read + close per inner chunk
+    (StoreHandleDataProvider, ShardingIndexedCodec.java:253,333-357) — and the part array's
+    second copy into the output (M/core/Array.java:422-426).  All usable threads, then one;
+    plus the c2 "scaled chunk" proxy (1 GiB bytes(big) chunks, 2 per region).  k is sized to
+    the budget.  The reference Java is not timed: there is no JDK on the box."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O
+    info = host_cpu_info()
+    threads = info["threads"]
+    n = meta.ndim
+    region = [1, 1024, 1024, 512]
+    rbytes = 4 * 1024 * 1024 * 512
+    d = _store_dir(shard_nbytes + 2 * GiB)
+    if d is None:
+        return {"value": None, "unit": "GiB/s", "cores": threads, "kind": "port",
+                "sample": "skipped: no tmpfs room for a 4 GiB shard file", **info}
+    base = os.path.join(d, f"zh_cpu_store_{os.getpid()}")
+    os.makedirs(os.path.join(base, "c", "0", "0", "0"), exist_ok=True)
+    shard_path = os.path.join(base, "c", "0", "0", "0", "0")
+    pin = dev.malloc_pinned(shard_nbytes)
+    dev.memcpy(pin, shard_ptr, shard_nbytes, 1, None, True)
+    with open(shard_path, "wb") as f:   # the store file, written from the device encode
+        f.write((C.c_char * shard_nbytes).from_address(pin))
+    out = dev.malloc_pinned(rbytes)
+    chk = dev.malloc(rbytes)
+    res = {"unit": "GiB/s", "kind": "port", "cores": threads, **info,
+           "reference_java": "not timed (no JDK on the box)"}
     try:
-        cores = min(16, len(os.sched_getaffinity(0)))
-    except AttributeError:
-        cores = min(16, os.cpu_count() or 1)
-    host = (C.c_char * shard_nbytes)()
-    dev.memcpy(C.addressof(host), shard_ptr, shard_nbytes, 1, None, True)
-    srcs = (A.zh_chunk_src * 1)()
-    srcs[0].data = C.addressof(host)
-    srcs[0].nbytes = shard_nbytes
-    shape = [1, 1024, 1024, 64]
-    nbytes_out = 1024 * 1024 * 64 * 4
-    out = (C.c_char * nbytes_out)()
-    total_bytes, total_t, reps = 0, 0.0, 0
-    z = 0
-    while total_t < budget_s and reps < 64:
-        off = [0, 0, 0, z]
-        t0 = time.perf_counter()
-        O.array_read_into(meta, srcs, 1, off, shape, C.addressof(out), nthreads=cores)
-        total_t += time.perf_counter() - t0
-        total_bytes += nbytes_out
-        reps += 1
-        z = (z + 64) % 1024
-    # the same oracle on ONE core (BASELINE.md §3 asks for 1 thread and all cores), over
-    # smaller [1,256,256,64] reads (16 MiB each) for about a sixth of the budget
-    small = [1, 256, 256, 64]
-    b1, t1, r1 = 0, 0.0, 0
-    while t1 < budget_s / 6 and r1 < 64:
-        off = [0, 256 * (r1 % 4), 256 * ((r1 // 4) % 4), 64 * (r1 % 16)]
-        t0 = time.perf_counter()
-        O.array_read_into(meta, srcs, 1, off, small, C.addressof(out), nthreads=1)
-        t1 += time.perf_counter() - t0
-        b1 += 256 * 256 * 64 * 4
-        r1 += 1
-    return {"value": round(total_bytes / total_t / GiB, 4), "unit": "GiB/s",
-            "cores": cores, "kind": "port",
-            "single_core": {"value": round(b1 / t1 / GiB, 4), "unit": "GiB/s", "cores": 1,
-                            "sample": f"{r1} x Array.read [1,256,256,64] (16 MiB each), "
-                                      f"{t1:.1f} s"},
-            "sample": f"{reps} x Array.read [1,1024,1024,64] (256 MiB each) from one "
-                      f"device-encoded shard, C oracle (oracle/zh_oracle.c, OpenMP over inner "
-                      f"chunks), {total_t:.1f} s"}
+        def timed(paths_meta, paths, off, shp, nthreads, budget, max_reps):
+            t, reps = 0.0, 0
+            while reps < max_reps and (reps == 0 or t < budget):
+                o = list(off(reps))
+                t0 = time.perf_counter()
+                O.array_read_store(paths_meta, paths, o, shp, out_addr=out, nthreads=nthreads)
+                t += time.perf_counter() - t0
+                reps += 1
+            return t, reps
+
+        zoff = lambda r: [0, 0, 0, 512 * (r % 2)]   # noqa: E731  z ∈ {0, 512} inside shard 0
+        # first read checked element-by-element against the generator (on the device)
+        O.array_read_store(meta, [shard_path], [0] * n, region, out_addr=out, nthreads=threads)
+        dev.memcpy(chk, out, rbytes, 0, None, True)
+        bad = dev.synth_verify(chk, [meta.shape[d] for d in range(n)], [0] * n, region, 4, SEED)
+        if bad:
+            raise SystemExit(f"cpu baseline read differs from the generator: {bad}")
+        t, r = timed(meta, [shard_path], zoff, region, threads, budget_s * 0.6, 48)
+        res["value"] = round(r * rbytes / t / GiB, 4)
+        res["sample"] = (f"{r} x Array.read [1,1024,1024,512] (2 GiB out each) from a "
+                         f"FilesystemStore shard file on {d} through the partial path "
+                         f"(C oracle, OpenMP over inner chunks, {threads} threads), {t:.1f} s; "
+                         f"first read verified vs the generator")
+        t1, r1 = timed(meta, [shard_path], zoff, region, 1, budget_s * 0.2, 48)
+        res["single_core"] = {"value": round(r1 * rbytes / t1 / GiB, 4), "unit": "GiB/s",
+                              "cores": 1, "sample": f"{r1} x the same read, 1 thread, {t1:.1f} s"}
+    finally:
+        os.unlink(shard_path)
+    # c2 "scaled chunk" proxy (BASELINE.md §2): bytes(big) chunks [1,1024,1024,256] (1 GiB
+    # objects); the region spans 2 chunks, so the fill + copyRegion scatter path runs
+    pm = A.make_meta([1, 1024, 1024, 512], [1, 1024, 1024, 256], 4, endian=A.ZH_ENDIAN_BIG)
+    src = dev.malloc(rbytes)
+    dev.synth_fill(src, rbytes // 4, 4, 0, SEED)
+    cb = [dev.malloc(rbytes // 2) for _ in range(2)]
+    sizes = dev.array_write(pm, src, [0] * 4, region, [(b, rbytes // 2) for b in cb])
+    paths = []
+    for i, (b, sz) in enumerate(zip(cb, sizes)):
+        p = os.path.join(base, f"c2_{i}")
+        dev.memcpy(pin, b, sz, 1, None, True)
+        with open(p, "wb") as f:
+            f.write((C.c_char * sz).from_address(pin))
+        paths.append(p)
+    try:
+        t2, r2 = timed(pm, paths, lambda r: [0] * 4, region, threads, budget_s * 0.2, 48)
+        dev.memcpy(chk, out, rbytes, 0, None, True)
+        bad = dev.synth_verify(chk, region, [0] * 4, region, 4, SEED)
+        res["c2_scaled_chunk"] = {
+            "value": round(r2 * rbytes / t2 / GiB, 4), "unit": "GiB/s", "cores": threads,
+            "verify_mismatches": int(bad),
+            "sample": f"{r2} x Array.read [1,1024,1024,512] of a bytes(big) array with "
+                      f"[1,1024,1024,256] chunks (1 GiB files, 2 per read: fill + scatter), "
+                      f"{t2:.1f} s"}
+    finally:
+        for p in paths:
+            os.unlink(p)
+        import shutil
+        shutil.rmtree(base, ignore_errors=True)
+        for b in cb + [src, chk]:
+            dev.free(b)
+        dev.free_pinned(out)
+        dev.free_pinned(pin)
+    return res
+
+
+# ------------------------------------------------------------------------------------------
+# N > 1: one array split over the GPUs (strong scaling, SURVEY §8e)
+# ------------------------------------------------------------------------------------------
+def _mem_available():
+    try:
+        for line in open("/proc/meminfo"):
+            if line.startswith("MemAvailable:"):
+                return int(line.split()[1]) * 1024
+    except OSError:
+        pass
+    return 0
 
 
 def host_terminated(args, dist, dev, plan, out, out_bytes, shape, so, ss, rank, ws):
-    """Host-terminated multi-GPU read (no gather): each rank decodes its slab and
-    copies it D2H into ITS slice of one host buffer that holds the whole region (POSIX shared
-    memory mapped by every rank; the slabs are contiguous in C order), so N GPUs drive N PCIe
-    links at once.  Each rank page-locks only its own slice (zh_host_register).  Falls back
-    to a private pinned slab per rank when /dev/shm cannot hold the region.  Timed: barrier,
-    K x (decode + D2H) on the plan's stream, sync, max over ranks; D2H alone timed likewise."""
+    """Host-terminated read (no gather): each rank decodes its slab and copies it
+    D2H into ITS slice of one host buffer that holds the whole region (POSIX shared memory
+    mapped by every rank; the slabs are contiguous in C order), so N GPUs drive N PCIe links
+    at once.  Each rank page-locks only its own slice (zh_host_register).  When the host
+    cannot hold the region (tmpfs or MemAvailable short by the region + 32 GiB), each rank
+    streams its slab through a private 2 GiB pinned ring instead (same links, nothing kept),
+    and says so.  Timed: barrier, reps x (decode + D2H), sync, max over ranks."""
     import mmap
     from zarrhip.parallel import slab_byte_offset
     full = 4
@@ -328,11 +508,14 @@ def host_terminated(args, dist, dev, plan, out, out_bytes, shape, so, ss, rank, 
     name = f"/dev/shm/zh_region_{os.environ.get('MASTER_PORT', 'solo')}_{os.getuid()}"
     try:
         vfs = os.statvfs("/dev/shm")
-        shared = vfs.f_bavail * vfs.f_frsize >= full + (1 << 30)
+        room = vfs.f_bavail * vfs.f_frsize >= full + (1 << 30)
     except OSError:
-        shared = False
+        room = False
+    shared = int(dist.max(0 if (room and _mem_available() >= full + (32 << 30)) else 1)) == 0
+    reps = max(1, min(args.steps, 3))
     mm = cbuf = None
     reg = 0
+    ring = 2 << 30
     if shared:
         if rank == 0:
             fd = os.open(name, os.O_RDWR | os.O_CREAT | os.O_TRUNC, 0o600)
@@ -348,33 +531,39 @@ def host_terminated(args, dist, dev, plan, out, out_bytes, shape, so, ss, rank, 
         reg = dst & ~4095
         dev.host_register(reg, ((dst + out_bytes + 4095) & ~4095) - reg)
         kind = "one region buffer in /dev/shm shared by the ranks; each pins its slice"
+
+        def copy_out():
+            dev.memcpy(dst, out, out_bytes, 1, None, False)
     else:
-        dst = dev.malloc_pinned(out_bytes)
-        kind = "private pinned slab per rank (/dev/shm too small for the region)"
-    for _ in range(max(1, args.warmup)):
-        plan.execute(out)
-        dev.memcpy(dst, out, out_bytes, 1, None, False)
+        dst = dev.malloc_pinned(min(ring, out_bytes))
+        kind = "bounded: each rank streams its slab through a private 2 GiB pinned ring"
+
+        def copy_out():
+            for o in range(0, out_bytes, ring):
+                dev.memcpy(dst, out + o, min(ring, out_bytes - o), 1, None, False)
+    plan.execute(out)
+    copy_out()
     plan.wait()
-    dist.barrier()
     dev.sync()
+    dist.barrier()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    for _ in range(reps):
         plan.execute(out)
-        dev.memcpy(dst, out, out_bytes, 1, None, False)
+        copy_out()
     plan.wait()
     dev.sync()
     t = dist.max(time.perf_counter() - t0)
     dist.barrier()
     t1 = time.perf_counter()
-    for _ in range(args.steps):
-        dev.memcpy(dst, out, out_bytes, 1, None, False)
+    for _ in range(reps):
+        copy_out()
     dev.sync()
     t_copy = dist.max(time.perf_counter() - t1)
-    # the host slice must hold this rank's slab of the generator's array
-    dev.memset(out, 0, out_bytes)
-    dev.memcpy(out, dst, out_bytes, 0, None, True)
-    bad = dist.max(dev.synth_verify(out, shape, so, ss, 4, SEED))
-    if shared:
+    bad = 0
+    if shared:  # the host slice must hold this rank's slab of the generator's array
+        dev.memset(out, 0, out_bytes)
+        dev.memcpy(out, dst, out_bytes, 0, None, True)
+        bad = dist.max(dev.synth_verify(out, shape, so, ss, 4, SEED))
         dev.host_unregister(reg)
         del cbuf
         mm.close()
@@ -385,68 +574,88 @@ def host_terminated(args, dist, dev, plan, out, out_bytes, shape, so, ss, rank, 
         dev.free_pinned(dst)
     if bad:
         raise SystemExit(f"[rank {rank}] host-terminated slab verification FAILED: {bad}")
-    return {"buffer": kind, "ms_per_step": round(t * 1e3 / args.steps, 3),
-            "value": round(full * args.steps / t / GiB, 2), "unit": "GiB/s",
-            "d2h_only_ms_per_step": round(t_copy * 1e3 / args.steps, 3),
-            "d2h_GBps_per_rank": round(out_bytes * args.steps / t_copy / 1e9, 2),
-            "region_bytes": full, "verify_mismatches": int(bad)}
+    return {"buffer": kind, "reps": reps, "ms_per_step": round(t * 1e3 / reps, 3),
+            "value": round(full * reps / t / GiB, 2), "unit": "GiB/s",
+            "d2h_only_ms_per_step": round(t_copy * 1e3 / reps, 3),
+            "d2h_GBps_per_rank": round(out_bytes * reps / t_copy / 1e9, 2),
+            "region_bytes": full, "verified": shared}
 
 
-def run_strong(args, dist, dev, A, L, meta, rank, ws, local):
+def visible_devices():
+    """GPUs this rank can see (torch.cuda.device_count does not initialise HIP here)."""
+    import torch
+    return torch.cuda.device_count()
+
+
+def run_strong(args, dist, A, meta, rank, ws, local):
     """Strong scaling: ONE full array split into per-rank y-slabs (512 rows at
-    N=8, aligned to inner chunks); each rank holds only the shards its slab touches
-    (encoded on its own GPU), decodes its slab, and optionally gathers the assembled region
-    to rank 0 (RCCL over xGMI via torch.distributed 'nccl', or 'gloo' through the host)."""
-    import ctypes as C
-    sys.path.insert(0, os.path.join(ROOT, "zarr-java_amd"))
-    from zarrhip.parallel import slab_partition
-    from zarrhip._lib import i32arr, i64arr
+    N=8, aligned to inner chunks); each rank holds only the shards its slab touches (encoded
+    on its own GPU), decodes its slab, the root assembles the region over RCCL, and every
+    rank copies its slab to its slice of one host buffer."""
+    import torch
+    from zarrhip._lib import DeviceContext, lib
+    from zarrhip.parallel import slab_byte_offset, slab_partition
+    L = lib()
+    ndev = visible_devices()
+    device = local % max(1, ndev)
+    backend = args.gather_backend
+    shared_gpu = ndev < ws
+    if backend == "nccl" and shared_gpu:
+        backend = "gloo"   # rehearsal with several ranks on one GPU: RCCL needs distinct GPUs
+    if backend == "nccl":
+        torch.cuda.set_device(device)
+    dev = DeviceContext(device)
+    info = dev.info()
     n = meta.ndim
     shape = [meta.shape[d] for d in range(n)]
     cs = [meta.chunk_shape[d] for d in range(n)]
     inner_y = meta.chain.inner_chunk_shape[1] if meta.chain.sharded else 1
-    so, ss = slab_partition([0] * n, shape, ws, align=inner_y)[rank]
+    parts = slab_partition([0] * n, shape, ws, align=inner_y)
+    so, ss = parts[rank]
     lo = [(so[d] // cs[d]) * cs[d] for d in range(n)]
     hi = [min(-(-(so[d] + ss[d]) // cs[d]) * cs[d], shape[d]) for d in range(n)]
     ext = [h - l for l, h in zip(lo, hi)]
     for d in range(2, n):
         assert lo[d] == 0 and ext[d] == shape[d]
-
-    def coords_of(off, shp):
-        num = L.zh_compute_chunk_coords(n, i64arr(shape), i32arr(cs), i64arr(off), i64arr(shp),
-                                        None, 0)
-        buf = (C.c_int64 * (num * n))()
-        L.zh_compute_chunk_coords(n, i64arr(shape), i32arr(cs), i64arr(off), i64arr(shp), buf, num)
-        return [tuple(buf[i * n + d] for d in range(n)) for i in range(num)]
-    cover = coords_of(lo, ext)
+    cover = all_coords(L, meta, lo, ext)
     caps = chunk_capacities(meta, cover)
     nel_cover = 1
     for e in ext:
         nel_cover *= e
     first = lo[1] * shape[2] * shape[3] if n == 4 else 0
+    t0 = time.perf_counter()
     src = dev.malloc(nel_cover * 4)
     dev.synth_fill(src, nel_cover, 4, first, SEED)
-    offs, tot = [], 0
-    for c in caps:
-        offs.append(tot)
-        tot += (c + 255) // 256 * 256
+    offs, tot = slab_layout(caps)
     slab_buf = dev.malloc(tot)
     sizes = dev.array_write(meta, src, lo, ext, [(slab_buf + o, c) for o, c in zip(offs, caps)])
     dev.free(src)
+    log(f"[rank {rank}/{ws}] device {device} of {ndev} ({info['arch']}): slab y "
+        f"[{so[1]}, {so[1] + ss[1]}), {len(cover)} shards encoded in "
+        f"{time.perf_counter() - t0:.2f}s")
     where = {c: (slab_buf + o, s) for c, o, s in zip(cover, offs, sizes)}
-    mine = coords_of(so, ss)
+    mine = all_coords(L, meta, so, ss)
     nel = 1
     for s in ss:
         nel *= s
     out_bytes = nel * 4
-    backend = args.gather_backend if ws > 1 else None
+    full_bytes = 4
+    for s in shape:
+        full_bytes *= s
+    # the root decodes straight into its slice of the assembled region buffer
+    region_t = out_t = None
     if backend == "nccl":
-        import torch
-        out_t = torch.empty(out_bytes, dtype=torch.uint8, device=f"cuda:{local}")
+        if rank == 0:
+            region_t = torch.empty(full_bytes, dtype=torch.uint8, device=f"cuda:{device}")
+            base = slab_byte_offset(shape, so, 4)
+            out_t = region_t[base:base + out_bytes]
+        else:
+            out_t = torch.empty(out_bytes, dtype=torch.uint8, device=f"cuda:{device}")
         out = out_t.data_ptr()
     else:
         out = dev.malloc(out_bytes)
     plan = dev.plan(meta, [where[c] for c in mine], so, ss, A.ZH_SRC_DEVICE | A.ZH_OUT_DEVICE)
+    st = plan.stats()
     for _ in range(max(1, args.warmup)):
         plan.execute(out)
     plan.wait()
@@ -460,60 +669,126 @@ def run_strong(args, dist, dev, A, L, meta, rank, ws, local):
     for _ in range(args.steps):
         plan.execute(out)
     plan.wait()
-    t_dec = dist.max(time.perf_counter() - t0)
-    kt = plan.kernel_time()
-    host_out = None
-    if args.host_out:
-        host_out = host_terminated(args, dist, dev, plan, out, out_bytes, shape, so, ss, rank, ws)
+    dev.sync()
+    t_rank = time.perf_counter() - t0
+    t_dec = dist.max(t_rank)
+    dist.barrier()
+    roof = roofline_of(plan, st)
+    kern_max = dist.max(roof["kernel_ms"])
     gather = None
-    if backend is not None:
-        import torch
-        import torch.distributed as tdist
-        grp = tdist.new_group(backend=backend)
-        if backend == "nccl":
-            send = out_t
-            recv = [torch.empty_like(out_t) for _ in range(ws)] if rank == 0 else None
-        else:
-            host = (C.c_char * out_bytes)()
-            dev.memcpy(C.addressof(host), out, out_bytes, 1, None, True)
-            send = torch.frombuffer(host, dtype=torch.uint8)
-            recv = [torch.empty(out_bytes, dtype=torch.uint8) for _ in range(ws)] if rank == 0 \
-                else None
-        dist.barrier()
-        t1 = time.perf_counter()
-        tdist.gather(send, recv, dst=0, group=grp)
-        if backend == "nccl":
-            torch.cuda.synchronize(local)
-        t_g = dist.max(time.perf_counter() - t1)
-        if rank == 0 and backend == "nccl":  # every gathered slab must be the generator's
-            tot_bad = 0
-            parts = slab_partition([0] * n, shape, ws, align=inner_y)
-            for r in range(ws):
-                tot_bad += dev.synth_verify(recv[r].data_ptr(), shape, parts[r][0], parts[r][1],
-                                            4, SEED)
-            if tot_bad:
-                raise SystemExit(f"gathered region verification FAILED: {tot_bad}")
-        full = 1
-        for s in shape:
-            full *= s
-        gather = {"backend": backend, "gather_ms": round(t_g * 1e3, 3),
-                  "value_incl_one_decode": round(full * 4 / (t_dec / args.steps + t_g) / GiB, 2),
-                  "unit": "GiB/s"}
-    full = 1
-    for s in shape:
-        full *= s
-    res = {"mode": "strong", "slab_offset": so, "slab_shape": ss,
+    if backend in ("nccl", "gloo"):
+        gather = gather_to_root(args, dist, dev, backend, out, out_t, region_t, out_bytes,
+                                full_bytes, parts, shape, rank, ws, device, t_dec)
+    host_out = None
+    if not args.no_host_out:
+        host_out = host_terminated(args, dist, dev, plan, out, out_bytes, shape, so, ss, rank,
+                                   ws)
+    res = {"slab_offset": so, "slab_shape": ss, "device": device, "shared_gpu": shared_gpu,
            "decode_ms_per_step": round(t_dec * 1e3 / args.steps, 3),
-           "value": round(full * 4 * args.steps / t_dec / GiB, 2),
-           "scatter_ms": round(kt["scatter_ms"] / max(1, kt["launches"]), 3), "gather": gather,
-           "host_out": host_out}
+           "rank_ms_per_step": round(t_rank * 1e3 / args.steps, 3),
+           "value": round(full_bytes * args.steps / t_dec / GiB, 2), "roofline": roof,
+           "kernel_ms_max_over_ranks": round(kern_max, 3), "gather": gather,
+           "host_terminated": host_out, "info": info}
     plan.close()
     if backend != "nccl":
         dev.free(out)
+    del out_t, region_t
     dev.free(slab_buf)
     return res
 
 
+def gather_to_root(args, dist, dev, backend, out, out_t, region_t, out_bytes, full_bytes, parts,
+                   shape, rank, ws, device, t_dec):
+    """Assemble the region on rank 0: RCCL grouped point-to-point (each rank's slab is one
+    contiguous C-order slice, sent straight into its place in the root's region buffer;
+    the root's own slab was decoded in place), then the root re-verifies every element of
+    the assembled region against the generator.  gloo (ranks sharing one GPU, rehearsal):
+    through host tensors, verified per slab."""
+    import torch
+    import torch.distributed as tdist
+    from zarrhip.parallel import slab_byte_offset
+    sizes = [4 * int(__import__("numpy").prod(s)) for _, s in parts]
+    if backend == "nccl":
+        grp = tdist.new_group(backend="nccl")
+        world = tdist.get_world_size(grp)
+
+        def once():
+            ops = []
+            if rank == 0:
+                for r in range(1, ws):
+                    b = slab_byte_offset(shape, parts[r][0], 4)
+                    ops.append(tdist.P2POp(tdist.irecv, region_t[b:b + sizes[r]], r, grp))
+            else:
+                ops.append(tdist.P2POp(tdist.isend, out_t, 0, grp))
+            for w in tdist.batch_isend_irecv(ops):
+                w.wait()
+            torch.cuda.synchronize(device)
+        once()                      # warm the communicator and the P2P channels
+        reps = max(1, min(args.steps, 3))
+        dist.barrier()
+        t1 = time.perf_counter()
+        for _ in range(reps):
+            once()
+        t_g = dist.max(time.perf_counter() - t1) / reps
+        bad = 0
+        if rank == 0:
+            bad = dev.synth_verify(region_t.data_ptr(), shape, [0] * len(shape), shape, 4, SEED)
+        bad = int(dist.max(bad))
+        if bad:
+            raise SystemExit(f"gathered region verification FAILED: {bad}")
+        how = "RCCL grouped send/recv into the root's region buffer (xGMI)"
+    else:
+        world = ws
+        host = (C.c_char * out_bytes)()
+        dev.memcpy(C.addressof(host), out, out_bytes, 1, None, True)
+        send = torch.frombuffer(host, dtype=torch.uint8)
+        mx = max(sizes)
+        if out_bytes < mx:
+            send = torch.cat([send, torch.zeros(mx - out_bytes, dtype=torch.uint8)])
+        recv = [torch.empty(mx, dtype=torch.uint8) for _ in range(ws)] if rank == 0 else None
+        dist.barrier()
+        t1 = time.perf_counter()
+        tdist.gather(send, recv, dst=0)
+        t_g = dist.max(time.perf_counter() - t1)
+        bad = 0
+        if rank == 0:
+            chk = dev.malloc(mx)
+            for r in range(ws):
+                dev.memcpy(chk, recv[r].data_ptr(), sizes[r], 0, None, True)
+                bad += dev.synth_verify(chk, shape, parts[r][0], parts[r][1], 4, SEED)
+            dev.free(chk)
+        bad = int(dist.max(bad))
+        if bad:
+            raise SystemExit(f"gathered region verification FAILED: {bad}")
+        how = "gloo gather through host memory (ranks share one GPU: rehearsal only)"
+    return {"backend": backend, "how": how, "world_size": world,
+            "gather_ms": round(t_g * 1e3, 3),
+            "root_ingress_GBps": round((full_bytes - sizes[0]) / t_g / 1e9, 1),
+            "value_incl_gather": round(full_bytes / (t_dec / args.steps + t_g) / GiB, 2),
+            "unit": "GiB/s", "root_verified_elements": full_bytes // 4}
+
+
+def dry_run(args, dist, rank, ws):
+    """--dry-run: the N>1 harness without a GPU (launch, process group, slab partition,
+    barrier, max over ranks, one JSON line); no decode runs, so there is no value."""
+    from zarrhip.parallel import slab_partition
+    shape = [1, 4096, 4096, 1536]
+    so, ss = slab_partition([0] * 4, shape, ws, align=32)[rank]
+    dist.barrier()
+    rows = int(dist.max(ss[1]))
+    if rank == 0:
+        print(json.dumps({"metric": METRIC, "value": None, "unit": "GiB/s", "n_gpus": ws,
+                          "steps": args.steps, "warmup": args.warmup, "ms_per_step": None,
+                          "higher_is_better": True, "scaling": "strong", "vs_baseline": None,
+                          "dtype": "u32", "data": "synthetic", "dry_run": True,
+                          "config": {"workload": "dry run (no GPU): harness only",
+                                     "slab_rows_max": rows,
+                                     "parallelism": f"slab-parallel x{ws}"}}), flush=True)
+
+
+# ------------------------------------------------------------------------------------------
+# write path (SURVEY §8(f) rank 1)
+# ------------------------------------------------------------------------------------------
 def run_write(args, dist, dev, A, meta, shape, region, out_bytes, shard_slab, offs, caps, rank,
               ws):
     """Write path: zh_array_write of the full array = core.Array.write
@@ -585,6 +860,88 @@ def run_write(args, dist, dev, A, meta, shape, region, out_bytes, shard_slab, of
                          "alg_bytes_per_launch": in_bytes + out_bytes}}), flush=True)
 
 
+# ------------------------------------------------------------------------------------------
+# N = 1 extras: other configs, one-shot read
+# ------------------------------------------------------------------------------------------
+def time_steps(dev, plan, out, steps):
+    """Per-step wall times (execute + wait each) → (min, median) ms."""
+    ts = []
+    for _ in range(steps):
+        t0 = time.perf_counter()
+        plan.execute(out)
+        plan.wait()
+        ts.append((time.perf_counter() - t0) * 1e3)
+    ts.sort()
+    return ts[0], ts[len(ts) // 2]
+
+
+def extra_config(dev, A, L, cfg, out, shape, steps, slab=None):
+    """Re-encode the resident decoded array (= the generator's values) with config `cfg`,
+    decode it `steps` times, verify every element, and report its rate and roofline.
+    Reuses `slab` when it holds the encoded size; returns (result, slab, slab_bytes)."""
+    meta = build_meta(A, cfg)
+    n = meta.ndim
+    coords = all_coords(L, meta)
+    caps = chunk_capacities(meta, coords)
+    offs, tot = slab_layout(caps)
+    buf, cap = slab if slab else (None, 0)
+    if cap < tot:
+        if buf:
+            dev.free(buf)
+        buf, cap = dev.malloc(tot), tot
+    sizes = dev.array_write(meta, out, [0] * n, shape, [(buf + o, c) for o, c in zip(offs, caps)])
+    plan = dev.plan(meta, [(buf + o, s) for o, s in zip(offs, sizes)], [0] * n, shape,
+                    A.ZH_SRC_DEVICE | A.ZH_OUT_DEVICE)
+    st = plan.stats()
+    dev.memset(out, 0, st["out_bytes"])
+    for _ in range(2):
+        plan.execute(out)
+    plan.wait()
+    bad = dev.synth_verify(out, shape, [0] * n, shape, 4, SEED)
+    if bad:
+        raise SystemExit(f"{cfg} decode verification FAILED: {bad}")
+    plan.set_timing(True)
+    dev.sync()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        plan.execute(out)
+    plan.wait()
+    el = time.perf_counter() - t0
+    roof = roofline_of(plan, st, cfg)
+    plan.set_timing(False)
+    mn, med = time_steps(dev, plan, out, 5)
+    plan.close()
+    res = {"description": CONFIGS[cfg][0], "value": round(steps * st["out_bytes"] / el / GiB, 2),
+           "unit": "GiB/s", "ms_per_step": round(el * 1e3 / steps, 3), "steps": steps,
+           "step_ms_min": round(mn, 3), "step_ms_median": round(med, 3),
+           "allocations_sampled": {"output": 1, "input_slab": 1},
+           "verified_elements": st["out_bytes"] // 4, "roofline": roof}
+    return res, (buf, cap)
+
+
+def oneshot_read(dev, A, meta, sources, shape, out, reps=3):
+    """zh_array_read of the whole array, device in and out: plan + tables upload + execute +
+    status read-back + teardown in one call, as core.Array.read does every call."""
+    n = meta.ndim
+    ts = []
+    for _ in range(reps):
+        dev.sync()
+        t0 = time.perf_counter()
+        dev.array_read(meta, sources, [0] * n, shape, out, A.ZH_SRC_DEVICE | A.ZH_OUT_DEVICE)
+        ts.append(time.perf_counter() - t0)
+    bad = dev.synth_verify(out, shape, [0] * n, shape, 4, SEED)
+    if bad:
+        raise SystemExit(f"one-shot read verification FAILED: {bad}")
+    nb = 4
+    for s in shape:
+        nb *= s
+    ts.sort()
+    return {"ms_min": round(ts[0] * 1e3, 3), "ms_median": round(ts[len(ts) // 2] * 1e3, 3),
+            "value": round(nb / ts[len(ts) // 2] / GiB, 2), "unit": "GiB/s", "reps": reps,
+            "call": "zh_array_read (plan + execute + wait + teardown), device in/out"}
+
+
+# ------------------------------------------------------------------------------------------
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -592,6 +949,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="c4", choices=sorted(CONFIGS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-extras", action="store_true",
+                    help="N=1: skip extra_configs (c3, c2, c4le) and the one-shot read")
     ap.add_argument("--op", default="read", choices=["read", "write"],
                     help="read: the decode path (the metric); write: zh_array_write, the "
                          "encode path (SURVEY §8(f) rank 1)")
@@ -599,63 +958,69 @@ def main():
                     help="--op write: elide 1/128 of the inner chunks (all fill_value), so the "
                          "write takes its second pass")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
-    ap.add_argument("--mode", default="weak", choices=["weak", "strong"],
-                    help="weak: one full array per GPU (the metric); strong: one array split "
-                         "into per-GPU slabs, plus a gather to rank 0")
+    ap.add_argument("--mode", default=None, choices=["weak", "strong"],
+                    help="default: weak at N=1 (one full array), strong at N>1 (one array "
+                         "split into per-GPU slabs + gather + host-terminated copy)")
     ap.add_argument("--gather-backend", default="nccl", choices=["nccl", "gloo", "none"])
-    ap.add_argument("--host-out", action="store_true",
-                    help="strong mode: also time decode + D2H of each slab into its slice of "
-                         "one host buffer (the host-terminated read, no gather)")
+    ap.add_argument("--no-host-out", action="store_true",
+                    help="strong mode: skip the host-terminated copy")
     ap.add_argument("--ydiv", type=int, default=1,
                     help="rehearsal only: divide the array's y extent (not a bench config)")
     ap.add_argument("--host-inclusive", action="store_true",
                     help="also measure pinned H2D + decode + D2H (adds 'host_inclusive')")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="N>1 harness without a GPU (launch, partition, barrier, JSON line)")
     args = ap.parse_args()
 
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(self_launch(args.gpus))
     ws, rank, local = dist_env()
-    if args.gpus != ws and ws > 1:
-        log(f"warning: --gpus {args.gpus} but WORLD_SIZE {ws}")
-    dist = Dist(ws, need_torch=args.mode == "strong")
+    if args.gpus != ws:
+        log(f"warning: --gpus {args.gpus} but WORLD_SIZE {ws}: measuring {ws} rank(s)")
+    mode = args.mode or ("strong" if ws > 1 else "weak")
+    if args.gather_backend == "none":
+        args.gather_backend = None
+    dist = Dist(ws, need_torch=mode == "strong")
+    if args.dry_run:
+        dry_run(args, dist, rank, ws)
+        dist.close()
+        return
 
     from zarrhip import _abi as A
-    from zarrhip._lib import DeviceContext, lib
-
-    dev = DeviceContext(int(os.environ.get("ZH_DEVICE", local)))
-    info = dev.info()
     meta = build_meta(A, args.config, args.ydiv)
-    if args.mode == "strong":
-        if args.gather_backend == "none":
-            args.gather_backend = None
-        res = run_strong(args, dist, dev, A, lib(), meta, rank, ws, local)
-        log(f"[rank {rank}] strong: {res}")
+    if mode == "strong":
+        res = run_strong(args, dist, A, meta, rank, ws, local)
+        log(f"[rank {rank}] strong: {json.dumps(res)}")
         if rank == 0:
             n = meta.ndim
+            g = res["gather"]
             print(json.dumps({
-                "metric": "GiB/s device-resident chunk decode (sharding+bytes+transpose), "
-                          "uint32 1024³ — strong scaling (one array split over GPUs)",
-                "value": res["value"], "unit": "GiB/s", "n_gpus": ws, "steps": args.steps,
+                "metric": METRIC, "value": res["value"], "unit": "GiB/s",
+                "n_gpus": g["world_size"] if g else ws, "steps": args.steps,
                 "warmup": args.warmup, "ms_per_step": res["decode_ms_per_step"],
                 "higher_is_better": True, "scaling": "strong", "vs_baseline": None,
                 "dtype": "u32", "data": "synthetic",
-                "config": {"workload": f"{args.config}: Array.read of "
+                "config": {"workload": f"{args.config}: one Array.read of the full "
                                        f"{'x'.join(str(meta.shape[d]) for d in range(n))} "
-                                       f"uint32 split into {ws} y-slabs",
-                           "parallelism": f"slab-parallel x{ws}"},
-                "strong": res}), flush=True)
+                                       f"uint32 array ({CONFIGS[args.config][0]}) split into "
+                                       f"{ws} contiguous y-slabs of {res['slab_shape'][1]} rows, "
+                                       f"one per GPU; value = decode-only aggregate",
+                           "parallelism": f"slab-parallel x{ws}",
+                           "ranks_share_one_gpu": res["shared_gpu"]},
+                "roofline": res["roofline"],
+                "kernel_ms_max_over_ranks": res["kernel_ms_max_over_ranks"],
+                "gather": g, "host_terminated": res["host_terminated"],
+                "cpu_baseline": None}), flush=True)
         dist.close()
         return
+
+    from zarrhip._lib import DeviceContext, lib
+    dev = DeviceContext(int(os.environ.get("ZH_DEVICE", local)))
+    info = dev.info()
     n = meta.ndim
     shape = [meta.shape[d] for d in range(n)]
     L = lib()
-    ncoords = L.zh_compute_chunk_coords(n, (C.c_int64 * 8)(*shape),
-                                        (C.c_int32 * 8)(*[meta.chunk_shape[d] for d in range(n)]),
-                                        (C.c_int64 * 8)(*([0] * n)), (C.c_int64 * 8)(*shape),
-                                        None, 0)
-    cbuf = (C.c_int64 * (ncoords * n))()
-    L.zh_compute_chunk_coords(n, (C.c_int64 * 8)(*shape),
-                              (C.c_int32 * 8)(*[meta.chunk_shape[d] for d in range(n)]),
-                              (C.c_int64 * 8)(*([0] * n)), (C.c_int64 * 8)(*shape), cbuf, ncoords)
-    coords = [tuple(cbuf[i * n + d] for d in range(n)) for i in range(ncoords)]
+    coords = all_coords(L, meta)
     caps = chunk_capacities(meta, coords)
     nel = 1
     for s in shape:
@@ -665,10 +1030,7 @@ def main():
     # device buffers: decoded region (also the encode source) + one slab for all shards
     t0 = time.perf_counter()
     out = dev.malloc(out_bytes)
-    offs, tot = [], 0
-    for cap in caps:
-        offs.append(tot)
-        tot += (cap + 255) // 256 * 256
+    offs, tot = slab_layout(caps)
     shard_slab = dev.malloc(tot)
     dev.synth_fill(out, nel, 4, 0, SEED)
     dev.sync()
@@ -689,8 +1051,8 @@ def main():
         dist.close()
         return
     flags = A.ZH_SRC_DEVICE | A.ZH_OUT_DEVICE
-    plan = dev.plan(meta, [(shard_slab + o, s) for o, s in zip(offs, sizes)], [0] * n, shape,
-                    flags)
+    sources = [(shard_slab + o, s) for o, s in zip(offs, sizes)]
+    plan = dev.plan(meta, sources, [0] * n, shape, flags)
     st = plan.stats()
     dev.memset(out, 0, out_bytes)
     for _ in range(max(1, args.warmup)):
@@ -711,32 +1073,21 @@ def main():
     t_end = time.perf_counter()
     dist.barrier()
     elapsed = dist.max(t_end - t_start)
-    kt = plan.kernel_time()
-    scatter_ms = kt["scatter_ms"] / max(1, kt["launches"])
-    index_ms = kt["index_ms"] / max(1, kt["launches"])
-
     ms_per_step = elapsed * 1000.0 / args.steps
     value = ws * args.steps * out_bytes / elapsed / GiB
-    traffic_alg = st["in_bytes"] + st["out_bytes"]
-    achieved = traffic_alg / (scatter_ms / 1000.0) / 1e9
-    traffic, traffic_src = pmc_traffic(args.config) if args.ydiv == 1 else (None, None)
-    roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
-                "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                "traffic_source": traffic_src,
-                "kernel": ("decode_tiles_kernel" if meta.chain.has_transpose
-                           else "decode_rows_kernel<4,4>"),
-                "kernel_ms": round(scatter_ms, 3), "index_kernels_ms": round(index_ms, 4),
-                "alg_bytes_per_launch": traffic_alg}
+    roofline = roofline_of(plan, st, args.config if args.ydiv == 1 else None)
+    plan.set_timing(False)
     hinc = None
     if args.host_inclusive and meta.chain.sharded:
         hinc = host_inclusive(dev, A, meta, coords, offs, sizes, shard_slab)
         log(f"[rank {rank}] host-inclusive: {hinc}")
     cpu = None
     if rank == 0 and ws == 1 and not args.no_cpu_baseline and meta.chain.sharded:
-        cpu = cpu_baseline(dev, A, meta, shard_slab + offs[0], sizes[0], args.cpu_budget)
+        cpu = cpu_baseline(dev, A, L, meta, shard_slab + offs[0], sizes[0], args.cpu_budget)
+        log(f"[rank {rank}] cpu baseline: {json.dumps(cpu)}")
 
     line = {
-        "metric": "GiB/s device-resident chunk decode (sharding+bytes+transpose), uint32 1024³",
+        "metric": METRIC,
         "value": round(value, 2), "unit": "GiB/s", "n_gpus": ws, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3), "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "u32", "data": "synthetic",
@@ -751,7 +1102,20 @@ def main():
     }
     if hinc is not None:
         line["host_inclusive"] = hinc
-    plan.close()
+    if not args.no_extras and ws == 1 and args.ydiv == 1 and args.config == "c4":
+        line["oneshot_read"] = oneshot_read(dev, A, meta, sources, shape, out)
+        plan.close()
+        plan = None
+        extras = {}
+        slab = (shard_slab, tot)
+        for cfg in ("c4le", "c3", "c2"):
+            extras[cfg], slab = extra_config(dev, A, L, cfg, out, shape, min(args.steps, 10),
+                                             slab)
+            log(f"[rank {rank}] {cfg}: {json.dumps(extras[cfg])}")
+        shard_slab = slab[0]
+        line["extra_configs"] = extras
+    if plan is not None:
+        plan.close()
     dev.free(shard_slab)
     dev.free(out)
     if rank == 0:

@@ -212,7 +212,8 @@ int zh_array_read(zh_ctx* ctx, const zh_array_meta* meta, const zh_chunk_src* ch
  *                        `out` with zh_host_register for the full rate);
  *     ZH_OUT_DEVICE    : `out` is a buffer on ctxs[root]'s device; the other devices decode
  *                        into their own HBM and copy their slab to the root's slice over
- *                        xGMI (hipMemcpyPeerAsync).
+ *                        xGMI (hipMemcpyPeerAsync), or through pinned host memory when the
+ *                        pair has no peer access (see zh_array_read_multi_routed).
  *   Errors: the first failing slab in C order, with zh_array_read's messages.
  * zh_slab_partition writes nslabs rows of ndim int64 offsets / shapes (ZH_EINVAL when the
  * region cannot be split into nslabs contiguous slabs).
@@ -221,8 +222,34 @@ int zh_array_read_multi(zh_ctx* const* ctxs, int ndev, int root, const zh_array_
                         const zh_chunk_src* chunks, int64_t nchunks, const int64_t* offset,
                         const int64_t* shape, void* out, uint32_t flags, char* err,
                         size_t errlen);
+/*
+ * zh_array_read_multi with a per-slab route report (slab_route: ndev int32, may be NULL):
+ *   output  ZH_ROUTE_DIRECT  decoded straight into its destination (root slab / host slice)
+ *           ZH_ROUTE_PEER    device-to-device copy to the root over xGMI (peer access on)
+ *           ZH_ROUTE_STAGED  no peer access: D2H into pinned host memory, then H2D on a fresh
+ *                            stream of the root device
+ *           ZH_ROUTE_SAME    two contexts on one device: a device-local copy
+ *   sources (ZH_SRC_DEVICE chunks on another device than the slab's), OR-ed in:
+ *           ZH_ROUTE_SRC_PEER    the kernels read them over xGMI (peer access on)
+ *           ZH_ROUTE_SRC_STAGED  copied to the slab's device first (no peer access)
+ *   ZH_MULTI_PEER=0 in the environment disables peer access (forces the staged routes);
+ *   ZH_MULTI_FORCE_STAGED=1 stages every non-root slab even on one device (tests).
+ */
+#define ZH_ROUTE_DIRECT 0
+#define ZH_ROUTE_PEER 1
+#define ZH_ROUTE_STAGED 2
+#define ZH_ROUTE_SAME 3
+#define ZH_ROUTE_SRC_PEER 4
+#define ZH_ROUTE_SRC_STAGED 8
+int zh_array_read_multi_routed(zh_ctx* const* ctxs, int ndev, int root,
+                               const zh_array_meta* meta, const zh_chunk_src* chunks,
+                               int64_t nchunks, const int64_t* offset, const int64_t* shape,
+                               void* out, uint32_t flags, int32_t* slab_route, char* err,
+                               size_t errlen);
 int zh_slab_partition(int ndim, const int64_t* offset, const int64_t* shape, int nslabs,
                       int64_t align, int64_t* slab_off, int64_t* slab_shape);
+/* Number of visible HIP devices (0 when none). */
+int zh_device_count(void);
 
 /* ShardingIndexedCodec.decode: whole shard → chunk_shape elements. */
 int zh_sharding_decode(zh_ctx* ctx, const zh_array_meta* meta, const void* shard, int64_t nbytes,

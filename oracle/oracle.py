@@ -46,6 +46,9 @@ def lib():
         L.zo_array_read.restype = C.c_int
         L.zo_array_read.argtypes = [PM, C.POINTER(A.zh_chunk_src), I64, PI64, PI64, P, C.c_int,
                                     C.c_char_p, C.c_size_t]
+        L.zo_array_read_store.restype = C.c_int
+        L.zo_array_read_store.argtypes = [PM, C.POINTER(C.c_char_p), I64, PI64, PI64, P, C.c_int,
+                                          C.c_char_p, C.c_size_t]
         L.zo_sharding_decode_partial.restype = C.c_int
         L.zo_sharding_decode_partial.argtypes = [PM, P, I64, PI64, PI32, P, C.c_int, C.c_char_p,
                                                  C.c_size_t]
@@ -132,6 +135,28 @@ def array_read_into(meta, srcs_struct, nsrc, offset, shape, out_addr, nthreads=1
                              C.c_void_p(out_addr), nthreads, err, 1024)
     if st != 0:
         raise OracleError(st, err.value.decode())
+
+
+def array_read_store(meta, paths, offset, shape, out_addr=None, nthreads=1):
+    """core.Array.read from a FilesystemStore: `paths` = one file path (str) or None per chunk
+    key, in computeChunkCoords order.  Sub-shard regions go through the partial path's
+    per-inner-chunk range reads.  Returns bytes, or fills `out_addr` when given."""
+    n = meta.ndim
+    nel = 1
+    for d in range(n):
+        nel *= int(shape[d])
+    buf = None
+    if out_addr is None:
+        buf = (C.c_char * max(1, nel * meta.dtype_size))()
+        out_addr = C.addressof(buf)
+    arr = (C.c_char_p * max(1, len(paths)))(*[None if p is None else os.fsencode(p)
+                                               for p in paths])
+    err = C.create_string_buffer(1024)
+    st = lib().zo_array_read_store(C.byref(meta), arr, len(paths), _i64(offset), _i64(shape),
+                                   C.c_void_p(out_addr), nthreads, err, 1024)
+    if st != 0:
+        raise OracleError(st, err.value.decode())
+    return None if buf is None else bytes(buf)[: nel * meta.dtype_size]
 
 
 def array_write(meta, src, offset, shape):

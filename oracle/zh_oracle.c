@@ -16,10 +16,13 @@
  */
 #include "zh_oracle.h"
 
+#include <fcntl.h>
 #include <stdarg.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <sys/stat.h>
+#include <unistd.h>
 #ifdef _OPENMP
 #include <omp.h>
 #endif
@@ -320,8 +323,37 @@ static void nested_meta(const zh_array_meta* m, zh_array_meta* m2) {
 }
 
 static int sharding_decode_internal(const zh_array_meta* m, const uint8_t* shard, int64_t nbytes,
-                                    const int64_t* offset, const int32_t* shape, uint8_t* out,
-                                    int nthreads, char* err, size_t errlen);
+                                    const char* path, const int64_t* offset, const int32_t* shape,
+                                    uint8_t* out, int nthreads, char* err, size_t errlen);
+
+/* FilesystemStore.get(keys, start, end) — M/store/FilesystemStore.java:85-102: one
+ * Files.newByteChannel open, a position + read into a freshly allocated buffer, and a close
+ * per call; a negative start counts from the end (:74-77, the suffix read of the index).
+ * Returns a malloc'd buffer of `len` bytes, or NULL (missing file / short read). */
+static uint8_t* file_range_read(const char* path, int64_t start, int64_t len, int64_t* fsize) {
+  int fd = open(path, O_RDONLY);
+  if (fd < 0) return NULL;
+  struct stat sb;
+  if (fstat(fd, &sb) != 0) {
+    close(fd);
+    return NULL;
+  }
+  if (fsize) *fsize = (int64_t)sb.st_size;
+  if (start < 0) start += (int64_t)sb.st_size;
+  uint8_t* b = (uint8_t*)malloc(len > 0 ? len : 1);
+  int64_t got = 0;
+  while (got < len) {
+    ssize_t r = pread(fd, b + got, (size_t)(len - got), (off_t)(start + got));
+    if (r <= 0) break;
+    got += r;
+  }
+  close(fd);
+  if (got != len) {
+    free(b);
+    return NULL;
+  }
+  return b;
+}
 
 static uint64_t load_u64(const uint8_t* p, int big) {
   uint64_t v = 0;
@@ -341,7 +373,8 @@ static void store_u64(uint8_t* p, uint64_t v, int big) {
 
 typedef struct {
   const zh_array_meta* m;
-  const uint8_t* shard;
+  const uint8_t* shard;       /* ByteBufferDataProvider (:301-331), or NULL with ... */
+  const char* path;           /* ... StoreHandleDataProvider over a file (:333-357) */
   int64_t nbytes;
   const uint8_t* index;       /* index entries (CRC stripped) */
   const int64_t* inner_coords;
@@ -382,6 +415,18 @@ static int decode_one_inner(inner_job_t* J, int64_t k, char* err, size_t errlen)
     set_err(err, errlen, "Could not load byte data for chunk %s", cs);
     return ZH_EDATA;
   }
+  const uint8_t* bytes = J->shard ? J->shard + off : NULL;
+  uint8_t* fbuf = NULL;
+  if (J->path) { /* dataProvider.read(off, len) → storeHandle.read(off, off + len) :354-356 */
+    fbuf = file_range_read(J->path, off, len, NULL);
+    if (!fbuf) {
+      char cs[256];
+      fmt_coords(cs, sizeof cs, c, n);
+      set_err(err, errlen, "Could not load byte data for chunk %s", cs);
+      return ZH_EDATA;
+    }
+    bytes = fbuf;
+  }
   uint8_t* buf = NULL;
   nd_t arr;
   int st;
@@ -392,9 +437,10 @@ static int decode_one_inner(inner_job_t* J, int64_t k, char* err, size_t errlen)
     int64_t nel1 = 1, zoff[ZH_MAX_DIMS] = {0};
     for (int d = 0; d < n; d++) nel1 *= inner[d];
     buf = (uint8_t*)malloc(nel1 * m->dtype_size > 0 ? nel1 * m->dtype_size : 1);
-    st = sharding_decode_internal(&m2, J->shard + off, len, zoff, inner, buf, 1, err, errlen);
+    st = sharding_decode_internal(&m2, bytes, len, NULL, zoff, inner, buf, 1, err, errlen);
     if (st != ZH_OK) {
       free(buf);
+      free(fbuf);
       return st;
     }
     arr.data = buf;
@@ -403,9 +449,13 @@ static int decode_one_inner(inner_job_t* J, int64_t k, char* err, size_t errlen)
     for (int d = 0; d < n; d++) arr.shape[d] = inner[d];
     nd_c_order(&arr);
   } else {
-    st = inner_decode(m, inner, J->shard + off, len, &buf, &arr, err, errlen); /* :231 */
-    if (st != ZH_OK) return st;
+    st = inner_decode(m, inner, bytes, len, &buf, &arr, err, errlen); /* :231 */
+    if (st != ZH_OK) {
+      free(fbuf);
+      return st;
+    }
   }
+  free(fbuf);
   int64_t so[ZH_MAX_DIMS], dof[ZH_MAX_DIMS], sh[ZH_MAX_DIMS];
   for (int d = 0; d < n; d++) {
     so[d] = co[d];
@@ -420,8 +470,8 @@ static int decode_one_inner(inner_job_t* J, int64_t k, char* err, size_t errlen)
 /* ShardingIndexedCodec.decodeInternal — ShardingIndexedCodec.java:183-243, with the shard
  * bytes in memory (ByteBufferDataProvider :301-331). */
 static int sharding_decode_internal(const zh_array_meta* m, const uint8_t* shard, int64_t nbytes,
-                                    const int64_t* offset, const int32_t* shape, uint8_t* out,
-                                    int nthreads, char* err, size_t errlen) {
+                                    const char* path, const int64_t* offset, const int32_t* shape,
+                                    uint8_t* out, int nthreads, char* err, size_t errlen) {
   int n = m->ndim, ds = m->dtype_size;
   nd_t part;                                                          /* :189 zero-filled */
   part.data = out;
@@ -435,13 +485,24 @@ static int sharding_decode_internal(const zh_array_meta* m, const uint8_t* shard
   nd_c_order(&part);
   memset(out, 0, nel * ds);
   int64_t isz = shard_index_size(m);                                  /* :190 */
+  uint8_t* fidx = NULL;
+  if (path) { /* StoreHandleDataProvider.readPrefix / readSuffix :340-352 */
+    fidx = file_range_read(path, m->chain.index_location == ZH_INDEX_START ? 0 : -isz, isz,
+                           &nbytes);
+    if (!fidx) { /* a null index buffer → fill_value (:199-204) */
+      fill_elems(out, nel, ds, m->fill_value);
+      return ZH_OK;
+    }
+  }
   if (nbytes < isz) {
     set_err(err, errlen, "Shard of %lld bytes is smaller than its index (%lld bytes).",
             (long long)nbytes, (long long)isz);
+    free(fidx);
     return ZH_EDATA;
   }
-  const uint8_t* ib = m->chain.index_location == ZH_INDEX_START ? shard       /* :192-193 */
-                                                                : shard + nbytes - isz; /* :194-195 */
+  const uint8_t* ib = fidx ? fidx
+                           : m->chain.index_location == ZH_INDEX_START ? shard  /* :192-193 */
+                                                                       : shard + nbytes - isz; /* :194-195 */
   int64_t ilen = isz;
   if (m->chain.index_has_crc32c) {                /* Crc32cCodec.decode, Crc32cCodec.java:24-48 */
     ilen -= 4;
@@ -452,6 +513,7 @@ static int sharding_decode_internal(const zh_array_meta* m, const uint8_t* shard
       set_err(err, errlen,
               "The checksum of the sharding index is invalid. Stored: %d Computed: %d", stored,
               computed);
+      free(fidx);
       return ZH_EDATA;
     }
   }
@@ -464,12 +526,13 @@ static int sharding_decode_internal(const zh_array_meta* m, const uint8_t* shard
                                            sel_shape, NULL, 0);       /* :206-208 */
   if (ninner < 0) {
     set_err(err, errlen, "Number of chunks exceeds Integer.MAX_VALUE");
+    free(fidx);
     return ZH_EARITH;
   }
   int64_t* coords = (int64_t*)malloc(sizeof(int64_t) * n * (ninner > 0 ? ninner : 1));
   zo_compute_chunk_coords(n, shard_shape, m->chain.inner_chunk_shape, offset, sel_shape, coords,
                           ninner);
-  inner_job_t J = {m, shard, nbytes, ib, coords, offset, shape, &part, ZH_OK, err, errlen};
+  inner_job_t J = {m, shard, path, nbytes, ib, coords, offset, shape, &part, ZH_OK, err, errlen};
   int status = ZH_OK;
   /* :210-212 parallel stream over inner chunks; each copy targets a disjoint region. */
 #ifdef _OPENMP
@@ -493,20 +556,22 @@ static int sharding_decode_internal(const zh_array_meta* m, const uint8_t* shard
   }
   (void)nthreads;
   free(coords);
+  free(fidx);
   return status;
 }
 
 int zo_sharding_decode_partial(const zh_array_meta* m, const void* shard, int64_t nbytes,
                                const int64_t* offset, const int32_t* shape, void* out,
                                int nthreads, char* err, size_t errlen) {
-  return sharding_decode_internal(m, (const uint8_t*)shard, nbytes, offset, shape,
+  return sharding_decode_internal(m, (const uint8_t*)shard, nbytes, NULL, offset, shape,
                                   (uint8_t*)out, nthreads, err, errlen);
 }
 
 /* core.Array.read — M/core/Array.java:378-441 */
-int zo_array_read(const zh_array_meta* m, const zh_chunk_src* chunks, int64_t nchunks,
-                  const int64_t* offset, const int64_t* shape, void* out_v, int nthreads,
-                  char* err, size_t errlen) {
+static int array_read_impl(const zh_array_meta* m, const zh_chunk_src* chunks,
+                           const char* const* paths, int64_t nchunks, const int64_t* offset,
+                           const int64_t* shape, void* out_v, int nthreads, char* err,
+                           size_t errlen) {
   int n = m->ndim, ds = m->dtype_size;
   uint8_t* out = (uint8_t*)out_v;
   for (int d = 0; d < n; d++)                                          /* :386-390 */
@@ -549,7 +614,27 @@ int zo_array_read(const zh_array_meta* m, const zh_chunk_src* chunks, int64_t nc
       status = ZH_EARITH;
       break;
     }
-    const zh_chunk_src* s = &chunks[i];
+    zh_chunk_src fsrc = {NULL, 0};
+    uint8_t* whole = NULL; /* StoreHandle.read() = FilesystemStore.get(keys) (:49-59) */
+    const char* spath = NULL;
+    if (paths) {
+      int full = 1;
+      for (int d = 0; d < n; d++) full &= ps[d] == m->chunk_shape[d];
+      if (paths[i] && (!m->chain.sharded || full)) { /* decodePartial :246-252 / readChunk */
+        int64_t fsz = 0;
+        struct stat sb;
+        if (stat(paths[i], &sb) == 0) {
+          fsz = (int64_t)sb.st_size;
+          whole = file_range_read(paths[i], 0, fsz, NULL);
+        }
+        fsrc.data = whole;
+        fsrc.nbytes = fsz;
+      } else if (paths[i]) {
+        spath = paths[i]; /* StoreHandleDataProvider (:253) */
+        fsrc.data = (const void*)1; /* exists (:419) */
+      }
+    }
+    const zh_chunk_src* s = paths ? &fsrc : &chunks[i];
     int64_t pdoff[ZH_MAX_DIMS], psh[ZH_MAX_DIMS], zero[ZH_MAX_DIMS] = {0}, so[ZH_MAX_DIMS];
     int64_t pnel = 1;
     for (int d = 0; d < n; d++) {
@@ -563,8 +648,9 @@ int zo_array_read(const zh_array_meta* m, const zh_chunk_src* chunks, int64_t nc
       uint8_t* pbuf = (uint8_t*)malloc(pnel * ds > 0 ? pnel * ds : 1);
       int64_t coff[ZH_MAX_DIMS];
       for (int d = 0; d < n; d++) coff[d] = co[d];
-      status = sharding_decode_internal(m, (const uint8_t*)s->data, s->nbytes, coff, ps, pbuf,
-                                        nthreads, err, errlen);      /* :422-423 */
+      status = sharding_decode_internal(m, spath ? NULL : (const uint8_t*)s->data, s->nbytes,
+                                        spath, coff, ps, pbuf, nthreads, err,
+                                        errlen); /* :422-423 */
       if (status == ZH_OK) {
         nd_t part;
         part.data = pbuf;
@@ -584,9 +670,27 @@ int zo_array_read(const zh_array_meta* m, const zh_chunk_src* chunks, int64_t nc
       if (status == ZH_OK) copy_region(&arr, so, &outa, pdoff, psh);  /* :430-432 */
       free(buf);
     }
+    free(whole);
   }
   free(coords);
   return status;
+}
+
+int zo_array_read(const zh_array_meta* m, const zh_chunk_src* chunks, int64_t nchunks,
+                  const int64_t* offset, const int64_t* shape, void* out_v, int nthreads,
+                  char* err, size_t errlen) {
+  return array_read_impl(m, chunks, NULL, nchunks, offset, shape, out_v, nthreads, err, errlen);
+}
+
+/* core.Array.read against a FilesystemStore: one file path per chunk key (NULL = the key
+ * does not exist).  Sub-shard regions take StoreHandleDataProvider's range reads (suffix
+ * read of the index, then one open + read + close per referenced inner chunk,
+ * ShardingIndexedCodec.java:253,333-357); whole chunks and unsharded chunks are read whole
+ * (FilesystemStore.get(keys), M/store/FilesystemStore.java:49-59). */
+int zo_array_read_store(const zh_array_meta* m, const char* const* paths, int64_t nchunks,
+                        const int64_t* offset, const int64_t* shape, void* out_v, int nthreads,
+                        char* err, size_t errlen) {
+  return array_read_impl(m, NULL, paths, nchunks, offset, shape, out_v, nthreads, err, errlen);
 }
 
 /* ---------------------------------------------------------------------------------

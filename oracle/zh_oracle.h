@@ -37,6 +37,11 @@ int zo_inverse_permutation(int n, const int32_t* order, int32_t* inverse);
 int zo_array_read(const zh_array_meta* meta, const zh_chunk_src* chunks, int64_t nchunks,
                   const int64_t* offset, const int64_t* shape, void* out, int nthreads,
                   char* err, size_t errlen);
+/* core.Array.read against a FilesystemStore (one path per chunk key, NULL = missing): the
+ * partial path's range reads per inner chunk (StoreHandleDataProvider). */
+int zo_array_read_store(const zh_array_meta* meta, const char* const* paths, int64_t nchunks,
+                        const int64_t* offset, const int64_t* shape, void* out, int nthreads,
+                        char* err, size_t errlen);
 /* ShardingIndexedCodec.decodeInternal over a whole shard buffer (decode / decodePartial). */
 int zo_sharding_decode_partial(const zh_array_meta* meta, const void* shard, int64_t nbytes,
                                const int64_t* offset, const int32_t* shape, void* out,

@@ -113,3 +113,23 @@ def test_c_slab_partition_matches_python(seed):
             slab_partition(off, shape, world, align)
         return
     assert slab_partition(off, shape, world, align) == want
+
+
+def test_bench_self_launches_ranks_without_a_launcher():
+    """`python bench.py --gpus 2` with no WORLD_SIZE starts its two ranks itself (before any
+    GPU call, as child processes) and rank 0 prints exactly one JSON line with n_gpus 2 and
+    strong scaling; --dry-run keeps it off the GPU so the harness runs here."""
+    import json
+    import subprocess
+    import sys
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2",
+                        "--dry-run", "--steps", "2", "--warmup", "1"], capture_output=True,
+                       text=True, timeout=600, env=env)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.strip()]
+    assert len(lines) == 1, r.stdout
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["scaling"] == "strong" and d["dry_run"] is True
+    assert d["config"]["slab_rows_max"] == 2048

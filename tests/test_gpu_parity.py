@@ -44,6 +44,38 @@ def test_reference_fixtures_decode_to_arange(dev):
                                       np.arange(4096).reshape(16, 16, 16)[3:12, 5:12, 1:15])
 
 
+@pytest.mark.parametrize("loc,stored_crc", [("end", 0xB756D1D4), ("start", 0x56F05363)])
+def test_device_crc_on_reference_index_bytes(dev, loc, stored_crc):
+    """The device index-CRC kernel on the reference fixture's own, untouched 68-byte index
+    (testdata/sharding_index_location, Crc32cCodec.decode, Crc32cCodec.java:24-48).  With
+    only the stored crc zeroed, the device must report Computed = the crc the reference
+    stored; with the index intact the CRC passes and the read stops at the next stage (the
+    blosc-framed inner chunks are not raw `bytes`), exactly as the oracle does."""
+    import os
+    import struct
+    from helpers import GOLDEN
+    _, meta, _ = load_reference_fixture(loc)
+    raw = open(os.path.join(GOLDEN, "sharding_index_location", loc, "c", "0", "0", "0"),
+               "rb").read()
+    cpos = 64 if loc == "start" else len(raw) - 4
+    assert struct.unpack("<I", raw[cpos:cpos + 4])[0] == stored_crc
+    zeroed = raw[:cpos] + b"\0\0\0\0" + raw[cpos + 4:]
+    signed = struct.unpack("<i", struct.pack("<I", stored_crc))[0]
+    with pytest.raises(ZhError) as ed:
+        device_read(dev, meta, [zeroed], [0, 0, 0], [16, 8, 8])
+    assert str(ed.value) == ("The checksum of the sharding index is invalid. Stored: 0 "
+                             f"Computed: {signed}")
+    with pytest.raises(O.OracleError) as eo:
+        O.array_read(meta, [zeroed], [0, 0, 0], [16, 8, 8])
+    assert str(eo.value) == str(ed.value)
+    with pytest.raises(ZhError) as ed2:
+        device_read(dev, meta, [raw], [0, 0, 0], [16, 8, 8])
+    with pytest.raises(O.OracleError) as eo2:
+        O.array_read(meta, [raw], [0, 0, 0], [16, 8, 8])
+    assert "checksum" not in str(ed2.value)
+    assert str(ed2.value) == str(eo2.value)
+
+
 @pytest.mark.parametrize("dsize", [1, 2, 4, 8])
 @pytest.mark.parametrize("endian", [A.ZH_ENDIAN_LITTLE, A.ZH_ENDIAN_BIG])
 def test_unsharded_bytes(dev, dsize, endian):

@@ -188,6 +188,10 @@ int zh_blosc_decompress(const void* src_v, size_t srclen, void* dst_v, size_t ds
     const bool leftover = bs < bsize;
     const size_t nsplit = ((flags & 0x10) || leftover) ? 1 : ts;
     const size_t neb = bs / nsplit;
+    if (nsplit > 1 && bs % nsplit != 0) {  // split streams must tile the block exactly
+      set_err(err, errlen, "blosc frame header corrupt (block not a multiple of the typesize)");
+      return ZH_EDATA;
+    }
     size_t p = rd32(src + 16 + 4 * k);
     uint8_t* blk = (flags & 0x01) && ts > 1 ? tmp.data() : dst + k * bsize;
     for (size_t sidx = 0; sidx < nsplit; sidx++) {

@@ -1585,24 +1585,80 @@ int zh_array_read(zh_ctx* ctx, const zh_array_meta* meta, const zh_chunk_src* ch
 
 namespace {
 // Peer access from device `from` to device `to` (once per pair per process), so that the
-// slab copies to the root device go device to device over xGMI.  Same device, or a pair
-// without peer support: nothing to do (hipMemcpyPeerAsync still works, staged).
-void enable_peer(int from, int to) {
-  if (from == to) return;
+// slab copies to the root device go device to device over xGMI and kernels on `from` may
+// read `to`'s memory.  Returns false when the pair has no peer access (or ZH_MULTI_PEER=0):
+// the caller then stages through host memory.
+bool enable_peer(int from, int to) {
+  if (from == to) return true;
+  const char* env = getenv("ZH_MULTI_PEER");
+  if (env && env[0] == '0') return false;
   static std::mutex mu;
-  static std::vector<std::pair<int, int>> done;
+  static std::vector<std::pair<std::pair<int, int>, bool>> done;
   std::lock_guard<std::mutex> lk(mu);
   for (auto& p : done)
-    if (p.first == from && p.second == to) return;
-  done.emplace_back(from, to);
+    if (p.first.first == from && p.first.second == to) return p.second;
   int can = 0;
-  if (hipDeviceCanAccessPeer(&can, from, to) != hipSuccess || !can) return;
+  bool ok = hipDeviceCanAccessPeer(&can, from, to) == hipSuccess && can;
+  if (ok) {
+    int cur = 0;
+    (void)hipGetDevice(&cur);
+    (void)hipSetDevice(from);
+    const hipError_t e = hipDeviceEnablePeerAccess(to, 0);
+    if (e == hipErrorPeerAccessAlreadyEnabled) (void)hipGetLastError();
+    ok = e == hipSuccess || e == hipErrorPeerAccessAlreadyEnabled;
+    if (!ok) (void)hipGetLastError();
+    (void)hipSetDevice(cur);
+  }
+  done.push_back({{from, to}, ok});
+  return ok;
+}
+
+// Device holding a device pointer (-1: host / unknown).
+int pointer_device(const void* p) {
+  hipPointerAttribute_t a;
+  if (!p || hipPointerGetAttributes(&a, p) != hipSuccess) {
+    (void)hipGetLastError();
+    return -1;
+  }
+  return a.type == hipMemoryTypeDevice ? a.device : -1;
+}
+
+// Copy `bytes` from `src` on device `sdev` to `dst` on device `ddev` through pinned host
+// memory in bounded pieces (no peer access between the two), on fresh streams of each
+// device.  Leaves the current device as it found it.
+int staged_copy(void* dst, int ddev, const void* src, int sdev, size_t bytes) {
+  const size_t piece = (size_t)256 << 20;
   int cur = 0;
   (void)hipGetDevice(&cur);
-  (void)hipSetDevice(from);
-  const hipError_t e = hipDeviceEnablePeerAccess(to, 0);
-  if (e == hipErrorPeerAccessAlreadyEnabled) (void)hipGetLastError();
+  void* host = nullptr;
+  hipStream_t ss = nullptr, ds = nullptr;
+  int rc = ZH_OK;
+  if (hipHostMalloc(&host, std::min(piece, bytes > 0 ? bytes : 1), 0) != hipSuccess) rc = ZH_ENOMEM;
+  if (rc == ZH_OK && (hipSetDevice(sdev) != hipSuccess || hipStreamCreate(&ss) != hipSuccess))
+    rc = ZH_EHIP;
+  if (rc == ZH_OK && (hipSetDevice(ddev) != hipSuccess || hipStreamCreate(&ds) != hipSuccess))
+    rc = ZH_EHIP;
+  for (size_t o = 0; rc == ZH_OK && o < bytes; o += piece) {
+    const size_t b = std::min(piece, bytes - o);
+    if (hipSetDevice(sdev) != hipSuccess ||
+        hipMemcpyAsync(host, (const uint8_t*)src + o, b, hipMemcpyDeviceToHost, ss) != hipSuccess ||
+        hipStreamSynchronize(ss) != hipSuccess || hipSetDevice(ddev) != hipSuccess ||
+        hipMemcpyAsync((uint8_t*)dst + o, host, b, hipMemcpyHostToDevice, ds) != hipSuccess ||
+        hipStreamSynchronize(ds) != hipSuccess)
+      rc = ZH_EHIP;
+  }
+  if (ss) {
+    (void)hipSetDevice(sdev);
+    (void)hipStreamDestroy(ss);
+  }
+  if (ds) {
+    (void)hipSetDevice(ddev);
+    (void)hipStreamDestroy(ds);
+  }
+  if (host) (void)hipHostFree(host);
+  if (rc != ZH_OK) (void)hipGetLastError();
   (void)hipSetDevice(cur);
+  return rc;
 }
 }  // namespace
 
@@ -1642,10 +1698,30 @@ int zh_slab_partition(int ndim, const int64_t* offset, const int64_t* shape, int
   return ZH_OK;
 }
 
+int zh_device_count(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) {
+    (void)hipGetLastError();
+    return 0;
+  }
+  return n;
+}
+
 int zh_array_read_multi(zh_ctx* const* ctxs, int ndev, int root, const zh_array_meta* meta,
                         const zh_chunk_src* chunks, int64_t nchunks, const int64_t* offset,
                         const int64_t* shape, void* out, uint32_t flags, char* err,
                         size_t errlen) {
+  return zh_array_read_multi_routed(ctxs, ndev, root, meta, chunks, nchunks, offset, shape, out,
+                                    flags, nullptr, err, errlen);
+}
+
+int zh_array_read_multi_routed(zh_ctx* const* ctxs, int ndev, int root,
+                               const zh_array_meta* meta, const zh_chunk_src* chunks,
+                               int64_t nchunks, const int64_t* offset, const int64_t* shape,
+                               void* out, uint32_t flags, int32_t* slab_route, char* err,
+                               size_t errlen) {
+  if (slab_route)
+    for (int k = 0; k < ndev; k++) slab_route[k] = ZH_ROUTE_DIRECT;
   if (!ctxs || ndev <= 0 || root < 0 || root >= ndev || !meta || !offset || !shape || !out)
     return ZH_EINVAL;
   for (int k = 0; k < ndev; k++)
@@ -1723,27 +1799,75 @@ int zh_array_read_multi(zh_ctx* const* ctxs, int ndev, int root, const zh_array_
     std::lock_guard<std::mutex> lk(ctx->mu);
     (void)hipSetDevice(ctx->device);
     const int rdev = ctxs[root]->device;
-    const bool peer = out_dev && ctx != ctxs[root];
-    if (peer) enable_peer(ctx->device, rdev);  // xGMI copies straight into the root's buffer
+    const size_t sbytes = (size_t)(nel * meta->dtype_size);
+    int route = ZH_ROUTE_DIRECT;
+    // device sources on another device: read them over xGMI, or stage them here
+    std::vector<void*> staged;
+    // ZH_MULTI_FORCE_STAGED=1 (tests): every non-root slab takes the staged routes, so the
+    // no-peer fallback runs even with all contexts on one device
+    const char* fenv = getenv("ZH_MULTI_FORCE_STAGED");
+    const bool force = fenv && fenv[0] == '1' && ctx != ctxs[root];
+    if (flags & ZH_SRC_DEVICE) {
+      for (auto& c : sub) {
+        if (!c.data || c.nbytes <= 0) continue;
+        const int sdev = pointer_device(c.data);
+        if (sdev < 0 || (sdev == ctx->device && !force)) continue;
+        if (!force && enable_peer(ctx->device, sdev)) {
+          route |= ZH_ROUTE_SRC_PEER;
+          continue;
+        }
+        void* loc = nullptr;
+        if (hipMalloc(&loc, (size_t)c.nbytes) != hipSuccess) {
+          (void)hipGetLastError();
+          rc = ZH_ENOMEM;
+          snprintf(e, sizeof(e), "hipMalloc of a staged chunk on device %d failed", ctx->device);
+          break;
+        }
+        staged.push_back(loc);
+        rc = staged_copy(loc, ctx->device, c.data, sdev, (size_t)c.nbytes);
+        if (rc != ZH_OK) {
+          snprintf(e, sizeof(e), "staging a chunk from device %d to %d failed", sdev,
+                   ctx->device);
+          break;
+        }
+        c.data = loc;
+        route |= ZH_ROUTE_SRC_STAGED;
+      }
+    }
+    const bool remote = out_dev && ctx != ctxs[root];  // decode locally, then deliver
+    int oroute = ZH_ROUTE_DIRECT;
+    if (remote)
+      oroute = force                     ? ZH_ROUTE_STAGED
+               : ctx->device == rdev     ? ZH_ROUTE_SAME
+               : enable_peer(ctx->device, rdev) ? ZH_ROUTE_PEER
+                                         : ZH_ROUTE_STAGED;
+    route |= oroute;
     void* local = nullptr;
-    if (peer && hipMalloc(&local, (size_t)(nel * meta->dtype_size)) != hipSuccess) {
-      status[r] = ZH_ENOMEM;
-      msgs[r] = "hipMalloc of a slab buffer failed";
-      return;
+    if (rc == ZH_OK && remote && hipMalloc(&local, sbytes) != hipSuccess) {
+      (void)hipGetLastError();
+      rc = ZH_ENOMEM;
+      snprintf(e, sizeof(e), "hipMalloc of a slab buffer failed");
     }
     zh_plan* p = nullptr;
     uint32_t pf = (flags & ZH_SRC_DEVICE) | (out_dev ? ZH_OUT_DEVICE : 0u);
-    rc = zh_plan_create(ctx, meta, sub.data(), m, o, s, pf, &p, e, sizeof(e));
-    if (rc == ZH_OK) rc = zh_plan_execute(p, peer ? local : (void*)dst, nullptr);
-    if (rc == ZH_OK && peer &&
-        hipMemcpyPeerAsync(dst, rdev, local, ctx->device, (size_t)(nel * meta->dtype_size),
-                           ctx->stream) != hipSuccess) {
+    if (rc == ZH_OK) rc = zh_plan_create(ctx, meta, sub.data(), m, o, s, pf, &p, e, sizeof(e));
+    if (rc == ZH_OK) rc = zh_plan_execute(p, remote ? local : (void*)dst, nullptr);
+    if (rc == ZH_OK && (oroute == ZH_ROUTE_PEER || oroute == ZH_ROUTE_SAME) &&
+        hipMemcpyPeerAsync(dst, rdev, local, ctx->device, sbytes, ctx->stream) != hipSuccess) {
+      (void)hipGetLastError();
       rc = ZH_EHIP;
       snprintf(e, sizeof(e), "slab copy to device %d failed", rdev);
     }
     if (rc == ZH_OK) rc = zh_plan_wait(p, e, sizeof(e));
+    if (rc == ZH_OK && oroute == ZH_ROUTE_STAGED) {
+      rc = staged_copy(dst, rdev, local, ctx->device, sbytes);
+      if (rc != ZH_OK) snprintf(e, sizeof(e), "staged slab copy to device %d failed", rdev);
+    }
     if (p) plan_free(p);
+    (void)hipSetDevice(ctx->device);
     if (local) (void)hipFree(local);
+    for (void* x : staged) (void)hipFree(x);
+    if (slab_route) slab_route[r] = route;
     status[r] = rc;
     msgs[r] = e;
   };

@@ -11,6 +11,7 @@
  */
 #include <jni.h>
 #include <stdint.h>
+#include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 
@@ -128,12 +129,35 @@ static jint array_read_common(JNIEnv* env, zh_ctx* const* ctxs, int nctx, jintAr
     o64[d] = off[d];
     r64[d] = reg[d];
   }
-  void* dst = (*env)->GetPrimitiveArrayCritical(env, (jarray)out, NULL);
-  if (nctx == 1)
-    st = zh_array_read(ctxs[0], &m, srcs, n, o64, r64, dst, 0, NULL, err, sizeof err);
-  else  /* one slab per device, each D2H'd straight into its slice of the Java array */
-    st = zh_array_read_multi(ctxs, nctx, 0, &m, srcs, n, o64, r64, dst, 0, err, sizeof err);
-  (*env)->ReleasePrimitiveArrayCritical(env, (jarray)out, dst, 0);
+  /* decode into native memory, then hold the critical section only for the final copy
+   * (a critical section around device work would stall every other Java thread's GC) */
+  int64_t nel = 1;
+  for (int d = 0; d < m.ndim; d++) nel *= r64[d];
+  const size_t obytes = (size_t)nel * (size_t)m.dtype_size;
+  void* tmp = NULL;
+  if ((int64_t)(*env)->GetArrayLength(env, (jarray)out) != nel) {
+    st = ZH_EINVAL;
+    snprintf(err, sizeof err, "output array holds %lld elements, the region %lld",
+             (long long)(*env)->GetArrayLength(env, (jarray)out), (long long)nel);
+  } else if (!(tmp = malloc(obytes > 0 ? obytes : 1))) {
+    st = ZH_ENOMEM;
+    snprintf(err, sizeof err, "out of host memory for the decoded region");
+  } else if (nctx == 1) {
+    st = zh_array_read(ctxs[0], &m, srcs, n, o64, r64, tmp, 0, NULL, err, sizeof err);
+  } else { /* one slab per device, each D2H'd into its slice of the region */
+    st = zh_array_read_multi(ctxs, nctx, 0, &m, srcs, n, o64, r64, tmp, 0, err, sizeof err);
+  }
+  if (st == ZH_OK) {
+    void* dst = (*env)->GetPrimitiveArrayCritical(env, (jarray)out, NULL);
+    if (dst) {
+      memcpy(dst, tmp, obytes);
+      (*env)->ReleasePrimitiveArrayCritical(env, (jarray)out, dst, 0);
+    } else {
+      st = ZH_ENOMEM;
+      snprintf(err, sizeof err, "could not access the output array");
+    }
+  }
+  free(tmp);
   for (jsize i = 0; i < n; i++) free(copies[i]);
   free(copies);
   free(arrs);
@@ -186,12 +210,33 @@ JNIEXPORT jint JNICALL Java_dev_zarr_zarrjava_hip_ZarrHip_shardDecodePartial(
   int64_t o64[ZH_MAX_DIMS];
   for (int d = 0; d < m.ndim; d++) o64[d] = off[d];
   jsize len = (*env)->GetArrayLength(env, shard);
+  int64_t nel = 1;
+  for (int d = 0; d < m.ndim; d++) nel *= part[d];
+  const size_t obytes = (size_t)nel * (size_t)m.dtype_size;
+  if ((int64_t)(*env)->GetArrayLength(env, (jarray)out) != nel)
+    return throw_status(env, ZH_EINVAL, "output array size does not match the part shape");
   void* src = malloc((size_t)(len > 0 ? len : 1));
+  void* tmp = malloc(obytes > 0 ? obytes : 1);
+  if (!src || !tmp) {
+    free(src);
+    free(tmp);
+    return throw_status(env, ZH_ENOMEM, "out of host memory for the shard");
+  }
   (*env)->GetByteArrayRegion(env, shard, 0, len, (jbyte*)src);
-  void* dst = (*env)->GetPrimitiveArrayCritical(env, (jarray)out, NULL);
-  st = zh_sharding_decode_partial((zh_ctx*)(intptr_t)ctx, &m, src, len, o64, part, dst, 0, NULL,
+  /* decode into native memory; the critical section covers only the final copy */
+  st = zh_sharding_decode_partial((zh_ctx*)(intptr_t)ctx, &m, src, len, o64, part, tmp, 0, NULL,
                                   err, sizeof err);
-  (*env)->ReleasePrimitiveArrayCritical(env, (jarray)out, dst, 0);
+  if (st == ZH_OK) {
+    void* dst = (*env)->GetPrimitiveArrayCritical(env, (jarray)out, NULL);
+    if (dst) {
+      memcpy(dst, tmp, obytes);
+      (*env)->ReleasePrimitiveArrayCritical(env, (jarray)out, dst, 0);
+    } else {
+      st = ZH_ENOMEM;
+      snprintf(err, sizeof err, "could not access the output array");
+    }
+  }
+  free(tmp);
   free(src);
   if (st == ZH_EUNSUPPORTED) return st;
   if (st != ZH_OK) return throw_status(env, st, err);
@@ -251,14 +296,25 @@ JNIEXPORT jobjectArray JNICALL Java_dev_zarr_zarrjava_hip_ZarrHip_arrayWrite(
     /* copy the region out of the heap: the call stages it to the device (no long critical
      * section around device work) */
     jsize nel = (*env)->GetArrayLength(env, (jarray)data);
+    int64_t want = 1;
+    for (int d = 0; d < m.ndim; d++) want *= r64[d];
+    if ((int64_t)nel != want) {
+      /* a Java array of another length (or element type) than the region: never read past
+       * its end; the caller keeps core.Array.write */
+      for (int64_t i = 0; i < n; i++) free(outs[i]);
+      free(outs);
+      free(caps);
+      free(sizes);
+      return NULL;
+    }
     const size_t rbytes = (size_t)nel * (size_t)m.dtype_size;
     void* src = malloc(rbytes > 0 ? rbytes : 1);
     void* pin = (*env)->GetPrimitiveArrayCritical(env, (jarray)data, NULL);
     if (src && pin) memcpy(src, pin, rbytes);
     if (pin) (*env)->ReleasePrimitiveArrayCritical(env, (jarray)data, pin, JNI_ABORT);
-    st = src ? zh_array_write_host((zh_ctx*)(intptr_t)ctx, &m, src, o64, r64, outs, caps, sizes,
-                                   n, err, sizeof err)
-             : ZH_ENOMEM;
+    st = src && pin ? zh_array_write_host((zh_ctx*)(intptr_t)ctx, &m, src, o64, r64, outs, caps,
+                                          sizes, n, err, sizeof err)
+                    : ZH_ENOMEM;
     free(src);
     if (st == ZH_OK) {
       jclass bcls = (*env)->FindClass(env, "[B");

@@ -91,7 +91,14 @@ public class HipArray extends Array {
     @Override
     public void write(long[] offset, ucar.ma2.Array array, boolean parallel) {
         ArrayMetadata md = metadata();
-        if (chain == null || offset.length != md.ndim() || array.getRank() != md.ndim()) {
+        // zh_array_write_host emits raw `bytes` payloads only: chains with host byte-to-byte
+        // stages (zstd, gzip, blosc, a non-final crc32c) keep the reference's encode, and the
+        // region's element type must be the array's (its bytes are copied as dtype elements)
+        if (chain == null || chain.innerHost != null || offset.length != md.ndim()
+                || array.getRank() != md.ndim()
+                || array.getDataType().getSize() != md.dataType().getByteCount()
+                || array.getDataType().isFloatingPoint()
+                    != md.dataType().getMA2DataType().isFloatingPoint()) {
             super.write(offset, array, parallel);
             return;
         }

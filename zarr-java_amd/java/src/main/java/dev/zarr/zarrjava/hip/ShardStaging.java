@@ -50,6 +50,9 @@ final class ShardStaging {
         }
         final long isz = 16L * nIn + (crc ? 4 : 0);
         if (!h.exists()) return null;
+        // the shard's length bounds every index entry (a corrupt entry must not turn into a
+        // huge range read / allocation)
+        long shardLen = -1;
         ByteBuffer ib = start ? h.read(0, isz) : h.read(-isz);
         if (ib == null) return null;
         byte[] idx = bytes(ib);
@@ -82,7 +85,20 @@ final class ShardStaging {
             int lin = 0;
             for (int d = 0; d < n; d++) lin = lin * cps[d] + b0[d] + cur[d];
             long off = entries.getLong(16 * lin), nb = entries.getLong(16 * lin + 8);
-            if (off != -1 && nb != -1) refs.add(new long[]{off, nb, lin});
+            if (off != -1 && nb != -1) {
+                if (shardLen < 0) shardLen = shardLength(h);
+                if (off < 0 || nb < 0 || off > shardLen - nb || nb > Integer.MAX_VALUE) {
+                    long[] c = new long[n];
+                    int rem = lin;
+                    for (int d = n - 1; d >= 0; d--) {
+                        c[d] = rem % cps[d];
+                        rem /= cps[d];
+                    }
+                    throw new ZarrException("Could not load byte data for chunk "
+                            + Arrays.toString(c));
+                }
+                refs.add(new long[]{off, nb, lin});
+            }
             for (int d = n - 1; d >= 0; d--) {
                 if (++cur[d] < cnt[d]) break;
                 cur[d] = 0;
@@ -139,6 +155,11 @@ final class ShardStaging {
             System.arraycopy(nib, 0, out, pb.length, nib.length);
         }
         return out;
+    }
+
+    /** Byte length of the shard at {@code h} (StoreHandle.getSize, M/store/StoreHandle.java:83-85). */
+    private static long shardLength(StoreHandle h) {
+        return h.getSize();
     }
 
     /**

@@ -21,6 +21,13 @@ ZH_MALLOC_CONTIGUOUS = 0x1
 ZH_MALLOC_REQUIRE = 0x2
 ZH_MALLOC_SCATTER = 0x4
 ZH_OUT_DEVICE = 0x2
+# zh_array_read_multi_routed per-slab routes (include/zarrhip.h)
+ZH_ROUTE_DIRECT = 0
+ZH_ROUTE_PEER = 1
+ZH_ROUTE_STAGED = 2
+ZH_ROUTE_SAME = 3
+ZH_ROUTE_SRC_PEER = 4
+ZH_ROUTE_SRC_STAGED = 8
 
 
 class zh_codec_chain(C.Structure):

@@ -50,6 +50,10 @@ _SIGS = {
     "zh_array_read_multi": (C.c_int, [C.POINTER(P), C.c_int, C.c_int, PMETA,
                                       C.POINTER(A.zh_chunk_src), I64, PI64, PI64, P, U32, CH,
                                       SZ]),
+    "zh_array_read_multi_routed": (C.c_int, [C.POINTER(P), C.c_int, C.c_int, PMETA,
+                                             C.POINTER(A.zh_chunk_src), I64, PI64, PI64, P, U32,
+                                             PI32, CH, SZ]),
+    "zh_device_count": (C.c_int, []),
     "zh_slab_partition": (C.c_int, [C.c_int, PI64, PI64, C.c_int, I64, PI64, PI64]),
     "zh_sharding_decode": (C.c_int, [P, PMETA, P, I64, P, U32, P, CH, SZ]),
     "zh_sharding_decode_partial": (C.c_int, [P, PMETA, P, I64, PI64, PI32, P, U32, P, CH, SZ]),
@@ -305,18 +309,27 @@ class DeviceContext:
 
 
 def array_read_multi(ctxs, meta, sources, offset, shape, out, flags, root=0):
-    """zh_array_read_multi: one region read split into per-device slabs (one DeviceContext
-    per slab), delivered to a host buffer or to a buffer on ctxs[root]'s device."""
+    """zh_array_read_multi_routed: one region read split into per-device slabs (one
+    DeviceContext per slab), delivered to a host buffer or to a buffer on ctxs[root]'s
+    device.  Returns the per-slab routes (A.ZH_ROUTE_*)."""
     L = lib()
     hs = (P * len(ctxs))(*[c.h for c in ctxs])
     srcs = (A.zh_chunk_src * max(1, len(sources)))()
     for i, (ptr, nb) in enumerate(sources):
         srcs[i].data = ptr
         srcs[i].nbytes = int(nb)
+    routes = (C.c_int32 * len(ctxs))()
     err = C.create_string_buffer(1024)
-    st = L.zh_array_read_multi(hs, len(ctxs), int(root), C.byref(meta), srcs, len(sources),
-                               i64arr(offset), i64arr(shape), P(out), int(flags), err, 1024)
+    st = L.zh_array_read_multi_routed(hs, len(ctxs), int(root), C.byref(meta), srcs,
+                                      len(sources), i64arr(offset), i64arr(shape), P(out),
+                                      int(flags), routes, err, 1024)
     check(st, err)
+    return list(routes)
+
+
+def device_count():
+    """Visible HIP devices (zh_device_count)."""
+    return int(lib().zh_device_count())
 
 
 def slab_partition(offset, shape, nslabs, align=1):
