@@ -328,12 +328,27 @@ int zh_device_info(zh_ctx* ctx, char* name, size_t namelen, int64_t* total_mem,
 
 /* ---- host byte-to-byte stage: blosc1 frames ----------------------------------------
  * Replaces the blosc-java call inside BloscCodec.decode (M/v3/codec/core/BloscCodec.java,
- * M/v2/codec/core/BloscCodec.java) for hosts without the blosc library: BloscLZ, LZ4/LZ4HC
- * and zlib payloads, byte shuffle, split and unsplit blocks, memcpyed frames.  dst == NULL
- * only reports the decompressed size in *nbytes_out.  Bit shuffle, snappy and zstd payloads
+ * M/v2/codec/core/BloscCodec.java) for hosts without the blosc library: BloscLZ, LZ4/LZ4HC,
+ * zlib and zstd payloads, byte and bit shuffle, split and unsplit blocks, memcpyed frames.
+ * dst == NULL only reports the decompressed size in *nbytes_out.  Snappy payloads
  * → ZH_EUNSUPPORTED. */
 int zh_blosc_decompress(const void* src, size_t srclen, void* dst, size_t dstcap,
                         size_t* nbytes_out, char* err, size_t errlen);
+
+/* ---- host byte-to-byte stage: zstd frames (RFC 8878) ------------------------------
+ * Replaces zstd-jni inside ZstdCodec.decode (M/core/codec/core/ZstdCodec.java:14-22) and the
+ * zstd compressor of blosc frames (BloscCodec.java; CodecBuilder.withBlosc() defaults to
+ * cname "zstd", M/v3/codec/CodecBuilder.java:58-60).  One or more frames (skippable frames
+ * skipped); the XXH64 content checksum is verified when a frame carries one; frames that need
+ * a dictionary → ZH_EUNSUPPORTED.  dst == NULL: *dstlen = the decoded size.
+ * zh_zstd_compress_raw writes a valid frame of raw (stored) blocks with the content size and,
+ * if asked, the checksum (the write path's encoder; no compression); dst == NULL: the size.
+ * zh_xxh64: XXH64 of a buffer (the checksum's hash). */
+int zh_zstd_decompress(const void* src, size_t srclen, void* dst, size_t dstcap, size_t* dstlen,
+                       char* err, size_t errlen);
+int zh_zstd_compress_raw(const void* src, size_t srclen, int checksum, void* dst, size_t dstcap,
+                         size_t* dstlen);
+uint64_t zh_xxh64(const void* data, size_t len, uint64_t seed);
 
 /* ---- synthetic data (bench / property tests) -------------------------------------- */
 /* dst[i] = low dtype_size bytes of splitmix64((first + i) ^ seed), i in [0, n). */

@@ -97,14 +97,43 @@ def blosclz_compress(src):
     return bytes(out)
 
 
-def frame(data, typesize, blocksize, comp="lz4", shuffle=True, split=None):
-    """A blosc1 frame of `data` (comp: blosclz / lz4 / zlib / raw-streams)."""
+def zstd_compress(b, level=3):
+    """libzstd (bundled with pyarrow) — an independent zstd encoder for test vectors."""
+    import pyarrow as pa
+    return pa.Codec("zstd", compression_level=level).compress(bytes(b), asbytes=True)
+
+
+def bit_shuffle(blk, typesize, version=2):
+    """bitshuffle's bshuf_trans_bit_elem layout as blosc's bitshuffle() applies it per block:
+    for byte position j and bit k, a row of ne/8 bytes whose bit m of byte q is bit k of byte
+    j of element 8q+m.  Blosc format 2 (c-blosc 1.x): only blocks whose element count is a
+    multiple of 8 are shuffled (others stored as is); later formats shuffle the multiple-of-8
+    prefix and keep the leftover bytes."""
+    ne = len(blk) // typesize
+    if version <= 2 and ne % 8:
+        return bytes(blk)
+    ne -= ne % 8
+    if ne == 0:
+        return bytes(blk)
+    a = np.frombuffer(blk[:ne * typesize], np.uint8).reshape(ne, typesize)
+    bits = np.unpackbits(a, axis=1, bitorder="little").reshape(ne, typesize, 8)  # [e, j, k]
+    rows = bits.transpose(1, 2, 0).reshape(typesize * 8, ne // 8, 8)           # [(j,k), q, m]
+    out = np.packbits(rows, axis=2, bitorder="little").ravel()
+    return out.tobytes() + bytes(blk[ne * typesize:])
+
+
+def frame(data, typesize, blocksize, comp="lz4", shuffle=True, split=None, bitshuffle=False,
+          version=2):
+    """A blosc1 frame of `data` (comp: blosclz / lz4 / zlib / zstd / raw-streams)."""
     data = bytes(data)
     nbytes = len(data)
-    code = {"blosclz": 0, "lz4": 1, "zlib": 3}[comp]
+    code = {"blosclz": 0, "lz4": 1, "zlib": 3, "zstd": 4}[comp]
     if split is None:
         split = comp == "blosclz" and blocksize // typesize >= 128
-    flags = (code << 5) | (0x01 if shuffle else 0) | (0 if split else 0x10)
+    if bitshuffle:
+        shuffle = False
+    flags = (code << 5) | (0x01 if shuffle else 0) | (0x04 if bitshuffle else 0) | \
+        (0 if split else 0x10)
     nblocks = -(-nbytes // blocksize) if nbytes else 0
     body, starts = bytearray(), []
     base = 16 + 4 * nblocks
@@ -115,15 +144,18 @@ def frame(data, typesize, blocksize, comp="lz4", shuffle=True, split=None):
             ne = bs // typesize
             a = np.frombuffer(blk[:ne * typesize], np.uint8).reshape(ne, typesize).T.ravel()
             blk = a.tobytes() + blk[ne * typesize:]
+        elif bitshuffle:
+            blk = bit_shuffle(blk, typesize, version)
         nsplit = typesize if split and bs == blocksize else 1
         neb = bs // nsplit
         starts.append(base + len(body))
         for s in range(nsplit):
             part = blk[s * neb:(s + 1) * neb]
             c = {"blosclz": blosclz_compress, "lz4": lz4_compress,
-                 "zlib": lambda p: zlib.compress(p, 6)}[comp](part)
+                 "zlib": lambda p: zlib.compress(p, 6), "zstd": zstd_compress}[comp](part)
             if len(c) >= len(part):
                 c = part  # stored raw (csize == stream size)
             body += struct.pack("<i", len(c)) + c
-    hdr = struct.pack("<BBBBIII", 2, 1, flags, typesize, nbytes, blocksize, base + len(body))
+    hdr = struct.pack("<BBBBIII", version, 1, flags, typesize, nbytes, blocksize,
+                      base + len(body))
     return hdr + struct.pack("<%di" % nblocks, *starts) + bytes(body)

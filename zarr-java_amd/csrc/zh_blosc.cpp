@@ -6,9 +6,9 @@
 //
 // Frame (16-byte header, little-endian): version, versionlz, flags, typesize, nbytes,
 // blocksize, cbytes; then one int32 start offset per block.  flags: 0x01 byte shuffle,
-// 0x02 memcpyed (raw bytes follow the header), 0x04 bit shuffle (unsupported here), 0x10
-// blocks not split into typesize streams, bits 5-7 compressor (0 BloscLZ, 1 LZ4/LZ4HC,
-// 3 zlib).  A split block is typesize streams of blocksize/typesize bytes; each stream is
+// 0x02 memcpyed (raw bytes follow the header), 0x04 bit shuffle, 0x10 blocks not split into
+// typesize streams, bits 5-7 compressor (0 BloscLZ, 1 LZ4/LZ4HC, 3 zlib, 4 zstd through
+// zh_zstd.cpp; 2 snappy is not available).  A split block is typesize streams of blocksize/typesize bytes; each stream is
 // int32 csize + payload (csize == stream size: stored raw).  The last (short) block is never
 // split.  Pinned by the reference's v2_sample fixtures (BloscLZ split + shuffle, LZ4
 // unsplit + shuffle, memcpyed), tests/test_blosc.py.
@@ -123,6 +123,32 @@ int64_t zlib_block(const uint8_t* s, size_t n, uint8_t* d, size_t cap) {
   return (int64_t)dl;
 }
 
+int64_t zstd_block(const uint8_t* s, size_t n, uint8_t* d, size_t cap) {
+  size_t got = 0;
+  if (zh_zstd_decompress(s, n, nullptr, 0, &got, nullptr, 0) != ZH_OK || got != cap) return -1;
+  if (zh_zstd_decompress(s, n, d, cap, &got, nullptr, 0) != ZH_OK) return -1;
+  return (int64_t)got;
+}
+
+// Bit unshuffle of ne elements (ne % 8 == 0) of ts bytes: the shuffled block holds, for
+// each byte position j and bit k, a row of ne/8 bytes whose bit m of byte q is bit k of byte
+// j of element 8q+m (bitshuffle's bshuf_trans_bit_elem layout, which blosc's bitshuffle()
+// applies per block).
+void bit_unshuffle(const uint8_t* in, uint8_t* out, size_t ne, size_t ts) {
+  const size_t rowb = ne / 8;
+  memset(out, 0, ne * ts);
+  for (size_t j = 0; j < ts; j++)
+    for (size_t k = 0; k < 8; k++) {
+      const uint8_t* row = in + (j * 8 + k) * rowb;
+      for (size_t q = 0; q < rowb; q++) {
+        const uint8_t b = row[q];
+        if (!b) continue;
+        for (size_t m = 0; m < 8; m++)
+          out[(8 * q + m) * ts + j] |= (uint8_t)(((b >> m) & 1) << k);
+      }
+    }
+}
+
 }  // namespace
 
 extern "C" {
@@ -172,13 +198,10 @@ int zh_blosc_decompress(const void* src_v, size_t srclen, void* dst_v, size_t ds
     memcpy(dst, src + 16, nbytes);
     return ZH_OK;
   }
-  if (flags & 0x04) {
-    set_err(err, errlen, "blosc bit-shuffled frames are not supported");
-    return ZH_EUNSUPPORTED;
-  }
+  const bool bitshuf = (flags & 0x04) && !(flags & 0x01);
   const int comp = flags >> 5;
-  if (comp != 0 && comp != 1 && comp != 3) {
-    set_err(err, errlen, "blosc compressor (snappy/zstd) not available on this host");
+  if (comp != 0 && comp != 1 && comp != 3 && comp != 4) {
+    set_err(err, errlen, "blosc compressor (snappy) not available on this host");
     return ZH_EUNSUPPORTED;
   }
   if (nbytes == 0) return ZH_OK;
@@ -193,7 +216,7 @@ int zh_blosc_decompress(const void* src_v, size_t srclen, void* dst_v, size_t ds
       return ZH_EDATA;
     }
     size_t p = rd32(src + 16 + 4 * k);
-    uint8_t* blk = (flags & 0x01) && ts > 1 ? tmp.data() : dst + k * bsize;
+    uint8_t* blk = ((flags & 0x01) && ts > 1) || bitshuf ? tmp.data() : dst + k * bsize;
     for (size_t sidx = 0; sidx < nsplit; sidx++) {
       if (p + 4 > srclen) {
         set_err(err, errlen, "blosc frame truncated");
@@ -214,8 +237,10 @@ int zh_blosc_decompress(const void* src_v, size_t srclen, void* dst_v, size_t ds
         got = blosclz_block(src + p, cs, out, neb);
       } else if (comp == 1) {
         got = lz4_block(src + p, cs, out, neb);
-      } else {
+      } else if (comp == 3) {
         got = zlib_block(src + p, cs, out, neb);
+      } else {
+        got = zstd_block(src + p, cs, out, neb);
       }
       if (got != (int64_t)neb) {
         set_err(err, errlen, "corrupt blosc block");
@@ -223,7 +248,17 @@ int zh_blosc_decompress(const void* src_v, size_t srclen, void* dst_v, size_t ds
       }
       p += cs;
     }
-    if (blk == tmp.data()) {  // byte unshuffle: stream j holds byte j of every element
+    if (bitshuf) {
+      // c-blosc 1.x (frame version <= 2): whole block bit-shuffled when its element count is
+      // a multiple of 8, else stored as is; later formats shuffle the multiple-of-8 prefix and
+      // keep the leftover bytes
+      uint8_t* d = dst + k * bsize;
+      size_t ne = ts ? bs / ts : 0;
+      if (src[0] <= 2 && ne % 8 != 0) ne = 0;
+      ne -= ne % 8;
+      if (ne) bit_unshuffle(tmp.data(), d, ne, ts);
+      memcpy(d + ne * ts, tmp.data() + ne * ts, bs - ne * ts);
+    } else if (blk == tmp.data()) {  // byte unshuffle: stream j holds byte j of every element
       uint8_t* d = dst + k * bsize;
       const size_t ne = bs / ts;
       for (size_t e = 0; e < ne; e++)

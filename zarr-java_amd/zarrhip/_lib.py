@@ -65,6 +65,9 @@ _SIGS = {
     "zh_abi_sizes": (C.c_int, [C.POINTER(C.c_int64), C.c_int]),
     "zh_plan_staged_bytes": (C.c_int64, [P]),
     "zh_blosc_decompress": (C.c_int, [P, SZ, P, SZ, C.POINTER(SZ), C.c_char_p, SZ]),
+    "zh_zstd_decompress": (C.c_int, [P, SZ, P, SZ, C.POINTER(SZ), C.c_char_p, SZ]),
+    "zh_zstd_compress_raw": (C.c_int, [P, SZ, C.c_int, P, SZ, C.POINTER(SZ)]),
+    "zh_xxh64": (U64, [P, SZ, U64]),
     "zh_device_malloc": (C.c_int, [P, SZ, C.POINTER(P)]),
     "zh_device_malloc_ex": (C.c_int, [P, SZ, C.c_uint, C.POINTER(P)]),
     "zh_device_free": (C.c_int, [P, P]),
