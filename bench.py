@@ -1027,9 +1027,12 @@ def main():
         nel *= s
     out_bytes = nel * 4
 
-    # device buffers: decoded region (also the encode source) + one slab for all shards
+    # device buffers: decoded region (also the encode source) + one slab for all shards.  The
+    # region is the decode's write target: it comes from 1 GiB physical chunks mapped in a
+    # coprime order (ZH_MALLOC_SCATTER, DESIGN §4 "Placement"; ZH_MALLOC=0 for hipMalloc)
     t0 = time.perf_counter()
-    out = dev.malloc(out_bytes)
+    out_flags = int(os.environ.get("ZH_MALLOC", str(A.ZH_MALLOC_SCATTER)), 0)
+    out = dev.malloc(out_bytes, out_flags)
     offs, tot = slab_layout(caps)
     shard_slab = dev.malloc(tot)
     dev.synth_fill(out, nel, 4, 0, SEED)
@@ -1096,7 +1099,9 @@ def main():
                    "array_shape": shape, "chunk_shape": [1, 1024, 1024, 1024],
                    "inner_chunk_shape": [1, 32, 32, 32] if meta.chain.sharded else None,
                    "shards": st["shards"], "inner_chunks": st["items"],
-                   "decoded_bytes_per_gpu": out_bytes, "parallelism": f"shard-parallel x{ws}"},
+                   "decoded_bytes_per_gpu": out_bytes, "parallelism": f"shard-parallel x{ws}",
+                   "output_allocation": ("VMM 1 GiB physical chunks, coprime order"
+                                         if out_flags & A.ZH_MALLOC_SCATTER else "hipMalloc")},
         "roofline": roofline,
         "cpu_baseline": cpu,
     }

@@ -290,15 +290,17 @@ int zh_array_write_host(zh_ctx* ctx, const zh_array_meta* meta, const void* src_
  * out[0..3] = zh_codec_chain, zh_array_meta, zh_chunk_src, zh_chunk_dst.  Returns 4. */
 int zh_abi_sizes(int64_t* out, int n);
 int zh_device_malloc(zh_ctx* ctx, size_t bytes, void** out);
-/* Allocation flags for zh_device_malloc_ex.  ZH_MALLOC_CONTIGUOUS asks for physically
- * contiguous HBM (hipDeviceMallocContiguous): the scattered row/tile writes of the decode
- * kernels are sensitive to the allocation's physical fragmentation (TLB reach), while plain
- * copies are not (DESIGN.md "Placement").  Falls back to hipMalloc unless ZH_MALLOC_REQUIRE. */
+/* Allocation flags for zh_device_malloc_ex.  The write bandwidth a large buffer gets depends
+ * on where its physical memory lands (DESIGN.md §4 "Placement": writes only, any access
+ * pattern, not TLB or L2-channel balance).  ZH_MALLOC_CONTIGUOUS asks for physically
+ * contiguous HBM (hipDeviceMallocContiguous).  Falls back to hipMalloc unless
+ * ZH_MALLOC_REQUIRE. */
 #define ZH_MALLOC_CONTIGUOUS 0x1u
 #define ZH_MALLOC_REQUIRE 0x2u
-/* Physical chunks (hipMemCreate, ZH_SCATTER_MB MiB each, default 2) mapped into one virtual
+/* Physical chunks (hipMemCreate, ZH_SCATTER_MB MiB each, default 1024) mapped into one virtual
  * range in a coprime-stride order, so that virtually adjacent chunks are not physically
- * adjacent (DESIGN.md "Placement").  Freed by zh_device_free. */
+ * adjacent: the decode's output arena in bench.py (DESIGN.md §4 "Placement": mean +5.6 % over
+ * hipMalloc on 18 buffers, 3 boxes).  Freed by zh_device_free. */
 #define ZH_MALLOC_SCATTER 0x4u
 int zh_device_malloc_ex(zh_ctx* ctx, size_t bytes, unsigned flags, void** out);
 int zh_device_free(zh_ctx* ctx, void* ptr);

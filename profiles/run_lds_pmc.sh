@@ -19,9 +19,9 @@ step() {  # name, timeout, cmd...
   if [ $rc -ne 0 ]; then exit $rc; fi
 }
 step trace_c4 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace_c4" -o run -- \
-  python3 "$R/bench.py" --config c4 --steps 5 --warmup 2 --no-cpu-baseline
+  python3 "$R/bench.py" --config c4 --steps 5 --warmup 2 --no-cpu-baseline --no-extras
 for cfg in c4 c4crc; do
   step lds_$cfg 120 rocprofv3 --pmc SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_LDS SQ_WAVES \
     --output-format csv -d "$OUT/lds_$cfg" -o run -- \
-    python3 "$R/bench.py" --config $cfg --steps 1 --warmup 1 --no-cpu-baseline
+    python3 "$R/bench.py" --config $cfg --steps 1 --warmup 1 --no-cpu-baseline --no-extras
 done

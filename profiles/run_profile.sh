@@ -20,9 +20,9 @@ step() {  # name, timeout, cmd...
 }
 for cfg in ${CONFIGS:-c3 c4 c2}; do
   step trace_$cfg 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace_$cfg" -o run -- \
-    python3 "$R/bench.py" --config $cfg --steps 5 --warmup 2 --no-cpu-baseline
+    python3 "$R/bench.py" --config $cfg --steps 5 --warmup 2 --no-cpu-baseline --no-extras
   step pmc_fetch_$cfg 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch_$cfg" -o run -- \
-    python3 "$R/bench.py" --config $cfg --steps 2 --warmup 1 --no-cpu-baseline
+    python3 "$R/bench.py" --config $cfg --steps 2 --warmup 1 --no-cpu-baseline --no-extras
   step pmc_write_$cfg 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write_$cfg" -o run -- \
-    python3 "$R/bench.py" --config $cfg --steps 2 --warmup 1 --no-cpu-baseline
+    python3 "$R/bench.py" --config $cfg --steps 2 --warmup 1 --no-cpu-baseline --no-extras
 done

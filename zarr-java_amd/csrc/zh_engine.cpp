@@ -2691,7 +2691,8 @@ int scatter_malloc(int device, size_t bytes, void** out) {
   if (hipMemGetAllocationGranularity(&gran, &prop, hipMemAllocationGranularityRecommended) !=
           hipSuccess || gran == 0)
     return ZH_EHIP;
-  size_t chunk = (size_t)std::max(1, env_int("ZH_SCATTER_MB", 2)) << 20;
+  size_t chunk = (size_t)std::max(1, env_int("ZH_SCATTER_MB", 1024)) << 20;
+  chunk = std::min(chunk, std::max(bytes, (size_t)1));  // small buffers: one chunk
   chunk = (chunk + gran - 1) / gran * gran;
   const size_t n = std::max<size_t>(1, (bytes + chunk - 1) / chunk);
   ScatterAlloc A;
