@@ -642,7 +642,11 @@ def run_strong(args, dist, A, meta, rank, ws, local):
     full_bytes = 4
     for s in shape:
         full_bytes *= s
-    # the root decodes straight into its slice of the assembled region buffer
+    # the decode's write target: 1 GiB VMM chunks in coprime order, as at N=1 (DESIGN §4
+    # "Placement"); RCCL only ever sees torch-allocated buffers: a send buffer on every rank
+    # and the assembled region on the root, filled by a device copy before the gather
+    out_flags = int(os.environ.get("ZH_MALLOC", str(A.ZH_MALLOC_SCATTER)), 0)
+    out = dev.malloc(out_bytes, out_flags)
     region_t = out_t = None
     if backend == "nccl":
         if rank == 0:
@@ -651,9 +655,6 @@ def run_strong(args, dist, A, meta, rank, ws, local):
             out_t = region_t[base:base + out_bytes]
         else:
             out_t = torch.empty(out_bytes, dtype=torch.uint8, device=f"cuda:{device}")
-        out = out_t.data_ptr()
-    else:
-        out = dev.malloc(out_bytes)
     plan = dev.plan(meta, [where[c] for c in mine], so, ss, A.ZH_SRC_DEVICE | A.ZH_OUT_DEVICE)
     st = plan.stats()
     for _ in range(max(1, args.warmup)):
@@ -690,8 +691,7 @@ def run_strong(args, dist, A, meta, rank, ws, local):
            "kernel_ms_max_over_ranks": round(kern_max, 3), "gather": gather,
            "host_terminated": host_out, "info": info}
     plan.close()
-    if backend != "nccl":
-        dev.free(out)
+    dev.free(out)
     del out_t, region_t
     dev.free(slab_buf)
     return res
@@ -711,6 +711,11 @@ def gather_to_root(args, dist, dev, backend, out, out_t, region_t, out_bytes, fu
     if backend == "nccl":
         grp = tdist.new_group(backend="nccl")
         world = tdist.get_world_size(grp)
+        # decoded slab → this rank's RCCL send buffer (the root: its slice of the region)
+        dev.sync()
+        tc = time.perf_counter()
+        dev.memcpy(out_t.data_ptr(), out, out_bytes, 2, None, True)
+        t_stage = dist.max(time.perf_counter() - tc)
 
         def once():
             ops = []
@@ -736,7 +741,9 @@ def gather_to_root(args, dist, dev, backend, out, out_t, region_t, out_bytes, fu
         bad = int(dist.max(bad))
         if bad:
             raise SystemExit(f"gathered region verification FAILED: {bad}")
-        how = "RCCL grouped send/recv into the root's region buffer (xGMI)"
+        how = ("RCCL grouped send/recv into the root's region buffer (xGMI); the decoded "
+               f"slab is first copied to the send buffer ({t_stage * 1e3:.2f} ms, not in "
+               "gather_ms)")
     else:
         world = ws
         host = (C.c_char * out_bytes)()

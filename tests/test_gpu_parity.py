@@ -77,6 +77,26 @@ def test_device_crc_on_reference_index_bytes(dev, loc, stored_crc):
         assert str(e).startswith("unexpected inner chunk byte length")
 
 
+@pytest.mark.parametrize("zext", [24, 20, 22, 17, 32])
+@pytest.mark.parametrize("dsize", [2, 4, 8])
+@pytest.mark.parametrize("sharded", [False, True])
+def test_row_clipped_items(dev, zext, dsize, sharded):
+    """Items cut only along the unit-stride dim (c2's boundary chunks: 512 of 1024 z in
+    bounds) go through the row kernel with narrower rows when the in-bounds prefix is a
+    power-of-two number of 16-B vectors (z 24 / 20 with 16-wide chunks), else the generic
+    kernel (22, 17); regions that end inside the last chunk along z only, too."""
+    shape = [1, 8, 12, zext]
+    if sharded:
+        meta = A.make_meta(shape, [1, 8, 12, 32], dsize, endian=A.ZH_ENDIAN_BIG, sharded=True,
+                           inner_chunk_shape=[1, 4, 4, 16])
+    else:
+        meta = A.make_meta(shape, [1, 4, 4, 16], dsize, endian=A.ZH_ENDIAN_BIG)
+    arr = rand_array(shape, dsize, seed=zext + dsize)
+    roundtrip(dev, meta, arr, [([0, 0, 0, 0], shape), ([0, 0, 0, 0], [1, 8, 12, 8]),
+                               ([0, 4, 0, 0], [1, 4, 12, min(zext, 20)]),
+                               ([0, 1, 0, 0], [1, 7, 12, zext])])
+
+
 @pytest.mark.parametrize("dsize", [1, 2, 4, 8])
 @pytest.mark.parametrize("endian", [A.ZH_ENDIAN_LITTLE, A.ZH_ENDIAN_BIG])
 def test_unsharded_bytes(dev, dsize, endian):

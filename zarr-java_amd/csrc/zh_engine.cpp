@@ -118,6 +118,20 @@ uint32_t gf2_xpow8n(uint64_t n) {
   return p;
 }
 
+// The tile kernels' fused chunk CRC: when every unit u + kTG (the same lane's next group)
+// ends a constant Δ bytes after unit u, a lane folds its groups as r = r·x^(8Δ) ⊕ acc and
+// multiplies by its last unit's K once per piece; returns x^(8Δ) (0 = irregular layout,
+// the kernel then multiplies every group by its K).
+uint32_t tile_crc_step(const std::vector<int64_t>& ends) {
+  constexpr size_t kGroup = 8;  // kTG in zh_kernels.hip
+  if (ends.size() <= kGroup) return 0;
+  const int64_t delta = ends[kGroup] - ends[0];
+  if (delta <= 0) return 0;
+  for (size_t u = 0; u + kGroup < ends.size(); u++)
+    if (ends[u + kGroup] - ends[u] != delta) return 0;
+  return gf2_xpow8n((uint64_t)delta);
+}
+
 // ---- IndexingUtils (M/utils/IndexingUtils.java) ----
 int64_t chunk_coords(int n, const int32_t* chunk, const int64_t* off, const int64_t* shp,
                      int64_t* start, int64_t* count) {
@@ -1079,15 +1093,19 @@ int zh_plan_create(zh_ctx* ctx, const zh_array_meta* m, const zh_chunk_src* chun
   const bool tile_crc =
       c.inner_crc32c && items > 0 && p->tile_mode && p->args.fast_mode == kFastTileTable &&
       p->args.tile_variant == 1 && env_int("ZH_CRC_FUSE", 1) != 0 &&
-      ((int64_t)p->args.fast_n * 8 + 15) / 16 * 16 + 8 * 1057 * 4 + 12 * 256 * 4 +
+      ((int64_t)p->args.fast_n * 8 + 15) / 16 * 16 + 8 * 1057 * 4 + 16 * 256 * 4 +
               (int64_t)p->args.fast_n * 4 <= 65536;
+  p->args.crc_tile_step = 0;
   if (tile_crc) {
     const ScatterArgs& g = p->args;
     const int64_t L = g.inner_nbytes, s_fd = g.pstride[g.fd];
+    std::vector<int64_t> ends;
     for (int32_t u = 0; u < g.fast_n; u++) {
       const int64_t end = 4 * (int64_t)tab[2 * (size_t)u] + 4 * 31 * s_fd + 128;
+      ends.push_back(end);
       tab.push_back(gf2_xpow8n((uint64_t)(L - end)));
     }
+    p->args.crc_tile_step = tile_crc_step(ends);
   }
   // All plan tables in one allocation, the uploaded ones (shards, CRC jobs, zeroed CRC
   // partials + completion counters, fast-path table) as one prefix in one copy: a one-shot
@@ -2166,14 +2184,18 @@ static int array_write_fast(zh_ctx* ctx, const zh_array_meta* m, ScatterArgs a,
   const bool tile_crc =
       c.inner_crc32c && tile_mode && v.fast_mode == kFastTileTable &&
       env_int("ZH_CRC_FUSE", 1) != 0 &&
-      ((int64_t)v.fast_n * 8 + 15) / 16 * 16 + 8 * 1057 * 4 + 12 * 256 * 4 +
+      ((int64_t)v.fast_n * 8 + 15) / 16 * 16 + 8 * 1057 * 4 + 16 * 256 * 4 +
               (int64_t)v.fast_n * 4 <= 65536;
+  v.crc_tile_step = 0;
   if (tile_crc) {
     const int64_t L = a.inner_nbytes, d_fs = v.rstride[v.fs];
+    std::vector<int64_t> ends;
     for (int32_t u = 0; u < v.fast_n; u++) {
       const int64_t end = 4 * (int64_t)tab[2 * (size_t)u + 1] + 4 * 31 * d_fs + 128;
+      ends.push_back(end);
       tab.push_back(gf2_xpow8n((uint64_t)(L - end)));
     }
+    v.crc_tile_step = tile_crc_step(ends);
   }
   const int64_t cspan = tile_crc ? a.inner_nbytes
                                  : (crc_fuse ? a.inner_nbytes / pieces : (int64_t)kCrcSpan);

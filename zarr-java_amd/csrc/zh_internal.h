@@ -69,7 +69,11 @@ struct DevShard {
 // by the scatter kernel, one item ahead of use.
 enum : int32_t { kFastNone = 0, kFastRowArith = 1, kFastRowTable = 2, kFastTileTable = 3 };
 enum : uint32_t { kDescFullCopy = 0, kDescFullFill = 1, kDescClip = 2, kDescSkip = 3,
-                  kDescModeMask = 0xFF, kDescFast = 0x100 };
+                  kDescModeMask = 0xFF, kDescFast = 0x100,
+                  // kDescClip copy cut only along the unit-stride dim (rows keep their start,
+                  // a 16-byte-multiple, power-of-two-vector prefix is in bounds): the row
+                  // kernel takes it with log2(vectors per row) in ItemDesc.fill
+                  kDescClipRow = 0x200 };
 struct ItemDesc {
   uint64_t src;   // absolute address of the inner chunk's bytes (kDescFullCopy)
   int64_t d0;     // destination element offset of the inner chunk origin
@@ -129,6 +133,9 @@ struct ScatterArgs {
                                 // end, per-unit shifts after the (src, dst) pairs of fast_tab)
   uint32_t* crc_partials;       // raw CRC registers, XOR-accumulated: per item (rows) or per
                                 // chunk (tiles)
+  uint32_t crc_tile_step;       // tile CRC: x^(8Δ) when unit u + kTG ends Δ bytes after unit u
+                                // for every u (a lane then folds its groups with one table
+                                // shift instead of a multiply per group); 0 = irregular
 };
 
 // Chunk-payload CRC-32C pass (inner crc32c codec): one workgroup per (item, 64 KiB span) of

@@ -631,7 +631,8 @@ __device__ __forceinline__ ItemDesc resolve_one(const ScatterArgs& a, int64_t ci
       j = q;
     }
   }
-  bool full = true;
+  bool full = true, row_clip = true;  // row_clip: cut only along the unit-stride dim
+  int32_t hi_f = 0;
   int64_t d0 = S.out_base, lin = 0;
 #pragma unroll
   for (int d = 0; d < kMaxDims; d++) {
@@ -640,6 +641,8 @@ __device__ __forceinline__ ItemDesc resolve_one(const ScatterArgs& a, int64_t ci
     const int32_t lo = max(io, S.part_lo[d]) - io;
     const int32_t hi = min(io + a.inner[d], S.part_hi[d]) - io;
     full &= lo == 0 && hi == a.inner[d];
+    row_clip &= lo == 0 && (d == a.fs || hi == a.inner[d]);
+    if (d == a.fs) hi_f = hi;
     d0 += (int64_t)(io + lo - S.part_lo[d]) * a.rstride[d];
     lin += (int64_t)ic[d] * a.cps_stride[d];
   }
@@ -673,6 +676,18 @@ __device__ __forceinline__ ItemDesc resolve_one(const ScatterArgs& a, int64_t ci
   }
   D.src = (uint64_t)(uintptr_t)src;
   D.kind = full ? kDescFullCopy : kDescClip;
+  if (!full && row_clip && !a.tile && a.crc_extra == 0 &&
+      (a.fast_mode == kFastRowArith || a.fast_mode == kFastRowTable)) {
+    // e.g. c2's boundary chunks (512 of 1024 z in bounds): the row kernel moves the row
+    // prefix with the lanes remapped to its width (the chunk CRC, when fused, needs whole
+    // payload rows: crc_extra == 0 only)
+    const int64_t vb = (int64_t)hi_f * a.dsize;
+    const int64_t vpr = vb / 16;
+    if (vb % 16 == 0 && vpr > 0 && (vpr & (vpr - 1)) == 0 && vpr <= (1 << a.fast_vpr_shift)) {
+      D.kind |= kDescClipRow;
+      D.fill = (uint64_t)(63 - __clzll((unsigned long long)vpr));
+    }
+  }
   return D;
 }
 
@@ -680,7 +695,10 @@ __device__ __forceinline__ ItemDesc resolve_one(const ScatterArgs& a, int64_t ci
 // table path moves uint32 copies only)
 __device__ __forceinline__ bool is_fast(const ScatterArgs& a, const ItemDesc& D) {
   const uint32_t mode = D.kind & kDescModeMask;
-  if (a.fast_mode == kFastNone || (mode != kDescFullCopy && mode != kDescFullFill)) return false;
+  const bool row_clip = mode == kDescClip && (D.kind & kDescClipRow);
+  if (a.fast_mode == kFastNone ||
+      (mode != kDescFullCopy && mode != kDescFullFill && !row_clip))
+    return false;
   if ((((uintptr_t)a.region) + (uint64_t)D.d0 * a.dsize) & 15) return false;
   if (mode == kDescFullCopy && (D.src & 3)) return false;  // dword-aligned sources suffice
   if (a.tile && (a.dsize != 4 || mode != kDescFullCopy)) return false;
@@ -1003,10 +1021,12 @@ __global__ __launch_bounds__(kBlock) void decode_rows_kernel(ScatterArgs a) {
     kfull = g_crc.kfull[threadIdx.x];
   }
   __syncthreads();
-  const int vs = a.fast_vpr_shift;
-  const uint32_t col = (threadIdx.x & ((1u << vs) - 1)) * 16;
-  const uint32_t lr = threadIdx.x >> vs;
-  const uint32_t rstep = kBlock >> vs;
+  // lane geometry: one 16-byte column per lane, rows per step = kBlock / vectors per row;
+  // per item, since a row-clipped item (kDescClipRow) moves narrower rows
+  int vs = a.fast_vpr_shift;
+  uint32_t col = (threadIdx.x & ((1u << vs) - 1)) * 16;
+  uint32_t lr = threadIdx.x >> vs;
+  uint32_t rstep = kBlock >> vs;
   const uint32_t nrows = (uint32_t)a.fast_rows, pieces = 1u << a.piece_shift;
   const uint32_t pmask = pieces - 1;
   const int64_t total = a.total_items;
@@ -1039,6 +1059,15 @@ __global__ __launch_bounds__(kBlock) void decode_rows_kernel(ScatterArgs a) {
     const uint32_t piece = (uint32_t)pitem(a, item) & pmask;
     rbase = (uint32_t)(((uint64_t)nrows * piece) / pieces);
     r1 = (uint32_t)(((uint64_t)nrows * (piece + 1)) / pieces);
+    if constexpr (!FLAGS && !CRC) {
+      const int v = (D.kind & kDescClipRow) ? (int)D.fill : a.fast_vpr_shift;
+      if (v != vs) {  // uniform: the whole block moves to the item's row width
+        vs = v;
+        col = (threadIdx.x & ((1u << vs) - 1)) * 16;
+        lr = threadIdx.x >> vs;
+        rstep = kBlock >> vs;
+      }
+    }
     src = (const uint8_t*)(uintptr_t)D.src + col;
     dst = a.region + D.d0 * DS + col;
     fill = (D.kind & kDescModeMask) == kDescFullFill;
@@ -1141,12 +1170,20 @@ __global__ __launch_bounds__(kBlock) void decode_rows_kernel(ScatterArgs a) {
 // L − P_7 − 16 = (L − E_u) + B_lane, E_u = the end of unit u's last payload row.  The host
 // table gives K[u] = x^(8(L − E_u)); the caller applies the lane constant x^(8·B_lane) once
 // per piece.  Returns the lane's share (zero without CRC).
+//
+// The lane's vector contributions c_k = upd16(0, v_k) are independent (no chain through the
+// register: 16 lookups each); the register then folds them as acc = shift_{G+16}(acc) ⊕ c_k
+// (S holds the shift by G + 16 bytes: upd16(c, v) = c·x^128 ⊕ upd16(0, v)), so the serial
+// chain per vector is 4 lookups.  With a regular unit layout (crc_tile_step = x^(8Δ), host
+// checked) the lane folds its groups as r = shift_Δ(r) ⊕ acc (table SD) and multiplies by its
+// last unit's K once per piece, instead of one GF(2) multiply per group.
 template <int NT, bool CRC, bool FLAGS = false>
 __device__ __forceinline__ uint32_t fast_tiles_rows(const ScatterArgs& a, const uint2* tab,
                                                     const uint8_t* src, uint8_t* dst,
                                                     uint32_t piece, uint32_t* lds,
                                                     const uint32_t (*T)[256],
                                                     const uint32_t (*S)[256],
+                                                    const uint32_t (*SD)[256],
                                                     const uint32_t* K, bool& differs) {
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int t = lane >> 3, g = lane & 7;
@@ -1155,7 +1192,9 @@ __device__ __forceinline__ uint32_t fast_tiles_rows(const ScatterArgs& a, const 
   const uint32_t u0 = (uint32_t)(((uint64_t)units * piece) / pieces);
   const uint32_t u1 = (uint32_t)(((uint64_t)units * (piece + 1)) / pieces);
   uint32_t* mine = lds + t * kTilePitch;
-  uint32_t share = 0;
+  uint32_t share = 0, run = 0;
+  uint32_t ulast = ~0u;  // the lane's last live unit (regular layout: one K multiply)
+  const bool regular = CRC && a.crc_tile_step != 0;
   uint4 x[8];
   auto load = [&](uint32_t ub) {
     const uint32_t u = ub + t;
@@ -1208,7 +1247,8 @@ __device__ __forceinline__ uint32_t fast_tiles_rows(const ScatterArgs& a, const 
         st16s<(NT & 2) != 0>(base + (size_t)r * d_fs * 4, y);
         if constexpr (CRC && FLAGS) {  // the stored rows have the decode loads' geometry
           const v4u w = {y.x, y.y, y.z, y.w};
-          eacc = crc_upd16(k ? crc_shift_tab(eacc, S) : eacc, w, T);
+          const uint32_t ck = crc_upd16(0u, w, T);
+          eacc = k ? crc_shift_tab(eacc, S) ^ ck : ck;
         }
       }
     }
@@ -1217,16 +1257,23 @@ __device__ __forceinline__ uint32_t fast_tiles_rows(const ScatterArgs& a, const 
         uint32_t acc = eacc;
         if constexpr (!FLAGS) {
 #pragma unroll
-          for (int k = 0; k < 8; k++) {
+          for (int k = 0; k < 8; k++) {  // c_k does not depend on the register
             const v4u w = {xc[k].x, xc[k].y, xc[k].z, xc[k].w};
-            acc = crc_upd16(k ? crc_shift_tab(acc, S) : acc, w, T);
+            const uint32_t ck = crc_upd16(0u, w, T);
+            acc = k ? crc_shift_tab(acc, S) ^ ck : ck;
           }
         }
-        share ^= multmodp(K[ub + t], acc);
+        if (regular) {
+          run = (ulast == ~0u ? 0u : crc_shift_tab(run, SD)) ^ acc;
+          ulast = ub + t;
+        } else {
+          share ^= multmodp(K[ub + t], acc);
+        }
       }
     }
     __syncthreads();
   }
+  if (regular && ulast != ~0u) share = multmodp(K[ulast], run);
   return share;
 }
 
@@ -1234,8 +1281,8 @@ __device__ __forceinline__ uint32_t fast_tiles_rows(const ScatterArgs& a, const 
 // origins come from the LDS table.  CRC: the chunk CRC is fused (row-interleaved variant);
 // each wave XORs its lanes' shares, already shifted to the payload end, into the chunk's
 // partial, which data_crc_finalize_kernel compares with the stored value.
-template <int NT, int VARIANT, bool CRC = false, bool FLAGS = false>
-__global__ __launch_bounds__(kBlock) void decode_tiles_kernel(ScatterArgs a) {
+template <int NT, int VARIANT, bool CRC, bool FLAGS>
+__device__ __forceinline__ void decode_tiles_body(const ScatterArgs& a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   uint2* tab = reinterpret_cast<uint2*>(smem);
   uint8_t* after_tab = smem + (((size_t)a.fast_n * 8 + 15) & ~(size_t)15);
@@ -1244,21 +1291,27 @@ __global__ __launch_bounds__(kBlock) void decode_tiles_kernel(ScatterArgs a) {
     tab[i] = reinterpret_cast<const uint2*>(a.fast_tab)[i];
   uint32_t(*T)[256] = nullptr;
   uint32_t(*S)[256] = nullptr;
+  uint32_t(*SD)[256] = nullptr;
   uint32_t* K = nullptr;
   uint32_t kb = 0;
   if constexpr (CRC) {
-    // slicing tables, the zero-shift by the row gap G, the per-unit end shifts (host table
-    // after the (src, dst) pairs) and this lane's constant x^(8·B_lane)
+    // slicing tables, the shift by the row pitch G + 16, the group step Δ, the per-unit end
+    // shifts (host table after the (src, dst) pairs) and this lane's constant x^(8·B_lane)
     T = reinterpret_cast<uint32_t(*)[256]>(after_tab + (size_t)kTG * kTilePitch * 4);
     S = T + 8;
-    K = reinterpret_cast<uint32_t*>(S + 4);
+    SD = S + 4;
+    K = reinterpret_cast<uint32_t*>(SD + 4);
     init_crc_tables(T);
     // payload row stride of the lane's vectors: the loaded rows (decode) or, on the encode
     // view, the stored rows (the same lane/row geometry on the destination side)
     const int64_t s_fd = FLAGS ? a.rstride[a.fs] : a.pstride[a.fd];
-    const uint32_t kg = x2nmodp((uint64_t)(4 * s_fd - 16), 3);
+    const uint32_t kg = x2nmodp((uint64_t)(4 * s_fd), 3);
 #pragma unroll
-    for (int b = 0; b < 4; b++) S[b][threadIdx.x] = multmodp(kg, (uint32_t)threadIdx.x << (8 * b));
+    for (int b = 0; b < 4; b++) {
+      S[b][threadIdx.x] = multmodp(kg, (uint32_t)threadIdx.x << (8 * b));
+      SD[b][threadIdx.x] =
+          a.crc_tile_step ? multmodp(a.crc_tile_step, (uint32_t)threadIdx.x << (8 * b)) : 0u;
+    }
     for (int i = threadIdx.x; i < a.fast_n; i += kBlock) K[i] = a.fast_tab[2 * a.fast_n + i];
     const int w = threadIdx.x >> 6, g = threadIdx.x & 7;
     kb = x2nmodp((uint64_t)(4 * (24 - 8 * w) * s_fd + 112 - 16 * g), 3);
@@ -1282,8 +1335,8 @@ __global__ __launch_bounds__(kBlock) void decode_tiles_kernel(ScatterArgs a) {
         const int64_t pi = pitem(a, item);
         bool differs = false;
         const uint32_t share = fast_tiles_rows<NT, CRC, FLAGS>(
-            a, tab, src, dst, (uint32_t)pi & pmask, reinterpret_cast<uint32_t*>(tile), T, S, K,
-            differs);
+            a, tab, src, dst, (uint32_t)pi & pmask, reinterpret_cast<uint32_t*>(tile), T, S, SD,
+            K, differs);
         if constexpr (FLAGS) {
           if (__ballot(differs) != 0 && (threadIdx.x & 63) == 0) a.flags[pi >> a.piece_shift] = 1;
         }
@@ -1297,6 +1350,19 @@ __global__ __launch_bounds__(kBlock) void decode_tiles_kernel(ScatterArgs a) {
     }
     D = Dn;
   }
+}
+
+template <int NT, int VARIANT, bool CRC = false, bool FLAGS = false>
+__global__ __launch_bounds__(kBlock) void decode_tiles_kernel(ScatterArgs a) {
+  decode_tiles_body<NT, VARIANT, CRC, FLAGS>(a);
+}
+
+// The CRC-fused decode variant held to 3 waves per SIMD (LDS allows 3 blocks of 4 waves per
+// CU; unconstrained it takes 172 VGPRs and runs 2)
+template <int NT, bool FLAGS>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3)))
+void decode_tiles_crc_w3_kernel(ScatterArgs a) {
+  decode_tiles_body<NT, 1, true, FLAGS>(a);
 }
 
 // decode, slow kernel: the items the resolve kernel listed (clipped by the region,
@@ -2096,9 +2162,15 @@ static void launch_scatter_ds(const ScatterArgs& a, int tile, int enc, int grid,
         lds += v == 0 ? (size_t)kFastTPB * 32 * 33 * 4 : (size_t)kTG * kTilePitch * 4;
         const bool ntx = nt == 3;
         if (v == 1 && a.crc_fused) {
-          lds += 12 * 256 * 4 + (size_t)a.fast_n * 4;  // T[8][256] + S[4][256] + K[fast_n]
-          if (ntx) hipLaunchKernelGGL((decode_tiles_kernel<3, 1, true>), dim3(grid), dim3(kBlock), lds, s, a);
-          else hipLaunchKernelGGL((decode_tiles_kernel<0, 1, true>), dim3(grid), dim3(kBlock), lds, s, a);
+          lds += 16 * 256 * 4 + (size_t)a.fast_n * 4;  // T[8][256] + S, SD[4][256] + K[fast_n]
+          static const bool w3 = [] {  // ZH_CRC_W3=0: the unconstrained variant (A/B)
+            const char* e = getenv("ZH_CRC_W3");
+            return !(e && e[0] == '0');
+          }();
+          if (!w3)
+            hipLaunchKernelGGL((decode_tiles_kernel<3, 1, true>), dim3(grid), dim3(kBlock), lds, s, a);
+          else if (ntx) hipLaunchKernelGGL((decode_tiles_crc_w3_kernel<3, false>), dim3(grid), dim3(kBlock), lds, s, a);
+          else hipLaunchKernelGGL((decode_tiles_crc_w3_kernel<0, false>), dim3(grid), dim3(kBlock), lds, s, a);
         } else if (v == 1) {
           if (ntx) hipLaunchKernelGGL((decode_tiles_kernel<3, 1>), dim3(grid), dim3(kBlock), lds, s, a);
           else hipLaunchKernelGGL((decode_tiles_kernel<0, 1>), dim3(grid), dim3(kBlock), lds, s, a);
@@ -2169,7 +2241,7 @@ static void launch_encode_fast_ds(const ScatterArgs& v, int grid, int deep, hipS
       const size_t l = lds + (size_t)kTG * kTilePitch * 4;
       if (v.crc_fused) {  // chunk crc32c of the stored payload: tables + per-unit shifts
         hipLaunchKernelGGL((decode_tiles_kernel<3, 1, true, true>), dim3(grid), dim3(kBlock),
-                           l + 12 * 256 * 4 + (size_t)v.fast_n * 4, s, v);
+                           l + 16 * 256 * 4 + (size_t)v.fast_n * 4, s, v);
         return;
       }
       switch (v.nt) {
