@@ -926,6 +926,74 @@ def extra_config(dev, A, L, cfg, out, shape, steps, slab=None):
     return res, (buf, cap)
 
 
+def store_inclusive(dev, A, shard_slab, offs, sizes, coords, scratch):
+    """core.Array.read from a FilesystemStore on tmpfs through the Python mirror of the
+    reference's Array (zarrhip.Array.read: store reads of the shard files — whole shards, or
+    the index + the referenced inner-chunk ranges of a partly covered shard
+    (StoreHandleDataProvider) — then one zh_array_read: pageable H2D, decode, D2H into a
+    numpy array).  Region 1: shards (0,0,0,0) and (0,0,0,1), [1,1024,1024,1536] (6 GiB out);
+    region 2: BASELINE.md §3's sub-shard read [1,1024,1024,512] (the CPU baseline's
+    workload).  Every element of region 1 is verified against the generator."""
+    import shutil
+    import numpy as np
+    import zarrhip as z
+    want = [(0, 0, 0, 0), (0, 0, 0, 1)]
+    pos = {c: i for i, c in enumerate(coords)}
+    need = sum(sizes[pos[c]] for c in want)
+    d = _store_dir(need + (8 << 30))
+    if d is None:
+        return {"skipped": "no tmpfs room for the two shard files"}
+    base = os.path.join(d, f"zh_store_{os.getpid()}")
+    res = {}
+    try:
+        m = (z.ArrayMetadataBuilder().withShape(1, 4096, 4096, 1536)
+             .withDataType(z.DataType.UINT32).withChunkShape(1, 1024, 1024, 1024).withFillValue(0)
+             .withCodecs(lambda c: c.withSharding(
+                 [1, 32, 32, 32], lambda c1: c1.withTranspose([0, 3, 2, 1]).withBytes("BIG")))
+             .build())
+        z.Array.create(z.FilesystemStore(base).resolve("c4"), m)
+        pin = dev.malloc_pinned(max(sizes[pos[c]] for c in want))
+        for c in want:
+            i = pos[c]
+            path = os.path.join(base, "c4", "c", *map(str, c))
+            os.makedirs(os.path.dirname(path), exist_ok=True)
+            dev.memcpy(pin, shard_slab + offs[i], sizes[i], 1, None, True)
+            with open(path, "wb") as f:
+                f.write((C.c_char * sizes[i]).from_address(pin))
+        dev.free_pinned(pin)
+        arr = z.Array.open(z.FilesystemStore(base).resolve("c4"))
+        shape = [1, 4096, 4096, 1536]
+        for name, off, shp, reps in (("two_shards", [0, 0, 0, 0], [1, 1024, 1024, 1536], 2),
+                                     ("sub_shard", [0, 0, 0, 512], [1, 1024, 1024, 512], 3)):
+            ts, parts = [], []
+            got = None
+            for _ in range(reps):
+                del got  # the previous result's pages go back outside the timed call
+                arr.staged_bytes = 0
+                t0 = time.perf_counter()
+                got = arr.read(off, shp)
+                ts.append(time.perf_counter() - t0)
+                parts.append(arr.last_read_timing)
+            nb = got.nbytes
+            k = ts.index(min(ts))
+            r = {"region_offset": off, "region_shape": shp, "ms_min": round(min(ts) * 1e3, 1),
+                 "value": round(nb / min(ts) / GiB, 2), "unit": "GiB/s",
+                 "store_stage_ms": round(parts[k]["stage_s"] * 1e3, 1),
+                 "zh_array_read_ms": round(parts[k]["device_s"] * 1e3, 1),
+                 "staged_bytes": arr.staged_bytes}
+            if name == "two_shards":
+                dev.memcpy(scratch, got.ctypes.data, nb, 0, None, True)
+                r["verify_mismatches"] = int(dev.synth_verify(scratch, shape, off, shp, 4, SEED))
+            res[name] = r
+            del got
+        res["path"] = ("zarrhip.Array.read (Python mirror of core.Array.read) from a "
+                       f"FilesystemStore on {d}: store reads + host index check + one "
+                       "zh_array_read (pageable H2D, decode, D2H into numpy)")
+    finally:
+        shutil.rmtree(base, ignore_errors=True)
+    return res
+
+
 def oneshot_read(dev, A, meta, sources, shape, out, reps=3):
     """zh_array_read of the whole array, device in and out: plan + tables upload + execute +
     status read-back + teardown in one call, as core.Array.read does every call."""
@@ -1126,6 +1194,12 @@ def main():
             log(f"[rank {rank}] {cfg}: {json.dumps(extras[cfg])}")
         shard_slab = slab[0]
         line["extra_configs"] = extras
+        # the store-inclusive read needs the c4 shards again: re-encode them into the slab
+        sizes = dev.array_write(meta, out, [0] * n, shape,
+                                [(shard_slab + o, c) for o, c in zip(offs, caps)])
+        line["store_inclusive"] = store_inclusive(dev, A, shard_slab, offs, sizes, coords,
+                                                  out + (8 << 30))
+        log(f"[rank {rank}] store-inclusive: {json.dumps(line['store_inclusive'])}")
     if plan is not None:
         plan.close()
     dev.free(shard_slab)

@@ -15,6 +15,7 @@ import ctypes as C
 import json
 import os
 import struct
+import time
 import threading
 
 import numpy as np
@@ -55,6 +56,36 @@ def devices():
         return _multi[spec]
 
 
+def _parallel(fn, jobs, width=8):
+    """Run fn over jobs on up to `width` threads (store reads release the GIL)."""
+    if len(jobs) <= 1:
+        for j in jobs:
+            fn(j)
+        return
+    from concurrent.futures import ThreadPoolExecutor
+    with ThreadPoolExecutor(max_workers=min(width, len(jobs))) as ex:
+        for _ in ex.map(fn, jobs):
+            pass
+
+
+def _read_whole(h, piece=64 << 20):
+    """StoreHandle.read() of a whole chunk; stores that report sizes are read in parallel
+    pieces straight into one buffer (a 4 GiB shard is one bytes copy otherwise)."""
+    n = h.size() if hasattr(h, "size") else None
+    if n is None or n <= piece:
+        return h.read()
+    out = np.empty(n, np.uint8)
+    mv = memoryview(out)
+
+    def fetch(o):
+        ln = min(piece, n - o)
+        got = h.read_into(mv[o:o + ln], o, o + ln)
+        if got is None or got < ln:
+            raise ZarrException(f"Could not load byte data of {h!r}")
+    _parallel(fetch, list(range(0, n, piece)))
+    return out
+
+
 def _host_buf(b):
     return (C.c_char * max(1, len(b))).from_buffer_copy(bytes(b) if len(b) else b"\0")
 
@@ -64,6 +95,7 @@ class Array:
         self.storeHandle = store_handle
         self.metadata = metadata
         self.staged_bytes = 0  # encoded bytes read from the store and handed to the device
+        self._stage_lock = threading.Lock()  # chunk loads run on several threads
         self.chain = device_chain(metadata.codecs, metadata.ndim,
                                   metadata.data_type.getByteCount(), metadata.chunk_shape)
         self.zmeta = metadata.to_zh_meta(self.chain)
@@ -121,6 +153,10 @@ class Array:
         for d in range(n):  # M/core/Array.java:386-390
             if offset[d] < 0 or offset[d] + shape[d] > self.metadata.shape[d]:
                 raise ZarrException("Requested data is outside of the array's domain.")
+
+    def _count_staged(self, n):
+        with self._stage_lock:
+            self.staged_bytes += n
 
     def _n_inner(self):
         inner = self.chain.chain["inner_chunk_shape"]
@@ -191,8 +227,9 @@ class Array:
         """StoreHandleDataProvider semantics (ShardingIndexedCodec.java:333-357): read the
         index with one range read, verify its crc32c on the host (same message as the
         device), then read only the inner chunks the part references (adjacent ranges
-        coalesced) and rebuild a compact raw shard for the device: referenced chunks only,
-        their host byte-to-byte codecs already undone, a fresh index (+crc)."""
+        coalesced into one store read each) and build a compact raw shard for the device:
+        the runs side by side, their host byte-to-byte codecs already undone, a fresh index
+        (+crc).  The index is handled as arrays (numpy), not entry by entry."""
         ch = self.chain.chain
         inner = ch["inner_chunk_shape"]
         n_in = self._n_inner()
@@ -205,49 +242,76 @@ class Array:
         if len(idx) < isz:
             raise ZarrException(f"Shard {h!r} is smaller than its index ({isz} bytes).")
         body = self.chain.index_codecs[1].decode(idx) if crc else idx
-        fmt = ">QQ" if ch["index_endian"] == A.ZH_ENDIAN_BIG else "<QQ"
+        edt = np.dtype(">u8" if ch["index_endian"] == A.ZH_ENDIAN_BIG else "<u8")
         cps = [c // i for c, i in zip(self.metadata.chunk_shape, inner)]
-        b0 = [lo // i for lo, i in zip(part_lo, inner)]
-        b1 = [(hi - 1) // i for hi, i in zip(part_hi, inner)]
-        refs = []
-        for ic in np.ndindex(*[e - s + 1 for s, e in zip(b0, b1)]):
-            lin = 0
-            for d, c in enumerate(ic):
-                lin = lin * cps[d] + b0[d] + c
-            off, nb = struct.unpack(fmt, body[16 * lin:16 * lin + 16])
-            if off == 2 ** 64 - 1 or nb == 2 ** 64 - 1:
-                continue
-            refs.append((off, nb, lin))
-        refs.sort()
-        data = {}
-        i = 0
-        while i < len(refs):  # coalesce adjacent ranges into one store read
-            j = i
-            while j + 1 < len(refs) and refs[j + 1][0] == refs[j][0] + refs[j][1]:
-                j += 1
-            s0, s1 = refs[i][0], refs[j][0] + refs[j][1]
-            blob = h.read(s0, s1)
-            if blob is None or len(blob) < s1 - s0:
-                raise ZarrException(f"Could not load byte data for chunk range [{s0}, {s1})")
-            for off, nb, lin in refs[i:j + 1]:
-                raw = blob[off - s0:off - s0 + nb]
-                if self.chain.inner_host_bb:
-                    raw = host_bb_decode(self.chain.inner_host_bb, raw)
-                data[lin] = raw
-            self.staged_bytes += s1 - s0
-            i = j + 1
-        self.staged_bytes += isz
-        ents = [(2 ** 64 - 1, 2 ** 64 - 1)] * n_in
-        payload, pos = [], isz if start else 0
-        for lin in sorted(data):
-            ents[lin] = (pos, len(data[lin]))
-            payload.append(data[lin])
-            pos += len(data[lin])
-        ib = b"".join(struct.pack(fmt, *e) for e in ents)
+        ents = np.frombuffer(body, edt, 2 * n_in).reshape(cps + [2])
+        box = tuple(slice(lo // i, (hi - 1) // i + 1) for lo, hi, i in zip(part_lo, part_hi, inner))
+        lin = np.arange(n_in, dtype=np.int64).reshape(cps)[box].ravel()
+        off = ents[box + (0,)].ravel().astype(np.uint64)
+        nb = ents[box + (1,)].ravel().astype(np.uint64)
+        keep = (off != np.uint64(2 ** 64 - 1)) & (nb != np.uint64(2 ** 64 - 1))
+        lin, off, nb = lin[keep], off[keep].astype(np.int64), nb[keep].astype(np.int64)
+        order = np.argsort(off, kind="stable")
+        lin, off, nb = lin[order], off[order], nb[order]
+        # runs of adjacent ranges: one store read each
+        brk = np.nonzero(off[1:] != off[:-1] + nb[:-1])[0] + 1 if len(off) else np.zeros(0, int)
+        rs = np.concatenate([[0], brk]).astype(np.int64) if len(off) else np.zeros(0, np.int64)
+        re = np.concatenate([brk, [len(off)]]).astype(np.int64) if len(off) else rs
+        new_off = np.full(n_in, 2 ** 64 - 1, np.uint64)
+        new_nb = np.full(n_in, 2 ** 64 - 1, np.uint64)
+
+        def bad(s0, s1):
+            return ZarrException(f"Could not load byte data for chunk range [{s0}, {s1})")
+        if self.chain.inner_host_bb:  # per chunk: undo the host codecs
+            pos = isz if start else 0
+            blobs = []
+            for a, b in zip(rs.tolist(), re.tolist()):
+                s0, s1 = int(off[a]), int(off[b - 1] + nb[b - 1])
+                blob = h.read(s0, s1)
+                if blob is None or len(blob) < s1 - s0:
+                    raise bad(s0, s1)
+                self._count_staged(s1 - s0)
+                for k in range(a, b):
+                    raw = host_bb_decode(self.chain.inner_host_bb,
+                                         blob[int(off[k]) - s0:int(off[k] + nb[k]) - s0])
+                    new_off[lin[k]], new_nb[lin[k]] = pos, len(raw)
+                    blobs.append(raw)
+                    pos += len(raw)
+            pb = b"".join(blobs)
+            out = np.empty(len(pb) + isz, np.uint8)
+            out[isz if start else 0:(isz if start else 0) + len(pb)] = np.frombuffer(pb, np.uint8)
+        else:  # runs side by side in one buffer, each read straight into its place
+            lens = [int(off[b - 1] + nb[b - 1] - off[a]) for a, b in zip(rs.tolist(), re.tolist())]
+            out = np.empty(sum(lens) + isz, np.uint8)
+            mv = memoryview(out)
+            pos = isz if start else 0
+            jobs = []
+            for (a, b), ln in zip(zip(rs.tolist(), re.tolist()), lens):
+                s0 = int(off[a])
+                jobs.append((pos, s0, ln))
+                new_off[lin[a:b]] = (pos + off[a:b] - s0).astype(np.uint64)
+                new_nb[lin[a:b]] = nb[a:b].astype(np.uint64)
+                pos += ln
+
+            def fetch(job):
+                p0, s0, ln = job
+                got = h.read_into(mv[p0:p0 + ln], s0, s0 + ln)
+                if got is None or got < ln:
+                    raise bad(s0, s0 + ln)
+                self._count_staged(ln)
+            _parallel(fetch, jobs)
+        self._count_staged(isz)
+        ib = np.empty((n_in, 2), edt)
+        ib[:, 0], ib[:, 1] = new_off, new_nb
+        ib = ib.tobytes()
         if crc:
             ib = self.chain.index_codecs[1].encode(ib)
-        pb = b"".join(payload)
-        return ib + pb if start else pb + ib
+        ibv = np.frombuffer(ib, np.uint8)
+        if start:
+            out[:isz] = ibv
+        else:
+            out[len(out) - isz:] = ibv
+        return out
 
     def _load_source(self, coords, part_lo=None, part_hi=None):
         h = self._handle(coords)
@@ -259,10 +323,12 @@ class Array:
                 if not h.exists():
                     return None
                 return self._stage_partial(h, part_lo, part_hi)
-        b = h.read()
+        # raw payloads go to the device as they are: parallel reads into one buffer; host
+        # byte-to-byte stages take the store's bytes
+        b = h.read() if (self.chain.host_bb or self.chain.inner_host_bb) else _read_whole(h)
         if b is None:
             return None
-        self.staged_bytes += len(b)
+        self._count_staged(len(b))
         if self.chain.host_bb:
             b = host_bb_decode(self.chain.host_bb, b)
         elif self.chain.inner_host_bb:
@@ -280,14 +346,26 @@ class Array:
         if any(s == 0 for s in shape):
             return np.zeros(shape, dtype=dt)
         coords = self._chunk_coords(offset, shape)
-        sources = []
-        for c in coords:
+        t0 = time.perf_counter()
+
+        def load(c):
             lo = [max(o, ci * cs) - ci * cs for o, ci, cs in zip(offset, c, self.metadata.chunk_shape)]
             hi = [min(o + s, (ci + 1) * cs) - ci * cs
                   for o, s, ci, cs in zip(offset, shape, c, self.metadata.chunk_shape)]
-            sources.append(self._load_source(c, lo, hi))
-        bufs = [(_host_buf(s) if s is not None else None) for s in sources]
-        srcs = [((C.addressof(b), len(s)) if s is not None else (None, 0))
+            return self._load_source(c, lo, hi)
+        if parallel and len(coords) > 1:  # the store reads of the chunks, concurrently
+            # (core.Array.read's parallel stream over chunks, M/core/Array.java:403-407)
+            from concurrent.futures import ThreadPoolExecutor
+            with ThreadPoolExecutor(max_workers=min(8, len(coords))) as ex:
+                sources = list(ex.map(load, coords))
+        else:
+            sources = [load(c) for c in coords]
+        t1 = time.perf_counter()
+        # views of the staged bytes (the library only reads them); an empty but present
+        # chunk keeps a non-null pointer (null = missing key → fill)
+        bufs = [None if s is None else np.frombuffer(s if len(s) else b"\0", np.uint8)
+                for s in sources]
+        srcs = [((int(b.ctypes.data), len(s)) if s is not None else (None, 0))
                 for b, s in zip(bufs, sources)]
         out = np.empty(shape, dtype=dt)
         devs = devices()
@@ -298,6 +376,7 @@ class Array:
                 devs[0].array_read(self.zmeta, srcs, offset, shape, out.ctypes.data, 0)
         except _lib.ZhError as e:
             raise_for(e)
+        self.last_read_timing = {"stage_s": t1 - t0, "device_s": time.perf_counter() - t1}
         return out
 
     def readChunk(self, coords):

@@ -19,6 +19,20 @@ class Store:
     def set(self, keys, data):
         raise NotImplementedError
 
+    def size(self, keys):
+        """Byte length of the key's value, or None when unknown / missing."""
+        return None
+
+    def get_into(self, keys, view, start, end):
+        """get(keys, start, end) written into `view` (a writable memoryview of end - start
+        bytes); returns the bytes written, or None for a missing key.  Stores override it to
+        skip the intermediate buffer."""
+        b = self.get(keys, start, end)
+        if b is None:
+            return None
+        view[:len(b)] = b
+        return len(b)
+
     def delete(self, keys):
         raise NotImplementedError
 
@@ -49,6 +63,26 @@ class FilesystemStore(Store):
                 e = size if end is None else end
                 f.seek(s)
                 return f.read(e - s)
+        except FileNotFoundError:
+            return None
+
+    def size(self, keys):
+        try:
+            return os.stat(self._p(keys)).st_size
+        except FileNotFoundError:
+            return None
+
+    def get_into(self, keys, view, start, end):
+        try:
+            with open(self._p(keys), "rb", buffering=0) as f:
+                f.seek(start)
+                got = 0
+                while got < len(view):
+                    r = f.readinto(view[got:])
+                    if not r:
+                        break
+                    got += r
+                return got
         except FileNotFoundError:
             return None
 
@@ -112,6 +146,12 @@ class StoreHandle:
 
     def read(self, start=None, end=None):
         return self.store.get(self.keys, start, end)
+
+    def read_into(self, view, start, end):
+        return self.store.get_into(self.keys, view, start, end)
+
+    def size(self):
+        return self.store.size(self.keys)
 
     def exists(self):
         return self.store.exists(self.keys)
