@@ -895,7 +895,7 @@ def extra_config(dev, A, L, cfg, out, shape, steps, slab=None):
     if cap < tot:
         if buf:
             dev.free(buf)
-        buf, cap = dev.malloc(tot), tot
+        buf, cap = dev.malloc(tot, int(os.environ.get("ZH_MALLOC", str(A.ZH_MALLOC_SCATTER)), 0)), tot
     sizes = dev.array_write(meta, out, [0] * n, shape, [(buf + o, c) for o, c in zip(offs, caps)])
     plan = dev.plan(meta, [(buf + o, s) for o, s in zip(offs, sizes)], [0] * n, shape,
                     A.ZH_SRC_DEVICE | A.ZH_OUT_DEVICE)
@@ -1109,7 +1109,7 @@ def main():
     out_flags = int(os.environ.get("ZH_MALLOC", str(A.ZH_MALLOC_SCATTER)), 0)
     out = dev.malloc(out_bytes, out_flags)
     offs, tot = slab_layout(caps)
-    shard_slab = dev.malloc(tot)
+    shard_slab = dev.malloc(tot, out_flags)  # the write path's target (--op write)
     dev.synth_fill(out, nel, 4, 0, SEED)
     dev.sync()
     t1 = time.perf_counter()
