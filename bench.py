@@ -482,13 +482,23 @@ def cpu_baseline(dev, A, L, meta, shard_ptr, shard_nbytes, budget_s=12.0):
 # N > 1: one array split over the GPUs (strong scaling)
 # ------------------------------------------------------------------------------------------
 def _mem_available():
+    """Host memory this job may still use: MemAvailable, capped by the cgroup's limit
+    (memory.max − memory.current), which /proc/meminfo does not show."""
+    avail = 0
     try:
         for line in open("/proc/meminfo"):
             if line.startswith("MemAvailable:"):
-                return int(line.split()[1]) * 1024
+                avail = int(line.split()[1]) * 1024
     except OSError:
         pass
-    return 0
+    try:
+        lim = open("/sys/fs/cgroup/memory.max").read().strip()
+        if lim != "max":
+            cur = int(open("/sys/fs/cgroup/memory.current").read().strip())
+            avail = min(avail, int(lim) - cur)
+    except (OSError, ValueError):
+        pass
+    return avail
 
 
 def host_terminated(args, dist, dev, plan, out, out_bytes, shape, so, ss, rank, ws):
