@@ -591,6 +591,28 @@ def host_terminated(args, dist, dev, plan, out, out_bytes, shape, so, ss, rank, 
             "region_bytes": full, "verified": shared}
 
 
+def gpus_shared(dist, device, ndev, ws):
+    """Do two ranks drive the same physical GPU?  Compared by device UUID / PCI address over
+    the process group (a launcher may give each rank one visible device); without either,
+    fewer visible devices than ranks means sharing."""
+    import torch
+    ident = None
+    try:
+        pr = torch.cuda.get_device_properties(device)
+        for attr in ("uuid", "pci_bus_id"):
+            v = getattr(pr, attr, None)
+            if v is not None and str(v):
+                ident = f"{attr}:{v}:{getattr(pr, 'pci_domain_id', '')}:{getattr(pr, 'pci_device_id', '')}"
+                break
+    except Exception:
+        ident = None
+    ids = [None] * ws
+    dist.dist.all_gather_object(ids, ident)
+    if all(i is not None for i in ids):
+        return len(set(ids)) < ws
+    return ndev < ws
+
+
 def visible_devices():
     """GPUs this rank can see (torch.cuda.device_count does not initialise HIP here)."""
     import torch
@@ -609,7 +631,7 @@ def run_strong(args, dist, A, meta, rank, ws, local):
     ndev = visible_devices()
     device = local % max(1, ndev)
     backend = args.gather_backend
-    shared_gpu = ndev < ws
+    shared_gpu = gpus_shared(dist, device, ndev, ws)
     if backend == "nccl" and shared_gpu:
         backend = "gloo"   # rehearsal with several ranks on one GPU: RCCL needs distinct GPUs
     if backend == "nccl":

@@ -37,12 +37,13 @@ def main():
     nel = 1
     for s in shape:
         nel *= s
-    out = dev.malloc(nel * 4)
+    mflags = int(os.environ.get("ZH_MALLOC", str(A.ZH_MALLOC_SCATTER)), 0)  # bench's arena
+    out = dev.malloc(nel * 4, mflags)
     offs, tot = [], 0
     for c in caps:
         offs.append(tot)
         tot += (c + 255) // 256 * 256
-    slab = dev.malloc(tot)
+    slab = dev.malloc(tot, mflags)
     dev.synth_fill(out, nel, 4, 0, bench.SEED)
     sizes = dev.array_write(meta, out, [0] * n, shape, [(slab + o, c) for o, c in zip(offs, caps)])
     plans = {}
@@ -78,7 +79,8 @@ def main():
         med = statistics.median(v)
         rows.append({"blocks_per_cu": g, "nt": nt, "tile_variant": var, "median_ms": round(med, 3),
                      "min_ms": round(min(v), 3), "GiB/s": round(nel * 4 / med * 1e3 / 2**30, 1)})
-    print(json.dumps({"config": cfg, "rounds": rounds, "verify_mismatches": bad, "results": rows}))
+    print(json.dumps({"config": cfg, "rounds": rounds, "malloc_flags": mflags,
+                      "verify_mismatches": bad, "results": rows}))
 
 
 if __name__ == "__main__":
