@@ -1026,6 +1026,65 @@ def store_inclusive(dev, A, shard_slab, offs, sizes, coords, scratch):
     return res
 
 
+def shuffled_variant(dev, A, L, meta, out, shape, slab, offs, sizes, steps, classes=5):
+    """SURVEY §8(d)'s second variant: the same c4 shards with their inner chunks stored out of
+    C order (Q7: the reference appends them in a nondeterministic order), so only the index
+    says where each chunk is.  Chunk rank k moves to class k mod `classes`, each class packed
+    in rank order (one block-gather kernel per shard), then the index entries are rewritten
+    and re-checksummed.  Decoded, verified against the generator, timed like the headline."""
+    import struct
+    import numpy as np
+    n = meta.ndim
+    cb = 4 * 32 * 32 * 32                       # stored inner chunk bytes (c4: 128 KiB)
+    isz = int(L.zh_shard_index_size(C.byref(meta)))
+    tmp = dev.malloc(max(sizes))
+    for o, sz in zip(offs, sizes):
+        nchunk = (sz - isz) // cb
+        base = slab + o
+        starts, pos, src_of = [], 0, []
+        for r in range(classes):
+            cnt = (nchunk - r + classes - 1) // classes if nchunk > r else 0
+            starts.append(pos)
+            src_of.extend(range(r, nchunk, classes))
+            pos += cnt
+        dev.gather_blocks(tmp, base, cb, src_of)      # new position p <- old rank src_of[p]
+        dev.memcpy(base, tmp, nchunk * cb, 2, None, True)
+        ib = bytearray(dev.d2h(base + sz - isz, isz))
+        ent = np.frombuffer(ib, "<u8", count=(isz - 4) // 8).reshape(-1, 2).copy()
+        live = ent[:, 0] != np.uint64(2 ** 64 - 1)
+        rank = (ent[live, 0] // np.uint64(cb)).astype(np.int64)
+        newpos = np.asarray(starts, np.int64)[rank % classes] + rank // classes
+        ent[live, 0] = (newpos * cb).astype(np.uint64)
+        body = ent.tobytes()
+        crc = L.zh_crc32c(0, body, len(body))
+        dev.h2d(base + sz - isz, body + struct.pack("<I", crc))
+    dev.free(tmp)
+    plan = dev.plan(meta, [(slab + o, sz) for o, sz in zip(offs, sizes)], [0] * n, shape,
+                    A.ZH_SRC_DEVICE | A.ZH_OUT_DEVICE)
+    st = plan.stats()
+    dev.memset(out, 0, st["out_bytes"])
+    plan.execute(out)
+    plan.wait()
+    bad = dev.synth_verify(out, shape, [0] * n, shape, 4, SEED)
+    if bad:
+        raise SystemExit(f"shuffled-order decode verification FAILED: {bad}")
+    plan.set_timing(True)
+    dev.sync()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        plan.execute(out)
+    plan.wait()
+    el = time.perf_counter() - t0
+    roof = roofline_of(plan, st)
+    plan.close()
+    return {"description": f"c4 with each shard's inner chunks stored in {classes} interleaved "
+                           "classes (rank k → class k mod 5), index rewritten: decoding follows "
+                           "the index (Q7)",
+            "value": round(steps * st["out_bytes"] / el / GiB, 2), "unit": "GiB/s",
+            "ms_per_step": round(el * 1e3 / steps, 3), "verified_elements": st["out_bytes"] // 4,
+            "roofline": roof}
+
+
 def oneshot_read(dev, A, meta, sources, shape, out, reps=3):
     """zh_array_read of the whole array, device in and out: plan + tables upload + execute +
     status read-back + teardown in one call, as core.Array.read does every call."""
@@ -1232,6 +1291,9 @@ def main():
         line["store_inclusive"] = store_inclusive(dev, A, shard_slab, offs, sizes, coords,
                                                   out + (8 << 30))
         log(f"[rank {rank}] store-inclusive: {json.dumps(line['store_inclusive'])}")
+        extras["c4shuf"] = shuffled_variant(dev, A, L, meta, out, shape, shard_slab, offs,
+                                            sizes, min(args.steps, 10))
+        log(f"[rank {rank}] c4shuf: {json.dumps(extras['c4shuf'])}")
     if plan is not None:
         plan.close()
     dev.free(shard_slab)

@@ -352,6 +352,12 @@ int zh_zstd_compress_raw(const void* src, size_t srclen, int checksum, void* dst
                          size_t* dstlen);
 uint64_t zh_xxh64(const void* data, size_t len, uint64_t seed);
 
+/* dst block b ← src block src_block[b] (device buffers, blocks of block_bytes, a multiple of
+ * 16; 16-byte aligned; src_block on the host), synchronous: re-lays out encoded shards, e.g.
+ * the bench's shuffled inner-chunk order. */
+int zh_gather_blocks(zh_ctx* ctx, void* dst, const void* src, int64_t block_bytes,
+                     const int64_t* src_block, int64_t n);
+
 /* ---- synthetic data (bench / property tests) -------------------------------------- */
 /* dst[i] = low dtype_size bytes of splitmix64((first + i) ^ seed), i in [0, n). */
 int zh_synth_fill(zh_ctx* ctx, void* dst, int64_t n, int dtype_size, int64_t first,

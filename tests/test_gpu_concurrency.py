@@ -1,0 +1,77 @@
+"""Concurrent codec-path calls (the reference's ForkJoin threads call the sharding codec once
+per shard, M/core/Array.java:403-407): threads decoding different shards through a pool of
+contexts on one GPU (the Java side's ZH_CODEC_CONTEXTS pool, ZarrHip.codecCtx) and through one
+shared context (calls serialise on its mutex) give the oracle's bytes."""
+import ctypes as C
+import threading
+
+import numpy as np
+import pytest
+
+import oracle as O
+from helpers import encode_oracle, rand_array
+from zarrhip import _abi as A
+from zarrhip._lib import DeviceContext, i32arr, i64arr
+
+pytestmark = pytest.mark.gpu
+
+
+def _decode_partial(ctx, meta, shard, off, shp):
+    out = (C.c_char * (int(np.prod(shp)) * 4))()
+    buf = (C.c_char * len(shard)).from_buffer_copy(shard)
+    err = C.create_string_buffer(512)
+    st = ctx.L.zh_sharding_decode_partial(ctx.h, C.byref(meta), buf, len(shard), i64arr(off),
+                                          i32arr(shp), out, 0, None, err, 512)
+    assert st == 0, err.value
+    return np.frombuffer(bytes(out), np.uint32).reshape(shp)
+
+
+@pytest.mark.parametrize("ncontexts", [1, 4])
+def test_threads_decode_shards_concurrently(dev, ncontexts):
+    shape = [1, 64, 64, 64]
+    meta = A.make_meta(shape, [1, 32, 32, 64], 4, endian=A.ZH_ENDIAN_BIG, sharded=True,
+                       inner_chunk_shape=[1, 8, 8, 16], transpose_order=[0, 3, 2, 1])
+    arr = rand_array(shape, 4, seed=31)
+    shards = encode_oracle(meta, arr)
+    smeta = A.zh_array_meta.from_buffer_copy(meta)
+    for d in range(4):
+        smeta.shape[d] = meta.chunk_shape[d]
+    ctxs = [dev] + [DeviceContext(0) for _ in range(ncontexts - 1)]
+    jobs = [(i, [0, 3 * (k % 5), 2 * (k % 7), k % 9], [1, 20, 20, 40])
+            for k, i in enumerate(list(range(len(shards))) * 4)]
+    results, errors = {}, []
+
+    def work(t):
+        try:
+            ctx = ctxs[t % len(ctxs)]
+            for j in range(t, len(jobs), 8):
+                i, off, shp = jobs[j]
+                results[j] = _decode_partial(ctx, smeta, shards[i], off, shp)
+        except Exception as e:  # surfaced below
+            errors.append(e)
+    th = [threading.Thread(target=work, args=(t,)) for t in range(8)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    for c in ctxs[1:]:
+        c.close()
+    assert not errors, errors
+    for j, (i, off, shp) in enumerate(jobs):
+        want = np.frombuffer(O.array_read(smeta, [shards[i]], off, shp), np.uint32).reshape(shp)
+        np.testing.assert_array_equal(results[j], want)
+
+
+def test_gather_blocks(dev):
+    """zh_gather_blocks (the bench's shuffled-layout helper) against numpy indexing."""
+    rng = np.random.default_rng(5)
+    nb, bb = 37, 4096
+    src_h = rng.integers(0, 256, nb * bb, dtype=np.uint8)
+    perm = rng.permutation(nb)
+    src, dst = dev.malloc(nb * bb), dev.malloc(nb * bb)
+    dev.h2d(src, src_h.tobytes())
+    dev.gather_blocks(dst, src, bb, perm.tolist())
+    got = np.frombuffer(dev.d2h(dst, nb * bb), np.uint8).reshape(nb, bb)
+    dev.free(src)
+    dev.free(dst)
+    np.testing.assert_array_equal(got, src_h.reshape(nb, bb)[perm])

@@ -236,6 +236,70 @@ def test_corrupt_offset_rejected(dev):
     assert str(ed.value) == str(eo.value) == "Could not load byte data for chunk [0, 1]"
 
 
+def _shuffle_shard(meta, shard, rng, gap=True, dup=True):
+    """Rewrite one shard with its inner chunks in a random order (Q7: the reference appends
+    them in a nondeterministic order, ShardingIndexedCodec.java:116-147), random gaps between
+    them, and (dup) two index entries sharing one payload; index rewritten with its crc32c."""
+    import struct
+    n = meta.ndim
+    ch = meta.chain
+    cps = 1
+    for d in range(n):
+        cps *= meta.chunk_shape[d] // ch.inner_chunk_shape[d]
+    crc = bool(ch.index_has_crc32c)
+    isz = 16 * cps + (4 if crc else 0)
+    start = ch.index_location == A.ZH_INDEX_START
+    fmt = ">QQ" if ch.index_endian == A.ZH_ENDIAN_BIG else "<QQ"
+    ib = shard[:isz] if start else shard[len(shard) - isz:]
+    ents = [struct.unpack(fmt, ib[16 * k:16 * k + 16]) for k in range(cps)]
+    order = rng.permutation(cps)
+    body, new = bytearray(), [None] * cps
+    base = isz if start else 0
+    for k in order:
+        off, nb = ents[k]
+        if off == 2 ** 64 - 1:
+            new[k] = (off, nb)
+            continue
+        if gap:
+            body += bytes(rng.integers(0, 256, int(rng.integers(0, 40)), dtype=np.uint8))
+        new[k] = (base + len(body), nb)
+        body += shard[off:off + nb]
+    if dup:  # a later entry reuses an earlier payload: same bytes, read twice
+        live = [k for k in range(cps) if new[k][0] != 2 ** 64 - 1]
+        if len(live) >= 2:
+            a, b = live[0], live[1]
+            if shard[ents[a][0]:ents[a][0] + ents[a][1]] == shard[ents[b][0]:ents[b][0] + ents[b][1]]:
+                new[b] = new[a]
+    idx = b"".join(struct.pack(fmt, *e) for e in new)
+    if crc:
+        idx += struct.pack("<I", O.crc32c(idx))
+    return (idx + bytes(body)) if start else (bytes(body) + idx)
+
+
+@pytest.mark.parametrize("loc", [A.ZH_INDEX_END, A.ZH_INDEX_START])
+@pytest.mark.parametrize("order", [None, [0, 3, 2, 1]])
+def test_shuffled_inner_order_is_index_driven(dev, loc, order):
+    """shards whose inner chunks sit in a random order with gaps decode
+    exactly as the C-order shards do — the device follows the index, never the layout."""
+    rng = np.random.default_rng(17)
+    shape = [1, 24, 20, 40]
+    meta = A.make_meta(shape, [1, 16, 16, 32], 4, endian=A.ZH_ENDIAN_BIG, sharded=True,
+                       inner_chunk_shape=[1, 4, 4, 8], transpose_order=order,
+                       index_location=loc)
+    arr = rand_array(shape, 4, seed=23)
+    arr[0, :4, :4, :8] = 0                    # one all-fill inner chunk: missing entry
+    shards = encode_oracle(meta, arr)
+    mixed = [None if s is None else _shuffle_shard(meta, s, rng) for s in shards]
+    for off, shp in [([0, 0, 0, 0], shape), ([0, 3, 5, 7], [1, 18, 13, 30])]:
+        sel = chunk_coords(meta, off, shp)
+        pos = {c: i for i, c in enumerate(chunk_coords(meta, [0] * 4, shape))}
+        src = [mixed[pos[c]] for c in sel]
+        got = device_read(dev, meta, src, off, shp)
+        want = np.frombuffer(O.array_read(meta, src, off, shp), np.uint32).reshape(shp)
+        np.testing.assert_array_equal(got, want)
+        np.testing.assert_array_equal(got, arr[tuple(slice(o, o + s) for o, s in zip(off, shp))])
+
+
 def test_domain_error(dev):
     meta = A.make_meta([8, 8], [4, 4], 4)
     with pytest.raises(ZhError) as ed:

@@ -2922,6 +2922,31 @@ int zh_device_info(zh_ctx* ctx, char* name, size_t namelen, int64_t* total_mem, 
   return ZH_OK;
 }
 
+int zh_gather_blocks(zh_ctx* ctx, void* dst, const void* src, int64_t block_bytes,
+                     const int64_t* src_block, int64_t n) {
+  if (!ctx || !dst || !src || !src_block || n < 0 || block_bytes <= 0 || block_bytes % 16 ||
+      ((uintptr_t)dst | (uintptr_t)src) & 15)
+    return ZH_EINVAL;
+  if (n == 0) return ZH_OK;
+  (void)hipSetDevice(ctx->device);
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  int64_t* d = nullptr;
+  if (hipMalloc((void**)&d, (size_t)n * sizeof(int64_t)) != hipSuccess) {
+    (void)hipGetLastError();
+    return ZH_ENOMEM;
+  }
+  int rc = ZH_OK;
+  if (hipMemcpyAsync(d, src_block, (size_t)n * sizeof(int64_t), hipMemcpyHostToDevice,
+                     ctx->stream) != hipSuccess ||
+      launch_gather_blocks(dst, src, d, n, block_bytes, ctx->stream) != hipSuccess ||
+      hipStreamSynchronize(ctx->stream) != hipSuccess) {
+    (void)hipGetLastError();
+    rc = ZH_EHIP;
+  }
+  (void)hipFree(d);
+  return rc;
+}
+
 int zh_synth_fill(zh_ctx* ctx, void* dst, int64_t n, int dtype_size, int64_t first,
                   uint64_t seed, void* stream) {
   if (!ctx || !dst) return ZH_EINVAL;

@@ -2342,6 +2342,27 @@ hipError_t launch_flags(const ScatterArgs& a, int dsize, int grid, hipStream_t s
   return hipGetLastError();
 }
 
+// dst block b ← src block idx[b] (blocks of bb bytes, bb % 16 == 0, 16-B aligned): one
+// workgroup per block, 16-B vectors (bench / tests: shards re-laid out in another order)
+__global__ __launch_bounds__(kBlock) void gather_blocks_kernel(uint8_t* dst, const uint8_t* src,
+                                                               const int64_t* idx, int64_t n,
+                                                               int64_t bb) {
+  for (int64_t b = blockIdx.x; b < n; b += gridDim.x) {
+    const uint4* s = reinterpret_cast<const uint4*>(src + idx[b] * bb);
+    uint4* d = reinterpret_cast<uint4*>(dst + b * bb);
+    for (int64_t v = threadIdx.x; v < bb / 16; v += kBlock) d[v] = s[v];
+  }
+}
+
+hipError_t launch_gather_blocks(void* dst, const void* src, const int64_t* d_idx, int64_t n,
+                                int64_t bb, hipStream_t stream) {
+  if (n <= 0) return hipSuccess;
+  const int grid = (int)std::min<int64_t>(n, 65536);
+  hipLaunchKernelGGL(gather_blocks_kernel, dim3(grid), dim3(kBlock), 0, stream, (uint8_t*)dst,
+                     (const uint8_t*)src, d_idx, n, bb);
+  return hipGetLastError();
+}
+
 hipError_t launch_synth_fill(void* dst, int64_t n, int dsize, int64_t first, uint64_t seed,
                              hipStream_t stream) {
   if (n <= 0) return hipSuccess;

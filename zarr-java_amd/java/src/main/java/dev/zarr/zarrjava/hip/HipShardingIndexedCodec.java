@@ -38,7 +38,7 @@ public class HipShardingIndexedCodec extends ShardingIndexedCodec {
 
     private Array device(byte[] shard, long[] offset, int[] shape) throws ZarrException {
         Array out = Array.factory(arrayMetadata.dataType.getMA2DataType(), shape);
-        int st = ZarrHip.shardDecodePartial(ZarrHip.ctx(), chain.meta, chain.shape,
+        int st = ZarrHip.shardDecodePartial(ZarrHip.codecCtx(), chain.meta, chain.shape,
                 chain.chunkShape, chain.innerShape, chain.order, chain.fill, shard, offset, shape,
                 out.getStorage());
         return st == 0 ? out : null;

@@ -9,12 +9,23 @@ package dev.zarr.zarrjava.hip;
  * Devices: ZH_DEVICES="0,1,...,7" spreads every region read over those GPUs
  * (zh_array_read_multi: one slab per device, each copied straight into its slice of the
  * result); otherwise ZH_DEVICE (default 0) is the one device.
+ *
+ * The codec path (HipShardingIndexedCodec, one shard per call) is called concurrently by
+ * core.Array.read's ForkJoin threads (M/core/Array.java:403-407).  A zh_ctx serialises its
+ * calls on its own stream, so those threads draw from a pool of ZH_CODEC_CONTEXTS contexts on
+ * the first device (default 4): each ForkJoin thread keeps one, and the shards' H2D, decode
+ * and D2H overlap across contexts instead of queueing on one.
  */
 public final class ZarrHip {
     public static final int UNSUPPORTED = 3;
 
     private static final boolean AVAILABLE;
     private static final long[] CTXS;
+    private static final long[] CODEC_POOL;
+    private static final java.util.concurrent.atomic.AtomicInteger NEXT =
+            new java.util.concurrent.atomic.AtomicInteger();
+    private static final ThreadLocal<Long> CODEC_CTX = ThreadLocal.withInitial(
+            () -> CODEC_POOL[Math.floorMod(NEXT.getAndIncrement(), CODEC_POOL.length)]);
 
     static {
         long[] ctxs = new long[0];
@@ -41,6 +52,29 @@ public final class ZarrHip {
         }
         AVAILABLE = ctxs.length > 0;
         CTXS = ctxs;
+        long[] pool = ctxs.length > 0 ? new long[]{ctxs[0]} : new long[0];
+        if (ctxs.length > 0) {
+            String n = System.getenv("ZH_CODEC_CONTEXTS");
+            int want = 4;
+            try {
+                if (n != null) want = Math.max(1, Integer.parseInt(n.trim()));
+            } catch (NumberFormatException e) {
+                want = 4;
+            }
+            String list = System.getenv("ZH_DEVICES");
+            if (list == null) list = System.getenv("ZH_DEVICE") == null ? "0" : System.getenv("ZH_DEVICE");
+            int dev0 = Integer.parseInt(list.split(",")[0].trim());
+            java.util.List<Long> extra = new java.util.ArrayList<>();
+            extra.add(ctxs[0]);
+            for (int i = 1; i < want; i++) {
+                long c = ctxCreate(dev0);
+                if (c == 0) break;
+                extra.add(c);
+            }
+            pool = new long[extra.size()];
+            for (int i = 0; i < pool.length; i++) pool[i] = extra.get(i);
+        }
+        CODEC_POOL = pool;
     }
 
     private ZarrHip() {
@@ -56,6 +90,11 @@ public final class ZarrHip {
 
     static long[] ctxs() {
         return CTXS;
+    }
+
+    /** The calling thread's context of the codec pool (see the class comment). */
+    static long codecCtx() {
+        return CODEC_CTX.get();
     }
 
     static native long ctxCreate(int device);

@@ -87,6 +87,7 @@ _SIGS = {
     "zh_event_record": (C.c_int, [P, P, P]),
     "zh_event_elapsed_ms": (C.c_int, [P, P, P, C.POINTER(C.c_float)]),
     "zh_device_info": (C.c_int, [P, CH, SZ, PI64, C.POINTER(C.c_int), CH, SZ]),
+    "zh_gather_blocks": (C.c_int, [P, P, P, I64, PI64, I64]),
     "zh_synth_fill": (C.c_int, [P, P, I64, C.c_int, I64, U64, P]),
     "zh_synth_verify": (C.c_int, [P, P, C.c_int, PI64, PI64, PI64, C.c_int, U64,
                                   C.POINTER(U64), P]),
@@ -252,6 +253,12 @@ class DeviceContext:
         ms = C.c_float()
         check(self.L.zh_event_elapsed_ms(self.h, P(a), P(b), C.byref(ms)))
         return ms.value
+
+    def gather_blocks(self, dst, src, block_bytes, src_blocks):
+        """zh_gather_blocks: dst block b <- src block src_blocks[b] (synchronous)."""
+        idx = (C.c_int64 * max(1, len(src_blocks)))(*[int(x) for x in src_blocks])
+        check(self.L.zh_gather_blocks(self.h, P(dst), P(src), int(block_bytes), idx,
+                                      len(src_blocks)))
 
     # -- synthetic data ---------------------------------------------------------------
     def synth_fill(self, dst, n, dtype_size, first=0, seed=0x5A5A2026, stream=None):
