@@ -374,6 +374,33 @@ def test_device_encode_grouped_rows(dev, dsize, order):
     assert device_write(dev, meta, arr) == want
 
 
+@pytest.mark.parametrize("dsize", [1, 4, 8])
+@pytest.mark.parametrize("group,rows", [("0", "4"), ("1", "2"), ("2", "4"), ("4", "8"),
+                                        ("8", "4"), ("-1", "4")])
+def test_device_encode_chunk_groups(dev, monkeypatch, dsize, group, rows):
+    """encode_group_rows_kernel (G consecutive inner chunks per work item, ZH_ENC_GROUP; rows
+    in flight ZH_ENC_GU): an odd number of inner chunks along each shard row (groups straddle
+    shard rows and the item list's end), all-fill chunks beside data chunks in one group
+    (per-chunk flags from one ballot), clipped boundary chunks on the slow list."""
+    monkeypatch.setenv("ZH_ENC_GROUP", group)
+    monkeypatch.setenv("ZH_ENC_GU", rows)
+    inner_last = 128 // dsize
+    shape = [13, 24, inner_last * 7 + inner_last // 2]
+    meta = A.make_meta(shape, [8, 8, inner_last * 5], dsize, endian=A.ZH_ENDIAN_BIG,
+                       sharded=True, inner_chunk_shape=[4, 4, inner_last],
+                       fill=(5).to_bytes(dsize, "little"))
+    arr = rand_array(shape, dsize, seed=53 + dsize)
+    arr[arr == 5] = 6
+    arr[0:4, 0:4, inner_last:2 * inner_last] = 5          # all-fill chunk next to data
+    arr[4:8, 4:8, 0:3 * inner_last] = 5                   # a run of three
+    arr[8:12, 0:4, 2 * inner_last:3 * inner_last] = 5
+    arr[8:12, 0:4, 2 * inner_last + 1] = 9                # one element differs: kept
+    want = encode_oracle(meta, arr)
+    got = device_write(dev, meta, arr)
+    assert [len(g) if g else 0 for g in got] == [len(w) if w else 0 for w in want]
+    assert got == want
+
+
 @pytest.mark.parametrize("order", [[0, 3, 2, 1], [0, 1, 3, 2]])
 def test_tile_encode_chunk_crc_fused(dev, monkeypatch, order):
     """c4crc-shaped chain at small extent: [transpose, bytes(big), crc32c] with 32x32 tiles,

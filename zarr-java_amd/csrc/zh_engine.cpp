@@ -2293,8 +2293,24 @@ static int array_write_fast(zh_ctx* ctx, const zh_array_meta* m, ScatterArgs a,
   if (crc_fuse)
     ZH_HIPF(hipMemsetAsync(W + o_cpart, 0, (size_t)(items * nspan) * sizeof(uint32_t), s));
   v.nt = env_int("ZH_ENC_NT", 3) & 3;
-  const int grid = grid_for(ctx, pitems);
-  ZH_HIPF(launch_encode_fast(v, grid, env_int("ZH_ENC_DEEP", 1), s));
+  // narrow rows: G consecutive chunks per work item so a wave load covers G·row bytes of a
+  // region row (ZH_ENC_GROUP: 0 off, default G·row = 256 B; encode_group_rows_kernel; c3
+  // write G × U grid in profiles/r02/write/ab_enc3.txt: G = 2, U = 4 best, 40.1 → 36.2 ms)
+  int group = 0;
+  // (not nested: c3nest measured 42 → 48 ms grouped, profiles/r02/write/ab_enc.txt)
+  if ((v.fast_mode == kFastRowArith || v.fast_mode == kFastRowTable) && !crc_fuse &&
+      v.nt == 3 && a.piece_shift == 0 && (!nz.cell || env_int("ZH_ENC_GROUP", -1) > 0)) {
+    const int want = env_int("ZH_ENC_GROUP", -1);
+    int G = want >= 0 ? want : (16 >> std::min(v.fast_vpr_shift, 5));
+    G = G >= 8 ? 8 : G >= 4 ? 4 : G >= 2 ? 2 : G;
+    if (G && (G << v.fast_vpr_shift) <= 64) group = G;
+  }
+  if (group) v.item_mul = env_int("ZH_ITEM_PERM", 1) ? golden_item_mul((items + group - 1) / group) : 0;
+  const int grid = grid_for(ctx, group ? (items + group - 1) / group : pitems);
+  const int gu = env_int("ZH_ENC_GU", 4);  // grouped kernel: rows in flight per lane
+  ZH_HIPF(launch_encode_fast(v, grid,
+                             group ? (gu <= 2 ? 0 : gu <= 4 ? 1 : 2) : env_int("ZH_ENC_DEEP", 1),
+                             group, s));
   ZH_HIPF(launch_encode_slow(a, grid, s));
   ZH_HIPF(launch_encode_finish(a, nz, cn, d_cnt, d_cdesc, s));
   if (!jobs.empty()) {

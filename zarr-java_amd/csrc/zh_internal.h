@@ -219,7 +219,10 @@ struct EncNest {
 hipError_t launch_encode_resolve(const ScatterArgs& a, const EncNest& nz, int64_t* item_off,
                                  int64_t base_off, int64_t cn, const uint8_t* vbase, int vfast,
                                  hipStream_t stream);
-hipError_t launch_encode_fast(const ScatterArgs& view, int grid, int deep, hipStream_t stream);
+// group > 1: encode_group_rows_kernel over groups of `group` consecutive chunks (row modes,
+// no fused CRC, piece_shift 0, group << fast_vpr_shift <= 64; view.item_mul over the groups)
+hipError_t launch_encode_fast(const ScatterArgs& view, int grid, int deep, int group,
+                              hipStream_t stream);
 hipError_t launch_encode_slow(const ScatterArgs& a, int grid, hipStream_t stream);
 hipError_t launch_encode_finish(const ScatterArgs& a, const EncNest& nz, int64_t chunk_nbytes,
                                 uint32_t* bad, ItemDesc* crc_desc, hipStream_t stream);

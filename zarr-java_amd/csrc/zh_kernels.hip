@@ -1162,6 +1162,79 @@ __global__ __launch_bounds__(kBlock) void decode_rows_kernel(ScatterArgs a) {
   }
 }
 
+// encode, grouped row kernel (write path, narrow rows): a work item is G consecutive inner
+// chunks — z-adjacent in the region when they sit in one shard row — and lane group q of
+// every G·vpr lanes moves chunk q.  A wave load then covers G·(row bytes) of one region row
+// instead of vpr-lane segments of 64/vpr different rows (region rows of a 32³ uint32 chunk
+// are 128 B, 6 KiB apart in c3): +7 % in profiles/r02/enc_lab.json (G·row = 512 B).  Each
+// lane group reads its own descriptor (not wave-uniform), so any item mix is correct;
+// non-fast items idle their lane group (the slow kernel encodes them).  Rows per item and
+// the row table are shared by every fast item (setup_fast); piece_shift == 0, no CRC.
+template <int DS, int G, int U, int NT>
+__global__ __launch_bounds__(kBlock) void encode_group_rows_kernel(ScatterArgs a) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  uint2* tab = reinterpret_cast<uint2*>(smem);
+  for (int i = threadIdx.x; i < a.fast_n; i += kBlock)
+    tab[i] = reinterpret_cast<const uint2*>(a.fast_tab)[i];
+  __syncthreads();
+  const int vs = a.fast_vpr_shift;
+  const int GL = G << vs;  // lanes per group row (≤ 64, host-checked)
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int q = (tid % GL) >> vs;
+  const uint32_t col = (tid & ((1u << vs) - 1)) * 16;
+  const uint32_t lr = tid / GL, rstep = kBlock / GL;
+  const uint32_t nrows = (uint32_t)a.fast_rows;
+  const int64_t ngroups = (a.n_citems + G - 1) / G;
+  // this lane's group leader (first lane of q's segment in the wave) and q's ballot mask
+  uint64_t qmask = 0;
+  for (int o = 0; o < 64; o += GL) qmask |= (((1ull << (1 << vs)) - 1) << (q << vs)) << o;
+  const bool leader = lane == (q << vs);
+  const uint4 ffill = fill16<DS>(a.fill);
+  for (int64_t g = blockIdx.x; g < ngroups; g += gridDim.x) {
+    const int64_t pg = a.item_mul ? (int64_t)(((uint64_t)g * a.item_mul) % (uint64_t)ngroups) : g;
+    const int64_t c = pg * G + q;
+    bool on = false;
+    const uint8_t* src = nullptr;
+    uint8_t* dst = nullptr;
+    if (c < a.n_citems) {
+      const uint4* dp = reinterpret_cast<const uint4*>(a.desc + c);
+      const uint4 x = dp[0], y = dp[1];
+      on = (y.z & kDescFast) != 0;
+      src = (const uint8_t*)(uintptr_t)(((uint64_t)x.y << 32) | x.x) + col;
+      dst = a.region + (int64_t)(((uint64_t)x.w << 32) | x.z) * DS + col;
+    }
+    if (__syncthreads_or(on) == 0) continue;  // block-uniform: no fast chunk in the group
+    bool differs = false;
+    // load U rows, then store them (no cross-step pipelining: the double-buffered form measured
+    // 36.2 → 44.4 ms at G = 2, U = 4; profiles/r02/write/ab_enc4.txt)
+#pragma unroll 1
+    for (uint32_t r0 = 0; r0 < nrows; r0 += rstep * U) {
+      uint4 v[U];
+      uint64_t dd[U];
+#pragma unroll
+      for (int u = 0; u < U; u++) {
+        const uint32_t r = r0 + lr + u * rstep;
+        dd[u] = ~0ull;
+        if (on && r < nrows) {
+          uint64_t so, dof;
+          row_offsets(a, tab, r, so, dof);
+          dd[u] = dof * DS;
+          v[u] = ld16s<(NT & 1) != 0>(src + so * DS);
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < U; u++)
+        if (dd[u] != ~0ull) {
+          st16s<(NT & 2) != 0>(dst + dd[u], xform16<DS>(v[u], a.swap, a.is_bool));
+          differs |= (v[u].x != ffill.x) | (v[u].y != ffill.y) | (v[u].z != ffill.z) |
+                     (v[u].w != ffill.w);
+        }
+    }
+    // one flag byte per chunk, set by q's leader in any wave whose lanes saw data
+    if ((__ballot(differs) & qmask) != 0 && leader && on) a.flags[c] = 1;
+  }
+}
+
 // Row-interleaved tile path (see kTG above).  With CRC (inner crc32c fused): lane (w, t, g)
 // holds the payload vectors at bytes P_k = 4·tab[u].x + 4·(8w + k)·s_fd + 16g, k = 0..7,
 // a constant gap G = 4·s_fd − 16 apart, so its raw register over [v0, G zeros, v1, …, v7]
@@ -2234,8 +2307,28 @@ hipError_t launch_decode_slow(const ScatterArgs& a, int grid, hipStream_t stream
 // the encode view through the fast kernels (FLAGS); v.nt picks the cache policy and
 // `deep` 8 rows in flight per lane instead of 4 (uint32 rows; tuning, ZH_ENC_NT/ZH_ENC_DEEP)
 template <int DS>
-static void launch_encode_fast_ds(const ScatterArgs& v, int grid, int deep, hipStream_t s) {
+static void launch_encode_fast_ds(const ScatterArgs& v, int grid, int deep, int group,
+                                  hipStream_t s) {
   const size_t lds = ((size_t)v.fast_n * 8 + 15) & ~(size_t)15;
+  if (group > 0 && v.fast_mode != kFastTileTable && !v.crc_fused && v.nt == 3) {
+    // host: G·vpr ≤ 64 lanes, piece_shift == 0, v.item_mul over groups; deep: U (rows per
+    // lane in flight) 2 / 4 / 8 for deep = 0 / 1 / 2
+#define ZH_EG(G, U) hipLaunchKernelGGL((encode_group_rows_kernel<DS, G, U, 3>), dim3(grid), dim3(kBlock), lds, s, v); return
+    switch (group * 10 + (deep <= 0 ? 2 : deep == 1 ? 4 : 8)) {
+      case 12: ZH_EG(1, 2);
+      case 14: ZH_EG(1, 4);
+      case 18: ZH_EG(1, 8);
+      case 22: ZH_EG(2, 2);
+      case 24: ZH_EG(2, 4);
+      case 28: ZH_EG(2, 8);
+      case 42: ZH_EG(4, 2);
+      case 44: ZH_EG(4, 4);
+      case 48: ZH_EG(4, 8);
+      case 84: ZH_EG(8, 4);
+      default: break;
+    }
+#undef ZH_EG
+  }
   if (v.fast_mode == kFastTileTable) {
     if constexpr (DS == 4) {
       const size_t l = lds + (size_t)kTG * kTilePitch * 4;
@@ -2280,13 +2373,14 @@ static void launch_encode_fast_ds(const ScatterArgs& v, int grid, int deep, hipS
   }
 }
 
-hipError_t launch_encode_fast(const ScatterArgs& view, int grid, int deep, hipStream_t stream) {
+hipError_t launch_encode_fast(const ScatterArgs& view, int grid, int deep, int group,
+                              hipStream_t stream) {
   if (view.total_items == 0 || view.fast_mode == kFastNone) return hipSuccess;
   switch (view.dsize) {
-    case 1: launch_encode_fast_ds<1>(view, grid, deep, stream); break;
-    case 2: launch_encode_fast_ds<2>(view, grid, deep, stream); break;
-    case 4: launch_encode_fast_ds<4>(view, grid, deep, stream); break;
-    case 8: launch_encode_fast_ds<8>(view, grid, deep, stream); break;
+    case 1: launch_encode_fast_ds<1>(view, grid, deep, group, stream); break;
+    case 2: launch_encode_fast_ds<2>(view, grid, deep, group, stream); break;
+    case 4: launch_encode_fast_ds<4>(view, grid, deep, group, stream); break;
+    case 8: launch_encode_fast_ds<8>(view, grid, deep, group, stream); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();
