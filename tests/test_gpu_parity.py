@@ -401,6 +401,29 @@ def test_device_encode_chunk_groups(dev, monkeypatch, dsize, group, rows):
     assert got == want
 
 
+@pytest.mark.parametrize("group", ["0", "1", "2", "4", "-1"])
+@pytest.mark.parametrize("loc", [A.ZH_INDEX_END, A.ZH_INDEX_START])
+def test_device_encode_tile_groups(dev, monkeypatch, group, loc):
+    """encode_tiles_group_kernel (ZH_ENC_TGROUP chunks per work item, 8/G tiles of each per
+    step): uint32 inner chunks transposed through 32x32 tiles, an odd number of chunks along
+    each shard row, all-fill chunks inside groups, clipped boundary chunks."""
+    monkeypatch.setenv("ZH_ENC_TGROUP", group)
+    shape = [40, 7, 32 * 7 + 16]
+    meta = A.make_meta(shape, [32, 4, 32 * 5], 4, endian=A.ZH_ENDIAN_BIG, sharded=True,
+                       inner_chunk_shape=[32, 2, 32], transpose_order=[2, 1, 0],
+                       index_location=loc, fill=(5).to_bytes(4, "little"))
+    arr = rand_array(shape, 4, seed=61)
+    arr[arr == 5] = 6
+    arr[0:32, 0:2, 32:64] = 5
+    arr[0:32, 2:4, 0:96] = 5
+    arr[0:32, 4:6, 64:96] = 5
+    arr[7, 5, 70] = 9
+    want = encode_oracle(meta, arr)
+    got = device_write(dev, meta, arr)
+    assert [len(g) if g else 0 for g in got] == [len(w) if w else 0 for w in want]
+    assert got == want
+
+
 @pytest.mark.parametrize("order", [[0, 3, 2, 1], [0, 1, 3, 2]])
 def test_tile_encode_chunk_crc_fused(dev, monkeypatch, order):
     """c4crc-shaped chain at small extent: [transpose, bytes(big), crc32c] with 32x32 tiles,

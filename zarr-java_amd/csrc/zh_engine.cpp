@@ -1211,6 +1211,19 @@ int zh_plan_create(zh_ctx* ctx, const zh_array_meta* m, const zh_chunk_src* chun
   p->args.item_mul =
       env_int("ZH_ITEM_PERM", p->tile_mode ? 1 : 0) ? golden_item_mul(p->args.total_items) : 0;
   p->slow_grid = p->grid;
+  // ZH_DEC_TGROUP = G (1, 2, 4): the tile decode over G consecutive chunks per work item
+  // (encode_tiles_group_kernel in the decode direction; tile_variant 10 + G)
+  {
+    const int G = env_int("ZH_DEC_TGROUP", 0);
+    if ((G == 1 || G == 2 || G == 4 || G == 8) && p->tile_mode && p->args.fast_mode == kFastTileTable &&
+        p->args.tile_variant == 1 && !p->args.crc_fused && p->args.piece_shift == 0 &&
+        (p->args.nt & 3) == 3 && items > 0) {
+      const int64_t groups = (items + G - 1) / G;
+      p->args.tile_variant = 10 + G;
+      p->args.item_mul = env_int("ZH_ITEM_PERM", 1) ? golden_item_mul(groups) : 0;
+      p->grid = grid_for(ctx, groups);
+    }
+  }
   *out = p;
   return ZH_OK;
 }
@@ -2304,6 +2317,14 @@ static int array_write_fast(zh_ctx* ctx, const zh_array_meta* m, ScatterArgs a,
     int G = want >= 0 ? want : (16 >> std::min(v.fast_vpr_shift, 5));
     G = G >= 8 ? 8 : G >= 4 ? 4 : G >= 2 ? 2 : G;
     if (G && (G << v.fast_vpr_shift) <= 64) group = G;
+  }
+  // tiles (uint32 transposed chunks): G chunks per work item, 8/G tiles of each per step
+  // (ZH_ENC_TGROUP: 0 off; encode_tiles_group_kernel)
+  if (v.fast_mode == kFastTileTable && !crc_fuse && v.nt == 3 && a.piece_shift == 0 &&
+      (!nz.cell || env_int("ZH_ENC_TGROUP", -1) > 0)) {
+    const int want = env_int("ZH_ENC_TGROUP", -1);
+    const int G = want < 0 ? 2 : want;
+    if (G == 1 || G == 2 || G == 4) group = G;
   }
   if (group) v.item_mul = env_int("ZH_ITEM_PERM", 1) ? golden_item_mul((items + group - 1) / group) : 0;
   const int grid = grid_for(ctx, group ? (items + group - 1) / group : pitems);

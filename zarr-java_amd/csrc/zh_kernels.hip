@@ -1430,6 +1430,90 @@ __global__ __launch_bounds__(kBlock) void decode_tiles_kernel(ScatterArgs a) {
   decode_tiles_body<NT, VARIANT, CRC, FLAGS>(a);
 }
 
+// encode, grouped tile kernel (write path, uint32, transposed inner chunks): the tile path of
+// the encode view reads region rows of 128 B, one per tile (the 8 tiles of a step are
+// x-neighbours, a region row pitch apart), where the decode mirror reads 1 KiB of payload.
+// Here a work item is G consecutive (z-adjacent) inner chunks and a step moves 8/G tiles of
+// each: lane (t, g) with t = q·(8/G) + i moves tile i of chunk q, so a wave load covers
+// G·128 B contiguous of each of 8/G region rows.  Same LDS tiles and bank layout as
+// fast_tiles_rows; per-lane descriptors (any chunk mix is correct; non-fast chunks idle their
+// lanes and stay on the slow list).  No CRC, piece_shift == 0 (host-checked).
+//
+// FLAGS = false: the decode direction (payload → region; every fast tile item is a full copy),
+// ZH_DEC_TGROUP.
+template <int NT, int G, bool FLAGS = true>
+__global__ __launch_bounds__(kBlock) void encode_tiles_group_kernel(ScatterArgs a) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  uint2* tab = reinterpret_cast<uint2*>(smem);
+  uint32_t* lds = reinterpret_cast<uint32_t*>(smem + (((size_t)a.fast_n * 8 + 15) & ~(size_t)15));
+  for (int i = threadIdx.x; i < a.fast_n; i += kBlock)
+    tab[i] = reinterpret_cast<const uint2*>(a.fast_tab)[i];
+  __syncthreads();
+  constexpr int TG = kTG / G;  // tiles of each chunk per step
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int t = lane >> 3, g = lane & 7, q = t / TG, ti = t % TG;
+  const int64_t s_fd = a.pstride[a.fd], d_fs = a.rstride[a.fs];
+  const uint32_t units = (uint32_t)a.fast_n;
+  const int64_t ngroups = (a.n_citems + G - 1) / G;
+  const uint64_t qmask = (TG * 8 == 64 ? ~0ull : ((1ull << (TG * 8)) - 1)) << (q * TG * 8);
+  const bool leader = lane == q * TG * 8;
+  const uint32_t f = (uint32_t)a.fill;
+  uint32_t* mine = lds + t * kTilePitch;
+  for (int64_t gi = blockIdx.x; gi < ngroups; gi += gridDim.x) {
+    const int64_t pg = a.item_mul ? (int64_t)(((uint64_t)gi * a.item_mul) % (uint64_t)ngroups) : gi;
+    const int64_t c = pg * G + q;
+    bool on = false;
+    const uint8_t* src = nullptr;
+    uint8_t* dst = nullptr;
+    if (c < a.n_citems) {
+      const uint4* dp = reinterpret_cast<const uint4*>(a.desc + c);
+      const uint4 x = dp[0], y = dp[1];
+      on = (y.z & kDescFast) != 0;
+      src = (const uint8_t*)(uintptr_t)(((uint64_t)x.y << 32) | x.x);
+      dst = a.region + (int64_t)(((uint64_t)x.w << 32) | x.z) * 4;
+    }
+    if (__syncthreads_or(on) == 0) continue;  // block-uniform
+    bool differs = false;
+#pragma unroll 1
+    for (uint32_t ub = 0; ub < units; ub += TG) {
+      const uint32_t u = ub + ti;
+      const bool live = on && u < units;
+      if (live) {
+        const uint8_t* base = src + ((size_t)tab[u].x + g * 4) * 4;
+        uint4 x[8];
+#pragma unroll
+        for (int k = 0; k < 8; k++)
+          x[k] = ld16s<(NT & 1) != 0>(base + (size_t)(wave * 8 + k) * s_fd * 4);
+#pragma unroll
+        for (int k = 0; k < 8; k++) {
+          if (FLAGS) differs |= (x[k].x != f) | (x[k].y != f) | (x[k].z != f) | (x[k].w != f);
+          uint32_t* row = mine + (wave * 8 + k) * 33 + g * 4;
+          row[0] = xform1<4>(x[k].x, a.swap, 0);
+          row[1] = xform1<4>(x[k].y, a.swap, 0);
+          row[2] = xform1<4>(x[k].z, a.swap, 0);
+          row[3] = xform1<4>(x[k].w, a.swap, 0);
+        }
+      }
+      __syncthreads();
+      if (live) {
+        uint8_t* base = dst + ((size_t)tab[u].y + g * 4) * 4;
+#pragma unroll
+        for (int k = 0; k < 8; k++) {
+          const int r = wave * 8 + k;
+          uint4 y;
+          y.x = mine[(g * 4 + 0) * 33 + r];
+          y.y = mine[(g * 4 + 1) * 33 + r];
+          y.z = mine[(g * 4 + 2) * 33 + r];
+          y.w = mine[(g * 4 + 3) * 33 + r];
+          st16s<(NT & 2) != 0>(base + (size_t)r * d_fs * 4, y);
+        }
+      }
+      __syncthreads();
+    }
+    if (FLAGS && (__ballot(differs) & qmask) != 0 && leader && on) a.flags[c] = 1;
+  }
+}
+
 // The CRC-fused decode variant held to 3 waves per SIMD (LDS allows 3 blocks of 4 waves per
 // CU; unconstrained it takes 172 VGPRs and runs 2)
 template <int NT, bool FLAGS>
@@ -2234,6 +2318,15 @@ static void launch_scatter_ds(const ScatterArgs& a, int tile, int enc, int grid,
         const int v = a.tile_variant;
         lds += v == 0 ? (size_t)kFastTPB * 32 * 33 * 4 : (size_t)kTG * kTilePitch * 4;
         const bool ntx = nt == 3;
+        if (v > 10) {  // host: G chunks per work item, item_mul and grid over the groups
+          switch (v - 10) {
+            case 1: hipLaunchKernelGGL((encode_tiles_group_kernel<3, 1, false>), dim3(grid), dim3(kBlock), lds, s, a); return;
+            case 2: hipLaunchKernelGGL((encode_tiles_group_kernel<3, 2, false>), dim3(grid), dim3(kBlock), lds, s, a); return;
+            case 4: hipLaunchKernelGGL((encode_tiles_group_kernel<3, 4, false>), dim3(grid), dim3(kBlock), lds, s, a); return;
+            case 8: hipLaunchKernelGGL((encode_tiles_group_kernel<3, 8, false>), dim3(grid), dim3(kBlock), lds, s, a); return;
+            default: return;
+          }
+        }
         if (v == 1 && a.crc_fused) {
           lds += 16 * 256 * 4 + (size_t)a.fast_n * 4;  // T[8][256] + S, SD[4][256] + K[fast_n]
           static const bool w3 = [] {  // ZH_CRC_W3=0: the unconstrained variant (A/B)
@@ -2332,6 +2425,14 @@ static void launch_encode_fast_ds(const ScatterArgs& v, int grid, int deep, int 
   if (v.fast_mode == kFastTileTable) {
     if constexpr (DS == 4) {
       const size_t l = lds + (size_t)kTG * kTilePitch * 4;
+      if (group > 0 && !v.crc_fused && v.nt == 3) {  // host: piece_shift == 0, item_mul
+        switch (group) {
+          case 1: hipLaunchKernelGGL((encode_tiles_group_kernel<3, 1>), dim3(grid), dim3(kBlock), l, s, v); return;
+          case 2: hipLaunchKernelGGL((encode_tiles_group_kernel<3, 2>), dim3(grid), dim3(kBlock), l, s, v); return;
+          case 4: hipLaunchKernelGGL((encode_tiles_group_kernel<3, 4>), dim3(grid), dim3(kBlock), l, s, v); return;
+          default: break;
+        }
+      }
       if (v.crc_fused) {  // chunk crc32c of the stored payload: tables + per-unit shifts
         hipLaunchKernelGGL((decode_tiles_kernel<3, 1, true, true>), dim3(grid), dim3(kBlock),
                            l + 16 * 256 * 4 + (size_t)v.fast_n * 4, s, v);
