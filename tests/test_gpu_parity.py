@@ -374,27 +374,30 @@ def test_device_encode_grouped_rows(dev, dsize, order):
     assert device_write(dev, meta, arr) == want
 
 
+@pytest.mark.parametrize("crc", [False, True])
 @pytest.mark.parametrize("dsize", [1, 4, 8])
 @pytest.mark.parametrize("group,rows", [("0", "4"), ("1", "2"), ("2", "4"), ("4", "8"),
                                         ("8", "4"), ("-1", "4")])
-def test_device_encode_chunk_groups(dev, monkeypatch, dsize, group, rows):
+def test_device_encode_chunk_groups(dev, monkeypatch, dsize, group, rows, crc):
     """encode_group_rows_kernel (G consecutive inner chunks per work item, ZH_ENC_GROUP; rows
     in flight ZH_ENC_GU): an odd number of inner chunks along each shard row (groups straddle
     shard rows and the item list's end), all-fill chunks beside data chunks in one group
-    (per-chunk flags from one ballot), clipped boundary chunks on the slow list."""
+    (per-chunk flags from one ballot), clipped boundary chunks on the slow list.  crc: inner
+    [bytes(big), crc32c] with 4 KiB chunk payloads, the chunk CRC fused into the grouped
+    kernel (256/G lanes per chunk)."""
     monkeypatch.setenv("ZH_ENC_GROUP", group)
     monkeypatch.setenv("ZH_ENC_GU", rows)
     inner_last = 128 // dsize
     shape = [13, 24, inner_last * 7 + inner_last // 2]
     meta = A.make_meta(shape, [8, 8, inner_last * 5], dsize, endian=A.ZH_ENDIAN_BIG,
-                       sharded=True, inner_chunk_shape=[4, 4, inner_last],
-                       fill=(5).to_bytes(dsize, "little"))
+                       sharded=True, inner_chunk_shape=[4, 8, inner_last],
+                       fill=(5).to_bytes(dsize, "little"), inner_crc32c=crc)
     arr = rand_array(shape, dsize, seed=53 + dsize)
     arr[arr == 5] = 6
-    arr[0:4, 0:4, inner_last:2 * inner_last] = 5          # all-fill chunk next to data
-    arr[4:8, 4:8, 0:3 * inner_last] = 5                   # a run of three
-    arr[8:12, 0:4, 2 * inner_last:3 * inner_last] = 5
-    arr[8:12, 0:4, 2 * inner_last + 1] = 9                # one element differs: kept
+    arr[0:4, 0:8, inner_last:2 * inner_last] = 5          # all-fill chunk next to data
+    arr[4:8, 8:16, 0:3 * inner_last] = 5                  # a run of three
+    arr[8:12, 0:8, 2 * inner_last:3 * inner_last] = 5
+    arr[8:12, 0:8, 2 * inner_last + 1] = 9                # one element differs: kept
     want = encode_oracle(meta, arr)
     got = device_write(dev, meta, arr)
     assert [len(g) if g else 0 for g in got] == [len(w) if w else 0 for w in want]
@@ -425,11 +428,14 @@ def test_device_encode_tile_groups(dev, monkeypatch, group, loc):
 
 
 @pytest.mark.parametrize("order", [[0, 3, 2, 1], [0, 1, 3, 2]])
-def test_tile_encode_chunk_crc_fused(dev, monkeypatch, order):
+@pytest.mark.parametrize("group", ["-1", "0", "1", "4"])
+def test_tile_encode_chunk_crc_fused(dev, monkeypatch, order, group):
     """c4crc-shaped chain at small extent: [transpose, bytes(big), crc32c] with 32x32 tiles,
     the chunk CRC fused into the tile encode (stored vectors, per-unit end shifts from the
     payload side of the table), boundary chunks through the slow list + CRC pass; equals the
-    oracle and the unfused pass, and decodes back."""
+    oracle and the unfused pass, and decodes back.  ZH_ENC_TGROUP: the grouped tile encode
+    (the unit fold step for 8/G units), or the ungrouped kernel (0)."""
+    monkeypatch.setenv("ZH_ENC_TGROUP", group)
     shape = [1, 64, 80, 96]
     meta = A.make_meta(shape, [1, 64, 64, 64], 4, endian=A.ZH_ENDIAN_BIG, sharded=True,
                        inner_chunk_shape=[1, 32, 32, 32], transpose_order=order,

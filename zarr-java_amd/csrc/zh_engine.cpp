@@ -122,8 +122,7 @@ uint32_t gf2_xpow8n(uint64_t n) {
 // ends a constant Δ bytes after unit u, a lane folds its groups as r = r·x^(8Δ) ⊕ acc and
 // multiplies by its last unit's K once per piece; returns x^(8Δ) (0 = irregular layout,
 // the kernel then multiplies every group by its K).
-uint32_t tile_crc_step(const std::vector<int64_t>& ends) {
-  constexpr size_t kGroup = 8;  // kTG in zh_kernels.hip
+uint32_t tile_crc_step(const std::vector<int64_t>& ends, size_t kGroup = 8 /* kTG */) {
   if (ends.size() <= kGroup) return 0;
   const int64_t delta = ends[kGroup] - ends[0];
   if (delta <= 0) return 0;
@@ -2200,9 +2199,10 @@ static int array_write_fast(zh_ctx* ctx, const zh_array_meta* m, ScatterArgs a,
       ((int64_t)v.fast_n * 8 + 15) / 16 * 16 + 8 * 1057 * 4 + 16 * 256 * 4 +
               (int64_t)v.fast_n * 4 <= 65536;
   v.crc_tile_step = 0;
+  std::vector<int64_t> tile_ends;  // per-unit payload ends (tile CRC; the grouped step below)
   if (tile_crc) {
     const int64_t L = a.inner_nbytes, d_fs = v.rstride[v.fs];
-    std::vector<int64_t> ends;
+    std::vector<int64_t>& ends = tile_ends;
     for (int32_t u = 0; u < v.fast_n; u++) {
       const int64_t end = 4 * (int64_t)tab[2 * (size_t)u + 1] + 4 * 31 * d_fs + 128;
       ends.push_back(end);
@@ -2311,24 +2311,30 @@ static int array_write_fast(zh_ctx* ctx, const zh_array_meta* m, ScatterArgs a,
   // write G × U grid in profiles/r02/write/ab_enc3.txt: G = 2, U = 4 best, 40.1 → 36.2 ms)
   int group = 0;
   // (not nested: c3nest measured 42 → 48 ms grouped, profiles/r02/write/ab_enc.txt)
-  if ((v.fast_mode == kFastRowArith || v.fast_mode == kFastRowTable) && !crc_fuse &&
-      v.nt == 3 && a.piece_shift == 0 && (!nz.cell || env_int("ZH_ENC_GROUP", -1) > 0)) {
+  // (with the chunk CRC fused: rows sequential in the payload, checked above; whole chunks)
+  if ((v.fast_mode == kFastRowArith || v.fast_mode == kFastRowTable) && v.nt == 3 &&
+      a.piece_shift == 0 && (!nz.cell || env_int("ZH_ENC_GROUP", -1) > 0)) {
     const int want = env_int("ZH_ENC_GROUP", -1);
     int G = want >= 0 ? want : (16 >> std::min(v.fast_vpr_shift, 5));
     G = G >= 8 ? 8 : G >= 4 ? 4 : G >= 2 ? 2 : G;
+    if (crc_fuse && G > 4) G = 4;  // the CRC variants: G 1, 2, 4 with 4 rows per lane
     if (G && (G << v.fast_vpr_shift) <= 64) group = G;
   }
   // tiles (uint32 transposed chunks): G chunks per work item, 8/G tiles of each per step
   // (ZH_ENC_TGROUP: 0 off; encode_tiles_group_kernel)
-  if (v.fast_mode == kFastTileTable && !crc_fuse && v.nt == 3 && a.piece_shift == 0 &&
-      (!nz.cell || env_int("ZH_ENC_TGROUP", -1) > 0)) {
+  // With the tile CRC fused, the kernel folds each lane's units (8/G apart) with the step
+  // for that stride.
+  if (v.fast_mode == kFastTileTable && (!crc_fuse || tile_crc) && v.nt == 3 &&
+      a.piece_shift == 0 && (!nz.cell || env_int("ZH_ENC_TGROUP", -1) > 0)) {
     const int want = env_int("ZH_ENC_TGROUP", -1);
     const int G = want < 0 ? 2 : want;
     if (G == 1 || G == 2 || G == 4) group = G;
+    if (group && tile_crc) v.crc_tile_step = tile_crc_step(tile_ends, (size_t)(8 / group));
   }
   if (group) v.item_mul = env_int("ZH_ITEM_PERM", 1) ? golden_item_mul((items + group - 1) / group) : 0;
   const int grid = grid_for(ctx, group ? (items + group - 1) / group : pitems);
-  const int gu = env_int("ZH_ENC_GU", 4);  // grouped kernel: rows in flight per lane
+  // grouped kernel: rows in flight per lane (2, 4, 8; G = 8 and the CRC variants: 4)
+  const int gu = group == 8 || crc_fuse ? 4 : env_int("ZH_ENC_GU", 4);
   ZH_HIPF(launch_encode_fast(v, grid,
                              group ? (gu <= 2 ? 0 : gu <= 4 ? 1 : 2) : env_int("ZH_ENC_DEEP", 1),
                              group, s));

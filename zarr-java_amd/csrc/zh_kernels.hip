@@ -1169,20 +1169,40 @@ __global__ __launch_bounds__(kBlock) void decode_rows_kernel(ScatterArgs a) {
 // are 128 B, 6 KiB apart in c3): +7 % in profiles/r02/enc_lab.json (G·row = 512 B).  Each
 // lane group reads its own descriptor (not wave-uniform), so any item mix is correct;
 // non-fast items idle their lane group (the slow kernel encodes them).  Rows per item and
-// the row table are shared by every fast item (setup_fast); piece_shift == 0, no CRC.
-template <int DS, int G, int U, int NT>
+// the row table are shared by every fast item (setup_fast); piece_shift == 0.
+//
+// CRC (inner crc32c fused; rows sequential in the payload, host-checked): chunk q's
+// Lc = 256/G lanes store payload vectors j + Lc·m (j = the lane's index in the chunk), so a
+// lane's raw register over its vectors is acc = shift_{16·Lc}(acc) ⊕ upd16(0, v) (table S),
+// shifted to the payload end by x^(8·16·(Lc − 1 − j)); the chunk's lanes XOR their shares
+// (CRC is linear over GF(2)) into its partial, one atomic per wave.
+template <int DS, int G, int U, int NT, bool CRC = false>
 __global__ __launch_bounds__(kBlock) void encode_group_rows_kernel(ScatterArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   uint2* tab = reinterpret_cast<uint2*>(smem);
   for (int i = threadIdx.x; i < a.fast_n; i += kBlock)
     tab[i] = reinterpret_cast<const uint2*>(a.fast_tab)[i];
-  __syncthreads();
   const int vs = a.fast_vpr_shift;
   const int GL = G << vs;  // lanes per group row (≤ 64, host-checked)
   const int tid = threadIdx.x, lane = tid & 63;
   const int q = (tid % GL) >> vs;
   const uint32_t col = (tid & ((1u << vs) - 1)) * 16;
   const uint32_t lr = tid / GL, rstep = kBlock / GL;
+  uint32_t(*T)[256] = nullptr;
+  uint32_t(*S)[256] = nullptr;
+  uint32_t kl = 0;
+  if constexpr (CRC) {
+    T = reinterpret_cast<uint32_t(*)[256]>(smem + (((size_t)a.fast_n * 8 + 15) & ~(size_t)15));
+    S = T + 8;
+    init_crc_tables(T);
+    constexpr uint32_t Lc = kBlock / G;
+    const uint32_t kg = x2nmodp((uint64_t)(16 * Lc), 3);
+#pragma unroll
+    for (int b = 0; b < 4; b++) S[b][tid] = multmodp(kg, (uint32_t)tid << (8 * b));
+    const uint32_t j = (lr << vs) + (uint32_t)(tid & ((1 << vs) - 1));
+    kl = x2nmodp((uint64_t)(16 * (Lc - 1 - j)), 3);
+  }
+  __syncthreads();
   const uint32_t nrows = (uint32_t)a.fast_rows;
   const int64_t ngroups = (a.n_citems + G - 1) / G;
   // this lane's group leader (first lane of q's segment in the wave) and q's ballot mask
@@ -1205,6 +1225,7 @@ __global__ __launch_bounds__(kBlock) void encode_group_rows_kernel(ScatterArgs a
     }
     if (__syncthreads_or(on) == 0) continue;  // block-uniform: no fast chunk in the group
     bool differs = false;
+    uint32_t acc = 0;
     // load U rows, then store them (no cross-step pipelining: the double-buffered form measured
     // 36.2 → 44.4 ms at G = 2, U = 4; profiles/r02/write/ab_enc4.txt)
 #pragma unroll 1
@@ -1225,13 +1246,24 @@ __global__ __launch_bounds__(kBlock) void encode_group_rows_kernel(ScatterArgs a
 #pragma unroll
       for (int u = 0; u < U; u++)
         if (dd[u] != ~0ull) {
-          st16s<(NT & 2) != 0>(dst + dd[u], xform16<DS>(v[u], a.swap, a.is_bool));
+          const uint4 w = xform16<DS>(v[u], a.swap, a.is_bool);
+          st16s<(NT & 2) != 0>(dst + dd[u], w);
           differs |= (v[u].x != ffill.x) | (v[u].y != ffill.y) | (v[u].z != ffill.z) |
                      (v[u].w != ffill.w);
+          if constexpr (CRC) {
+            const v4u wv = {w.x, w.y, w.z, w.w};
+            acc = crc_shift_tab(acc, S) ^ crc_upd16(0u, wv, T);
+          }
         }
     }
     // one flag byte per chunk, set by q's leader in any wave whose lanes saw data
     if ((__ballot(differs) & qmask) != 0 && leader && on) a.flags[c] = 1;
+    if constexpr (CRC) {
+      uint32_t cr = multmodp(kl, acc);
+      for (int o = 1; o < (1 << vs); o <<= 1) cr ^= (uint32_t)__shfl_xor((int)cr, o, 64);
+      for (int o = GL; o < 64; o <<= 1) cr ^= (uint32_t)__shfl_xor((int)cr, o, 64);
+      if (leader && on) atomicXor(a.crc_partials + c, cr);
+    }
   }
 }
 
@@ -1440,19 +1472,46 @@ __global__ __launch_bounds__(kBlock) void decode_tiles_kernel(ScatterArgs a) {
 // lanes and stay on the slow list).  No CRC, piece_shift == 0 (host-checked).
 //
 // FLAGS = false: the decode direction (payload → region; every fast tile item is a full copy),
-// ZH_DEC_TGROUP.
-template <int NT, int G, bool FLAGS = true>
+// ZH_DEC_TGROUP.  CRC (encode only): the chunk crc32c of the stored payload, fused as in
+// fast_tiles_rows (the stored rows have the decode loads' geometry): a lane's 8 stored vectors
+// fold with S, its units (u, u + 8/G, …) with SD = x^(8Δ) for that unit stride (host:
+// tile_crc_step(ends, 8/G)), one K multiply per chunk, the lane constant kb, then an XOR over
+// the chunk's lane segment and one atomic per wave.
+template <int NT, int G, bool FLAGS = true, bool CRC = false>
 __global__ __launch_bounds__(kBlock) void encode_tiles_group_kernel(ScatterArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   uint2* tab = reinterpret_cast<uint2*>(smem);
-  uint32_t* lds = reinterpret_cast<uint32_t*>(smem + (((size_t)a.fast_n * 8 + 15) & ~(size_t)15));
+  uint8_t* after_tab = smem + (((size_t)a.fast_n * 8 + 15) & ~(size_t)15);
+  uint32_t* lds = reinterpret_cast<uint32_t*>(after_tab);
   for (int i = threadIdx.x; i < a.fast_n; i += kBlock)
     tab[i] = reinterpret_cast<const uint2*>(a.fast_tab)[i];
-  __syncthreads();
   constexpr int TG = kTG / G;  // tiles of each chunk per step
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int t = lane >> 3, g = lane & 7, q = t / TG, ti = t % TG;
   const int64_t s_fd = a.pstride[a.fd], d_fs = a.rstride[a.fs];
+  uint32_t(*T)[256] = nullptr;
+  uint32_t(*S)[256] = nullptr;
+  uint32_t(*SD)[256] = nullptr;
+  uint32_t* K = nullptr;
+  uint32_t kb = 0;
+  if constexpr (CRC) {
+    T = reinterpret_cast<uint32_t(*)[256]>(after_tab + (size_t)kTG * kTilePitch * 4);
+    S = T + 8;
+    SD = S + 4;
+    K = reinterpret_cast<uint32_t*>(SD + 4);
+    init_crc_tables(T);
+    const uint32_t kg = x2nmodp((uint64_t)(4 * d_fs), 3);  // stored row pitch
+#pragma unroll
+    for (int b = 0; b < 4; b++) {
+      S[b][threadIdx.x] = multmodp(kg, (uint32_t)threadIdx.x << (8 * b));
+      SD[b][threadIdx.x] =
+          a.crc_tile_step ? multmodp(a.crc_tile_step, (uint32_t)threadIdx.x << (8 * b)) : 0u;
+    }
+    for (int i = threadIdx.x; i < a.fast_n; i += kBlock) K[i] = a.fast_tab[2 * a.fast_n + i];
+    kb = x2nmodp((uint64_t)(4 * (24 - 8 * wave) * d_fs + 112 - 16 * g), 3);
+  }
+  __syncthreads();
+  const bool regular = CRC && a.crc_tile_step != 0;
   const uint32_t units = (uint32_t)a.fast_n;
   const int64_t ngroups = (a.n_citems + G - 1) / G;
   const uint64_t qmask = (TG * 8 == 64 ? ~0ull : ((1ull << (TG * 8)) - 1)) << (q * TG * 8);
@@ -1474,6 +1533,7 @@ __global__ __launch_bounds__(kBlock) void encode_tiles_group_kernel(ScatterArgs 
     }
     if (__syncthreads_or(on) == 0) continue;  // block-uniform
     bool differs = false;
+    uint32_t share = 0, run = 0, ulast = ~0u;
 #pragma unroll 1
     for (uint32_t ub = 0; ub < units; ub += TG) {
       const uint32_t u = ub + ti;
@@ -1497,6 +1557,7 @@ __global__ __launch_bounds__(kBlock) void encode_tiles_group_kernel(ScatterArgs 
       __syncthreads();
       if (live) {
         uint8_t* base = dst + ((size_t)tab[u].y + g * 4) * 4;
+        uint32_t eacc = 0;
 #pragma unroll
         for (int k = 0; k < 8; k++) {
           const int r = wave * 8 + k;
@@ -1506,11 +1567,31 @@ __global__ __launch_bounds__(kBlock) void encode_tiles_group_kernel(ScatterArgs 
           y.z = mine[(g * 4 + 2) * 33 + r];
           y.w = mine[(g * 4 + 3) * 33 + r];
           st16s<(NT & 2) != 0>(base + (size_t)r * d_fs * 4, y);
+          if constexpr (CRC) {
+            const v4u w = {y.x, y.y, y.z, y.w};
+            const uint32_t ck = crc_upd16(0u, w, T);
+            eacc = k ? crc_shift_tab(eacc, S) ^ ck : ck;
+          }
+        }
+        if constexpr (CRC) {
+          if (regular) {
+            run = (ulast == ~0u ? 0u : crc_shift_tab(run, SD)) ^ eacc;
+            ulast = u;
+          } else {
+            share ^= multmodp(K[u], eacc);
+          }
         }
       }
       __syncthreads();
     }
     if (FLAGS && (__ballot(differs) & qmask) != 0 && leader && on) a.flags[c] = 1;
+    if constexpr (CRC) {
+      if (regular && ulast != ~0u) share = multmodp(K[ulast], run);
+      uint32_t cr = multmodp(kb, share);
+#pragma unroll
+      for (int o = TG * 4; o > 0; o >>= 1) cr ^= (uint32_t)__shfl_xor((int)cr, o, 64);
+      if (leader && on) atomicXor(a.crc_partials + c, cr);
+    }
   }
 }
 
@@ -2399,14 +2480,25 @@ hipError_t launch_decode_slow(const ScatterArgs& a, int grid, hipStream_t stream
 
 // the encode view through the fast kernels (FLAGS); v.nt picks the cache policy and
 // `deep` 8 rows in flight per lane instead of 4 (uint32 rows; tuning, ZH_ENC_NT/ZH_ENC_DEEP)
+// Returns false when a grouped launch (group > 0) found no kernel for its combination: the
+// host set the visit order and grid over groups, so no ungrouped kernel may run instead.
 template <int DS>
-static void launch_encode_fast_ds(const ScatterArgs& v, int grid, int deep, int group,
+static bool launch_encode_fast_ds(const ScatterArgs& v, int grid, int deep, int group,
                                   hipStream_t s) {
   const size_t lds = ((size_t)v.fast_n * 8 + 15) & ~(size_t)15;
+  if (group > 0 && v.fast_mode != kFastTileTable && v.crc_fused && v.nt == 3) {
+    const size_t lc = lds + 12 * 256 * 4;  // + slicing tables T[8][256], shift table S[4][256]
+    switch (group) {  // host: rows sequential in the payload, whole chunks (piece_shift 0)
+      case 1: hipLaunchKernelGGL((encode_group_rows_kernel<DS, 1, 4, 3, true>), dim3(grid), dim3(kBlock), lc, s, v); return true;
+      case 2: hipLaunchKernelGGL((encode_group_rows_kernel<DS, 2, 4, 3, true>), dim3(grid), dim3(kBlock), lc, s, v); return true;
+      case 4: hipLaunchKernelGGL((encode_group_rows_kernel<DS, 4, 4, 3, true>), dim3(grid), dim3(kBlock), lc, s, v); return true;
+      default: break;
+    }
+  }
   if (group > 0 && v.fast_mode != kFastTileTable && !v.crc_fused && v.nt == 3) {
     // host: G·vpr ≤ 64 lanes, piece_shift == 0, v.item_mul over groups; deep: U (rows per
     // lane in flight) 2 / 4 / 8 for deep = 0 / 1 / 2
-#define ZH_EG(G, U) hipLaunchKernelGGL((encode_group_rows_kernel<DS, G, U, 3>), dim3(grid), dim3(kBlock), lds, s, v); return
+#define ZH_EG(G, U) hipLaunchKernelGGL((encode_group_rows_kernel<DS, G, U, 3>), dim3(grid), dim3(kBlock), lds, s, v); return true
     switch (group * 10 + (deep <= 0 ? 2 : deep == 1 ? 4 : 8)) {
       case 12: ZH_EG(1, 2);
       case 14: ZH_EG(1, 4);
@@ -2422,21 +2514,38 @@ static void launch_encode_fast_ds(const ScatterArgs& v, int grid, int deep, int 
     }
 #undef ZH_EG
   }
+  if (group > 0 && v.fast_mode != kFastTileTable) return false;
   if (v.fast_mode == kFastTileTable) {
     if constexpr (DS == 4) {
       const size_t l = lds + (size_t)kTG * kTilePitch * 4;
-      if (group > 0 && !v.crc_fused && v.nt == 3) {  // host: piece_shift == 0, item_mul
+      if (group > 0 && v.crc_fused && v.nt == 3) {  // host: crc_tile_step for 8/G units
+        const size_t lc = l + 16 * 256 * 4 + (size_t)v.fast_n * 4;
         switch (group) {
-          case 1: hipLaunchKernelGGL((encode_tiles_group_kernel<3, 1>), dim3(grid), dim3(kBlock), l, s, v); return;
-          case 2: hipLaunchKernelGGL((encode_tiles_group_kernel<3, 2>), dim3(grid), dim3(kBlock), l, s, v); return;
-          case 4: hipLaunchKernelGGL((encode_tiles_group_kernel<3, 4>), dim3(grid), dim3(kBlock), l, s, v); return;
+          case 1: hipLaunchKernelGGL((encode_tiles_group_kernel<3, 1, true, true>), dim3(grid), dim3(kBlock), lc, s, v); return true;
+          case 2: hipLaunchKernelGGL((encode_tiles_group_kernel<3, 2, true, true>), dim3(grid), dim3(kBlock), lc, s, v); return true;
+          case 4: hipLaunchKernelGGL((encode_tiles_group_kernel<3, 4, true, true>), dim3(grid), dim3(kBlock), lc, s, v); return true;
           default: break;
         }
       }
+      if (group > 0 && !v.crc_fused && v.nt == 3) {  // host: piece_shift == 0, item_mul
+        switch (group) {
+          case 1: hipLaunchKernelGGL((encode_tiles_group_kernel<3, 1>), dim3(grid), dim3(kBlock), l, s, v); return true;
+          case 2: hipLaunchKernelGGL((encode_tiles_group_kernel<3, 2>), dim3(grid), dim3(kBlock), l, s, v); return true;
+          case 4: hipLaunchKernelGGL((encode_tiles_group_kernel<3, 4>), dim3(grid), dim3(kBlock), l, s, v); return true;
+          default: break;
+        }
+      }
+      if (group > 0) return false;
       if (v.crc_fused) {  // chunk crc32c of the stored payload: tables + per-unit shifts
-        hipLaunchKernelGGL((decode_tiles_kernel<3, 1, true, true>), dim3(grid), dim3(kBlock),
-                           l + 16 * 256 * 4 + (size_t)v.fast_n * 4, s, v);
-        return;
+        // (3 waves per SIMD as on decode unless ZH_CRC_W3=0)
+        const char* e = getenv("ZH_CRC_W3");
+        if (e && e[0] == '0')
+          hipLaunchKernelGGL((decode_tiles_kernel<3, 1, true, true>), dim3(grid), dim3(kBlock),
+                             l + 16 * 256 * 4 + (size_t)v.fast_n * 4, s, v);
+        else
+          hipLaunchKernelGGL((decode_tiles_crc_w3_kernel<3, true>), dim3(grid), dim3(kBlock),
+                             l + 16 * 256 * 4 + (size_t)v.fast_n * 4, s, v);
+        return true;
       }
       switch (v.nt) {
         case 0: hipLaunchKernelGGL((decode_tiles_kernel<0, 1, false, true>), dim3(grid), dim3(kBlock), l, s, v); break;
@@ -2447,8 +2556,10 @@ static void launch_encode_fast_ds(const ScatterArgs& v, int grid, int deep, int 
     }
   } else if (v.fast_mode != kFastNone && v.crc_fused) {
     // chunk crc32c of the stored payload, fused (rows sequential in the payload)
+    // 4 rows in flight per lane unless deep ≥ 2 (c3crc write 52.6 → 47.4 ms with 4,
+    // profiles/r02/write/ab_crcw.txt)
     const size_t l = lds + 12 * 256 * 4;
-    if (deep)
+    if (deep >= 2)
       hipLaunchKernelGGL((decode_rows_kernel<DS, 8, 3, true, true>), dim3(grid), dim3(kBlock), l, s, v);
     else
       hipLaunchKernelGGL((decode_rows_kernel<DS, 4, 3, true, true>), dim3(grid), dim3(kBlock), l, s, v);
@@ -2456,34 +2567,37 @@ static void launch_encode_fast_ds(const ScatterArgs& v, int grid, int deep, int 
     if constexpr (DS == 4) {
       if (deep) {
         switch (v.nt) {
-          case 0: hipLaunchKernelGGL((decode_rows_kernel<DS, 8, 0, false, true>), dim3(grid), dim3(kBlock), lds, s, v); return;
-          case 1: hipLaunchKernelGGL((decode_rows_kernel<DS, 8, 1, false, true>), dim3(grid), dim3(kBlock), lds, s, v); return;
-          case 2: hipLaunchKernelGGL((decode_rows_kernel<DS, 8, 2, false, true>), dim3(grid), dim3(kBlock), lds, s, v); return;
-          default: hipLaunchKernelGGL((decode_rows_kernel<DS, 8, 3, false, true>), dim3(grid), dim3(kBlock), lds, s, v); return;
+          case 0: hipLaunchKernelGGL((decode_rows_kernel<DS, 8, 0, false, true>), dim3(grid), dim3(kBlock), lds, s, v); return true;
+          case 1: hipLaunchKernelGGL((decode_rows_kernel<DS, 8, 1, false, true>), dim3(grid), dim3(kBlock), lds, s, v); return true;
+          case 2: hipLaunchKernelGGL((decode_rows_kernel<DS, 8, 2, false, true>), dim3(grid), dim3(kBlock), lds, s, v); return true;
+          default: hipLaunchKernelGGL((decode_rows_kernel<DS, 8, 3, false, true>), dim3(grid), dim3(kBlock), lds, s, v); return true;
         }
       }
       switch (v.nt) {
-        case 0: hipLaunchKernelGGL((decode_rows_kernel<DS, 4, 0, false, true>), dim3(grid), dim3(kBlock), lds, s, v); return;
-        case 1: hipLaunchKernelGGL((decode_rows_kernel<DS, 4, 1, false, true>), dim3(grid), dim3(kBlock), lds, s, v); return;
-        case 2: hipLaunchKernelGGL((decode_rows_kernel<DS, 4, 2, false, true>), dim3(grid), dim3(kBlock), lds, s, v); return;
+        case 0: hipLaunchKernelGGL((decode_rows_kernel<DS, 4, 0, false, true>), dim3(grid), dim3(kBlock), lds, s, v); return true;
+        case 1: hipLaunchKernelGGL((decode_rows_kernel<DS, 4, 1, false, true>), dim3(grid), dim3(kBlock), lds, s, v); return true;
+        case 2: hipLaunchKernelGGL((decode_rows_kernel<DS, 4, 2, false, true>), dim3(grid), dim3(kBlock), lds, s, v); return true;
         default: break;
       }
     }
     hipLaunchKernelGGL((decode_rows_kernel<DS, 4, 3, false, true>), dim3(grid), dim3(kBlock), lds,
                        s, v);
   }
+  return true;
 }
 
 hipError_t launch_encode_fast(const ScatterArgs& view, int grid, int deep, int group,
                               hipStream_t stream) {
   if (view.total_items == 0 || view.fast_mode == kFastNone) return hipSuccess;
+  bool ok = false;
   switch (view.dsize) {
-    case 1: launch_encode_fast_ds<1>(view, grid, deep, group, stream); break;
-    case 2: launch_encode_fast_ds<2>(view, grid, deep, group, stream); break;
-    case 4: launch_encode_fast_ds<4>(view, grid, deep, group, stream); break;
-    case 8: launch_encode_fast_ds<8>(view, grid, deep, group, stream); break;
+    case 1: ok = launch_encode_fast_ds<1>(view, grid, deep, group, stream); break;
+    case 2: ok = launch_encode_fast_ds<2>(view, grid, deep, group, stream); break;
+    case 4: ok = launch_encode_fast_ds<4>(view, grid, deep, group, stream); break;
+    case 8: ok = launch_encode_fast_ds<8>(view, grid, deep, group, stream); break;
     default: return hipErrorInvalidValue;
   }
+  if (!ok) return hipErrorInvalidValue;
   return hipGetLastError();
 }
 
