@@ -11,11 +11,12 @@ from .codecs import (BloscCodec, BytesCodec, CodecBuilder, CodecRegistry, Crc32c
 from .dtypes import DataType
 from .errors import UnsupportedChainError, ZarrException
 from .metadata import ArrayMetadata, ArrayMetadataBuilder, ChunkKeyEncoding, parse_fill_value
-from .store import FilesystemStore, MemoryStore, StoreHandle
+from .store import FilesystemStore, HttpStore, MemoryStore, StoreException, StoreHandle
 
 __all__ = ["Array", "ArrayAccessor", "ArrayMetadata", "ArrayMetadataBuilder", "BloscCodec",
            "ReshapeCodec",
            "BytesCodec", "ChunkKeyEncoding", "CodecBuilder", "CodecRegistry", "Crc32cCodec",
-           "DataType", "FilesystemStore", "GzipCodec", "MemoryStore", "ShardingIndexedCodec",
+           "DataType", "FilesystemStore", "GzipCodec", "HttpStore", "MemoryStore",
+           "ShardingIndexedCodec", "StoreException",
            "StoreHandle", "TransposeCodec", "UnsupportedChainError", "ZarrException",
            "ZstdCodec", "device", "device_chain", "parse_fill_value"]

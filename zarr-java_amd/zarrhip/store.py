@@ -1,12 +1,25 @@
 """Key/value stores with the reference's range-read contract (host byte sources).
 
-Mirrors M/store/Store.java:9-41, StoreHandle.java:20-70, FilesystemStore.java:40-102 and
-MemoryStore.java:17-56: `get(keys)` whole value or None; `get(keys, start)` from start
-(negative start = suffix); `get(keys, start, end)` = [start, end) with a negative start
-counted from the end.
+Mirrors M/store/Store.java:9-41, StoreHandle.java:20-70, FilesystemStore.java:40-102,
+MemoryStore.java:17-56 and HttpStore.java:13-232: `get(keys)` whole value or None;
+`get(keys, start)` from start (negative start = suffix); `get(keys, start, end)` = [start, end)
+with a negative start counted from the end (HttpStore: rejected, as in the reference).
 """
 import os
 import threading
+import time
+import urllib.error
+import urllib.parse
+import urllib.request
+
+
+class StoreException(RuntimeError):
+    """M/store/StoreException.java: `readFailed` wraps the cause's message."""
+
+    @staticmethod
+    def read_failed(store_path, keys, cause):
+        return StoreException("Failed to read from store '%s' at key '%s': %s"
+                              % (store_path, "/".join(keys), cause))
 
 
 class Store:
@@ -132,6 +145,113 @@ class MemoryStore(Store):
     def delete(self, keys):
         with self.lock:
             self.map.pop(tuple(keys), None)
+
+
+class HttpStore(Store):
+    """HttpStore.java: read-only HTTP(S) store.  Keys are appended as path segments
+    (`resolveKeys`, :34-45); ranges go out as `Range` headers (:79-98: `bytes=s-`,
+    `bytes=-n` suffix, `bytes=s-(e-1)`); 404 → None, other failures raise StoreException
+    (`readFailed`); 502/503/504-style 5xx responses and I/O errors are retried
+    `max_retries` times `retry_delay_ms` apart (RetryInterceptor, :200-231); `size` is a
+    HEAD Content-Length with identity encoding (:166-196, -1 → None here)."""
+
+    def __init__(self, uri, timeout_seconds=60, max_retries=3, retry_delay_ms=1000):
+        if not urllib.parse.urlparse(uri).scheme.startswith("http"):
+            raise ValueError("Invalid base URI: " + uri)
+        self.uri = uri
+        self.timeout = timeout_seconds
+        self.max_retries = max_retries
+        self.delay = retry_delay_ms / 1000.0
+
+    def _url(self, keys):
+        segs = [urllib.parse.quote(seg, safe="") for k in keys for seg in str(k).split("/")]
+        return self.uri.rstrip("/") + "/" + "/".join(segs)
+
+    def _open(self, req):
+        """RetryInterceptor: the response, or None for 404; raises HTTPError / OSError."""
+        last = None
+        for i in range(self.max_retries + 1):
+            if i:
+                time.sleep(self.delay)
+            try:
+                return urllib.request.urlopen(req, timeout=self.timeout)
+            except urllib.error.HTTPError as e:
+                if e.code == 404:
+                    return None
+                if e.code < 500 or i == self.max_retries:
+                    raise
+                last = e
+            except OSError as e:
+                last = e
+                if i == self.max_retries:
+                    raise
+        raise last if last else OSError("Request failed after retries")
+
+    def _get(self, keys, headers):
+        req = urllib.request.Request(self._url(keys), headers=headers)
+        try:
+            r = self._open(req)
+            if r is None:
+                return None
+            with r:
+                return r.read()
+        except urllib.error.HTTPError as e:
+            raise StoreException.read_failed(
+                self.uri, keys, "HTTP request failed with status code: %d %s" % (e.code, e.reason)) from None
+        except OSError as e:
+            raise StoreException.read_failed(self.uri, keys, e) from None
+
+    def exists(self, keys):
+        try:
+            r = self._open(urllib.request.Request(self._url(keys), method="HEAD"))
+        except OSError:
+            return False
+        if r is None:
+            return False
+        with r:
+            return 200 <= r.status < 300
+
+    def get(self, keys, start=None, end=None):
+        if start is None:
+            return self._get(keys, {})
+        if end is None:
+            rng = "bytes=%d" % start if start < 0 else "bytes=%d-" % start
+            return self._get(keys, {"Range": rng})
+        if start < 0:
+            raise ValueError("Argument 'start' needs to be non-negative.")
+        return self._get(keys, {"Range": "bytes=%d-%d" % (start, end - 1)})
+
+    def size(self, keys):
+        req = urllib.request.Request(self._url(keys), method="HEAD",
+                                     headers={"Accept-Encoding": "identity"})
+        try:
+            r = self._open(req)
+        except urllib.error.HTTPError:
+            return None
+        except OSError as e:
+            raise StoreException.read_failed(
+                self.uri, keys, "Failed to get content length from HTTP HEAD request to: "
+                + self._url(keys) + " (%s)" % e) from None
+        if r is None:
+            return None
+        with r:
+            n = r.headers.get("Content-Length")
+        if n is None:
+            return None
+        try:
+            return int(n)
+        except ValueError:
+            raise StoreException.read_failed(
+                self.uri, keys, "Invalid Content-Length header value from: " + self._url(keys)) from None
+
+    def set(self, keys, data):
+        raise NotImplementedError("Not implemented")
+
+    def delete(self, keys):
+        raise NotImplementedError("Not implemented")
+
+    def __repr__(self):
+        return self.uri
 
 
 class StoreHandle:
