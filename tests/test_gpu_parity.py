@@ -77,6 +77,34 @@ def test_device_crc_on_reference_index_bytes(dev, loc, stored_crc):
         assert str(e).startswith("unexpected inner chunk byte length")
 
 
+@pytest.mark.parametrize("loc,stored_crc", [("end", 0xB756D1D4), ("start", 0x56F05363)])
+def test_device_chunk_crc_on_reference_bytes(dev, loc, stored_crc):
+    """The inner-chunk crc32c path (Crc32cCodec.encode/decode, Crc32cCodec.java:24-60, run as
+    an inner codec) pinned to reference-produced bytes: an inner chunk whose 64-byte payload
+    is the reference fixture's index body must carry the crc the reference stored for it;
+    that chunk decodes, and with the crc flipped the read reports the reference message."""
+    import os
+    import struct
+    from helpers import GOLDEN
+    raw = open(os.path.join(GOLDEN, "sharding_index_location", loc, "c", "0", "0", "0"),
+               "rb").read()
+    body = raw[:64] if loc == "start" else raw[len(raw) - 68:len(raw) - 4]
+    data = np.frombuffer(body, "<u4").reshape(4, 4)
+    meta = A.make_meta([4, 4], [4, 4], 4, endian=A.ZH_ENDIAN_LITTLE, sharded=True,
+                       inner_chunk_shape=[4, 4], inner_crc32c=True)
+    shard = device_write(dev, meta, data)[0]
+    assert shard[:64] == body
+    assert struct.unpack("<I", shard[64:68])[0] == stored_crc
+    assert shard == encode_oracle(meta, data)[0]
+    np.testing.assert_array_equal(device_read(dev, meta, [shard], [0, 0], [4, 4]), data)
+    bad = shard[:64] + struct.pack("<I", stored_crc ^ 1) + shard[68:]
+    signed = struct.unpack("<i", struct.pack("<I", stored_crc))[0]
+    with pytest.raises(ZhError) as ed:
+        device_read(dev, meta, [bad], [0, 0], [4, 4])
+    assert str(ed.value) == ("The checksum of the sharding index is invalid. Stored: "
+                             f"{signed ^ 1} Computed: {signed}")
+
+
 @pytest.mark.parametrize("zext", [24, 20, 22, 17, 32])
 @pytest.mark.parametrize("dsize", [2, 4, 8])
 @pytest.mark.parametrize("sharded", [False, True])

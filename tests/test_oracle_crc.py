@@ -48,3 +48,22 @@ def test_oracle_chunk_crc_mismatch_message(sharded):
     with pytest.raises(O.OracleError, match=r"The checksum of the sharding index is invalid\. "
                                              r"Stored: -?\d+ Computed: -?\d+"):
         O.array_read(m, [bytes(b)], [0, 0], shape)
+
+
+@pytest.mark.parametrize("loc,stored_crc", [("end", 0xB756D1D4), ("start", 0x56F05363)])
+def test_oracle_inner_chunk_crc_on_reference_bytes(loc, stored_crc):
+    """The oracle's inner crc32c encode (Crc32cCodec.encode, Crc32cCodec.java:50-60) of a
+    chunk whose payload is the reference fixture's 64-byte index body appends the crc the
+    reference stored for those bytes."""
+    import os
+    import struct
+    import numpy as np
+    from helpers import GOLDEN, encode_oracle
+    from zarrhip import _abi as A
+    raw = open(os.path.join(GOLDEN, "sharding_index_location", loc, "c", "0", "0", "0"),
+               "rb").read()
+    body = raw[:64] if loc == "start" else raw[len(raw) - 68:len(raw) - 4]
+    meta = A.make_meta([4, 4], [4, 4], 4, endian=A.ZH_ENDIAN_LITTLE, sharded=True,
+                       inner_chunk_shape=[4, 4], inner_crc32c=True)
+    shard = encode_oracle(meta, np.frombuffer(body, "<u4").reshape(4, 4))[0]
+    assert shard[:64] == body and struct.unpack("<I", shard[64:68])[0] == stored_crc
