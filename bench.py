@@ -216,7 +216,11 @@ def pmc_traffic(config):
 
 
 def kernel_name(meta):
-    return "decode_tiles_kernel" if meta.chain.has_transpose else "decode_rows_kernel<4,4>"
+    # tile chains: tiles_group_kernel (ZH_DEC_TGROUP=0: decode_tiles_kernel)
+    if meta.chain.has_transpose:
+        return "decode_tiles_kernel" if os.environ.get("ZH_DEC_TGROUP") == "0" else \
+            "tiles_group_kernel"
+    return "decode_rows_kernel<4,4>"
 
 
 def roofline_of(plan, st, config=None):

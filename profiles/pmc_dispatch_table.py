@@ -8,7 +8,8 @@ import sys
 
 for d in sys.argv[1:]:
     rows = [r for r in csv.DictReader(open(os.path.join(d, "run_counter_collection.csv")))
-            if "decode_tiles_kernel" in r["Kernel_Name"] or "decode_rows_kernel" in r["Kernel_Name"]]
+            if any(k in r["Kernel_Name"] for k in ("decode_tiles_kernel", "decode_rows_kernel",
+                                                  "tiles_group_kernel"))]
     rows = [r for r in rows if not r["Kernel_Name"].split(">")[0].rstrip().endswith("true")]
     by = collections.OrderedDict()
     for r in rows:

@@ -76,3 +76,27 @@ def test_tile_crc_variants_and_item_order(dev, monkeypatch, variant, perm):
     np.testing.assert_array_equal(got, arr)
     # shard (1,0,0) holds 4 inner chunks; flip a bit of the 4th one's last payload byte
     _corrupt_matches_oracle(dev, meta, shards, 2, 3 * CHUNK + CHUNK - 5)
+
+
+@pytest.mark.parametrize("order", [[0, 2, 1], [2, 1, 0], [1, 2, 0]])
+@pytest.mark.parametrize("group,pf", [("0", "1"), ("1", "0"), ("1", "1"), ("2", "0"),
+                                      ("2", "1"), ("4", "0"), ("4", "1"), ("8", "0")])
+@pytest.mark.parametrize("crc", [True, False])
+def test_grouped_tile_decode(dev, monkeypatch, order, group, pf, crc):
+    """tiles_group_kernel in the decode direction (ZH_DEC_TGROUP chunks per work item, 8/G
+    tiles of each per step; ZH_DEC_TPF: the next step's loads before this step's stores),
+    with and without the fused chunk CRC (unit fold for the 8/G stride): an elided inner
+    chunk, a missing shard, a clipped region; a corrupt byte of a fast chunk is caught."""
+    monkeypatch.setenv("ZH_DEC_TGROUP", group)
+    monkeypatch.setenv("ZH_DEC_TPF", pf)
+    meta = A.make_meta(SHAPE, [32, 64, 64], 4, endian=A.ZH_ENDIAN_BIG, sharded=True,
+                       inner_chunk_shape=[32, 32, 32], transpose_order=order, inner_crc32c=crc)
+    arr = rand_array(SHAPE, 4, seed=47)
+    arr[32:64, 0:32, 32:64] = 0
+    shards = encode_oracle(meta, arr)
+    shards[2] = None
+    for off, shp in [([0, 0, 0], SHAPE), ([5, 3, 7], [50, 60, 80])]:
+        got, want = _read_both(dev, meta, shards, off, shp)
+        np.testing.assert_array_equal(got, want)
+    if crc:
+        _corrupt_matches_oracle(dev, meta, shards, 1, CHUNK + 1000)

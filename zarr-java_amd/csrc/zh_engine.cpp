@@ -1095,10 +1095,10 @@ int zh_plan_create(zh_ctx* ctx, const zh_array_meta* m, const zh_chunk_src* chun
       ((int64_t)p->args.fast_n * 8 + 15) / 16 * 16 + 8 * 1057 * 4 + 16 * 256 * 4 +
               (int64_t)p->args.fast_n * 4 <= 65536;
   p->args.crc_tile_step = 0;
+  std::vector<int64_t> ends;  // per-unit payload ends (tile CRC; the grouped step below)
   if (tile_crc) {
     const ScatterArgs& g = p->args;
     const int64_t L = g.inner_nbytes, s_fd = g.pstride[g.fd];
-    std::vector<int64_t> ends;
     for (int32_t u = 0; u < g.fast_n; u++) {
       const int64_t end = 4 * (int64_t)tab[2 * (size_t)u] + 4 * 31 * s_fd + 128;
       ends.push_back(end);
@@ -1210,15 +1210,20 @@ int zh_plan_create(zh_ctx* ctx, const zh_array_meta* m, const zh_chunk_src* chun
   p->args.item_mul =
       env_int("ZH_ITEM_PERM", p->tile_mode ? 1 : 0) ? golden_item_mul(p->args.total_items) : 0;
   p->slow_grid = p->grid;
-  // ZH_DEC_TGROUP = G (1, 2, 4): the tile decode over G consecutive chunks per work item
-  // (encode_tiles_group_kernel in the decode direction; tile_variant 10 + G)
+  // The tile decode over G consecutive (z-adjacent) chunks per work item, the next step's
+  // loads issued before this step's stores (tiles_group_kernel; tile_variant 20 + G, 10 + G
+  // without the prefetch): c4 33.4 → 32.9 ms (G = 4), c4crc 39.5 → 38.3 ms (G = 2), interleaved
+  // A/B in profiles/r02/experiments/ab_r02abdtgpf*.txt.  ZH_DEC_TGROUP = G (0: the
+  // row-interleaved tile kernel; 1, 2, 4, 8, with the chunk CRC 1, 2, 4), ZH_DEC_TPF = 0/1.
   {
-    const int G = env_int("ZH_DEC_TGROUP", 0);
-    if ((G == 1 || G == 2 || G == 4 || G == 8) && p->tile_mode && p->args.fast_mode == kFastTileTable &&
-        p->args.tile_variant == 1 && !p->args.crc_fused && p->args.piece_shift == 0 &&
-        (p->args.nt & 3) == 3 && items > 0) {
+    const bool crc = p->args.crc_fused != 0;
+    const int G = env_int("ZH_DEC_TGROUP", crc ? 2 : 4);
+    if ((G == 1 || G == 2 || G == 4 || (G == 8 && !crc)) && p->tile_mode &&
+        p->args.fast_mode == kFastTileTable && p->args.tile_variant == 1 &&
+        (!crc || tile_crc) && p->args.piece_shift == 0 && (p->args.nt & 3) == 3 && items > 0) {
       const int64_t groups = (items + G - 1) / G;
-      p->args.tile_variant = 10 + G;
+      p->args.tile_variant = (env_int("ZH_DEC_TPF", 1) && G != 8 ? 20 : 10) + G;
+      if (crc) p->args.crc_tile_step = tile_crc_step(ends, (size_t)(8 / G));
       p->args.item_mul = env_int("ZH_ITEM_PERM", 1) ? golden_item_mul(groups) : 0;
       p->grid = grid_for(ctx, groups);
     }
@@ -2321,7 +2326,7 @@ static int array_write_fast(zh_ctx* ctx, const zh_array_meta* m, ScatterArgs a,
     if (G && (G << v.fast_vpr_shift) <= 64) group = G;
   }
   // tiles (uint32 transposed chunks): G chunks per work item, 8/G tiles of each per step
-  // (ZH_ENC_TGROUP: 0 off; encode_tiles_group_kernel)
+  // (ZH_ENC_TGROUP: 0 off; tiles_group_kernel)
   // With the tile CRC fused, the kernel folds each lane's units (8/G apart) with the step
   // for that stride.
   if (v.fast_mode == kFastTileTable && (!crc_fuse || tile_crc) && v.nt == 3 &&

@@ -1472,13 +1472,16 @@ __global__ __launch_bounds__(kBlock) void decode_tiles_kernel(ScatterArgs a) {
 // lanes and stay on the slow list).  No CRC, piece_shift == 0 (host-checked).
 //
 // FLAGS = false: the decode direction (payload → region; every fast tile item is a full copy),
-// ZH_DEC_TGROUP.  CRC (encode only): the chunk crc32c of the stored payload, fused as in
-// fast_tiles_rows (the stored rows have the decode loads' geometry): a lane's 8 stored vectors
+// ZH_DEC_TGROUP.  CRC: the chunk crc32c of the payload (encode: the stored vectors, which
+// have the decode loads' geometry; decode: the loaded ones), fused as in fast_tiles_rows: a
+// lane's 8 vectors
 // fold with S, its units (u, u + 8/G, …) with SD = x^(8Δ) for that unit stride (host:
 // tile_crc_step(ends, 8/G)), one K multiply per chunk, the lane constant kb, then an XOR over
 // the chunk's lane segment and one atomic per wave.
-template <int NT, int G, bool FLAGS = true, bool CRC = false>
-__global__ __launch_bounds__(kBlock) void encode_tiles_group_kernel(ScatterArgs a) {
+//
+// PF: the next step's loads are issued before this step's stores (decode_tiles_body's order).
+template <int NT, int G, bool CRC, bool PF, bool FLAGS>
+__global__ __launch_bounds__(kBlock) void tiles_group_kernel(ScatterArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   uint2* tab = reinterpret_cast<uint2*>(smem);
   uint8_t* after_tab = smem + (((size_t)a.fast_n * 8 + 15) & ~(size_t)15);
@@ -1500,7 +1503,9 @@ __global__ __launch_bounds__(kBlock) void encode_tiles_group_kernel(ScatterArgs 
     SD = S + 4;
     K = reinterpret_cast<uint32_t*>(SD + 4);
     init_crc_tables(T);
-    const uint32_t kg = x2nmodp((uint64_t)(4 * d_fs), 3);  // stored row pitch
+    // payload row pitch of the lane's vectors: the stored rows (encode) or the loaded rows
+    const int64_t pitch = FLAGS ? d_fs : s_fd;
+    const uint32_t kg = x2nmodp((uint64_t)(4 * pitch), 3);
 #pragma unroll
     for (int b = 0; b < 4; b++) {
       S[b][threadIdx.x] = multmodp(kg, (uint32_t)threadIdx.x << (8 * b));
@@ -1508,7 +1513,7 @@ __global__ __launch_bounds__(kBlock) void encode_tiles_group_kernel(ScatterArgs 
           a.crc_tile_step ? multmodp(a.crc_tile_step, (uint32_t)threadIdx.x << (8 * b)) : 0u;
     }
     for (int i = threadIdx.x; i < a.fast_n; i += kBlock) K[i] = a.fast_tab[2 * a.fast_n + i];
-    kb = x2nmodp((uint64_t)(4 * (24 - 8 * wave) * d_fs + 112 - 16 * g), 3);
+    kb = x2nmodp((uint64_t)(4 * (24 - 8 * wave) * pitch + 112 - 16 * g), 3);
   }
   __syncthreads();
   const bool regular = CRC && a.crc_tile_step != 0;
@@ -1534,16 +1539,23 @@ __global__ __launch_bounds__(kBlock) void encode_tiles_group_kernel(ScatterArgs 
     if (__syncthreads_or(on) == 0) continue;  // block-uniform
     bool differs = false;
     uint32_t share = 0, run = 0, ulast = ~0u;
+    uint4 x[8];
+    auto load = [&](uint32_t ub_) {
+      const uint32_t uu = ub_ + ti;
+      if (on && uu < units) {
+        const uint8_t* base = src + ((size_t)tab[uu].x + g * 4) * 4;
+#pragma unroll
+        for (int k = 0; k < 8; k++)
+          x[k] = ld16s<(NT & 1) != 0>(base + (size_t)(wave * 8 + k) * s_fd * 4);
+      }
+    };
+    if (PF) load(0);
 #pragma unroll 1
     for (uint32_t ub = 0; ub < units; ub += TG) {
       const uint32_t u = ub + ti;
       const bool live = on && u < units;
+      if (!PF) load(ub);
       if (live) {
-        const uint8_t* base = src + ((size_t)tab[u].x + g * 4) * 4;
-        uint4 x[8];
-#pragma unroll
-        for (int k = 0; k < 8; k++)
-          x[k] = ld16s<(NT & 1) != 0>(base + (size_t)(wave * 8 + k) * s_fd * 4);
 #pragma unroll
         for (int k = 0; k < 8; k++) {
           if (FLAGS) differs |= (x[k].x != f) | (x[k].y != f) | (x[k].z != f) | (x[k].w != f);
@@ -1555,6 +1567,12 @@ __global__ __launch_bounds__(kBlock) void encode_tiles_group_kernel(ScatterArgs 
         }
       }
       __syncthreads();
+      uint4 xc[8];  // this step's payload vectors (decode CRC) while x takes the next step's
+      if constexpr (CRC && !FLAGS) {
+#pragma unroll
+        for (int k = 0; k < 8; k++) xc[k] = x[k];
+      }
+      if (PF && ub + TG < units) load(ub + TG);
       if (live) {
         uint8_t* base = dst + ((size_t)tab[u].y + g * 4) * 4;
         uint32_t eacc = 0;
@@ -1567,8 +1585,16 @@ __global__ __launch_bounds__(kBlock) void encode_tiles_group_kernel(ScatterArgs 
           y.z = mine[(g * 4 + 2) * 33 + r];
           y.w = mine[(g * 4 + 3) * 33 + r];
           st16s<(NT & 2) != 0>(base + (size_t)r * d_fs * 4, y);
-          if constexpr (CRC) {
+          if constexpr (CRC && FLAGS) {  // encode: the stored vectors
             const v4u w = {y.x, y.y, y.z, y.w};
+            const uint32_t ck = crc_upd16(0u, w, T);
+            eacc = k ? crc_shift_tab(eacc, S) ^ ck : ck;
+          }
+        }
+        if constexpr (CRC && !FLAGS) {  // decode: the loaded payload vectors, stores in flight
+#pragma unroll
+          for (int k = 0; k < 8; k++) {
+            const v4u w = {xc[k].x, xc[k].y, xc[k].z, xc[k].w};
             const uint32_t ck = crc_upd16(0u, w, T);
             eacc = k ? crc_shift_tab(eacc, S) ^ ck : ck;
           }
@@ -2399,12 +2425,38 @@ static void launch_scatter_ds(const ScatterArgs& a, int tile, int enc, int grid,
         const int v = a.tile_variant;
         lds += v == 0 ? (size_t)kFastTPB * 32 * 33 * 4 : (size_t)kTG * kTilePitch * 4;
         const bool ntx = nt == 3;
+        if (v > 20 && a.crc_fused) {  // prefetching form (ZH_DEC_TPF=1)
+          const size_t lc = lds + 16 * 256 * 4 + (size_t)a.fast_n * 4;
+          switch (v - 20) {
+            case 1: hipLaunchKernelGGL((tiles_group_kernel<3, 1, true, true, false>), dim3(grid), dim3(kBlock), lc, s, a); return;
+            case 2: hipLaunchKernelGGL((tiles_group_kernel<3, 2, true, true, false>), dim3(grid), dim3(kBlock), lc, s, a); return;
+            case 4: hipLaunchKernelGGL((tiles_group_kernel<3, 4, true, true, false>), dim3(grid), dim3(kBlock), lc, s, a); return;
+            default: return;
+          }
+        }
+        if (v > 20) {
+          switch (v - 20) {
+            case 1: hipLaunchKernelGGL((tiles_group_kernel<3, 1, false, true, false>), dim3(grid), dim3(kBlock), lds, s, a); return;
+            case 2: hipLaunchKernelGGL((tiles_group_kernel<3, 2, false, true, false>), dim3(grid), dim3(kBlock), lds, s, a); return;
+            case 4: hipLaunchKernelGGL((tiles_group_kernel<3, 4, false, true, false>), dim3(grid), dim3(kBlock), lds, s, a); return;
+            default: return;
+          }
+        }
+        if (v > 10 && a.crc_fused) {  // + the chunk CRC (host: unit step for 8/G units)
+          const size_t lc = lds + 16 * 256 * 4 + (size_t)a.fast_n * 4;
+          switch (v - 10) {
+            case 1: hipLaunchKernelGGL((tiles_group_kernel<3, 1, true, false, false>), dim3(grid), dim3(kBlock), lc, s, a); return;
+            case 2: hipLaunchKernelGGL((tiles_group_kernel<3, 2, true, false, false>), dim3(grid), dim3(kBlock), lc, s, a); return;
+            case 4: hipLaunchKernelGGL((tiles_group_kernel<3, 4, true, false, false>), dim3(grid), dim3(kBlock), lc, s, a); return;
+            default: return;
+          }
+        }
         if (v > 10) {  // host: G chunks per work item, item_mul and grid over the groups
           switch (v - 10) {
-            case 1: hipLaunchKernelGGL((encode_tiles_group_kernel<3, 1, false>), dim3(grid), dim3(kBlock), lds, s, a); return;
-            case 2: hipLaunchKernelGGL((encode_tiles_group_kernel<3, 2, false>), dim3(grid), dim3(kBlock), lds, s, a); return;
-            case 4: hipLaunchKernelGGL((encode_tiles_group_kernel<3, 4, false>), dim3(grid), dim3(kBlock), lds, s, a); return;
-            case 8: hipLaunchKernelGGL((encode_tiles_group_kernel<3, 8, false>), dim3(grid), dim3(kBlock), lds, s, a); return;
+            case 1: hipLaunchKernelGGL((tiles_group_kernel<3, 1, false, false, false>), dim3(grid), dim3(kBlock), lds, s, a); return;
+            case 2: hipLaunchKernelGGL((tiles_group_kernel<3, 2, false, false, false>), dim3(grid), dim3(kBlock), lds, s, a); return;
+            case 4: hipLaunchKernelGGL((tiles_group_kernel<3, 4, false, false, false>), dim3(grid), dim3(kBlock), lds, s, a); return;
+            case 8: hipLaunchKernelGGL((tiles_group_kernel<3, 8, false, false, false>), dim3(grid), dim3(kBlock), lds, s, a); return;
             default: return;
           }
         }
@@ -2521,17 +2573,17 @@ static bool launch_encode_fast_ds(const ScatterArgs& v, int grid, int deep, int 
       if (group > 0 && v.crc_fused && v.nt == 3) {  // host: crc_tile_step for 8/G units
         const size_t lc = l + 16 * 256 * 4 + (size_t)v.fast_n * 4;
         switch (group) {
-          case 1: hipLaunchKernelGGL((encode_tiles_group_kernel<3, 1, true, true>), dim3(grid), dim3(kBlock), lc, s, v); return true;
-          case 2: hipLaunchKernelGGL((encode_tiles_group_kernel<3, 2, true, true>), dim3(grid), dim3(kBlock), lc, s, v); return true;
-          case 4: hipLaunchKernelGGL((encode_tiles_group_kernel<3, 4, true, true>), dim3(grid), dim3(kBlock), lc, s, v); return true;
+          case 1: hipLaunchKernelGGL((tiles_group_kernel<3, 1, true, false, true>), dim3(grid), dim3(kBlock), lc, s, v); return true;
+          case 2: hipLaunchKernelGGL((tiles_group_kernel<3, 2, true, false, true>), dim3(grid), dim3(kBlock), lc, s, v); return true;
+          case 4: hipLaunchKernelGGL((tiles_group_kernel<3, 4, true, false, true>), dim3(grid), dim3(kBlock), lc, s, v); return true;
           default: break;
         }
       }
       if (group > 0 && !v.crc_fused && v.nt == 3) {  // host: piece_shift == 0, item_mul
         switch (group) {
-          case 1: hipLaunchKernelGGL((encode_tiles_group_kernel<3, 1>), dim3(grid), dim3(kBlock), l, s, v); return true;
-          case 2: hipLaunchKernelGGL((encode_tiles_group_kernel<3, 2>), dim3(grid), dim3(kBlock), l, s, v); return true;
-          case 4: hipLaunchKernelGGL((encode_tiles_group_kernel<3, 4>), dim3(grid), dim3(kBlock), l, s, v); return true;
+          case 1: hipLaunchKernelGGL((tiles_group_kernel<3, 1, false, false, true>), dim3(grid), dim3(kBlock), l, s, v); return true;
+          case 2: hipLaunchKernelGGL((tiles_group_kernel<3, 2, false, false, true>), dim3(grid), dim3(kBlock), l, s, v); return true;
+          case 4: hipLaunchKernelGGL((tiles_group_kernel<3, 4, false, false, true>), dim3(grid), dim3(kBlock), l, s, v); return true;
           default: break;
         }
       }
