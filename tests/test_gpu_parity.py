@@ -455,6 +455,44 @@ def test_device_encode_tile_groups(dev, monkeypatch, group, loc):
     assert got == want
 
 
+@pytest.mark.parametrize("crc", [False, True])
+@pytest.mark.parametrize("dsize", [1, 4, 8])
+@pytest.mark.parametrize("group", ["0", "-1", "1", "2", "4"])
+def test_grouped_row_decode(dev, monkeypatch, crc, dsize, group):
+    """rows_group_kernel in the decode direction (ZH_DEC_RGROUP): G consecutive inner chunks
+    per work item with per-lane-group descriptors — copies beside Q1 zero-fill items (elided
+    chunks) and a missing shard's fill, an odd chunk count per shard row, row-clipped boundary
+    chunks sent to the generic kernel, the fused chunk CRC over 256/G lanes per chunk (and a
+    corrupt payload byte caught with the oracle's message)."""
+    monkeypatch.setenv("ZH_DEC_RGROUP", group)
+    inner_last = 128 // dsize
+    shape = [13, 24, inner_last * 7 + inner_last // 2]
+    meta = A.make_meta(shape, [8, 8, inner_last * 5], dsize, endian=A.ZH_ENDIAN_BIG,
+                       sharded=True, inner_chunk_shape=[4, 8, inner_last],
+                       fill=(5).to_bytes(dsize, "little"), inner_crc32c=crc)
+    arr = rand_array(shape, dsize, seed=71 + dsize)
+    arr[arr == 5] = 6
+    arr[0:4, 0:8, inner_last:2 * inner_last] = 5          # elided → Q1 zeros on read
+    shards = encode_oracle(meta, arr)
+    pos = {c: i for i, c in enumerate(chunk_coords(meta, [0, 0, 0], shape))}
+    shards[pos[(1, 1, 0)]] = None                          # missing shard → fill
+    for off, shp in [([0, 0, 0], shape), ([1, 3, 5], [11, 20, shape[2] - 9])]:
+        sel = chunk_coords(meta, off, shp)
+        src = [shards[pos[c]] for c in sel]
+        got = device_read(dev, meta, src, off, shp)
+        want = np.frombuffer(O.array_read(meta, src, off, shp), arr.dtype).reshape(shp)
+        np.testing.assert_array_equal(got, want)
+    if crc:
+        bad = bytearray(shards[0])
+        bad[100] ^= 0x10
+        src = [bytes(bad)] + shards[1:]
+        with pytest.raises(O.OracleError) as eo:
+            O.array_read(meta, src, [0, 0, 0], shape)
+        with pytest.raises(ZhError) as ed:
+            device_read(dev, meta, src, [0, 0, 0], shape)
+        assert str(ed.value) == str(eo.value)
+
+
 @pytest.mark.parametrize("order", [[0, 3, 2, 1], [0, 1, 3, 2]])
 @pytest.mark.parametrize("group", ["-1", "0", "1", "4"])
 def test_tile_encode_chunk_crc_fused(dev, monkeypatch, order, group):

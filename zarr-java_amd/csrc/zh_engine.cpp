@@ -1228,6 +1228,26 @@ int zh_plan_create(zh_ctx* ctx, const zh_array_meta* m, const zh_chunk_src* chun
       p->grid = grid_for(ctx, groups);
     }
   }
+  // The row decode over G consecutive chunks per work item (rows_group_kernel, narrow rows:
+  // G·row bytes of a region row per wave store).  ZH_DEC_RGROUP: 0 off, -1 G·row = 256 B,
+  // or G (1, 2, 4).  Row-clipped items then take the generic kernel (is_fast).  Default: on
+  // with the fused chunk CRC only (c3crc 37.2 → 35.9 ms; plain c3 33.2 → 33.5 ms, so off;
+  // profiles/r02/experiments/ab_r02drg_*.txt).
+  {
+    const int want = env_int("ZH_DEC_RGROUP", p->args.crc_fused ? -1 : 0);
+    const ScatterArgs& g = p->args;
+    if (want != 0 && !p->tile_mode && (g.fast_mode == kFastRowArith || g.fast_mode == kFastRowTable) &&
+        g.piece_shift == 0 && (g.nt & 3) == 3 && items > 0) {
+      int G = want > 0 ? want : (16 >> std::min(g.fast_vpr_shift, 5));
+      G = G >= 4 ? 4 : G >= 2 ? 2 : G;
+      if (G >= 1 && (G << g.fast_vpr_shift) <= 64) {
+        const int64_t groups = (items + G - 1) / G;
+        p->args.row_group = G;
+        p->args.item_mul = env_int("ZH_ITEM_PERM", 0) ? golden_item_mul(groups) : 0;
+        p->grid = grid_for(ctx, groups);
+      }
+    }
+  }
   *out = p;
   return ZH_OK;
 }

@@ -123,7 +123,10 @@ struct ScatterArgs {
   int32_t dsize;
   int32_t tile;
   int32_t nt;                   // fast kernels: bit 0 non-temporal loads, bit 1 stores
-  int32_t tile_variant;         // tile fast path: 0 row-per-tile loads, 1 row-interleaved groups
+  int32_t tile_variant;         // tile fast path: 0 row-per-tile loads, 1 row-interleaved groups,
+                                // 10 + G / 20 + G: tiles_group_kernel (without / with prefetch)
+  int32_t row_group;            // row fast path (decode): G > 0 = rows_group_kernel over G
+                                // chunks per work item (row-clipped items then go slow)
   int32_t crc_extra;            // 4 when each stored chunk carries a trailing crc32c, else 0
   uint64_t item_mul;            // fast kernels visit items in the order (i * item_mul) mod
                                 // total_items (coprime; 0 = identity): decorrelates the

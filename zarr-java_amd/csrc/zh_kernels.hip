@@ -695,7 +695,7 @@ __device__ __forceinline__ ItemDesc resolve_one(const ScatterArgs& a, int64_t ci
 // table path moves uint32 copies only)
 __device__ __forceinline__ bool is_fast(const ScatterArgs& a, const ItemDesc& D) {
   const uint32_t mode = D.kind & kDescModeMask;
-  const bool row_clip = mode == kDescClip && (D.kind & kDescClipRow);
+  const bool row_clip = mode == kDescClip && (D.kind & kDescClipRow) && a.row_group == 0;
   if (a.fast_mode == kFastNone ||
       (mode != kDescFullCopy && mode != kDescFullFill && !row_clip))
     return false;
@@ -1176,8 +1176,11 @@ __global__ __launch_bounds__(kBlock) void decode_rows_kernel(ScatterArgs a) {
 // lane's raw register over its vectors is acc = shift_{16·Lc}(acc) ⊕ upd16(0, v) (table S),
 // shifted to the payload end by x^(8·16·(Lc − 1 − j)); the chunk's lanes XOR their shares
 // (CRC is linear over GF(2)) into its partial, one atomic per wave.
-template <int DS, int G, int U, int NT, bool CRC = false>
-__global__ __launch_bounds__(kBlock) void encode_group_rows_kernel(ScatterArgs a) {
+//
+// FLAGS = false: the decode direction (payload rows → region rows; ZH_DEC_RGROUP): full-fill
+// items store their fill value, the CRC runs over the loaded payload vectors.
+template <int DS, int G, int U, int NT, bool CRC, bool FLAGS>
+__global__ __launch_bounds__(kBlock) void rows_group_kernel(ScatterArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   uint2* tab = reinterpret_cast<uint2*>(smem);
   for (int i = threadIdx.x; i < a.fast_n; i += kBlock)
@@ -1213,7 +1216,8 @@ __global__ __launch_bounds__(kBlock) void encode_group_rows_kernel(ScatterArgs a
   for (int64_t g = blockIdx.x; g < ngroups; g += gridDim.x) {
     const int64_t pg = a.item_mul ? (int64_t)(((uint64_t)g * a.item_mul) % (uint64_t)ngroups) : g;
     const int64_t c = pg * G + q;
-    bool on = false;
+    bool on = false, fill = false;
+    uint4 fv = ffill;
     const uint8_t* src = nullptr;
     uint8_t* dst = nullptr;
     if (c < a.n_citems) {
@@ -1222,6 +1226,10 @@ __global__ __launch_bounds__(kBlock) void encode_group_rows_kernel(ScatterArgs a
       on = (y.z & kDescFast) != 0;
       src = (const uint8_t*)(uintptr_t)(((uint64_t)x.y << 32) | x.x) + col;
       dst = a.region + (int64_t)(((uint64_t)x.w << 32) | x.z) * DS + col;
+      if (!FLAGS) {
+        fill = (y.z & kDescModeMask) == kDescFullFill;
+        fv = fill16<DS>(((uint64_t)y.y << 32) | y.x);
+      }
     }
     if (__syncthreads_or(on) == 0) continue;  // block-uniform: no fast chunk in the group
     bool differs = false;
@@ -1240,29 +1248,32 @@ __global__ __launch_bounds__(kBlock) void encode_group_rows_kernel(ScatterArgs a
           uint64_t so, dof;
           row_offsets(a, tab, r, so, dof);
           dd[u] = dof * DS;
-          v[u] = ld16s<(NT & 1) != 0>(src + so * DS);
+          v[u] = fv;
+          if (!fill) v[u] = ld16s<(NT & 1) != 0>(src + so * DS);
         }
       }
 #pragma unroll
       for (int u = 0; u < U; u++)
         if (dd[u] != ~0ull) {
-          const uint4 w = xform16<DS>(v[u], a.swap, a.is_bool);
+          const uint4 w = fill ? fv : xform16<DS>(v[u], a.swap, a.is_bool);
           st16s<(NT & 2) != 0>(dst + dd[u], w);
-          differs |= (v[u].x != ffill.x) | (v[u].y != ffill.y) | (v[u].z != ffill.z) |
-                     (v[u].w != ffill.w);
-          if constexpr (CRC) {
-            const v4u wv = {w.x, w.y, w.z, w.w};
-            acc = crc_shift_tab(acc, S) ^ crc_upd16(0u, wv, T);
+          if (FLAGS)
+            differs |= (v[u].x != ffill.x) | (v[u].y != ffill.y) | (v[u].z != ffill.z) |
+                       (v[u].w != ffill.w);
+          if constexpr (CRC) {  // the payload vector: stored (encode) or loaded (decode)
+            const uint4 pv = FLAGS ? w : v[u];
+            const v4u wv = {pv.x, pv.y, pv.z, pv.w};
+            if (!fill) acc = crc_shift_tab(acc, S) ^ crc_upd16(0u, wv, T);
           }
         }
     }
     // one flag byte per chunk, set by q's leader in any wave whose lanes saw data
-    if ((__ballot(differs) & qmask) != 0 && leader && on) a.flags[c] = 1;
+    if (FLAGS && (__ballot(differs) & qmask) != 0 && leader && on) a.flags[c] = 1;
     if constexpr (CRC) {
       uint32_t cr = multmodp(kl, acc);
       for (int o = 1; o < (1 << vs); o <<= 1) cr ^= (uint32_t)__shfl_xor((int)cr, o, 64);
       for (int o = GL; o < 64; o <<= 1) cr ^= (uint32_t)__shfl_xor((int)cr, o, 64);
-      if (leader && on) atomicXor(a.crc_partials + c, cr);
+      if (leader && on && !fill) atomicXor(a.crc_partials + c, cr);
     }
   }
 }
@@ -2478,6 +2489,17 @@ static void launch_scatter_ds(const ScatterArgs& a, int tile, int enc, int grid,
           else hipLaunchKernelGGL((decode_tiles_kernel<0, 0>), dim3(grid), dim3(kBlock), lds, s, a);
         }
       }
+    } else if (a.fast_mode != kFastNone && a.row_group > 0) {  // host: nt 3, piece_shift 0
+      const size_t lc = lds + (a.crc_fused ? 12 * 256 * 4 : 0);
+      switch (a.row_group * 2 + (a.crc_fused ? 1 : 0)) {
+        case 2: hipLaunchKernelGGL((rows_group_kernel<DS, 1, 4, 3, false, false>), dim3(grid), dim3(kBlock), lc, s, a); break;
+        case 3: hipLaunchKernelGGL((rows_group_kernel<DS, 1, 4, 3, true, false>), dim3(grid), dim3(kBlock), lc, s, a); break;
+        case 4: hipLaunchKernelGGL((rows_group_kernel<DS, 2, 4, 3, false, false>), dim3(grid), dim3(kBlock), lc, s, a); break;
+        case 5: hipLaunchKernelGGL((rows_group_kernel<DS, 2, 4, 3, true, false>), dim3(grid), dim3(kBlock), lc, s, a); break;
+        case 8: hipLaunchKernelGGL((rows_group_kernel<DS, 4, 4, 3, false, false>), dim3(grid), dim3(kBlock), lc, s, a); break;
+        case 9: hipLaunchKernelGGL((rows_group_kernel<DS, 4, 4, 3, true, false>), dim3(grid), dim3(kBlock), lc, s, a); break;
+        default: break;  // host only sets 1, 2, 4
+      }
     } else if (a.fast_mode != kFastNone && a.crc_fused) {
       lds += 12 * 256 * 4;  // slicing tables T[8][256] + zero-shift tables S[4][256]
       switch (nt) {
@@ -2541,16 +2563,16 @@ static bool launch_encode_fast_ds(const ScatterArgs& v, int grid, int deep, int 
   if (group > 0 && v.fast_mode != kFastTileTable && v.crc_fused && v.nt == 3) {
     const size_t lc = lds + 12 * 256 * 4;  // + slicing tables T[8][256], shift table S[4][256]
     switch (group) {  // host: rows sequential in the payload, whole chunks (piece_shift 0)
-      case 1: hipLaunchKernelGGL((encode_group_rows_kernel<DS, 1, 4, 3, true>), dim3(grid), dim3(kBlock), lc, s, v); return true;
-      case 2: hipLaunchKernelGGL((encode_group_rows_kernel<DS, 2, 4, 3, true>), dim3(grid), dim3(kBlock), lc, s, v); return true;
-      case 4: hipLaunchKernelGGL((encode_group_rows_kernel<DS, 4, 4, 3, true>), dim3(grid), dim3(kBlock), lc, s, v); return true;
+      case 1: hipLaunchKernelGGL((rows_group_kernel<DS, 1, 4, 3, true, true>), dim3(grid), dim3(kBlock), lc, s, v); return true;
+      case 2: hipLaunchKernelGGL((rows_group_kernel<DS, 2, 4, 3, true, true>), dim3(grid), dim3(kBlock), lc, s, v); return true;
+      case 4: hipLaunchKernelGGL((rows_group_kernel<DS, 4, 4, 3, true, true>), dim3(grid), dim3(kBlock), lc, s, v); return true;
       default: break;
     }
   }
   if (group > 0 && v.fast_mode != kFastTileTable && !v.crc_fused && v.nt == 3) {
     // host: G·vpr ≤ 64 lanes, piece_shift == 0, v.item_mul over groups; deep: U (rows per
     // lane in flight) 2 / 4 / 8 for deep = 0 / 1 / 2
-#define ZH_EG(G, U) hipLaunchKernelGGL((encode_group_rows_kernel<DS, G, U, 3>), dim3(grid), dim3(kBlock), lds, s, v); return true
+#define ZH_EG(G, U) hipLaunchKernelGGL((rows_group_kernel<DS, G, U, 3, false, true>), dim3(grid), dim3(kBlock), lds, s, v); return true
     switch (group * 10 + (deep <= 0 ? 2 : deep == 1 ? 4 : 8)) {
       case 12: ZH_EG(1, 2);
       case 14: ZH_EG(1, 4);
