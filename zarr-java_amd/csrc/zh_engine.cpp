@@ -2360,9 +2360,11 @@ static int array_write_fast(zh_ctx* ctx, const zh_array_meta* m, ScatterArgs a,
   const int grid = grid_for(ctx, group ? (items + group - 1) / group : pitems);
   // grouped kernel: rows in flight per lane (2, 4, 8; G = 8 and the CRC variants: 4)
   const int gu = group == 8 || crc_fuse ? 4 : env_int("ZH_ENC_GU", 4);
-  ZH_HIPF(launch_encode_fast(v, grid,
-                             group ? (gu <= 2 ? 0 : gu <= 4 ? 1 : 2) : env_int("ZH_ENC_DEEP", 1),
-                             group, s));
+  // tile groups: deep = 9 selects the prefetching form (ZH_ENC_TPF=1)
+  const int deep = v.fast_mode == kFastTileTable && group ? (env_int("ZH_ENC_TPF", 0) ? 9 : 1)
+                   : group ? (gu <= 2 ? 0 : gu <= 4 ? 1 : 2)
+                           : env_int("ZH_ENC_DEEP", 1);
+  ZH_HIPF(launch_encode_fast(v, grid, deep, group, s));
   ZH_HIPF(launch_encode_slow(a, grid, s));
   ZH_HIPF(launch_encode_finish(a, nz, cn, d_cnt, d_cdesc, s));
   if (!jobs.empty()) {

@@ -1565,8 +1565,8 @@ __global__ __launch_bounds__(kBlock) void tiles_group_kernel(ScatterArgs a) {
     for (uint32_t ub = 0; ub < units; ub += TG) {
       const uint32_t u = ub + ti;
       const bool live = on && u < units;
-      if (!PF) load(ub);
       if (live) {
+        if (!PF) load(ub);  // inside the live branch: 46.3 → 42.3 ms on the c4crc encode
 #pragma unroll
         for (int k = 0; k < 8; k++) {
           if (FLAGS) differs |= (x[k].x != f) | (x[k].y != f) | (x[k].z != f) | (x[k].w != f);
@@ -2598,6 +2598,23 @@ static bool launch_encode_fast_ds(const ScatterArgs& v, int grid, int deep, int 
           case 1: hipLaunchKernelGGL((tiles_group_kernel<3, 1, true, false, true>), dim3(grid), dim3(kBlock), lc, s, v); return true;
           case 2: hipLaunchKernelGGL((tiles_group_kernel<3, 2, true, false, true>), dim3(grid), dim3(kBlock), lc, s, v); return true;
           case 4: hipLaunchKernelGGL((tiles_group_kernel<3, 4, true, false, true>), dim3(grid), dim3(kBlock), lc, s, v); return true;
+          default: break;
+        }
+      }
+      if (group > 0 && !v.crc_fused && v.nt == 3 && deep == 9) {  // + prefetch (ZH_ENC_TPF=1)
+        switch (group) {
+          case 1: hipLaunchKernelGGL((tiles_group_kernel<3, 1, false, true, true>), dim3(grid), dim3(kBlock), l, s, v); return true;
+          case 2: hipLaunchKernelGGL((tiles_group_kernel<3, 2, false, true, true>), dim3(grid), dim3(kBlock), l, s, v); return true;
+          case 4: hipLaunchKernelGGL((tiles_group_kernel<3, 4, false, true, true>), dim3(grid), dim3(kBlock), l, s, v); return true;
+          default: break;
+        }
+      }
+      if (group > 0 && v.crc_fused && v.nt == 3 && deep == 9) {
+        const size_t lc = l + 16 * 256 * 4 + (size_t)v.fast_n * 4;
+        switch (group) {
+          case 1: hipLaunchKernelGGL((tiles_group_kernel<3, 1, true, true, true>), dim3(grid), dim3(kBlock), lc, s, v); return true;
+          case 2: hipLaunchKernelGGL((tiles_group_kernel<3, 2, true, true, true>), dim3(grid), dim3(kBlock), lc, s, v); return true;
+          case 4: hipLaunchKernelGGL((tiles_group_kernel<3, 4, true, true, true>), dim3(grid), dim3(kBlock), lc, s, v); return true;
           default: break;
         }
       }
