@@ -681,8 +681,9 @@ def run_strong(args, dist, A, meta, rank, ws, local):
     # the decode's write target: 1 GiB VMM chunks in coprime order, as at N=1 (DESIGN §4
     # "Placement"); RCCL only ever sees torch-allocated buffers: a send buffer on every rank
     # and the assembled region on the root, filled by a device copy before the gather
-    out_flags = int(os.environ.get("ZH_MALLOC", str(A.ZH_MALLOC_SCATTER)), 0)
+    out_flags = int(os.environ.get("ZH_MALLOC", str(A.ZH_MALLOC_SCATTER | A.ZH_MALLOC_CALIBRATE)), 0)
     out = dev.malloc(out_bytes, out_flags)
+    out_probes = dev.alloc_probes(out)
     region_t = out_t = None
     if backend == "nccl":
         if rank == 0:
@@ -725,7 +726,8 @@ def run_strong(args, dist, A, meta, rank, ws, local):
            "rank_ms_per_step": round(t_rank * 1e3 / args.steps, 3),
            "value": round(full_bytes * args.steps / t_dec / GiB, 2), "roofline": roof,
            "kernel_ms_max_over_ranks": round(kern_max, 3), "gather": gather,
-           "host_terminated": host_out, "info": info}
+           "host_terminated": host_out, "info": info,
+           "output_arena_probes": {"GBps": out_probes[0], "kept": out_probes[1]}}
     plan.close()
     dev.free(out)
     del out_t, region_t
@@ -1176,7 +1178,10 @@ def main():
                                        f"{ws} contiguous y-slabs of {res['slab_shape'][1]} rows, "
                                        f"one per GPU; value = decode-only aggregate",
                            "parallelism": f"slab-parallel x{ws}",
-                           "ranks_share_one_gpu": res["shared_gpu"]},
+                           "ranks_share_one_gpu": res["shared_gpu"],
+                           "output_allocation": "VMM 1 GiB physical chunks per rank, best of "
+                                                "the candidate arenas by a store probe (rank 0: "
+                                                f"{res['output_arena_probes']})"},
                 "roofline": res["roofline"],
                 "kernel_ms_max_over_ranks": res["kernel_ms_max_over_ranks"],
                 "gather": g, "host_terminated": res["host_terminated"],
@@ -1197,14 +1202,26 @@ def main():
         nel *= s
     out_bytes = nel * 4
 
-    # device buffers: decoded region (also the encode source) + one slab for all shards.  The
-    # region is the decode's write target: it comes from 1 GiB physical chunks mapped in a
-    # coprime order (ZH_MALLOC_SCATTER, DESIGN §4 "Placement"; ZH_MALLOC=0 for hipMalloc)
+    # device buffers: decoded region (also the encode source) + one slab for all shards.  Both
+    # come from 1 GiB physical chunks mapped in a coprime order (ZH_MALLOC_SCATTER, DESIGN §4
+    # "Placement"; ZH_MALLOC=0 for hipMalloc).  The one the timed kernel writes (the region for
+    # a read, the shard slab for --op write) is allocated first, as the best of two candidate
+    # arenas by a store probe (ZH_MALLOC_CALIBRATE), while the memory for both is free.
     t0 = time.perf_counter()
-    out_flags = int(os.environ.get("ZH_MALLOC", str(A.ZH_MALLOC_SCATTER)), 0)
-    out = dev.malloc(out_bytes, out_flags)
+    out_flags = int(os.environ.get("ZH_MALLOC", str(A.ZH_MALLOC_SCATTER | A.ZH_MALLOC_CALIBRATE)), 0)
+    in_flags = out_flags & ~A.ZH_MALLOC_CALIBRATE
     offs, tot = slab_layout(caps)
-    shard_slab = dev.malloc(tot, out_flags)  # the write path's target (--op write)
+    if args.op == "write":
+        shard_slab = dev.malloc(tot, out_flags)
+        out = dev.malloc(out_bytes, in_flags)
+        target_probes = dev.alloc_probes(shard_slab)
+    else:
+        out = dev.malloc(out_bytes, out_flags)
+        shard_slab = dev.malloc(tot, in_flags)
+        target_probes = dev.alloc_probes(out)
+    if target_probes[0]:
+        log(f"[rank {rank}] write-target arena: probes {target_probes[0]} GB/s, kept "
+            f"candidate {target_probes[1]}")
     dev.synth_fill(out, nel, 4, 0, SEED)
     dev.sync()
     t1 = time.perf_counter()
@@ -1270,7 +1287,12 @@ def main():
                    "inner_chunk_shape": [1, 32, 32, 32] if meta.chain.sharded else None,
                    "shards": st["shards"], "inner_chunks": st["items"],
                    "decoded_bytes_per_gpu": out_bytes, "parallelism": f"shard-parallel x{ws}",
-                   "output_allocation": ("VMM 1 GiB physical chunks, coprime order"
+                   "output_allocation": ("VMM 1 GiB physical chunks, coprime order" +
+                                         (", best of %d candidate arenas by a store probe "
+                                          "(GB/s %s, kept %d)" % (len(target_probes[0]),
+                                                                  target_probes[0],
+                                                                  target_probes[1])
+                                          if target_probes[0] else "")
                                          if out_flags & A.ZH_MALLOC_SCATTER else "hipMalloc")},
         "roofline": roofline,
         "cpu_baseline": cpu,

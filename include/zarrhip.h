@@ -302,7 +302,32 @@ int zh_device_malloc(zh_ctx* ctx, size_t bytes, void** out);
  * adjacent: the decode's output arena in bench.py (DESIGN.md §4 "Placement": mean +5.6 % over
  * hipMalloc on 18 buffers, 3 boxes).  Freed by zh_device_free. */
 #define ZH_MALLOC_SCATTER 0x4u
+/* With ZH_MALLOC_SCATTER: allocate up to ZH_CALIB_TRIES candidate arenas (default 2, each
+ * held while the next is allocated, so each gets other physical chunks), time a contiguous
+ * store probe over each (zh_device_write_rate pattern 0) and keep the fastest.  A large
+ * arena's write rate is set by its physical chunks (not their order or its address) and the
+ * probe predicts the decode's rate into it (DESIGN.md §4 "Placement").  Needs the memory of
+ * two arenas while it runs; a candidate that does not fit ends the search.  The buffer's
+ * contents are undefined.  zh_device_alloc_probes reports the probes. */
+#define ZH_MALLOC_CALIBRATE 0x8u
 int zh_device_malloc_ex(zh_ctx* ctx, size_t bytes, unsigned flags, void** out);
+/* Map a ZH_MALLOC_SCATTER allocation's physical chunks a second time, at a fresh virtual
+ * range, in chunk order `order` (0 = the allocation's order: slot i <- chunk (i*m) mod n;
+ * k > 0: another coprime stride and a rotation).  The view aliases the allocation's memory;
+ * free it with zh_device_free before the allocation.  ZH_EINVAL for a pointer that is not a
+ * scatter allocation.  (Re-mapping a live range in place is not offered: on ROCm 7.2 the
+ * device kept translations of the old mapping, DESIGN.md §4 "Placement".) */
+/* Probe rates (GB/s) of the candidates ZH_MALLOC_CALIBRATE tried for `ptr`, in allocation
+ * order; *chosen = the index of `ptr` among them.  Returns the number of candidates (0 for an
+ * allocation that was not calibrated), or -ZH_EINVAL. */
+int zh_device_alloc_probes(zh_ctx* ctx, void* ptr, double* gbps, int cap, int* chosen);
+int zh_device_scatter_view(zh_ctx* ctx, void* ptr, uint64_t order, void** out);
+/* Write bandwidth of [ptr, ptr+bytes): one untimed and `reps` timed launches of a store-only
+ * probe on the context stream (pattern 0: contiguous 16-B stores; 1: the decode kernels' store
+ * pattern, 128-B lines 6 KiB apart).  *gbps = bytes / median time, in 1e9 B/s.  Overwrites
+ * the buffer. */
+int zh_device_write_rate(zh_ctx* ctx, void* ptr, size_t bytes, int pattern, int reps,
+                         double* gbps);
 int zh_device_free(zh_ctx* ctx, void* ptr);
 int zh_host_malloc_pinned(zh_ctx* ctx, size_t bytes, void** out);
 int zh_host_free_pinned(zh_ctx* ctx, void* ptr);

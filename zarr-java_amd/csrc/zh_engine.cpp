@@ -11,6 +11,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cmath>
 #include <array>
 #include <cstdarg>
 #include <cstdio>
@@ -1239,8 +1240,10 @@ int zh_plan_create(zh_ctx* ctx, const zh_array_meta* m, const zh_chunk_src* chun
     if (want != 0 && !p->tile_mode && (g.fast_mode == kFastRowArith || g.fast_mode == kFastRowTable) &&
         g.piece_shift == 0 && (g.nt & 3) == 3 && items > 0) {
       int G = want > 0 ? want : (16 >> std::min(g.fast_vpr_shift, 5));
-      G = G >= 4 ? 4 : G >= 2 ? 2 : G;
-      if (G >= 1 && (G << g.fast_vpr_shift) <= 64) {
+      // 8: rows_xpose_kernel (128-B rows, no fused CRC, rows a multiple of 8)
+      const bool xpose = G == 8 && g.fast_vpr_shift == 3 && !g.crc_fused && g.fast_rows % 8 == 0;
+      G = xpose ? 8 : G >= 4 ? 4 : G >= 2 ? 2 : G;
+      if (G >= 1 && (xpose || (G << g.fast_vpr_shift) <= 64)) {
         const int64_t groups = (items + G - 1) / G;
         p->args.row_group = G;
         p->args.item_mul = env_int("ZH_ITEM_PERM", 0) ? golden_item_mul(groups) : 0;
@@ -2357,11 +2360,20 @@ static int array_write_fast(zh_ctx* ctx, const zh_array_meta* m, ScatterArgs a,
     if (group && tile_crc) v.crc_tile_step = tile_crc_step(tile_ends, (size_t)(8 / group));
   }
   if (group) v.item_mul = env_int("ZH_ITEM_PERM", 1) ? golden_item_mul((items + group - 1) / group) : 0;
-  const int grid = grid_for(ctx, group ? (items + group - 1) / group : pitems);
   // grouped kernel: rows in flight per lane (2, 4, 8; G = 8 and the CRC variants: 4)
   const int gu = group == 8 || crc_fuse ? 4 : env_int("ZH_ENC_GU", 4);
   // tile groups: deep = 9 selects the prefetching form (ZH_ENC_TPF=1)
-  const int deep = v.fast_mode == kFastTileTable && group ? (env_int("ZH_ENC_TPF", 0) ? 9 : 1)
+  // 128-B rows, no fused CRC: 8 chunks per work item through the lane exchange
+  // (rows_xpose_kernel, ZH_ENC_XPOSE; deep = 20 selects it)
+  const bool xpose = group && v.fast_mode != kFastTileTable && !crc_fuse &&
+                     v.fast_vpr_shift == 3 && v.fast_rows % 8 == 0 && env_int("ZH_ENC_XPOSE", 0);
+  if (xpose && group != 8) {
+    group = 8;
+    v.item_mul = env_int("ZH_ITEM_PERM", 1) ? golden_item_mul((items + 7) / 8) : 0;
+  }
+  const int grid = grid_for(ctx, group ? (items + group - 1) / group : pitems);
+  const int deep = xpose ? 20
+                   : v.fast_mode == kFastTileTable && group ? (env_int("ZH_ENC_TPF", 0) ? 9 : 1)
                    : group ? (gu <= 2 ? 0 : gu <= 4 ? 1 : 2)
                            : env_int("ZH_ENC_DEEP", 1);
   ZH_HIPF(launch_encode_fast(v, grid, deep, group, s));
@@ -2766,13 +2778,85 @@ int zh_array_write_host(zh_ctx* ctx, const zh_array_meta* m, const void* src_hos
 }  // extern "C"
 
 namespace {
-// ZH_MALLOC_SCATTER allocations: VA base → (size, physical chunk handles)
+// ZH_MALLOC_SCATTER allocations: VA base → (size, chunk size, physical chunk handles).  A view
+// (zh_device_scatter_view) maps another allocation's handles at a fresh VA and owns none.
 struct ScatterAlloc {
-  size_t size = 0;
+  size_t size = 0, chunk = 0;
+  int device = 0;
+  bool view = false;
   std::vector<hipMemGenericAllocationHandle_t> handles;
+  std::vector<double> probes;  // ZH_MALLOC_CALIBRATE: write probe of every candidate, GB/s
+  int chosen = -1;             // index of this allocation among them
 };
 std::mutex g_scatter_mu;
 std::map<void*, ScatterAlloc> g_scatter;
+std::vector<std::pair<void*, size_t>> g_va_retired;  // freed ranges, kept reserved
+
+uint64_t gcd_u64(uint64_t x, uint64_t y) {
+  while (y) {
+    const uint64_t r = x % y;
+    x = y;
+    y = r;
+  }
+  return x;
+}
+
+// Map A's chunks into [base, base+size): slot i <- chunk (a + i*m) mod n.  Order 0 is the
+// golden-ratio stride with a = 0; order k > 0 takes a further stride coprime with n (from a
+// second irrational fraction) and a rotation.  On failure nothing stays mapped.
+int scatter_map(void* base, const ScatterAlloc& A, uint64_t order) {
+  const size_t n = A.handles.size(), chunk = A.chunk;
+  uint64_t m = 1, a = 0;
+  if (n > 1) {
+    const double frac = order == 0 ? 0.6180339887498949
+                                   : std::fmod(0.4142135623730950 * (double)(order + 1), 1.0);
+    m = ((uint64_t)((double)n * frac)) | 1;
+    if (m >= n) m = 1;
+    while (gcd_u64(m, n) != 1) m += 2;
+    a = order == 0 ? 0 : (order * ((n + 6) / 7)) % n;
+  }
+  for (size_t i = 0; i < n; i++) {
+    const size_t src = n > 1 ? (size_t)((a + (uint64_t)i * m) % n) : 0;
+    if (hipMemMap((uint8_t*)base + i * chunk, chunk, 0, A.handles[src], 0) != hipSuccess) {
+      for (size_t k = 0; k < i; k++) (void)hipMemUnmap((uint8_t*)base + k * chunk, chunk);
+      (void)hipGetLastError();
+      return ZH_EHIP;
+    }
+  }
+  hipMemAccessDesc acc = {};
+  acc.location.type = hipMemLocationTypeDevice;
+  acc.location.id = A.device;
+  acc.flags = hipMemAccessFlagsProtReadWrite;
+  if (hipMemSetAccess(base, A.size, &acc, 1) != hipSuccess) {
+    for (size_t k = 0; k < n; k++) (void)hipMemUnmap((uint8_t*)base + k * chunk, chunk);
+    (void)hipGetLastError();
+    return ZH_EHIP;
+  }
+  return ZH_OK;
+}
+
+void scatter_unmap(void* base, const ScatterAlloc& A) {
+  for (size_t k = 0; k < A.handles.size(); k++)
+    (void)hipMemUnmap((uint8_t*)base + k * A.chunk, A.chunk);
+  (void)hipGetLastError();
+}
+
+// reserve a fresh VA range for A and map its chunks there
+int scatter_place(ScatterAlloc& A, uint64_t order, void** out) {
+  void* base = nullptr;
+  if (hipMemAddressReserve(&base, A.size, A.chunk, nullptr, 0) != hipSuccess) {
+    (void)hipGetLastError();
+    return ZH_ENOMEM;
+  }
+  const int st = scatter_map(base, A, order);
+  if (st != ZH_OK) {
+    (void)hipMemAddressFree(base, A.size);
+    (void)hipGetLastError();
+    return st;
+  }
+  *out = base;
+  return ZH_OK;
+}
 
 int scatter_malloc(int device, size_t bytes, void** out) {
   hipMemAllocationProp prop = {};
@@ -2789,54 +2873,43 @@ int scatter_malloc(int device, size_t bytes, void** out) {
   const size_t n = std::max<size_t>(1, (bytes + chunk - 1) / chunk);
   ScatterAlloc A;
   A.size = n * chunk;
-  void* base = nullptr;
-  auto undo = [&]() {
-    for (auto h : A.handles) (void)hipMemRelease(h);
-    if (base) (void)hipMemAddressFree(base, A.size);
-    (void)hipGetLastError();
-  };
+  A.chunk = chunk;
+  A.device = device;
   for (size_t i = 0; i < n; i++) {
     hipMemGenericAllocationHandle_t h;
     if (hipMemCreate(&h, chunk, &prop, 0) != hipSuccess) {
-      undo();
+      for (auto hh : A.handles) (void)hipMemRelease(hh);
+      (void)hipGetLastError();
       return ZH_ENOMEM;
     }
     A.handles.push_back(h);
   }
-  if (hipMemAddressReserve(&base, A.size, chunk, nullptr, 0) != hipSuccess) {
-    base = nullptr;
-    undo();
-    return ZH_ENOMEM;
-  }
-  // virtual slot i ← physical chunk (i * m) mod n, m coprime with n (golden-ratio stride)
-  uint64_t m = ((uint64_t)((double)n * 0.6180339887498949)) | 1;
-  auto gcd = [](uint64_t x, uint64_t y) {
-    while (y) {
-      const uint64_t r = x % y;
-      x = y;
-      y = r;
-    }
-    return x;
-  };
-  while (n > 1 && gcd(m, n) != 1) m += 2;
-  for (size_t i = 0; i < n; i++) {
-    const size_t src = n > 1 ? (size_t)(((uint64_t)i * m) % n) : 0;
-    if (hipMemMap((uint8_t*)base + i * chunk, chunk, 0, A.handles[src], 0) != hipSuccess) {
-      for (size_t k = 0; k < i; k++) (void)hipMemUnmap((uint8_t*)base + k * chunk, chunk);
-      undo();
-      return ZH_EHIP;
-    }
-  }
-  hipMemAccessDesc acc = {};
-  acc.location = prop.location;
-  acc.flags = hipMemAccessFlagsProtReadWrite;
-  if (hipMemSetAccess(base, A.size, &acc, 1) != hipSuccess) {
-    (void)hipMemUnmap(base, A.size);
-    undo();
-    return ZH_EHIP;
+  void* base = nullptr;
+  const int st = scatter_place(A, 0, &base);
+  if (st != ZH_OK) {
+    for (auto h : A.handles) (void)hipMemRelease(h);
+    return st;
   }
   std::lock_guard<std::mutex> lk(g_scatter_mu);
   g_scatter[base] = std::move(A);
+  *out = base;
+  return ZH_OK;
+}
+
+int scatter_view(void* ptr, uint64_t order, void** out) {
+  ScatterAlloc V;
+  {
+    std::lock_guard<std::mutex> lk(g_scatter_mu);
+    auto it = g_scatter.find(ptr);
+    if (it == g_scatter.end() || it->second.view) return ZH_EINVAL;
+    V = it->second;
+  }
+  V.view = true;
+  void* base = nullptr;
+  const int st = scatter_place(V, order, &base);
+  if (st != ZH_OK) return st;
+  std::lock_guard<std::mutex> lk(g_scatter_mu);
+  g_scatter[base] = std::move(V);
   *out = base;
   return ZH_OK;
 }
@@ -2851,10 +2924,82 @@ bool scatter_free(void* ptr) {
     g_scatter.erase(it);
   }
   (void)hipDeviceSynchronize();
-  (void)hipMemUnmap(ptr, A.size);
-  for (auto h : A.handles) (void)hipMemRelease(h);
+  scatter_unmap(ptr, A);
+  if (!A.view)
+    for (auto h : A.handles) (void)hipMemRelease(h);
+  if (env_int("ZH_SCATTER_RETIRE", 0)) {  // lab switch: keep the range reserved
+    std::lock_guard<std::mutex> lk(g_scatter_mu);
+    g_va_retired.emplace_back(ptr, A.size);
+    return true;
+  }
   (void)hipMemAddressFree(ptr, A.size);
+  (void)hipGetLastError();
   return true;
+}
+
+int write_rate(hipStream_t s, void* ptr, size_t bytes, int pattern, int reps, double* gbps) {
+  hipEvent_t e0, e1;
+  if (hipEventCreate(&e0) != hipSuccess) return ZH_EHIP;
+  if (hipEventCreate(&e1) != hipSuccess) {
+    (void)hipEventDestroy(e0);
+    return ZH_EHIP;
+  }
+  int rc = ZH_OK;
+  std::vector<float> ms;
+  if (launch_write_probe(ptr, (int64_t)bytes, pattern, s) != hipSuccess) rc = ZH_EHIP;
+  for (int r = 0; rc == ZH_OK && r < reps; r++) {
+    float t = 0;
+    if (hipEventRecord(e0, s) != hipSuccess ||
+        launch_write_probe(ptr, (int64_t)bytes, pattern, s) != hipSuccess ||
+        hipEventRecord(e1, s) != hipSuccess || hipEventSynchronize(e1) != hipSuccess ||
+        hipEventElapsedTime(&t, e0, e1) != hipSuccess)
+      rc = ZH_EHIP;
+    else
+      ms.push_back(t);
+  }
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
+  if (rc != ZH_OK) {
+    (void)hipGetLastError();
+    return rc;
+  }
+  std::sort(ms.begin(), ms.end());
+  const double med = ms[ms.size() / 2];
+  *gbps = med > 0 ? (double)bytes / (med * 1e-3) / 1e9 : 0.0;
+  return ZH_OK;
+}
+
+// ZH_MALLOC_CALIBRATE: the write rate of a large scatter arena is set by which physical chunks
+// it got (not their order, not its virtual address), and a contiguous store probe predicts
+// the decode's rate into it (profiles/r02/placement/calib*.jsonl).  Allocate up to
+// ZH_CALIB_TRIES candidates (default 2) while holding the earlier ones, so the driver hands out
+// different chunks, probe each, keep the fastest.  A candidate that does not fit ends the
+// search.  On return *out is the kept allocation, with every probe recorded on it.
+void scatter_calibrate(zh_ctx* ctx, size_t bytes, void** out) {
+  const int tries = std::max(1, env_int("ZH_CALIB_TRIES", 2));
+  std::vector<void*> cand{*out};
+  std::vector<double> rate;
+  for (int k = 0;; k++) {
+    double g = 0;
+    if (write_rate(ctx->stream, cand[(size_t)k], bytes, 0, 2, &g) != ZH_OK) g = 0;
+    rate.push_back(g);
+    if (k + 1 >= tries) break;
+    void* next = nullptr;
+    if (scatter_malloc(ctx->device, bytes, &next) != ZH_OK) break;
+    cand.push_back(next);
+  }
+  size_t best = 0;
+  for (size_t i = 1; i < rate.size(); i++)
+    if (rate[i] > rate[best]) best = i;
+  for (size_t i = 0; i < cand.size(); i++)
+    if (i != best) scatter_free(cand[i]);
+  std::lock_guard<std::mutex> lk(g_scatter_mu);
+  auto it = g_scatter.find(cand[best]);
+  if (it != g_scatter.end()) {
+    it->second.probes = rate;
+    it->second.chosen = (int)best;
+  }
+  *out = cand[best];
 }
 }  // namespace
 
@@ -2878,6 +3023,7 @@ int zh_device_malloc_ex(zh_ctx* ctx, size_t bytes, unsigned flags, void** out) {
   hipError_t e = hipErrorOutOfMemory;
   if (flags & ZH_MALLOC_SCATTER) {
     const int st = scatter_malloc(ctx->device, bytes, out);
+    if (st == ZH_OK && (flags & ZH_MALLOC_CALIBRATE)) scatter_calibrate(ctx, bytes, out);
     if (st == ZH_OK || (flags & ZH_MALLOC_REQUIRE)) return st;
   }
   if (flags & ZH_MALLOC_CONTIGUOUS) {
@@ -2886,6 +3032,28 @@ int zh_device_malloc_ex(zh_ctx* ctx, size_t bytes, unsigned flags, void** out) {
   }
   if (e != hipSuccess && !(flags & ZH_MALLOC_REQUIRE)) e = hipMalloc(out, bytes);
   return e == hipSuccess ? ZH_OK : (e == hipErrorOutOfMemory ? ZH_ENOMEM : ZH_EHIP);
+}
+int zh_device_scatter_view(zh_ctx* ctx, void* ptr, uint64_t order, void** out) {
+  if (!ctx || !ptr || !out) return ZH_EINVAL;
+  (void)hipSetDevice(ctx->device);
+  return scatter_view(ptr, order, out);
+}
+int zh_device_alloc_probes(zh_ctx* ctx, void* ptr, double* gbps, int cap, int* chosen) {
+  if (!ctx || !ptr) return -ZH_EINVAL;
+  std::lock_guard<std::mutex> lk(g_scatter_mu);
+  auto it = g_scatter.find(ptr);
+  if (it == g_scatter.end()) return 0;
+  const auto& P = it->second.probes;
+  for (int i = 0; i < cap && i < (int)P.size(); i++) gbps[i] = P[(size_t)i];
+  if (chosen) *chosen = it->second.chosen;
+  return (int)P.size();
+}
+int zh_device_write_rate(zh_ctx* ctx, void* ptr, size_t bytes, int pattern, int reps,
+                         double* gbps) {
+  if (!ctx || !ptr || !gbps || bytes == 0 || reps <= 0 || pattern < 0 || pattern > 1)
+    return ZH_EINVAL;
+  (void)hipSetDevice(ctx->device);
+  return write_rate(ctx->stream, ptr, bytes, pattern, reps, gbps);
 }
 int zh_device_free(zh_ctx* ctx, void* ptr) {
   if (!ctx) return ZH_EINVAL;

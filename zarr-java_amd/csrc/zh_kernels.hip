@@ -1278,6 +1278,122 @@ __global__ __launch_bounds__(kBlock) void rows_group_kernel(ScatterArgs a) {
   }
 }
 
+// Grouped row kernel with a lane exchange (128-B rows, 8 chunks per work item, no CRC).
+// rows_group_kernel at G = 8 moves 1 KiB of contiguous region per wave instruction but stores
+// each chunk's rows from 8 lanes, 128 B to each of 8 payloads.  Here every wave instruction is
+// 1 KiB contiguous on both sides: a wave takes 8 rows of the 8 chunks, the region side in
+// layout A (lane = (chunk q, 16-B column), register = row) and the payload side in layout B
+// (lane = (row, column), register = chunk), and swaps layouts through LDS (8 KiB per wave;
+// rows 72 vectors apart, so the 16-lane groups of ds_read_b128 and the 8-lane groups of
+// ds_write_b128 hit distinct banks).  ENC: region rows (src, so) → payload (dst, dof), the
+// fill test on the loaded vectors; decode: payload (src, so) → region (dst, dof), full-fill
+// chunks store their fill value.  Each lane group reads its own chunk's descriptor; the
+// others come through readlane, so any chunk mix is correct (non-fast chunks stay on the slow
+// list).  Host: fast_vpr_shift == 3, piece_shift == 0, item_mul over groups of 8.
+constexpr int kXRow = 72;  // 16-B vectors per exchange row (64 + 8)
+
+template <int DS, bool ENC>
+__global__ __launch_bounds__(kBlock) void rows_xpose_kernel(ScatterArgs a) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  uint2* tab = reinterpret_cast<uint2*>(smem);
+  for (int i = threadIdx.x; i < a.fast_n; i += kBlock)
+    tab[i] = reinterpret_cast<const uint2*>(a.fast_tab)[i];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int hi = lane >> 3, col = lane & 7;  // layout A: hi = chunk; layout B: hi = row
+  uint4* xw = reinterpret_cast<uint4*>(smem + (((size_t)a.fast_n * 8 + 15) & ~(size_t)15)) +
+              wave * 8 * kXRow;
+  __syncthreads();
+  const uint32_t nrows = (uint32_t)a.fast_rows;
+  const int64_t ngroups = (a.n_citems + 7) / 8;
+  const uint4 ffill = fill16<DS>(a.fill);
+  for (int64_t g = blockIdx.x; g < ngroups; g += gridDim.x) {
+    const int64_t pg = a.item_mul ? (int64_t)(((uint64_t)g * a.item_mul) % (uint64_t)ngroups) : g;
+    const int64_t c = pg * 8 + hi;
+    bool on = false, fill = false;
+    uint4 fv = ffill;
+    uint64_t sb = 0, db = 0;  // this lane's chunk: source and destination bases
+    if (c < a.n_citems) {
+      const uint4* dp = reinterpret_cast<const uint4*>(a.desc + c);
+      const uint4 x = dp[0], y = dp[1];
+      on = (y.z & kDescFast) != 0;
+      sb = ((uint64_t)x.y << 32) | x.x;
+      db = (uint64_t)(uintptr_t)(a.region + (int64_t)(((uint64_t)x.w << 32) | x.z) * DS);
+      if (!ENC) {
+        fill = (y.z & kDescModeMask) == kDescFullFill;
+        fv = fill16<DS>(((uint64_t)y.y << 32) | y.x);
+      }
+    }
+    if (__syncthreads_or(on) == 0) continue;  // block-uniform: no fast chunk in the group
+    const uint64_t onm = __ballot(on), fillm = __ballot(on && fill);
+    bool differs = false;
+#pragma unroll 1
+    for (uint32_t rb = wave * 8; rb < nrows; rb += 32) {
+      uint4 v[8];
+      if constexpr (ENC) {  // layout A loads: row rb + r of chunk hi
+#pragma unroll
+        for (int r = 0; r < 8; r++) {
+          uint64_t so, dof;
+          row_offsets(a, tab, rb + r, so, dof);
+          v[r] = ffill;
+          if (on && rb + r < nrows) v[r] = ld16s<true>((const uint8_t*)sb + so * DS + col * 16);
+          differs |= (v[r].x != ffill.x) | (v[r].y != ffill.y) | (v[r].z != ffill.z) |
+                     (v[r].w != ffill.w);
+        }
+#pragma unroll
+        for (int r = 0; r < 8; r++) xw[r * kXRow + hi * 8 + col] = v[r];
+      } else {  // layout B loads: row rb + hi of chunk k
+        uint64_t so, dof;
+        row_offsets(a, tab, rb + hi, so, dof);
+#pragma unroll
+        for (int k = 0; k < 8; k++) {
+          const uint64_t s = ((uint64_t)__builtin_amdgcn_readlane((int)(sb >> 32), k * 8) << 32) |
+                             (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)sb, k * 8);
+          v[k] = make_uint4(0, 0, 0, 0);
+          if (((onm & ~fillm) >> (k * 8)) & 1 && rb + hi < nrows)
+            v[k] = ld16s<true>((const uint8_t*)s + so * DS + col * 16);
+        }
+#pragma unroll
+        for (int k = 0; k < 8; k++) xw[hi * kXRow + k * 8 + col] = v[k];
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      uint4 y[8];
+      if constexpr (ENC) {  // layout B: chunk k, row rb + hi
+#pragma unroll
+        for (int k = 0; k < 8; k++) y[k] = xw[hi * kXRow + k * 8 + col];
+      } else {  // layout A: chunk hi, row rb + r
+#pragma unroll
+        for (int r = 0; r < 8; r++) y[r] = xw[r * kXRow + hi * 8 + col];
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      if constexpr (ENC) {  // layout B stores into chunk k's payload
+        uint64_t so, dof;
+        row_offsets(a, tab, rb + hi, so, dof);
+#pragma unroll
+        for (int k = 0; k < 8; k++) {
+          const uint64_t d = ((uint64_t)__builtin_amdgcn_readlane((int)(db >> 32), k * 8) << 32) |
+                             (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)db, k * 8);
+          if ((onm >> (k * 8)) & 1 && rb + hi < nrows)
+            st16s<true>((uint8_t*)d + dof * DS + col * 16, xform16<DS>(y[k], a.swap, a.is_bool));
+        }
+      } else {  // layout A stores into chunk hi's region rows
+#pragma unroll
+        for (int r = 0; r < 8; r++) {
+          uint64_t so, dof;
+          row_offsets(a, tab, rb + r, so, dof);
+          if (on && rb + r < nrows)
+            st16s<true>((uint8_t*)db + dof * DS + col * 16,
+                        fill ? fv : xform16<DS>(y[r], a.swap, a.is_bool));
+        }
+      }
+    }
+    if (ENC && (__ballot(differs) & (0xFFull << (hi * 8))) != 0 && col == 0 && on) a.flags[c] = 1;
+  }
+}
+
 // Row-interleaved tile path (see kTG above).  With CRC (inner crc32c fused): lane (w, t, g)
 // holds the payload vectors at bytes P_k = 4·tab[u].x + 4·(8w + k)·s_fd + 16g, k = 0..7,
 // a constant gap G = 4·s_fd − 16 apart, so its raw register over [v0, G zeros, v1, …, v7]
@@ -2489,6 +2605,9 @@ static void launch_scatter_ds(const ScatterArgs& a, int tile, int enc, int grid,
           else hipLaunchKernelGGL((decode_tiles_kernel<0, 0>), dim3(grid), dim3(kBlock), lds, s, a);
         }
       }
+    } else if (a.fast_mode != kFastNone && a.row_group == 8) {  // host: 128-B rows, no CRC
+      hipLaunchKernelGGL((rows_xpose_kernel<DS, false>), dim3(grid), dim3(kBlock),
+                         lds + 4 * 8 * kXRow * 16, s, a);
     } else if (a.fast_mode != kFastNone && a.row_group > 0) {  // host: nt 3, piece_shift 0
       const size_t lc = lds + (a.crc_fused ? 12 * 256 * 4 : 0);
       switch (a.row_group * 2 + (a.crc_fused ? 1 : 0)) {
@@ -2568,6 +2687,12 @@ static bool launch_encode_fast_ds(const ScatterArgs& v, int grid, int deep, int 
       case 4: hipLaunchKernelGGL((rows_group_kernel<DS, 4, 4, 3, true, true>), dim3(grid), dim3(kBlock), lc, s, v); return true;
       default: break;
     }
+  }
+  if (group == 8 && deep == 20 && v.fast_mode != kFastTileTable && !v.crc_fused) {
+    // host: 128-B rows (fast_vpr_shift 3), rows per chunk a multiple of 8
+    hipLaunchKernelGGL((rows_xpose_kernel<DS, true>), dim3(grid), dim3(kBlock),
+                       lds + 4 * 8 * kXRow * 16, s, v);
+    return true;
   }
   if (group > 0 && v.fast_mode != kFastTileTable && !v.crc_fused && v.nt == 3) {
     // host: G·vpr ≤ 64 lanes, piece_shift == 0, v.item_mul over groups; deep: U (rows per
@@ -2760,6 +2885,43 @@ hipError_t launch_gather_blocks(void* dst, const void* src, const int64_t* d_idx
   const int grid = (int)std::min<int64_t>(n, 65536);
   hipLaunchKernelGGL(gather_blocks_kernel, dim3(grid), dim3(kBlock), 0, stream, (uint8_t*)dst,
                      (const uint8_t*)src, d_idx, n, bb);
+  return hipGetLastError();
+}
+
+// Write-bandwidth probe of a large output buffer (allocation calibration, DESIGN §4
+// "Placement"): non-temporal 16-B stores, no loads.
+//   pattern 0: contiguous, 4 KiB per workgroup step
+//   pattern 1: the decode kernels' store pattern: a work item is 1024 lines of 128 B, 6 KiB
+//              apart (one 32x32x32 uint32 chunk of a region with 1536-element rows); a wave
+//              stores 8 lines per instruction
+__global__ __launch_bounds__(kBlock) void write_probe_kernel(uint8_t* __restrict__ dst,
+                                                              int64_t bytes, int pattern) {
+  const uint4 v = make_uint4(0x5A5A5A5Au, 0xA5A5A5A5u, 0x0F0F0F0Fu, 0xF0F0F0F0u);
+  if (pattern == 0) {
+    const int64_t nv = bytes >> 4;
+    for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < nv;
+         i += (int64_t)gridDim.x * kBlock)
+      st16s<true>(dst + (i << 4), v);
+    return;
+  }
+  constexpr int64_t kLine = 128, kPitch = 6144, kLines = 1024;
+  constexpr int64_t kGroup = kPitch * kLines;           // 48 items share 6 MiB
+  const int64_t items = bytes / kGroup * (kPitch / kLine);
+  const int t = threadIdx.x, c = t & 7, r0 = t >> 3;    // 16-B column, line within step
+  for (int64_t it = blockIdx.x; it < items; it += gridDim.x) {
+    uint8_t* base = dst + (it / (kPitch / kLine)) * kGroup + (it % (kPitch / kLine)) * kLine;
+    for (int64_t l = r0; l < kLines; l += kBlock / 8) st16s<true>(base + l * kPitch + c * 16, v);
+  }
+}
+
+hipError_t launch_write_probe(void* dst, int64_t bytes, int pattern, hipStream_t stream) {
+  if (bytes <= 0) return hipSuccess;
+  int dev = 0, cus = 256;
+  (void)hipGetDevice(&dev);
+  (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  const int grid = cus * 32;
+  hipLaunchKernelGGL(write_probe_kernel, dim3(grid), dim3(kBlock), 0, stream, (uint8_t*)dst,
+                     bytes, pattern);
   return hipGetLastError();
 }
 

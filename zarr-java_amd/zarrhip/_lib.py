@@ -71,6 +71,10 @@ _SIGS = {
     "zh_device_malloc": (C.c_int, [P, SZ, C.POINTER(P)]),
     "zh_device_malloc_ex": (C.c_int, [P, SZ, C.c_uint, C.POINTER(P)]),
     "zh_device_free": (C.c_int, [P, P]),
+    "zh_device_scatter_view": (C.c_int, [P, P, U64, C.POINTER(P)]),
+    "zh_device_alloc_probes": (C.c_int, [P, P, C.POINTER(C.c_double), C.c_int,
+                                         C.POINTER(C.c_int)]),
+    "zh_device_write_rate": (C.c_int, [P, P, SZ, C.c_int, C.c_int, C.POINTER(C.c_double)]),
     "zh_host_malloc_pinned": (C.c_int, [P, SZ, C.POINTER(P)]),
     "zh_host_free_pinned": (C.c_int, [P, P]),
     "zh_host_register": (C.c_int, [P, P, SZ]),
@@ -177,6 +181,30 @@ class DeviceContext:
     def free(self, ptr):
         if ptr:
             self.L.zh_device_free(self.h, P(ptr))
+
+    def scatter_view(self, ptr, order=0):
+        """Map a ZH_MALLOC_SCATTER allocation's chunks again at a fresh virtual range, in
+        chunk order `order`; free the view (self.free) before the allocation."""
+        p = P()
+        check(self.L.zh_device_scatter_view(self.h, P(ptr), int(order), C.byref(p)))
+        return p.value
+
+    def alloc_probes(self, ptr):
+        """ZH_MALLOC_CALIBRATE record of `ptr`: (probe GB/s of every candidate, chosen index),
+        ([], -1) for an allocation that was not calibrated."""
+        buf = (C.c_double * 16)()
+        ch = C.c_int(-1)
+        k = self.L.zh_device_alloc_probes(self.h, P(ptr), buf, 16, C.byref(ch))
+        if k < 0:
+            check(-k)
+        return [round(buf[i], 1) for i in range(min(k, 16))], ch.value
+
+    def write_rate(self, ptr, nbytes, pattern=1, reps=3):
+        """Write bandwidth of a device range by a store-only probe, GB/s (overwrites it)."""
+        g = C.c_double()
+        check(self.L.zh_device_write_rate(self.h, P(ptr), int(nbytes), int(pattern), int(reps),
+                                          C.byref(g)))
+        return g.value
 
     def malloc_pinned(self, nbytes):
         p = P()
