@@ -220,6 +220,12 @@ def kernel_name(meta):
     if meta.chain.has_transpose:
         return "decode_tiles_kernel" if os.environ.get("ZH_DEC_TGROUP") == "0" else \
             "tiles_group_kernel"
+    # row chains with 128-B rows and no chunk CRC: the lane-exchange kernel (ZH_DEC_RGROUP=8)
+    c = meta.chain
+    rg = os.environ.get("ZH_DEC_RGROUP")
+    if c.sharded and not c.inner_crc32c and rg in (None, "8") and \
+            c.inner_chunk_shape[meta.ndim - 1] * meta.dtype_size == 128:
+        return "rows_xpose_kernel"
     return "decode_rows_kernel<4,4>"
 
 
@@ -623,6 +629,30 @@ def visible_devices():
     return torch.cuda.device_count()
 
 
+def arena_pair(dev, A, nbytes):
+    """Two device arenas of `nbytes` (ZH_MALLOC, default ZH_MALLOC_SCATTER: 1 GiB physical
+    chunks in a coprime order).  A large arena's write rate is set by which physical chunks it
+    got, and a contiguous store probe predicts the decode's rate into it; reads are not
+    affected (DESIGN §4 "Placement").  So the faster of the two by the probe takes the timed
+    kernel's writes and the other holds what it reads: no arena is freed and reallocated.
+    Returns (fast, slow, record); slow is None when the second does not fit (ZH_CALIB=0: no
+    probe, first = fast)."""
+    flags = int(os.environ.get("ZH_MALLOC", str(A.ZH_MALLOC_SCATTER)), 0)
+    a = dev.malloc(nbytes, flags)
+    try:
+        b = dev.malloc(nbytes, flags)
+    except Exception:
+        b = None
+    kind = "VMM 1 GiB physical chunks, coprime order" if flags & A.ZH_MALLOC_SCATTER else \
+        "hipMalloc"
+    if b is None or os.environ.get("ZH_CALIB", "1") == "0":
+        return a, b, {"kind": kind, "arenas": 1 if b is None else 2, "probe_GBps": None}
+    ra, rb = dev.write_rate(a, nbytes, 0, 2), dev.write_rate(b, nbytes, 0, 2)
+    fast, slow = (a, b) if ra >= rb else (b, a)
+    return fast, slow, {"kind": kind, "arenas": 2, "probe_GBps": [round(ra, 1), round(rb, 1)],
+                        "write_target": "first" if ra >= rb else "second"}
+
+
 def run_strong(args, dist, A, meta, rank, ws, local):
     """Strong scaling: ONE full array split into per-rank y-slabs (512 rows at
     N=8, aligned to inner chunks); each rank holds only the shards its slab touches (encoded
@@ -660,12 +690,14 @@ def run_strong(args, dist, A, meta, rank, ws, local):
         nel_cover *= e
     first = lo[1] * shape[2] * shape[3] if n == 4 else 0
     t0 = time.perf_counter()
-    src = dev.malloc(nel_cover * 4)
-    dev.synth_fill(src, nel_cover, 4, first, SEED)
     offs, tot = slab_layout(caps)
-    slab_buf = dev.malloc(tot)
+    # two arenas: the faster by a store probe is the synthesis source and then the decode's
+    # output, the other holds the shards (arena_pair)
+    fast, slow, arena = arena_pair(dev, A, max(nel_cover * 4, tot))
+    src = fast
+    dev.synth_fill(src, nel_cover, 4, first, SEED)
+    slab_buf = slow if slow is not None else dev.malloc(tot)
     sizes = dev.array_write(meta, src, lo, ext, [(slab_buf + o, c) for o, c in zip(offs, caps)])
-    dev.free(src)
     log(f"[rank {rank}/{ws}] device {device} of {ndev} ({info['arch']}): slab y "
         f"[{so[1]}, {so[1] + ss[1]}), {len(cover)} shards encoded in "
         f"{time.perf_counter() - t0:.2f}s")
@@ -681,9 +713,7 @@ def run_strong(args, dist, A, meta, rank, ws, local):
     # the decode's write target: 1 GiB VMM chunks in coprime order, as at N=1 (DESIGN §4
     # "Placement"); RCCL only ever sees torch-allocated buffers: a send buffer on every rank
     # and the assembled region on the root, filled by a device copy before the gather
-    out_flags = int(os.environ.get("ZH_MALLOC", str(A.ZH_MALLOC_SCATTER | A.ZH_MALLOC_CALIBRATE)), 0)
-    out = dev.malloc(out_bytes, out_flags)
-    out_probes = dev.alloc_probes(out)
+    out = fast
     region_t = out_t = None
     if backend == "nccl":
         if rank == 0:
@@ -727,7 +757,7 @@ def run_strong(args, dist, A, meta, rank, ws, local):
            "value": round(full_bytes * args.steps / t_dec / GiB, 2), "roofline": roof,
            "kernel_ms_max_over_ranks": round(kern_max, 3), "gather": gather,
            "host_terminated": host_out, "info": info,
-           "output_arena_probes": {"GBps": out_probes[0], "kept": out_probes[1]}}
+           "arenas": arena}
     plan.close()
     dev.free(out)
     del out_t, region_t
@@ -1179,9 +1209,9 @@ def main():
                                        f"one per GPU; value = decode-only aggregate",
                            "parallelism": f"slab-parallel x{ws}",
                            "ranks_share_one_gpu": res["shared_gpu"],
-                           "output_allocation": "VMM 1 GiB physical chunks per rank, best of "
-                                                "the candidate arenas by a store probe (rank 0: "
-                                                f"{res['output_arena_probes']})"},
+                           "output_allocation": "per rank: the faster of two arenas by a "
+                                                "store probe (rank 0: "
+                                                f"{res['arenas']})"},
                 "roofline": res["roofline"],
                 "kernel_ms_max_over_ranks": res["kernel_ms_max_over_ranks"],
                 "gather": g, "host_terminated": res["host_terminated"],
@@ -1208,20 +1238,15 @@ def main():
     # a read, the shard slab for --op write) is allocated first, as the best of two candidate
     # arenas by a store probe (ZH_MALLOC_CALIBRATE), while the memory for both is free.
     t0 = time.perf_counter()
-    out_flags = int(os.environ.get("ZH_MALLOC", str(A.ZH_MALLOC_SCATTER | A.ZH_MALLOC_CALIBRATE)), 0)
-    in_flags = out_flags & ~A.ZH_MALLOC_CALIBRATE
     offs, tot = slab_layout(caps)
-    if args.op == "write":
-        shard_slab = dev.malloc(tot, out_flags)
-        out = dev.malloc(out_bytes, in_flags)
-        target_probes = dev.alloc_probes(shard_slab)
+    fast, slow, arena = arena_pair(dev, A, max(out_bytes, tot))
+    if slow is None:
+        slow = dev.malloc(max(out_bytes, tot))
+    if args.op == "write":   # the shard slab takes the timed writes
+        shard_slab, out = fast, slow
     else:
-        out = dev.malloc(out_bytes, out_flags)
-        shard_slab = dev.malloc(tot, in_flags)
-        target_probes = dev.alloc_probes(out)
-    if target_probes[0]:
-        log(f"[rank {rank}] write-target arena: probes {target_probes[0]} GB/s, kept "
-            f"candidate {target_probes[1]}")
+        out, shard_slab = fast, slow
+    log(f"[rank {rank}] arenas: {json.dumps(arena)}")
     dev.synth_fill(out, nel, 4, 0, SEED)
     dev.sync()
     t1 = time.perf_counter()
@@ -1287,13 +1312,9 @@ def main():
                    "inner_chunk_shape": [1, 32, 32, 32] if meta.chain.sharded else None,
                    "shards": st["shards"], "inner_chunks": st["items"],
                    "decoded_bytes_per_gpu": out_bytes, "parallelism": f"shard-parallel x{ws}",
-                   "output_allocation": ("VMM 1 GiB physical chunks, coprime order" +
-                                         (", best of %d candidate arenas by a store probe "
-                                          "(GB/s %s, kept %d)" % (len(target_probes[0]),
-                                                                  target_probes[0],
-                                                                  target_probes[1])
-                                          if target_probes[0] else "")
-                                         if out_flags & A.ZH_MALLOC_SCATTER else "hipMalloc")},
+                   "output_allocation": f"{arena['kind']}; the faster of {arena['arenas']} "
+                                        f"arenas by a store probe takes the decode's writes "
+                                        f"(GB/s {arena['probe_GBps']})"},
         "roofline": roofline,
         "cpu_baseline": cpu,
     }

@@ -493,6 +493,61 @@ def test_grouped_row_decode(dev, monkeypatch, crc, dsize, group):
         assert str(ed.value) == str(eo.value)
 
 
+@pytest.mark.parametrize("inner_rows", [(4, 8), (2, 4), (8, 16), (3, 5)])
+@pytest.mark.parametrize("dsize", [1, 2, 4, 8])
+@pytest.mark.parametrize("crc", [False, True])
+def test_device_encode_lane_exchange(dev, monkeypatch, dsize, inner_rows, crc):
+    """rows_xpose_kernel on the encode view (ZH_ENC_XPOSE=1: 128-B rows, 8 chunks per work
+    item, region rows and payload rows exchanged through LDS): groups straddling shard rows and
+    the item list's end, all-fill chunks beside data chunks (per-chunk flags), clipped boundary
+    chunks on the slow list, 8 rows per chunk (one wave step), and chains it must leave to the
+    grouped kernel (15 rows per chunk; the fused chunk CRC)."""
+    monkeypatch.setenv("ZH_ENC_XPOSE", "1")
+    L = 128 // dsize
+    a, b = inner_rows
+    shape = [a * 3 + 1, b * 3, L * 9 + L // 2]
+    meta = A.make_meta(shape, [a * 2, b * 2, L * 5], dsize, endian=A.ZH_ENDIAN_BIG,
+                       sharded=True, inner_chunk_shape=[a, b, L],
+                       fill=(5).to_bytes(dsize, "little"), inner_crc32c=crc)
+    arr = rand_array(shape, dsize, seed=81 + dsize + a)
+    arr[arr == 5] = 6
+    arr[0:a, 0:b, L:2 * L] = 5                    # all-fill chunk next to data
+    arr[a:2 * a, b:2 * b, 0:3 * L] = 5            # a run of three
+    arr[a:2 * a, 0:b, 2 * L + 1] = 9
+    want = encode_oracle(meta, arr)
+    got = device_write(dev, meta, arr)
+    assert [len(g) if g else 0 for g in got] == [len(w) if w else 0 for w in want]
+    assert got == want
+
+
+@pytest.mark.parametrize("inner_rows", [(4, 8), (2, 4), (3, 5)])
+@pytest.mark.parametrize("dsize", [1, 4, 8])
+@pytest.mark.parametrize("crc", [False, True])
+def test_lane_exchange_row_decode(dev, monkeypatch, dsize, inner_rows, crc):
+    """rows_xpose_kernel in the decode direction (ZH_DEC_RGROUP=8): copies beside Q1 zero-fill
+    items and a missing shard's fill inside one group of 8 chunks, row-clipped boundary chunks
+    on the generic kernel, partial regions; the fused-CRC and 15-row chains fall back."""
+    monkeypatch.setenv("ZH_DEC_RGROUP", "8")
+    L = 128 // dsize
+    a, b = inner_rows
+    shape = [a * 3 + 1, b * 3, L * 9 + L // 2]
+    meta = A.make_meta(shape, [a * 2, b * 2, L * 5], dsize, endian=A.ZH_ENDIAN_BIG,
+                       sharded=True, inner_chunk_shape=[a, b, L],
+                       fill=(5).to_bytes(dsize, "little"), inner_crc32c=crc)
+    arr = rand_array(shape, dsize, seed=91 + dsize + a)
+    arr[arr == 5] = 6
+    arr[0:a, 0:b, L:2 * L] = 5                    # elided → Q1 zeros on read
+    shards = encode_oracle(meta, arr)
+    pos = {c: i for i, c in enumerate(chunk_coords(meta, [0, 0, 0], shape))}
+    shards[pos[(1, 0, 1)]] = None                 # missing shard → fill
+    for off, shp in [([0, 0, 0], shape), ([1, 1, 3], [shape[0] - 1, shape[1] - 2, shape[2] - 7])]:
+        sel = chunk_coords(meta, off, shp)
+        src = [shards[pos[c]] for c in sel]
+        got = device_read(dev, meta, src, off, shp)
+        want = np.frombuffer(O.array_read(meta, src, off, shp), arr.dtype).reshape(shp)
+        np.testing.assert_array_equal(got, want)
+
+
 @pytest.mark.parametrize("order", [[0, 3, 2, 1], [0, 1, 3, 2]])
 @pytest.mark.parametrize("group", ["-1", "0", "1", "4"])
 def test_tile_encode_chunk_crc_fused(dev, monkeypatch, order, group):

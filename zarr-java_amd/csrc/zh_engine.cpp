@@ -1231,11 +1231,15 @@ int zh_plan_create(zh_ctx* ctx, const zh_array_meta* m, const zh_chunk_src* chun
   }
   // The row decode over G consecutive chunks per work item (rows_group_kernel, narrow rows:
   // G·row bytes of a region row per wave store).  ZH_DEC_RGROUP: 0 off, -1 G·row = 256 B,
-  // or G (1, 2, 4).  Row-clipped items then take the generic kernel (is_fast).  Default: on
-  // with the fused chunk CRC only (c3crc 37.2 → 35.9 ms; plain c3 33.2 → 33.5 ms, so off;
-  // profiles/r02/experiments/ab_r02drg_*.txt).
+  // or G (1, 2, 4; 8 = rows_xpose_kernel: 128-B rows, 8 chunks, 1 KiB contiguous on both
+  // sides through an LDS lane exchange).  Row-clipped items then take the generic kernel
+  // (is_fast).  Default: with the fused chunk CRC -1 (c3crc 37.2 → 35.9 ms); without it, 8 for
+  // 128-B rows (c3, quarter array: 8.71 → 8.49 ms, profiles/r02/experiments/ab_xpose_c3.json)
+  // and off otherwise (plain c3 with G = 2: 33.2 → 33.5 ms, profiles/r02/experiments/
+  // ab_r02drg_*.txt).
   {
-    const int want = env_int("ZH_DEC_RGROUP", p->args.crc_fused ? -1 : 0);
+    const int want = env_int("ZH_DEC_RGROUP", p->args.crc_fused ? -1
+                                              : p->args.fast_vpr_shift == 3 ? 8 : 0);
     const ScatterArgs& g = p->args;
     if (want != 0 && !p->tile_mode && (g.fast_mode == kFastRowArith || g.fast_mode == kFastRowTable) &&
         g.piece_shift == 0 && (g.nt & 3) == 3 && items > 0) {
@@ -2790,7 +2794,16 @@ struct ScatterAlloc {
 };
 std::mutex g_scatter_mu;
 std::map<void*, ScatterAlloc> g_scatter;
-std::vector<std::pair<void*, size_t>> g_va_retired;  // freed ranges, kept reserved
+std::vector<std::pair<void*, size_t>> g_va_retired;  // lab switch ZH_SCATTER_RETIRE only
+// Every virtual range a scatter allocation or view ever used, [begin, end), and reservations
+// set aside because they overlapped one.  ROCm 7.2 did not drop the device's translations of a
+// freed range: a later range reserved over it and mapped to other chunks was partly written
+// through the old mapping (kernel stores lost, copies reading zeros; profiles/va_reuse_lab.py,
+// profiles/r02/placement/va_reuse.jsonl).  So no range is ever mapped twice: a reservation
+// that overlaps a used range stays reserved, unmapped (address space only), and another is
+// taken above the highest address used so far.
+std::vector<std::pair<uintptr_t, uintptr_t>> g_va_used;
+std::vector<std::pair<void*, size_t>> g_va_quarantine;
 
 uint64_t gcd_u64(uint64_t x, uint64_t y) {
   while (y) {
@@ -2841,13 +2854,36 @@ void scatter_unmap(void* base, const ScatterAlloc& A) {
   (void)hipGetLastError();
 }
 
+// reserve a virtual range that overlaps no range used before (see g_va_used)
+int reserve_fresh(size_t size, size_t align, void** out) {
+  std::lock_guard<std::mutex> lk(g_scatter_mu);
+  uintptr_t top = 0;
+  for (auto& u : g_va_used) top = std::max(top, u.second);
+  for (int attempt = 0; attempt < 16; attempt++) {
+    void* base = nullptr;
+    void* hint = attempt == 0 || top == 0 ? nullptr
+                 : (void*)((top + align - 1) / align * align + (uintptr_t)attempt * align);
+    if (hipMemAddressReserve(&base, size, align, hint, 0) != hipSuccess) {
+      (void)hipGetLastError();
+      return ZH_ENOMEM;
+    }
+    const uintptr_t b = (uintptr_t)base, e = b + size;
+    bool clash = false;
+    for (auto& u : g_va_used) clash |= b < u.second && u.first < e;
+    if (!clash) {
+      g_va_used.emplace_back(b, e);
+      *out = base;
+      return ZH_OK;
+    }
+    g_va_quarantine.emplace_back(base, size);  // never mapped; kept out of the next answer
+  }
+  return ZH_ENOMEM;
+}
+
 // reserve a fresh VA range for A and map its chunks there
 int scatter_place(ScatterAlloc& A, uint64_t order, void** out) {
   void* base = nullptr;
-  if (hipMemAddressReserve(&base, A.size, A.chunk, nullptr, 0) != hipSuccess) {
-    (void)hipGetLastError();
-    return ZH_ENOMEM;
-  }
+  if (reserve_fresh(A.size, A.chunk, &base) != ZH_OK) return ZH_ENOMEM;
   const int st = scatter_map(base, A, order);
   if (st != ZH_OK) {
     (void)hipMemAddressFree(base, A.size);
