@@ -22,17 +22,19 @@ def kernel_rows(path, match):
     return rows
 
 
+FAST = ("decode_rows_kernel", "decode_tiles_kernel", "tiles_group_kernel", "rows_group_kernel",
+        "rows_xpose_kernel")
+
+
 def main(src, config, out):
     def encode_view(n):  # the bench's setup encode runs the fast kernels with FLAGS = true
-        return ("decode_rows_kernel" in n or "decode_tiles_kernel" in n or "tiles_group_kernel" in n) and \
-            n.split(">")[0].split(",")[-1].strip() == "true"
+        return any(k in n for k in FAST) and n.split(">")[0].split(",")[-1].strip() == "true"
 
     def decode(n):  # every decode kernel of one step: fast rows/tiles + the generic list
-        return any(k in n for k in ("decode_rows_kernel", "decode_tiles_kernel", "tiles_group_kernel",
-                                     "decode_slow_kernel")) and not encode_view(n)
+        return any(k in n for k in FAST + ("decode_slow_kernel",)) and not encode_view(n)
 
     def fast(n):
-        return ("decode_rows_kernel" in n or "decode_tiles_kernel" in n or "tiles_group_kernel" in n) and not encode_view(n)
+        return any(k in n for k in FAST) and not encode_view(n)
     fetch = kernel_rows(os.path.join(src, f"pmc_fetch_{config}", "run_counter_collection.csv"),
                         decode)
     write = kernel_rows(os.path.join(src, f"pmc_write_{config}", "run_counter_collection.csv"),
