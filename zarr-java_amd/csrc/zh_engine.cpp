@@ -1223,7 +1223,7 @@ int zh_plan_create(zh_ctx* ctx, const zh_array_meta* m, const zh_chunk_src* chun
         p->args.fast_mode == kFastTileTable && p->args.tile_variant == 1 &&
         (!crc || tile_crc) && p->args.piece_shift == 0 && (p->args.nt & 3) == 3 && items > 0) {
       const int64_t groups = (items + G - 1) / G;
-      p->args.tile_variant = (env_int("ZH_DEC_TPF", 1) && G != 8 ? 20 : 10) + G;
+      p->args.tile_variant = (env_int("ZH_DEC_TPF", 1) ? 20 : 10) + G;
       if (crc) p->args.crc_tile_step = tile_crc_step(ends, (size_t)(8 / G));
       p->args.item_mul = env_int("ZH_ITEM_PERM", 1) ? golden_item_mul(groups) : 0;
       p->grid = grid_for(ctx, groups);

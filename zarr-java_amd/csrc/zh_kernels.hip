@@ -2566,6 +2566,7 @@ static void launch_scatter_ds(const ScatterArgs& a, int tile, int enc, int grid,
             case 1: hipLaunchKernelGGL((tiles_group_kernel<3, 1, false, true, false>), dim3(grid), dim3(kBlock), lds, s, a); return;
             case 2: hipLaunchKernelGGL((tiles_group_kernel<3, 2, false, true, false>), dim3(grid), dim3(kBlock), lds, s, a); return;
             case 4: hipLaunchKernelGGL((tiles_group_kernel<3, 4, false, true, false>), dim3(grid), dim3(kBlock), lds, s, a); return;
+            case 8: hipLaunchKernelGGL((tiles_group_kernel<3, 8, false, true, false>), dim3(grid), dim3(kBlock), lds, s, a); return;
             default: return;
           }
         }
