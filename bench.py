@@ -1046,6 +1046,7 @@ def store_inclusive(dev, A, shard_slab, offs, sizes, coords, scratch):
             k = ts.index(min(ts))
             r = {"region_offset": off, "region_shape": shp, "ms_min": round(min(ts) * 1e3, 1),
                  "value": round(nb / min(ts) / GiB, 2), "unit": "GiB/s",
+                 "prep_ms": round(parts[k]["prep_s"] * 1e3, 1),
                  "store_stage_ms": round(parts[k]["stage_s"] * 1e3, 1),
                  "zh_array_read_ms": round(parts[k]["device_s"] * 1e3, 1),
                  "staged_bytes": arr.staged_bytes}

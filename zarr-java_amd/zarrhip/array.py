@@ -338,6 +338,7 @@ class Array:
     # ---------------------------------------------------------------- read
     def read(self, offset=None, shape=None, parallel=True):
         """core.Array.read → numpy array (C order, the array's dtype)."""
+        t_enter = time.perf_counter()
         n = self.ndim
         offset = [0] * n if offset is None else [int(o) for o in offset]
         shape = list(self.metadata.shape) if shape is None else [int(s) for s in shape]
@@ -376,7 +377,8 @@ class Array:
                 devs[0].array_read(self.zmeta, srcs, offset, shape, out.ctypes.data, 0)
         except _lib.ZhError as e:
             raise_for(e)
-        self.last_read_timing = {"stage_s": t1 - t0, "device_s": time.perf_counter() - t1}
+        self.last_read_timing = {"prep_s": t0 - t_enter, "stage_s": t1 - t0,
+                                 "device_s": time.perf_counter() - t1}
         return out
 
     def readChunk(self, coords):
