@@ -202,3 +202,32 @@ def test_nested_sharding_chain_mapping():
     assert zm.chain.nested == 1 and list(zm.chain.nested_chunk_shape)[:3] == [2, 1, 2]
     assert zm.chain.nested_index_has_crc32c == 1
     assert zm.chain.nested_index_location == A.ZH_INDEX_END
+
+
+def test_staging_pool_reuses_buffers():
+    """StagingPool (host staging of store bytes for Array.read): the smallest free buffer
+    that fits is handed out again, views have the requested length, the pool keeps at most
+    `cap` bytes (oldest dropped first)."""
+    from zarrhip.array import StagingPool
+    pool = StagingPool(cap=10 << 20)
+    lease = []
+    a = pool.take(100, lease)
+    b = pool.take(3 << 20, lease)
+    assert len(a) == 100 and len(b) == 3 << 20 and len(lease) == 2
+    base_a, base_b = lease[0], lease[1]
+    pool.give(lease)
+    assert lease == []
+    lease2 = []
+    c = pool.take(50, lease2)          # the smallest fit: a's buffer
+    assert lease2[0] is base_a and len(c) == 50
+    d = pool.take(2 << 20, lease2)     # b's buffer
+    assert lease2[1] is base_b and len(d) == 2 << 20
+    e = pool.take(1 << 20, lease2)     # nothing free: new
+    assert lease2[2] is not base_a and lease2[2] is not base_b and len(e) == 1 << 20
+    pool.give(lease2)
+    big = []
+    pool.take(9 << 20, big)
+    pool.give(big)                     # over the cap: the oldest go first
+    assert sum(x.nbytes for x in pool._free) <= 10 << 20
+    pool.release()
+    assert pool._free == []

@@ -86,12 +86,8 @@ class StagingPool:
         """A uint8 view of at least n bytes; its buffer is appended to `lease` (give back
         with give(lease) once the device has consumed it)."""
         with self._lock:
-            fit = [b for b in self._free if b.nbytes >= n]
-            if fit:
-                b = min(fit, key=lambda x: x.nbytes)
-                self._free.remove(b)
-            else:
-                b = None
+            fit = [i for i, x in enumerate(self._free) if x.nbytes >= n]
+            b = self._free.pop(min(fit, key=lambda i: self._free[i].nbytes)) if fit else None
         if b is None:
             b = np.empty(max(1, -(-n // self.ROUND) * self.ROUND) if n > self.ROUND else
                          max(n, 1), np.uint8)
