@@ -100,3 +100,28 @@ def test_grouped_tile_decode(dev, monkeypatch, order, group, pf, crc):
         np.testing.assert_array_equal(got, want)
     if crc:
         _corrupt_matches_oracle(dev, meta, shards, 1, CHUNK + 1000)
+
+
+@pytest.mark.parametrize("order", [[0, 2, 1], [2, 1, 0], [1, 2, 0], [2, 0, 1]])
+@pytest.mark.parametrize("group", ["1", "2", "4"])
+@pytest.mark.parametrize("endian", [A.ZH_ENDIAN_BIG, A.ZH_ENDIAN_LITTLE])
+@pytest.mark.parametrize("crcw", ["1", "2", "3", "4"])
+def test_crc_waves_tile_decode(dev, monkeypatch, order, group, endian, crcw):
+    """tiles_crcw_kernel (ZH_DEC_CRCW=1, 2): four waves move the tiles, four compute the chunk
+    crc32c from the LDS rows (byte-swapped back for big endian).  Same bytes as the oracle
+    with an elided chunk, a missing shard and a clipped region; corruption in a chunk's first
+    payload row, in a middle row and in its last byte is reported with the oracle's message."""
+    monkeypatch.setenv("ZH_DEC_CRCW", crcw)  # 1: movers prefetch, 2: not, 3: LDS rows, 4: split
+    monkeypatch.setenv("ZH_DEC_TGROUP", group)
+    meta = A.make_meta(SHAPE, [32, 64, 64], 4, endian=endian, sharded=True,
+                       inner_chunk_shape=[32, 32, 32], transpose_order=order, inner_crc32c=True)
+    arr = rand_array(SHAPE, 4, seed=53)
+    arr[32:64, 0:32, 32:64] = 0
+    shards = encode_oracle(meta, arr)
+    shards[2] = None
+    for off, shp in [([0, 0, 0], SHAPE), ([5, 3, 7], [50, 60, 80])]:
+        got, want = _read_both(dev, meta, shards, off, shp)
+        np.testing.assert_array_equal(got, want)
+    full = encode_oracle(meta, arr)  # shard 0: four in-bounds chunks of random data
+    for pos in (3, CHUNK + 1000, 2 * CHUNK + 70001, CHUNK - 5):
+        _corrupt_matches_oracle(dev, meta, full, 0, pos)

@@ -1086,6 +1086,7 @@ int zh_plan_create(zh_ctx* ctx, const zh_array_meta* m, const zh_chunk_src* chun
       p->args.piece_shift++;
   std::vector<uint32_t> tab = setup_fast(m, p->args, p->tile_mode);
   p->args.tile_variant = std::min(1, std::max(0, env_int("ZH_TILE_VARIANT", 1)));
+  p->args.lds_pad = std::max(0, env_int("ZH_LDS_PAD", 0));
   // Chunk CRC fused into the row-interleaved tile kernel: every payload byte of a fast item
   // is loaded exactly once by some lane, and each lane's share is shifted to the payload end
   // by K[u] = x^(8(L − E_u)) (E_u = end of unit u's last row, appended to the table) and a
@@ -1224,6 +1225,12 @@ int zh_plan_create(zh_ctx* ctx, const zh_array_meta* m, const zh_chunk_src* chun
         (!crc || tile_crc) && p->args.piece_shift == 0 && (p->args.nt & 3) == 3 && items > 0) {
       const int64_t groups = (items + G - 1) / G;
       p->args.tile_variant = (env_int("ZH_DEC_TPF", 1) ? 20 : 10) + G;
+      // the chunk CRC on waves of its own (tiles_crcw_kernel: 8-wave blocks, 4 move, 4 CRC)
+      // (1: the movers prefetch, 2: they do not); 3: every lane moves tiles and takes one LDS
+      // payload row for the CRC (tiles_rowcrc_kernel)
+      const int crcw = env_int("ZH_DEC_CRCW", 0);
+      if (crc && G <= 4 && crcw >= 1 && crcw <= 3)
+        p->args.tile_variant = 30 + G + 10 * (crcw - 1);
       if (crc) p->args.crc_tile_step = tile_crc_step(ends, (size_t)(8 / G));
       p->args.item_mul = env_int("ZH_ITEM_PERM", 1) ? golden_item_mul(groups) : 0;
       p->grid = grid_for(ctx, groups);
@@ -2445,7 +2452,7 @@ int zh_array_write(zh_ctx* ctx, const zh_array_meta* m, const void* src, const i
   }
   (void)hipSetDevice(ctx->device);
   hipStream_t s = stream_v ? (hipStream_t)stream_v : ctx->stream;
-  ScatterArgs a;
+  ScatterArgs a{};
   int tile_mode = 0;
   fill_common_args(m, shape, true, a, tile_mode);
   const zh_codec_chain& c = m->chain;

@@ -124,7 +124,10 @@ struct ScatterArgs {
   int32_t tile;
   int32_t nt;                   // fast kernels: bit 0 non-temporal loads, bit 1 stores
   int32_t tile_variant;         // tile fast path: 0 row-per-tile loads, 1 row-interleaved groups,
-                                // 10 + G / 20 + G: tiles_group_kernel (without / with prefetch)
+                                // 10 + G / 20 + G: tiles_group_kernel (without / with prefetch);
+                                // 30 + G (+10, +20, +30): chunk CRC on waves of its own / over
+                                // LDS rows (ZH_DEC_CRCW)
+  int32_t lds_pad;              // extra dynamic LDS per block (ZH_LDS_PAD; occupancy lab only)
   int32_t row_group;            // row fast path (decode): G > 0 = rows_group_kernel over G
                                 // chunks per work item (row-clipped items then go slow)
   int32_t crc_extra;            // 4 when each stored chunk carries a trailing crc32c, else 0

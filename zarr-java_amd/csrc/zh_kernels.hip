@@ -1748,6 +1748,325 @@ __global__ __launch_bounds__(kBlock) void tiles_group_kernel(ScatterArgs a) {
   }
 }
 
+// decode, grouped tile kernel with the chunk CRC on waves of their own (ZH_DEC_CRCW).  A block
+// is 8 waves: waves 0-3 move tiles exactly as tiles_group_kernel<…, CRC = false, PF = true>
+// does, and waves 4-7 compute the crc32c of the same payload from the LDS tiles.  After the
+// barrier that publishes a step's tiles, CRC lane (cw, L) copies payload row r = L & 31 of
+// tile slot t = 2·cw + (L >> 5) (128 contiguous payload bytes; banks 33·(t + r) + j, distinct
+// within each 32-lane half) into registers; after the second barrier, while the movers write
+// the next step's tiles, it runs the plain slicing-by-8 update over those 128 bytes: 16
+// lookups per 16-B vector and no zero-shift, where the fused kernels pay 20 and hold the
+// movers' registers.  Row r of unit u ends (31 − r)·4·s_fd bytes before the unit end E_u, so
+// the lane's share is K[u]·x^(8·(31 − r)·4·s_fd)·row_crc; its units u, u + 8/G, … fold with SD
+// (regular layout) as in the fused kernels.  For G ≤ 4 a CRC wave's two tiles belong to one
+// chunk: one XOR-reduce and one atomic per wave.  LDS holds the byte-swapped words; the lanes
+// swap them back.
+//
+// PF = true: the movers prefetch the next step (more registers: held to 4 waves per SIMD, two
+// blocks per CU); PF = false: load, LDS, store, held to 6 waves per SIMD (three blocks).
+template <int G, bool PF>
+__global__ __launch_bounds__(2 * kBlock) __attribute__((amdgpu_waves_per_eu(PF ? 4 : 6)))
+void tiles_crcw_kernel(ScatterArgs a) {
+  static_assert(G == 1 || G == 2 || G == 4, "a CRC wave's tiles must belong to one chunk");
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  uint2* tab = reinterpret_cast<uint2*>(smem);
+  uint8_t* after_tab = smem + (((size_t)a.fast_n * 8 + 15) & ~(size_t)15);
+  uint32_t* lds = reinterpret_cast<uint32_t*>(after_tab);
+  const int tid = threadIdx.x;
+  for (int i = tid; i < a.fast_n; i += 2 * kBlock) tab[i] = reinterpret_cast<const uint2*>(a.fast_tab)[i];
+  uint32_t(*T)[256] = reinterpret_cast<uint32_t(*)[256]>(after_tab + (size_t)kTG * kTilePitch * 4);
+  uint32_t(*SD)[256] = T + 12;  // same layout as the fused kernels (T, S, SD, K); S unused
+  uint32_t* K = reinterpret_cast<uint32_t*>(SD + 4);
+  if (tid < 256) {
+#pragma unroll
+    for (int k = 0; k < 8; k++) T[k][tid] = g_crc.T[k][tid];
+#pragma unroll
+    for (int b = 0; b < 4; b++)
+      SD[b][tid] = a.crc_tile_step ? multmodp(a.crc_tile_step, (uint32_t)tid << (8 * b)) : 0u;
+  }
+  for (int i = tid; i < a.fast_n; i += 2 * kBlock) K[i] = a.fast_tab[2 * a.fast_n + i];
+  __syncthreads();
+  constexpr int TG = kTG / G;  // tiles of each chunk per step
+  const bool crcw = tid >= kBlock;
+  const int wave = (tid >> 6) & 3, lane = tid & 63;
+  // movers: lane (t, g) moves tile t; CRC lanes: tile slot 2·wave + (lane >> 5), row lane & 31
+  const int t = crcw ? 2 * wave + (lane >> 5) : lane >> 3, g = lane & 7;
+  const int q = t / TG, ti = t % TG, r = lane & 31;
+  const int64_t s_fd = a.pstride[a.fd], d_fs = a.rstride[a.fs];
+  const bool regular = a.crc_tile_step != 0;
+  const uint32_t units = (uint32_t)a.fast_n;
+  const int64_t ngroups = (a.n_citems + G - 1) / G;
+  const uint32_t kr = crcw ? x2nmodp((uint64_t)(31 - r) * 4 * (uint64_t)s_fd, 3) : 0u;
+  uint32_t* mine = lds + t * kTilePitch;
+  for (int64_t gi = blockIdx.x; gi < ngroups; gi += gridDim.x) {
+    const int64_t pg = a.item_mul ? (int64_t)(((uint64_t)gi * a.item_mul) % (uint64_t)ngroups) : gi;
+    const int64_t c = pg * G + q;
+    bool on = false;
+    const uint8_t* src = nullptr;
+    uint8_t* dst = nullptr;
+    if (c < a.n_citems) {
+      const uint4* dp = reinterpret_cast<const uint4*>(a.desc + c);
+      const uint4 x = dp[0], y = dp[1];
+      on = (y.z & kDescFast) != 0;
+      src = (const uint8_t*)(uintptr_t)(((uint64_t)x.y << 32) | x.x);
+      dst = a.region + (int64_t)(((uint64_t)x.w << 32) | x.z) * 4;
+    }
+    if (__syncthreads_or(on) == 0) continue;  // block-uniform
+    if (!crcw) {  // movers (tiles_group_kernel's prefetching decode loop)
+      uint4 x[8];
+      auto load = [&](uint32_t ub_) {
+        const uint32_t uu = ub_ + ti;
+        if (on && uu < units) {
+          const uint8_t* base = src + ((size_t)tab[uu].x + g * 4) * 4;
+#pragma unroll
+          for (int k = 0; k < 8; k++)
+            x[k] = ld16s<true>(base + (size_t)(wave * 8 + k) * s_fd * 4);
+        }
+      };
+      if (PF) load(0);
+#pragma unroll 1
+      for (uint32_t ub = 0; ub < units; ub += TG) {
+        const uint32_t u = ub + ti;
+        const bool live = on && u < units;
+        if (live) {
+          if (!PF) load(ub);
+#pragma unroll
+          for (int k = 0; k < 8; k++) {
+            uint32_t* row = mine + (wave * 8 + k) * 33 + g * 4;
+            row[0] = xform1<4>(x[k].x, a.swap, 0);
+            row[1] = xform1<4>(x[k].y, a.swap, 0);
+            row[2] = xform1<4>(x[k].z, a.swap, 0);
+            row[3] = xform1<4>(x[k].w, a.swap, 0);
+          }
+        }
+        __syncthreads();
+        if (PF && ub + TG < units) load(ub + TG);
+        if (live) {
+          uint8_t* base = dst + ((size_t)tab[u].y + g * 4) * 4;
+#pragma unroll
+          for (int k = 0; k < 8; k++) {
+            const int rr = wave * 8 + k;
+            uint4 y;
+            y.x = mine[(g * 4 + 0) * 33 + rr];
+            y.y = mine[(g * 4 + 1) * 33 + rr];
+            y.z = mine[(g * 4 + 2) * 33 + rr];
+            y.w = mine[(g * 4 + 3) * 33 + rr];
+            st16s<true>(base + (size_t)rr * d_fs * 4, y);
+          }
+        }
+        __syncthreads();
+      }
+    } else {  // CRC waves
+      uint32_t share = 0, run = 0, ulast = ~0u;
+#pragma unroll 1
+      for (uint32_t ub = 0; ub < units; ub += TG) {
+        const uint32_t u = ub + ti;
+        const bool live = on && u < units;
+        __syncthreads();
+        uint32_t w[32];
+        if (live) {
+          const uint32_t* row = mine + r * 33;
+#pragma unroll
+          for (int j = 0; j < 32; j++) w[j] = row[j];
+        }
+        __syncthreads();
+        if (live) {
+          uint32_t acc = 0;
+#pragma unroll
+          for (int v = 0; v < 8; v++) {
+            v4u wv;
+            wv.x = xform1<4>(w[4 * v + 0], a.swap, 0);
+            wv.y = xform1<4>(w[4 * v + 1], a.swap, 0);
+            wv.z = xform1<4>(w[4 * v + 2], a.swap, 0);
+            wv.w = xform1<4>(w[4 * v + 3], a.swap, 0);
+            acc = crc_upd16(acc, wv, T);
+          }
+          if (regular) {
+            run = (ulast == ~0u ? 0u : crc_shift_tab(run, SD)) ^ acc;
+            ulast = u;
+          } else {
+            share ^= multmodp(K[u], acc);
+          }
+        }
+      }
+      if (regular && ulast != ~0u) share = multmodp(K[ulast], run);
+      uint32_t cr = multmodp(kr, share);
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) cr ^= (uint32_t)__shfl_xor((int)cr, o, 64);
+      if (lane == 0 && on) atomicXor(a.crc_partials + c, cr);
+    }
+  }
+}
+
+// 4·(byte SEL of w) in one SDWA shift: the LDS byte offset of a 4-B table entry
+template <int SEL>
+__device__ __forceinline__ uint32_t byte_x4(uint32_t w) {
+  uint32_t r;
+  if constexpr (SEL == 0)
+    asm("v_lshlrev_b32_sdwa %0, 2, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_0" : "=v"(r) : "v"(w));
+  else if constexpr (SEL == 1)
+    asm("v_lshlrev_b32_sdwa %0, 2, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_1" : "=v"(r) : "v"(w));
+  else if constexpr (SEL == 2)
+    asm("v_lshlrev_b32_sdwa %0, 2, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_2" : "=v"(r) : "v"(w));
+  else
+    asm("v_lshlrev_b32_sdwa %0, 2, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_3" : "=v"(r) : "v"(w));
+  return r;
+}
+
+// a dword of LDS at a byte address known relative to LDS offset 0 (constant parts fold into
+// the ds_read immediate)
+__device__ __forceinline__ uint32_t lds_word(uint32_t byte_addr) {
+  return *reinterpret_cast<const __attribute__((address_space(3))) uint32_t*>((size_t)byte_addr);
+}
+
+// a ^ b ^ c in one VALU op (v_bitop3_b32, truth table 0x96)
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+  uint32_t r;
+  asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
+
+// Slicing-by-8 step over the 8 raw payload bytes held by the words w0, w1 as they sit in the LDS
+// tiles; the 8 tables T[7..0] are at LDS bytes 0, 1024, … (a kernel without static LDS, tables
+// first in the dynamic block).  SWAP: the tiles hold byte-swapped words, so raw byte k of a word
+// is its byte 3 − k; the tables then hold byte-swapped entries and the register is carried
+// byte-swapped (c' = bswap(c): raw lo ^ c = bswap(w0 ^ c'), and the XOR of swapped entries is
+// the swapped result).  Per 8 bytes: one XOR in, 8 SDWA offsets, 8 lookups, a 3-input XOR tree.
+template <bool SWAP>
+__device__ __forceinline__ uint32_t crc_upd8_lds(uint32_t c, uint32_t w0, uint32_t w1) {
+  const uint32_t lo = w0 ^ c, hi = w1;
+  constexpr int s0 = SWAP ? 3 : 0, s1 = SWAP ? 2 : 1, s2 = SWAP ? 1 : 2, s3 = SWAP ? 0 : 3;
+  const uint32_t a0 = xor3(lds_word(byte_x4<s0>(lo) + 7 * 1024), lds_word(byte_x4<s1>(lo) + 6 * 1024),
+                           lds_word(byte_x4<s2>(lo) + 5 * 1024));
+  const uint32_t a1 = xor3(lds_word(byte_x4<s3>(lo) + 4 * 1024), lds_word(byte_x4<s0>(hi) + 3 * 1024),
+                           lds_word(byte_x4<s1>(hi) + 2 * 1024));
+  const uint32_t a2 = lds_word(byte_x4<s2>(hi) + 1 * 1024) ^ lds_word(byte_x4<s3>(hi));
+  return xor3(a0, a1, a2);
+}
+
+// decode, grouped tile kernel with the chunk CRC over LDS rows (ZH_DEC_CRCW=3).  The lanes
+// move tiles as tiles_group_kernel<…, PF = true> does; for the CRC, lane i of the block takes
+// payload row i & 31 of tile slot i >> 5 (128 contiguous payload bytes) from the LDS tiles after
+// the stores of a step, and runs the plain slicing-by-8 update over it after the barrier: 16
+// lookups per 16-B vector, no zero-shift (the fused kernel: 20), and no register copy of the
+// loaded vectors.  A lane's CRC row and the tile it moves may belong to different chunks of
+// the group; the CRC role reads its chunk's descriptor.  Shares as in tiles_crcw_kernel.
+// SWAP (= a.swap, bytes(big) on uint32) is a template argument: the byte swap of the movers and
+// the CRC's byte order cost no select per word.  LDS: T, S (unused), SD, K, table, tiles.
+template <int G, bool SWAP>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3)))
+void tiles_rowcrc_kernel(ScatterArgs a) {
+  static_assert(G == 1 || G == 2 || G == 4, "a wave's CRC rows must belong to one chunk");
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  uint32_t(*T)[256] = reinterpret_cast<uint32_t(*)[256]>(smem);
+  uint32_t(*SD)[256] = T + 12;
+  uint32_t* K = reinterpret_cast<uint32_t*>(SD + 4);
+  uint2* tab = reinterpret_cast<uint2*>(smem + ((16 * 1024 + (size_t)a.fast_n * 4 + 15) & ~(size_t)15));
+  uint32_t* lds = reinterpret_cast<uint32_t*>(
+      reinterpret_cast<uint8_t*>(tab) + (((size_t)a.fast_n * 8 + 15) & ~(size_t)15));
+  const int tid = threadIdx.x;
+  for (int i = tid; i < a.fast_n; i += kBlock) tab[i] = reinterpret_cast<const uint2*>(a.fast_tab)[i];
+#pragma unroll
+  for (int k = 0; k < 8; k++) T[k][tid] = SWAP ? __builtin_bswap32(g_crc.T[k][tid]) : g_crc.T[k][tid];
+#pragma unroll
+  for (int b = 0; b < 4; b++)
+    SD[b][tid] = a.crc_tile_step ? multmodp(a.crc_tile_step, (uint32_t)tid << (8 * b)) : 0u;
+  for (int i = tid; i < a.fast_n; i += kBlock) K[i] = a.fast_tab[2 * a.fast_n + i];
+  __syncthreads();
+  constexpr int TG = kTG / G;
+  const int wave = tid >> 6, lane = tid & 63;
+  const int t = lane >> 3, g = lane & 7, q = t / TG, ti = t % TG;  // mover role
+  const int tc = tid >> 5, r = tid & 31, qc = tc / TG, tic = tc % TG;  // CRC role (wave-uniform qc)
+  const int64_t s_fd = a.pstride[a.fd], d_fs = a.rstride[a.fs];
+  const bool regular = a.crc_tile_step != 0;
+  const uint32_t units = (uint32_t)a.fast_n;
+  const int64_t ngroups = (a.n_citems + G - 1) / G;
+  const uint32_t kr = x2nmodp((uint64_t)(31 - r) * 4 * (uint64_t)s_fd, 3);
+  uint32_t* mine = lds + t * kTilePitch;
+  const uint32_t* crow = lds + tc * kTilePitch + r * 33;
+  auto sw = [](uint32_t x) { return SWAP ? __builtin_bswap32(x) : x; };
+  for (int64_t gi = blockIdx.x; gi < ngroups; gi += gridDim.x) {
+    const int64_t pg = a.item_mul ? (int64_t)(((uint64_t)gi * a.item_mul) % (uint64_t)ngroups) : gi;
+    const int64_t c = pg * G + q, cc = pg * G + qc;
+    bool on = false, onc = false;
+    const uint8_t* src = nullptr;
+    uint8_t* dst = nullptr;
+    if (c < a.n_citems) {
+      const uint4* dp = reinterpret_cast<const uint4*>(a.desc + c);
+      const uint4 x = dp[0], y = dp[1];
+      on = (y.z & kDescFast) != 0;
+      src = (const uint8_t*)(uintptr_t)(((uint64_t)x.y << 32) | x.x);
+      dst = a.region + (int64_t)(((uint64_t)x.w << 32) | x.z) * 4;
+    }
+    if (cc < a.n_citems) onc = (reinterpret_cast<const uint4*>(a.desc + cc)[1].z & kDescFast) != 0;
+    if (__syncthreads_or(on) == 0) continue;  // block-uniform
+    uint32_t share = 0, run = 0, ulast = ~0u;
+    uint4 x[8];
+    auto load = [&](uint32_t ub_) {
+      const uint32_t uu = ub_ + ti;
+      if (on && uu < units) {
+        const uint8_t* base = src + ((size_t)tab[uu].x + g * 4) * 4;
+#pragma unroll
+        for (int k = 0; k < 8; k++) x[k] = ld16s<true>(base + (size_t)(wave * 8 + k) * s_fd * 4);
+      }
+    };
+    load(0);
+#pragma unroll 1
+    for (uint32_t ub = 0; ub < units; ub += TG) {
+      const uint32_t u = ub + ti, uc = ub + tic;
+      const bool live = on && u < units, livec = onc && uc < units;
+      if (live) {
+#pragma unroll
+        for (int k = 0; k < 8; k++) {
+          uint32_t* row = mine + (wave * 8 + k) * 33 + g * 4;
+          row[0] = sw(x[k].x);
+          row[1] = sw(x[k].y);
+          row[2] = sw(x[k].z);
+          row[3] = sw(x[k].w);
+        }
+      }
+      __syncthreads();
+      if (ub + TG < units) load(ub + TG);
+      if (live) {
+        uint8_t* base = dst + ((size_t)tab[u].y + g * 4) * 4;
+#pragma unroll
+        for (int k = 0; k < 8; k++) {
+          const int rr = wave * 8 + k;
+          uint4 y;
+          y.x = mine[(g * 4 + 0) * 33 + rr];
+          y.y = mine[(g * 4 + 1) * 33 + rr];
+          y.z = mine[(g * 4 + 2) * 33 + rr];
+          y.w = mine[(g * 4 + 3) * 33 + rr];
+          st16s<true>(base + (size_t)rr * d_fs * 4, y);
+        }
+      }
+      uint32_t w[32];
+      if (livec) {
+#pragma unroll
+        for (int j = 0; j < 32; j++) w[j] = crow[j];
+      }
+      __syncthreads();
+      if (livec) {
+        uint32_t acc = 0;  // byte-swapped with SWAP
+#pragma unroll
+        for (int j = 0; j < 32; j += 2) acc = crc_upd8_lds<SWAP>(acc, w[j], w[j + 1]);
+        if (SWAP) acc = __builtin_bswap32(acc);
+        if (regular) {
+          run = (ulast == ~0u ? 0u : crc_shift_tab(run, SD)) ^ acc;
+          ulast = uc;
+        } else {
+          share ^= multmodp(K[uc], acc);
+        }
+      }
+    }
+    if (regular && ulast != ~0u) share = multmodp(K[ulast], run);
+    uint32_t cr = multmodp(kr, share);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) cr ^= (uint32_t)__shfl_xor((int)cr, o, 64);
+    if (lane == 0 && onc) atomicXor(a.crc_partials + cc, cr);
+  }
+}
+
 // The CRC-fused decode variant held to 3 waves per SIMD (LDS allows 3 blocks of 4 waves per
 // CU; unconstrained it takes 172 VGPRs and runs 2)
 template <int NT, bool FLAGS>
@@ -2552,6 +2871,21 @@ static void launch_scatter_ds(const ScatterArgs& a, int tile, int enc, int grid,
         const int v = a.tile_variant;
         lds += v == 0 ? (size_t)kFastTPB * 32 * 33 * 4 : (size_t)kTG * kTilePitch * 4;
         const bool ntx = nt == 3;
+        if (v > 30 && a.crc_fused) {  // chunk CRC on waves of its own (ZH_DEC_CRCW=1, 2)
+          const size_t lc = lds + 16 * 256 * 4 + (size_t)a.fast_n * 4;
+          switch (v - 30) {
+            case 1: hipLaunchKernelGGL((tiles_crcw_kernel<1, true>), dim3(grid), dim3(2 * kBlock), lc, s, a); return;
+            case 2: hipLaunchKernelGGL((tiles_crcw_kernel<2, true>), dim3(grid), dim3(2 * kBlock), lc, s, a); return;
+            case 4: hipLaunchKernelGGL((tiles_crcw_kernel<4, true>), dim3(grid), dim3(2 * kBlock), lc, s, a); return;
+            case 11: hipLaunchKernelGGL((tiles_crcw_kernel<1, false>), dim3(grid), dim3(2 * kBlock), lc, s, a); return;
+            case 12: hipLaunchKernelGGL((tiles_crcw_kernel<2, false>), dim3(grid), dim3(2 * kBlock), lc, s, a); return;
+            case 14: hipLaunchKernelGGL((tiles_crcw_kernel<4, false>), dim3(grid), dim3(2 * kBlock), lc, s, a); return;
+            case 21: if (a.swap) hipLaunchKernelGGL((tiles_rowcrc_kernel<1, true>), dim3(grid), dim3(kBlock), lc + 64, s, a); else hipLaunchKernelGGL((tiles_rowcrc_kernel<1, false>), dim3(grid), dim3(kBlock), lc + 64, s, a); return;
+            case 22: if (a.swap) hipLaunchKernelGGL((tiles_rowcrc_kernel<2, true>), dim3(grid), dim3(kBlock), lc + 64, s, a); else hipLaunchKernelGGL((tiles_rowcrc_kernel<2, false>), dim3(grid), dim3(kBlock), lc + 64, s, a); return;
+            case 24: if (a.swap) hipLaunchKernelGGL((tiles_rowcrc_kernel<4, true>), dim3(grid), dim3(kBlock), lc + 64, s, a); else hipLaunchKernelGGL((tiles_rowcrc_kernel<4, false>), dim3(grid), dim3(kBlock), lc + 64, s, a); return;
+            default: return;
+          }
+        }
         if (v > 20 && a.crc_fused) {  // prefetching form (ZH_DEC_TPF=1)
           const size_t lc = lds + 16 * 256 * 4 + (size_t)a.fast_n * 4;
           switch (v - 20) {
@@ -2562,6 +2896,7 @@ static void launch_scatter_ds(const ScatterArgs& a, int tile, int enc, int grid,
           }
         }
         if (v > 20) {
+          lds += (size_t)a.lds_pad;  // occupancy lab (ZH_LDS_PAD), 0 by default
           switch (v - 20) {
             case 1: hipLaunchKernelGGL((tiles_group_kernel<3, 1, false, true, false>), dim3(grid), dim3(kBlock), lds, s, a); return;
             case 2: hipLaunchKernelGGL((tiles_group_kernel<3, 2, false, true, false>), dim3(grid), dim3(kBlock), lds, s, a); return;
