@@ -9,7 +9,7 @@ import pytest
 import oracle as O
 from helpers import chunk_coords, device_read, encode_oracle, rand_array
 from zarrhip import _abi as A
-from zarrhip._lib import ZhError
+from zarrhip._lib import ZhError, lib
 
 pytestmark = pytest.mark.gpu
 
@@ -28,6 +28,11 @@ def _read_both(dev, meta, shards, off, shp):
     srcs = [shards[pos[c]] for c in sel]
     want = np.frombuffer(O.array_read(meta, srcs, off, shp), np.uint32).reshape(shp)
     return device_read(dev, meta, srcs, off, shp), want
+
+
+def _variant():
+    """Kernel variant of the last decode scatter launch (zh_debug_last_fast_path)."""
+    return (lib().zh_debug_last_fast_path() // 1000) % 1000
 
 
 def _corrupt_matches_oracle(dev, meta, shards, k, pos):
@@ -89,15 +94,20 @@ def test_grouped_tile_decode(dev, monkeypatch, order, group, pf, crc):
     chunk, a missing shard, a clipped region; a corrupt byte of a fast chunk is caught."""
     monkeypatch.setenv("ZH_DEC_TGROUP", group)
     monkeypatch.setenv("ZH_DEC_TPF", pf)
+    monkeypatch.setenv("ZH_SMALL_SPLIT", "0")  # whole chunks: the grouped kernels need them
     meta = A.make_meta(SHAPE, [32, 64, 64], 4, endian=A.ZH_ENDIAN_BIG, sharded=True,
                        inner_chunk_shape=[32, 32, 32], transpose_order=order, inner_crc32c=crc)
     arr = rand_array(SHAPE, 4, seed=47)
     arr[32:64, 0:32, 32:64] = 0
     shards = encode_oracle(meta, arr)
     shards[2] = None
+    G = int(group)
+    want_variant = 1 if G == 0 or (G == 8 and crc) else (20 if pf == "1" else 10) + G
     for off, shp in [([0, 0, 0], SHAPE), ([5, 3, 7], [50, 60, 80])]:
         got, want = _read_both(dev, meta, shards, off, shp)
         np.testing.assert_array_equal(got, want)
+        if off == [0, 0, 0]:
+            assert _variant() == want_variant
     if crc:
         _corrupt_matches_oracle(dev, meta, shards, 1, CHUNK + 1000)
 
@@ -105,14 +115,15 @@ def test_grouped_tile_decode(dev, monkeypatch, order, group, pf, crc):
 @pytest.mark.parametrize("order", [[0, 2, 1], [2, 1, 0], [1, 2, 0], [2, 0, 1]])
 @pytest.mark.parametrize("group", ["1", "2", "4"])
 @pytest.mark.parametrize("endian", [A.ZH_ENDIAN_BIG, A.ZH_ENDIAN_LITTLE])
-@pytest.mark.parametrize("crcw", ["1", "2", "3", "4"])
+@pytest.mark.parametrize("crcw", ["1", "2", "3"])
 def test_crc_waves_tile_decode(dev, monkeypatch, order, group, endian, crcw):
     """tiles_crcw_kernel (ZH_DEC_CRCW=1, 2): four waves move the tiles, four compute the chunk
     crc32c from the LDS rows (byte-swapped back for big endian).  Same bytes as the oracle
     with an elided chunk, a missing shard and a clipped region; corruption in a chunk's first
     payload row, in a middle row and in its last byte is reported with the oracle's message."""
-    monkeypatch.setenv("ZH_DEC_CRCW", crcw)  # 1: movers prefetch, 2: not, 3: LDS rows, 4: split
+    monkeypatch.setenv("ZH_DEC_CRCW", crcw)  # 1: movers prefetch, 2: not, 3: LDS rows
     monkeypatch.setenv("ZH_DEC_TGROUP", group)
+    monkeypatch.setenv("ZH_SMALL_SPLIT", "0")
     meta = A.make_meta(SHAPE, [32, 64, 64], 4, endian=endian, sharded=True,
                        inner_chunk_shape=[32, 32, 32], transpose_order=order, inner_crc32c=True)
     arr = rand_array(SHAPE, 4, seed=53)
@@ -122,6 +133,8 @@ def test_crc_waves_tile_decode(dev, monkeypatch, order, group, endian, crcw):
     for off, shp in [([0, 0, 0], SHAPE), ([5, 3, 7], [50, 60, 80])]:
         got, want = _read_both(dev, meta, shards, off, shp)
         np.testing.assert_array_equal(got, want)
+        if off == [0, 0, 0]:
+            assert _variant() == 30 + int(group) + 10 * (int(crcw) - 1)
     full = encode_oracle(meta, arr)  # shard 0: four in-bounds chunks of random data
     for pos in (3, CHUNK + 1000, 2 * CHUNK + 70001, CHUNK - 5):
         _corrupt_matches_oracle(dev, meta, full, 0, pos)

@@ -1229,7 +1229,7 @@ int zh_plan_create(zh_ctx* ctx, const zh_array_meta* m, const zh_chunk_src* chun
       // (1: the movers prefetch, 2: they do not); 3: every lane moves tiles and takes one LDS
       // payload row for the CRC (tiles_rowcrc_kernel)
       const int crcw = env_int("ZH_DEC_CRCW", 0);
-      if (crc && G <= 4 && crcw >= 1 && crcw <= 3)
+      if (crc && G <= 4 && crcw >= 1 && crcw <= 3 && (crcw != 3 || zh::rowcrc_lds_at_zero()))
         p->args.tile_variant = 30 + G + 10 * (crcw - 1);
       if (crc) p->args.crc_tile_step = tile_crc_step(ends, (size_t)(8 / G));
       p->args.item_mul = env_int("ZH_ITEM_PERM", 1) ? golden_item_mul(groups) : 0;
@@ -1435,6 +1435,8 @@ int zh_plan_stats(const zh_plan* p, int64_t* in_bytes, int64_t* out_bytes, int64
   if (nshards) *nshards = p->nshards;
   return ZH_OK;
 }
+
+int64_t zh_debug_last_fast_path(void) { return zh::g_last_fast_path.load(); }
 
 int64_t zh_plan_staged_bytes(const zh_plan* p) {
   if (!p) return -1;

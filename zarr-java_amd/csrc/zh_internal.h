@@ -3,6 +3,8 @@
 #pragma once
 
 #include <hip/hip_runtime.h>
+
+#include <atomic>
 #include <stdint.h>
 
 #include "../../include/zarrhip.h"
@@ -203,6 +205,8 @@ hipError_t launch_nested_index(const NestArgs& a, int grid, hipStream_t stream);
 hipError_t launch_data_crc(const DataCrcArgs& a, int grid, hipStream_t stream);
 hipError_t launch_data_crc_partial(const DataCrcArgs& a, int grid, hipStream_t stream);
 hipError_t launch_data_crc_finalize(const DataCrcArgs& a, hipStream_t stream);
+extern std::atomic<int64_t> g_last_fast_path;  // diagnostic, zh_debug_last_fast_path
+bool rowcrc_lds_at_zero();  // tiles_rowcrc_kernel has no static LDS
 hipError_t launch_scatter(const ScatterArgs& a, int dsize, int tile_mode, int encode, int grid,
                           hipStream_t stream);
 hipError_t launch_decode_slow(const ScatterArgs& a, int grid, hipStream_t stream);

@@ -19,6 +19,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cstdlib>
 
 #include "zh_internal.h"
@@ -1944,7 +1945,9 @@ __device__ __forceinline__ uint32_t crc_upd8_lds(uint32_t c, uint32_t w0, uint32
   return xor3(a0, a1, a2);
 }
 
-// decode, grouped tile kernel with the chunk CRC over LDS rows (ZH_DEC_CRCW=3).  The lanes
+// decode, grouped tile kernel with the chunk CRC over LDS rows (ZH_DEC_CRCW=3).  The kernel
+// must have no static LDS, since its tables are addressed from LDS offset 0: the host selects it
+// only when rowcrc_lds_at_zero() confirms that for every instantiation.  The lanes
 // move tiles as tiles_group_kernel<…, PF = true> does; for the CRC, lane i of the block takes
 // payload row i & 31 of tile slot i >> 5 (128 contiguous payload bytes) from the LDS tiles after
 // the stores of a step, and runs the plain slicing-by-8 update over it after the barrier: 16
@@ -1959,6 +1962,7 @@ void tiles_rowcrc_kernel(ScatterArgs a) {
   static_assert(G == 1 || G == 2 || G == 4, "a wave's CRC rows must belong to one chunk");
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   uint32_t(*T)[256] = reinterpret_cast<uint32_t(*)[256]>(smem);
+  uint32_t* flag = T[8];  // 8 words of the S area (no zero-shift table here)
   uint32_t(*SD)[256] = T + 12;
   uint32_t* K = reinterpret_cast<uint32_t*>(SD + 4);
   uint2* tab = reinterpret_cast<uint2*>(smem + ((16 * 1024 + (size_t)a.fast_n * 4 + 15) & ~(size_t)15));
@@ -1999,7 +2003,16 @@ void tiles_rowcrc_kernel(ScatterArgs a) {
       dst = a.region + (int64_t)(((uint64_t)x.w << 32) | x.z) * 4;
     }
     if (cc < a.n_citems) onc = (reinterpret_cast<const uint4*>(a.desc + cc)[1].z & kDescFast) != 0;
-    if (__syncthreads_or(on) == 0) continue;  // block-uniform
+    // block-uniform skip; __syncthreads_or would add static LDS and move the tables off 0.
+    // Per-wave flags in the unused S area, by iteration parity (every iteration has this
+    // barrier, so no wave is more than one iteration ahead of another here).
+    {
+      const uint32_t any = __ballot(on) != 0 ? 1u : 0u;
+      if (lane == 0) flag[((gi / gridDim.x) & 1) * 4 + wave] = any;
+      __syncthreads();
+      const uint32_t* f = flag + ((gi / gridDim.x) & 1) * 4;
+      if ((f[0] | f[1] | f[2] | f[3]) == 0) continue;
+    }
     uint32_t share = 0, run = 0, ulast = ~0u;
     uint4 x[8];
     auto load = [&](uint32_t ub_) {
@@ -2975,9 +2988,31 @@ static void launch_scatter_ds(const ScatterArgs& a, int tile, int enc, int grid,
   }
 }
 
+// tiles_rowcrc_kernel addresses its CRC tables from LDS offset 0: true when no instantiation
+// has static LDS (the dynamic block then starts at 0)
+bool rowcrc_lds_at_zero() {
+  static const bool ok = [] {
+    const void* fns[] = {(const void*)tiles_rowcrc_kernel<1, false>, (const void*)tiles_rowcrc_kernel<1, true>,
+                         (const void*)tiles_rowcrc_kernel<2, false>, (const void*)tiles_rowcrc_kernel<2, true>,
+                         (const void*)tiles_rowcrc_kernel<4, false>, (const void*)tiles_rowcrc_kernel<4, true>};
+    for (const void* f : fns) {
+      hipFuncAttributes at;
+      if (hipFuncGetAttributes(&at, f) != hipSuccess || at.sharedSizeBytes != 0) return false;
+    }
+    return true;
+  }();
+  return ok;
+}
+
+// the fast-path selection of the last decode scatter launch (diagnostic: zh_debug_last_fast_path)
+std::atomic<int64_t> g_last_fast_path{-1};
+
 hipError_t launch_scatter(const ScatterArgs& a, int dsize, int tile_mode, int encode, int grid,
                           hipStream_t stream) {
   if (a.total_items == 0) return hipSuccess;
+  if (!encode)
+    g_last_fast_path.store((int64_t)a.fast_mode * 1000000 + (int64_t)a.tile_variant * 1000 +
+                           (int64_t)(a.row_group & 0xFF) * 4 + (a.piece_shift ? 1 : 0));
   switch (dsize) {
     case 1: launch_scatter_ds<1>(a, tile_mode, encode, grid, stream); break;
     case 2: launch_scatter_ds<2>(a, tile_mode, encode, grid, stream); break;
