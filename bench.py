@@ -216,10 +216,14 @@ def pmc_traffic(config):
 
 
 def kernel_name(meta):
-    # tile chains: tiles_group_kernel (ZH_DEC_TGROUP=0: decode_tiles_kernel)
+    # tile chains: tiles_group_kernel (ZH_DEC_TGROUP=0: decode_tiles_kernel); with the chunk
+    # crc32c the row-CRC tile kernel (ZH_DEC_CRCW=3, the default)
     if meta.chain.has_transpose:
-        return "decode_tiles_kernel" if os.environ.get("ZH_DEC_TGROUP") == "0" else \
-            "tiles_group_kernel"
+        if os.environ.get("ZH_DEC_TGROUP") == "0":
+            return "decode_tiles_kernel"
+        if meta.chain.inner_crc32c and os.environ.get("ZH_DEC_CRCW", "3") == "3":
+            return "tiles_rowcrc_kernel"
+        return "tiles_group_kernel"
     # row chains with 128-B rows and no chunk CRC: the lane-exchange kernel (ZH_DEC_RGROUP=8)
     c = meta.chain
     rg = os.environ.get("ZH_DEC_RGROUP")

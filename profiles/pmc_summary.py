@@ -23,12 +23,14 @@ def kernel_rows(path, match):
 
 
 FAST = ("decode_rows_kernel", "decode_tiles_kernel", "tiles_group_kernel", "rows_group_kernel",
-        "rows_xpose_kernel")
+        "rows_xpose_kernel", "tiles_rowcrc_kernel", "tiles_crcw_kernel")
+DECODE_ONLY = ("tiles_rowcrc_kernel", "tiles_crcw_kernel")  # last template argument is not FLAGS
 
 
 def main(src, config, out):
     def encode_view(n):  # the bench's setup encode runs the fast kernels with FLAGS = true
-        return any(k in n for k in FAST) and n.split(">")[0].split(",")[-1].strip() == "true"
+        return any(k in n for k in FAST) and not any(k in n for k in DECODE_ONLY) and \
+            n.split(">")[0].split(",")[-1].strip() == "true"
 
     def decode(n):  # every decode kernel of one step: fast rows/tiles + the generic list
         return any(k in n for k in FAST + ("decode_slow_kernel",)) and not encode_view(n)

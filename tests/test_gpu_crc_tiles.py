@@ -64,6 +64,23 @@ def test_chunk_crc32c_fused_tile_kernel(dev, monkeypatch, order, piece_kb, fuse)
     _corrupt_matches_oracle(dev, meta, shards, 0, 70000)  # first stored chunk: a fast item
 
 
+@pytest.mark.parametrize("order", [[0, 2, 1], [2, 0, 1], [2, 1, 0]])
+def test_row_crc_tile_kernel_is_the_default(dev, monkeypatch, order):
+    """Without switches a whole-chunk [transpose, bytes(big), crc32c] read runs
+    tiles_rowcrc_kernel at G = 1 (variant 51) and matches the oracle; a flipped payload byte
+    in the middle of a chunk is reported with the oracle's message."""
+    for k in ("ZH_DEC_CRCW", "ZH_DEC_TGROUP", "ZH_DEC_TPF"):
+        monkeypatch.delenv(k, raising=False)
+    monkeypatch.setenv("ZH_SMALL_SPLIT", "0")
+    meta = _meta(order)
+    arr = rand_array(SHAPE, 4, seed=57)
+    shards = encode_oracle(meta, arr)
+    got, want = _read_both(dev, meta, shards, [0, 0, 0], SHAPE)
+    np.testing.assert_array_equal(got, want)
+    assert _variant() == 51
+    _corrupt_matches_oracle(dev, meta, shards, 0, CHUNK + 65536 + 77)
+
+
 @pytest.mark.parametrize("variant", ["0", "1"])
 @pytest.mark.parametrize("perm", ["0", "1"])
 def test_tile_crc_variants_and_item_order(dev, monkeypatch, variant, perm):
@@ -94,6 +111,7 @@ def test_grouped_tile_decode(dev, monkeypatch, order, group, pf, crc):
     chunk, a missing shard, a clipped region; a corrupt byte of a fast chunk is caught."""
     monkeypatch.setenv("ZH_DEC_TGROUP", group)
     monkeypatch.setenv("ZH_DEC_TPF", pf)
+    monkeypatch.setenv("ZH_DEC_CRCW", "0")  # the fused grouped kernel (not the row-CRC default)
     monkeypatch.setenv("ZH_SMALL_SPLIT", "0")  # whole chunks: the grouped kernels need them
     meta = A.make_meta(SHAPE, [32, 64, 64], 4, endian=A.ZH_ENDIAN_BIG, sharded=True,
                        inner_chunk_shape=[32, 32, 32], transpose_order=order, inner_crc32c=crc)

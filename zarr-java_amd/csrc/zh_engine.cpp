@@ -1217,9 +1217,16 @@ int zh_plan_create(zh_ctx* ctx, const zh_array_meta* m, const zh_chunk_src* chun
   // without the prefetch): c4 33.4 → 32.9 ms (G = 4), c4crc 39.5 → 38.3 ms (G = 2), interleaved
   // A/B in profiles/r02/experiments/ab_r02abdtgpf*.txt.  ZH_DEC_TGROUP = G (0: the
   // row-interleaved tile kernel; 1, 2, 4, 8, with the chunk CRC 1, 2, 4), ZH_DEC_TPF = 0/1.
+  //
+  // With the fused chunk CRC the default is tiles_rowcrc_kernel at G = 1 (ZH_DEC_CRCW=3: every
+  // lane also CRCs one payload row from the LDS tiles, 16 lookups per 16-B vector): c4crc
+  // 38.27 → 36.92 ms, interleaved A/B in profiles/r02/crc/ab_rowcrc.json (G = 2 37.16, the
+  // CRC-wave kernel 39.6, ZH_DEC_CRCW=0 restores the fused grouped kernel at G = 2).
   {
     const bool crc = p->args.crc_fused != 0;
-    const int G = env_int("ZH_DEC_TGROUP", crc ? 2 : 4);
+    const int crcw = crc ? env_int("ZH_DEC_CRCW", 3) : 0;
+    const bool rowcrc_ok = crcw != 3 || zh::rowcrc_lds_at_zero();
+    const int G = env_int("ZH_DEC_TGROUP", crc ? (crcw == 3 && rowcrc_ok ? 1 : 2) : 4);
     if ((G == 1 || G == 2 || G == 4 || (G == 8 && !crc)) && p->tile_mode &&
         p->args.fast_mode == kFastTileTable && p->args.tile_variant == 1 &&
         (!crc || tile_crc) && p->args.piece_shift == 0 && (p->args.nt & 3) == 3 && items > 0) {
@@ -1228,8 +1235,7 @@ int zh_plan_create(zh_ctx* ctx, const zh_array_meta* m, const zh_chunk_src* chun
       // the chunk CRC on waves of its own (tiles_crcw_kernel: 8-wave blocks, 4 move, 4 CRC)
       // (1: the movers prefetch, 2: they do not); 3: every lane moves tiles and takes one LDS
       // payload row for the CRC (tiles_rowcrc_kernel)
-      const int crcw = env_int("ZH_DEC_CRCW", 0);
-      if (crc && G <= 4 && crcw >= 1 && crcw <= 3 && (crcw != 3 || zh::rowcrc_lds_at_zero()))
+      if (crc && G <= 4 && crcw >= 1 && crcw <= 3 && rowcrc_ok)
         p->args.tile_variant = 30 + G + 10 * (crcw - 1);
       if (crc) p->args.crc_tile_step = tile_crc_step(ends, (size_t)(8 / G));
       p->args.item_mul = env_int("ZH_ITEM_PERM", 1) ? golden_item_mul(groups) : 0;
