@@ -32,7 +32,7 @@ def _read_both(dev, meta, shards, off, shp):
 
 def _variant():
     """Kernel variant of the last decode scatter launch (zh_debug_last_fast_path)."""
-    return (lib().zh_debug_last_fast_path() // 1000) % 1000
+    return (lib().zh_debug_last_fast_path(0) // 1000) % 1000
 
 
 def _corrupt_matches_oracle(dev, meta, shards, k, pos):

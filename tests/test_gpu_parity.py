@@ -11,7 +11,7 @@ import oracle as O
 from helpers import (chunk_coords, device_read, device_write, encode_oracle, load_reference_fixture,
                      rand_array, shape_of)
 from zarrhip import _abi as A
-from zarrhip._lib import ZhError
+from zarrhip._lib import lib, ZhError
 
 pytestmark = pytest.mark.gpu
 
@@ -549,14 +549,16 @@ def test_lane_exchange_row_decode(dev, monkeypatch, dsize, inner_rows, crc):
 
 
 @pytest.mark.parametrize("order", [[0, 3, 2, 1], [0, 1, 3, 2]])
-@pytest.mark.parametrize("group", ["-1", "0", "1", "4"])
-def test_tile_encode_chunk_crc_fused(dev, monkeypatch, order, group):
+@pytest.mark.parametrize("group,rowcrc", [("-1", "0"), ("0", "0"), ("1", "0"), ("4", "0"),
+                                          ("1", "1"), ("2", "1"), ("4", "1")])
+def test_tile_encode_chunk_crc_fused(dev, monkeypatch, order, group, rowcrc):
     """c4crc-shaped chain at small extent: [transpose, bytes(big), crc32c] with 32x32 tiles,
     the chunk CRC fused into the tile encode (stored vectors, per-unit end shifts from the
     payload side of the table), boundary chunks through the slow list + CRC pass; equals the
     oracle and the unfused pass, and decodes back.  ZH_ENC_TGROUP: the grouped tile encode
     (the unit fold step for 8/G units), or the ungrouped kernel (0)."""
     monkeypatch.setenv("ZH_ENC_TGROUP", group)
+    monkeypatch.setenv("ZH_ENC_ROWCRC", rowcrc)  # 1: tiles_rowcrc_kernel on the encode view
     shape = [1, 64, 80, 96]
     meta = A.make_meta(shape, [1, 64, 64, 64], 4, endian=A.ZH_ENDIAN_BIG, sharded=True,
                        inner_chunk_shape=[1, 32, 32, 32], transpose_order=order,
@@ -565,6 +567,8 @@ def test_tile_encode_chunk_crc_fused(dev, monkeypatch, order, group):
     arr[arr == 0] = 1
     want = encode_oracle(meta, arr)
     assert device_write(dev, meta, arr) == want
+    if rowcrc == "1":  # the encode view ran the row-CRC kernel (kernel form 30) at group G
+        assert lib().zh_debug_last_fast_path(1) % 1000000 == int(group) * 1000 + 30
     monkeypatch.setenv("ZH_CRC_FUSE", "0")
     assert device_write(dev, meta, arr) == want
     monkeypatch.delenv("ZH_CRC_FUSE")

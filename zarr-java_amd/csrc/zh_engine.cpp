@@ -1442,7 +1442,9 @@ int zh_plan_stats(const zh_plan* p, int64_t* in_bytes, int64_t* out_bytes, int64
   return ZH_OK;
 }
 
-int64_t zh_debug_last_fast_path(void) { return zh::g_last_fast_path.load(); }
+int64_t zh_debug_last_fast_path(int encode) {
+  return encode ? zh::g_last_encode_path.load() : zh::g_last_fast_path.load();
+}
 
 int64_t zh_plan_staged_bytes(const zh_plan* p) {
   if (!p) return -1;
@@ -2391,7 +2393,12 @@ static int array_write_fast(zh_ctx* ctx, const zh_array_meta* m, ScatterArgs a,
     v.item_mul = env_int("ZH_ITEM_PERM", 1) ? golden_item_mul((items + 7) / 8) : 0;
   }
   const int grid = grid_for(ctx, group ? (items + group - 1) / group : pitems);
+  // tile groups with the chunk CRC: ZH_ENC_ROWCRC=1 selects the row-CRC encode (deep = 30;
+  // tiles_rowcrc_kernel<…, ENC>: every lane also CRCs one stored payload row from the tiles)
+  const bool enc_rowcrc = v.fast_mode == kFastTileTable && group && crc_fuse && tile_crc &&
+                          env_int("ZH_ENC_ROWCRC", 0) != 0 && zh::rowcrc_lds_at_zero();
   const int deep = xpose ? 20
+                   : enc_rowcrc ? 30
                    : v.fast_mode == kFastTileTable && group ? (env_int("ZH_ENC_TPF", 0) ? 9 : 1)
                    : group ? (gu <= 2 ? 0 : gu <= 4 ? 1 : 2)
                            : env_int("ZH_ENC_DEEP", 1);

@@ -206,6 +206,7 @@ hipError_t launch_data_crc(const DataCrcArgs& a, int grid, hipStream_t stream);
 hipError_t launch_data_crc_partial(const DataCrcArgs& a, int grid, hipStream_t stream);
 hipError_t launch_data_crc_finalize(const DataCrcArgs& a, hipStream_t stream);
 extern std::atomic<int64_t> g_last_fast_path;  // diagnostic, zh_debug_last_fast_path
+extern std::atomic<int64_t> g_last_encode_path;
 bool rowcrc_lds_at_zero();  // tiles_rowcrc_kernel has no static LDS
 hipError_t launch_scatter(const ScatterArgs& a, int dsize, int tile_mode, int encode, int grid,
                           hipStream_t stream);

@@ -1163,6 +1163,55 @@ __global__ __launch_bounds__(kBlock) void decode_rows_kernel(ScatterArgs a) {
   }
 }
 
+// 4·(byte SEL of w) in one SDWA shift: the LDS byte offset of a 4-B table entry
+template <int SEL>
+__device__ __forceinline__ uint32_t byte_x4(uint32_t w) {
+  uint32_t r;
+  if constexpr (SEL == 0)
+    asm("v_lshlrev_b32_sdwa %0, 2, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_0" : "=v"(r) : "v"(w));
+  else if constexpr (SEL == 1)
+    asm("v_lshlrev_b32_sdwa %0, 2, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_1" : "=v"(r) : "v"(w));
+  else if constexpr (SEL == 2)
+    asm("v_lshlrev_b32_sdwa %0, 2, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_2" : "=v"(r) : "v"(w));
+  else
+    asm("v_lshlrev_b32_sdwa %0, 2, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_3" : "=v"(r) : "v"(w));
+  return r;
+}
+
+// a ^ b ^ c in one VALU op (v_bitop3_b32, truth table 0x96)
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+  uint32_t r;
+  asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
+
+// Table lookups at a byte offset (4·index) from tables whose LDS position is a compile-time
+// constant (the dynamic block's start plus a constant): base and table offsets fold into the
+// ds_read immediate, so a lookup costs one SDWA op and the read.
+__device__ __forceinline__ uint32_t tlook(const uint32_t (*T)[256], int k, uint32_t off4) {
+  return *reinterpret_cast<const uint32_t*>(reinterpret_cast<const uint8_t*>(T[k]) + off4);
+}
+
+// crc_upd16 / crc_shift_tab for tables at a constant LDS position (slicing-by-8 in two
+// dependent halves; three-input XOR trees)
+__device__ __forceinline__ uint32_t crc_upd8_k(uint32_t c, uint32_t w0, uint32_t w1,
+                                               const uint32_t (*T)[256]) {
+  const uint32_t lo = w0 ^ c, hi = w1;
+  const uint32_t a0 = xor3(tlook(T, 7, byte_x4<0>(lo)), tlook(T, 6, byte_x4<1>(lo)),
+                           tlook(T, 5, byte_x4<2>(lo)));
+  const uint32_t a1 = xor3(tlook(T, 4, byte_x4<3>(lo)), tlook(T, 3, byte_x4<0>(hi)),
+                           tlook(T, 2, byte_x4<1>(hi)));
+  const uint32_t a2 = tlook(T, 1, byte_x4<2>(hi)) ^ tlook(T, 0, byte_x4<3>(hi));
+  return xor3(a0, a1, a2);
+}
+__device__ __forceinline__ uint32_t crc_upd16_k(uint32_t c, v4u v, const uint32_t (*T)[256]) {
+  return crc_upd8_k(crc_upd8_k(c, v.x, v.y, T), v.z, v.w, T);
+}
+__device__ __forceinline__ uint32_t crc_shift_k(uint32_t c, const uint32_t (*S)[256]) {
+  return xor3(tlook(S, 0, byte_x4<0>(c)), tlook(S, 1, byte_x4<1>(c)), tlook(S, 2, byte_x4<2>(c))) ^
+         tlook(S, 3, byte_x4<3>(c));
+}
+
 // encode, grouped row kernel (write path, narrow rows): a work item is G consecutive inner
 // chunks — z-adjacent in the region when they sit in one shard row — and lane group q of
 // every G·vpr lanes moves chunk q.  A wave load then covers G·(row bytes) of one region row
@@ -1183,7 +1232,8 @@ __global__ __launch_bounds__(kBlock) void decode_rows_kernel(ScatterArgs a) {
 template <int DS, int G, int U, int NT, bool CRC, bool FLAGS>
 __global__ __launch_bounds__(kBlock) void rows_group_kernel(ScatterArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-  uint2* tab = reinterpret_cast<uint2*>(smem);
+  // CRC: the tables first (a constant LDS position: crc_upd16_k / crc_shift_k), then the rows
+  uint2* tab = reinterpret_cast<uint2*>(smem + (CRC ? 12 * 256 * 4 : 0));
   for (int i = threadIdx.x; i < a.fast_n; i += kBlock)
     tab[i] = reinterpret_cast<const uint2*>(a.fast_tab)[i];
   const int vs = a.fast_vpr_shift;
@@ -1196,7 +1246,7 @@ __global__ __launch_bounds__(kBlock) void rows_group_kernel(ScatterArgs a) {
   uint32_t(*S)[256] = nullptr;
   uint32_t kl = 0;
   if constexpr (CRC) {
-    T = reinterpret_cast<uint32_t(*)[256]>(smem + (((size_t)a.fast_n * 8 + 15) & ~(size_t)15));
+    T = reinterpret_cast<uint32_t(*)[256]>(smem);
     S = T + 8;
     init_crc_tables(T);
     constexpr uint32_t Lc = kBlock / G;
@@ -1264,7 +1314,7 @@ __global__ __launch_bounds__(kBlock) void rows_group_kernel(ScatterArgs a) {
           if constexpr (CRC) {  // the payload vector: stored (encode) or loaded (decode)
             const uint4 pv = FLAGS ? w : v[u];
             const v4u wv = {pv.x, pv.y, pv.z, pv.w};
-            if (!fill) acc = crc_shift_tab(acc, S) ^ crc_upd16(0u, wv, T);
+            if (!fill) acc = crc_shift_k(acc, S) ^ crc_upd16_k(0u, wv, T);
           }
         }
     }
@@ -1611,8 +1661,11 @@ __global__ __launch_bounds__(kBlock) void decode_tiles_kernel(ScatterArgs a) {
 template <int NT, int G, bool CRC, bool PF, bool FLAGS>
 __global__ __launch_bounds__(kBlock) void tiles_group_kernel(ScatterArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-  uint2* tab = reinterpret_cast<uint2*>(smem);
-  uint8_t* after_tab = smem + (((size_t)a.fast_n * 8 + 15) & ~(size_t)15);
+  // CRC: the tables first (T, S, SD: a constant LDS position for crc_upd16_k / crc_shift_k),
+  // then K, the unit table and the tiles
+  uint8_t* tab_at = CRC ? smem + ((16 * 256 * 4 + (size_t)a.fast_n * 4 + 15) & ~(size_t)15) : smem;
+  uint2* tab = reinterpret_cast<uint2*>(tab_at);
+  uint8_t* after_tab = tab_at + (((size_t)a.fast_n * 8 + 15) & ~(size_t)15);
   uint32_t* lds = reinterpret_cast<uint32_t*>(after_tab);
   for (int i = threadIdx.x; i < a.fast_n; i += kBlock)
     tab[i] = reinterpret_cast<const uint2*>(a.fast_tab)[i];
@@ -1626,7 +1679,7 @@ __global__ __launch_bounds__(kBlock) void tiles_group_kernel(ScatterArgs a) {
   uint32_t* K = nullptr;
   uint32_t kb = 0;
   if constexpr (CRC) {
-    T = reinterpret_cast<uint32_t(*)[256]>(after_tab + (size_t)kTG * kTilePitch * 4);
+    T = reinterpret_cast<uint32_t(*)[256]>(smem);
     S = T + 8;
     SD = S + 4;
     K = reinterpret_cast<uint32_t*>(SD + 4);
@@ -1715,21 +1768,21 @@ __global__ __launch_bounds__(kBlock) void tiles_group_kernel(ScatterArgs a) {
           st16s<(NT & 2) != 0>(base + (size_t)r * d_fs * 4, y);
           if constexpr (CRC && FLAGS) {  // encode: the stored vectors
             const v4u w = {y.x, y.y, y.z, y.w};
-            const uint32_t ck = crc_upd16(0u, w, T);
-            eacc = k ? crc_shift_tab(eacc, S) ^ ck : ck;
+            const uint32_t ck = crc_upd16_k(0u, w, T);
+            eacc = k ? crc_shift_k(eacc, S) ^ ck : ck;
           }
         }
         if constexpr (CRC && !FLAGS) {  // decode: the loaded payload vectors, stores in flight
 #pragma unroll
           for (int k = 0; k < 8; k++) {
             const v4u w = {xc[k].x, xc[k].y, xc[k].z, xc[k].w};
-            const uint32_t ck = crc_upd16(0u, w, T);
-            eacc = k ? crc_shift_tab(eacc, S) ^ ck : ck;
+            const uint32_t ck = crc_upd16_k(0u, w, T);
+            eacc = k ? crc_shift_k(eacc, S) ^ ck : ck;
           }
         }
         if constexpr (CRC) {
           if (regular) {
-            run = (ulast == ~0u ? 0u : crc_shift_tab(run, SD)) ^ eacc;
+            run = (ulast == ~0u ? 0u : crc_shift_k(run, SD)) ^ eacc;
             ulast = u;
           } else {
             share ^= multmodp(K[u], eacc);
@@ -1899,32 +1952,10 @@ void tiles_crcw_kernel(ScatterArgs a) {
   }
 }
 
-// 4·(byte SEL of w) in one SDWA shift: the LDS byte offset of a 4-B table entry
-template <int SEL>
-__device__ __forceinline__ uint32_t byte_x4(uint32_t w) {
-  uint32_t r;
-  if constexpr (SEL == 0)
-    asm("v_lshlrev_b32_sdwa %0, 2, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_0" : "=v"(r) : "v"(w));
-  else if constexpr (SEL == 1)
-    asm("v_lshlrev_b32_sdwa %0, 2, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_1" : "=v"(r) : "v"(w));
-  else if constexpr (SEL == 2)
-    asm("v_lshlrev_b32_sdwa %0, 2, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_2" : "=v"(r) : "v"(w));
-  else
-    asm("v_lshlrev_b32_sdwa %0, 2, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_3" : "=v"(r) : "v"(w));
-  return r;
-}
-
 // a dword of LDS at a byte address known relative to LDS offset 0 (constant parts fold into
 // the ds_read immediate)
 __device__ __forceinline__ uint32_t lds_word(uint32_t byte_addr) {
   return *reinterpret_cast<const __attribute__((address_space(3))) uint32_t*>((size_t)byte_addr);
-}
-
-// a ^ b ^ c in one VALU op (v_bitop3_b32, truth table 0x96)
-__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
-  uint32_t r;
-  asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(r) : "v"(a), "v"(b), "v"(c));
-  return r;
 }
 
 // Slicing-by-8 step over the 8 raw payload bytes held by the words w0, w1 as they sit in the LDS
@@ -1956,7 +1987,12 @@ __device__ __forceinline__ uint32_t crc_upd8_lds(uint32_t c, uint32_t w0, uint32
 // the group; the CRC role reads its chunk's descriptor.  Shares as in tiles_crcw_kernel.
 // SWAP (= a.swap, bytes(big) on uint32) is a template argument: the byte swap of the movers and
 // the CRC's byte order cost no select per word.  LDS: T, S (unused), SD, K, table, tiles.
-template <int G, bool SWAP>
+// ENC: the encode view (source = region rows, destination = payloads; the write path's
+// tiles_group_kernel<…, CRC, FLAGS> role): the movers load inside the live branch (no prefetch,
+// as the fused tile encode), test every loaded vector against fill_value (one flag byte per
+// chunk), and the LDS tiles then hold payload words, so payload row r of a tile is LDS column r
+// (banks (33·j + r) mod 32: distinct over a 32-lane half) and needs no swap back.
+template <int G, bool SWAP, bool ENC = false>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3)))
 void tiles_rowcrc_kernel(ScatterArgs a) {
   static_assert(G == 1 || G == 2 || G == 4, "a wave's CRC rows must belong to one chunk");
@@ -1970,8 +2006,9 @@ void tiles_rowcrc_kernel(ScatterArgs a) {
       reinterpret_cast<uint8_t*>(tab) + (((size_t)a.fast_n * 8 + 15) & ~(size_t)15));
   const int tid = threadIdx.x;
   for (int i = tid; i < a.fast_n; i += kBlock) tab[i] = reinterpret_cast<const uint2*>(a.fast_tab)[i];
+  constexpr bool CSW = SWAP && !ENC;  // the CRC reads byte-swapped words (decode, big endian)
 #pragma unroll
-  for (int k = 0; k < 8; k++) T[k][tid] = SWAP ? __builtin_bswap32(g_crc.T[k][tid]) : g_crc.T[k][tid];
+  for (int k = 0; k < 8; k++) T[k][tid] = CSW ? __builtin_bswap32(g_crc.T[k][tid]) : g_crc.T[k][tid];
 #pragma unroll
   for (int b = 0; b < 4; b++)
     SD[b][tid] = a.crc_tile_step ? multmodp(a.crc_tile_step, (uint32_t)tid << (8 * b)) : 0u;
@@ -1985,9 +2022,13 @@ void tiles_rowcrc_kernel(ScatterArgs a) {
   const bool regular = a.crc_tile_step != 0;
   const uint32_t units = (uint32_t)a.fast_n;
   const int64_t ngroups = (a.n_citems + G - 1) / G;
-  const uint32_t kr = x2nmodp((uint64_t)(31 - r) * 4 * (uint64_t)s_fd, 3);
+  // payload row pitch: the loaded rows (decode) or the stored rows (encode view)
+  const uint32_t kr = x2nmodp((uint64_t)(31 - r) * 4 * (uint64_t)(ENC ? d_fs : s_fd), 3);
   uint32_t* mine = lds + t * kTilePitch;
-  const uint32_t* crow = lds + tc * kTilePitch + r * 33;
+  const uint32_t* crow = lds + tc * kTilePitch + (ENC ? r : r * 33);
+  const uint64_t qmask = (TG * 8 == 64 ? ~0ull : ((1ull << (TG * 8)) - 1)) << (q * TG * 8);
+  const bool leader = lane == q * TG * 8;
+  const uint32_t fillv = (uint32_t)a.fill;
   auto sw = [](uint32_t x) { return SWAP ? __builtin_bswap32(x) : x; };
   for (int64_t gi = blockIdx.x; gi < ngroups; gi += gridDim.x) {
     const int64_t pg = a.item_mul ? (int64_t)(((uint64_t)gi * a.item_mul) % (uint64_t)ngroups) : gi;
@@ -2014,6 +2055,7 @@ void tiles_rowcrc_kernel(ScatterArgs a) {
       if ((f[0] | f[1] | f[2] | f[3]) == 0) continue;
     }
     uint32_t share = 0, run = 0, ulast = ~0u;
+    bool differs = false;
     uint4 x[8];
     auto load = [&](uint32_t ub_) {
       const uint32_t uu = ub_ + ti;
@@ -2023,14 +2065,17 @@ void tiles_rowcrc_kernel(ScatterArgs a) {
         for (int k = 0; k < 8; k++) x[k] = ld16s<true>(base + (size_t)(wave * 8 + k) * s_fd * 4);
       }
     };
-    load(0);
+    if (!ENC) load(0);
 #pragma unroll 1
     for (uint32_t ub = 0; ub < units; ub += TG) {
       const uint32_t u = ub + ti, uc = ub + tic;
       const bool live = on && u < units, livec = onc && uc < units;
       if (live) {
+        if (ENC) load(ub);
 #pragma unroll
         for (int k = 0; k < 8; k++) {
+          if (ENC)
+            differs |= (x[k].x != fillv) | (x[k].y != fillv) | (x[k].z != fillv) | (x[k].w != fillv);
           uint32_t* row = mine + (wave * 8 + k) * 33 + g * 4;
           row[0] = sw(x[k].x);
           row[1] = sw(x[k].y);
@@ -2039,7 +2084,7 @@ void tiles_rowcrc_kernel(ScatterArgs a) {
         }
       }
       __syncthreads();
-      if (ub + TG < units) load(ub + TG);
+      if (!ENC && ub + TG < units) load(ub + TG);
       if (live) {
         uint8_t* base = dst + ((size_t)tab[u].y + g * 4) * 4;
 #pragma unroll
@@ -2056,14 +2101,14 @@ void tiles_rowcrc_kernel(ScatterArgs a) {
       uint32_t w[32];
       if (livec) {
 #pragma unroll
-        for (int j = 0; j < 32; j++) w[j] = crow[j];
+        for (int j = 0; j < 32; j++) w[j] = crow[ENC ? j * 33 : j];
       }
       __syncthreads();
       if (livec) {
-        uint32_t acc = 0;  // byte-swapped with SWAP
+        uint32_t acc = 0;  // byte-swapped with CSW
 #pragma unroll
-        for (int j = 0; j < 32; j += 2) acc = crc_upd8_lds<SWAP>(acc, w[j], w[j + 1]);
-        if (SWAP) acc = __builtin_bswap32(acc);
+        for (int j = 0; j < 32; j += 2) acc = crc_upd8_lds<CSW>(acc, w[j], w[j + 1]);
+        if (CSW) acc = __builtin_bswap32(acc);
         if (regular) {
           run = (ulast == ~0u ? 0u : crc_shift_tab(run, SD)) ^ acc;
           ulast = uc;
@@ -2072,6 +2117,7 @@ void tiles_rowcrc_kernel(ScatterArgs a) {
         }
       }
     }
+    if (ENC && (__ballot(differs) & qmask) != 0 && leader && on) a.flags[c] = 1;
     if (regular && ulast != ~0u) share = multmodp(K[ulast], run);
     uint32_t cr = multmodp(kr, share);
 #pragma unroll
@@ -2900,7 +2946,7 @@ static void launch_scatter_ds(const ScatterArgs& a, int tile, int enc, int grid,
           }
         }
         if (v > 20 && a.crc_fused) {  // prefetching form (ZH_DEC_TPF=1)
-          const size_t lc = lds + 16 * 256 * 4 + (size_t)a.fast_n * 4;
+          const size_t lc = lds + 16 * 256 * 4 + (size_t)a.fast_n * 4 + 64;  // + alignment
           switch (v - 20) {
             case 1: hipLaunchKernelGGL((tiles_group_kernel<3, 1, true, true, false>), dim3(grid), dim3(kBlock), lc, s, a); return;
             case 2: hipLaunchKernelGGL((tiles_group_kernel<3, 2, true, true, false>), dim3(grid), dim3(kBlock), lc, s, a); return;
@@ -2919,7 +2965,7 @@ static void launch_scatter_ds(const ScatterArgs& a, int tile, int enc, int grid,
           }
         }
         if (v > 10 && a.crc_fused) {  // + the chunk CRC (host: unit step for 8/G units)
-          const size_t lc = lds + 16 * 256 * 4 + (size_t)a.fast_n * 4;
+          const size_t lc = lds + 16 * 256 * 4 + (size_t)a.fast_n * 4 + 64;  // + alignment
           switch (v - 10) {
             case 1: hipLaunchKernelGGL((tiles_group_kernel<3, 1, true, false, false>), dim3(grid), dim3(kBlock), lc, s, a); return;
             case 2: hipLaunchKernelGGL((tiles_group_kernel<3, 2, true, false, false>), dim3(grid), dim3(kBlock), lc, s, a); return;
@@ -2994,7 +3040,10 @@ bool rowcrc_lds_at_zero() {
   static const bool ok = [] {
     const void* fns[] = {(const void*)tiles_rowcrc_kernel<1, false>, (const void*)tiles_rowcrc_kernel<1, true>,
                          (const void*)tiles_rowcrc_kernel<2, false>, (const void*)tiles_rowcrc_kernel<2, true>,
-                         (const void*)tiles_rowcrc_kernel<4, false>, (const void*)tiles_rowcrc_kernel<4, true>};
+                         (const void*)tiles_rowcrc_kernel<4, false>, (const void*)tiles_rowcrc_kernel<4, true>,
+                         (const void*)tiles_rowcrc_kernel<1, false, true>, (const void*)tiles_rowcrc_kernel<1, true, true>,
+                         (const void*)tiles_rowcrc_kernel<2, false, true>, (const void*)tiles_rowcrc_kernel<2, true, true>,
+                         (const void*)tiles_rowcrc_kernel<4, false, true>, (const void*)tiles_rowcrc_kernel<4, true, true>};
     for (const void* f : fns) {
       hipFuncAttributes at;
       if (hipFuncGetAttributes(&at, f) != hipSuccess || at.sharedSizeBytes != 0) return false;
@@ -3006,6 +3055,8 @@ bool rowcrc_lds_at_zero() {
 
 // the fast-path selection of the last decode scatter launch (diagnostic: zh_debug_last_fast_path)
 std::atomic<int64_t> g_last_fast_path{-1};
+// the encode view's fast-path selection of the last write: fast_mode·10⁶ + group·10³ + deep
+std::atomic<int64_t> g_last_encode_path{-1};
 
 hipError_t launch_scatter(const ScatterArgs& a, int dsize, int tile_mode, int encode, int grid,
                           hipStream_t stream) {
@@ -3088,8 +3139,20 @@ static bool launch_encode_fast_ds(const ScatterArgs& v, int grid, int deep, int 
   if (v.fast_mode == kFastTileTable) {
     if constexpr (DS == 4) {
       const size_t l = lds + (size_t)kTG * kTilePitch * 4;
+      if (group > 0 && v.crc_fused && v.nt == 3 && deep == 30) {  // row-CRC encode (ZH_ENC_ROWCRC)
+        const size_t lc = l + 16 * 256 * 4 + (size_t)v.fast_n * 4 + 64;
+#define ZH_RC(G) if (v.swap) hipLaunchKernelGGL((tiles_rowcrc_kernel<G, true, true>), dim3(grid), dim3(kBlock), lc, s, v); \
+                 else hipLaunchKernelGGL((tiles_rowcrc_kernel<G, false, true>), dim3(grid), dim3(kBlock), lc, s, v); return true
+        switch (group) {
+          case 1: ZH_RC(1);
+          case 2: ZH_RC(2);
+          case 4: ZH_RC(4);
+          default: break;
+        }
+#undef ZH_RC
+      }
       if (group > 0 && v.crc_fused && v.nt == 3) {  // host: crc_tile_step for 8/G units
-        const size_t lc = l + 16 * 256 * 4 + (size_t)v.fast_n * 4;
+        const size_t lc = l + 16 * 256 * 4 + (size_t)v.fast_n * 4 + 64;  // + alignment
         switch (group) {
           case 1: hipLaunchKernelGGL((tiles_group_kernel<3, 1, true, false, true>), dim3(grid), dim3(kBlock), lc, s, v); return true;
           case 2: hipLaunchKernelGGL((tiles_group_kernel<3, 2, true, false, true>), dim3(grid), dim3(kBlock), lc, s, v); return true;
@@ -3106,7 +3169,7 @@ static bool launch_encode_fast_ds(const ScatterArgs& v, int grid, int deep, int 
         }
       }
       if (group > 0 && v.crc_fused && v.nt == 3 && deep == 9) {
-        const size_t lc = l + 16 * 256 * 4 + (size_t)v.fast_n * 4;
+        const size_t lc = l + 16 * 256 * 4 + (size_t)v.fast_n * 4 + 64;  // + alignment
         switch (group) {
           case 1: hipLaunchKernelGGL((tiles_group_kernel<3, 1, true, true, true>), dim3(grid), dim3(kBlock), lc, s, v); return true;
           case 2: hipLaunchKernelGGL((tiles_group_kernel<3, 2, true, true, true>), dim3(grid), dim3(kBlock), lc, s, v); return true;
@@ -3176,6 +3239,7 @@ static bool launch_encode_fast_ds(const ScatterArgs& v, int grid, int deep, int 
 hipError_t launch_encode_fast(const ScatterArgs& view, int grid, int deep, int group,
                               hipStream_t stream) {
   if (view.total_items == 0 || view.fast_mode == kFastNone) return hipSuccess;
+  g_last_encode_path.store((int64_t)view.fast_mode * 1000000 + (int64_t)group * 1000 + deep);
   bool ok = false;
   switch (view.dsize) {
     case 1: ok = launch_encode_fast_ds<1>(view, grid, deep, group, stream); break;

@@ -92,7 +92,7 @@ _SIGS = {
     "zh_event_elapsed_ms": (C.c_int, [P, P, P, C.POINTER(C.c_float)]),
     "zh_device_info": (C.c_int, [P, CH, SZ, PI64, C.POINTER(C.c_int), CH, SZ]),
     "zh_gather_blocks": (C.c_int, [P, P, P, I64, PI64, I64]),
-    "zh_debug_last_fast_path": (I64, []),
+    "zh_debug_last_fast_path": (I64, [C.c_int]),
     "zh_synth_fill": (C.c_int, [P, P, I64, C.c_int, I64, U64, P]),
     "zh_synth_verify": (C.c_int, [P, P, C.c_int, PI64, PI64, PI64, C.c_int, U64,
                                   C.POINTER(U64), P]),
