@@ -547,7 +547,11 @@ void fill_common_args(const zh_array_meta* m, const int64_t* region_shape, bool 
   }
   tile_mode = a.fs != a.fd;
   a.tile = tile_mode;
-  const int64_t piece_kb = std::max(1, env_int("ZH_PIECE_KB", 128));
+  // Work-item size along a large inner chunk: 2 MiB pieces (c2's 4 GiB chunks: decode 33.5 →
+  // 32.65 ms against 128 KiB, 512 KiB 32.77, 4 MiB 32.90, 8 MiB 33.05; encode view 40.66 →
+  // 39.38 ms; interleaved A/B, profiles/r02/experiments/ab_c2_piece*.json).  Chunks of at most
+  // 2 MiB (c3, c4: 128 KiB) are one piece either way.
+  const int64_t piece_kb = std::max(1, env_int("ZH_PIECE_KB", 2048));
   const uint64_t pieces = (uint64_t)((a.inner_nbytes + piece_kb * 1024 - 1) / (piece_kb * 1024));
   a.piece_shift = (int32_t)next_pow2_shift(std::max<uint64_t>(1, pieces));
 }
