@@ -1061,7 +1061,8 @@ def store_inclusive(dev, A, shard_slab, offs, sizes, coords, scratch):
             del got
         res["path"] = ("zarrhip.Array.read (Python mirror of core.Array.read) from a "
                        f"FilesystemStore on {d}: store reads + host index check + one "
-                       "zh_array_read (pageable H2D, decode, D2H into numpy)")
+                       "zh_array_read (H2D from the staging pool, page-locked once a buffer is reused; "
+                       "decode; D2H into a fresh numpy array)")
     finally:
         shutil.rmtree(base, ignore_errors=True)
     return res

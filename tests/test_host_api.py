@@ -231,3 +231,60 @@ def test_staging_pool_reuses_buffers():
     assert sum(x.nbytes for x in pool._free) <= 10 << 20
     pool.release()
     assert pool._free == []
+
+
+def test_staging_pool_page_locks_large_buffers():
+    """Buffers of at least pin_min bytes are page-aligned and registered through the pool's
+    context when handed out a second time (a one-off buffer never pays for pinning); they are
+    unregistered when the cap evicts them and on release(); small buffers and a failing
+    registration stay pageable (no record, no unregister)."""
+    from zarrhip.array import StagingPool
+
+    class Ctx:
+        def __init__(self, fail=False):
+            self.fail, self.reg, self.unreg = fail, [], []
+
+        def host_register(self, ptr, n):
+            if self.fail:
+                raise RuntimeError("refused")
+            self.reg.append((ptr, n))
+
+        def host_unregister(self, ptr):
+            self.unreg.append(ptr)
+
+    ctx = Ctx()
+    pool = StagingPool(cap=6 << 20, pin=lambda: ctx, pin_min=1 << 20)
+    lease = []
+    small = pool.take(1000, lease)
+    big = pool.take(3 << 20, lease)
+    assert len(small) == 1000 and len(big) == 3 << 20 and big.ctypes.data % 4096 == 0
+    assert ctx.reg == []                 # first use: not pinned
+    pool.give(lease)
+    again = []
+    pool.take(2 << 20, again)            # second use of the 3 MiB buffer: pinned now
+    assert ctx.reg == [(big.ctypes.data, 3 << 20)]
+    pool.give(again)
+    assert pool.pinned_bytes() == 3 << 20
+    third = []
+    pool.take(2 << 20, third)            # already pinned: no second registration
+    pool.give(third)
+    assert len(ctx.reg) == 1
+    l1 = []
+    pool.take(1000, l1)                  # the small buffer again: below pin_min
+    pool.give(l1)
+    assert len(ctx.reg) == 1
+    more = []
+    pool.take(4 << 20, more)             # a new buffer; giving it back exceeds the cap
+    pool.give(more)
+    assert ctx.unreg in ([], [big.ctypes.data])
+    pool.release()
+    assert sorted(ctx.unreg) == sorted(p for p, _ in ctx.reg) and pool._free == []
+    bad = Ctx(fail=True)
+    pool2 = StagingPool(pin=lambda: bad, pin_min=1 << 20)
+    for _ in range(2):
+        l3 = []
+        pool2.take(2 << 20, l3)
+        pool2.give(l3)
+    assert pool2.pinned_bytes() == 0
+    pool2.release()
+    assert bad.unreg == []

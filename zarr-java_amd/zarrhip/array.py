@@ -11,6 +11,7 @@ chunk codec work done by the HIP path through the C-ABI (libzarrhip.so).
 Byte-to-byte compressors stay on the host (north star): their frames are decoded here and
 the raw chunk bytes are handed to the device.
 """
+import atexit
 import ctypes as C
 import json
 import os
@@ -74,13 +75,46 @@ class StagingPool:
     read fills it, and they are unmapped when it is dropped at the end of the read (a 2 GiB
     sub-shard read: 194 ms inside Array.read, 283 ms around it).  The reference's JVM heap
     keeps such memory; this pool does the same for the mirror.  Buffers are kept up to `cap`
-    bytes; `release()` returns them."""
-    ROUND = 64 << 20
+    bytes; `release()` returns them.
 
-    def __init__(self, cap=8 << 30):
+    Buffers of at least `pin_min` bytes are page-aligned, and page-locked (zh_host_register
+    through the process's DeviceContext, `pin`) when the pool hands one out a second time, so
+    repeated reads' H2D copies run as direct DMA instead of through the runtime's pageable
+    staging, while a one-off buffer (or one the cap keeps evicting) never pays for pinning
+    (≈40 ms per GiB).  Pinned buffers are unregistered before the pool lets go of them.
+    Without a usable device (CPU-only use, or a failing registration) they stay pageable."""
+    ROUND = 64 << 20
+    PAGE = 4096
+
+    def __init__(self, cap=8 << 30, pin=None, pin_min=64 << 20):
         self.cap = cap
+        self.pin = pin  # callable returning a DeviceContext, or None: pageable buffers
+        self.pin_min = pin_min
         self._free = []
+        self._pinned = {}  # id(buffer) -> (context, address)
         self._lock = threading.Lock()
+
+    def _alloc(self, size):
+        if self.pin is None or size < self.pin_min:
+            return np.empty(size, np.uint8)
+        raw = np.empty(size + self.PAGE, np.uint8)
+        a = (-raw.ctypes.data) % self.PAGE
+        return raw[a:a + size]  # page-aligned; keeps `raw` alive through .base
+
+    def _register(self, b):  # caller holds the lock
+        if self.pin is None or b.nbytes < self.pin_min or id(b) in self._pinned:
+            return
+        try:
+            ctx = self.pin()
+            ctx.host_register(b.ctypes.data, b.nbytes)
+            self._pinned[id(b)] = (ctx, b.ctypes.data)
+        except Exception:  # no device or registration refused: stays pageable
+            pass
+
+    def _drop(self, b):
+        rec = self._pinned.pop(id(b), None)
+        if rec is not None:
+            rec[0].host_unregister(rec[1])
 
     def take(self, n, lease):
         """A uint8 view of at least n bytes; its buffer is appended to `lease` (give back
@@ -88,9 +122,11 @@ class StagingPool:
         with self._lock:
             fit = [i for i, x in enumerate(self._free) if x.nbytes >= n]
             b = self._free.pop(min(fit, key=lambda i: self._free[i].nbytes)) if fit else None
+            if b is not None:
+                self._register(b)  # second use: worth page-locking
         if b is None:
-            b = np.empty(max(1, -(-n // self.ROUND) * self.ROUND) if n > self.ROUND else
-                         max(n, 1), np.uint8)
+            b = self._alloc(max(1, -(-n // self.ROUND) * self.ROUND) if n > self.ROUND else
+                            max(n, 1))
         lease.append(b)
         return b[:n]
 
@@ -99,15 +135,24 @@ class StagingPool:
             self._free.extend(lease)
             tot = sum(b.nbytes for b in self._free)
             while tot > self.cap and self._free:  # drop the oldest first
-                tot -= self._free.pop(0).nbytes
+                b = self._free.pop(0)
+                tot -= b.nbytes
+                self._drop(b)
         lease.clear()
+
+    def pinned_bytes(self):
+        with self._lock:
+            return sum(b.nbytes for b in self._free if id(b) in self._pinned)
 
     def release(self):
         with self._lock:
+            for b in self._free:
+                self._drop(b)
             self._free.clear()
 
 
-staging_pool = StagingPool()
+staging_pool = StagingPool(pin=lambda: devices()[0])
+atexit.register(staging_pool.release)  # unregister before the buffers' memory goes
 
 
 def _new_buf(n, lease=None):
