@@ -156,3 +156,34 @@ def test_crc_waves_tile_decode(dev, monkeypatch, order, group, endian, crcw):
     full = encode_oracle(meta, arr)  # shard 0: four in-bounds chunks of random data
     for pos in (3, CHUNK + 1000, 2 * CHUNK + 70001, CHUNK - 5):
         _corrupt_matches_oracle(dev, meta, full, 0, pos)
+
+
+def test_row_crc_tile_kernel_many_groups(dev, monkeypatch):
+    """The c4crc chain ([transpose [0,3,2,1], bytes(big), crc32c], 32³ uint32 inner chunks) at
+    64 MiB: 512 inner chunks over 8 shards, the golden-ratio group order and the default
+    row-CRC tile kernel; equals the oracle, and a flipped byte deep inside the last shard is
+    reported with the oracle's message."""
+    for k in ("ZH_DEC_CRCW", "ZH_DEC_TGROUP", "ZH_DEC_TPF", "ZH_SMALL_SPLIT"):
+        monkeypatch.delenv(k, raising=False)
+    shape = [1, 256, 256, 256]
+    meta = A.make_meta(shape, [1, 128, 128, 128], 4, endian=A.ZH_ENDIAN_BIG, sharded=True,
+                       inner_chunk_shape=[1, 32, 32, 32], transpose_order=[0, 3, 2, 1],
+                       inner_crc32c=True)
+    arr = rand_array(shape, 4, seed=59)
+    arr[arr == 0] = 1
+    shards = encode_oracle(meta, arr)
+    want = np.frombuffer(O.array_read(meta, shards, [0, 0, 0, 0], shape), np.uint32).reshape(shape)
+    got = device_read(dev, meta, shards, [0, 0, 0, 0], shape)
+    np.testing.assert_array_equal(got, want)
+    np.testing.assert_array_equal(got, arr)
+    assert _variant() == 51
+    bad = list(shards)
+    k = len(bad) - 1
+    b = bytearray(bad[k])
+    b[37 * CHUNK + 99999] ^= 0x01
+    bad[k] = bytes(b)
+    with pytest.raises(O.OracleError) as eo:
+        O.array_read(meta, bad, [0, 0, 0, 0], shape)
+    with pytest.raises(ZhError) as ed:
+        device_read(dev, meta, bad, [0, 0, 0, 0], shape)
+    assert str(ed.value) == str(eo.value)
