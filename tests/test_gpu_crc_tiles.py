@@ -187,3 +187,40 @@ def test_row_crc_tile_kernel_many_groups(dev, monkeypatch):
     with pytest.raises(ZhError) as ed:
         device_read(dev, meta, bad, [0, 0, 0, 0], shape)
     assert str(ed.value) == str(eo.value)
+
+
+@pytest.mark.parametrize("units,order", [(5, [0, 2, 1]), (3, [0, 2, 1]), (12, [0, 2, 1])])
+def test_row_crc_tile_kernel_unit_layouts(dev, monkeypatch, units, order):
+    """Row-CRC tile kernel over inner chunks of `units` 32x32 tiles: at most 8 units take the
+    per-unit K multiply (no regular fold step: crc_tile_step 0), 12 units the regular fold
+    over a partly filled last step.  Equals the oracle; a flipped byte in the last unit of a
+    chunk is caught with the oracle's message."""
+    for k in ("ZH_DEC_CRCW", "ZH_DEC_TGROUP", "ZH_DEC_TPF"):
+        monkeypatch.delenv(k, raising=False)
+    monkeypatch.setenv("ZH_SMALL_SPLIT", "0")
+    shape = [units * 2, 64, 96]
+    meta = A.make_meta(shape, [units * 2, 64, 64], 4, endian=A.ZH_ENDIAN_BIG, sharded=True,
+                       inner_chunk_shape=[units, 32, 32], transpose_order=order,
+                       inner_crc32c=True)
+    arr = rand_array(shape, 4, seed=61 + units)
+    arr[arr == 0] = 1
+    shards = encode_oracle(meta, arr)
+    got, want = _read_both_shape(dev, meta, shards, shape)
+    np.testing.assert_array_equal(got, want)
+    np.testing.assert_array_equal(got, arr)
+    assert _variant() == 51
+    chunk = units * 32 * 32 * 4 + 4
+    bad = list(shards)
+    b = bytearray(bad[0])
+    b[chunk + chunk - 4 - 700] ^= 0x40  # second chunk, inside its last unit
+    bad[0] = bytes(b)
+    with pytest.raises(O.OracleError) as eo:
+        O.array_read(meta, bad, [0, 0, 0], shape)
+    with pytest.raises(ZhError) as ed:
+        device_read(dev, meta, bad, [0, 0, 0], shape)
+    assert str(ed.value) == str(eo.value)
+
+
+def _read_both_shape(dev, meta, shards, shape):
+    want = np.frombuffer(O.array_read(meta, shards, [0, 0, 0], shape), np.uint32).reshape(shape)
+    return device_read(dev, meta, shards, [0, 0, 0], shape), want
