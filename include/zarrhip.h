@@ -12,6 +12,9 @@
  *   zh_plan_* (prepared read)   same, split into plan (host) + execute (device)
  *   zh_sharding_decode          ShardingIndexedCodec.decode(ByteBuffer)      M/v3/codec/core/ShardingIndexedCodec.java:98-103
  *   zh_sharding_decode_partial  ShardingIndexedCodec.decodePartial(...)      M/v3/codec/core/ShardingIndexedCodec.java:245-255
+ *   zh_shard_ranges             StoreHandleDataProvider reads of decodeInternal ShardingIndexedCodec.java:190-230, 333-357
+ *   zh_array_read_pieces        core.Array.read with sub-shard parts         M/core/Array.java:378-441 + the above
+ *   zh_sharding_decode_pieces   ShardingIndexedCodec.decodePartial(StoreHandle, ...) ShardingIndexedCodec.java:245-255
  *   zh_array_write              core.Array.write + writeChunk + ShardingIndexedCodec.encode
  *                                                                            M/core/Array.java:83-156, ShardingIndexedCodec.java:105-168
  *   zh_shard_index_size         ShardingIndexedCodec.getShardIndexSize       ShardingIndexedCodec.java:176-181
@@ -255,6 +258,83 @@ int zh_slab_partition(int ndim, const int64_t* offset, const int64_t* shape, int
                       int64_t align, int64_t* slab_off, int64_t* slab_shape);
 /* Number of visible HIP devices (0 when none). */
 int zh_device_count(void);
+
+/* ---- sub-shard reads from the index and the referenced pieces ------------------------
+ * core.Array.read of a region that covers part of a shard goes through
+ * ShardingIndexedCodec.decodePartial → StoreHandleDataProvider (ShardingIndexedCodec.java:
+ * 245-255, 333-357): one prefix/suffix read of the shard's index, then one range read per
+ * referenced inner chunk.  The Java side does exactly that I/O and nothing else; the stored
+ * index goes to the device unchanged, where its crc32c is verified (Crc32cCodec.decode,
+ * Crc32cCodec.java:24-48) and its entries are parsed and mapped onto the pieces.  A shard is
+ * never assembled on the host, so a part whose referenced payload exceeds 2^31 bytes (a Java
+ * array) reads like any other.
+ *
+ * zh_shard_ranges: the byte ranges of one stored shard a part needs.  index = the
+ * index_nbytes bytes the prefix/suffix read returned (16 per inner chunk [+ 4 crc32c]);
+ * shard_nbytes = StoreHandle.getSize() or -1 when the store cannot tell; [part_lo, part_hi) =
+ * shard-local element box.  Entries of the part's inner-chunk box (nested sharding: its
+ * level-1 cells, read whole), missing ones (-1) dropped, are sorted by offset and adjacent
+ * ranges merged while a run stays <= max_run bytes (0: one range per entry; a run never
+ * exceeds 2^31 - 1 bytes).  Entries that cannot be read (negative, beyond a known
+ * shard_nbytes, longer than 2^31 - 1) are left out: the device then reports them with the
+ * reference's "Could not load byte data for chunk [...]" unless the index crc32c fails first.
+ * The index crc32c is NOT checked here.  Writes up to `cap` (offset, nbytes) pairs to
+ * `ranges` (may be NULL) and returns the number of ranges; a negative return is -zh_status
+ * (EINVAL: not a sharded meta, index_nbytes below the index size, bad part box). */
+int64_t zh_shard_ranges(const zh_array_meta* meta, const void* index, int64_t index_nbytes,
+                        int64_t shard_nbytes, const int64_t* part_lo, const int64_t* part_hi,
+                        int64_t max_run, int64_t* ranges, int64_t cap);
+
+/* One byte range of a stored shard as the store returned it. */
+typedef struct zh_shard_piece {
+  int64_t offset;      /* shard byte offset of the range                                       */
+  int64_t nbytes;      /* stored bytes in the range (one inner chunk or a run of adjacent ones) */
+  const void* data;    /* the bytes: host memory, or device memory with ZH_SRC_DEVICE          */
+  int64_t data_nbytes; /* == nbytes: the stored bytes.  Otherwise the range is exactly one
+                          inner chunk whose host byte-to-byte stages (zstd, gzip, blosc) were
+                          undone: data holds its raw `bytes` payload (+ crc32c)               */
+} zh_shard_piece;
+
+/* One stored shard of a region read (computeChunkCoords order).
+ *   missing key (StoreHandle.exists() false): index = NULL, npieces = 0 → fill_value;
+ *   whole shard as one object: index = NULL, one piece at offset 0 holding all its bytes;
+ *   sub-shard part: index = the stored index bytes, pieces = the ranges zh_shard_ranges
+ *     named (in any grouping: a piece must cover each entry it serves; sorted by offset,
+ *     not overlapping).  An entry no piece covers reads as "Could not load byte data". */
+typedef struct zh_shard_src {
+  const void* index;
+  int64_t index_nbytes;
+  int64_t shard_nbytes;           /* StoreHandle.getSize(), -1 when unknown                   */
+  const zh_shard_piece* pieces;
+  int64_t npieces;
+} zh_shard_src;
+
+/* zh_array_read over shards given as index + pieces (HipArray.read's sub-shard form).
+ * Sharded chains only (ZH_EINVAL otherwise).  Host pieces are staged into the device (page-
+ * locked sources by direct DMA, pageable ones through the context's pinned ring); the device
+ * checks each stored index's crc32c and resolves every entry against the pieces.  Large host
+ * reads run pipelined (H2D | decode | D2H) as zh_array_read does. */
+int zh_array_read_pieces(zh_ctx* ctx, const zh_array_meta* meta, const zh_shard_src* shards,
+                         int64_t nshards, const int64_t* offset, const int64_t* shape, void* out,
+                         uint32_t flags, void* stream, char* err, size_t errlen);
+/* zh_array_read_multi_routed over shards given as index + pieces (one JVM, several GPUs). */
+int zh_array_read_pieces_multi(zh_ctx* const* ctxs, int ndev, int root,
+                               const zh_array_meta* meta, const zh_shard_src* shards,
+                               int64_t nshards, const int64_t* offset, const int64_t* shape,
+                               void* out, uint32_t flags, int32_t* slab_route, char* err,
+                               size_t errlen);
+/* ShardingIndexedCodec.decodePartial(StoreHandle, offset, shape) over one shard given as
+ * index + pieces (HipShardingIndexedCodec's form): shard-local offset/shape → shape elements. */
+int zh_sharding_decode_pieces(zh_ctx* ctx, const zh_array_meta* meta, const zh_shard_src* shard,
+                              const int64_t* offset, const int32_t* shape, void* out,
+                              uint32_t flags, void* stream, char* err, size_t errlen);
+/* Page-locked host staging owned by the context, for bindings that must copy their sources
+ * out of a managed heap (the JNI shim copies each piece's byte[] here once, and the decoded
+ * region comes back through it): at least `bytes`, valid until the next call on this context
+ * or zh_ctx_destroy; grown on demand, kept across calls up to ZH_STAGING_MAX_MB (default
+ * 8192; larger requests get a one-off buffer that the next call frees).  Not thread-safe
+ * against other calls on the same context. */
+int zh_host_staging(zh_ctx* ctx, size_t bytes, void** out);
 
 /* ShardingIndexedCodec.decode: whole shard → chunk_shape elements. */
 int zh_sharding_decode(zh_ctx* ctx, const zh_array_meta* meta, const void* shard, int64_t nbytes,

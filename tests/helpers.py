@@ -113,3 +113,121 @@ def load_reference_fixture(loc):
         raw = open(os.path.join(base, "c", *map(str, c)), "rb").read()
         srcs.append(unwrap_blosc_memcpyed_shard(raw, 4, loc))
     return meta_json, m, srcs
+
+
+# ---- the JNI shim's call sequence for HipArray.read (java/jni/zarrhip_jni.c) ------------
+def shard_part(meta, coords, offset, shape):
+    """Shard-local [lo, hi) of the region inside the shard at `coords`."""
+    n = meta.ndim
+    lo, hi = [], []
+    for d in range(n):
+        c0 = coords[d] * meta.chunk_shape[d]
+        lo.append(max(offset[d], c0) - c0)
+        hi.append(min(offset[d] + shape[d], c0 + meta.chunk_shape[d]) - c0)
+    return lo, hi
+
+
+def jni_fetch(meta, paths, offset, shape, max_run=64 << 20, size_known=True, drop=None):
+    """HipArray.read's store I/O (FilesystemStore): per shard of the region either the whole
+    object (part == shard) or the stored index by one prefix/suffix read, zh_shard_ranges, and
+    one range read per returned range.  Returns [(index bytes|None, shard size, [(offset,
+    bytes)])] in computeChunkCoords order (None = missing key).  `drop`: (shard, range) pairs
+    whose store read "fails" (returns null: the piece is not passed on)."""
+    from zarrhip._lib import shard_ranges
+    n = meta.ndim
+    isz = lib().zh_shard_index_size(C.byref(meta))
+    start = meta.chain.index_location == A.ZH_INDEX_START
+    out = []
+    for si, (c, path) in enumerate(zip(chunk_coords(meta, offset, shape), paths)):
+        if path is None or not os.path.exists(path):
+            out.append(None)
+            continue
+        size = os.path.getsize(path)
+        lo, hi = shard_part(meta, c, offset, shape)
+        with open(path, "rb") as f:
+            if lo == [0] * n and hi == [meta.chunk_shape[d] for d in range(n)]:
+                out.append((None, size, [(0, f.read())]))
+                continue
+            f.seek(0 if start else size - isz)
+            idx = f.read(isz)
+            rs = shard_ranges(meta, idx, size if size_known else -1, lo, hi, max_run)
+            pieces = []
+            for k, (o, nb) in enumerate(rs):
+                if drop and (si, k) in drop:
+                    continue
+                f.seek(o)
+                pieces.append((o, f.read(nb)))
+        out.append((idx, size if size_known else -1, pieces))
+    return out
+
+
+def jni_read(dev, meta, fetched, offset, shape):
+    """The JNI marshalling of arrayReadPieces: one zh_host_staging block holds every index
+    and piece (each byte[] copied in once) followed by the output; zh_array_read_pieces
+    decodes into the staging; the region is then copied out (into the Java array)."""
+    from zarrhip._lib import ShardSource
+    nel = int(np.prod(shape))
+    obytes = nel * meta.dtype_size
+    tot = 0
+    for s in fetched:
+        if s is not None:
+            tot += (len(s[0]) if s[0] is not None else 0) + sum(len(b) for _, b in s[2])
+    in_cap = (tot + 255) // 256 * 256
+    base = dev.host_staging(in_cap + obytes)
+    pos = 0
+
+    def put(b):
+        nonlocal pos
+        p = base + pos
+        C.memmove(p, b, len(b))
+        pos += len(b)
+        return p
+    shards = []
+    for s in fetched:
+        if s is None:
+            shards.append(None)
+            continue
+        idx, size, pieces = s
+        ip = put(idx) if idx is not None else None
+        ps = [(o, len(b), put(b), len(b)) for o, b in pieces]
+        shards.append(ShardSource(ip, len(idx) if idx is not None else 0, size, ps))
+    dev.array_read_pieces(meta, shards, offset, shape, base + in_cap, 0)
+    out = np.empty(nel, NP_DT[meta.dtype_size])
+    C.memmove(out.ctypes.data, base + in_cap, obytes)
+    return out.reshape(shape)
+
+
+def shard_from_pieces(meta, ss):
+    """A shard the oracle can read, rebuilt from a sub-shard form (zarrhip ShardSource): the
+    stored index plus the pieces at their offsets (bytes no piece holds stay zero).  Pieces
+    whose host stages were undone (held bytes != stored bytes) go into a fresh raw layout
+    with the index rewritten to them (+ its crc32c)."""
+    isz = lib().zh_shard_index_size(C.byref(meta))
+    idx = C.string_at(ss.index_ptr, ss.index_nbytes)
+    start = meta.chain.index_location == A.ZH_INDEX_START
+    idx = idx[:isz] if start else idx[len(idx) - isz:]
+    fmt = ">QQ" if meta.chain.index_endian == A.ZH_ENDIAN_BIG else "<QQ"
+    if all(nb == held for _, nb, _, held in ss.pieces):
+        end = max([o + nb for o, nb, _, _ in ss.pieces] + [0])
+        size = ss.shard_nbytes if ss.shard_nbytes >= 0 else end + (0 if start else isz)
+        buf = bytearray(size)
+        for o, nb, ptr, _ in ss.pieces:
+            buf[o:o + nb] = C.string_at(ptr, nb)
+        if start:
+            buf[:isz] = idx
+        else:
+            buf[size - isz:] = idx
+        return bytes(buf)
+    held = {o: C.string_at(ptr, h) for o, nb, ptr, h in ss.pieces}
+    ents = [struct.unpack(fmt, idx[16 * k:16 * k + 16]) for k in range((isz - 4) // 16)]
+    payload, new = b"", []
+    base = isz if start else 0
+    for o, nb in ents:
+        if o in held:
+            new.append((base + len(payload), len(held[o])))
+            payload += held[o]
+        else:
+            new.append((2 ** 64 - 1, 2 ** 64 - 1))
+    body = b"".join(struct.pack(fmt, *e) for e in new)
+    ib = body + struct.pack("<I", O.crc32c(body))
+    return ib + payload if start else payload + ib

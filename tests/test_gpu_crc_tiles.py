@@ -173,9 +173,11 @@ def test_row_crc_tile_kernel_many_groups(dev, monkeypatch):
     arr[arr == 0] = 1
     shards = encode_oracle(meta, arr)
     want = np.frombuffer(O.array_read(meta, shards, [0, 0, 0, 0], shape), np.uint32).reshape(shape)
-    got = device_read(dev, meta, shards, [0, 0, 0, 0], shape)
+    got = device_read(dev, meta, shards, [0, 0, 0, 0], shape)  # pipelined (128 MiB host side)
     np.testing.assert_array_equal(got, want)
     np.testing.assert_array_equal(got, arr)
+    monkeypatch.setenv("ZH_PIPE", "0")  # one plan over the whole array: the kernel it selects
+    np.testing.assert_array_equal(device_read(dev, meta, shards, [0, 0, 0, 0], shape), arr)
     assert _variant() == 51
     bad = list(shards)
     k = len(bad) - 1

@@ -872,12 +872,13 @@ def test_rank_1_to_8(dev, case, dsize):
 
 @pytest.mark.parametrize("case", ["sharded_transpose", "unsharded", "nested", "missing_shard"])
 def test_host_output_slab_pipeline(dev, monkeypatch, case):
-    """Large host-output reads go through C-order slabs double-buffered on the device (decode
-    of slab r+1 beside the copy-out of slab r).  The thresholds are shrunk here so small
-    arrays take that path: results equal the oracle, missing shards read fill_value, and a
-    CRC error reports the reference's message."""
-    monkeypatch.setenv("ZH_HOST_SLAB_MIN_KB", "1")
-    monkeypatch.setenv("ZH_HOST_SLAB_KB", "4")
+    """Large host reads go through the pipelined path (C-order slabs: H2D through the pinned
+    ring | decode | D2H through the ring, zh_pipeline.cpp).  The thresholds are shrunk here so
+    small arrays take that path: results equal the oracle, missing shards read fill_value, and
+    a CRC error reports the reference's message."""
+    monkeypatch.setenv("ZH_PIPE_MIN_KB", "1")
+    monkeypatch.setenv("ZH_PIPE_SLAB_KB", "4")
+    monkeypatch.setenv("ZH_PIPE_CHUNK_KB", "64")
     shape = [24, 40, 36]
     kw = dict(endian=A.ZH_ENDIAN_BIG, fill=(9).to_bytes(4, "little"))
     if case != "unsharded":

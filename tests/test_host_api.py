@@ -166,7 +166,7 @@ def test_partial_staging_compacts_shard(loc, gz):
     same region as the whole shard, and reads far fewer bytes."""
     import numpy as np
     import oracle as O
-    from helpers import encode_oracle
+    from helpers import encode_oracle, shard_from_pieces
     fn = (lambda c: c.withBytes("BIG").withGzip()) if gz else (lambda c: c.withBytes("BIG"))
     m = (z.ArrayMetadataBuilder().withShape(32, 32, 16).withDataType(z.DataType.UINT32)
          .withChunkShape(32, 32, 16).withCodecs(lambda c: c.withSharding([4, 4, 4], fn, loc))
@@ -181,7 +181,9 @@ def test_partial_staging_compacts_shard(loc, gz):
     a._handle((0, 0, 0)).set(shard)
     lo, hi = [3, 5, 2], [13, 11, 9]
     a.staged_bytes = 0
-    compact = a._stage_partial(a._handle((0, 0, 0)), lo, hi)
+    lease = []
+    ss, keep = a._stage_shard(a._handle((0, 0, 0)), lo, hi, lease)
+    compact = shard_from_pieces(a.zmeta, ss)
     assert a.staged_bytes < len(shard) / 4
     off, shp = lo, [h - l for l, h in zip(lo, hi)]
     got = np.frombuffer(O.array_read(a.zmeta, [compact], off, shp), np.uint32).reshape(shp)

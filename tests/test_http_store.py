@@ -130,7 +130,7 @@ def test_http_partial_staging(server, loc):
     """A sub-shard part read over HTTP stages the index (one suffix/prefix range) and the
     referenced inner-chunk runs (range reads) only, and decodes (oracle) to the region."""
     import oracle as O
-    from helpers import encode_oracle
+    from helpers import encode_oracle, shard_from_pieces
     root, url = server
     m = (z.ArrayMetadataBuilder().withShape(32, 32, 16).withDataType(z.DataType.UINT32)
          .withChunkShape(32, 32, 16)
@@ -145,7 +145,9 @@ def test_http_partial_staging(server, loc):
     lo, hi = [3, 5, 2], [13, 11, 9]
     _Handler.requests.clear()
     b.staged_bytes = 0
-    compact = b._stage_partial(b._handle((0, 0, 0)), lo, hi)
+    lease = []
+    ss, keep = b._stage_shard(b._handle((0, 0, 0)), lo, hi, lease)
+    compact = shard_from_pieces(b.zmeta, ss)
     assert b.staged_bytes < len(shard) / 4
     gets = [r for mth, p, r in _Handler.requests if mth == "GET"]
     assert all(r is not None for r in gets)     # ranges only, never the whole shard

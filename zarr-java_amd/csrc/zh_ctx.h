@@ -1,0 +1,161 @@
+// zh_ctx.h — host-side state shared by the planner (zh_engine.cpp), the sub-shard source
+// forms (zh_pieces.cpp) and the pipelined host read (zh_pipeline.cpp).  Not public ABI.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <array>
+#include <map>
+#include <mutex>
+#include <string>
+#include <utility>
+#include <vector>
+
+#include "zh_internal.h"
+
+// =====================================================================================
+// context
+// =====================================================================================
+struct zh_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  int cu_count = 256;
+  std::mutex mu;
+  // write-path scratch (grow-only, under mu; zh_array_write synchronises before it returns)
+  uint8_t* wscratch = nullptr;
+  size_t wscratch_cap = 0;
+  // device blocks released by finished plans, reused by later plans of this context: fresh
+  // device memory pays for its first touch (a 2 GiB staging buffer cost ~30 ms in page
+  // setup on every one-shot host-output read) and small allocations pay per call
+  std::mutex cache_mu;
+  std::multimap<size_t, void*> cache;  // block bytes → block
+  size_t cache_bytes = 0;
+  // pipelined host reads (zh_pipeline.cpp): the copy streams and the page-locked rings the
+  // pageable sources / outputs pass through, created on first use and kept
+  hipStream_t pipe_in = nullptr, pipe_out = nullptr;
+  std::vector<void*> ring_in, ring_out;  // pinned slots
+  size_t ring_slot = 0;
+  // zh_host_staging: page-locked staging for bindings (the JNI shim)
+  void* staging = nullptr;
+  size_t staging_cap = 0;
+  bool staging_oneoff = false;
+};
+
+namespace zh {
+
+// One stored chunk / shard as the planner takes it: a whole object (data, nbytes), or a
+// sub-shard form (the stored index + the byte ranges held, zh_shard_src); data == nullptr and
+// index == nullptr: the key is missing.
+struct SrcDesc {
+  const uint8_t* data = nullptr;
+  int64_t nbytes = 0;
+  const uint8_t* index = nullptr;
+  int64_t index_nbytes = 0;
+  int64_t shard_nbytes = -1;
+  const zh_shard_piece* pieces = nullptr;
+  int64_t npieces = 0;
+};
+
+}  // namespace zh
+
+struct zh_plan {
+  zh_ctx* ctx = nullptr;
+  zh_array_meta meta{};
+  uint32_t flags = 0;
+  int64_t nshards = 0;
+  int64_t n_items = 0;          // inner-chunk items (without pieces)
+  int64_t in_bytes = 0, out_bytes = 0;
+  std::vector<int64_t> coords;  // chunk coords (for messages)
+  // device state
+  std::vector<std::pair<void*, size_t>> blocks;  // context-cache blocks owned by the plan
+  hipEvent_t done_ev = nullptr;  // recorded after every execute (plan_free waits on it)
+  uint8_t* d_tables = nullptr;   // one allocation holding the tables below
+  zh::DevShard* d_shards = nullptr;
+  uint64_t* d_status = nullptr;
+  zh::CrcJob* d_crc_jobs = nullptr;
+  uint32_t* d_crc_partials = nullptr;
+  int64_t n_crc_jobs = 0, n_crc_spans = 0;
+  int crc_shift = 0;            // index-CRC span = kIdxSpan << crc_shift
+  uint8_t* d_input = nullptr;   // staged host sources
+  std::vector<std::pair<int64_t, const void*>> h2d;  // (offset in d_input, host ptr)
+  std::vector<int64_t> h2d_len;
+  bool external_h2d = false;    // the pipelined read does the h2d copies (plan_enqueue skips)
+  uint8_t* d_out = nullptr;     // staging when the output is host memory
+  zh::ScatterArgs args{};
+  zh::ItemDesc* d_desc = nullptr;   // per inner-chunk descriptors (resolve kernel)
+  uint32_t* d_slow = nullptr;   // [count, list...] of items for the generic kernel
+  uint32_t* d_fast_tab = nullptr;
+  uint8_t* d_flat = nullptr;    // nested sharding: flattened leaf indexes
+  uint32_t* d_dcrc = nullptr;   // inner crc32c: span partials per chunk
+  zh::DataCrcArgs dcrc{};
+  int dcrc_grid = 0;
+  zh::NestArgs nest{};
+  int nest_grid = 0;
+  int tile_mode = 0;
+  int grid = 0;
+  int slow_grid = 0;
+  hipStream_t last_stream = nullptr;
+  // hipGraph replay of execute (zh_plan_set_graph)
+  bool use_graph = false;
+  hipGraphExec_t graph_exec = nullptr;
+  void* graph_out = nullptr;
+  hipStream_t graph_stream = nullptr;
+  // timing
+  bool timing = false;
+  std::vector<hipEvent_t> ev_pool;
+  std::vector<std::array<hipEvent_t, 3>> ev_pending;
+};
+
+namespace zh {
+
+constexpr int64_t kIntMax = 2147483647LL;
+
+void set_err(char* err, size_t errlen, const char* fmt, ...);
+int env_int(const char* name, int def);
+std::string fmt_ints(const int64_t* v, int n);
+uint64_t ld_u64_host(const uint8_t* p, bool be);
+int64_t chunk_coords(int n, const int32_t* chunk, const int64_t* off, const int64_t* shp,
+                     int64_t* start, int64_t* count);
+const int32_t* leaf_shape(const zh_array_meta* m);
+hipError_t ctx_alloc(zh_ctx* ctx, size_t bytes, void** p, size_t* got);
+void ctx_release(zh_ctx* ctx, void* p, size_t bytes);
+
+// Planner over generic sources (zh_plan_create / zh_array_read_pieces); external_h2d: the
+// caller copies p->h2d itself (the pipelined read).
+int plan_create(zh_ctx* ctx, const zh_array_meta* m, const SrcDesc* srcs, int64_t nchunks,
+                const int64_t* offset, const int64_t* shape, uint32_t flags, bool external_h2d,
+                zh_plan** out, char* err, size_t errlen);
+void plan_free(zh_plan* p);
+
+// The byte ranges of one stored shard a part [part_lo, part_hi) needs (zh_shard_ranges):
+// (offset, nbytes) pairs sorted by offset, adjacent runs merged up to max_run bytes.
+int shard_ranges(const zh_array_meta* m, const uint8_t* index, int64_t shard_nbytes,
+                 const int64_t* part_lo, const int64_t* part_hi, int64_t max_run,
+                 std::vector<std::pair<int64_t, int64_t>>& out);
+
+// Region read over generic sources: the pipelined path for large host reads (zh_pipeline.cpp),
+// else one plan.  Caller holds ctx->mu.
+int read_region(zh_ctx* ctx, const zh_array_meta* meta, const SrcDesc* srcs, int64_t nsrc,
+                const int64_t* offset, const int64_t* shape, void* out, uint32_t flags,
+                void* stream, char* err, size_t errlen);
+// One plan: create, execute, wait, free.
+int read_one_plan(zh_ctx* ctx, const zh_array_meta* meta, const SrcDesc* srcs, int64_t nsrc,
+                  const int64_t* offset, const int64_t* shape, void* out, uint32_t flags,
+                  void* stream, char* err, size_t errlen);
+// Pipelined host read; ZH_EUNSUPPORTED when the region does not qualify or split.
+int read_pipelined(zh_ctx* ctx, const zh_array_meta* meta, const SrcDesc* srcs, int64_t nsrc,
+                   const int64_t* offset, const int64_t* shape, void* out, uint32_t flags,
+                   void* stream, char* err, size_t errlen);
+void pipeline_release(zh_ctx* ctx);  // zh_ctx_destroy: streams and rings
+// One region over several contexts (zh_array_read_multi_routed / zh_array_read_pieces_multi).
+int read_multi_impl(zh_ctx* const* ctxs, int ndev, int root, const zh_array_meta* meta,
+                    const SrcDesc* chunks, int64_t nchunks, const int64_t* offset,
+                    const int64_t* shape, void* out, uint32_t flags, int32_t* slab_route,
+                    char* err, size_t errlen);
+
+// Enqueue one execution of a plan (kernels; the h2d copies unless external_h2d; the d2h copy
+// for host outputs) on stream s.
+int plan_enqueue_impl(zh_plan* p, void* out, hipStream_t s);
+int plan_mark_done_impl(zh_plan* p, hipStream_t s);
+
+}  // namespace zh

@@ -23,13 +23,13 @@
 #include <thread>
 #include <vector>
 
-#include "zh_internal.h"
+#include "zh_ctx.h"
 
 using namespace zh;
 
-namespace {
+namespace zh {
 
-constexpr int64_t kIntMax = 2147483647LL;
+
 
 void set_err(char* err, size_t errlen, const char* fmt, ...) {
   if (!err || errlen == 0) return;
@@ -195,28 +195,10 @@ int env_int(const char* name, int def) {
   return v && *v ? atoi(v) : def;
 }
 
-}  // namespace
+}  // namespace zh
 
-// =====================================================================================
-// context
-// =====================================================================================
-struct zh_ctx {
-  int device = 0;
-  hipStream_t stream = nullptr;
-  int cu_count = 256;
-  std::mutex mu;
-  // write-path scratch (grow-only, under mu; zh_array_write synchronises before it returns)
-  uint8_t* wscratch = nullptr;
-  size_t wscratch_cap = 0;
-  // device blocks released by finished plans, reused by later plans of this context: fresh
-  // device memory pays for its first touch (a 2 GiB staging buffer cost ~30 ms in page
-  // setup on every one-shot host-output read) and small allocations pay per call
-  std::mutex cache_mu;
-  std::multimap<size_t, void*> cache;  // block bytes → block
-  size_t cache_bytes = 0;
-};
 
-namespace {
+namespace zh {
 constexpr size_t kCacheMaxBlock = (size_t)4 << 30;   // larger blocks go back to the runtime
 constexpr size_t kCacheMaxTotal = (size_t)8 << 30;
 
@@ -264,55 +246,8 @@ void ctx_release(zh_ctx* ctx, void* p, size_t bytes) {
   }
   (void)hipFree(p);
 }
-}  // namespace
+}  // namespace zh
 
-struct zh_plan {
-  zh_ctx* ctx = nullptr;
-  zh_array_meta meta{};
-  uint32_t flags = 0;
-  int64_t nshards = 0;
-  int64_t n_items = 0;          // inner-chunk items (without pieces)
-  int64_t in_bytes = 0, out_bytes = 0;
-  std::vector<int64_t> coords;  // chunk coords (for messages)
-  // device state
-  std::vector<std::pair<void*, size_t>> blocks;  // context-cache blocks owned by the plan
-  hipEvent_t done_ev = nullptr;  // recorded after every execute (plan_free waits on it)
-  uint8_t* d_tables = nullptr;   // one allocation holding the tables below
-  DevShard* d_shards = nullptr;
-  uint64_t* d_status = nullptr;
-  CrcJob* d_crc_jobs = nullptr;
-  uint32_t* d_crc_partials = nullptr;
-  int64_t n_crc_jobs = 0, n_crc_spans = 0;
-  int crc_shift = 0;            // index-CRC span = kIdxSpan << crc_shift
-  uint8_t* d_input = nullptr;   // staged host sources
-  std::vector<std::pair<int64_t, const void*>> h2d;  // (offset in d_input, host ptr)
-  std::vector<int64_t> h2d_len;
-  std::vector<std::vector<uint8_t>> h_index;  // rewritten indexes of compact-staged shards
-  uint8_t* d_out = nullptr;     // staging when the output is host memory
-  ScatterArgs args{};
-  ItemDesc* d_desc = nullptr;   // per inner-chunk descriptors (resolve kernel)
-  uint32_t* d_slow = nullptr;   // [count, list...] of items for the generic kernel
-  uint32_t* d_fast_tab = nullptr;
-  uint8_t* d_flat = nullptr;    // nested sharding: flattened leaf indexes
-  uint32_t* d_dcrc = nullptr;   // inner crc32c: span partials per chunk
-  DataCrcArgs dcrc{};
-  int dcrc_grid = 0;
-  NestArgs nest{};
-  int nest_grid = 0;
-  int tile_mode = 0;
-  int grid = 0;
-  int slow_grid = 0;
-  hipStream_t last_stream = nullptr;
-  // hipGraph replay of execute (zh_plan_set_graph)
-  bool use_graph = false;
-  hipGraphExec_t graph_exec = nullptr;
-  void* graph_out = nullptr;
-  hipStream_t graph_stream = nullptr;
-  // timing
-  bool timing = false;
-  std::vector<hipEvent_t> ev_pool;
-  std::vector<std::array<hipEvent_t, 3>> ev_pending;
-};
 
 extern "C" {
 
@@ -345,6 +280,7 @@ void zh_ctx_destroy(zh_ctx* c) {
   if (c->stream) (void)hipStreamDestroy(c->stream);
   if (c->wscratch) (void)hipFree(c->wscratch);
   for (auto& kv : c->cache) (void)hipFree(kv.second);
+  pipeline_release(c);
   delete c;
 }
 
@@ -483,7 +419,7 @@ int zh_validate_meta(const zh_array_meta* m, char* err, size_t errlen) {
 // =====================================================================================
 // planning
 // =====================================================================================
-namespace {
+namespace zh {
 
 // Shape of the chunks the scatter kernels move: the chunk (unsharded), the inner chunk
 // (sharded) or the leaf of the level-2 shard (nested: the flattened leaf grid).
@@ -726,103 +662,105 @@ uint64_t ld_u64_host(const uint8_t* p, bool be) {
   return v;
 }
 
-// Host sources, single-level sharding: StoreHandleDataProvider semantics
-// (ShardingIndexedCodec.java:333-357) inside the planner.  Read the index from host memory,
-// verify its crc32c here (Crc32cCodec.java:39-44), validate the part's entries with the
-// device's messages, and plan a compact
-// device copy: a rewritten index (same endianness, entries outside the part missing) followed
-// by the referenced payloads, copied as coalesced ranges.  *compact_size = -1 keeps the
-// whole-shard copy (parts referencing over 90 % of the shard).
-struct StageRange {
-  int64_t shard, src, dst, len;  // host shard offset → offset in the compact stage
+// The bytes of one stored shard the device will hold: the stored index and the byte ranges
+// of the shard it needs (sub-shard reads), or the whole object.
+struct HeldPieces {
+  const uint8_t* index = nullptr;       // the stored index (isz bytes), host or device
+  std::vector<zh_shard_piece> pieces;   // sorted, disjoint
 };
 
-int compact_stage(zh_plan* p, const zh_array_meta* m, const DevShard& S, int64_t si, int64_t isz,
-                  std::vector<char>& host_checked, std::vector<StageRange>& ranges,
-                  int64_t* compact_size, char* err, size_t errlen) {
-  *compact_size = -1;
-  if (!env_int("ZH_COMPACT", 1)) return ZH_OK;  // A/B switch: whole-shard staging
-  const int n = m->ndim;
-  const ScatterArgs& g = p->args;
-  const bool be = g.index_be != 0;
-  const uint8_t* shard = (const uint8_t*)S.data;
-  const uint8_t* idx = shard + S.index_off;
-  // entries of the part's inner-chunk box, C order (the resolve kernel's enumeration)
-  int64_t nit = 1;
-  for (int d = 0; d < n; d++) nit *= S.box_count[d];
-  struct Ent {
-    uint64_t off, nb;
-    int64_t lin;
-  };
-  std::vector<Ent> ents;
-  int64_t ref_bytes = isz;
-  const uint64_t want = (uint64_t)(g.inner_nbytes + g.crc_extra);
-  int64_t ic[kMaxDims];
-  for (int64_t j = 0; j < nit; j++) {
-    int64_t q = j, lin = 0;
-    for (int d = n - 1; d >= 0; d--) {
-      ic[d] = S.box_start[d] + q % S.box_count[d];
-      q /= S.box_count[d];
-    }
-    for (int d = 0; d < n; d++) lin += ic[d] * g.cps_stride[d];
-    const uint64_t off = ld_u64_host(idx + 16 * lin, be), nb = ld_u64_host(idx + 16 * lin + 8, be);
-    if (off == ~0ull || nb == ~0ull) continue;  // Q1
-    ents.push_back({off, nb, lin});
-    ref_bytes += (int64_t)std::min<uint64_t>(nb, (uint64_t)S.nbytes);
+// Host whole-shard sources, single-level sharding: StoreHandleDataProvider semantics
+// (ShardingIndexedCodec.java:333-357) inside the planner.  The stored index is read on the
+// host only to know which ranges the part references (shard_ranges, adjacent ranges merged);
+// the device gets the stored index unchanged plus those ranges, checks the index crc32c and
+// resolves every entry against the ranges (an entry outside them reads as the reference's
+// "Could not load byte data").  Returns false when the part references over 90 % of the
+// shard: the whole object is copied then.
+bool compact_pieces(const zh_array_meta* m, const DevShard& S, int64_t isz, HeldPieces& hp) {
+  if (!env_int("ZH_COMPACT", 1)) return false;  // A/B switch: whole-shard staging
+  int64_t lo[kMaxDims], hi[kMaxDims];
+  for (int d = 0; d < m->ndim; d++) {
+    lo[d] = S.part_lo[d];
+    hi[d] = S.part_hi[d];
   }
+  std::vector<std::pair<int64_t, int64_t>> rs;
+  if (shard_ranges(m, S.data + S.index_off, S.nbytes, lo, hi, INT64_MAX, rs) != ZH_OK)
+    return false;
+  int64_t ref = isz;
+  for (auto& r : rs) ref += r.second;
   // H2D is bandwidth-bound: compacting pays whenever it skips a tenth of the shard
-  if (10 * ref_bytes > 9 * S.nbytes) return ZH_OK;
-  // from here the host owns the checks the device would have made on this shard
-  if (m->chain.index_has_crc32c) {  // Crc32cCodec.decode (:24-48)
-    const uint32_t computed = crc32c_host(0, idx, (size_t)(isz - 4));
-    const uint8_t* s = idx + isz - 4;
-    const uint32_t stored = (uint32_t)s[0] | ((uint32_t)s[1] << 8) | ((uint32_t)s[2] << 16) |
-                            ((uint32_t)s[3] << 24);
-    if (computed != stored) {
-      set_err(err, errlen, "The checksum of the sharding index is invalid. Stored: %d Computed: %d",
-              (int32_t)stored, (int32_t)computed);
-      return ZH_EDATA;
+  if (10 * ref > 9 * S.nbytes) return false;
+  hp.index = S.data + S.index_off;
+  hp.pieces.clear();
+  for (auto& r : rs) hp.pieces.push_back({r.first, r.second, S.data + r.first, r.second});
+  return true;
+}
+
+int caller_pieces_all(const zh_array_meta* m, const SrcDesc& src, int64_t isz, const int64_t* cc,
+                      HeldPieces& hp, char* err, size_t errlen);
+
+// Validates a caller's sub-shard form (zh_shard_src) and collects its pieces.  For host
+// sources only what this part references is kept (a pipelined read plans one part per slab,
+// and each slab must copy only its own ranges): the caller's raw pieces cut to the ranges
+// the stored index names for the part (read on the host only to know what to copy; checked
+// on the device), host-decoded pieces kept whole when referenced.
+int caller_pieces(const zh_array_meta* m, const SrcDesc& src, int64_t isz, const int64_t* cc,
+                  const DevShard& S, bool src_dev, HeldPieces& hp, char* err, size_t errlen) {
+  int st = caller_pieces_all(m, src, isz, cc, hp, err, errlen);
+  if (st != ZH_OK || src_dev) return st;
+  int64_t lo[kMaxDims], hi[kMaxDims];
+  for (int d = 0; d < m->ndim; d++) {
+    lo[d] = S.part_lo[d];
+    hi[d] = S.part_hi[d];
+  }
+  std::vector<std::pair<int64_t, int64_t>> need;
+  if (shard_ranges(m, hp.index, src.shard_nbytes, lo, hi, INT64_MAX, need) != ZH_OK) return ZH_OK;
+  std::vector<zh_shard_piece> kept;
+  size_t r = 0;
+  for (const zh_shard_piece& q : hp.pieces) {
+    const int64_t qe = q.offset + q.nbytes;
+    while (r < need.size() && need[r].first + need[r].second <= q.offset) r++;
+    for (size_t k = r; k < need.size() && need[k].first < qe; k++) {
+      const int64_t a = std::max(q.offset, need[k].first);
+      const int64_t b = std::min(qe, need[k].first + need[k].second);
+      if (b <= a) continue;
+      if (q.data_nbytes != q.nbytes) {  // one host-decoded chunk: whole or nothing
+        kept.push_back(q);
+        break;
+      }
+      kept.push_back({a, b - a, (const uint8_t*)q.data + (a - q.offset), b - a});
     }
   }
-  for (const Ent& e : ents) {  // first failure in C order = the device's smallest-lin report
-    const uint64_t total = (uint64_t)S.nbytes;
-    const bool range_ok = e.off <= total && e.nb <= total - e.off;
-    if (range_ok && e.nb == want) continue;
-    int64_t q = e.lin;
-    for (int d = n - 1; d >= 0; d--) {
-      const int64_t cps = m->chunk_shape[d] / m->chain.inner_chunk_shape[d];
-      ic[d] = q % cps;
-      q /= cps;
-    }
-    if (!range_ok)  // ShardingIndexedCodec.java:227-230
-      set_err(err, errlen, "Could not load byte data for chunk %s", fmt_ints(ic, n).c_str());
-    else
-      set_err(err, errlen, "unexpected inner chunk byte length for chunk %s", fmt_ints(ic, n).c_str());
+  hp.pieces.swap(kept);
+  return ZH_OK;
+}
+
+int caller_pieces_all(const zh_array_meta* m, const SrcDesc& src, int64_t isz, const int64_t* cc,
+                      HeldPieces& hp, char* err, size_t errlen) {
+  const int n = m->ndim;
+  if (src.index_nbytes < isz) {
+    set_err(err, errlen, "Shard %s is smaller than its index (%lld bytes).",
+            fmt_ints(cc, n).c_str(), (long long)isz);
     return ZH_EDATA;
   }
-  // compact layout: [index][payloads in source order]; adjacent sources → one copy
-  std::sort(ents.begin(), ents.end(), [](const Ent& x, const Ent& y) { return x.off < y.off; });
-  std::vector<uint8_t> nidx((size_t)isz, 0xFF);  // entries outside the part: missing
-  int64_t pos = isz;
-  for (size_t k = 0; k < ents.size(); k++) {
-    const Ent& e = ents[k];
-    uint8_t* d = nidx.data() + 16 * e.lin;
-    for (int b = 0; b < 8; b++) {
-      const int sh = be ? 56 - 8 * b : 8 * b;
-      d[b] = (uint8_t)((uint64_t)pos >> sh);
-      d[8 + b] = (uint8_t)(e.nb >> sh);
+  hp.index = src.index + (m->chain.index_location == ZH_INDEX_START ? 0 : src.index_nbytes - isz);
+  hp.pieces.assign(src.pieces, src.pieces + std::max<int64_t>(0, src.npieces));
+  for (size_t k = 0; k < hp.pieces.size(); k++) {
+    const zh_shard_piece& q = hp.pieces[k];
+    const bool bad = q.offset < 0 || q.nbytes < 0 || q.data_nbytes < 0 ||
+                     (q.data_nbytes > 0 && !q.data) ||
+                     (k > 0 && q.offset < hp.pieces[k - 1].offset + hp.pieces[k - 1].nbytes) ||
+                     (q.data_nbytes != q.nbytes && m->chain.nested);
+    if (bad) {
+      set_err(err, errlen,
+              "shard %s: piece %lld (offset %lld, %lld bytes, %lld held) is invalid: pieces "
+              "must be sorted by offset, disjoint, and hold their bytes (host-decoded pieces "
+              "only below single-level sharding)",
+              fmt_ints(cc, n).c_str(), (long long)k, (long long)q.offset, (long long)q.nbytes,
+              (long long)q.data_nbytes);
+      return ZH_EINVAL;
     }
-    if (!ranges.empty() && ranges.back().shard == si &&
-        ranges.back().src + ranges.back().len == (int64_t)e.off &&
-        ranges.back().dst + ranges.back().len == pos)
-      ranges.back().len += (int64_t)e.nb;
-    else
-      ranges.push_back({si, (int64_t)e.off, pos, (int64_t)e.nb});
-    pos += (int64_t)e.nb;
   }
-  p->h_index.push_back(std::move(nidx));
-  host_checked[si] = 1;
-  *compact_size = pos;
   return ZH_OK;
 }
 
@@ -842,13 +780,13 @@ void plan_free(zh_plan* p) {
   delete p;
 }
 
-}  // namespace
+}  // namespace zh
 
-extern "C" {
+namespace zh {
 
-int zh_plan_create(zh_ctx* ctx, const zh_array_meta* m, const zh_chunk_src* chunks,
-                   int64_t nchunks, const int64_t* offset, const int64_t* shape, uint32_t flags,
-                   zh_plan** out, char* err, size_t errlen) {
+int plan_create(zh_ctx* ctx, const zh_array_meta* m, const SrcDesc* srcs, int64_t nchunks,
+                const int64_t* offset, const int64_t* shape, uint32_t flags, bool external_h2d,
+                zh_plan** out, char* err, size_t errlen) {
   if (!ctx || !m || !offset || !shape || !out) return ZH_EINVAL;
   *out = nullptr;
   int st = zh_validate_meta(m, err, errlen);
@@ -870,7 +808,7 @@ int zh_plan_create(zh_ctx* ctx, const zh_array_meta* m, const zh_chunk_src* chun
     set_err(err, errlen, "Number of chunks exceeds Integer.MAX_VALUE");
     return ZH_EARITH;
   }
-  if (ncoords != nchunks || (nchunks > 0 && !chunks)) {
+  if (ncoords != nchunks || (nchunks > 0 && !srcs)) {
     set_err(err, errlen, "expected %lld chunk sources (computeChunkCoords order), got %lld",
             (long long)ncoords, (long long)nchunks);
     return ZH_EINVAL;
@@ -881,10 +819,12 @@ int zh_plan_create(zh_ctx* ctx, const zh_array_meta* m, const zh_chunk_src* chun
   p->meta = *m;
   p->flags = flags;
   p->nshards = ncoords;
+  p->external_h2d = external_h2d;
   fill_common_args(m, shape, false, p->args, p->tile_mode);
   const zh_codec_chain& c = m->chain;
   const int32_t* inner = leaf_shape(m);
   const int64_t isz = zh_shard_index_size(m);
+  const bool src_dev = (flags & ZH_SRC_DEVICE) != 0;
   // nested sharding: level-1 cells and the flattened leaf index per shard
   const bool nested = c.sharded && c.nested;
   int64_t cps_leaf = 1, cps2 = 1;
@@ -901,8 +841,15 @@ int zh_plan_create(zh_ctx* ctx, const zh_array_meta* m, const zh_chunk_src* chun
   int64_t cur[kMaxDims] = {0};
   int64_t items = 0, staged = 0, in_bytes = 0;
   std::vector<int64_t> stage_off(ncoords, -1);
-  std::vector<char> host_checked(ncoords, 0);  // index CRC verified on the host (compact)
-  std::vector<StageRange> compact_ranges;
+  // shards held as index + pieces (sub-shard forms): the pieces of shard i are
+  // held[i].pieces, laid out after its index in its staging block at piece_dst
+  std::vector<HeldPieces> held(ncoords);
+  std::vector<char> is_held(ncoords, 0);
+  std::vector<std::vector<int64_t>> piece_dst(ncoords);
+  auto fail = [&](int code) {
+    plan_free(p);
+    return code;
+  };
   for (int64_t i = 0; i < ncoords; i++) {
     int64_t cc[kMaxDims];
     for (int d = 0; d < n; d++) cc[d] = p->coords[i * n + d] = cstart[d] + cur[d];
@@ -913,13 +860,19 @@ int zh_plan_create(zh_ctx* ctx, const zh_array_meta* m, const zh_chunk_src* chun
     int32_t co[kMaxDims], oo[kMaxDims], ps[kMaxDims];
     if (projection(n, cc, m->shape, m->chunk_shape, offset, shape, co, oo, ps) != ZH_OK) {
       set_err(err, errlen, "projection exceeds Integer.MAX_VALUE");
-      plan_free(p);
-      return ZH_EARITH;
+      return fail(ZH_EARITH);
     }
+    const SrcDesc& src = srcs[i];
     DevShard& S = hs[i];
     memset(&S, 0, sizeof(S));
-    S.data = (const uint8_t*)chunks[i].data;
-    S.nbytes = chunks[i].nbytes;
+    const bool pieced = src.index != nullptr;
+    if (pieced && !c.sharded) {
+      set_err(err, errlen, "chunk %s: index + pieces sources need a sharding_indexed chain",
+              fmt_ints(cc, n).c_str());
+      return fail(ZH_EINVAL);
+    }
+    S.data = pieced ? src.index : src.data;
+    S.nbytes = pieced ? (src.shard_nbytes >= 0 ? src.shard_nbytes : INT64_MAX) : src.nbytes;
     S.item_begin = items;
     int64_t ob = 0, nit = 1;
     for (int d = 0; d < n; d++) {
@@ -939,61 +892,70 @@ int zh_plan_create(zh_ctx* ctx, const zh_array_meta* m, const zh_chunk_src* chun
     S.out_base = ob;
     S.l1_begin = l1_items;
     items += nit;
-    if (S.data) {
-      if (c.sharded) {
-        if (S.nbytes < isz) {
-          set_err(err, errlen, "Shard %s of %lld bytes is smaller than its index (%lld bytes).",
-                  fmt_ints(cc, n).c_str(), (long long)S.nbytes, (long long)isz);
-          plan_free(p);
-          return ZH_EDATA;
-        }
-        S.index_off = c.index_location == ZH_INDEX_START ? 0 : S.nbytes - isz;
-      } else if (S.nbytes != p->args.inner_nbytes + p->args.crc_extra) {  // Q12 (knowing divergence)
-        set_err(err, errlen,
-                "unexpected inner chunk byte length: %lld (expected %lld) for chunk %s",
-                (long long)S.nbytes, (long long)(p->args.inner_nbytes + p->args.crc_extra),
-                fmt_ints(cc, n).c_str());
-        plan_free(p);
-        return ZH_EDATA;
+    if (!S.data) continue;
+    if (pieced) {
+      if ((st = caller_pieces(m, src, isz, cc, S, src_dev, held[i], err, errlen)) != ZH_OK) return fail(st);
+      is_held[i] = 1;
+      S.index_off = 0;
+    } else if (c.sharded) {
+      if (S.nbytes < isz) {
+        set_err(err, errlen, "Shard %s of %lld bytes is smaller than its index (%lld bytes).",
+                fmt_ints(cc, n).c_str(), (long long)S.nbytes, (long long)isz);
+        return fail(ZH_EDATA);
       }
-      if (nested) {
-        int64_t ncell = 1;
-        S.l1_begin = l1_items;
-        for (int d = 0; d < n; d++) {
-          const int32_t i1 = c.inner_chunk_shape[d];
-          S.l1_box_start[d] = co[d] / i1;
-          S.l1_box_count[d] = (co[d] + ps[d] - 1) / i1 - S.l1_box_start[d] + 1;
-          ncell *= S.l1_box_count[d];
-        }
-        for (int d = n; d < kMaxDims; d++) S.l1_box_count[d] = 1;
-        l1_items += ncell;
-        flat_off[i] = flat_bytes;
-        flat_bytes += 16 * cps_leaf;
-        in_bytes += ncell * sub_isz;  // the referenced sub-shard indexes
-      }
-      // algorithmic input bytes: referenced inner chunks + the index for a
-      // shard; only the in-bounds part of an unsharded chunk
-      if (c.sharded) {
-        in_bytes += nit * (p->args.inner_nbytes + p->args.crc_extra) + isz;
-      } else {
-        int64_t pb = m->dtype_size;
-        for (int d = 0; d < n; d++) pb *= ps[d];
-        in_bytes += pb;
-      }
-      if (!(flags & ZH_SRC_DEVICE)) {
-        int64_t compact = -1;
-        if (c.sharded && !nested) {
-          st = compact_stage(p, m, S, i, isz, host_checked, compact_ranges, &compact, err,
-                             errlen);
-          if (st != ZH_OK) {
-            plan_free(p);
-            return st;
-          }
-        }
-        stage_off[i] = staged;
-        staged += ((compact >= 0 ? compact : S.nbytes) + 255) & ~(int64_t)255;
-      }
+      S.index_off = c.index_location == ZH_INDEX_START ? 0 : S.nbytes - isz;
+    } else if (S.nbytes != p->args.inner_nbytes + p->args.crc_extra) {  // Q12 (knowing divergence)
+      set_err(err, errlen,
+              "unexpected inner chunk byte length: %lld (expected %lld) for chunk %s",
+              (long long)S.nbytes, (long long)(p->args.inner_nbytes + p->args.crc_extra),
+              fmt_ints(cc, n).c_str());
+      return fail(ZH_EDATA);
     }
+    if (nested) {
+      int64_t ncell = 1;
+      S.l1_begin = l1_items;
+      for (int d = 0; d < n; d++) {
+        const int32_t i1 = c.inner_chunk_shape[d];
+        S.l1_box_start[d] = co[d] / i1;
+        S.l1_box_count[d] = (co[d] + ps[d] - 1) / i1 - S.l1_box_start[d] + 1;
+        ncell *= S.l1_box_count[d];
+      }
+      for (int d = n; d < kMaxDims; d++) S.l1_box_count[d] = 1;
+      l1_items += ncell;
+      flat_off[i] = flat_bytes;
+      flat_bytes += 16 * cps_leaf;
+      in_bytes += ncell * sub_isz;  // the referenced sub-shard indexes
+    }
+    // algorithmic input bytes: referenced inner chunks + the index for a
+    // shard; only the in-bounds part of an unsharded chunk
+    if (c.sharded) {
+      in_bytes += nit * (p->args.inner_nbytes + p->args.crc_extra) + isz;
+    } else {
+      int64_t pb = m->dtype_size;
+      for (int d = 0; d < n; d++) pb *= ps[d];
+      in_bytes += pb;
+    }
+    if (src_dev) continue;  // device sources are read where they are
+    // host sources: a whole object is staged as it is, unless the part references little
+    // of a single-level shard (then its index + the referenced ranges, as a caller's pieces)
+    if (!is_held[i] && c.sharded && !nested && compact_pieces(m, S, isz, held[i])) {
+      is_held[i] = 1;
+      S.index_off = 0;  // the staging block starts with the stored index
+    }
+    stage_off[i] = staged;
+    if (!is_held[i]) {
+      staged += (S.nbytes + 255) & ~(int64_t)255;
+      continue;
+    }
+    // staging block: [index][pieces], each raw piece at its shard offset's residue mod 256
+    // (the payload alignment the fast kernels see is the stored one)
+    int64_t pos = isz;
+    for (const zh_shard_piece& q : held[i].pieces) {
+      pos = ((pos + 255) & ~(int64_t)255) + (q.data_nbytes == q.nbytes ? (q.offset & 255) : 0);
+      piece_dst[i].push_back(pos);
+      pos += q.data_nbytes;
+    }
+    staged += (pos + 255) & ~(int64_t)255;
   }
   p->n_items = items;
   p->in_bytes = in_bytes;
@@ -1002,27 +964,18 @@ int zh_plan_create(zh_ctx* ctx, const zh_array_meta* m, const zh_chunk_src* chun
   p->out_bytes = onel * m->dtype_size;
   // stage host sources
   if (staged > 0) {
-    st = plan_alloc(p, &p->d_input, (size_t)staged, err, errlen);
-    if (st != ZH_OK) {
-      plan_free(p);
-      return st;
-    }
-    size_t rk = 0, ik = 0;
+    if ((st = plan_alloc(p, &p->d_input, (size_t)staged, err, errlen)) != ZH_OK) return fail(st);
     for (int64_t i = 0; i < ncoords; i++) {
       if (stage_off[i] < 0) continue;
-      if (host_checked[i]) {  // compact shard: rewritten index + the referenced ranges
-        p->h2d.push_back({stage_off[i], p->h_index[ik].data()});
-        p->h2d_len.push_back((int64_t)p->h_index[ik].size());
-        ik++;
-        int64_t total = isz;
-        for (; rk < compact_ranges.size() && compact_ranges[rk].shard == i; rk++) {
-          const StageRange& R = compact_ranges[rk];
-          p->h2d.push_back({stage_off[i] + R.dst, (const uint8_t*)hs[i].data + R.src});
-          p->h2d_len.push_back(R.len);
-          total = std::max(total, R.dst + R.len);
+      if (is_held[i]) {
+        p->h2d.push_back({stage_off[i], held[i].index});
+        p->h2d_len.push_back(isz);
+        const auto& pv = held[i].pieces;
+        for (size_t k = 0; k < pv.size(); k++) {
+          if (pv[k].data_nbytes <= 0) continue;
+          p->h2d.push_back({stage_off[i] + piece_dst[i][k], pv[k].data});
+          p->h2d_len.push_back(pv[k].data_nbytes);
         }
-        hs[i].nbytes = total;
-        hs[i].index_off = 0;
       } else {
         p->h2d.push_back({stage_off[i], hs[i].data});
         p->h2d_len.push_back(hs[i].nbytes);
@@ -1030,12 +983,22 @@ int zh_plan_create(zh_ctx* ctx, const zh_array_meta* m, const zh_chunk_src* chun
       hs[i].data = p->d_input + stage_off[i];
     }
   }
-  if (nested && flat_bytes > 0) {
-    st = plan_alloc(p, &p->d_flat, (size_t)flat_bytes, err, errlen);
-    if (st != ZH_OK) {
-      plan_free(p);
-      return st;
+  // the piece tables (device addresses of every held range)
+  std::vector<DevPiece> dpieces;
+  std::vector<int64_t> piece_first(ncoords, -1);
+  for (int64_t i = 0; i < ncoords; i++) {
+    if (!is_held[i]) continue;
+    piece_first[i] = (int64_t)dpieces.size();
+    const auto& pv = held[i].pieces;
+    for (size_t k = 0; k < pv.size(); k++) {
+      const uint8_t* dsrc = src_dev ? (const uint8_t*)pv[k].data : hs[i].data + piece_dst[i][k];
+      dpieces.push_back({(uint64_t)pv[k].offset, (uint64_t)pv[k].nbytes, dsrc,
+                         (uint64_t)pv[k].data_nbytes});
     }
+    hs[i].npieces = (int64_t)pv.size();
+  }
+  if (nested && flat_bytes > 0) {
+    if ((st = plan_alloc(p, &p->d_flat, (size_t)flat_bytes, err, errlen)) != ZH_OK) return fail(st);
     for (int64_t i = 0; i < ncoords; i++)
       if (flat_off[i] >= 0) hs[i].flat = p->d_flat + flat_off[i];
     NestArgs& N = p->nest;
@@ -1059,10 +1022,11 @@ int zh_plan_create(zh_ctx* ctx, const zh_array_meta* m, const zh_chunk_src* chun
     }
     p->nest_grid = (int)std::min<int64_t>(l1_items, (int64_t)ctx->cu_count * 16);
   }
-  // CRC jobs over the device copies of the indexes
+  // CRC jobs over the device copies of the stored indexes (Crc32cCodec.decode, :24-48): every
+  // shard's, the sub-shard forms' included — the host never checks an index
   if (c.sharded && c.index_has_crc32c) {
     for (int64_t i = 0; i < ncoords; i++) {
-      if (!hs[i].data || host_checked[i]) continue;
+      if (!hs[i].data) continue;
       CrcJob J;
       J.base = hs[i].data + hs[i].index_off;
       J.len = isz - 4;
@@ -1126,6 +1090,7 @@ int zh_plan_create(zh_ctx* ctx, const zh_array_meta* m, const zh_chunk_src* chun
     const size_t o_jobs = carve(jobs.size() * sizeof(CrcJob));
     const size_t o_part = carve((size_t)(p->n_crc_spans + p->n_crc_jobs) * 4);
     const size_t o_tab = carve(tab.size() * 4);
+    const size_t o_pieces = carve(dpieces.size() * sizeof(DevPiece));
     const size_t up = off;  // uploaded prefix
     const size_t o_status = carve((size_t)ncoords * kStWords * 8);
     const size_t o_desc = carve((size_t)items * sizeof(ItemDesc));
@@ -1135,7 +1100,12 @@ int zh_plan_create(zh_ctx* ctx, const zh_array_meta* m, const zh_chunk_src* chun
       return st;
     }
     std::vector<uint8_t> blob(up, 0);
+    for (int64_t i = 0; i < ncoords; i++)
+      if (piece_first[i] >= 0)
+        hs[i].pieces = (const DevPiece*)(p->d_tables + o_pieces) + piece_first[i];
     memcpy(blob.data() + o_shards, hs.data(), hs.size() * sizeof(DevShard));
+    if (!dpieces.empty())
+      memcpy(blob.data() + o_pieces, dpieces.data(), dpieces.size() * sizeof(DevPiece));
     if (!jobs.empty()) memcpy(blob.data() + o_jobs, jobs.data(), jobs.size() * sizeof(CrcJob));
     if (!tab.empty()) memcpy(blob.data() + o_tab, tab.data(), tab.size() * 4);
     uint8_t* T = p->d_tables;
@@ -1277,10 +1247,10 @@ int zh_plan_create(zh_ctx* ctx, const zh_array_meta* m, const zh_chunk_src* chun
 }
 
 // Enqueues one execution of the plan on stream s (also the body a hipGraph captures).
-static int plan_enqueue(zh_plan* p, void* out, hipStream_t s) {
+int plan_enqueue_impl(zh_plan* p, void* out, hipStream_t s) {
   char* err = nullptr;
   size_t errlen = 0;
-  for (size_t k = 0; k < p->h2d.size(); k++)
+  for (size_t k = 0; !p->external_h2d && k < p->h2d.size(); k++)
     ZH_HIP(hipMemcpyAsync(p->d_input + p->h2d[k].first, p->h2d[k].second, (size_t)p->h2d_len[k],
                           hipMemcpyHostToDevice, s));
   ZH_HIP(hipMemsetAsync(p->d_status, 0, (size_t)p->nshards * kStWords * sizeof(uint64_t), s));
@@ -1320,28 +1290,38 @@ static int plan_enqueue(zh_plan* p, void* out, hipStream_t s) {
   return ZH_OK;
 }
 
-static void plan_drop_graph(zh_plan* p) {
+void plan_drop_graph(zh_plan* p) {
   if (p->graph_exec) (void)hipGraphExecDestroy(p->graph_exec);
   p->graph_exec = nullptr;
   p->graph_out = nullptr;
   p->graph_stream = nullptr;
 }
 
-}  // extern "C"
-
-namespace {
 // Records the end of the plan's latest execution: plan_free waits on this event before its
 // device blocks go back to the context's cache (an event outlives a caller's stream).
-int plan_mark_done(zh_plan* p, hipStream_t s) {
+int plan_mark_done_impl(zh_plan* p, hipStream_t s) {
   if (!p->done_ev && hipEventCreateWithFlags(&p->done_ev, hipEventDisableTiming) != hipSuccess) {
     p->done_ev = nullptr;
     return ZH_EHIP;
   }
   return hipEventRecord(p->done_ev, s) == hipSuccess ? ZH_OK : ZH_EHIP;
 }
-}  // namespace
+
+}  // namespace zh
 
 extern "C" {
+
+int zh_plan_create(zh_ctx* ctx, const zh_array_meta* m, const zh_chunk_src* chunks,
+                   int64_t nchunks, const int64_t* offset, const int64_t* shape, uint32_t flags,
+                   zh_plan** out, char* err, size_t errlen) {
+  std::vector<SrcDesc> srcs((size_t)std::max<int64_t>(0, nchunks));
+  for (int64_t i = 0; chunks && i < nchunks; i++) {
+    srcs[(size_t)i].data = (const uint8_t*)chunks[i].data;
+    srcs[(size_t)i].nbytes = chunks[i].nbytes;
+  }
+  return plan_create(ctx, m, chunks ? srcs.data() : nullptr, nchunks, offset, shape, flags,
+                     false, out, err, errlen);
+}
 
 int zh_plan_execute(zh_plan* p, void* out, void* stream_v) {
   if (!p || !out) return ZH_EINVAL;
@@ -1356,7 +1336,7 @@ int zh_plan_execute(zh_plan* p, void* out, void* stream_v) {
     if (!p->graph_exec || p->graph_out != out || p->graph_stream != s) {
       plan_drop_graph(p);
       ZH_HIP(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
-      const int st = plan_enqueue(p, out, s);
+      const int st = plan_enqueue_impl(p, out, s);
       hipGraph_t g = nullptr;
       const hipError_t e = hipStreamEndCapture(s, &g);
       if (st != ZH_OK || e != hipSuccess) {
@@ -1374,11 +1354,11 @@ int zh_plan_execute(zh_plan* p, void* out, void* stream_v) {
     }
     ZH_HIP(hipGraphLaunch(p->graph_exec, s));
     p->last_stream = s;
-    return plan_mark_done(p, s);
+    return plan_mark_done_impl(p, s);
   }
-  const int st = plan_enqueue(p, out, s);
+  const int st = plan_enqueue_impl(p, out, s);
   if (st == ZH_OK) p->last_stream = s;
-  return st == ZH_OK ? plan_mark_done(p, s) : st;
+  return st == ZH_OK ? plan_mark_done_impl(p, s) : st;
 }
 
 int zh_plan_set_graph(zh_plan* p, int enable) {
@@ -1488,170 +1468,13 @@ int zh_plan_kernel_time(zh_plan* p, double* scatter_ms, int64_t* launches, doubl
 
 }  // extern "C"
 
-namespace {
-// The chunks of slab (o, s) picked out of the caller's list for the whole region (offset,
-// shape), which follows computeChunkCoords order.
-std::vector<zh_chunk_src> slab_chunks(const zh_array_meta* meta, const zh_chunk_src* chunks,
-                                      const int64_t* offset, const int64_t* shape,
-                                      const int64_t* o, const int64_t* s) {
-  const int n = meta->ndim;
-  int64_t cstart[kMaxDims], ccount[kMaxDims], cstride[kMaxDims], st0[kMaxDims], cnt[kMaxDims];
-  chunk_coords(n, meta->chunk_shape, offset, shape, cstart, ccount);
-  int64_t s2 = 1;
-  for (int d = n - 1; d >= 0; d--) {
-    cstride[d] = s2;
-    s2 *= ccount[d];
-  }
-  const int64_t m = chunk_coords(n, meta->chunk_shape, o, s, st0, cnt);
-  std::vector<zh_chunk_src> sub((size_t)m);
-  int64_t cur[kMaxDims] = {0};
-  for (int64_t i = 0; i < m; i++) {
-    int64_t lin = 0;
-    for (int d = 0; d < n; d++) lin += (st0[d] + cur[d] - cstart[d]) * cstride[d];
-    sub[(size_t)i] = chunks[lin];
-    for (int d = n - 1; d >= 0; d--) {
-      if (++cur[d] < cnt[d]) break;
-      cur[d] = 0;
-    }
-  }
-  return sub;
-}
+namespace zh {
 
-// Host outputs above ZH_HOST_SLAB_MIN_KB (4 GiB: larger than the block cache keeps) are
-// slabbed, ZH_HOST_SLAB_KB (1 GiB) per slab; up to 4 GiB one cached staging buffer is 3-4 %
-// faster (profiles/r01/experiments/oneshot_latency.json).  The tests shrink both to run the
-// path on small arrays.
-int64_t host_slab_min() { return (int64_t)env_int("ZH_HOST_SLAB_MIN_KB", 4 << 20) << 10; }
-int64_t host_slab_bytes() { return (int64_t)std::max(1, env_int("ZH_HOST_SLAB_KB", 1 << 20)) << 10; }
-
-// A large read into host memory, in C-order slabs of about 1 GiB: each slab is decoded
-// into one of two device buffers (from the context's block cache) while the previous slab is
-// copied out on a second stream.  Device memory stays bounded and reused across calls; a
-// single staging buffer of the whole output paid its first touch on every call (fresh device
-// memory) and held the output twice.  Returns ZH_EUNSUPPORTED when the region does not split.
-int array_read_host_slabs(zh_ctx* ctx, const zh_array_meta* meta, const zh_chunk_src* chunks,
-                          int64_t nchunks, const int64_t* offset, const int64_t* shape,
-                          void* out, uint32_t flags, void* stream_v, char* err, size_t errlen) {
-  const int n = meta->ndim;
-  int64_t nel = 1;
-  for (int d = 0; d < n; d++) nel *= shape[d];
-  const int64_t bytes = nel * meta->dtype_size;
-  const int64_t per = host_slab_bytes();
-  int64_t nslab = (bytes + per - 1) / per;
-  int ax = -1;
-  for (int d = 0; d < n; d++) {
-    if (shape[d] >= 2) {
-      ax = d;
-      break;
-    }
-  }
-  if (ax < 0) return ZH_EUNSUPPORTED;
-  nslab = std::min<int64_t>(nslab, shape[ax]);
-  if (nslab < 2) return ZH_EUNSUPPORTED;
-  {
-    int64_t cs[kMaxDims], cc[kMaxDims];  // the caller's list must match the whole region
-    if (chunk_coords(n, meta->chunk_shape, offset, shape, cs, cc) != nchunks || !chunks)
-      return ZH_EUNSUPPORTED;  // the one-plan path reports it
-  }
-  std::vector<int64_t> so((size_t)nslab * n), ss((size_t)nslab * n);
-  if (zh_slab_partition(n, offset, shape, (int)nslab, leaf_shape(meta)[ax], so.data(),
-                        ss.data()) != ZH_OK)
-    return ZH_EUNSUPPORTED;
-  int64_t rstride[kMaxDims], sr = 1, maxb = 0;
-  for (int d = n - 1; d >= 0; d--) {
-    rstride[d] = sr;
-    sr *= shape[d];
-  }
-  for (int64_t r = 0; r < nslab; r++) {
-    int64_t e = meta->dtype_size;
-    for (int d = 0; d < n; d++) e *= ss[(size_t)(r * n + d)];
-    maxb = std::max(maxb, e);
-  }
-  (void)hipSetDevice(ctx->device);
-  hipStream_t s = stream_v ? (hipStream_t)stream_v : ctx->stream, s2 = nullptr;
-  void* ring[2] = {nullptr, nullptr};
-  size_t got[2] = {0, 0};
-  std::vector<zh_plan*> plans;
-  std::vector<hipEvent_t> evs;
-  int st = ZH_OK;
-  hipError_t he = hipStreamCreateWithFlags(&s2, hipStreamNonBlocking);
-  for (int k = 0; k < 2 && he == hipSuccess; k++) he = ctx_alloc(ctx, (size_t)maxb, &ring[k], &got[k]);
-  std::vector<hipEvent_t> decoded((size_t)nslab, nullptr), copied((size_t)nslab, nullptr);
-  for (int64_t r = 0; r < nslab && he == hipSuccess && st == ZH_OK; r++) {
-    const int64_t* o = &so[(size_t)(r * n)];
-    const int64_t* sh = &ss[(size_t)(r * n)];
-    int64_t base = 0, e = meta->dtype_size;
-    for (int d = 0; d < n; d++) {
-      base += (o[d] - offset[d]) * rstride[d];
-      e *= sh[d];
-    }
-    std::vector<zh_chunk_src> sub = slab_chunks(meta, chunks, offset, shape, o, sh);
-    zh_plan* p = nullptr;
-    st = zh_plan_create(ctx, meta, sub.data(), (int64_t)sub.size(), o, sh,
-                        (flags & ZH_SRC_DEVICE) | ZH_OUT_DEVICE, &p, err, errlen);
-    if (st != ZH_OK) break;
-    plans.push_back(p);
-    he = hipEventCreateWithFlags(&decoded[(size_t)r], hipEventDisableTiming);
-    if (he == hipSuccess) he = hipEventCreateWithFlags(&copied[(size_t)r], hipEventDisableTiming);
-    if (he != hipSuccess) break;
-    if (r >= 2) he = hipStreamWaitEvent(s, copied[(size_t)(r - 2)], 0);  // slot drained
-    if (he != hipSuccess) break;
-    st = zh_plan_execute(p, ring[r & 1], s);
-    if (st != ZH_OK) break;
-    he = hipEventRecord(decoded[(size_t)r], s);
-    if (he == hipSuccess) he = hipStreamWaitEvent(s2, decoded[(size_t)r], 0);
-    if (he == hipSuccess)
-      he = hipMemcpyAsync((uint8_t*)out + base * meta->dtype_size, ring[r & 1], (size_t)e,
-                          hipMemcpyDeviceToHost, s2);
-    if (he == hipSuccess) he = hipEventRecord(copied[(size_t)r], s2);
-  }
-  if (s2) (void)hipStreamSynchronize(s2);
-  (void)hipStreamSynchronize(s);
-  // status of every slab (deferred: the first failing slab in C order is reported)
-  for (size_t r = 0; r < plans.size(); r++) {
-    const int rc = zh_plan_wait(plans[r], st == ZH_OK && he == hipSuccess ? err : nullptr,
-                                st == ZH_OK && he == hipSuccess ? errlen : 0);
-    if (rc != ZH_OK && st == ZH_OK && he == hipSuccess) st = rc;
-  }
-  for (zh_plan* p : plans) plan_free(p);
-  for (auto ev : decoded)
-    if (ev) (void)hipEventDestroy(ev);
-  for (auto ev : copied)
-    if (ev) (void)hipEventDestroy(ev);
-  for (int k = 0; k < 2; k++)
-    if (ring[k]) ctx_release(ctx, ring[k], got[k]);
-  if (s2) (void)hipStreamDestroy(s2);
-  if (he != hipSuccess && st == ZH_OK) {
-    set_err(err, errlen, "HIP error %s (%s)", hipGetErrorName(he), hipGetErrorString(he));
-    st = he == hipErrorOutOfMemory ? ZH_ENOMEM : ZH_EHIP;
-  }
-  return st;
-}
-}  // namespace
-
-extern "C" {
-
-int zh_array_read(zh_ctx* ctx, const zh_array_meta* meta, const zh_chunk_src* chunks,
-                  int64_t nchunks, const int64_t* offset, const int64_t* shape, void* out,
-                  uint32_t flags, void* stream, char* err, size_t errlen) {
-  if (!ctx) return ZH_EINVAL;
-  std::lock_guard<std::mutex> lk(ctx->mu);
-  if (meta && offset && shape && out && !(flags & ZH_OUT_DEVICE) &&
-      env_int("ZH_HOST_SLABS", 1) != 0 && zh_validate_meta(meta, nullptr, 0) == ZH_OK) {
-    bool inside = true;
-    int64_t bytes = meta->dtype_size;
-    for (int d = 0; d < meta->ndim; d++) {
-      inside &= offset[d] >= 0 && shape[d] > 0 && offset[d] + shape[d] <= meta->shape[d];
-      bytes *= shape[d];
-    }
-    if (inside && bytes > host_slab_min()) {
-      const int st = array_read_host_slabs(ctx, meta, chunks, nchunks, offset, shape, out,
-                                           flags, stream, err, errlen);
-      if (st != ZH_EUNSUPPORTED) return st;
-    }
-  }
+int read_one_plan(zh_ctx* ctx, const zh_array_meta* meta, const SrcDesc* srcs, int64_t nsrc,
+                  const int64_t* offset, const int64_t* shape, void* out, uint32_t flags,
+                  void* stream, char* err, size_t errlen) {
   zh_plan* p = nullptr;
-  int st = zh_plan_create(ctx, meta, chunks, nchunks, offset, shape, flags, &p, err, errlen);
+  int st = plan_create(ctx, meta, srcs, nsrc, offset, shape, flags, false, &p, err, errlen);
   if (st != ZH_OK) return st;
   st = zh_plan_execute(p, out, stream);
   if (st != ZH_OK) {
@@ -1662,6 +1485,38 @@ int zh_array_read(zh_ctx* ctx, const zh_array_meta* meta, const zh_chunk_src* ch
   st = zh_plan_wait(p, err, errlen);
   plan_free(p);
   return st;
+}
+
+// A region read: large reads with a host side (host sources or a host output) go through the
+// pipelined path (H2D | decode | D2H per slab, zh_pipeline.cpp); everything else, and regions
+// that do not split, as one plan.
+int read_region(zh_ctx* ctx, const zh_array_meta* meta, const SrcDesc* srcs, int64_t nsrc,
+                const int64_t* offset, const int64_t* shape, void* out, uint32_t flags,
+                void* stream, char* err, size_t errlen) {
+  if (meta && offset && shape && out && env_int("ZH_PIPE", 1) != 0) {
+    const int st = read_pipelined(ctx, meta, srcs, nsrc, offset, shape, out, flags, stream, err,
+                                  errlen);
+    if (st != ZH_EUNSUPPORTED) return st;
+  }
+  return read_one_plan(ctx, meta, srcs, nsrc, offset, shape, out, flags, stream, err, errlen);
+}
+
+}  // namespace zh
+
+extern "C" {
+
+int zh_array_read(zh_ctx* ctx, const zh_array_meta* meta, const zh_chunk_src* chunks,
+                  int64_t nchunks, const int64_t* offset, const int64_t* shape, void* out,
+                  uint32_t flags, void* stream, char* err, size_t errlen) {
+  if (!ctx) return ZH_EINVAL;
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  std::vector<SrcDesc> srcs((size_t)std::max<int64_t>(0, nchunks));
+  for (int64_t i = 0; chunks && i < nchunks; i++) {
+    srcs[(size_t)i].data = (const uint8_t*)chunks[i].data;
+    srcs[(size_t)i].nbytes = chunks[i].nbytes;
+  }
+  return read_region(ctx, meta, chunks ? srcs.data() : nullptr, nchunks, offset, shape, out,
+                     flags, stream, err, errlen);
 }
 
 }  // extern "C"
@@ -1798,11 +1653,14 @@ int zh_array_read_multi(zh_ctx* const* ctxs, int ndev, int root, const zh_array_
                                     flags, nullptr, err, errlen);
 }
 
-int zh_array_read_multi_routed(zh_ctx* const* ctxs, int ndev, int root,
-                               const zh_array_meta* meta, const zh_chunk_src* chunks,
-                               int64_t nchunks, const int64_t* offset, const int64_t* shape,
-                               void* out, uint32_t flags, int32_t* slab_route, char* err,
-                               size_t errlen) {
+}  // extern "C"
+
+namespace zh {
+
+int read_multi_impl(zh_ctx* const* ctxs, int ndev, int root, const zh_array_meta* meta,
+                    const SrcDesc* chunks, int64_t nchunks, const int64_t* offset,
+                    const int64_t* shape, void* out, uint32_t flags, int32_t* slab_route,
+                    char* err, size_t errlen) {
   if (slab_route)
     for (int k = 0; k < ndev; k++) slab_route[k] = ZH_ROUTE_DIRECT;
   if (!ctxs || ndev <= 0 || root < 0 || root >= ndev || !meta || !offset || !shape || !out)
@@ -1867,7 +1725,8 @@ int zh_array_read_multi_routed(zh_ctx* const* ctxs, int ndev, int root,
     // this slab's chunks, picked out of the caller's (full region) list
     int64_t st0[kMaxDims], cnt[kMaxDims];
     const int64_t m = chunk_coords(n, meta->chunk_shape, o, s, st0, cnt);
-    std::vector<zh_chunk_src> sub((size_t)m);
+    std::vector<SrcDesc> sub((size_t)m);
+    std::vector<std::vector<zh_shard_piece>> moved;  // pieces restaged on this device
     int64_t cur[kMaxDims] = {0};
     for (int64_t i = 0; i < m; i++) {
       int64_t lin = 0;
@@ -1891,30 +1750,52 @@ int zh_array_read_multi_routed(zh_ctx* const* ctxs, int ndev, int root,
     const char* fenv = getenv("ZH_MULTI_FORCE_STAGED");
     const bool force = fenv && fenv[0] == '1' && ctx != ctxs[root];
     if (flags & ZH_SRC_DEVICE) {
-      for (auto& c : sub) {
-        if (!c.data || c.nbytes <= 0) continue;
-        const int sdev = pointer_device(c.data);
-        if (sdev < 0 || (sdev == ctx->device && !force)) continue;
+      // a device range on another device: read over xGMI when the pair has peer access,
+      // else copied here first (a whole object, or a sub-shard form's index and pieces)
+      auto localize = [&](const void* p, int64_t nb, const void** to) -> bool {
+        if (!p || nb <= 0) return true;
+        const int sdev = pointer_device(p);
+        if (sdev < 0 || (sdev == ctx->device && !force)) return true;
         if (!force && enable_peer(ctx->device, sdev)) {
           route |= ZH_ROUTE_SRC_PEER;
-          continue;
+          return true;
         }
         void* loc = nullptr;
-        if (hipMalloc(&loc, (size_t)c.nbytes) != hipSuccess) {
+        if (hipMalloc(&loc, (size_t)nb) != hipSuccess) {
           (void)hipGetLastError();
           rc = ZH_ENOMEM;
           snprintf(e, sizeof(e), "hipMalloc of a staged chunk on device %d failed", ctx->device);
-          break;
+          return false;
         }
         staged.push_back(loc);
-        rc = staged_copy(loc, ctx->device, c.data, sdev, (size_t)c.nbytes);
+        rc = staged_copy(loc, ctx->device, p, sdev, (size_t)nb);
         if (rc != ZH_OK) {
           snprintf(e, sizeof(e), "staging a chunk from device %d to %d failed", sdev,
                    ctx->device);
-          break;
+          return false;
         }
-        c.data = loc;
+        *to = loc;
         route |= ZH_ROUTE_SRC_STAGED;
+        return true;
+      };
+      for (auto& c : sub) {
+        const void* p = c.data;
+        if (!localize(c.data, c.nbytes, &p)) break;
+        c.data = (const uint8_t*)p;
+        p = c.index;
+        if (!localize(c.index, c.index_nbytes, &p)) break;
+        c.index = (const uint8_t*)p;
+        if (c.npieces > 0) {
+          moved.emplace_back(c.pieces, c.pieces + c.npieces);
+          bool ok = true;
+          for (auto& q : moved.back()) {
+            const void* qp = q.data;
+            if (!(ok = localize(q.data, q.data_nbytes, &qp))) break;
+            q.data = qp;
+          }
+          if (!ok) break;
+          c.pieces = moved.back().data();
+        }
       }
     }
     const bool remote = out_dev && ctx != ctxs[root];  // decode locally, then deliver
@@ -1933,18 +1814,23 @@ int zh_array_read_multi_routed(zh_ctx* const* ctxs, int ndev, int root,
     }
     zh_plan* p = nullptr;
     uint32_t pf = (flags & ZH_SRC_DEVICE) | (out_dev ? ZH_OUT_DEVICE : 0u);
-    if (rc == ZH_OK) rc = zh_plan_create(ctx, meta, sub.data(), m, o, s, pf, &p, e, sizeof(e));
-    if (rc == ZH_OK) rc = zh_plan_execute(p, remote ? local : (void*)dst, nullptr);
-    if (rc == ZH_OK && (oroute == ZH_ROUTE_PEER || oroute == ZH_ROUTE_SAME) &&
-        hipMemcpyPeerAsync(dst, rdev, local, ctx->device, sbytes, ctx->stream) != hipSuccess) {
-      (void)hipGetLastError();
-      rc = ZH_EHIP;
-      snprintf(e, sizeof(e), "slab copy to device %d failed", rdev);
-    }
-    if (rc == ZH_OK) rc = zh_plan_wait(p, e, sizeof(e));
-    if (rc == ZH_OK && oroute == ZH_ROUTE_STAGED) {
-      rc = staged_copy(dst, rdev, local, ctx->device, sbytes);
-      if (rc != ZH_OK) snprintf(e, sizeof(e), "staged slab copy to device %d failed", rdev);
+    if (rc == ZH_OK && !remote) {
+      // straight into its destination: the region read itself (large host slabs pipelined)
+      rc = read_region(ctx, meta, sub.data(), m, o, s, dst, pf, nullptr, e, sizeof(e));
+    } else {
+      if (rc == ZH_OK) rc = plan_create(ctx, meta, sub.data(), m, o, s, pf, false, &p, e, sizeof(e));
+      if (rc == ZH_OK) rc = zh_plan_execute(p, local, nullptr);
+      if (rc == ZH_OK && (oroute == ZH_ROUTE_PEER || oroute == ZH_ROUTE_SAME) &&
+          hipMemcpyPeerAsync(dst, rdev, local, ctx->device, sbytes, ctx->stream) != hipSuccess) {
+        (void)hipGetLastError();
+        rc = ZH_EHIP;
+        snprintf(e, sizeof(e), "slab copy to device %d failed", rdev);
+      }
+      if (rc == ZH_OK) rc = zh_plan_wait(p, e, sizeof(e));
+      if (rc == ZH_OK && oroute == ZH_ROUTE_STAGED) {
+        rc = staged_copy(dst, rdev, local, ctx->device, sbytes);
+        if (rc != ZH_OK) snprintf(e, sizeof(e), "staged slab copy to device %d failed", rdev);
+      }
     }
     if (p) plan_free(p);
     (void)hipSetDevice(ctx->device);
@@ -1963,6 +1849,24 @@ int zh_array_read_multi_routed(zh_ctx* const* ctxs, int ndev, int root,
       return status[r];
     }
   return ZH_OK;
+}
+
+}  // namespace zh
+
+extern "C" {
+
+int zh_array_read_multi_routed(zh_ctx* const* ctxs, int ndev, int root,
+                               const zh_array_meta* meta, const zh_chunk_src* chunks,
+                               int64_t nchunks, const int64_t* offset, const int64_t* shape,
+                               void* out, uint32_t flags, int32_t* slab_route, char* err,
+                               size_t errlen) {
+  std::vector<SrcDesc> srcs((size_t)std::max<int64_t>(0, nchunks));
+  for (int64_t i = 0; chunks && i < nchunks; i++) {
+    srcs[(size_t)i].data = (const uint8_t*)chunks[i].data;
+    srcs[(size_t)i].nbytes = chunks[i].nbytes;
+  }
+  return read_multi_impl(ctxs, ndev, root, meta, chunks ? srcs.data() : nullptr, nchunks, offset,
+                         shape, out, flags, slab_route, err, errlen);
 }
 
 // ShardingIndexedCodec.decode / decodePartial: one shard viewed as a one-chunk array.

@@ -46,12 +46,27 @@ __host__ __device__ inline uint32_t fdiv(uint32_t n, const FastDiv& f) {
   return (uint32_t)(((uint64_t)n * f.m) >> f.s);
 }
 
+// One byte range of a stored shard the device holds (sub-shard reads: the index and the
+// referenced ranges only, zh_array_read_pieces / compact host staging).  Entry (off, nb) of
+// the stored index is served by the piece with p.off <= off and off + nb <= p.off + p.len,
+// read at p.src + (off - p.off).  A piece with dlen != len is exactly one inner chunk whose
+// host byte-to-byte stages were undone: it serves only (p.off, p.len) and holds dlen bytes.
+struct DevPiece {
+  uint64_t off;
+  uint64_t len;
+  const uint8_t* src;
+  uint64_t dlen;
+};
+
 // One stored chunk object (a shard when sharded) touched by a region.
 struct DevShard {
-  const uint8_t* data;      // decode: encoded bytes (nullptr: key missing → fill_value)
+  const uint8_t* data;      // decode: encoded bytes (nullptr: key missing → fill_value); with
+                            // pieces: the stored index (index_off 0)
   uint8_t* wdata;           // encode: destination buffer
-  int64_t nbytes;           // decode: object size
+  int64_t nbytes;           // decode: object size (StoreHandle.getSize(); INT64_MAX unknown)
   int64_t index_off;        // decode (sharded): byte offset of the index entries
+  const DevPiece* pieces;   // decode: sorted, disjoint byte ranges held (nullptr: the whole
+  int64_t npieces;          //   object is at data)
   int64_t item_begin;       // prefix sum of inner-chunk items before this shard
   int64_t out_base;         // element offset of part_lo inside the region buffer
   int32_t box_start[kMaxDims];  // first inner-chunk coordinate of the box

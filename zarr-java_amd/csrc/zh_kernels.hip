@@ -204,9 +204,44 @@ __device__ __forceinline__ void index_entry(const ScatterArgs& a, const DevShard
   nb = ld_u64_unaligned(ent + 8, a.index_be);
 }
 
-// Builds the geometry of work item `item` (returns the shard slot).
+// Device address of the stored range [off, off + nb) of shard S (range-checked against the
+// object size by the caller).  Without a piece table the object is whole at S.data.  With
+// one (sub-shard reads: StoreHandleDataProvider.read(off, nb), ShardingIndexedCodec.java:
+// 226-230, 353-356) the range must lie inside one piece; a host-decoded piece serves exactly
+// its own range and *nb becomes its payload length.  false: no piece holds the range → the
+// reference's "Could not load byte data for chunk".
+__device__ __forceinline__ bool piece_src(const DevShard& S, uint64_t off, uint64_t& nb,
+                                          const uint8_t*& src) {
+  if (S.pieces == nullptr) {
+    src = S.data + off;
+    return true;
+  }
+  int64_t lo = 0, hi = S.npieces - 1;
+  if (hi < 0 || S.pieces[0].off > off) return false;
+  while (lo < hi) {  // last piece with p.off <= off
+    const int64_t mid = (lo + hi + 1) >> 1;
+    if (S.pieces[mid].off <= off) lo = mid;
+    else hi = mid - 1;
+  }
+  const DevPiece P = S.pieces[lo];
+  const uint64_t rel = off - P.off;
+  if (P.dlen != P.len) {  // one host-decoded inner chunk
+    if (rel != 0 || nb != P.len) return false;
+    nb = P.dlen;
+    src = P.src;
+    return true;
+  }
+  if (rel > P.len || nb > P.len - rel) return false;
+  src = P.src + rel;
+  return true;
+}
+
+// Builds the geometry of work item `item` (returns the shard slot).  Decode (the generic
+// kernel's clipped items): source, fill and mode come from the item's descriptor `D`, which
+// the resolve kernel wrote after parsing and validating the index entry.
 template <bool ENC>
-__device__ __forceinline__ int64_t make_item(const ScatterArgs& a, int64_t item, Item& it) {
+__device__ __forceinline__ int64_t make_item(const ScatterArgs& a, int64_t item, Item& it,
+                                             const ItemDesc* D = nullptr) {
   const int n = a.ndim;
   const int64_t citem = item >> a.piece_shift;
   it.piece = (uint32_t)(item & ((1ll << a.piece_shift) - 1));
@@ -229,43 +264,15 @@ __device__ __forceinline__ int64_t make_item(const ScatterArgs& a, int64_t item,
   it.mode = kCopy;
   it.fill = 0;
   if constexpr (!ENC) {
-    if (S.data == nullptr) {
-      // missing shard: region keeps fill_value (M/core/Array.java:400-402, 419-421)
-      it.mode = kFill;
-      it.fill = a.fill;
-      it.sbase = nullptr;
-    } else if (a.sharded) {
-      int64_t lin = 0;
-#pragma unroll
-      for (int d = 0; d < kMaxDims; d++)
-        if (d < n) lin += (int64_t)ic[d] * a.cps_stride[d];
-      uint64_t off, nb;
-      index_entry(a, S, lin, off, nb);
-      if (off == ~0ull || nb == ~0ull) {
-        // missing inner chunk: the zero-initialised part array shows through (Q1,
-        // ShardingIndexedCodec.java:189, 219-221)
-        it.mode = kFill;
-        it.fill = 0;
-        it.sbase = nullptr;
-      } else {
-        const uint64_t total = (uint64_t)S.nbytes;
-        const bool range_ok = off <= total && nb <= total - off;
-        if (!range_ok || nb != (uint64_t)(a.inner_nbytes + a.crc_extra)) {
-          if (threadIdx.x == 0 && it.piece == 0) {
-            const uint32_t kind = range_ok ? kFlagLength : kFlagRange;
-            const uint64_t key = ((uint64_t)(0xFFFFFFFFu - (uint32_t)lin) << 8) | kind;
-            atomicOr((unsigned long long*)(a.status + s * kStWords + kStFlags),
-                     (unsigned long long)kind);
-            atomicMax((unsigned long long*)(a.status + s * kStWords + kStBadChunk),
-                      (unsigned long long)key);
-          }
-          it.mode = kSkip;
-          return s;
-        }
-        it.sbase = S.data + off;
-      }
+    // kDescClip: src != 0 copies; src == 0 keeps the constant the resolve kernel chose
+    // (fill_value for a missing shard, M/core/Array.java:400-402, 419-421; 0 for a missing
+    // inner chunk, Q1, ShardingIndexedCodec.java:189, 219-221)
+    if (D->src != 0) {
+      it.sbase = (const uint8_t*)(uintptr_t)D->src;
     } else {
-      it.sbase = S.data;  // object size validated on the host
+      it.mode = kFill;
+      it.fill = D->fill;
+      it.sbase = nullptr;
     }
     it.dbase = a.region;
     int64_t s0 = 0, d0 = S.out_base;
@@ -663,7 +670,8 @@ __device__ __forceinline__ ItemDesc resolve_one(const ScatterArgs& a, int64_t ci
       return D;
     }
     const uint64_t total = (uint64_t)S.nbytes;
-    const bool range_ok = off <= total && nb <= total - off;
+    bool range_ok = off <= total && nb <= total - off;
+    if (range_ok) range_ok = piece_src(S, off, nb, src);  // sub-shard reads: the held pieces
     if (!range_ok || nb != (uint64_t)(a.inner_nbytes + a.crc_extra)) {
       const uint32_t kind = range_ok ? kFlagLength : kFlagRange;
       const uint64_t key = ((uint64_t)(0xFFFFFFFFu - (uint32_t)lin) << 8) | kind;
@@ -673,7 +681,6 @@ __device__ __forceinline__ ItemDesc resolve_one(const ScatterArgs& a, int64_t ci
       D.kind = kDescSkip;
       return D;
     }
-    src = S.data + off;
   }
   D.src = (uint64_t)(uintptr_t)src;
   D.kind = full ? kDescFullCopy : kDescClip;
@@ -2148,8 +2155,7 @@ __global__ __launch_bounds__(kBlock) void decode_slow_kernel(ScatterArgs a) {
     const ItemDesc D = ld_desc(a.desc + citem);
     Item it;
     if ((D.kind & kDescModeMask) == kDescClip) {
-      make_item<false>(a, ((int64_t)citem << a.piece_shift) | piece, it);
-      if (it.mode == kSkip) continue;
+      make_item<false>(a, ((int64_t)citem << a.piece_shift) | piece, it, &D);
     } else {
       full_item(a, D, piece, it);
     }
@@ -2747,11 +2753,13 @@ __global__ __launch_bounds__(kBlock) void nested_index_kernel(NestArgs a) {
     const uint64_t nb1 = ld_u64_unaligned(ent + 8, a.index_be);
     const uint64_t total = (uint64_t)S.nbytes;
     bool ok = !(off1 == ~0ull || nb1 == ~0ull);  // missing sub-shard: zeros (Q1)
-    if (ok && !(off1 <= total && nb1 <= total - off1 && nb1 >= (uint64_t)a.sub_isz)) {
+    const uint8_t* sub = nullptr;
+    uint64_t held = nb1;  // the sub-shard must be held whole (sub-shard reads: one piece)
+    if (ok && !(off1 <= total && nb1 <= total - off1 && nb1 >= (uint64_t)a.sub_isz &&
+                piece_src(S, off1, held, sub) && held == nb1)) {
       if (tid == 0) nest_error(a, lo, (uint32_t)lin1, kFlagRange | kFlagL1);
       ok = false;
     }
-    const uint8_t* sub = S.data + off1;
     const uint8_t* ib = ok ? (a.sub_start ? sub : sub + nb1 - a.sub_isz) : nullptr;
     if (ok && a.sub_crc) {  // Crc32cCodec.decode on the sub-shard index (:24-48)
       const int64_t len = a.sub_isz - 4;

@@ -243,6 +243,255 @@ JNIEXPORT jint JNICALL Java_dev_zarr_zarrjava_hip_ZarrHip_shardDecodePartial(
   return 0;
 }
 
+/* ---- sub-shard reads: stored index + pieces (zh_array_read_pieces) ---------------------
+ * Pure argument marshalling: every index and piece byte[] is copied once into the context's
+ * page-locked staging (zh_host_staging), the decoded region comes back through the same
+ * staging (direct DMA both ways) and is copied once into the Java array.  The index is never
+ * read here; the device checks it.  tests/helpers.py jni_fetch/jni_read restate this sequence
+ * in ctypes and the GPU tests run it (tests/test_gpu_pieces.py). */
+
+JNIEXPORT jlongArray JNICALL Java_dev_zarr_zarrjava_hip_ZarrHip_shardRanges(
+    JNIEnv* env, jclass cls, jintArray jm, jlongArray jshape, jintArray jchunk, jintArray jinner,
+    jintArray jorder, jbyteArray jfill, jbyteArray jindex, jlong size, jlongArray jlo,
+    jlongArray jhi, jlong max_run) {
+  (void)cls;
+  zh_array_meta m;
+  if (build_meta(env, jm, jshape, jchunk, jinner, jorder, jfill, &m) != ZH_OK) {
+    throw_status(env, ZH_EINVAL, "bad array metadata");
+    return NULL;
+  }
+  jsize ilen = (*env)->GetArrayLength(env, jindex);
+  void* idx = malloc((size_t)(ilen > 0 ? ilen : 1));
+  jlong lo[ZH_MAX_DIMS], hi[ZH_MAX_DIMS];
+  int64_t lo64[ZH_MAX_DIMS], hi64[ZH_MAX_DIMS];
+  if (!idx) {
+    throw_status(env, ZH_ENOMEM, "out of host memory for the shard index");
+    return NULL;
+  }
+  (*env)->GetByteArrayRegion(env, jindex, 0, ilen, (jbyte*)idx);
+  (*env)->GetLongArrayRegion(env, jlo, 0, m.ndim, lo);
+  (*env)->GetLongArrayRegion(env, jhi, 0, m.ndim, hi);
+  for (int d = 0; d < m.ndim; d++) {
+    lo64[d] = lo[d];
+    hi64[d] = hi[d];
+  }
+  const int64_t n = zh_shard_ranges(&m, idx, ilen, size, lo64, hi64, max_run, NULL, 0);
+  jlongArray res = NULL;
+  if (n < 0) {
+    throw_status(env, (int)-n, "zh_shard_ranges: invalid shard index or part");
+  } else {
+    int64_t* r = (int64_t*)malloc((size_t)(2 * n > 0 ? 2 * n : 1) * sizeof(int64_t));
+    if (r && zh_shard_ranges(&m, idx, ilen, size, lo64, hi64, max_run, r, n) == n) {
+      res = (*env)->NewLongArray(env, (jsize)(2 * n));
+      if (res) (*env)->SetLongArrayRegion(env, res, 0, (jsize)(2 * n), (const jlong*)r);
+    } else {
+      throw_status(env, ZH_ENOMEM, "out of host memory for the shard ranges");
+    }
+    free(r);
+  }
+  free(idx);
+  return res;
+}
+
+/* The shards of a read into zh_shard_src form, their bytes copied into `staging` (which has
+ * room for them: the caller sized it with pieces_bytes). */
+static jlong pieces_bytes(JNIEnv* env, jobjectArray jidx, jobjectArray jdata) {
+  jsize n = (*env)->GetArrayLength(env, jidx);
+  jlong tot = 0;
+  for (jsize i = 0; i < n; i++) {
+    jbyteArray ib = (jbyteArray)(*env)->GetObjectArrayElement(env, jidx, i);
+    if (ib) tot += (*env)->GetArrayLength(env, ib);
+    if (ib) (*env)->DeleteLocalRef(env, ib);
+    jobjectArray ps = (jobjectArray)(*env)->GetObjectArrayElement(env, jdata, i);
+    jsize np = ps ? (*env)->GetArrayLength(env, ps) : 0;
+    for (jsize k = 0; k < np; k++) {
+      jbyteArray b = (jbyteArray)(*env)->GetObjectArrayElement(env, ps, k);
+      if (b) tot += (*env)->GetArrayLength(env, b);
+      if (b) (*env)->DeleteLocalRef(env, b);
+    }
+    if (ps) (*env)->DeleteLocalRef(env, ps);
+  }
+  return tot;
+}
+
+static int marshal_pieces(JNIEnv* env, jobjectArray jidx, jlongArray jsizes, jobjectArray joffs,
+                          jobjectArray jlens, jobjectArray jdata, uint8_t* staging,
+                          zh_shard_src* srcs, zh_shard_piece** pieces_out) {
+  jsize n = (*env)->GetArrayLength(env, jidx);
+  jsize total_pieces = 0;
+  for (jsize i = 0; i < n; i++) {
+    jobjectArray ps = (jobjectArray)(*env)->GetObjectArrayElement(env, jdata, i);
+    if (ps) total_pieces += (*env)->GetArrayLength(env, ps);
+    if (ps) (*env)->DeleteLocalRef(env, ps);
+  }
+  zh_shard_piece* pc = (zh_shard_piece*)calloc((size_t)(total_pieces > 0 ? total_pieces : 1),
+                                               sizeof(zh_shard_piece));
+  if (!pc) return ZH_ENOMEM;
+  *pieces_out = pc;
+  jlong pos = 0;
+  jsize used = 0;
+  for (jsize i = 0; i < n; i++) {
+    memset(&srcs[i], 0, sizeof(srcs[i]));
+    jlong size = -1;
+    (*env)->GetLongArrayRegion(env, jsizes, i, 1, &size);
+    srcs[i].shard_nbytes = size;
+    jbyteArray ib = (jbyteArray)(*env)->GetObjectArrayElement(env, jidx, i);
+    if (ib) {
+      jsize len = (*env)->GetArrayLength(env, ib);
+      (*env)->GetByteArrayRegion(env, ib, 0, len, (jbyte*)(staging + pos));
+      srcs[i].index = staging + pos;
+      srcs[i].index_nbytes = len;
+      pos += len;
+      (*env)->DeleteLocalRef(env, ib);
+    }
+    jobjectArray ps = (jobjectArray)(*env)->GetObjectArrayElement(env, jdata, i);
+    jlongArray po = (jlongArray)(*env)->GetObjectArrayElement(env, joffs, i);
+    jlongArray pl = (jlongArray)(*env)->GetObjectArrayElement(env, jlens, i);
+    jsize np = ps ? (*env)->GetArrayLength(env, ps) : 0;
+    srcs[i].pieces = pc + used;
+    srcs[i].npieces = np;
+    for (jsize k = 0; k < np; k++) {
+      jbyteArray b = (jbyteArray)(*env)->GetObjectArrayElement(env, ps, k);
+      jlong off = 0, nb = 0;
+      (*env)->GetLongArrayRegion(env, po, k, 1, &off);
+      (*env)->GetLongArrayRegion(env, pl, k, 1, &nb);
+      jsize len = b ? (*env)->GetArrayLength(env, b) : 0;
+      if (b) (*env)->GetByteArrayRegion(env, b, 0, len, (jbyte*)(staging + pos));
+      pc[used + k].offset = off;
+      pc[used + k].nbytes = nb;
+      pc[used + k].data = staging + pos;
+      pc[used + k].data_nbytes = len;
+      pos += len;
+      if (b) (*env)->DeleteLocalRef(env, b);
+    }
+    used += np;
+    if (ps) (*env)->DeleteLocalRef(env, ps);
+    if (po) (*env)->DeleteLocalRef(env, po);
+    if (pl) (*env)->DeleteLocalRef(env, pl);
+  }
+  return ZH_OK;
+}
+
+/* The decoded region from the staging into the primitive array behind the ucar.ma2.Array. */
+static int copy_out(JNIEnv* env, jobject out, const void* src, size_t obytes, char* err,
+                    size_t errlen) {
+  void* dst = (*env)->GetPrimitiveArrayCritical(env, (jarray)out, NULL);
+  if (!dst) {
+    snprintf(err, errlen, "could not access the output array");
+    return ZH_ENOMEM;
+  }
+  memcpy(dst, src, obytes);
+  (*env)->ReleasePrimitiveArrayCritical(env, (jarray)out, dst, 0);
+  return ZH_OK;
+}
+
+JNIEXPORT jint JNICALL Java_dev_zarr_zarrjava_hip_ZarrHip_arrayReadPieces(
+    JNIEnv* env, jclass cls, jlongArray jctxs, jintArray jm, jlongArray jshape,
+    jintArray jchunk, jintArray jinner, jintArray jorder, jbyteArray jfill, jobjectArray jidx,
+    jlongArray jsizes, jobjectArray joffs, jobjectArray jlens, jobjectArray jdata,
+    jlongArray joffset, jlongArray jregion, jobject out) {
+  (void)cls;
+  zh_array_meta m;
+  int st = build_meta(env, jm, jshape, jchunk, jinner, jorder, jfill, &m);
+  if (st != ZH_OK) return st;
+  char err[1024] = {0};
+  st = zh_validate_meta(&m, err, sizeof err);
+  if (st == ZH_EUNSUPPORTED) return st;
+  if (st != ZH_OK) return throw_status(env, st, err);
+  jsize k = (*env)->GetArrayLength(env, jctxs);
+  if (k <= 0 || k > 64) return throw_status(env, ZH_EINVAL, "bad device context list");
+  jlong raw[64];
+  zh_ctx* ctxs[64];
+  (*env)->GetLongArrayRegion(env, jctxs, 0, k, raw);
+  for (jsize i = 0; i < k; i++) ctxs[i] = (zh_ctx*)(intptr_t)raw[i];
+  jlong off[ZH_MAX_DIMS], reg[ZH_MAX_DIMS];
+  int64_t o64[ZH_MAX_DIMS], r64[ZH_MAX_DIMS];
+  (*env)->GetLongArrayRegion(env, joffset, 0, m.ndim, off);
+  (*env)->GetLongArrayRegion(env, jregion, 0, m.ndim, reg);
+  int64_t nel = 1;
+  for (int d = 0; d < m.ndim; d++) {
+    o64[d] = off[d];
+    r64[d] = reg[d];
+    nel *= r64[d];
+  }
+  if ((int64_t)(*env)->GetArrayLength(env, (jarray)out) != nel)
+    return throw_status(env, ZH_EINVAL, "output array size does not match the region");
+  const size_t obytes = (size_t)nel * (size_t)m.dtype_size;
+  const jlong in_bytes = pieces_bytes(env, jidx, jdata);
+  const size_t in_cap = ((size_t)in_bytes + 255) & ~(size_t)255;
+  void* staging = NULL;
+  st = zh_host_staging(ctxs[0], in_cap + obytes, &staging);
+  if (st != ZH_OK) return throw_status(env, st, "page-locked staging: allocation failed");
+  jsize n = (*env)->GetArrayLength(env, jidx);
+  zh_shard_src* srcs = (zh_shard_src*)calloc((size_t)(n > 0 ? n : 1), sizeof(zh_shard_src));
+  zh_shard_piece* pcs = NULL;
+  st = srcs ? marshal_pieces(env, jidx, jsizes, joffs, jlens, jdata, (uint8_t*)staging, srcs, &pcs)
+            : ZH_ENOMEM;
+  uint8_t* dst = (uint8_t*)staging + in_cap;
+  if (st == ZH_OK)
+    st = k == 1 ? zh_array_read_pieces(ctxs[0], &m, srcs, n, o64, r64, dst, 0, NULL, err, sizeof err)
+                : zh_array_read_pieces_multi(ctxs, (int)k, 0, &m, srcs, n, o64, r64, dst, 0, NULL,
+                                             err, sizeof err);
+  if (st == ZH_OK) st = copy_out(env, out, dst, obytes, err, sizeof err);
+  free(pcs);
+  free(srcs);
+  if (st == ZH_EUNSUPPORTED) return st;
+  if (st != ZH_OK) return throw_status(env, st, err);
+  return 0;
+}
+
+JNIEXPORT jint JNICALL Java_dev_zarr_zarrjava_hip_ZarrHip_shardDecodePieces(
+    JNIEnv* env, jclass cls, jlong ctx, jintArray jm, jlongArray jshape, jintArray jchunk,
+    jintArray jinner, jintArray jorder, jbyteArray jfill, jbyteArray jindex, jlong size,
+    jlongArray joffs, jlongArray jlens, jobjectArray jdata, jlongArray joffset, jintArray jpart,
+    jobject out) {
+  (void)cls;
+  zh_array_meta m;
+  int st = build_meta(env, jm, jshape, jchunk, jinner, jorder, jfill, &m);
+  if (st != ZH_OK) return st;
+  char err[1024] = {0};
+  jlong off[ZH_MAX_DIMS];
+  jint part[ZH_MAX_DIMS];
+  (*env)->GetLongArrayRegion(env, joffset, 0, m.ndim, off);
+  (*env)->GetIntArrayRegion(env, jpart, 0, m.ndim, part);
+  int64_t o64[ZH_MAX_DIMS], nel = 1;
+  for (int d = 0; d < m.ndim; d++) {
+    o64[d] = off[d];
+    nel *= part[d];
+  }
+  if ((int64_t)(*env)->GetArrayLength(env, (jarray)out) != nel)
+    return throw_status(env, ZH_EINVAL, "output array size does not match the part shape");
+  const size_t obytes = (size_t)nel * (size_t)m.dtype_size;
+  /* one shard: wrap its arrays as the one-element arrays of the read form */
+  jclass bcls = (*env)->FindClass(env, "[B"), lcls = (*env)->FindClass(env, "[J"),
+         bbcls = (*env)->FindClass(env, "[[B");
+  jobjectArray jidx = (*env)->NewObjectArray(env, 1, bcls, jindex);
+  jobjectArray jo = (*env)->NewObjectArray(env, 1, lcls, joffs);
+  jobjectArray jl = (*env)->NewObjectArray(env, 1, lcls, jlens);
+  jobjectArray jd = (*env)->NewObjectArray(env, 1, bbcls, jdata);
+  jlongArray js = (*env)->NewLongArray(env, 1);
+  if (!jidx || !jo || !jl || !jd || !js) return throw_status(env, ZH_ENOMEM, "out of memory");
+  (*env)->SetLongArrayRegion(env, js, 0, 1, &size);
+  const jlong in_bytes = pieces_bytes(env, jidx, jd);
+  const size_t in_cap = ((size_t)in_bytes + 255) & ~(size_t)255;
+  void* staging = NULL;
+  zh_ctx* c = (zh_ctx*)(intptr_t)ctx;
+  st = zh_host_staging(c, in_cap + obytes, &staging);
+  if (st != ZH_OK) return throw_status(env, st, "page-locked staging: allocation failed");
+  zh_shard_src src;
+  zh_shard_piece* pcs = NULL;
+  st = marshal_pieces(env, jidx, js, jo, jl, jd, (uint8_t*)staging, &src, &pcs);
+  uint8_t* dst = (uint8_t*)staging + in_cap;
+  if (st == ZH_OK)
+    st = zh_sharding_decode_pieces(c, &m, &src, o64, (const int32_t*)part, dst, 0, NULL, err,
+                                   sizeof err);
+  if (st == ZH_OK) st = copy_out(env, out, dst, obytes, err, sizeof err);
+  free(pcs);
+  if (st == ZH_EUNSUPPORTED) return st;
+  if (st != ZH_OK) return throw_status(env, st, err);
+  return 0;
+}
+
 /* core.Array.write replacement for a region of whole chunks (clipped only by the array
  * boundary): data = the primitive array of the region in C order (ucar storage copied to
  * 1-D); returns byte[][] in computeChunkCoords order, null = chunk all fill_value (the

@@ -86,6 +86,13 @@ final class DeviceChain {
         return true;
     }
 
+    /** ShardingIndexedCodec.getShardIndexSize (:176-181): 16 per inner chunk (+ 4 crc32c). */
+    long indexSize() {
+        long n = 1;
+        for (int d = 0; d < meta[0]; d++) n *= chunkShape[d] / innerShape[d];
+        return 16 * n + (meta[7] == 1 ? 4 : 0);
+    }
+
     /** The raw `bytes` payload of one stored chunk: the host stages decoded in reverse order. */
     byte[] hostDecode(byte[] stored) throws ZarrException {
         ByteBuffer b = ByteBuffer.wrap(stored);

@@ -10,12 +10,18 @@ import dev.zarr.zarrjava.v3.ArrayMetadata;
 import javax.annotation.Nonnull;
 import java.io.IOException;
 import java.nio.ByteBuffer;
+import java.util.stream.IntStream;
 
 /**
  * v3.Array whose {@code read(offset, shape, parallel)} hands every chunk/shard of the
  * region to the device in ONE native call (thousands of inner chunks per launch) instead
  * of the per-shard ForkJoin loop of core.Array.read (M/core/Array.java:378-441).
  * Unsupported chains use {@code super.read}.
+ *
+ * The store I/O keeps the reference's shape and parallelism (the chunk loop runs as a
+ * parallel stream, M/core/Array.java:403-407): a whole shard is one read; a sub-shard part is
+ * its stored index plus the ranges it references (ShardPieces, StoreHandleDataProvider
+ * semantics).  The index is checked on the device.
  */
 public class HipArray extends Array {
     private final DeviceChain chain;
@@ -42,42 +48,60 @@ public class HipArray extends Array {
                 throw new ZarrException("Requested data is outside of the array's domain.");
             }
         }
-        int[] cs = md.chunkShape();
-        long[][] coords = IndexingUtils.computeChunkCoords(md.shape, cs, offset, shape);
-        byte[][] chunks = new byte[coords.length][];
-        for (int i = 0; i < coords.length; i++) {
-            StoreHandle h = storeHandle.resolve(md.chunkKeyEncoding().encodeChunkKey(coords[i]));
-            if (chain.meta[3] == 1) {  // the part of this shard the region covers
-                long[] lo = new long[cs.length], hi = new long[cs.length];
-                for (int d = 0; d < cs.length; d++) {
-                    long c0 = coords[i][d] * cs[d];
-                    lo[d] = Math.max(offset[d], c0) - c0;
-                    hi[d] = Math.min(offset[d] + shape[d], c0 + cs[d]) - c0;
+        final int[] cs = md.chunkShape();
+        final long[][] coords = IndexingUtils.computeChunkCoords(md.shape, cs, offset, shape);
+        final boolean sharded = chain.meta[3] == 1;
+        final ShardPieces[] shards = new ShardPieces[coords.length];
+        final byte[][] chunks = new byte[coords.length][];
+        IntStream loop = IntStream.range(0, coords.length);
+        try {
+            (parallel ? loop.parallel() : loop).forEach(i -> {
+                StoreHandle h = storeHandle.resolve(md.chunkKeyEncoding().encodeChunkKey(coords[i]));
+                try {
+                    if (sharded) {
+                        long[] lo = new long[cs.length], hi = new long[cs.length];
+                        for (int d = 0; d < cs.length; d++) {
+                            long c0 = coords[i][d] * cs[d];
+                            lo[d] = Math.max(offset[d], c0) - c0;
+                            hi[d] = Math.min(offset[d] + shape[d], c0 + cs[d]) - c0;
+                        }
+                        shards[i] = ShardPieces.isWhole(chain, lo, hi) ? ShardPieces.whole(h)
+                                : ShardPieces.part(h, chain, lo, hi);
+                        return;
+                    }
+                    ByteBuffer b = h.read();
+                    if (b != null) {
+                        chunks[i] = ShardPieces.bytes(b);
+                        // unsharded chain with host stages (e.g. [bytes, zstd]): raw payload
+                        if (chain.innerHost != null) chunks[i] = chain.hostDecode(chunks[i]);
+                    }
+                } catch (ZarrException e) {
+                    throw new RuntimeException(e);
                 }
-                if (!ShardStaging.whole(chain, lo, hi)) {
-                    // sub-shard part: the index + the referenced inner chunks only
-                    chunks[i] = ShardStaging.compact(h, chain, lo, hi);
-                    continue;
-                }
-            }
-            ByteBuffer b = h.read();
-            if (b != null) {
-                chunks[i] = new byte[b.remaining()];
-                b.duplicate().get(chunks[i]);
-                // unsharded chain with host stages (e.g. [bytes, zstd]): raw payload for the device
-                if (chain.innerHost != null) chunks[i] = chain.hostDecode(chunks[i]);
-            }
+            });
+        } catch (RuntimeException e) {
+            if (e.getCause() instanceof ZarrException) throw (ZarrException) e.getCause();
+            throw e;
         }
         ucar.ma2.Array out = ucar.ma2.Array.factory(md.dataType().getMA2DataType(),
                 Utils.toIntArray(shape));
         long[] ctxs = ZarrHip.ctxs();
-        int st = ctxs.length > 1
-                ? ZarrHip.arrayReadMulti(ctxs, chain.meta, chain.shape, chain.chunkShape,
-                        chain.innerShape, chain.order, chain.fill, chunks, offset, shape,
-                        out.getStorage())
-                : ZarrHip.arrayRead(ctxs[0], chain.meta, chain.shape, chain.chunkShape,
-                        chain.innerShape, chain.order, chain.fill, chunks, offset, shape,
-                        out.getStorage());
+        int st;
+        if (sharded) {
+            st = ZarrHip.arrayReadPieces(ctxs, chain.meta, chain.shape, chain.chunkShape,
+                    chain.innerShape, chain.order, chain.fill, ZarrHip.indexes(shards),
+                    ZarrHip.sizes(shards), ZarrHip.pieceOffsets(shards),
+                    ZarrHip.pieceLens(shards), ZarrHip.pieceData(shards), offset, shape,
+                    out.getStorage());
+        } else {
+            st = ctxs.length > 1
+                    ? ZarrHip.arrayReadMulti(ctxs, chain.meta, chain.shape, chain.chunkShape,
+                            chain.innerShape, chain.order, chain.fill, chunks, offset, shape,
+                            out.getStorage())
+                    : ZarrHip.arrayRead(ctxs[0], chain.meta, chain.shape, chain.chunkShape,
+                            chain.innerShape, chain.order, chain.fill, chunks, offset, shape,
+                            out.getStorage());
+        }
         return st == 0 ? out : super.read(offset, shape, parallel);
     }
 

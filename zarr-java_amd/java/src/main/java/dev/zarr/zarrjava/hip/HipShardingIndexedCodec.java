@@ -61,25 +61,21 @@ public class HipShardingIndexedCodec extends ShardingIndexedCodec {
         if (chain != null) {
             long[] hi = new long[offset.length];
             for (int d = 0; d < offset.length; d++) hi[d] = offset[d] + shape[d];
-            if (!ShardStaging.whole(chain, offset, hi)) {
-                // the index + the referenced inner chunks only (StoreHandleDataProvider)
-                byte[] compact = ShardStaging.compact(chunkHandle, chain, offset, hi);
-                if (compact != null) {
-                    Array a = device(compact, offset, shape);
-                    if (a != null) return a;
-                }
-                return super.decodePartial(chunkHandle, offset, shape);
-            }
-            ByteBuffer bytes = chunkHandle.read();
-            if (bytes == null) {
+            // the whole shard in one read, or its stored index + the referenced ranges
+            // (StoreHandleDataProvider, ShardingIndexedCodec.java:245-255, 333-357)
+            ShardPieces p = ShardPieces.isWhole(chain, offset, hi) ? ShardPieces.whole(chunkHandle)
+                    : ShardPieces.part(chunkHandle, chain, offset, hi);
+            if (p == null) {
                 return Arrays.equals(shape, arrayMetadata.chunkShape)
                         ? arrayMetadata.allocateFillValueChunk()
                         : super.decodePartial(chunkHandle, offset, shape);
             }
-            byte[] b = new byte[bytes.remaining()];
-            bytes.duplicate().get(b);
-            Array a = device(b, offset, shape);
-            if (a != null) return a;
+            Array out = Array.factory(arrayMetadata.dataType.getMA2DataType(), shape);
+            int st = ZarrHip.shardDecodePieces(ZarrHip.codecCtx(), chain.meta, chain.shape,
+                    chain.chunkShape, chain.innerShape, chain.order, chain.fill, p.index,
+                    p.shardSize, p.offsets, p.storedLens, p.data, offset, shape,
+                    out.getStorage());
+            if (st == 0) return out;
         }
         return super.decodePartial(chunkHandle, offset, shape);
     }

@@ -124,4 +124,62 @@ public final class ZarrHip {
     static native int shardDecodePartial(long ctx, int[] meta, long[] shape, int[] chunkShape,
                                          int[] innerShape, int[] order, byte[] fill, byte[] shard,
                                          long[] offset, int[] partShape, Object out);
+
+    /**
+     * zh_shard_ranges: the (offset, nbytes) pairs of the stored shard a part references, read
+     * from its stored index (not checked here: the device does), adjacent ranges merged up to
+     * maxRun bytes (0: one per inner chunk).
+     */
+    static native long[] shardRanges(int[] meta, long[] shape, int[] chunkShape,
+                                     int[] innerShape, int[] order, byte[] fill, byte[] index,
+                                     long shardSize, long[] partLo, long[] partHi, long maxRun);
+
+    /**
+     * core.Array.read over shards given as stored index + pieces (zh_array_read_pieces; with
+     * several contexts zh_array_read_pieces_multi).  Per shard i: indexes[i] (null: whole in
+     * piece 0, or missing when it has no pieces), sizes[i] (-1 unknown), and its pieces.
+     */
+    static native int arrayReadPieces(long[] ctxs, int[] meta, long[] shape, int[] chunkShape,
+                                      int[] innerShape, int[] order, byte[] fill,
+                                      byte[][] indexes, long[] sizes, long[][] pieceOffsets,
+                                      long[][] pieceLens, byte[][][] pieceData, long[] offset,
+                                      long[] regionShape, Object out);
+
+    /** ShardingIndexedCodec.decodePartial over one shard as index + pieces. */
+    static native int shardDecodePieces(long ctx, int[] meta, long[] shape, int[] chunkShape,
+                                        int[] innerShape, int[] order, byte[] fill, byte[] index,
+                                        long size, long[] pieceOffsets, long[] pieceLens,
+                                        byte[][] pieceData, long[] offset, int[] partShape,
+                                        Object out);
+
+    // ---- flattening of ShardPieces[] into the JNI's arrays (null entries: missing shards)
+    static byte[][] indexes(ShardPieces[] s) {
+        byte[][] r = new byte[s.length][];
+        for (int i = 0; i < s.length; i++) r[i] = s[i] == null ? null : s[i].index;
+        return r;
+    }
+
+    static long[] sizes(ShardPieces[] s) {
+        long[] r = new long[s.length];
+        for (int i = 0; i < s.length; i++) r[i] = s[i] == null ? -1 : s[i].shardSize;
+        return r;
+    }
+
+    static long[][] pieceOffsets(ShardPieces[] s) {
+        long[][] r = new long[s.length][];
+        for (int i = 0; i < s.length; i++) r[i] = s[i] == null ? new long[0] : s[i].offsets;
+        return r;
+    }
+
+    static long[][] pieceLens(ShardPieces[] s) {
+        long[][] r = new long[s.length][];
+        for (int i = 0; i < s.length; i++) r[i] = s[i] == null ? new long[0] : s[i].storedLens;
+        return r;
+    }
+
+    static byte[][][] pieceData(ShardPieces[] s) {
+        byte[][][] r = new byte[s.length][][];
+        for (int i = 0; i < s.length; i++) r[i] = s[i] == null ? new byte[0][] : s[i].data;
+        return r;
+    }
 }

@@ -71,6 +71,19 @@ class zh_chunk_dst(C.Structure):
     _fields_ = [("data", C.c_void_p), ("capacity", C.c_int64), ("nbytes", C.c_int64)]
 
 
+class zh_shard_piece(C.Structure):
+    """One byte range of a stored shard (zarrhip.h zh_shard_piece)."""
+    _fields_ = [("offset", C.c_int64), ("nbytes", C.c_int64), ("data", C.c_void_p),
+                ("data_nbytes", C.c_int64)]
+
+
+class zh_shard_src(C.Structure):
+    """One stored shard as its index + the ranges read (zarrhip.h zh_shard_src)."""
+    _fields_ = [("index", C.c_void_p), ("index_nbytes", C.c_int64),
+                ("shard_nbytes", C.c_int64), ("pieces", C.POINTER(zh_shard_piece)),
+                ("npieces", C.c_int64)]
+
+
 def make_meta(shape, chunk_shape, dtype_size, *, fill=b"\0" * 8, is_bool=False, sharded=False,
               inner_chunk_shape=None, transpose_order=None, endian=ZH_ENDIAN_LITTLE,
               index_endian=ZH_ENDIAN_LITTLE, index_crc32c=True, index_location=ZH_INDEX_END,

@@ -57,6 +57,15 @@ _SIGS = {
     "zh_slab_partition": (C.c_int, [C.c_int, PI64, PI64, C.c_int, I64, PI64, PI64]),
     "zh_sharding_decode": (C.c_int, [P, PMETA, P, I64, P, U32, P, CH, SZ]),
     "zh_sharding_decode_partial": (C.c_int, [P, PMETA, P, I64, PI64, PI32, P, U32, P, CH, SZ]),
+    "zh_shard_ranges": (I64, [PMETA, P, I64, I64, PI64, PI64, I64, PI64, I64]),
+    "zh_array_read_pieces": (C.c_int, [P, PMETA, C.POINTER(A.zh_shard_src), I64, PI64, PI64, P,
+                                       U32, P, CH, SZ]),
+    "zh_array_read_pieces_multi": (C.c_int, [C.POINTER(P), C.c_int, C.c_int, PMETA,
+                                             C.POINTER(A.zh_shard_src), I64, PI64, PI64, P, U32,
+                                             PI32, CH, SZ]),
+    "zh_sharding_decode_pieces": (C.c_int, [P, PMETA, C.POINTER(A.zh_shard_src), PI64, PI32, P,
+                                            U32, P, CH, SZ]),
+    "zh_host_staging": (C.c_int, [P, SZ, C.POINTER(P)]),
     "zh_array_encoded_bound": (I64, [PMETA]),
     "zh_array_write": (C.c_int, [P, PMETA, P, PI64, PI64, C.POINTER(A.zh_chunk_dst), I64, P, CH,
                                  SZ]),
@@ -315,6 +324,31 @@ class DeviceContext:
                                   i64arr(shape), P(out), int(flags), P(stream), err, 1024)
         check(st, err)
 
+    def array_read_pieces(self, meta, shards, offset, shape, out, flags, stream=None):
+        """zh_array_read_pieces.  shards: list of ShardSource (or None = missing key)."""
+        arr, keep = shard_src_array(shards)
+        err = C.create_string_buffer(1024)
+        st = self.L.zh_array_read_pieces(self.h, C.byref(meta), arr, len(shards), i64arr(offset),
+                                         i64arr(shape), P(out), int(flags), P(stream), err, 1024)
+        del keep
+        check(st, err)
+
+    def sharding_decode_pieces(self, meta, shard, offset, shape, out, flags=0, stream=None):
+        """zh_sharding_decode_pieces: decodePartial of one shard given as index + pieces."""
+        arr, keep = shard_src_array([shard])
+        err = C.create_string_buffer(1024)
+        st = self.L.zh_sharding_decode_pieces(self.h, C.byref(meta), arr, i64arr(offset),
+                                              i32arr(shape), P(out), int(flags), P(stream), err,
+                                              1024)
+        del keep
+        check(st, err)
+
+    def host_staging(self, nbytes):
+        """zh_host_staging: the context's page-locked staging (valid until the next call)."""
+        p = P()
+        check(self.L.zh_host_staging(self.h, int(nbytes), C.byref(p)))
+        return p.value
+
     def plan(self, meta, sources, offset, shape, flags):
         return Plan(self, meta, sources, offset, shape, flags)
 
@@ -362,6 +396,69 @@ def array_read_multi(ctxs, meta, sources, offset, shape, out, flags, root=0):
     st = L.zh_array_read_multi_routed(hs, len(ctxs), int(root), C.byref(meta), srcs,
                                       len(sources), i64arr(offset), i64arr(shape), P(out),
                                       int(flags), routes, err, 1024)
+    check(st, err)
+    return list(routes)
+
+
+class ShardSource:
+    """One stored shard of a pieces read (zh_shard_src): the stored index bytes as the
+    prefix/suffix read returned them (None: a whole shard in one piece at offset 0), the
+    shard size (StoreHandle.getSize(), -1 unknown) and its pieces as (offset, stored nbytes,
+    pointer, held nbytes) tuples."""
+
+    def __init__(self, index_ptr, index_nbytes, shard_nbytes, pieces):
+        self.index_ptr = index_ptr
+        self.index_nbytes = int(index_nbytes)
+        self.shard_nbytes = int(shard_nbytes)
+        self.pieces = list(pieces)
+
+
+def shard_src_array(shards):
+    """ctypes zh_shard_src[] for a list of ShardSource / None; returns (array, keepalive)."""
+    arr = (A.zh_shard_src * max(1, len(shards)))()
+    keep = []
+    for i, s in enumerate(shards):
+        if s is None:
+            continue
+        ps = (A.zh_shard_piece * max(1, len(s.pieces)))()
+        for k, (off, nb, ptr, held) in enumerate(s.pieces):
+            ps[k].offset, ps[k].nbytes, ps[k].data, ps[k].data_nbytes = int(off), int(nb), ptr, \
+                int(held)
+        keep.append(ps)
+        arr[i].index = s.index_ptr
+        arr[i].index_nbytes = s.index_nbytes
+        arr[i].shard_nbytes = s.shard_nbytes
+        arr[i].pieces = ps
+        arr[i].npieces = len(s.pieces)
+    return arr, keep
+
+
+def shard_ranges(meta, index, shard_nbytes, part_lo, part_hi, max_run=64 << 20):
+    """zh_shard_ranges over index bytes (bytes-like) → [(offset, nbytes)] to read."""
+    L = lib()
+    buf = (C.c_char * max(1, len(index))).from_buffer_copy(bytes(index) or b"\0")
+    n = L.zh_shard_ranges(C.byref(meta), buf, len(index), int(shard_nbytes), i64arr(part_lo),
+                          i64arr(part_hi), int(max_run), None, 0)
+    if n < 0:
+        check(-n)
+    out = (C.c_int64 * max(2, 2 * n))()
+    n2 = L.zh_shard_ranges(C.byref(meta), buf, len(index), int(shard_nbytes), i64arr(part_lo),
+                           i64arr(part_hi), int(max_run), out, n)
+    assert n2 == n
+    return [(out[2 * k], out[2 * k + 1]) for k in range(n)]
+
+
+def array_read_pieces_multi(ctxs, meta, shards, offset, shape, out, flags, root=0):
+    """zh_array_read_pieces_multi: the pieces form of array_read_multi; returns the routes."""
+    L = lib()
+    hs = (P * len(ctxs))(*[c.h for c in ctxs])
+    arr, keep = shard_src_array(shards)
+    routes = (C.c_int32 * len(ctxs))()
+    err = C.create_string_buffer(1024)
+    st = L.zh_array_read_pieces_multi(hs, len(ctxs), int(root), C.byref(meta), arr, len(shards),
+                                      i64arr(offset), i64arr(shape), P(out), int(flags), routes,
+                                      err, 1024)
+    del keep
     check(st, err)
     return list(routes)
 

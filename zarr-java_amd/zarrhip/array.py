@@ -256,37 +256,6 @@ class Array:
             n *= c // i
         return n
 
-    def _unwrap_inner(self, shard):
-        """Host hand-off for inner byte-to-byte codecs: verify/parse the index with the
-        index codecs, decode every inner chunk's frame on the host and rebuild a raw shard
-        (same index location/endianness) for the device."""
-        ch = self.chain.chain
-        n_in = self._n_inner()
-        crc = ch["index_crc32c"]
-        isz = 16 * n_in + (4 if crc else 0)
-        start = ch["index_location"] == A.ZH_INDEX_START
-        idx = shard[:isz] if start else shard[len(shard) - isz:]
-        body = self.chain.index_codecs[1].decode(idx) if crc else idx
-        big = ch["index_endian"] == A.ZH_ENDIAN_BIG
-        fmt = ">QQ" if big else "<QQ"
-        ents = [struct.unpack(fmt, body[16 * k:16 * k + 16]) for k in range(n_in)]
-        payload = []
-        pos = isz if start else 0
-        new = []
-        for off, nb in ents:
-            if off == 2 ** 64 - 1 or nb == 2 ** 64 - 1:
-                new.append((off, nb))
-                continue
-            raw = host_bb_decode(self.chain.inner_host_bb, shard[off:off + nb])
-            new.append((pos, len(raw)))
-            payload.append(raw)
-            pos += len(raw)
-        ib = b"".join(struct.pack(fmt, *e) for e in new)
-        if crc:
-            ib = self.chain.index_codecs[1].encode(ib)
-        pb = b"".join(payload)
-        return ib + pb if start else pb + ib
-
     def _wrap_inner(self, shard):
         """Inverse of _unwrap_inner for the write path."""
         ch = self.chain.chain
@@ -314,118 +283,88 @@ class Array:
         pb = b"".join(payload)
         return ib + pb if start else pb + ib
 
-    def _stage_partial(self, h, part_lo, part_hi, lease=None):
-        """StoreHandleDataProvider semantics (ShardingIndexedCodec.java:333-357): read the
-        index with one range read, verify its crc32c on the host (same message as the
-        device), then read only the inner chunks the part references (adjacent ranges
-        coalesced into one store read each) and build a compact raw shard for the device:
-        the runs side by side, their host byte-to-byte codecs already undone, a fresh index
-        (+crc).  The index is handled as arrays (numpy), not entry by entry."""
-        ch = self.chain.chain
-        inner = ch["inner_chunk_shape"]
-        n_in = self._n_inner()
-        crc = ch["index_crc32c"]
-        isz = 16 * n_in + (4 if crc else 0)
-        start = ch["index_location"] == A.ZH_INDEX_START
+    def _stage_shard(self, h, part_lo, part_hi, lease):
+        """StoreHandleDataProvider semantics (ShardingIndexedCodec.java:190-230, 333-357): one
+        range read for the index, zh_shard_ranges for the inner chunks the part references,
+        one store read per range (in parallel, straight into one pooled buffer).  The stored
+        index goes to the device unchanged — its crc32c and entries are checked there, never
+        here — so a corrupt entry cannot size a host allocation.  Inner host byte-to-byte
+        stages (zstd, gzip, blosc) are undone per inner chunk: those pieces hold the raw
+        payload.  A range the store cannot deliver is left out (the device then reports the
+        reference's "Could not load byte data for chunk").  Returns a ShardSource plus the
+        buffers it points into, or None for a missing shard."""
+        if not h.exists():
+            return None
+        isz = _lib.lib().zh_shard_index_size(C.byref(self.zmeta))
+        start = self.chain.chain["index_location"] == A.ZH_INDEX_START
         idx = h.read(0, isz) if start else h.read(-isz)
         if idx is None:
             return None
-        if len(idx) < isz:
-            raise ZarrException(f"Shard {h!r} is smaller than its index ({isz} bytes).")
-        body = self.chain.index_codecs[1].decode(idx) if crc else idx
-        edt = np.dtype(">u8" if ch["index_endian"] == A.ZH_ENDIAN_BIG else "<u8")
-        cps = [c // i for c, i in zip(self.metadata.chunk_shape, inner)]
-        ents = np.frombuffer(body, edt, 2 * n_in).reshape(cps + [2])
-        box = tuple(slice(lo // i, (hi - 1) // i + 1) for lo, hi, i in zip(part_lo, part_hi, inner))
-        lin = np.arange(n_in, dtype=np.int64).reshape(cps)[box].ravel()
-        off = ents[box + (0,)].ravel().astype(np.uint64)
-        nb = ents[box + (1,)].ravel().astype(np.uint64)
-        keep = (off != np.uint64(2 ** 64 - 1)) & (nb != np.uint64(2 ** 64 - 1))
-        lin, off, nb = lin[keep], off[keep].astype(np.int64), nb[keep].astype(np.int64)
-        order = np.argsort(off, kind="stable")
-        lin, off, nb = lin[order], off[order], nb[order]
-        # runs of adjacent ranges: one store read each
-        brk = np.nonzero(off[1:] != off[:-1] + nb[:-1])[0] + 1 if len(off) else np.zeros(0, int)
-        rs = np.concatenate([[0], brk]).astype(np.int64) if len(off) else np.zeros(0, np.int64)
-        re = np.concatenate([brk, [len(off)]]).astype(np.int64) if len(off) else rs
-        new_off = np.full(n_in, 2 ** 64 - 1, np.uint64)
-        new_nb = np.full(n_in, 2 ** 64 - 1, np.uint64)
+        idx = bytes(idx)
+        size = h.size() if hasattr(h, "size") else None
+        size = -1 if size is None else int(size)
+        ibuf = np.frombuffer(idx if idx else b"\0", np.uint8)
+        keep = [ibuf]
+        self._count_staged(len(idx))
+        if len(idx) < isz:  # the device reports "Shard [..] is smaller than its index"
+            return _lib.ShardSource(ibuf.ctypes.data, len(idx), size, []), keep
+        host = self.chain.inner_host_bb
+        rs = _lib.shard_ranges(self.zmeta, idx, size, part_lo, part_hi,
+                               0 if host else 64 << 20)
+        pieces = []
+        if host:  # per inner chunk: undo the host codecs
+            for o, nb in rs:
+                blob = h.read(o, o + nb)
+                if blob is None or len(blob) < nb:
+                    continue
+                self._count_staged(nb)
+                raw = np.frombuffer(host_bb_decode(host, blob) or b"\0", np.uint8)
+                keep.append(raw)
+                pieces.append((o, nb, raw.ctypes.data, len(raw)))
+            return _lib.ShardSource(ibuf.ctypes.data, len(idx), size, pieces), keep
+        buf = _new_buf(max(1, sum(nb for _, nb in rs)), lease)
+        keep.append(buf)
+        mv = memoryview(buf)
+        jobs, pos = [], 0
+        for o, nb in rs:
+            jobs.append((pos, o, nb))
+            pos += nb
+        got = [0] * len(jobs)
 
-        def bad(s0, s1):
-            return ZarrException(f"Could not load byte data for chunk range [{s0}, {s1})")
-        if self.chain.inner_host_bb:  # per chunk: undo the host codecs
-            pos = isz if start else 0
-            blobs = []
-            for a, b in zip(rs.tolist(), re.tolist()):
-                s0, s1 = int(off[a]), int(off[b - 1] + nb[b - 1])
-                blob = h.read(s0, s1)
-                if blob is None or len(blob) < s1 - s0:
-                    raise bad(s0, s1)
-                self._count_staged(s1 - s0)
-                for k in range(a, b):
-                    raw = host_bb_decode(self.chain.inner_host_bb,
-                                         blob[int(off[k]) - s0:int(off[k] + nb[k]) - s0])
-                    new_off[lin[k]], new_nb[lin[k]] = pos, len(raw)
-                    blobs.append(raw)
-                    pos += len(raw)
-            pb = b"".join(blobs)
-            out = np.empty(len(pb) + isz, np.uint8)
-            out[isz if start else 0:(isz if start else 0) + len(pb)] = np.frombuffer(pb, np.uint8)
-        else:  # runs side by side in one buffer, each read straight into its place
-            lens = [int(off[b - 1] + nb[b - 1] - off[a]) for a, b in zip(rs.tolist(), re.tolist())]
-            out = _new_buf(sum(lens) + isz, lease)
-            mv = memoryview(out)
-            pos = isz if start else 0
-            jobs = []
-            for (a, b), ln in zip(zip(rs.tolist(), re.tolist()), lens):
-                s0 = int(off[a])
-                jobs.append((pos, s0, ln))
-                new_off[lin[a:b]] = (pos + off[a:b] - s0).astype(np.uint64)
-                new_nb[lin[a:b]] = nb[a:b].astype(np.uint64)
-                pos += ln
-
-            def fetch(job):
-                p0, s0, ln = job
-                got = h.read_into(mv[p0:p0 + ln], s0, s0 + ln)
-                if got is None or got < ln:
-                    raise bad(s0, s0 + ln)
-                self._count_staged(ln)
-            _parallel(fetch, jobs)
-        self._count_staged(isz)
-        ib = np.empty((n_in, 2), edt)
-        ib[:, 0], ib[:, 1] = new_off, new_nb
-        ib = ib.tobytes()
-        if crc:
-            ib = self.chain.index_codecs[1].encode(ib)
-        ibv = np.frombuffer(ib, np.uint8)
-        if start:
-            out[:isz] = ibv
-        else:
-            out[len(out) - isz:] = ibv
-        return out
+        def fetch(k):
+            p0, o, nb = jobs[k]
+            g = h.read_into(mv[p0:p0 + nb], o, o + nb)
+            got[k] = g or 0
+        _parallel(fetch, list(range(len(jobs))))
+        for k, (p0, o, nb) in enumerate(jobs):
+            if got[k] >= nb:
+                self._count_staged(nb)
+                pieces.append((o, nb, buf.ctypes.data + p0, nb))
+        return _lib.ShardSource(ibuf.ctypes.data, len(idx), size, pieces), keep
 
     def _load_source(self, coords, part_lo=None, part_hi=None, lease=None):
+        """One stored chunk / shard of a read: None (missing key), ("whole", bytes-like), or
+        ("pieces", ShardSource, keepalive) for a sharded part."""
         h = self._handle(coords)
         ch = self.chain.chain
-        if ch["sharded"] and part_lo is not None:
+        if ch["sharded"]:
+            n = self.ndim
+            if part_lo is None:
+                part_lo, part_hi = [0] * n, list(self.metadata.chunk_shape)
             full = all(lo == 0 and hi == c for lo, hi, c in
                        zip(part_lo, part_hi, self.metadata.chunk_shape))
-            if not full:  # sub-shard part: stage only what it references
-                if not h.exists():
-                    return None
-                return self._stage_partial(h, part_lo, part_hi, lease)
+            if not full or self.chain.inner_host_bb:  # the index + the referenced ranges
+                st = self._stage_shard(h, part_lo, part_hi, lease)
+                return None if st is None else ("pieces",) + st
         # raw payloads go to the device as they are: parallel reads into one buffer; host
         # byte-to-byte stages take the store's bytes
-        b = h.read() if (self.chain.host_bb or self.chain.inner_host_bb) else \
-            _read_whole(h, lease=lease)
+        b = h.read() if self.chain.host_bb else _read_whole(h, lease=lease)
         if b is None:
             return None
         self._count_staged(len(b))
         if self.chain.host_bb:
             b = host_bb_decode(self.chain.host_bb, b)
-        elif self.chain.inner_host_bb:
-            b = self._unwrap_inner(b)
-        return b
+        return ("whole", b)
 
     # ---------------------------------------------------------------- read
     def read(self, offset=None, shape=None, parallel=True):
@@ -441,37 +380,66 @@ class Array:
         coords = self._chunk_coords(offset, shape)
         t0 = time.perf_counter()
         lease = []  # staging buffers of this read, back to the pool after the device read
-
-        def load(c):
-            lo = [max(o, ci * cs) - ci * cs for o, ci, cs in zip(offset, c, self.metadata.chunk_shape)]
-            hi = [min(o + s, (ci + 1) * cs) - ci * cs
-                  for o, s, ci, cs in zip(offset, shape, c, self.metadata.chunk_shape)]
-            return self._load_source(c, lo, hi, lease)
-        if parallel and len(coords) > 1:  # the store reads of the chunks, concurrently
-            # (core.Array.read's parallel stream over chunks, M/core/Array.java:403-407)
-            from concurrent.futures import ThreadPoolExecutor
-            with ThreadPoolExecutor(max_workers=min(8, len(coords))) as ex:
-                sources = list(ex.map(load, coords))
-        else:
-            sources = [load(c) for c in coords]
-        t1 = time.perf_counter()
-        # views of the staged bytes (the library only reads them); an empty but present
-        # chunk keeps a non-null pointer (null = missing key → fill)
-        bufs = [None if s is None else np.frombuffer(s if len(s) else b"\0", np.uint8)
-                for s in sources]
-        srcs = [((int(b.ctypes.data), len(s)) if s is not None else (None, 0))
-                for b, s in zip(bufs, sources)]
         out = np.empty(shape, dtype=dt)
         devs = devices()
+        sharded = self.chain.chain["sharded"]
         try:
-            if len(devs) > 1:  # one slab per device, each D2H'd into its slice of `out`
-                _lib.array_read_multi(devs, self.zmeta, srcs, offset, shape, out.ctypes.data, 0)
+            def load(c):
+                lo = [max(o, ci * cs) - ci * cs
+                      for o, ci, cs in zip(offset, c, self.metadata.chunk_shape)]
+                hi = [min(o + s, (ci + 1) * cs) - ci * cs
+                      for o, s, ci, cs in zip(offset, shape, c, self.metadata.chunk_shape)]
+                return self._load_source(c, lo, hi, lease)
+            if parallel and len(coords) > 1:  # the store reads of the chunks, concurrently
+                # (core.Array.read's parallel stream over chunks, M/core/Array.java:403-407)
+                from concurrent.futures import ThreadPoolExecutor
+                with ThreadPoolExecutor(max_workers=min(8, len(coords))) as ex:
+                    sources = list(ex.map(load, coords))
             else:
-                devs[0].array_read(self.zmeta, srcs, offset, shape, out.ctypes.data, 0)
-        except _lib.ZhError as e:
-            raise_for(e)
-        finally:  # the call has consumed the staged bytes (it returns after its copies)
-            del bufs, srcs, sources
+                sources = [load(c) for c in coords]
+            t1 = time.perf_counter()
+            keep = []
+            try:
+                if sharded:  # index + pieces (or whole objects as one piece at 0)
+                    shards = []
+                    for s in sources:
+                        if s is None:
+                            shards.append(None)
+                        elif s[0] == "pieces":
+                            shards.append(s[1])
+                            keep.append(s[2])
+                        else:
+                            v = np.frombuffer(s[1], np.uint8) if len(s[1]) else \
+                                np.zeros(1, np.uint8)
+                            keep.append(v)
+                            shards.append(_lib.ShardSource(None, 0, len(s[1]),
+                                                           [(0, len(s[1]), v.ctypes.data,
+                                                             len(s[1]))]))
+                    if len(devs) > 1:
+                        _lib.array_read_pieces_multi(devs, self.zmeta, shards, offset, shape,
+                                                     out.ctypes.data, 0)
+                    else:
+                        devs[0].array_read_pieces(self.zmeta, shards, offset, shape,
+                                                  out.ctypes.data, 0)
+                else:
+                    # views of the staged bytes (the library only reads them); an empty but
+                    # present chunk keeps a non-null pointer (null = missing key → fill)
+                    bufs = [None if s is None else
+                            np.frombuffer(s[1] if len(s[1]) else b"\0", np.uint8)
+                            for s in sources]
+                    keep.append(bufs)
+                    srcs = [((int(b.ctypes.data), len(s[1])) if s is not None else (None, 0))
+                            for b, s in zip(bufs, sources)]
+                    if len(devs) > 1:  # one slab per device, each D2H'd into its slice of `out`
+                        _lib.array_read_multi(devs, self.zmeta, srcs, offset, shape,
+                                              out.ctypes.data, 0)
+                    else:
+                        devs[0].array_read(self.zmeta, srcs, offset, shape, out.ctypes.data, 0)
+            except _lib.ZhError as e:
+                raise_for(e)
+            finally:  # the call has consumed the staged bytes (it returns after its copies)
+                del keep, sources
+        finally:  # also when a store read or a host codec raised: the lease goes back
             staging_pool.give(lease)
         self.last_read_timing = {"prep_s": t0 - t_enter, "stage_s": t1 - t0,
                                  "device_s": time.perf_counter() - t1}
@@ -483,8 +451,8 @@ class Array:
         for d, c in enumerate(coords):
             if c < 0 or c * cs[d] >= self.metadata.shape[d]:
                 raise ZarrException("Attempting to read data outside of the array's domain.")
-        src = self._load_source(tuple(coords))
         out = np.empty(cs, dtype=self.metadata.data_type.numpy)
+        src = self._load_source(tuple(coords))
         if src is None:
             out.view(np.uint8).reshape(-1)[:] = np.frombuffer(
                 self.metadata.fill_bytes * int(np.prod(cs)), np.uint8)
@@ -493,10 +461,14 @@ class Array:
         m = A.zh_array_meta.from_buffer_copy(self.zmeta)
         for d in range(self.ndim):
             m.shape[d] = cs[d]
-        b = _host_buf(src)
         try:
-            device().array_read(m, [(C.addressof(b), len(src))], [0] * self.ndim, cs,
-                                out.ctypes.data, 0)
+            if src[0] == "pieces":
+                device().array_read_pieces(m, [src[1]], [0] * self.ndim, cs, out.ctypes.data,
+                                           0)
+            else:
+                b = _host_buf(src[1])
+                device().array_read(m, [(C.addressof(b), len(src[1]))], [0] * self.ndim, cs,
+                                    out.ctypes.data, 0)
         except _lib.ZhError as e:
             raise_for(e)
         return out
