@@ -250,108 +250,66 @@ def roofline_of(plan, st, config=None):
 # ------------------------------------------------------------------------------------------
 # host-inclusive readChunk pipeline
 # ------------------------------------------------------------------------------------------
-def host_inclusive(dev, A, meta, coords, offs, sizes, shard_slab, n_shards=4, reps=2, slabs=8,
-                   nslots=3):
-    """Host-resident bytes in, host-resident decoded array out: the readChunk /
-    ShardingIndexedCodec.decode(ByteBuffer) of `n_shards` interior shards (4 GiB each way)
-    from pinned host memory, pipelined over three streams (H2D | decode | D2H) so PCIe traffic
-    in both directions overlaps the decode.  Each shard moves as `slabs` y-slabs: a slab's
-    inner chunks are one contiguous byte range of the C-order payload, so a unit is that
-    range + the index, copied into a device slot that mirrors the shard's address range (the
-    decode touches only the index and the referenced chunks), and its decoded rows are one
-    contiguous part of the shard's output.  32 units of 512 MiB instead of 4 of 4 GiB cut
-    the pipeline's fill and drain from a quarter of the run to 1/32."""
+def host_inclusive(dev, A, meta, coords, offs, sizes, shard_slab, scratch, reps=3):
+    """Host-resident bytes in, host-resident decoded array out, through the library's own
+    read: one zh_array_read of the region [1,1024,4096,1024] (the four interior shards
+    (0,0,k,0): 16 GiB of stored shards in, 16 GiB out) from host sources into a host output.
+    The library pipelines it (zh_pipeline.cpp: 512 MiB C-order slabs, H2D | decode | D2H
+    overlapped, page-locked sources and output by direct DMA, pageable ones through its pinned
+    rings and host copy lanes).  Two forms, timed the same way (min of `reps`):
+      pinned   — shards and output in page-locked host memory (hipHostMalloc);
+      pageable — ordinary host memory touched once before (the JVM heap's state).
+    Each output is checked element by element against the generator on the device."""
+    import numpy as np
     n = meta.ndim
     cs = [meta.chunk_shape[d] for d in range(n)]
-    sel = [i for i, c in enumerate(coords)
-           if all((c[d] + 1) * cs[d] <= meta.shape[d] for d in range(n))][:n_shards]
+    off, shp = [0, 0, 0, 0], [1, cs[1], 4 * cs[2], cs[3]]
+    pos = {c: i for i, c in enumerate(coords)}
+    sel = [pos[(0, 0, k, 0)] for k in range(4)]
     in_sz = [sizes[i] for i in sel]
     out_sz = 4
-    for c in cs:
-        out_sz *= c
-    ch = meta.chain
-    inner = [ch.inner_chunk_shape[d] for d in range(n)]
-    cps = 1
-    for d in range(n):
-        cps *= cs[d] // inner[d]
-    isz = 16 * cps + 4
-    cn = 4
-    for d in range(n):
-        cn *= inner[d]
-    ys = cs[1] // slabs                    # decoded rows per slab (dim 0 is 1)
-    slab_chunks = cps // slabs             # inner chunks per slab: contiguous in C order
-    slab_in, slab_out = slab_chunks * cn, out_sz // slabs
-    assert cs[0] == 1 and ys % inner[1] == 0 and all(s == in_sz[0] for s in in_sz)
+    for v in shp:
+        out_sz *= v
+    res = {"region_offset": off, "region_shape": shp, "h2d_bytes": sum(in_sz),
+           "d2h_bytes": out_sz,
+           "call": "zh_array_read(host shards, host output): the library's pipelined host read"}
+    chk = scratch  # device room for the check (the headline's output buffer, rewritten later)
     hin = dev.malloc_pinned(sum(in_sz))
-    hout = dev.malloc_pinned(out_sz * len(sel))
-    pos, p = [], 0
-    for k, i in enumerate(sel):  # stage the encoded shards into pinned host memory
-        pos.append(p)
+    hout = dev.malloc_pinned(out_sz)
+    pin_ptrs, p = [], 0
+    for k, i in enumerate(sel):  # stage the encoded shards into host memory
+        pin_ptrs.append(hin + p)
         dev.memcpy(hin + p, shard_slab + offs[i], in_sz[k], 1, None, True)
         p += in_sz[k]
-    smeta = A.zh_array_meta.from_buffer_copy(meta)
-    for d in range(n):
-        smeta.shape[d] = cs[d]
-    din = [dev.malloc(in_sz[0]) for _ in range(nslots)]
-    dout = [dev.malloc(slab_out) for _ in range(nslots)]
-    flags = A.ZH_SRC_DEVICE | A.ZH_OUT_DEVICE
-    plans = [[dev.plan(smeta, [(din[j], in_sz[0])], [0, ys * q] + [0] * (n - 2),
-                       [1, ys] + cs[2:], flags) for q in range(slabs)] for j in range(nslots)]
-    s_in, s_dec, s_out = dev.stream(), dev.stream(), dev.stream()
-    units = [(k, q) for k in range(len(sel)) for q in range(slabs)]
-    times = []
-    for _ in range(reps):
-        ev = [[dev.event() for _ in range(3)] for _ in units]
-        dev.sync()
-        t0 = time.perf_counter()
-        for u, (k, q) in enumerate(units):
-            j = u % nslots
-            if u >= nslots:
-                dev.wait_event(s_in, ev[u - nslots][1])       # slot j's input consumed
-            ioff = in_sz[k] - isz                             # index at the end
-            dev.memcpy(din[j] + q * slab_in, hin + pos[k] + q * slab_in, slab_in, 0, s_in, False)
-            dev.memcpy(din[j] + ioff, hin + pos[k] + ioff, isz, 0, s_in, False)
-            dev.record(ev[u][0], s_in)
-            dev.wait_event(s_dec, ev[u][0])
-            if u >= nslots:
-                dev.wait_event(s_dec, ev[u - nslots][2])      # slot j's output drained
-            plans[j][q].execute(dout[j], s_dec)
-            dev.record(ev[u][1], s_dec)
-            dev.wait_event(s_out, ev[u][1])
-            dev.memcpy(hout + k * out_sz + q * slab_out, dout[j], slab_out, 1, s_out, False)
-            dev.record(ev[u][2], s_out)
-        for s in (s_in, s_dec, s_out):
-            dev.sync(s)
-        times.append(time.perf_counter() - t0)
-        for row in plans:
-            for pl in row:
-                pl.wait()
-    t = min(times)
-    res = {"value": round(len(sel) * out_sz / t / GiB, 2), "unit": "GiB/s",
-           "h2d_bytes": len(units) * (slab_in + isz), "d2h_bytes": out_sz * len(sel),
-           "seconds": round(t, 4),
-           "workload": f"readChunk of {len(sel)} interior shards (4 GiB in + 4 GiB out each) "
-                       f"from pinned host memory as {len(units)} y-slab units (chunk range + "
-                       f"index in, slab out), H2D | decode | D2H pipelined on 3 streams, "
-                       f"{nslots} device slots"}
-    # every decoded shard must equal the generator's values of its region
-    chk = dev.malloc(out_sz)
-    bad = 0
-    for k, i in enumerate(sel):
-        dev.memcpy(chk, hout + k * out_sz, out_sz, 0, None, True)
-        c = coords[i]
-        bad += dev.synth_verify(chk, [meta.shape[d] for d in range(n)],
-                                [c[d] * cs[d] for d in range(n)], cs, 4, SEED)
-    res["verify_mismatches"] = bad
-    for row in plans:
-        for pl in row:
-            pl.close()
-    for x in din + dout + [chk]:
-        dev.free(x)
-    dev.free_pinned(hin)
-    dev.free_pinned(hout)
-    for s in (s_in, s_dec, s_out):
-        dev.stream_destroy(s)
+    try:
+        page_in = [np.empty(sz, np.uint8) for sz in in_sz]
+        for buf, ptr, sz in zip(page_in, pin_ptrs, in_sz):
+            C.memmove(buf.ctypes.data, ptr, sz)
+        page_out = np.empty(out_sz, np.uint8)
+        page_out[:] = 1  # touched once, as a warm heap is
+        for name, srcs, outp in (
+                ("pinned", [(q, sz) for q, sz in zip(pin_ptrs, in_sz)], hout),
+                ("pageable", [(b.ctypes.data, sz) for b, sz in zip(page_in, in_sz)],
+                 page_out.ctypes.data)):
+            ts = []
+            for _ in range(reps):
+                t0 = time.perf_counter()
+                dev.array_read(meta, srcs, off, shp, outp, 0)
+                ts.append(time.perf_counter() - t0)
+            dev.memcpy(chk, outp, out_sz, 0, None, True)
+            bad = int(dev.synth_verify(chk, [meta.shape[d] for d in range(n)], off, shp, 4, SEED))
+            ts.sort()
+            res[name] = {"value": round(out_sz / ts[0] / GiB, 2), "unit": "GiB/s",
+                         "ms_min": round(ts[0] * 1e3, 1),
+                         "ms_median": round(ts[len(ts) // 2] * 1e3, 1),
+                         "verify_mismatches": bad}
+            log(f"host-inclusive {name}: {json.dumps(res[name])}")
+        del page_in, page_out
+    finally:
+        dev.free_pinned(hin)
+        dev.free_pinned(hout)
+    res["value"] = res["pinned"]["value"]
+    res["unit"] = "GiB/s"
     return res
 
 
@@ -695,9 +653,22 @@ def run_strong(args, dist, A, meta, rank, ws, local):
     first = lo[1] * shape[2] * shape[3] if n == 4 else 0
     t0 = time.perf_counter()
     offs, tot = slab_layout(caps)
+    full_bytes = 4
+    for s_ in shape:
+        full_bytes *= s_
+    # memory plan, checked before anything is allocated: two arenas (the decode's output and
+    # the shards) + on the root the assembled region (RCCL) + tables/staging headroom
+    arena_bytes = max(nel_cover * 4, tot)
+    need = 2 * arena_bytes + (full_bytes if rank == 0 and backend == "nccl" else 0) + (4 << 30)
+    if need > info["total_mem"]:
+        raise SystemExit(f"[rank {rank}] memory plan: {need / GiB:.1f} GiB needed (2 x "
+                         f"{arena_bytes / GiB:.1f} GiB arenas"
+                         f"{' + the region' if rank == 0 and backend == 'nccl' else ''} + 4 GiB) > "
+                         f"{info['total_mem'] / GiB:.1f} GiB on device {device}; use more ranks")
+    log(f"[rank {rank}] memory plan: {need / GiB:.1f} of {info['total_mem'] / GiB:.1f} GiB")
     # two arenas: the faster by a store probe is the synthesis source and then the decode's
     # output, the other holds the shards (arena_pair)
-    fast, slow, arena = arena_pair(dev, A, max(nel_cover * 4, tot))
+    fast, slow, arena = arena_pair(dev, A, arena_bytes)
     src = fast
     dev.synth_fill(src, nel_cover, 4, first, SEED)
     slab_buf = slow if slow is not None else dev.malloc(tot)
@@ -711,9 +682,6 @@ def run_strong(args, dist, A, meta, rank, ws, local):
     for s in ss:
         nel *= s
     out_bytes = nel * 4
-    full_bytes = 4
-    for s in shape:
-        full_bytes *= s
     # the decode's write target: 1 GiB VMM chunks in coprime order, as at N=1 (DESIGN §4
     # "Placement"); RCCL only ever sees torch-allocated buffers: a send buffer on every rank
     # and the assembled region on the root, filled by a device copy before the gather
@@ -747,9 +715,15 @@ def run_strong(args, dist, A, meta, rank, ws, local):
     dist.barrier()
     roof = roofline_of(plan, st)
     kern_max = dist.max(roof["kernel_ms"])
+    if roof.get("kernel_ms"):  # the line's roofline: the slowest rank's kernel time
+        roof["kernel_ms_rank0"] = roof["kernel_ms"]
+        roof["achieved"] = round(roof["achieved"] * roof["kernel_ms"] / kern_max, 1)
+        roof["frac"] = round(roof["achieved"] / roof["peak"], 4)
+        roof["kernel_ms"] = round(kern_max, 3)
+        roof["kernel_ms_is"] = "max over ranks"
     gather = None
     if backend in ("nccl", "gloo"):
-        gather = gather_to_root(args, dist, dev, backend, out, out_t, region_t, out_bytes,
+        gather = gather_to_root(args, dist, dev, backend, plan, out, out_t, region_t, out_bytes,
                                 full_bytes, parts, shape, rank, ws, device, t_dec)
     host_out = None
     if not args.no_host_out:
@@ -769,13 +743,15 @@ def run_strong(args, dist, A, meta, rank, ws, local):
     return res
 
 
-def gather_to_root(args, dist, dev, backend, out, out_t, region_t, out_bytes, full_bytes, parts,
-                   shape, rank, ws, device, t_dec):
+def gather_to_root(args, dist, dev, backend, plan, out, out_t, region_t, out_bytes, full_bytes,
+                   parts, shape, rank, ws, device, t_dec):
     """Assemble the region on rank 0: RCCL grouped point-to-point (each rank's slab is one
-    contiguous C-order slice, sent straight into its place in the root's region buffer;
-    the root's own slab was decoded in place), then the root re-verifies every element of
-    the assembled region against the generator.  gloo (ranks sharing one GPU, rehearsal):
-    through host tensors, verified per slab."""
+    contiguous C-order slice, sent straight into its place in the root's region buffer),
+    then the root re-verifies every element of the assembled region against the generator.
+    For the gather-inclusive rate every rank decodes its slab straight into its torch-
+    allocated RCCL buffer (the root: its slice of the region), timed like the headline, so
+    nothing is staged between the decode and the send.  gloo (ranks sharing one GPU,
+    rehearsal): through host tensors, verified per slab."""
     import torch
     import torch.distributed as tdist
     from zarrhip.parallel import slab_byte_offset
@@ -783,11 +759,18 @@ def gather_to_root(args, dist, dev, backend, out, out_t, region_t, out_bytes, fu
     if backend == "nccl":
         grp = tdist.new_group(backend="nccl")
         world = tdist.get_world_size(grp)
-        # decoded slab → this rank's RCCL send buffer (the root: its slice of the region)
+        # decode straight into this rank's RCCL send buffer (the root: its slice of the
+        # region), timed as the headline loop: no staging copy between decode and send
+        reps_d = max(1, min(args.steps, 5))
+        plan.execute(out_t.data_ptr())
+        plan.wait()
+        dist.barrier()
         dev.sync()
         tc = time.perf_counter()
-        dev.memcpy(out_t.data_ptr(), out, out_bytes, 2, None, True)
-        t_stage = dist.max(time.perf_counter() - tc)
+        for _ in range(reps_d):
+            plan.execute(out_t.data_ptr())
+        plan.wait()
+        t_dec_send = dist.max(time.perf_counter() - tc) / reps_d
 
         def once():
             ops = []
@@ -813,9 +796,8 @@ def gather_to_root(args, dist, dev, backend, out, out_t, region_t, out_bytes, fu
         bad = int(dist.max(bad))
         if bad:
             raise SystemExit(f"gathered region verification FAILED: {bad}")
-        how = ("RCCL grouped send/recv into the root's region buffer (xGMI); the decoded "
-               f"slab is first copied to the send buffer ({t_stage * 1e3:.2f} ms, not in "
-               "gather_ms)")
+        how = ("RCCL grouped send/recv into the root's region buffer (xGMI); each rank "
+               "decodes straight into its send buffer (decode_into_send_ms, max over ranks)")
     else:
         world = ws
         host = (C.c_char * out_bytes)()
@@ -840,10 +822,12 @@ def gather_to_root(args, dist, dev, backend, out, out_t, region_t, out_bytes, fu
         if bad:
             raise SystemExit(f"gathered region verification FAILED: {bad}")
         how = "gloo gather through host memory (ranks share one GPU: rehearsal only)"
+        t_dec_send = t_dec / args.steps  # the headline decode; the copy out is in t_g
     return {"backend": backend, "how": how, "world_size": world,
             "gather_ms": round(t_g * 1e3, 3),
+            "decode_into_send_ms": round(t_dec_send * 1e3, 3),
             "root_ingress_GBps": round((full_bytes - sizes[0]) / t_g / 1e9, 1),
-            "value_incl_gather": round(full_bytes / (t_dec / args.steps + t_g) / GiB, 2),
+            "value_incl_gather": round(full_bytes / (t_dec_send + t_g) / GiB, 2),
             "unit": "GiB/s", "root_verified_elements": full_bytes // 4}
 
 
@@ -1174,8 +1158,9 @@ def main():
                     help="strong mode: skip the host-terminated copy")
     ap.add_argument("--ydiv", type=int, default=1,
                     help="rehearsal only: divide the array's y extent (not a bench config)")
-    ap.add_argument("--host-inclusive", action="store_true",
-                    help="also measure pinned H2D + decode + D2H (adds 'host_inclusive')")
+    ap.add_argument("--no-host-inclusive", action="store_true",
+                    help="N=1 c4: skip the host-terminated read (pinned and pageable host "
+                         "shards in, host array out: 'host_inclusive')")
     ap.add_argument("--dry-run", action="store_true",
                     help="N>1 harness without a GPU (launch, partition, barrier, JSON line)")
     args = ap.parse_args()
@@ -1299,8 +1284,9 @@ def main():
     roofline = roofline_of(plan, st, args.config if args.ydiv == 1 else None)
     plan.set_timing(False)
     hinc = None
-    if args.host_inclusive and meta.chain.sharded:
-        hinc = host_inclusive(dev, A, meta, coords, offs, sizes, shard_slab)
+    if (not args.no_host_inclusive and ws == 1 and args.ydiv == 1 and args.config == "c4"
+            and meta.chain.sharded):
+        hinc = host_inclusive(dev, A, meta, coords, offs, sizes, shard_slab, out)
         log(f"[rank {rank}] host-inclusive: {hinc}")
     cpu = None
     if rank == 0 and ws == 1 and not args.no_cpu_baseline and meta.chain.sharded:

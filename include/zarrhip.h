@@ -385,7 +385,8 @@ int zh_device_malloc(zh_ctx* ctx, size_t bytes, void** out);
 /* Physical chunks (hipMemCreate, ZH_SCATTER_MB MiB each, default 1024) mapped into one virtual
  * range in a coprime-stride order, so that virtually adjacent chunks are not physically
  * adjacent: the decode's output arena in bench.py (DESIGN.md §4 "Placement": mean +5.6 % over
- * hipMalloc on 18 buffers, 3 boxes).  Freed by zh_device_free. */
+ * hipMalloc on 18 buffers, 3 boxes).  The rest beyond the last whole chunk gets one smaller
+ * chunk (rounded up to the allocation granularity), mapped last.  Freed by zh_device_free. */
 #define ZH_MALLOC_SCATTER 0x4u
 /* With ZH_MALLOC_SCATTER: allocate up to ZH_CALIB_TRIES candidate arenas (default 2, each
  * held while the next is allocated, so each gets other physical chunks), time a contiguous

@@ -134,3 +134,66 @@ def test_mutated_frames_never_crash(comp, split):
             assert isinstance(out, (bytes, bytearray))
         except (z.ZarrException, z.UnsupportedChainError):
             pass
+
+
+# ---- the reference's OME-Zarr v0.4 arrays: blosc LZ4 + byte shuffle, <f4 / <u4 ------------
+OME_BLOSC = [("v0.4/0", "0.0.0.0.0"), ("v0.4/0", "0.1.0.0.0"), ("v0.4/1", "0.0.0.0.0"),
+             ("v0.4/1", "0.1.0.0.0"), ("v0.4/labels/nuclei/0", "0.0.0"),
+             ("v0.4_hcs/A/1/0/0", "0.0.0.0.0"), ("v0.4_hcs/A/1/0/0", "0.1.0.0.0")]
+
+
+def independent_blosc_lz4(frame):
+    """An independent decode of a blosc1 frame with LZ4 streams: the header and block/stream
+    layout parsed here, every stream decompressed by liblz4 (pyarrow's lz4_raw codec, not
+    this repo's decoder), byte shuffle undone with numpy.  Test infrastructure only."""
+    pa = pytest.importorskip("pyarrow")
+    import struct
+    ver, verlz, flags, typesize = frame[0], frame[1], frame[2], frame[3]
+    nbytes, blocksize, cbytes = struct.unpack("<III", frame[4:16])
+    assert cbytes == len(frame) and ver >= 2
+    assert flags >> 5 == 1, "LZ4 streams"
+    assert not flags & 0x02, "not memcpyed"
+    nblocks = -(-nbytes // blocksize)
+    bstarts = struct.unpack(f"<{nblocks}I", frame[16:16 + 4 * nblocks])
+    out = bytearray()
+    for b in range(nblocks):
+        bsize = min(blocksize, nbytes - b * blocksize)
+        split = not flags & 0x10 and typesize <= 16 and bsize // typesize >= 128
+        nsplits = typesize if split else 1
+        pos, blk = bstarts[b], bytearray()
+        for _ in range(nsplits):
+            (cs,) = struct.unpack("<i", frame[pos:pos + 4])
+            pos += 4
+            want = bsize // nsplits
+            data = frame[pos:pos + cs]
+            pos += cs
+            blk += data if cs == want else pa.Codec("lz4_raw").decompress(
+                data, decompressed_size=want, asbytes=True)
+        if flags & 0x01 and typesize > 1:  # byte shuffle: typesize planes of bsize / typesize
+            n = bsize // typesize
+            planes = np.frombuffer(bytes(blk[:n * typesize]), np.uint8).reshape(typesize, n)
+            blk = bytearray(planes.T.tobytes()) + blk[n * typesize:]
+        out += blk
+    assert len(out) == nbytes
+    return bytes(out)
+
+
+@pytest.mark.parametrize("array,key", OME_BLOSC)
+def test_ome_v04_blosc_lz4_pinned_by_liblz4(array, key):
+    """zh_blosc_decompress on the reference's own LZ4 + byte-shuffle frames equals liblz4's
+    decode of the same streams unshuffled in numpy; the decoded size is the chunk's and the
+    values are finite (images) / small labels."""
+    import json
+    root = os.path.join(GOLDEN, "ome_blosc", *array.split("/"))
+    za = json.load(open(os.path.join(root, ".zarray")))
+    frame = open(os.path.join(root, key), "rb").read()
+    dt = np.dtype(za["dtype"])
+    want = independent_blosc_lz4(frame)
+    assert len(want) == int(np.prod(za["chunks"])) * dt.itemsize
+    got = bytes(BloscCodec().decode(frame))
+    assert got == want
+    vals = np.frombuffer(got, dt)
+    if dt.kind == "f":
+        assert np.isfinite(vals).all() and vals.any()
+    else:
+        assert vals.max() < 1 << 16

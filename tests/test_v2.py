@@ -176,3 +176,33 @@ def test_null_fill_keeps_zero_chunks(tmp_path):
                         .withChunks(2, 4).withFillValue(0).build())
     a.write(None, np.zeros((4, 4), np.int16))
     assert sorted(os.listdir(os.path.join(tmp_path, "k2"))) == [".zarray"]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["v0.4/0", "v0.4/1", "v0.4/labels/nuclei/0",
+                                  "v0.4_hcs/A/1/0/0"])
+def test_ome_v04_blosc_lz4_fixture_read(name):
+    """The reference's OME-Zarr v0.4 arrays (v2, blosc LZ4 + byte shuffle, '.'-separated keys):
+    host blosc (zh_blosc_decompress) then the device bytes + scatter stages; equal to the
+    chunks decoded by liblz4 (pyarrow) with the shuffle undone and assembled in numpy
+    (test_blosc.independent_blosc_lz4), whole and for an interior region."""
+    import json
+    from test_blosc import independent_blosc_lz4
+    root = os.path.join(GOLDEN, "ome_blosc", *name.split("/"))
+    za = json.load(open(os.path.join(root, ".zarray")))
+    shape, cs, dt = za["shape"], za["chunks"], np.dtype(za["dtype"])
+    want = np.zeros(shape, dt)
+    for idx in np.ndindex(*[-(-s // c) for s, c in zip(shape, cs)]):
+        path = os.path.join(root, ".".join(map(str, idx)))
+        if not os.path.exists(path):
+            continue
+        blk = np.frombuffer(independent_blosc_lz4(open(path, "rb").read()), dt).reshape(cs)
+        sl = tuple(slice(i * c, min((i + 1) * c, s)) for i, c, s in zip(idx, cs, shape))
+        want[sl] = blk[tuple(slice(0, x.stop - x.start) for x in sl)]
+    a = v2.Array.open(z.FilesystemStore(os.path.join(GOLDEN, "ome_blosc")).resolve(
+        *name.split("/")))
+    np.testing.assert_array_equal(a.read(), want)
+    off = [s // 3 for s in shape]
+    shp = [max(1, s - o - 1) for s, o in zip(shape, off)]
+    np.testing.assert_array_equal(a.read(off, shp),
+                                  want[tuple(slice(o, o + n) for o, n in zip(off, shp))])

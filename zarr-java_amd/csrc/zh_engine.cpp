@@ -1180,6 +1180,7 @@ int plan_create(zh_ctx* ctx, const zh_array_meta* m, const SrcDesc* srcs, int64_
   // non-temporal loads + stores: +4 % on the row path, +1 % on the tile path (interleaved
   // A/B in one process, profiles/r01/experiments/tune_*.json)
   p->args.nt = env_int("ZH_NT", 3) & 7;  // bit 2: 8 rows in flight per lane (rows)
+  p->args.crc_edge = env_int("ZH_CRC_EDGE", 0);
   // Visit items in a golden-ratio stride order: +3.6 % on the tile path (c4) on every normal
   // allocation, neutral on the row path (interleaved A/B, profiles/placement_perm.py), so
   // on by default for tiles.  ZH_ITEM_PERM=0/1 overrides.
@@ -2263,6 +2264,7 @@ static int array_write_fast(zh_ctx* ctx, const zh_array_meta* m, ScatterArgs a,
   if (crc_fuse)
     ZH_HIPF(hipMemsetAsync(W + o_cpart, 0, (size_t)(items * nspan) * sizeof(uint32_t), s));
   v.nt = env_int("ZH_ENC_NT", 3) & 3;
+  v.crc_edge = env_int("ZH_ENC_CRC_EDGE", 0);
   // narrow rows: G consecutive chunks per work item so a wave load covers G·row bytes of a
   // region row (ZH_ENC_GROUP: 0 off, default G·row = 256 B; encode_group_rows_kernel; c3
   // write G × U grid in profiles/r02/write/ab_enc3.txt: G = 2, U = 4 best, 40.1 → 36.2 ms)
@@ -2716,6 +2718,7 @@ namespace {
 // (zh_device_scatter_view) maps another allocation's handles at a fresh VA and owns none.
 struct ScatterAlloc {
   size_t size = 0, chunk = 0;
+  size_t tail = 0;  // bytes of the last handle when smaller than a chunk (mapped last, unpermuted)
   int device = 0;
   bool view = false;
   std::vector<hipMemGenericAllocationHandle_t> handles;
@@ -2748,7 +2751,7 @@ uint64_t gcd_u64(uint64_t x, uint64_t y) {
 // golden-ratio stride with a = 0; order k > 0 takes a further stride coprime with n (from a
 // second irrational fraction) and a rotation.  On failure nothing stays mapped.
 int scatter_map(void* base, const ScatterAlloc& A, uint64_t order) {
-  const size_t n = A.handles.size(), chunk = A.chunk;
+  const size_t n = A.handles.size() - (A.tail ? 1 : 0), chunk = A.chunk;
   uint64_t m = 1, a = 0;
   if (n > 1) {
     const double frac = order == 0 ? 0.6180339887498949
@@ -2766,12 +2769,18 @@ int scatter_map(void* base, const ScatterAlloc& A, uint64_t order) {
       return ZH_EHIP;
     }
   }
+  if (A.tail && hipMemMap((uint8_t*)base + n * chunk, A.tail, 0, A.handles[n], 0) != hipSuccess) {
+    for (size_t k = 0; k < n; k++) (void)hipMemUnmap((uint8_t*)base + k * chunk, chunk);
+    (void)hipGetLastError();
+    return ZH_EHIP;
+  }
   hipMemAccessDesc acc = {};
   acc.location.type = hipMemLocationTypeDevice;
   acc.location.id = A.device;
   acc.flags = hipMemAccessFlagsProtReadWrite;
   if (hipMemSetAccess(base, A.size, &acc, 1) != hipSuccess) {
     for (size_t k = 0; k < n; k++) (void)hipMemUnmap((uint8_t*)base + k * chunk, chunk);
+    if (A.tail) (void)hipMemUnmap((uint8_t*)base + n * chunk, A.tail);
     (void)hipGetLastError();
     return ZH_EHIP;
   }
@@ -2779,8 +2788,9 @@ int scatter_map(void* base, const ScatterAlloc& A, uint64_t order) {
 }
 
 void scatter_unmap(void* base, const ScatterAlloc& A) {
-  for (size_t k = 0; k < A.handles.size(); k++)
-    (void)hipMemUnmap((uint8_t*)base + k * A.chunk, A.chunk);
+  const size_t n = A.handles.size() - (A.tail ? 1 : 0);
+  for (size_t k = 0; k < n; k++) (void)hipMemUnmap((uint8_t*)base + k * A.chunk, A.chunk);
+  if (A.tail) (void)hipMemUnmap((uint8_t*)base + n * A.chunk, A.tail);
   (void)hipGetLastError();
 }
 
@@ -2836,14 +2846,19 @@ int scatter_malloc(int device, size_t bytes, void** out) {
   size_t chunk = (size_t)std::max(1, env_int("ZH_SCATTER_MB", 1024)) << 20;
   chunk = std::min(chunk, std::max(bytes, (size_t)1));  // small buffers: one chunk
   chunk = (chunk + gran - 1) / gran * gran;
-  const size_t n = std::max<size_t>(1, (bytes + chunk - 1) / chunk);
+  // whole chunks, then a tail chunk only as large as the rest (rounded to the granularity):
+  // a request just above a chunk multiple must not take a whole extra chunk
+  const size_t n = std::max<size_t>(1, bytes / chunk);
+  size_t rest = bytes > n * chunk ? bytes - n * chunk : 0;
+  rest = (rest + gran - 1) / gran * gran;
   ScatterAlloc A;
-  A.size = n * chunk;
+  A.size = n * chunk + rest;
   A.chunk = chunk;
+  A.tail = rest;
   A.device = device;
-  for (size_t i = 0; i < n; i++) {
+  for (size_t i = 0; i < n + (rest ? 1 : 0); i++) {
     hipMemGenericAllocationHandle_t h;
-    if (hipMemCreate(&h, chunk, &prop, 0) != hipSuccess) {
+    if (hipMemCreate(&h, i < n ? chunk : rest, &prop, 0) != hipSuccess) {
       for (auto hh : A.handles) (void)hipMemRelease(hh);
       (void)hipGetLastError();
       return ZH_ENOMEM;

@@ -18,14 +18,16 @@
 //
 // so both PCIe directions, the host copies and the kernels overlap.  Each slab is planned
 // over only the chunks it touches, and a sub-shard part stages only the ranges it references
-// (zh_engine.cpp caller_pieces / compact_pieces).  Errors: the first failing slab in C order
-// (plans are created up front; a planning failure at slab r runs slabs < r and reports a
-// device error among them first, as the one-plan read would).
+// (zh_engine.cpp caller_pieces / compact_pieces).  At most ZH_PIPE_PLANS (4) slab plans are
+// alive, so their device staging cycles through the context's block cache.  Errors: the first
+// failing slab in C order (a planning failure at slab r runs slabs < r and reports a device
+// error among them first, as the one-plan read would; a device error stops the read).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
 #include <atomic>
 #include <condition_variable>
+#include <deque>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -107,11 +109,11 @@ struct OutJob {
   int64_t len;
 };
 
-// Splits the plan's h2d list into jobs: page-locked entries of at least kDirectMin bytes go
+// Splits the plan's h2d list into jobs: page-locked entries of at least kDirectMin (1 MiB) go
 // as their own DMA; the rest is packed into windows of at most `chunk` bytes of the staging.
 void in_jobs(zh_plan* p, int64_t slab, int64_t chunk, std::vector<InJob>& jobs,
              bool* any_pageable) {
-  constexpr int64_t kDirectMin = 4 << 20;
+  constexpr int64_t kDirectMin = 1 << 20;
   InJob cur;
   cur.slab = slab;
   cur.dst = nullptr;
@@ -261,66 +263,55 @@ int read_pipelined(zh_ctx* ctx, const zh_array_meta* meta, const SrcDesc* srcs, 
   }
   (void)hipSetDevice(ctx->device);
   hipStream_t sdec = stream_v ? (hipStream_t)stream_v : ctx->stream;
-  // ---- plan every slab (host work; device tables uploaded), up front
-  std::vector<zh_plan*> plans;
-  std::vector<int64_t> obase, obytes_r;
-  int plan_st = ZH_OK;
-  std::string plan_msg;
-  for (int64_t r = 0; r < nslab; r++) {
+  // ---- slab geometry: offset, shape, output byte range, sources (host work only)
+  struct Slab {
     int64_t o[kMaxDims], s[kMaxDims];
+    int64_t obase, obytes;
+    std::vector<SrcDesc> sub;
+  };
+  std::vector<Slab> slabs((size_t)nslab);
+  int64_t max_slab = 0;
+  for (int64_t r = 0; r < nslab; r++) {
+    Slab& S = slabs[(size_t)r];
     for (int d = 0; d < n; d++) {
-      o[d] = offset[d];
-      s[d] = shape[d];
+      S.o[d] = offset[d];
+      S.s[d] = shape[d];
     }
-    o[ax] = bound[(size_t)r];
-    s[ax] = bound[(size_t)r + 1] - bound[(size_t)r];
+    S.o[ax] = bound[(size_t)r];
+    S.s[ax] = bound[(size_t)r + 1] - bound[(size_t)r];
     int64_t st0[kMaxDims], cnt[kMaxDims];
-    const int64_t m = chunk_coords(n, meta->chunk_shape, o, s, st0, cnt);
-    std::vector<SrcDesc> sub((size_t)m);
+    const int64_t m = chunk_coords(n, meta->chunk_shape, S.o, S.s, st0, cnt);
+    S.sub.resize((size_t)m);
     int64_t cur[kMaxDims] = {0};
     for (int64_t i = 0; i < m; i++) {
       int64_t lin = 0;
       for (int d = 0; d < n; d++) lin += (st0[d] + cur[d] - cstart[d]) * cstride[d];
-      sub[(size_t)i] = srcs[lin];
+      S.sub[(size_t)i] = srcs[lin];
       for (int d = n - 1; d >= 0; d--) {
         if (++cur[d] < cnt[d]) break;
         cur[d] = 0;
       }
     }
-    zh_plan* p = nullptr;
-    char e[1024] = {0};
-    const int st = plan_create(ctx, meta, sub.data(), m, o, s, (flags & ZH_SRC_DEVICE) | ZH_OUT_DEVICE,
-                               true, &p, e, sizeof e);
-    if (st != ZH_OK) {
-      plan_st = st;
-      plan_msg = e;
-      break;
-    }
-    plans.push_back(p);
     int64_t base = 0, sb = meta->dtype_size;
     for (int d = 0; d < n; d++) {
-      base += (o[d] - offset[d]) * rstride[d];
-      sb *= s[d];
+      base += (S.o[d] - offset[d]) * rstride[d];
+      sb *= S.s[d];
     }
-    obase.push_back(base * meta->dtype_size);
-    obytes_r.push_back(sb);
+    S.obase = base * meta->dtype_size;
+    S.obytes = sb;
+    max_slab = std::max(max_slab, sb);
   }
-  const int64_t np = (int64_t)plans.size();
+  // At most `W` slab plans are alive: each holds its device staging, which then comes back
+  // from the context's block cache for the next slab and the next call (fresh device memory
+  // pays for its first touch: all slabs' staging at once cost ~15 ms per GiB on every call).
+  const int W = std::max(2, std::min(16, env_int("ZH_PIPE_PLANS", 4)));
+  std::vector<zh_plan*> plans((size_t)nslab, nullptr);
   int st = ZH_OK;
   hipError_t he = hipSuccess;
-  // ---- jobs, rings, device output slots
-  std::vector<InJob> ijobs;
-  bool in_pageable = false;
-  for (int64_t r = 0; r < np; r++) in_jobs(plans[(size_t)r], r, cfg.chunk, ijobs, &in_pageable);
-  std::vector<int64_t> in_total((size_t)np, 0);
-  for (auto& j : ijobs) in_total[(size_t)j.slab]++;
   const bool out_pinned = host_out && host_pinned(out);
-  std::vector<OutJob> ojobs;
-  int64_t max_slab = 0;
-  for (int64_t r = 0; r < np; r++) max_slab = std::max(max_slab, obytes_r[(size_t)r]);
   std::vector<void*> dslot;
   std::vector<size_t> dslot_got;
-  const int nds = host_out && np > 0 ? (int)std::min<int64_t>(cfg.dslots, np) : 0;
+  const int nds = host_out ? (int)std::min<int64_t>(cfg.dslots, nslab) : 0;
   for (int k = 0; k < nds && he == hipSuccess; k++) {
     void* q = nullptr;
     size_t got = 0;
@@ -330,30 +321,31 @@ int read_pipelined(zh_ctx* ctx, const zh_array_meta* meta, const SrcDesc* srcs, 
       dslot_got.push_back(got);
     }
   }
-  std::vector<int64_t> out_total((size_t)np, 0);
+  std::vector<OutJob> ojobs;
+  std::vector<int64_t> out_total((size_t)nslab, 0);
   if (nds > 0 && he == hipSuccess)
-    for (int64_t r = 0; r < np; r++) {
+    for (int64_t r = 0; r < nslab; r++) {
+      const Slab& S = slabs[(size_t)r];
       const uint8_t* dsrc = (const uint8_t*)dslot[(size_t)(r % nds)];
-      const int64_t step = out_pinned ? obytes_r[(size_t)r] : cfg.chunk;
-      for (int64_t o = 0; o < obytes_r[(size_t)r]; o += step) {
-        ojobs.push_back(OutJob{r, dsrc + o, (uint8_t*)out + obase[(size_t)r] + o,
-                               std::min(step, obytes_r[(size_t)r] - o)});
+      const int64_t step = out_pinned ? S.obytes : cfg.chunk;
+      for (int64_t o = 0; o < S.obytes; o += step) {
+        ojobs.push_back(OutJob{r, dsrc + o, (uint8_t*)out + S.obase + o, std::min(step, S.obytes - o)});
         out_total[(size_t)r]++;
       }
     }
-  const int lanes_in = ijobs.empty() ? 0 : (in_pageable ? cfg.threads : 1);
+  const int lanes_in = host_in ? cfg.threads : 0;
   const int lanes_out = ojobs.empty() ? 0 : (out_pinned ? 1 : cfg.threads);
   if (he == hipSuccess && (lanes_in || lanes_out)) {
     st = ensure_pipe(ctx, 2 * std::max(lanes_in, lanes_out), (size_t)cfg.chunk);
     if (st != ZH_OK) set_err(err, errlen, "page-locked staging rings: allocation failed");
   }
-  std::vector<hipEvent_t> in_ev((size_t)np, nullptr), dec_ev((size_t)np, nullptr),
-      out_ev((size_t)np, nullptr);
+  std::vector<hipEvent_t> in_ev((size_t)nslab, nullptr), dec_ev((size_t)nslab, nullptr),
+      out_ev((size_t)nslab, nullptr);
   std::vector<hipEvent_t> slot_ev;
   auto mk = [&](hipEvent_t* e) {
     if (he == hipSuccess) he = hipEventCreateWithFlags(e, hipEventDisableTiming);
   };
-  for (int64_t r = 0; r < np; r++) {
+  for (int64_t r = 0; r < nslab; r++) {
     mk(&in_ev[(size_t)r]);
     mk(&dec_ev[(size_t)r]);
     mk(&out_ev[(size_t)r]);
@@ -362,40 +354,60 @@ int read_pipelined(zh_ctx* ctx, const zh_array_meta* meta, const SrcDesc* srcs, 
   const int E = 2 * std::max(lanes_in, lanes_out);
   slot_ev.assign((size_t)(2 * E), nullptr);
   for (auto& e : slot_ev) mk(&e);
-  Flags fin((size_t)std::max<int64_t>(np, 1)), fdec((size_t)std::max<int64_t>(np, 1)),
-      fout((size_t)std::max<int64_t>(np, 1));
+  Flags fin((size_t)nslab), fdec((size_t)nslab), fout((size_t)nslab);
   std::atomic<int> lane_err{ZH_OK};
   std::string lane_msg;
   std::mutex lane_mu;
-  auto lane_fail = [&](hipError_t e, const char* what) {
-    std::lock_guard<std::mutex> lk(lane_mu);
-    if (lane_err.load() == ZH_OK) {
-      lane_err = e == hipErrorOutOfMemory ? ZH_ENOMEM : ZH_EHIP;
-      lane_msg = std::string(what) + ": " + hipGetErrorName(e) + " (" + hipGetErrorString(e) + ")";
-    }
+  // the in lanes' job queue, filled as plans are created (deque: stable references)
+  std::deque<InJob> ijobs;
+  std::vector<int64_t> in_total((size_t)nslab, 0);
+  std::mutex qmu;
+  std::condition_variable qcv;
+  size_t next_in = 0;
+  bool all_published = false, q_abort = false;
+  auto abort_all = [&] {
     fin.abort();
     fdec.abort();
     fout.abort();
+    std::lock_guard<std::mutex> lk(qmu);
+    q_abort = true;
+    qcv.notify_all();
+  };
+  auto lane_fail = [&](hipError_t e, const char* what) {
+    {
+      std::lock_guard<std::mutex> lk(lane_mu);
+      if (lane_err.load() == ZH_OK) {
+        lane_err = e == hipErrorOutOfMemory ? ZH_ENOMEM : ZH_EHIP;
+        lane_msg = std::string(what) + ": " + hipGetErrorName(e) + " (" + hipGetErrorString(e) + ")";
+      }
+    }
+    abort_all();
   };
   std::vector<std::thread> th;
-  std::atomic<int64_t> next_in{0}, next_out{0};
-  std::vector<std::atomic<int64_t>> in_done((size_t)np), out_done((size_t)np);
+  std::atomic<int64_t> next_out{0};
+  std::vector<std::atomic<int64_t>> in_done((size_t)nslab), out_done((size_t)nslab);
   for (auto& x : in_done) x = 0;
   for (auto& x : out_done) x = 0;
+  // status of the slabs, in C order: planning failure (from slab plan_fail on), device errors
+  int plan_st = ZH_OK, dev_st = ZH_OK;
+  std::string plan_msg, dev_msg;
+  int64_t nplan = nslab;  // slabs that got a plan
   const bool go = st == ZH_OK && he == hipSuccess;
   if (go) {
-    // slabs with nothing to copy in are ready at once
-    for (int64_t r = 0; r < np; r++)
-      if (in_total[(size_t)r] == 0) fin.set((size_t)r);
     // ---- in lanes
     for (int L = 0; L < lanes_in; L++)
       th.emplace_back([&, L] {
         (void)hipSetDevice(ctx->device);
         int flip = 0;
         for (;;) {
-          const int64_t j = next_in.fetch_add(1);
-          if (j >= (int64_t)ijobs.size() || lane_err.load() != ZH_OK) break;
-          InJob& J = ijobs[(size_t)j];
+          InJob* Jp = nullptr;
+          {
+            std::unique_lock<std::mutex> lk(qmu);
+            qcv.wait(lk, [&] { return next_in < ijobs.size() || all_published || q_abort; });
+            if (q_abort || next_in >= ijobs.size()) break;
+            Jp = &ijobs[next_in++];
+          }
+          InJob& J = *Jp;
           hipError_t e = hipSuccess;
           if (J.direct) {
             e = hipMemcpyAsync(J.dst, J.direct, (size_t)J.len, hipMemcpyHostToDevice, ctx->pipe_in);
@@ -483,12 +495,73 @@ int read_pipelined(zh_ctx* ctx, const zh_array_meta* meta, const SrcDesc* srcs, 
         }
         if (lane_err.load() == ZH_OK) drain();
       });
-    // ---- decode (this thread)
-    for (int64_t r = 0; r < np; r++) {
+    // ---- this thread: plans (at most W alive), decode, status
+    int64_t created = 0, retired = 0;
+    auto publish_done = [&] {
+      std::lock_guard<std::mutex> lk(qmu);
+      all_published = true;
+      qcv.notify_all();
+    };
+    auto create = [&](int64_t r) -> bool {
+      Slab& S = slabs[(size_t)r];
+      char e[1024] = {0};
+      zh_plan* p = nullptr;
+      const int rc = plan_create(ctx, meta, S.sub.data(), (int64_t)S.sub.size(), S.o, S.s,
+                                 (flags & ZH_SRC_DEVICE) | ZH_OUT_DEVICE, true, &p, e, sizeof e);
+      if (rc != ZH_OK) {
+        plan_st = rc;
+        plan_msg = e;
+        return false;
+      }
+      plans[(size_t)r] = p;
+      std::vector<InJob> js;
+      bool pg = false;
+      in_jobs(p, r, cfg.chunk, js, &pg);
+      {
+        std::lock_guard<std::mutex> lk(qmu);
+        in_total[(size_t)r] = (int64_t)js.size();
+        for (auto& j : js) ijobs.push_back(std::move(j));
+        qcv.notify_all();
+      }
+      if (js.empty()) fin.set((size_t)r);
+      return true;
+    };
+    // retire: the plan's status (deferred device errors, C order), then its blocks go back
+    auto retire = [&](int64_t k) {
+      zh_plan* p = plans[(size_t)k];
+      if (!p) return;
+      char e[1024] = {0};
+      // its own decode only (the stream holds later slabs' work)
+      if (p->done_ev) (void)hipEventSynchronize(p->done_ev);
+      p->last_stream = nullptr;
+      if (dev_st == ZH_OK && lane_err.load() == ZH_OK) {
+        const int rc = zh_plan_wait(p, e, sizeof e);
+        if (rc != ZH_OK) {
+          dev_st = rc;
+          dev_msg = e;
+        }
+      }
+      plan_free(p);
+      plans[(size_t)k] = nullptr;
+    };
+    auto top_up = [&](int64_t upto) {  // plans for slabs < upto
+      while (created < upto && created < nplan) {
+        if (created - retired >= W) retire(retired++);
+        if (dev_st != ZH_OK) return;
+        if (!create(created)) {
+          nplan = created;
+          return;
+        }
+        created++;
+      }
+    };
+    top_up(W);
+    if (created >= nplan) publish_done();
+    for (int64_t r = 0; r < nplan && dev_st == ZH_OK; r++) {
       if (!fin.wait((size_t)r)) break;
       hipError_t e = hipSuccess;
       if (in_total[(size_t)r] > 0) e = hipStreamWaitEvent(sdec, in_ev[(size_t)r], 0);
-      void* dst = (uint8_t*)out + obase[(size_t)r];
+      void* dst = (uint8_t*)out + slabs[(size_t)r].obase;
       if (host_out) {
         dst = dslot[(size_t)(r % nds)];
         if (r >= nds) {  // the slot's previous slab has been copied out
@@ -500,20 +573,33 @@ int read_pipelined(zh_ctx* ctx, const zh_array_meta* meta, const SrcDesc* srcs, 
         lane_fail(e, "pipelined read: stream wait");
         break;
       }
-      int rc = plan_enqueue_impl(plans[(size_t)r], dst, sdec);
-      if (rc == ZH_OK) rc = plan_mark_done_impl(plans[(size_t)r], sdec);
-      if (rc == ZH_OK) plans[(size_t)r]->last_stream = sdec;
+      zh_plan* p = plans[(size_t)r];
+      int rc = plan_enqueue_impl(p, dst, sdec);
+      if (rc == ZH_OK) rc = plan_mark_done_impl(p, sdec);
+      if (rc == ZH_OK) p->last_stream = sdec;
       e = rc == ZH_OK ? hipEventRecord(dec_ev[(size_t)r], sdec) : hipErrorLaunchFailure;
       if (e != hipSuccess) {
         lane_fail(e, "pipelined read: kernel launch");
         break;
       }
       fdec.set((size_t)r);
+      // the next plan (its input copies start while this slab decodes); the slab W back is
+      // retired first: its decode was enqueued before this one
+      top_up(r + W + 1);
+      if (created >= nplan) publish_done();
     }
+    if (dev_st != ZH_OK || lane_err.load() != ZH_OK || nplan < nslab) {
+      // stop: no further slab is decoded, so nothing waits for the lanes' remaining jobs
+      if (dev_st != ZH_OK || lane_err.load() != ZH_OK) abort_all();
+    }
+    publish_done();
+    // out lanes wait for slabs that were never decoded (a planning failure): release them
+    if (nplan < nslab) fdec.abort();
     for (auto& t : th) t.join();
     (void)hipStreamSynchronize(sdec);
     if (ctx->pipe_in) (void)hipStreamSynchronize(ctx->pipe_in);
     if (ctx->pipe_out) (void)hipStreamSynchronize(ctx->pipe_out);
+    while (retired < created) retire(retired++);
   }
   // ---- status: the first failing slab in C order
   if (st == ZH_OK && he != hipSuccess) {
@@ -524,14 +610,16 @@ int read_pipelined(zh_ctx* ctx, const zh_array_meta* meta, const SrcDesc* srcs, 
     set_err(err, errlen, "%s", lane_msg.c_str());
     st = lane_err.load();
   }
-  if (st == ZH_OK) {
-    for (int64_t r = 0; r < np && st == ZH_OK; r++) st = zh_plan_wait(plans[(size_t)r], err, errlen);
-    if (st == ZH_OK && plan_st != ZH_OK) {
-      set_err(err, errlen, "%s", plan_msg.c_str());
-      st = plan_st;
-    }
+  if (st == ZH_OK && dev_st != ZH_OK) {
+    set_err(err, errlen, "%s", dev_msg.c_str());
+    st = dev_st;
   }
-  for (zh_plan* p : plans) plan_free(p);
+  if (st == ZH_OK && plan_st != ZH_OK) {
+    set_err(err, errlen, "%s", plan_msg.c_str());
+    st = plan_st;
+  }
+  for (zh_plan* p : plans)
+    if (p) plan_free(p);
   for (size_t k = 0; k < dslot.size(); k++) ctx_release(ctx, dslot[k], dslot_got[k]);
   for (auto* v : {&in_ev, &dec_ev, &out_ev, &slot_ev})
     for (hipEvent_t e : *v)

@@ -320,6 +320,11 @@ class ZstdCodec(Codec):
         n = C.c_size_t()
         err = C.create_string_buffer(256)
         st = L.zh_zstd_decompress(b, len(b), None, 0, C.byref(n), err, 256)
+        # the size query answers from the frame header without decoding a block: never size an
+        # allocation beyond what the frame can expand to (an RLE block: 4 bytes → 128 KiB)
+        if st == A.ZH_OK and n.value > len(b) * 32768 + (64 << 10):
+            raise ZarrException(f"Error in decoding zstd: frame content size {n.value} exceeds "
+                                f"what {len(b)} bytes of frame can hold")
         if st == A.ZH_OK:
             out = (C.c_char * max(1, n.value))()
             st = L.zh_zstd_decompress(b, len(b), out, n.value, C.byref(n), err, 256)
