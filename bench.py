@@ -1111,6 +1111,49 @@ def shuffled_variant(dev, A, L, meta, out, shape, slab, offs, sizes, steps, clas
             "roofline": roof}
 
 
+def default_alloc_variant(dev, A, L, meta, out, shard_slab, offs, caps, shape, steps):
+    """The headline decode into a plain hipMalloc output instead of the probe-selected VMM
+    arena (what a library caller gets with a default allocation, DESIGN §4 "Placement").  The
+    c4 shards are re-encoded from `out` (it holds the generator's array), `out` is freed and a
+    hipMalloc buffer of the same size takes the decode; verified, timed like the headline.
+    Frees `out`."""
+    n = meta.ndim
+    nel = 1
+    for v in shape:
+        nel *= v
+    nb = nel * 4
+    sizes = dev.array_write(meta, out, [0] * n, shape,
+                            [(shard_slab + o, c) for o, c in zip(offs, caps)])
+    dev.free(out)
+    plain = dev.malloc(nb, 0)
+    try:
+        plan = dev.plan(meta, [(shard_slab + o, s) for o, s in zip(offs, sizes)], [0] * n,
+                        shape, A.ZH_SRC_DEVICE | A.ZH_OUT_DEVICE)
+        st = plan.stats()
+        dev.memset(plain, 0, nb)
+        plan.execute(plain)
+        plan.wait()
+        bad = dev.synth_verify(plain, shape, [0] * n, shape, 4, SEED)
+        if bad:
+            raise SystemExit(f"hipMalloc-output decode verification FAILED: {bad}")
+        plan.set_timing(True)
+        dev.sync()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            plan.execute(plain)
+        plan.wait()
+        el = time.perf_counter() - t0
+        roof = roofline_of(plan, st)
+        plan.close()
+        rate = dev.write_rate(plain, nb, 0, 2)
+    finally:
+        dev.free(plain)
+    return {"description": "c4 decoded into a plain hipMalloc output (no arena probe)",
+            "value": round(steps * nb / el / GiB, 2), "unit": "GiB/s",
+            "ms_per_step": round(el * 1e3 / steps, 3), "verified_elements": nel,
+            "store_probe_GBps": round(rate, 1), "roofline": roof}
+
+
 def oneshot_read(dev, A, meta, sources, shape, out, reps=3):
     """zh_array_read of the whole array, device in and out: plan + tables upload + execute +
     status read-back + teardown in one call, as core.Array.read does every call."""
@@ -1333,10 +1376,15 @@ def main():
         extras["c4shuf"] = shuffled_variant(dev, A, L, meta, out, shape, shard_slab, offs,
                                             sizes, min(args.steps, 10))
         log(f"[rank {rank}] c4shuf: {json.dumps(extras['c4shuf'])}")
+        extras["c4_hipmalloc"] = default_alloc_variant(dev, A, L, meta, out, shard_slab, offs,
+                                                       caps, shape, min(args.steps, 10))
+        out = None  # freed by default_alloc_variant
+        log(f"[rank {rank}] c4_hipmalloc: {json.dumps(extras['c4_hipmalloc'])}")
     if plan is not None:
         plan.close()
     dev.free(shard_slab)
-    dev.free(out)
+    if out is not None:
+        dev.free(out)
     if rank == 0:
         print(json.dumps(line), flush=True)
     dist.close()

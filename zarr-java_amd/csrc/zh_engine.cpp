@@ -982,6 +982,23 @@ int plan_create(zh_ctx* ctx, const zh_array_meta* m, const SrcDesc* srcs, int64_
       }
       hs[i].data = p->d_input + stage_off[i];
     }
+    // copies adjacent on both sides become one (a run of pieces read side by side into one
+    // host buffer lands side by side in the staging when their stored offsets share a residue
+    // mod 256): fewer, larger DMAs
+    size_t w = 0;
+    for (size_t k = 0; k < p->h2d.size(); k++) {
+      if (w > 0 && p->h2d[w - 1].first + p->h2d_len[w - 1] == p->h2d[k].first &&
+          (const uint8_t*)p->h2d[w - 1].second + p->h2d_len[w - 1] ==
+              (const uint8_t*)p->h2d[k].second) {
+        p->h2d_len[w - 1] += p->h2d_len[k];
+        continue;
+      }
+      p->h2d[w] = p->h2d[k];
+      p->h2d_len[w] = p->h2d_len[k];
+      w++;
+    }
+    p->h2d.resize(w);
+    p->h2d_len.resize(w);
   }
   // the piece tables (device addresses of every held range)
   std::vector<DevPiece> dpieces;
