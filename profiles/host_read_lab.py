@@ -128,6 +128,14 @@ def main():
     pieces = [ShardSource(base, isz, nb, ps)]
     run("pieces_pinned_in_pinned_out", None, lambda: pin_out, pieces=pieces)
     run("pieces_pinned_in_warm_out", None, lambda: warm_out, pieces=pieces)
+    # the pieces form as the JNI passes it: each piece its own pageable (Java heap) array
+    heap = [np.frombuffer(bytes((C.c_char * x).from_address(pin_shard + o)), np.uint8).copy()
+            for o, x in rs]
+    hidx = np.frombuffer(idx, np.uint8).copy()
+    hp = [ShardSource(hidx.ctypes.data, isz, nb,
+                      [(o, x, h.ctypes.data, x) for (o, x), h in zip(rs, heap)])]
+    run("pieces_pageable_in_warm_out", None, lambda: warm_out, pieces=hp)
+    run("pieces_pageable_in_fresh_out", None, lambda: np.empty(obytes, np.uint8), pieces=hp)
     dev.free_pinned(pin_out)
     dev.free_pinned(pin_shard)
     dev.free(dshard)

@@ -162,38 +162,32 @@ def jni_fetch(meta, paths, offset, shape, max_run=64 << 20, size_known=True, dro
 
 
 def jni_read(dev, meta, fetched, offset, shape):
-    """The JNI marshalling of arrayReadPieces: one zh_host_staging block holds every index
-    and piece (each byte[] copied in once) followed by the output; zh_array_read_pieces
-    decodes into the staging; the region is then copied out (into the Java array)."""
+    """The JNI marshalling of arrayReadPieces (java/jni/zarrhip_jni.c): no copy on the binding
+    side.  Every index and piece byte[] (here: one host buffer each, as the store returned it)
+    and the result's primitive array (allocated zeroed, as the JVM does) are passed to
+    zh_array_read_pieces as they are; the library's pipelined read copies the sources once into
+    its page-locked ring and the region straight into the result."""
     from zarrhip._lib import ShardSource
     nel = int(np.prod(shape))
-    obytes = nel * meta.dtype_size
-    tot = 0
-    for s in fetched:
-        if s is not None:
-            tot += (len(s[0]) if s[0] is not None else 0) + sum(len(b) for _, b in s[2])
-    in_cap = (tot + 255) // 256 * 256
-    base = dev.host_staging(in_cap + obytes)
-    pos = 0
-
-    def put(b):
-        nonlocal pos
-        p = base + pos
-        C.memmove(p, b, len(b))
-        pos += len(b)
-        return p
-    shards = []
+    keep, shards = [], []
     for s in fetched:
         if s is None:
             shards.append(None)
             continue
         idx, size, pieces = s
-        ip = put(idx) if idx is not None else None
-        ps = [(o, len(b), put(b), len(b)) for o, b in pieces]
+        ip = None
+        if idx is not None:
+            ib = (C.c_char * max(1, len(idx))).from_buffer_copy(idx or b"\0")
+            keep.append(ib)
+            ip = C.addressof(ib)
+        ps = []
+        for o, b in pieces:
+            pb = (C.c_char * max(1, len(b))).from_buffer_copy(b or b"\0")
+            keep.append(pb)
+            ps.append((o, len(b), C.addressof(pb), len(b)))
         shards.append(ShardSource(ip, len(idx) if idx is not None else 0, size, ps))
-    dev.array_read_pieces(meta, shards, offset, shape, base + in_cap, 0)
-    out = np.empty(nel, NP_DT[meta.dtype_size])
-    C.memmove(out.ctypes.data, base + in_cap, obytes)
+    out = np.zeros(nel, NP_DT[meta.dtype_size])
+    dev.array_read_pieces(meta, shards, offset, shape, out.ctypes.data, 0)
     return out.reshape(shape)
 
 

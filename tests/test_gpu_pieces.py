@@ -336,7 +336,8 @@ def test_jni_sequence_sub_shard_2gib(dev, tmp_path):
     [0,3,2,1], bytes big, index crc32c at the end) references 16 384 inner chunks = 2^31
     bytes of payload — more than one Java array holds, which is why the JNI passes pieces and
     never a compacted shard.  The shard is encoded on the device, stored as a file, fetched as
-    index + ranges, staged once into zh_host_staging and decoded; the result equals the oracle's
+    index + ranges, passed as they are (the JNI's critical-section form) and decoded through the
+    pipelined read; the result equals the oracle's
     FilesystemStore read (zo_array_read_store: suffix index read, one range read per inner
     chunk, ShardingIndexedCodec.java:253, 333-357)."""
     shape = [1, 1024, 1024, 1024]
@@ -388,3 +389,139 @@ def test_jni_sequence_sub_shard_2gib(dev, tmp_path):
         assert str(ed.value) == str(eo.value)
     finally:
         os.unlink(path)
+
+
+def test_pieces_form_errors(dev, tmp_path):
+    """Malformed sub-shard forms fail before any device work: unsorted or overlapping pieces
+    and a host-decoded piece under nested sharding → ZH_EINVAL; an index shorter than the
+    index size → the 'smaller than its index' message; a shard without index must be one
+    whole piece at offset 0."""
+    meta, arr, shards = make_case("sharded", seed=43)
+    paths = write_store(tmp_path, meta, shards)
+    off, shp = [1, 1, 1], [6, 14, 22]
+    fetched = jni_fetch(meta, region_paths(meta, paths, off, shp), off, shp, max_run=0)
+    idx, size, pieces = fetched[0]
+    keep = [(C.c_char * len(idx)).from_buffer_copy(idx)]
+    ps = []
+    for o, b in pieces:
+        keep.append((C.c_char * len(b)).from_buffer_copy(b))
+        ps.append((o, len(b), C.addressof(keep[-1]), len(b)))
+    out = np.empty(shp, np.uint32)
+    ip = C.addressof(keep[0])
+    with pytest.raises(ZhError) as e:  # unsorted
+        dev.array_read_pieces(meta, [ShardSource(ip, len(idx), size, ps[::-1])], off, shp,
+                              out.ctypes.data, 0)
+    assert e.value.status == A.ZH_EINVAL
+    o0, n0, p0, h0 = ps[0]
+    with pytest.raises(ZhError) as e:  # overlapping
+        dev.array_read_pieces(meta, [ShardSource(ip, len(idx), size, [ps[0], (o0 + 4, n0, p0,
+                                                                         n0)] + ps[1:])],
+                              off, shp, out.ctypes.data, 0)
+    assert e.value.status == A.ZH_EINVAL
+    with pytest.raises(ZhError) as e:  # short index
+        dev.array_read_pieces(meta, [ShardSource(ip, len(idx) - 1, size, ps)], off, shp,
+                              out.ctypes.data, 0)
+    assert e.value.status == A.ZH_EDATA and "smaller than its index" in str(e.value)
+    with pytest.raises(ZhError) as e:  # no index, not a whole piece
+        dev.array_read_pieces(meta, [ShardSource(None, 0, size, ps[:2])], off, shp,
+                              out.ctypes.data, 0)
+    assert e.value.status == A.ZH_EINVAL
+    # the well-formed call still reads correctly
+    dev.array_read_pieces(meta, [ShardSource(ip, len(idx), size, ps)], off, shp,
+                          out.ctypes.data, 0)
+    np.testing.assert_array_equal(out, oracle_region(meta, shards, off, shp))
+
+
+def test_pieces_unknown_size_out_of_range_entry(dev):
+    """shard_nbytes = -1 (StoreHandle.getSize() unknown): an entry pointing beyond the bytes
+    the store could deliver has no piece, so the device reports the reference's "Could not
+    load byte data for chunk [...]" — after a correct index crc32c."""
+    meta, arr, shards = make_case("sharded", seed=47, fill_frac=0.0)
+    isz = lib().zh_shard_index_size(C.byref(meta))
+    raw = shards[0]
+    body = bytearray(raw[-isz:-4])
+    o, nb = struct.unpack("<QQ", body[16:32])  # inner chunk [0, 0, 1]
+    body[16:24] = struct.pack("<Q", o + (1 << 40))
+    nidx = bytes(body) + struct.pack("<I", O.crc32c(bytes(body)))
+    from zarrhip._lib import shard_ranges
+    off, shp = [0, 0, 0], [8, 16, 24]
+    lo, hi = [0, 0, 0], [8, 16, 24]
+    rs = shard_ranges(meta, nidx, -1, lo, hi, 0)
+    keep = [(C.c_char * isz).from_buffer_copy(nidx)]
+    ps = []
+    for ro, rn in rs:
+        if ro >= len(raw):  # the store read fails: no piece
+            continue
+        keep.append((C.c_char * rn).from_buffer_copy(raw[ro:ro + rn]))
+        ps.append((ro, rn, C.addressof(keep[-1]), rn))
+    out = np.empty(shp, np.uint32)
+    with pytest.raises(ZhError) as e:
+        dev.array_read_pieces(meta, [ShardSource(C.addressof(keep[0]), isz, -1, ps)], off,
+                              [7, 16, 24], out.ctypes.data, 0)
+    assert str(e.value) == "Could not load byte data for chunk [0, 0, 1]"
+
+
+def test_pieces_nested_and_multi_context(dev, tmp_path):
+    """Nested sharding through the pieces form on three contexts of the card
+    (zh_array_read_pieces_multi: one slab per context, same-device routes)."""
+    from zarrhip._lib import DeviceContext, array_read_pieces_multi
+    meta, arr, shards = make_case("nested", seed=53)
+    paths = write_store(tmp_path, meta, shards)
+    off, shp = [2, 3, 5], [21, 27, 40]
+    fetched = jni_fetch(meta, region_paths(meta, paths, off, shp), off, shp, max_run=1 << 16)
+    keep, srcs = [], []
+    for s in fetched:
+        if s is None:
+            srcs.append(None)
+            continue
+        idx, size, pieces = s
+        ib = (C.c_char * len(idx)).from_buffer_copy(idx) if idx is not None else None
+        keep.append(ib)
+        ps = []
+        for o, b in pieces:
+            keep.append((C.c_char * len(b)).from_buffer_copy(b))
+            ps.append((o, len(b), C.addressof(keep[-1]), len(b)))
+        srcs.append(ShardSource(C.addressof(ib) if ib is not None else None,
+                                len(idx) if idx is not None else 0, size, ps))
+    ctxs = [dev, DeviceContext(0), DeviceContext(0)]
+    try:
+        out = np.empty(shp, np.uint32)
+        array_read_pieces_multi(ctxs, meta, srcs, off, shp, out.ctypes.data, 0)
+        np.testing.assert_array_equal(out, oracle_region(meta, shards, off, shp))
+    finally:
+        for c in ctxs[1:]:
+            c.close()
+
+
+def test_pieces_from_pinned_staging(dev, tmp_path):
+    """zh_host_staging: a binding that copies its sources into the context's page-locked
+    staging (and takes the region back through it) gets direct DMA both ways."""
+    meta, arr, shards = make_case("transpose_be", seed=59)
+    paths = write_store(tmp_path, meta, shards)
+    off, shp = [1, 2, 3], [22, 28, 40]
+    fetched = jni_fetch(meta, region_paths(meta, paths, off, shp), off, shp, max_run=1 << 20)
+    tot = sum((len(s[0]) if s[0] is not None else 0) + sum(len(b) for _, b in s[2])
+              for s in fetched if s is not None)
+    obytes = int(np.prod(shp)) * 4
+    in_cap = (tot + 255) // 256 * 256
+    base = dev.host_staging(in_cap + obytes)
+    pos, srcs = 0, []
+    for s in fetched:
+        if s is None:
+            srcs.append(None)
+            continue
+        idx, size, pieces = s
+        ip = None
+        if idx is not None:
+            C.memmove(base + pos, idx, len(idx))
+            ip = base + pos
+            pos += len(idx)
+        ps = []
+        for o, b in pieces:
+            C.memmove(base + pos, b, len(b))
+            ps.append((o, len(b), base + pos, len(b)))
+            pos += len(b)
+        srcs.append(ShardSource(ip, len(idx) if idx is not None else 0, size, ps))
+    dev.array_read_pieces(meta, srcs, off, shp, base + in_cap, 0)
+    got = np.frombuffer(C.string_at(base + in_cap, obytes), np.uint32).reshape(shp)
+    np.testing.assert_array_equal(got, oracle_region(meta, shards, off, shp))

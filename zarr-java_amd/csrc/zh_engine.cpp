@@ -1197,7 +1197,6 @@ int plan_create(zh_ctx* ctx, const zh_array_meta* m, const SrcDesc* srcs, int64_
   // non-temporal loads + stores: +4 % on the row path, +1 % on the tile path (interleaved
   // A/B in one process, profiles/r01/experiments/tune_*.json)
   p->args.nt = env_int("ZH_NT", 3) & 7;  // bit 2: 8 rows in flight per lane (rows)
-  p->args.crc_edge = env_int("ZH_CRC_EDGE", 0);
   // Visit items in a golden-ratio stride order: +3.6 % on the tile path (c4) on every normal
   // allocation, neutral on the row path (interleaved A/B, profiles/placement_perm.py), so
   // on by default for tiles.  ZH_ITEM_PERM=0/1 overrides.
@@ -2281,7 +2280,6 @@ static int array_write_fast(zh_ctx* ctx, const zh_array_meta* m, ScatterArgs a,
   if (crc_fuse)
     ZH_HIPF(hipMemsetAsync(W + o_cpart, 0, (size_t)(items * nspan) * sizeof(uint32_t), s));
   v.nt = env_int("ZH_ENC_NT", 3) & 3;
-  v.crc_edge = env_int("ZH_ENC_CRC_EDGE", 0);
   // narrow rows: G consecutive chunks per work item so a wave load covers G·row bytes of a
   // region row (ZH_ENC_GROUP: 0 off, default G·row = 256 B; encode_group_rows_kernel; c3
   // write G × U grid in profiles/r02/write/ab_enc3.txt: G = 2, U = 4 best, 40.1 → 36.2 ms)

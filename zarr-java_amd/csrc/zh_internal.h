@@ -140,11 +140,6 @@ struct ScatterArgs {
   int32_t dsize;
   int32_t tile;
   int32_t nt;                   // fast kernels: bit 0 non-temporal loads, bit 1 stores
-  int32_t crc_edge;             // chunk-CRC kernels (lab switch): the first / last 16 B of each
-                                // contiguous payload segment loaded (decode) or stored (encode)
-                                // temporal; such a payload starts off the line grid (4-byte
-                                // crc32c before it), so its edge lines are shared with the
-                                // neighbouring segments
   int32_t tile_variant;         // tile fast path: 0 row-per-tile loads, 1 row-interleaved groups,
                                 // 10 + G / 20 + G: tiles_group_kernel (without / with prefetch);
                                 // 30 + G (+10, +20, +30): chunk CRC on waves of its own / over

@@ -1271,11 +1271,6 @@ __global__ __launch_bounds__(kBlock) void rows_group_kernel(ScatterArgs a) {
   for (int o = 0; o < 64; o += GL) qmask |= (((1ull << (1 << vs)) - 1) << (q << vs)) << o;
   const bool leader = lane == (q << vs);
   const uint4 ffill = fill16<DS>(a.fill);
-  // a wave's rows of one chunk are one contiguous payload segment: its first / last vector
-  const uint32_t wrows = 64 / GL;  // rows of one chunk per wave instruction
-  const bool edge_cached = CRC && a.crc_edge != 0;
-  const bool edge = (col == 0 && lr % wrows == 0) ||
-                    (col == (16u << vs) - 16 && lr % wrows == wrows - 1);
   for (int64_t g = blockIdx.x; g < ngroups; g += gridDim.x) {
     const int64_t pg = a.item_mul ? (int64_t)(((uint64_t)g * a.item_mul) % (uint64_t)ngroups) : g;
     const int64_t c = pg * G + q;
@@ -1312,22 +1307,14 @@ __global__ __launch_bounds__(kBlock) void rows_group_kernel(ScatterArgs a) {
           row_offsets(a, tab, r, so, dof);
           dd[u] = dof * DS;
           v[u] = fv;
-          if (!fill) {
-            if (!FLAGS && edge_cached && edge)  // ZH_CRC_EDGE (see tiles_rowcrc_kernel)
-              v[u] = ld16s<false>(src + so * DS);
-            else
-              v[u] = ld16s<(NT & 1) != 0>(src + so * DS);
-          }
+          if (!fill) v[u] = ld16s<(NT & 1) != 0>(src + so * DS);
         }
       }
 #pragma unroll
       for (int u = 0; u < U; u++)
         if (dd[u] != ~0ull) {
           const uint4 w = fill ? fv : xform16<DS>(v[u], a.swap, a.is_bool);
-          if (FLAGS && edge_cached && edge)  // ZH_ENC_CRC_EDGE: the payload segment's edges
-            st16s<false>(dst + dd[u], w);
-          else
-            st16s<(NT & 2) != 0>(dst + dd[u], w);
+          st16s<(NT & 2) != 0>(dst + dd[u], w);
           if (FLAGS)
             differs |= (v[u].x != ffill.x) | (v[u].y != ffill.y) | (v[u].z != ffill.z) |
                        (v[u].w != ffill.w);
@@ -1785,11 +1772,7 @@ __global__ __launch_bounds__(kBlock) void tiles_group_kernel(ScatterArgs a) {
           y.y = mine[(g * 4 + 1) * 33 + r];
           y.z = mine[(g * 4 + 2) * 33 + r];
           y.w = mine[(g * 4 + 3) * 33 + r];
-          if (CRC && FLAGS && a.crc_edge != 0 &&
-              ((ti == 0 && g == 0) || (ti == TG - 1 && g == 7)))  // ZH_ENC_CRC_EDGE
-            st16s<false>(base + (size_t)r * d_fs * 4, y);
-          else
-            st16s<(NT & 2) != 0>(base + (size_t)r * d_fs * 4, y);
+          st16s<(NT & 2) != 0>(base + (size_t)r * d_fs * 4, y);
           if constexpr (CRC && FLAGS) {  // encode: the stored vectors
             const v4u w = {y.x, y.y, y.z, y.w};
             const uint32_t ck = crc_upd16_k(0u, w, T);
@@ -2054,11 +2037,6 @@ void tiles_rowcrc_kernel(ScatterArgs a) {
   const bool leader = lane == q * TG * 8;
   const uint32_t fillv = (uint32_t)a.fill;
   auto sw = [](uint32_t x) { return SWAP ? __builtin_bswap32(x) : x; };
-  // the first and last 16 B of a wave's contiguous payload segment (tiles ti = 0 / TG - 1):
-  // a payload after a 4-byte crc32c starts off the line grid, so those lines are shared with
-  // the neighbouring segments (ZH_NT bit 3 loads them temporal so the neighbour hits in L2)
-  const bool edge_cached = a.crc_edge != 0 && !ENC;
-  const bool edge = (ti == 0 && g == 0) || (ti == TG - 1 && g == 7);
   for (int64_t gi = blockIdx.x; gi < ngroups; gi += gridDim.x) {
     const int64_t pg = a.item_mul ? (int64_t)(((uint64_t)gi * a.item_mul) % (uint64_t)ngroups) : gi;
     const int64_t c = pg * G + q, cc = pg * G + qc;
@@ -2090,16 +2068,8 @@ void tiles_rowcrc_kernel(ScatterArgs a) {
       const uint32_t uu = ub_ + ti;
       if (on && uu < units) {
         const uint8_t* base = src + ((size_t)tab[uu].x + g * 4) * 4;
-        if (edge_cached) {  // ZH_CRC_EDGE: the segment's edge vectors as temporal loads
 #pragma unroll
-          for (int k = 0; k < 8; k++) {
-            const uint8_t* p = base + (size_t)(wave * 8 + k) * s_fd * 4;
-            x[k] = edge ? ld16s<false>(p) : ld16s<true>(p);
-          }
-        } else {
-#pragma unroll
-          for (int k = 0; k < 8; k++) x[k] = ld16s<true>(base + (size_t)(wave * 8 + k) * s_fd * 4);
-        }
+        for (int k = 0; k < 8; k++) x[k] = ld16s<true>(base + (size_t)(wave * 8 + k) * s_fd * 4);
       }
     };
     if (!ENC) load(0);

@@ -244,11 +244,16 @@ JNIEXPORT jint JNICALL Java_dev_zarr_zarrjava_hip_ZarrHip_shardDecodePartial(
 }
 
 /* ---- sub-shard reads: stored index + pieces (zh_array_read_pieces) ---------------------
- * Pure argument marshalling: every index and piece byte[] is copied once into the context's
- * page-locked staging (zh_host_staging), the decoded region comes back through the same
- * staging (direct DMA both ways) and is copied once into the Java array.  The index is never
- * read here; the device checks it.  tests/helpers.py jni_fetch/jni_read restate this sequence
- * in ctypes and the GPU tests run it (tests/test_gpu_pieces.py). */
+ * Pure argument marshalling, no copy on this side: the index and piece byte[]s and the
+ * result's primitive array are held with GetPrimitiveArrayCritical for the duration of the
+ * call and handed to the library as host memory.  The library's pipelined read copies each
+ * source once, on several threads, into its page-locked ring and DMAs it (and back out into
+ * the result the same way); a single-threaded copy here (GetByteArrayRegion into a staging
+ * buffer, then a memcpy into the result) would cost more than the whole read for GiB-sized
+ * regions.  While the critical sections are held the call makes no JNI call; the GC waits for
+ * at most the read itself.  The shim never reads the index (the device checks it).
+ * tests/helpers.py jni_fetch / jni_read restate this call sequence in ctypes, and the GPU
+ * tests run it (tests/test_gpu_pieces.py). */
 
 JNIEXPORT jlongArray JNICALL Java_dev_zarr_zarrjava_hip_ZarrHip_shardRanges(
     JNIEnv* env, jclass cls, jintArray jm, jlongArray jshape, jintArray jchunk, jintArray jinner,
@@ -293,96 +298,110 @@ JNIEXPORT jlongArray JNICALL Java_dev_zarr_zarrjava_hip_ZarrHip_shardRanges(
   return res;
 }
 
-/* The shards of a read into zh_shard_src form, their bytes copied into `staging` (which has
- * room for them: the caller sized it with pieces_bytes). */
-static jlong pieces_bytes(JNIEnv* env, jobjectArray jidx, jobjectArray jdata) {
-  jsize n = (*env)->GetArrayLength(env, jidx);
-  jlong tot = 0;
-  for (jsize i = 0; i < n; i++) {
-    jbyteArray ib = (jbyteArray)(*env)->GetObjectArrayElement(env, jidx, i);
-    if (ib) tot += (*env)->GetArrayLength(env, ib);
-    if (ib) (*env)->DeleteLocalRef(env, ib);
-    jobjectArray ps = (jobjectArray)(*env)->GetObjectArrayElement(env, jdata, i);
-    jsize np = ps ? (*env)->GetArrayLength(env, ps) : 0;
-    for (jsize k = 0; k < np; k++) {
-      jbyteArray b = (jbyteArray)(*env)->GetObjectArrayElement(env, ps, k);
-      if (b) tot += (*env)->GetArrayLength(env, b);
-      if (b) (*env)->DeleteLocalRef(env, b);
-    }
-    if (ps) (*env)->DeleteLocalRef(env, ps);
-  }
-  return tot;
+/* The shards of a read as zh_shard_src: every index / piece array is collected (local
+ * references, lengths, offsets: JNI calls) first, then all of them and the output enter their
+ * critical sections together (no JNI call in between).  pin_release() leaves them. */
+typedef struct {
+  jsize n;                 /* arrays held */
+  jarray* arr;             /* index / piece byte[]s, then the output */
+  void** ptr;              /* their critical addresses */
+  zh_shard_piece* pieces;
+} Pinned;
+
+static void pin_release(JNIEnv* env, Pinned* P, jsize n_out) {
+  /* the output (the last `n_out` entries) is written back; the sources are not */
+  for (jsize k = P->n - 1; k >= 0; k--)
+    if (P->ptr[k])
+      (*env)->ReleasePrimitiveArrayCritical(env, P->arr[k], P->ptr[k],
+                                            k >= P->n - n_out ? 0 : JNI_ABORT);
+  free(P->arr);
+  free(P->ptr);
+  free(P->pieces);
+  memset(P, 0, sizeof(*P));
 }
 
-static int marshal_pieces(JNIEnv* env, jobjectArray jidx, jlongArray jsizes, jobjectArray joffs,
-                          jobjectArray jlens, jobjectArray jdata, uint8_t* staging,
-                          zh_shard_src* srcs, zh_shard_piece** pieces_out) {
-  jsize n = (*env)->GetArrayLength(env, jidx);
-  jsize total_pieces = 0;
+/* srcs[i] for each shard i; out_arr (may be NULL) is pinned last, its address in *out_ptr. */
+static int pin_pieces(JNIEnv* env, jobjectArray jidx, jlongArray jsizes, jobjectArray joffs,
+                      jobjectArray jlens, jobjectArray jdata, jobject out_arr, zh_shard_src* srcs,
+                      Pinned* P, void** out_ptr) {
+  memset(P, 0, sizeof(*P));
+  jsize n = (*env)->GetArrayLength(env, jidx), total = 0;
   for (jsize i = 0; i < n; i++) {
     jobjectArray ps = (jobjectArray)(*env)->GetObjectArrayElement(env, jdata, i);
-    if (ps) total_pieces += (*env)->GetArrayLength(env, ps);
+    if (ps) total += (*env)->GetArrayLength(env, ps);
     if (ps) (*env)->DeleteLocalRef(env, ps);
   }
-  zh_shard_piece* pc = (zh_shard_piece*)calloc((size_t)(total_pieces > 0 ? total_pieces : 1),
-                                               sizeof(zh_shard_piece));
-  if (!pc) return ZH_ENOMEM;
-  *pieces_out = pc;
-  jlong pos = 0;
-  jsize used = 0;
+  /* one local reference per held array (+ the per-shard arrays, released as we go) */
+  if ((*env)->EnsureLocalCapacity(env, n + total + 16) != 0) return ZH_ENOMEM;
+  P->arr = (jarray*)calloc((size_t)(n + total + 1), sizeof(jarray));
+  P->ptr = (void**)calloc((size_t)(n + total + 1), sizeof(void*));
+  P->pieces = (zh_shard_piece*)calloc((size_t)(total > 0 ? total : 1), sizeof(zh_shard_piece));
+  if (!P->arr || !P->ptr || !P->pieces) return ZH_ENOMEM;
+  jsize na = 0, used = 0;
+  /* per shard: the index array, then its pieces (references and lengths only) */
+  jsize* idx_slot = (jsize*)malloc((size_t)(n > 0 ? n : 1) * sizeof(jsize));
+  jsize* piece_first = (jsize*)malloc((size_t)(n > 0 ? n : 1) * sizeof(jsize));
+  if (!idx_slot || !piece_first) {
+    free(idx_slot);
+    free(piece_first);
+    return ZH_ENOMEM;
+  }
   for (jsize i = 0; i < n; i++) {
     memset(&srcs[i], 0, sizeof(srcs[i]));
     jlong size = -1;
     (*env)->GetLongArrayRegion(env, jsizes, i, 1, &size);
     srcs[i].shard_nbytes = size;
+    idx_slot[i] = -1;
     jbyteArray ib = (jbyteArray)(*env)->GetObjectArrayElement(env, jidx, i);
     if (ib) {
-      jsize len = (*env)->GetArrayLength(env, ib);
-      (*env)->GetByteArrayRegion(env, ib, 0, len, (jbyte*)(staging + pos));
-      srcs[i].index = staging + pos;
-      srcs[i].index_nbytes = len;
-      pos += len;
-      (*env)->DeleteLocalRef(env, ib);
+      srcs[i].index_nbytes = (*env)->GetArrayLength(env, ib);
+      idx_slot[i] = na;
+      P->arr[na++] = ib;
     }
     jobjectArray ps = (jobjectArray)(*env)->GetObjectArrayElement(env, jdata, i);
     jlongArray po = (jlongArray)(*env)->GetObjectArrayElement(env, joffs, i);
     jlongArray pl = (jlongArray)(*env)->GetObjectArrayElement(env, jlens, i);
     jsize np = ps ? (*env)->GetArrayLength(env, ps) : 0;
-    srcs[i].pieces = pc + used;
+    piece_first[i] = na;
+    srcs[i].pieces = P->pieces + used;
     srcs[i].npieces = np;
     for (jsize k = 0; k < np; k++) {
       jbyteArray b = (jbyteArray)(*env)->GetObjectArrayElement(env, ps, k);
       jlong off = 0, nb = 0;
       (*env)->GetLongArrayRegion(env, po, k, 1, &off);
       (*env)->GetLongArrayRegion(env, pl, k, 1, &nb);
-      jsize len = b ? (*env)->GetArrayLength(env, b) : 0;
-      if (b) (*env)->GetByteArrayRegion(env, b, 0, len, (jbyte*)(staging + pos));
-      pc[used + k].offset = off;
-      pc[used + k].nbytes = nb;
-      pc[used + k].data = staging + pos;
-      pc[used + k].data_nbytes = len;
-      pos += len;
-      if (b) (*env)->DeleteLocalRef(env, b);
+      P->pieces[used + k].offset = off;
+      P->pieces[used + k].nbytes = nb;
+      P->pieces[used + k].data_nbytes = b ? (*env)->GetArrayLength(env, b) : 0;
+      P->arr[na++] = b; /* may be NULL: an empty piece */
     }
     used += np;
     if (ps) (*env)->DeleteLocalRef(env, ps);
     if (po) (*env)->DeleteLocalRef(env, po);
     if (pl) (*env)->DeleteLocalRef(env, pl);
   }
-  return ZH_OK;
-}
-
-/* The decoded region from the staging into the primitive array behind the ucar.ma2.Array. */
-static int copy_out(JNIEnv* env, jobject out, const void* src, size_t obytes, char* err,
-                    size_t errlen) {
-  void* dst = (*env)->GetPrimitiveArrayCritical(env, (jarray)out, NULL);
-  if (!dst) {
-    snprintf(err, errlen, "could not access the output array");
-    return ZH_ENOMEM;
+  if (out_arr) P->arr[na++] = (jarray)out_arr;
+  P->n = na;
+  /* enter every critical section; from here on no JNI call until pin_release */
+  int st = ZH_OK;
+  for (jsize k = 0; k < na && st == ZH_OK; k++) {
+    if (!P->arr[k]) continue;
+    P->ptr[k] = (*env)->GetPrimitiveArrayCritical(env, P->arr[k], NULL);
+    if (!P->ptr[k]) st = ZH_ENOMEM;
   }
-  memcpy(dst, src, obytes);
-  (*env)->ReleasePrimitiveArrayCritical(env, (jarray)out, dst, 0);
-  return ZH_OK;
+  if (st == ZH_OK) {
+    used = 0;
+    for (jsize i = 0; i < n; i++) {
+      if (idx_slot[i] >= 0) srcs[i].index = P->ptr[idx_slot[i]];
+      for (jsize k = 0; k < srcs[i].npieces; k++)
+        P->pieces[used + k].data = P->ptr[piece_first[i] + k];
+      used += (jsize)srcs[i].npieces;
+    }
+    if (out_arr && out_ptr) *out_ptr = P->ptr[na - 1];
+  }
+  free(idx_slot);
+  free(piece_first);
+  return st;
 }
 
 JNIEXPORT jint JNICALL Java_dev_zarr_zarrjava_hip_ZarrHip_arrayReadPieces(
@@ -416,24 +435,19 @@ JNIEXPORT jint JNICALL Java_dev_zarr_zarrjava_hip_ZarrHip_arrayReadPieces(
   }
   if ((int64_t)(*env)->GetArrayLength(env, (jarray)out) != nel)
     return throw_status(env, ZH_EINVAL, "output array size does not match the region");
-  const size_t obytes = (size_t)nel * (size_t)m.dtype_size;
-  const jlong in_bytes = pieces_bytes(env, jidx, jdata);
-  const size_t in_cap = ((size_t)in_bytes + 255) & ~(size_t)255;
-  void* staging = NULL;
-  st = zh_host_staging(ctxs[0], in_cap + obytes, &staging);
-  if (st != ZH_OK) return throw_status(env, st, "page-locked staging: allocation failed");
   jsize n = (*env)->GetArrayLength(env, jidx);
   zh_shard_src* srcs = (zh_shard_src*)calloc((size_t)(n > 0 ? n : 1), sizeof(zh_shard_src));
-  zh_shard_piece* pcs = NULL;
-  st = srcs ? marshal_pieces(env, jidx, jsizes, joffs, jlens, jdata, (uint8_t*)staging, srcs, &pcs)
-            : ZH_ENOMEM;
-  uint8_t* dst = (uint8_t*)staging + in_cap;
+  if (!srcs) return throw_status(env, ZH_ENOMEM, "out of host memory");
+  Pinned P;
+  void* dst = NULL;
+  st = pin_pieces(env, jidx, jsizes, joffs, jlens, jdata, out, srcs, &P, &dst);
   if (st == ZH_OK)
     st = k == 1 ? zh_array_read_pieces(ctxs[0], &m, srcs, n, o64, r64, dst, 0, NULL, err, sizeof err)
                 : zh_array_read_pieces_multi(ctxs, (int)k, 0, &m, srcs, n, o64, r64, dst, 0, NULL,
                                              err, sizeof err);
-  if (st == ZH_OK) st = copy_out(env, out, dst, obytes, err, sizeof err);
-  free(pcs);
+  else
+    snprintf(err, sizeof err, "could not access the source or output arrays");
+  pin_release(env, &P, 1);
   free(srcs);
   if (st == ZH_EUNSUPPORTED) return st;
   if (st != ZH_OK) return throw_status(env, st, err);
@@ -461,7 +475,6 @@ JNIEXPORT jint JNICALL Java_dev_zarr_zarrjava_hip_ZarrHip_shardDecodePieces(
   }
   if ((int64_t)(*env)->GetArrayLength(env, (jarray)out) != nel)
     return throw_status(env, ZH_EINVAL, "output array size does not match the part shape");
-  const size_t obytes = (size_t)nel * (size_t)m.dtype_size;
   /* one shard: wrap its arrays as the one-element arrays of the read form */
   jclass bcls = (*env)->FindClass(env, "[B"), lcls = (*env)->FindClass(env, "[J"),
          bbcls = (*env)->FindClass(env, "[[B");
@@ -472,21 +485,17 @@ JNIEXPORT jint JNICALL Java_dev_zarr_zarrjava_hip_ZarrHip_shardDecodePieces(
   jlongArray js = (*env)->NewLongArray(env, 1);
   if (!jidx || !jo || !jl || !jd || !js) return throw_status(env, ZH_ENOMEM, "out of memory");
   (*env)->SetLongArrayRegion(env, js, 0, 1, &size);
-  const jlong in_bytes = pieces_bytes(env, jidx, jd);
-  const size_t in_cap = ((size_t)in_bytes + 255) & ~(size_t)255;
-  void* staging = NULL;
   zh_ctx* c = (zh_ctx*)(intptr_t)ctx;
-  st = zh_host_staging(c, in_cap + obytes, &staging);
-  if (st != ZH_OK) return throw_status(env, st, "page-locked staging: allocation failed");
   zh_shard_src src;
-  zh_shard_piece* pcs = NULL;
-  st = marshal_pieces(env, jidx, js, jo, jl, jd, (uint8_t*)staging, &src, &pcs);
-  uint8_t* dst = (uint8_t*)staging + in_cap;
+  Pinned P;
+  void* dst = NULL;
+  st = pin_pieces(env, jidx, js, jo, jl, jd, out, &src, &P, &dst);
   if (st == ZH_OK)
     st = zh_sharding_decode_pieces(c, &m, &src, o64, (const int32_t*)part, dst, 0, NULL, err,
                                    sizeof err);
-  if (st == ZH_OK) st = copy_out(env, out, dst, obytes, err, sizeof err);
-  free(pcs);
+  else
+    snprintf(err, sizeof err, "could not access the source or output arrays");
+  pin_release(env, &P, 1);
   if (st == ZH_EUNSUPPORTED) return st;
   if (st != ZH_OK) return throw_status(env, st, err);
   return 0;
