@@ -183,7 +183,8 @@ void zh_plan_destroy(zh_plan* plan);
 int zh_plan_stats(const zh_plan* plan, int64_t* in_bytes, int64_t* out_bytes,
                   int64_t* items, int64_t* nshards);
 /* Diagnostic: the fast-path selection of the last decode scatter launch in this process
- * (encode = 0: fast_mode * 1000000 + kernel variant * 1000 + row group * 4 + (pieces ? 1 : 0))
+ * (encode = 0: aligned windows * 10^9 + fast_mode * 1000000 + kernel variant * 1000 +
+ *  row group * 4 + (pieces ? 1 : 0))
  * or of the last write's encode view (encode = 1: fast_mode * 1000000 + chunk group * 1000 +
  * kernel form), or -1.  Tests use it to check that a switch reached the kernel it names. */
 int64_t zh_debug_last_fast_path(int encode);

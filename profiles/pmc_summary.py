@@ -23,8 +23,9 @@ def kernel_rows(path, match):
 
 
 FAST = ("decode_rows_kernel", "decode_tiles_kernel", "tiles_group_kernel", "rows_group_kernel",
-        "rows_xpose_kernel", "tiles_rowcrc_kernel", "tiles_crcw_kernel")
-DECODE_ONLY = ("tiles_rowcrc_kernel", "tiles_crcw_kernel")  # last template argument is not FLAGS
+        "rows_xpose_kernel", "tiles_rowcrc_kernel", "tiles_crcw_kernel",
+        "tiles_rowcrc_aln_kernel")
+DECODE_ONLY = ("tiles_rowcrc_kernel", "tiles_crcw_kernel", "tiles_rowcrc_aln_kernel")  # last template argument is not FLAGS
 
 
 def main(src, config, out):

@@ -226,3 +226,64 @@ def test_row_crc_tile_kernel_unit_layouts(dev, monkeypatch, units, order):
 def _read_both_shape(dev, meta, shards, shape):
     want = np.frombuffer(O.array_read(meta, shards, [0, 0, 0], shape), np.uint32).reshape(shape)
     return device_read(dev, meta, shards, [0, 0, 0], shape), want
+
+
+def _aligned():
+    """Whether the last decode scatter launch took the aligned-window row-CRC kernel."""
+    return lib().zh_debug_last_fast_path(0) // 10**9
+
+
+@pytest.mark.parametrize("nb", [16, 24, 32])
+@pytest.mark.parametrize("endian", [A.ZH_ENDIAN_BIG, A.ZH_ENDIAN_LITTLE])
+def test_row_crc_aligned_windows(dev, monkeypatch, nb, endian):
+    """tiles_rowcrc_aln_kernel: inner chunks [32, nb, 32] under transpose [2, 1, 0] store
+    [32 rows][nb units][32 words] (c4's layout), so the movers load 128-B aligned lines and
+    carry each step's last line into the next step's tile through a ring of 9 LDS slots.  One
+    shard of 36 inner chunks puts the payloads at every offset 4i mod 128 (the head lines, the
+    carried line ends and the row tails of every δ, and δ = 0; 2, 3 and 4 steps per chunk).  Equals the oracle over the
+    whole array and a ragged region, with an elided chunk; ZH_DEC_ALIGN=0 gives the same bytes
+    through the unaligned loads; flipped bytes in a row tail (read at the last step from the
+    box), in a carried line end and in a head line are reported with the oracle's message."""
+    for k in ("ZH_DEC_CRCW", "ZH_DEC_TGROUP", "ZH_DEC_TPF"):
+        monkeypatch.delenv(k, raising=False)
+    monkeypatch.setenv("ZH_SMALL_SPLIT", "0")
+    monkeypatch.setenv("ZH_DEC_ALIGN", "1")
+    shape = [64, 6 * nb, 96]
+    meta = A.make_meta(shape, shape, 4, endian=endian, sharded=True,
+                       inner_chunk_shape=[32, nb, 32], transpose_order=[2, 1, 0],
+                       inner_crc32c=True)
+    arr = rand_array(shape, 4, seed=67 + nb)
+    arr[arr == 0] = 1
+    arr[32:64, 0:nb, 0:32] = 0  # one elided inner chunk (shifts the later payloads by a chunk)
+    shards = encode_oracle(meta, arr)
+    got, want = _read_both_shape(dev, meta, shards, shape)
+    np.testing.assert_array_equal(got, want)
+    np.testing.assert_array_equal(got, arr)
+    assert _variant() == 51 and _aligned() == 1
+    off, shp = [3, 5, 7], [58, 6 * nb - 9, 80]
+    sel = np.frombuffer(O.array_read(meta, shards, off, shp), np.uint32).reshape(shp)
+    np.testing.assert_array_equal(device_read(dev, meta, shards, off, shp), sel)
+    monkeypatch.setenv("ZH_DEC_ALIGN", "0")
+    np.testing.assert_array_equal(device_read(dev, meta, shards, [0, 0, 0], shape), arr)
+    assert _variant() == 51 and _aligned() == 0
+    monkeypatch.setenv("ZH_DEC_ALIGN", "1")
+    chunk = 32 * nb * 32 * 4 + 4
+    row = nb * 128  # bytes of one payload row (all units)
+    for i in (5, 31):  # δ = 20 and 124
+        p = i * chunk
+        for pos in (p + 11 * row - 3,            # row 10's tail (the box, last step)
+                    p + 4 * row + 1024 + 2,      # row 4, step 1: a carried line end
+                    p + 7 * row + 1):            # row 7's head line
+            _corrupt_matches_oracle_shape(dev, meta, shards, 0, pos, shape)
+
+
+def _corrupt_matches_oracle_shape(dev, meta, shards, k, pos, shape):
+    bad = bytearray(shards[k])
+    bad[pos] ^= 0x08
+    srcs = list(shards)
+    srcs[k] = bytes(bad)
+    with pytest.raises(O.OracleError) as eo:
+        O.array_read(meta, srcs, [0] * len(shape), shape)
+    with pytest.raises(ZhError) as ed:
+        device_read(dev, meta, srcs, [0] * len(shape), shape)
+    assert str(ed.value) == str(eo.value)

@@ -31,8 +31,14 @@ namespace zh {
 
 
 
+// the last message of a call made without an error buffer (zh_plan_execute), per thread
+thread_local char g_quiet_err[256];
+
 void set_err(char* err, size_t errlen, const char* fmt, ...) {
-  if (!err || errlen == 0) return;
+  if (!err || errlen == 0) {
+    err = g_quiet_err;
+    errlen = sizeof g_quiet_err;
+  }
   va_list ap;
   va_start(ap, fmt);
   vsnprintf(err, errlen, fmt, ap);
@@ -1082,6 +1088,8 @@ int plan_create(zh_ctx* ctx, const zh_array_meta* m, const SrcDesc* srcs, int64_
       ((int64_t)p->args.fast_n * 8 + 15) / 16 * 16 + 8 * 1057 * 4 + 16 * 256 * 4 +
               (int64_t)p->args.fast_n * 4 <= 65536;
   p->args.crc_tile_step = 0;
+  p->args.tile_align = 0;
+  p->args.tile_ystride = 0;
   std::vector<int64_t> ends;  // per-unit payload ends (tile CRC; the grouped step below)
   if (tile_crc) {
     const ScatterArgs& g = p->args;
@@ -1228,6 +1236,26 @@ int plan_create(zh_ctx* ctx, const zh_array_meta* m, const SrcDesc* srcs, int64_
       // payload row for the CRC (tiles_rowcrc_kernel)
       if (crc && G <= 4 && crcw >= 1 && crcw <= 3 && rowcrc_ok)
         p->args.tile_variant = 30 + G + 10 * (crcw - 1);
+      // Aligned windows for the row-CRC kernel (G = 1): every payload after a 4-byte crc32c
+      // starts at 4·i mod 128, so a 1 KiB wave load of it touched 9 lines and the shared line
+      // was fetched twice.  When unit u's rows start at 32u elements and row r + 1 follows row
+      // r (the payload is [32 rows][units][32 words], c4's layout), the movers load 128-B
+      // aligned lines and route each word to its tile in LDS (ZH_DEC_ALIGN=1: on; off by default
+      // until it is faster than the unaligned loads).
+      if (p->args.tile_variant == 51 && env_int("ZH_DEC_ALIGN", 0) != 0) {
+        const ScatterArgs& g = p->args;
+        const int64_t nu = g.fast_n;
+        // [32 rows][nu units][32 words], 2-4 steps of 8 units (K fits the box area), unit u's
+        // region offset u·ys, the stores' lane offsets 4·(u·ys) + 128 within 32 bits
+        bool al = nu >= 16 && nu <= 32 && nu % 8 == 0 && g.pstride[g.fd] == 32 * nu &&
+                  g.inner_nbytes == 4096 * nu && (int64_t)tab.size() >= 2 * nu;
+        const uint64_t ys = al ? tab[3] : 0;
+        for (int64_t u = 0; al && u < nu; u++)
+          al = tab[2 * (size_t)u] == (uint32_t)(32 * u) &&
+               tab[2 * (size_t)u + 1] == (uint64_t)u * ys && 4 * (uint64_t)u * ys + 128 <= 0xFFFFFFFFull;
+        p->args.tile_align = al ? 1 : 0;
+        p->args.tile_ystride = al ? (int64_t)ys : 0;
+      }
       if (crc) p->args.crc_tile_step = tile_crc_step(ends, (size_t)(8 / G));
       p->args.item_mul = env_int("ZH_ITEM_PERM", 1) ? golden_item_mul(groups) : 0;
       p->grid = grid_for(ctx, groups);
@@ -1493,9 +1521,10 @@ int read_one_plan(zh_ctx* ctx, const zh_array_meta* meta, const SrcDesc* srcs, i
   zh_plan* p = nullptr;
   int st = plan_create(ctx, meta, srcs, nsrc, offset, shape, flags, false, &p, err, errlen);
   if (st != ZH_OK) return st;
+  g_quiet_err[0] = 0;
   st = zh_plan_execute(p, out, stream);
   if (st != ZH_OK) {
-    set_err(err, errlen, "kernel launch failed");
+    set_err(err, errlen, "kernel launch failed%s%s", g_quiet_err[0] ? ": " : "", g_quiet_err);
     plan_free(p);
     return st;
   }
@@ -2173,6 +2202,8 @@ static int array_write_fast(zh_ctx* ctx, const zh_array_meta* m, ScatterArgs a,
       ((int64_t)v.fast_n * 8 + 15) / 16 * 16 + 8 * 1057 * 4 + 16 * 256 * 4 +
               (int64_t)v.fast_n * 4 <= 65536;
   v.crc_tile_step = 0;
+  v.tile_align = 0;
+  v.tile_ystride = 0;
   std::vector<int64_t> tile_ends;  // per-unit payload ends (tile CRC; the grouped step below)
   if (tile_crc) {
     const int64_t L = a.inner_nbytes, d_fs = v.rstride[v.fs];

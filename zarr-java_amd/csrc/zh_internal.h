@@ -159,6 +159,10 @@ struct ScatterArgs {
   uint32_t crc_tile_step;       // tile CRC: x^(8Δ) when unit u + kTG ends Δ bytes after unit u
                                 // for every u (a lane then folds its groups with one table
                                 // shift instead of a multiply per group); 0 = irregular
+  int32_t tile_align;           // row-CRC tile decode: units are consecutive 128-B payload rows
+                                // and the tile rows follow each other (host-checked), so the
+                                // movers load 128-B aligned lines (tiles_rowcrc_aln_kernel)
+  int64_t tile_ystride;         // tile_align: unit u's region offset is u · tile_ystride
 };
 
 // Chunk-payload CRC-32C pass (inner crc32c codec): one workgroup per (item, 64 KiB span) of

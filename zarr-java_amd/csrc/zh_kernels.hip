@@ -135,6 +135,20 @@ __device__ __forceinline__ uint4 ld16s(const uint8_t* p) {
     return ld16(p);
   }
 }
+// non-temporal 16-B global load at a wave-uniform base + a 32-bit lane offset (global_load with
+// a scalar base: no 64-bit address per load in VGPRs)
+__device__ __forceinline__ uint4 ld16g(const uint8_t* base, uint32_t off) {
+  const v4u v = __builtin_nontemporal_load(
+      reinterpret_cast<const __attribute__((address_space(1))) v4u*>(
+          (const __attribute__((address_space(1))) uint8_t*)base + off));
+  return make_uint4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ void st16g(uint8_t* base, uint32_t off, uint4 v) {
+  __builtin_nontemporal_store(
+      v4u{v.x, v.y, v.z, v.w},
+      reinterpret_cast<__attribute__((address_space(1))) v4u*>(
+          (__attribute__((address_space(1))) uint8_t*)base + off));
+}
 template <bool NT>
 __device__ __forceinline__ void st16s(uint8_t* p, uint4 v) {
   if constexpr (NT) {
@@ -2133,6 +2147,168 @@ void tiles_rowcrc_kernel(ScatterArgs a) {
   }
 }
 
+// decode, the row-CRC tile kernel over 128-B aligned lines (ZH_DEC_ALIGN; host: a.tile_align,
+// one chunk per work item, 16 ≤ fast_n ≤ 32 units, fast_n % 8 == 0, tab[u] = (32u, u·ystride)).
+// The payload is then [32 rows][fast_n units][32 words]: step s of row r is the contiguous 1 KiB
+// L(r, s) at 4096r·(fast_n/32) + 1024s.  A payload after a 4-byte crc32c starts δ = 4i mod 128
+// bytes into a line, so a 1 KiB wave load of L(r, s) touched 9 lines, the first and last shared
+// with other loads (the row-CRC kernel read ≈1.11× the payload bytes, PMC).  Here the movers
+// load the aligned lines 1..8 of L(r, s) (lane λ: 16 B at 128 + 16λ from its first line) and
+// write word j of lane λ, element e = 32 − δ/4 + 4λ + j of L(r, s), to tile e / 32, column
+// e mod 32.  Elements e ≥ 256 (the start of L(r, s + 1), lanes 56-63) go to step s + 1's tile 0:
+// the tiles live in a ring of 9 LDS slots (step s's tile t' in slot (8s + t') mod 9, so its
+// "tile 8" IS the next step's tile 0, and that slot held the previous step's tile 7, already
+// read).  Line 0 of L(r, 0) is the end of row r − 1: the head loads before step 0 (lane (t, g):
+// 16 B of row 8w + t's first line) put its first δ bytes in the box (row r − 1's tail, taken by
+// lanes 56-63 at the last step, which load no line 8 for rows < 31) and the rest in tile 0.
+// Per chunk 1025 line fetches, the minimum for a misaligned 128 KiB (1 shared with the previous
+// chunk).  CRC as tiles_rowcrc_kernel (lane i: payload row i & 31 of tile i >> 5 from LDS).
+// LDS (bytes): T[8][256] at 0 (byte-swapped entries with SWAP), the box (31 rows × 32 words)
+// and K (≤ 32 words) in the S area at 8192, SD[4][256] at 12288, the 9 slots at 16384: 54 436 B,
+// 3 workgroups per CU.  Every lane reads the same descriptor (G = 1): the skip is block-uniform.
+template <bool SWAP>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3)))
+void tiles_rowcrc_aln_kernel(ScatterArgs a) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  uint32_t(*T)[256] = reinterpret_cast<uint32_t(*)[256]>(smem);
+  uint32_t* const box = T[8];
+  uint32_t* const K = T[8] + 992;
+  uint32_t(*SD)[256] = T + 12;
+  uint32_t* const lds = reinterpret_cast<uint32_t*>(smem + 16384);
+  const int tid = threadIdx.x;
+#pragma unroll
+  for (int k = 0; k < 8; k++) T[k][tid] = SWAP ? __builtin_bswap32(g_crc.T[k][tid]) : g_crc.T[k][tid];
+#pragma unroll
+  for (int b = 0; b < 4; b++)
+    SD[b][tid] = a.crc_tile_step ? multmodp(a.crc_tile_step, (uint32_t)tid << (8 * b)) : 0u;
+  for (int i = tid; i < a.fast_n; i += kBlock) K[i] = a.fast_tab[2 * a.fast_n + i];
+  __syncthreads();
+  const int wave = tid >> 6, lane = tid & 63, t = lane >> 3, g = lane & 7;
+  const int wv = __builtin_amdgcn_readfirstlane(wave);
+  const int tc = tid >> 5, r = tid & 31;  // CRC role
+  const int64_t s_fd = a.pstride[a.fd], d_fs = a.rstride[a.fs];
+  const bool regular = a.crc_tile_step != 0;
+  const uint32_t units = (uint32_t)a.fast_n, ys = (uint32_t)a.tile_ystride;
+  const uint32_t kr = x2nmodp((uint64_t)(31 - r) * 4 * (uint64_t)s_fd, 3);
+  auto sw = [](uint32_t v) { return SWAP ? __builtin_bswap32(v) : v; };
+  auto rfl = [](uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); };
+  for (int64_t gi = blockIdx.x; gi < a.n_citems; gi += gridDim.x) {
+    const int64_t c = a.item_mul ? (int64_t)(((uint64_t)gi * a.item_mul) % (uint64_t)a.n_citems) : gi;
+    const uint4* dp = reinterpret_cast<const uint4*>(a.desc + c);
+    const uint4 dx = dp[0], dy = dp[1];
+    if ((rfl(dy.z) & kDescFast) == 0) continue;  // block-uniform
+    const uint8_t* src = (const uint8_t*)(uintptr_t)(((uint64_t)rfl(dx.y) << 32) | rfl(dx.x));
+    uint8_t* dst = a.region + (int64_t)(((uint64_t)rfl(dx.w) << 32) | rfl(dx.z)) * 4;
+    const uint32_t dl = (uint32_t)(uintptr_t)src & 127u;
+    const int Dp = dl ? (int)(dl >> 2) : 32;  // δ/4; 32: aligned (no head, carry or tail)
+    const uint8_t* wsrc = dl ? src - dl + 128 : src;
+    uint4 x[8];
+    auto load = [&](uint32_t ub, bool last) {
+      const uint8_t* base = wsrc + (size_t)ub * 128;
+      // last step: lines 8 of rows < 31 are the next rows' head lines, already loaded
+      const bool skip = dl && last && t == 7;
+#pragma unroll
+      for (int k = 0; k < 8; k++)
+        if (!(skip && wv * 8 + k < 31))
+          x[k] = ld16g(base + (size_t)(wv * 8 + k) * s_fd * 4, (uint32_t)(16 * lane));
+    };
+    if (dl) {  // head lines: row hr − 1's tail | row hr's tile-0 head (slot 0)
+      const uint4 h = ld16g(src - dl + (size_t)wv * 8 * s_fd * 4, (uint32_t)(t * s_fd * 4 + 16 * g));
+      load(0, false);
+      const int hr = wv * 8 + t;
+      const uint32_t hv[4] = {h.x, h.y, h.z, h.w};
+#pragma unroll
+      for (int j = 0; j < 4; j++) {
+        const int d = 4 * g + j;
+        if (d < Dp) {
+          if (hr > 0) box[(hr - 1) * 32 + d] = sw(hv[j]);
+        } else {
+          lds[hr * 33 + d - Dp] = sw(hv[j]);
+        }
+      }
+    } else {
+      load(0, false);
+    }
+    uint32_t share = 0, run = 0, ulast = ~0u;
+    int sb = 0;  // slot of this step's tile 0: (8s) mod 9
+#pragma unroll 1
+    for (uint32_t ub = 0; ub < units; ub += kTG) {
+      const bool last = ub + kTG >= units;
+      {
+        int e0 = 32 - Dp + 4 * lane;  // element of L(r, s) held by word 0
+        asm volatile("" : "+v"(e0));  // the word addresses stay per-step registers
+        int wa[4];
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+          const int e = e0 + j;
+          int sl = sb + (e >> 5);
+          sl -= sl >= 9 ? 9 : 0;
+          wa[j] = sl * kTilePitch + (e & 31);
+        }
+        const bool tl = dl && last && t == 7;  // the row tails come from the box
+#pragma unroll
+        for (int k = 0; k < 8; k++) {
+          const int rr = wv * 8 + k;
+          uint32_t v[4] = {sw(x[k].x), sw(x[k].y), sw(x[k].z), sw(x[k].w)};
+          if (tl && rr < 31) {
+            const uint4 bv = *reinterpret_cast<const uint4*>(box + rr * 32 + 4 * g);
+            const uint32_t b4[4] = {bv.x, bv.y, bv.z, bv.w};
+#pragma unroll
+            for (int j = 0; j < 4; j++)
+              if (4 * g + j < Dp) v[j] = b4[j];
+          }
+#pragma unroll
+          for (int j = 0; j < 4; j++) lds[wa[j] + rr * 33] = v[j];
+        }
+      }
+      __syncthreads();
+      if (!last) load(ub + kTG, ub + 2 * kTG >= units);
+      {  // movers: tile t (slot (sb + t) mod 9) to the region, scalar chunk base + row
+        int st = sb + t;
+        st -= st >= 9 ? 9 : 0;
+        const uint32_t* mine = lds + st * kTilePitch;
+        const uint32_t voff = ((ub + t) * ys + 4 * g) * 4;
+#pragma unroll
+        for (int k = 0; k < 8; k++) {
+          const int rr = wave * 8 + k;
+          uint4 y;
+          y.x = mine[(g * 4 + 0) * 33 + rr];
+          y.y = mine[(g * 4 + 1) * 33 + rr];
+          y.z = mine[(g * 4 + 2) * 33 + rr];
+          y.w = mine[(g * 4 + 3) * 33 + rr];
+          st16g(dst + (size_t)(wv * 8 + k) * d_fs * 4, voff, y);
+        }
+      }
+      uint32_t w[32];
+      {
+        int sc = sb + tc;
+        sc -= sc >= 9 ? 9 : 0;
+        const uint32_t* crow = lds + sc * kTilePitch + r * 33;
+#pragma unroll
+        for (int j = 0; j < 32; j++) w[j] = crow[j];
+      }
+      __syncthreads();
+      uint32_t acc = 0;  // byte-swapped with SWAP
+#pragma unroll
+      for (int j = 0; j < 32; j += 2) acc = crc_upd8_lds<SWAP>(acc, w[j], w[j + 1]);
+      if (SWAP) acc = __builtin_bswap32(acc);
+      const uint32_t uc = ub + tc;
+      if (regular) {
+        run = (ulast == ~0u ? 0u : crc_shift_tab(run, SD)) ^ acc;
+        ulast = uc;
+      } else {
+        share ^= multmodp(K[uc], acc);
+      }
+      sb = sb == 0 ? 8 : sb - 1;
+    }
+    if (regular && ulast != ~0u) share = multmodp(K[ulast], run);
+    uint32_t cr = multmodp(kr, share);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) cr ^= (uint32_t)__shfl_xor((int)cr, o, 64);
+    if (lane == 0) atomicXor(a.crc_partials + c, cr);
+  }
+}
+
 // The CRC-fused decode variant held to 3 waves per SIMD (LDS allows 3 blocks of 4 waves per
 // CU; unconstrained it takes 172 VGPRs and runs 2)
 template <int NT, bool FLAGS>
@@ -2947,7 +3123,14 @@ static void launch_scatter_ds(const ScatterArgs& a, int tile, int enc, int grid,
             case 11: hipLaunchKernelGGL((tiles_crcw_kernel<1, false>), dim3(grid), dim3(2 * kBlock), lc, s, a); return;
             case 12: hipLaunchKernelGGL((tiles_crcw_kernel<2, false>), dim3(grid), dim3(2 * kBlock), lc, s, a); return;
             case 14: hipLaunchKernelGGL((tiles_crcw_kernel<4, false>), dim3(grid), dim3(2 * kBlock), lc, s, a); return;
-            case 21: if (a.swap) hipLaunchKernelGGL((tiles_rowcrc_kernel<1, true>), dim3(grid), dim3(kBlock), lc + 64, s, a); else hipLaunchKernelGGL((tiles_rowcrc_kernel<1, false>), dim3(grid), dim3(kBlock), lc + 64, s, a); return;
+            case 21:
+              if (a.tile_align) {  // LDS: tables 16 KiB + 9 slots (the host checked the rest)
+                const size_t la = 16384 + (size_t)9 * kTilePitch * 4;
+                if (a.swap) hipLaunchKernelGGL((tiles_rowcrc_aln_kernel<true>), dim3(grid), dim3(kBlock), la, s, a);
+                else hipLaunchKernelGGL((tiles_rowcrc_aln_kernel<false>), dim3(grid), dim3(kBlock), la, s, a);
+                return;
+              }
+              if (a.swap) hipLaunchKernelGGL((tiles_rowcrc_kernel<1, true>), dim3(grid), dim3(kBlock), lc + 64 + a.lds_pad, s, a); else hipLaunchKernelGGL((tiles_rowcrc_kernel<1, false>), dim3(grid), dim3(kBlock), lc + 64 + a.lds_pad, s, a); return;
             case 22: if (a.swap) hipLaunchKernelGGL((tiles_rowcrc_kernel<2, true>), dim3(grid), dim3(kBlock), lc + 64, s, a); else hipLaunchKernelGGL((tiles_rowcrc_kernel<2, false>), dim3(grid), dim3(kBlock), lc + 64, s, a); return;
             case 24: if (a.swap) hipLaunchKernelGGL((tiles_rowcrc_kernel<4, true>), dim3(grid), dim3(kBlock), lc + 64, s, a); else hipLaunchKernelGGL((tiles_rowcrc_kernel<4, false>), dim3(grid), dim3(kBlock), lc + 64, s, a); return;
             default: return;
@@ -3051,7 +3234,9 @@ bool rowcrc_lds_at_zero() {
                          (const void*)tiles_rowcrc_kernel<4, false>, (const void*)tiles_rowcrc_kernel<4, true>,
                          (const void*)tiles_rowcrc_kernel<1, false, true>, (const void*)tiles_rowcrc_kernel<1, true, true>,
                          (const void*)tiles_rowcrc_kernel<2, false, true>, (const void*)tiles_rowcrc_kernel<2, true, true>,
-                         (const void*)tiles_rowcrc_kernel<4, false, true>, (const void*)tiles_rowcrc_kernel<4, true, true>};
+                         (const void*)tiles_rowcrc_kernel<4, false, true>, (const void*)tiles_rowcrc_kernel<4, true, true>,
+                         (const void*)tiles_rowcrc_aln_kernel<false>,
+                         (const void*)tiles_rowcrc_aln_kernel<true>};
     for (const void* f : fns) {
       hipFuncAttributes at;
       if (hipFuncGetAttributes(&at, f) != hipSuccess || at.sharedSizeBytes != 0) return false;
@@ -3070,7 +3255,8 @@ hipError_t launch_scatter(const ScatterArgs& a, int dsize, int tile_mode, int en
                           hipStream_t stream) {
   if (a.total_items == 0) return hipSuccess;
   if (!encode)
-    g_last_fast_path.store((int64_t)a.fast_mode * 1000000 + (int64_t)a.tile_variant * 1000 +
+    g_last_fast_path.store((int64_t)a.tile_align * 1000000000 + (int64_t)a.fast_mode * 1000000 +
+                           (int64_t)a.tile_variant * 1000 +
                            (int64_t)(a.row_group & 0xFF) * 4 + (a.piece_shift ? 1 : 0));
   switch (dsize) {
     case 1: launch_scatter_ds<1>(a, tile_mode, encode, grid, stream); break;
