@@ -18,7 +18,7 @@ step() {  # name, timeout, cmd...
 cd "$R" || exit 1
 step tests 600 python -u -m pytest tests/test_gpu_crc_tiles.py -x -q --timeout 120 --timeout-method thread
 cd /tmp || exit 1
-step ab 600 python3 $R/profiles/ab_decode_env.py c4crc 1 6 ZH_DEC_ALIGN=1 -
+step ab 600 python3 $R/profiles/ab_decode_env.py c4crc 1 6 - ZH_DEC_ALIGN=0
 export ZH_DEC_ALIGN=1  # the profiles below: the aligned kernel
 B="python3 $R/bench.py --no-cpu-baseline --no-extras --no-host-inclusive"
 step trace 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o run -- $B --config c4crc --steps 5 --warmup 2

@@ -8,5 +8,5 @@ OUT=$R/gpurun_out/r03occ
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 cd /tmp || exit 1
-timeout -k 10 600 python3 $R/profiles/ab_decode_env.py c4crc 1 4 ZH_DEC_ALIGN=1 - \
-  ZH_LDS_PAD=3716 ZH_LDS_PAD=2400 > "$OUT/ab.out" 2> "$OUT/ab.err"
+timeout -k 10 600 python3 $R/profiles/ab_decode_env.py c4crc 1 6 - ZH_DEC_ALIGN=0 \
+  ZH_DEC_ALIGN=0,ZH_LDS_PAD=160 > "$OUT/ab.out" 2> "$OUT/ab.err"

@@ -1240,9 +1240,8 @@ int plan_create(zh_ctx* ctx, const zh_array_meta* m, const SrcDesc* srcs, int64_
       // starts at 4·i mod 128, so a 1 KiB wave load of it touched 9 lines and the shared line
       // was fetched twice.  When unit u's rows start at 32u elements and row r + 1 follows row
       // r (the payload is [32 rows][units][32 words], c4's layout), the movers load 128-B
-      // aligned lines and route each word to its tile in LDS (ZH_DEC_ALIGN=1: on; off by default
-      // until it is faster than the unaligned loads).
-      if (p->args.tile_variant == 51 && env_int("ZH_DEC_ALIGN", 0) != 0) {
+      // aligned lines and route each word to its tile in LDS (ZH_DEC_ALIGN=0: off).
+      if (p->args.tile_variant == 51 && env_int("ZH_DEC_ALIGN", 1) != 0) {
         const ScatterArgs& g = p->args;
         const int64_t nu = g.fast_n;
         // [32 rows][nu units][32 words], 2-4 steps of 8 units (K fits the box area), unit u's

@@ -2164,8 +2164,11 @@ void tiles_rowcrc_kernel(ScatterArgs a) {
 // Per chunk 1025 line fetches, the minimum for a misaligned 128 KiB (1 shared with the previous
 // chunk).  CRC as tiles_rowcrc_kernel (lane i: payload row i & 31 of tile i >> 5 from LDS).
 // LDS (bytes): T[8][256] at 0 (byte-swapped entries with SWAP), the box (31 rows × 32 words)
-// and K (≤ 32 words) in the S area at 8192, SD[4][256] at 12288, the 9 slots at 16384: 54 436 B,
-// 3 workgroups per CU.  Every lane reads the same descriptor (G = 1): the skip is block-uniform.
+// and K (≤ 32 words) in the S area at 8192, the unit-step shift as nibble tables SDn[8][16] at
+// 12288 (8 lookups per step instead of 4; byte tables would take 4 KiB), the 9 slots at 12800:
+// 50 852 B, 3 workgroups per CU (54 436 B, with byte tables, ran 2 per CU: 42.4 vs 36.4 ms, the
+// same as the unaligned kernel padded to that size, profiles/r03/occ).  Every lane reads the
+// same descriptor (G = 1): the skip is block-uniform.
 template <bool SWAP>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3)))
 void tiles_rowcrc_aln_kernel(ScatterArgs a) {
@@ -2173,14 +2176,14 @@ void tiles_rowcrc_aln_kernel(ScatterArgs a) {
   uint32_t(*T)[256] = reinterpret_cast<uint32_t(*)[256]>(smem);
   uint32_t* const box = T[8];
   uint32_t* const K = T[8] + 992;
-  uint32_t(*SD)[256] = T + 12;
-  uint32_t* const lds = reinterpret_cast<uint32_t*>(smem + 16384);
+  uint32_t(*SDn)[16] = reinterpret_cast<uint32_t(*)[16]>(smem + 12288);
+  uint32_t* const lds = reinterpret_cast<uint32_t*>(smem + 12800);
   const int tid = threadIdx.x;
 #pragma unroll
   for (int k = 0; k < 8; k++) T[k][tid] = SWAP ? __builtin_bswap32(g_crc.T[k][tid]) : g_crc.T[k][tid];
-#pragma unroll
-  for (int b = 0; b < 4; b++)
-    SD[b][tid] = a.crc_tile_step ? multmodp(a.crc_tile_step, (uint32_t)tid << (8 * b)) : 0u;
+  if (tid < 128)
+    SDn[tid >> 4][tid & 15] =
+        a.crc_tile_step ? multmodp(a.crc_tile_step, (uint32_t)(tid & 15) << (4 * (tid >> 4))) : 0u;
   for (int i = tid; i < a.fast_n; i += kBlock) K[i] = a.fast_tab[2 * a.fast_n + i];
   __syncthreads();
   const int wave = tid >> 6, lane = tid & 63, t = lane >> 3, g = lane & 7;
@@ -2294,7 +2297,10 @@ void tiles_rowcrc_aln_kernel(ScatterArgs a) {
       if (SWAP) acc = __builtin_bswap32(acc);
       const uint32_t uc = ub + tc;
       if (regular) {
-        run = (ulast == ~0u ? 0u : crc_shift_tab(run, SD)) ^ acc;
+        uint32_t sh = 0;  // run · x^(8Δ), nibble by nibble
+#pragma unroll
+        for (int i = 0; i < 8; i++) sh ^= SDn[i][(run >> (4 * i)) & 15];
+        run = (ulast == ~0u ? 0u : sh) ^ acc;
         ulast = uc;
       } else {
         share ^= multmodp(K[uc], acc);
@@ -3124,8 +3130,8 @@ static void launch_scatter_ds(const ScatterArgs& a, int tile, int enc, int grid,
             case 12: hipLaunchKernelGGL((tiles_crcw_kernel<2, false>), dim3(grid), dim3(2 * kBlock), lc, s, a); return;
             case 14: hipLaunchKernelGGL((tiles_crcw_kernel<4, false>), dim3(grid), dim3(2 * kBlock), lc, s, a); return;
             case 21:
-              if (a.tile_align) {  // LDS: tables 16 KiB + 9 slots (the host checked the rest)
-                const size_t la = 16384 + (size_t)9 * kTilePitch * 4;
+              if (a.tile_align) {  // LDS: tables 12.5 KiB + 9 slots (the host checked the rest)
+                const size_t la = 12800 + (size_t)9 * kTilePitch * 4;
                 if (a.swap) hipLaunchKernelGGL((tiles_rowcrc_aln_kernel<true>), dim3(grid), dim3(kBlock), la, s, a);
                 else hipLaunchKernelGGL((tiles_rowcrc_aln_kernel<false>), dim3(grid), dim3(kBlock), la, s, a);
                 return;
