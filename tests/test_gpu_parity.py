@@ -964,3 +964,48 @@ def test_truncated_shards_raise(dev, loc):
             device_read(dev, meta, [short], [0, 0], shape)
         assert str(ed.value) == str(eo.value)
         assert str(ed.value).startswith("Could not load byte data for chunk")
+
+
+@pytest.mark.parametrize("loadnt", ["0", "1"])
+def test_grouped_row_crc_decode_cache_policy(dev, monkeypatch, loadnt):
+    """The grouped row-CRC decode (rows_group_kernel, G = 2) with cached payload loads (the
+    default, ZH_CRC_LOADNT=0) and with non-temporal ones: misaligned payloads after each 4-byte
+    crc32c, the same bytes as the oracle and a corrupt payload byte reported alike."""
+    monkeypatch.setenv("ZH_CRC_LOADNT", loadnt)
+    monkeypatch.setenv("ZH_SMALL_SPLIT", "0")  # whole chunks: the grouped kernel needs them
+    monkeypatch.delenv("ZH_DEC_RGROUP", raising=False)
+    shape = [64, 64, 96]
+    meta = A.make_meta(shape, [32, 64, 64], 4, endian=A.ZH_ENDIAN_BIG, sharded=True,
+                       inner_chunk_shape=[32, 32, 32], inner_crc32c=True)
+    arr = rand_array(shape, 4, seed=83)
+    shards = encode_oracle(meta, arr)
+    got = device_read(dev, meta, shards, [0, 0, 0], shape)
+    np.testing.assert_array_equal(got, arr)
+    assert (lib().zh_debug_last_fast_path(0) % 1000) // 4 == 2  # row group 2
+    bad = bytearray(shards[1])
+    bad[3 * (32 * 32 * 32 * 4 + 4) + 4097] ^= 0x02
+    src = list(shards)
+    src[1] = bytes(bad)
+    with pytest.raises(O.OracleError) as eo:
+        O.array_read(meta, src, [0, 0, 0], shape)
+    with pytest.raises(ZhError) as ed:
+        device_read(dev, meta, src, [0, 0, 0], shape)
+    assert str(ed.value) == str(eo.value)
+
+
+@pytest.mark.parametrize("order", [None, [2, 1, 0]])
+@pytest.mark.parametrize("stnt", ["0", "1"])
+def test_grouped_crc_encode_cache_policy(dev, monkeypatch, order, stnt):
+    """The grouped encodes with the fused chunk CRC (row kernel for [bytes, crc32c], tile
+    kernel for [transpose, bytes, crc32c]) with payload stores through the cache
+    (ZH_ENC_CRC_STNT=0) and non-temporal ones: byte-identical to the oracle's shards."""
+    monkeypatch.setenv("ZH_ENC_CRC_STNT", stnt)
+    shape = [64, 64, 96]
+    meta = A.make_meta(shape, [32, 64, 64], 4, endian=A.ZH_ENDIAN_BIG, sharded=True,
+                       inner_chunk_shape=[32, 32, 32], transpose_order=order,
+                       inner_crc32c=True)
+    arr = rand_array(shape, 4, seed=89)
+    arr[0:32, 0:32, 32:64] = 0  # an all-fill chunk: elided, the layout shifts
+    want = encode_oracle(meta, arr)
+    got = device_write(dev, meta, arr)
+    assert got == want

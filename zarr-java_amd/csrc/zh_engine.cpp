@@ -1205,6 +1205,11 @@ int plan_create(zh_ctx* ctx, const zh_array_meta* m, const SrcDesc* srcs, int64_
   // non-temporal loads + stores: +4 % on the row path, +1 % on the tile path (interleaved
   // A/B in one process, profiles/r01/experiments/tune_*.json)
   p->args.nt = env_int("ZH_NT", 3) & 7;  // bit 2: 8 rows in flight per lane (rows)
+  // the grouped row-CRC decode (G = 2) loads payloads through the cache: a payload after a
+  // 4-byte crc32c sits at 4 mod 16, and the line two loads share then hits in L2 (c3crc
+  // reads 1.087x -> 1.003x algorithmic, 35.87 -> 34.87 ms, profiles/r03/c3crc); ZH_CRC_LOADNT=1:
+  // non-temporal loads
+  if (env_int("ZH_CRC_LOADNT", 0) == 0) p->args.nt |= 8;
   // Visit items in a golden-ratio stride order: +3.6 % on the tile path (c4) on every normal
   // allocation, neutral on the row path (interleaved A/B, profiles/placement_perm.py), so
   // on by default for tiles.  ZH_ITEM_PERM=0/1 overrides.
@@ -2336,6 +2341,9 @@ static int array_write_fast(zh_ctx* ctx, const zh_array_meta* m, ScatterArgs a,
     if (group && tile_crc) v.crc_tile_step = tile_crc_step(tile_ends, (size_t)(8 / group));
   }
   if (group) v.item_mul = env_int("ZH_ITEM_PERM", 1) ? golden_item_mul((items + group - 1) / group) : 0;
+  // grouped encode with the chunk CRC: ZH_ENC_CRC_STNT=0 stores the payloads through the cache
+  // (nt bit 4; a misaligned payload's line shared by two stores can merge in L2; A/B lab)
+  if (group && crc_fuse && v.nt == 3 && env_int("ZH_ENC_CRC_STNT", 1) == 0) v.nt |= 16;
   // grouped kernel: rows in flight per lane (2, 4, 8; G = 8 and the CRC variants: 4)
   const int gu = group == 8 || crc_fuse ? 4 : env_int("ZH_ENC_GU", 4);
   // tile groups: deep = 9 selects the prefetching form (ZH_ENC_TPF=1)

@@ -2160,7 +2160,8 @@ void tiles_rowcrc_kernel(ScatterArgs a) {
 // "tile 8" IS the next step's tile 0, and that slot held the previous step's tile 7, already
 // read).  Line 0 of L(r, 0) is the end of row r − 1: the head loads before step 0 (lane (t, g):
 // 16 B of row 8w + t's first line) put its first δ bytes in the box (row r − 1's tail, taken by
-// lanes 56-63 at the last step, which load no line 8 for rows < 31) and the rest in tile 0.
+// lanes 56-63 at the last step, which load line 7 again instead of line 8 for rows < 31) and
+// the rest in tile 0.
 // Per chunk 1025 line fetches, the minimum for a misaligned 128 KiB (1 shared with the previous
 // chunk).  CRC as tiles_rowcrc_kernel (lane i: payload row i & 31 of tile i >> 5 from LDS).
 // LDS (bytes): T[8][256] at 0 (byte-swapped entries with SWAP), the box (31 rows × 32 words)
@@ -2208,12 +2209,14 @@ void tiles_rowcrc_aln_kernel(ScatterArgs a) {
     uint4 x[8];
     auto load = [&](uint32_t ub, bool last) {
       const uint8_t* base = wsrc + (size_t)ub * 128;
-      // last step: lines 8 of rows < 31 are the next rows' head lines, already loaded
-      const bool skip = dl && last && t == 7;
+      // last step: lines 8 of rows < 31 are the next rows' head lines, already loaded: lanes
+      // 56-63 then load line 7 again, in the same instruction as lanes 48-55 (no extra line,
+      // no divergent branch; the box replaces the words)
+      const uint32_t back = dl && last && t == 7 ? 128u : 0u;
 #pragma unroll
       for (int k = 0; k < 8; k++)
-        if (!(skip && wv * 8 + k < 31))
-          x[k] = ld16g(base + (size_t)(wv * 8 + k) * s_fd * 4, (uint32_t)(16 * lane));
+        x[k] = ld16g(base + (size_t)(wv * 8 + k) * s_fd * 4,
+                     (uint32_t)(16 * lane) - (wv * 8 + k < 31 ? back : 0u));
     };
     if (dl) {  // head lines: row hr − 1's tail | row hr's tile-0 head (slot 0)
       const uint4 h = ld16g(src - dl + (size_t)wv * 8 * s_fd * 4, (uint32_t)(t * s_fd * 4 + 16 * g));
@@ -2248,20 +2251,30 @@ void tiles_rowcrc_aln_kernel(ScatterArgs a) {
           sl -= sl >= 9 ? 9 : 0;
           wa[j] = sl * kTilePitch + (e & 31);
         }
-        const bool tl = dl && last && t == 7;  // the row tails come from the box
+        if (dl && last) {  // the row tails of rows < 31 come from the box (lanes 56-63)
 #pragma unroll
-        for (int k = 0; k < 8; k++) {
-          const int rr = wv * 8 + k;
-          uint32_t v[4] = {sw(x[k].x), sw(x[k].y), sw(x[k].z), sw(x[k].w)};
-          if (tl && rr < 31) {
-            const uint4 bv = *reinterpret_cast<const uint4*>(box + rr * 32 + 4 * g);
-            const uint32_t b4[4] = {bv.x, bv.y, bv.z, bv.w};
+          for (int k = 0; k < 8; k++) {
+            const int rr = wv * 8 + k;
+            uint32_t v[4] = {sw(x[k].x), sw(x[k].y), sw(x[k].z), sw(x[k].w)};
+            if (t == 7 && rr < 31) {
+              const uint4 bv = *reinterpret_cast<const uint4*>(box + rr * 32 + 4 * g);
+              const uint32_t b4[4] = {bv.x, bv.y, bv.z, bv.w};
 #pragma unroll
-            for (int j = 0; j < 4; j++)
-              if (4 * g + j < Dp) v[j] = b4[j];
+              for (int j = 0; j < 4; j++)
+                if (4 * g + j < Dp) v[j] = b4[j];
+            }
+#pragma unroll
+            for (int j = 0; j < 4; j++) lds[wa[j] + rr * 33] = v[j];
           }
+        } else {
 #pragma unroll
-          for (int j = 0; j < 4; j++) lds[wa[j] + rr * 33] = v[j];
+          for (int k = 0; k < 8; k++) {
+            const int rr = wv * 8 + k;
+            lds[wa[0] + rr * 33] = sw(x[k].x);
+            lds[wa[1] + rr * 33] = sw(x[k].y);
+            lds[wa[2] + rr * 33] = sw(x[k].z);
+            lds[wa[3] + rr * 33] = sw(x[k].w);
+          }
         }
       }
       __syncthreads();
@@ -3206,7 +3219,13 @@ static void launch_scatter_ds(const ScatterArgs& a, int tile, int enc, int grid,
         case 2: hipLaunchKernelGGL((rows_group_kernel<DS, 1, 4, 3, false, false>), dim3(grid), dim3(kBlock), lc, s, a); break;
         case 3: hipLaunchKernelGGL((rows_group_kernel<DS, 1, 4, 3, true, false>), dim3(grid), dim3(kBlock), lc, s, a); break;
         case 4: hipLaunchKernelGGL((rows_group_kernel<DS, 2, 4, 3, false, false>), dim3(grid), dim3(kBlock), lc, s, a); break;
-        case 5: hipLaunchKernelGGL((rows_group_kernel<DS, 2, 4, 3, true, false>), dim3(grid), dim3(kBlock), lc, s, a); break;
+        case 5: {
+          // nt bit 3 (ZH_CRC_LOADNT=0): cached payload loads (a misaligned payload's line
+          // shared by two loads can then hit in L2; A/B lab), stores stay non-temporal
+          if (a.nt & 8) hipLaunchKernelGGL((rows_group_kernel<DS, 2, 4, 2, true, false>), dim3(grid), dim3(kBlock), lc, s, a);
+          else hipLaunchKernelGGL((rows_group_kernel<DS, 2, 4, 3, true, false>), dim3(grid), dim3(kBlock), lc, s, a);
+          break;
+        }
         case 8: hipLaunchKernelGGL((rows_group_kernel<DS, 4, 4, 3, false, false>), dim3(grid), dim3(kBlock), lc, s, a); break;
         case 9: hipLaunchKernelGGL((rows_group_kernel<DS, 4, 4, 3, true, false>), dim3(grid), dim3(kBlock), lc, s, a); break;
         default: break;  // host only sets 1, 2, 4
@@ -3301,11 +3320,15 @@ template <int DS>
 static bool launch_encode_fast_ds(const ScatterArgs& v, int grid, int deep, int group,
                                   hipStream_t s) {
   const size_t lds = ((size_t)v.fast_n * 8 + 15) & ~(size_t)15;
-  if (group > 0 && v.fast_mode != kFastTileTable && v.crc_fused && v.nt == 3) {
+  if (group > 0 && v.fast_mode != kFastTileTable && v.crc_fused && (v.nt & 15) == 3) {
     const size_t lc = lds + 12 * 256 * 4;  // + slicing tables T[8][256], shift table S[4][256]
+    const bool cst = (v.nt & 16) != 0;     // cached stores (ZH_ENC_CRC_STNT=0)
     switch (group) {  // host: rows sequential in the payload, whole chunks (piece_shift 0)
       case 1: hipLaunchKernelGGL((rows_group_kernel<DS, 1, 4, 3, true, true>), dim3(grid), dim3(kBlock), lc, s, v); return true;
-      case 2: hipLaunchKernelGGL((rows_group_kernel<DS, 2, 4, 3, true, true>), dim3(grid), dim3(kBlock), lc, s, v); return true;
+      case 2:
+        if (cst) hipLaunchKernelGGL((rows_group_kernel<DS, 2, 4, 1, true, true>), dim3(grid), dim3(kBlock), lc, s, v);
+        else hipLaunchKernelGGL((rows_group_kernel<DS, 2, 4, 3, true, true>), dim3(grid), dim3(kBlock), lc, s, v);
+        return true;
       case 4: hipLaunchKernelGGL((rows_group_kernel<DS, 4, 4, 3, true, true>), dim3(grid), dim3(kBlock), lc, s, v); return true;
       default: break;
     }
@@ -3351,11 +3374,14 @@ static bool launch_encode_fast_ds(const ScatterArgs& v, int grid, int deep, int 
         }
 #undef ZH_RC
       }
-      if (group > 0 && v.crc_fused && v.nt == 3) {  // host: crc_tile_step for 8/G units
+      if (group > 0 && v.crc_fused && (v.nt & 15) == 3) {  // host: crc_tile_step for 8/G units
         const size_t lc = l + 16 * 256 * 4 + (size_t)v.fast_n * 4 + 64;  // + alignment
         switch (group) {
           case 1: hipLaunchKernelGGL((tiles_group_kernel<3, 1, true, false, true>), dim3(grid), dim3(kBlock), lc, s, v); return true;
-          case 2: hipLaunchKernelGGL((tiles_group_kernel<3, 2, true, false, true>), dim3(grid), dim3(kBlock), lc, s, v); return true;
+          case 2:
+            if (v.nt & 16) hipLaunchKernelGGL((tiles_group_kernel<1, 2, true, false, true>), dim3(grid), dim3(kBlock), lc, s, v);  // cached stores
+            else hipLaunchKernelGGL((tiles_group_kernel<3, 2, true, false, true>), dim3(grid), dim3(kBlock), lc, s, v);
+            return true;
           case 4: hipLaunchKernelGGL((tiles_group_kernel<3, 4, true, false, true>), dim3(grid), dim3(kBlock), lc, s, v); return true;
           default: break;
         }
