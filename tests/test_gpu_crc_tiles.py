@@ -287,3 +287,31 @@ def _corrupt_matches_oracle_shape(dev, meta, shards, k, pos, shape):
     with pytest.raises(ZhError) as ed:
         device_read(dev, meta, srcs, [0] * len(shape), shape)
     assert str(ed.value) == str(eo.value)
+
+
+@pytest.mark.parametrize("nb", [16, 32])
+@pytest.mark.parametrize("pf", ["1", "0"])
+@pytest.mark.parametrize("endian", [A.ZH_ENDIAN_BIG, A.ZH_ENDIAN_LITTLE])
+def test_row_crc_aligned_encode(dev, monkeypatch, nb, pf, endian):
+    """tiles_rowcrc_enc_aln_kernel (ZH_ENC_ALIGN=1; ZH_ENC_ALIGN_PF: prefetching region loads
+    or not): the [transpose [2, 1, 0], bytes, crc32c] write of inner chunks [32, nb, 32] stores
+    whole 128-B payload lines.  One shard of 36 inner chunks puts the payloads at every offset
+    4i mod 128; two all-fill chunks are elided (the later payloads move by a chunk, the flags
+    come from the fill test of the loaded rows).  The shards are byte-identical to the
+    oracle's, and decode back."""
+    from helpers import device_write
+    monkeypatch.setenv("ZH_ENC_ALIGN", "1")
+    monkeypatch.setenv("ZH_ENC_ALIGN_PF", pf)
+    shape = [64, 6 * nb, 96]
+    meta = A.make_meta(shape, shape, 4, endian=endian, sharded=True,
+                       inner_chunk_shape=[32, nb, 32], transpose_order=[2, 1, 0],
+                       inner_crc32c=True)
+    arr = rand_array(shape, 4, seed=97 + nb)
+    arr[arr == 0] = 1
+    arr[0:32, nb:2 * nb, 0:32] = 0
+    arr[32:64, 3 * nb:4 * nb, 64:96] = 0
+    want = encode_oracle(meta, arr)
+    got = device_write(dev, meta, arr)
+    assert lib().zh_debug_last_fast_path(1) % 1000 == (31 if pf == "1" else 32)
+    assert got == want
+    np.testing.assert_array_equal(device_read(dev, meta, got, [0, 0, 0], shape), arr)

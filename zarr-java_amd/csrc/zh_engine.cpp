@@ -2355,12 +2355,36 @@ static int array_write_fast(zh_ctx* ctx, const zh_array_meta* m, ScatterArgs a,
     group = 8;
     v.item_mul = env_int("ZH_ITEM_PERM", 1) ? golden_item_mul((items + 7) / 8) : 0;
   }
-  const int grid = grid_for(ctx, group ? (items + group - 1) / group : pitems);
+  int grid = grid_for(ctx, group ? (items + group - 1) / group : pitems);
   // tile groups with the chunk CRC: ZH_ENC_ROWCRC=1 selects the row-CRC encode (deep = 30;
   // tiles_rowcrc_kernel<…, ENC>: every lane also CRCs one stored payload row from the tiles)
   const bool enc_rowcrc = v.fast_mode == kFastTileTable && group && crc_fuse && tile_crc &&
                           env_int("ZH_ENC_ROWCRC", 0) != 0 && zh::rowcrc_lds_at_zero();
+  // tile groups with the chunk CRC and c4's payload layout ([32 rows][units][32 words], unit u
+  // at 32u, region offsets u·xs): the row-CRC encode with 128-B aligned payload stores, one
+  // chunk per work item (tiles_rowcrc_enc_aln_kernel; ZH_ENC_ALIGN=1, ZH_ENC_ALIGN_PF=0/1)
+  bool enc_aln = false;
+  if (v.fast_mode == kFastTileTable && group && crc_fuse && tile_crc && v.nt == 3 &&
+      env_int("ZH_ENC_ALIGN", 0) != 0 && zh::rowcrc_lds_at_zero()) {
+    const int64_t nu = v.fast_n;
+    bool al = nu >= 16 && nu <= 32 && nu % 8 == 0 && v.rstride[v.fs] == 32 * nu &&
+              a.inner_nbytes == 4096 * nu && (int64_t)tab.size() >= 2 * nu;
+    const uint64_t xs = al ? tab[2] : 0;
+    for (int64_t u = 0; al && u < nu; u++)
+      al = tab[2 * (size_t)u + 1] == (uint32_t)(32 * u) && tab[2 * (size_t)u] == (uint64_t)u * xs &&
+           4 * (uint64_t)u * xs + 128 <= 0xFFFFFFFFull;
+    if (al) {
+      enc_aln = true;
+      group = 1;
+      v.tile_align = 1;
+      v.tile_ystride = (int64_t)xs;
+      v.crc_tile_step = tile_crc_step(tile_ends, 8);
+      v.item_mul = env_int("ZH_ITEM_PERM", 1) ? golden_item_mul(items) : 0;
+      grid = grid_for(ctx, items);
+    }
+  }
   const int deep = xpose ? 20
+                   : enc_aln ? (env_int("ZH_ENC_ALIGN_PF", 1) ? 31 : 32)
                    : enc_rowcrc ? 30
                    : v.fast_mode == kFastTileTable && group ? (env_int("ZH_ENC_TPF", 0) ? 9 : 1)
                    : group ? (gu <= 2 ? 0 : gu <= 4 ? 1 : 2)

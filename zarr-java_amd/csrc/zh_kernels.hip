@@ -2328,6 +2328,180 @@ void tiles_rowcrc_aln_kernel(ScatterArgs a) {
   }
 }
 
+// encode, the row-CRC tile kernel with 128-B aligned payload stores (ZH_ENC_ALIGN; host:
+// a.tile_align on the encode view, one chunk per work item, 16 ≤ fast_n ≤ 32, fast_n % 8 == 0,
+// tab[u] = (u·tile_ystride region, 32u payload), payload rows following each other).  The
+// encode mirror of tiles_rowcrc_aln_kernel: the movers load region rows into the tiles (the
+// fill test on the way), the tiles then hold payload words (payload row r, word w at w·33 + r),
+// and each wave instruction stores 8 whole payload lines: lane λ stores 16 B at 16λ from the
+// first line of L(r, s), words e = 4λ + j − δ/4 of L(r, s).  Words e < 0 are the end of
+// L(r, s − 1), still in the ring (step s − 1's tile 7 is slot (8s + 8) mod 9, which step s
+// does not write).  Line 0 of L(r, 0) also holds the end of row r − 1: lanes 0-7 keep it in
+// the box at step 0 and lanes 0-7 store it at the last step as line 8 of row r − 1 (tile 7's
+// words, then the box's); row 0's first line and row 31's last line are shared with the
+// neighbouring chunks (and the chunk's crc32c, stored later) and take dword stores of their own
+// words only.  Every payload line is written once, whole, by one store (the unaligned encode
+// wrote 1.059× the payload bytes, PMC).  PF: the next step's region loads are issued after the
+// first barrier (the decode's order).  CRC as tiles_rowcrc_kernel<…, ENC> (plain tables: the
+// tiles hold payload words); LDS as tiles_rowcrc_aln_kernel (50 852 B).
+template <bool SWAP, bool PF>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3)))
+void tiles_rowcrc_enc_aln_kernel(ScatterArgs a) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  uint32_t(*T)[256] = reinterpret_cast<uint32_t(*)[256]>(smem);
+  uint32_t* const box = T[8];
+  uint32_t* const K = T[8] + 992;
+  uint32_t(*SDn)[16] = reinterpret_cast<uint32_t(*)[16]>(smem + 12288);
+  uint32_t* const lds = reinterpret_cast<uint32_t*>(smem + 12800);
+  const int tid = threadIdx.x;
+#pragma unroll
+  for (int k = 0; k < 8; k++) T[k][tid] = g_crc.T[k][tid];
+  if (tid < 128)
+    SDn[tid >> 4][tid & 15] =
+        a.crc_tile_step ? multmodp(a.crc_tile_step, (uint32_t)(tid & 15) << (4 * (tid >> 4))) : 0u;
+  for (int i = tid; i < a.fast_n; i += kBlock) K[i] = a.fast_tab[2 * a.fast_n + i];
+  __syncthreads();
+  const int wave = tid >> 6, lane = tid & 63, t = lane >> 3, g = lane & 7;
+  const int wv = __builtin_amdgcn_readfirstlane(wave);
+  const int tc = tid >> 5, r = tid & 31;  // CRC role
+  const int64_t s_fd = a.pstride[a.fd], d_fs = a.rstride[a.fs];  // region row, payload row pitch
+  const bool regular = a.crc_tile_step != 0;
+  const uint32_t units = (uint32_t)a.fast_n, xs = (uint32_t)a.tile_ystride;
+  const uint32_t kr = x2nmodp((uint64_t)(31 - r) * 4 * (uint64_t)d_fs, 3);
+  const uint32_t fillv = (uint32_t)a.fill;
+  auto sw = [](uint32_t v) { return SWAP ? __builtin_bswap32(v) : v; };
+  auto rfl = [](uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); };
+  for (int64_t gi = blockIdx.x; gi < a.n_citems; gi += gridDim.x) {
+    const int64_t c = a.item_mul ? (int64_t)(((uint64_t)gi * a.item_mul) % (uint64_t)a.n_citems) : gi;
+    const uint4* dp = reinterpret_cast<const uint4*>(a.desc + c);
+    const uint4 dx = dp[0], dy = dp[1];
+    if ((rfl(dy.z) & kDescFast) == 0) continue;  // block-uniform
+    const uint8_t* src = (const uint8_t*)(uintptr_t)(((uint64_t)rfl(dx.y) << 32) | rfl(dx.x));
+    uint8_t* dst = a.region + (int64_t)(((uint64_t)rfl(dx.w) << 32) | rfl(dx.z)) * 4;
+    const uint32_t dl = (uint32_t)(uintptr_t)dst & 127u;
+    const int Dp = (int)(dl >> 2);  // δ/4 (0: aligned, no held or extra line)
+    uint8_t* const A = dst - dl;
+    bool differs = false;
+    uint4 x[8];
+    auto load = [&](uint32_t ub) {
+      const uint32_t voff = ((ub + t) * xs + 4 * g) * 4;
+#pragma unroll
+      for (int k = 0; k < 8; k++) x[k] = ld16g(src + (size_t)(wv * 8 + k) * s_fd * 4, voff);
+    };
+    if (PF) load(0);
+    uint32_t share = 0, run = 0, ulast = ~0u;
+    int sb = 0;  // slot of this step's tile 0: (8s) mod 9
+#pragma unroll 1
+    for (uint32_t ub = 0; ub < units; ub += kTG) {
+      const bool last = ub + kTG >= units;
+      if (!PF) load(ub);
+      {  // the fill test and the tiles (region row rr of tile t: words 4g..4g+3)
+        int st = sb + t;
+        st -= st >= 9 ? 9 : 0;
+        uint32_t* mine = lds + st * kTilePitch;
+#pragma unroll
+        for (int k = 0; k < 8; k++) {
+          differs |= (x[k].x != fillv) | (x[k].y != fillv) | (x[k].z != fillv) | (x[k].w != fillv);
+          uint32_t* row = mine + (wave * 8 + k) * 33 + g * 4;
+          row[0] = sw(x[k].x);
+          row[1] = sw(x[k].y);
+          row[2] = sw(x[k].z);
+          row[3] = sw(x[k].w);
+        }
+      }
+      __syncthreads();
+      if (PF && !last) load(ub + kTG);
+      {  // whole payload lines: lane λ, words e = 4λ + j − δ/4 of L(rr, s) (e < 0: step s − 1)
+        int e1 = 32 - Dp + 4 * lane;  // e + 32
+        asm volatile("" : "+v"(e1));
+        int wa[4];
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+          const int e = e1 + j;
+          int sl = sb + 8 + (e >> 5);
+          sl -= sl >= 9 ? 9 : 0;
+          sl -= sl >= 9 ? 9 : 0;
+          wa[j] = sl * kTilePitch + (e & 31) * 33;
+        }
+        const bool hold = dl && ub == 0 && t == 0;  // line 0 of row rr: at the last step
+#pragma unroll
+        for (int k = 0; k < 8; k++) {
+          const int rr = wv * 8 + k;
+          uint4 y;
+          y.x = lds[wa[0] + rr];
+          y.y = lds[wa[1] + rr];
+          y.z = lds[wa[2] + rr];
+          y.w = lds[wa[3] + rr];
+          uint8_t* row = A + (size_t)rr * d_fs * 4 + (size_t)ub * 128;
+          if (!hold) {
+            st16g(row, (uint32_t)(16 * lane), y);
+          } else {
+            *reinterpret_cast<uint4*>(box + rr * 32 + 4 * g) = y;
+            if (rr == 0) {  // the chunk's first line: its own words only
+              const uint32_t yv[4] = {y.x, y.y, y.z, y.w};
+#pragma unroll
+              for (int j = 0; j < 4; j++)
+                if (4 * g + j >= Dp) reinterpret_cast<uint32_t*>(row + 16 * g)[j] = yv[j];
+            }
+          }
+        }
+        if (dl && last && t == 0) {  // line 8 of L(rr, last) = line 0 of row rr + 1
+          int st7 = sb + 7;
+          st7 -= st7 >= 9 ? 9 : 0;
+#pragma unroll
+          for (int k = 0; k < 8; k++) {
+            const int rr = wv * 8 + k;
+            uint32_t v[4];
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+              const int d = 4 * g + j;
+              v[j] = d < Dp ? lds[st7 * kTilePitch + (32 - Dp + d) * 33 + rr]
+                            : (rr < 31 ? box[(rr + 1) * 32 + d] : 0u);
+            }
+            uint8_t* nxt = A + (size_t)(rr + 1) * d_fs * 4 + 16 * g;
+            if (rr < 31) {
+              st16g(A + (size_t)(rr + 1) * d_fs * 4, (uint32_t)(16 * g), make_uint4(v[0], v[1], v[2], v[3]));
+            } else {  // the chunk's last line: the payload's last words only
+#pragma unroll
+              for (int j = 0; j < 4; j++)
+                if (4 * g + j < Dp) reinterpret_cast<uint32_t*>(nxt)[j] = v[j];
+            }
+          }
+        }
+      }
+      uint32_t w[32];
+      {
+        int sc = sb + tc;
+        sc -= sc >= 9 ? 9 : 0;
+        const uint32_t* crow = lds + sc * kTilePitch + r;
+#pragma unroll
+        for (int j = 0; j < 32; j++) w[j] = crow[j * 33];
+      }
+      __syncthreads();
+      uint32_t acc = 0;
+#pragma unroll
+      for (int j = 0; j < 32; j += 2) acc = crc_upd8_lds<false>(acc, w[j], w[j + 1]);
+      const uint32_t uc = ub + tc;
+      if (regular) {
+        uint32_t sh = 0;
+#pragma unroll
+        for (int i = 0; i < 8; i++) sh ^= SDn[i][(run >> (4 * i)) & 15];
+        run = (ulast == ~0u ? 0u : sh) ^ acc;
+        ulast = uc;
+      } else {
+        share ^= multmodp(K[uc], acc);
+      }
+      sb = sb == 0 ? 8 : sb - 1;
+    }
+    if (__ballot(differs) != 0 && lane == 0) a.flags[c] = 1;
+    if (regular && ulast != ~0u) share = multmodp(K[ulast], run);
+    uint32_t cr = multmodp(kr, share);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) cr ^= (uint32_t)__shfl_xor((int)cr, o, 64);
+    if (lane == 0) atomicXor(a.crc_partials + c, cr);
+  }
+}
+
 // The CRC-fused decode variant held to 3 waves per SIMD (LDS allows 3 blocks of 4 waves per
 // CU; unconstrained it takes 172 VGPRs and runs 2)
 template <int NT, bool FLAGS>
@@ -3261,7 +3435,11 @@ bool rowcrc_lds_at_zero() {
                          (const void*)tiles_rowcrc_kernel<2, false, true>, (const void*)tiles_rowcrc_kernel<2, true, true>,
                          (const void*)tiles_rowcrc_kernel<4, false, true>, (const void*)tiles_rowcrc_kernel<4, true, true>,
                          (const void*)tiles_rowcrc_aln_kernel<false>,
-                         (const void*)tiles_rowcrc_aln_kernel<true>};
+                         (const void*)tiles_rowcrc_aln_kernel<true>,
+                         (const void*)tiles_rowcrc_enc_aln_kernel<false, true>,
+                         (const void*)tiles_rowcrc_enc_aln_kernel<true, true>,
+                         (const void*)tiles_rowcrc_enc_aln_kernel<false, false>,
+                         (const void*)tiles_rowcrc_enc_aln_kernel<true, false>};
     for (const void* f : fns) {
       hipFuncAttributes at;
       if (hipFuncGetAttributes(&at, f) != hipSuccess || at.sharedSizeBytes != 0) return false;
@@ -3362,6 +3540,18 @@ static bool launch_encode_fast_ds(const ScatterArgs& v, int grid, int deep, int 
   if (v.fast_mode == kFastTileTable) {
     if constexpr (DS == 4) {
       const size_t l = lds + (size_t)kTG * kTilePitch * 4;
+      if (group == 1 && v.crc_fused && v.nt == 3 && v.tile_align && (deep == 31 || deep == 32)) {
+        // aligned payload lines (ZH_ENC_ALIGN; deep 31: prefetching loads, 32: not)
+        const size_t la = 12800 + (size_t)9 * kTilePitch * 4;
+        if (deep == 31) {
+          if (v.swap) hipLaunchKernelGGL((tiles_rowcrc_enc_aln_kernel<true, true>), dim3(grid), dim3(kBlock), la, s, v);
+          else hipLaunchKernelGGL((tiles_rowcrc_enc_aln_kernel<false, true>), dim3(grid), dim3(kBlock), la, s, v);
+        } else {
+          if (v.swap) hipLaunchKernelGGL((tiles_rowcrc_enc_aln_kernel<true, false>), dim3(grid), dim3(kBlock), la, s, v);
+          else hipLaunchKernelGGL((tiles_rowcrc_enc_aln_kernel<false, false>), dim3(grid), dim3(kBlock), la, s, v);
+        }
+        return true;
+      }
       if (group > 0 && v.crc_fused && v.nt == 3 && deep == 30) {  // row-CRC encode (ZH_ENC_ROWCRC)
         const size_t lc = l + 16 * 256 * 4 + (size_t)v.fast_n * 4 + 64;
 #define ZH_RC(G) if (v.swap) hipLaunchKernelGGL((tiles_rowcrc_kernel<G, true, true>), dim3(grid), dim3(kBlock), lc, s, v); \
