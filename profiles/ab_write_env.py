@@ -76,6 +76,8 @@ for r in range(rounds):
                 int(sz != sizes)
         else:
             bad[v] += int(sz != sizes)
+    print(f"round {r}: " + ", ".join(f"{v} {res[v][-1]} ms" for v in variants), file=sys.stderr,
+          flush=True)
 print(json.dumps({"config": cfg, "ydiv": ydiv, "arena": arena,
                   "results": {v: {"ms": ms, "median_ms": statistics.median(ms),
                                   "GiBps": round(nb / (statistics.median(ms) / 1e3) / 2**30, 1)}

@@ -876,6 +876,7 @@ constexpr uint32_t kPoly = 0x82F63B78u;
 
 // a(x) * b(x) mod P (reflected bit order)
 __device__ __forceinline__ uint32_t multmodp(uint32_t a, uint32_t b) {
+  if (a == 0) return 0;  // (the loop below ends at a's lowest set bit: never for a = 0)
   uint32_t m = 1u << 31, p = 0;
   for (;;) {
     if (a & m) {
@@ -2436,7 +2437,8 @@ void tiles_rowcrc_enc_aln_kernel(ScatterArgs a) {
           if (!hold) {
             st16g(row, (uint32_t)(16 * lane), y);
           } else {
-            *reinterpret_cast<uint4*>(box + rr * 32 + 4 * g) = y;
+            // row rr's line 0 in box row rr − 1 (box rows 0-30: K sits after them)
+            if (rr > 0) *reinterpret_cast<uint4*>(box + (rr - 1) * 32 + 4 * g) = y;
             if (rr == 0) {  // the chunk's first line: its own words only
               const uint32_t yv[4] = {y.x, y.y, y.z, y.w};
 #pragma unroll
@@ -2456,7 +2458,7 @@ void tiles_rowcrc_enc_aln_kernel(ScatterArgs a) {
             for (int j = 0; j < 4; j++) {
               const int d = 4 * g + j;
               v[j] = d < Dp ? lds[st7 * kTilePitch + (32 - Dp + d) * 33 + rr]
-                            : (rr < 31 ? box[(rr + 1) * 32 + d] : 0u);
+                            : (rr < 31 ? box[rr * 32 + d] : 0u);
             }
             uint8_t* nxt = A + (size_t)(rr + 1) * d_fs * 4 + 16 * g;
             if (rr < 31) {
