@@ -982,10 +982,11 @@ def test_grouped_row_crc_decode_cache_policy(dev, monkeypatch, loadnt):
     got = device_read(dev, meta, shards, [0, 0, 0], shape)
     np.testing.assert_array_equal(got, arr)
     assert (lib().zh_debug_last_fast_path(0) % 1000) // 4 == 2  # row group 2
-    bad = bytearray(shards[1])
-    bad[3 * (32 * 32 * 32 * 4 + 4) + 4097] ^= 0x02
+    k = max(range(len(shards)), key=lambda i: len(shards[i] or b""))  # a shard of 4 chunks
+    bad = bytearray(shards[k])
+    bad[3 * (32 * 32 * 32 * 4 + 4) + 4097] ^= 0x02  # chunk 3's payload: 4 mod 16 after 3 CRCs
     src = list(shards)
-    src[1] = bytes(bad)
+    src[k] = bytes(bad)
     with pytest.raises(O.OracleError) as eo:
         O.array_read(meta, src, [0, 0, 0], shape)
     with pytest.raises(ZhError) as ed:
