@@ -1038,15 +1038,15 @@ def store_inclusive(dev, A, shard_slab, offs, sizes, coords, scratch):
                  "store_stage_ms": round(parts[k]["stage_s"] * 1e3, 1),
                  "zh_array_read_ms": round(parts[k]["device_s"] * 1e3, 1),
                  "staged_bytes": arr.staged_bytes}
-            if name == "two_shards":
-                dev.memcpy(scratch, got.ctypes.data, nb, 0, None, True)
-                r["verify_mismatches"] = int(dev.synth_verify(scratch, shape, off, shp, 4, SEED))
+            dev.memcpy(scratch, got.ctypes.data, nb, 0, None, True)
+            r["verify_mismatches"] = int(dev.synth_verify(scratch, shape, off, shp, 4, SEED))
             res[name] = r
             del got
         res["path"] = ("zarrhip.Array.read (Python mirror of core.Array.read) from a "
-                       f"FilesystemStore on {d}: store reads + host index check + one "
-                       "zh_array_read (H2D from the staging pool, page-locked once a buffer is reused; "
-                       "decode; D2H into a fresh numpy array)")
+                       f"FilesystemStore on {d}: store reads (whole shards; for a partly covered "
+                       "shard the stored index + the referenced runs) + one library read "
+                       "(pipelined H2D through page-locked rings, the stored index's crc32c and "
+                       "the decode on the device, D2H into a fresh numpy array)")
     finally:
         shutil.rmtree(base, ignore_errors=True)
     return res
