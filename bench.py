@@ -222,7 +222,9 @@ def kernel_name(meta):
         if os.environ.get("ZH_DEC_TGROUP") == "0":
             return "decode_tiles_kernel"
         if meta.chain.inner_crc32c and os.environ.get("ZH_DEC_CRCW", "3") == "3":
-            return "tiles_rowcrc_kernel"
+            # 128-B aligned payload windows unless ZH_DEC_ALIGN=0 (round 3)
+            return ("tiles_rowcrc_kernel" if os.environ.get("ZH_DEC_ALIGN") == "0"
+                    else "tiles_rowcrc_aln_kernel")
         return "tiles_group_kernel"
     # row chains with 128-B rows and no chunk CRC: the lane-exchange kernel (ZH_DEC_RGROUP=8)
     c = meta.chain

@@ -2342,8 +2342,11 @@ static int array_write_fast(zh_ctx* ctx, const zh_array_meta* m, ScatterArgs a,
   }
   if (group) v.item_mul = env_int("ZH_ITEM_PERM", 1) ? golden_item_mul((items + group - 1) / group) : 0;
   // grouped encode with the chunk CRC: ZH_ENC_CRC_STNT=0 stores the payloads through the cache
-  // (nt bit 4; a misaligned payload's line shared by two stores can merge in L2; A/B lab)
-  if (group && crc_fuse && v.nt == 3 && env_int("ZH_ENC_CRC_STNT", 1) == 0) v.nt |= 16;
+  // (nt bit 4): a misaligned payload's line shared by two stores can merge in L2.  Default for
+  // the row groups (c3crc write 41.04 → 39.77 ms, profiles/r03/final/ab_write_stnt_c3crc.json);
+  // the tile groups keep non-temporal stores (c4crc 43.28 vs 43.66 ms cached)
+  const int stnt_def = v.fast_mode == kFastTileTable ? 1 : 0;
+  if (group && crc_fuse && v.nt == 3 && env_int("ZH_ENC_CRC_STNT", stnt_def) == 0) v.nt |= 16;
   // grouped kernel: rows in flight per lane (2, 4, 8; G = 8 and the CRC variants: 4)
   const int gu = group == 8 || crc_fuse ? 4 : env_int("ZH_ENC_GU", 4);
   // tile groups: deep = 9 selects the prefetching form (ZH_ENC_TPF=1)
