@@ -232,6 +232,9 @@ def kernel_name(meta):
     if c.sharded and not c.inner_crc32c and rg in (None, "8") and \
             c.inner_chunk_shape[meta.ndim - 1] * meta.dtype_size == 128:
         return "rows_xpose_kernel"
+    # with the chunk crc32c: the grouped row-CRC kernel (ZH_DEC_RGROUP=-1 picks its group)
+    if c.sharded and c.inner_crc32c and rg in (None, "-1", "1", "2", "4"):
+        return "rows_group_kernel"
     return "decode_rows_kernel<4,4>"
 
 

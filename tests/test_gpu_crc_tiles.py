@@ -315,3 +315,36 @@ def test_row_crc_aligned_encode(dev, monkeypatch, nb, pf, endian):
     assert lib().zh_debug_last_fast_path(1) % 1000 == (31 if pf == "1" else 32)
     assert got == want
     np.testing.assert_array_equal(device_read(dev, meta, got, [0, 0, 0], shape), arr)
+
+
+def test_row_crc_chain_64mib_defaults(dev, monkeypatch):
+    """The c3crc chain ([bytes(big), crc32c], 32³ uint32 inner chunks, no transpose) at 64 MiB
+    with the default kernels of both directions: the grouped row-CRC encode (2 chunks per work
+    item, payloads stored through the cache since round 3) gives the oracle's shard bytes, and
+    the grouped row-CRC decode (cached payload loads) gives the array back; a flipped byte deep
+    inside the last shard is reported with the oracle's message."""
+    for k in ("ZH_ENC_CRC_STNT", "ZH_ENC_GROUP", "ZH_CRC_LOADNT", "ZH_DEC_RGROUP",
+              "ZH_SMALL_SPLIT", "ZH_PIPE"):
+        monkeypatch.delenv(k, raising=False)
+    shape = [1, 256, 256, 256]
+    meta = A.make_meta(shape, [1, 128, 128, 128], 4, endian=A.ZH_ENDIAN_BIG, sharded=True,
+                       inner_chunk_shape=[1, 32, 32, 32], inner_crc32c=True)
+    arr = rand_array(shape, 4, seed=61)
+    arr[arr == 0] = 1
+    want = encode_oracle(meta, arr)
+    got = device_write(dev, meta, arr)
+    assert (lib().zh_debug_last_fast_path(1) % 1000000) // 1000 == 2  # row groups of 2
+    assert got == want
+    monkeypatch.setenv("ZH_PIPE", "0")  # one plan over the whole array
+    np.testing.assert_array_equal(device_read(dev, meta, want, [0, 0, 0, 0], shape), arr)
+    assert (lib().zh_debug_last_fast_path(0) % 1000) // 4 == 2  # decode row groups of 2
+    bad = list(want)
+    k = len(bad) - 1
+    b = bytearray(bad[k])
+    b[45 * CHUNK + 77777] ^= 0x10
+    bad[k] = bytes(b)
+    with pytest.raises(O.OracleError) as eo:
+        O.array_read(meta, bad, [0, 0, 0, 0], shape)
+    with pytest.raises(ZhError) as ed:
+        device_read(dev, meta, bad, [0, 0, 0, 0], shape)
+    assert str(ed.value) == str(eo.value)
