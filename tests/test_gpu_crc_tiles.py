@@ -7,7 +7,7 @@ import numpy as np
 import pytest
 
 import oracle as O
-from helpers import chunk_coords, device_read, encode_oracle, rand_array
+from helpers import chunk_coords, device_read, device_write, encode_oracle, rand_array
 from zarrhip import _abi as A
 from zarrhip._lib import ZhError, lib
 
@@ -172,6 +172,11 @@ def test_row_crc_tile_kernel_many_groups(dev, monkeypatch):
     arr = rand_array(shape, 4, seed=59)
     arr[arr == 0] = 1
     shards = encode_oracle(meta, arr)
+    # the default tile encode with the fused chunk CRC (2 chunks per work item) at this size
+    for k in ("ZH_ENC_CRC_STNT", "ZH_ENC_TGROUP", "ZH_ENC_ALIGN", "ZH_ENC_ROWCRC", "ZH_ENC_TPF"):
+        monkeypatch.delenv(k, raising=False)
+    assert device_write(dev, meta, arr) == shards
+    assert (lib().zh_debug_last_fast_path(1) % 1000000) // 1000 == 2
     want = np.frombuffer(O.array_read(meta, shards, [0, 0, 0, 0], shape), np.uint32).reshape(shape)
     got = device_read(dev, meta, shards, [0, 0, 0, 0], shape)  # pipelined (128 MiB host side)
     np.testing.assert_array_equal(got, want)
@@ -348,3 +353,49 @@ def test_row_crc_chain_64mib_defaults(dev, monkeypatch):
     with pytest.raises(ZhError) as ed:
         device_read(dev, meta, bad, [0, 0, 0, 0], shape)
     assert str(ed.value) == str(eo.value)
+
+
+@pytest.mark.parametrize("order", [None, [0, 3, 2, 1]])
+def test_plain_chains_64mib_defaults(dev, monkeypatch, order):
+    """c3 / c4 chains without the chunk CRC ([(transpose [0,3,2,1],) bytes(big)], 32³ uint32
+    inner chunks) at 64 MiB through the default kernels: the grouped encodes give the oracle's
+    shard bytes, and the decode (lane exchange for c3, tile groups for c4) gives the array
+    back, also for a region that cuts every shard."""
+    for k in ("ZH_ENC_GROUP", "ZH_ENC_TGROUP", "ZH_ENC_XPOSE", "ZH_DEC_RGROUP", "ZH_DEC_TGROUP",
+              "ZH_SMALL_SPLIT", "ZH_PIPE"):
+        monkeypatch.delenv(k, raising=False)
+    shape = [1, 256, 256, 256]
+    meta = A.make_meta(shape, [1, 128, 128, 128], 4, endian=A.ZH_ENDIAN_BIG, sharded=True,
+                       inner_chunk_shape=[1, 32, 32, 32], transpose_order=order)
+    arr = rand_array(shape, 4, seed=67)
+    arr[arr == 0] = 1
+    want = encode_oracle(meta, arr)
+    assert device_write(dev, meta, arr) == want
+    monkeypatch.setenv("ZH_PIPE", "0")
+    np.testing.assert_array_equal(device_read(dev, meta, want, [0, 0, 0, 0], shape), arr)
+    off, shp = [0, 40, 8, 100], [1, 200, 240, 140]
+    sel = chunk_coords(meta, off, shp)
+    pos = {c: i for i, c in enumerate(chunk_coords(meta, [0, 0, 0, 0], shape))}
+    got = device_read(dev, meta, [want[pos[c]] for c in sel], off, shp)
+    np.testing.assert_array_equal(got, arr[0:1, 40:240, 8:248, 100:240])
+
+
+@pytest.mark.parametrize("order", [[0, 2, 1], [2, 1, 0], [1, 2, 0]])
+@pytest.mark.parametrize("group", ["1", "2", "4"])
+@pytest.mark.parametrize("stnt", ["0", "1"])
+def test_tile_crc_encode_compact_tables(dev, monkeypatch, order, group, stnt):
+    """The tile encode with the fused chunk CRC over compact tables (ZH_ENC_CRCLOW=1:
+    slicing-by-4 and nibble shift tables, 4 workgroups per CU): byte-identical to the oracle's
+    shards (an all-fill chunk elided, so the later payloads shift), for 1, 2 and 4 chunks per
+    work item and both store policies, and the kernel that ran is that variant (deep 40)."""
+    monkeypatch.setenv("ZH_ENC_CRCLOW", "1")
+    monkeypatch.setenv("ZH_ENC_TGROUP", group)
+    monkeypatch.setenv("ZH_ENC_CRC_STNT", stnt)
+    meta = _meta(order)
+    arr = rand_array(SHAPE, 4, seed=97)
+    arr[0:32, 32:64, 0:32] = 0
+    want = encode_oracle(meta, arr)
+    got = device_write(dev, meta, arr)
+    assert got == want
+    path = lib().zh_debug_last_fast_path(1)
+    assert path % 1000 == 40 and (path % 1000000) // 1000 == int(group)

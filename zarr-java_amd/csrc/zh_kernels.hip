@@ -1234,6 +1234,27 @@ __device__ __forceinline__ uint32_t crc_shift_k(uint32_t c, const uint32_t (*S)[
          tlook(S, 3, byte_x4<3>(c));
 }
 
+// Compact CRC tables (LOW = true in tiles_group_kernel: 5 KiB of LDS instead of 16 KiB):
+// slicing-by-4 over T[0..3] (4 dependent word rounds per 16-B vector, the same 16 lookups as
+// slicing-by-8) and shifts by nibble tables Sn[8][16] (Sn[i][n] = k·n·x^(4i): 8 lookups
+// instead of 4, 512 B instead of 4 KiB).  Tables at a constant LDS position, as crc_upd16_k.
+__device__ __forceinline__ uint32_t crc_upd4_k(uint32_t c, uint32_t w, const uint32_t (*T)[256]) {
+  const uint32_t x = c ^ w;
+  return xor3(tlook(T, 3, byte_x4<0>(x)), tlook(T, 2, byte_x4<1>(x)), tlook(T, 1, byte_x4<2>(x))) ^
+         tlook(T, 0, byte_x4<3>(x));
+}
+__device__ __forceinline__ uint32_t crc_upd16_s4(uint32_t c, v4u v, const uint32_t (*T)[256]) {
+  return crc_upd4_k(crc_upd4_k(crc_upd4_k(crc_upd4_k(c, v.x, T), v.y, T), v.z, T), v.w, T);
+}
+__device__ __forceinline__ uint32_t crc_shift_n(uint32_t c, const uint32_t (*Sn)[16]) {
+  // byte offset of entry (i, nibble i of c): 64·i + 4·nibble
+  auto at = [&](int i) {
+    const uint32_t off = (i == 0 ? (c << 2) : (c >> (4 * i - 2))) & 0x3Cu;
+    return *reinterpret_cast<const uint32_t*>(reinterpret_cast<const uint8_t*>(Sn[i]) + off);
+  };
+  return xor3(at(0), at(1), at(2)) ^ xor3(at(3), at(4), at(5)) ^ (at(6) ^ at(7));
+}
+
 // encode, grouped row kernel (write path, narrow rows): a work item is G consecutive inner
 // chunks — z-adjacent in the region when they sit in one shard row — and lane group q of
 // every G·vpr lanes moves chunk q.  A wave load then covers G·(row bytes) of one region row
@@ -1680,12 +1701,17 @@ __global__ __launch_bounds__(kBlock) void decode_tiles_kernel(ScatterArgs a) {
 // the chunk's lane segment and one atomic per wave.
 //
 // PF: the next step's loads are issued before this step's stores (decode_tiles_body's order).
-template <int NT, int G, bool CRC, bool PF, bool FLAGS>
+//
+// LOW (CRC only): compact tables (crc_upd16_s4 / crc_shift_n: T[4][256], Sn[8][16], SDn[8][16],
+// 5 KiB instead of 16 KiB), so that tiles + tables fit 4 workgroups per CU (39.3 KB each;
+// 50.5 KB with the byte tables holds the kernel at 3); 7 more lookups per 8 vectors.
+template <int NT, int G, bool CRC, bool PF, bool FLAGS, bool LOW = false>
 __global__ __launch_bounds__(kBlock) void tiles_group_kernel(ScatterArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   // CRC: the tables first (T, S, SD: a constant LDS position for crc_upd16_k / crc_shift_k),
   // then K, the unit table and the tiles
-  uint8_t* tab_at = CRC ? smem + ((16 * 256 * 4 + (size_t)a.fast_n * 4 + 15) & ~(size_t)15) : smem;
+  constexpr size_t kTabBytes = LOW ? 4 * 256 * 4 + 2 * 8 * 16 * 4 : 16 * 256 * 4;
+  uint8_t* tab_at = CRC ? smem + ((kTabBytes + (size_t)a.fast_n * 4 + 15) & ~(size_t)15) : smem;
   uint2* tab = reinterpret_cast<uint2*>(tab_at);
   uint8_t* after_tab = tab_at + (((size_t)a.fast_n * 8 + 15) & ~(size_t)15);
   uint32_t* lds = reinterpret_cast<uint32_t*>(after_tab);
@@ -1698,22 +1724,37 @@ __global__ __launch_bounds__(kBlock) void tiles_group_kernel(ScatterArgs a) {
   uint32_t(*T)[256] = nullptr;
   uint32_t(*S)[256] = nullptr;
   uint32_t(*SD)[256] = nullptr;
+  uint32_t(*Sn)[16] = nullptr;  // LOW
+  uint32_t(*SDn)[16] = nullptr;
   uint32_t* K = nullptr;
   uint32_t kb = 0;
   if constexpr (CRC) {
     T = reinterpret_cast<uint32_t(*)[256]>(smem);
-    S = T + 8;
-    SD = S + 4;
-    K = reinterpret_cast<uint32_t*>(SD + 4);
-    init_crc_tables(T);
     // payload row pitch of the lane's vectors: the stored rows (encode) or the loaded rows
     const int64_t pitch = FLAGS ? d_fs : s_fd;
     const uint32_t kg = x2nmodp((uint64_t)(4 * pitch), 3);
+    if constexpr (LOW) {
+      Sn = reinterpret_cast<uint32_t(*)[16]>(smem + 4 * 256 * 4);
+      SDn = Sn + 8;
+      K = reinterpret_cast<uint32_t*>(SDn + 8);
 #pragma unroll
-    for (int b = 0; b < 4; b++) {
-      S[b][threadIdx.x] = multmodp(kg, (uint32_t)threadIdx.x << (8 * b));
-      SD[b][threadIdx.x] =
-          a.crc_tile_step ? multmodp(a.crc_tile_step, (uint32_t)threadIdx.x << (8 * b)) : 0u;
+      for (int k = 0; k < 4; k++) T[k][threadIdx.x] = g_crc.T[k][threadIdx.x];
+      if (threadIdx.x < 128) {
+        const uint32_t i = threadIdx.x >> 4, n = (uint32_t)(threadIdx.x & 15) << (4 * i);
+        Sn[i][threadIdx.x & 15] = multmodp(kg, n);
+        SDn[i][threadIdx.x & 15] = a.crc_tile_step ? multmodp(a.crc_tile_step, n) : 0u;
+      }
+    } else {
+      S = T + 8;
+      SD = S + 4;
+      K = reinterpret_cast<uint32_t*>(SD + 4);
+      init_crc_tables(T);
+#pragma unroll
+      for (int b = 0; b < 4; b++) {
+        S[b][threadIdx.x] = multmodp(kg, (uint32_t)threadIdx.x << (8 * b));
+        SD[b][threadIdx.x] =
+            a.crc_tile_step ? multmodp(a.crc_tile_step, (uint32_t)threadIdx.x << (8 * b)) : 0u;
+      }
     }
     for (int i = threadIdx.x; i < a.fast_n; i += kBlock) K[i] = a.fast_tab[2 * a.fast_n + i];
     kb = x2nmodp((uint64_t)(4 * (24 - 8 * wave) * pitch + 112 - 16 * g), 3);
@@ -1790,21 +1831,36 @@ __global__ __launch_bounds__(kBlock) void tiles_group_kernel(ScatterArgs a) {
           st16s<(NT & 2) != 0>(base + (size_t)r * d_fs * 4, y);
           if constexpr (CRC && FLAGS) {  // encode: the stored vectors
             const v4u w = {y.x, y.y, y.z, y.w};
-            const uint32_t ck = crc_upd16_k(0u, w, T);
-            eacc = k ? crc_shift_k(eacc, S) ^ ck : ck;
+            if constexpr (LOW) {
+              const uint32_t ck = crc_upd16_s4(0u, w, T);
+              eacc = k ? crc_shift_n(eacc, Sn) ^ ck : ck;
+            } else {
+              const uint32_t ck = crc_upd16_k(0u, w, T);
+              eacc = k ? crc_shift_k(eacc, S) ^ ck : ck;
+            }
           }
         }
         if constexpr (CRC && !FLAGS) {  // decode: the loaded payload vectors, stores in flight
 #pragma unroll
           for (int k = 0; k < 8; k++) {
             const v4u w = {xc[k].x, xc[k].y, xc[k].z, xc[k].w};
-            const uint32_t ck = crc_upd16_k(0u, w, T);
-            eacc = k ? crc_shift_k(eacc, S) ^ ck : ck;
+            if constexpr (LOW) {
+              const uint32_t ck = crc_upd16_s4(0u, w, T);
+              eacc = k ? crc_shift_n(eacc, Sn) ^ ck : ck;
+            } else {
+              const uint32_t ck = crc_upd16_k(0u, w, T);
+              eacc = k ? crc_shift_k(eacc, S) ^ ck : ck;
+            }
           }
         }
         if constexpr (CRC) {
           if (regular) {
-            run = (ulast == ~0u ? 0u : crc_shift_k(run, SD)) ^ eacc;
+            uint32_t sh = 0;
+            if (ulast != ~0u) {
+              if constexpr (LOW) sh = crc_shift_n(run, SDn);
+              else sh = crc_shift_k(run, SD);
+            }
+            run = sh ^ eacc;
             ulast = u;
           } else {
             share ^= multmodp(K[u], eacc);
@@ -3565,6 +3621,18 @@ static bool launch_encode_fast_ds(const ScatterArgs& v, int grid, int deep, int 
           default: break;
         }
 #undef ZH_RC
+      }
+      if (group > 0 && v.crc_fused && (v.nt & 15) == 3 && deep == 40) {  // compact tables
+        const size_t lc = l + 4 * 256 * 4 + 2 * 8 * 16 * 4 + (size_t)v.fast_n * 4 + 16;
+        switch (group) {
+          case 1: hipLaunchKernelGGL((tiles_group_kernel<3, 1, true, false, true, true>), dim3(grid), dim3(kBlock), lc, s, v); return true;
+          case 2:
+            if (v.nt & 16) hipLaunchKernelGGL((tiles_group_kernel<1, 2, true, false, true, true>), dim3(grid), dim3(kBlock), lc, s, v);
+            else hipLaunchKernelGGL((tiles_group_kernel<3, 2, true, false, true, true>), dim3(grid), dim3(kBlock), lc, s, v);
+            return true;
+          case 4: hipLaunchKernelGGL((tiles_group_kernel<3, 4, true, false, true, true>), dim3(grid), dim3(kBlock), lc, s, v); return true;
+          default: break;
+        }
       }
       if (group > 0 && v.crc_fused && (v.nt & 15) == 3) {  // host: crc_tile_step for 8/G units
         const size_t lc = l + 16 * 256 * 4 + (size_t)v.fast_n * 4 + 64;  // + alignment
