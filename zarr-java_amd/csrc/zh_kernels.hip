@@ -2251,6 +2251,9 @@ void tiles_rowcrc_aln_kernel(ScatterArgs a) {
   const bool regular = a.crc_tile_step != 0;
   const uint32_t units = (uint32_t)a.fast_n, ys = (uint32_t)a.tile_ystride;
   const uint32_t kr = x2nmodp((uint64_t)(31 - r) * 4 * (uint64_t)s_fd, 3);
+  // units % 8 == 0 (host): every lane's last unit is units − 8 + tc in every chunk, so its
+  // two end multiplies (K of that unit, then kr) fold into one lane constant
+  const uint32_t kq = regular ? multmodp(kr, K[units - kTG + tc]) : 0u;
   auto sw = [](uint32_t v) { return SWAP ? __builtin_bswap32(v) : v; };
   auto rfl = [](uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); };
   for (int64_t gi = blockIdx.x; gi < a.n_citems; gi += gridDim.x) {
@@ -2377,8 +2380,7 @@ void tiles_rowcrc_aln_kernel(ScatterArgs a) {
       }
       sb = sb == 0 ? 8 : sb - 1;
     }
-    if (regular && ulast != ~0u) share = multmodp(K[ulast], run);
-    uint32_t cr = multmodp(kr, share);
+    uint32_t cr = regular ? multmodp(kq, run) : multmodp(kr, share);
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) cr ^= (uint32_t)__shfl_xor((int)cr, o, 64);
     if (lane == 0) atomicXor(a.crc_partials + c, cr);
