@@ -1181,6 +1181,38 @@ def oneshot_read(dev, A, meta, sources, shape, out, reps=3):
             "call": "zh_array_read (plan + execute + wait + teardown), device in/out"}
 
 
+def small_read(dev, A, meta, sources, coords, shape, out, reps=200):
+    """BASELINE configs[0]'s call shape (the reference's l4_sample read of a 1x64x64x64
+    region, ZarrV3Test.java:283-307) on this array's device-resident c4 shards: one-shot
+    zh_array_read (plan + execute + status + teardown, as core.Array.read does per call) of an
+    unaligned 64³ region (offset {0,3,517,501}: 27 inner chunks, most clipped, one shard and
+    its 512 KiB index crc32c), into device memory and into pageable host memory (a Java
+    array).  Median of `reps` after 20 warmups; both results verified against the generator."""
+    import statistics
+    off, shp = [0, 3, 517, 501], [1, 64, 64, 64]
+    pos = {c: i for i, c in enumerate(coords)}
+    src = [sources[pos[(0, 0, 0, 0)]]]
+    nb = 4 * 64 ** 3
+    host = (C.c_char * nb)()
+    res = {"region_offset": off, "region_shape": shp, "reps": reps}
+    for tag, dst, flags in (("device_out_us", out, A.ZH_SRC_DEVICE | A.ZH_OUT_DEVICE),
+                            ("pageable_host_out_us", C.addressof(host), A.ZH_SRC_DEVICE)):
+        ts = []
+        for i in range(reps + 20):
+            t0 = time.perf_counter()
+            dev.array_read(meta, src, off, shp, dst, flags)
+            if i >= 20:
+                ts.append(time.perf_counter() - t0)
+        res[tag] = round(statistics.median(ts) * 1e6, 1)
+        if dst != out:
+            dev.memcpy(out, dst, nb, 0, None, True)
+        bad = int(dev.synth_verify(out, shape, off, shp, 4, SEED))
+        if bad:
+            raise SystemExit(f"small read verification FAILED ({tag}): {bad}")
+    res["call"] = "zh_array_read one shot (plan + execute + status + teardown), device shard in"
+    return res
+
+
 # ------------------------------------------------------------------------------------------
 def main():
     ap = argparse.ArgumentParser()
@@ -1362,6 +1394,8 @@ def main():
         line["host_inclusive"] = hinc
     if not args.no_extras and ws == 1 and args.ydiv == 1 and args.config == "c4":
         line["oneshot_read"] = oneshot_read(dev, A, meta, sources, shape, out)
+        line["small_read"] = small_read(dev, A, meta, sources, coords, shape, out)
+        log(f"[rank {rank}] small read: {json.dumps(line['small_read'])}")
         plan.close()
         plan = None
         extras = {}

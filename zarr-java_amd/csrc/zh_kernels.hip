@@ -1762,6 +1762,13 @@ __global__ __launch_bounds__(kBlock) void tiles_group_kernel(ScatterArgs a) {
   __syncthreads();
   const bool regular = CRC && a.crc_tile_step != 0;
   const uint32_t units = (uint32_t)a.fast_n;
+  // regular fold: a lane's last unit is the same in every fast chunk (ti + a multiple of TG),
+  // so its two end multiplies (K of that unit, then kb) fold into one lane constant
+  uint32_t kq = 0;
+  if constexpr (CRC) {
+    const uint32_t til = (uint32_t)ti;
+    if (regular && til < units) kq = multmodp(kb, K[til + (units - 1 - til) / TG * TG]);
+  }
   const int64_t ngroups = (a.n_citems + G - 1) / G;
   const uint64_t qmask = (TG * 8 == 64 ? ~0ull : ((1ull << (TG * 8)) - 1)) << (q * TG * 8);
   const bool leader = lane == q * TG * 8;
@@ -1871,8 +1878,7 @@ __global__ __launch_bounds__(kBlock) void tiles_group_kernel(ScatterArgs a) {
     }
     if (FLAGS && (__ballot(differs) & qmask) != 0 && leader && on) a.flags[c] = 1;
     if constexpr (CRC) {
-      if (regular && ulast != ~0u) share = multmodp(K[ulast], run);
-      uint32_t cr = multmodp(kb, share);
+      uint32_t cr = regular ? (ulast != ~0u ? multmodp(kq, run) : 0u) : multmodp(kb, share);
 #pragma unroll
       for (int o = TG * 4; o > 0; o >>= 1) cr ^= (uint32_t)__shfl_xor((int)cr, o, 64);
       if (leader && on) atomicXor(a.crc_partials + c, cr);
