@@ -1181,7 +1181,7 @@ def oneshot_read(dev, A, meta, sources, shape, out, reps=3):
             "call": "zh_array_read (plan + execute + wait + teardown), device in/out"}
 
 
-def small_read(dev, A, meta, sources, coords, shape, out, reps=200):
+def small_read(dev, A, meta, sources, coords, shape, reps=200):
     """BASELINE configs[0]'s call shape (the reference's l4_sample read of a 1x64x64x64
     region, ZarrV3Test.java:283-307) on this array's device-resident c4 shards: one-shot
     zh_array_read (plan + execute + status + teardown, as core.Array.read does per call) of an
@@ -1194,6 +1194,7 @@ def small_read(dev, A, meta, sources, coords, shape, out, reps=200):
     src = [sources[pos[(0, 0, 0, 0)]]]
     nb = 4 * 64 ** 3
     host = (C.c_char * nb)()
+    out = dev.malloc(nb)  # its own buffer: the caller's `out` holds the decoded array, reused
     res = {"region_offset": off, "region_shape": shp, "reps": reps}
     for tag, dst, flags in (("device_out_us", out, A.ZH_SRC_DEVICE | A.ZH_OUT_DEVICE),
                             ("pageable_host_out_us", C.addressof(host), A.ZH_SRC_DEVICE)):
@@ -1209,6 +1210,7 @@ def small_read(dev, A, meta, sources, coords, shape, out, reps=200):
         bad = int(dev.synth_verify(out, shape, off, shp, 4, SEED))
         if bad:
             raise SystemExit(f"small read verification FAILED ({tag}): {bad}")
+    dev.free(out)
     res["call"] = "zh_array_read one shot (plan + execute + status + teardown), device shard in"
     return res
 
@@ -1394,7 +1396,7 @@ def main():
         line["host_inclusive"] = hinc
     if not args.no_extras and ws == 1 and args.ydiv == 1 and args.config == "c4":
         line["oneshot_read"] = oneshot_read(dev, A, meta, sources, shape, out)
-        line["small_read"] = small_read(dev, A, meta, sources, coords, shape, out)
+        line["small_read"] = small_read(dev, A, meta, sources, coords, shape)
         log(f"[rank {rank}] small read: {json.dumps(line['small_read'])}")
         plan.close()
         plan = None

@@ -1,0 +1,25 @@
+#!/bin/bash
+# Round 3: GPU tests and smoke, the default bench line (now with small_read), the c4crc and
+# c3crc decode and write lines with the current binary.
+set -u
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+OUT=$R/gpurun_out/r03j
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+step() {  # name, timeout, cmd...
+  local name=$1 t=$2; shift 2
+  echo "== $name: $*" >&2
+  timeout -k 10 "$t" "$@" > "$OUT/$name.out" 2> "$OUT/$name.err"
+  local rc=$?
+  echo "== $name rc=$rc" >&2
+  if [ $rc -ne 0 ]; then exit $rc; fi
+}
+cd "$R" || exit 1
+step pytest 600 python3 -u -m pytest tests -m gpu -x -q --timeout 170 --timeout-method thread
+step smoke 120 python3 -c "import __graft_entry__ as g; g.smoke()"
+step bench 600 python3 bench.py
+B="python3 bench.py --no-cpu-baseline --no-extras --no-host-inclusive"
+step c4crc_read 300 $B --config c4crc
+step c3crc_read 300 $B --config c3crc
+step c4crc_write 300 $B --config c4crc --op write --steps 5 --warmup 2
+step c3crc_write 300 $B --config c3crc --op write --steps 5 --warmup 2
