@@ -399,3 +399,19 @@ def test_tile_crc_encode_compact_tables(dev, monkeypatch, order, group, stnt):
     assert got == want
     path = lib().zh_debug_last_fast_path(1)
     assert path % 1000 == 40 and (path % 1000000) // 1000 == int(group)
+
+
+@pytest.mark.parametrize("group", ["1", "2", "4"])
+@pytest.mark.parametrize("stnt", ["0", "1"])
+def test_row_crc_encode_groups_and_store_policy(dev, monkeypatch, group, stnt):
+    """The row encode with the fused chunk CRC ([bytes(big), crc32c], no transpose) over 1, 2
+    and 4 chunks per work item, payloads stored through the cache or non-temporally:
+    byte-identical to the oracle's shards (an all-fill chunk elided, so later payloads shift)."""
+    monkeypatch.setenv("ZH_ENC_GROUP", group)
+    monkeypatch.setenv("ZH_ENC_CRC_STNT", stnt)
+    meta = _meta(None)
+    arr = rand_array(SHAPE, 4, seed=101)
+    arr[32:64, 0:32, 32:64] = 0
+    want = encode_oracle(meta, arr)
+    assert device_write(dev, meta, arr) == want
+    assert (lib().zh_debug_last_fast_path(1) % 1000000) // 1000 == int(group)

@@ -3568,12 +3568,18 @@ static bool launch_encode_fast_ds(const ScatterArgs& v, int grid, int deep, int 
     const size_t lc = lds + 12 * 256 * 4;  // + slicing tables T[8][256], shift table S[4][256]
     const bool cst = (v.nt & 16) != 0;     // cached stores (ZH_ENC_CRC_STNT=0)
     switch (group) {  // host: rows sequential in the payload, whole chunks (piece_shift 0)
-      case 1: hipLaunchKernelGGL((rows_group_kernel<DS, 1, 4, 3, true, true>), dim3(grid), dim3(kBlock), lc, s, v); return true;
+      case 1:
+        if (cst) hipLaunchKernelGGL((rows_group_kernel<DS, 1, 4, 1, true, true>), dim3(grid), dim3(kBlock), lc, s, v);
+        else hipLaunchKernelGGL((rows_group_kernel<DS, 1, 4, 3, true, true>), dim3(grid), dim3(kBlock), lc, s, v);
+        return true;
       case 2:
         if (cst) hipLaunchKernelGGL((rows_group_kernel<DS, 2, 4, 1, true, true>), dim3(grid), dim3(kBlock), lc, s, v);
         else hipLaunchKernelGGL((rows_group_kernel<DS, 2, 4, 3, true, true>), dim3(grid), dim3(kBlock), lc, s, v);
         return true;
-      case 4: hipLaunchKernelGGL((rows_group_kernel<DS, 4, 4, 3, true, true>), dim3(grid), dim3(kBlock), lc, s, v); return true;
+      case 4:
+        if (cst) hipLaunchKernelGGL((rows_group_kernel<DS, 4, 4, 1, true, true>), dim3(grid), dim3(kBlock), lc, s, v);
+        else hipLaunchKernelGGL((rows_group_kernel<DS, 4, 4, 3, true, true>), dim3(grid), dim3(kBlock), lc, s, v);
+        return true;
       default: break;
     }
   }
