@@ -39,7 +39,18 @@ struct zh_ctx {
   void* staging = nullptr;
   size_t staging_cap = 0;
   bool staging_oneoff = false;
+  // page-locked slots for the plans' status read-back (zh_plan_wait: one async copy on the
+  // plan's stream and one synchronise, instead of a synchronise and a blocking copy)
+  std::mutex status_mu;
+  uint64_t* status_pin = nullptr;  // kStatusSlots × kStatusSlotWords, created on first use
+  std::vector<int> status_free;
+  bool status_failed = false;
 };
+
+namespace zh {
+constexpr int kStatusSlots = 64;
+constexpr int kStatusSlotWords = 128;  // 32 shards × kStWords
+}  // namespace zh
 
 namespace zh {
 
@@ -72,6 +83,7 @@ struct zh_plan {
   uint8_t* d_tables = nullptr;   // one allocation holding the tables below
   zh::DevShard* d_shards = nullptr;
   uint64_t* d_status = nullptr;
+  int status_slot = -1;         // the context's page-locked status slot (−1: blocking copy)
   zh::CrcJob* d_crc_jobs = nullptr;
   uint32_t* d_crc_partials = nullptr;
   int64_t n_crc_jobs = 0, n_crc_spans = 0;

@@ -284,6 +284,7 @@ void zh_ctx_destroy(zh_ctx* c) {
   if (!c) return;
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamDestroy(c->stream);
+  if (c->status_pin) (void)hipHostFree(c->status_pin);
   if (c->wscratch) (void)hipFree(c->wscratch);
   for (auto& kv : c->cache) (void)hipFree(kv.second);
   pipeline_release(c);
@@ -770,6 +771,26 @@ int caller_pieces_all(const zh_array_meta* m, const SrcDesc& src, int64_t isz, c
   return ZH_OK;
 }
 
+// A page-locked status slot of the context for plans of at most 32 shards (−1: none; the plan
+// then reads its status back with a blocking copy).
+static int status_slot_take(zh_ctx* c, int64_t nshards) {
+  if (nshards * kStWords > kStatusSlotWords) return -1;
+  std::lock_guard<std::mutex> lk(c->status_mu);
+  if (!c->status_pin && !c->status_failed) {
+    void* h = nullptr;
+    if (hipHostMalloc(&h, (size_t)kStatusSlots * kStatusSlotWords * sizeof(uint64_t)) != hipSuccess) {
+      c->status_failed = true;
+      return -1;
+    }
+    c->status_pin = (uint64_t*)h;
+    for (int i = kStatusSlots - 1; i >= 0; i--) c->status_free.push_back(i);
+  }
+  if (c->status_free.empty()) return -1;
+  const int k = c->status_free.back();
+  c->status_free.pop_back();
+  return k;
+}
+
 void plan_free(zh_plan* p) {
   if (!p) return;
   (void)hipSetDevice(p->ctx->device);
@@ -777,6 +798,10 @@ void plan_free(zh_plan* p) {
   if (p->done_ev) {
     (void)hipEventSynchronize(p->done_ev);
     (void)hipEventDestroy(p->done_ev);
+  }
+  if (p->status_slot >= 0) {  // after done_ev: a status copy of the plan may still be queued
+    std::lock_guard<std::mutex> lk(p->ctx->status_mu);
+    p->ctx->status_free.push_back(p->status_slot);
   }
   for (auto& b : p->blocks) ctx_release(p->ctx, b.first, b.second);
   for (auto& e : p->ev_pending)
@@ -1423,11 +1448,22 @@ int zh_plan_set_graph(zh_plan* p, int enable) {
 int zh_plan_wait(zh_plan* p, char* err, size_t errlen) {
   if (!p) return ZH_EINVAL;
   (void)hipSetDevice(p->ctx->device);
-  if (p->last_stream) ZH_HIP(hipStreamSynchronize(p->last_stream));
   std::vector<uint64_t> stv((size_t)p->nshards * kStWords);
-  if (!stv.empty())
-    ZH_HIP(hipMemcpy(stv.data(), p->d_status, stv.size() * sizeof(uint64_t),
-                     hipMemcpyDeviceToHost));
+  if (p->status_slot < 0 && p->last_stream && !stv.empty())
+    p->status_slot = status_slot_take(p->ctx, p->nshards);
+  if (p->status_slot >= 0 && p->last_stream && !stv.empty()) {
+    // the status copy rides on the plan's stream behind its kernels: one synchronise
+    uint64_t* h = p->ctx->status_pin + (size_t)p->status_slot * kStatusSlotWords;
+    ZH_HIP(hipMemcpyAsync(h, p->d_status, stv.size() * sizeof(uint64_t), hipMemcpyDeviceToHost,
+                          p->last_stream));
+    ZH_HIP(hipStreamSynchronize(p->last_stream));
+    std::copy(h, h + stv.size(), stv.begin());
+  } else {
+    if (p->last_stream) ZH_HIP(hipStreamSynchronize(p->last_stream));
+    if (!stv.empty())
+      ZH_HIP(hipMemcpy(stv.data(), p->d_status, stv.size() * sizeof(uint64_t),
+                       hipMemcpyDeviceToHost));
+  }
   const int n = p->meta.ndim;
   for (int64_t i = 0; i < p->nshards; i++) {
     const uint64_t* w = &stv[i * kStWords];
