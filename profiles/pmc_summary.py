@@ -14,6 +14,13 @@ import os
 import sys
 
 
+def flags_arg(n):
+    """The FLAGS template argument of a fast kernel's name: the last one, except
+    tiles_group_kernel<NT, G, CRC, PF, FLAGS, LOW> (round 3 added LOW after it)."""
+    args = [a.strip() for a in n.split("<", 1)[-1].split(">")[0].split(",")]
+    return args[4] if "tiles_group_kernel" in n and len(args) > 5 else args[-1]
+
+
 def kernel_rows(path, match):
     rows = []
     for r in csv.DictReader(open(path)):
@@ -31,7 +38,7 @@ DECODE_ONLY = ("tiles_rowcrc_kernel", "tiles_crcw_kernel", "tiles_rowcrc_aln_ker
 def main(src, config, out):
     def encode_view(n):  # the bench's setup encode runs the fast kernels with FLAGS = true
         return any(k in n for k in FAST) and not any(k in n for k in DECODE_ONLY) and \
-            n.split(">")[0].split(",")[-1].strip() == "true"
+            flags_arg(n) == "true"
 
     def decode(n):  # every decode kernel of one step: fast rows/tiles + the generic list
         return any(k in n for k in FAST + ("decode_slow_kernel",)) and not encode_view(n)

@@ -1143,8 +1143,8 @@ int plan_create(zh_ctx* ctx, const zh_array_meta* m, const SrcDesc* srcs, int64_
     const size_t o_pieces = carve(dpieces.size() * sizeof(DevPiece));
     const size_t up = off;  // uploaded prefix
     const size_t o_status = carve((size_t)ncoords * kStWords * 8);
+    const size_t o_slow = carve(((size_t)items + 4) * 4);  // right after the status: one memset
     const size_t o_desc = carve((size_t)items * sizeof(ItemDesc));
-    const size_t o_slow = carve(((size_t)items + 4) * 4);
     if ((st = plan_alloc(p, &p->d_tables, off, err, errlen)) != ZH_OK) {
       plan_free(p);
       return st;
@@ -1327,8 +1327,9 @@ int plan_enqueue_impl(zh_plan* p, void* out, hipStream_t s) {
   for (size_t k = 0; !p->external_h2d && k < p->h2d.size(); k++)
     ZH_HIP(hipMemcpyAsync(p->d_input + p->h2d[k].first, p->h2d[k].second, (size_t)p->h2d_len[k],
                           hipMemcpyHostToDevice, s));
-  ZH_HIP(hipMemsetAsync(p->d_status, 0, (size_t)p->nshards * kStWords * sizeof(uint64_t), s));
-  ZH_HIP(hipMemsetAsync(p->d_slow, 0, sizeof(uint32_t), s));
+  // the status words and the slow-list count (carved adjacent in the plan's tables)
+  ZH_HIP(hipMemsetAsync(p->d_status, 0,
+                        (size_t)((uint8_t*)p->d_slow - (uint8_t*)p->d_status) + sizeof(uint32_t), s));
   std::array<hipEvent_t, 3> ev{};
   if (p->timing) {
     for (int k = 0; k < 3; k++) {
