@@ -383,12 +383,14 @@ def test_plain_chains_64mib_defaults(dev, monkeypatch, order):
 @pytest.mark.parametrize("order", [[0, 2, 1], [2, 1, 0], [1, 2, 0]])
 @pytest.mark.parametrize("group", ["1", "2", "4"])
 @pytest.mark.parametrize("stnt", ["0", "1"])
-def test_tile_crc_encode_compact_tables(dev, monkeypatch, order, group, stnt):
+@pytest.mark.parametrize("tabs", ["ZH_ENC_CRCLOW", "ZH_ENC_CRCFIELD"])
+def test_tile_crc_encode_compact_tables(dev, monkeypatch, order, group, stnt, tabs):
     """The tile encode with the fused chunk CRC over compact tables (ZH_ENC_CRCLOW=1:
-    slicing-by-4 and nibble shift tables, 4 workgroups per CU): byte-identical to the oracle's
-    shards (an all-fill chunk elided, so the later payloads shift), for 1, 2 and 4 chunks per
-    work item and both store policies, and the kernel that ran is that variant (deep 40)."""
-    monkeypatch.setenv("ZH_ENC_CRCLOW", "1")
+    slicing-by-4 and nibble shift tables; ZH_ENC_CRCFIELD=1: conflict-free 5/4-bit field
+    tables; both 4 workgroups per CU): byte-identical to the oracle's shards (an all-fill chunk
+    elided, so the later payloads shift), for 1, 2 and 4 chunks per work item and both store
+    policies, and the kernel that ran is that variant (deep 40 / 41)."""
+    monkeypatch.setenv(tabs, "1")
     monkeypatch.setenv("ZH_ENC_TGROUP", group)
     monkeypatch.setenv("ZH_ENC_CRC_STNT", stnt)
     meta = _meta(order)
@@ -398,7 +400,8 @@ def test_tile_crc_encode_compact_tables(dev, monkeypatch, order, group, stnt):
     got = device_write(dev, meta, arr)
     assert got == want
     path = lib().zh_debug_last_fast_path(1)
-    assert path % 1000 == 40 and (path % 1000000) // 1000 == int(group)
+    assert path % 1000 == (41 if tabs == "ZH_ENC_CRCFIELD" else 40)
+    assert (path % 1000000) // 1000 == int(group)
 
 
 @pytest.mark.parametrize("group", ["1", "2", "4"])

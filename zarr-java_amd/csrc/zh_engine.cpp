@@ -2427,7 +2427,8 @@ static int array_write_fast(zh_ctx* ctx, const zh_array_meta* m, ScatterArgs a,
                    : enc_aln ? (env_int("ZH_ENC_ALIGN_PF", 1) ? 31 : 32)
                    : enc_rowcrc ? 30
                    : v.fast_mode == kFastTileTable && group && crc_fuse && tile_crc &&
-                             env_int("ZH_ENC_CRCLOW", 0) ? 40  // compact CRC tables, 4 WG/CU
+                             (env_int("ZH_ENC_CRCLOW", 0) || env_int("ZH_ENC_CRCFIELD", 0))
+                       ? (env_int("ZH_ENC_CRCFIELD", 0) ? 41 : 40)  // field / compact CRC tables
                    : v.fast_mode == kFastTileTable && group ? (env_int("ZH_ENC_TPF", 0) ? 9 : 1)
                    : group ? (gu <= 2 ? 0 : gu <= 4 ? 1 : 2)
                            : env_int("ZH_ENC_DEEP", 1);

@@ -916,7 +916,13 @@ struct CrcTabs {
   uint32_t kfull[256];
   uint32_t kspan;
   uint32_t kidx[256];  // x^(8·kIdxSpan·j): span j of an index shifted past j later spans
+  // field tables (conflict-free lookups, tiles_group_kernel TABS = 2): F[j][f][v] =
+  // upd16(0, a 16-B vector whose word j is v << kFieldOff[f], the rest 0); fields of 5 bits
+  // (32 entries: 32 banks) and 4 bits (16 entries, padded to 32)
+  uint32_t F[4][7][32];
 };
+constexpr int kFieldOff[7] = {0, 5, 10, 15, 20, 24, 28};
+constexpr int kFieldLen[7] = {5, 5, 5, 5, 4, 4, 4};
 
 constexpr uint32_t cx_mult(uint32_t a, uint32_t b) {  // a(x)·b(x) mod P, reflected
   uint32_t p = 0;
@@ -956,6 +962,17 @@ constexpr CrcTabs make_crc_tabs() {
   const uint32_t ki = cx_xpow8n(kIdxSpan);
   t.kidx[0] = 1u << 31;
   for (int j = 1; j < 256; j++) t.kidx[j] = cx_mult(ki, t.kidx[j - 1]);
+  for (int j = 0; j < 4; j++)
+    for (int f = 0; f < 7; f++)
+      for (uint32_t v = 0; v < 32; v++) {
+        const uint32_t w = v < (1u << kFieldLen[f]) ? v << kFieldOff[f] : 0u;
+        uint32_t c = 0;
+        for (int k = 0; k < 16; k++) {  // the vector's bytes in memory order
+          const uint32_t b = k / 4 == j ? (w >> (8 * (k % 4))) & 0xFFu : 0u;
+          c = t.T[0][(c ^ b) & 0xFFu] ^ (c >> 8);
+        }
+        t.F[j][f][v] = c;
+      }
   return t;
 }
 
@@ -1253,6 +1270,37 @@ __device__ __forceinline__ uint32_t crc_shift_n(uint32_t c, const uint32_t (*Sn)
     return *reinterpret_cast<const uint32_t*>(reinterpret_cast<const uint8_t*>(Sn[i]) + off);
   };
   return xor3(at(0), at(1), at(2)) ^ xor3(at(3), at(4), at(5)) ^ (at(6) ^ at(7));
+}
+
+// Field tables (TABS = 2 in tiles_group_kernel): every lookup indexes a table of at most 32
+// consecutive words, so the 32 lanes of a ds_read_b32 group hit distinct banks or the same
+// address (broadcast): no bank conflicts, where random byte indices into 256-entry tables
+// cost ≈2.4 LDS cycles per group.  28 lookups per 16-B vector (7 fields per word) and 7 per
+// shift, against 16 + 4 conflicting ones.  Table f of word j at byte 128·(7j + f).
+template <int F>
+__device__ __forceinline__ uint32_t field_off4(uint32_t w) {  // 4 · field F of w
+  constexpr int o = kFieldOff[F];
+  constexpr uint32_t m = ((1u << kFieldLen[F]) - 1) << 2;
+  if constexpr (o >= 2) return (w >> (o - 2)) & m;
+  else return (w << (2 - o)) & m;
+}
+__device__ __forceinline__ uint32_t fld(const uint8_t* tabs, int t, uint32_t off4) {
+  return *reinterpret_cast<const uint32_t*>(tabs + 128 * t + off4);
+}
+__device__ __forceinline__ uint32_t crc_word_fields(const uint8_t* tabs, int j, uint32_t w) {
+  const int b = 7 * j;
+  return xor3(fld(tabs, b + 0, field_off4<0>(w)), fld(tabs, b + 1, field_off4<1>(w)),
+              fld(tabs, b + 2, field_off4<2>(w))) ^
+         xor3(fld(tabs, b + 3, field_off4<3>(w)), fld(tabs, b + 4, field_off4<4>(w)),
+              fld(tabs, b + 5, field_off4<5>(w))) ^
+         fld(tabs, b + 6, field_off4<6>(w));
+}
+__device__ __forceinline__ uint32_t crc_upd16_f(v4u v, const uint8_t* F) {  // upd16(0, v)
+  return xor3(crc_word_fields(F, 0, v.x), crc_word_fields(F, 1, v.y), crc_word_fields(F, 2, v.z)) ^
+         crc_word_fields(F, 3, v.w);
+}
+__device__ __forceinline__ uint32_t crc_shift_f(uint32_t c, const uint8_t* Sf) {  // c · k
+  return crc_word_fields(Sf, 0, c);
 }
 
 // encode, grouped row kernel (write path, narrow rows): a work item is G consecutive inner
@@ -1702,15 +1750,19 @@ __global__ __launch_bounds__(kBlock) void decode_tiles_kernel(ScatterArgs a) {
 //
 // PF: the next step's loads are issued before this step's stores (decode_tiles_body's order).
 //
-// LOW (CRC only): compact tables (crc_upd16_s4 / crc_shift_n: T[4][256], Sn[8][16], SDn[8][16],
-// 5 KiB instead of 16 KiB), so that tiles + tables fit 4 workgroups per CU (39.3 KB each;
-// 50.5 KB with the byte tables holds the kernel at 3); 7 more lookups per 8 vectors.
-template <int NT, int G, bool CRC, bool PF, bool FLAGS, bool LOW = false>
+// TABS (CRC only): 0 the byte tables (T[8][256], S[4][256], SD[4][256]: 16 KiB);
+// 1 compact tables (crc_upd16_s4 / crc_shift_n: T[4][256], Sn[8][16], SDn[8][16], 5 KiB, so
+// that tiles + tables fit 4 workgroups per CU: 39.3 KB each, 50.5 KB with the byte tables);
+// 2 field tables (crc_upd16_f / crc_shift_f: F[4][7][32], Sf[7][32], SDf[7][32], 5.25 KiB, no
+// bank conflicts, 4 workgroups per CU).
+template <int NT, int G, bool CRC, bool PF, bool FLAGS, int TABS = 0>
 __global__ __launch_bounds__(kBlock) void tiles_group_kernel(ScatterArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   // CRC: the tables first (T, S, SD: a constant LDS position for crc_upd16_k / crc_shift_k),
   // then K, the unit table and the tiles
-  constexpr size_t kTabBytes = LOW ? 4 * 256 * 4 + 2 * 8 * 16 * 4 : 16 * 256 * 4;
+  constexpr bool LOW = TABS == 1, FLD = TABS == 2;
+  constexpr size_t kTabBytes = LOW ? 4 * 256 * 4 + 2 * 8 * 16 * 4
+                               : FLD ? (28 + 7 + 7) * 128 : 16 * 256 * 4;
   uint8_t* tab_at = CRC ? smem + ((kTabBytes + (size_t)a.fast_n * 4 + 15) & ~(size_t)15) : smem;
   uint2* tab = reinterpret_cast<uint2*>(tab_at);
   uint8_t* after_tab = tab_at + (((size_t)a.fast_n * 8 + 15) & ~(size_t)15);
@@ -1726,6 +1778,9 @@ __global__ __launch_bounds__(kBlock) void tiles_group_kernel(ScatterArgs a) {
   uint32_t(*SD)[256] = nullptr;
   uint32_t(*Sn)[16] = nullptr;  // LOW
   uint32_t(*SDn)[16] = nullptr;
+  const uint8_t* Ff = smem;      // FLD: F at 0, Sf at 3584, SDf at 4480
+  const uint8_t* Sf = smem + 28 * 128;
+  const uint8_t* SDf = smem + 35 * 128;
   uint32_t* K = nullptr;
   uint32_t kb = 0;
   if constexpr (CRC) {
@@ -1733,7 +1788,18 @@ __global__ __launch_bounds__(kBlock) void tiles_group_kernel(ScatterArgs a) {
     // payload row pitch of the lane's vectors: the stored rows (encode) or the loaded rows
     const int64_t pitch = FLAGS ? d_fs : s_fd;
     const uint32_t kg = x2nmodp((uint64_t)(4 * pitch), 3);
-    if constexpr (LOW) {
+    if constexpr (FLD) {
+      uint32_t* fw = reinterpret_cast<uint32_t*>(smem);
+      for (int i = threadIdx.x; i < 28 * 32; i += kBlock) fw[i] = (&g_crc.F[0][0][0])[i];
+      if (threadIdx.x < 7 * 32) {
+        const int f = threadIdx.x >> 5;
+        const uint32_t v = threadIdx.x & 31;
+        const uint32_t n = v < (1u << kFieldLen[f]) ? v << kFieldOff[f] : 0u;
+        fw[28 * 32 + threadIdx.x] = multmodp(kg, n);
+        fw[35 * 32 + threadIdx.x] = a.crc_tile_step ? multmodp(a.crc_tile_step, n) : 0u;
+      }
+      K = fw + 42 * 32;
+    } else if constexpr (LOW) {
       Sn = reinterpret_cast<uint32_t(*)[16]>(smem + 4 * 256 * 4);
       SDn = Sn + 8;
       K = reinterpret_cast<uint32_t*>(SDn + 8);
@@ -1838,7 +1904,10 @@ __global__ __launch_bounds__(kBlock) void tiles_group_kernel(ScatterArgs a) {
           st16s<(NT & 2) != 0>(base + (size_t)r * d_fs * 4, y);
           if constexpr (CRC && FLAGS) {  // encode: the stored vectors
             const v4u w = {y.x, y.y, y.z, y.w};
-            if constexpr (LOW) {
+            if constexpr (FLD) {
+              const uint32_t ck = crc_upd16_f(w, Ff);
+              eacc = k ? crc_shift_f(eacc, Sf) ^ ck : ck;
+            } else if constexpr (LOW) {
               const uint32_t ck = crc_upd16_s4(0u, w, T);
               eacc = k ? crc_shift_n(eacc, Sn) ^ ck : ck;
             } else {
@@ -1851,7 +1920,10 @@ __global__ __launch_bounds__(kBlock) void tiles_group_kernel(ScatterArgs a) {
 #pragma unroll
           for (int k = 0; k < 8; k++) {
             const v4u w = {xc[k].x, xc[k].y, xc[k].z, xc[k].w};
-            if constexpr (LOW) {
+            if constexpr (FLD) {
+              const uint32_t ck = crc_upd16_f(w, Ff);
+              eacc = k ? crc_shift_f(eacc, Sf) ^ ck : ck;
+            } else if constexpr (LOW) {
               const uint32_t ck = crc_upd16_s4(0u, w, T);
               eacc = k ? crc_shift_n(eacc, Sn) ^ ck : ck;
             } else {
@@ -1864,7 +1936,8 @@ __global__ __launch_bounds__(kBlock) void tiles_group_kernel(ScatterArgs a) {
           if (regular) {
             uint32_t sh = 0;
             if (ulast != ~0u) {
-              if constexpr (LOW) sh = crc_shift_n(run, SDn);
+              if constexpr (FLD) sh = crc_shift_f(run, SDf);
+              else if constexpr (LOW) sh = crc_shift_n(run, SDn);
               else sh = crc_shift_k(run, SD);
             }
             run = sh ^ eacc;
@@ -3639,12 +3712,24 @@ static bool launch_encode_fast_ds(const ScatterArgs& v, int grid, int deep, int 
       if (group > 0 && v.crc_fused && (v.nt & 15) == 3 && deep == 40) {  // compact tables
         const size_t lc = l + 4 * 256 * 4 + 2 * 8 * 16 * 4 + (size_t)v.fast_n * 4 + 16;
         switch (group) {
-          case 1: hipLaunchKernelGGL((tiles_group_kernel<3, 1, true, false, true, true>), dim3(grid), dim3(kBlock), lc, s, v); return true;
+          case 1: hipLaunchKernelGGL((tiles_group_kernel<3, 1, true, false, true, 1>), dim3(grid), dim3(kBlock), lc, s, v); return true;
           case 2:
-            if (v.nt & 16) hipLaunchKernelGGL((tiles_group_kernel<1, 2, true, false, true, true>), dim3(grid), dim3(kBlock), lc, s, v);
-            else hipLaunchKernelGGL((tiles_group_kernel<3, 2, true, false, true, true>), dim3(grid), dim3(kBlock), lc, s, v);
+            if (v.nt & 16) hipLaunchKernelGGL((tiles_group_kernel<1, 2, true, false, true, 1>), dim3(grid), dim3(kBlock), lc, s, v);
+            else hipLaunchKernelGGL((tiles_group_kernel<3, 2, true, false, true, 1>), dim3(grid), dim3(kBlock), lc, s, v);
             return true;
-          case 4: hipLaunchKernelGGL((tiles_group_kernel<3, 4, true, false, true, true>), dim3(grid), dim3(kBlock), lc, s, v); return true;
+          case 4: hipLaunchKernelGGL((tiles_group_kernel<3, 4, true, false, true, 1>), dim3(grid), dim3(kBlock), lc, s, v); return true;
+          default: break;
+        }
+      }
+      if (group > 0 && v.crc_fused && (v.nt & 15) == 3 && deep == 41) {  // field tables
+        const size_t lc = l + 42 * 128 + (size_t)v.fast_n * 4 + 16;
+        switch (group) {
+          case 1: hipLaunchKernelGGL((tiles_group_kernel<3, 1, true, false, true, 2>), dim3(grid), dim3(kBlock), lc, s, v); return true;
+          case 2:
+            if (v.nt & 16) hipLaunchKernelGGL((tiles_group_kernel<1, 2, true, false, true, 2>), dim3(grid), dim3(kBlock), lc, s, v);
+            else hipLaunchKernelGGL((tiles_group_kernel<3, 2, true, false, true, 2>), dim3(grid), dim3(kBlock), lc, s, v);
+            return true;
+          case 4: hipLaunchKernelGGL((tiles_group_kernel<3, 4, true, false, true, 2>), dim3(grid), dim3(kBlock), lc, s, v); return true;
           default: break;
         }
       }
