@@ -240,7 +240,8 @@ def _aligned():
 
 @pytest.mark.parametrize("nb", [16, 24, 32])
 @pytest.mark.parametrize("endian", [A.ZH_ENDIAN_BIG, A.ZH_ENDIAN_LITTLE])
-def test_row_crc_aligned_windows(dev, monkeypatch, nb, endian):
+@pytest.mark.parametrize("field", ["0", "1"])
+def test_row_crc_aligned_windows(dev, monkeypatch, nb, endian, field):
     """tiles_rowcrc_aln_kernel: inner chunks [32, nb, 32] under transpose [2, 1, 0] store
     [32 rows][nb units][32 words] (c4's layout), so the movers load 128-B aligned lines and
     carry each step's last line into the next step's tile through a ring of 9 LDS slots.  One
@@ -253,6 +254,7 @@ def test_row_crc_aligned_windows(dev, monkeypatch, nb, endian):
         monkeypatch.delenv(k, raising=False)
     monkeypatch.setenv("ZH_SMALL_SPLIT", "0")
     monkeypatch.setenv("ZH_DEC_ALIGN", "1")
+    monkeypatch.setenv("ZH_DEC_CRCFIELD", field)  # 1: the row CRC over field tables
     shape = [64, 6 * nb, 96]
     meta = A.make_meta(shape, shape, 4, endian=endian, sharded=True,
                        inner_chunk_shape=[32, nb, 32], transpose_order=[2, 1, 0],
@@ -264,7 +266,7 @@ def test_row_crc_aligned_windows(dev, monkeypatch, nb, endian):
     got, want = _read_both_shape(dev, meta, shards, shape)
     np.testing.assert_array_equal(got, want)
     np.testing.assert_array_equal(got, arr)
-    assert _variant() == 51 and _aligned() == 1
+    assert _variant() == 51 and _aligned() == 1 + int(field)
     off, shp = [3, 5, 7], [58, 6 * nb - 9, 80]
     sel = np.frombuffer(O.array_read(meta, shards, off, shp), np.uint32).reshape(shp)
     np.testing.assert_array_equal(device_read(dev, meta, shards, off, shp), sel)

@@ -1282,7 +1282,8 @@ int plan_create(zh_ctx* ctx, const zh_array_meta* m, const SrcDesc* srcs, int64_
         for (int64_t u = 0; al && u < nu; u++)
           al = tab[2 * (size_t)u] == (uint32_t)(32 * u) &&
                tab[2 * (size_t)u + 1] == (uint64_t)u * ys && 4 * (uint64_t)u * ys + 128 <= 0xFFFFFFFFull;
-        p->args.tile_align = al ? 1 : 0;
+        // 2: the row CRC over conflict-free field tables (ZH_DEC_CRCFIELD=1, A/B lab)
+        p->args.tile_align = al ? (env_int("ZH_DEC_CRCFIELD", 0) ? 2 : 1) : 0;
         p->args.tile_ystride = al ? (int64_t)ys : 0;
       }
       if (crc) p->args.crc_tile_step = tile_crc_step(ends, (size_t)(8 / G));

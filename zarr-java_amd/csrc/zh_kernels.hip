@@ -920,6 +920,9 @@ struct CrcTabs {
   // upd16(0, a 16-B vector whose word j is v << kFieldOff[f], the rest 0); fields of 5 bits
   // (32 entries: 32 banks) and 4 bits (16 entries, padded to 32)
   uint32_t F[4][7][32];
+  // the same for the serial 8-byte update of the row-CRC kernels (TABS = 2 / ZH_DEC_CRCFIELD):
+  // F8[i][f][v] = the register after 8 bytes from 0 whose word i is v << kFieldOff[f]
+  uint32_t F8[2][7][32];
 };
 constexpr int kFieldOff[7] = {0, 5, 10, 15, 20, 24, 28};
 constexpr int kFieldLen[7] = {5, 5, 5, 5, 4, 4, 4};
@@ -972,6 +975,17 @@ constexpr CrcTabs make_crc_tabs() {
           c = t.T[0][(c ^ b) & 0xFFu] ^ (c >> 8);
         }
         t.F[j][f][v] = c;
+      }
+  for (int j = 0; j < 2; j++)
+    for (int f = 0; f < 7; f++)
+      for (uint32_t v = 0; v < 32; v++) {
+        const uint32_t w = v < (1u << kFieldLen[f]) ? v << kFieldOff[f] : 0u;
+        uint32_t c = 0;
+        for (int k = 0; k < 8; k++) {
+          const uint32_t b = k / 4 == j ? (w >> (8 * (k % 4))) & 0xFFu : 0u;
+          c = t.T[0][(c ^ b) & 0xFFu] ^ (c >> 8);
+        }
+        t.F8[j][f][v] = c;
       }
   return t;
 }
@@ -2133,6 +2147,20 @@ __device__ __forceinline__ uint32_t crc_upd8_lds(uint32_t c, uint32_t w0, uint32
   return xor3(a0, a1, a2);
 }
 
+// The same 8-byte step over conflict-free field tables F8 at LDS offset 0 (table f of word i at
+// byte 128·(7i + f); 14 lookups, no bank conflicts).  w0, w1 are raw payload words and c the
+// plain (unswapped) register.
+__device__ __forceinline__ uint32_t crc_word_fields_lds(int b, uint32_t w) {
+  return xor3(lds_word(128 * (b + 0) + field_off4<0>(w)), lds_word(128 * (b + 1) + field_off4<1>(w)),
+              lds_word(128 * (b + 2) + field_off4<2>(w))) ^
+         xor3(lds_word(128 * (b + 3) + field_off4<3>(w)), lds_word(128 * (b + 4) + field_off4<4>(w)),
+              lds_word(128 * (b + 5) + field_off4<5>(w))) ^
+         lds_word(128 * (b + 6) + field_off4<6>(w));
+}
+__device__ __forceinline__ uint32_t crc_upd8_fld(uint32_t c, uint32_t w0, uint32_t w1) {
+  return crc_word_fields_lds(0, w0 ^ c) ^ crc_word_fields_lds(7, w1);
+}
+
 // decode, grouped tile kernel with the chunk CRC over LDS rows (ZH_DEC_CRCW=3).  The kernel
 // must have no static LDS, since its tables are addressed from LDS offset 0: the host selects it
 // only when rowcrc_lds_at_zero() confirms that for every instantiation.  The lanes
@@ -2306,7 +2334,10 @@ void tiles_rowcrc_kernel(ScatterArgs a) {
 // 50 852 B, 3 workgroups per CU (54 436 B, with byte tables, ran 2 per CU: 42.4 vs 36.4 ms, the
 // same as the unaligned kernel padded to that size, profiles/r03/occ).  Every lane reads the
 // same descriptor (G = 1): the skip is block-uniform.
-template <bool SWAP>
+//
+// FLD (ZH_DEC_CRCFIELD=1, a.tile_align == 2): the row CRC over the conflict-free field tables
+// F8 (crc_upd8_fld: 14 lookups per 8 bytes, no bank conflicts) on raw words, in the T area.
+template <bool SWAP, bool FLD = false>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3)))
 void tiles_rowcrc_aln_kernel(ScatterArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
@@ -2316,8 +2347,13 @@ void tiles_rowcrc_aln_kernel(ScatterArgs a) {
   uint32_t(*SDn)[16] = reinterpret_cast<uint32_t(*)[16]>(smem + 12288);
   uint32_t* const lds = reinterpret_cast<uint32_t*>(smem + 12800);
   const int tid = threadIdx.x;
+  if constexpr (FLD) {
+    for (int i = tid; i < 2 * 7 * 32; i += kBlock)
+      reinterpret_cast<uint32_t*>(smem)[i] = (&g_crc.F8[0][0][0])[i];
+  } else {
 #pragma unroll
-  for (int k = 0; k < 8; k++) T[k][tid] = SWAP ? __builtin_bswap32(g_crc.T[k][tid]) : g_crc.T[k][tid];
+    for (int k = 0; k < 8; k++) T[k][tid] = SWAP ? __builtin_bswap32(g_crc.T[k][tid]) : g_crc.T[k][tid];
+  }
   if (tid < 128)
     SDn[tid >> 4][tid & 15] =
         a.crc_tile_step ? multmodp(a.crc_tile_step, (uint32_t)(tid & 15) << (4 * (tid >> 4))) : 0u;
@@ -2443,10 +2479,17 @@ void tiles_rowcrc_aln_kernel(ScatterArgs a) {
         for (int j = 0; j < 32; j++) w[j] = crow[j];
       }
       __syncthreads();
-      uint32_t acc = 0;  // byte-swapped with SWAP
+      uint32_t acc = 0;  // byte-swapped with SWAP (byte tables)
+      if constexpr (FLD) {
 #pragma unroll
-      for (int j = 0; j < 32; j += 2) acc = crc_upd8_lds<SWAP>(acc, w[j], w[j + 1]);
-      if (SWAP) acc = __builtin_bswap32(acc);
+        for (int j = 0; j < 32; j += 2)
+          acc = crc_upd8_fld(acc, SWAP ? __builtin_bswap32(w[j]) : w[j],
+                             SWAP ? __builtin_bswap32(w[j + 1]) : w[j + 1]);
+      } else {
+#pragma unroll
+        for (int j = 0; j < 32; j += 2) acc = crc_upd8_lds<SWAP>(acc, w[j], w[j + 1]);
+        if (SWAP) acc = __builtin_bswap32(acc);
+      }
       const uint32_t uc = ub + tc;
       if (regular) {
         uint32_t sh = 0;  // run · x^(8Δ), nibble by nibble
@@ -3458,6 +3501,11 @@ static void launch_scatter_ds(const ScatterArgs& a, int tile, int enc, int grid,
             case 21:
               if (a.tile_align) {  // LDS: tables 12.5 KiB + 9 slots (the host checked the rest)
                 const size_t la = 12800 + (size_t)9 * kTilePitch * 4;
+                if (a.tile_align == 2) {  // field tables (ZH_DEC_CRCFIELD)
+                  if (a.swap) hipLaunchKernelGGL((tiles_rowcrc_aln_kernel<true, true>), dim3(grid), dim3(kBlock), la, s, a);
+                  else hipLaunchKernelGGL((tiles_rowcrc_aln_kernel<false, true>), dim3(grid), dim3(kBlock), la, s, a);
+                  return;
+                }
                 if (a.swap) hipLaunchKernelGGL((tiles_rowcrc_aln_kernel<true>), dim3(grid), dim3(kBlock), la, s, a);
                 else hipLaunchKernelGGL((tiles_rowcrc_aln_kernel<false>), dim3(grid), dim3(kBlock), la, s, a);
                 return;
@@ -3575,6 +3623,8 @@ bool rowcrc_lds_at_zero() {
                          (const void*)tiles_rowcrc_kernel<4, false, true>, (const void*)tiles_rowcrc_kernel<4, true, true>,
                          (const void*)tiles_rowcrc_aln_kernel<false>,
                          (const void*)tiles_rowcrc_aln_kernel<true>,
+                         (const void*)tiles_rowcrc_aln_kernel<false, true>,
+                         (const void*)tiles_rowcrc_aln_kernel<true, true>,
                          (const void*)tiles_rowcrc_enc_aln_kernel<false, true>,
                          (const void*)tiles_rowcrc_enc_aln_kernel<true, true>,
                          (const void*)tiles_rowcrc_enc_aln_kernel<false, false>,
