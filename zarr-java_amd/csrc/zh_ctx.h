@@ -45,11 +45,18 @@ struct zh_ctx {
   uint64_t* status_pin = nullptr;  // kStatusSlots × kStatusSlotWords, created on first use
   std::vector<int> status_free;
   bool status_failed = false;
+  // page-locked slots for small plans' table uploads (deferred to the first execute as an
+  // async copy on its stream, instead of a blocking pageable copy at plan creation)
+  uint8_t* upload_pin = nullptr;   // kUploadSlots × kUploadSlotBytes, created on first use
+  std::vector<int> upload_free;
+  bool upload_failed = false;
 };
 
 namespace zh {
 constexpr int kStatusSlots = 64;
 constexpr int kStatusSlotWords = 128;  // 32 shards × kStWords
+constexpr int kUploadSlots = 16;
+constexpr size_t kUploadSlotBytes = 64 << 10;
 }  // namespace zh
 
 namespace zh {
@@ -84,6 +91,9 @@ struct zh_plan {
   zh::DevShard* d_shards = nullptr;
   uint64_t* d_status = nullptr;
   int status_slot = -1;         // the context's page-locked status slot (−1: blocking copy)
+  int upload_slot = -1;         // page-locked copy of the tables' prefix (−1: uploaded at create)
+  size_t upload_bytes = 0;      // bytes of that prefix: the tables, then zeroed status words
+  bool upload_pending = false;  // the next enqueue copies it (and skips the status memset)
   zh::CrcJob* d_crc_jobs = nullptr;
   uint32_t* d_crc_partials = nullptr;
   int64_t n_crc_jobs = 0, n_crc_spans = 0;

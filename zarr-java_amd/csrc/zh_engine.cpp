@@ -285,6 +285,7 @@ void zh_ctx_destroy(zh_ctx* c) {
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   if (c->status_pin) (void)hipHostFree(c->status_pin);
+  if (c->upload_pin) (void)hipHostFree(c->upload_pin);
   if (c->wscratch) (void)hipFree(c->wscratch);
   for (auto& kv : c->cache) (void)hipFree(kv.second);
   pipeline_release(c);
@@ -791,6 +792,25 @@ static int status_slot_take(zh_ctx* c, int64_t nshards) {
   return k;
 }
 
+// A page-locked upload slot of the context for a plan whose table prefix fits one (−1: none).
+static int upload_slot_take(zh_ctx* c, size_t bytes) {
+  if (bytes > kUploadSlotBytes) return -1;
+  std::lock_guard<std::mutex> lk(c->status_mu);
+  if (!c->upload_pin && !c->upload_failed) {
+    void* h = nullptr;
+    if (hipHostMalloc(&h, (size_t)kUploadSlots * kUploadSlotBytes) != hipSuccess) {
+      c->upload_failed = true;
+      return -1;
+    }
+    c->upload_pin = (uint8_t*)h;
+    for (int i = kUploadSlots - 1; i >= 0; i--) c->upload_free.push_back(i);
+  }
+  if (c->upload_free.empty()) return -1;
+  const int k = c->upload_free.back();
+  c->upload_free.pop_back();
+  return k;
+}
+
 void plan_free(zh_plan* p) {
   if (!p) return;
   (void)hipSetDevice(p->ctx->device);
@@ -799,9 +819,10 @@ void plan_free(zh_plan* p) {
     (void)hipEventSynchronize(p->done_ev);
     (void)hipEventDestroy(p->done_ev);
   }
-  if (p->status_slot >= 0) {  // after done_ev: a status copy of the plan may still be queued
+  if (p->status_slot >= 0 || p->upload_slot >= 0) {  // after done_ev: copies may be queued
     std::lock_guard<std::mutex> lk(p->ctx->status_mu);
-    p->ctx->status_free.push_back(p->status_slot);
+    if (p->status_slot >= 0) p->ctx->status_free.push_back(p->status_slot);
+    if (p->upload_slot >= 0) p->ctx->upload_free.push_back(p->upload_slot);
   }
   for (auto& b : p->blocks) ctx_release(p->ctx, b.first, b.second);
   for (auto& e : p->ev_pending)
@@ -1166,7 +1187,18 @@ int plan_create(zh_ctx* ctx, const zh_array_meta* m, const SrcDesc* srcs, int64_
     p->d_status = (uint64_t*)(T + o_status);
     p->d_desc = (ItemDesc*)(T + o_desc);
     p->d_slow = (uint32_t*)(T + o_slow);
-    if (hipMemcpy(T, blob.data(), up, hipMemcpyHostToDevice) != hipSuccess) {
+    // small plans: the prefix and zeroed status words + slow-list count go to a page-locked
+    // slot and ride on the first execute's stream (no blocking copy here, no memset there)
+    const size_t upz = o_slow + sizeof(uint32_t);
+    const int slot = upload_slot_take(ctx, upz);
+    if (slot >= 0) {
+      uint8_t* h = ctx->upload_pin + (size_t)slot * kUploadSlotBytes;
+      memcpy(h, blob.data(), up);
+      memset(h + up, 0, upz - up);
+      p->upload_slot = slot;
+      p->upload_bytes = upz;
+      p->upload_pending = true;
+    } else if (hipMemcpy(T, blob.data(), up, hipMemcpyHostToDevice) != hipSuccess) {
       set_err(err, errlen, "plan upload failed");
       plan_free(p);
       return ZH_EHIP;
@@ -1328,9 +1360,16 @@ int plan_enqueue_impl(zh_plan* p, void* out, hipStream_t s) {
   for (size_t k = 0; !p->external_h2d && k < p->h2d.size(); k++)
     ZH_HIP(hipMemcpyAsync(p->d_input + p->h2d[k].first, p->h2d[k].second, (size_t)p->h2d_len[k],
                           hipMemcpyHostToDevice, s));
-  // the status words and the slow-list count (carved adjacent in the plan's tables)
-  ZH_HIP(hipMemsetAsync(p->d_status, 0,
-                        (size_t)((uint8_t*)p->d_slow - (uint8_t*)p->d_status) + sizeof(uint32_t), s));
+  if (p->upload_slot >= 0 && (p->upload_pending || p->use_graph)) {
+    // the tables with zeroed status words and slow-list count (a graph replays the copy)
+    ZH_HIP(hipMemcpyAsync(p->d_tables, p->ctx->upload_pin + (size_t)p->upload_slot * kUploadSlotBytes,
+                          p->upload_bytes, hipMemcpyHostToDevice, s));
+    p->upload_pending = false;
+  } else {
+    // the status words and the slow-list count (carved adjacent in the plan's tables)
+    ZH_HIP(hipMemsetAsync(p->d_status, 0,
+                          (size_t)((uint8_t*)p->d_slow - (uint8_t*)p->d_status) + sizeof(uint32_t), s));
+  }
   std::array<hipEvent_t, 3> ev{};
   if (p->timing) {
     for (int k = 0; k < 3; k++) {
