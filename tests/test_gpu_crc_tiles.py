@@ -420,3 +420,32 @@ def test_row_crc_encode_groups_and_store_policy(dev, monkeypatch, group, stnt):
     want = encode_oracle(meta, arr)
     assert device_write(dev, meta, arr) == want
     assert (lib().zh_debug_last_fast_path(1) % 1000000) // 1000 == int(group)
+
+
+@pytest.mark.parametrize("split", ["0", "1"])
+@pytest.mark.parametrize("start", [False, True])
+def test_index_crc_split_combine(dev, monkeypatch, split, start):
+    """The index crc32c with the span partials combined by the last workgroup (default) or by a
+    second launch (ZH_CRC_SPLIT=1): reads equal the oracle, a flipped index byte gives the
+    oracle's message, and the write path stores the same index checksums (index at the end or
+    at the start, an index of 4 KiB spans plus a tail)."""
+    monkeypatch.setenv("ZH_CRC_SPLIT", split)
+    shape = [1, 96, 200, 160]
+    meta = A.make_meta(shape, [1, 96, 100, 160], 4, endian=A.ZH_ENDIAN_BIG, sharded=True,
+                       inner_chunk_shape=[1, 4, 4, 160], index_crc32c=True,
+                       index_location=A.ZH_INDEX_START if start else A.ZH_INDEX_END)
+    arr = rand_array(shape, 4, seed=103)
+    shards = encode_oracle(meta, arr)
+    assert device_write(dev, meta, arr) == shards
+    np.testing.assert_array_equal(device_read(dev, meta, shards, [0, 0, 0, 0], shape), arr)
+    isz = 16 * (96 // 4) * (100 // 4) + 4
+    for k, pos in ((0, 5 if start else len(shards[0]) - isz + 4099), (1, isz // 2 if start else len(shards[1]) - 7)):
+        bad = list(shards)
+        b = bytearray(bad[k])
+        b[pos] ^= 0x40
+        bad[k] = bytes(b)
+        with pytest.raises(O.OracleError) as eo:
+            O.array_read(meta, bad, [0, 0, 0, 0], shape)
+        with pytest.raises(ZhError) as ed:
+            device_read(dev, meta, bad, [0, 0, 0, 0], shape)
+        assert str(ed.value) == str(eo.value)

@@ -3008,10 +3008,66 @@ __device__ uint32_t lanes_to_span_crc(uint32_t c, int64_t lb, int64_t llen, int6
 // it (status == nullptr: Crc32cCodec.encode :50-60).  A dword-aligned span is read as
 // coalesced 16-byte vectors (lane l: vectors l, l+256, ...) with the lane-interleaved update;
 // otherwise with a per-lane slicing-by-8 byte loop.
+// The combine of one job's span partials (the last workgroup of crc_index_kernel, or one
+// workgroup per job of crc_index_combine_kernel): shift every span register to the index end,
+// XOR, finish the CRC, then compare it with the stored one (read) or store it (write path).
+__device__ __forceinline__ void crc_index_finish(const CrcJob& J, const uint32_t* partials,
+                                                 int sshift, uint64_t* status, uint32_t* red,
+                                                 bool atomic_loads) {
+  const int tid = threadIdx.x;
+  const int64_t SPAN = (int64_t)kIdxSpan << sshift;
+  const int64_t njs = (J.len + SPAN - 1) / SPAN;
+  // span k ends at min((k+1)·SPAN, len); the bytes after it are (njs−1−k)·SPAN when the last
+  // span is full, else (njs−2−k)·SPAN + tail (the last span itself: 0)
+  const int64_t tail = J.len - (njs - 1) * SPAN;
+  const uint32_t xtail = tail == SPAN ? g_crc.kidx[1 << sshift] : x2nmodp((uint64_t)tail, 3);
+  uint32_t r = 0;
+  for (int64_t k = tid; k < njs; k += kBlock) {
+    const uint32_t pk = atomic_loads
+                            ? __hip_atomic_load(partials + J.span_begin + k, __ATOMIC_RELAXED,
+                                                __HIP_MEMORY_SCOPE_AGENT)
+                            : partials[J.span_begin + k];
+    const int64_t j = (njs - 2 - k) << sshift;  // 4 KiB units of the full spans after span k
+    uint32_t sh;
+    if (k == njs - 1) sh = 1u << 31;
+    else if (j < 256) sh = multmodp(g_crc.kidx[j], xtail);
+    else sh = x2nmodp((uint64_t)(J.len - (k + 1) * SPAN), 3);
+    r ^= multmodp(sh, pk);
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) r ^= (uint32_t)__shfl_xor((int)r, o, 64);
+  __syncthreads();
+  if ((tid & 63) == 0) red[tid >> 6] = r;
+  __syncthreads();
+  if (tid != 0) return;
+  r = red[0] ^ red[1] ^ red[2] ^ red[3];
+  const uint32_t c = multmodp(x2nmodp((uint64_t)J.len, 3), 0xFFFFFFFFu) ^ r ^ 0xFFFFFFFFu;
+  const uint8_t* sp = J.base + J.len;  // stored little-endian (Crc32cCodec.java:121,130)
+  if (!status) {  // write path: store it after the index (Crc32cCodec.encode :50-60)
+    uint8_t* w = const_cast<uint8_t*>(sp);
+    w[0] = (uint8_t)c;
+    w[1] = (uint8_t)(c >> 8);
+    w[2] = (uint8_t)(c >> 16);
+    w[3] = (uint8_t)(c >> 24);
+    return;
+  }
+  const uint32_t stored =
+      (uint32_t)sp[0] | ((uint32_t)sp[1] << 8) | ((uint32_t)sp[2] << 16) | ((uint32_t)sp[3] << 24);
+  uint64_t* st = status + (int64_t)J.shard * kStWords;
+  if (c != stored) {  // bit 32 marks the pair as set (nested sub-shard checks come later)
+    st[kStCrcStored] = (1ull << 32) | stored;
+    st[kStCrcComputed] = c;
+    atomicOr((unsigned long long*)(st + kStFlags), (unsigned long long)kFlagCrc);
+  }
+}
+
+// split (ZH_CRC_SPLIT): every workgroup only stores its span partial; crc_index_combine_kernel
+// (one workgroup per job, the next launch) combines them, so no workgroup takes the
+// device-scope release (a buffer_wbl2 + buffer_inv per workgroup) of the completion counter.
 __global__ __launch_bounds__(kBlock) void crc_index_kernel(const CrcJob* jobs, int64_t njobs,
                                                            int64_t nspans, int sshift,
                                                            uint32_t* partials,
-                                                           uint64_t* status) {
+                                                           uint64_t* status, int split) {
   const int64_t SPAN = (int64_t)kIdxSpan << sshift;
   __shared__ uint32_t T[8][256];
   __shared__ uint32_t S[4][256];
@@ -3080,6 +3136,10 @@ __global__ __launch_bounds__(kBlock) void crc_index_kernel(const CrcJob* jobs, i
     __syncthreads();
     raw = red[0] ^ red[1] ^ red[2] ^ red[3];
   }
+  if (split) {  // the combine runs as the next launch
+    if (tid == 0) partials[span] = raw;
+    return;
+  }
   uint32_t* counter = partials + nspans + lo;
   const int64_t njs = (J.len + SPAN - 1) / SPAN;
   if (tid == 0) {
@@ -3090,47 +3150,15 @@ __global__ __launch_bounds__(kBlock) void crc_index_kernel(const CrcJob* jobs, i
   __syncthreads();
   if (!last) return;  // uniform
   __threadfence();
-  // span k ends at min((k+1)·SPAN, len); the bytes after it are (njs−1−k)·SPAN when the last
-  // span is full, else (njs−2−k)·SPAN + tail (the last span itself: 0)
-  const int64_t tail = J.len - (njs - 1) * SPAN;
-  const uint32_t xtail = tail == SPAN ? g_crc.kidx[1 << sshift] : x2nmodp((uint64_t)tail, 3);
-  uint32_t r = 0;
-  for (int64_t k = tid; k < njs; k += kBlock) {
-    const uint32_t pk = __hip_atomic_load(partials + J.span_begin + k, __ATOMIC_RELAXED,
-                                          __HIP_MEMORY_SCOPE_AGENT);
-    const int64_t j = (njs - 2 - k) << sshift;  // 4 KiB units of the full spans after span k
-    uint32_t sh;
-    if (k == njs - 1) sh = 1u << 31;
-    else if (j < 256) sh = multmodp(g_crc.kidx[j], xtail);
-    else sh = x2nmodp((uint64_t)(J.len - (k + 1) * SPAN), 3);
-    r ^= multmodp(sh, pk);
-  }
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) r ^= (uint32_t)__shfl_xor((int)r, o, 64);
-  __syncthreads();
-  if ((tid & 63) == 0) red[tid >> 6] = r;
-  __syncthreads();
-  if (tid != 0) return;
-  *counter = 0;  // ready for the next launch
-  r = red[0] ^ red[1] ^ red[2] ^ red[3];
-  const uint32_t c = multmodp(x2nmodp((uint64_t)J.len, 3), 0xFFFFFFFFu) ^ r ^ 0xFFFFFFFFu;
-  const uint8_t* sp = J.base + J.len;  // stored little-endian (Crc32cCodec.java:121,130)
-  if (!status) {  // write path: store it after the index (Crc32cCodec.encode :50-60)
-    uint8_t* w = const_cast<uint8_t*>(sp);
-    w[0] = (uint8_t)c;
-    w[1] = (uint8_t)(c >> 8);
-    w[2] = (uint8_t)(c >> 16);
-    w[3] = (uint8_t)(c >> 24);
-    return;
-  }
-  const uint32_t stored =
-      (uint32_t)sp[0] | ((uint32_t)sp[1] << 8) | ((uint32_t)sp[2] << 16) | ((uint32_t)sp[3] << 24);
-  uint64_t* st = status + (int64_t)J.shard * kStWords;
-  if (c != stored) {  // bit 32 marks the pair as set (nested sub-shard checks come later)
-    st[kStCrcStored] = (1ull << 32) | stored;
-    st[kStCrcComputed] = c;
-    atomicOr((unsigned long long*)(st + kStFlags), (unsigned long long)kFlagCrc);
-  }
+  if (tid == 0) *counter = 0;  // ready for the next launch (every other workgroup has counted)
+  crc_index_finish(J, partials, sshift, status, red, true);
+}
+
+__global__ __launch_bounds__(kBlock) void crc_index_combine_kernel(const CrcJob* jobs, int sshift,
+                                                                   const uint32_t* partials,
+                                                                   uint64_t* status) {
+  __shared__ uint32_t red[kBlock];
+  crc_index_finish(jobs[blockIdx.x], partials, sshift, status, red, false);
 }
 
 // (crc_upd16 / crc_shift_tab: see "CRC-32C helpers" above the row kernel)
@@ -3461,8 +3489,13 @@ hipError_t launch_data_crc(const DataCrcArgs& a, int grid, hipStream_t stream) {
 hipError_t launch_crc(const CrcJob* jobs, int64_t njobs, int64_t nspans, int span_shift,
                       uint32_t* partials, uint64_t* status, hipStream_t stream) {
   if (njobs == 0) return hipSuccess;
+  const char* e = getenv("ZH_CRC_SPLIT");  // A/B switch, read per launch
+  const int split = e && e[0] == '1' ? 1 : 0;
   hipLaunchKernelGGL(crc_index_kernel, dim3((unsigned)nspans), dim3(kBlock), 0, stream, jobs,
-                     njobs, nspans, span_shift, partials, status);
+                     njobs, nspans, span_shift, partials, status, split);
+  if (split)
+    hipLaunchKernelGGL(crc_index_combine_kernel, dim3((unsigned)njobs), dim3(kBlock), 0, stream,
+                       jobs, span_shift, (const uint32_t*)partials, status);
   return hipGetLastError();
 }
 
