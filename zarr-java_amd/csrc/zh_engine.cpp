@@ -618,6 +618,8 @@ int64_t assign_crc_spans(std::vector<CrcJob>& jobs, int cu_count, int* shift) {
   int64_t small = 0;
   for (const CrcJob& J : jobs) small += (J.len + kIdxSpan - 1) / kIdxSpan;
   *shift = small >= 4 * (int64_t)cu_count ? 4 : 0;
+  const int force = env_int("ZH_CRC_SHIFT", -1);  // A/B: 4 KiB << force per workgroup (0-4)
+  if (force >= 0 && force <= 4) *shift = force;
   const int64_t span = (int64_t)kIdxSpan << *shift;
   int64_t spans = 0;
   for (CrcJob& J : jobs) {
