@@ -967,11 +967,13 @@ def test_truncated_shards_raise(dev, loc):
 
 
 @pytest.mark.parametrize("loadnt", ["0", "1"])
-def test_grouped_row_crc_decode_cache_policy(dev, monkeypatch, loadnt):
+@pytest.mark.parametrize("rgu", ["4", "8"])
+def test_grouped_row_crc_decode_cache_policy(dev, monkeypatch, loadnt, rgu):
     """The grouped row-CRC decode (rows_group_kernel, G = 2) with cached payload loads (the
     default, ZH_CRC_LOADNT=0) and with non-temporal ones: misaligned payloads after each 4-byte
     crc32c, the same bytes as the oracle and a corrupt payload byte reported alike."""
     monkeypatch.setenv("ZH_CRC_LOADNT", loadnt)
+    monkeypatch.setenv("ZH_DEC_RGU", rgu)  # rows in flight per lane
     monkeypatch.setenv("ZH_SMALL_SPLIT", "0")  # whole chunks: the grouped kernel needs them
     monkeypatch.delenv("ZH_DEC_RGROUP", raising=False)
     shape = [64, 64, 96]

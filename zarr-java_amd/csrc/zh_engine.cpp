@@ -1269,6 +1269,8 @@ int plan_create(zh_ctx* ctx, const zh_array_meta* m, const SrcDesc* srcs, int64_
   // reads 1.087x -> 1.003x algorithmic, 35.87 -> 34.87 ms, profiles/r03/c3crc); ZH_CRC_LOADNT=1:
   // non-temporal loads
   if (env_int("ZH_CRC_LOADNT", 0) == 0) p->args.nt |= 8;
+  // nt bit 5: the grouped row-CRC decode keeps 8 rows per lane in flight (ZH_DEC_RGU=8, A/B lab)
+  if (env_int("ZH_DEC_RGU", 4) == 8) p->args.nt |= 32;
   // Visit items in a golden-ratio stride order: +3.6 % on the tile path (c4) on every normal
   // allocation, neutral on the row path (interleaved A/B, profiles/placement_perm.py), so
   // on by default for tiles.  ZH_ITEM_PERM=0/1 overrides.

@@ -3616,6 +3616,12 @@ static void launch_scatter_ds(const ScatterArgs& a, int tile, int enc, int grid,
         case 5: {
           // nt bit 3 (ZH_CRC_LOADNT=0): cached payload loads (a misaligned payload's line
           // shared by two loads can then hit in L2; A/B lab), stores stay non-temporal
+          // nt bit 5 (ZH_DEC_RGU=8): 8 rows per lane in flight instead of 4
+          if (a.nt & 32) {
+            if (a.nt & 8) hipLaunchKernelGGL((rows_group_kernel<DS, 2, 8, 2, true, false>), dim3(grid), dim3(kBlock), lc, s, a);
+            else hipLaunchKernelGGL((rows_group_kernel<DS, 2, 8, 3, true, false>), dim3(grid), dim3(kBlock), lc, s, a);
+            break;
+          }
           if (a.nt & 8) hipLaunchKernelGGL((rows_group_kernel<DS, 2, 4, 2, true, false>), dim3(grid), dim3(kBlock), lc, s, a);
           else hipLaunchKernelGGL((rows_group_kernel<DS, 2, 4, 3, true, false>), dim3(grid), dim3(kBlock), lc, s, a);
           break;
