@@ -2209,6 +2209,8 @@ void tiles_rowcrc_kernel(ScatterArgs a) {
   const int64_t ngroups = (a.n_citems + G - 1) / G;
   // payload row pitch: the loaded rows (decode) or the stored rows (encode view)
   const uint32_t kr = x2nmodp((uint64_t)(31 - r) * 4 * (uint64_t)(ENC ? d_fs : s_fd), 3);
+  const uint32_t kq = regular && (uint32_t)tic < units
+                          ? multmodp(kr, K[tic + (units - 1 - tic) / TG * TG]) : 0u;
   uint32_t* mine = lds + t * kTilePitch;
   const uint32_t* crow = lds + tc * kTilePitch + (ENC ? r : r * 33);
   const uint64_t qmask = (TG * 8 == 64 ? ~0ull : ((1ull << (TG * 8)) - 1)) << (q * TG * 8);
@@ -2303,8 +2305,9 @@ void tiles_rowcrc_kernel(ScatterArgs a) {
       }
     }
     if (ENC && (__ballot(differs) & qmask) != 0 && leader && on) a.flags[c] = 1;
-    if (regular && ulast != ~0u) share = multmodp(K[ulast], run);
-    uint32_t cr = multmodp(kr, share);
+    // regular fold: the CRC role's last unit is tic + a multiple of TG in every fast chunk,
+    // so its two end multiplies fold into the lane constant kq
+    uint32_t cr = regular ? (ulast != ~0u ? multmodp(kq, run) : 0u) : multmodp(kr, share);
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) cr ^= (uint32_t)__shfl_xor((int)cr, o, 64);
     if (lane == 0 && onc) atomicXor(a.crc_partials + cc, cr);
