@@ -217,11 +217,11 @@ def pmc_traffic(config):
 
 def kernel_name(meta):
     # tile chains: tiles_group_kernel (ZH_DEC_TGROUP=0: decode_tiles_kernel); with the chunk
-    # crc32c the row-CRC tile kernel (ZH_DEC_CRCW=3, the default)
+    # crc32c the row-CRC tile kernel
     if meta.chain.has_transpose:
         if os.environ.get("ZH_DEC_TGROUP") == "0":
             return "decode_tiles_kernel"
-        if meta.chain.inner_crc32c and os.environ.get("ZH_DEC_CRCW", "3") == "3":
+        if meta.chain.inner_crc32c:
             # 128-B aligned payload windows unless ZH_DEC_ALIGN=0 (round 3)
             return ("tiles_rowcrc_kernel" if os.environ.get("ZH_DEC_ALIGN") == "0"
                     else "tiles_rowcrc_aln_kernel")

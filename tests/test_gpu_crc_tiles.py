@@ -69,7 +69,7 @@ def test_row_crc_tile_kernel_is_the_default(dev, monkeypatch, order):
     """Without switches a whole-chunk [transpose, bytes(big), crc32c] read runs
     tiles_rowcrc_kernel at G = 1 (variant 51) and matches the oracle; a flipped payload byte
     in the middle of a chunk is reported with the oracle's message."""
-    for k in ("ZH_DEC_CRCW", "ZH_DEC_TGROUP", "ZH_DEC_TPF"):
+    for k in ("ZH_DEC_TGROUP",):
         monkeypatch.delenv(k, raising=False)
     monkeypatch.setenv("ZH_SMALL_SPLIT", "0")
     meta = _meta(order)
@@ -101,17 +101,15 @@ def test_tile_crc_variants_and_item_order(dev, monkeypatch, variant, perm):
 
 
 @pytest.mark.parametrize("order", [[0, 2, 1], [2, 1, 0], [1, 2, 0]])
-@pytest.mark.parametrize("group,pf", [("0", "1"), ("1", "0"), ("1", "1"), ("2", "0"),
-                                      ("2", "1"), ("4", "0"), ("4", "1"), ("8", "0")])
+@pytest.mark.parametrize("group", ["0", "1", "2", "4", "8"])
 @pytest.mark.parametrize("crc", [True, False])
-def test_grouped_tile_decode(dev, monkeypatch, order, group, pf, crc):
+def test_grouped_tile_decode(dev, monkeypatch, order, group, crc):
     """tiles_group_kernel in the decode direction (ZH_DEC_TGROUP chunks per work item, 8/G
-    tiles of each per step; ZH_DEC_TPF: the next step's loads before this step's stores),
-    with and without the fused chunk CRC (unit fold for the 8/G stride): an elided inner
-    chunk, a missing shard, a clipped region; a corrupt byte of a fast chunk is caught."""
+    tiles of each per step, the next step's loads before this step's stores); with the chunk
+    CRC the row-CRC tile kernel at one chunk per work item whatever G (ZH_DEC_TGROUP=0: the
+    per-chunk row-interleaved kernels, CRC fused).  An elided inner chunk, a missing shard, a
+    clipped region; a corrupt byte of a fast chunk is caught."""
     monkeypatch.setenv("ZH_DEC_TGROUP", group)
-    monkeypatch.setenv("ZH_DEC_TPF", pf)
-    monkeypatch.setenv("ZH_DEC_CRCW", "0")  # the fused grouped kernel (not the row-CRC default)
     monkeypatch.setenv("ZH_SMALL_SPLIT", "0")  # whole chunks: the grouped kernels need them
     meta = A.make_meta(SHAPE, [32, 64, 64], 4, endian=A.ZH_ENDIAN_BIG, sharded=True,
                        inner_chunk_shape=[32, 32, 32], transpose_order=order, inner_crc32c=crc)
@@ -120,7 +118,7 @@ def test_grouped_tile_decode(dev, monkeypatch, order, group, pf, crc):
     shards = encode_oracle(meta, arr)
     shards[2] = None
     G = int(group)
-    want_variant = 1 if G == 0 or (G == 8 and crc) else (20 if pf == "1" else 10) + G
+    want_variant = 1 if G == 0 else 51 if crc else 20 + G
     for off, shp in [([0, 0, 0], SHAPE), ([5, 3, 7], [50, 60, 80])]:
         got, want = _read_both(dev, meta, shards, off, shp)
         np.testing.assert_array_equal(got, want)
@@ -131,16 +129,14 @@ def test_grouped_tile_decode(dev, monkeypatch, order, group, pf, crc):
 
 
 @pytest.mark.parametrize("order", [[0, 2, 1], [2, 1, 0], [1, 2, 0], [2, 0, 1]])
-@pytest.mark.parametrize("group", ["1", "2", "4"])
 @pytest.mark.parametrize("endian", [A.ZH_ENDIAN_BIG, A.ZH_ENDIAN_LITTLE])
-@pytest.mark.parametrize("crcw", ["1", "2", "3"])
-def test_crc_waves_tile_decode(dev, monkeypatch, order, group, endian, crcw):
-    """tiles_crcw_kernel (ZH_DEC_CRCW=1, 2): four waves move the tiles, four compute the chunk
-    crc32c from the LDS rows (byte-swapped back for big endian).  Same bytes as the oracle
-    with an elided chunk, a missing shard and a clipped region; corruption in a chunk's first
-    payload row, in a middle row and in its last byte is reported with the oracle's message."""
-    monkeypatch.setenv("ZH_DEC_CRCW", crcw)  # 1: movers prefetch, 2: not, 3: LDS rows
-    monkeypatch.setenv("ZH_DEC_TGROUP", group)
+def test_row_crc_tile_decode_endian(dev, monkeypatch, order, endian):
+    """tiles_rowcrc_kernel over both byte orders (big endian: byte-swapped tables, the register
+    carried swapped): same bytes as the oracle with an elided chunk, a missing shard and a
+    clipped region; corruption in a chunk's first payload row, in a middle row and in its last
+    byte is reported with the oracle's message."""
+    for k in ("ZH_DEC_TGROUP", "ZH_DEC_ALIGN"):
+        monkeypatch.delenv(k, raising=False)
     monkeypatch.setenv("ZH_SMALL_SPLIT", "0")
     meta = A.make_meta(SHAPE, [32, 64, 64], 4, endian=endian, sharded=True,
                        inner_chunk_shape=[32, 32, 32], transpose_order=order, inner_crc32c=True)
@@ -152,7 +148,7 @@ def test_crc_waves_tile_decode(dev, monkeypatch, order, group, endian, crcw):
         got, want = _read_both(dev, meta, shards, off, shp)
         np.testing.assert_array_equal(got, want)
         if off == [0, 0, 0]:
-            assert _variant() == 30 + int(group) + 10 * (int(crcw) - 1)
+            assert _variant() == 51
     full = encode_oracle(meta, arr)  # shard 0: four in-bounds chunks of random data
     for pos in (3, CHUNK + 1000, 2 * CHUNK + 70001, CHUNK - 5):
         _corrupt_matches_oracle(dev, meta, full, 0, pos)
@@ -163,7 +159,7 @@ def test_row_crc_tile_kernel_many_groups(dev, monkeypatch):
     64 MiB: 512 inner chunks over 8 shards, the golden-ratio group order and the default
     row-CRC tile kernel; equals the oracle, and a flipped byte deep inside the last shard is
     reported with the oracle's message."""
-    for k in ("ZH_DEC_CRCW", "ZH_DEC_TGROUP", "ZH_DEC_TPF", "ZH_SMALL_SPLIT"):
+    for k in ("ZH_DEC_TGROUP", "ZH_SMALL_SPLIT"):
         monkeypatch.delenv(k, raising=False)
     shape = [1, 256, 256, 256]
     meta = A.make_meta(shape, [1, 128, 128, 128], 4, endian=A.ZH_ENDIAN_BIG, sharded=True,
@@ -173,8 +169,7 @@ def test_row_crc_tile_kernel_many_groups(dev, monkeypatch):
     arr[arr == 0] = 1
     shards = encode_oracle(meta, arr)
     # the default tile encode with the fused chunk CRC (2 chunks per work item) at this size
-    for k in ("ZH_ENC_CRC_STNT", "ZH_ENC_TGROUP", "ZH_ENC_ALIGN", "ZH_ENC_ROWCRC", "ZH_ENC_TPF"):
-        monkeypatch.delenv(k, raising=False)
+    monkeypatch.delenv("ZH_ENC_TGROUP", raising=False)
     assert device_write(dev, meta, arr) == shards
     assert (lib().zh_debug_last_fast_path(1) % 1000000) // 1000 == 2
     want = np.frombuffer(O.array_read(meta, shards, [0, 0, 0, 0], shape), np.uint32).reshape(shape)
@@ -202,7 +197,7 @@ def test_row_crc_tile_kernel_unit_layouts(dev, monkeypatch, units, order):
     per-unit K multiply (no regular fold step: crc_tile_step 0), 12 units the regular fold
     over a partly filled last step.  Equals the oracle; a flipped byte in the last unit of a
     chunk is caught with the oracle's message."""
-    for k in ("ZH_DEC_CRCW", "ZH_DEC_TGROUP", "ZH_DEC_TPF"):
+    for k in ("ZH_DEC_TGROUP",):
         monkeypatch.delenv(k, raising=False)
     monkeypatch.setenv("ZH_SMALL_SPLIT", "0")
     shape = [units * 2, 64, 96]
@@ -240,8 +235,7 @@ def _aligned():
 
 @pytest.mark.parametrize("nb", [16, 24, 32])
 @pytest.mark.parametrize("endian", [A.ZH_ENDIAN_BIG, A.ZH_ENDIAN_LITTLE])
-@pytest.mark.parametrize("field", ["0", "1"])
-def test_row_crc_aligned_windows(dev, monkeypatch, nb, endian, field):
+def test_row_crc_aligned_windows(dev, monkeypatch, nb, endian):
     """tiles_rowcrc_aln_kernel: inner chunks [32, nb, 32] under transpose [2, 1, 0] store
     [32 rows][nb units][32 words] (c4's layout), so the movers load 128-B aligned lines and
     carry each step's last line into the next step's tile through a ring of 9 LDS slots.  One
@@ -250,11 +244,10 @@ def test_row_crc_aligned_windows(dev, monkeypatch, nb, endian, field):
     whole array and a ragged region, with an elided chunk; ZH_DEC_ALIGN=0 gives the same bytes
     through the unaligned loads; flipped bytes in a row tail (read at the last step from the
     box), in a carried line end and in a head line are reported with the oracle's message."""
-    for k in ("ZH_DEC_CRCW", "ZH_DEC_TGROUP", "ZH_DEC_TPF"):
+    for k in ("ZH_DEC_TGROUP",):
         monkeypatch.delenv(k, raising=False)
     monkeypatch.setenv("ZH_SMALL_SPLIT", "0")
     monkeypatch.setenv("ZH_DEC_ALIGN", "1")
-    monkeypatch.setenv("ZH_DEC_CRCFIELD", field)  # 1: the row CRC over field tables
     shape = [64, 6 * nb, 96]
     meta = A.make_meta(shape, shape, 4, endian=endian, sharded=True,
                        inner_chunk_shape=[32, nb, 32], transpose_order=[2, 1, 0],
@@ -266,7 +259,7 @@ def test_row_crc_aligned_windows(dev, monkeypatch, nb, endian, field):
     got, want = _read_both_shape(dev, meta, shards, shape)
     np.testing.assert_array_equal(got, want)
     np.testing.assert_array_equal(got, arr)
-    assert _variant() == 51 and _aligned() == 1 + int(field)
+    assert _variant() == 51 and _aligned() == 1
     off, shp = [3, 5, 7], [58, 6 * nb - 9, 80]
     sel = np.frombuffer(O.array_read(meta, shards, off, shp), np.uint32).reshape(shp)
     np.testing.assert_array_equal(device_read(dev, meta, shards, off, shp), sel)
@@ -296,42 +289,13 @@ def _corrupt_matches_oracle_shape(dev, meta, shards, k, pos, shape):
     assert str(ed.value) == str(eo.value)
 
 
-@pytest.mark.parametrize("nb", [16, 32])
-@pytest.mark.parametrize("pf", ["1", "0"])
-@pytest.mark.parametrize("endian", [A.ZH_ENDIAN_BIG, A.ZH_ENDIAN_LITTLE])
-def test_row_crc_aligned_encode(dev, monkeypatch, nb, pf, endian):
-    """tiles_rowcrc_enc_aln_kernel (ZH_ENC_ALIGN=1; ZH_ENC_ALIGN_PF: prefetching region loads
-    or not): the [transpose [2, 1, 0], bytes, crc32c] write of inner chunks [32, nb, 32] stores
-    whole 128-B payload lines.  One shard of 36 inner chunks puts the payloads at every offset
-    4i mod 128; two all-fill chunks are elided (the later payloads move by a chunk, the flags
-    come from the fill test of the loaded rows).  The shards are byte-identical to the
-    oracle's, and decode back."""
-    from helpers import device_write
-    monkeypatch.setenv("ZH_ENC_ALIGN", "1")
-    monkeypatch.setenv("ZH_ENC_ALIGN_PF", pf)
-    shape = [64, 6 * nb, 96]
-    meta = A.make_meta(shape, shape, 4, endian=endian, sharded=True,
-                       inner_chunk_shape=[32, nb, 32], transpose_order=[2, 1, 0],
-                       inner_crc32c=True)
-    arr = rand_array(shape, 4, seed=97 + nb)
-    arr[arr == 0] = 1
-    arr[0:32, nb:2 * nb, 0:32] = 0
-    arr[32:64, 3 * nb:4 * nb, 64:96] = 0
-    want = encode_oracle(meta, arr)
-    got = device_write(dev, meta, arr)
-    assert lib().zh_debug_last_fast_path(1) % 1000 == (31 if pf == "1" else 32)
-    assert got == want
-    np.testing.assert_array_equal(device_read(dev, meta, got, [0, 0, 0], shape), arr)
-
-
 def test_row_crc_chain_64mib_defaults(dev, monkeypatch):
     """The c3crc chain ([bytes(big), crc32c], 32³ uint32 inner chunks, no transpose) at 64 MiB
     with the default kernels of both directions: the grouped row-CRC encode (2 chunks per work
     item, payloads stored through the cache since round 3) gives the oracle's shard bytes, and
     the grouped row-CRC decode (cached payload loads) gives the array back; a flipped byte deep
     inside the last shard is reported with the oracle's message."""
-    for k in ("ZH_ENC_CRC_STNT", "ZH_ENC_GROUP", "ZH_CRC_LOADNT", "ZH_DEC_RGROUP",
-              "ZH_SMALL_SPLIT", "ZH_PIPE"):
+    for k in ("ZH_ENC_GROUP", "ZH_DEC_RGROUP", "ZH_SMALL_SPLIT", "ZH_PIPE"):
         monkeypatch.delenv(k, raising=False)
     shape = [1, 256, 256, 256]
     meta = A.make_meta(shape, [1, 128, 128, 128], 4, endian=A.ZH_ENDIAN_BIG, sharded=True,
@@ -363,7 +327,7 @@ def test_plain_chains_64mib_defaults(dev, monkeypatch, order):
     inner chunks) at 64 MiB through the default kernels: the grouped encodes give the oracle's
     shard bytes, and the decode (lane exchange for c3, tile groups for c4) gives the array
     back, also for a region that cuts every shard."""
-    for k in ("ZH_ENC_GROUP", "ZH_ENC_TGROUP", "ZH_ENC_XPOSE", "ZH_DEC_RGROUP", "ZH_DEC_TGROUP",
+    for k in ("ZH_ENC_GROUP", "ZH_ENC_TGROUP", "ZH_DEC_RGROUP", "ZH_DEC_TGROUP",
               "ZH_SMALL_SPLIT", "ZH_PIPE"):
         monkeypatch.delenv(k, raising=False)
     shape = [1, 256, 256, 256]
@@ -384,36 +348,26 @@ def test_plain_chains_64mib_defaults(dev, monkeypatch, order):
 
 @pytest.mark.parametrize("order", [[0, 2, 1], [2, 1, 0], [1, 2, 0]])
 @pytest.mark.parametrize("group", ["1", "2", "4"])
-@pytest.mark.parametrize("stnt", ["0", "1"])
-@pytest.mark.parametrize("tabs", ["ZH_ENC_CRCLOW", "ZH_ENC_CRCFIELD"])
-def test_tile_crc_encode_compact_tables(dev, monkeypatch, order, group, stnt, tabs):
-    """The tile encode with the fused chunk CRC over compact tables (ZH_ENC_CRCLOW=1:
-    slicing-by-4 and nibble shift tables; ZH_ENC_CRCFIELD=1: conflict-free 5/4-bit field
-    tables; both 4 workgroups per CU): byte-identical to the oracle's shards (an all-fill chunk
-    elided, so the later payloads shift), for 1, 2 and 4 chunks per work item and both store
-    policies, and the kernel that ran is that variant (deep 40 / 41)."""
-    monkeypatch.setenv(tabs, "1")
+def test_tile_crc_encode_groups(dev, monkeypatch, order, group):
+    """The tile encode with the fused chunk CRC over 1, 2 and 4 chunks per work item:
+    byte-identical to the oracle's shards (an all-fill chunk elided, so the later payloads
+    shift), and the kernel that ran is that group size."""
     monkeypatch.setenv("ZH_ENC_TGROUP", group)
-    monkeypatch.setenv("ZH_ENC_CRC_STNT", stnt)
     meta = _meta(order)
     arr = rand_array(SHAPE, 4, seed=97)
     arr[0:32, 32:64, 0:32] = 0
     want = encode_oracle(meta, arr)
     got = device_write(dev, meta, arr)
     assert got == want
-    path = lib().zh_debug_last_fast_path(1)
-    assert path % 1000 == (41 if tabs == "ZH_ENC_CRCFIELD" else 40)
-    assert (path % 1000000) // 1000 == int(group)
+    assert (lib().zh_debug_last_fast_path(1) % 1000000) // 1000 == int(group)
 
 
 @pytest.mark.parametrize("group", ["1", "2", "4"])
-@pytest.mark.parametrize("stnt", ["0", "1"])
-def test_row_crc_encode_groups_and_store_policy(dev, monkeypatch, group, stnt):
+def test_row_crc_encode_groups(dev, monkeypatch, group):
     """The row encode with the fused chunk CRC ([bytes(big), crc32c], no transpose) over 1, 2
-    and 4 chunks per work item, payloads stored through the cache or non-temporally:
-    byte-identical to the oracle's shards (an all-fill chunk elided, so later payloads shift)."""
+    and 4 chunks per work item, payloads stored through the cache: byte-identical to the
+    oracle's shards (an all-fill chunk elided, so later payloads shift)."""
     monkeypatch.setenv("ZH_ENC_GROUP", group)
-    monkeypatch.setenv("ZH_ENC_CRC_STNT", stnt)
     meta = _meta(None)
     arr = rand_array(SHAPE, 4, seed=101)
     arr[32:64, 0:32, 32:64] = 0
@@ -422,14 +376,12 @@ def test_row_crc_encode_groups_and_store_policy(dev, monkeypatch, group, stnt):
     assert (lib().zh_debug_last_fast_path(1) % 1000000) // 1000 == int(group)
 
 
-@pytest.mark.parametrize("split", ["0", "1"])
 @pytest.mark.parametrize("start", [False, True])
-def test_index_crc_split_combine(dev, monkeypatch, split, start):
-    """The index crc32c with the span partials combined by the last workgroup (default) or by a
-    second launch (ZH_CRC_SPLIT=1): reads equal the oracle, a flipped index byte gives the
-    oracle's message, and the write path stores the same index checksums (index at the end or
-    at the start, an index of 4 KiB spans plus a tail)."""
-    monkeypatch.setenv("ZH_CRC_SPLIT", split)
+def test_index_crc_span_combine(dev, monkeypatch, start):
+    """The index crc32c with the span partials combined by the last workgroup: reads equal the
+    oracle, a flipped index byte gives the oracle's message, and the write path stores the
+    same index checksums (index at the end or at the start, an index of 4 KiB spans plus a
+    tail)."""
     shape = [1, 96, 200, 160]
     meta = A.make_meta(shape, [1, 96, 100, 160], 4, endian=A.ZH_ENDIAN_BIG, sharded=True,
                        inner_chunk_shape=[1, 4, 4, 160], index_crc32c=True,

@@ -404,17 +404,15 @@ def test_device_encode_grouped_rows(dev, dsize, order):
 
 @pytest.mark.parametrize("crc", [False, True])
 @pytest.mark.parametrize("dsize", [1, 4, 8])
-@pytest.mark.parametrize("group,rows", [("0", "4"), ("1", "2"), ("2", "4"), ("4", "8"),
-                                        ("8", "4"), ("-1", "4")])
-def test_device_encode_chunk_groups(dev, monkeypatch, dsize, group, rows, crc):
-    """encode_group_rows_kernel (G consecutive inner chunks per work item, ZH_ENC_GROUP; rows
-    in flight ZH_ENC_GU): an odd number of inner chunks along each shard row (groups straddle
+@pytest.mark.parametrize("group", ["0", "1", "2", "4", "8", "-1"])
+def test_device_encode_chunk_groups(dev, monkeypatch, dsize, group, crc):
+    """rows_group_kernel on the encode view (G consecutive inner chunks per work item,
+    ZH_ENC_GROUP; 4 rows in flight per lane): an odd number of inner chunks along each shard row (groups straddle
     shard rows and the item list's end), all-fill chunks beside data chunks in one group
     (per-chunk flags from one ballot), clipped boundary chunks on the slow list.  crc: inner
     [bytes(big), crc32c] with 4 KiB chunk payloads, the chunk CRC fused into the grouped
     kernel (256/G lanes per chunk)."""
     monkeypatch.setenv("ZH_ENC_GROUP", group)
-    monkeypatch.setenv("ZH_ENC_GU", rows)
     inner_last = 128 // dsize
     shape = [13, 24, inner_last * 7 + inner_last // 2]
     meta = A.make_meta(shape, [8, 8, inner_last * 5], dsize, endian=A.ZH_ENDIAN_BIG,
@@ -493,33 +491,6 @@ def test_grouped_row_decode(dev, monkeypatch, crc, dsize, group):
         assert str(ed.value) == str(eo.value)
 
 
-@pytest.mark.parametrize("inner_rows", [(4, 8), (2, 4), (8, 16), (3, 5)])
-@pytest.mark.parametrize("dsize", [1, 2, 4, 8])
-@pytest.mark.parametrize("crc", [False, True])
-def test_device_encode_lane_exchange(dev, monkeypatch, dsize, inner_rows, crc):
-    """rows_xpose_kernel on the encode view (ZH_ENC_XPOSE=1: 128-B rows, 8 chunks per work
-    item, region rows and payload rows exchanged through LDS): groups straddling shard rows and
-    the item list's end, all-fill chunks beside data chunks (per-chunk flags), clipped boundary
-    chunks on the slow list, 8 rows per chunk (one wave step), and chains it must leave to the
-    grouped kernel (15 rows per chunk; the fused chunk CRC)."""
-    monkeypatch.setenv("ZH_ENC_XPOSE", "1")
-    L = 128 // dsize
-    a, b = inner_rows
-    shape = [a * 3 + 1, b * 3, L * 9 + L // 2]
-    meta = A.make_meta(shape, [a * 2, b * 2, L * 5], dsize, endian=A.ZH_ENDIAN_BIG,
-                       sharded=True, inner_chunk_shape=[a, b, L],
-                       fill=(5).to_bytes(dsize, "little"), inner_crc32c=crc)
-    arr = rand_array(shape, dsize, seed=81 + dsize + a)
-    arr[arr == 5] = 6
-    arr[0:a, 0:b, L:2 * L] = 5                    # all-fill chunk next to data
-    arr[a:2 * a, b:2 * b, 0:3 * L] = 5            # a run of three
-    arr[a:2 * a, 0:b, 2 * L + 1] = 9
-    want = encode_oracle(meta, arr)
-    got = device_write(dev, meta, arr)
-    assert [len(g) if g else 0 for g in got] == [len(w) if w else 0 for w in want]
-    assert got == want
-
-
 @pytest.mark.parametrize("inner_rows", [(4, 8), (2, 4), (3, 5)])
 @pytest.mark.parametrize("dsize", [1, 4, 8])
 @pytest.mark.parametrize("crc", [False, True])
@@ -549,16 +520,14 @@ def test_lane_exchange_row_decode(dev, monkeypatch, dsize, inner_rows, crc):
 
 
 @pytest.mark.parametrize("order", [[0, 3, 2, 1], [0, 1, 3, 2]])
-@pytest.mark.parametrize("group,rowcrc", [("-1", "0"), ("0", "0"), ("1", "0"), ("4", "0"),
-                                          ("1", "1"), ("2", "1"), ("4", "1")])
-def test_tile_encode_chunk_crc_fused(dev, monkeypatch, order, group, rowcrc):
+@pytest.mark.parametrize("group", ["-1", "0", "1", "2", "4"])
+def test_tile_encode_chunk_crc_fused(dev, monkeypatch, order, group):
     """c4crc-shaped chain at small extent: [transpose, bytes(big), crc32c] with 32x32 tiles,
     the chunk CRC fused into the tile encode (stored vectors, per-unit end shifts from the
     payload side of the table), boundary chunks through the slow list + CRC pass; equals the
     oracle and the unfused pass, and decodes back.  ZH_ENC_TGROUP: the grouped tile encode
     (the unit fold step for 8/G units), or the ungrouped kernel (0)."""
     monkeypatch.setenv("ZH_ENC_TGROUP", group)
-    monkeypatch.setenv("ZH_ENC_ROWCRC", rowcrc)  # 1: tiles_rowcrc_kernel on the encode view
     shape = [1, 64, 80, 96]
     meta = A.make_meta(shape, [1, 64, 64, 64], 4, endian=A.ZH_ENDIAN_BIG, sharded=True,
                        inner_chunk_shape=[1, 32, 32, 32], transpose_order=order,
@@ -567,8 +536,6 @@ def test_tile_encode_chunk_crc_fused(dev, monkeypatch, order, group, rowcrc):
     arr[arr == 0] = 1
     want = encode_oracle(meta, arr)
     assert device_write(dev, meta, arr) == want
-    if rowcrc == "1":  # the encode view ran the row-CRC kernel (kernel form 30) at group G
-        assert lib().zh_debug_last_fast_path(1) % 1000000 == int(group) * 1000 + 30
     monkeypatch.setenv("ZH_CRC_FUSE", "0")
     assert device_write(dev, meta, arr) == want
     monkeypatch.delenv("ZH_CRC_FUSE")
@@ -966,14 +933,10 @@ def test_truncated_shards_raise(dev, loc):
         assert str(ed.value).startswith("Could not load byte data for chunk")
 
 
-@pytest.mark.parametrize("loadnt", ["0", "1"])
-@pytest.mark.parametrize("rgu", ["4", "8"])
-def test_grouped_row_crc_decode_cache_policy(dev, monkeypatch, loadnt, rgu):
-    """The grouped row-CRC decode (rows_group_kernel, G = 2) with cached payload loads (the
-    default, ZH_CRC_LOADNT=0) and with non-temporal ones: misaligned payloads after each 4-byte
-    crc32c, the same bytes as the oracle and a corrupt payload byte reported alike."""
-    monkeypatch.setenv("ZH_CRC_LOADNT", loadnt)
-    monkeypatch.setenv("ZH_DEC_RGU", rgu)  # rows in flight per lane
+def test_grouped_row_crc_decode_misaligned(dev, monkeypatch):
+    """The grouped row-CRC decode (rows_group_kernel, G = 2, cached payload loads): misaligned
+    payloads after each 4-byte crc32c, the same bytes as the oracle and a corrupt payload byte
+    reported alike."""
     monkeypatch.setenv("ZH_SMALL_SPLIT", "0")  # whole chunks: the grouped kernel needs them
     monkeypatch.delenv("ZH_DEC_RGROUP", raising=False)
     shape = [64, 64, 96]
@@ -997,12 +960,10 @@ def test_grouped_row_crc_decode_cache_policy(dev, monkeypatch, loadnt, rgu):
 
 
 @pytest.mark.parametrize("order", [None, [2, 1, 0]])
-@pytest.mark.parametrize("stnt", ["0", "1"])
-def test_grouped_crc_encode_cache_policy(dev, monkeypatch, order, stnt):
-    """The grouped encodes with the fused chunk CRC (row kernel for [bytes, crc32c], tile
-    kernel for [transpose, bytes, crc32c]) with payload stores through the cache
-    (ZH_ENC_CRC_STNT=0) and non-temporal ones: byte-identical to the oracle's shards."""
-    monkeypatch.setenv("ZH_ENC_CRC_STNT", stnt)
+def test_grouped_crc_encode_misaligned(dev, monkeypatch, order):
+    """The grouped encodes with the fused chunk CRC (row kernel for [bytes, crc32c], payloads
+    stored through the cache; tile kernel for [transpose, bytes, crc32c], non-temporal):
+    byte-identical to the oracle's shards."""
     shape = [64, 64, 96]
     meta = A.make_meta(shape, [32, 64, 64], 4, endian=A.ZH_ENDIAN_BIG, sharded=True,
                        inner_chunk_shape=[32, 32, 32], transpose_order=order,

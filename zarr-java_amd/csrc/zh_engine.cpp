@@ -1125,7 +1125,6 @@ int plan_create(zh_ctx* ctx, const zh_array_meta* m, const SrcDesc* srcs, int64_
       p->args.piece_shift++;
   std::vector<uint32_t> tab = setup_fast(m, p->args, p->tile_mode);
   p->args.tile_variant = std::min(1, std::max(0, env_int("ZH_TILE_VARIANT", 1)));
-  p->args.lds_pad = std::max(0, env_int("ZH_LDS_PAD", 0));
   // Chunk CRC fused into the row-interleaved tile kernel: every payload byte of a fast item
   // is loaded exactly once by some lane, and each lane's share is shifted to the payload end
   // by K[u] = x^(8(L − E_u)) (E_u = end of unit u's last row, appended to the table) and a
@@ -1262,15 +1261,9 @@ int plan_create(zh_ctx* ctx, const zh_array_meta* m, const SrcDesc* srcs, int64_
   p->nest.status = p->d_status;
   p->grid = grid_for(ctx, p->args.total_items);
   // non-temporal loads + stores: +4 % on the row path, +1 % on the tile path (interleaved
-  // A/B in one process, profiles/r01/experiments/tune_*.json)
-  p->args.nt = env_int("ZH_NT", 3) & 7;  // bit 2: 8 rows in flight per lane (rows)
-  // the grouped row-CRC decode (G = 2) loads payloads through the cache: a payload after a
-  // 4-byte crc32c sits at 4 mod 16, and the line two loads share then hits in L2 (c3crc
-  // reads 1.087x -> 1.003x algorithmic, 35.87 -> 34.87 ms, profiles/r03/c3crc); ZH_CRC_LOADNT=1:
-  // non-temporal loads
-  if (env_int("ZH_CRC_LOADNT", 0) == 0) p->args.nt |= 8;
-  // nt bit 5: the grouped row-CRC decode keeps 8 rows per lane in flight (ZH_DEC_RGU=8, A/B lab)
-  if (env_int("ZH_DEC_RGU", 4) == 8) p->args.nt |= 32;
+  // A/B in one process, profiles/r01/experiments/tune_*.json); every decode fast kernel
+  // streams (the grouped row-CRC decode loads its payloads through the cache, launcher)
+  p->args.nt = 3;
   // Visit items in a golden-ratio stride order: +3.6 % on the tile path (c4) on every normal
   // allocation, neutral on the row path (interleaved A/B, profiles/placement_perm.py), so
   // on by default for tiles.  ZH_ITEM_PERM=0/1 overrides.
@@ -1278,48 +1271,43 @@ int plan_create(zh_ctx* ctx, const zh_array_meta* m, const SrcDesc* srcs, int64_
       env_int("ZH_ITEM_PERM", p->tile_mode ? 1 : 0) ? golden_item_mul(p->args.total_items) : 0;
   p->slow_grid = p->grid;
   // The tile decode over G consecutive (z-adjacent) chunks per work item, the next step's
-  // loads issued before this step's stores (tiles_group_kernel; tile_variant 20 + G, 10 + G
-  // without the prefetch): c4 33.4 → 32.9 ms (G = 4), c4crc 39.5 → 38.3 ms (G = 2), interleaved
-  // A/B in profiles/r02/experiments/ab_r02abdtgpf*.txt.  ZH_DEC_TGROUP = G (0: the
-  // row-interleaved tile kernel; 1, 2, 4, 8, with the chunk CRC 1, 2, 4), ZH_DEC_TPF = 0/1.
+  // loads issued before this step's stores (tiles_group_kernel; tile_variant 20 + G): c4
+  // 33.4 → 32.9 ms (G = 4), interleaved A/B in profiles/r02/experiments/ab_r02abdtgpf*.txt.
+  // ZH_DEC_TGROUP = G (0: the row-interleaved per-chunk tile kernel; 1, 2, 4, 8).
   //
-  // With the fused chunk CRC the default is tiles_rowcrc_kernel at G = 1 (ZH_DEC_CRCW=3: every
-  // lane also CRCs one payload row from the LDS tiles, 16 lookups per 16-B vector): c4crc
-  // 38.27 → 36.92 ms, interleaved A/B in profiles/r02/crc/ab_rowcrc.json (G = 2 37.16, the
-  // CRC-wave kernel 39.6, ZH_DEC_CRCW=0 restores the fused grouped kernel at G = 2).
+  // With the fused chunk CRC: tiles_rowcrc_kernel, one chunk per work item (tile_variant 51:
+  // every lane also CRCs one payload row from the LDS tiles, 16 lookups per 16-B vector):
+  // c4crc 38.27 → 36.92 ms, profiles/r02/crc/ab_rowcrc.json.  Round 4 removed the variants that
+  // measured slower (the fused grouped CRC decode, CRC waves of their own, rows per lane, field
+  // tables); their A/B records stay under profiles/.
   {
     const bool crc = p->args.crc_fused != 0;
-    const int crcw = crc ? env_int("ZH_DEC_CRCW", 3) : 0;
-    const bool rowcrc_ok = crcw != 3 || zh::rowcrc_lds_at_zero();
-    const int G = env_int("ZH_DEC_TGROUP", crc ? (crcw == 3 && rowcrc_ok ? 1 : 2) : 4);
-    if ((G == 1 || G == 2 || G == 4 || (G == 8 && !crc)) && p->tile_mode &&
+    const int G = crc ? 1 : env_int("ZH_DEC_TGROUP", 4);
+    const bool rowcrc_ok = !crc || zh::rowcrc_lds_at_zero();
+    if ((G == 1 || G == 2 || G == 4 || G == 8) && rowcrc_ok && p->tile_mode &&
         p->args.fast_mode == kFastTileTable && p->args.tile_variant == 1 &&
-        (!crc || tile_crc) && p->args.piece_shift == 0 && (p->args.nt & 3) == 3 && items > 0) {
+        (!crc || tile_crc) && p->args.piece_shift == 0 && items > 0 &&
+        (!crc || env_int("ZH_DEC_TGROUP", 1) != 0)) {
       const int64_t groups = (items + G - 1) / G;
-      p->args.tile_variant = (env_int("ZH_DEC_TPF", 1) ? 20 : 10) + G;
-      // the chunk CRC on waves of its own (tiles_crcw_kernel: 8-wave blocks, 4 move, 4 CRC)
-      // (1: the movers prefetch, 2: they do not); 3: every lane moves tiles and takes one LDS
-      // payload row for the CRC (tiles_rowcrc_kernel)
-      if (crc && G <= 4 && crcw >= 1 && crcw <= 3 && rowcrc_ok)
-        p->args.tile_variant = 30 + G + 10 * (crcw - 1);
-      // Aligned windows for the row-CRC kernel (G = 1): every payload after a 4-byte crc32c
-      // starts at 4·i mod 128, so a 1 KiB wave load of it touched 9 lines and the shared line
-      // was fetched twice.  When unit u's rows start at 32u elements and row r + 1 follows row
-      // r (the payload is [32 rows][units][32 words], c4's layout), the movers load 128-B
-      // aligned lines and route each word to its tile in LDS (ZH_DEC_ALIGN=0: off).
-      if (p->args.tile_variant == 51 && env_int("ZH_DEC_ALIGN", 1) != 0) {
+      p->args.tile_variant = crc ? 51 : 20 + G;
+      // Aligned windows for the row-CRC kernel: every payload after a 4-byte crc32c starts at
+      // 4·i mod 128, so a 1 KiB wave load of it touched 9 lines and the shared line was
+      // fetched twice.  When unit u's rows start at 32u elements and row r + 1 follows row r
+      // (the payload is [32 rows][units][32 words], c4's layout), the movers load 128-B aligned
+      // lines and route each word to its tile in LDS (ZH_DEC_ALIGN=0: off).
+      if (crc && env_int("ZH_DEC_ALIGN", 1) != 0) {
         const ScatterArgs& g = p->args;
         const int64_t nu = g.fast_n;
-        // [32 rows][nu units][32 words], 2-4 steps of 8 units (K fits the box area), unit u's
-        // region offset u·ys, the stores' lane offsets 4·(u·ys) + 128 within 32 bits
-        bool al = nu >= 16 && nu <= 32 && nu % 8 == 0 && g.pstride[g.fd] == 32 * nu &&
-                  g.inner_nbytes == 4096 * nu && (int64_t)tab.size() >= 2 * nu;
+        // [32 rows][nu units][32 words], 2-4 steps of 8 units (K fits the kernel's K area),
+        // unit u's region offset u·ys, the stores' lane offsets 4·(u·ys) + 128 within 32 bits
+        bool al = nu >= 16 && nu <= zh::kAlnUnitsMax && nu % 8 == 0 &&
+                  g.pstride[g.fd] == 32 * nu && g.inner_nbytes == 4096 * nu &&
+                  (int64_t)tab.size() >= 2 * nu;
         const uint64_t ys = al ? tab[3] : 0;
         for (int64_t u = 0; al && u < nu; u++)
           al = tab[2 * (size_t)u] == (uint32_t)(32 * u) &&
                tab[2 * (size_t)u + 1] == (uint64_t)u * ys && 4 * (uint64_t)u * ys + 128 <= 0xFFFFFFFFull;
-        // 2: the row CRC over conflict-free field tables (ZH_DEC_CRCFIELD=1, A/B lab)
-        p->args.tile_align = al ? (env_int("ZH_DEC_CRCFIELD", 0) ? 2 : 1) : 0;
+        p->args.tile_align = al ? 1 : 0;
         p->args.tile_ystride = al ? (int64_t)ys : 0;
       }
       if (crc) p->args.crc_tile_step = tile_crc_step(ends, (size_t)(8 / G));
@@ -1340,7 +1328,7 @@ int plan_create(zh_ctx* ctx, const zh_array_meta* m, const SrcDesc* srcs, int64_
                                               : p->args.fast_vpr_shift == 3 ? 8 : 0);
     const ScatterArgs& g = p->args;
     if (want != 0 && !p->tile_mode && (g.fast_mode == kFastRowArith || g.fast_mode == kFastRowTable) &&
-        g.piece_shift == 0 && (g.nt & 3) == 3 && items > 0) {
+        g.piece_shift == 0 && items > 0) {
       int G = want > 0 ? want : (16 >> std::min(g.fast_vpr_shift, 5));
       // 8: rows_xpose_kernel (128-B rows, no fused CRC, rows a multiple of 8)
       const bool xpose = G == 8 && g.fast_vpr_shift == 3 && !g.crc_fused && g.fast_rows % 8 == 0;
@@ -2395,88 +2383,35 @@ static int array_write_fast(zh_ctx* ctx, const zh_array_meta* m, ScatterArgs a,
   v.crc_partials = (uint32_t*)(W + o_cpart);
   if (crc_fuse)
     ZH_HIPF(hipMemsetAsync(W + o_cpart, 0, (size_t)(items * nspan) * sizeof(uint32_t), s));
-  v.nt = env_int("ZH_ENC_NT", 3) & 3;
+  v.nt = 3;  // non-temporal region loads and payload stores (launch_encode_fast_ds)
   // narrow rows: G consecutive chunks per work item so a wave load covers G·row bytes of a
-  // region row (ZH_ENC_GROUP: 0 off, default G·row = 256 B; encode_group_rows_kernel; c3
-  // write G × U grid in profiles/r02/write/ab_enc3.txt: G = 2, U = 4 best, 40.1 → 36.2 ms)
+  // region row (ZH_ENC_GROUP: 0 off, default G·row = 256 B; rows_group_kernel, 4 rows in
+  // flight per lane; c3 write G × U grid in profiles/r02/write/ab_enc3.txt: G = 2, U = 4 best,
+  // 40.1 → 36.2 ms)
   int group = 0;
   // (not nested: c3nest measured 42 → 48 ms grouped, profiles/r02/write/ab_enc.txt)
   // (with the chunk CRC fused: rows sequential in the payload, checked above; whole chunks)
-  if ((v.fast_mode == kFastRowArith || v.fast_mode == kFastRowTable) && v.nt == 3 &&
-      a.piece_shift == 0 && (!nz.cell || env_int("ZH_ENC_GROUP", -1) > 0)) {
+  if ((v.fast_mode == kFastRowArith || v.fast_mode == kFastRowTable) && a.piece_shift == 0 &&
+      (!nz.cell || env_int("ZH_ENC_GROUP", -1) > 0)) {
     const int want = env_int("ZH_ENC_GROUP", -1);
     int G = want >= 0 ? want : (16 >> std::min(v.fast_vpr_shift, 5));
     G = G >= 8 ? 8 : G >= 4 ? 4 : G >= 2 ? 2 : G;
-    if (crc_fuse && G > 4) G = 4;  // the CRC variants: G 1, 2, 4 with 4 rows per lane
+    if (crc_fuse && G > 4) G = 4;  // the CRC variants: G 1, 2, 4
     if (G && (G << v.fast_vpr_shift) <= 64) group = G;
   }
   // tiles (uint32 transposed chunks): G chunks per work item, 8/G tiles of each per step
-  // (ZH_ENC_TGROUP: 0 off; tiles_group_kernel)
-  // With the tile CRC fused, the kernel folds each lane's units (8/G apart) with the step
-  // for that stride.
-  if (v.fast_mode == kFastTileTable && (!crc_fuse || tile_crc) && v.nt == 3 &&
-      a.piece_shift == 0 && (!nz.cell || env_int("ZH_ENC_TGROUP", -1) > 0)) {
+  // (ZH_ENC_TGROUP: 0 off; tiles_group_kernel).  With the tile CRC fused, the kernel folds
+  // each lane's units (8/G apart) with the step for that stride.
+  if (v.fast_mode == kFastTileTable && (!crc_fuse || tile_crc) && a.piece_shift == 0 &&
+      (!nz.cell || env_int("ZH_ENC_TGROUP", -1) > 0)) {
     const int want = env_int("ZH_ENC_TGROUP", -1);
     const int G = want < 0 ? 2 : want;
     if (G == 1 || G == 2 || G == 4) group = G;
     if (group && tile_crc) v.crc_tile_step = tile_crc_step(tile_ends, (size_t)(8 / group));
   }
   if (group) v.item_mul = env_int("ZH_ITEM_PERM", 1) ? golden_item_mul((items + group - 1) / group) : 0;
-  // grouped encode with the chunk CRC: ZH_ENC_CRC_STNT=0 stores the payloads through the cache
-  // (nt bit 4): a misaligned payload's line shared by two stores can merge in L2.  Default for
-  // the row groups (c3crc write 41.04 → 39.77 ms, profiles/r03/final/ab_write_stnt_c3crc.json);
-  // the tile groups keep non-temporal stores (c4crc 43.28 vs 43.66 ms cached)
-  const int stnt_def = v.fast_mode == kFastTileTable ? 1 : 0;
-  if (group && crc_fuse && v.nt == 3 && env_int("ZH_ENC_CRC_STNT", stnt_def) == 0) v.nt |= 16;
-  // grouped kernel: rows in flight per lane (2, 4, 8; G = 8 and the CRC variants: 4)
-  const int gu = group == 8 || crc_fuse ? 4 : env_int("ZH_ENC_GU", 4);
-  // tile groups: deep = 9 selects the prefetching form (ZH_ENC_TPF=1)
-  // 128-B rows, no fused CRC: 8 chunks per work item through the lane exchange
-  // (rows_xpose_kernel, ZH_ENC_XPOSE; deep = 20 selects it)
-  const bool xpose = group && v.fast_mode != kFastTileTable && !crc_fuse &&
-                     v.fast_vpr_shift == 3 && v.fast_rows % 8 == 0 && env_int("ZH_ENC_XPOSE", 0);
-  if (xpose && group != 8) {
-    group = 8;
-    v.item_mul = env_int("ZH_ITEM_PERM", 1) ? golden_item_mul((items + 7) / 8) : 0;
-  }
-  int grid = grid_for(ctx, group ? (items + group - 1) / group : pitems);
-  // tile groups with the chunk CRC: ZH_ENC_ROWCRC=1 selects the row-CRC encode (deep = 30;
-  // tiles_rowcrc_kernel<…, ENC>: every lane also CRCs one stored payload row from the tiles)
-  const bool enc_rowcrc = v.fast_mode == kFastTileTable && group && crc_fuse && tile_crc &&
-                          env_int("ZH_ENC_ROWCRC", 0) != 0 && zh::rowcrc_lds_at_zero();
-  // tile groups with the chunk CRC and c4's payload layout ([32 rows][units][32 words], unit u
-  // at 32u, region offsets u·xs): the row-CRC encode with 128-B aligned payload stores, one
-  // chunk per work item (tiles_rowcrc_enc_aln_kernel; ZH_ENC_ALIGN=1, ZH_ENC_ALIGN_PF=0/1)
-  bool enc_aln = false;
-  if (v.fast_mode == kFastTileTable && group && crc_fuse && tile_crc && v.nt == 3 &&
-      env_int("ZH_ENC_ALIGN", 0) != 0 && zh::rowcrc_lds_at_zero()) {
-    const int64_t nu = v.fast_n;
-    bool al = nu >= 16 && nu <= 32 && nu % 8 == 0 && v.rstride[v.fs] == 32 * nu &&
-              a.inner_nbytes == 4096 * nu && (int64_t)tab.size() >= 2 * nu;
-    const uint64_t xs = al ? tab[2] : 0;
-    for (int64_t u = 0; al && u < nu; u++)
-      al = tab[2 * (size_t)u + 1] == (uint32_t)(32 * u) && tab[2 * (size_t)u] == (uint64_t)u * xs &&
-           4 * (uint64_t)u * xs + 128 <= 0xFFFFFFFFull;
-    if (al) {
-      enc_aln = true;
-      group = 1;
-      v.tile_align = 1;
-      v.tile_ystride = (int64_t)xs;
-      v.crc_tile_step = tile_crc_step(tile_ends, 8);
-      v.item_mul = env_int("ZH_ITEM_PERM", 1) ? golden_item_mul(items) : 0;
-      grid = grid_for(ctx, items);
-    }
-  }
-  const int deep = xpose ? 20
-                   : enc_aln ? (env_int("ZH_ENC_ALIGN_PF", 1) ? 31 : 32)
-                   : enc_rowcrc ? 30
-                   : v.fast_mode == kFastTileTable && group && crc_fuse && tile_crc &&
-                             (env_int("ZH_ENC_CRCLOW", 0) || env_int("ZH_ENC_CRCFIELD", 0))
-                       ? (env_int("ZH_ENC_CRCFIELD", 0) ? 41 : 40)  // field / compact CRC tables
-                   : v.fast_mode == kFastTileTable && group ? (env_int("ZH_ENC_TPF", 0) ? 9 : 1)
-                   : group ? (gu <= 2 ? 0 : gu <= 4 ? 1 : 2)
-                           : env_int("ZH_ENC_DEEP", 1);
-  ZH_HIPF(launch_encode_fast(v, grid, deep, group, s));
+  const int grid = grid_for(ctx, group ? (items + group - 1) / group : pitems);
+  ZH_HIPF(launch_encode_fast(v, grid, group, s));
   ZH_HIPF(launch_encode_slow(a, grid, s));
   ZH_HIPF(launch_encode_finish(a, nz, cn, d_cnt, d_cdesc, s));
   if (!jobs.empty()) {

@@ -139,12 +139,11 @@ struct ScatterArgs {
   uint32_t* slow_count;
   int32_t dsize;
   int32_t tile;
-  int32_t nt;                   // fast kernels: bit 0 non-temporal loads, bit 1 stores
+  int32_t nt;                   // fast kernels: bit 0 non-temporal loads, bit 1 stores (the
+                                // launchers require 3: every kept kernel streams)
   int32_t tile_variant;         // tile fast path: 0 row-per-tile loads, 1 row-interleaved groups,
-                                // 10 + G / 20 + G: tiles_group_kernel (without / with prefetch);
-                                // 30 + G (+10, +20, +30): chunk CRC on waves of its own / over
-                                // LDS rows (ZH_DEC_CRCW)
-  int32_t lds_pad;              // extra dynamic LDS per block (ZH_LDS_PAD; occupancy lab only)
+                                // 20 + G: tiles_group_kernel over G chunks (next step's loads
+                                // prefetched); 51: the row-CRC tile kernel (chunk crc32c)
   int32_t row_group;            // row fast path (decode): G > 0 = rows_group_kernel over G
                                 // chunks per work item (row-clipped items then go slow)
   int32_t crc_extra;            // 4 when each stored chunk carries a trailing crc32c, else 0
@@ -226,7 +225,8 @@ hipError_t launch_data_crc_partial(const DataCrcArgs& a, int grid, hipStream_t s
 hipError_t launch_data_crc_finalize(const DataCrcArgs& a, hipStream_t stream);
 extern std::atomic<int64_t> g_last_fast_path;  // diagnostic, zh_debug_last_fast_path
 extern std::atomic<int64_t> g_last_encode_path;
-bool rowcrc_lds_at_zero();  // tiles_rowcrc_kernel has no static LDS
+bool rowcrc_lds_at_zero();  // the row-CRC tile kernels have no static LDS
+constexpr int kAlnUnitsMax = 32;  // tiles_rowcrc_aln_kernel: units per chunk (its K capacity)
 hipError_t launch_scatter(const ScatterArgs& a, int dsize, int tile_mode, int encode, int grid,
                           hipStream_t stream);
 hipError_t launch_decode_slow(const ScatterArgs& a, int grid, hipStream_t stream);
@@ -249,10 +249,9 @@ struct EncNest {
 hipError_t launch_encode_resolve(const ScatterArgs& a, const EncNest& nz, int64_t* item_off,
                                  int64_t base_off, int64_t cn, const uint8_t* vbase, int vfast,
                                  hipStream_t stream);
-// group > 1: encode_group_rows_kernel over groups of `group` consecutive chunks (row modes,
-// no fused CRC, piece_shift 0, group << fast_vpr_shift <= 64; view.item_mul over the groups)
-hipError_t launch_encode_fast(const ScatterArgs& view, int grid, int deep, int group,
-                              hipStream_t stream);
+// group > 0: the grouped kernels over groups of `group` consecutive chunks (piece_shift 0;
+// rows: group << fast_vpr_shift <= 64; view.item_mul over the groups)
+hipError_t launch_encode_fast(const ScatterArgs& view, int grid, int group, hipStream_t stream);
 hipError_t launch_encode_slow(const ScatterArgs& a, int grid, hipStream_t stream);
 hipError_t launch_encode_finish(const ScatterArgs& a, const EncNest& nz, int64_t chunk_nbytes,
                                 uint32_t* bad, ItemDesc* crc_desc, hipStream_t stream);

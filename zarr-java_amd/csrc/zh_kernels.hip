@@ -874,16 +874,13 @@ __constant__ uint32_t c_x2n[32] = {
 
 constexpr uint32_t kPoly = 0x82F63B78u;
 
-// a(x) * b(x) mod P (reflected bit order)
+// a(x) * b(x) mod P (reflected bit order).  The loop consumes a's bits from the top and stops
+// once none is left (at most 32 steps for any a, 0 included).  The LDS tables the CRC kernels
+// feed it from are laid out by compile-time constants checked with static_assert (kAln* below).
 __device__ __forceinline__ uint32_t multmodp(uint32_t a, uint32_t b) {
-  if (a == 0) return 0;  // (the loop below ends at a's lowest set bit: never for a = 0)
-  uint32_t m = 1u << 31, p = 0;
-  for (;;) {
-    if (a & m) {
-      p ^= b;
-      if ((a & (m - 1)) == 0) break;
-    }
-    m >>= 1;
+  uint32_t p = 0;
+  for (; a; a <<= 1) {
+    if (a & 0x80000000u) p ^= b;
     b = (b & 1) ? (b >> 1) ^ kPoly : b >> 1;
   }
   return p;
@@ -916,16 +913,7 @@ struct CrcTabs {
   uint32_t kfull[256];
   uint32_t kspan;
   uint32_t kidx[256];  // x^(8·kIdxSpan·j): span j of an index shifted past j later spans
-  // field tables (conflict-free lookups, tiles_group_kernel TABS = 2): F[j][f][v] =
-  // upd16(0, a 16-B vector whose word j is v << kFieldOff[f], the rest 0); fields of 5 bits
-  // (32 entries: 32 banks) and 4 bits (16 entries, padded to 32)
-  uint32_t F[4][7][32];
-  // the same for the serial 8-byte update of the row-CRC kernels (TABS = 2 / ZH_DEC_CRCFIELD):
-  // F8[i][f][v] = the register after 8 bytes from 0 whose word i is v << kFieldOff[f]
-  uint32_t F8[2][7][32];
 };
-constexpr int kFieldOff[7] = {0, 5, 10, 15, 20, 24, 28};
-constexpr int kFieldLen[7] = {5, 5, 5, 5, 4, 4, 4};
 
 constexpr uint32_t cx_mult(uint32_t a, uint32_t b) {  // a(x)·b(x) mod P, reflected
   uint32_t p = 0;
@@ -965,28 +953,6 @@ constexpr CrcTabs make_crc_tabs() {
   const uint32_t ki = cx_xpow8n(kIdxSpan);
   t.kidx[0] = 1u << 31;
   for (int j = 1; j < 256; j++) t.kidx[j] = cx_mult(ki, t.kidx[j - 1]);
-  for (int j = 0; j < 4; j++)
-    for (int f = 0; f < 7; f++)
-      for (uint32_t v = 0; v < 32; v++) {
-        const uint32_t w = v < (1u << kFieldLen[f]) ? v << kFieldOff[f] : 0u;
-        uint32_t c = 0;
-        for (int k = 0; k < 16; k++) {  // the vector's bytes in memory order
-          const uint32_t b = k / 4 == j ? (w >> (8 * (k % 4))) & 0xFFu : 0u;
-          c = t.T[0][(c ^ b) & 0xFFu] ^ (c >> 8);
-        }
-        t.F[j][f][v] = c;
-      }
-  for (int j = 0; j < 2; j++)
-    for (int f = 0; f < 7; f++)
-      for (uint32_t v = 0; v < 32; v++) {
-        const uint32_t w = v < (1u << kFieldLen[f]) ? v << kFieldOff[f] : 0u;
-        uint32_t c = 0;
-        for (int k = 0; k < 8; k++) {
-          const uint32_t b = k / 4 == j ? (w >> (8 * (k % 4))) & 0xFFu : 0u;
-          c = t.T[0][(c ^ b) & 0xFFu] ^ (c >> 8);
-        }
-        t.F8[j][f][v] = c;
-      }
   return t;
 }
 
@@ -1265,58 +1231,6 @@ __device__ __forceinline__ uint32_t crc_shift_k(uint32_t c, const uint32_t (*S)[
          tlook(S, 3, byte_x4<3>(c));
 }
 
-// Compact CRC tables (LOW = true in tiles_group_kernel: 5 KiB of LDS instead of 16 KiB):
-// slicing-by-4 over T[0..3] (4 dependent word rounds per 16-B vector, the same 16 lookups as
-// slicing-by-8) and shifts by nibble tables Sn[8][16] (Sn[i][n] = k·n·x^(4i): 8 lookups
-// instead of 4, 512 B instead of 4 KiB).  Tables at a constant LDS position, as crc_upd16_k.
-__device__ __forceinline__ uint32_t crc_upd4_k(uint32_t c, uint32_t w, const uint32_t (*T)[256]) {
-  const uint32_t x = c ^ w;
-  return xor3(tlook(T, 3, byte_x4<0>(x)), tlook(T, 2, byte_x4<1>(x)), tlook(T, 1, byte_x4<2>(x))) ^
-         tlook(T, 0, byte_x4<3>(x));
-}
-__device__ __forceinline__ uint32_t crc_upd16_s4(uint32_t c, v4u v, const uint32_t (*T)[256]) {
-  return crc_upd4_k(crc_upd4_k(crc_upd4_k(crc_upd4_k(c, v.x, T), v.y, T), v.z, T), v.w, T);
-}
-__device__ __forceinline__ uint32_t crc_shift_n(uint32_t c, const uint32_t (*Sn)[16]) {
-  // byte offset of entry (i, nibble i of c): 64·i + 4·nibble
-  auto at = [&](int i) {
-    const uint32_t off = (i == 0 ? (c << 2) : (c >> (4 * i - 2))) & 0x3Cu;
-    return *reinterpret_cast<const uint32_t*>(reinterpret_cast<const uint8_t*>(Sn[i]) + off);
-  };
-  return xor3(at(0), at(1), at(2)) ^ xor3(at(3), at(4), at(5)) ^ (at(6) ^ at(7));
-}
-
-// Field tables (TABS = 2 in tiles_group_kernel): every lookup indexes a table of at most 32
-// consecutive words, so the 32 lanes of a ds_read_b32 group hit distinct banks or the same
-// address (broadcast): no bank conflicts, where random byte indices into 256-entry tables
-// cost ≈2.4 LDS cycles per group.  28 lookups per 16-B vector (7 fields per word) and 7 per
-// shift, against 16 + 4 conflicting ones.  Table f of word j at byte 128·(7j + f).
-template <int F>
-__device__ __forceinline__ uint32_t field_off4(uint32_t w) {  // 4 · field F of w
-  constexpr int o = kFieldOff[F];
-  constexpr uint32_t m = ((1u << kFieldLen[F]) - 1) << 2;
-  if constexpr (o >= 2) return (w >> (o - 2)) & m;
-  else return (w << (2 - o)) & m;
-}
-__device__ __forceinline__ uint32_t fld(const uint8_t* tabs, int t, uint32_t off4) {
-  return *reinterpret_cast<const uint32_t*>(tabs + 128 * t + off4);
-}
-__device__ __forceinline__ uint32_t crc_word_fields(const uint8_t* tabs, int j, uint32_t w) {
-  const int b = 7 * j;
-  return xor3(fld(tabs, b + 0, field_off4<0>(w)), fld(tabs, b + 1, field_off4<1>(w)),
-              fld(tabs, b + 2, field_off4<2>(w))) ^
-         xor3(fld(tabs, b + 3, field_off4<3>(w)), fld(tabs, b + 4, field_off4<4>(w)),
-              fld(tabs, b + 5, field_off4<5>(w))) ^
-         fld(tabs, b + 6, field_off4<6>(w));
-}
-__device__ __forceinline__ uint32_t crc_upd16_f(v4u v, const uint8_t* F) {  // upd16(0, v)
-  return xor3(crc_word_fields(F, 0, v.x), crc_word_fields(F, 1, v.y), crc_word_fields(F, 2, v.z)) ^
-         crc_word_fields(F, 3, v.w);
-}
-__device__ __forceinline__ uint32_t crc_shift_f(uint32_t c, const uint8_t* Sf) {  // c · k
-  return crc_word_fields(Sf, 0, c);
-}
-
 // encode, grouped row kernel (write path, narrow rows): a work item is G consecutive inner
 // chunks — z-adjacent in the region when they sit in one shard row — and lane group q of
 // every G·vpr lanes moves chunk q.  A wave load then covers G·(row bytes) of one region row
@@ -1434,21 +1348,21 @@ __global__ __launch_bounds__(kBlock) void rows_group_kernel(ScatterArgs a) {
   }
 }
 
-// Grouped row kernel with a lane exchange (128-B rows, 8 chunks per work item, no CRC).
-// rows_group_kernel at G = 8 moves 1 KiB of contiguous region per wave instruction but stores
-// each chunk's rows from 8 lanes, 128 B to each of 8 payloads.  Here every wave instruction is
-// 1 KiB contiguous on both sides: a wave takes 8 rows of the 8 chunks, the region side in
-// layout A (lane = (chunk q, 16-B column), register = row) and the payload side in layout B
-// (lane = (row, column), register = chunk), and swaps layouts through LDS (8 KiB per wave;
-// rows 72 vectors apart, so the 16-lane groups of ds_read_b128 and the 8-lane groups of
-// ds_write_b128 hit distinct banks).  ENC: region rows (src, so) → payload (dst, dof), the
-// fill test on the loaded vectors; decode: payload (src, so) → region (dst, dof), full-fill
-// chunks store their fill value.  Each lane group reads its own chunk's descriptor; the
-// others come through readlane, so any chunk mix is correct (non-fast chunks stay on the slow
-// list).  Host: fast_vpr_shift == 3, piece_shift == 0, item_mul over groups of 8.
+// Grouped row kernel with a lane exchange (decode, 128-B rows, 8 chunks per work item, no
+// CRC).  rows_group_kernel at G = 8 moves 1 KiB of contiguous payload per wave instruction but
+// stores each chunk's rows from 8 lanes, 128 B to each of 8 region rows.  Here every wave
+// instruction is 1 KiB contiguous on both sides: a wave takes 8 rows of the 8 chunks, the
+// payload side in layout B (lane = (row, 16-B column), register = chunk) and the region side
+// in layout A (lane = (chunk q, column), register = row), and swaps layouts through LDS (8 KiB
+// per wave; rows 72 vectors apart, so the 16-lane groups of ds_read_b128 and the 8-lane groups
+// of ds_write_b128 hit distinct banks).  Full-fill chunks store their fill value.  Each lane
+// group reads its own chunk's descriptor; the others come through readlane, so any chunk mix
+// is correct (non-fast chunks stay on the slow list).  Host: fast_vpr_shift == 3,
+// piece_shift == 0, item_mul over groups of 8.  (The encode-view form measured slower, 9.09 →
+// 9.71 ms, and was removed in round 4.)
 constexpr int kXRow = 72;  // 16-B vectors per exchange row (64 + 8)
 
-template <int DS, bool ENC>
+template <int DS>
 __global__ __launch_bounds__(kBlock) void rows_xpose_kernel(ScatterArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   uint2* tab = reinterpret_cast<uint2*>(smem);
@@ -1474,30 +1388,15 @@ __global__ __launch_bounds__(kBlock) void rows_xpose_kernel(ScatterArgs a) {
       on = (y.z & kDescFast) != 0;
       sb = ((uint64_t)x.y << 32) | x.x;
       db = (uint64_t)(uintptr_t)(a.region + (int64_t)(((uint64_t)x.w << 32) | x.z) * DS);
-      if (!ENC) {
-        fill = (y.z & kDescModeMask) == kDescFullFill;
-        fv = fill16<DS>(((uint64_t)y.y << 32) | y.x);
-      }
+      fill = (y.z & kDescModeMask) == kDescFullFill;
+      fv = fill16<DS>(((uint64_t)y.y << 32) | y.x);
     }
     if (__syncthreads_or(on) == 0) continue;  // block-uniform: no fast chunk in the group
     const uint64_t onm = __ballot(on), fillm = __ballot(on && fill);
-    bool differs = false;
 #pragma unroll 1
     for (uint32_t rb = wave * 8; rb < nrows; rb += 32) {
       uint4 v[8];
-      if constexpr (ENC) {  // layout A loads: row rb + r of chunk hi
-#pragma unroll
-        for (int r = 0; r < 8; r++) {
-          uint64_t so, dof;
-          row_offsets(a, tab, rb + r, so, dof);
-          v[r] = ffill;
-          if (on && rb + r < nrows) v[r] = ld16s<true>((const uint8_t*)sb + so * DS + col * 16);
-          differs |= (v[r].x != ffill.x) | (v[r].y != ffill.y) | (v[r].z != ffill.z) |
-                     (v[r].w != ffill.w);
-        }
-#pragma unroll
-        for (int r = 0; r < 8; r++) xw[r * kXRow + hi * 8 + col] = v[r];
-      } else {  // layout B loads: row rb + hi of chunk k
+      {  // layout B loads: row rb + hi of chunk k
         uint64_t so, dof;
         row_offsets(a, tab, rb + hi, so, dof);
 #pragma unroll
@@ -1514,39 +1413,21 @@ __global__ __launch_bounds__(kBlock) void rows_xpose_kernel(ScatterArgs a) {
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      uint4 y[8];
-      if constexpr (ENC) {  // layout B: chunk k, row rb + hi
+      uint4 y[8];  // layout A: chunk hi, row rb + r
 #pragma unroll
-        for (int k = 0; k < 8; k++) y[k] = xw[hi * kXRow + k * 8 + col];
-      } else {  // layout A: chunk hi, row rb + r
-#pragma unroll
-        for (int r = 0; r < 8; r++) y[r] = xw[r * kXRow + hi * 8 + col];
-      }
+      for (int r = 0; r < 8; r++) y[r] = xw[r * kXRow + hi * 8 + col];
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      if constexpr (ENC) {  // layout B stores into chunk k's payload
+#pragma unroll
+      for (int r = 0; r < 8; r++) {  // layout A stores into chunk hi's region rows
         uint64_t so, dof;
-        row_offsets(a, tab, rb + hi, so, dof);
-#pragma unroll
-        for (int k = 0; k < 8; k++) {
-          const uint64_t d = ((uint64_t)__builtin_amdgcn_readlane((int)(db >> 32), k * 8) << 32) |
-                             (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)db, k * 8);
-          if ((onm >> (k * 8)) & 1 && rb + hi < nrows)
-            st16s<true>((uint8_t*)d + dof * DS + col * 16, xform16<DS>(y[k], a.swap, a.is_bool));
-        }
-      } else {  // layout A stores into chunk hi's region rows
-#pragma unroll
-        for (int r = 0; r < 8; r++) {
-          uint64_t so, dof;
-          row_offsets(a, tab, rb + r, so, dof);
-          if (on && rb + r < nrows)
-            st16s<true>((uint8_t*)db + dof * DS + col * 16,
-                        fill ? fv : xform16<DS>(y[r], a.swap, a.is_bool));
-        }
+        row_offsets(a, tab, rb + r, so, dof);
+        if (on && rb + r < nrows)
+          st16s<true>((uint8_t*)db + dof * DS + col * 16,
+                      fill ? fv : xform16<DS>(y[r], a.swap, a.is_bool));
       }
     }
-    if (ENC && (__ballot(differs) & (0xFFull << (hi * 8))) != 0 && col == 0 && on) a.flags[c] = 1;
   }
 }
 
@@ -1764,19 +1645,15 @@ __global__ __launch_bounds__(kBlock) void decode_tiles_kernel(ScatterArgs a) {
 //
 // PF: the next step's loads are issued before this step's stores (decode_tiles_body's order).
 //
-// TABS (CRC only): 0 the byte tables (T[8][256], S[4][256], SD[4][256]: 16 KiB);
-// 1 compact tables (crc_upd16_s4 / crc_shift_n: T[4][256], Sn[8][16], SDn[8][16], 5 KiB, so
-// that tiles + tables fit 4 workgroups per CU: 39.3 KB each, 50.5 KB with the byte tables);
-// 2 field tables (crc_upd16_f / crc_shift_f: F[4][7][32], Sf[7][32], SDf[7][32], 5.25 KiB, no
-// bank conflicts, 4 workgroups per CU).
-template <int NT, int G, bool CRC, bool PF, bool FLAGS, int TABS = 0>
+// CRC tables: T[8][256], S[4][256], SD[4][256] (16 KiB; 50.5 KB per workgroup with the
+// tiles, 3 per CU).  Compact slicing-by-4 tables (4 per CU) and conflict-free field tables
+// measured slower or equal (round 3, profiles/r03/g, profiles/r03/l) and were removed.
+template <int NT, int G, bool CRC, bool PF, bool FLAGS>
 __global__ __launch_bounds__(kBlock) void tiles_group_kernel(ScatterArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   // CRC: the tables first (T, S, SD: a constant LDS position for crc_upd16_k / crc_shift_k),
   // then K, the unit table and the tiles
-  constexpr bool LOW = TABS == 1, FLD = TABS == 2;
-  constexpr size_t kTabBytes = LOW ? 4 * 256 * 4 + 2 * 8 * 16 * 4
-                               : FLD ? (28 + 7 + 7) * 128 : 16 * 256 * 4;
+  constexpr size_t kTabBytes = 16 * 256 * 4;
   uint8_t* tab_at = CRC ? smem + ((kTabBytes + (size_t)a.fast_n * 4 + 15) & ~(size_t)15) : smem;
   uint2* tab = reinterpret_cast<uint2*>(tab_at);
   uint8_t* after_tab = tab_at + (((size_t)a.fast_n * 8 + 15) & ~(size_t)15);
@@ -1790,11 +1667,6 @@ __global__ __launch_bounds__(kBlock) void tiles_group_kernel(ScatterArgs a) {
   uint32_t(*T)[256] = nullptr;
   uint32_t(*S)[256] = nullptr;
   uint32_t(*SD)[256] = nullptr;
-  uint32_t(*Sn)[16] = nullptr;  // LOW
-  uint32_t(*SDn)[16] = nullptr;
-  const uint8_t* Ff = smem;      // FLD: F at 0, Sf at 3584, SDf at 4480
-  const uint8_t* Sf = smem + 28 * 128;
-  const uint8_t* SDf = smem + 35 * 128;
   uint32_t* K = nullptr;
   uint32_t kb = 0;
   if constexpr (CRC) {
@@ -1802,39 +1674,15 @@ __global__ __launch_bounds__(kBlock) void tiles_group_kernel(ScatterArgs a) {
     // payload row pitch of the lane's vectors: the stored rows (encode) or the loaded rows
     const int64_t pitch = FLAGS ? d_fs : s_fd;
     const uint32_t kg = x2nmodp((uint64_t)(4 * pitch), 3);
-    if constexpr (FLD) {
-      uint32_t* fw = reinterpret_cast<uint32_t*>(smem);
-      for (int i = threadIdx.x; i < 28 * 32; i += kBlock) fw[i] = (&g_crc.F[0][0][0])[i];
-      if (threadIdx.x < 7 * 32) {
-        const int f = threadIdx.x >> 5;
-        const uint32_t v = threadIdx.x & 31;
-        const uint32_t n = v < (1u << kFieldLen[f]) ? v << kFieldOff[f] : 0u;
-        fw[28 * 32 + threadIdx.x] = multmodp(kg, n);
-        fw[35 * 32 + threadIdx.x] = a.crc_tile_step ? multmodp(a.crc_tile_step, n) : 0u;
-      }
-      K = fw + 42 * 32;
-    } else if constexpr (LOW) {
-      Sn = reinterpret_cast<uint32_t(*)[16]>(smem + 4 * 256 * 4);
-      SDn = Sn + 8;
-      K = reinterpret_cast<uint32_t*>(SDn + 8);
+    S = T + 8;
+    SD = S + 4;
+    K = reinterpret_cast<uint32_t*>(SD + 4);
+    init_crc_tables(T);
 #pragma unroll
-      for (int k = 0; k < 4; k++) T[k][threadIdx.x] = g_crc.T[k][threadIdx.x];
-      if (threadIdx.x < 128) {
-        const uint32_t i = threadIdx.x >> 4, n = (uint32_t)(threadIdx.x & 15) << (4 * i);
-        Sn[i][threadIdx.x & 15] = multmodp(kg, n);
-        SDn[i][threadIdx.x & 15] = a.crc_tile_step ? multmodp(a.crc_tile_step, n) : 0u;
-      }
-    } else {
-      S = T + 8;
-      SD = S + 4;
-      K = reinterpret_cast<uint32_t*>(SD + 4);
-      init_crc_tables(T);
-#pragma unroll
-      for (int b = 0; b < 4; b++) {
-        S[b][threadIdx.x] = multmodp(kg, (uint32_t)threadIdx.x << (8 * b));
-        SD[b][threadIdx.x] =
-            a.crc_tile_step ? multmodp(a.crc_tile_step, (uint32_t)threadIdx.x << (8 * b)) : 0u;
-      }
+    for (int b = 0; b < 4; b++) {
+      S[b][threadIdx.x] = multmodp(kg, (uint32_t)threadIdx.x << (8 * b));
+      SD[b][threadIdx.x] =
+          a.crc_tile_step ? multmodp(a.crc_tile_step, (uint32_t)threadIdx.x << (8 * b)) : 0u;
     }
     for (int i = threadIdx.x; i < a.fast_n; i += kBlock) K[i] = a.fast_tab[2 * a.fast_n + i];
     kb = x2nmodp((uint64_t)(4 * (24 - 8 * wave) * pitch + 112 - 16 * g), 3);
@@ -1918,43 +1766,21 @@ __global__ __launch_bounds__(kBlock) void tiles_group_kernel(ScatterArgs a) {
           st16s<(NT & 2) != 0>(base + (size_t)r * d_fs * 4, y);
           if constexpr (CRC && FLAGS) {  // encode: the stored vectors
             const v4u w = {y.x, y.y, y.z, y.w};
-            if constexpr (FLD) {
-              const uint32_t ck = crc_upd16_f(w, Ff);
-              eacc = k ? crc_shift_f(eacc, Sf) ^ ck : ck;
-            } else if constexpr (LOW) {
-              const uint32_t ck = crc_upd16_s4(0u, w, T);
-              eacc = k ? crc_shift_n(eacc, Sn) ^ ck : ck;
-            } else {
-              const uint32_t ck = crc_upd16_k(0u, w, T);
-              eacc = k ? crc_shift_k(eacc, S) ^ ck : ck;
-            }
+            const uint32_t ck = crc_upd16_k(0u, w, T);
+            eacc = k ? crc_shift_k(eacc, S) ^ ck : ck;
           }
         }
         if constexpr (CRC && !FLAGS) {  // decode: the loaded payload vectors, stores in flight
 #pragma unroll
           for (int k = 0; k < 8; k++) {
             const v4u w = {xc[k].x, xc[k].y, xc[k].z, xc[k].w};
-            if constexpr (FLD) {
-              const uint32_t ck = crc_upd16_f(w, Ff);
-              eacc = k ? crc_shift_f(eacc, Sf) ^ ck : ck;
-            } else if constexpr (LOW) {
-              const uint32_t ck = crc_upd16_s4(0u, w, T);
-              eacc = k ? crc_shift_n(eacc, Sn) ^ ck : ck;
-            } else {
-              const uint32_t ck = crc_upd16_k(0u, w, T);
-              eacc = k ? crc_shift_k(eacc, S) ^ ck : ck;
-            }
+            const uint32_t ck = crc_upd16_k(0u, w, T);
+            eacc = k ? crc_shift_k(eacc, S) ^ ck : ck;
           }
         }
         if constexpr (CRC) {
           if (regular) {
-            uint32_t sh = 0;
-            if (ulast != ~0u) {
-              if constexpr (FLD) sh = crc_shift_f(run, SDf);
-              else if constexpr (LOW) sh = crc_shift_n(run, SDn);
-              else sh = crc_shift_k(run, SD);
-            }
-            run = sh ^ eacc;
+            run = (ulast != ~0u ? crc_shift_k(run, SD) : 0u) ^ eacc;
             ulast = u;
           } else {
             share ^= multmodp(K[u], eacc);
@@ -1969,156 +1795,6 @@ __global__ __launch_bounds__(kBlock) void tiles_group_kernel(ScatterArgs a) {
 #pragma unroll
       for (int o = TG * 4; o > 0; o >>= 1) cr ^= (uint32_t)__shfl_xor((int)cr, o, 64);
       if (leader && on) atomicXor(a.crc_partials + c, cr);
-    }
-  }
-}
-
-// decode, grouped tile kernel with the chunk CRC on waves of their own (ZH_DEC_CRCW).  A block
-// is 8 waves: waves 0-3 move tiles exactly as tiles_group_kernel<…, CRC = false, PF = true>
-// does, and waves 4-7 compute the crc32c of the same payload from the LDS tiles.  After the
-// barrier that publishes a step's tiles, CRC lane (cw, L) copies payload row r = L & 31 of
-// tile slot t = 2·cw + (L >> 5) (128 contiguous payload bytes; banks 33·(t + r) + j, distinct
-// within each 32-lane half) into registers; after the second barrier, while the movers write
-// the next step's tiles, it runs the plain slicing-by-8 update over those 128 bytes: 16
-// lookups per 16-B vector and no zero-shift, where the fused kernels pay 20 and hold the
-// movers' registers.  Row r of unit u ends (31 − r)·4·s_fd bytes before the unit end E_u, so
-// the lane's share is K[u]·x^(8·(31 − r)·4·s_fd)·row_crc; its units u, u + 8/G, … fold with SD
-// (regular layout) as in the fused kernels.  For G ≤ 4 a CRC wave's two tiles belong to one
-// chunk: one XOR-reduce and one atomic per wave.  LDS holds the byte-swapped words; the lanes
-// swap them back.
-//
-// PF = true: the movers prefetch the next step (more registers: held to 4 waves per SIMD, two
-// blocks per CU); PF = false: load, LDS, store, held to 6 waves per SIMD (three blocks).
-template <int G, bool PF>
-__global__ __launch_bounds__(2 * kBlock) __attribute__((amdgpu_waves_per_eu(PF ? 4 : 6)))
-void tiles_crcw_kernel(ScatterArgs a) {
-  static_assert(G == 1 || G == 2 || G == 4, "a CRC wave's tiles must belong to one chunk");
-  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-  uint2* tab = reinterpret_cast<uint2*>(smem);
-  uint8_t* after_tab = smem + (((size_t)a.fast_n * 8 + 15) & ~(size_t)15);
-  uint32_t* lds = reinterpret_cast<uint32_t*>(after_tab);
-  const int tid = threadIdx.x;
-  for (int i = tid; i < a.fast_n; i += 2 * kBlock) tab[i] = reinterpret_cast<const uint2*>(a.fast_tab)[i];
-  uint32_t(*T)[256] = reinterpret_cast<uint32_t(*)[256]>(after_tab + (size_t)kTG * kTilePitch * 4);
-  uint32_t(*SD)[256] = T + 12;  // same layout as the fused kernels (T, S, SD, K); S unused
-  uint32_t* K = reinterpret_cast<uint32_t*>(SD + 4);
-  if (tid < 256) {
-#pragma unroll
-    for (int k = 0; k < 8; k++) T[k][tid] = g_crc.T[k][tid];
-#pragma unroll
-    for (int b = 0; b < 4; b++)
-      SD[b][tid] = a.crc_tile_step ? multmodp(a.crc_tile_step, (uint32_t)tid << (8 * b)) : 0u;
-  }
-  for (int i = tid; i < a.fast_n; i += 2 * kBlock) K[i] = a.fast_tab[2 * a.fast_n + i];
-  __syncthreads();
-  constexpr int TG = kTG / G;  // tiles of each chunk per step
-  const bool crcw = tid >= kBlock;
-  const int wave = (tid >> 6) & 3, lane = tid & 63;
-  // movers: lane (t, g) moves tile t; CRC lanes: tile slot 2·wave + (lane >> 5), row lane & 31
-  const int t = crcw ? 2 * wave + (lane >> 5) : lane >> 3, g = lane & 7;
-  const int q = t / TG, ti = t % TG, r = lane & 31;
-  const int64_t s_fd = a.pstride[a.fd], d_fs = a.rstride[a.fs];
-  const bool regular = a.crc_tile_step != 0;
-  const uint32_t units = (uint32_t)a.fast_n;
-  const int64_t ngroups = (a.n_citems + G - 1) / G;
-  const uint32_t kr = crcw ? x2nmodp((uint64_t)(31 - r) * 4 * (uint64_t)s_fd, 3) : 0u;
-  uint32_t* mine = lds + t * kTilePitch;
-  for (int64_t gi = blockIdx.x; gi < ngroups; gi += gridDim.x) {
-    const int64_t pg = a.item_mul ? (int64_t)(((uint64_t)gi * a.item_mul) % (uint64_t)ngroups) : gi;
-    const int64_t c = pg * G + q;
-    bool on = false;
-    const uint8_t* src = nullptr;
-    uint8_t* dst = nullptr;
-    if (c < a.n_citems) {
-      const uint4* dp = reinterpret_cast<const uint4*>(a.desc + c);
-      const uint4 x = dp[0], y = dp[1];
-      on = (y.z & kDescFast) != 0;
-      src = (const uint8_t*)(uintptr_t)(((uint64_t)x.y << 32) | x.x);
-      dst = a.region + (int64_t)(((uint64_t)x.w << 32) | x.z) * 4;
-    }
-    if (__syncthreads_or(on) == 0) continue;  // block-uniform
-    if (!crcw) {  // movers (tiles_group_kernel's prefetching decode loop)
-      uint4 x[8];
-      auto load = [&](uint32_t ub_) {
-        const uint32_t uu = ub_ + ti;
-        if (on && uu < units) {
-          const uint8_t* base = src + ((size_t)tab[uu].x + g * 4) * 4;
-#pragma unroll
-          for (int k = 0; k < 8; k++)
-            x[k] = ld16s<true>(base + (size_t)(wave * 8 + k) * s_fd * 4);
-        }
-      };
-      if (PF) load(0);
-#pragma unroll 1
-      for (uint32_t ub = 0; ub < units; ub += TG) {
-        const uint32_t u = ub + ti;
-        const bool live = on && u < units;
-        if (live) {
-          if (!PF) load(ub);
-#pragma unroll
-          for (int k = 0; k < 8; k++) {
-            uint32_t* row = mine + (wave * 8 + k) * 33 + g * 4;
-            row[0] = xform1<4>(x[k].x, a.swap, 0);
-            row[1] = xform1<4>(x[k].y, a.swap, 0);
-            row[2] = xform1<4>(x[k].z, a.swap, 0);
-            row[3] = xform1<4>(x[k].w, a.swap, 0);
-          }
-        }
-        __syncthreads();
-        if (PF && ub + TG < units) load(ub + TG);
-        if (live) {
-          uint8_t* base = dst + ((size_t)tab[u].y + g * 4) * 4;
-#pragma unroll
-          for (int k = 0; k < 8; k++) {
-            const int rr = wave * 8 + k;
-            uint4 y;
-            y.x = mine[(g * 4 + 0) * 33 + rr];
-            y.y = mine[(g * 4 + 1) * 33 + rr];
-            y.z = mine[(g * 4 + 2) * 33 + rr];
-            y.w = mine[(g * 4 + 3) * 33 + rr];
-            st16s<true>(base + (size_t)rr * d_fs * 4, y);
-          }
-        }
-        __syncthreads();
-      }
-    } else {  // CRC waves
-      uint32_t share = 0, run = 0, ulast = ~0u;
-#pragma unroll 1
-      for (uint32_t ub = 0; ub < units; ub += TG) {
-        const uint32_t u = ub + ti;
-        const bool live = on && u < units;
-        __syncthreads();
-        uint32_t w[32];
-        if (live) {
-          const uint32_t* row = mine + r * 33;
-#pragma unroll
-          for (int j = 0; j < 32; j++) w[j] = row[j];
-        }
-        __syncthreads();
-        if (live) {
-          uint32_t acc = 0;
-#pragma unroll
-          for (int v = 0; v < 8; v++) {
-            v4u wv;
-            wv.x = xform1<4>(w[4 * v + 0], a.swap, 0);
-            wv.y = xform1<4>(w[4 * v + 1], a.swap, 0);
-            wv.z = xform1<4>(w[4 * v + 2], a.swap, 0);
-            wv.w = xform1<4>(w[4 * v + 3], a.swap, 0);
-            acc = crc_upd16(acc, wv, T);
-          }
-          if (regular) {
-            run = (ulast == ~0u ? 0u : crc_shift_tab(run, SD)) ^ acc;
-            ulast = u;
-          } else {
-            share ^= multmodp(K[u], acc);
-          }
-        }
-      }
-      if (regular && ulast != ~0u) share = multmodp(K[ulast], run);
-      uint32_t cr = multmodp(kr, share);
-#pragma unroll
-      for (int o = 32; o > 0; o >>= 1) cr ^= (uint32_t)__shfl_xor((int)cr, o, 64);
-      if (lane == 0 && on) atomicXor(a.crc_partials + c, cr);
     }
   }
 }
@@ -2147,21 +1823,7 @@ __device__ __forceinline__ uint32_t crc_upd8_lds(uint32_t c, uint32_t w0, uint32
   return xor3(a0, a1, a2);
 }
 
-// The same 8-byte step over conflict-free field tables F8 at LDS offset 0 (table f of word i at
-// byte 128·(7i + f); 14 lookups, no bank conflicts).  w0, w1 are raw payload words and c the
-// plain (unswapped) register.
-__device__ __forceinline__ uint32_t crc_word_fields_lds(int b, uint32_t w) {
-  return xor3(lds_word(128 * (b + 0) + field_off4<0>(w)), lds_word(128 * (b + 1) + field_off4<1>(w)),
-              lds_word(128 * (b + 2) + field_off4<2>(w))) ^
-         xor3(lds_word(128 * (b + 3) + field_off4<3>(w)), lds_word(128 * (b + 4) + field_off4<4>(w)),
-              lds_word(128 * (b + 5) + field_off4<5>(w))) ^
-         lds_word(128 * (b + 6) + field_off4<6>(w));
-}
-__device__ __forceinline__ uint32_t crc_upd8_fld(uint32_t c, uint32_t w0, uint32_t w1) {
-  return crc_word_fields_lds(0, w0 ^ c) ^ crc_word_fields_lds(7, w1);
-}
-
-// decode, grouped tile kernel with the chunk CRC over LDS rows (ZH_DEC_CRCW=3).  The kernel
+// decode, grouped tile kernel with the chunk CRC over LDS rows.  The kernel
 // must have no static LDS, since its tables are addressed from LDS offset 0: the host selects it
 // only when rowcrc_lds_at_zero() confirms that for every instantiation.  The lanes
 // move tiles as tiles_group_kernel<…, PF = true> does; for the CRC, lane i of the block takes
@@ -2169,15 +1831,14 @@ __device__ __forceinline__ uint32_t crc_upd8_fld(uint32_t c, uint32_t w0, uint32
 // the stores of a step, and runs the plain slicing-by-8 update over it after the barrier: 16
 // lookups per 16-B vector, no zero-shift (the fused kernel: 20), and no register copy of the
 // loaded vectors.  A lane's CRC row and the tile it moves may belong to different chunks of
-// the group; the CRC role reads its chunk's descriptor.  Shares as in tiles_crcw_kernel.
+// the group; the CRC role reads its chunk's descriptor.  Row r of unit u ends (31 − r)·4·s_fd
+// bytes before the unit end E_u, so the lane's share is K[u]·x^(8·(31 − r)·4·s_fd)·crc(row);
+// its units u, u + 8/G, … fold with SD (regular layout) as in the fused kernels.
 // SWAP (= a.swap, bytes(big) on uint32) is a template argument: the byte swap of the movers and
 // the CRC's byte order cost no select per word.  LDS: T, S (unused), SD, K, table, tiles.
-// ENC: the encode view (source = region rows, destination = payloads; the write path's
-// tiles_group_kernel<…, CRC, FLAGS> role): the movers load inside the live branch (no prefetch,
-// as the fused tile encode), test every loaded vector against fill_value (one flag byte per
-// chunk), and the LDS tiles then hold payload words, so payload row r of a tile is LDS column r
-// (banks (33·j + r) mod 32: distinct over a 32-lane half) and needs no swap back.
-template <int G, bool SWAP, bool ENC = false>
+// (The same kernel on the encode view measured slower than the fused tile encode, 44.73 vs
+// 43.57 ms, profiles/r03/v, and was removed in round 4.)
+template <int G, bool SWAP>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3)))
 void tiles_rowcrc_kernel(ScatterArgs a) {
   static_assert(G == 1 || G == 2 || G == 4, "a wave's CRC rows must belong to one chunk");
@@ -2191,9 +1852,8 @@ void tiles_rowcrc_kernel(ScatterArgs a) {
       reinterpret_cast<uint8_t*>(tab) + (((size_t)a.fast_n * 8 + 15) & ~(size_t)15));
   const int tid = threadIdx.x;
   for (int i = tid; i < a.fast_n; i += kBlock) tab[i] = reinterpret_cast<const uint2*>(a.fast_tab)[i];
-  constexpr bool CSW = SWAP && !ENC;  // the CRC reads byte-swapped words (decode, big endian)
 #pragma unroll
-  for (int k = 0; k < 8; k++) T[k][tid] = CSW ? __builtin_bswap32(g_crc.T[k][tid]) : g_crc.T[k][tid];
+  for (int k = 0; k < 8; k++) T[k][tid] = SWAP ? __builtin_bswap32(g_crc.T[k][tid]) : g_crc.T[k][tid];
 #pragma unroll
   for (int b = 0; b < 4; b++)
     SD[b][tid] = a.crc_tile_step ? multmodp(a.crc_tile_step, (uint32_t)tid << (8 * b)) : 0u;
@@ -2207,15 +1867,11 @@ void tiles_rowcrc_kernel(ScatterArgs a) {
   const bool regular = a.crc_tile_step != 0;
   const uint32_t units = (uint32_t)a.fast_n;
   const int64_t ngroups = (a.n_citems + G - 1) / G;
-  // payload row pitch: the loaded rows (decode) or the stored rows (encode view)
-  const uint32_t kr = x2nmodp((uint64_t)(31 - r) * 4 * (uint64_t)(ENC ? d_fs : s_fd), 3);
+  const uint32_t kr = x2nmodp((uint64_t)(31 - r) * 4 * (uint64_t)s_fd, 3);
   const uint32_t kq = regular && (uint32_t)tic < units
                           ? multmodp(kr, K[tic + (units - 1 - tic) / TG * TG]) : 0u;
   uint32_t* mine = lds + t * kTilePitch;
-  const uint32_t* crow = lds + tc * kTilePitch + (ENC ? r : r * 33);
-  const uint64_t qmask = (TG * 8 == 64 ? ~0ull : ((1ull << (TG * 8)) - 1)) << (q * TG * 8);
-  const bool leader = lane == q * TG * 8;
-  const uint32_t fillv = (uint32_t)a.fill;
+  const uint32_t* crow = lds + tc * kTilePitch + r * 33;
   auto sw = [](uint32_t x) { return SWAP ? __builtin_bswap32(x) : x; };
   for (int64_t gi = blockIdx.x; gi < ngroups; gi += gridDim.x) {
     const int64_t pg = a.item_mul ? (int64_t)(((uint64_t)gi * a.item_mul) % (uint64_t)ngroups) : gi;
@@ -2242,7 +1898,6 @@ void tiles_rowcrc_kernel(ScatterArgs a) {
       if ((f[0] | f[1] | f[2] | f[3]) == 0) continue;
     }
     uint32_t share = 0, run = 0, ulast = ~0u;
-    bool differs = false;
     uint4 x[8];
     auto load = [&](uint32_t ub_) {
       const uint32_t uu = ub_ + ti;
@@ -2252,17 +1907,14 @@ void tiles_rowcrc_kernel(ScatterArgs a) {
         for (int k = 0; k < 8; k++) x[k] = ld16s<true>(base + (size_t)(wave * 8 + k) * s_fd * 4);
       }
     };
-    if (!ENC) load(0);
+    load(0);
 #pragma unroll 1
     for (uint32_t ub = 0; ub < units; ub += TG) {
       const uint32_t u = ub + ti, uc = ub + tic;
       const bool live = on && u < units, livec = onc && uc < units;
       if (live) {
-        if (ENC) load(ub);
 #pragma unroll
         for (int k = 0; k < 8; k++) {
-          if (ENC)
-            differs |= (x[k].x != fillv) | (x[k].y != fillv) | (x[k].z != fillv) | (x[k].w != fillv);
           uint32_t* row = mine + (wave * 8 + k) * 33 + g * 4;
           row[0] = sw(x[k].x);
           row[1] = sw(x[k].y);
@@ -2271,7 +1923,7 @@ void tiles_rowcrc_kernel(ScatterArgs a) {
         }
       }
       __syncthreads();
-      if (!ENC && ub + TG < units) load(ub + TG);
+      if (ub + TG < units) load(ub + TG);
       if (live) {
         uint8_t* base = dst + ((size_t)tab[u].y + g * 4) * 4;
 #pragma unroll
@@ -2288,14 +1940,14 @@ void tiles_rowcrc_kernel(ScatterArgs a) {
       uint32_t w[32];
       if (livec) {
 #pragma unroll
-        for (int j = 0; j < 32; j++) w[j] = crow[ENC ? j * 33 : j];
+        for (int j = 0; j < 32; j++) w[j] = crow[j];
       }
       __syncthreads();
       if (livec) {
-        uint32_t acc = 0;  // byte-swapped with CSW
+        uint32_t acc = 0;  // byte-swapped with SWAP
 #pragma unroll
-        for (int j = 0; j < 32; j += 2) acc = crc_upd8_lds<CSW>(acc, w[j], w[j + 1]);
-        if (CSW) acc = __builtin_bswap32(acc);
+        for (int j = 0; j < 32; j += 2) acc = crc_upd8_lds<SWAP>(acc, w[j], w[j + 1]);
+        if (SWAP) acc = __builtin_bswap32(acc);
         if (regular) {
           run = (ulast == ~0u ? 0u : crc_shift_tab(run, SD)) ^ acc;
           ulast = uc;
@@ -2304,7 +1956,6 @@ void tiles_rowcrc_kernel(ScatterArgs a) {
         }
       }
     }
-    if (ENC && (__ballot(differs) & qmask) != 0 && leader && on) a.flags[c] = 1;
     // regular fold: the CRC role's last unit is tic + a multiple of TG in every fast chunk,
     // so its two end multiplies fold into the lane constant kq
     uint32_t cr = regular ? (ulast != ~0u ? multmodp(kq, run) : 0u) : multmodp(kr, share);
@@ -2313,6 +1964,21 @@ void tiles_rowcrc_kernel(ScatterArgs a) {
     if (lane == 0 && onc) atomicXor(a.crc_partials + cc, cr);
   }
 }
+
+// LDS layout of tiles_rowcrc_aln_kernel (bytes from the dynamic block's start, which is LDS 0:
+// rowcrc_lds_at_zero).  A region overlapping the next one corrupts a table; round 3's aligned
+// encode once put a ring row over K and spun a zero-K multiply, so the offsets are checked here
+// and the host checks fast_n ≤ kAlnKMax before it selects the kernel.
+constexpr int kAlnBoxAt = 8 * 256 * 4;                   // after T[8][256]
+constexpr int kAlnBoxWords = 31 * 32;                    // rows 0-30 of a 32-word line each
+constexpr int kAlnKAt = kAlnBoxAt + 4 * kAlnBoxWords;    // K[unit]
+constexpr int kAlnKMax = kAlnUnitsMax;                   // units per chunk (host: fast_n ≤ 32)
+constexpr int kAlnSDnAt = 12288;                         // SDn[8][16]
+constexpr int kAlnSlotsAt = kAlnSDnAt + 8 * 16 * 4;      // 9 tile slots
+static_assert(kAlnKAt + 4 * kAlnKMax <= kAlnSDnAt, "aligned row-CRC LDS: K overlaps SDn");
+static_assert(kAlnSDnAt % 16 == 0 && kAlnSlotsAt % 16 == 0, "aligned row-CRC LDS alignment");
+static_assert(kAlnSlotsAt + 9 * kTilePitch * 4 <= 160 * 1024 / 3,
+              "aligned row-CRC LDS: 3 workgroups per CU (160 KiB)");
 
 // decode, the row-CRC tile kernel over 128-B aligned lines (ZH_DEC_ALIGN; host: a.tile_align,
 // one chunk per work item, 16 ≤ fast_n ≤ 32 units, fast_n % 8 == 0, tab[u] = (32u, u·ystride)).
@@ -2337,26 +2003,18 @@ void tiles_rowcrc_kernel(ScatterArgs a) {
 // 50 852 B, 3 workgroups per CU (54 436 B, with byte tables, ran 2 per CU: 42.4 vs 36.4 ms, the
 // same as the unaligned kernel padded to that size, profiles/r03/occ).  Every lane reads the
 // same descriptor (G = 1): the skip is block-uniform.
-//
-// FLD (ZH_DEC_CRCFIELD=1, a.tile_align == 2): the row CRC over the conflict-free field tables
-// F8 (crc_upd8_fld: 14 lookups per 8 bytes, no bank conflicts) on raw words, in the T area.
-template <bool SWAP, bool FLD = false>
+template <bool SWAP>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3)))
 void tiles_rowcrc_aln_kernel(ScatterArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   uint32_t(*T)[256] = reinterpret_cast<uint32_t(*)[256]>(smem);
-  uint32_t* const box = T[8];
-  uint32_t* const K = T[8] + 992;
-  uint32_t(*SDn)[16] = reinterpret_cast<uint32_t(*)[16]>(smem + 12288);
-  uint32_t* const lds = reinterpret_cast<uint32_t*>(smem + 12800);
+  uint32_t* const box = reinterpret_cast<uint32_t*>(smem + kAlnBoxAt);
+  uint32_t* const K = reinterpret_cast<uint32_t*>(smem + kAlnKAt);
+  uint32_t(*SDn)[16] = reinterpret_cast<uint32_t(*)[16]>(smem + kAlnSDnAt);
+  uint32_t* const lds = reinterpret_cast<uint32_t*>(smem + kAlnSlotsAt);
   const int tid = threadIdx.x;
-  if constexpr (FLD) {
-    for (int i = tid; i < 2 * 7 * 32; i += kBlock)
-      reinterpret_cast<uint32_t*>(smem)[i] = (&g_crc.F8[0][0][0])[i];
-  } else {
 #pragma unroll
-    for (int k = 0; k < 8; k++) T[k][tid] = SWAP ? __builtin_bswap32(g_crc.T[k][tid]) : g_crc.T[k][tid];
-  }
+  for (int k = 0; k < 8; k++) T[k][tid] = SWAP ? __builtin_bswap32(g_crc.T[k][tid]) : g_crc.T[k][tid];
   if (tid < 128)
     SDn[tid >> 4][tid & 15] =
         a.crc_tile_step ? multmodp(a.crc_tile_step, (uint32_t)(tid & 15) << (4 * (tid >> 4))) : 0u;
@@ -2483,16 +2141,9 @@ void tiles_rowcrc_aln_kernel(ScatterArgs a) {
       }
       __syncthreads();
       uint32_t acc = 0;  // byte-swapped with SWAP (byte tables)
-      if constexpr (FLD) {
 #pragma unroll
-        for (int j = 0; j < 32; j += 2)
-          acc = crc_upd8_fld(acc, SWAP ? __builtin_bswap32(w[j]) : w[j],
-                             SWAP ? __builtin_bswap32(w[j + 1]) : w[j + 1]);
-      } else {
-#pragma unroll
-        for (int j = 0; j < 32; j += 2) acc = crc_upd8_lds<SWAP>(acc, w[j], w[j + 1]);
-        if (SWAP) acc = __builtin_bswap32(acc);
-      }
+      for (int j = 0; j < 32; j += 2) acc = crc_upd8_lds<SWAP>(acc, w[j], w[j + 1]);
+      if (SWAP) acc = __builtin_bswap32(acc);
       const uint32_t uc = ub + tc;
       if (regular) {
         uint32_t sh = 0;  // run · x^(8Δ), nibble by nibble
@@ -2506,181 +2157,6 @@ void tiles_rowcrc_aln_kernel(ScatterArgs a) {
       sb = sb == 0 ? 8 : sb - 1;
     }
     uint32_t cr = regular ? multmodp(kq, run) : multmodp(kr, share);
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) cr ^= (uint32_t)__shfl_xor((int)cr, o, 64);
-    if (lane == 0) atomicXor(a.crc_partials + c, cr);
-  }
-}
-
-// encode, the row-CRC tile kernel with 128-B aligned payload stores (ZH_ENC_ALIGN; host:
-// a.tile_align on the encode view, one chunk per work item, 16 ≤ fast_n ≤ 32, fast_n % 8 == 0,
-// tab[u] = (u·tile_ystride region, 32u payload), payload rows following each other).  The
-// encode mirror of tiles_rowcrc_aln_kernel: the movers load region rows into the tiles (the
-// fill test on the way), the tiles then hold payload words (payload row r, word w at w·33 + r),
-// and each wave instruction stores 8 whole payload lines: lane λ stores 16 B at 16λ from the
-// first line of L(r, s), words e = 4λ + j − δ/4 of L(r, s).  Words e < 0 are the end of
-// L(r, s − 1), still in the ring (step s − 1's tile 7 is slot (8s + 8) mod 9, which step s
-// does not write).  Line 0 of L(r, 0) also holds the end of row r − 1: lanes 0-7 keep it in
-// the box at step 0 and lanes 0-7 store it at the last step as line 8 of row r − 1 (tile 7's
-// words, then the box's); row 0's first line and row 31's last line are shared with the
-// neighbouring chunks (and the chunk's crc32c, stored later) and take dword stores of their own
-// words only.  Every payload line is written once, whole, by one store (the unaligned encode
-// wrote 1.059× the payload bytes, PMC).  PF: the next step's region loads are issued after the
-// first barrier (the decode's order).  CRC as tiles_rowcrc_kernel<…, ENC> (plain tables: the
-// tiles hold payload words); LDS as tiles_rowcrc_aln_kernel (50 852 B).
-template <bool SWAP, bool PF>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3)))
-void tiles_rowcrc_enc_aln_kernel(ScatterArgs a) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-  uint32_t(*T)[256] = reinterpret_cast<uint32_t(*)[256]>(smem);
-  uint32_t* const box = T[8];
-  uint32_t* const K = T[8] + 992;
-  uint32_t(*SDn)[16] = reinterpret_cast<uint32_t(*)[16]>(smem + 12288);
-  uint32_t* const lds = reinterpret_cast<uint32_t*>(smem + 12800);
-  const int tid = threadIdx.x;
-#pragma unroll
-  for (int k = 0; k < 8; k++) T[k][tid] = g_crc.T[k][tid];
-  if (tid < 128)
-    SDn[tid >> 4][tid & 15] =
-        a.crc_tile_step ? multmodp(a.crc_tile_step, (uint32_t)(tid & 15) << (4 * (tid >> 4))) : 0u;
-  for (int i = tid; i < a.fast_n; i += kBlock) K[i] = a.fast_tab[2 * a.fast_n + i];
-  __syncthreads();
-  const int wave = tid >> 6, lane = tid & 63, t = lane >> 3, g = lane & 7;
-  const int wv = __builtin_amdgcn_readfirstlane(wave);
-  const int tc = tid >> 5, r = tid & 31;  // CRC role
-  const int64_t s_fd = a.pstride[a.fd], d_fs = a.rstride[a.fs];  // region row, payload row pitch
-  const bool regular = a.crc_tile_step != 0;
-  const uint32_t units = (uint32_t)a.fast_n, xs = (uint32_t)a.tile_ystride;
-  const uint32_t kr = x2nmodp((uint64_t)(31 - r) * 4 * (uint64_t)d_fs, 3);
-  const uint32_t fillv = (uint32_t)a.fill;
-  auto sw = [](uint32_t v) { return SWAP ? __builtin_bswap32(v) : v; };
-  auto rfl = [](uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); };
-  for (int64_t gi = blockIdx.x; gi < a.n_citems; gi += gridDim.x) {
-    const int64_t c = a.item_mul ? (int64_t)(((uint64_t)gi * a.item_mul) % (uint64_t)a.n_citems) : gi;
-    const uint4* dp = reinterpret_cast<const uint4*>(a.desc + c);
-    const uint4 dx = dp[0], dy = dp[1];
-    if ((rfl(dy.z) & kDescFast) == 0) continue;  // block-uniform
-    const uint8_t* src = (const uint8_t*)(uintptr_t)(((uint64_t)rfl(dx.y) << 32) | rfl(dx.x));
-    uint8_t* dst = a.region + (int64_t)(((uint64_t)rfl(dx.w) << 32) | rfl(dx.z)) * 4;
-    const uint32_t dl = (uint32_t)(uintptr_t)dst & 127u;
-    const int Dp = (int)(dl >> 2);  // δ/4 (0: aligned, no held or extra line)
-    uint8_t* const A = dst - dl;
-    bool differs = false;
-    uint4 x[8];
-    auto load = [&](uint32_t ub) {
-      const uint32_t voff = ((ub + t) * xs + 4 * g) * 4;
-#pragma unroll
-      for (int k = 0; k < 8; k++) x[k] = ld16g(src + (size_t)(wv * 8 + k) * s_fd * 4, voff);
-    };
-    if (PF) load(0);
-    uint32_t share = 0, run = 0, ulast = ~0u;
-    int sb = 0;  // slot of this step's tile 0: (8s) mod 9
-#pragma unroll 1
-    for (uint32_t ub = 0; ub < units; ub += kTG) {
-      const bool last = ub + kTG >= units;
-      if (!PF) load(ub);
-      {  // the fill test and the tiles (region row rr of tile t: words 4g..4g+3)
-        int st = sb + t;
-        st -= st >= 9 ? 9 : 0;
-        uint32_t* mine = lds + st * kTilePitch;
-#pragma unroll
-        for (int k = 0; k < 8; k++) {
-          differs |= (x[k].x != fillv) | (x[k].y != fillv) | (x[k].z != fillv) | (x[k].w != fillv);
-          uint32_t* row = mine + (wave * 8 + k) * 33 + g * 4;
-          row[0] = sw(x[k].x);
-          row[1] = sw(x[k].y);
-          row[2] = sw(x[k].z);
-          row[3] = sw(x[k].w);
-        }
-      }
-      __syncthreads();
-      if (PF && !last) load(ub + kTG);
-      {  // whole payload lines: lane λ, words e = 4λ + j − δ/4 of L(rr, s) (e < 0: step s − 1)
-        int e1 = 32 - Dp + 4 * lane;  // e + 32
-        asm volatile("" : "+v"(e1));
-        int wa[4];
-#pragma unroll
-        for (int j = 0; j < 4; j++) {
-          const int e = e1 + j;
-          int sl = sb + 8 + (e >> 5);
-          sl -= sl >= 9 ? 9 : 0;
-          sl -= sl >= 9 ? 9 : 0;
-          wa[j] = sl * kTilePitch + (e & 31) * 33;
-        }
-        const bool hold = dl && ub == 0 && t == 0;  // line 0 of row rr: at the last step
-#pragma unroll
-        for (int k = 0; k < 8; k++) {
-          const int rr = wv * 8 + k;
-          uint4 y;
-          y.x = lds[wa[0] + rr];
-          y.y = lds[wa[1] + rr];
-          y.z = lds[wa[2] + rr];
-          y.w = lds[wa[3] + rr];
-          uint8_t* row = A + (size_t)rr * d_fs * 4 + (size_t)ub * 128;
-          if (!hold) {
-            st16g(row, (uint32_t)(16 * lane), y);
-          } else {
-            // row rr's line 0 in box row rr − 1 (box rows 0-30: K sits after them)
-            if (rr > 0) *reinterpret_cast<uint4*>(box + (rr - 1) * 32 + 4 * g) = y;
-            if (rr == 0) {  // the chunk's first line: its own words only
-              const uint32_t yv[4] = {y.x, y.y, y.z, y.w};
-#pragma unroll
-              for (int j = 0; j < 4; j++)
-                if (4 * g + j >= Dp) reinterpret_cast<uint32_t*>(row + 16 * g)[j] = yv[j];
-            }
-          }
-        }
-        if (dl && last && t == 0) {  // line 8 of L(rr, last) = line 0 of row rr + 1
-          int st7 = sb + 7;
-          st7 -= st7 >= 9 ? 9 : 0;
-#pragma unroll
-          for (int k = 0; k < 8; k++) {
-            const int rr = wv * 8 + k;
-            uint32_t v[4];
-#pragma unroll
-            for (int j = 0; j < 4; j++) {
-              const int d = 4 * g + j;
-              v[j] = d < Dp ? lds[st7 * kTilePitch + (32 - Dp + d) * 33 + rr]
-                            : (rr < 31 ? box[rr * 32 + d] : 0u);
-            }
-            uint8_t* nxt = A + (size_t)(rr + 1) * d_fs * 4 + 16 * g;
-            if (rr < 31) {
-              st16g(A + (size_t)(rr + 1) * d_fs * 4, (uint32_t)(16 * g), make_uint4(v[0], v[1], v[2], v[3]));
-            } else {  // the chunk's last line: the payload's last words only
-#pragma unroll
-              for (int j = 0; j < 4; j++)
-                if (4 * g + j < Dp) reinterpret_cast<uint32_t*>(nxt)[j] = v[j];
-            }
-          }
-        }
-      }
-      uint32_t w[32];
-      {
-        int sc = sb + tc;
-        sc -= sc >= 9 ? 9 : 0;
-        const uint32_t* crow = lds + sc * kTilePitch + r;
-#pragma unroll
-        for (int j = 0; j < 32; j++) w[j] = crow[j * 33];
-      }
-      __syncthreads();
-      uint32_t acc = 0;
-#pragma unroll
-      for (int j = 0; j < 32; j += 2) acc = crc_upd8_lds<false>(acc, w[j], w[j + 1]);
-      const uint32_t uc = ub + tc;
-      if (regular) {
-        uint32_t sh = 0;
-#pragma unroll
-        for (int i = 0; i < 8; i++) sh ^= SDn[i][(run >> (4 * i)) & 15];
-        run = (ulast == ~0u ? 0u : sh) ^ acc;
-        ulast = uc;
-      } else {
-        share ^= multmodp(K[uc], acc);
-      }
-      sb = sb == 0 ? 8 : sb - 1;
-    }
-    if (__ballot(differs) != 0 && lane == 0) a.flags[c] = 1;
-    if (regular && ulast != ~0u) share = multmodp(K[ulast], run);
-    uint32_t cr = multmodp(kr, share);
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) cr ^= (uint32_t)__shfl_xor((int)cr, o, 64);
     if (lane == 0) atomicXor(a.crc_partials + c, cr);
@@ -3011,12 +2487,13 @@ __device__ uint32_t lanes_to_span_crc(uint32_t c, int64_t lb, int64_t llen, int6
 // it (status == nullptr: Crc32cCodec.encode :50-60).  A dword-aligned span is read as
 // coalesced 16-byte vectors (lane l: vectors l, l+256, ...) with the lane-interleaved update;
 // otherwise with a per-lane slicing-by-8 byte loop.
-// The combine of one job's span partials (the last workgroup of crc_index_kernel, or one
-// workgroup per job of crc_index_combine_kernel): shift every span register to the index end,
-// XOR, finish the CRC, then compare it with the stored one (read) or store it (write path).
+// The combine of one job's span partials (the last workgroup of crc_index_kernel): shift every
+// span register to the index end, XOR, finish the CRC, then compare it with the stored one
+// (read) or store it (write path).  (A second launch for the combine, without the per-workgroup
+// device-scope release of the completion counter, measured slower: 74.2 vs 69.7 µs per small
+// read, profiles/r03/q; removed in round 4.)
 __device__ __forceinline__ void crc_index_finish(const CrcJob& J, const uint32_t* partials,
-                                                 int sshift, uint64_t* status, uint32_t* red,
-                                                 bool atomic_loads) {
+                                                 int sshift, uint64_t* status, uint32_t* red) {
   const int tid = threadIdx.x;
   const int64_t SPAN = (int64_t)kIdxSpan << sshift;
   const int64_t njs = (J.len + SPAN - 1) / SPAN;
@@ -3026,10 +2503,8 @@ __device__ __forceinline__ void crc_index_finish(const CrcJob& J, const uint32_t
   const uint32_t xtail = tail == SPAN ? g_crc.kidx[1 << sshift] : x2nmodp((uint64_t)tail, 3);
   uint32_t r = 0;
   for (int64_t k = tid; k < njs; k += kBlock) {
-    const uint32_t pk = atomic_loads
-                            ? __hip_atomic_load(partials + J.span_begin + k, __ATOMIC_RELAXED,
-                                                __HIP_MEMORY_SCOPE_AGENT)
-                            : partials[J.span_begin + k];
+    const uint32_t pk = __hip_atomic_load(partials + J.span_begin + k, __ATOMIC_RELAXED,
+                                          __HIP_MEMORY_SCOPE_AGENT);
     const int64_t j = (njs - 2 - k) << sshift;  // 4 KiB units of the full spans after span k
     uint32_t sh;
     if (k == njs - 1) sh = 1u << 31;
@@ -3064,13 +2539,10 @@ __device__ __forceinline__ void crc_index_finish(const CrcJob& J, const uint32_t
   }
 }
 
-// split (ZH_CRC_SPLIT): every workgroup only stores its span partial; crc_index_combine_kernel
-// (one workgroup per job, the next launch) combines them, so no workgroup takes the
-// device-scope release (a buffer_wbl2 + buffer_inv per workgroup) of the completion counter.
 __global__ __launch_bounds__(kBlock) void crc_index_kernel(const CrcJob* jobs, int64_t njobs,
                                                            int64_t nspans, int sshift,
                                                            uint32_t* partials,
-                                                           uint64_t* status, int split) {
+                                                           uint64_t* status) {
   const int64_t SPAN = (int64_t)kIdxSpan << sshift;
   __shared__ uint32_t T[8][256];
   __shared__ uint32_t S[4][256];
@@ -3139,10 +2611,6 @@ __global__ __launch_bounds__(kBlock) void crc_index_kernel(const CrcJob* jobs, i
     __syncthreads();
     raw = red[0] ^ red[1] ^ red[2] ^ red[3];
   }
-  if (split) {  // the combine runs as the next launch
-    if (tid == 0) partials[span] = raw;
-    return;
-  }
   uint32_t* counter = partials + nspans + lo;
   const int64_t njs = (J.len + SPAN - 1) / SPAN;
   if (tid == 0) {
@@ -3154,14 +2622,7 @@ __global__ __launch_bounds__(kBlock) void crc_index_kernel(const CrcJob* jobs, i
   if (!last) return;  // uniform
   __threadfence();
   if (tid == 0) *counter = 0;  // ready for the next launch (every other workgroup has counted)
-  crc_index_finish(J, partials, sshift, status, red, true);
-}
-
-__global__ __launch_bounds__(kBlock) void crc_index_combine_kernel(const CrcJob* jobs, int sshift,
-                                                                   const uint32_t* partials,
-                                                                   uint64_t* status) {
-  __shared__ uint32_t red[kBlock];
-  crc_index_finish(jobs[blockIdx.x], partials, sshift, status, red, false);
+  crc_index_finish(J, partials, sshift, status, red);
 }
 
 // (crc_upd16 / crc_shift_tab: see "CRC-32C helpers" above the row kernel)
@@ -3492,13 +2953,8 @@ hipError_t launch_data_crc(const DataCrcArgs& a, int grid, hipStream_t stream) {
 hipError_t launch_crc(const CrcJob* jobs, int64_t njobs, int64_t nspans, int span_shift,
                       uint32_t* partials, uint64_t* status, hipStream_t stream) {
   if (njobs == 0) return hipSuccess;
-  const char* e = getenv("ZH_CRC_SPLIT");  // A/B switch, read per launch
-  const int split = e && e[0] == '1' ? 1 : 0;
   hipLaunchKernelGGL(crc_index_kernel, dim3((unsigned)nspans), dim3(kBlock), 0, stream, jobs,
-                     njobs, nspans, span_shift, partials, status, split);
-  if (split)
-    hipLaunchKernelGGL(crc_index_combine_kernel, dim3((unsigned)njobs), dim3(kBlock), 0, stream,
-                       jobs, span_shift, (const uint32_t*)partials, status);
+                     njobs, nspans, span_shift, partials, status);
   return hipGetLastError();
 }
 
@@ -3517,160 +2973,78 @@ static void launch_scatter_ds(const ScatterArgs& a, int tile, int enc, int grid,
       hipLaunchKernelGGL((encode_kernel<DS, true>), dim3(grid), dim3(kBlock), 0, s, a);
     else
       hipLaunchKernelGGL((encode_kernel<DS, false>), dim3(grid), dim3(kBlock), 0, s, a);
-  } else {
-    size_t lds = ((size_t)a.fast_n * 8 + 15) & ~(size_t)15;
-    const int nt = a.nt & 3;  // streaming cache policy (per plan)
-    if (a.fast_mode == kFastTileTable) {
-      if (DS == 4) {
-        const int v = a.tile_variant;
-        lds += v == 0 ? (size_t)kFastTPB * 32 * 33 * 4 : (size_t)kTG * kTilePitch * 4;
-        const bool ntx = nt == 3;
-        if (v > 30 && a.crc_fused) {  // chunk CRC on waves of its own (ZH_DEC_CRCW=1, 2)
-          const size_t lc = lds + 16 * 256 * 4 + (size_t)a.fast_n * 4;
-          switch (v - 30) {
-            case 1: hipLaunchKernelGGL((tiles_crcw_kernel<1, true>), dim3(grid), dim3(2 * kBlock), lc, s, a); return;
-            case 2: hipLaunchKernelGGL((tiles_crcw_kernel<2, true>), dim3(grid), dim3(2 * kBlock), lc, s, a); return;
-            case 4: hipLaunchKernelGGL((tiles_crcw_kernel<4, true>), dim3(grid), dim3(2 * kBlock), lc, s, a); return;
-            case 11: hipLaunchKernelGGL((tiles_crcw_kernel<1, false>), dim3(grid), dim3(2 * kBlock), lc, s, a); return;
-            case 12: hipLaunchKernelGGL((tiles_crcw_kernel<2, false>), dim3(grid), dim3(2 * kBlock), lc, s, a); return;
-            case 14: hipLaunchKernelGGL((tiles_crcw_kernel<4, false>), dim3(grid), dim3(2 * kBlock), lc, s, a); return;
-            case 21:
-              if (a.tile_align) {  // LDS: tables 12.5 KiB + 9 slots (the host checked the rest)
-                const size_t la = 12800 + (size_t)9 * kTilePitch * 4;
-                if (a.tile_align == 2) {  // field tables (ZH_DEC_CRCFIELD)
-                  if (a.swap) hipLaunchKernelGGL((tiles_rowcrc_aln_kernel<true, true>), dim3(grid), dim3(kBlock), la, s, a);
-                  else hipLaunchKernelGGL((tiles_rowcrc_aln_kernel<false, true>), dim3(grid), dim3(kBlock), la, s, a);
-                  return;
-                }
-                if (a.swap) hipLaunchKernelGGL((tiles_rowcrc_aln_kernel<true>), dim3(grid), dim3(kBlock), la, s, a);
-                else hipLaunchKernelGGL((tiles_rowcrc_aln_kernel<false>), dim3(grid), dim3(kBlock), la, s, a);
-                return;
-              }
-              if (a.swap) hipLaunchKernelGGL((tiles_rowcrc_kernel<1, true>), dim3(grid), dim3(kBlock), lc + 64 + a.lds_pad, s, a); else hipLaunchKernelGGL((tiles_rowcrc_kernel<1, false>), dim3(grid), dim3(kBlock), lc + 64 + a.lds_pad, s, a); return;
-            case 22: if (a.swap) hipLaunchKernelGGL((tiles_rowcrc_kernel<2, true>), dim3(grid), dim3(kBlock), lc + 64, s, a); else hipLaunchKernelGGL((tiles_rowcrc_kernel<2, false>), dim3(grid), dim3(kBlock), lc + 64, s, a); return;
-            case 24: if (a.swap) hipLaunchKernelGGL((tiles_rowcrc_kernel<4, true>), dim3(grid), dim3(kBlock), lc + 64, s, a); else hipLaunchKernelGGL((tiles_rowcrc_kernel<4, false>), dim3(grid), dim3(kBlock), lc + 64, s, a); return;
-            default: return;
-          }
+    return;
+  }
+  // Every decode fast kernel streams non-temporal loads and stores (host: nt & 3 == 3); the
+  // host picks the kernel (tile_variant, row_group, crc_fused, tile_align) and checks the LDS
+  // layout each one assumes (check_lds_layouts).
+  size_t lds = ((size_t)a.fast_n * 8 + 15) & ~(size_t)15;
+  if (a.fast_mode == kFastTileTable) {
+    if constexpr (DS == 4) {
+      const int v = a.tile_variant;
+      lds += v == 0 ? (size_t)kFastTPB * 32 * 33 * 4 : (size_t)kTG * kTilePitch * 4;
+      if (v == 51 && a.crc_fused) {  // the row-CRC tile kernel, one chunk per work item
+        if (a.tile_align) {  // LDS: tables 12.5 KiB + 9 slots (the host checked the rest)
+          const size_t la = kAlnSlotsAt + (size_t)9 * kTilePitch * 4;
+          if (a.swap) hipLaunchKernelGGL((tiles_rowcrc_aln_kernel<true>), dim3(grid), dim3(kBlock), la, s, a);
+          else hipLaunchKernelGGL((tiles_rowcrc_aln_kernel<false>), dim3(grid), dim3(kBlock), la, s, a);
+          return;
         }
-        if (v > 20 && a.crc_fused) {  // prefetching form (ZH_DEC_TPF=1)
-          const size_t lc = lds + 16 * 256 * 4 + (size_t)a.fast_n * 4 + 64;  // + alignment
-          switch (v - 20) {
-            case 1: hipLaunchKernelGGL((tiles_group_kernel<3, 1, true, true, false>), dim3(grid), dim3(kBlock), lc, s, a); return;
-            case 2: hipLaunchKernelGGL((tiles_group_kernel<3, 2, true, true, false>), dim3(grid), dim3(kBlock), lc, s, a); return;
-            case 4: hipLaunchKernelGGL((tiles_group_kernel<3, 4, true, true, false>), dim3(grid), dim3(kBlock), lc, s, a); return;
-            default: return;
-          }
-        }
-        if (v > 20) {
-          lds += (size_t)a.lds_pad;  // occupancy lab (ZH_LDS_PAD), 0 by default
-          switch (v - 20) {
-            case 1: hipLaunchKernelGGL((tiles_group_kernel<3, 1, false, true, false>), dim3(grid), dim3(kBlock), lds, s, a); return;
-            case 2: hipLaunchKernelGGL((tiles_group_kernel<3, 2, false, true, false>), dim3(grid), dim3(kBlock), lds, s, a); return;
-            case 4: hipLaunchKernelGGL((tiles_group_kernel<3, 4, false, true, false>), dim3(grid), dim3(kBlock), lds, s, a); return;
-            case 8: hipLaunchKernelGGL((tiles_group_kernel<3, 8, false, true, false>), dim3(grid), dim3(kBlock), lds, s, a); return;
-            default: return;
-          }
-        }
-        if (v > 10 && a.crc_fused) {  // + the chunk CRC (host: unit step for 8/G units)
-          const size_t lc = lds + 16 * 256 * 4 + (size_t)a.fast_n * 4 + 64;  // + alignment
-          switch (v - 10) {
-            case 1: hipLaunchKernelGGL((tiles_group_kernel<3, 1, true, false, false>), dim3(grid), dim3(kBlock), lc, s, a); return;
-            case 2: hipLaunchKernelGGL((tiles_group_kernel<3, 2, true, false, false>), dim3(grid), dim3(kBlock), lc, s, a); return;
-            case 4: hipLaunchKernelGGL((tiles_group_kernel<3, 4, true, false, false>), dim3(grid), dim3(kBlock), lc, s, a); return;
-            default: return;
-          }
-        }
-        if (v > 10) {  // host: G chunks per work item, item_mul and grid over the groups
-          switch (v - 10) {
-            case 1: hipLaunchKernelGGL((tiles_group_kernel<3, 1, false, false, false>), dim3(grid), dim3(kBlock), lds, s, a); return;
-            case 2: hipLaunchKernelGGL((tiles_group_kernel<3, 2, false, false, false>), dim3(grid), dim3(kBlock), lds, s, a); return;
-            case 4: hipLaunchKernelGGL((tiles_group_kernel<3, 4, false, false, false>), dim3(grid), dim3(kBlock), lds, s, a); return;
-            case 8: hipLaunchKernelGGL((tiles_group_kernel<3, 8, false, false, false>), dim3(grid), dim3(kBlock), lds, s, a); return;
-            default: return;
-          }
-        }
-        if (v == 1 && a.crc_fused) {
-          lds += 16 * 256 * 4 + (size_t)a.fast_n * 4;  // T[8][256] + S, SD[4][256] + K[fast_n]
-          static const bool w3 = [] {  // ZH_CRC_W3=0: the unconstrained variant (A/B)
-            const char* e = getenv("ZH_CRC_W3");
-            return !(e && e[0] == '0');
-          }();
-          if (!w3)
-            hipLaunchKernelGGL((decode_tiles_kernel<3, 1, true>), dim3(grid), dim3(kBlock), lds, s, a);
-          else if (ntx) hipLaunchKernelGGL((decode_tiles_crc_w3_kernel<3, false>), dim3(grid), dim3(kBlock), lds, s, a);
-          else hipLaunchKernelGGL((decode_tiles_crc_w3_kernel<0, false>), dim3(grid), dim3(kBlock), lds, s, a);
-        } else if (v == 1) {
-          if (ntx) hipLaunchKernelGGL((decode_tiles_kernel<3, 1>), dim3(grid), dim3(kBlock), lds, s, a);
-          else hipLaunchKernelGGL((decode_tiles_kernel<0, 1>), dim3(grid), dim3(kBlock), lds, s, a);
-        } else {
-          if (ntx) hipLaunchKernelGGL((decode_tiles_kernel<3, 0>), dim3(grid), dim3(kBlock), lds, s, a);
-          else hipLaunchKernelGGL((decode_tiles_kernel<0, 0>), dim3(grid), dim3(kBlock), lds, s, a);
+        const size_t lc = lds + 16 * 256 * 4 + (size_t)a.fast_n * 4 + 64;
+        if (a.swap) hipLaunchKernelGGL((tiles_rowcrc_kernel<1, true>), dim3(grid), dim3(kBlock), lc, s, a);
+        else hipLaunchKernelGGL((tiles_rowcrc_kernel<1, false>), dim3(grid), dim3(kBlock), lc, s, a);
+        return;
+      }
+      if (v > 20 && !a.crc_fused) {  // G chunks per work item, next step's loads prefetched
+        switch (v - 20) {
+          case 1: hipLaunchKernelGGL((tiles_group_kernel<3, 1, false, true, false>), dim3(grid), dim3(kBlock), lds, s, a); return;
+          case 2: hipLaunchKernelGGL((tiles_group_kernel<3, 2, false, true, false>), dim3(grid), dim3(kBlock), lds, s, a); return;
+          case 4: hipLaunchKernelGGL((tiles_group_kernel<3, 4, false, true, false>), dim3(grid), dim3(kBlock), lds, s, a); return;
+          case 8: hipLaunchKernelGGL((tiles_group_kernel<3, 8, false, true, false>), dim3(grid), dim3(kBlock), lds, s, a); return;
+          default: return;
         }
       }
-    } else if (a.fast_mode != kFastNone && a.row_group == 8) {  // host: 128-B rows, no CRC
-      hipLaunchKernelGGL((rows_xpose_kernel<DS, false>), dim3(grid), dim3(kBlock),
-                         lds + 4 * 8 * kXRow * 16, s, a);
-    } else if (a.fast_mode != kFastNone && a.row_group > 0) {  // host: nt 3, piece_shift 0
-      const size_t lc = lds + (a.crc_fused ? 12 * 256 * 4 : 0);
-      switch (a.row_group * 2 + (a.crc_fused ? 1 : 0)) {
-        case 2: hipLaunchKernelGGL((rows_group_kernel<DS, 1, 4, 3, false, false>), dim3(grid), dim3(kBlock), lc, s, a); break;
-        case 3: hipLaunchKernelGGL((rows_group_kernel<DS, 1, 4, 3, true, false>), dim3(grid), dim3(kBlock), lc, s, a); break;
-        case 4: hipLaunchKernelGGL((rows_group_kernel<DS, 2, 4, 3, false, false>), dim3(grid), dim3(kBlock), lc, s, a); break;
-        case 5: {
-          // nt bit 3 (ZH_CRC_LOADNT=0): cached payload loads (a misaligned payload's line
-          // shared by two loads can then hit in L2; A/B lab), stores stay non-temporal
-          // nt bit 5 (ZH_DEC_RGU=8): 8 rows per lane in flight instead of 4
-          if (a.nt & 32) {
-            if (a.nt & 8) hipLaunchKernelGGL((rows_group_kernel<DS, 2, 8, 2, true, false>), dim3(grid), dim3(kBlock), lc, s, a);
-            else hipLaunchKernelGGL((rows_group_kernel<DS, 2, 8, 3, true, false>), dim3(grid), dim3(kBlock), lc, s, a);
-            break;
-          }
-          if (a.nt & 8) hipLaunchKernelGGL((rows_group_kernel<DS, 2, 4, 2, true, false>), dim3(grid), dim3(kBlock), lc, s, a);
-          else hipLaunchKernelGGL((rows_group_kernel<DS, 2, 4, 3, true, false>), dim3(grid), dim3(kBlock), lc, s, a);
-          break;
-        }
-        case 8: hipLaunchKernelGGL((rows_group_kernel<DS, 4, 4, 3, false, false>), dim3(grid), dim3(kBlock), lc, s, a); break;
-        case 9: hipLaunchKernelGGL((rows_group_kernel<DS, 4, 4, 3, true, false>), dim3(grid), dim3(kBlock), lc, s, a); break;
-        default: break;  // host only sets 1, 2, 4
-      }
-    } else if (a.fast_mode != kFastNone && a.crc_fused) {
-      lds += 12 * 256 * 4;  // slicing tables T[8][256] + zero-shift tables S[4][256]
-      switch (nt) {
-        case 0: hipLaunchKernelGGL((decode_rows_kernel<DS, 4, 0, true>), dim3(grid), dim3(kBlock), lds, s, a); break;
-        default: hipLaunchKernelGGL((decode_rows_kernel<DS, 4, 3, true>), dim3(grid), dim3(kBlock), lds, s, a); break;
-      }
-    } else if (a.fast_mode != kFastNone && (a.nt & 4) && nt == 3) {
-      // 8 rows in flight per lane (ZH_NT bit 2; A/B switch)
-      hipLaunchKernelGGL((decode_rows_kernel<DS, 8, 3>), dim3(grid), dim3(kBlock), lds, s, a);
-    } else if (a.fast_mode != kFastNone) {
-      switch (nt) {
-        case 0: hipLaunchKernelGGL((decode_rows_kernel<DS, 4, 0>), dim3(grid), dim3(kBlock), lds, s, a); break;
-        case 1: hipLaunchKernelGGL((decode_rows_kernel<DS, 4, 1>), dim3(grid), dim3(kBlock), lds, s, a); break;
-        case 2: hipLaunchKernelGGL((decode_rows_kernel<DS, 4, 2>), dim3(grid), dim3(kBlock), lds, s, a); break;
-        default: hipLaunchKernelGGL((decode_rows_kernel<DS, 4, 3>), dim3(grid), dim3(kBlock), lds, s, a); break;
+      if (v == 1 && a.crc_fused) {
+        lds += 16 * 256 * 4 + (size_t)a.fast_n * 4;  // T[8][256] + S, SD[4][256] + K[fast_n]
+        hipLaunchKernelGGL((decode_tiles_crc_w3_kernel<3, false>), dim3(grid), dim3(kBlock), lds, s, a);
+      } else if (v == 1) {
+        hipLaunchKernelGGL((decode_tiles_kernel<3, 1>), dim3(grid), dim3(kBlock), lds, s, a);
+      } else {
+        hipLaunchKernelGGL((decode_tiles_kernel<3, 0>), dim3(grid), dim3(kBlock), lds, s, a);
       }
     }
+  } else if (a.fast_mode != kFastNone && a.row_group == 8) {  // host: 128-B rows, no CRC
+    hipLaunchKernelGGL((rows_xpose_kernel<DS>), dim3(grid), dim3(kBlock), lds + 4 * 8 * kXRow * 16,
+                       s, a);
+  } else if (a.fast_mode != kFastNone && a.row_group > 0) {  // host: piece_shift 0
+    // with the chunk CRC the payload loads go through the cache (NT = 2): a payload after a
+    // 4-byte crc32c sits at 4 mod 16 and the line two wave loads share then hits in L2
+    // (c3crc reads 1.085× → 1.0016× algorithmic, profiles/r03/c3crc_summary.json)
+    const size_t lc = lds + (a.crc_fused ? 12 * 256 * 4 : 0);
+    switch (a.row_group * 2 + (a.crc_fused ? 1 : 0)) {
+      case 2: hipLaunchKernelGGL((rows_group_kernel<DS, 1, 4, 3, false, false>), dim3(grid), dim3(kBlock), lc, s, a); break;
+      case 3: hipLaunchKernelGGL((rows_group_kernel<DS, 1, 4, 2, true, false>), dim3(grid), dim3(kBlock), lc, s, a); break;
+      case 4: hipLaunchKernelGGL((rows_group_kernel<DS, 2, 4, 3, false, false>), dim3(grid), dim3(kBlock), lc, s, a); break;
+      case 5: hipLaunchKernelGGL((rows_group_kernel<DS, 2, 4, 2, true, false>), dim3(grid), dim3(kBlock), lc, s, a); break;
+      case 8: hipLaunchKernelGGL((rows_group_kernel<DS, 4, 4, 3, false, false>), dim3(grid), dim3(kBlock), lc, s, a); break;
+      case 9: hipLaunchKernelGGL((rows_group_kernel<DS, 4, 4, 2, true, false>), dim3(grid), dim3(kBlock), lc, s, a); break;
+      default: break;  // host only sets 1, 2, 4
+    }
+  } else if (a.fast_mode != kFastNone && a.crc_fused) {
+    lds += 12 * 256 * 4;  // slicing tables T[8][256] + zero-shift tables S[4][256]
+    hipLaunchKernelGGL((decode_rows_kernel<DS, 4, 3, true>), dim3(grid), dim3(kBlock), lds, s, a);
+  } else if (a.fast_mode != kFastNone) {
+    hipLaunchKernelGGL((decode_rows_kernel<DS, 4, 3>), dim3(grid), dim3(kBlock), lds, s, a);
   }
 }
 
-// tiles_rowcrc_kernel addresses its CRC tables from LDS offset 0: true when no instantiation
-// has static LDS (the dynamic block then starts at 0)
+// tiles_rowcrc_kernel and tiles_rowcrc_aln_kernel address their CRC tables from LDS offset 0:
+// true when no instantiation has static LDS (the dynamic block then starts at 0)
 bool rowcrc_lds_at_zero() {
   static const bool ok = [] {
     const void* fns[] = {(const void*)tiles_rowcrc_kernel<1, false>, (const void*)tiles_rowcrc_kernel<1, true>,
-                         (const void*)tiles_rowcrc_kernel<2, false>, (const void*)tiles_rowcrc_kernel<2, true>,
-                         (const void*)tiles_rowcrc_kernel<4, false>, (const void*)tiles_rowcrc_kernel<4, true>,
-                         (const void*)tiles_rowcrc_kernel<1, false, true>, (const void*)tiles_rowcrc_kernel<1, true, true>,
-                         (const void*)tiles_rowcrc_kernel<2, false, true>, (const void*)tiles_rowcrc_kernel<2, true, true>,
-                         (const void*)tiles_rowcrc_kernel<4, false, true>, (const void*)tiles_rowcrc_kernel<4, true, true>,
                          (const void*)tiles_rowcrc_aln_kernel<false>,
-                         (const void*)tiles_rowcrc_aln_kernel<true>,
-                         (const void*)tiles_rowcrc_aln_kernel<false, true>,
-                         (const void*)tiles_rowcrc_aln_kernel<true, true>,
-                         (const void*)tiles_rowcrc_enc_aln_kernel<false, true>,
-                         (const void*)tiles_rowcrc_enc_aln_kernel<true, true>,
-                         (const void*)tiles_rowcrc_enc_aln_kernel<false, false>,
-                         (const void*)tiles_rowcrc_enc_aln_kernel<true, false>};
+                         (const void*)tiles_rowcrc_aln_kernel<true>};
     for (const void* f : fns) {
       hipFuncAttributes at;
       if (hipFuncGetAttributes(&at, f) != hipSuccess || at.sharedSizeBytes != 0) return false;
@@ -3721,208 +3095,85 @@ hipError_t launch_decode_slow(const ScatterArgs& a, int grid, hipStream_t stream
   return hipGetLastError();
 }
 
-// the encode view through the fast kernels (FLAGS); v.nt picks the cache policy and
-// `deep` 8 rows in flight per lane instead of 4 (uint32 rows; tuning, ZH_ENC_NT/ZH_ENC_DEEP)
-// Returns false when a grouped launch (group > 0) found no kernel for its combination: the
-// host set the visit order and grid over groups, so no ungrouped kernel may run instead.
+// the encode view through the fast kernels (FLAGS).  Returns false when a grouped launch
+// (group > 0) found no kernel for its combination: the host set the visit order and grid over
+// groups, so no ungrouped kernel may run instead.  Region loads and payload stores stream
+// non-temporally, except the grouped row encode with the chunk CRC, which stores its payloads
+// through the cache: a payload after a 4-byte crc32c sits at 4 mod 16, and L2 merges the line two
+// stores share (c3crc write 41.04 → 39.77 ms, writes 1.079× → 1.007×; the tile encode measured
+// 43.28 → 43.66 ms that way and keeps non-temporal stores).
 template <int DS>
-static bool launch_encode_fast_ds(const ScatterArgs& v, int grid, int deep, int group,
-                                  hipStream_t s) {
+static bool launch_encode_fast_ds(const ScatterArgs& v, int grid, int group, hipStream_t s) {
   const size_t lds = ((size_t)v.fast_n * 8 + 15) & ~(size_t)15;
-  if (group > 0 && v.fast_mode != kFastTileTable && v.crc_fused && (v.nt & 15) == 3) {
-    const size_t lc = lds + 12 * 256 * 4;  // + slicing tables T[8][256], shift table S[4][256]
-    const bool cst = (v.nt & 16) != 0;     // cached stores (ZH_ENC_CRC_STNT=0)
-    switch (group) {  // host: rows sequential in the payload, whole chunks (piece_shift 0)
-      case 1:
-        if (cst) hipLaunchKernelGGL((rows_group_kernel<DS, 1, 4, 1, true, true>), dim3(grid), dim3(kBlock), lc, s, v);
-        else hipLaunchKernelGGL((rows_group_kernel<DS, 1, 4, 3, true, true>), dim3(grid), dim3(kBlock), lc, s, v);
-        return true;
-      case 2:
-        if (cst) hipLaunchKernelGGL((rows_group_kernel<DS, 2, 4, 1, true, true>), dim3(grid), dim3(kBlock), lc, s, v);
-        else hipLaunchKernelGGL((rows_group_kernel<DS, 2, 4, 3, true, true>), dim3(grid), dim3(kBlock), lc, s, v);
-        return true;
-      case 4:
-        if (cst) hipLaunchKernelGGL((rows_group_kernel<DS, 4, 4, 1, true, true>), dim3(grid), dim3(kBlock), lc, s, v);
-        else hipLaunchKernelGGL((rows_group_kernel<DS, 4, 4, 3, true, true>), dim3(grid), dim3(kBlock), lc, s, v);
-        return true;
-      default: break;
+  if (v.fast_mode != kFastTileTable) {
+    if (group > 0 && v.crc_fused) {  // host: rows sequential in the payload, whole chunks
+      const size_t lc = lds + 12 * 256 * 4;  // + slicing tables T[8][256], shift table S[4][256]
+      switch (group) {
+        case 1: hipLaunchKernelGGL((rows_group_kernel<DS, 1, 4, 1, true, true>), dim3(grid), dim3(kBlock), lc, s, v); return true;
+        case 2: hipLaunchKernelGGL((rows_group_kernel<DS, 2, 4, 1, true, true>), dim3(grid), dim3(kBlock), lc, s, v); return true;
+        case 4: hipLaunchKernelGGL((rows_group_kernel<DS, 4, 4, 1, true, true>), dim3(grid), dim3(kBlock), lc, s, v); return true;
+        default: return false;
+      }
     }
-  }
-  if (group == 8 && deep == 20 && v.fast_mode != kFastTileTable && !v.crc_fused) {
-    // host: 128-B rows (fast_vpr_shift 3), rows per chunk a multiple of 8
-    hipLaunchKernelGGL((rows_xpose_kernel<DS, true>), dim3(grid), dim3(kBlock),
-                       lds + 4 * 8 * kXRow * 16, s, v);
+    if (group > 0) {  // host: G·vpr ≤ 64 lanes, piece_shift == 0, v.item_mul over groups
+      switch (group) {
+        case 1: hipLaunchKernelGGL((rows_group_kernel<DS, 1, 4, 3, false, true>), dim3(grid), dim3(kBlock), lds, s, v); return true;
+        case 2: hipLaunchKernelGGL((rows_group_kernel<DS, 2, 4, 3, false, true>), dim3(grid), dim3(kBlock), lds, s, v); return true;
+        case 4: hipLaunchKernelGGL((rows_group_kernel<DS, 4, 4, 3, false, true>), dim3(grid), dim3(kBlock), lds, s, v); return true;
+        case 8: hipLaunchKernelGGL((rows_group_kernel<DS, 8, 4, 3, false, true>), dim3(grid), dim3(kBlock), lds, s, v); return true;
+        default: return false;
+      }
+    }
+    if (v.crc_fused) {  // chunk crc32c of the stored payload, fused (rows sequential in the payload)
+      hipLaunchKernelGGL((decode_rows_kernel<DS, 4, 3, true, true>), dim3(grid), dim3(kBlock),
+                         lds + 12 * 256 * 4, s, v);
+      return true;
+    }
+    // uint32 rows: 8 rows in flight per lane (+2.4 % on c3, profiles/r01/experiments/)
+    if constexpr (DS == 4)
+      hipLaunchKernelGGL((decode_rows_kernel<DS, 8, 3, false, true>), dim3(grid), dim3(kBlock), lds, s, v);
+    else
+      hipLaunchKernelGGL((decode_rows_kernel<DS, 4, 3, false, true>), dim3(grid), dim3(kBlock), lds, s, v);
     return true;
   }
-  if (group > 0 && v.fast_mode != kFastTileTable && !v.crc_fused && v.nt == 3) {
-    // host: G·vpr ≤ 64 lanes, piece_shift == 0, v.item_mul over groups; deep: U (rows per
-    // lane in flight) 2 / 4 / 8 for deep = 0 / 1 / 2
-#define ZH_EG(G, U) hipLaunchKernelGGL((rows_group_kernel<DS, G, U, 3, false, true>), dim3(grid), dim3(kBlock), lds, s, v); return true
-    switch (group * 10 + (deep <= 0 ? 2 : deep == 1 ? 4 : 8)) {
-      case 12: ZH_EG(1, 2);
-      case 14: ZH_EG(1, 4);
-      case 18: ZH_EG(1, 8);
-      case 22: ZH_EG(2, 2);
-      case 24: ZH_EG(2, 4);
-      case 28: ZH_EG(2, 8);
-      case 42: ZH_EG(4, 2);
-      case 44: ZH_EG(4, 4);
-      case 48: ZH_EG(4, 8);
-      case 84: ZH_EG(8, 4);
-      default: break;
-    }
-#undef ZH_EG
-  }
-  if (group > 0 && v.fast_mode != kFastTileTable) return false;
-  if (v.fast_mode == kFastTileTable) {
-    if constexpr (DS == 4) {
-      const size_t l = lds + (size_t)kTG * kTilePitch * 4;
-      if (group == 1 && v.crc_fused && v.nt == 3 && v.tile_align && (deep == 31 || deep == 32)) {
-        // aligned payload lines (ZH_ENC_ALIGN; deep 31: prefetching loads, 32: not)
-        const size_t la = 12800 + (size_t)9 * kTilePitch * 4;
-        if (deep == 31) {
-          if (v.swap) hipLaunchKernelGGL((tiles_rowcrc_enc_aln_kernel<true, true>), dim3(grid), dim3(kBlock), la, s, v);
-          else hipLaunchKernelGGL((tiles_rowcrc_enc_aln_kernel<false, true>), dim3(grid), dim3(kBlock), la, s, v);
-        } else {
-          if (v.swap) hipLaunchKernelGGL((tiles_rowcrc_enc_aln_kernel<true, false>), dim3(grid), dim3(kBlock), la, s, v);
-          else hipLaunchKernelGGL((tiles_rowcrc_enc_aln_kernel<false, false>), dim3(grid), dim3(kBlock), la, s, v);
-        }
-        return true;
-      }
-      if (group > 0 && v.crc_fused && v.nt == 3 && deep == 30) {  // row-CRC encode (ZH_ENC_ROWCRC)
-        const size_t lc = l + 16 * 256 * 4 + (size_t)v.fast_n * 4 + 64;
-#define ZH_RC(G) if (v.swap) hipLaunchKernelGGL((tiles_rowcrc_kernel<G, true, true>), dim3(grid), dim3(kBlock), lc, s, v); \
-                 else hipLaunchKernelGGL((tiles_rowcrc_kernel<G, false, true>), dim3(grid), dim3(kBlock), lc, s, v); return true
-        switch (group) {
-          case 1: ZH_RC(1);
-          case 2: ZH_RC(2);
-          case 4: ZH_RC(4);
-          default: break;
-        }
-#undef ZH_RC
-      }
-      if (group > 0 && v.crc_fused && (v.nt & 15) == 3 && deep == 40) {  // compact tables
-        const size_t lc = l + 4 * 256 * 4 + 2 * 8 * 16 * 4 + (size_t)v.fast_n * 4 + 16;
-        switch (group) {
-          case 1: hipLaunchKernelGGL((tiles_group_kernel<3, 1, true, false, true, 1>), dim3(grid), dim3(kBlock), lc, s, v); return true;
-          case 2:
-            if (v.nt & 16) hipLaunchKernelGGL((tiles_group_kernel<1, 2, true, false, true, 1>), dim3(grid), dim3(kBlock), lc, s, v);
-            else hipLaunchKernelGGL((tiles_group_kernel<3, 2, true, false, true, 1>), dim3(grid), dim3(kBlock), lc, s, v);
-            return true;
-          case 4: hipLaunchKernelGGL((tiles_group_kernel<3, 4, true, false, true, 1>), dim3(grid), dim3(kBlock), lc, s, v); return true;
-          default: break;
-        }
-      }
-      if (group > 0 && v.crc_fused && (v.nt & 15) == 3 && deep == 41) {  // field tables
-        const size_t lc = l + 42 * 128 + (size_t)v.fast_n * 4 + 16;
-        switch (group) {
-          case 1: hipLaunchKernelGGL((tiles_group_kernel<3, 1, true, false, true, 2>), dim3(grid), dim3(kBlock), lc, s, v); return true;
-          case 2:
-            if (v.nt & 16) hipLaunchKernelGGL((tiles_group_kernel<1, 2, true, false, true, 2>), dim3(grid), dim3(kBlock), lc, s, v);
-            else hipLaunchKernelGGL((tiles_group_kernel<3, 2, true, false, true, 2>), dim3(grid), dim3(kBlock), lc, s, v);
-            return true;
-          case 4: hipLaunchKernelGGL((tiles_group_kernel<3, 4, true, false, true, 2>), dim3(grid), dim3(kBlock), lc, s, v); return true;
-          default: break;
-        }
-      }
-      if (group > 0 && v.crc_fused && (v.nt & 15) == 3) {  // host: crc_tile_step for 8/G units
-        const size_t lc = l + 16 * 256 * 4 + (size_t)v.fast_n * 4 + 64;  // + alignment
-        switch (group) {
-          case 1: hipLaunchKernelGGL((tiles_group_kernel<3, 1, true, false, true>), dim3(grid), dim3(kBlock), lc, s, v); return true;
-          case 2:
-            if (v.nt & 16) hipLaunchKernelGGL((tiles_group_kernel<1, 2, true, false, true>), dim3(grid), dim3(kBlock), lc, s, v);  // cached stores
-            else hipLaunchKernelGGL((tiles_group_kernel<3, 2, true, false, true>), dim3(grid), dim3(kBlock), lc, s, v);
-            return true;
-          case 4: hipLaunchKernelGGL((tiles_group_kernel<3, 4, true, false, true>), dim3(grid), dim3(kBlock), lc, s, v); return true;
-          default: break;
-        }
-      }
-      if (group > 0 && !v.crc_fused && v.nt == 3 && deep == 9) {  // + prefetch (ZH_ENC_TPF=1)
-        switch (group) {
-          case 1: hipLaunchKernelGGL((tiles_group_kernel<3, 1, false, true, true>), dim3(grid), dim3(kBlock), l, s, v); return true;
-          case 2: hipLaunchKernelGGL((tiles_group_kernel<3, 2, false, true, true>), dim3(grid), dim3(kBlock), l, s, v); return true;
-          case 4: hipLaunchKernelGGL((tiles_group_kernel<3, 4, false, true, true>), dim3(grid), dim3(kBlock), l, s, v); return true;
-          default: break;
-        }
-      }
-      if (group > 0 && v.crc_fused && v.nt == 3 && deep == 9) {
-        const size_t lc = l + 16 * 256 * 4 + (size_t)v.fast_n * 4 + 64;  // + alignment
-        switch (group) {
-          case 1: hipLaunchKernelGGL((tiles_group_kernel<3, 1, true, true, true>), dim3(grid), dim3(kBlock), lc, s, v); return true;
-          case 2: hipLaunchKernelGGL((tiles_group_kernel<3, 2, true, true, true>), dim3(grid), dim3(kBlock), lc, s, v); return true;
-          case 4: hipLaunchKernelGGL((tiles_group_kernel<3, 4, true, true, true>), dim3(grid), dim3(kBlock), lc, s, v); return true;
-          default: break;
-        }
-      }
-      if (group > 0 && !v.crc_fused && v.nt == 3) {  // host: piece_shift == 0, item_mul
-        switch (group) {
-          case 1: hipLaunchKernelGGL((tiles_group_kernel<3, 1, false, false, true>), dim3(grid), dim3(kBlock), l, s, v); return true;
-          case 2: hipLaunchKernelGGL((tiles_group_kernel<3, 2, false, false, true>), dim3(grid), dim3(kBlock), l, s, v); return true;
-          case 4: hipLaunchKernelGGL((tiles_group_kernel<3, 4, false, false, true>), dim3(grid), dim3(kBlock), l, s, v); return true;
-          default: break;
-        }
-      }
-      if (group > 0) return false;
-      if (v.crc_fused) {  // chunk crc32c of the stored payload: tables + per-unit shifts
-        // (3 waves per SIMD as on decode unless ZH_CRC_W3=0)
-        const char* e = getenv("ZH_CRC_W3");
-        if (e && e[0] == '0')
-          hipLaunchKernelGGL((decode_tiles_kernel<3, 1, true, true>), dim3(grid), dim3(kBlock),
-                             l + 16 * 256 * 4 + (size_t)v.fast_n * 4, s, v);
-        else
-          hipLaunchKernelGGL((decode_tiles_crc_w3_kernel<3, true>), dim3(grid), dim3(kBlock),
-                             l + 16 * 256 * 4 + (size_t)v.fast_n * 4, s, v);
-        return true;
-      }
-      switch (v.nt) {
-        case 0: hipLaunchKernelGGL((decode_tiles_kernel<0, 1, false, true>), dim3(grid), dim3(kBlock), l, s, v); break;
-        case 1: hipLaunchKernelGGL((decode_tiles_kernel<1, 1, false, true>), dim3(grid), dim3(kBlock), l, s, v); break;
-        case 2: hipLaunchKernelGGL((decode_tiles_kernel<2, 1, false, true>), dim3(grid), dim3(kBlock), l, s, v); break;
-        default: hipLaunchKernelGGL((decode_tiles_kernel<3, 1, false, true>), dim3(grid), dim3(kBlock), l, s, v); break;
+  if constexpr (DS == 4) {
+    const size_t l = lds + (size_t)kTG * kTilePitch * 4;
+    if (group > 0 && v.crc_fused) {  // host: crc_tile_step for 8/G units
+      const size_t lc = l + 16 * 256 * 4 + (size_t)v.fast_n * 4 + 64;  // + alignment
+      switch (group) {
+        case 1: hipLaunchKernelGGL((tiles_group_kernel<3, 1, true, false, true>), dim3(grid), dim3(kBlock), lc, s, v); return true;
+        case 2: hipLaunchKernelGGL((tiles_group_kernel<3, 2, true, false, true>), dim3(grid), dim3(kBlock), lc, s, v); return true;
+        case 4: hipLaunchKernelGGL((tiles_group_kernel<3, 4, true, false, true>), dim3(grid), dim3(kBlock), lc, s, v); return true;
+        default: return false;
       }
     }
-  } else if (v.fast_mode != kFastNone && v.crc_fused) {
-    // chunk crc32c of the stored payload, fused (rows sequential in the payload)
-    // 4 rows in flight per lane unless deep ≥ 2 (c3crc write 52.6 → 47.4 ms with 4,
-    // profiles/r02/write/ab_crcw.txt)
-    const size_t l = lds + 12 * 256 * 4;
-    if (deep >= 2)
-      hipLaunchKernelGGL((decode_rows_kernel<DS, 8, 3, true, true>), dim3(grid), dim3(kBlock), l, s, v);
+    if (group > 0) {  // host: piece_shift == 0, item_mul
+      switch (group) {
+        case 1: hipLaunchKernelGGL((tiles_group_kernel<3, 1, false, false, true>), dim3(grid), dim3(kBlock), l, s, v); return true;
+        case 2: hipLaunchKernelGGL((tiles_group_kernel<3, 2, false, false, true>), dim3(grid), dim3(kBlock), l, s, v); return true;
+        case 4: hipLaunchKernelGGL((tiles_group_kernel<3, 4, false, false, true>), dim3(grid), dim3(kBlock), l, s, v); return true;
+        default: return false;
+      }
+    }
+    if (v.crc_fused)  // chunk crc32c of the stored payload: tables + per-unit shifts
+      hipLaunchKernelGGL((decode_tiles_crc_w3_kernel<3, true>), dim3(grid), dim3(kBlock),
+                         l + 16 * 256 * 4 + (size_t)v.fast_n * 4, s, v);
     else
-      hipLaunchKernelGGL((decode_rows_kernel<DS, 4, 3, true, true>), dim3(grid), dim3(kBlock), l, s, v);
-  } else if (v.fast_mode != kFastNone) {
-    if constexpr (DS == 4) {
-      if (deep) {
-        switch (v.nt) {
-          case 0: hipLaunchKernelGGL((decode_rows_kernel<DS, 8, 0, false, true>), dim3(grid), dim3(kBlock), lds, s, v); return true;
-          case 1: hipLaunchKernelGGL((decode_rows_kernel<DS, 8, 1, false, true>), dim3(grid), dim3(kBlock), lds, s, v); return true;
-          case 2: hipLaunchKernelGGL((decode_rows_kernel<DS, 8, 2, false, true>), dim3(grid), dim3(kBlock), lds, s, v); return true;
-          default: hipLaunchKernelGGL((decode_rows_kernel<DS, 8, 3, false, true>), dim3(grid), dim3(kBlock), lds, s, v); return true;
-        }
-      }
-      switch (v.nt) {
-        case 0: hipLaunchKernelGGL((decode_rows_kernel<DS, 4, 0, false, true>), dim3(grid), dim3(kBlock), lds, s, v); return true;
-        case 1: hipLaunchKernelGGL((decode_rows_kernel<DS, 4, 1, false, true>), dim3(grid), dim3(kBlock), lds, s, v); return true;
-        case 2: hipLaunchKernelGGL((decode_rows_kernel<DS, 4, 2, false, true>), dim3(grid), dim3(kBlock), lds, s, v); return true;
-        default: break;
-      }
-    }
-    hipLaunchKernelGGL((decode_rows_kernel<DS, 4, 3, false, true>), dim3(grid), dim3(kBlock), lds,
-                       s, v);
+      hipLaunchKernelGGL((decode_tiles_kernel<3, 1, false, true>), dim3(grid), dim3(kBlock), l, s, v);
+    return true;
   }
-  return true;
+  return group == 0;
 }
 
-hipError_t launch_encode_fast(const ScatterArgs& view, int grid, int deep, int group,
-                              hipStream_t stream) {
+hipError_t launch_encode_fast(const ScatterArgs& view, int grid, int group, hipStream_t stream) {
   if (view.total_items == 0 || view.fast_mode == kFastNone) return hipSuccess;
-  g_last_encode_path.store((int64_t)view.fast_mode * 1000000 + (int64_t)group * 1000 + deep);
+  g_last_encode_path.store((int64_t)view.fast_mode * 1000000 + (int64_t)group * 1000);
   bool ok = false;
   switch (view.dsize) {
-    case 1: ok = launch_encode_fast_ds<1>(view, grid, deep, group, stream); break;
-    case 2: ok = launch_encode_fast_ds<2>(view, grid, deep, group, stream); break;
-    case 4: ok = launch_encode_fast_ds<4>(view, grid, deep, group, stream); break;
-    case 8: ok = launch_encode_fast_ds<8>(view, grid, deep, group, stream); break;
+    case 1: ok = launch_encode_fast_ds<1>(view, grid, group, stream); break;
+    case 2: ok = launch_encode_fast_ds<2>(view, grid, group, stream); break;
+    case 4: ok = launch_encode_fast_ds<4>(view, grid, group, stream); break;
+    case 8: ok = launch_encode_fast_ds<8>(view, grid, group, stream); break;
     default: return hipErrorInvalidValue;
   }
   if (!ok) return hipErrorInvalidValue;
