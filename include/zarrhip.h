@@ -15,6 +15,7 @@
  *   zh_shard_ranges             StoreHandleDataProvider reads of decodeInternal ShardingIndexedCodec.java:190-230, 333-357
  *   zh_array_read_pieces        core.Array.read with sub-shard parts         M/core/Array.java:378-441 + the above
  *   zh_sharding_decode_pieces   ShardingIndexedCodec.decodePartial(StoreHandle, ...) ShardingIndexedCodec.java:245-255
+ *   zh_shard_index_check        Crc32cCodec.decode of a shard index (host)    M/v3/codec/core/Crc32cCodec.java:24-48
  *   zh_array_write              core.Array.write + writeChunk + ShardingIndexedCodec.encode
  *                                                                            M/core/Array.java:83-156, ShardingIndexedCodec.java:105-168
  *   zh_shard_index_size         ShardingIndexedCodec.getShardIndexSize       ShardingIndexedCodec.java:176-181
@@ -274,19 +275,34 @@ int zh_device_count(void);
  * index_nbytes bytes the prefix/suffix read returned (16 per inner chunk [+ 4 crc32c]);
  * shard_nbytes = StoreHandle.getSize() or -1 when the store cannot tell; [part_lo, part_hi) =
  * shard-local element box.  Entries of the part's inner-chunk box (nested sharding: its
- * level-1 cells, read whole), missing ones (-1) dropped, are sorted by offset and adjacent
- * ranges merged while a run stays <= max_run bytes (0: one range per entry; a run never
- * exceeds 2^31 - 1 bytes).  Entries that cannot be read (negative, beyond a known
- * shard_nbytes, longer than 2^31 - 1) are left out: the device then reports them with the
- * reference's "Could not load byte data for chunk [...]" unless the index crc32c fails first.
- * The index crc32c is NOT checked here.  Writes up to `cap` (offset, nbytes) pairs to
+ * level-1 cells, read whole), missing ones (-1) dropped, are sorted by offset.  max_run > 0:
+ * overlapping entries are united and adjacent ranges merged while a run stays <= max_run
+ * bytes; no range ever exceeds 2^31 - 1 bytes (a union that would continues as a new range).
+ * max_run == 0 (chains whose host stages decode each inner chunk on its own): one range per
+ * entry, overlapping or not, exact duplicates once.  Entries that cannot be read (negative,
+ * beyond a known shard_nbytes, longer than 2^31 - 1) are left out: the device then reports
+ * them with the reference's "Could not load byte data for chunk [...]" unless the index
+ * crc32c fails first.  The index crc32c is NOT checked here (zh_shard_index_check).  Writes up to `cap` (offset, nbytes) pairs to
  * `ranges` (may be NULL) and returns the number of ranges; a negative return is -zh_status
  * (EINVAL: not a sharded meta, index_nbytes below the index size, bad part box). */
 int64_t zh_shard_ranges(const zh_array_meta* meta, const void* index, int64_t index_nbytes,
                         int64_t shard_nbytes, const int64_t* part_lo, const int64_t* part_hi,
                         int64_t max_run, int64_t* ranges, int64_t cap);
 
-/* One byte range of a stored shard as the store returned it. */
+/* Crc32cCodec.decode of a stored shard index on the host (Crc32cCodec.java:24-48): ZH_OK when
+ * the chain's index has no crc32c or it matches, ZH_EDATA with the reference's message
+ * ("The checksum of the sharding index is invalid. Stored: <int> Computed: <int>") when it does
+ * not.  A sub-shard read normally leaves the check to the device; a binding calls this first
+ * when the index decides host work before the device sees it: inner chains with host stages
+ * (each referenced range is decoded on the host) or a store that cannot tell the shard size
+ * (a corrupt entry could ask for a 2^31-byte range read).  The reference checks the index
+ * before any range read (ShardingIndexedCodec.java:205). */
+int zh_shard_index_check(const zh_array_meta* meta, const void* index, int64_t index_nbytes,
+                         char* err, size_t errlen);
+
+/* One byte range of a stored shard as the store returned it.  Pieces are sorted by offset and
+ * disjoint, except host-decoded pieces (data_nbytes != nbytes), which may overlap one another
+ * at distinct offsets: each serves exactly the entry (offset, nbytes) it was read for. */
 typedef struct zh_shard_piece {
   int64_t offset;      /* shard byte offset of the range                                       */
   int64_t nbytes;      /* stored bytes in the range (one inner chunk or a run of adjacent ones) */
@@ -329,12 +345,13 @@ int zh_array_read_pieces_multi(zh_ctx* const* ctxs, int ndev, int root,
 int zh_sharding_decode_pieces(zh_ctx* ctx, const zh_array_meta* meta, const zh_shard_src* shard,
                               const int64_t* offset, const int32_t* shape, void* out,
                               uint32_t flags, void* stream, char* err, size_t errlen);
-/* Page-locked host staging owned by the context, for bindings that must copy their sources
- * out of a managed heap (the JNI shim copies each piece's byte[] here once, and the decoded
- * region comes back through it): at least `bytes`, valid until the next call on this context
- * or zh_ctx_destroy; grown on demand, kept across calls up to ZH_STAGING_MAX_MB (default
- * 8192; larger requests get a one-off buffer that the next call frees).  Not thread-safe
- * against other calls on the same context. */
+/* Page-locked host staging owned by the context, for bindings that copy their sources out of
+ * a managed heap before a read (the JNI shim does not: it hands the library its arrays in
+ * bounded critical sections): at least `bytes`, valid until the next call on
+ * this context or zh_ctx_destroy; grown on demand, kept across calls up to ZH_STAGING_MAX_MB
+ * (default 8192; larger requests get a one-off buffer that the next call frees).  Takes the
+ * context's lock, so it never replaces the staging under a read in flight on another thread;
+ * the caller must not use the previous pointer once it calls again. */
 int zh_host_staging(zh_ctx* ctx, size_t bytes, void** out);
 
 /* ShardingIndexedCodec.decode: whole shard → chunk_shape elements. */

@@ -1,0 +1,291 @@
+"""Drives the JNI shim (zarr-java_amd/java/jni/zarrhip_jni.c) through the test-only fake JVM
+(tests/jni/: stand-in jni.h + fake_jvm.c, built by __graft_entry__.build()).  The Java side is
+restated as HipArray / ShardPieces / ZarrHip would call it: the DeviceChain meta packing
+(DeviceChain.java:20-23), the store I/O of tests/helpers.py jni_fetch, and the native methods'
+exact argument lists (ZarrHip.java).  Every call is followed by the fake's bookkeeping: critical
+sections paired and never nested around another JNI call, sources left with JNI_ABORT and
+unmodified, the output written back with mode 0, exceptions mapped to the reference's classes."""
+import ctypes as C
+import os
+
+import numpy as np
+
+from zarrhip import _abi as A
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+P = C.c_void_p
+
+KIND = {1: b"B", 2: b"S", 4: b"I", 8: b"J"}
+
+
+class FStats(C.Structure):
+    _fields_ = [(n, C.c_int64) for n in (
+        "gets", "releases", "releases_commit", "releases_abort", "max_depth",
+        "calls_in_critical", "dead_ref_uses", "calls_with_pending", "oob", "modified_sources",
+        "windows", "max_window_ns", "total_window_ns", "live_local_refs", "peak_local_refs",
+        "capacity_requested", "bad_release")]
+
+
+def lib_path():
+    return os.environ.get("ZH_JNI_TEST_LIB",
+                          os.path.join(ROOT, "tests", "jni", "_build", "libzh_jni_test.so"))
+
+
+_LIB = None
+
+
+def jni_lib():
+    global _LIB
+    if _LIB is None:
+        from zarrhip._lib import lib
+        lib()  # the product library first: the shim's DT_NEEDED resolves to the same file
+        L = C.CDLL(lib_path())
+        L.fj_env.restype = P
+        L.fj_reset.argtypes = [C.c_int]
+        L.fj_new_array.restype = P
+        L.fj_new_array.argtypes = [C.c_char, C.c_int64, P]
+        L.fj_new_object_array.restype = P
+        L.fj_new_object_array.argtypes = [C.c_int64, C.c_char_p]
+        L.fj_set.argtypes = [P, C.c_int64, P]
+        L.fj_get.restype = P
+        L.fj_get.argtypes = [P, C.c_int64]
+        L.fj_data.restype = P
+        L.fj_data.argtypes = [P]
+        L.fj_len.restype = C.c_int64
+        L.fj_len.argtypes = [P]
+        L.fj_obj_stats.argtypes = [P, C.POINTER(C.c_int64)]
+        L.fj_stats.argtypes = [C.POINTER(FStats)]
+        L.fj_exception.argtypes = [C.c_char_p, C.c_int64, C.c_char_p, C.c_int64]
+        L.fj_last_violation.restype = C.c_char_p
+        for name in ("arrayRead", "arrayReadMulti", "shardDecodePartial", "arrayReadPieces",
+                     "shardDecodePieces"):
+            getattr(L, "Java_dev_zarr_zarrjava_hip_ZarrHip_" + name).restype = C.c_int32
+        L.Java_dev_zarr_zarrjava_hip_ZarrHip_shardRanges.restype = P
+        L.Java_dev_zarr_zarrjava_hip_ZarrHip_arrayWrite.restype = P
+        L.Java_dev_zarr_zarrjava_hip_ZarrHip_ctxCreate.restype = C.c_int64
+        _LIB = L
+    return _LIB
+
+
+class JavaException(Exception):
+    def __init__(self, cls, msg):
+        super().__init__(f"{cls}: {msg}")
+        self.cls = cls
+        self.msg = msg
+
+
+class FakeJVM:
+    """One fake JVM session: Java arrays, the native methods, the JNI-rule bookkeeping."""
+
+    def __init__(self, copy_mode=True):
+        self.L = jni_lib()
+        self.L.fj_reset(1 if copy_mode else 0)
+        self.env = self.L.fj_env()
+        self.sources = []   # arrays the shim must only read
+        self.outputs = []   # arrays it must write back
+
+    # ---- Java values ---------------------------------------------------------------------
+    def prim(self, kind, values=None, n=None):
+        if values is None:
+            return self.L.fj_new_array(kind, int(n), None)
+        a = np.ascontiguousarray(values)
+        return self.L.fj_new_array(kind, a.size, a.ctypes.data)
+
+    def ints(self, v):
+        return self.prim(b"I", np.asarray(v, np.int32))
+
+    def longs(self, v):
+        return self.prim(b"J", np.asarray(v, np.int64))
+
+    def bytes_(self, b, source=True):
+        """A byte[] holding b (None: a null reference)."""
+        if b is None:
+            return None
+        a = np.frombuffer(bytes(b), np.uint8)
+        h = self.L.fj_new_array(b"B", a.size, a.ctypes.data if a.size else None)
+        if source:
+            self.sources.append(h)
+        return h
+
+    def objs(self, items, cls):
+        h = self.L.fj_new_object_array(len(items), cls)
+        for i, x in enumerate(items):
+            self.L.fj_set(h, i, x)
+        return h
+
+    def output(self, dsize, nel):
+        h = self.prim(KIND[dsize], n=nel)
+        self.outputs.append(h)
+        return h
+
+    def array_of(self, h, dtype):
+        n = self.L.fj_len(h)
+        if n <= 0:
+            return np.zeros(0, dtype)
+        es = np.dtype(dtype).itemsize
+        return np.frombuffer(C.string_at(self.L.fj_data(h), n * es), dtype).copy()
+
+    def meta_args(self, meta):
+        """DeviceChain's packing: int[14] meta, long[] shape, int[] chunkShape, int[] innerShape
+        (nested: inner then leaf shape), int[] order, byte[] fill."""
+        n, ch = meta.ndim, meta.chain
+        mi = [n, meta.dtype_size, meta.dtype_is_bool, ch.sharded, ch.has_transpose, ch.endian,
+              ch.index_endian, ch.index_has_crc32c, ch.index_location, ch.nested,
+              ch.nested_index_endian, ch.nested_index_has_crc32c, ch.nested_index_location,
+              ch.inner_crc32c]
+        inner = [ch.inner_chunk_shape[d] for d in range(n)]
+        if ch.nested:
+            inner += [ch.nested_chunk_shape[d] for d in range(n)]
+        return (self.ints(mi), self.longs([meta.shape[d] for d in range(n)]),
+                self.ints([meta.chunk_shape[d] for d in range(n)]), self.ints(inner or [0] * n),
+                self.ints([ch.transpose_order[d] for d in range(n)]),
+                self.prim(b"B", np.frombuffer(bytes(meta.fill_value)[:meta.dtype_size], np.int8)))
+
+    # ---- after a call ----------------------------------------------------------------------
+    def exception(self):
+        c, m = C.create_string_buffer(128), C.create_string_buffer(4096)
+        if self.L.fj_exception(c, 128, m, 4096):
+            self.L.fj_clear_exception()
+            return JavaException(c.value.decode(), m.value.decode())
+        return None
+
+    def stats(self):
+        s = FStats()
+        self.L.fj_stats(C.byref(s))
+        return s
+
+    def obj_stats(self, h):
+        v = (C.c_int64 * 4)()
+        self.L.fj_obj_stats(h, v)
+        return list(v)
+
+    def check_rules(self):
+        """The JNI rules the shim relies on held for every call so far; returns the stats."""
+        s = self.stats()
+        v = self.L.fj_last_violation().decode()
+        assert not v, v
+        assert s.calls_in_critical == 0 and s.dead_ref_uses == 0 and s.calls_with_pending == 0
+        assert s.bad_release == 0 and s.modified_sources == 0 and s.oob == 0
+        assert s.gets == s.releases and self.L.fj_depth() == 0
+        for h in self.sources:
+            g, commit, abort, bad = self.obj_stats(h)
+            assert commit == 0 and abort == g and bad == 0, (g, commit, abort, bad)
+        for h in self.outputs:
+            g, commit, abort, bad = self.obj_stats(h)
+            assert abort == 0 and commit == g and bad == 0, (g, commit, abort, bad)
+        return s
+
+    # ---- the native methods (ZarrHip.java), as HipArray / the codec call them ---------------
+    def _fn(self, name):
+        return getattr(self.L, "Java_dev_zarr_zarrjava_hip_ZarrHip_" + name)
+
+    def _done(self, rc):
+        e = self.exception()
+        if e is not None:
+            raise e
+        return rc
+
+    def ctx_create(self, device=0):
+        h = self._fn("ctxCreate")(P(self.env), None, C.c_int32(device))
+        e = self.exception()
+        if e is not None:
+            raise e
+        return h
+
+    def array_read(self, ctx, meta, chunks, offset, shape, ctxs=None):
+        """arrayRead (ctxs: arrayReadMulti): chunks in computeChunkCoords order, None = missing.
+        Returns (status, decoded array or None)."""
+        nel = int(np.prod(shape))
+        out = self.output(meta.dtype_size, nel)
+        jc = self.objs([self.bytes_(c) for c in chunks], b"[B")
+        args = self.meta_args(meta) + (jc, self.longs(offset), self.longs(shape), out)
+        if ctxs is None:
+            rc = self._fn("arrayRead")(P(self.env), None, C.c_int64(int(ctx or 0)), *map(P, args))
+        else:
+            rc = self._fn("arrayReadMulti")(P(self.env), None, P(self.longs([int(c) for c in ctxs])),
+                                             *map(P, args))
+        rc = self._done(rc)
+        dt = {1: np.uint8, 2: np.uint16, 4: np.uint32, 8: np.uint64}[meta.dtype_size]
+        return rc, (self.array_of(out, dt).reshape(shape) if rc == 0 else None)
+
+    def shard_decode_partial(self, ctx, meta, shard, offset, part):
+        nel = int(np.prod(part))
+        out = self.output(meta.dtype_size, nel)
+        args = self.meta_args(meta) + (self.bytes_(shard), self.longs(offset), self.ints(part), out)
+        rc = self._done(self._fn("shardDecodePartial")(P(self.env), None,
+                                                       C.c_int64(int(ctx or 0)), *map(P, args)))
+        dt = {1: np.uint8, 2: np.uint16, 4: np.uint32, 8: np.uint64}[meta.dtype_size]
+        return rc, (self.array_of(out, dt).reshape(part) if rc == 0 else None)
+
+    def shard_ranges(self, meta, index, size, lo, hi, max_run, check=False):
+        args = self.meta_args(meta) + (self.bytes_(index),)
+        r = self._fn("shardRanges")(P(self.env), None, *map(P, args), C.c_int64(size),
+                                    P(self.longs(lo)), P(self.longs(hi)), C.c_int64(max_run),
+                                    C.c_uint8(1 if check else 0))
+        self._done(0)
+        v = self.array_of(r, np.int64)
+        return [(int(v[2 * k]), int(v[2 * k + 1])) for k in range(len(v) // 2)]
+
+    def _pieces_args(self, fetched):
+        idx, sizes, offs, lens, data = [], [], [], [], []
+        for s in fetched:
+            if s is None:
+                idx.append(None)
+                sizes.append(-1)
+                offs.append(self.longs([]))
+                lens.append(self.longs([]))
+                data.append(self.objs([], b"[B"))
+                continue
+            ib, size, pieces = s
+            idx.append(self.bytes_(ib))
+            sizes.append(size)
+            offs.append(self.longs([o for o, _ in pieces]))
+            lens.append(self.longs([len(b) for _, b in pieces]))
+            data.append(self.objs([self.bytes_(b) for _, b in pieces], b"[B"))
+        return (self.objs(idx, b"[B"), self.longs(sizes), self.objs(offs, b"[J"),
+                self.objs(lens, b"[J"), self.objs(data, b"[[B"))
+
+    def array_read_pieces(self, ctxs, meta, fetched, offset, shape, stored_lens=None):
+        """arrayReadPieces over jni_fetch's shards [(index|None, size, [(offset, bytes)])];
+        stored_lens: per shard the stored length of each piece when host stages were undone."""
+        nel = int(np.prod(shape))
+        out = self.output(meta.dtype_size, nel)
+        pa = list(self._pieces_args(fetched))
+        if stored_lens is not None:
+            pa[3] = self.objs([self.longs(v) for v in stored_lens], b"[J")
+        args = (self.longs([int(c) for c in ctxs]),) + self.meta_args(meta) + tuple(pa) + \
+            (self.longs(offset), self.longs(shape), out)
+        rc = self._done(self._fn("arrayReadPieces")(P(self.env), None, *map(P, args)))
+        dt = {1: np.uint8, 2: np.uint16, 4: np.uint32, 8: np.uint64}[meta.dtype_size]
+        return rc, (self.array_of(out, dt).reshape(shape) if rc == 0 else None)
+
+    def shard_decode_pieces(self, ctx, meta, index, size, pieces, offset, part):
+        nel = int(np.prod(part))
+        out = self.output(meta.dtype_size, nel)
+        args = self.meta_args(meta) + (self.bytes_(index),)
+        tail = (self.longs([o for o, _ in pieces]), self.longs([len(b) for _, b in pieces]),
+                self.objs([self.bytes_(b) for _, b in pieces], b"[B"), self.longs(offset),
+                self.ints(part), out)
+        rc = self._done(self._fn("shardDecodePieces")(P(self.env), None, C.c_int64(int(ctx or 0)),
+                                                      *map(P, args), C.c_int64(size),
+                                                      *map(P, tail)))
+        dt = {1: np.uint8, 2: np.uint16, 4: np.uint32, 8: np.uint64}[meta.dtype_size]
+        return rc, (self.array_of(out, dt).reshape(part) if rc == 0 else None)
+
+    def array_write(self, ctx, meta, arr, offset):
+        """arrayWrite: the region's primitive array → byte[][] (None: all fill, or the whole
+        result None when the call declined)."""
+        kind = KIND[meta.dtype_size]
+        data = self.prim(kind, np.ascontiguousarray(arr).view(
+            {1: np.int8, 2: np.int16, 4: np.int32, 8: np.int64}[meta.dtype_size]).ravel())
+        self.sources.append(data)
+        args = self.meta_args(meta) + (self.longs(offset), self.longs(list(arr.shape)), data)
+        r = self._fn("arrayWrite")(P(self.env), None, C.c_int64(int(ctx or 0)), *map(P, args))
+        self._done(0)
+        if not r:
+            return None
+        out = []
+        for i in range(self.L.fj_len(r)):
+            e = self.L.fj_get(r, i)
+            out.append(None if not e else self.array_of(e, np.uint8).tobytes())
+        return out

@@ -35,9 +35,18 @@ def model_ranges(meta, index, size, lo, hi, max_run, unit=None):
         ents.append((off, nb))
     out = []
     for off, nb in sorted(ents):
+        if out and max_run <= 0:  # one range per entry (host-decoded chains): duplicates once
+            if (off, nb) != out[-1]:
+                out.append((off, nb))
+            continue
         if out and off < out[-1][0] + out[-1][1]:
             o0, n0 = out[-1]
-            out[-1] = (o0, max(o0 + n0, off + nb) - o0)
+            if off + nb <= o0 + n0:
+                continue
+            if off + nb - o0 <= 2 ** 31 - 1:
+                out[-1] = (o0, off + nb - o0)
+            else:  # a union longer than one Java read: continue from the previous end
+                out.append((o0 + n0, off + nb - o0 - n0))
         elif out and off == out[-1][0] + out[-1][1] and max_run > 0 and out[-1][1] + nb <= max_run:
             out[-1] = (out[-1][0], out[-1][1] + nb)
         else:
@@ -106,3 +115,63 @@ def test_ranges_errors():
     assert L.zh_shard_ranges(C.byref(meta), buf, 68, 100, lo, bad, 0, None, 0) == -A.ZH_EINVAL
     un = A.make_meta([8, 8], [8, 8], 1)
     assert L.zh_shard_ranges(C.byref(un), buf, 68, 100, lo, hi, 0, None, 0) == -A.ZH_EINVAL
+
+
+def _index(ents, fmt="<QQ"):
+    body = b"".join(struct.pack(fmt, *e) for e in ents)
+    return body + struct.pack("<I", O.crc32c(body))
+
+
+def test_ranges_overlapping_entries():
+    """Entries that share stored bytes (a writer may point several inner chunks at one payload):
+    raw reads (max_run > 0) unite them into one range; host-decoded chains (max_run == 0) read
+    and decode each entry on its own, as StoreHandleDataProvider does, so every distinct entry
+    is its own range and exact duplicates are read once."""
+    meta = A.make_meta([8, 8], [8, 8], 1, sharded=True, inner_chunk_shape=[4, 4])
+    idx = _index([(0, 16), (0, 16), (8, 16), (40, 8)])
+    assert shard_ranges(meta, idx, -1, [0, 0], [8, 8], 1 << 20) == [(0, 24), (40, 8)]
+    assert shard_ranges(meta, idx, -1, [0, 0], [8, 8], 0) == [(0, 16), (8, 16), (40, 8)]
+    for run in (0, 1 << 20):
+        assert shard_ranges(meta, idx, -1, [0, 0], [8, 8], run) == \
+            model_ranges(meta, idx, -1, [0, 0], [8, 8], run)
+
+
+def test_ranges_union_never_exceeds_a_java_read():
+    """Two overlapping entries of 2^30 + 2^29 bytes each, 2^30 apart: their union (2^31 + 2^29)
+    would not fit one byte[]; the second range continues from the first one's end."""
+    meta = A.make_meta([8, 8], [8, 8], 1, sharded=True, inner_chunk_shape=[4, 4])
+    a, b = (0, 3 << 29), (1 << 30, 3 << 29)
+    idx = _index([a, b, (M1, M1), (M1, M1)])
+    got = shard_ranges(meta, idx, -1, [0, 0], [8, 8], 1 << 40)
+    assert got == [(0, 3 << 29), (3 << 29, (1 << 30) + (3 << 29) - (3 << 29))]
+    assert all(nb <= 2 ** 31 - 1 for _, nb in got)
+    assert got == model_ranges(meta, idx, -1, [0, 0], [8, 8], 1 << 40)
+
+
+@pytest.mark.parametrize("loc", [A.ZH_INDEX_END, A.ZH_INDEX_START])
+def test_shard_index_check_matches_the_oracle_message(loc):
+    """zh_shard_index_check (Crc32cCodec.decode of the index on the host, for reads whose host
+    work the index decides): an intact index passes, a flipped byte fails with exactly the
+    message the oracle's read raises, a chain without an index crc32c is never checked."""
+    from zarrhip._lib import ZhError, shard_index_check
+    shape = [16, 16]
+    meta = A.make_meta(shape, [16, 16], 4, sharded=True, inner_chunk_shape=[4, 8],
+                       index_location=loc, endian=A.ZH_ENDIAN_BIG)
+    shard = encode_oracle(meta, rand_array(shape, 4, seed=3))[0]
+    idx = index_of(meta, shard)
+    shard_index_check(meta, idx)
+    shard_index_check(meta, b"junk" + idx if loc == A.ZH_INDEX_END else idx + b"junk")
+    isz = len(idx)
+    pos = 5 if loc == A.ZH_INDEX_START else len(shard) - isz + 5
+    bad = bytearray(shard)
+    bad[pos] ^= 0x10
+    with pytest.raises(O.OracleError) as eo:
+        O.array_read(meta, [bytes(bad)], [0, 0], shape)
+    with pytest.raises(ZhError) as ed:
+        shard_index_check(meta, index_of(meta, bytes(bad)))
+    assert ed.value.status == A.ZH_EDATA
+    assert str(ed.value) == str(eo.value)
+    assert str(ed.value).startswith("The checksum of the sharding index is invalid. Stored: ")
+    nocrc = A.make_meta(shape, [16, 16], 4, sharded=True, inner_chunk_shape=[4, 8],
+                        index_location=loc, index_crc32c=False)
+    shard_index_check(nocrc, b"\xff" * lib().zh_shard_index_size(C.byref(nocrc)))

@@ -757,15 +757,21 @@ int caller_pieces_all(const zh_array_meta* m, const SrcDesc& src, int64_t isz, c
   hp.pieces.assign(src.pieces, src.pieces + std::max<int64_t>(0, src.npieces));
   for (size_t k = 0; k < hp.pieces.size(); k++) {
     const zh_shard_piece& q = hp.pieces[k];
+    // disjoint, except host-decoded pieces among themselves at distinct offsets: each serves
+    // exactly the entry it was read for (piece_src), as the reference decodes each entry
+    const bool dec = q.data_nbytes != q.nbytes;
+    const bool overlap =
+        k > 0 && (q.offset < hp.pieces[k - 1].offset + hp.pieces[k - 1].nbytes) &&
+        !(dec && hp.pieces[k - 1].data_nbytes != hp.pieces[k - 1].nbytes &&
+          q.offset > hp.pieces[k - 1].offset);
     const bool bad = q.offset < 0 || q.nbytes < 0 || q.data_nbytes < 0 ||
-                     (q.data_nbytes > 0 && !q.data) ||
-                     (k > 0 && q.offset < hp.pieces[k - 1].offset + hp.pieces[k - 1].nbytes) ||
-                     (q.data_nbytes != q.nbytes && m->chain.nested);
+                     (q.data_nbytes > 0 && !q.data) || overlap ||
+                     (k > 0 && q.offset < hp.pieces[k - 1].offset) || (dec && m->chain.nested);
     if (bad) {
       set_err(err, errlen,
               "shard %s: piece %lld (offset %lld, %lld bytes, %lld held) is invalid: pieces "
-              "must be sorted by offset, disjoint, and hold their bytes (host-decoded pieces "
-              "only below single-level sharding)",
+              "must be sorted by offset, disjoint (host-decoded ones: distinct offsets), and "
+              "hold their bytes (host-decoded pieces only below single-level sharding)",
               fmt_ints(cc, n).c_str(), (long long)k, (long long)q.offset, (long long)q.nbytes,
               (long long)q.data_nbytes);
       return ZH_EINVAL;

@@ -22,8 +22,12 @@ namespace zh {
 
 // Entries of the part's box (level-1 cells for nested sharding, read whole), missing ones
 // dropped, unreadable ones (negative, beyond a known shard size, longer than max_entry) left
-// out, sorted by offset; overlapping ranges united and adjacent ones merged while a run stays
-// within max_run bytes.
+// out, sorted by offset.  max_run > 0 (raw ranges): overlapping entries united and adjacent
+// ones merged while a range stays within max_run bytes, and no range exceeds max_entry (an
+// overlap that would continues as a new range from the previous end).  max_run == 0 (each
+// range is read and decoded on its own by host stages): exact duplicates once, every other
+// entry its own range, overlapping or not — the reference reads and decodes each entry
+// separately (StoreHandleDataProvider.read, ShardingIndexedCodec.java:226-231, 353-356).
 static int shard_ranges_impl(const zh_array_meta* m, const uint8_t* index, int64_t shard_nbytes,
                              const int64_t* part_lo, const int64_t* part_hi, int64_t max_run,
                              int64_t max_entry,
@@ -67,12 +71,22 @@ static int shard_ranges_impl(const zh_array_meta* m, const uint8_t* index, int64
   for (const auto& e : ents) {
     if (!out.empty()) {
       auto& b = out.back();
-      const int64_t bend = b.first + b.second;
-      if (e.first < bend) {  // overlapping entries (shared payloads): one range
-        b.second = std::max(bend, e.first + e.second) - b.first;
+      const int64_t bend = b.first + b.second, eend = e.first + e.second;
+      if (max_run <= 0) {  // one range per entry: only exact duplicates collapse
+        if (e == b) continue;
+        out.push_back(e);
         continue;
       }
-      if (e.first == bend && max_run > 0 && b.second + e.second <= max_run) {
+      if (e.first < bend) {  // overlapping entries (shared payloads): one range
+        if (eend <= bend) continue;
+        if (eend - b.first <= max_entry) {
+          b.second = eend - b.first;
+        } else {  // the union would exceed what one read may return: continue from bend
+          out.push_back({bend, eend - bend});
+        }
+        continue;
+      }
+      if (e.first == bend && b.second + e.second <= max_run) {
         b.second += e.second;
         continue;
       }
@@ -196,9 +210,30 @@ int zh_sharding_decode_pieces(zh_ctx* ctx, const zh_array_meta* meta, const zh_s
   return zh_array_read_pieces(ctx, &sm, shard, 1, offset, shp, out, flags, stream, err, errlen);
 }
 
+int zh_shard_index_check(const zh_array_meta* meta, const void* index, int64_t index_nbytes,
+                         char* err, size_t errlen) {
+  if (!meta || !index || !meta->chain.sharded) return ZH_EINVAL;
+  if (!meta->chain.index_has_crc32c) return ZH_OK;
+  const int64_t isz = zh_shard_index_size(meta);
+  if (isz < 4 || index_nbytes < isz) return ZH_OK;  // the read reports the short index
+  const uint8_t* ib = (const uint8_t*)index +
+                      (meta->chain.index_location == ZH_INDEX_START ? 0 : index_nbytes - isz);
+  const uint32_t computed = zh_crc32c(0, ib, (size_t)(isz - 4));
+  const uint8_t* sp = ib + isz - 4;  // stored little-endian (Crc32cCodec.java:36-37)
+  const uint32_t stored =
+      (uint32_t)sp[0] | ((uint32_t)sp[1] << 8) | ((uint32_t)sp[2] << 16) | ((uint32_t)sp[3] << 24);
+  if (computed == stored) return ZH_OK;
+  set_err(err, errlen, "The checksum of the sharding index is invalid. Stored: %d Computed: %d",
+          (int32_t)stored, (int32_t)computed);  // Crc32cCodec.java:39-44 (signed ints)
+  return ZH_EDATA;
+}
+
 int zh_host_staging(zh_ctx* ctx, size_t bytes, void** out) {
   if (!ctx || !out) return ZH_EINVAL;
   *out = nullptr;
+  // the same lock as every read on this context: a concurrent read never sees its staging
+  // freed or replaced under its DMA
+  std::lock_guard<std::mutex> lk(ctx->mu);
   (void)hipSetDevice(ctx->device);
   const size_t cap = (size_t)std::max(64, env_int("ZH_STAGING_MAX_MB", 8192)) << 20;
   const size_t want = std::max<size_t>(bytes, 1);

@@ -1,13 +1,27 @@
 /*
  * zarrhip_jni.c — thin JNI shim from zarr-java to the zarrhip C-ABI (include/zarrhip.h).
- * Built only where a JDK exists (needs $JAVA_HOME/include/jni.h); see INTEGRATION.md.
+ * Built only where a JDK exists (needs $JAVA_HOME/include/jni.h); see INTEGRATION.md.  The
+ * test harness (tests/jni/) compiles it against a test-only stand-in header and drives every
+ * entry point through a fake JNIEnv.
  *
- * Every native method assembles a zh_array_meta from Java primitives, pins the Java
- * arrays for the duration of the call (GetPrimitiveArrayCritical: no JNI calls while
- * pinned), and maps zh_status to the reference's exceptions:
+ * Every native method assembles a zh_array_meta from Java primitives and maps zh_status to the
+ * reference's exceptions:
  *   ZH_EDATA → dev.zarr.zarrjava.ZarrException, ZH_EINVAL → IllegalArgumentException,
  *   ZH_EARITH → ArithmeticException, ZH_EUNSUPPORTED → returned as 3 (Java falls back to
  *   the reference codec), anything else → RuntimeException.
+ *
+ * Critical sections, one policy for every entry point: a Java array is held with
+ * GetPrimitiveArrayCritical only for one slab of the work, and no JNI call is made while one
+ * is held.  A read is cut into C-order slabs of at most ZH_JNI_SLAB_MB (default 256) MiB of
+ * output along the region's first axis of extent >= 2 (so each slab is one contiguous part of
+ * the result), at stored-chunk boundaries along that axis where a slab spans several; per slab
+ * the shim enters the critical sections of the sources that slab needs and of the result,
+ * makes one library call on the slab's sub-region straight into the result (no copy on this
+ * side: the library's pipelined read copies each source once into its page-locked ring), and
+ * leaves them: sources with JNI_ABORT (never written), the result with 0.  arrayWrite copies
+ * its region out of the heap in windows of the same size.  On collectors with a GC locker
+ * (JDK 8-21) a held critical section defers every GC; this bounds the deferral by one slab's
+ * read time instead of the whole read's (INTEGRATION.md "GC and critical sections").
  */
 #include <jni.h>
 #include <stdint.h>
@@ -91,6 +105,125 @@ static int build_meta(JNIEnv* env, jintArray jm, jlongArray jshape, jintArray jc
   return ZH_OK;
 }
 
+/* ---- slabs ------------------------------------------------------------------------------ */
+static int64_t slab_cap_bytes(void) {
+  const char* e = getenv("ZH_JNI_SLAB_MB");
+  long v = e ? strtol(e, NULL, 10) : 256;
+  return (int64_t)(v < 1 ? 1 : v) << 20;
+}
+
+/* A region (or a shard part) cut into slabs along `axis`, the first axis of extent >= 2
+ * (axis 0 when there is none: one slab).  row = output bytes of one index along the axis. */
+typedef struct {
+  int axis;
+  int64_t row;   /* bytes per step along the axis                       */
+  int64_t unit;  /* stored-chunk extent along the axis (slab boundaries) */
+  int64_t cap;   /* output bytes per slab                               */
+} SlabPlan;
+
+static SlabPlan slab_plan(const zh_array_meta* m, const int64_t* shp, int64_t unit_of_axis[],
+                          int64_t cap) {
+  SlabPlan P;
+  P.axis = 0;
+  for (int d = 0; d < m->ndim; d++)
+    if (shp[d] >= 2) {
+      P.axis = d;
+      break;
+    }
+  P.row = m->dtype_size;
+  for (int d = P.axis + 1; d < m->ndim; d++) P.row *= shp[d];
+  P.unit = unit_of_axis[P.axis] > 0 ? unit_of_axis[P.axis] : 1;
+  P.cap = cap;
+  return P;
+}
+
+/* End (exclusive, absolute coordinate) of the slab that starts at s; `end` = region end. */
+static int64_t slab_end(const SlabPlan* P, int64_t s, int64_t end) {
+  int64_t t = P->row > 0 ? P->cap / P->row : 1;
+  if (t < 1) t = 1;
+  if (t >= end - s) return end;
+  int64_t e = s + t;
+  const int64_t al = e / P->unit * P->unit;  /* the last unit boundary inside the slab */
+  return al > s ? al : e;
+}
+
+/* The stored unit along each axis: the inner chunk (sharded: a piece names inner chunks) or
+ * the chunk. */
+static void units_of(const zh_array_meta* m, int sharded_part, int64_t* u) {
+  for (int d = 0; d < m->ndim; d++)
+    u[d] = m->chain.sharded && sharded_part ? m->chain.inner_chunk_shape[d] : m->chunk_shape[d];
+}
+
+/* computeChunkCoords order of the region's chunks: the slab [s, e) along P->axis is the
+ * contiguous index range [*first, *first + *count) of that list (every earlier axis has
+ * extent 1). */
+static void slab_chunks(const zh_array_meta* m, const int64_t* off, const int64_t* shp, int a,
+                        int64_t s, int64_t e, jsize* first, jsize* count) {
+  int64_t stride = 1;
+  for (int d = m->ndim - 1; d > a; d--) {
+    const int64_t c0 = off[d] / m->chunk_shape[d], c1 = (off[d] + shp[d] - 1) / m->chunk_shape[d];
+    stride *= c1 - c0 + 1;
+  }
+  const int64_t lo = off[a] / m->chunk_shape[a];
+  const int64_t b0 = s / m->chunk_shape[a], b1 = (e - 1) / m->chunk_shape[a];
+  *first = (jsize)((b0 - lo) * stride);
+  *count = (jsize)((b1 - b0 + 1) * stride);
+}
+
+/* ---- critical sections ------------------------------------------------------------------ */
+/* The arrays one call holds: sources first, the output last.  pin_enter collects nothing and
+ * makes no JNI call but the Get; pin_release leaves every one (sources JNI_ABORT, the output
+ * 0) in reverse order and frees the bookkeeping. */
+typedef struct {
+  jsize n;                 /* arrays held */
+  jarray* arr;             /* sources (byte[]s), then the output */
+  void** ptr;              /* their critical addresses */
+  int has_out;             /* the last entry is the output */
+  zh_shard_piece* pieces;  /* piece table of a pieces call */
+} Pinned;
+
+static int pin_alloc(Pinned* P, jsize narr, jsize npieces) {
+  memset(P, 0, sizeof(*P));
+  P->arr = (jarray*)calloc((size_t)(narr > 0 ? narr : 1), sizeof(jarray));
+  P->ptr = (void**)calloc((size_t)(narr > 0 ? narr : 1), sizeof(void*));
+  P->pieces = (zh_shard_piece*)calloc((size_t)(npieces > 0 ? npieces : 1), sizeof(zh_shard_piece));
+  return P->arr && P->ptr && P->pieces ? ZH_OK : ZH_ENOMEM;
+}
+
+static int pin_enter(JNIEnv* env, Pinned* P) {
+  for (jsize k = 0; k < P->n; k++) {
+    if (!P->arr[k]) continue;
+    P->ptr[k] = (*env)->GetPrimitiveArrayCritical(env, P->arr[k], NULL);
+    if (!P->ptr[k]) return ZH_ENOMEM;
+  }
+  return ZH_OK;
+}
+
+static void pin_release(JNIEnv* env, Pinned* P) {
+  for (jsize k = P->n - 1; k >= 0; k--)
+    if (P->ptr && P->ptr[k])
+      (*env)->ReleasePrimitiveArrayCritical(env, P->arr[k], P->ptr[k],
+                                            P->has_out && k == P->n - 1 ? 0 : JNI_ABORT);
+  /* local references of the sources (the output is the caller's) */
+  for (jsize k = 0; P->arr && k < P->n - (P->has_out ? 1 : 0); k++)
+    if (P->arr[k]) (*env)->DeleteLocalRef(env, P->arr[k]);
+  free(P->arr);
+  free(P->ptr);
+  free(P->pieces);
+  memset(P, 0, sizeof(*P));
+}
+
+static void region_of(JNIEnv* env, int n, jlongArray joffset, jlongArray jregion, int64_t* o64,
+                      int64_t* r64) {
+  jlong off[ZH_MAX_DIMS], reg[ZH_MAX_DIMS];
+  (*env)->GetLongArrayRegion(env, joffset, 0, n, off);
+  (*env)->GetLongArrayRegion(env, jregion, 0, n, reg);
+  for (int d = 0; d < n; d++) {
+    o64[d] = off[d];
+    r64[d] = reg[d];
+  }
+}
+
 /* core.Array.read replacement: chunks[i] = bytes of the i-th chunk of
  * computeChunkCoords(shape, chunkShape, offset, regionShape) or null (missing key);
  * out = the primitive array behind the result ucar.ma2.Array (C order).
@@ -106,62 +239,64 @@ static jint array_read_common(JNIEnv* env, zh_ctx* const* ctxs, int nctx, jintAr
   st = zh_validate_meta(&m, err, sizeof err);
   if (st == ZH_EUNSUPPORTED) return st;
   if (st != ZH_OK) return throw_status(env, st, err);
-  jsize n = (*env)->GetArrayLength(env, jchunks);
-  zh_chunk_src* srcs = (zh_chunk_src*)calloc((size_t)(n > 0 ? n : 1), sizeof(zh_chunk_src));
-  jbyteArray* arrs = (jbyteArray*)calloc((size_t)(n > 0 ? n : 1), sizeof(jbyteArray));
-  /* copy chunk bytes out of the heap (several may be large: no long critical sections) */
-  void** copies = (void**)calloc((size_t)(n > 0 ? n : 1), sizeof(void*));
-  for (jsize i = 0; i < n; i++) {
-    arrs[i] = (jbyteArray)(*env)->GetObjectArrayElement(env, jchunks, i);
-    if (!arrs[i]) continue;
-    jsize len = (*env)->GetArrayLength(env, arrs[i]);
-    copies[i] = malloc((size_t)(len > 0 ? len : 1));
-    (*env)->GetByteArrayRegion(env, arrs[i], 0, len, (jbyte*)copies[i]);
-    srcs[i].data = copies[i];
-    srcs[i].nbytes = len;
-    (*env)->DeleteLocalRef(env, arrs[i]);
-  }
-  jlong off[ZH_MAX_DIMS], reg[ZH_MAX_DIMS];
-  (*env)->GetLongArrayRegion(env, joffset, 0, m.ndim, off);
-  (*env)->GetLongArrayRegion(env, jregion, 0, m.ndim, reg);
-  int64_t o64[ZH_MAX_DIMS], r64[ZH_MAX_DIMS];
-  for (int d = 0; d < m.ndim; d++) {
-    o64[d] = off[d];
-    r64[d] = reg[d];
-  }
-  /* decode into native memory, then hold the critical section only for the final copy
-   * (a critical section around device work would stall every other Java thread's GC) */
+  int64_t o64[ZH_MAX_DIMS], r64[ZH_MAX_DIMS], u[ZH_MAX_DIMS];
+  region_of(env, m.ndim, joffset, jregion, o64, r64);
   int64_t nel = 1;
   for (int d = 0; d < m.ndim; d++) nel *= r64[d];
-  const size_t obytes = (size_t)nel * (size_t)m.dtype_size;
-  void* tmp = NULL;
-  if ((int64_t)(*env)->GetArrayLength(env, (jarray)out) != nel) {
-    st = ZH_EINVAL;
-    snprintf(err, sizeof err, "output array holds %lld elements, the region %lld",
-             (long long)(*env)->GetArrayLength(env, (jarray)out), (long long)nel);
-  } else if (!(tmp = malloc(obytes > 0 ? obytes : 1))) {
-    st = ZH_ENOMEM;
-    snprintf(err, sizeof err, "out of host memory for the decoded region");
-  } else if (nctx == 1) {
-    st = zh_array_read(ctxs[0], &m, srcs, n, o64, r64, tmp, 0, NULL, err, sizeof err);
-  } else { /* one slab per device, each D2H'd into its slice of the region */
-    st = zh_array_read_multi(ctxs, nctx, 0, &m, srcs, n, o64, r64, tmp, 0, err, sizeof err);
-  }
-  if (st == ZH_OK) {
-    void* dst = (*env)->GetPrimitiveArrayCritical(env, (jarray)out, NULL);
-    if (dst) {
-      memcpy(dst, tmp, obytes);
-      (*env)->ReleasePrimitiveArrayCritical(env, (jarray)out, dst, 0);
-    } else {
-      st = ZH_ENOMEM;
-      snprintf(err, sizeof err, "could not access the output array");
+  if ((int64_t)(*env)->GetArrayLength(env, (jarray)out) != nel)
+    return throw_status(env, ZH_EINVAL, "output array size does not match the region");
+  const jsize nchunks = (*env)->GetArrayLength(env, jchunks);
+  units_of(&m, 0, u);
+  const SlabPlan SP = slab_plan(&m, r64, u, slab_cap_bytes() * (nctx > 1 ? nctx : 1));
+  const int a = SP.axis;
+  for (int64_t s = o64[a]; st == ZH_OK && s < o64[a] + r64[a];) {
+    const int64_t e = slab_end(&SP, s, o64[a] + r64[a]);
+    jsize first = 0, cnt = 0;
+    slab_chunks(&m, o64, r64, a, s, e, &first, &cnt);
+    if (first < 0 || first + cnt > nchunks) {
+      st = ZH_EINVAL;
+      snprintf(err, sizeof err, "%d chunk arrays for a region of more chunks", (int)nchunks);
+      break;
     }
+    Pinned P;
+    zh_chunk_src* srcs = (zh_chunk_src*)calloc((size_t)(cnt > 0 ? cnt : 1), sizeof(zh_chunk_src));
+    if (!srcs || pin_alloc(&P, cnt + 1, 0) != ZH_OK) {
+      free(srcs);
+      free(P.arr);
+      free(P.ptr);
+      free(P.pieces);
+      st = ZH_ENOMEM;
+      snprintf(err, sizeof err, "out of host memory");
+      break;
+    }
+    for (jsize i = 0; i < cnt; i++) {  /* references and lengths first: JNI calls */
+      P.arr[i] = (jarray)(*env)->GetObjectArrayElement(env, jchunks, first + i);
+      srcs[i].nbytes = P.arr[i] ? (*env)->GetArrayLength(env, P.arr[i]) : 0;
+    }
+    P.arr[cnt] = (jarray)out;
+    P.n = cnt + 1;
+    P.has_out = 1;
+    int64_t so[ZH_MAX_DIMS], ss[ZH_MAX_DIMS];
+    for (int d = 0; d < m.ndim; d++) {
+      so[d] = o64[d];
+      ss[d] = r64[d];
+    }
+    so[a] = s;
+    ss[a] = e - s;
+    st = pin_enter(env, &P);
+    if (st == ZH_OK) {
+      for (jsize i = 0; i < cnt; i++) srcs[i].data = P.ptr[i];
+      uint8_t* dst = (uint8_t*)P.ptr[cnt] + (size_t)((s - o64[a]) * SP.row);
+      st = nctx == 1 ? zh_array_read(ctxs[0], &m, srcs, cnt, so, ss, dst, 0, NULL, err, sizeof err)
+                     : zh_array_read_multi(ctxs, nctx, 0, &m, srcs, cnt, so, ss, dst, 0, err,
+                                           sizeof err);
+    } else {
+      snprintf(err, sizeof err, "could not access the chunk or output arrays");
+    }
+    pin_release(env, &P);
+    free(srcs);
+    s = e;
   }
-  free(tmp);
-  for (jsize i = 0; i < n; i++) free(copies[i]);
-  free(copies);
-  free(arrs);
-  free(srcs);
   if (st == ZH_EUNSUPPORTED) return st;
   if (st != ZH_OK) return throw_status(env, st, err);
   return 0;
@@ -193,7 +328,9 @@ JNIEXPORT jint JNICALL Java_dev_zarr_zarrjava_hip_ZarrHip_arrayReadMulti(
                            jchunks, joffset, jregion, out);
 }
 
-/* ShardingIndexedCodec.decode / decodePartial replacement for one shard's bytes. */
+/* ShardingIndexedCodec.decode / decodePartial replacement for one shard's bytes: the part
+ * [offset, offset + partShape) of the shard, in slabs (the shard array and the result held per
+ * slab). */
 JNIEXPORT jint JNICALL Java_dev_zarr_zarrjava_hip_ZarrHip_shardDecodePartial(
     JNIEnv* env, jclass cls, jlong ctx, jintArray jm, jlongArray jshape, jintArray jchunk,
     jintArray jinner, jintArray jorder, jbyteArray jfill, jbyteArray shard, jlongArray joffset,
@@ -207,58 +344,66 @@ JNIEXPORT jint JNICALL Java_dev_zarr_zarrjava_hip_ZarrHip_shardDecodePartial(
   jint part[ZH_MAX_DIMS];
   (*env)->GetLongArrayRegion(env, joffset, 0, m.ndim, off);
   (*env)->GetIntArrayRegion(env, jpart, 0, m.ndim, part);
-  int64_t o64[ZH_MAX_DIMS];
-  for (int d = 0; d < m.ndim; d++) o64[d] = off[d];
-  jsize len = (*env)->GetArrayLength(env, shard);
-  int64_t nel = 1;
-  for (int d = 0; d < m.ndim; d++) nel *= part[d];
-  const size_t obytes = (size_t)nel * (size_t)m.dtype_size;
+  int64_t o64[ZH_MAX_DIMS], p64[ZH_MAX_DIMS], u[ZH_MAX_DIMS], nel = 1;
+  for (int d = 0; d < m.ndim; d++) {
+    o64[d] = off[d];
+    p64[d] = part[d];
+    nel *= part[d];
+  }
   if ((int64_t)(*env)->GetArrayLength(env, (jarray)out) != nel)
     return throw_status(env, ZH_EINVAL, "output array size does not match the part shape");
-  void* src = malloc((size_t)(len > 0 ? len : 1));
-  void* tmp = malloc(obytes > 0 ? obytes : 1);
-  if (!src || !tmp) {
-    free(src);
-    free(tmp);
-    return throw_status(env, ZH_ENOMEM, "out of host memory for the shard");
-  }
-  (*env)->GetByteArrayRegion(env, shard, 0, len, (jbyte*)src);
-  /* decode into native memory; the critical section covers only the final copy */
-  st = zh_sharding_decode_partial((zh_ctx*)(intptr_t)ctx, &m, src, len, o64, part, tmp, 0, NULL,
-                                  err, sizeof err);
-  if (st == ZH_OK) {
-    void* dst = (*env)->GetPrimitiveArrayCritical(env, (jarray)out, NULL);
-    if (dst) {
-      memcpy(dst, tmp, obytes);
-      (*env)->ReleasePrimitiveArrayCritical(env, (jarray)out, dst, 0);
-    } else {
-      st = ZH_ENOMEM;
-      snprintf(err, sizeof err, "could not access the output array");
+  const jsize len = (*env)->GetArrayLength(env, shard);
+  units_of(&m, 1, u);
+  const SlabPlan SP = slab_plan(&m, p64, u, slab_cap_bytes());
+  const int a = SP.axis;
+  for (int64_t s = o64[a]; st == ZH_OK && s < o64[a] + p64[a];) {
+    const int64_t e = slab_end(&SP, s, o64[a] + p64[a]);
+    int64_t so[ZH_MAX_DIMS];
+    int32_t sp[ZH_MAX_DIMS];
+    for (int d = 0; d < m.ndim; d++) {
+      so[d] = o64[d];
+      sp[d] = (int32_t)p64[d];
     }
+    so[a] = s;
+    sp[a] = (int32_t)(e - s);
+    Pinned P;
+    if (pin_alloc(&P, 2, 0) != ZH_OK) {
+      pin_release(env, &P);
+      return throw_status(env, ZH_ENOMEM, "out of host memory");
+    }
+    P.arr[0] = (jarray)(*env)->NewLocalRef(env, shard);
+    P.arr[1] = (jarray)out;
+    P.n = 2;
+    P.has_out = 1;
+    st = pin_enter(env, &P);
+    if (st == ZH_OK)
+      st = zh_sharding_decode_partial((zh_ctx*)(intptr_t)ctx, &m, P.ptr[0], len, so, sp,
+                                      (uint8_t*)P.ptr[1] + (size_t)((s - o64[a]) * SP.row), 0,
+                                      NULL, err, sizeof err);
+    else
+      snprintf(err, sizeof err, "could not access the shard or output arrays");
+    pin_release(env, &P);
+    s = e;
   }
-  free(tmp);
-  free(src);
   if (st == ZH_EUNSUPPORTED) return st;
   if (st != ZH_OK) return throw_status(env, st, err);
   return 0;
 }
 
 /* ---- sub-shard reads: stored index + pieces (zh_array_read_pieces) ---------------------
- * Pure argument marshalling, no copy on this side: the index and piece byte[]s and the
- * result's primitive array are held with GetPrimitiveArrayCritical for the duration of the
- * call and handed to the library as host memory.  The library's pipelined read copies each
- * source once, on several threads, into its page-locked ring and DMAs it (and back out into
- * the result the same way); a single-threaded copy here (GetByteArrayRegion into a staging
- * buffer, then a memcpy into the result) would cost more than the whole read for GiB-sized
- * regions.  While the critical sections are held the call makes no JNI call; the GC waits for
- * at most the read itself.  The shim never reads the index (the device checks it).
- * tests/helpers.py jni_fetch / jni_read restate this call sequence in ctypes, and the GPU
- * tests run it (tests/test_gpu_pieces.py). */
+ * Pure argument marshalling, no copy on this side: per slab the index and piece byte[]s of
+ * the shards the slab touches and the result's primitive array are held with
+ * GetPrimitiveArrayCritical and handed to the library as host memory (the policy at the top).
+ * The library's pipelined read copies each referenced source range once, on several threads,
+ * into its page-locked ring and DMAs it, and the region back out into the result the same way;
+ * a single-threaded copy here (GetByteArrayRegion into a staging buffer, then a memcpy into the
+ * result) would cost more than the whole read for GiB-sized regions.  The shim never reads the
+ * index unless asked to check it (shardRanges' checkIndex; otherwise the device checks it). */
 
 JNIEXPORT jlongArray JNICALL Java_dev_zarr_zarrjava_hip_ZarrHip_shardRanges(
     JNIEnv* env, jclass cls, jintArray jm, jlongArray jshape, jintArray jchunk, jintArray jinner,
     jintArray jorder, jbyteArray jfill, jbyteArray jindex, jlong size, jlongArray jlo,
-    jlongArray jhi, jlong max_run) {
+    jlongArray jhi, jlong max_run, jboolean check_index) {
   (void)cls;
   zh_array_meta m;
   if (build_meta(env, jm, jshape, jchunk, jinner, jorder, jfill, &m) != ZH_OK) {
@@ -274,6 +419,15 @@ JNIEXPORT jlongArray JNICALL Java_dev_zarr_zarrjava_hip_ZarrHip_shardRanges(
     return NULL;
   }
   (*env)->GetByteArrayRegion(env, jindex, 0, ilen, (jbyte*)idx);
+  if (check_index) {  /* Crc32cCodec.decode of the index before any range read (:205) */
+    char err[1024] = {0};
+    const int st = zh_shard_index_check(&m, idx, ilen, err, sizeof err);
+    if (st != ZH_OK) {
+      free(idx);
+      throw_status(env, st, err);
+      return NULL;
+    }
+  }
   (*env)->GetLongArrayRegion(env, jlo, 0, m.ndim, lo);
   (*env)->GetLongArrayRegion(env, jhi, 0, m.ndim, hi);
   for (int d = 0; d < m.ndim; d++) {
@@ -298,71 +452,42 @@ JNIEXPORT jlongArray JNICALL Java_dev_zarr_zarrjava_hip_ZarrHip_shardRanges(
   return res;
 }
 
-/* The shards of a read as zh_shard_src: every index / piece array is collected (local
- * references, lengths, offsets: JNI calls) first, then all of them and the output enter their
- * critical sections together (no JNI call in between).  pin_release() leaves them. */
-typedef struct {
-  jsize n;                 /* arrays held */
-  jarray* arr;             /* index / piece byte[]s, then the output */
-  void** ptr;              /* their critical addresses */
-  zh_shard_piece* pieces;
-} Pinned;
-
-static void pin_release(JNIEnv* env, Pinned* P, jsize n_out) {
-  /* the output (the last `n_out` entries) is written back; the sources are not */
-  for (jsize k = P->n - 1; k >= 0; k--)
-    if (P->ptr[k])
-      (*env)->ReleasePrimitiveArrayCritical(env, P->arr[k], P->ptr[k],
-                                            k >= P->n - n_out ? 0 : JNI_ABORT);
-  free(P->arr);
-  free(P->ptr);
-  free(P->pieces);
-  memset(P, 0, sizeof(*P));
-}
-
-/* srcs[i] for each shard i; out_arr (may be NULL) is pinned last, its address in *out_ptr. */
-static int pin_pieces(JNIEnv* env, jobjectArray jidx, jlongArray jsizes, jobjectArray joffs,
-                      jobjectArray jlens, jobjectArray jdata, jobject out_arr, zh_shard_src* srcs,
-                      Pinned* P, void** out_ptr) {
-  memset(P, 0, sizeof(*P));
-  jsize n = (*env)->GetArrayLength(env, jidx), total = 0;
-  for (jsize i = 0; i < n; i++) {
-    jobjectArray ps = (jobjectArray)(*env)->GetObjectArrayElement(env, jdata, i);
-    if (ps) total += (*env)->GetArrayLength(env, ps);
-    if (ps) (*env)->DeleteLocalRef(env, ps);
+/* Shards [first, first + count) of a pieces call as zh_shard_src: every index / piece array of
+ * those shards is collected (local references, lengths, offsets: JNI calls) into P, followed by
+ * the output, before any critical section is entered.  pin_enter / pin_release then hold and
+ * leave them; pieces_bind points srcs at the held addresses. */
+static int pieces_collect(JNIEnv* env, jobjectArray jidx, jlongArray jsizes, jobjectArray joffs,
+                          jobjectArray jlens, jobjectArray jdata, jsize first, jsize count,
+                          jobject out_arr, zh_shard_src* srcs, Pinned* P, jsize* slot) {
+  jsize total = 0;
+  for (jsize i = 0; i < count; i++) {
+    jobjectArray ps = (jobjectArray)(*env)->GetObjectArrayElement(env, jdata, first + i);
+    if (ps) {
+      total += (*env)->GetArrayLength(env, ps);
+      (*env)->DeleteLocalRef(env, ps);
+    }
   }
   /* one local reference per held array (+ the per-shard arrays, released as we go) */
-  if ((*env)->EnsureLocalCapacity(env, n + total + 16) != 0) return ZH_ENOMEM;
-  P->arr = (jarray*)calloc((size_t)(n + total + 1), sizeof(jarray));
-  P->ptr = (void**)calloc((size_t)(n + total + 1), sizeof(void*));
-  P->pieces = (zh_shard_piece*)calloc((size_t)(total > 0 ? total : 1), sizeof(zh_shard_piece));
-  if (!P->arr || !P->ptr || !P->pieces) return ZH_ENOMEM;
+  if ((*env)->EnsureLocalCapacity(env, count + total + 16) != 0) return ZH_ENOMEM;
+  if (pin_alloc(P, count + total + 1, total) != ZH_OK) return ZH_ENOMEM;
   jsize na = 0, used = 0;
-  /* per shard: the index array, then its pieces (references and lengths only) */
-  jsize* idx_slot = (jsize*)malloc((size_t)(n > 0 ? n : 1) * sizeof(jsize));
-  jsize* piece_first = (jsize*)malloc((size_t)(n > 0 ? n : 1) * sizeof(jsize));
-  if (!idx_slot || !piece_first) {
-    free(idx_slot);
-    free(piece_first);
-    return ZH_ENOMEM;
-  }
-  for (jsize i = 0; i < n; i++) {
+  for (jsize i = 0; i < count; i++) {
     memset(&srcs[i], 0, sizeof(srcs[i]));
     jlong size = -1;
-    (*env)->GetLongArrayRegion(env, jsizes, i, 1, &size);
+    (*env)->GetLongArrayRegion(env, jsizes, first + i, 1, &size);
     srcs[i].shard_nbytes = size;
-    idx_slot[i] = -1;
-    jbyteArray ib = (jbyteArray)(*env)->GetObjectArrayElement(env, jidx, i);
+    slot[2 * i] = -1;  /* index array slot */
+    jbyteArray ib = (jbyteArray)(*env)->GetObjectArrayElement(env, jidx, first + i);
     if (ib) {
       srcs[i].index_nbytes = (*env)->GetArrayLength(env, ib);
-      idx_slot[i] = na;
+      slot[2 * i] = na;
       P->arr[na++] = ib;
     }
-    jobjectArray ps = (jobjectArray)(*env)->GetObjectArrayElement(env, jdata, i);
-    jlongArray po = (jlongArray)(*env)->GetObjectArrayElement(env, joffs, i);
-    jlongArray pl = (jlongArray)(*env)->GetObjectArrayElement(env, jlens, i);
+    jobjectArray ps = (jobjectArray)(*env)->GetObjectArrayElement(env, jdata, first + i);
+    jlongArray po = (jlongArray)(*env)->GetObjectArrayElement(env, joffs, first + i);
+    jlongArray pl = (jlongArray)(*env)->GetObjectArrayElement(env, jlens, first + i);
     jsize np = ps ? (*env)->GetArrayLength(env, ps) : 0;
-    piece_first[i] = na;
+    slot[2 * i + 1] = na;  /* first piece slot */
     srcs[i].pieces = P->pieces + used;
     srcs[i].npieces = np;
     for (jsize k = 0; k < np; k++) {
@@ -380,28 +505,18 @@ static int pin_pieces(JNIEnv* env, jobjectArray jidx, jlongArray jsizes, jobject
     if (po) (*env)->DeleteLocalRef(env, po);
     if (pl) (*env)->DeleteLocalRef(env, pl);
   }
-  if (out_arr) P->arr[na++] = (jarray)out_arr;
+  P->arr[na++] = (jarray)out_arr;
   P->n = na;
-  /* enter every critical section; from here on no JNI call until pin_release */
-  int st = ZH_OK;
-  for (jsize k = 0; k < na && st == ZH_OK; k++) {
-    if (!P->arr[k]) continue;
-    P->ptr[k] = (*env)->GetPrimitiveArrayCritical(env, P->arr[k], NULL);
-    if (!P->ptr[k]) st = ZH_ENOMEM;
+  P->has_out = 1;
+  return ZH_OK;
+}
+
+static void pieces_bind(Pinned* P, zh_shard_src* srcs, jsize count, const jsize* slot) {
+  for (jsize i = 0; i < count; i++) {
+    srcs[i].index = slot[2 * i] >= 0 ? P->ptr[slot[2 * i]] : NULL;
+    zh_shard_piece* q = (zh_shard_piece*)srcs[i].pieces;
+    for (jsize k = 0; k < (jsize)srcs[i].npieces; k++) q[k].data = P->ptr[slot[2 * i + 1] + k];
   }
-  if (st == ZH_OK) {
-    used = 0;
-    for (jsize i = 0; i < n; i++) {
-      if (idx_slot[i] >= 0) srcs[i].index = P->ptr[idx_slot[i]];
-      for (jsize k = 0; k < srcs[i].npieces; k++)
-        P->pieces[used + k].data = P->ptr[piece_first[i] + k];
-      used += (jsize)srcs[i].npieces;
-    }
-    if (out_arr && out_ptr) *out_ptr = P->ptr[na - 1];
-  }
-  free(idx_slot);
-  free(piece_first);
-  return st;
 }
 
 JNIEXPORT jint JNICALL Java_dev_zarr_zarrjava_hip_ZarrHip_arrayReadPieces(
@@ -423,32 +538,54 @@ JNIEXPORT jint JNICALL Java_dev_zarr_zarrjava_hip_ZarrHip_arrayReadPieces(
   zh_ctx* ctxs[64];
   (*env)->GetLongArrayRegion(env, jctxs, 0, k, raw);
   for (jsize i = 0; i < k; i++) ctxs[i] = (zh_ctx*)(intptr_t)raw[i];
-  jlong off[ZH_MAX_DIMS], reg[ZH_MAX_DIMS];
-  int64_t o64[ZH_MAX_DIMS], r64[ZH_MAX_DIMS];
-  (*env)->GetLongArrayRegion(env, joffset, 0, m.ndim, off);
-  (*env)->GetLongArrayRegion(env, jregion, 0, m.ndim, reg);
-  int64_t nel = 1;
-  for (int d = 0; d < m.ndim; d++) {
-    o64[d] = off[d];
-    r64[d] = reg[d];
-    nel *= r64[d];
-  }
+  int64_t o64[ZH_MAX_DIMS], r64[ZH_MAX_DIMS], u[ZH_MAX_DIMS], nel = 1;
+  region_of(env, m.ndim, joffset, jregion, o64, r64);
+  for (int d = 0; d < m.ndim; d++) nel *= r64[d];
   if ((int64_t)(*env)->GetArrayLength(env, (jarray)out) != nel)
     return throw_status(env, ZH_EINVAL, "output array size does not match the region");
-  jsize n = (*env)->GetArrayLength(env, jidx);
-  zh_shard_src* srcs = (zh_shard_src*)calloc((size_t)(n > 0 ? n : 1), sizeof(zh_shard_src));
-  if (!srcs) return throw_status(env, ZH_ENOMEM, "out of host memory");
-  Pinned P;
-  void* dst = NULL;
-  st = pin_pieces(env, jidx, jsizes, joffs, jlens, jdata, out, srcs, &P, &dst);
-  if (st == ZH_OK)
-    st = k == 1 ? zh_array_read_pieces(ctxs[0], &m, srcs, n, o64, r64, dst, 0, NULL, err, sizeof err)
-                : zh_array_read_pieces_multi(ctxs, (int)k, 0, &m, srcs, n, o64, r64, dst, 0, NULL,
-                                             err, sizeof err);
-  else
-    snprintf(err, sizeof err, "could not access the source or output arrays");
-  pin_release(env, &P, 1);
-  free(srcs);
+  const jsize n = (*env)->GetArrayLength(env, jidx);
+  units_of(&m, 1, u);
+  const SlabPlan SP = slab_plan(&m, r64, u, slab_cap_bytes() * k);
+  const int a = SP.axis;
+  for (int64_t s = o64[a]; st == ZH_OK && s < o64[a] + r64[a];) {
+    const int64_t e = slab_end(&SP, s, o64[a] + r64[a]);
+    jsize first = 0, cnt = 0;
+    slab_chunks(&m, o64, r64, a, s, e, &first, &cnt);
+    if (first < 0 || first + cnt > n) {
+      st = ZH_EINVAL;
+      snprintf(err, sizeof err, "%d shard sources for a region of more shards", (int)n);
+      break;
+    }
+    zh_shard_src* srcs = (zh_shard_src*)calloc((size_t)(cnt > 0 ? cnt : 1), sizeof(zh_shard_src));
+    jsize* slot = (jsize*)malloc((size_t)(cnt > 0 ? 2 * cnt : 2) * sizeof(jsize));
+    Pinned P;
+    memset(&P, 0, sizeof P);
+    st = srcs && slot ? pieces_collect(env, jidx, jsizes, joffs, jlens, jdata, first, cnt, out,
+                                       srcs, &P, slot)
+                      : ZH_ENOMEM;
+    if (st == ZH_OK) st = pin_enter(env, &P);
+    if (st == ZH_OK) {
+      int64_t so[ZH_MAX_DIMS], ss[ZH_MAX_DIMS];
+      for (int d = 0; d < m.ndim; d++) {
+        so[d] = o64[d];
+        ss[d] = r64[d];
+      }
+      so[a] = s;
+      ss[a] = e - s;
+      pieces_bind(&P, srcs, cnt, slot);
+      uint8_t* dst = (uint8_t*)P.ptr[P.n - 1] + (size_t)((s - o64[a]) * SP.row);
+      st = k == 1 ? zh_array_read_pieces(ctxs[0], &m, srcs, cnt, so, ss, dst, 0, NULL, err,
+                                         sizeof err)
+                  : zh_array_read_pieces_multi(ctxs, (int)k, 0, &m, srcs, cnt, so, ss, dst, 0,
+                                               NULL, err, sizeof err);
+    } else {
+      snprintf(err, sizeof err, "could not access the source or output arrays");
+    }
+    pin_release(env, &P);
+    free(slot);
+    free(srcs);
+    s = e;
+  }
   if (st == ZH_EUNSUPPORTED) return st;
   if (st != ZH_OK) return throw_status(env, st, err);
   return 0;
@@ -468,9 +605,10 @@ JNIEXPORT jint JNICALL Java_dev_zarr_zarrjava_hip_ZarrHip_shardDecodePieces(
   jint part[ZH_MAX_DIMS];
   (*env)->GetLongArrayRegion(env, joffset, 0, m.ndim, off);
   (*env)->GetIntArrayRegion(env, jpart, 0, m.ndim, part);
-  int64_t o64[ZH_MAX_DIMS], nel = 1;
+  int64_t o64[ZH_MAX_DIMS], p64[ZH_MAX_DIMS], u[ZH_MAX_DIMS], nel = 1;
   for (int d = 0; d < m.ndim; d++) {
     o64[d] = off[d];
+    p64[d] = part[d];
     nel *= part[d];
   }
   if ((int64_t)(*env)->GetArrayLength(env, (jarray)out) != nel)
@@ -486,16 +624,41 @@ JNIEXPORT jint JNICALL Java_dev_zarr_zarrjava_hip_ZarrHip_shardDecodePieces(
   if (!jidx || !jo || !jl || !jd || !js) return throw_status(env, ZH_ENOMEM, "out of memory");
   (*env)->SetLongArrayRegion(env, js, 0, 1, &size);
   zh_ctx* c = (zh_ctx*)(intptr_t)ctx;
-  zh_shard_src src;
-  Pinned P;
-  void* dst = NULL;
-  st = pin_pieces(env, jidx, js, jo, jl, jd, out, &src, &P, &dst);
-  if (st == ZH_OK)
-    st = zh_sharding_decode_pieces(c, &m, &src, o64, (const int32_t*)part, dst, 0, NULL, err,
-                                   sizeof err);
-  else
-    snprintf(err, sizeof err, "could not access the source or output arrays");
-  pin_release(env, &P, 1);
+  units_of(&m, 1, u);
+  const SlabPlan SP = slab_plan(&m, p64, u, slab_cap_bytes());
+  const int a = SP.axis;
+  for (int64_t s = o64[a]; st == ZH_OK && s < o64[a] + p64[a];) {
+    const int64_t e = slab_end(&SP, s, o64[a] + p64[a]);
+    int64_t so[ZH_MAX_DIMS];
+    int32_t sp[ZH_MAX_DIMS];
+    for (int d = 0; d < m.ndim; d++) {
+      so[d] = o64[d];
+      sp[d] = (int32_t)p64[d];
+    }
+    so[a] = s;
+    sp[a] = (int32_t)(e - s);
+    zh_shard_src src;
+    jsize slot[2];
+    Pinned P;
+    memset(&P, 0, sizeof P);
+    st = pieces_collect(env, jidx, js, jo, jl, jd, 0, 1, out, &src, &P, slot);
+    if (st == ZH_OK) st = pin_enter(env, &P);
+    if (st == ZH_OK) {
+      pieces_bind(&P, &src, 1, slot);
+      st = zh_sharding_decode_pieces(c, &m, &src, so, sp,
+                                     (uint8_t*)P.ptr[P.n - 1] + (size_t)((s - o64[a]) * SP.row),
+                                     0, NULL, err, sizeof err);
+    } else {
+      snprintf(err, sizeof err, "could not access the source or output arrays");
+    }
+    pin_release(env, &P);
+    s = e;
+  }
+  (*env)->DeleteLocalRef(env, jidx);
+  (*env)->DeleteLocalRef(env, jo);
+  (*env)->DeleteLocalRef(env, jl);
+  (*env)->DeleteLocalRef(env, jd);
+  (*env)->DeleteLocalRef(env, js);
   if (st == ZH_EUNSUPPORTED) return st;
   if (st != ZH_OK) return throw_status(env, st, err);
   return 0;
@@ -551,8 +714,6 @@ JNIEXPORT jobjectArray JNICALL Java_dev_zarr_zarrjava_hip_ZarrHip_arrayWrite(
   if (!ok) {
     throw_status(env, ZH_ENOMEM, "out of host memory for the encoded chunks");
   } else {
-    /* copy the region out of the heap: the call stages it to the device (no long critical
-     * section around device work) */
     jsize nel = (*env)->GetArrayLength(env, (jarray)data);
     int64_t want = 1;
     for (int d = 0; d < m.ndim; d++) want *= r64[d];
@@ -565,14 +726,24 @@ JNIEXPORT jobjectArray JNICALL Java_dev_zarr_zarrjava_hip_ZarrHip_arrayWrite(
       free(sizes);
       return NULL;
     }
+    /* copy the region out of the heap in windows of one slab (the critical-section policy):
+     * the call stages it to the device */
     const size_t rbytes = (size_t)nel * (size_t)m.dtype_size;
-    void* src = malloc(rbytes > 0 ? rbytes : 1);
-    void* pin = (*env)->GetPrimitiveArrayCritical(env, (jarray)data, NULL);
-    if (src && pin) memcpy(src, pin, rbytes);
-    if (pin) (*env)->ReleasePrimitiveArrayCritical(env, (jarray)data, pin, JNI_ABORT);
-    st = src && pin ? zh_array_write_host((zh_ctx*)(intptr_t)ctx, &m, src, o64, r64, outs, caps,
-                                          sizes, n, err, sizeof err)
-                    : ZH_ENOMEM;
+    const size_t win = (size_t)slab_cap_bytes();
+    uint8_t* src = (uint8_t*)malloc(rbytes > 0 ? rbytes : 1);
+    int pinned = src != NULL;
+    for (size_t o = 0; pinned && o < rbytes; o += win) {
+      void* pin = (*env)->GetPrimitiveArrayCritical(env, (jarray)data, NULL);
+      if (!pin) {
+        pinned = 0;
+        break;
+      }
+      memcpy(src + o, (const uint8_t*)pin + o, rbytes - o < win ? rbytes - o : win);
+      (*env)->ReleasePrimitiveArrayCritical(env, (jarray)data, pin, JNI_ABORT);
+    }
+    st = pinned ? zh_array_write_host((zh_ctx*)(intptr_t)ctx, &m, src, o64, r64, outs, caps,
+                                      sizes, n, err, sizeof err)
+                : ZH_ENOMEM;
     free(src);
     if (st == ZH_OK) {
       jclass bcls = (*env)->FindClass(env, "[B");

@@ -43,6 +43,13 @@ public class HipArray extends Array {
             throws ZarrException {
         if (chain == null) return super.read(offset, shape, parallel);
         ArrayMetadata md = metadata();
+        // core.Array.read's argument checks, same order and messages (M/core/Array.java:380-390)
+        if (offset.length != md.ndim()) {
+            throw new IllegalArgumentException("'offset' needs to have rank '" + md.ndim() + "'.");
+        }
+        if (shape.length != md.ndim()) {
+            throw new IllegalArgumentException("'shape' needs to have rank '" + md.ndim() + "'.");
+        }
         for (int d = 0; d < md.ndim(); d++) {
             if (offset[d] < 0 || offset[d] + shape[d] > md.shape[d]) {
                 throw new ZarrException("Requested data is outside of the array's domain.");

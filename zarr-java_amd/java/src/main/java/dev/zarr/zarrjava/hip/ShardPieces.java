@@ -11,7 +11,8 @@ import java.nio.ByteBuffer;
  * prefix/suffix read of the stored index, zh_shard_ranges (via JNI) for the byte ranges the part
  * references, one store read per range.  For a whole shard: one read.  The stored index is
  * handed to the device unchanged, where its crc32c (Crc32cCodec.java:24-48) and its entries are
- * checked; nothing here parses or trusts it.  No shard is ever assembled on the heap, so a part
+ * checked; nothing here parses or trusts it (with host stages or an unknown shard size the
+ * crc32c is checked on the host first, see part()).  No shard is ever assembled on the heap, so a part
  * whose referenced payload exceeds 2^31 bytes reads like any other (each range is at most
  * 64 MiB; one inner chunk with host stages).
  *
@@ -80,9 +81,15 @@ final class ShardPieces {
             return new ShardPieces(index, size, new long[0], new long[0], new byte[0][]);
         }
         final boolean host = chain.innerHost != null;
+        // The index decides host work before the device sees it when the ranges are decoded
+        // on the host (innerHost) or the shard size is unknown (a corrupt entry could ask for a
+        // 2^31-byte read): then its crc32c is checked here first, as the reference checks it
+        // before any range read (ShardingIndexedCodec.java:205); a mismatch throws the
+        // reference's ZarrException.  Otherwise the device checks it.
+        final boolean check = chain.meta[7] == 1 && (host || size < 0);
         long[] rs = ZarrHip.shardRanges(chain.meta, chain.shape, chain.chunkShape,
                 chain.innerShape, chain.order, chain.fill, index, size, partLo, partHi,
-                host ? 0 : MAX_RUN);
+                host ? 0 : MAX_RUN, check);
         int n = rs.length / 2, k = 0;
         long[] offs = new long[n], lens = new long[n];
         byte[][] data = new byte[n][];

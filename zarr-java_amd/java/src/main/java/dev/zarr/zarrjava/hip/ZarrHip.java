@@ -127,12 +127,14 @@ public final class ZarrHip {
 
     /**
      * zh_shard_ranges: the (offset, nbytes) pairs of the stored shard a part references, read
-     * from its stored index (not checked here: the device does), adjacent ranges merged up to
-     * maxRun bytes (0: one per inner chunk).
+     * from its stored index, adjacent ranges merged up to maxRun bytes (0: one per inner
+     * chunk).  checkIndex: first zh_shard_index_check (the index crc32c on the host; a mismatch
+     * throws the reference's ZarrException); otherwise the device checks it.
      */
     static native long[] shardRanges(int[] meta, long[] shape, int[] chunkShape,
                                      int[] innerShape, int[] order, byte[] fill, byte[] index,
-                                     long shardSize, long[] partLo, long[] partHi, long maxRun);
+                                     long shardSize, long[] partLo, long[] partHi, long maxRun,
+                                     boolean checkIndex) throws dev.zarr.zarrjava.ZarrException;
 
     /**
      * core.Array.read over shards given as stored index + pieces (zh_array_read_pieces; with

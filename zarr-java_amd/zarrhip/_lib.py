@@ -58,6 +58,7 @@ _SIGS = {
     "zh_sharding_decode": (C.c_int, [P, PMETA, P, I64, P, U32, P, CH, SZ]),
     "zh_sharding_decode_partial": (C.c_int, [P, PMETA, P, I64, PI64, PI32, P, U32, P, CH, SZ]),
     "zh_shard_ranges": (I64, [PMETA, P, I64, I64, PI64, PI64, I64, PI64, I64]),
+    "zh_shard_index_check": (C.c_int, [PMETA, P, I64, C.c_char_p, SZ]),
     "zh_array_read_pieces": (C.c_int, [P, PMETA, C.POINTER(A.zh_shard_src), I64, PI64, PI64, P,
                                        U32, P, CH, SZ]),
     "zh_array_read_pieces_multi": (C.c_int, [C.POINTER(P), C.c_int, C.c_int, PMETA,
@@ -448,6 +449,15 @@ def shard_ranges(meta, index, shard_nbytes, part_lo, part_hi, max_run=64 << 20):
                            i64arr(part_hi), int(max_run), out, n)
     assert n2 == n
     return [(out[2 * k], out[2 * k + 1]) for k in range(n)]
+
+
+def shard_index_check(meta, index):
+    """zh_shard_index_check: Crc32cCodec.decode of a stored shard index on the host; raises
+    ZhError(ZH_EDATA) with the reference's message when its crc32c does not match."""
+    L = lib()
+    buf = (C.c_char * max(1, len(index))).from_buffer_copy(bytes(index) or b"\0")
+    err = C.create_string_buffer(1024)
+    check(L.zh_shard_index_check(C.byref(meta), buf, len(index), err, 1024), err)
 
 
 def array_read_pieces_multi(ctxs, meta, shards, offset, shape, out, flags, root=0):

@@ -309,6 +309,14 @@ class Array:
         if len(idx) < isz:  # the device reports "Shard [..] is smaller than its index"
             return _lib.ShardSource(ibuf.ctypes.data, len(idx), size, []), keep
         host = self.chain.inner_host_bb
+        if host or size < 0:
+            # the index decides host work before the device sees it (host decodes of every
+            # referenced range; range reads bounded by nothing but the entries): check its
+            # crc32c first, as the reference does (ShardingIndexedCodec.java:205)
+            try:
+                _lib.shard_index_check(self.zmeta, idx)
+            except _lib.ZhError as e:
+                raise_for(e)
         rs = _lib.shard_ranges(self.zmeta, idx, size, part_lo, part_hi,
                                0 if host else 64 << 20)
         pieces = []
