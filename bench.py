@@ -728,8 +728,12 @@ def run_strong(args, dist, A, meta, rank, ws, local):
         roof["kernel_ms_is"] = "max over ranks"
     gather = None
     if backend in ("nccl", "gloo"):
+        def make_plan(po, ps):  # a plan of one piece of this rank's slab (the overlapped gather)
+            return dev.plan(meta, [where[c] for c in all_coords(L, meta, po, ps)], po, ps,
+                            A.ZH_SRC_DEVICE | A.ZH_OUT_DEVICE)
         gather = gather_to_root(args, dist, dev, backend, plan, out, out_t, region_t, out_bytes,
-                                full_bytes, parts, shape, rank, ws, device, t_dec)
+                                full_bytes, parts, shape, rank, ws, device, t_dec, make_plan,
+                                inner_y)
     host_out = None
     if not args.no_host_out:
         host_out = host_terminated(args, dist, dev, plan, out, out_bytes, shape, so, ss, rank,
@@ -749,21 +753,33 @@ def run_strong(args, dist, A, meta, rank, ws, local):
 
 
 def gather_to_root(args, dist, dev, backend, plan, out, out_t, region_t, out_bytes, full_bytes,
-                   parts, shape, rank, ws, device, t_dec):
-    """Assemble the region on rank 0: RCCL grouped point-to-point (each rank's slab is one
-    contiguous C-order slice, sent straight into its place in the root's region buffer),
-    then the root re-verifies every element of the assembled region against the generator.
-    For the gather-inclusive rate every rank decodes its slab straight into its torch-
-    allocated RCCL buffer (the root: its slice of the region), timed like the headline, so
-    nothing is staged between the decode and the send.  gloo (ranks sharing one GPU,
-    rehearsal): through host tensors, verified per slab."""
+                   parts, shape, rank, ws, device, t_dec, make_plan, align):
+    """Assemble the region on rank 0.  RCCL: every rank's slab is cut into pieces
+    of at most --gather-piece-mb (1 GiB) along y at inner-chunk rows (zarrhip.parallel.
+    gather_pieces); each piece is one contiguous C-order slice, decoded by a plan of its own
+    straight into the rank's RCCL send buffer (the root: into its slice of the region) and sent
+    point-to-point into its place in the root's region buffer as soon as its decode is done:
+    the decode of piece k+1 runs while piece k is on the wire (the send waits only for its own
+    decode: the plan executes on torch's current stream, which the RCCL stream waits on at the
+    send).  The root decodes its own slab on a side stream so that its receives never wait for
+    it, and receives round k of every peer as one group (the peers' links in parallel).  The
+    root then re-verifies every element of the assembled region against the generator.
+    Reported: the overlapped timeline (value_incl_gather), and for comparison the decode into
+    the send buffer followed by the same bounded pieces sent back to back (gather_ms).  gloo
+    (ranks sharing one GPU, rehearsal): through host tensors, verified per slab."""
     import torch
     import torch.distributed as tdist
-    from zarrhip.parallel import slab_byte_offset
+    from zarrhip.parallel import gather_pieces, gather_pieces_p2p, slab_byte_offset
     sizes = [4 * int(__import__("numpy").prod(s)) for _, s in parts]
+    cap = int(args.gather_piece_mb) << 20
+    sched = gather_pieces(shape, parts, 4, cap, align=align)
+    npieces = max(len(p) for p in sched)
     if backend == "nccl":
         grp = tdist.new_group(backend="nccl")
         world = tdist.get_world_size(grp)
+        base = slab_byte_offset(shape, parts[rank][0], 4)
+        # this rank's pieces: a plan each, decoding into its slice of the send buffer
+        mine = [(make_plan(po, ps), b - base, nb) for po, ps, b, nb in sched[rank]]
         # decode straight into this rank's RCCL send buffer (the root: its slice of the
         # region), timed as the headline loop: no staging copy between decode and send
         reps_d = max(1, min(args.steps, 5))
@@ -777,33 +793,70 @@ def gather_to_root(args, dist, dev, backend, plan, out, out_t, region_t, out_byt
         plan.wait()
         t_dec_send = dist.max(time.perf_counter() - tc) / reps_d
 
-        def once():
-            ops = []
-            if rank == 0:
-                for r in range(1, ws):
-                    b = slab_byte_offset(shape, parts[r][0], 4)
-                    ops.append(tdist.P2POp(tdist.irecv, region_t[b:b + sizes[r]], r, grp))
-            else:
-                ops.append(tdist.P2POp(tdist.isend, out_t, 0, grp))
-            for w in tdist.batch_isend_irecv(ops):
+        def sequential():  # the decoded slab sent in bounded pieces, back to back
+            for w in gather_pieces_p2p(tdist, grp, rank, ws, sched, out_t, region_t):
                 w.wait()
             torch.cuda.synchronize(device)
-        once()                      # warm the communicator and the P2P channels
+
+        cur = torch.cuda.current_stream(device)
+        side = torch.cuda.Stream(device)
+
+        def overlapped():  # decode piece k+1 while piece k is on the wire
+            if rank == 0:  # the root's own slab on a side stream: its receives never wait
+                for p, o, _ in mine:
+                    p.execute(out_t.data_ptr() + o, side.cuda_stream)
+
+            def decode(k):  # on torch's current stream: the send of piece k waits for it
+                p, o, _ = mine[k]
+                p.execute(out_t.data_ptr() + o, cur.cuda_stream)
+            for w in gather_pieces_p2p(tdist, grp, rank, ws, sched, out_t, region_t,
+                                       decode if rank else None):
+                w.wait()
+            torch.cuda.synchronize(device)
+            for p, _, _ in mine:
+                p.wait()
+
+        sequential()  # warm the communicator and the P2P channels
+        overlapped()
         reps = max(1, min(args.steps, 3))
         dist.barrier()
         t1 = time.perf_counter()
         for _ in range(reps):
-            once()
+            sequential()
         t_g = dist.max(time.perf_counter() - t1) / reps
+        if rank == 0:
+            torch.cuda.synchronize(device)
+            region_t.zero_()  # the overlapped timeline must fill every byte again
+            torch.cuda.synchronize(device)
+        dist.barrier()
+        t2 = time.perf_counter()
+        for _ in range(reps):
+            overlapped()
+        t_ov = dist.max(time.perf_counter() - t2) / reps
         bad = 0
         if rank == 0:
             bad = dev.synth_verify(region_t.data_ptr(), shape, [0] * len(shape), shape, 4, SEED)
         bad = int(dist.max(bad))
         if bad:
             raise SystemExit(f"gathered region verification FAILED: {bad}")
-        how = ("RCCL grouped send/recv into the root's region buffer (xGMI); each rank "
-               "decodes straight into its send buffer (decode_into_send_ms, max over ranks)")
-    else:
+        for p, _, _ in mine:
+            p.close()
+        how = ("RCCL point-to-point into the root's region buffer (xGMI) in pieces of at most "
+               f"{args.gather_piece_mb} MiB, each sent as soon as its own plan has decoded it "
+               "into the send buffer (the root's own slab on a side stream); gather_ms: the "
+               "decoded slab sent in the same pieces back to back")
+        return {"backend": backend, "how": how, "world_size": world,
+                "piece_cap_bytes": cap, "pieces_per_rank": [len(p) for p in sched],
+                "max_piece_bytes": max(nb for p in sched for _, _, _, nb in p),
+                "gather_ms": round(t_g * 1e3, 3),
+                "decode_into_send_ms": round(t_dec_send * 1e3, 3),
+                "overlapped_ms": round(t_ov * 1e3, 3),
+                "root_ingress_GBps": round((full_bytes - sizes[0]) / t_g / 1e9, 1),
+                "value_incl_gather": round(full_bytes / t_ov / GiB, 2),
+                "value_incl_gather_sequential": round(full_bytes / (t_dec_send + t_g) / GiB, 2),
+                "unit": "GiB/s", "root_verified_elements": full_bytes // 4}
+    # gloo (ranks sharing one GPU): a rehearsal through host tensors
+    if backend != "nccl":
         world = ws
         host = (C.c_char * out_bytes)()
         dev.memcpy(C.addressof(host), out, out_bytes, 1, None, True)
@@ -839,9 +892,11 @@ def gather_to_root(args, dist, dev, backend, plan, out, out_t, region_t, out_byt
 def dry_run(args, dist, rank, ws):
     """--dry-run: the N>1 harness without a GPU (launch, process group, slab partition,
     barrier, max over ranks, one JSON line); no decode runs, so there is no value."""
-    from zarrhip.parallel import slab_partition
+    from zarrhip.parallel import gather_pieces, slab_partition
     shape = [1, 4096, 4096, 1536]
-    so, ss = slab_partition([0] * 4, shape, ws, align=32)[rank]
+    parts = slab_partition([0] * 4, shape, ws, align=32)
+    so, ss = parts[rank]
+    sched = gather_pieces(shape, parts, 4, int(args.gather_piece_mb) << 20, align=32)
     dist.barrier()
     rows = int(dist.max(ss[1]))
     if rank == 0:
@@ -851,6 +906,9 @@ def dry_run(args, dist, rank, ws):
                           "dtype": "u32", "data": "synthetic", "dry_run": True,
                           "config": {"workload": "dry run (no GPU): harness only",
                                      "slab_rows_max": rows,
+                                     "gather_pieces_per_rank": [len(p) for p in sched],
+                                     "gather_max_piece_bytes": max(
+                                         nb for p in sched for _, _, _, nb in p),
                                      "parallelism": f"slab-parallel x{ws}"}}), flush=True)
 
 
@@ -1236,6 +1294,8 @@ def main():
                     help="default: weak at N=1 (one full array), strong at N>1 (one array "
                          "split into per-GPU slabs + gather + host-terminated copy)")
     ap.add_argument("--gather-backend", default="nccl", choices=["nccl", "gloo", "none"])
+    ap.add_argument("--gather-piece-mb", type=int, default=1024,
+                    help="strong mode: largest RCCL message of the overlapped gather (MiB)")
     ap.add_argument("--no-host-out", action="store_true",
                     help="strong mode: skip the host-terminated copy")
     ap.add_argument("--ydiv", type=int, default=1,

@@ -13,7 +13,7 @@ step() {  # name, timeout, cmd...
   timeout -k 10 "$t" "$@" > "$OUT/$name.out" 2> "$OUT/$name.err"
   local rc=$?
   echo "== $name rc=$rc" >&2
-  if [ $rc -ne 0 ]; then tail -40 "$OUT/$name.out" "$OUT/$name.err" >&2; exit $rc; fi
+  if [ $rc -ne 0 ]; then tail -n 40 "$OUT/$name.out" "$OUT/$name.err" >&2; exit $rc; fi
 }
 cd "$R" || exit 1
 step jnitests 300 python3 -u -m pytest tests/test_jni_shim.py -x -v --timeout 120 --timeout-method thread -p no:cacheprovider

@@ -118,12 +118,15 @@ class FakeJVM:
         self.outputs.append(h)
         return h
 
-    def array_of(self, h, dtype):
+    def array_of(self, h, dtype, copy=True):
+        """The elements of a Java array as numpy (copy=False: a view of the fake's buffer)."""
         n = self.L.fj_len(h)
         if n <= 0:
             return np.zeros(0, dtype)
         es = np.dtype(dtype).itemsize
-        return np.frombuffer(C.string_at(self.L.fj_data(h), n * es), dtype).copy()
+        buf = (C.c_char * (n * es)).from_address(self.L.fj_data(h))
+        a = np.frombuffer(buf, dtype)
+        return a.copy() if copy else a
 
     def meta_args(self, meta):
         """DeviceChain's packing: int[14] meta, long[] shape, int[] chunkShape, int[] innerShape

@@ -133,3 +133,99 @@ def test_bench_self_launches_ranks_without_a_launcher():
     d = json.loads(lines[0])
     assert d["n_gpus"] == 2 and d["scaling"] == "strong" and d["dry_run"] is True
     assert d["config"]["slab_rows_max"] == 2048
+    # the overlapped gather's schedule: 2048 rows of 24 MiB per rank in 1 GiB-capped pieces of
+    # 32 rows (inner-chunk aligned) = 64 pieces of 768 MiB each
+    assert d["config"]["gather_pieces_per_rank"] == [64, 64]
+    assert d["config"]["gather_max_piece_bytes"] == 32 * 4096 * 1536 * 4
+
+
+@pytest.mark.parametrize("world", [1, 2, 4, 8])
+@pytest.mark.parametrize("cap_mb,align", [(1024, 32), (100, 32), (10, 32), (64, 1), (1, 7)])
+def test_gather_piece_schedule(world, cap_mb, align):
+    """zarrhip.parallel.gather_pieces (bench.py's bounded, overlapped RCCL gather): every rank's
+    pieces tile its slab exactly once, in order, as contiguous byte ranges of the C-order
+    region; none exceeds the cap unless one row does; boundaries fall on the `align` grid when
+    `align` rows fit the cap."""
+    shape = [1, 4096, 4096, 1536]
+    row = 4096 * 1536 * 4
+    cap = cap_mb << 20
+    parts = P.slab_partition([0] * 4, shape, world, align=32)
+    sched = P.gather_pieces(shape, parts, 4, cap, align=align)
+    assert len(sched) == world
+    covered = 0
+    for (so, ss), pieces in zip(parts, sched):
+        b0 = P.slab_byte_offset(shape, so, 4)
+        pos = b0
+        y = so[1]
+        for po, ps, b, nb in pieces:
+            assert po[0] == 0 and po[2:] == [0, 0] and ps[2:] == [4096, 1536] and ps[0] == 1
+            assert po[1] == y and ps[1] > 0 and b == pos and nb == ps[1] * row
+            if row <= cap:
+                assert nb <= cap
+            else:
+                assert ps[1] == 1
+            if align > 1 and align * row <= cap and po[1] + ps[1] < so[1] + ss[1]:
+                assert (po[1] + ps[1]) % align == 0
+            pos += nb
+            y += ps[1]
+        assert y == so[1] + ss[1] and pos == b0 + ss[1] * row
+        covered += pos - b0
+    assert covered == 4096 * row
+
+
+def test_gather_piece_schedule_small_regions():
+    """Ragged slabs of a small region and an empty slab: same tiling rules."""
+    shape = [1, 1, 37, 5]
+    parts = P.slab_partition([0] * 4, shape, 3, align=1)
+    sched = P.gather_pieces(shape, parts, 2, 3 * 5 * 2, align=1)
+    got = [(po[2], ps[2]) for pieces in sched for po, ps, _, _ in pieces]
+    assert got[0] == (0, 3) and sum(n for _, n in got) == 37
+    assert [b for pieces in sched for _, _, b, _ in pieces] == [o * 10 for o, _ in got]
+    empty = P.gather_pieces([1, 2, 8], [([0, 0, 0], [1, 2, 8]), ([0, 2, 0], [1, 0, 8])], 4,
+                            1 << 20)
+    assert len(empty[0]) == 1 and empty[1] == []
+
+
+def _pieces_worker(rank, world, port, tmp):
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "zarr-java_amd"))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world))
+    import torch
+    import torch.distributed as dist
+    from zarrhip import parallel as PP
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    grp = dist.new_group(backend="gloo")
+    shape = [1, 40, 6, 5]
+    full = np.arange(int(np.prod(shape)) * 4, dtype=np.int64).astype(np.uint8)
+    parts = PP.slab_partition([0] * 4, shape, world, align=4)
+    sched = PP.gather_pieces(shape, parts, 4, 5 * 6 * 5 * 4, align=4)  # pieces of 4 rows
+    so, ss = parts[rank]
+    b0 = PP.slab_byte_offset(shape, so, 4)
+    nb = 4 * int(np.prod(ss))
+    region = torch.zeros(full.size, dtype=torch.uint8)
+    region[b0:b0 + nb] = torch.from_numpy(full[b0:b0 + nb])  # the root's own slab in place
+    send = torch.from_numpy(full[b0:b0 + nb].copy())
+    decoded = []
+    for w in PP.gather_pieces_p2p(dist, grp, rank, world, sched, send, region,
+                                  decode=lambda k: decoded.append(k)):
+        w.wait()
+    if rank == 0:
+        np.save(os.path.join(tmp, "region.npy"), region.numpy())
+        np.save(os.path.join(tmp, "full.npy"), full)
+    with open(os.path.join(tmp, f"decoded{rank}.txt"), "w") as f:
+        f.write(",".join(map(str, decoded)) + "|" + str(len(sched[rank])))
+    dist.destroy_process_group()
+
+
+def test_pieced_gather_p2p_three_ranks(tmp_path):
+    """gather_pieces_p2p (bench.py strong mode's gather) on gloo with three ranks: bounded pieces
+    of every peer's slab land in their places of the root's region (batched on both sides), and a
+    peer calls decode(k) once per piece, in order, before sending it."""
+    import torch.multiprocessing as mp
+    world = 3
+    mp.spawn(_pieces_worker, args=(world, free_port(), str(tmp_path)), nprocs=world, join=True)
+    np.testing.assert_array_equal(np.load(tmp_path / "region.npy"), np.load(tmp_path / "full.npy"))
+    for r in range(1, world):
+        dec, n = open(tmp_path / f"decoded{r}.txt").read().split("|")
+        assert int(n) > 1 and dec == ",".join(map(str, range(int(n))))

@@ -2899,12 +2899,18 @@ void scatter_unmap(void* base, const ScatterAlloc& A) {
   (void)hipGetLastError();
 }
 
-// reserve a virtual range that overlaps no range used before (see g_va_used)
+// reserve a virtual range that overlaps no range used before (see g_va_used).  The driver
+// hands freed address space out again, lowest first; an answer inside a used range is kept
+// reserved (quarantined, never mapped), and that whole used range is reserved too when it is
+// still free, so the next answer skips it instead of walking through it one request at a time
+// (after many arenas a 2 MiB request met more than 16 such answers in a row).
+std::vector<uintptr_t> g_va_blocked;  // starts of used ranges reserved whole
+
 int reserve_fresh(size_t size, size_t align, void** out) {
   std::lock_guard<std::mutex> lk(g_scatter_mu);
   uintptr_t top = 0;
   for (auto& u : g_va_used) top = std::max(top, u.second);
-  for (int attempt = 0; attempt < 16; attempt++) {
+  for (int attempt = 0; attempt < 256; attempt++) {
     void* base = nullptr;
     void* hint = attempt == 0 || top == 0 ? nullptr
                  : (void*)((top + align - 1) / align * align + (uintptr_t)attempt * align);
@@ -2913,14 +2919,38 @@ int reserve_fresh(size_t size, size_t align, void** out) {
       return ZH_ENOMEM;
     }
     const uintptr_t b = (uintptr_t)base, e = b + size;
-    bool clash = false;
-    for (auto& u : g_va_used) clash |= b < u.second && u.first < e;
-    if (!clash) {
+    const std::pair<uintptr_t, uintptr_t>* hit = nullptr;
+    for (auto& u : g_va_used)
+      if (b < u.second && u.first < e) {
+        hit = &u;
+        break;
+      }
+    if (!hit) {
       g_va_used.emplace_back(b, e);
       *out = base;
       return ZH_OK;
     }
     g_va_quarantine.emplace_back(base, size);  // never mapped; kept out of the next answer
+    const uintptr_t u0 = hit->first, u1 = hit->second;
+    if (std::find(g_va_blocked.begin(), g_va_blocked.end(), u0) == g_va_blocked.end()) {
+      g_va_blocked.push_back(u0);  // one try per used range
+      // the parts of the used range around this answer, each reserved at its exact address
+      const std::pair<uintptr_t, uintptr_t> parts[2] = {{u0, b}, {e, u1}};
+      for (const auto& pr : parts) {
+        if (pr.second <= pr.first) continue;
+        void* q = nullptr;
+        if (hipMemAddressReserve(&q, pr.second - pr.first, 0, (void*)pr.first, 0) != hipSuccess) {
+          (void)hipGetLastError();
+          continue;
+        }
+        if ((uintptr_t)q == pr.first) {
+          g_va_quarantine.emplace_back(q, pr.second - pr.first);
+        } else {
+          (void)hipMemAddressFree(q, pr.second - pr.first);
+          (void)hipGetLastError();
+        }
+      }
+    }
   }
   return ZH_ENOMEM;
 }

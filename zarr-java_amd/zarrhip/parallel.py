@@ -57,6 +57,70 @@ def slab_byte_offset(shape, slab_offset, itemsize):
     return off * itemsize
 
 
+def gather_pieces(shape, parts, itemsize, cap_bytes, align=1):
+    """The bounded, overlapped gather's schedule (bench.py strong mode): every
+    rank's slab cut, in order, into pieces of at most `cap_bytes` along the slab's first axis
+    of extent >= 2 (all earlier axes have extent 1, so each piece is one contiguous C-order
+    part of the region, sent into its place in the root's buffer as its decode finishes).
+    Piece boundaries fall on multiples of `align` rows (the inner-chunk extent: no inner chunk
+    is decoded twice) whenever `align` rows fit the cap; a single row larger than the cap is
+    one piece.  Returns, per rank, [(piece_offset, piece_shape, region_byte_offset, nbytes)]."""
+    out = []
+    for so, ss in parts:
+        so, ss = [int(v) for v in so], [int(v) for v in ss]
+        pieces = []
+        if all(v > 0 for v in ss):
+            ax = next((d for d, v in enumerate(ss) if v >= 2), len(ss) - 1)
+            if any(ss[d] != 1 for d in range(ax)):
+                raise ValueError(f"slab {ss} is not one contiguous C-order part of {shape}")
+            row = int(itemsize)
+            for d in range(ax + 1, len(ss)):
+                row *= ss[d]
+            per = max(1, int(cap_bytes) // row)
+            if align > 1 and per >= align:
+                per = per // align * align
+            lo, end = so[ax], so[ax] + ss[ax]
+            while lo < end:
+                hi = min(end, lo + per)
+                if align > 1 and hi < end and hi % align:  # snap to the unit grid
+                    snapped = hi // align * align
+                    hi = snapped if snapped > lo else hi
+                po, ps = list(so), list(ss)
+                po[ax], ps[ax] = lo, hi - lo
+                nb = (hi - lo) * row
+                pieces.append((po, ps, slab_byte_offset(shape, po, itemsize), nb))
+                lo = hi
+        out.append(pieces)
+    return out
+
+
+def gather_pieces_p2p(tdist, grp, rank, world, sched, send_buf, region, decode=None):
+    """The point-to-point part of the pieced gather into rank 0's region buffer (bench.py strong
+    mode; gloo on CPU tensors in tests/test_distributed.py).  `sched` = gather_pieces(...);
+    `send_buf` holds this rank's slab (byte tensor, piece k at its offset within the slab),
+    `region` the root's whole region (byte tensor).  Rank 0 posts round k of every peer as one
+    batch (the peers' links in parallel); a peer sends piece k as a batch of one, after calling
+    decode(k) when given (the send then waits only for that piece's decode).  Every op, batched
+    on both sides, runs on the group's communicator.  Returns the works to wait on."""
+    works = []
+    if rank == 0:
+        for k in range(max((len(p) for p in sched), default=0)):
+            ops = [tdist.P2POp(tdist.irecv, region[sched[r][k][2]:sched[r][k][2] + sched[r][k][3]],
+                               r, grp)
+                   for r in range(1, world) if k < len(sched[r])]
+            if ops:
+                works += tdist.batch_isend_irecv(ops)
+        return works
+    mine = sched[rank]
+    base = mine[0][2] if mine else 0
+    for k, (_, _, b, nb) in enumerate(mine):
+        if decode is not None:
+            decode(k)
+        works += tdist.batch_isend_irecv(
+            [tdist.P2POp(tdist.isend, send_buf[b - base:b - base + nb], 0, grp)])
+    return works
+
+
 def assemble(slabs, shape, axis):
     """Concatenate per-rank slabs (in rank order) into the full region."""
     parts = [np.asarray(s) for s in slabs if np.asarray(s).size]
