@@ -777,6 +777,10 @@ def gather_to_root(args, dist, dev, backend, plan, out, out_t, region_t, out_byt
     if backend == "nccl":
         grp = tdist.new_group(backend="nccl")
         world = tdist.get_world_size(grp)
+        # one collective over the whole group first: every rank creates the RCCL communicator
+        # together (the batched point-to-point ops below then run on it)
+        tdist.all_reduce(torch.zeros(1, device=f"cuda:{device}"), group=grp)
+        torch.cuda.synchronize(device)
         base = slab_byte_offset(shape, parts[rank][0], 4)
         # this rank's pieces: a plan each, decoding into its slice of the send buffer
         mine = [(make_plan(po, ps), b - base, nb) for po, ps, b, nb in sched[rank]]
