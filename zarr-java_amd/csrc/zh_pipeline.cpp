@@ -244,7 +244,11 @@ int read_pipelined(zh_ctx* ctx, const zh_array_meta* meta, const SrcDesc* srcs, 
       meta->chain.sharded ? meta->chain.inner_chunk_shape[ax] : meta->chunk_shape[ax];
   const int64_t a0 = offset[ax], a1 = offset[ax] + shape[ax];
   const int64_t u0 = a0 / unit, u1 = (a1 + unit - 1) / unit, nu = u1 - u0;
-  int64_t want = (std::max(host_out ? obytes : 0, ibytes) + cfg.slab_bytes - 1) / cfg.slab_bytes;
+  const int64_t big = std::max(host_out ? obytes : 0, ibytes);
+  int64_t want = (big + cfg.slab_bytes - 1) / cfg.slab_bytes;
+  // at least 8 slabs of >= 8 MiB: a read of a few hundred MiB (the JNI shim's bounded slabs,
+  // §1 "The JNI shim") otherwise ran as 2 slabs with H2D, decode and D2H barely overlapped
+  want = std::max(want, std::min<int64_t>(8, big / ((int64_t)8 << 20)));
   const int64_t nslab = std::min<int64_t>(std::max<int64_t>(want, 2), nu);
   if (nslab < 2) return ZH_EUNSUPPORTED;
   std::vector<int64_t> bound((size_t)nslab + 1);
