@@ -340,3 +340,36 @@ def test_data_errors_become_zarr_exceptions(dev, tmp_path):
         jvm.array_read_pieces([dev.h.value], meta, fetched, [1, 0, 0], [7, 16, 24])
     assert ej.value.cls == ZE and ej.value.msg.startswith("Could not load byte data for chunk")
     jvm.check_rules()
+
+
+@pytest.mark.gpu
+def test_multi_context_reads_via_shim(dev, tmp_path, slab_mb):
+    """arrayReadPieces and arrayReadMulti with several contexts (ZarrHip.ctxs() under
+    ZH_DEVICES: zh_array_read_pieces_multi / zh_array_read_multi, one slab per context); two
+    extra contexts on the box's one GPU, slabs of 1 MiB per context."""
+    from zarrhip._lib import DeviceContext
+    slab_mb(1)
+    shape = [64, 32, 48]
+    meta, arr, shards = _case("c4", shape=shape, seed=31)
+    paths = _write_store(tmp_path, shards)
+    c1, c2 = DeviceContext(0), DeviceContext(0)
+    try:
+        ctxs = [dev.h.value, c1.h.value, c2.h.value]
+        jvm = FakeJVM()
+        off, shp = [2, 3, 4], [60, 27, 40]
+        n = meta.ndim
+        allc = chunk_coords(meta, [0] * n, shape)
+        pos = {c: i for i, c in enumerate(allc)}
+        rp = [paths[pos[c]] for c in chunk_coords(meta, off, shp)]
+        fetched = jni_fetch(meta, rp, off, shp, max_run=64 << 20)
+        rc, got = jvm.array_read_pieces(ctxs, meta, fetched, off, shp)
+        assert rc == 0
+        np.testing.assert_array_equal(got, _oracle(meta, shards, off, shp))
+        rc, got = jvm.array_read(None, meta, _region_chunks(meta, shards, off, shp), off, shp,
+                                 ctxs=ctxs)
+        assert rc == 0
+        np.testing.assert_array_equal(got, _oracle(meta, shards, off, shp))
+        jvm.check_rules()
+    finally:
+        c1.close()
+        c2.close()

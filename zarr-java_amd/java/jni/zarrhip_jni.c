@@ -12,7 +12,7 @@
  *
  * Critical sections, one policy for every entry point: a Java array is held with
  * GetPrimitiveArrayCritical only for one slab of the work, and no JNI call is made while one
- * is held.  A read is cut into C-order slabs of at most ZH_JNI_SLAB_MB (default 256) MiB of
+ * is held.  A read is cut into C-order slabs of at most ZH_JNI_SLAB_MB (default 1024) MiB of
  * output along the region's first axis of extent >= 2 (so each slab is one contiguous part of
  * the result), at stored-chunk boundaries along that axis where a slab spans several; per slab
  * the shim enters the critical sections of the sources that slab needs and of the result,
@@ -108,7 +108,7 @@ static int build_meta(JNIEnv* env, jintArray jm, jlongArray jshape, jintArray jc
 /* ---- slabs ------------------------------------------------------------------------------ */
 static int64_t slab_cap_bytes(void) {
   const char* e = getenv("ZH_JNI_SLAB_MB");
-  long v = e ? strtol(e, NULL, 10) : 256;
+  long v = e ? strtol(e, NULL, 10) : 1024;
   return (int64_t)(v < 1 ? 1 : v) << 20;
 }
 
