@@ -306,7 +306,7 @@ def test_array_write_via_shim(dev, slab_mb, chain):
     """HipArray.write → arrayWrite: the region copied out of the heap in slab windows, the
     encoded chunk objects equal the oracle's (null where a chunk is all fill_value)."""
     slab_mb(1)
-    shape = [64, 32, 48]
+    shape = [64, 64, 96]  # 1.5 MiB of uint32: two copy windows at ZH_JNI_SLAB_MB=1
     meta, arr, shards = _case(chain, shape=shape, seed=17)
     arr[0:8, 0:16, 0:24] = 7  # one chunk all fill_value: deleted (null)
     want = encode_oracle(meta, arr)
@@ -314,7 +314,7 @@ def test_array_write_via_shim(dev, slab_mb, chain):
     got = jvm.array_write(dev.h.value, meta, arr, [0, 0, 0])
     assert got == want and got[0] is None
     s = jvm.check_rules()
-    assert s.windows == -(-arr.nbytes // (1 << 20))
+    assert s.windows == -(-arr.nbytes // (1 << 20)) == 2
 
 
 @pytest.mark.gpu
