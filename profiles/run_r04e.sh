@@ -17,8 +17,10 @@ step() {  # name, timeout, cmd...
   if [ $rc -ne 0 ]; then tail -n 40 "$OUT/$name.out" "$OUT/$name.err" >&2; exit $rc; fi
 }
 cd "$R" || exit 1
-step smoke_tests 300 python3 -u -m pytest tests/test_gpu_crc_tiles.py tests/test_gpu_c2.py -x -q --timeout 120 --timeout-method thread -p no:cacheprovider
-for cfg in c4 c3 c4crc c3crc; do
+step smoke_tests 300 python3 -u -m pytest tests/test_gpu_crc_tiles.py tests/test_gpu_c2.py "tests/test_gpu_parity.py::test_item_row_order" "tests/test_gpu_parity.py::test_device_encode_tile_groups" -x -q --timeout 120 --timeout-method thread -p no:cacheprovider
+step abw_c4 500 python3 profiles/ab_write_env.py c4 1 3 - ZH_ITEM_ROW=4 ZH_ITEM_ROW=8 ZH_ITEM_ROW=16 ZH_ENC_TGROUP=8 ZH_ENC_TGROUP=8,ZH_ITEM_ROW=2 ZH_ENC_TGROUP=4,ZH_ITEM_ROW=4
+step abw_c3 500 python3 profiles/ab_write_env.py c3 1 3 - ZH_ITEM_ROW=4 ZH_ITEM_ROW=8 ZH_ITEM_ROW=16 ZH_ENC_GROUP=4,ZH_ITEM_ROW=4
+for cfg in c4crc c3crc; do
   step abw_$cfg 500 python3 profiles/ab_write_env.py $cfg 1 3 - ZH_ITEM_ROW=4 ZH_ITEM_ROW=8 ZH_ITEM_ROW=16
 done
 for cfg in c4 c3 c4crc; do

@@ -2425,7 +2425,7 @@ static int array_write_fast(zh_ctx* ctx, const zh_array_meta* m, ScatterArgs a,
       (!nz.cell || env_int("ZH_ENC_TGROUP", -1) > 0)) {
     const int want = env_int("ZH_ENC_TGROUP", -1);
     const int G = want < 0 ? 2 : want;
-    if (G == 1 || G == 2 || G == 4) group = G;
+    if (G == 1 || G == 2 || G == 4 || (G == 8 && !tile_crc)) group = G;
     if (group && tile_crc) v.crc_tile_step = tile_crc_step(tile_ends, (size_t)(8 / group));
   }
   if (group) group_order(v, (items + group - 1) / group, env_int("ZH_ITEM_PERM", 1) != 0);

@@ -3163,6 +3163,7 @@ static bool launch_encode_fast_ds(const ScatterArgs& v, int grid, int group, hip
         case 1: hipLaunchKernelGGL((tiles_group_kernel<3, 1, false, false, true>), dim3(grid), dim3(kBlock), l, s, v); return true;
         case 2: hipLaunchKernelGGL((tiles_group_kernel<3, 2, false, false, true>), dim3(grid), dim3(kBlock), l, s, v); return true;
         case 4: hipLaunchKernelGGL((tiles_group_kernel<3, 4, false, false, true>), dim3(grid), dim3(kBlock), l, s, v); return true;
+        case 8: hipLaunchKernelGGL((tiles_group_kernel<3, 8, false, false, true>), dim3(grid), dim3(kBlock), l, s, v); return true;
         default: return false;
       }
     }
