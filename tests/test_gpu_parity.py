@@ -430,7 +430,7 @@ def test_device_encode_chunk_groups(dev, monkeypatch, dsize, group, crc):
     assert got == want
 
 
-@pytest.mark.parametrize("group", ["0", "1", "2", "4", "8", "-1"])
+@pytest.mark.parametrize("group", ["0", "1", "2", "4", "-1"])
 @pytest.mark.parametrize("loc", [A.ZH_INDEX_END, A.ZH_INDEX_START])
 def test_device_encode_tile_groups(dev, monkeypatch, group, loc):
     """encode_tiles_group_kernel (ZH_ENC_TGROUP chunks per work item, 8/G tiles of each per
@@ -682,29 +682,6 @@ def test_item_permutation_order(dev, monkeypatch, mode):
     meta = A.make_meta(shape, [32, 64, 64], 4, **kw)
     arr = rand_array(shape, 4, seed=31)
     roundtrip(dev, meta, arr, [([0, 0, 0], shape), ([3, 2, 1], [60, 61, 90])])
-
-
-@pytest.mark.parametrize("row", ["2", "3", "4"])
-@pytest.mark.parametrize("mode", ["rows", "tiles", "rows_crc", "tiles_crc"])
-def test_item_row_order(dev, monkeypatch, mode, row):
-    """ZH_ITEM_ROW=R (the grouped kernels visit runs of R consecutive groups, the runs in the
-    golden-ratio order): decode and the one-pass encode give the oracle's bytes, for group
-    counts R divides and (R = 3) ones it does not (the plain order then)."""
-    monkeypatch.setenv("ZH_ITEM_ROW", row)
-    shape = [64, 64, 256]
-    kw = dict(endian=A.ZH_ENDIAN_BIG, sharded=True, inner_chunk_shape=[32, 32, 32])
-    if mode.startswith("tiles"):
-        kw["transpose_order"] = [2, 1, 0]
-    if mode.endswith("crc"):
-        kw["inner_crc32c"] = True
-    meta = A.make_meta(shape, [32, 64, 256], 4, **kw)
-    arr = rand_array(shape, 4, seed=37)
-    shards = roundtrip(dev, meta, arr, [([0, 0, 0], shape), ([1, 3, 5], [62, 60, 250])])
-    for g in ("2", "4", "8"):
-        if mode.endswith("crc") and g == "8":
-            continue
-        monkeypatch.setenv("ZH_ENC_TGROUP" if mode.startswith("tiles") else "ZH_ENC_GROUP", g)
-        assert device_write(dev, meta, arr) == shards
 
 
 def _plan_read_host(dev, meta, srcs, off, shp):

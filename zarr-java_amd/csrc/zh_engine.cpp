@@ -610,19 +610,6 @@ uint64_t golden_item_mul(int64_t total) {
   return m % t;
 }
 
-// The grouped kernels' visit order over `groups` groups: golden-ratio stride (perm), or with
-// ZH_ITEM_ROW = R the same order over runs of R consecutive groups (pgroup in zh_kernels.hip;
-// A/B switch, groups % R == 0 only).
-static void group_order(ScatterArgs& g, int64_t groups, bool perm) {
-  g.item_row = 0;
-  g.item_mul = perm ? golden_item_mul(groups) : 0;
-  const int R = env_int("ZH_ITEM_ROW", 0);
-  if (perm && R > 1 && groups % R == 0 && groups / R > 1) {
-    g.item_row = R;
-    g.item_mul = golden_item_mul(groups / R);
-  }
-}
-
 // Index-CRC spans: 4 KiB per workgroup when the indexes are few (a small read: a 512 KiB
 // index in 128 workgroups instead of 8, the span CRC no longer latency-bound), 64 KiB when
 // there are enough spans to fill the chip anyway (each workgroup also loads 12 KiB of tables).
@@ -1330,7 +1317,7 @@ int plan_create(zh_ctx* ctx, const zh_array_meta* m, const SrcDesc* srcs, int64_
         p->args.tile_ystride = al ? (int64_t)ys : 0;
       }
       if (crc) p->args.crc_tile_step = tile_crc_step(ends, (size_t)(8 / G));
-      group_order(p->args, groups, env_int("ZH_ITEM_PERM", 1) != 0);
+      p->args.item_mul = env_int("ZH_ITEM_PERM", 1) ? golden_item_mul(groups) : 0;
       p->grid = grid_for(ctx, groups);
     }
   }
@@ -1355,7 +1342,7 @@ int plan_create(zh_ctx* ctx, const zh_array_meta* m, const SrcDesc* srcs, int64_
       if (G >= 1 && (xpose || (G << g.fast_vpr_shift) <= 64)) {
         const int64_t groups = (items + G - 1) / G;
         p->args.row_group = G;
-        group_order(p->args, groups, env_int("ZH_ITEM_PERM", 0) != 0);
+        p->args.item_mul = env_int("ZH_ITEM_PERM", 0) ? golden_item_mul(groups) : 0;
         p->grid = grid_for(ctx, groups);
       }
     }
@@ -2425,10 +2412,10 @@ static int array_write_fast(zh_ctx* ctx, const zh_array_meta* m, ScatterArgs a,
       (!nz.cell || env_int("ZH_ENC_TGROUP", -1) > 0)) {
     const int want = env_int("ZH_ENC_TGROUP", -1);
     const int G = want < 0 ? 2 : want;
-    if (G == 1 || G == 2 || G == 4 || (G == 8 && !tile_crc)) group = G;
+    if (G == 1 || G == 2 || G == 4) group = G;
     if (group && tile_crc) v.crc_tile_step = tile_crc_step(tile_ends, (size_t)(8 / group));
   }
-  if (group) group_order(v, (items + group - 1) / group, env_int("ZH_ITEM_PERM", 1) != 0);
+  if (group) v.item_mul = env_int("ZH_ITEM_PERM", 1) ? golden_item_mul((items + group - 1) / group) : 0;
   const int grid = grid_for(ctx, group ? (items + group - 1) / group : pitems);
   ZH_HIPF(launch_encode_fast(v, grid, group, s));
   ZH_HIPF(launch_encode_slow(a, grid, s));

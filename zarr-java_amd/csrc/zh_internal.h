@@ -162,8 +162,6 @@ struct ScatterArgs {
                                 // and the tile rows follow each other (host-checked), so the
                                 // movers load 128-B aligned lines (tiles_rowcrc_aln_kernel)
   int64_t tile_ystride;         // tile_align: unit u's region offset is u · tile_ystride
-  int64_t item_row;             // grouped kernels: > 1 = the visit order permutes runs of this
-                                // many consecutive groups (pgroup); 0/1 = groups one by one
 };
 
 // Chunk-payload CRC-32C pass (inner crc32c codec): one workgroup per (item, 64 KiB span) of

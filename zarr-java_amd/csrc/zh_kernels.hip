@@ -1013,17 +1013,6 @@ __device__ __forceinline__ int64_t pitem(const ScatterArgs& a, int64_t i) {
   return a.item_mul ? (int64_t)(((uint64_t)i * a.item_mul) % (uint64_t)a.total_items) : i;
 }
 
-// Work order of the grouped kernels over `ngroups` groups: the golden-ratio stride order, or
-// (item_row = R > 1, host: ngroups % R == 0) the same order over runs of R consecutive groups,
-// each run kept in order, so the workgroups running at once read R neighbouring groups
-// (z-adjacent chunks: one longer region run) instead of unrelated ones.
-__device__ __forceinline__ int64_t pgroup(const ScatterArgs& a, int64_t gi, int64_t ngroups) {
-  if (!a.item_mul) return gi;
-  if (a.item_row <= 1) return (int64_t)(((uint64_t)gi * a.item_mul) % (uint64_t)ngroups);
-  const uint64_t R = (uint64_t)a.item_row, nrun = (uint64_t)ngroups / R;
-  return (int64_t)((((uint64_t)gi / R) * a.item_mul) % nrun * R + (uint64_t)gi % R);
-}
-
 // decode, fast row kernel: unclipped aligned items whose rows (along the unit-stride dim)
 // are whole 16-byte vectors.  Each lane owns one 16-byte column; the block walks
 // (item, row batch) steps uniformly, and the loads of step k+1 are issued before the
@@ -1295,7 +1284,7 @@ __global__ __launch_bounds__(kBlock) void rows_group_kernel(ScatterArgs a) {
   const bool leader = lane == (q << vs);
   const uint4 ffill = fill16<DS>(a.fill);
   for (int64_t g = blockIdx.x; g < ngroups; g += gridDim.x) {
-    const int64_t pg = pgroup(a, g, ngroups);
+    const int64_t pg = a.item_mul ? (int64_t)(((uint64_t)g * a.item_mul) % (uint64_t)ngroups) : g;
     const int64_t c = pg * G + q;
     bool on = false, fill = false;
     uint4 fv = ffill;
@@ -1388,7 +1377,7 @@ __global__ __launch_bounds__(kBlock) void rows_xpose_kernel(ScatterArgs a) {
   const int64_t ngroups = (a.n_citems + 7) / 8;
   const uint4 ffill = fill16<DS>(a.fill);
   for (int64_t g = blockIdx.x; g < ngroups; g += gridDim.x) {
-    const int64_t pg = pgroup(a, g, ngroups);
+    const int64_t pg = a.item_mul ? (int64_t)(((uint64_t)g * a.item_mul) % (uint64_t)ngroups) : g;
     const int64_t c = pg * 8 + hi;
     bool on = false, fill = false;
     uint4 fv = ffill;
@@ -1714,7 +1703,7 @@ __global__ __launch_bounds__(kBlock) void tiles_group_kernel(ScatterArgs a) {
   const uint32_t f = (uint32_t)a.fill;
   uint32_t* mine = lds + t * kTilePitch;
   for (int64_t gi = blockIdx.x; gi < ngroups; gi += gridDim.x) {
-    const int64_t pg = pgroup(a, gi, ngroups);
+    const int64_t pg = a.item_mul ? (int64_t)(((uint64_t)gi * a.item_mul) % (uint64_t)ngroups) : gi;
     const int64_t c = pg * G + q;
     bool on = false;
     const uint8_t* src = nullptr;
@@ -1885,7 +1874,7 @@ void tiles_rowcrc_kernel(ScatterArgs a) {
   const uint32_t* crow = lds + tc * kTilePitch + r * 33;
   auto sw = [](uint32_t x) { return SWAP ? __builtin_bswap32(x) : x; };
   for (int64_t gi = blockIdx.x; gi < ngroups; gi += gridDim.x) {
-    const int64_t pg = pgroup(a, gi, ngroups);
+    const int64_t pg = a.item_mul ? (int64_t)(((uint64_t)gi * a.item_mul) % (uint64_t)ngroups) : gi;
     const int64_t c = pg * G + q, cc = pg * G + qc;
     bool on = false, onc = false;
     const uint8_t* src = nullptr;
@@ -2044,7 +2033,7 @@ void tiles_rowcrc_aln_kernel(ScatterArgs a) {
   auto sw = [](uint32_t v) { return SWAP ? __builtin_bswap32(v) : v; };
   auto rfl = [](uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); };
   for (int64_t gi = blockIdx.x; gi < a.n_citems; gi += gridDim.x) {
-    const int64_t c = pgroup(a, gi, a.n_citems);
+    const int64_t c = a.item_mul ? (int64_t)(((uint64_t)gi * a.item_mul) % (uint64_t)a.n_citems) : gi;
     const uint4* dp = reinterpret_cast<const uint4*>(a.desc + c);
     const uint4 dx = dp[0], dy = dp[1];
     if ((rfl(dy.z) & kDescFast) == 0) continue;  // block-uniform
@@ -3163,7 +3152,6 @@ static bool launch_encode_fast_ds(const ScatterArgs& v, int grid, int group, hip
         case 1: hipLaunchKernelGGL((tiles_group_kernel<3, 1, false, false, true>), dim3(grid), dim3(kBlock), l, s, v); return true;
         case 2: hipLaunchKernelGGL((tiles_group_kernel<3, 2, false, false, true>), dim3(grid), dim3(kBlock), l, s, v); return true;
         case 4: hipLaunchKernelGGL((tiles_group_kernel<3, 4, false, false, true>), dim3(grid), dim3(kBlock), l, s, v); return true;
-        case 8: hipLaunchKernelGGL((tiles_group_kernel<3, 8, false, false, true>), dim3(grid), dim3(kBlock), l, s, v); return true;
         default: return false;
       }
     }
