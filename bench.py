@@ -1086,8 +1086,7 @@ def store_inclusive(dev, A, shard_slab, offs, sizes, coords, scratch):
         dev.free_pinned(pin)
         arr = z.Array.open(z.FilesystemStore(base).resolve("c4"))
         shape = [1, 4096, 4096, 1536]
-        for name, off, shp, reps in (("two_shards", [0, 0, 0, 0], [1, 1024, 1024, 1536], 2),
-                                     ("sub_shard", [0, 0, 0, 512], [1, 1024, 1024, 512], 3)):
+        def timed(off, shp, reps):
             ts, parts = [], []
             got = None
             for _ in range(reps):
@@ -1097,23 +1096,42 @@ def store_inclusive(dev, A, shard_slab, offs, sizes, coords, scratch):
                 got = arr.read(off, shp)
                 ts.append(time.perf_counter() - t0)
                 parts.append(arr.last_read_timing)
+            return got, ts, parts[ts.index(min(ts))]
+
+        for name, off, shp, reps in (("two_shards", [0, 0, 0, 0], [1, 1024, 1024, 1536], 2),
+                                     ("sub_shard", [0, 0, 0, 512], [1, 1024, 1024, 512], 3)):
+            # the mirror's own store reads into staging buffers, then one library read
+            # (ZH_FILES=0; the default before zh_array_read_files)
+            os.environ["ZH_FILES"] = "0"
+            try:
+                got, ts0, p0 = timed(off, shp, reps)
+                staged = arr.staged_bytes
+            finally:
+                os.environ.pop("ZH_FILES", None)
+            del got
+            got, ts, p = timed(off, shp, reps)  # the default: the library reads the files
             nb = got.nbytes
-            k = ts.index(min(ts))
             r = {"region_offset": off, "region_shape": shp, "ms_min": round(min(ts) * 1e3, 1),
                  "value": round(nb / min(ts) / GiB, 2), "unit": "GiB/s",
-                 "prep_ms": round(parts[k]["prep_s"] * 1e3, 1),
-                 "store_stage_ms": round(parts[k]["stage_s"] * 1e3, 1),
-                 "zh_array_read_ms": round(parts[k]["device_s"] * 1e3, 1),
-                 "staged_bytes": arr.staged_bytes}
+                 "call": "zh_array_read_files (pread into the pipelined read's page-locked "
+                         "ring)" if p.get("files") else "store reads + zh_array_read_pieces",
+                 "store_reads": {"ms_min": round(min(ts0) * 1e3, 1),
+                                 "value": round(nb / min(ts0) / GiB, 2),
+                                 "store_stage_ms": round(p0["stage_s"] * 1e3, 1),
+                                 "zh_array_read_ms": round(p0["device_s"] * 1e3, 1),
+                                 "staged_bytes": staged}}
             dev.memcpy(scratch, got.ctypes.data, nb, 0, None, True)
             r["verify_mismatches"] = int(dev.synth_verify(scratch, shape, off, shp, 4, SEED))
             res[name] = r
             del got
         res["path"] = ("zarrhip.Array.read (Python mirror of core.Array.read) from a "
-                       f"FilesystemStore on {d}: store reads (whole shards; for a partly covered "
-                       "shard the stored index + the referenced runs) + one library read "
-                       "(pipelined H2D through page-locked rings, the stored index's crc32c and "
-                       "the decode on the device, D2H into a fresh numpy array)")
+                       f"FilesystemStore on {d}: one zh_array_read_files call — the library "
+                       "reads each shard's stored index and the ranges the region references "
+                       "(whole shards: all of them) with pread straight into the pipelined "
+                       "read's page-locked ring, overlapped with the H2D, the index crc32c and "
+                       "decode on the device and the D2H into a fresh numpy array; "
+                       "store_reads: the same read with the store reads done by the mirror "
+                       "into staging buffers first (ZH_FILES=0)")
     finally:
         shutil.rmtree(base, ignore_errors=True)
     return res

@@ -16,6 +16,8 @@
  *   zh_array_read_pieces        core.Array.read with sub-shard parts         M/core/Array.java:378-441 + the above
  *   zh_sharding_decode_pieces   ShardingIndexedCodec.decodePartial(StoreHandle, ...) ShardingIndexedCodec.java:245-255
  *   zh_shard_index_check        Crc32cCodec.decode of a shard index (host)    M/v3/codec/core/Crc32cCodec.java:24-48
+ *   zh_array_read_files         core.Array.read over a FilesystemStore        M/core/Array.java:378-441 +
+ *                               (exists / get(keys,start,end) per chunk)     M/store/FilesystemStore.java:43-102
  *   zh_array_write              core.Array.write + writeChunk + ShardingIndexedCodec.encode
  *                                                                            M/core/Array.java:83-156, ShardingIndexedCodec.java:105-168
  *   zh_shard_index_size         ShardingIndexedCodec.getShardIndexSize       ShardingIndexedCodec.java:176-181
@@ -30,6 +32,7 @@
  *   ZH_EDATA   → dev.zarr.zarrjava.ZarrException (message text reproduces the reference's)
  *   ZH_EUNSUPPORTED → caller falls back to the Java codec (chain not device-supported)
  *   ZH_EARITH  → ArithmeticException            (IndexingUtils overflow checks)
+ *   ZH_EIO     → dev.zarr.zarrjava.store.StoreException (a RuntimeException; zh_array_read_files)
  *   ZH_EHIP / ZH_ENOMEM → RuntimeException
  */
 #ifndef ZARRHIP_H
@@ -51,7 +54,8 @@ enum zh_status {
   ZH_EUNSUPPORTED = 3,
   ZH_EHIP = 4,
   ZH_ENOMEM = 5,
-  ZH_EARITH = 6
+  ZH_EARITH = 6,
+  ZH_EIO = 7 /* a store file could not be read (StoreException.readFailed) */
 };
 
 enum zh_endian { ZH_ENDIAN_LITTLE = 0, ZH_ENDIAN_BIG = 1 };
@@ -353,6 +357,28 @@ int zh_sharding_decode_pieces(zh_ctx* ctx, const zh_array_meta* meta, const zh_s
  * context's lock, so it never replaces the staging under a read in flight on another thread;
  * the caller must not use the previous pointer once it calls again. */
 int zh_host_staging(zh_ctx* ctx, size_t bytes, void** out);
+
+/* ---- region reads straight from a FilesystemStore ---------------------------------------
+ * core.Array.read when every chunk key resolves to a file (StoreHandle.toPath(),
+ * M/store/StoreHandle.java:100-105): the library does the store I/O itself.  paths[i] is the
+ * file of the i-th chunk of computeChunkCoords(meta->shape, meta->chunk_shape, offset, shape);
+ * NULL, or a path that is not a regular file, is a missing key (FilesystemStore.exists,
+ * FilesystemStore.java:43-46) → fill_value.  Per file the reads are the reference's:
+ *   unsharded: the whole object (get(keys), :49-58);
+ *   sharded:   the stored index (a prefix or suffix read, get(keys, start), :62-80), then the
+ *              ranges of the inner chunks the part references (StoreHandleDataProvider,
+ *              ShardingIndexedCodec.java:333-357; adjacent ranges merged); the index crc32c
+ *              and every entry are checked on the device, as with zh_array_read_pieces.
+ * The range reads (pread) write straight into the page-locked ring of the pipelined read, so
+ * the file bytes are copied once on the host and the reads overlap the H2D copies, the decode
+ * and the D2H of earlier slabs.  `out`: host memory (flags 0) or device memory (ZH_OUT_DEVICE);
+ * ZH_SRC_DEVICE is not allowed.  A file that cannot be opened or read (other than missing) →
+ * ZH_EIO, "Failed to read from store at '<path>': <reason>".  The chain must be device-
+ * supported (zh_validate_meta); chains with host byte-to-byte stages keep their store reads on
+ * the binding side (zh_array_read_pieces). */
+int zh_array_read_files(zh_ctx* ctx, const zh_array_meta* meta, const char* const* paths,
+                        int64_t npaths, const int64_t* offset, const int64_t* shape, void* out,
+                        uint32_t flags, char* err, size_t errlen);
 
 /* ShardingIndexedCodec.decode: whole shard → chunk_shape elements. */
 int zh_sharding_decode(zh_ctx* ctx, const zh_array_meta* meta, const void* shard, int64_t nbytes,

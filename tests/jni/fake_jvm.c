@@ -22,7 +22,8 @@
 #include "jni.h"
 
 typedef struct FObj {
-  char kind;          /* 'B' 'Z' 'S' 'I' 'J' 'F' 'D' primitive arrays, 'L' object array, 'C' class */
+  char kind;          /* 'B' 'Z' 'S' 'I' 'J' 'F' 'D' primitive arrays, 'L' object array, 'C' class,
+                         'T' java.lang.String (data: its UTF-8 bytes, NUL-terminated) */
   int esize;          /* element bytes (primitive arrays) */
   int64_t len;        /* elements */
   void* data;         /* elements (object arrays: struct FObj*[]) */
@@ -46,6 +47,7 @@ typedef struct {
   int64_t calls_in_critical, dead_ref_uses, calls_with_pending, oob, modified_sources;
   int64_t windows, max_window_ns, total_window_ns, live_local_refs, peak_local_refs;
   int64_t capacity_requested, bad_release;
+  int64_t string_gets, string_releases;
 } FStats;
 
 static FObj* g_objs;
@@ -324,6 +326,35 @@ static void f_ReleasePrimitiveArrayCritical(JNIEnv* env, jarray array, void* car
   }
 }
 
+/* GetStringUTFChars hands out a copy (as a JVM may), freed by the matching Release */
+static const char* f_GetStringUTFChars(JNIEnv* env, jstring str, jboolean* isCopy) {
+  (void)env;
+  enter_call("GetStringUTFChars");
+  FObj* o = deref(str);
+  if (!o || o->kind != 'T') {
+    violation("GetStringUTFChars of a non-string");
+    return NULL;
+  }
+  if (isCopy) *isCopy = 1;
+  g_st.string_gets++;
+  char* c = (char*)malloc((size_t)o->len + 1);
+  memcpy(c, o->data, (size_t)o->len + 1);
+  return c;
+}
+
+static void f_ReleaseStringUTFChars(JNIEnv* env, jstring str, const char* chars) {
+  (void)env;
+  enter_call("ReleaseStringUTFChars");
+  FObj* o = deref(str);
+  if (!o || o->kind != 'T' || !chars) {
+    g_st.bad_release++;
+    violation("ReleaseStringUTFChars without a matching Get");
+    return;
+  }
+  g_st.string_releases++;
+  free((void*)chars);
+}
+
 static struct JNINativeInterface_ g_table = {
     NULL,
     f_FindClass,
@@ -344,6 +375,8 @@ static struct JNINativeInterface_ g_table = {
     (void (*)(JNIEnv*, jlongArray, jsize, jsize, const jlong*))f_SetLongArrayRegion,
     f_GetPrimitiveArrayCritical,
     f_ReleasePrimitiveArrayCritical,
+    f_GetStringUTFChars,
+    f_ReleaseStringUTFChars,
 };
 static JNIEnv g_env = &g_table;
 
@@ -386,6 +419,15 @@ JNIEXPORT jobject fj_new_array(char kind, int64_t len, const void* data) {
   if (!es) return NULL;
   FObj* o = new_obj(kind, es, len, NULL);
   if (data) memcpy(o->data, data, (size_t)len * (size_t)es);
+  return new_ref(o, 0);
+}
+
+/* a java.lang.String holding the UTF-8 text s */
+JNIEXPORT jobject fj_new_string(const char* s) {
+  const size_t n = strlen(s);
+  FObj* o = new_obj('T', 1, (int64_t)n + 1, "java/lang/String");
+  memcpy(o->data, s, n + 1);
+  o->len = (int64_t)n;
   return new_ref(o, 0);
 }
 

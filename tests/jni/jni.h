@@ -33,6 +33,7 @@ typedef jarray jbyteArray;
 typedef jarray jintArray;
 typedef jarray jlongArray;
 typedef jarray jobjectArray;
+typedef jobject jstring;
 
 struct JNINativeInterface_;
 typedef const struct JNINativeInterface_* JNIEnv;
@@ -59,6 +60,8 @@ struct JNINativeInterface_ {
                              const jlong* buf);
   void* (*GetPrimitiveArrayCritical)(JNIEnv* env, jarray array, jboolean* isCopy);
   void (*ReleasePrimitiveArrayCritical)(JNIEnv* env, jarray array, void* carray, jint mode);
+  const char* (*GetStringUTFChars)(JNIEnv* env, jstring str, jboolean* isCopy);
+  void (*ReleaseStringUTFChars)(JNIEnv* env, jstring str, const char* chars);
 };
 
 #endif

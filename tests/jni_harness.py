@@ -23,7 +23,7 @@ class FStats(C.Structure):
         "gets", "releases", "releases_commit", "releases_abort", "max_depth",
         "calls_in_critical", "dead_ref_uses", "calls_with_pending", "oob", "modified_sources",
         "windows", "max_window_ns", "total_window_ns", "live_local_refs", "peak_local_refs",
-        "capacity_requested", "bad_release")]
+        "capacity_requested", "bad_release", "string_gets", "string_releases")]
 
 
 def lib_path():
@@ -44,6 +44,8 @@ def jni_lib():
         L.fj_reset.argtypes = [C.c_int]
         L.fj_new_array.restype = P
         L.fj_new_array.argtypes = [C.c_char, C.c_int64, P]
+        L.fj_new_string.restype = P
+        L.fj_new_string.argtypes = [C.c_char_p]
         L.fj_new_object_array.restype = P
         L.fj_new_object_array.argtypes = [C.c_int64, C.c_char_p]
         L.fj_set.argtypes = [P, C.c_int64, P]
@@ -58,7 +60,7 @@ def jni_lib():
         L.fj_exception.argtypes = [C.c_char_p, C.c_int64, C.c_char_p, C.c_int64]
         L.fj_last_violation.restype = C.c_char_p
         for name in ("arrayRead", "arrayReadMulti", "shardDecodePartial", "arrayReadPieces",
-                     "shardDecodePieces"):
+                     "shardDecodePieces", "arrayReadFiles"):
             getattr(L, "Java_dev_zarr_zarrjava_hip_ZarrHip_" + name).restype = C.c_int32
         L.Java_dev_zarr_zarrjava_hip_ZarrHip_shardRanges.restype = P
         L.Java_dev_zarr_zarrjava_hip_ZarrHip_arrayWrite.restype = P
@@ -170,6 +172,7 @@ class FakeJVM:
         assert s.calls_in_critical == 0 and s.dead_ref_uses == 0 and s.calls_with_pending == 0
         assert s.bad_release == 0 and s.modified_sources == 0 and s.oob == 0
         assert s.gets == s.releases and self.L.fj_depth() == 0
+        assert s.string_gets == s.string_releases
         for h in self.sources:
             g, commit, abort, bad = self.obj_stats(h)
             assert commit == 0 and abort == g and bad == 0, (g, commit, abort, bad)
@@ -274,6 +277,22 @@ class FakeJVM:
                                                       *map(P, tail)))
         dt = {1: np.uint8, 2: np.uint16, 4: np.uint32, 8: np.uint64}[meta.dtype_size]
         return rc, (self.array_of(out, dt).reshape(part) if rc == 0 else None)
+
+    def string(self, text):
+        """A java.lang.String (None: a null reference)."""
+        return None if text is None else self.L.fj_new_string(os.fsencode(text))
+
+    def array_read_files(self, ctx, meta, paths, offset, shape):
+        """arrayReadFiles: HipArray.read over a FilesystemStore — the chunk keys' paths
+        (StoreHandle.toPath()) in computeChunkCoords order, None = no path."""
+        nel = int(np.prod(shape))
+        out = self.output(meta.dtype_size, nel)
+        jp = self.objs([self.string(p) for p in paths], b"java/lang/String")
+        args = self.meta_args(meta) + (jp, self.longs(offset), self.longs(shape), out)
+        rc = self._done(self._fn("arrayReadFiles")(P(self.env), None, C.c_int64(int(ctx or 0)),
+                                                   *map(P, args)))
+        dt = {1: np.uint8, 2: np.uint16, 4: np.uint32, 8: np.uint64}[meta.dtype_size]
+        return rc, (self.array_of(out, dt).reshape(shape) if rc == 0 else None)
 
     def array_write(self, ctx, meta, arr, offset):
         """arrayWrite: the region's primitive array → byte[][] (None: all fill, or the whole

@@ -216,10 +216,13 @@ def test_array_read_matches_oracle_with_missing_shards(tmp_path):
 
 @pytest.mark.parametrize("loc", ["start", "end"])
 @pytest.mark.parametrize("inner_bb", [False, True])
-def test_partial_shard_staging_reads_only_referenced_chunks(tmp_path, loc, inner_bb):
+def test_partial_shard_staging_reads_only_referenced_chunks(tmp_path, monkeypatch, loc,
+                                                           inner_bb):
     """Sub-shard reads fetch the index + referenced inner chunks only (the reference's
     StoreHandleDataProvider path, ShardingIndexedCodec.java:333-357), with identical
-    results."""
+    results.  The mirror's own store reads (ZH_FILES=0; with the default a FilesystemStore's
+    files go to zh_array_read_files: tests/test_gpu_files.py)."""
+    monkeypatch.setenv("ZH_FILES", "0")
     shape = [64, 64, 32]
     fn = (lambda c1: c1.withBytes("BIG").withGzip()) if inner_bb else (lambda c1: c1.withBytes("BIG"))
     m = (z.ArrayMetadataBuilder().withShape(*shape).withDataType(z.DataType.UINT32)

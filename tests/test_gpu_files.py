@@ -1,0 +1,224 @@
+"""Region reads straight from a FilesystemStore's files (zh_array_read_files).
+
+Reference: core.Array.read over a FilesystemStore (M/core/Array.java:378-441) —
+`exists` per chunk key (a regular file, FilesystemStore.java:43-46), `get(keys)` for a whole
+chunk (:49-58), and for a shard the StoreHandleDataProvider reads (ShardingIndexedCodec.java:
+333-357): the index by a prefix / suffix read, one range per referenced inner chunk.  Here the
+library does those reads (pread straight into the pipelined read's page-locked ring); every case
+is compared bit-exactly with the oracle (oracle/zh_oracle.c) on the same stored bytes."""
+import os
+import stat
+
+import numpy as np
+import pytest
+
+import oracle as O
+import zarrhip as z
+from helpers import NP_DT, chunk_coords, encode_oracle, rand_array
+from test_gpu_pieces import CHAINS, REGIONS, make_case, oracle_region, region_paths, write_store
+from zarrhip import _abi as A
+from zarrhip._lib import ZhError
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(params=["one_plan", "pipelined"])
+def mode(request, monkeypatch):
+    """one_plan: a small read (the files are read into host buffers, then one plan);
+    pipelined: thresholds shrunk so that the same reads run in slabs through the rings, each
+    range pread straight into a ring slot."""
+    if request.param == "pipelined":
+        monkeypatch.setenv("ZH_PIPE_MIN_KB", "1")
+        monkeypatch.setenv("ZH_PIPE_SLAB_KB", "4")
+        monkeypatch.setenv("ZH_PIPE_CHUNK_KB", "64")
+        monkeypatch.setenv("ZH_PIPE_THREADS", "3")
+    return request.param
+
+
+def files_read(dev, meta, paths, off, shp, flags=0):
+    out = np.empty(shp, NP_DT[meta.dtype_size])
+    dev.array_read_files(meta, paths, off, shp, out.ctypes.data, flags)
+    return out
+
+
+@pytest.mark.parametrize("chain", list(CHAINS))
+def test_files_read_matches_oracle(dev, tmp_path, mode, chain):
+    meta, arr, shards = make_case(chain, seed=43)
+    shards[3] = None  # a missing shard (no file) reads fill_value
+    paths = write_store(tmp_path, meta, shards)
+    paths[5] = str(tmp_path / "no_such_file")  # a key whose file does not exist: fill too
+    shards[5] = None
+    for off, shp in REGIONS:
+        got = files_read(dev, meta, region_paths(meta, paths, off, shp), off, shp)
+        np.testing.assert_array_equal(got, oracle_region(meta, shards, off, shp))
+
+
+@pytest.mark.parametrize("order", [None, [2, 0, 1]])
+def test_files_unsharded(dev, tmp_path, mode, order):
+    """Unsharded chunks: each file is one whole object (get(keys))."""
+    shape = [24, 32, 48]
+    meta = A.make_meta(shape, [8, 16, 24], 4, fill=(9).to_bytes(4, "little"),
+                       endian=A.ZH_ENDIAN_BIG, transpose_order=order)
+    arr = rand_array(shape, 4, seed=47, fill_frac=0.1, fill=9)
+    chunks = encode_oracle(meta, arr)
+    chunks[2] = None
+    paths = write_store(tmp_path, meta, chunks)
+    for off, shp in REGIONS:
+        got = files_read(dev, meta, region_paths(meta, paths, off, shp), off, shp)
+        np.testing.assert_array_equal(got, oracle_region(meta, chunks, off, shp))
+
+
+def test_files_directory_is_a_missing_key(dev, tmp_path):
+    """FilesystemStore.exists is Files.isRegularFile: a directory at a key reads as fill."""
+    meta, arr, shards = make_case("sharded", seed=53)
+    paths = write_store(tmp_path, meta, shards)
+    os.remove(paths[0])
+    os.mkdir(paths[0])
+    shards[0] = None
+    off, shp = [0, 0, 0], [24, 32, 48]
+    got = files_read(dev, meta, region_paths(meta, paths, off, shp), off, shp)
+    np.testing.assert_array_equal(got, oracle_region(meta, shards, off, shp))
+
+
+@pytest.mark.parametrize("where", ["entry", "stored_crc"])
+def test_files_corrupt_index_reports_device_crc(dev, tmp_path, mode, where):
+    """The stored index goes to the device unchanged: the device's crc32c fails with the
+    reference's message (Crc32cCodec.java:39-44), the oracle's text, for whole shards and
+    parts."""
+    meta, arr, shards = make_case("sharded", seed=59, fill_frac=0.0)
+    bad = list(shards)
+    b = bytearray(bad[1])
+    b[-9 if where == "entry" else -2] ^= 0x10
+    bad[1] = bytes(b)
+    paths = write_store(tmp_path, meta, bad)
+    with pytest.raises(O.OracleError) as eo:
+        O.array_read(meta, [bad[1]], [0, 0, 24], [8, 16, 24])
+    for off, shp in (([0, 0, 24], [8, 16, 24]), ([1, 0, 24], [6, 16, 24])):
+        with pytest.raises(ZhError) as ed:
+            files_read(dev, meta, region_paths(meta, paths, off, shp), off, shp)
+        assert str(ed.value) == str(eo.value)
+        assert str(ed.value).startswith("The checksum of the sharding index is invalid.")
+
+
+def test_files_truncated_shard(dev, tmp_path):
+    """A shard file cut short: entries beyond its end are never read and report the
+    reference's "Could not load byte data for chunk [...]" (ShardingIndexedCodec.java:
+    226-230); a file shorter than its index reports that."""
+    meta, arr, shards = make_case("start_beindex", seed=61, fill_frac=0.0)
+    paths = write_store(tmp_path, meta, shards)
+    full = os.path.getsize(paths[0])
+    os.truncate(paths[0], full - 100)  # the last inner chunk's payload loses 100 bytes
+    off, shp = [0, 0, 0], [8, 16, 24]
+    with pytest.raises(ZhError) as ed:
+        files_read(dev, meta, region_paths(meta, paths, off, shp), off, shp)
+    assert str(ed.value).startswith("Could not load byte data for chunk [")
+    os.truncate(paths[0], 10)
+    with pytest.raises(ZhError) as ed:
+        files_read(dev, meta, region_paths(meta, paths, off, shp), off, shp)
+    assert "is smaller than its index" in str(ed.value)
+
+
+@pytest.mark.skipif(os.geteuid() == 0, reason="root reads files regardless of their mode")
+def test_files_unreadable_is_store_exception(dev, tmp_path):
+    """A file that exists but cannot be read: ZH_EIO → StoreException (readFailed)."""
+    meta, arr, shards = make_case("sharded", seed=67)
+    paths = write_store(tmp_path, meta, shards)
+    os.chmod(paths[0], 0)
+    try:
+        off, shp = [0, 0, 0], [8, 16, 24]
+        with pytest.raises(ZhError) as ed:
+            files_read(dev, meta, region_paths(meta, paths, off, shp), off, shp)
+        assert ed.value.status == A.ZH_EIO
+        assert str(ed.value).startswith(f"Failed to read from store at '{paths[0]}': ")
+    finally:
+        os.chmod(paths[0], stat.S_IRUSR | stat.S_IWUSR)
+
+
+def test_files_device_output(dev, tmp_path, mode):
+    meta, arr, shards = make_case("transpose_be", seed=71)
+    paths = write_store(tmp_path, meta, shards)
+    off, shp = [2, 3, 4], [20, 25, 40]
+    nb = int(np.prod(shp)) * 4
+    d = dev.malloc(nb)
+    try:
+        dev.array_read_files(meta, region_paths(meta, paths, off, shp), off, shp, d,
+                             A.ZH_OUT_DEVICE)
+        got = np.frombuffer(dev.d2h(d, nb), np.uint32).reshape(shp)
+    finally:
+        dev.free(d)
+    np.testing.assert_array_equal(got, oracle_region(meta, shards, off, shp))
+
+
+def test_files_argument_errors(dev, tmp_path):
+    meta, arr, shards = make_case("sharded", seed=73)
+    paths = write_store(tmp_path, meta, shards)
+    off, shp = [0, 0, 0], [24, 32, 48]
+    out = np.empty(shp, np.uint32)
+    with pytest.raises(ZhError) as ed:  # one path short
+        dev.array_read_files(meta, region_paths(meta, paths, off, shp)[:-1], off, shp,
+                             out.ctypes.data)
+    assert ed.value.status == A.ZH_EINVAL
+    with pytest.raises(ZhError) as ed:
+        dev.array_read_files(meta, region_paths(meta, paths, off, shp), off, shp,
+                             out.ctypes.data, A.ZH_SRC_DEVICE)
+    assert ed.value.status == A.ZH_EINVAL
+    with pytest.raises(ZhError) as ed:  # M/core/Array.java:386-390
+        dev.array_read_files(meta, region_paths(meta, paths, off, shp), [1, 0, 0], shp,
+                             out.ctypes.data)
+    assert str(ed.value) == "Requested data is outside of the array's domain."
+
+
+def _rchar():
+    with open("/proc/self/io") as f:
+        for line in f:
+            if line.startswith("rchar:"):
+                return int(line.split()[1])
+    return None
+
+
+def test_files_read_only_referenced_bytes(dev, tmp_path, mode):
+    """StoreHandleDataProvider semantics: a sub-shard part reads the index and the ranges it
+    references, not the shard (bytes read by this process's read calls, /proc/self/io)."""
+    shape = [64, 64, 32]
+    meta = A.make_meta(shape, [64, 64, 32], 4, sharded=True, inner_chunk_shape=[8, 8, 8],
+                       endian=A.ZH_ENDIAN_BIG)
+    arr = rand_array(shape, 4, seed=79, fill_frac=0.0, fill=0)
+    shards = encode_oracle(meta, arr)
+    paths = write_store(tmp_path, meta, shards)
+    if _rchar() is None:
+        pytest.skip("no /proc/self/io")
+    off, shp = [5, 9, 3], [10, 12, 6]
+    r0 = _rchar()
+    got = files_read(dev, meta, paths, off, shp)
+    used = _rchar() - r0
+    np.testing.assert_array_equal(got, arr[5:15, 9:21, 3:9])
+    assert used < len(shards[0]) / 4, used
+    r0 = _rchar()
+    np.testing.assert_array_equal(files_read(dev, meta, paths, [0, 0, 0], shape), arr)
+    assert _rchar() - r0 >= len(shards[0])
+
+
+@pytest.mark.parametrize("inner", [[1, 16, 16, 16], [1, 32, 32, 32]])
+def test_array_read_goes_through_files(dev, tmp_path, monkeypatch, inner):
+    """zarrhip.Array.read over a FilesystemStore hands the files to the library (a region of
+    96 MiB: the default pipelined thresholds), with the result of the mirror's own store reads
+    (ZH_FILES=0) and of the written data."""
+    shape = [1, 256, 384, 256]
+    m = (z.ArrayMetadataBuilder().withShape(*shape).withDataType(z.DataType.UINT32)
+         .withChunkShape(1, 128, 128, 128).withFillValue(0)
+         .withCodecs(lambda c: c.withSharding(
+             inner, lambda c1: c1.withTranspose([0, 3, 2, 1]).withBytes("BIG")))
+         .build())
+    a = z.Array.create(z.FilesystemStore(tmp_path).resolve("f"), m)
+    data = np.random.default_rng(83).integers(0, 2 ** 32, shape, dtype=np.uint32)
+    a.write(None, data)
+    b = z.Array.open(z.FilesystemStore(tmp_path).resolve("f"))
+    got = b.read()
+    assert b.last_read_timing.get("files") is True
+    np.testing.assert_array_equal(got, data)
+    off, shp = [0, 17, 33, 5], [1, 200, 300, 250]
+    part = b.read(off, shp)
+    np.testing.assert_array_equal(part, data[:, 17:217, 33:333, 5:255])
+    monkeypatch.setenv("ZH_FILES", "0")
+    np.testing.assert_array_equal(b.read(off, shp), part)
+    assert b.last_read_timing.get("files") is None

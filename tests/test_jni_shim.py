@@ -174,6 +174,24 @@ def test_pieces_critical_bookkeeping_without_device(slab_mb, mb):
     assert s.windows == 1 and s.gets >= 2
 
 
+@pytest.mark.parametrize("mb", [None, 1])
+def test_files_critical_bookkeeping_without_device(tmp_path, slab_mb, mb):
+    """arrayReadFiles with no context: every path string is converted and released before the
+    first critical section, only the result is held (mode 0) and the library's ZH_EINVAL
+    surfaces as IllegalArgumentException."""
+    slab_mb(mb)
+    shape = [64, 64, 96]
+    meta, arr, shards = _case("c4", shape=shape, seed=5)
+    paths = _write_store(tmp_path, _region_chunks(meta, shards, [0, 0, 0], shape))
+    jvm = FakeJVM()
+    with pytest.raises(JavaException) as e:
+        jvm.array_read_files(0, meta, paths, [0, 0, 0], shape)
+    assert e.value.cls == IAE
+    s = jvm.check_rules()
+    assert s.windows == 1 and s.gets == 1
+    assert s.string_gets == sum(p is not None for p in paths)
+
+
 def test_array_write_declines_a_mismatched_array():
     """arrayWrite returns null (the caller keeps core.Array.write) when the Java array's length
     is not the region's, without entering a critical section."""
@@ -218,6 +236,70 @@ def test_array_read_pieces_via_shim(dev, tmp_path, slab_mb, chain, mb):
             assert slabs > 1
         else:
             assert slabs == 1
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("chain", ["c3", "c4", "crc", "start", "nested", "bytes"])
+@pytest.mark.parametrize("mb", [None, 1])
+def test_array_read_files_via_shim(dev, tmp_path, slab_mb, chain, mb):
+    """HipArray.read over a FilesystemStore: the chunk keys' paths go to arrayReadFiles and the
+    library reads the files (zh_array_read_files); whole shards, parts, a missing file, a null
+    path, one element.  Only the result is held critical, one window per slab."""
+    slab_mb(mb)
+    shape = [64, 32, 48]
+    meta, arr, shards = _case(chain, shape=shape, seed=13)
+    shards[1] = None
+    paths = _write_store(tmp_path, shards)
+    paths[2] = str(tmp_path / "absent")  # a key without a file: fill, as a null path
+    shards[2] = None
+    n = meta.ndim
+    allc = chunk_coords(meta, [0] * n, shape)
+    pos = {c: i for i, c in enumerate(allc)}
+    jvm = FakeJVM()
+    windows = 0
+    for off, shp in [([0, 0, 0], shape), ([3, 5, 7], [57, 20, 33]), ([9, 17, 0], [1, 1, 1])]:
+        rp = [paths[pos[c]] for c in chunk_coords(meta, off, shp)]
+        rc, got = jvm.array_read_files(dev.h.value, meta, rp, off, shp)
+        assert rc == 0
+        np.testing.assert_array_equal(got, _oracle(meta, shards, off, shp))
+        s = jvm.check_rules()
+        assert s.gets == s.windows  # the result only
+        slabs = s.windows - windows
+        windows = s.windows
+        row = 4 * int(np.prod(shp[1:]))
+        if mb == 1 and shp[0] * row > (1 << 20):
+            assert slabs > 1
+        else:
+            assert slabs == 1
+
+
+@pytest.mark.gpu
+def test_array_read_files_errors_via_shim(dev, tmp_path):
+    """A corrupt shard index → ZarrException with the reference's CRC text; an unreadable file
+    (when not root) → StoreException."""
+    meta, arr, shards = _case("c4", seed=17)
+    bad = list(shards)
+    b = bytearray(bad[0])
+    b[-2] ^= 0x10
+    bad[0] = bytes(b)
+    paths = _write_store(tmp_path, bad)
+    off, shp = [0, 0, 0], [8, 16, 24]
+    with pytest.raises(O.OracleError) as eo:
+        O.array_read(meta, [bad[0]], off, shp)
+    jvm = FakeJVM()
+    with pytest.raises(JavaException) as ej:
+        jvm.array_read_files(dev.h.value, meta, [paths[0]], off, shp)
+    assert ej.value.cls == ZE and ej.value.msg == str(eo.value)
+    if os.geteuid() != 0:
+        os.chmod(paths[0], 0)
+        try:
+            with pytest.raises(JavaException) as ej:
+                jvm.array_read_files(dev.h.value, meta, [paths[0]], off, shp)
+            assert ej.value.cls == "dev/zarr/zarrjava/store/StoreException"
+            assert ej.value.msg.startswith("Failed to read from store at ")
+        finally:
+            os.chmod(paths[0], 0o600)
+    jvm.check_rules()
 
 
 @pytest.mark.gpu

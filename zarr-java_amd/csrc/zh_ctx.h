@@ -50,6 +50,10 @@ struct zh_ctx {
   uint8_t* upload_pin = nullptr;   // kUploadSlots × kUploadSlotBytes, created on first use
   std::vector<int> upload_free;
   bool upload_failed = false;
+  // zh_array_read_files: the open store files of the read in progress (under mu), which the
+  // sources' file addresses (zh::file_addr) name by slot
+  std::vector<int> files;
+  std::vector<std::string> file_paths;
 };
 
 namespace zh {
@@ -179,5 +183,25 @@ int read_multi_impl(zh_ctx* const* ctxs, int ndev, int root, const zh_array_meta
 // for host outputs) on stream s.
 int plan_enqueue_impl(zh_plan* p, void* out, hipStream_t s);
 int plan_mark_done_impl(zh_plan* p, hipStream_t s);
+
+int projection(int n, const int64_t* cc, const int64_t* ashape, const int32_t* chunk,
+               const int64_t* soff, const int64_t* sshape, int32_t* co, int32_t* oo, int32_t* ps);
+
+// File addresses (zh_array_read_files): a source byte that lives in store file `slot` of the
+// context's read in progress at byte `off` is named by kFileTag | slot << kFileOffBits | off, a
+// value no host pointer takes (bit 62 set: not a canonical x86-64 user address).  The planner
+// treats it as an opaque host pointer (offsets add, adjacent ranges merge); only the pipelined
+// read's in lanes (and file_materialize) dereference it, with pread.  off < 2^40, slot < 2^22.
+constexpr uint64_t kFileTag = 1ull << 62;
+constexpr int kFileOffBits = 40;
+constexpr int64_t kFileMaxBytes = (int64_t)1 << kFileOffBits;
+constexpr int64_t kFileMaxSlots = (int64_t)1 << (62 - kFileOffBits);
+inline bool is_file_addr(const void* p) { return ((uint64_t)(uintptr_t)p & kFileTag) != 0; }
+inline const uint8_t* file_addr(int64_t slot, int64_t off) {
+  return (const uint8_t*)(uintptr_t)(kFileTag | ((uint64_t)slot << kFileOffBits) | (uint64_t)off);
+}
+// Reads n bytes named by the file address src into dst (pread, retried on EINTR / short
+// reads).  Returns "" or the failure's message (the path and the reason).
+std::string file_fetch(const zh_ctx* ctx, void* dst, const void* src, int64_t n);
 
 }  // namespace zh

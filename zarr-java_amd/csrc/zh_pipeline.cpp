@@ -132,7 +132,7 @@ void in_jobs(zh_plan* p, int64_t slab, int64_t chunk, std::vector<InJob>& jobs,
     const int64_t off = p->h2d[k].first, len = p->h2d_len[k];
     const uint8_t* src = (const uint8_t*)p->h2d[k].second;
     if (len <= 0) continue;
-    if (len >= kDirectMin && host_pinned(src)) {
+    if (len >= kDirectMin && !is_file_addr(src) && host_pinned(src)) {
       flush();  // a window must not span (and overwrite) a directly copied range
       jobs.push_back(InJob{slab, p->d_input + off, len, src, {}});
       continue;
@@ -387,6 +387,16 @@ int read_pipelined(zh_ctx* ctx, const zh_array_meta* meta, const SrcDesc* srcs, 
     }
     abort_all();
   };
+  auto lane_fail_io = [&](const std::string& msg) {  // a store file read failed (ZH_EIO)
+    {
+      std::lock_guard<std::mutex> lk(lane_mu);
+      if (lane_err.load() == ZH_OK) {
+        lane_err = ZH_EIO;
+        lane_msg = msg;
+      }
+    }
+    abort_all();
+  };
   std::vector<std::thread> th;
   std::atomic<int64_t> next_out{0};
   std::vector<std::atomic<int64_t>> in_done((size_t)nslab), out_done((size_t)nslab);
@@ -420,8 +430,20 @@ int read_pipelined(zh_ctx* ctx, const zh_array_meta* meta, const SrcDesc* srcs, 
             flip ^= 1;
             e = hipEventSynchronize(slot_ev[(size_t)k]);  // the slot's previous DMA is done
             uint8_t* slot = (uint8_t*)ctx->ring_in[(size_t)k];
-            for (auto& part : J.parts)
-              copy_bytes(slot + part.first, part.second.first, part.second.second);
+            std::string io;
+            for (auto& part : J.parts) {
+              if (!is_file_addr(part.second.first)) {
+                copy_bytes(slot + part.first, part.second.first, part.second.second);
+                continue;
+              }
+              // a store file's range (zh_array_read_files): read straight into the slot
+              io = file_fetch(ctx, slot + part.first, part.second.first, part.second.second);
+              if (!io.empty()) break;
+            }
+            if (!io.empty()) {
+              lane_fail_io(io);
+              break;
+            }
             if (e == hipSuccess)
               e = hipMemcpyAsync(J.dst, slot, (size_t)J.len, hipMemcpyHostToDevice, ctx->pipe_in);
             if (e == hipSuccess) e = hipEventRecord(slot_ev[(size_t)k], ctx->pipe_in);

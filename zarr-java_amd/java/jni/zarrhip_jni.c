@@ -7,8 +7,9 @@
  * Every native method assembles a zh_array_meta from Java primitives and maps zh_status to the
  * reference's exceptions:
  *   ZH_EDATA → dev.zarr.zarrjava.ZarrException, ZH_EINVAL → IllegalArgumentException,
- *   ZH_EARITH → ArithmeticException, ZH_EUNSUPPORTED → returned as 3 (Java falls back to
- *   the reference codec), anything else → RuntimeException.
+ *   ZH_EARITH → ArithmeticException, ZH_EIO → dev.zarr.zarrjava.store.StoreException (a
+ *   RuntimeException, as FilesystemStore's readFailed), ZH_EUNSUPPORTED → returned as 3 (Java
+ *   falls back to the reference codec), anything else → RuntimeException.
  *
  * Critical sections, one policy for every entry point: a Java array is held with
  * GetPrimitiveArrayCritical only for one slab of the work, and no JNI call is made while one
@@ -36,6 +37,7 @@ static int throw_status(JNIEnv* env, int st, const char* msg) {
   if (st == ZH_EDATA) cls = "dev/zarr/zarrjava/ZarrException";
   else if (st == ZH_EINVAL) cls = "java/lang/IllegalArgumentException";
   else if (st == ZH_EARITH) cls = "java/lang/ArithmeticException";
+  else if (st == ZH_EIO) cls = "dev/zarr/zarrjava/store/StoreException";
   jclass c = (*env)->FindClass(env, cls);
   if (c) (*env)->ThrowNew(env, c, msg && *msg ? msg : "zarrhip error");
   return st;
@@ -326,6 +328,85 @@ JNIEXPORT jint JNICALL Java_dev_zarr_zarrjava_hip_ZarrHip_arrayReadMulti(
   for (jsize i = 0; i < k; i++) ctxs[i] = (zh_ctx*)(intptr_t)raw[i];
   return array_read_common(env, ctxs, (int)k, jm, jshape, jchunk, jinner, jorder, jfill,
                            jchunks, joffset, jregion, out);
+}
+
+/* core.Array.read over a FilesystemStore (HipArray.read): paths[i] = StoreHandle.toPath() of the
+ * i-th chunk of computeChunkCoords(shape, chunkShape, offset, regionShape), or null.  The library
+ * reads the files itself (zh_array_read_files): no source array crosses the boundary, so per
+ * slab only the result is held critical.  The paths are converted before any critical section
+ * (GetStringUTFChars is a JNI call; its modified UTF-8 equals UTF-8 for every path without
+ * NUL or supplementary characters). */
+JNIEXPORT jint JNICALL Java_dev_zarr_zarrjava_hip_ZarrHip_arrayReadFiles(
+    JNIEnv* env, jclass cls, jlong ctx, jintArray jm, jlongArray jshape, jintArray jchunk,
+    jintArray jinner, jintArray jorder, jbyteArray jfill, jobjectArray jpaths,
+    jlongArray joffset, jlongArray jregion, jobject out) {
+  (void)cls;
+  zh_array_meta m;
+  int st = build_meta(env, jm, jshape, jchunk, jinner, jorder, jfill, &m);
+  if (st != ZH_OK) return st;
+  char err[1024] = {0};
+  st = zh_validate_meta(&m, err, sizeof err);
+  if (st == ZH_EUNSUPPORTED) return st;
+  if (st != ZH_OK) return throw_status(env, st, err);
+  int64_t o64[ZH_MAX_DIMS], r64[ZH_MAX_DIMS], u[ZH_MAX_DIMS], nel = 1;
+  region_of(env, m.ndim, joffset, jregion, o64, r64);
+  for (int d = 0; d < m.ndim; d++) nel *= r64[d];
+  if ((int64_t)(*env)->GetArrayLength(env, (jarray)out) != nel)
+    return throw_status(env, ZH_EINVAL, "output array size does not match the region");
+  const jsize n = (*env)->GetArrayLength(env, jpaths);
+  char** paths = (char**)calloc((size_t)(n > 0 ? n : 1), sizeof(char*));
+  if (!paths) return throw_status(env, ZH_ENOMEM, "out of host memory");
+  for (jsize i = 0; st == ZH_OK && i < n; i++) {
+    jstring js = (jstring)(*env)->GetObjectArrayElement(env, jpaths, i);
+    if (!js) continue;
+    const char* c = (*env)->GetStringUTFChars(env, js, NULL);
+    if (c) {
+      paths[i] = strdup(c);
+      (*env)->ReleaseStringUTFChars(env, js, c);
+    }
+    (*env)->DeleteLocalRef(env, js);
+    if (!c || !paths[i]) {
+      st = ZH_ENOMEM;
+      snprintf(err, sizeof err, "out of host memory");
+    }
+  }
+  zh_ctx* c = (zh_ctx*)(intptr_t)ctx;
+  units_of(&m, 0, u);
+  const SlabPlan SP = slab_plan(&m, r64, u, slab_cap_bytes());
+  const int a = SP.axis;
+  for (int64_t s = o64[a]; st == ZH_OK && s < o64[a] + r64[a];) {
+    const int64_t e = slab_end(&SP, s, o64[a] + r64[a]);
+    jsize first = 0, cnt = 0;
+    slab_chunks(&m, o64, r64, a, s, e, &first, &cnt);
+    if (first < 0 || first + cnt > n) {
+      st = ZH_EINVAL;
+      snprintf(err, sizeof err, "%d chunk paths for a region of more chunks", (int)n);
+      break;
+    }
+    int64_t so[ZH_MAX_DIMS], ss[ZH_MAX_DIMS];
+    for (int d = 0; d < m.ndim; d++) {
+      so[d] = o64[d];
+      ss[d] = r64[d];
+    }
+    so[a] = s;
+    ss[a] = e - s;
+    void* pin = (*env)->GetPrimitiveArrayCritical(env, (jarray)out, NULL);
+    if (pin) {
+      st = zh_array_read_files(c, &m, (const char* const*)(paths + first), cnt, so, ss,
+                               (uint8_t*)pin + (size_t)((s - o64[a]) * SP.row), 0, err,
+                               sizeof err);
+      (*env)->ReleasePrimitiveArrayCritical(env, (jarray)out, pin, 0);
+    } else {
+      st = ZH_ENOMEM;
+      snprintf(err, sizeof err, "could not access the output array");
+    }
+    s = e;
+  }
+  for (jsize i = 0; i < n; i++) free(paths[i]);
+  free(paths);
+  if (st == ZH_EUNSUPPORTED) return st;
+  if (st != ZH_OK) return throw_status(env, st, err);
+  return 0;
 }
 
 /* ShardingIndexedCodec.decode / decodePartial replacement for one shard's bytes: the part

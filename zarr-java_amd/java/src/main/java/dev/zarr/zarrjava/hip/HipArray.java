@@ -1,6 +1,7 @@
 package dev.zarr.zarrjava.hip;
 
 import dev.zarr.zarrjava.ZarrException;
+import dev.zarr.zarrjava.store.FilesystemStore;
 import dev.zarr.zarrjava.store.StoreHandle;
 import dev.zarr.zarrjava.utils.IndexingUtils;
 import dev.zarr.zarrjava.utils.Utils;
@@ -18,10 +19,12 @@ import java.util.stream.IntStream;
  * of the per-shard ForkJoin loop of core.Array.read (M/core/Array.java:378-441).
  * Unsupported chains use {@code super.read}.
  *
- * The store I/O keeps the reference's shape and parallelism (the chunk loop runs as a
- * parallel stream, M/core/Array.java:403-407): a whole shard is one read; a sub-shard part is
- * its stored index plus the ranges it references (ShardPieces, StoreHandleDataProvider
- * semantics).  The index is checked on the device.
+ * Over a FilesystemStore (one device, no host byte-to-byte stages) the chunk files' paths
+ * (StoreHandle.toPath(), M/store/StoreHandle.java:100-105) go to the library, which does the
+ * store reads itself (arrayReadFiles).  Otherwise the store I/O keeps the reference's shape and
+ * parallelism (the chunk loop runs as a parallel stream, M/core/Array.java:403-407): a whole
+ * shard is one read; a sub-shard part is its stored index plus the ranges it references
+ * (ShardPieces, StoreHandleDataProvider semantics).  The index is checked on the device.
  */
 public class HipArray extends Array {
     private final DeviceChain chain;
@@ -58,6 +61,24 @@ public class HipArray extends Array {
         final int[] cs = md.chunkShape();
         final long[][] coords = IndexingUtils.computeChunkCoords(md.shape, cs, offset, shape);
         final boolean sharded = chain.meta[3] == 1;
+        long[] ctxs = ZarrHip.ctxs();
+        if (storeHandle.store instanceof FilesystemStore && chain.innerHost == null
+                && ctxs.length == 1) {
+            // the library reads the chunk files itself (FilesystemStore.exists / get semantics,
+            // M/store/FilesystemStore.java:43-102): pread into its page-locked ring, overlapped
+            // with the device work; nothing of the chunks enters the Java heap
+            String[] paths = new String[coords.length];
+            for (int i = 0; i < coords.length; i++) {
+                paths[i] = storeHandle.resolve(md.chunkKeyEncoding().encodeChunkKey(coords[i]))
+                        .toPath().toString();
+            }
+            ucar.ma2.Array out = ucar.ma2.Array.factory(md.dataType().getMA2DataType(),
+                    Utils.toIntArray(shape));
+            int st = ZarrHip.arrayReadFiles(ctxs[0], chain.meta, chain.shape, chain.chunkShape,
+                    chain.innerShape, chain.order, chain.fill, paths, offset, shape,
+                    out.getStorage());
+            return st == 0 ? out : super.read(offset, shape, parallel);
+        }
         final ShardPieces[] shards = new ShardPieces[coords.length];
         final byte[][] chunks = new byte[coords.length][];
         IntStream loop = IntStream.range(0, coords.length);
@@ -92,7 +113,6 @@ public class HipArray extends Array {
         }
         ucar.ma2.Array out = ucar.ma2.Array.factory(md.dataType().getMA2DataType(),
                 Utils.toIntArray(shape));
-        long[] ctxs = ZarrHip.ctxs();
         int st;
         if (sharded) {
             st = ZarrHip.arrayReadPieces(ctxs, chain.meta, chain.shape, chain.chunkShape,

@@ -147,6 +147,17 @@ public final class ZarrHip {
                                       long[][] pieceLens, byte[][][] pieceData, long[] offset,
                                       long[] regionShape, Object out);
 
+    /**
+     * core.Array.read over a FilesystemStore (zh_array_read_files): paths[i] is
+     * StoreHandle.toPath() of the i-th chunk of computeChunkCoords (null: no key); the library
+     * reads the files (exists, the index and the referenced ranges, or whole chunks) with the
+     * pipelined read, so no chunk bytes cross into the Java heap.  An unreadable file throws
+     * dev.zarr.zarrjava.store.StoreException.
+     */
+    static native int arrayReadFiles(long ctx, int[] meta, long[] shape, int[] chunkShape,
+                                     int[] innerShape, int[] order, byte[] fill, String[] paths,
+                                     long[] offset, long[] regionShape, Object out);
+
     /** ShardingIndexedCodec.decodePartial over one shard as index + pieces. */
     static native int shardDecodePieces(long ctx, int[] meta, long[] shape, int[] chunkShape,
                                         int[] innerShape, int[] order, byte[] fill, byte[] index,

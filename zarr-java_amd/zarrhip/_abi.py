@@ -10,6 +10,7 @@ ZH_EUNSUPPORTED = 3
 ZH_EHIP = 4
 ZH_ENOMEM = 5
 ZH_EARITH = 6
+ZH_EIO = 7
 
 ZH_ENDIAN_LITTLE = 0
 ZH_ENDIAN_BIG = 1

@@ -67,6 +67,8 @@ _SIGS = {
     "zh_sharding_decode_pieces": (C.c_int, [P, PMETA, C.POINTER(A.zh_shard_src), PI64, PI32, P,
                                             U32, P, CH, SZ]),
     "zh_host_staging": (C.c_int, [P, SZ, C.POINTER(P)]),
+    "zh_array_read_files": (C.c_int, [P, PMETA, C.POINTER(C.c_char_p), I64, PI64, PI64, P, U32,
+                                      CH, SZ]),
     "zh_array_encoded_bound": (I64, [PMETA]),
     "zh_array_write": (C.c_int, [P, PMETA, P, PI64, PI64, C.POINTER(A.zh_chunk_dst), I64, P, CH,
                                  SZ]),
@@ -344,6 +346,16 @@ class DeviceContext:
                                               i32arr(shape), P(out), int(flags), P(stream), err,
                                               1024)
         del keep
+        check(st, err)
+
+    def array_read_files(self, meta, paths, offset, shape, out, flags=0):
+        """zh_array_read_files: the chunks as files of a FilesystemStore (None or a path that
+        is not a regular file = missing key); the library does the store reads."""
+        arr = (C.c_char_p * max(1, len(paths)))(
+            *[None if p is None else os.fsencode(p) for p in paths])
+        err = C.create_string_buffer(1024)
+        st = self.L.zh_array_read_files(self.h, C.byref(meta), arr, len(paths), i64arr(offset),
+                                        i64arr(shape), P(out), int(flags), err, 1024)
         check(st, err)
 
     def host_staging(self, nbytes):

@@ -23,4 +23,7 @@ def raise_for(err):
         raise ValueError(msg) from None
     if st == A.ZH_EARITH:
         raise ArithmeticError(msg) from None
+    if st == A.ZH_EIO:  # a store file could not be read (StoreException.readFailed)
+        from .store import StoreException
+        raise StoreException(msg) from None
     raise RuntimeError(msg) from None
