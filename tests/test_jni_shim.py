@@ -274,6 +274,26 @@ def test_array_read_files_via_shim(dev, tmp_path, slab_mb, chain, mb):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("chain", ["c4", "start", "nested"])
+def test_codec_decode_partial_files_via_shim(dev, tmp_path, chain):
+    """HipShardingIndexedCodec.decodePartial over a FilesystemStore: arrayReadFiles on the shard
+    viewed as a one-chunk array (shape = the shard shape), one path, a shard-local part."""
+    meta, arr, shards = _case(chain, seed=19)
+    paths = _write_store(tmp_path, shards)
+    sm = A.zh_array_meta.from_buffer_copy(meta)
+    for d in range(meta.ndim):
+        sm.shape[d] = meta.chunk_shape[d]
+    jvm = FakeJVM()
+    for lo, part in [([0, 0, 0], [8, 16, 24]), ([1, 3, 5], [6, 9, 17])]:
+        rc, got = jvm.array_read_files(dev.h.value, sm, [paths[0]], lo, part)
+        assert rc == 0
+        want = np.frombuffer(O.array_read(sm, [shards[0]], lo, part),
+                             NP_DT[meta.dtype_size]).reshape(part)
+        np.testing.assert_array_equal(got, want)
+    jvm.check_rules()
+
+
+@pytest.mark.gpu
 def test_array_read_files_errors_via_shim(dev, tmp_path):
     """A corrupt shard index → ZarrException with the reference's CRC text; an unreadable file
     (when not root) → StoreException."""

@@ -4,6 +4,7 @@ import com.fasterxml.jackson.annotation.JsonCreator;
 import com.fasterxml.jackson.annotation.JsonProperty;
 import dev.zarr.zarrjava.ZarrException;
 import dev.zarr.zarrjava.core.ArrayMetadata.CoreArrayMetadata;
+import dev.zarr.zarrjava.store.FilesystemStore;
 import dev.zarr.zarrjava.store.StoreHandle;
 import dev.zarr.zarrjava.v3.codec.Codec;
 import dev.zarr.zarrjava.v3.codec.core.ShardingIndexedCodec;
@@ -58,6 +59,24 @@ public class HipShardingIndexedCodec extends ShardingIndexedCodec {
     @Override
     public Array decodePartial(StoreHandle chunkHandle, long[] offset, int[] shape)
             throws ZarrException {
+        if (chain != null && chain.innerHost == null
+                && chunkHandle.store instanceof FilesystemStore) {
+            // the library reads the shard file itself (zh_array_read_files over the shard viewed
+            // as a one-chunk array): the stored index, then the referenced ranges
+            java.nio.file.Path path = chunkHandle.toPath();
+            if (java.nio.file.Files.isRegularFile(path)) {
+                long[] shardShape = new long[shape.length], part = new long[shape.length];
+                for (int d = 0; d < shape.length; d++) {
+                    shardShape[d] = chain.chunkShape[d];
+                    part[d] = shape[d];
+                }
+                Array out = Array.factory(arrayMetadata.dataType.getMA2DataType(), shape);
+                int st = ZarrHip.arrayReadFiles(ZarrHip.codecCtx(), chain.meta, shardShape,
+                        chain.chunkShape, chain.innerShape, chain.order, chain.fill,
+                        new String[]{path.toString()}, offset, part, out.getStorage());
+                if (st == 0) return out;
+            }
+        }
         if (chain != null) {
             long[] hi = new long[offset.length];
             for (int d = 0; d < offset.length; d++) hi[d] = offset[d] + shape[d];
