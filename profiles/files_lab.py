@@ -49,9 +49,8 @@ res = {"reps": reps, "runs": []}
 cases = {"sub_shard": ([0, 0, 0, 512], [1, 1024, 1024, 512], paths[:1]),
          "two_shards": ([0, 0, 0, 0], [1, 1024, 1024, 2048], paths),
          "two_shards_pageable": ([0, 0, 0, 0], [1, 1024, 1024, 2048], None)}
-settings = [dict(), dict(ZH_PIPE_THREADS="8"), dict(ZH_PIPE_CHUNK_KB="32768"),
-            dict(ZH_PIPE_THREADS="8", ZH_PIPE_CHUNK_KB="32768"),
-            dict(ZH_PIPE_THREADS="10", ZH_PIPE_CHUNK_KB="32768")]
+settings = [dict(), dict(ZH_PIPE_THREADS="8"), dict(ZH_PIPE_THREADS="10"),
+            dict(ZH_PIPE_CHUNK_KB="32768"), dict(ZH_PIPE_THREADS="8", ZH_PIPE_CHUNK_KB="32768")]
 # the generic pipelined read from pageable host memory (the shards read into numpy first)
 host = [np.fromfile(p, np.uint8) for p in paths]
 try:
@@ -62,15 +61,18 @@ try:
             for i, st in enumerate(settings):
                 for k, v in st.items():
                     os.environ[k] = v
-                got = np.empty(shp, np.uint32)
-                t0 = time.perf_counter()
-                if ps is None:
-                    dev.array_read(meta, [(h.ctypes.data, h.size) for h in host], off, shp,
-                                   got.ctypes.data, 0)
-                else:
-                    dev.array_read_files(meta, ps, off, shp, got.ctypes.data, 0)
-                if rnd:
-                    ts[i].append(time.perf_counter() - t0)
+                for warm in (True, False):  # an untimed read after each switch: a new ring
+                    got = np.empty(shp, np.uint32)  # window size re-allocates the rings
+                    t0 = time.perf_counter()
+                    if ps is None:
+                        dev.array_read(meta, [(h.ctypes.data, h.size) for h in host], off, shp,
+                                       got.ctypes.data, 0)
+                    else:
+                        dev.array_read_files(meta, ps, off, shp, got.ctypes.data, 0)
+                    if rnd and not warm:
+                        ts[i].append(time.perf_counter() - t0)
+                    if warm:
+                        del got
                 for k in st:
                     os.environ.pop(k, None)
                 if rnd == reps:

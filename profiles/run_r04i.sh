@@ -3,7 +3,7 @@
 # two-shard store reads (profiles/files_lab.py).
 set -u
 R=${GRAFT_REPO_ROOT:-$(pwd)}
-OUT=$R/gpurun_out/r04j
+OUT=$R/gpurun_out/r04k
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 step() {  # name, timeout, cmd...
@@ -15,5 +15,5 @@ step() {  # name, timeout, cmd...
   if [ $rc -ne 0 ]; then tail -n 40 "$OUT/$name.out" "$OUT/$name.err" >&2; exit $rc; fi
 }
 cd "$R" || exit 1
-step fileslab 500 python3 -u profiles/files_lab.py "$OUT/files_lab.json" 6
+step fileslab 500 python3 -u profiles/files_lab.py "$OUT/files_lab.json" 5
 echo done >&2
