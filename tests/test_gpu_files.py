@@ -222,3 +222,30 @@ def test_array_read_goes_through_files(dev, tmp_path, monkeypatch, inner):
     monkeypatch.setenv("ZH_FILES", "0")
     np.testing.assert_array_equal(b.read(off, shp), part)
     assert b.last_read_timing.get("files") is None
+
+
+@pytest.mark.parametrize("sharded", [False, True])
+def test_read_chunk_goes_through_files(dev, tmp_path, monkeypatch, sharded):
+    """zarrhip.Array.readChunk (M/core/Array.java:167-182) over a FilesystemStore: the chunk's
+    file read by the library (the chunk viewed as a one-chunk array); a boundary chunk keeps
+    its padding, a missing chunk is fill — the same as the mirror's own store reads."""
+    shape = [40, 56, 24]
+    b = (z.ArrayMetadataBuilder().withShape(*shape).withDataType(z.DataType.UINT32)
+         .withChunkShape(16, 32, 24).withFillValue(3))
+    if sharded:
+        b = b.withCodecs(lambda c: c.withSharding(
+            [8, 8, 8], lambda c1: c1.withTranspose([2, 0, 1]).withBytes("BIG")))
+    else:
+        b = b.withCodecs(lambda c: c.withBytes("BIG"))
+    a = z.Array.create(z.FilesystemStore(tmp_path).resolve("r"), b.build())
+    data = np.random.default_rng(89).integers(0, 2 ** 32, shape, dtype=np.uint32)
+    data[32:, 32:, :] = 3  # chunk (2, 1, 0) all fill: deleted on write
+    a.write(None, data)
+    for c in [(0, 0, 0), (2, 0, 0), (1, 1, 0), (2, 1, 0)]:
+        got = a.readChunk(list(c))
+        monkeypatch.setenv("ZH_FILES", "0")
+        want = a.readChunk(list(c))
+        monkeypatch.delenv("ZH_FILES")
+        np.testing.assert_array_equal(got, want)
+        sl = tuple(slice(ci * cs, min((ci + 1) * cs, n)) for ci, cs, n in zip(c, [16, 32, 24], shape))
+        np.testing.assert_array_equal(got[tuple(slice(0, s.stop - s.start) for s in sl)], data[sl])

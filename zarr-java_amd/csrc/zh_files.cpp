@@ -169,8 +169,13 @@ int zh_array_read_files(zh_ctx* ctx, const zh_array_meta* meta, const char* cons
     if (!path) continue;  // missing key
     const int fd = open(path, O_RDONLY | O_CLOEXEC);
     if (fd < 0) {
-      if (errno == ENOENT || errno == ENOTDIR) continue;  // FilesystemStore.exists: false
-      set_err(err, errlen, "Failed to read from store at '%s': %s", path, strerror(errno));
+      const int oe = errno;
+      // FilesystemStore.exists is Files.isRegularFile (false when the file is absent, is no
+      // regular file, or cannot be stat'ed); an existing regular file that cannot be opened is
+      // a failed read (readAllBytes / newByteChannel → StoreException.readFailed)
+      struct stat sb;
+      if (oe == ENOENT || oe == ENOTDIR || stat(path, &sb) != 0 || !S_ISREG(sb.st_mode)) continue;
+      set_err(err, errlen, "Failed to read from store at '%s': %s", path, strerror(oe));
       return ZH_EIO;
     }
     ctx->files.back() = fd;
