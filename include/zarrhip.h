@@ -16,7 +16,7 @@
  *   zh_array_read_pieces        core.Array.read with sub-shard parts         M/core/Array.java:378-441 + the above
  *   zh_sharding_decode_pieces   ShardingIndexedCodec.decodePartial(StoreHandle, ...) ShardingIndexedCodec.java:245-255
  *   zh_shard_index_check        Crc32cCodec.decode of a shard index (host)    M/v3/codec/core/Crc32cCodec.java:24-48
- *   zh_array_read_files         core.Array.read over a FilesystemStore        M/core/Array.java:378-441 +
+ *   zh_array_read_files(_multi) core.Array.read over a FilesystemStore        M/core/Array.java:378-441 +
  *                               (exists / get(keys,start,end) per chunk)     M/store/FilesystemStore.java:43-102
  *   zh_array_write              core.Array.write + writeChunk + ShardingIndexedCodec.encode
  *                                                                            M/core/Array.java:83-156, ShardingIndexedCodec.java:105-168
@@ -379,6 +379,14 @@ int zh_host_staging(zh_ctx* ctx, size_t bytes, void** out);
 int zh_array_read_files(zh_ctx* ctx, const zh_array_meta* meta, const char* const* paths,
                         int64_t npaths, const int64_t* offset, const int64_t* shape, void* out,
                         uint32_t flags, char* err, size_t errlen);
+/* zh_array_read_files spread over several GPUs in one process (zh_array_read_multi_routed's
+ * slabs and routes; HipArray.read with ZH_DEVICES): every device reads the files of its slab
+ * and decodes it, a host-terminated read copying each slab straight into its slice of `out`
+ * (each device over its own PCIe link). */
+int zh_array_read_files_multi(zh_ctx* const* ctxs, int ndev, int root, const zh_array_meta* meta,
+                              const char* const* paths, int64_t npaths, const int64_t* offset,
+                              const int64_t* shape, void* out, uint32_t flags,
+                              int32_t* slab_route, char* err, size_t errlen);
 
 /* ShardingIndexedCodec.decode: whole shard → chunk_shape elements. */
 int zh_sharding_decode(zh_ctx* ctx, const zh_array_meta* meta, const void* shard, int64_t nbytes,

@@ -282,15 +282,17 @@ class FakeJVM:
         """A java.lang.String (None: a null reference)."""
         return None if text is None else self.L.fj_new_string(os.fsencode(text))
 
-    def array_read_files(self, ctx, meta, paths, offset, shape):
+    def array_read_files(self, ctxs, meta, paths, offset, shape):
         """arrayReadFiles: HipArray.read over a FilesystemStore — the chunk keys' paths
-        (StoreHandle.toPath()) in computeChunkCoords order, None = no path."""
+        (StoreHandle.toPath()) in computeChunkCoords order, None = no path; ctxs: one context
+        or a list (ZH_DEVICES)."""
         nel = int(np.prod(shape))
         out = self.output(meta.dtype_size, nel)
         jp = self.objs([self.string(p) for p in paths], b"java/lang/String")
-        args = self.meta_args(meta) + (jp, self.longs(offset), self.longs(shape), out)
-        rc = self._done(self._fn("arrayReadFiles")(P(self.env), None, C.c_int64(int(ctx or 0)),
-                                                   *map(P, args)))
+        cl = ctxs if isinstance(ctxs, (list, tuple)) else [ctxs or 0]
+        args = (self.longs([int(c) for c in cl]),) + self.meta_args(meta) + \
+            (jp, self.longs(offset), self.longs(shape), out)
+        rc = self._done(self._fn("arrayReadFiles")(P(self.env), None, *map(P, args)))
         dt = {1: np.uint8, 2: np.uint16, 4: np.uint32, 8: np.uint64}[meta.dtype_size]
         return rc, (self.array_of(out, dt).reshape(shape) if rc == 0 else None)
 

@@ -249,3 +249,46 @@ def test_read_chunk_goes_through_files(dev, tmp_path, monkeypatch, sharded):
         np.testing.assert_array_equal(got, want)
         sl = tuple(slice(ci * cs, min((ci + 1) * cs, n)) for ci, cs, n in zip(c, [16, 32, 24], shape))
         np.testing.assert_array_equal(got[tuple(slice(0, s.stop - s.start) for s in sl)], data[sl])
+
+
+@pytest.fixture(scope="module")
+def three_ctxs():
+    from zarrhip._lib import DeviceContext
+    cs = [DeviceContext(0) for _ in range(3)]
+    yield cs
+    for c in cs:
+        c.close()
+
+
+@pytest.mark.parametrize("ndev", [2, 3])
+@pytest.mark.parametrize("out_dev", [False, True])
+def test_files_multi_context(three_ctxs, tmp_path, mode, ndev, out_dev):
+    """zh_array_read_files_multi: one slab per context (here contexts on one device), each
+    reading the files of its slab; host-terminated slices, or the root's device buffer (the
+    other slabs decoded by plans that read their file bytes into host buffers first)."""
+    from zarrhip._lib import array_read_files_multi
+    shape = [1, 96, 64, 80]
+    meta = A.make_meta(shape, [1, 32, 32, 64], 4, endian=A.ZH_ENDIAN_BIG, sharded=True,
+                       inner_chunk_shape=[1, 8, 16, 16], transpose_order=[0, 3, 2, 1])
+    arr = rand_array(shape, 4, seed=97)
+    shards = encode_oracle(meta, arr)
+    shards[1] = None
+    paths = write_store(tmp_path, meta, shards)
+    cs = three_ctxs[:ndev]
+    for off, shp in [([0, 0, 0, 0], shape), ([0, 5, 3, 7], [1, 83, 50, 61])]:
+        want = oracle_region(meta, shards, off, shp)
+        rp = region_paths(meta, paths, off, shp)
+        nb = int(np.prod(shp)) * 4
+        if out_dev:
+            d = cs[0].malloc(nb)
+            try:
+                routes = array_read_files_multi(cs, meta, rp, off, shp, d, A.ZH_OUT_DEVICE)
+                got = np.frombuffer(cs[0].d2h(d, nb), np.uint32).reshape(shp)
+            finally:
+                cs[0].free(d)
+            assert routes[1] == 3  # ZH_ROUTE_SAME: decoded on its context, copied to the root
+        else:
+            got = np.empty(shp, np.uint32)
+            routes = array_read_files_multi(cs, meta, rp, off, shp, got.ctypes.data, 0)
+            assert all(r == 0 for r in routes)  # every slab straight into its host slice
+        np.testing.assert_array_equal(got, want)

@@ -446,8 +446,9 @@ def test_data_errors_become_zarr_exceptions(dev, tmp_path):
 
 @pytest.mark.gpu
 def test_multi_context_reads_via_shim(dev, tmp_path, slab_mb):
-    """arrayReadPieces and arrayReadMulti with several contexts (ZarrHip.ctxs() under
-    ZH_DEVICES: zh_array_read_pieces_multi / zh_array_read_multi, one slab per context); two
+    """arrayReadPieces, arrayReadMulti and arrayReadFiles with several contexts (ZarrHip.ctxs()
+    under ZH_DEVICES: zh_array_read_pieces_multi / zh_array_read_multi /
+    zh_array_read_files_multi, one slab per context); two
     extra contexts on the box's one GPU, slabs of 1 MiB per context."""
     from zarrhip._lib import DeviceContext
     slab_mb(1)
@@ -469,6 +470,10 @@ def test_multi_context_reads_via_shim(dev, tmp_path, slab_mb):
         np.testing.assert_array_equal(got, _oracle(meta, shards, off, shp))
         rc, got = jvm.array_read(None, meta, _region_chunks(meta, shards, off, shp), off, shp,
                                  ctxs=ctxs)
+        assert rc == 0
+        np.testing.assert_array_equal(got, _oracle(meta, shards, off, shp))
+        # arrayReadFiles over the same contexts (zh_array_read_files_multi)
+        rc, got = jvm.array_read_files(ctxs, meta, rp, off, shp)
         assert rc == 0
         np.testing.assert_array_equal(got, _oracle(meta, shards, off, shp))
         jvm.check_rules()

@@ -50,10 +50,6 @@ struct zh_ctx {
   uint8_t* upload_pin = nullptr;   // kUploadSlots × kUploadSlotBytes, created on first use
   std::vector<int> upload_free;
   bool upload_failed = false;
-  // zh_array_read_files: the open store files of the read in progress (under mu), which the
-  // sources' file addresses (zh::file_addr) name by slot
-  std::vector<int> files;
-  std::vector<std::string> file_paths;
 };
 
 namespace zh {
@@ -105,6 +101,7 @@ struct zh_plan {
   uint8_t* d_input = nullptr;   // staged host sources
   std::vector<std::pair<int64_t, const void*>> h2d;  // (offset in d_input, host ptr)
   std::vector<int64_t> h2d_len;
+  std::vector<std::vector<uint8_t>> h2d_keep;  // file bytes read for its own h2d copies
   bool external_h2d = false;    // the pipelined read does the h2d copies (plan_enqueue skips)
   uint8_t* d_out = nullptr;     // staging when the output is host memory
   zh::ScatterArgs args{};
@@ -187,11 +184,13 @@ int plan_mark_done_impl(zh_plan* p, hipStream_t s);
 int projection(int n, const int64_t* cc, const int64_t* ashape, const int32_t* chunk,
                const int64_t* soff, const int64_t* sshape, int32_t* co, int32_t* oo, int32_t* ps);
 
-// File addresses (zh_array_read_files): a source byte that lives in store file `slot` of the
-// context's read in progress at byte `off` is named by kFileTag | slot << kFileOffBits | off, a
-// value no host pointer takes (bit 62 set: not a canonical x86-64 user address).  The planner
-// treats it as an opaque host pointer (offsets add, adjacent ranges merge); only the pipelined
-// read's in lanes (and file_materialize) dereference it, with pread.  off < 2^40, slot < 2^22.
+// File addresses (zh_array_read_files): a source byte that lives at byte `off` of the store
+// file registered in `slot` of the process-wide file table (zh_files.cpp) is named by
+// kFileTag | slot << kFileOffBits | off, a value no host pointer takes (bit 62 set: not a
+// canonical x86-64 user address).  The planner treats it as an opaque host pointer (offsets
+// add, adjacent ranges merge); the pipelined read's in lanes read it with pread straight into
+// their ring slots, and plan_create reads the file bytes of a plan that stages its own copies
+// (not pipelined) into host buffers the plan keeps.  off < 2^40, slot < 2^22.
 constexpr uint64_t kFileTag = 1ull << 62;
 constexpr int kFileOffBits = 40;
 constexpr int64_t kFileMaxBytes = (int64_t)1 << kFileOffBits;
@@ -202,6 +201,6 @@ inline const uint8_t* file_addr(int64_t slot, int64_t off) {
 }
 // Reads n bytes named by the file address src into dst (pread, retried on EINTR / short
 // reads).  Returns "" or the failure's message (the path and the reason).
-std::string file_fetch(const zh_ctx* ctx, void* dst, const void* src, int64_t n);
+std::string file_fetch(void* dst, const void* src, int64_t n);
 
 }  // namespace zh

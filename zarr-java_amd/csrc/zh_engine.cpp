@@ -1059,6 +1059,18 @@ int plan_create(zh_ctx* ctx, const zh_array_meta* m, const SrcDesc* srcs, int64_
     }
     p->h2d.resize(w);
     p->h2d_len.resize(w);
+    // store-file sources (zh_array_read_files): a plan that does its own h2d copies reads
+    // their bytes now into buffers it keeps (the pipelined read's in lanes read them instead)
+    for (size_t k = 0; !external_h2d && k < p->h2d.size(); k++) {
+      if (!is_file_addr(p->h2d[k].second)) continue;
+      p->h2d_keep.emplace_back((size_t)std::max<int64_t>(1, p->h2d_len[k]));
+      const std::string m = file_fetch(p->h2d_keep.back().data(), p->h2d[k].second, p->h2d_len[k]);
+      if (!m.empty()) {
+        set_err(err, errlen, "%s", m.c_str());
+        return fail(ZH_EIO);
+      }
+      p->h2d[k].second = p->h2d_keep.back().data();
+    }
   }
   // the piece tables (device addresses of every held range)
   std::vector<DevPiece> dpieces;

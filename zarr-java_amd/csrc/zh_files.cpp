@@ -10,7 +10,9 @@
 // that is DMA'd to the device (zh_pipeline.cpp).  The bytes are copied once on the host, not
 // read into a store buffer first and copied into the ring after, and the reads of slab r + 1
 // overlap the decode and D2H of slab r.  Sources name the file bytes by file addresses
-// (zh_ctx.h): the planner lays them out like any host bytes and never dereferences them.
+// (zh_ctx.h) into a process-wide table of open files, so one read may span several contexts
+// (zh_array_read_files_multi); the planner lays file bytes out like any host bytes and reads
+// them itself only for a plan that stages its own copies (not pipelined).
 #include <errno.h>
 #include <fcntl.h>
 #include <sys/stat.h>
@@ -24,21 +26,73 @@
 
 #include "zh_ctx.h"
 
+namespace {
+
+// The process-wide table of the store files open for reads in flight: slot → (fd, path).
+// Slots are taken and given back per read; file addresses name a slot.
+struct FileSlots {
+  std::mutex mu;
+  std::vector<int> fd;
+  std::vector<std::string> path;
+  std::vector<int64_t> free;
+};
+
+FileSlots& slots() {
+  static FileSlots s;
+  return s;
+}
+
+int64_t slot_take(int fd, const char* path) {
+  FileSlots& s = slots();
+  std::lock_guard<std::mutex> lk(s.mu);
+  int64_t k;
+  if (!s.free.empty()) {
+    k = s.free.back();
+    s.free.pop_back();
+    s.fd[(size_t)k] = fd;
+    s.path[(size_t)k] = path;
+  } else {
+    if ((int64_t)s.fd.size() >= zh::kFileMaxSlots) return -1;
+    k = (int64_t)s.fd.size();
+    s.fd.push_back(fd);
+    s.path.push_back(path);
+  }
+  return k;
+}
+
+void slot_give(int64_t k) {
+  FileSlots& s = slots();
+  std::lock_guard<std::mutex> lk(s.mu);
+  if (s.fd[(size_t)k] >= 0) close(s.fd[(size_t)k]);
+  s.fd[(size_t)k] = -1;
+  s.path[(size_t)k].clear();
+  s.free.push_back(k);
+}
+
+}  // namespace
+
 namespace zh {
 
-std::string file_fetch(const zh_ctx* ctx, void* dst, const void* src, int64_t n) {
+std::string file_fetch(void* dst, const void* src, int64_t n) {
   const uint64_t a = (uint64_t)(uintptr_t)src & ~kFileTag;
-  const size_t slot = (size_t)(a >> kFileOffBits);
+  const size_t k = (size_t)(a >> kFileOffBits);
   int64_t off = (int64_t)(a & ((1ull << kFileOffBits) - 1));
-  if (slot >= ctx->files.size()) return "file source outside the read's file table";
-  const int fd = ctx->files[slot];
+  int fd = -1;
+  {
+    FileSlots& s = slots();
+    std::lock_guard<std::mutex> lk(s.mu);
+    if (k < s.fd.size()) fd = s.fd[k];
+  }
+  if (fd < 0) return "a file source that no read has open";
   uint8_t* d = (uint8_t*)dst;
   while (n > 0) {
     const ssize_t r = pread(fd, d, (size_t)std::min<int64_t>(n, (int64_t)1 << 30), (off_t)off);
     if (r < 0 && errno == EINTR) continue;
     if (r <= 0) {  // an error, or the file ended (it shrank after its size was taken)
-      std::string why = r < 0 ? strerror(errno) : "unexpected end of file";
-      return "Failed to read from store at '" + ctx->file_paths[slot] + "': " + why;
+      const std::string why = r < 0 ? strerror(errno) : "unexpected end of file";
+      FileSlots& s = slots();
+      std::lock_guard<std::mutex> lk(s.mu);
+      return "Failed to read from store at '" + s.path[k] + "': " + why;
     }
     d += r;
     off += r;
@@ -53,78 +107,22 @@ using namespace zh;
 
 namespace {
 
-// The open files of one zh_array_read_files call, registered on the context for the read
-// (ctx->mu held) and closed on every exit.
-struct FileTable {
-  zh_ctx* ctx;
-  explicit FileTable(zh_ctx* c) : ctx(c) {
-    ctx->files.clear();
-    ctx->file_paths.clear();
-  }
-  ~FileTable() {
-    for (int fd : ctx->files)
-      if (fd >= 0) close(fd);
-    ctx->files.clear();
-    ctx->file_paths.clear();
+// The files of one read, open for its duration: their slots go back (and the files are closed)
+// on every exit.
+struct FileSet {
+  std::vector<int64_t> taken;
+  ~FileSet() {
+    for (int64_t k : taken) slot_give(k);
   }
 };
 
-// Reads [off, off + n) of file slot into dst; ZH_EIO with the message on failure.
-int read_range(zh_ctx* ctx, int64_t slot, int64_t off, int64_t n, uint8_t* dst, char* err,
-               size_t errlen) {
-  const std::string m = file_fetch(ctx, dst, file_addr(slot, off), n);
-  if (m.empty()) return ZH_OK;
-  set_err(err, errlen, "%s", m.c_str());
-  return ZH_EIO;
-}
-
-// A read that does not run pipelined (small, or not splittable): the file bytes the sources
-// name are read into host buffers first and the sources pointed at them (one plan then
-// stages them as it stages any host bytes).
-int file_materialize(zh_ctx* ctx, std::vector<SrcDesc>& srcs,
-                     std::vector<std::vector<zh_shard_piece>>& pieces,
-                     std::vector<std::vector<uint8_t>>& keep, char* err, size_t errlen) {
-  auto fetch = [&](const void* a, int64_t n, const uint8_t** out) -> int {
-    keep.emplace_back((size_t)std::max<int64_t>(n, 1));
-    const std::string m = file_fetch(ctx, keep.back().data(), a, n);
-    if (!m.empty()) {
-      set_err(err, errlen, "%s", m.c_str());
-      return ZH_EIO;
-    }
-    *out = keep.back().data();
-    return ZH_OK;
-  };
-  for (size_t i = 0; i < srcs.size(); i++) {
-    SrcDesc& s = srcs[i];
-    if (s.data && is_file_addr(s.data)) {
-      int st = fetch(s.data, s.nbytes, &s.data);
-      if (st != ZH_OK) return st;
-    }
-    for (zh_shard_piece& q : pieces[i]) {
-      if (!q.data || !is_file_addr(q.data) || q.data_nbytes <= 0) continue;
-      const uint8_t* p = nullptr;
-      int st = fetch(q.data, q.data_nbytes, &p);
-      if (st != ZH_OK) return st;
-      q.data = p;
-    }
-  }
-  return ZH_OK;
-}
-
-}  // namespace
-
-extern "C" {
-
-int zh_array_read_files(zh_ctx* ctx, const zh_array_meta* meta, const char* const* paths,
-                        int64_t npaths, const int64_t* offset, const int64_t* shape, void* out,
-                        uint32_t flags, char* err, size_t errlen) {
-  if (!ctx || !meta || !offset || !shape || !out || (npaths > 0 && !paths)) return ZH_EINVAL;
-  if (flags & ZH_SRC_DEVICE) {
-    set_err(err, errlen, "zh_array_read_files reads host files: ZH_SRC_DEVICE is not allowed");
-    return ZH_EINVAL;
-  }
-  int st = zh_validate_meta(meta, err, errlen);
-  if (st != ZH_OK) return st;
+// Sources for a read of the files `paths` (computeChunkCoords order of [offset, offset+shape)):
+// per file the reference's store reads up to the ranges (open / exists, the stored index), the
+// ranges as file addresses.  index / pieces hold what the sources point into.
+int file_sources(const zh_array_meta* meta, const char* const* paths, int64_t npaths,
+                 const int64_t* offset, const int64_t* shape, FileSet& set,
+                 std::vector<SrcDesc>& srcs, std::vector<std::vector<uint8_t>>& index,
+                 std::vector<std::vector<zh_shard_piece>>& pieces, char* err, size_t errlen) {
   const int n = meta->ndim;
   for (int d = 0; d < n; d++) {  // M/core/Array.java:386-390 (the planner's check, early)
     if (offset[d] < 0 || offset[d] + shape[d] > meta->shape[d]) {
@@ -147,14 +145,11 @@ int zh_array_read_files(zh_ctx* ctx, const zh_array_meta* meta, const char* cons
             (long long)ncoords, (long long)npaths);
     return ZH_EINVAL;
   }
-  if (npaths > kFileMaxSlots) return ZH_EUNSUPPORTED;
-  std::lock_guard<std::mutex> lk(ctx->mu);
-  FileTable table(ctx);
   const zh_codec_chain& c = meta->chain;
   const int64_t isz = c.sharded ? zh_shard_index_size(meta) : 0;
-  std::vector<SrcDesc> srcs((size_t)npaths);
-  std::vector<std::vector<uint8_t>> index((size_t)npaths);
-  std::vector<std::vector<zh_shard_piece>> pieces((size_t)npaths);
+  srcs.assign((size_t)npaths, SrcDesc());
+  index.assign((size_t)npaths, {});
+  pieces.assign((size_t)npaths, {});
   int64_t cur[kMaxDims] = {0};
   for (int64_t i = 0; i < npaths; i++) {
     int64_t cc[kMaxDims];
@@ -164,8 +159,6 @@ int zh_array_read_files(zh_ctx* ctx, const zh_array_meta* meta, const char* cons
       cur[d] = 0;
     }
     const char* path = paths[i];
-    ctx->files.push_back(-1);
-    ctx->file_paths.push_back(path ? path : "");
     if (!path) continue;  // missing key
     const int fd = open(path, O_RDONLY | O_CLOEXEC);
     if (fd < 0) {
@@ -178,18 +171,27 @@ int zh_array_read_files(zh_ctx* ctx, const zh_array_meta* meta, const char* cons
       set_err(err, errlen, "Failed to read from store at '%s': %s", path, strerror(oe));
       return ZH_EIO;
     }
-    ctx->files.back() = fd;
     struct stat sb;
     if (fstat(fd, &sb) != 0) {
-      set_err(err, errlen, "Failed to read from store at '%s': %s", path, strerror(errno));
+      const int fe = errno;
+      close(fd);
+      set_err(err, errlen, "Failed to read from store at '%s': %s", path, strerror(fe));
       return ZH_EIO;
     }
-    if (!S_ISREG(sb.st_mode)) continue;  // Files.isRegularFile (FilesystemStore.java:44-46)
+    if (!S_ISREG(sb.st_mode)) {  // Files.isRegularFile (FilesystemStore.java:44-46)
+      close(fd);
+      continue;
+    }
     const int64_t size = (int64_t)sb.st_size;
-    if (size >= kFileMaxBytes) return ZH_EUNSUPPORTED;
+    const int64_t k = size < kFileMaxBytes ? slot_take(fd, path) : -1;
+    if (k < 0) {
+      close(fd);
+      return ZH_EUNSUPPORTED;
+    }
+    set.taken.push_back(k);
     SrcDesc& s = srcs[(size_t)i];
     if (!c.sharded) {  // get(keys): the whole object
-      s.data = file_addr(i, 0);
+      s.data = file_addr(k, 0);
       s.nbytes = size;
       continue;
     }
@@ -200,7 +202,11 @@ int zh_array_read_files(zh_ctx* ctx, const zh_array_meta* meta, const char* cons
     auto& ib = index[(size_t)i];
     ib.resize((size_t)std::max<int64_t>(ilen, 1));
     const int64_t ioff = c.index_location == ZH_INDEX_START ? 0 : size - ilen;
-    if ((st = read_range(ctx, i, ioff, ilen, ib.data(), err, errlen)) != ZH_OK) return st;
+    const std::string m = file_fetch(ib.data(), file_addr(k, ioff), ilen);
+    if (!m.empty()) {
+      set_err(err, errlen, "%s", m.c_str());
+      return ZH_EIO;
+    }
     s.index = ib.data();
     s.index_nbytes = ilen;
     s.shard_nbytes = size;
@@ -219,22 +225,60 @@ int zh_array_read_files(zh_ctx* ctx, const zh_array_meta* meta, const char* cons
     // beyond the file are left out and read as "Could not load byte data" on the device
     std::vector<std::pair<int64_t, int64_t>> rs;
     if (shard_ranges(meta, ib.data(), size, lo, hi, INT64_MAX, rs) != ZH_OK) continue;
-    for (auto& r : rs) pieces[(size_t)i].push_back({r.first, r.second, file_addr(i, r.first), r.second});
+    for (auto& r : rs) pieces[(size_t)i].push_back({r.first, r.second, file_addr(k, r.first), r.second});
     s.pieces = pieces[(size_t)i].data();
     s.npieces = (int64_t)pieces[(size_t)i].size();
   }
-  const uint32_t f = flags & ZH_OUT_DEVICE;
-  if (env_int("ZH_PIPE", 1) != 0) {
-    st = read_pipelined(ctx, meta, srcs.data(), npaths, offset, shape, out, f, nullptr, err,
-                        errlen);
-    if (st != ZH_EUNSUPPORTED) return st;
+  return ZH_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int zh_array_read_files(zh_ctx* ctx, const zh_array_meta* meta, const char* const* paths,
+                        int64_t npaths, const int64_t* offset, const int64_t* shape, void* out,
+                        uint32_t flags, char* err, size_t errlen) {
+  if (!ctx || !meta || !offset || !shape || !out || (npaths > 0 && !paths)) return ZH_EINVAL;
+  if (flags & ZH_SRC_DEVICE) {
+    set_err(err, errlen, "zh_array_read_files reads host files: ZH_SRC_DEVICE is not allowed");
+    return ZH_EINVAL;
   }
-  std::vector<std::vector<uint8_t>> keep;
-  if ((st = file_materialize(ctx, srcs, pieces, keep, err, errlen)) != ZH_OK) return st;
-  for (size_t i = 0; i < srcs.size(); i++)
-    if (srcs[i].pieces) srcs[i].pieces = pieces[i].data();
-  return read_one_plan(ctx, meta, srcs.data(), npaths, offset, shape, out, f, nullptr, err,
-                       errlen);
+  int st = zh_validate_meta(meta, err, errlen);
+  if (st != ZH_OK) return st;
+  FileSet set;
+  std::vector<SrcDesc> srcs;
+  std::vector<std::vector<uint8_t>> index;
+  std::vector<std::vector<zh_shard_piece>> pieces;
+  st = file_sources(meta, paths, npaths, offset, shape, set, srcs, index, pieces, err, errlen);
+  if (st != ZH_OK) return st;
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  // large reads pipelined (the in lanes pread the ranges into the ring); otherwise one plan,
+  // which reads the file bytes into host buffers first
+  return read_region(ctx, meta, srcs.data(), npaths, offset, shape, out, flags & ZH_OUT_DEVICE,
+                     nullptr, err, errlen);
+}
+
+int zh_array_read_files_multi(zh_ctx* const* ctxs, int ndev, int root, const zh_array_meta* meta,
+                              const char* const* paths, int64_t npaths, const int64_t* offset,
+                              const int64_t* shape, void* out, uint32_t flags,
+                              int32_t* slab_route, char* err, size_t errlen) {
+  if (!ctxs || ndev <= 0 || !meta || !offset || !shape || !out || (npaths > 0 && !paths))
+    return ZH_EINVAL;
+  if (flags & ZH_SRC_DEVICE) {
+    set_err(err, errlen, "zh_array_read_files reads host files: ZH_SRC_DEVICE is not allowed");
+    return ZH_EINVAL;
+  }
+  int st = zh_validate_meta(meta, err, errlen);
+  if (st != ZH_OK) return st;
+  FileSet set;
+  std::vector<SrcDesc> srcs;
+  std::vector<std::vector<uint8_t>> index;
+  std::vector<std::vector<zh_shard_piece>> pieces;
+  st = file_sources(meta, paths, npaths, offset, shape, set, srcs, index, pieces, err, errlen);
+  if (st != ZH_OK) return st;
+  return read_multi_impl(ctxs, ndev, root, meta, srcs.data(), npaths, offset, shape, out,
+                         flags & ZH_OUT_DEVICE, slab_route, err, errlen);
 }
 
 }  // extern "C"

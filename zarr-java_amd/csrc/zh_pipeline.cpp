@@ -437,7 +437,7 @@ int read_pipelined(zh_ctx* ctx, const zh_array_meta* meta, const SrcDesc* srcs, 
                 continue;
               }
               // a store file's range (zh_array_read_files): read straight into the slot
-              io = file_fetch(ctx, slot + part.first, part.second.first, part.second.second);
+              io = file_fetch(slot + part.first, part.second.first, part.second.second);
               if (!io.empty()) break;
             }
             if (!io.empty()) {

@@ -332,12 +332,13 @@ JNIEXPORT jint JNICALL Java_dev_zarr_zarrjava_hip_ZarrHip_arrayReadMulti(
 
 /* core.Array.read over a FilesystemStore (HipArray.read): paths[i] = StoreHandle.toPath() of the
  * i-th chunk of computeChunkCoords(shape, chunkShape, offset, regionShape), or null.  The library
- * reads the files itself (zh_array_read_files): no source array crosses the boundary, so per
- * slab only the result is held critical.  The paths are converted before any critical section
+ * reads the files itself (zh_array_read_files; with several contexts zh_array_read_files_multi,
+ * one slab per device): no source array crosses the boundary, so per slab only the result is
+ * held critical.  The paths are converted before any critical section
  * (GetStringUTFChars is a JNI call; its modified UTF-8 equals UTF-8 for every path without
  * NUL or supplementary characters). */
 JNIEXPORT jint JNICALL Java_dev_zarr_zarrjava_hip_ZarrHip_arrayReadFiles(
-    JNIEnv* env, jclass cls, jlong ctx, jintArray jm, jlongArray jshape, jintArray jchunk,
+    JNIEnv* env, jclass cls, jlongArray jctxs, jintArray jm, jlongArray jshape, jintArray jchunk,
     jintArray jinner, jintArray jorder, jbyteArray jfill, jobjectArray jpaths,
     jlongArray joffset, jlongArray jregion, jobject out) {
   (void)cls;
@@ -348,6 +349,12 @@ JNIEXPORT jint JNICALL Java_dev_zarr_zarrjava_hip_ZarrHip_arrayReadFiles(
   st = zh_validate_meta(&m, err, sizeof err);
   if (st == ZH_EUNSUPPORTED) return st;
   if (st != ZH_OK) return throw_status(env, st, err);
+  const jsize k = (*env)->GetArrayLength(env, jctxs);
+  if (k <= 0 || k > 64) return throw_status(env, ZH_EINVAL, "bad device context list");
+  jlong raw[64];
+  zh_ctx* ctxs[64];
+  (*env)->GetLongArrayRegion(env, jctxs, 0, k, raw);
+  for (jsize i = 0; i < k; i++) ctxs[i] = (zh_ctx*)(intptr_t)raw[i];
   int64_t o64[ZH_MAX_DIMS], r64[ZH_MAX_DIMS], u[ZH_MAX_DIMS], nel = 1;
   region_of(env, m.ndim, joffset, jregion, o64, r64);
   for (int d = 0; d < m.ndim; d++) nel *= r64[d];
@@ -370,9 +377,8 @@ JNIEXPORT jint JNICALL Java_dev_zarr_zarrjava_hip_ZarrHip_arrayReadFiles(
       snprintf(err, sizeof err, "out of host memory");
     }
   }
-  zh_ctx* c = (zh_ctx*)(intptr_t)ctx;
   units_of(&m, 0, u);
-  const SlabPlan SP = slab_plan(&m, r64, u, slab_cap_bytes());
+  const SlabPlan SP = slab_plan(&m, r64, u, slab_cap_bytes() * k);
   const int a = SP.axis;
   for (int64_t s = o64[a]; st == ZH_OK && s < o64[a] + r64[a];) {
     const int64_t e = slab_end(&SP, s, o64[a] + r64[a]);
@@ -392,9 +398,12 @@ JNIEXPORT jint JNICALL Java_dev_zarr_zarrjava_hip_ZarrHip_arrayReadFiles(
     ss[a] = e - s;
     void* pin = (*env)->GetPrimitiveArrayCritical(env, (jarray)out, NULL);
     if (pin) {
-      st = zh_array_read_files(c, &m, (const char* const*)(paths + first), cnt, so, ss,
-                               (uint8_t*)pin + (size_t)((s - o64[a]) * SP.row), 0, err,
-                               sizeof err);
+      uint8_t* dst = (uint8_t*)pin + (size_t)((s - o64[a]) * SP.row);
+      st = k == 1 ? zh_array_read_files(ctxs[0], &m, (const char* const*)(paths + first), cnt,
+                                        so, ss, dst, 0, err, sizeof err)
+                  : zh_array_read_files_multi(ctxs, (int)k, 0, &m,
+                                              (const char* const*)(paths + first), cnt, so, ss,
+                                              dst, 0, NULL, err, sizeof err);
       (*env)->ReleasePrimitiveArrayCritical(env, (jarray)out, pin, 0);
     } else {
       st = ZH_ENOMEM;

@@ -19,7 +19,8 @@ import java.util.stream.IntStream;
  * of the per-shard ForkJoin loop of core.Array.read (M/core/Array.java:378-441).
  * Unsupported chains use {@code super.read}.
  *
- * Over a FilesystemStore (one device, no host byte-to-byte stages) the chunk files' paths
+ * Over a FilesystemStore (no host byte-to-byte stages; ZH_DEVICES: one slab per device) the
+ * chunk files' paths
  * (StoreHandle.toPath(), M/store/StoreHandle.java:100-105) go to the library, which does the
  * store reads itself (arrayReadFiles).  Otherwise the store I/O keeps the reference's shape and
  * parallelism (the chunk loop runs as a parallel stream, M/core/Array.java:403-407): a whole
@@ -62,8 +63,7 @@ public class HipArray extends Array {
         final long[][] coords = IndexingUtils.computeChunkCoords(md.shape, cs, offset, shape);
         final boolean sharded = chain.meta[3] == 1;
         long[] ctxs = ZarrHip.ctxs();
-        if (storeHandle.store instanceof FilesystemStore && chain.innerHost == null
-                && ctxs.length == 1) {
+        if (storeHandle.store instanceof FilesystemStore && chain.innerHost == null) {
             // the library reads the chunk files itself (FilesystemStore.exists / get semantics,
             // M/store/FilesystemStore.java:43-102): pread into its page-locked ring, overlapped
             // with the device work; nothing of the chunks enters the Java heap
@@ -74,7 +74,7 @@ public class HipArray extends Array {
             }
             ucar.ma2.Array out = ucar.ma2.Array.factory(md.dataType().getMA2DataType(),
                     Utils.toIntArray(shape));
-            int st = ZarrHip.arrayReadFiles(ctxs[0], chain.meta, chain.shape, chain.chunkShape,
+            int st = ZarrHip.arrayReadFiles(ctxs, chain.meta, chain.shape, chain.chunkShape,
                     chain.innerShape, chain.order, chain.fill, paths, offset, shape,
                     out.getStorage());
             return st == 0 ? out : super.read(offset, shape, parallel);

@@ -71,7 +71,8 @@ public class HipShardingIndexedCodec extends ShardingIndexedCodec {
                     part[d] = shape[d];
                 }
                 Array out = Array.factory(arrayMetadata.dataType.getMA2DataType(), shape);
-                int st = ZarrHip.arrayReadFiles(ZarrHip.codecCtx(), chain.meta, shardShape,
+                int st = ZarrHip.arrayReadFiles(new long[]{ZarrHip.codecCtx()}, chain.meta,
+                        shardShape,
                         chain.chunkShape, chain.innerShape, chain.order, chain.fill,
                         new String[]{path.toString()}, offset, part, out.getStorage());
                 if (st == 0) return out;

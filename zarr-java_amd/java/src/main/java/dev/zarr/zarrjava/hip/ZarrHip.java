@@ -148,13 +148,14 @@ public final class ZarrHip {
                                       long[] regionShape, Object out);
 
     /**
-     * core.Array.read over a FilesystemStore (zh_array_read_files): paths[i] is
+     * core.Array.read over a FilesystemStore (zh_array_read_files; with several contexts
+     * zh_array_read_files_multi, one slab per device): paths[i] is
      * StoreHandle.toPath() of the i-th chunk of computeChunkCoords (null: no key); the library
      * reads the files (exists, the index and the referenced ranges, or whole chunks) with the
      * pipelined read, so no chunk bytes cross into the Java heap.  An unreadable file throws
      * dev.zarr.zarrjava.store.StoreException.
      */
-    static native int arrayReadFiles(long ctx, int[] meta, long[] shape, int[] chunkShape,
+    static native int arrayReadFiles(long[] ctxs, int[] meta, long[] shape, int[] chunkShape,
                                      int[] innerShape, int[] order, byte[] fill, String[] paths,
                                      long[] offset, long[] regionShape, Object out);
 

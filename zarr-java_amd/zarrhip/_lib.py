@@ -69,6 +69,9 @@ _SIGS = {
     "zh_host_staging": (C.c_int, [P, SZ, C.POINTER(P)]),
     "zh_array_read_files": (C.c_int, [P, PMETA, C.POINTER(C.c_char_p), I64, PI64, PI64, P, U32,
                                       CH, SZ]),
+    "zh_array_read_files_multi": (C.c_int, [C.POINTER(P), C.c_int, C.c_int, PMETA,
+                                            C.POINTER(C.c_char_p), I64, PI64, PI64, P, U32, PI32,
+                                            CH, SZ]),
     "zh_array_encoded_bound": (I64, [PMETA]),
     "zh_array_write": (C.c_int, [P, PMETA, P, PI64, PI64, C.POINTER(A.zh_chunk_dst), I64, P, CH,
                                  SZ]),
@@ -351,8 +354,7 @@ class DeviceContext:
     def array_read_files(self, meta, paths, offset, shape, out, flags=0):
         """zh_array_read_files: the chunks as files of a FilesystemStore (None or a path that
         is not a regular file = missing key); the library does the store reads."""
-        arr = (C.c_char_p * max(1, len(paths)))(
-            *[None if p is None else os.fsencode(p) for p in paths])
+        arr = path_array(paths)
         err = C.create_string_buffer(1024)
         st = self.L.zh_array_read_files(self.h, C.byref(meta), arr, len(paths), i64arr(offset),
                                         i64arr(shape), P(out), int(flags), err, 1024)
@@ -483,6 +485,25 @@ def array_read_pieces_multi(ctxs, meta, shards, offset, shape, out, flags, root=
                                       i64arr(offset), i64arr(shape), P(out), int(flags), routes,
                                       err, 1024)
     del keep
+    check(st, err)
+    return list(routes)
+
+
+def path_array(paths):
+    """char*[] of chunk file paths (None → NULL: a missing key)."""
+    return (C.c_char_p * max(1, len(paths)))(
+        *[None if p is None else os.fsencode(p) for p in paths])
+
+
+def array_read_files_multi(ctxs, meta, paths, offset, shape, out, flags=0, root=0):
+    """zh_array_read_files_multi: the files form of array_read_multi; returns the routes."""
+    L = lib()
+    hs = (P * len(ctxs))(*[c.h for c in ctxs])
+    routes = (C.c_int32 * len(ctxs))()
+    err = C.create_string_buffer(1024)
+    st = L.zh_array_read_files_multi(hs, len(ctxs), int(root), C.byref(meta), path_array(paths),
+                                     len(paths), i64arr(offset), i64arr(shape), P(out),
+                                     int(flags), routes, err, 1024)
     check(st, err)
     return list(routes)
 

@@ -375,15 +375,14 @@ class Array:
         return ("whole", b)
 
     def _file_paths(self, coords, devs):
-        """The chunk files of a read that zh_array_read_files can do (FilesystemStore, a chain
-        without host byte-to-byte stages, one device; ZH_FILES=0 keeps the store reads here),
-        in computeChunkCoords order, else None.  The reads themselves follow
+        """The chunk files of a read that zh_array_read_files(_multi) can do (FilesystemStore,
+        a chain without host byte-to-byte stages; ZH_FILES=0 keeps the store reads here), in
+        computeChunkCoords order, else None.  The reads themselves follow
         FilesystemStore.exists / get (M/store/FilesystemStore.java:43-102) in the library."""
         from .store import FilesystemStore
         st = self.storeHandle.store
         if (not isinstance(st, FilesystemStore) or self.chain.host_bb or
-                self.chain.inner_host_bb or len(devs) != 1 or
-                os.environ.get("ZH_FILES", "1") == "0"):
+                self.chain.inner_host_bb or os.environ.get("ZH_FILES", "1") == "0"):
             return None
         return [st._p(self._handle(c).keys) for c in coords]
 
@@ -406,7 +405,12 @@ class Array:
         if paths is not None:  # the library reads the store's files itself
             t1 = time.perf_counter()
             try:
-                devs[0].array_read_files(self.zmeta, paths, offset, shape, out.ctypes.data, 0)
+                if len(devs) > 1:  # one slab per device, each over its own PCIe link
+                    _lib.array_read_files_multi(devs, self.zmeta, paths, offset, shape,
+                                                out.ctypes.data, 0)
+                else:
+                    devs[0].array_read_files(self.zmeta, paths, offset, shape, out.ctypes.data,
+                                             0)
             except _lib.ZhError as e:
                 raise_for(e)
             self.last_read_timing = {"prep_s": t0 - t_enter, "stage_s": t1 - t0,
