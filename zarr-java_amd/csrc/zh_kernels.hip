@@ -2613,15 +2613,20 @@ __global__ __launch_bounds__(kBlock) void crc_index_kernel(const CrcJob* jobs, i
   }
   uint32_t* counter = partials + nspans + lo;
   const int64_t njs = (J.len + SPAN - 1) / SPAN;
+  // Publish the span's register write-through (an agent-scope store: sc1, past this XCD's L2)
+  // and wait for it before the ticket; the last workgroup reads every partial with agent-scope
+  // loads.  No release / acquire fence: __threadfence() here wrote back the whole XCD L2 in
+  // every workgroup (MI355X_MICROARCH.md "Workgroup dispatch ... inter-workgroup visibility").
   if (tid == 0) {
-    partials[span] = raw;
-    __threadfence();
-    last = atomicAdd(counter, 1u) == (uint32_t)(njs - 1);
+    __hip_atomic_store(partials + span, raw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    last = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+           (uint32_t)(njs - 1);
   }
   __syncthreads();
   if (!last) return;  // uniform
-  __threadfence();
-  if (tid == 0) *counter = 0;  // ready for the next launch (every other workgroup has counted)
+  // ready for the next launch (every other workgroup has counted)
+  if (tid == 0) __hip_atomic_store(counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   crc_index_finish(J, partials, sshift, status, red);
 }
 
