@@ -18,7 +18,7 @@
  *   zh_shard_index_check        Crc32cCodec.decode of a shard index (host)    M/v3/codec/core/Crc32cCodec.java:24-48
  *   zh_array_read_files(_multi) core.Array.read over a FilesystemStore        M/core/Array.java:378-441 +
  *                               (exists / get(keys,start,end) per chunk)     M/store/FilesystemStore.java:43-102
- *   zh_array_write              core.Array.write + writeChunk + ShardingIndexedCodec.encode
+ *   zh_array_write(_files)      core.Array.write + writeChunk + ShardingIndexedCodec.encode
  *                                                                            M/core/Array.java:83-156, ShardingIndexedCodec.java:105-168
  *   zh_shard_index_size         ShardingIndexedCodec.getShardIndexSize       ShardingIndexedCodec.java:176-181
  *   zh_crc32c                   utils.CRC32C.update/getValue                 M/utils/CRC32C.java:119-125,137-139
@@ -383,6 +383,20 @@ int zh_array_read_files(zh_ctx* ctx, const zh_array_meta* meta, const char* cons
  * slabs and routes; HipArray.read with ZH_DEVICES): every device reads the files of its slab
  * and decodes it, a host-terminated read copying each slab straight into its slice of `out`
  * (each device over its own PCIe link). */
+/* core.Array.write of a region of whole chunks (clipped only by the array boundary) into a
+ * FilesystemStore: the device encode of zh_array_write, then per chunk writeChunk's store call
+ * (M/core/Array.java:143-156) done here — all fill_value → the file deleted (FilesystemStore.delete,
+ * a missing file is fine), otherwise the parent directories created and the file created or
+ * truncated and written (FilesystemStore.set, M/store/FilesystemStore.java:105-127), the encoded
+ * bytes going D2H through the page-locked ring in windows that several lanes pwrite.  paths[i]:
+ * the i-th chunk of computeChunkCoords; src: the region in C order on the host, or on the device
+ * with ZH_SRC_DEVICE; nbytes (may be NULL): per chunk the bytes written (0: deleted).  A region
+ * that cuts chunks → ZH_EUNSUPPORTED (the binding's read-modify-write); a store failure →
+ * ZH_EIO ("Failed to write to store at '<path>': <reason>"). */
+int zh_array_write_files(zh_ctx* ctx, const zh_array_meta* meta, const void* src,
+                         const int64_t* offset, const int64_t* shape, const char* const* paths,
+                         int64_t npaths, uint32_t flags, int64_t* nbytes, char* err,
+                         size_t errlen);
 int zh_array_read_files_multi(zh_ctx* const* ctxs, int ndev, int root, const zh_array_meta* meta,
                               const char* const* paths, int64_t npaths, const int64_t* offset,
                               const int64_t* shape, void* out, uint32_t flags,

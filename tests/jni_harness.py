@@ -296,6 +296,19 @@ class FakeJVM:
         dt = {1: np.uint8, 2: np.uint16, 4: np.uint32, 8: np.uint64}[meta.dtype_size]
         return rc, (self.array_of(out, dt).reshape(shape) if rc == 0 else None)
 
+    def array_write_files(self, ctx, meta, arr, offset, paths):
+        """arrayWriteFiles: HipArray.write over a FilesystemStore — the region's primitive
+        array and the chunk keys' paths; returns the status (0, or 3: the caller writes)."""
+        kind = KIND[meta.dtype_size]
+        data = self.prim(kind, np.ascontiguousarray(arr).view(
+            {1: np.int8, 2: np.int16, 4: np.int32, 8: np.int64}[meta.dtype_size]).ravel())
+        self.sources.append(data)
+        jp = self.objs([self.string(p) for p in paths], b"java/lang/String")
+        args = self.meta_args(meta) + (self.longs(offset), self.longs(list(arr.shape)), data, jp)
+        fn = self._fn("arrayWriteFiles")
+        fn.restype = C.c_int32
+        return self._done(fn(P(self.env), None, C.c_int64(int(ctx or 0)), *map(P, args)))
+
     def array_write(self, ctx, meta, arr, offset):
         """arrayWrite: the region's primitive array → byte[][] (None: all fill, or the whole
         result None when the call declined)."""

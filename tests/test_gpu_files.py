@@ -292,3 +292,110 @@ def test_files_multi_context(three_ctxs, tmp_path, mode, ndev, out_dev):
             routes = array_read_files_multi(cs, meta, rp, off, shp, got.ctypes.data, 0)
             assert all(r == 0 for r in routes)  # every slab straight into its host slice
         np.testing.assert_array_equal(got, want)
+
+
+# ---- the write side: zh_array_write_files ------------------------------------------------
+WCHAINS = {
+    "sharded_t": dict(sharded=True, inner_chunk_shape=[4, 8, 8], transpose_order=[2, 0, 1],
+                      endian=A.ZH_ENDIAN_BIG),
+    "start_crc": dict(sharded=True, inner_chunk_shape=[4, 8, 8], inner_crc32c=True,
+                      index_location=A.ZH_INDEX_START),
+    "nested": dict(sharded=True, inner_chunk_shape=[8, 8, 8], nested_chunk_shape=[4, 4, 8]),
+    "bytes": dict(endian=A.ZH_ENDIAN_BIG),
+}
+
+
+@pytest.fixture(params=["one_window", "windows"])
+def wmode(request, monkeypatch):
+    """windows: 64 KiB ring windows over 3 lanes, so every chunk file is written in many
+    pwrite windows by several lanes."""
+    if request.param == "windows":
+        monkeypatch.setenv("ZH_PIPE_CHUNK_KB", "64")
+        monkeypatch.setenv("ZH_PIPE_THREADS", "3")
+    return request.param
+
+
+@pytest.mark.parametrize("chain", list(WCHAINS))
+def test_write_files_matches_oracle(dev, tmp_path, wmode, chain):
+    """Each chunk file holds exactly the oracle's encoded bytes (ShardingIndexedCodec.encode /
+    BytesCodec.encode); an all-fill chunk's existing file is deleted (writeChunk → delete); the
+    parent directories are created (FilesystemStore.set)."""
+    shape = [24, 32, 48]
+    meta = A.make_meta(shape, [8, 16, 24], 4, fill=(7).to_bytes(4, "little"), **WCHAINS[chain])
+    arr = rand_array(shape, 4, seed=101, fill_frac=0.1, fill=7)
+    arr[8:16, 0:16, 24:48] = 7  # chunk (1, 0, 1): all fill → deleted
+    want = encode_oracle(meta, arr)
+    coords = chunk_coords(meta, [0, 0, 0], shape)
+    paths = [str(tmp_path / "w" / "c" / "/".join(map(str, c))) for c in coords]
+    k = coords.index((1, 0, 1))
+    assert want[k] is None
+    os.makedirs(os.path.dirname(paths[k]), exist_ok=True)
+    with open(paths[k], "wb") as f:
+        f.write(b"stale")
+    sizes = dev.array_write_files(meta, arr.ctypes.data, [0, 0, 0], shape, paths)
+    for p, w, sz in zip(paths, want, sizes):
+        if w is None:
+            assert sz == 0 and not os.path.exists(p)
+        else:
+            assert sz == len(w)
+            assert open(p, "rb").read() == w
+    # and read back through the files
+    got = files_read(dev, meta, paths, [0, 0, 0], shape)
+    np.testing.assert_array_equal(got, arr)
+
+
+def test_write_files_device_source_and_errors(dev, tmp_path):
+    shape = [24, 32, 48]
+    meta = A.make_meta(shape, [8, 16, 24], 4, **WCHAINS["sharded_t"])
+    arr = rand_array(shape, 4, seed=103)
+    want = encode_oracle(meta, arr)
+    coords = chunk_coords(meta, [0, 0, 0], shape)
+    paths = [str(tmp_path / "d" / "_".join(map(str, c))) for c in coords]
+    d = dev.malloc(arr.nbytes)
+    try:
+        dev.h2d(d, arr.tobytes())
+        dev.array_write_files(meta, d, [0, 0, 0], shape, paths, A.ZH_SRC_DEVICE)
+    finally:
+        dev.free(d)
+    assert [open(p, "rb").read() for p in paths] == want
+    # a region that cuts chunks: the binding's read-modify-write
+    with pytest.raises(ZhError) as ed:
+        dev.array_write_files(meta, arr.ctypes.data, [0, 0, 1], [8, 16, 24], paths[:1])
+    assert ed.value.status == A.ZH_EUNSUPPORTED
+    # a parent path that is a file: the directories cannot be created → StoreException
+    blocker = tmp_path / "blocker"
+    blocker.write_bytes(b"x")
+    bad = [str(blocker / "c" / str(i)) for i in range(len(paths))]
+    with pytest.raises(ZhError) as ed:
+        dev.array_write_files(meta, arr.ctypes.data, [0, 0, 0], shape, bad)
+    assert ed.value.status == A.ZH_EIO
+    assert str(ed.value).startswith(f"Failed to write to store at '{bad[0]}': ")
+
+
+def test_array_write_goes_through_files(dev, tmp_path, monkeypatch):
+    """zarrhip.Array.write over a FilesystemStore: the library writes the chunk files; the
+    files equal the ones the mirror's own store writes make (ZH_FILES=0)."""
+    shape = [1, 64, 96, 80]
+    m = (z.ArrayMetadataBuilder().withShape(*shape).withDataType(z.DataType.UINT32)
+         .withChunkShape(1, 32, 32, 64).withFillValue(0)
+         .withCodecs(lambda c: c.withSharding(
+             [1, 8, 16, 16], lambda c1: c1.withTranspose([0, 3, 2, 1]).withBytes("BIG")))
+         .build())
+    data = np.random.default_rng(107).integers(0, 2 ** 32, shape, dtype=np.uint32)
+    data[0, 32:, 32:64, :] = 0  # two all-fill shards
+    a = z.Array.create(z.FilesystemStore(tmp_path / "lib").resolve("a"), m)
+    a.write(None, data)
+    monkeypatch.setenv("ZH_FILES", "0")
+    b = z.Array.create(z.FilesystemStore(tmp_path / "mirror").resolve("a"), m)
+    b.write(None, data)
+    monkeypatch.delenv("ZH_FILES")
+    for root, _, files in os.walk(tmp_path / "mirror" / "a"):
+        for fn in files:
+            rel = os.path.relpath(os.path.join(root, fn), tmp_path / "mirror")
+            assert open(tmp_path / "lib" / rel, "rb").read() == \
+                open(tmp_path / "mirror" / rel, "rb").read(), rel
+    n_lib = sum(len(f) for _, _, f in os.walk(tmp_path / "lib"))
+    n_mir = sum(len(f) for _, _, f in os.walk(tmp_path / "mirror"))
+    assert n_lib == n_mir
+    np.testing.assert_array_equal(z.Array.open(z.FilesystemStore(tmp_path / "lib").resolve("a"))
+                                  .read(), data)

@@ -420,6 +420,37 @@ def test_array_write_via_shim(dev, slab_mb, chain):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("chain", ["c3", "c4", "crc", "nested", "bytes"])
+@pytest.mark.parametrize("mb", [None, 1])
+def test_array_write_files_via_shim(dev, tmp_path, slab_mb, chain, mb):
+    """HipArray.write over a FilesystemStore: arrayWriteFiles copies the region out of the heap
+    in slab windows and the library writes each chunk file (all-fill chunks deleted); the files
+    hold the oracle's encoded bytes."""
+    slab_mb(mb)
+    shape = [64, 32, 48]
+    meta, arr, shards = _case(chain, shape=shape, seed=37)
+    coords = chunk_coords(meta, [0, 0, 0], shape)
+    paths = [str(tmp_path / "s" / "c" / "/".join(map(str, c))) for c in coords]
+    jvm = FakeJVM()
+    rc = jvm.array_write_files(dev.h.value, meta, arr, [0, 0, 0], paths)
+    assert rc == 0
+    for p, w in zip(paths, shards):
+        if w is None:
+            assert not os.path.exists(p)
+        else:
+            assert open(p, "rb").read() == w
+    s = jvm.check_rules()
+    nbytes = arr.nbytes
+    assert s.windows == (1 if mb is None else -(-nbytes // (1 << 20)))
+    # a region that cuts chunks: 3 (the caller's read-modify-write), nothing written
+    sub = np.ascontiguousarray(arr[1:9, :16, :24])
+    assert jvm.array_write_files(dev.h.value, meta, sub, [1, 0, 0],
+                                 [str(tmp_path / "x")]) == 3
+    assert not os.path.exists(tmp_path / "x")
+    jvm.check_rules()
+
+
+@pytest.mark.gpu
 def test_data_errors_become_zarr_exceptions(dev, tmp_path):
     """ZH_EDATA → dev.zarr.zarrjava.ZarrException with the oracle's (the reference's) text:
     a corrupt stored index on the device, a missing range ("Could not load byte data")."""

@@ -170,6 +170,9 @@ int read_pipelined(zh_ctx* ctx, const zh_array_meta* meta, const SrcDesc* srcs, 
                    const int64_t* offset, const int64_t* shape, void* out, uint32_t flags,
                    void* stream, char* err, size_t errlen);
 void pipeline_release(zh_ctx* ctx);  // zh_ctx_destroy: streams and rings
+// The pipelined read's copy lanes (ZH_PIPE_THREADS) and ring window (ZH_PIPE_CHUNK_KB), with
+// both rings holding two slots per lane and the copy streams created (caller holds ctx->mu).
+int pipe_out_ring(zh_ctx* ctx, int* lanes, int64_t* window);
 // One region over several contexts (zh_array_read_multi_routed / zh_array_read_pieces_multi).
 int read_multi_impl(zh_ctx* const* ctxs, int ndev, int root, const zh_array_meta* meta,
                     const SrcDesc* chunks, int64_t nchunks, const int64_t* offset,

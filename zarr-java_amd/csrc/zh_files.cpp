@@ -13,15 +13,21 @@
 // (zh_ctx.h) into a process-wide table of open files, so one read may span several contexts
 // (zh_array_read_files_multi); the planner lays file bytes out like any host bytes and reads
 // them itself only for a plan that stages its own copies (not pipelined).
+//
+// zh_array_write_files is the write side: the device encode, then writeChunk's store calls
+// (FilesystemStore.set / delete) here, the encoded bytes D2H'd through the page-locked ring in
+// windows that the copy lanes pwrite straight into the chunk files.
 #include <errno.h>
 #include <fcntl.h>
 #include <sys/stat.h>
 #include <unistd.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cstring>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "zh_ctx.h"
@@ -232,9 +238,202 @@ int file_sources(const zh_array_meta* meta, const char* const* paths, int64_t np
   return ZH_OK;
 }
 
+// Files.createDirectories(parent) (FilesystemStore.set, M/store/FilesystemStore.java:106-115):
+// every missing directory above `path`.  "" or the failure's message.
+std::string make_parents(const char* path) {
+  std::string p(path);
+  for (size_t k = 1; k < p.size(); k++) {
+    if (p[k] != '/') continue;
+    const std::string dir = p.substr(0, k);
+    if (mkdir(dir.c_str(), 0777) != 0 && errno != EEXIST) {
+      struct stat sb;
+      if (stat(dir.c_str(), &sb) == 0 && S_ISDIR(sb.st_mode)) continue;
+      return "Failed to create parent directories for path: " + dir + ": " + strerror(errno);
+    }
+  }
+  return "";
+}
+
+// pwrite of n bytes at off, retried on EINTR / short writes; "" or strerror.
+std::string write_all(int fd, const uint8_t* p, int64_t n, int64_t off) {
+  while (n > 0) {
+    const ssize_t w = pwrite(fd, p, (size_t)std::min<int64_t>(n, (int64_t)1 << 30), (off_t)off);
+    if (w < 0 && errno == EINTR) continue;
+    if (w <= 0) return w < 0 ? strerror(errno) : "no progress";
+    p += w;
+    off += w;
+    n -= w;
+  }
+  return "";
+}
+
 }  // namespace
 
 extern "C" {
+
+int zh_array_write_files(zh_ctx* ctx, const zh_array_meta* m, const void* src,
+                         const int64_t* offset, const int64_t* shape, const char* const* paths,
+                         int64_t npaths, uint32_t flags, int64_t* nbytes, char* err,
+                         size_t errlen) {
+  if (!ctx || !m || !src || !offset || !shape || (npaths > 0 && !paths)) return ZH_EINVAL;
+  int st = zh_validate_meta(m, err, errlen);
+  if (st != ZH_OK) return st;
+  for (int64_t i = 0; i < npaths; i++)
+    if (!paths[i]) {
+      set_err(err, errlen, "chunk path %lld is null", (long long)i);
+      return ZH_EINVAL;
+    }
+  (void)hipSetDevice(ctx->device);
+  int64_t rbytes = m->dtype_size;
+  for (int d = 0; d < m->ndim; d++) rbytes *= std::max<int64_t>(0, shape[d]);
+  const int64_t bound = zh_array_encoded_bound(m);
+  void* dsrc = nullptr;
+  void* ddst = nullptr;
+  size_t gsrc = 0, gdst = 0;
+  hipError_t e = hipSuccess;
+  if (!(flags & ZH_SRC_DEVICE)) {  // the region to the device (pageable or page-locked)
+    e = ctx_alloc(ctx, (size_t)std::max<int64_t>(1, rbytes), &dsrc, &gsrc);
+    if (e == hipSuccess) e = hipMemcpy(dsrc, src, (size_t)rbytes, hipMemcpyHostToDevice);
+  }
+  if (e == hipSuccess)
+    e = ctx_alloc(ctx, (size_t)std::max<int64_t>(1, bound * npaths), &ddst, &gdst);
+  std::vector<zh_chunk_dst> dsts((size_t)std::max<int64_t>(1, npaths));
+  if (e == hipSuccess) {
+    for (int64_t i = 0; i < npaths; i++) {
+      dsts[(size_t)i].data = (uint8_t*)ddst + i * bound;
+      dsts[(size_t)i].capacity = bound;
+      dsts[(size_t)i].nbytes = 0;
+    }
+    // ShardingIndexedCodec.encode of every chunk on the device (all-fill chunks: nbytes 0)
+    st = zh_array_write(ctx, m, dsrc ? dsrc : src, offset, shape, dsts.data(), npaths, nullptr,
+                        err, errlen);
+  }
+  std::vector<int> fds((size_t)std::max<int64_t>(1, npaths), -1);
+  if (e == hipSuccess && st == ZH_OK) {
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    // writeChunk per chunk (M/core/Array.java:143-156): all fill → delete the key
+    // (FilesystemStore.delete: a missing file is fine), else set: the parent directories, then
+    // the file created or truncated and written
+    for (int64_t i = 0; st == ZH_OK && i < npaths; i++) {
+      const int64_t nb = dsts[(size_t)i].nbytes;
+      if (nbytes) nbytes[i] = nb;
+      if (nb == 0) {
+        if (unlink(paths[i]) != 0 && errno != ENOENT) {
+          set_err(err, errlen, "Failed to delete from store at '%s': %s", paths[i],
+                  strerror(errno));
+          st = ZH_EIO;
+        }
+        continue;
+      }
+      std::string msg = make_parents(paths[i]);
+      int fd = -1;
+      if (msg.empty()) {
+        fd = open(paths[i], O_WRONLY | O_CREAT | O_TRUNC | O_CLOEXEC, 0666);
+        if (fd < 0) msg = strerror(errno);
+      }
+      if (!msg.empty()) {
+        set_err(err, errlen, "Failed to write to store at '%s': %s", paths[i], msg.c_str());
+        st = ZH_EIO;
+        break;
+      }
+      fds[(size_t)i] = fd;
+    }
+    // the encoded bytes out: windows of the ring size, the copy lanes each D2H'ing one window
+    // into a page-locked slot of their own while pwrite-ing the previous one
+    int lanes = 1;
+    int64_t win = 16 << 20;
+    if (st == ZH_OK && (st = pipe_out_ring(ctx, &lanes, &win)) != ZH_OK)
+      set_err(err, errlen, "page-locked staging rings: allocation failed");
+    struct Job {
+      int64_t chunk, off, len;
+    };
+    std::vector<Job> jobs;
+    for (int64_t i = 0; st == ZH_OK && i < npaths; i++)
+      for (int64_t o = 0; o < dsts[(size_t)i].nbytes; o += win)
+        jobs.push_back({i, o, std::min(win, dsts[(size_t)i].nbytes - o)});
+    lanes = (int)std::max<int64_t>(1, std::min<int64_t>(lanes, (int64_t)jobs.size()));
+    std::atomic<size_t> next{0};
+    std::atomic<int> fail{ZH_OK};
+    std::mutex fmu;
+    std::string fmsg;
+    auto lane_fail = [&](int code, const std::string& m2) {
+      std::lock_guard<std::mutex> g(fmu);
+      if (fail.load() == ZH_OK) {
+        fail = code;
+        fmsg = m2;
+      }
+    };
+    auto lane = [&](int L) {
+      (void)hipSetDevice(ctx->device);
+      hipEvent_t ev[2] = {nullptr, nullptr};
+      for (auto& x : ev)
+        if (hipEventCreateWithFlags(&x, hipEventDisableTiming) != hipSuccess) {
+          lane_fail(ZH_EHIP, "hipEventCreate failed");
+          return;
+        }
+      const Job* pend = nullptr;
+      int pslot = 0, flip = 0;
+      auto drain = [&]() {
+        if (!pend) return;
+        if (hipEventSynchronize(ev[pslot]) != hipSuccess) {
+          lane_fail(ZH_EHIP, "device-to-host copy of an encoded chunk failed");
+        } else {
+          const std::string w = write_all(fds[(size_t)pend->chunk],
+                                          (const uint8_t*)ctx->ring_out[(size_t)(2 * L + pslot)],
+                                          pend->len, pend->off);
+          if (!w.empty())
+            lane_fail(ZH_EIO, std::string("Failed to write to store at '") + paths[pend->chunk] +
+                                  "': " + w);
+        }
+        pend = nullptr;
+      };
+      for (;;) {
+        const size_t j = next.fetch_add(1);
+        if (j >= jobs.size() || fail.load() != ZH_OK) break;
+        const Job& J = jobs[j];
+        const int k = flip;
+        flip ^= 1;
+        void* slot = ctx->ring_out[(size_t)(2 * L + k)];
+        if (hipMemcpyAsync(slot, (const uint8_t*)dsts[(size_t)J.chunk].data + J.off,
+                           (size_t)J.len, hipMemcpyDeviceToHost, ctx->pipe_out) != hipSuccess ||
+            hipEventRecord(ev[k], ctx->pipe_out) != hipSuccess) {
+          lane_fail(ZH_EHIP, "device-to-host copy of an encoded chunk failed");
+          break;
+        }
+        drain();  // the previous window (the other slot) while this one copies
+        pend = &J;
+        pslot = k;
+      }
+      drain();
+      for (auto& x : ev)
+        if (x) (void)hipEventDestroy(x);
+    };
+    if (st == ZH_OK && !jobs.empty()) {
+      std::vector<std::thread> th;
+      for (int L = 0; L < lanes; L++) th.emplace_back(lane, L);
+      for (auto& t : th) t.join();
+      if (fail.load() != ZH_OK) {
+        st = fail.load();
+        set_err(err, errlen, "%s", fmsg.c_str());
+      }
+    }
+    for (size_t i = 0; i < fds.size(); i++) {
+      if (fds[i] < 0) continue;
+      if (close(fds[i]) != 0 && st == ZH_OK) {
+        set_err(err, errlen, "Failed to write to store at '%s': %s", paths[i], strerror(errno));
+        st = ZH_EIO;
+      }
+    }
+  }
+  if (dsrc) ctx_release(ctx, dsrc, gsrc);
+  if (ddst) ctx_release(ctx, ddst, gdst);
+  if (e != hipSuccess) {
+    (void)hipGetLastError();
+    set_err(err, errlen, "HIP error %s (%s)", hipGetErrorName(e), hipGetErrorString(e));
+    return e == hipErrorOutOfMemory ? ZH_ENOMEM : ZH_EHIP;
+  }
+  return st;
+}
 
 int zh_array_read_files(zh_ctx* ctx, const zh_array_meta* meta, const char* const* paths,
                         int64_t npaths, const int64_t* offset, const int64_t* shape, void* out,

@@ -186,6 +186,13 @@ int ensure_pipe(zh_ctx* ctx, int slots, size_t slot_bytes) {
 
 }  // namespace
 
+int pipe_out_ring(zh_ctx* ctx, int* lanes, int64_t* window) {
+  const PipeCfg c = pipe_cfg();
+  *lanes = c.threads;
+  *window = c.chunk;
+  return ensure_pipe(ctx, 2 * c.threads, (size_t)c.chunk);
+}
+
 void pipeline_release(zh_ctx* ctx) {
   if (!ctx) return;
   for (void* q : ctx->ring_in) (void)hipHostFree(q);

@@ -754,6 +754,82 @@ JNIEXPORT jint JNICALL Java_dev_zarr_zarrjava_hip_ZarrHip_shardDecodePieces(
   return 0;
 }
 
+/* The region of a Java array copied out of the heap in windows of one slab, each under its own
+ * critical section (released with JNI_ABORT): the write paths' one use of a critical section.
+ * Returns a malloc'd copy (the caller frees it) or NULL. */
+static uint8_t* copy_region_out(JNIEnv* env, jobject data, size_t rbytes) {
+  const size_t win = (size_t)slab_cap_bytes();
+  uint8_t* src = (uint8_t*)malloc(rbytes > 0 ? rbytes : 1);
+  for (size_t o = 0; src && o < rbytes; o += win) {
+    void* pin = (*env)->GetPrimitiveArrayCritical(env, (jarray)data, NULL);
+    if (!pin) {
+      free(src);
+      return NULL;
+    }
+    memcpy(src + o, (const uint8_t*)pin + o, rbytes - o < win ? rbytes - o : win);
+    (*env)->ReleasePrimitiveArrayCritical(env, (jarray)data, pin, JNI_ABORT);
+  }
+  return src;
+}
+
+/* core.Array.write of a region of whole chunks into a FilesystemStore (HipArray.write):
+ * paths[i] = StoreHandle.toPath() of the i-th chunk of computeChunkCoords; the library encodes
+ * on the device and writes (or, all fill_value, deletes) the chunk files itself
+ * (zh_array_write_files).  Returns 0, or 3 (ZH_EUNSUPPORTED: the caller keeps its own write) for
+ * a chain, region or Java array the device path does not take. */
+JNIEXPORT jint JNICALL Java_dev_zarr_zarrjava_hip_ZarrHip_arrayWriteFiles(
+    JNIEnv* env, jclass cls, jlong ctx, jintArray jm, jlongArray jshape, jintArray jchunk,
+    jintArray jinner, jintArray jorder, jbyteArray jfill, jlongArray joffset,
+    jlongArray jregion, jobject data, jobjectArray jpaths) {
+  (void)cls;
+  zh_array_meta m;
+  int st = build_meta(env, jm, jshape, jchunk, jinner, jorder, jfill, &m);
+  if (st != ZH_OK) return st;
+  char err[1024] = {0};
+  st = zh_validate_meta(&m, err, sizeof err);
+  if (st == ZH_EUNSUPPORTED) return st;
+  if (st != ZH_OK) return throw_status(env, st, err);
+  int64_t o64[ZH_MAX_DIMS], r64[ZH_MAX_DIMS], want = 1;
+  region_of(env, m.ndim, joffset, jregion, o64, r64);
+  for (int d = 0; d < m.ndim; d++) want *= r64[d];
+  /* a Java array of another length than the region: never read past its end */
+  if ((int64_t)(*env)->GetArrayLength(env, (jarray)data) != want) return ZH_EUNSUPPORTED;
+  const jsize n = (*env)->GetArrayLength(env, jpaths);
+  char** paths = (char**)calloc((size_t)(n > 0 ? n : 1), sizeof(char*));
+  if (!paths) return throw_status(env, ZH_ENOMEM, "out of host memory");
+  for (jsize i = 0; st == ZH_OK && i < n; i++) {
+    jstring js = (jstring)(*env)->GetObjectArrayElement(env, jpaths, i);
+    if (!js) continue;
+    const char* c = (*env)->GetStringUTFChars(env, js, NULL);
+    if (c) {
+      paths[i] = strdup(c);
+      (*env)->ReleaseStringUTFChars(env, js, c);
+    }
+    (*env)->DeleteLocalRef(env, js);
+    if (!c || !paths[i]) {
+      st = ZH_ENOMEM;
+      snprintf(err, sizeof err, "out of host memory");
+    }
+  }
+  uint8_t* src = NULL;
+  if (st == ZH_OK) {
+    src = copy_region_out(env, data, (size_t)want * (size_t)m.dtype_size);
+    if (!src) {
+      st = ZH_ENOMEM;
+      snprintf(err, sizeof err, "could not copy the region out of the Java heap");
+    }
+  }
+  if (st == ZH_OK)
+    st = zh_array_write_files((zh_ctx*)(intptr_t)ctx, &m, src, o64, r64,
+                              (const char* const*)paths, n, 0, NULL, err, sizeof err);
+  free(src);
+  for (jsize i = 0; i < n; i++) free(paths[i]);
+  free(paths);
+  if (st == ZH_EUNSUPPORTED) return st;
+  if (st != ZH_OK) return throw_status(env, st, err);
+  return 0;
+}
+
 /* core.Array.write replacement for a region of whole chunks (clipped only by the array
  * boundary): data = the primitive array of the region in C order (ucar storage copied to
  * 1-D); returns byte[][] in computeChunkCoords order, null = chunk all fill_value (the
@@ -818,19 +894,8 @@ JNIEXPORT jobjectArray JNICALL Java_dev_zarr_zarrjava_hip_ZarrHip_arrayWrite(
     }
     /* copy the region out of the heap in windows of one slab (the critical-section policy):
      * the call stages it to the device */
-    const size_t rbytes = (size_t)nel * (size_t)m.dtype_size;
-    const size_t win = (size_t)slab_cap_bytes();
-    uint8_t* src = (uint8_t*)malloc(rbytes > 0 ? rbytes : 1);
-    int pinned = src != NULL;
-    for (size_t o = 0; pinned && o < rbytes; o += win) {
-      void* pin = (*env)->GetPrimitiveArrayCritical(env, (jarray)data, NULL);
-      if (!pin) {
-        pinned = 0;
-        break;
-      }
-      memcpy(src + o, (const uint8_t*)pin + o, rbytes - o < win ? rbytes - o : win);
-      (*env)->ReleasePrimitiveArrayCritical(env, (jarray)data, pin, JNI_ABORT);
-    }
+    uint8_t* src = copy_region_out(env, data, (size_t)nel * (size_t)m.dtype_size);
+    const int pinned = src != NULL;
     st = pinned ? zh_array_write_host((zh_ctx*)(intptr_t)ctx, &m, src, o64, r64, outs, caps,
                                       sizes, n, err, sizeof err)
                 : ZH_ENOMEM;

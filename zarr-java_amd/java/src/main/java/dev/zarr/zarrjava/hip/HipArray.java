@@ -162,6 +162,21 @@ public class HipArray extends Array {
                 return;
             }
         }
+        if (storeHandle.store instanceof FilesystemStore && md.parsedFillValue() != null) {
+            // the library encodes and writes (or deletes) the chunk files itself
+            // (FilesystemStore.set / delete semantics, M/store/FilesystemStore.java:105-142)
+            long[][] coords = IndexingUtils.computeChunkCoords(md.shape, cs, offset, shape);
+            String[] paths = new String[coords.length];
+            for (int i = 0; i < coords.length; i++) {
+                paths[i] = storeHandle.resolve(md.chunkKeyEncoding().encodeChunkKey(coords[i]))
+                        .toPath().toString();
+            }
+            if (ZarrHip.arrayWriteFiles(ZarrHip.ctx(), chain.meta, chain.shape, chain.chunkShape,
+                    chain.innerShape, chain.order, chain.fill, offset, shape,
+                    array.copyTo1DJavaArray(), paths) == 0) {
+                return;
+            }
+        }
         byte[][] enc = ZarrHip.arrayWrite(ZarrHip.ctx(), chain.meta, chain.shape,
                 chain.chunkShape, chain.innerShape, chain.order, chain.fill, offset, shape,
                 array.copyTo1DJavaArray());

@@ -120,6 +120,16 @@ public final class ZarrHip {
                                       int[] innerShape, int[] order, byte[] fill, long[] offset,
                                       long[] regionShape, Object data);
 
+    /**
+     * core.Array.write of a region of whole chunks into a FilesystemStore
+     * (zh_array_write_files): paths[i] is StoreHandle.toPath() of the i-th chunk of
+     * computeChunkCoords; the library encodes on the device and writes (all fill_value:
+     * deletes) the chunk files.  Returns 0, or UNSUPPORTED when the caller must write itself.
+     */
+    static native int arrayWriteFiles(long ctx, int[] meta, long[] shape, int[] chunkShape,
+                                      int[] innerShape, int[] order, byte[] fill, long[] offset,
+                                      long[] regionShape, Object data, String[] paths);
+
     /** ShardingIndexedCodec.decodePartial over one shard's bytes. */
     static native int shardDecodePartial(long ctx, int[] meta, long[] shape, int[] chunkShape,
                                          int[] innerShape, int[] order, byte[] fill, byte[] shard,

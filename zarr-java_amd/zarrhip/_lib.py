@@ -69,6 +69,8 @@ _SIGS = {
     "zh_host_staging": (C.c_int, [P, SZ, C.POINTER(P)]),
     "zh_array_read_files": (C.c_int, [P, PMETA, C.POINTER(C.c_char_p), I64, PI64, PI64, P, U32,
                                       CH, SZ]),
+    "zh_array_write_files": (C.c_int, [P, PMETA, P, PI64, PI64, C.POINTER(C.c_char_p), I64, U32,
+                                       PI64, CH, SZ]),
     "zh_array_read_files_multi": (C.c_int, [C.POINTER(P), C.c_int, C.c_int, PMETA,
                                             C.POINTER(C.c_char_p), I64, PI64, PI64, P, U32, PI32,
                                             CH, SZ]),
@@ -359,6 +361,18 @@ class DeviceContext:
         st = self.L.zh_array_read_files(self.h, C.byref(meta), arr, len(paths), i64arr(offset),
                                         i64arr(shape), P(out), int(flags), err, 1024)
         check(st, err)
+
+    def array_write_files(self, meta, src, offset, shape, paths, flags=0):
+        """zh_array_write_files: encode the region (host pointer, or device with ZH_SRC_DEVICE)
+        and write / delete the chunk files; returns the bytes written per chunk (0: deleted)."""
+        n = len(paths)
+        sizes = (C.c_int64 * max(1, n))()
+        err = C.create_string_buffer(1024)
+        st = self.L.zh_array_write_files(self.h, C.byref(meta), P(src), i64arr(offset),
+                                         i64arr(shape), path_array(paths), n, int(flags), sizes,
+                                         err, 1024)
+        check(st, err)
+        return [int(sizes[i]) for i in range(n)]
 
     def host_staging(self, nbytes):
         """zh_host_staging: the context's page-locked staging (valid until the next call)."""

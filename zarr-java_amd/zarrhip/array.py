@@ -538,6 +538,15 @@ class Array:
             data, offset, shape = region, lo, ext
         coords = self._chunk_coords(offset, shape)
         dev = device()
+        keep_fill = getattr(self.metadata, "fill_value", 0) is None and \
+            not self.chain.chain["sharded"]
+        paths = None if keep_fill else self._file_paths(coords, [dev])
+        if paths is not None:  # the library writes (and deletes) the chunk files itself
+            try:
+                dev.array_write_files(self.zmeta, data.ctypes.data, offset, shape, paths)
+            except _lib.ZhError as e:
+                raise_for(e)
+            return
         L = _lib.lib()
         cap = L.zh_array_encoded_bound(C.byref(self.zmeta))
         src = dev.malloc(max(1, data.nbytes))
@@ -549,8 +558,6 @@ class Array:
                 sizes = dev.array_write(self.zmeta, src, offset, shape, [(b, cap) for b in bufs])
             except _lib.ZhError as e:
                 raise_for(e)
-            keep_fill = getattr(self.metadata, "fill_value", 0) is None and \
-                not self.chain.chain["sharded"]
             for c, b, sz in zip(coords, bufs, sizes):
                 h = self._handle(c)
                 if sz == 0 and not keep_fill:
