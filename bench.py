@@ -1124,6 +1124,47 @@ def store_inclusive(dev, A, shard_slab, offs, sizes, coords, scratch):
             r["verify_mismatches"] = int(dev.synth_verify(scratch, shape, off, shp, 4, SEED))
             res[name] = r
             del got
+        # the write side: Array.write of shard (0,0,0,0)'s region from host memory into a fresh
+        # FilesystemStore — the library encodes and writes the file (zh_array_write_files) vs
+        # the mirror's own store writes (ZH_FILES=0); the file must equal the stored shard
+        wshp = [1, 1024, 1024, 1024]
+        wdata = arr.read([0, 0, 0, 0], wshp)
+        src_path = os.path.join(base, "c4", "c", "0", "0", "0", "0")
+        wres = {"region_offset": [0, 0, 0, 0], "region_shape": wshp,
+                "bytes_in": int(wdata.nbytes)}
+        for mode in ("store_writes", "files"):
+            tgt = os.path.join(base, "w_" + mode)
+            wa = z.Array.create(z.FilesystemStore(tgt).resolve("c4"), m)
+            if mode == "store_writes":
+                os.environ["ZH_FILES"] = "0"
+            try:
+                t0 = time.perf_counter()
+                wa.write([0, 0, 0, 0], wdata)
+                tw = time.perf_counter() - t0
+            finally:
+                os.environ.pop("ZH_FILES", None)
+            out_path = os.path.join(tgt, "c4", "c", "0", "0", "0", "0")
+            same = os.path.getsize(out_path) == os.path.getsize(src_path)
+            if same:
+                a_ = np.memmap(out_path, np.uint8, "r")
+                b_ = np.memmap(src_path, np.uint8, "r")
+                for o in range(0, a_.size, 256 << 20):
+                    if not np.array_equal(a_[o:o + (256 << 20)], b_[o:o + (256 << 20)]):
+                        same = False
+                        break
+                del a_, b_
+            r = {"ms": round(tw * 1e3, 1), "value": round(wdata.nbytes / tw / GiB, 2),
+                 "unit": "GiB/s", "file_equals_stored_shard": bool(same)}
+            if mode == "files":
+                wres.update(r)
+            else:
+                wres["store_writes"] = r
+            shutil.rmtree(tgt, ignore_errors=True)
+        wres["call"] = ("zarrhip.Array.write → zh_array_write_files (H2D, device encode, D2H "
+                        "through the page-locked ring, pwrite by the copy lanes); store_writes: "
+                        "the mirror's encode + per-chunk store writes (ZH_FILES=0)")
+        res["write"] = wres
+        del wdata
         res["path"] = ("zarrhip.Array.read (Python mirror of core.Array.read) from a "
                        f"FilesystemStore on {d}: one zh_array_read_files call — the library "
                        "reads each shard's stored index and the ranges the region references "
