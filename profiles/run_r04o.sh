@@ -1,0 +1,18 @@
+#!/bin/bash
+# Round 4: zh_array_write_files stages (H2D, encode, D2H, file writes) on one c4 shard region.
+set -u
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+OUT=$R/gpurun_out/r04k
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+step() {  # name, timeout, cmd...
+  local name=$1 t=$2; shift 2
+  echo "== $name: $*" >&2
+  timeout -k 10 "$t" "$@" > "$OUT/$name.out" 2> "$OUT/$name.err"
+  local rc=$?
+  echo "== $name rc=$rc" >&2
+  if [ $rc -ne 0 ]; then tail -n 40 "$OUT/$name.out" "$OUT/$name.err" >&2; exit $rc; fi
+}
+cd "$R" || exit 1
+step wlab 500 python3 -u profiles/write_files_lab.py "$OUT/write_files_lab.json" 3
+echo done >&2
