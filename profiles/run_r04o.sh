@@ -2,7 +2,7 @@
 # Round 4: zh_array_write_files stages (H2D, encode, D2H, file writes) on one c4 shard region.
 set -u
 R=${GRAFT_REPO_ROOT:-$(pwd)}
-OUT=$R/gpurun_out/r04k
+OUT=$R/gpurun_out/r04o
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 step() {  # name, timeout, cmd...
