@@ -104,6 +104,25 @@ try:
     dev.host_register(host.ctypes.data, host.nbytes)
     one("host_pinned", host.ctypes.data, 0)
     dev.host_unregister(host.ctypes.data)
+    # two shards (8 GiB in, two files written by the lanes together)
+    meta2 = A.make_meta([1, 1024, 1024, 2048], [1, 1024, 1024, 1024], 4,
+                        endian=A.ZH_ENDIAN_BIG, sharded=True, inner_chunk_shape=[1, 32, 32, 32],
+                        transpose_order=[0, 3, 2, 1], index_crc32c=True)
+    host2 = np.empty((1024, 1024, 2048), np.uint32)
+    host2[:, :, :1024] = host.reshape(1024, 1024, 1024)
+    host2[:, :, 1024:] = host.reshape(1024, 1024, 1024)
+    ts = []
+    for r in range(reps):
+        ps = [os.path.join(d, f"two_{r}", "c", "0", "0", "0", str(z_)) for z_ in (0, 1)]
+        t0 = time.perf_counter()
+        sz = dev.array_write_files(meta2, host2.ctypes.data, [0] * 4, [1, 1024, 1024, 2048], ps)
+        ts.append(time.perf_counter() - t0)
+        shutil.rmtree(os.path.join(d, f"two_{r}"), ignore_errors=True)
+    rec = {"case": "two_shards_pageable", "ms_min": round(min(ts) * 1e3, 1),
+           "GiBps_in": round(host2.nbytes / min(ts) / 2 ** 30, 2), "file_bytes": sz}
+    print(json.dumps(rec), file=sys.stderr, flush=True)
+    res["runs"].append(rec)
+    del host2
 finally:
     shutil.rmtree(d, ignore_errors=True)
 print(json.dumps(res))

@@ -347,10 +347,16 @@ int zh_array_write_files(zh_ctx* ctx, const zh_array_meta* m, const void* src,
     struct Job {
       int64_t chunk, off, len;
     };
+    // windows taken round-robin over the chunks: buffered writes to one file serialize on its
+    // inode lock, so the lanes spread over as many files as the write has
     std::vector<Job> jobs;
+    int64_t most = 0;
     for (int64_t i = 0; st == ZH_OK && i < npaths; i++)
-      for (int64_t o = 0; o < dsts[(size_t)i].nbytes; o += win)
-        jobs.push_back({i, o, std::min(win, dsts[(size_t)i].nbytes - o)});
+      most = std::max(most, dsts[(size_t)i].nbytes);
+    for (int64_t o = 0; st == ZH_OK && o < most; o += win)
+      for (int64_t i = 0; i < npaths; i++)
+        if (o < dsts[(size_t)i].nbytes)
+          jobs.push_back({i, o, std::min(win, dsts[(size_t)i].nbytes - o)});
     lanes = (int)std::max<int64_t>(1, std::min<int64_t>(lanes, (int64_t)jobs.size()));
     std::atomic<size_t> next{0};
     std::atomic<int> fail{ZH_OK};
