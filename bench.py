@@ -1124,6 +1124,31 @@ def store_inclusive(dev, A, shard_slab, offs, sizes, coords, scratch):
             r["verify_mismatches"] = int(dev.synth_verify(scratch, shape, off, shp, 4, SEED))
             res[name] = r
             del got
+        # BASELINE configs[0]'s call shape from the store: Array.read of the unaligned 64^3 region
+        # {0,3,517,501} (27 inner chunks, most clipped) from the shard file, median of 200
+        sro, srs = [0, 3, 517, 501], [1, 64, 64, 64]
+        small = {"region_offset": sro, "region_shape": srs, "reps": 200}
+        for mode in ("store_reads", "files"):
+            if mode == "store_reads":
+                os.environ["ZH_FILES"] = "0"
+            try:
+                ts = []
+                for k in range(220):
+                    t0 = time.perf_counter()
+                    got = arr.read(sro, srs)
+                    if k >= 20:
+                        ts.append(time.perf_counter() - t0)
+            finally:
+                os.environ.pop("ZH_FILES", None)
+            ts.sort()
+            small[("us_median" if mode == "files" else "store_reads_us_median")] = \
+                round(ts[len(ts) // 2] * 1e6, 1)
+        dev.memcpy(scratch, got.ctypes.data, got.nbytes, 0, None, True)
+        small["verify_mismatches"] = int(dev.synth_verify(scratch, shape, sro, srs, 4, SEED))
+        small["call"] = ("zarrhip.Array.read → zh_array_read_files (index + 27 ranges pread, one "
+                         "plan) into a fresh numpy array; store_reads: the mirror's store reads "
+                         "+ zh_array_read_pieces")
+        res["small_read"] = small
         # the write side: Array.write of shard (0,0,0,0)'s region from host memory into a fresh
         # FilesystemStore — the library encodes and writes the file (zh_array_write_files) vs
         # the mirror's own store writes (ZH_FILES=0); the file must equal the stored shard
