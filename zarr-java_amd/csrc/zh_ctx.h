@@ -205,5 +205,15 @@ inline const uint8_t* file_addr(int64_t slot, int64_t off) {
 // Reads n bytes named by the file address src into dst (pread, retried on EINTR / short
 // reads).  Returns "" or the failure's message (the path and the reason).
 std::string file_fetch(void* dst, const void* src, int64_t n);
+// file_fetch of every (dst, src, n) in `reads`, spread in pieces of about 512 KiB over a small
+// pool of reader threads (ZH_FILE_THREADS, default 8) when there is more than one piece: the
+// small reads a plan stages itself (a 64^3 region's index + 27 inner chunks).  "" or the first
+// failure's message.
+struct FileRead {
+  void* dst;
+  const void* src;
+  int64_t n;
+};
+std::string file_fetch_all(const std::vector<FileRead>& reads);
 
 }  // namespace zh

@@ -1061,15 +1061,19 @@ int plan_create(zh_ctx* ctx, const zh_array_meta* m, const SrcDesc* srcs, int64_
     p->h2d_len.resize(w);
     // store-file sources (zh_array_read_files): a plan that does its own h2d copies reads
     // their bytes now into buffers it keeps (the pipelined read's in lanes read them instead)
+    std::vector<FileRead> freads;
     for (size_t k = 0; !external_h2d && k < p->h2d.size(); k++) {
       if (!is_file_addr(p->h2d[k].second)) continue;
       p->h2d_keep.emplace_back((size_t)std::max<int64_t>(1, p->h2d_len[k]));
-      const std::string m = file_fetch(p->h2d_keep.back().data(), p->h2d[k].second, p->h2d_len[k]);
+      freads.push_back({p->h2d_keep.back().data(), p->h2d[k].second, p->h2d_len[k]});
+      p->h2d[k].second = p->h2d_keep.back().data();
+    }
+    if (!freads.empty()) {  // the small reads of a plan, several reader threads
+      const std::string m = file_fetch_all(freads);
       if (!m.empty()) {
         set_err(err, errlen, "%s", m.c_str());
         return fail(ZH_EIO);
       }
-      p->h2d[k].second = p->h2d_keep.back().data();
     }
   }
   // the piece tables (device addresses of every held range)

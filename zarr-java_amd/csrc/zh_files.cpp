@@ -24,6 +24,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <condition_variable>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -107,6 +108,81 @@ std::string file_fetch(void* dst, const void* src, int64_t n) {
   return "";
 }
 
+namespace {
+
+// A small pool of reader threads for file_fetch_all, created on first use and kept: a read
+// below the pipeline threshold would otherwise pay a thread start per call.
+struct ReadPool {
+  std::mutex mu;
+  std::condition_variable cv, done_cv;
+  std::vector<std::thread> th;
+  std::vector<FileRead> q;
+  size_t next = 0, finished = 0, total = 0;
+  std::string fail;
+  bool stop = false;
+  ~ReadPool() {
+    {
+      std::lock_guard<std::mutex> lk(mu);
+      stop = true;
+    }
+    cv.notify_all();
+    for (auto& t : th) t.join();
+  }
+  void worker() {
+    std::unique_lock<std::mutex> lk(mu);
+    for (;;) {
+      cv.wait(lk, [&] { return stop || next < q.size(); });
+      if (stop) return;
+      const FileRead r = q[next++];
+      lk.unlock();
+      const std::string m = file_fetch(r.dst, r.src, r.n);
+      lk.lock();
+      if (!m.empty() && fail.empty()) fail = m;
+      if (++finished == total) done_cv.notify_all();
+    }
+  }
+};
+
+ReadPool& read_pool(int want) {
+  static ReadPool p;
+  std::lock_guard<std::mutex> lk(p.mu);
+  while ((int)p.th.size() < want) p.th.emplace_back([] { read_pool(0).worker(); });
+  return p;
+}
+
+std::mutex g_pool_call;  // one batch at a time
+
+}  // namespace
+
+std::string file_fetch_all(const std::vector<FileRead>& reads) {
+  constexpr int64_t kPiece = 512 << 10;
+  std::vector<FileRead> pieces;
+  for (const FileRead& r : reads)
+    for (int64_t o = 0; o < r.n; o += kPiece)
+      pieces.push_back({(uint8_t*)r.dst + o, (const uint8_t*)r.src + o, std::min(kPiece, r.n - o)});
+  const int threads = std::min(32, std::max(1, env_int("ZH_FILE_THREADS", 8)));
+  if (pieces.size() <= 1 || threads <= 1) {
+    for (const FileRead& r : pieces) {
+      const std::string m = file_fetch(r.dst, r.src, r.n);
+      if (!m.empty()) return m;
+    }
+    return "";
+  }
+  std::lock_guard<std::mutex> call(g_pool_call);
+  ReadPool& p = read_pool(threads);
+  std::unique_lock<std::mutex> lk(p.mu);
+  p.q = std::move(pieces);
+  p.next = p.finished = 0;
+  p.total = p.q.size();
+  p.fail.clear();
+  p.cv.notify_all();
+  p.done_cv.wait(lk, [&] { return p.finished == p.total; });
+  std::string m = p.fail;
+  p.q.clear();
+  p.next = p.total = p.finished = 0;
+  return m;
+}
+
 }  // namespace zh
 
 using namespace zh;
@@ -157,13 +233,9 @@ int file_sources(const zh_array_meta* meta, const char* const* paths, int64_t np
   index.assign((size_t)npaths, {});
   pieces.assign((size_t)npaths, {});
   int64_t cur[kMaxDims] = {0};
+  std::vector<FileRead> ireads;
+  std::vector<const uint8_t*> ireads_slot((size_t)npaths, nullptr);  // file address of byte 0
   for (int64_t i = 0; i < npaths; i++) {
-    int64_t cc[kMaxDims];
-    for (int d = 0; d < n; d++) cc[d] = cstart[d] + cur[d];
-    for (int d = n - 1; d >= 0; d--) {
-      if (++cur[d] < ccount[d]) break;
-      cur[d] = 0;
-    }
     const char* path = paths[i];
     if (!path) continue;  // missing key
     const int fd = open(path, O_RDONLY | O_CLOEXEC);
@@ -195,6 +267,7 @@ int file_sources(const zh_array_meta* meta, const char* const* paths, int64_t np
       return ZH_EUNSUPPORTED;
     }
     set.taken.push_back(k);
+    ireads_slot[(size_t)i] = file_addr(k, 0);
     SrcDesc& s = srcs[(size_t)i];
     if (!c.sharded) {  // get(keys): the whole object
       s.data = file_addr(k, 0);
@@ -208,15 +281,29 @@ int file_sources(const zh_array_meta* meta, const char* const* paths, int64_t np
     auto& ib = index[(size_t)i];
     ib.resize((size_t)std::max<int64_t>(ilen, 1));
     const int64_t ioff = c.index_location == ZH_INDEX_START ? 0 : size - ilen;
-    const std::string m = file_fetch(ib.data(), file_addr(k, ioff), ilen);
-    if (!m.empty()) {
-      set_err(err, errlen, "%s", m.c_str());
-      return ZH_EIO;
-    }
+    ireads.push_back({ib.data(), file_addr(k, ioff), ilen});
     s.index = ib.data();
     s.index_nbytes = ilen;
     s.shard_nbytes = size;
-    if (ilen < isz) continue;  // no ranges: the planner reports the short index
+  }
+  // every shard's index in one batch (several reader threads), then the ranges from each
+  const std::string m = file_fetch_all(ireads);
+  if (!m.empty()) {
+    set_err(err, errlen, "%s", m.c_str());
+    return ZH_EIO;
+  }
+  std::fill(cur, cur + kMaxDims, 0);
+  for (int64_t i = 0; c.sharded && i < npaths; i++) {
+    int64_t cc[kMaxDims];
+    for (int d = 0; d < n; d++) cc[d] = cstart[d] + cur[d];
+    for (int d = n - 1; d >= 0; d--) {
+      if (++cur[d] < ccount[d]) break;
+      cur[d] = 0;
+    }
+    SrcDesc& s = srcs[(size_t)i];
+    if (!s.index || s.index_nbytes < isz) continue;  // missing, or the planner reports it short
+    const int64_t k = (int64_t)((((uint64_t)(uintptr_t)ireads_slot[(size_t)i]) & ~kFileTag) >>
+                                kFileOffBits);
     int32_t co[kMaxDims], oo[kMaxDims], ps[kMaxDims];
     if (projection(n, cc, meta->shape, meta->chunk_shape, offset, shape, co, oo, ps) != ZH_OK) {
       set_err(err, errlen, "projection exceeds Integer.MAX_VALUE");
@@ -230,7 +317,7 @@ int file_sources(const zh_array_meta* meta, const char* const* paths, int64_t np
     // the referenced inner chunks' ranges, adjacent ones merged (one pread per run); entries
     // beyond the file are left out and read as "Could not load byte data" on the device
     std::vector<std::pair<int64_t, int64_t>> rs;
-    if (shard_ranges(meta, ib.data(), size, lo, hi, INT64_MAX, rs) != ZH_OK) continue;
+    if (shard_ranges(meta, s.index, s.shard_nbytes, lo, hi, INT64_MAX, rs) != ZH_OK) continue;
     for (auto& r : rs) pieces[(size_t)i].push_back({r.first, r.second, file_addr(k, r.first), r.second});
     s.pieces = pieces[(size_t)i].data();
     s.npieces = (int64_t)pieces[(size_t)i].size();
