@@ -6,6 +6,7 @@
 
 #include <array>
 #include <map>
+#include <memory>
 #include <mutex>
 #include <string>
 #include <utility>
@@ -101,7 +102,7 @@ struct zh_plan {
   uint8_t* d_input = nullptr;   // staged host sources
   std::vector<std::pair<int64_t, const void*>> h2d;  // (offset in d_input, host ptr)
   std::vector<int64_t> h2d_len;
-  std::vector<std::vector<uint8_t>> h2d_keep;  // file bytes read for its own h2d copies
+  std::vector<std::unique_ptr<uint8_t[]>> h2d_keep;  // file bytes read for its own h2d copies
   bool external_h2d = false;    // the pipelined read does the h2d copies (plan_enqueue skips)
   uint8_t* d_out = nullptr;     // staging when the output is host memory
   zh::ScatterArgs args{};
@@ -205,10 +206,10 @@ inline const uint8_t* file_addr(int64_t slot, int64_t off) {
 // Reads n bytes named by the file address src into dst (pread, retried on EINTR / short
 // reads).  Returns "" or the failure's message (the path and the reason).
 std::string file_fetch(void* dst, const void* src, int64_t n);
-// file_fetch of every (dst, src, n) in `reads`, spread in pieces of about 512 KiB over a small
-// pool of reader threads (ZH_FILE_THREADS, default 8) when there is more than one piece: the
-// small reads a plan stages itself (a 64^3 region's index + 27 inner chunks).  "" or the first
-// failure's message.
+// file_fetch of every (dst, src, n) in `reads`: the small reads a plan stages itself (a 64^3
+// region's index + 27 inner chunks) and the shards' indexes.  ZH_FILE_THREADS > 1 spreads them
+// in pieces of 512 KiB over a small pool of reader threads (default 1: on the GPU box 8 readers
+// made a 64^3 store read 2.2x slower, profiles/r04/q).  "" or the first failure's message.
 struct FileRead {
   void* dst;
   const void* src;

@@ -1064,11 +1064,12 @@ int plan_create(zh_ctx* ctx, const zh_array_meta* m, const SrcDesc* srcs, int64_
     std::vector<FileRead> freads;
     for (size_t k = 0; !external_h2d && k < p->h2d.size(); k++) {
       if (!is_file_addr(p->h2d[k].second)) continue;
-      p->h2d_keep.emplace_back((size_t)std::max<int64_t>(1, p->h2d_len[k]));
-      freads.push_back({p->h2d_keep.back().data(), p->h2d[k].second, p->h2d_len[k]});
-      p->h2d[k].second = p->h2d_keep.back().data();
+      // uninitialised: the read fills every byte
+      p->h2d_keep.emplace_back(new uint8_t[(size_t)std::max<int64_t>(1, p->h2d_len[k])]);
+      freads.push_back({p->h2d_keep.back().get(), p->h2d[k].second, p->h2d_len[k]});
+      p->h2d[k].second = p->h2d_keep.back().get();
     }
-    if (!freads.empty()) {  // the small reads of a plan, several reader threads
+    if (!freads.empty()) {  // the small reads of a plan
       const std::string m = file_fetch_all(freads);
       if (!m.empty()) {
         set_err(err, errlen, "%s", m.c_str());

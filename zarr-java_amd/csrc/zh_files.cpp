@@ -160,7 +160,7 @@ std::string file_fetch_all(const std::vector<FileRead>& reads) {
   for (const FileRead& r : reads)
     for (int64_t o = 0; o < r.n; o += kPiece)
       pieces.push_back({(uint8_t*)r.dst + o, (const uint8_t*)r.src + o, std::min(kPiece, r.n - o)});
-  const int threads = std::min(32, std::max(1, env_int("ZH_FILE_THREADS", 8)));
+  const int threads = std::min(32, std::max(1, env_int("ZH_FILE_THREADS", 1)));
   if (pieces.size() <= 1 || threads <= 1) {
     for (const FileRead& r : pieces) {
       const std::string m = file_fetch(r.dst, r.src, r.n);
