@@ -21,6 +21,7 @@ from zarrhip.array import device  # noqa: E402
 
 out_path = sys.argv[1]
 reps = int(sys.argv[2]) if len(sys.argv) > 2 else 200
+trace = len(sys.argv) > 3 and sys.argv[3] == "trace"  # one setting, one round (rocprofv3)
 dev = device()
 shape = [1, 1024, 1024, 1024]
 meta = A.make_meta(shape, [1, 1024, 1024, 1024], 4, endian=A.ZH_ENDIAN_BIG, sharded=True,
@@ -50,9 +51,11 @@ arr = z.Array.open(z.FilesystemStore(base).resolve("a"))
 off, shp = [0, 3, 517, 501], [1, 64, 64, 64]
 settings = [("files_1", {"ZH_FILE_THREADS": "1"}), ("files_4", {"ZH_FILE_THREADS": "4"}),
             ("files_8", {"ZH_FILE_THREADS": "8"}), ("store_reads", {"ZH_FILES": "0"})]
+if trace:
+    settings = settings[:1]
 res = {"reps": reps, "region_offset": off, "region_shape": shp, "rounds": []}
 try:
-    for rnd in range(3):
+    for rnd in range(1 if trace else 3):
         row = {}
         for name, env in settings:
             os.environ.update(env)
