@@ -397,6 +397,14 @@ int zh_array_write_files(zh_ctx* ctx, const zh_array_meta* meta, const void* src
                          const int64_t* offset, const int64_t* shape, const char* const* paths,
                          int64_t npaths, uint32_t flags, int64_t* nbytes, char* err,
                          size_t errlen);
+/* Diagnostic (no device needed): the store reads zh_array_read_files would make for these
+ * paths, as (chunk index, file offset, bytes) triples in order — a whole object, or a shard's
+ * index read followed by its merged range reads; missing keys make none.  Writes up to `cap`
+ * triples to `reads` (may be NULL) and returns their number, or -zh_status with err set (the
+ * same checks and messages as the read).  Tests use it to check the read plan on the host. */
+int64_t zh_debug_file_reads(const zh_array_meta* meta, const char* const* paths, int64_t npaths,
+                            const int64_t* offset, const int64_t* shape, int64_t* reads,
+                            int64_t cap, char* err, size_t errlen);
 int zh_array_read_files_multi(zh_ctx* const* ctxs, int ndev, int root, const zh_array_meta* meta,
                               const char* const* paths, int64_t npaths, const int64_t* offset,
                               const int64_t* shape, void* out, uint32_t flags,

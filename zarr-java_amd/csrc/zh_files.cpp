@@ -528,6 +528,40 @@ int zh_array_write_files(zh_ctx* ctx, const zh_array_meta* m, const void* src,
   return st;
 }
 
+int64_t zh_debug_file_reads(const zh_array_meta* meta, const char* const* paths, int64_t npaths,
+                            const int64_t* offset, const int64_t* shape, int64_t* reads,
+                            int64_t cap, char* err, size_t errlen) {
+  if (!meta || !offset || !shape || (npaths > 0 && !paths)) return -ZH_EINVAL;
+  int st = zh_validate_meta(meta, err, errlen);
+  if (st != ZH_OK) return -st;
+  FileSet set;
+  std::vector<SrcDesc> srcs;
+  std::vector<std::vector<uint8_t>> index;
+  std::vector<std::vector<zh_shard_piece>> pieces;
+  st = file_sources(meta, paths, npaths, offset, shape, set, srcs, index, pieces, err, errlen);
+  if (st != ZH_OK) return -st;
+  int64_t k = 0;
+  auto put = [&](int64_t i, int64_t off, int64_t n) {
+    if (reads && k < cap) {
+      reads[3 * k] = i;
+      reads[3 * k + 1] = off;
+      reads[3 * k + 2] = n;
+    }
+    k++;
+  };
+  const int64_t isz = meta->chain.sharded ? zh_shard_index_size(meta) : 0;
+  for (int64_t i = 0; i < npaths; i++) {
+    const SrcDesc& s = srcs[(size_t)i];
+    if (s.data) put(i, 0, s.nbytes);  // a whole object
+    if (s.index)  // the index read: a prefix, or the last index_nbytes bytes
+      put(i, meta->chain.index_location == ZH_INDEX_START ? 0 : s.shard_nbytes - s.index_nbytes,
+          s.index_nbytes);
+    (void)isz;
+    for (int64_t q = 0; q < s.npieces; q++) put(i, s.pieces[q].offset, s.pieces[q].nbytes);
+  }
+  return k;
+}
+
 int zh_array_read_files(zh_ctx* ctx, const zh_array_meta* meta, const char* const* paths,
                         int64_t npaths, const int64_t* offset, const int64_t* shape, void* out,
                         uint32_t flags, char* err, size_t errlen) {

@@ -69,6 +69,8 @@ _SIGS = {
     "zh_host_staging": (C.c_int, [P, SZ, C.POINTER(P)]),
     "zh_array_read_files": (C.c_int, [P, PMETA, C.POINTER(C.c_char_p), I64, PI64, PI64, P, U32,
                                       CH, SZ]),
+    "zh_debug_file_reads": (I64, [PMETA, C.POINTER(C.c_char_p), I64, PI64, PI64, PI64, I64, CH,
+                                  SZ]),
     "zh_array_write_files": (C.c_int, [P, PMETA, P, PI64, PI64, C.POINTER(C.c_char_p), I64, U32,
                                        PI64, CH, SZ]),
     "zh_array_read_files_multi": (C.c_int, [C.POINTER(P), C.c_int, C.c_int, PMETA,
@@ -507,6 +509,22 @@ def path_array(paths):
     """char*[] of chunk file paths (None → NULL: a missing key)."""
     return (C.c_char_p * max(1, len(paths)))(
         *[None if p is None else os.fsencode(p) for p in paths])
+
+
+def file_reads(meta, paths, offset, shape):
+    """zh_debug_file_reads: [(chunk index, file offset, bytes)] the files read would make
+    (raises ZhError with the read's status and message)."""
+    L = lib()
+    arr = path_array(paths)
+    err = C.create_string_buffer(1024)
+    n = L.zh_debug_file_reads(C.byref(meta), arr, len(paths), i64arr(offset), i64arr(shape),
+                              None, 0, err, 1024)
+    if n < 0:
+        check(-n, err)
+    buf = (C.c_int64 * max(1, 3 * n))()
+    L.zh_debug_file_reads(C.byref(meta), arr, len(paths), i64arr(offset), i64arr(shape), buf, n,
+                          err, 1024)
+    return [tuple(buf[3 * k:3 * k + 3]) for k in range(n)]
 
 
 def array_read_files_multi(ctxs, meta, paths, offset, shape, out, flags=0, root=0):
