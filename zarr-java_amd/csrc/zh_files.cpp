@@ -234,7 +234,7 @@ int file_sources(const zh_array_meta* meta, const char* const* paths, int64_t np
   pieces.assign((size_t)npaths, {});
   int64_t cur[kMaxDims] = {0};
   std::vector<FileRead> ireads;
-  std::vector<const uint8_t*> ireads_slot((size_t)npaths, nullptr);  // file address of byte 0
+  std::vector<int64_t> slot_of((size_t)npaths, -1);  // the file's slot in the table
   for (int64_t i = 0; i < npaths; i++) {
     const char* path = paths[i];
     if (!path) continue;  // missing key
@@ -267,7 +267,7 @@ int file_sources(const zh_array_meta* meta, const char* const* paths, int64_t np
       return ZH_EUNSUPPORTED;
     }
     set.taken.push_back(k);
-    ireads_slot[(size_t)i] = file_addr(k, 0);
+    slot_of[(size_t)i] = k;
     SrcDesc& s = srcs[(size_t)i];
     if (!c.sharded) {  // get(keys): the whole object
       s.data = file_addr(k, 0);
@@ -286,7 +286,7 @@ int file_sources(const zh_array_meta* meta, const char* const* paths, int64_t np
     s.index_nbytes = ilen;
     s.shard_nbytes = size;
   }
-  // every shard's index in one batch (several reader threads), then the ranges from each
+  // every shard's index in one batch (file_fetch_all), then the ranges from each
   const std::string m = file_fetch_all(ireads);
   if (!m.empty()) {
     set_err(err, errlen, "%s", m.c_str());
@@ -302,8 +302,7 @@ int file_sources(const zh_array_meta* meta, const char* const* paths, int64_t np
     }
     SrcDesc& s = srcs[(size_t)i];
     if (!s.index || s.index_nbytes < isz) continue;  // missing, or the planner reports it short
-    const int64_t k = (int64_t)((((uint64_t)(uintptr_t)ireads_slot[(size_t)i]) & ~kFileTag) >>
-                                kFileOffBits);
+    const int64_t k = slot_of[(size_t)i];
     int32_t co[kMaxDims], oo[kMaxDims], ps[kMaxDims];
     if (projection(n, cc, meta->shape, meta->chunk_shape, offset, shape, co, oo, ps) != ZH_OK) {
       set_err(err, errlen, "projection exceeds Integer.MAX_VALUE");
