@@ -75,3 +75,56 @@ def test_gather_blocks(dev):
     dev.free(src)
     dev.free(dst)
     np.testing.assert_array_equal(got, src_h.reshape(nb, bb)[perm])
+
+
+@pytest.mark.parametrize("ncontexts", [1, 4])
+@pytest.mark.parametrize("pipelined", [False, True])
+def test_threads_read_files_concurrently(dev, tmp_path, monkeypatch, ncontexts, pipelined):
+    """HipShardingIndexedCodec.decodePartial over a FilesystemStore from eight threads
+    (zh_array_read_files on the shard viewed as a one-chunk array): the process-wide file table
+    and the contexts' pipelines under concurrent calls give the oracle's bytes."""
+    if pipelined:
+        monkeypatch.setenv("ZH_PIPE_MIN_KB", "1")
+        monkeypatch.setenv("ZH_PIPE_SLAB_KB", "16")
+        monkeypatch.setenv("ZH_PIPE_CHUNK_KB", "64")
+        monkeypatch.setenv("ZH_PIPE_THREADS", "2")
+    shape = [1, 64, 64, 64]
+    meta = A.make_meta(shape, [1, 32, 32, 64], 4, endian=A.ZH_ENDIAN_BIG, sharded=True,
+                       inner_chunk_shape=[1, 8, 8, 16], transpose_order=[0, 3, 2, 1])
+    arr = rand_array(shape, 4, seed=37)
+    shards = encode_oracle(meta, arr)
+    paths = []
+    for i, s in enumerate(shards):
+        p = str(tmp_path / f"s{i}")
+        with open(p, "wb") as f:
+            f.write(s)
+        paths.append(p)
+    smeta = A.zh_array_meta.from_buffer_copy(meta)
+    for d in range(4):
+        smeta.shape[d] = meta.chunk_shape[d]
+    ctxs = [dev] + [DeviceContext(0) for _ in range(ncontexts - 1)]
+    jobs = [(i, [0, 3 * (k % 5), 2 * (k % 7), k % 9], [1, 20, 20, 40])
+            for k, i in enumerate(list(range(len(shards))) * 4)]
+    results, errors = {}, []
+
+    def work(t):
+        try:
+            ctx = ctxs[t % len(ctxs)]
+            for j in range(t, len(jobs), 8):
+                i, off, shp = jobs[j]
+                out = np.empty(shp, np.uint32)
+                ctx.array_read_files(smeta, [paths[i]], off, shp, out.ctypes.data)
+                results[j] = out
+        except Exception as e:  # surfaced below
+            errors.append(e)
+    th = [threading.Thread(target=work, args=(t,)) for t in range(8)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    for c in ctxs[1:]:
+        c.close()
+    assert not errors, errors
+    for j, (i, off, shp) in enumerate(jobs):
+        want = np.frombuffer(O.array_read(smeta, [shards[i]], off, shp), np.uint32).reshape(shp)
+        np.testing.assert_array_equal(results[j], want)
