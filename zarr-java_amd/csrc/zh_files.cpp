@@ -264,6 +264,9 @@ int file_sources(const zh_array_meta* meta, const char* const* paths, int64_t np
     const int64_t k = size < kFileMaxBytes ? slot_take(fd, path) : -1;
     if (k < 0) {
       close(fd);
+      set_err(err, errlen, "'%s': %s", path,
+              size < kFileMaxBytes ? "too many store files open for reads at once"
+                                   : "file larger than a file address can name");
       return ZH_EUNSUPPORTED;
     }
     set.taken.push_back(k);
@@ -548,14 +551,12 @@ int64_t zh_debug_file_reads(const zh_array_meta* meta, const char* const* paths,
     }
     k++;
   };
-  const int64_t isz = meta->chain.sharded ? zh_shard_index_size(meta) : 0;
   for (int64_t i = 0; i < npaths; i++) {
     const SrcDesc& s = srcs[(size_t)i];
     if (s.data) put(i, 0, s.nbytes);  // a whole object
     if (s.index)  // the index read: a prefix, or the last index_nbytes bytes
       put(i, meta->chain.index_location == ZH_INDEX_START ? 0 : s.shard_nbytes - s.index_nbytes,
           s.index_nbytes);
-    (void)isz;
     for (int64_t q = 0; q < s.npieces; q++) put(i, s.pieces[q].offset, s.pieces[q].nbytes);
   }
   return k;
