@@ -344,6 +344,46 @@ def test_write_files_matches_oracle(dev, tmp_path, wmode, chain):
     np.testing.assert_array_equal(got, arr)
 
 
+def _wchar():
+    with open("/proc/self/io") as f:
+        return next(int(l.split()[1]) for l in f if l.startswith("wchar:"))
+
+
+@pytest.mark.parametrize("mapped", ["1", "0"])
+def test_write_files_mapped_windows(dev, tmp_path, monkeypatch, mapped):
+    """A chunk file of several ring windows (here 64 KiB, three lanes) is written through a
+    shared mapping (ZH_WRITE_MAP=1, the default: the lanes' stores into one file do not
+    serialize on its inode lock) or by pwrite; either way it holds exactly the oracle's bytes,
+    a longer stale file is cut to the new size, and the boundary chunk's size is no multiple of
+    the window.  With the mapping the file bytes never pass through write(2) (/proc/self/io)."""
+    monkeypatch.setenv("ZH_PIPE_CHUNK_KB", "64")
+    monkeypatch.setenv("ZH_PIPE_THREADS", "3")
+    monkeypatch.setenv("ZH_WRITE_MAP", mapped)
+    shape = [40, 64, 72]
+    meta = A.make_meta(shape, [32, 64, 72], 4, sharded=True, inner_chunk_shape=[8, 16, 24],
+                       inner_crc32c=True, transpose_order=[1, 2, 0], endian=A.ZH_ENDIAN_BIG)
+    arr = rand_array(shape, 4, seed=109, fill_frac=0.05)
+    want = encode_oracle(meta, arr)
+    coords = chunk_coords(meta, [0, 0, 0], shape)
+    paths = [str(tmp_path / "m" / "c" / "/".join(map(str, c))) for c in coords]
+    assert all(len(w) > 64 << 10 and len(w) % (64 << 10) for w in want)
+    os.makedirs(os.path.dirname(paths[0]), exist_ok=True)
+    with open(paths[0], "wb") as f:
+        f.write(b"\xab" * (2 * len(want[0])))
+    w0 = _wchar()
+    sizes = dev.array_write_files(meta, arr.ctypes.data, [0, 0, 0], shape, paths)
+    wrote = _wchar() - w0
+    assert list(sizes) == [len(w) for w in want]
+    for p, w in zip(paths, want):
+        assert open(p, "rb").read() == w
+    total = sum(len(w) for w in want)
+    if mapped == "1":
+        assert wrote < total // 4, (wrote, total)
+    else:
+        assert wrote >= total, (wrote, total)
+    np.testing.assert_array_equal(files_read(dev, meta, paths, [0, 0, 0], shape), arr)
+
+
 def test_write_files_device_source_and_errors(dev, tmp_path):
     shape = [24, 32, 48]
     meta = A.make_meta(shape, [8, 16, 24], 4, **WCHAINS["sharded_t"])
