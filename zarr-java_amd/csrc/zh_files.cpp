@@ -432,7 +432,11 @@ int zh_array_write_files(zh_ctx* ctx, const zh_array_meta* m, const void* src,
       std::string msg = make_parents(paths[i]);
       int fd = -1;
       if (msg.empty()) {
-        fd = open(paths[i], O_WRONLY | O_CREAT | O_TRUNC | O_CLOEXEC, 0666);
+        // read-write: a shared writable mapping needs it (below); a file that may only be
+        // written is opened write-only and written by pwrite
+        fd = open(paths[i], O_RDWR | O_CREAT | O_TRUNC | O_CLOEXEC, 0666);
+        if (fd < 0 && errno == EACCES)
+          fd = open(paths[i], O_WRONLY | O_CREAT | O_TRUNC | O_CLOEXEC, 0666);
         if (fd < 0) msg = strerror(errno);
       }
       if (!msg.empty()) {
