@@ -388,8 +388,7 @@ int zh_array_read_files(zh_ctx* ctx, const zh_array_meta* meta, const char* cons
  * (M/core/Array.java:143-156) done here — all fill_value → the file deleted (FilesystemStore.delete,
  * a missing file is fine), otherwise the parent directories created and the file created or
  * truncated and written (FilesystemStore.set, M/store/FilesystemStore.java:105-127), the encoded
- * bytes going D2H through the page-locked ring in windows that several lanes write (pwrite, or
- * for a file of several windows stores into a shared mapping of it).  paths[i]:
+ * bytes going D2H through the page-locked ring in windows that several lanes pwrite.  paths[i]:
  * the i-th chunk of computeChunkCoords; src: the region in C order on the host, or on the device
  * with ZH_SRC_DEVICE; nbytes (may be NULL): per chunk the bytes written (0: deleted).  A region
  * that cuts chunks → ZH_EUNSUPPORTED (the binding's read-modify-write); a store failure →

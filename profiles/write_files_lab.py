@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """zh_array_write_files stages (DESIGN §1 "Reads straight from a FilesystemStore", write side):
 one c4 shard region [1,1024,1024,1024] (4 GiB of uint32) written into a FilesystemStore on
-/dev/shm, through the shared mapping (default) and by pwrite (ZH_WRITE_MAP=0), from a pageable host array, a page-locked one, and device memory (no H2D), with the
+/dev/shm, from a pageable host array, a page-locked one, and device memory (no H2D), with the
 copy lanes at 6 and 12; the encode alone (zh_array_write device to device) and the region's H2D
 alone for the split.  Min of R runs, every file compared with the first.  One JSON object.
 usage: write_files_lab.py out.json [reps]"""
@@ -99,8 +99,6 @@ try:
     dev.free_pinned(pin)
     dev.free(d_out)
     one("host_pageable", host.ctypes.data, 0)
-    one("host_pageable_pwrite", host.ctypes.data, 0, {"ZH_WRITE_MAP": "0"})
-    one("device_src_pwrite", d_region, A.ZH_SRC_DEVICE, {"ZH_WRITE_MAP": "0"})
     one("host_pageable_12", host.ctypes.data, 0, {"ZH_PIPE_THREADS": "12"})
     one("device_src", d_region, A.ZH_SRC_DEVICE)
     dev.host_register(host.ctypes.data, host.nbytes)

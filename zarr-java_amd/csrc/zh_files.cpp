@@ -19,7 +19,6 @@
 // windows that the copy lanes pwrite straight into the chunk files.
 #include <errno.h>
 #include <fcntl.h>
-#include <sys/mman.h>
 #include <sys/stat.h>
 #include <unistd.h>
 
@@ -357,20 +356,6 @@ std::string write_all(int fd, const uint8_t* p, int64_t n, int64_t off) {
   return "";
 }
 
-#ifndef MADV_POPULATE_WRITE
-#define MADV_POPULATE_WRITE 23  // Linux 5.14
-#endif
-
-// One window of a mapped chunk file: its pages allocated first (MADV_POPULATE_WRITE reports a
-// failed allocation as an error, where a store into the mapping would raise SIGBUS), then the
-// copy.  A window the kernel cannot populate (an older kernel, a full file system) is pwrite'd
-// instead, which writes it or returns the honest error.
-std::string write_mapped(uint8_t* map, int fd, const uint8_t* p, int64_t n, int64_t off) {
-  if (madvise(map + off, (size_t)n, MADV_POPULATE_WRITE) != 0) return write_all(fd, p, n, off);
-  std::memcpy(map + off, p, (size_t)n);
-  return "";
-}
-
 }  // namespace
 
 extern "C" {
@@ -432,11 +417,7 @@ int zh_array_write_files(zh_ctx* ctx, const zh_array_meta* m, const void* src,
       std::string msg = make_parents(paths[i]);
       int fd = -1;
       if (msg.empty()) {
-        // read-write: a shared writable mapping needs it (below); a file that may only be
-        // written is opened write-only and written by pwrite
-        fd = open(paths[i], O_RDWR | O_CREAT | O_TRUNC | O_CLOEXEC, 0666);
-        if (fd < 0 && errno == EACCES)
-          fd = open(paths[i], O_WRONLY | O_CREAT | O_TRUNC | O_CLOEXEC, 0666);
+        fd = open(paths[i], O_WRONLY | O_CREAT | O_TRUNC | O_CLOEXEC, 0666);
         if (fd < 0) msg = strerror(errno);
       }
       if (!msg.empty()) {
@@ -466,17 +447,6 @@ int zh_array_write_files(zh_ctx* ctx, const zh_array_meta* m, const void* src,
         if (o < dsts[(size_t)i].nbytes)
           jobs.push_back({i, o, std::min(win, dsts[(size_t)i].nbytes - o)});
     lanes = (int)std::max<int64_t>(1, std::min<int64_t>(lanes, (int64_t)jobs.size()));
-    // a file of several windows is written through a shared mapping: buffered writes into one
-    // file take its inode lock, so the lanes' pwrites of one 4 GiB shard would run one at a time
-    // (6 GiB/s on tmpfs); stores into the mapping's pages do not
-    std::vector<uint8_t*> maps((size_t)std::max<int64_t>(1, npaths), nullptr);
-    const bool map_ok = env_int("ZH_WRITE_MAP", 1) != 0;
-    for (int64_t i = 0; st == ZH_OK && map_ok && lanes > 1 && i < npaths; i++) {
-      const int64_t nb = dsts[(size_t)i].nbytes;
-      if (nb <= win || fds[(size_t)i] < 0 || ftruncate(fds[(size_t)i], (off_t)nb) != 0) continue;
-      void* mp = mmap(nullptr, (size_t)nb, PROT_WRITE, MAP_SHARED, fds[(size_t)i], 0);
-      if (mp != MAP_FAILED) maps[(size_t)i] = (uint8_t*)mp;
-    }
     std::atomic<size_t> next{0};
     std::atomic<int> fail{ZH_OK};
     std::mutex fmu;
@@ -503,11 +473,9 @@ int zh_array_write_files(zh_ctx* ctx, const zh_array_meta* m, const void* src,
         if (hipEventSynchronize(ev[pslot]) != hipSuccess) {
           lane_fail(ZH_EHIP, "device-to-host copy of an encoded chunk failed");
         } else {
-          const uint8_t* buf = (const uint8_t*)ctx->ring_out[(size_t)(2 * L + pslot)];
-          const int fd = fds[(size_t)pend->chunk];
-          uint8_t* mp = maps[(size_t)pend->chunk];
-          const std::string w = mp ? write_mapped(mp, fd, buf, pend->len, pend->off)
-                                   : write_all(fd, buf, pend->len, pend->off);
+          const std::string w = write_all(fds[(size_t)pend->chunk],
+                                          (const uint8_t*)ctx->ring_out[(size_t)(2 * L + pslot)],
+                                          pend->len, pend->off);
           if (!w.empty())
             lane_fail(ZH_EIO, std::string("Failed to write to store at '") + paths[pend->chunk] +
                                   "': " + w);
@@ -544,8 +512,6 @@ int zh_array_write_files(zh_ctx* ctx, const zh_array_meta* m, const void* src,
         set_err(err, errlen, "%s", fmsg.c_str());
       }
     }
-    for (size_t i = 0; i < maps.size(); i++)
-      if (maps[i]) (void)munmap(maps[i], (size_t)dsts[i].nbytes);
     for (size_t i = 0; i < fds.size(); i++) {
       if (fds[i] < 0) continue;
       if (close(fds[i]) != 0 && st == ZH_OK) {
