@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """BASELINE configs[0]'s call shape from the store: zarrhip.Array.read of the unaligned 64^3
 region {0,3,517,501} from a c4 shard file on /dev/shm (zh_array_read_files: the index + 27
-ranges read, one plan), per ZH_FILE_THREADS setting, interleaved; plus the mirror's own store
+ranges read, one plan), through the page-locked staging (default) and into heap buffers
+(ZH_FILE_PIN=0), interleaved; plus the mirror's own store
 reads (ZH_FILES=0) and the device-resident one-shot read for reference.  Median of R reads per
 setting and round.  Prints one JSON object.  usage: small_store_lab.py out.json [reps]"""
 import json
@@ -49,8 +50,8 @@ with open(p, "wb") as f:
 dev.free_pinned(pin)
 arr = z.Array.open(z.FilesystemStore(base).resolve("a"))
 off, shp = [0, 3, 517, 501], [1, 64, 64, 64]
-settings = [("files_1", {"ZH_FILE_THREADS": "1"}), ("files_4", {"ZH_FILE_THREADS": "4"}),
-            ("files_8", {"ZH_FILE_THREADS": "8"}), ("store_reads", {"ZH_FILES": "0"})]
+settings = [("files", {}), ("files_heap", {"ZH_FILE_PIN": "0"}),
+            ("store_reads", {"ZH_FILES": "0"})]
 if trace:
     settings = settings[:1]
 res = {"reps": reps, "region_offset": off, "region_shape": shp, "rounds": []}
@@ -69,8 +70,9 @@ try:
                 os.environ.pop(key, None)
             ts.sort()
             row[name] = round(ts[len(ts) // 2] * 1e6, 1)
-        dev.memcpy(region, got.ctypes.data, got.nbytes, 0, None, True)
-        row["verify_mismatches"] = int(dev.synth_verify(region, shape, off, shp, 4, bench.SEED))
+            dev.memcpy(region, got.ctypes.data, got.nbytes, 0, None, True)
+            row[name + "_mismatches"] = int(dev.synth_verify(region, shape, off, shp, 4,
+                                                             bench.SEED))
         print(json.dumps(row), file=sys.stderr, flush=True)
         res["rounds"].append(row)
     out = dev.malloc(64 ** 3 * 4)

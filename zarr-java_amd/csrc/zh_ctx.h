@@ -51,6 +51,11 @@ struct zh_ctx {
   uint8_t* upload_pin = nullptr;   // kUploadSlots × kUploadSlotBytes, created on first use
   std::vector<int> upload_free;
   bool upload_failed = false;
+  // page-locked buffer a one-plan read of store files (zh_array_read_files) reads its bytes
+  // into, so that the plan's H2D is one DMA; grow-only, used under mu by plans that are
+  // created, run and freed while mu is held (read_region, read_multi_impl)
+  uint8_t* file_pin = nullptr;
+  size_t file_pin_cap = 0;
 };
 
 namespace zh {
@@ -199,6 +204,8 @@ constexpr uint64_t kFileTag = 1ull << 62;
 constexpr int kFileOffBits = 40;
 constexpr int64_t kFileMaxBytes = (int64_t)1 << kFileOffBits;
 constexpr int64_t kFileMaxSlots = (int64_t)1 << (62 - kFileOffBits);
+// the largest extent a one-plan file read stages in zh_ctx::file_pin
+constexpr int64_t kFilePinMax = (int64_t)256 << 20;
 inline bool is_file_addr(const void* p) { return ((uint64_t)(uintptr_t)p & kFileTag) != 0; }
 inline const uint8_t* file_addr(int64_t slot, int64_t off) {
   return (const uint8_t*)(uintptr_t)(kFileTag | ((uint64_t)slot << kFileOffBits) | (uint64_t)off);

@@ -286,6 +286,7 @@ void zh_ctx_destroy(zh_ctx* c) {
   if (c->stream) (void)hipStreamDestroy(c->stream);
   if (c->status_pin) (void)hipHostFree(c->status_pin);
   if (c->upload_pin) (void)hipHostFree(c->upload_pin);
+  if (c->file_pin) (void)hipHostFree(c->file_pin);
   if (c->wscratch) (void)hipFree(c->wscratch);
   for (auto& kv : c->cache) (void)hipFree(kv.second);
   pipeline_release(c);
@@ -844,6 +845,25 @@ void plan_free(zh_plan* p) {
 
 namespace zh {
 
+// zh_ctx::file_pin with at least n bytes (grown to a power of two from 4 MiB), or null when
+// the page-locked allocation fails.  Caller holds ctx->mu.
+uint8_t* ctx_file_pin(zh_ctx* ctx, size_t n) {
+  if (ctx->file_pin_cap >= n) return ctx->file_pin;
+  if (ctx->file_pin) (void)hipHostFree(ctx->file_pin);
+  ctx->file_pin = nullptr;
+  ctx->file_pin_cap = 0;
+  size_t cap = (size_t)4 << 20;
+  while (cap < n) cap <<= 1;
+  void* q = nullptr;
+  if (hipHostMalloc(&q, cap, hipHostMallocDefault) != hipSuccess) {
+    (void)hipGetLastError();
+    return nullptr;
+  }
+  ctx->file_pin = (uint8_t*)q;
+  ctx->file_pin_cap = cap;
+  return ctx->file_pin;
+}
+
 int plan_create(zh_ctx* ctx, const zh_array_meta* m, const SrcDesc* srcs, int64_t nchunks,
                 const int64_t* offset, const int64_t* shape, uint32_t flags, bool external_h2d,
                 zh_plan** out, char* err, size_t errlen) {
@@ -1060,14 +1080,43 @@ int plan_create(zh_ctx* ctx, const zh_array_meta* m, const SrcDesc* srcs, int64_
     p->h2d.resize(w);
     p->h2d_len.resize(w);
     // store-file sources (zh_array_read_files): a plan that does its own h2d copies reads
-    // their bytes now into buffers it keeps (the pipelined read's in lanes read them instead)
+    // their bytes now (the pipelined read's in lanes read them instead).  They go into the
+    // context's page-locked buffer at their staging offsets, the host entries (the stored
+    // indexes) copied beside them, and the plan's H2D becomes one DMA of that extent (several
+    // pageable copies cost ~30 us each in the runtime's staging); into buffers the plan keeps
+    // when the extent is large or sparse, or the buffer cannot be had
     std::vector<FileRead> freads;
+    bool files = false;
+    int64_t lo = INT64_MAX, hi = 0, sum = 0;
     for (size_t k = 0; !external_h2d && k < p->h2d.size(); k++) {
-      if (!is_file_addr(p->h2d[k].second)) continue;
+      files = files || is_file_addr(p->h2d[k].second);
+      lo = std::min(lo, p->h2d[k].first);
+      hi = std::max(hi, p->h2d[k].first + p->h2d_len[k]);
+      sum += p->h2d_len[k];
+    }
+    uint8_t* pin = nullptr;
+    if (files && env_int("ZH_FILE_PIN", 1) != 0 && hi - lo <= kFilePinMax &&
+        hi - lo <= 2 * sum + ((int64_t)1 << 20))
+      pin = ctx_file_pin(ctx, (size_t)(hi - lo));
+    for (size_t k = 0; files && k < p->h2d.size(); k++) {
+      const bool f = is_file_addr(p->h2d[k].second);
+      if (pin) {
+        uint8_t* dst = pin + (p->h2d[k].first - lo);
+        if (f)
+          freads.push_back({dst, p->h2d[k].second, p->h2d_len[k]});
+        else
+          std::memcpy(dst, p->h2d[k].second, (size_t)p->h2d_len[k]);
+        continue;
+      }
+      if (!f) continue;
       // uninitialised: the read fills every byte
       p->h2d_keep.emplace_back(new uint8_t[(size_t)std::max<int64_t>(1, p->h2d_len[k])]);
       freads.push_back({p->h2d_keep.back().get(), p->h2d[k].second, p->h2d_len[k]});
       p->h2d[k].second = p->h2d_keep.back().get();
+    }
+    if (pin) {
+      p->h2d.assign(1, {lo, pin});
+      p->h2d_len.assign(1, hi - lo);
     }
     if (!freads.empty()) {  // the small reads of a plan
       const std::string m = file_fetch_all(freads);
