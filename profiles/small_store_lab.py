@@ -51,7 +51,6 @@ dev.free_pinned(pin)
 arr = z.Array.open(z.FilesystemStore(base).resolve("a"))
 off, shp = [0, 3, 517, 501], [1, 64, 64, 64]
 settings = [("files", {}), ("files_heap", {"ZH_FILE_PIN": "0"}),
-            ("files_t2", {"ZH_FILE_THREADS": "2"}), ("files_t4", {"ZH_FILE_THREADS": "4"}),
             ("store_reads", {"ZH_FILES": "0"})]
 if trace:
     settings = settings[:1]

@@ -109,6 +109,7 @@ struct zh_plan {
   std::vector<int64_t> h2d_len;
   std::vector<std::unique_ptr<uint8_t[]>> h2d_keep;  // file bytes read for its own h2d copies
   bool external_h2d = false;    // the pipelined read does the h2d copies (plan_enqueue skips)
+  bool early_h2d = false;       // plan_create queued the h2d copies on the context's stream
   uint8_t* d_out = nullptr;     // staging when the output is host memory
   zh::ScatterArgs args{};
   zh::ItemDesc* d_desc = nullptr;   // per inner-chunk descriptors (resolve kernel)

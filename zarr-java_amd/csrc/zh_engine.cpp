@@ -824,6 +824,7 @@ void plan_free(zh_plan* p) {
   if (!p) return;
   (void)hipSetDevice(p->ctx->device);
   // the blocks go back to the context's cache: the plan's last work on them must be done
+  if (p->early_h2d) (void)hipStreamSynchronize(p->ctx->stream);  // and file_pin is free again
   if (p->done_ev) {
     (void)hipEventSynchronize(p->done_ev);
     (void)hipEventDestroy(p->done_ev);
@@ -1098,6 +1099,29 @@ int plan_create(zh_ctx* ctx, const zh_array_meta* m, const SrcDesc* srcs, int64_
     if (files && env_int("ZH_FILE_PIN", 1) != 0 && hi - lo <= kFilePinMax &&
         hi - lo <= 2 * sum + ((int64_t)1 << 20))
       pin = ctx_file_pin(ctx, (size_t)(hi - lo));
+    // staged in batches of about 1 MiB, each DMA'd on the context's stream (the one the plan
+    // runs on: read_one_plan, read_multi_impl) as soon as it is in, so the H2D of one batch
+    // runs under the reads of the next
+    int64_t b_lo = INT64_MAX, b_hi = 0;
+    auto flush = [&]() -> int {
+      if (b_lo >= b_hi) return ZH_OK;
+      const std::string m = file_fetch_all(freads);
+      freads.clear();
+      if (!m.empty()) {
+        set_err(err, errlen, "%s", m.c_str());
+        return ZH_EIO;
+      }
+      p->early_h2d = true;
+      if (hipMemcpyAsync(p->d_input + b_lo, pin + (b_lo - lo), (size_t)(b_hi - b_lo),
+                         hipMemcpyHostToDevice, ctx->stream) != hipSuccess) {
+        (void)hipGetLastError();
+        set_err(err, errlen, "host-to-device copy of store file bytes failed");
+        return ZH_EHIP;
+      }
+      b_lo = INT64_MAX;
+      b_hi = 0;
+      return ZH_OK;
+    };
     for (size_t k = 0; files && k < p->h2d.size(); k++) {
       const bool f = is_file_addr(p->h2d[k].second);
       if (pin) {
@@ -1106,6 +1130,12 @@ int plan_create(zh_ctx* ctx, const zh_array_meta* m, const SrcDesc* srcs, int64_
           freads.push_back({dst, p->h2d[k].second, p->h2d_len[k]});
         else
           std::memcpy(dst, p->h2d[k].second, (size_t)p->h2d_len[k]);
+        b_lo = std::min(b_lo, p->h2d[k].first);
+        b_hi = std::max(b_hi, p->h2d[k].first + p->h2d_len[k]);
+        if (b_hi - b_lo >= ((int64_t)1 << 20)) {
+          const int rc = flush();
+          if (rc != ZH_OK) return fail(rc);
+        }
         continue;
       }
       if (!f) continue;
@@ -1115,8 +1145,10 @@ int plan_create(zh_ctx* ctx, const zh_array_meta* m, const SrcDesc* srcs, int64_
       p->h2d[k].second = p->h2d_keep.back().get();
     }
     if (pin) {
-      p->h2d.assign(1, {lo, pin});
-      p->h2d_len.assign(1, hi - lo);
+      const int rc = flush();
+      if (rc != ZH_OK) return fail(rc);
+      p->h2d.clear();  // queued already
+      p->h2d_len.clear();
     }
     if (!freads.empty()) {  // the small reads of a plan
       const std::string m = file_fetch_all(freads);
