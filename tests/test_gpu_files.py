@@ -68,6 +68,27 @@ def test_files_unsharded(dev, tmp_path, mode, order):
         np.testing.assert_array_equal(got, oracle_region(meta, chunks, off, shp))
 
 
+@pytest.mark.parametrize("pin", ["1", "0"])
+def test_files_one_plan_batches(dev, tmp_path, monkeypatch, pin):
+    """A one-plan read whose staged bytes span several 1 MiB batches: each batch is DMA'd from
+    the context's page-locked buffer while the next is read (ZH_FILE_PIN=1, the default), or
+    the bytes go through buffers of the plan's own (0).  Two shards with index crc32c and a
+    transpose, an unaligned region over both; then a second, smaller read on the same context
+    reuses the buffer."""
+    monkeypatch.setenv("ZH_FILE_PIN", pin)
+    shape = [1, 96, 96, 192]
+    meta = A.make_meta(shape, [1, 96, 96, 96], 4, sharded=True, inner_chunk_shape=[1, 16, 16, 32],
+                       transpose_order=[0, 3, 2, 1], endian=A.ZH_ENDIAN_BIG, index_crc32c=True)
+    arr = rand_array(shape, 4, seed=113)
+    shards = encode_oracle(meta, arr)
+    paths = write_store(tmp_path, meta, shards)
+    for off, shp in (([0, 5, 3, 40], [1, 90, 91, 140]), ([0, 17, 33, 90], [1, 9, 40, 12])):
+        got = files_read(dev, meta, region_paths(meta, paths, off, shp), off, shp)
+        want = arr[tuple(slice(o, o + s) for o, s in zip(off, shp))]
+        np.testing.assert_array_equal(got, want)
+        np.testing.assert_array_equal(got, oracle_region(meta, shards, off, shp))
+
+
 def test_files_directory_is_a_missing_key(dev, tmp_path):
     """FilesystemStore.exists is Files.isRegularFile: a directory at a key reads as fill."""
     meta, arr, shards = make_case("sharded", seed=53)
