@@ -57,6 +57,8 @@ PipeCfg pipe_cfg() {
   return c;
 }
 
+}  // namespace
+
 // Page-locked host memory (hipHostMalloc'd or hipHostRegister'd) can be DMA'd directly.
 bool host_pinned(const void* p) {
   hipPointerAttribute_t a;
@@ -66,6 +68,8 @@ bool host_pinned(const void* p) {
   }
   return a.type == hipMemoryTypeHost;
 }
+
+namespace {
 
 // Per-slab completion flags the stages wait on; abort() wakes every waiter (a failed stage).
 struct Flags {
