@@ -51,8 +51,7 @@ dev.free_pinned(pin)
 arr = z.Array.open(z.FilesystemStore(base).resolve("a"))
 off, shp = [0, 3, 517, 501], [1, 64, 64, 64]
 settings = [("files", {}), ("files_heap", {"ZH_FILE_PIN": "0"}),
-            ("store_reads", {"ZH_FILES": "0"}),
-            ("store_reads_nopin", {"ZH_FILES": "0", "ZH_FILE_PIN": "0"})]
+            ("store_reads", {"ZH_FILES": "0"})]
 if trace:
     settings = settings[:1]
 res = {"reps": reps, "region_offset": off, "region_shape": shp, "rounds": []}

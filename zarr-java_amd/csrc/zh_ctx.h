@@ -151,14 +151,10 @@ hipError_t ctx_alloc(zh_ctx* ctx, size_t bytes, void** p, size_t* got);
 void ctx_release(zh_ctx* ctx, void* p, size_t bytes);
 
 // Planner over generic sources (zh_plan_create / zh_array_read_pieces); external_h2d: the
-// caller copies p->h2d itself (the pipelined read); transient: the plan is created, run once
-// and freed under ctx->mu (read_one_plan, read_multi_impl), so it may stage its host bytes in
-// the context's page-locked buffer (zh_ctx::file_pin).
+// caller copies p->h2d itself (the pipelined read).
 int plan_create(zh_ctx* ctx, const zh_array_meta* m, const SrcDesc* srcs, int64_t nchunks,
                 const int64_t* offset, const int64_t* shape, uint32_t flags, bool external_h2d,
-                zh_plan** out, char* err, size_t errlen, bool transient = false);
-// Page-locked host memory (hipHostMalloc'd or hipHostRegister'd): DMA'd directly.
-bool host_pinned(const void* p);
+                zh_plan** out, char* err, size_t errlen);
 void plan_free(zh_plan* p);
 
 // The byte ranges of one stored shard a part [part_lo, part_hi) needs (zh_shard_ranges):
@@ -211,8 +207,6 @@ constexpr int64_t kFileMaxBytes = (int64_t)1 << kFileOffBits;
 constexpr int64_t kFileMaxSlots = (int64_t)1 << (62 - kFileOffBits);
 // the largest extent a one-plan file read stages in zh_ctx::file_pin
 constexpr int64_t kFilePinMax = (int64_t)256 << 20;
-// the largest extent of host (not file) sources a transient plan stages there
-constexpr int64_t kHostPinMax = (int64_t)8 << 20;
 inline bool is_file_addr(const void* p) { return ((uint64_t)(uintptr_t)p & kFileTag) != 0; }
 inline const uint8_t* file_addr(int64_t slot, int64_t off) {
   return (const uint8_t*)(uintptr_t)(kFileTag | ((uint64_t)slot << kFileOffBits) | (uint64_t)off);

@@ -867,7 +867,7 @@ uint8_t* ctx_file_pin(zh_ctx* ctx, size_t n) {
 
 int plan_create(zh_ctx* ctx, const zh_array_meta* m, const SrcDesc* srcs, int64_t nchunks,
                 const int64_t* offset, const int64_t* shape, uint32_t flags, bool external_h2d,
-                zh_plan** out, char* err, size_t errlen, bool transient) {
+                zh_plan** out, char* err, size_t errlen) {
   if (!ctx || !m || !offset || !shape || !out) return ZH_EINVAL;
   *out = nullptr;
   int st = zh_validate_meta(m, err, errlen);
@@ -1095,13 +1095,8 @@ int plan_create(zh_ctx* ctx, const zh_array_meta* m, const SrcDesc* srcs, int64_
       hi = std::max(hi, p->h2d[k].first + p->h2d_len[k]);
       sum += p->h2d_len[k];
     }
-    // a small read of pageable host sources in a transient plan is staged the same way: one
-    // DMA per batch instead of one runtime-staged copy per entry (page-locked sources, e.g.
-    // zh_host_staging, stay direct DMAs)
-    const bool host_small = !files && transient && !p->h2d.empty() && hi - lo <= kHostPinMax &&
-                            !host_pinned(p->h2d[0].second);
     uint8_t* pin = nullptr;
-    if ((files || host_small) && env_int("ZH_FILE_PIN", 1) != 0 && hi - lo <= kFilePinMax &&
+    if (files && env_int("ZH_FILE_PIN", 1) != 0 && hi - lo <= kFilePinMax &&
         hi - lo <= 2 * sum + ((int64_t)1 << 20))
       pin = ctx_file_pin(ctx, (size_t)(hi - lo));
     // staged in batches of about 1 MiB, each DMA'd on the context's stream (the one the plan
@@ -1127,7 +1122,7 @@ int plan_create(zh_ctx* ctx, const zh_array_meta* m, const SrcDesc* srcs, int64_
       b_hi = 0;
       return ZH_OK;
     };
-    for (size_t k = 0; (files || pin) && k < p->h2d.size(); k++) {
+    for (size_t k = 0; files && k < p->h2d.size(); k++) {
       const bool f = is_file_addr(p->h2d[k].second);
       if (pin) {
         uint8_t* dst = pin + (p->h2d[k].first - lo);
@@ -1701,7 +1696,7 @@ int read_one_plan(zh_ctx* ctx, const zh_array_meta* meta, const SrcDesc* srcs, i
                   const int64_t* offset, const int64_t* shape, void* out, uint32_t flags,
                   void* stream, char* err, size_t errlen) {
   zh_plan* p = nullptr;
-  int st = plan_create(ctx, meta, srcs, nsrc, offset, shape, flags, false, &p, err, errlen, true);
+  int st = plan_create(ctx, meta, srcs, nsrc, offset, shape, flags, false, &p, err, errlen);
   if (st != ZH_OK) return st;
   g_quiet_err[0] = 0;
   st = zh_plan_execute(p, out, stream);
@@ -2046,8 +2041,7 @@ int read_multi_impl(zh_ctx* const* ctxs, int ndev, int root, const zh_array_meta
       // straight into its destination: the region read itself (large host slabs pipelined)
       rc = read_region(ctx, meta, sub.data(), m, o, s, dst, pf, nullptr, e, sizeof(e));
     } else {
-      if (rc == ZH_OK)
-        rc = plan_create(ctx, meta, sub.data(), m, o, s, pf, false, &p, e, sizeof(e), true);
+      if (rc == ZH_OK) rc = plan_create(ctx, meta, sub.data(), m, o, s, pf, false, &p, e, sizeof(e));
       if (rc == ZH_OK) rc = zh_plan_execute(p, local, nullptr);
       if (rc == ZH_OK && (oroute == ZH_ROUTE_PEER || oroute == ZH_ROUTE_SAME) &&
           hipMemcpyPeerAsync(dst, rdev, local, ctx->device, sbytes, ctx->stream) != hipSuccess) {

@@ -57,8 +57,6 @@ PipeCfg pipe_cfg() {
   return c;
 }
 
-}  // namespace
-
 // Page-locked host memory (hipHostMalloc'd or hipHostRegister'd) can be DMA'd directly.
 bool host_pinned(const void* p) {
   hipPointerAttribute_t a;
@@ -68,8 +66,6 @@ bool host_pinned(const void* p) {
   }
   return a.type == hipMemoryTypeHost;
 }
-
-namespace {
 
 // Per-slab completion flags the stages wait on; abort() wakes every waiter (a failed stage).
 struct Flags {
