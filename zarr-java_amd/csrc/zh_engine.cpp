@@ -1453,6 +1453,14 @@ int plan_create(zh_ctx* ctx, const zh_array_meta* m, const SrcDesc* srcs, int64_
 int plan_enqueue_impl(zh_plan* p, void* out, hipStream_t s) {
   char* err = nullptr;
   size_t errlen = 0;
+  if (p->early_h2d && s != p->ctx->stream) {  // the staged bytes were queued on ctx->stream
+    hipEvent_t e;
+    ZH_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    const bool ok = hipEventRecord(e, p->ctx->stream) == hipSuccess &&
+                    hipStreamWaitEvent(s, e, 0) == hipSuccess;
+    (void)hipEventDestroy(e);
+    if (!ok) return ZH_EHIP;
+  }
   for (size_t k = 0; !p->external_h2d && k < p->h2d.size(); k++)
     ZH_HIP(hipMemcpyAsync(p->d_input + p->h2d[k].first, p->h2d[k].second, (size_t)p->h2d_len[k],
                           hipMemcpyHostToDevice, s));
