@@ -24,7 +24,8 @@ pytestmark = pytest.mark.gpu
 
 @pytest.fixture(params=["one_plan", "pipelined"])
 def mode(request, monkeypatch):
-    """one_plan: a small read (the files are read into host buffers, then one plan);
+    """one_plan: a small read (the file bytes staged in the context's page-locked buffer and
+    DMA'd batch by batch, then one plan);
     pipelined: thresholds shrunk so that the same reads run in slabs through the rings, each
     range pread straight into a ring slot."""
     if request.param == "pipelined":
