@@ -246,6 +246,49 @@ def test_array_read_goes_through_files(dev, tmp_path, monkeypatch, inner):
     assert b.last_read_timing.get("files") is None
 
 
+def _outcome(fn):
+    try:
+        return ("ok", fn())
+    except Exception as e:  # noqa: BLE001 - compared by type and message
+        return (type(e).__name__, str(e))
+
+
+@pytest.mark.parametrize("sharded", [False, True])
+def test_empty_chunk_file_same_as_store_reads(dev, tmp_path, monkeypatch, sharded):
+    """A chunk file of zero bytes (it exists: FilesystemStore.exists is true, get returns an
+    empty buffer) fails or reads exactly as it does through the mirror's own store reads
+    (ZH_FILES=0): for a shard, smaller than its index; for an unsharded chunk, the bytes
+    codec's length check."""
+    shape = [32, 32, 48]
+    b = (z.ArrayMetadataBuilder().withShape(*shape).withDataType(z.DataType.UINT32)
+         .withChunkShape(16, 32, 24).withFillValue(0))
+    if sharded:
+        b = b.withCodecs(lambda c: c.withSharding([8, 8, 8], lambda c1: c1.withBytes("LITTLE")))
+    else:
+        b = b.withCodecs(lambda c: c.withBytes("BIG"))
+    a = z.Array.create(z.FilesystemStore(tmp_path).resolve("e"), b.build())
+    data = np.random.default_rng(127).integers(1, 2 ** 32, shape, dtype=np.uint32)
+    a.write(None, data)
+    victim = tmp_path / "e" / "c" / "1" / "0" / "1"
+    assert victim.is_file()
+    victim.write_bytes(b"")
+    a = z.Array.open(z.FilesystemStore(tmp_path).resolve("e"))
+    kinds = []
+    for off, shp in (([0, 0, 0], shape), ([16, 0, 24], [16, 32, 24]), ([3, 1, 2], [9, 30, 20])):
+        files = _outcome(lambda: a.read(off, shp).copy())
+        monkeypatch.setenv("ZH_FILES", "0")
+        mirror = _outcome(lambda: a.read(off, shp).copy())
+        monkeypatch.delenv("ZH_FILES")
+        assert files[0] == mirror[0], (files, mirror)
+        if files[0] == "ok":
+            np.testing.assert_array_equal(files[1], mirror[1])
+        else:
+            assert files[1] == mirror[1]
+        kinds.append(files[0])
+    # the regions with chunk (1, 0, 1) fail; the last one avoids it and reads the data
+    assert kinds[0] != "ok" and kinds[1] != "ok" and kinds[2] == "ok", kinds
+
+
 @pytest.mark.parametrize("sharded", [False, True])
 def test_read_chunk_goes_through_files(dev, tmp_path, monkeypatch, sharded):
     """zarrhip.Array.readChunk (M/core/Array.java:167-182) over a FilesystemStore: the chunk's
