@@ -14,7 +14,7 @@ step() {  # name, timeout, cmd...
   if [ $rc -ne 0 ]; then tail -n 40 "$OUT/$name.out" "$OUT/$name.err" >&2; exit $rc; fi
 }
 cd "$R" || exit 1
-step filetests 300 python3 -u -m pytest tests/test_gpu_files.py tests/test_jni_shim.py tests/test_gpu_concurrency.py -x -v --timeout 120 --timeout-method thread -p no:cacheprovider
+step filetests 300 python3 -u -m pytest tests/test_gpu_files.py tests/test_jni_shim.py tests/test_gpu_pieces.py tests/test_gpu_concurrency.py -x -v --timeout 120 --timeout-method thread -p no:cacheprovider
 
 cd /tmp || exit 1
 

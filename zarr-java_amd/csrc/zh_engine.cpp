@@ -749,9 +749,13 @@ int caller_pieces(const zh_array_meta* m, const SrcDesc& src, int64_t isz, const
 int caller_pieces_all(const zh_array_meta* m, const SrcDesc& src, int64_t isz, const int64_t* cc,
                       HeldPieces& hp, char* err, size_t errlen) {
   const int n = m->ndim;
-  if (src.index_nbytes < isz) {
-    set_err(err, errlen, "Shard %s is smaller than its index (%lld bytes).",
-            fmt_ints(cc, n).c_str(), (long long)isz);
+  if (src.index_nbytes < isz) {  // worded as for a whole shard when its size is known
+    if (src.shard_nbytes >= 0)
+      set_err(err, errlen, "Shard %s of %lld bytes is smaller than its index (%lld bytes).",
+              fmt_ints(cc, n).c_str(), (long long)src.shard_nbytes, (long long)isz);
+    else
+      set_err(err, errlen, "Shard %s is smaller than its index (%lld bytes).",
+              fmt_ints(cc, n).c_str(), (long long)isz);
     return ZH_EDATA;
   }
   hp.index = src.index + (m->chain.index_location == ZH_INDEX_START ? 0 : src.index_nbytes - isz);
