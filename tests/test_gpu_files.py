@@ -54,6 +54,23 @@ def test_files_read_matches_oracle(dev, tmp_path, mode, chain):
         np.testing.assert_array_equal(got, oracle_region(meta, shards, off, shp))
 
 
+@pytest.mark.parametrize("chain", list(CHAINS))
+def test_files_random_regions(dev, tmp_path, mode, chain):
+    """Seeded random regions (any offset and extent inside the array) over a store with a
+    missing shard: every read equals the oracle's."""
+    meta, arr, shards = make_case(chain, seed=131)
+    shards[4] = None
+    paths = write_store(tmp_path, meta, shards)
+    rng = np.random.default_rng(137)
+    shape = [meta.shape[d] for d in range(meta.ndim)]
+    for _ in range(12):
+        off = [int(rng.integers(0, s)) for s in shape]
+        shp = [int(rng.integers(1, s - o + 1)) for s, o in zip(shape, off)]
+        got = files_read(dev, meta, region_paths(meta, paths, off, shp), off, shp)
+        np.testing.assert_array_equal(got, oracle_region(meta, shards, off, shp),
+                                      err_msg=f"offset {off} shape {shp}")
+
+
 @pytest.mark.parametrize("order", [None, [2, 0, 1]])
 def test_files_unsharded(dev, tmp_path, mode, order):
     """Unsharded chunks: each file is one whole object (get(keys))."""
