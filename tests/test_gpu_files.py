@@ -107,6 +107,52 @@ def test_files_one_plan_batches(dev, tmp_path, monkeypatch, pin):
         np.testing.assert_array_equal(got, oracle_region(meta, shards, off, shp))
 
 
+def test_files_shrinking_file_mid_read(dev, tmp_path, monkeypatch):
+    """A shard file cut short by someone else while the pipelined read is under way: the read
+    either completes (the cut came after the last pread), reports what the reference reports
+    for the shorter file (the cut came before the file's size was taken), or fails with the store
+    error of a pread that hit the end (ZH_EIO, "unexpected end of file") — never a hang or a
+    crash — and the context reads correctly afterwards (the aborted lanes left it clean)."""
+    import threading
+    import time
+    monkeypatch.setenv("ZH_PIPE_MIN_KB", "1")
+    monkeypatch.setenv("ZH_PIPE_SLAB_KB", "512")
+    monkeypatch.setenv("ZH_PIPE_CHUNK_KB", "64")
+    monkeypatch.setenv("ZH_PIPE_THREADS", "2")
+    shape = [1, 256, 256, 256]
+    meta = A.make_meta(shape, shape, 4, sharded=True, inner_chunk_shape=[1, 32, 32, 32],
+                       transpose_order=[0, 3, 2, 1], endian=A.ZH_ENDIAN_BIG, index_crc32c=True)
+    arr = rand_array(shape, 4, seed=139)
+    shard = encode_oracle(meta, arr)[0]
+    p = tmp_path / "s"
+    seen = set()
+    for delay in (0.0, 0.002, 0.01, 0.05):
+        p.write_bytes(shard)
+        cut = threading.Timer(delay, lambda: os.truncate(p, len(shard) // 2))
+        cut.start()
+        try:
+            got = files_read(dev, meta, [str(p)], [0] * 4, shape)
+            np.testing.assert_array_equal(got, arr)
+            seen.add("complete")
+        except ZhError as e:
+            msg = str(e)
+            if e.status == A.ZH_EIO:
+                assert msg == f"Failed to read from store at '{p}': unexpected end of file", msg
+                seen.add("eio")
+            else:  # the size was taken after the cut: entries past the end, or the index
+                # read from the middle of the old payload
+                assert e.status == A.ZH_EDATA, (e.status, msg)
+                assert (msg.startswith("Could not load byte data for chunk [")
+                        or msg.startswith("The checksum of the sharding index is invalid.")), msg
+                seen.add("short")
+        finally:
+            cut.join()
+        time.sleep(0.01)
+    p.write_bytes(shard)
+    np.testing.assert_array_equal(files_read(dev, meta, [str(p)], [0] * 4, shape), arr)
+    assert seen  # which outcomes occurred depends on timing; all of them are correct
+
+
 def test_files_directory_is_a_missing_key(dev, tmp_path):
     """FilesystemStore.exists is Files.isRegularFile: a directory at a key reads as fill."""
     meta, arr, shards = make_case("sharded", seed=53)
