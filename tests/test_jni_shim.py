@@ -451,6 +451,25 @@ def test_array_write_files_via_shim(dev, tmp_path, slab_mb, chain, mb):
 
 
 @pytest.mark.gpu
+def test_array_write_files_store_error_via_shim(dev, tmp_path):
+    """A chunk path whose parent directory cannot be created (a file is in the way): ZH_EIO →
+    dev.zarr.zarrjava.store.StoreException with the store's message; the region's primitive
+    array is released (JNI_ABORT) and no critical section stays open."""
+    shape = [64, 32, 48]
+    meta, arr, shards = _case("c4", shape=shape, seed=41)
+    coords = chunk_coords(meta, [0, 0, 0], shape)
+    blocker = tmp_path / "blocker"
+    blocker.write_bytes(b"x")
+    paths = [str(blocker / "c" / "/".join(map(str, c))) for c in coords]
+    jvm = FakeJVM()
+    with pytest.raises(JavaException) as ej:
+        jvm.array_write_files(dev.h.value, meta, arr, [0, 0, 0], paths)
+    assert ej.value.cls == "dev/zarr/zarrjava/store/StoreException"
+    assert ej.value.msg.startswith(f"Failed to write to store at '{paths[0]}': ")
+    jvm.check_rules()
+
+
+@pytest.mark.gpu
 def test_data_errors_become_zarr_exceptions(dev, tmp_path):
     """ZH_EDATA → dev.zarr.zarrjava.ZarrException with the oracle's (the reference's) text:
     a corrupt stored index on the device, a missing range ("Could not load byte data")."""
