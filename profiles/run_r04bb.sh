@@ -1,0 +1,21 @@
+#!/bin/bash
+# Round 4: file tests, then the 64^3 store read with page-locked vs heap staging, and its trace.
+set -u
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+OUT=$R/gpurun_out/r04bb
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+step() {  # name, timeout, cmd...
+  local name=$1 t=$2; shift 2
+  echo "== $name: $*" >&2
+  timeout -k 10 "$t" "$@" > "$OUT/$name.out" 2> "$OUT/$name.err"
+  local rc=$?
+  echo "== $name rc=$rc" >&2
+  if [ $rc -ne 0 ]; then tail -n 40 "$OUT/$name.out" "$OUT/$name.err" >&2; exit $rc; fi
+}
+cd "$R" || exit 1
+
+step slab 400 python3 -u profiles/small_store_lab.py "$OUT/small_store_lab.json" 200
+cd /tmp || exit 1
+
+echo done >&2
