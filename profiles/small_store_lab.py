@@ -51,8 +51,6 @@ dev.free_pinned(pin)
 arr = z.Array.open(z.FilesystemStore(base).resolve("a"))
 off, shp = [0, 3, 517, 501], [1, 64, 64, 64]
 settings = [("files", {}), ("files_heap", {"ZH_FILE_PIN": "0"}),
-            ("files_b256", {"ZH_FILE_BATCH_KB": "256"}), ("files_b512", {"ZH_FILE_BATCH_KB": "512"}),
-            ("files_b2048", {"ZH_FILE_BATCH_KB": "2048"}),
             ("store_reads", {"ZH_FILES": "0"})]
 if trace:
     settings = settings[:1]

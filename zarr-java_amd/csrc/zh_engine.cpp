@@ -1107,7 +1107,6 @@ int plan_create(zh_ctx* ctx, const zh_array_meta* m, const SrcDesc* srcs, int64_
     // runs on: read_one_plan, read_multi_impl) as soon as it is in, so the H2D of one batch
     // runs under the reads of the next
     int64_t b_lo = INT64_MAX, b_hi = 0;
-    const int64_t batch = (int64_t)std::max(64, env_int("ZH_FILE_BATCH_KB", 1024)) << 10;
     auto flush = [&]() -> int {
       if (b_lo >= b_hi) return ZH_OK;
       const std::string m = file_fetch_all(freads);
@@ -1137,7 +1136,7 @@ int plan_create(zh_ctx* ctx, const zh_array_meta* m, const SrcDesc* srcs, int64_
           std::memcpy(dst, p->h2d[k].second, (size_t)p->h2d_len[k]);
         b_lo = std::min(b_lo, p->h2d[k].first);
         b_hi = std::max(b_hi, p->h2d[k].first + p->h2d_len[k]);
-        if (b_hi - b_lo >= batch) {
+        if (b_hi - b_lo >= ((int64_t)1 << 20)) {
           const int rc = flush();
           if (rc != ZH_OK) return fail(rc);
         }
