@@ -473,6 +473,33 @@ def test_write_files_matches_oracle(dev, tmp_path, wmode, chain):
     np.testing.assert_array_equal(got, arr)
 
 
+@pytest.mark.parametrize("chain", list(WCHAINS))
+def test_write_files_random_regions(dev, tmp_path, wmode, chain):
+    """Seeded random regions of whole chunks (the array boundary clips the last ones), written
+    one after another into the same store: every chunk file the region covers holds exactly the
+    oracle's encoding of that region (ShardingIndexedCodec.encode / BytesCodec.encode)."""
+    shape = [20, 40, 56]
+    cs = [8, 16, 24]
+    meta = A.make_meta(shape, cs, 4, fill=(5).to_bytes(4, "little"), **WCHAINS[chain])
+    rng = np.random.default_rng(149)
+    grid = [-(-s // c) for s, c in zip(shape, cs)]
+    for k in range(6):
+        c0 = [int(rng.integers(0, g)) for g in grid]
+        c1 = [int(rng.integers(a + 1, g + 1)) for a, g in zip(c0, grid)]
+        off = [a * c for a, c in zip(c0, cs)]
+        shp = [min(b * c, s) - o for b, c, s, o in zip(c1, cs, shape, off)]
+        arr = rand_array(shp, 4, seed=151 + k, fill_frac=0.2, fill=5)
+        want = O.array_write(meta, arr.tobytes(), off, shp)
+        coords = chunk_coords(meta, off, shp)
+        paths = [str(tmp_path / "r" / "c" / "/".join(map(str, c))) for c in coords]
+        sizes = dev.array_write_files(meta, arr.ctypes.data, off, shp, paths)
+        for p, w, sz in zip(paths, want, sizes):
+            if w is None:
+                assert sz == 0 and not os.path.exists(p)
+            else:
+                assert sz == len(w) and open(p, "rb").read() == w, (off, shp, p)
+
+
 def test_write_files_windows_of_one_file(dev, tmp_path, monkeypatch):
     """Chunk files of several ring windows (here 64 KiB, three lanes), so the lanes write
     windows of the same file at once: each file holds exactly the oracle's bytes, a longer stale
