@@ -71,6 +71,28 @@ def test_files_random_regions(dev, tmp_path, mode, chain):
                                       err_msg=f"offset {off} shape {shp}")
 
 
+@pytest.mark.parametrize("dsize", [1, 2, 8])
+def test_files_dtypes_read_and_write(dev, tmp_path, mode, dsize):
+    """1-, 2- and 8-byte elements (endian ignored for 1 byte, core BytesCodec.java:16-18)
+    through both file entry points: the written files equal the oracle's encoding and read
+    back, whole and as an unaligned part, equal to the oracle's reads."""
+    shape = [24, 32, 48]
+    meta = A.make_meta(shape, [8, 16, 24], dsize, fill=(3).to_bytes(dsize, "little"),
+                       **CHAINS["transpose_be"])
+    arr = rand_array(shape, dsize, seed=157, fill_frac=0.1, fill=3)
+    want = encode_oracle(meta, arr)
+    coords = chunk_coords(meta, [0, 0, 0], shape)
+    paths = [str(tmp_path / "d" / "c" / "/".join(map(str, c))) for c in coords]
+    dev.array_write_files(meta, arr.ctypes.data, [0, 0, 0], shape, paths)
+    for p, w in zip(paths, want):
+        assert (not os.path.exists(p)) if w is None else open(p, "rb").read() == w
+    files = [p if w is not None else None for p, w in zip(paths, want)]
+    for off, shp in REGIONS:
+        got = files_read(dev, meta, region_paths(meta, files, off, shp), off, shp)
+        np.testing.assert_array_equal(got, oracle_region(meta, want, off, shp))
+        np.testing.assert_array_equal(got, arr[tuple(slice(o, o + s) for o, s in zip(off, shp))])
+
+
 @pytest.mark.parametrize("order", [None, [2, 0, 1]])
 def test_files_unsharded(dev, tmp_path, mode, order):
     """Unsharded chunks: each file is one whole object (get(keys))."""
