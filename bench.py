@@ -1441,7 +1441,8 @@ def main():
         return
 
     from zarrhip._lib import DeviceContext, lib
-    dev = DeviceContext(int(os.environ.get("ZH_DEVICE", local)))
+    # one GPU per rank; ranks beyond the visible GPUs share them (a rehearsal on fewer cards)
+    dev = DeviceContext(int(os.environ.get("ZH_DEVICE", local % max(1, visible_devices()))))
     info = dev.info()
     n = meta.ndim
     shape = [meta.shape[d] for d in range(n)]
