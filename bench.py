@@ -1442,7 +1442,8 @@ def main():
 
     from zarrhip._lib import DeviceContext, lib
     # one GPU per rank; ranks beyond the visible GPUs share them (a rehearsal on fewer cards)
-    dev = DeviceContext(int(os.environ.get("ZH_DEVICE", local % max(1, visible_devices()))))
+    dev = DeviceContext(int(os.environ.get(
+        "ZH_DEVICE", local % max(1, visible_devices()) if local else 0)))
     info = dev.info()
     n = meta.ndim
     shape = [meta.shape[d] for d in range(n)]
