@@ -1,7 +1,6 @@
 #!/bin/bash
 # Round 4, last tree: the default bench line, then the 2-rank weak-mode rehearsal at a quarter
-# of the array (ranks share the card, so gloo through host memory stands in for RCCL), and
-# the weak mode with two ranks on the same card.
+# of the array (both ranks on the same card).
 set -u
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$R/gpurun_out/r04dd
