@@ -360,55 +360,85 @@ int zh_host_staging(zh_ctx* ctx, size_t bytes, void** out);
 
 /* ---- region reads straight from a FilesystemStore ---------------------------------------
  * core.Array.read when every chunk key resolves to a file (StoreHandle.toPath(),
- * M/store/StoreHandle.java:100-105): the library does the store I/O itself.  paths[i] is the
- * file of the i-th chunk of computeChunkCoords(meta->shape, meta->chunk_shape, offset, shape);
- * NULL, or a path that is not a regular file, is a missing key (FilesystemStore.exists,
- * FilesystemStore.java:43-46) → fill_value.  Per file the reads are the reference's:
- *   unsharded: the whole object (get(keys), :49-58);
- *   sharded:   the stored index (a prefix or suffix read, get(keys, start), :62-80), then the
- *              ranges of the inner chunks the part references (StoreHandleDataProvider,
- *              ShardingIndexedCodec.java:333-357; adjacent ranges merged); the index crc32c
- *              and every entry are checked on the device, as with zh_array_read_pieces.
+ * M/store/StoreHandle.java:96-101): the library does the store I/O itself.
+ *
+ * The store: root = FilesystemStore's directory, name = FilesystemStore.toString() (its file:
+ * URI without the trailing '/', FilesystemStore.java:194-197; NULL → "file://" + root).  A
+ * NULL store means the filesystem root ("/", named "file://").  Errors name the store and the
+ * key as StoreException does (StoreException.java:17-35): "Failed to read from store '<name>'
+ * at key '<key>': <reason>", the key being the path below root ('/'-joined keys).
+ *
+ * paths[i] is the file of the i-th chunk of computeChunkCoords(meta->shape, meta->chunk_shape,
+ * offset, shape); NULL, or a path that is not a regular file, is a missing key
+ * (FilesystemStore.exists, FilesystemStore.java:42-45) → fill_value.  Per file the reads are
+ * the reference's:
+ *   unsharded:           the whole object (get(keys), :47-57);
+ *   sharded, whole shard (the part is the full chunk: decodePartial → chunkHandle.read(),
+ *                        ShardingIndexedCodec.java:246-251): the index and the referenced
+ *                        ranges of the file as it is; an index or entry beyond the file is an
+ *                        error (ZH_EDATA; the reference's ByteBuffer slicing throws);
+ *   sharded, part        (StoreHandleDataProvider, ShardingIndexedCodec.java:333-357): the
+ *                        index by a prefix (index_location start, get(keys, 0, n)) or suffix
+ *                        (get(keys, -n)) read, then the referenced inner-chunk ranges
+ *                        (get(keys, off, off + n), adjacent ranges merged).  As in
+ *                        get(keys, start, end) (:84-102), bytes past the end of the file read as
+ *                        zeros: a truncated file decodes with zeros where its bytes are missing,
+ *                        and a prefix index read of a file shorter than the index is zero-padded
+ *                        (its crc32c then fails).  A suffix read of a file shorter than the
+ *                        index is an error (ZH_EDATA; the reference's position(< 0) throws).
+ * The index crc32c and every entry are checked on the device, as with zh_array_read_pieces.
  * The range reads (pread) write straight into the page-locked ring of the pipelined read, so
  * the file bytes are copied once on the host and the reads overlap the H2D copies, the decode
- * and the D2H of earlier slabs.  `out`: host memory (flags 0) or device memory (ZH_OUT_DEVICE);
- * ZH_SRC_DEVICE is not allowed.  A file that cannot be opened or read (other than missing) →
- * ZH_EIO, "Failed to read from store at '<path>': <reason>".  The chain must be device-
- * supported (zh_validate_meta); chains with host byte-to-byte stages keep their store reads on
- * the binding side (zh_array_read_pieces). */
-int zh_array_read_files(zh_ctx* ctx, const zh_array_meta* meta, const char* const* paths,
-                        int64_t npaths, const int64_t* offset, const int64_t* shape, void* out,
-                        uint32_t flags, char* err, size_t errlen);
+ * and the D2H of earlier slabs.  At most 64 files are open at once whatever the region's
+ * chunk count (a closed one is reopened by path for its next range).  `out`: host memory
+ * (flags 0) or device memory (ZH_OUT_DEVICE); ZH_SRC_DEVICE is not allowed.  A file that cannot
+ * be opened or read (other than missing) → ZH_EIO with the readFailed text.  The chain must be
+ * device-supported (zh_validate_meta); chains with host byte-to-byte stages keep their store
+ * reads on the binding side (zh_array_read_pieces). */
+typedef struct zh_file_store {
+  const char* root; /* FilesystemStore's directory                                          */
+  const char* name; /* FilesystemStore.toString(); NULL: "file://" + root                     */
+} zh_file_store;
+int zh_array_read_files(zh_ctx* ctx, const zh_array_meta* meta, const zh_file_store* store,
+                        const char* const* paths, int64_t npaths, const int64_t* offset,
+                        const int64_t* shape, void* out, uint32_t flags, char* err,
+                        size_t errlen);
 /* zh_array_read_files spread over several GPUs in one process (zh_array_read_multi_routed's
  * slabs and routes; HipArray.read with ZH_DEVICES): every device reads the files of its slab
  * and decodes it, a host-terminated read copying each slab straight into its slice of `out`
  * (each device over its own PCIe link). */
+int zh_array_read_files_multi(zh_ctx* const* ctxs, int ndev, int root, const zh_array_meta* meta,
+                              const zh_file_store* store, const char* const* paths,
+                              int64_t npaths, const int64_t* offset, const int64_t* shape,
+                              void* out, uint32_t flags, int32_t* slab_route, char* err,
+                              size_t errlen);
 /* core.Array.write of a region of whole chunks (clipped only by the array boundary) into a
  * FilesystemStore: the device encode of zh_array_write, then per chunk writeChunk's store call
  * (M/core/Array.java:143-156) done here — all fill_value → the file deleted (FilesystemStore.delete,
- * a missing file is fine), otherwise the parent directories created and the file created or
- * truncated and written (FilesystemStore.set, M/store/FilesystemStore.java:105-127), the encoded
- * bytes going D2H through the page-locked ring in windows that several lanes pwrite.  paths[i]:
- * the i-th chunk of computeChunkCoords; src: the region in C order on the host, or on the device
- * with ZH_SRC_DEVICE; nbytes (may be NULL): per chunk the bytes written (0: deleted).  A region
- * that cuts chunks → ZH_EUNSUPPORTED (the binding's read-modify-write); a store failure →
- * ZH_EIO ("Failed to write to store at '<path>': <reason>"). */
+ * a missing file is fine), otherwise the parent directories created and the chunk's bytes
+ * stored at its path (FilesystemStore.set, M/store/FilesystemStore.java:105-128).  The encoded
+ * bytes go D2H through the page-locked ring in windows that several lanes pwrite into a
+ * temporary file beside the chunk's, renamed over it once complete: a failure leaves every
+ * chunk it did not complete as it was (the reference truncates a file before writing it), and
+ * at most 3 files per lane are open at once.  paths[i]: the i-th chunk of computeChunkCoords;
+ * src: the region in C order on the host, or on the device with ZH_SRC_DEVICE; nbytes (may be
+ * NULL): per chunk the bytes written (0: deleted).  A region that cuts chunks → ZH_EUNSUPPORTED
+ * (the binding's read-modify-write); a store failure → ZH_EIO with StoreException's text
+ * (writeFailed: "... Failed to write <n> bytes to file: <path>" or "... Failed to create parent
+ * directories for path: <dir>"; deleteFailed: "... Failed to delete file: <path>"). */
 int zh_array_write_files(zh_ctx* ctx, const zh_array_meta* meta, const void* src,
-                         const int64_t* offset, const int64_t* shape, const char* const* paths,
-                         int64_t npaths, uint32_t flags, int64_t* nbytes, char* err,
-                         size_t errlen);
+                         const int64_t* offset, const int64_t* shape, const zh_file_store* store,
+                         const char* const* paths, int64_t npaths, uint32_t flags,
+                         int64_t* nbytes, char* err, size_t errlen);
 /* Diagnostic (no device needed): the store reads zh_array_read_files would make for these
  * paths, as (chunk index, file offset, bytes) triples in order — a whole object, or a shard's
  * index read followed by its merged range reads; missing keys make none.  Writes up to `cap`
  * triples to `reads` (may be NULL) and returns their number, or -zh_status with err set (the
  * same checks and messages as the read).  Tests use it to check the read plan on the host. */
-int64_t zh_debug_file_reads(const zh_array_meta* meta, const char* const* paths, int64_t npaths,
-                            const int64_t* offset, const int64_t* shape, int64_t* reads,
-                            int64_t cap, char* err, size_t errlen);
-int zh_array_read_files_multi(zh_ctx* const* ctxs, int ndev, int root, const zh_array_meta* meta,
-                              const char* const* paths, int64_t npaths, const int64_t* offset,
-                              const int64_t* shape, void* out, uint32_t flags,
-                              int32_t* slab_route, char* err, size_t errlen);
+int64_t zh_debug_file_reads(const zh_array_meta* meta, const zh_file_store* store,
+                            const char* const* paths, int64_t npaths, const int64_t* offset,
+                            const int64_t* shape, int64_t* reads, int64_t cap, char* err,
+                            size_t errlen);
 
 /* ShardingIndexedCodec.decode: whole shard → chunk_shape elements. */
 int zh_sharding_decode(zh_ctx* ctx, const zh_array_meta* meta, const void* shard, int64_t nbytes,

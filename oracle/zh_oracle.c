@@ -326,33 +326,42 @@ static int sharding_decode_internal(const zh_array_meta* m, const uint8_t* shard
                                     const char* path, const int64_t* offset, const int32_t* shape,
                                     uint8_t* out, int nthreads, char* err, size_t errlen);
 
-/* FilesystemStore.get(keys, start, end) — M/store/FilesystemStore.java:85-102: one
- * Files.newByteChannel open, a position + read into a freshly allocated buffer, and a close
- * per call; a negative start counts from the end (:74-77, the suffix read of the index).
- * Returns a malloc'd buffer of `len` bytes, or NULL (missing file / short read). */
-static uint8_t* file_range_read(const char* path, int64_t start, int64_t len, int64_t* fsize) {
+/* FilesystemStore.get(keys, start, end) and get(keys, start) — M/store/FilesystemStore.java:
+ * 59-102: one Files.newByteChannel open per call; a negative start counts from the end
+ * (:63-68, :87-91: the suffix read of the index); Utils.allocateNative(end - start) (a fresh,
+ * zeroed heap buffer, M/utils/Utils.java:17-20), position(start), one read of what the file
+ * holds, close.  So a range past the end of the file comes back zero-padded to its length.
+ *   FR_OK       *out = malloc'd buffer of `len` bytes (the file's bytes, then zeros)
+ *   FR_MISSING  the file does not exist (NoSuchFileException → null)
+ *   FR_NEGATIVE the resolved start is below 0 (position(< 0) throws IllegalArgumentException)
+ * *fsize (may be NULL) = the file's size. */
+enum { FR_OK = 0, FR_MISSING = 1, FR_NEGATIVE = 2 };
+static int file_range_read(const char* path, int64_t start, int64_t len, uint8_t** out,
+                           int64_t* fsize) {
+  *out = NULL;
   int fd = open(path, O_RDONLY);
-  if (fd < 0) return NULL;
+  if (fd < 0) return FR_MISSING;
   struct stat sb;
   if (fstat(fd, &sb) != 0) {
     close(fd);
-    return NULL;
+    return FR_MISSING;
   }
   if (fsize) *fsize = (int64_t)sb.st_size;
   if (start < 0) start += (int64_t)sb.st_size;
-  uint8_t* b = (uint8_t*)malloc(len > 0 ? len : 1);
+  if (start < 0) {
+    close(fd);
+    return FR_NEGATIVE;
+  }
+  uint8_t* b = (uint8_t*)calloc(len > 0 ? len : 1, 1);
   int64_t got = 0;
   while (got < len) {
     ssize_t r = pread(fd, b + got, (size_t)(len - got), (off_t)(start + got));
-    if (r <= 0) break;
+    if (r <= 0) break; /* end of file: the rest stays zero */
     got += r;
   }
   close(fd);
-  if (got != len) {
-    free(b);
-    return NULL;
-  }
-  return b;
+  *out = b;
+  return FR_OK;
 }
 
 static uint64_t load_u64(const uint8_t* p, int big) {
@@ -409,7 +418,14 @@ static int decode_one_inner(inner_job_t* J, int64_t k, char* err, size_t errlen)
     set_err(err, errlen, "projection overflow");
     return ZH_EARITH;                                                /* :222-225 */
   }
-  if (off < 0 || len < 0 || off + len > J->nbytes) {                 /* :226-230 */
+  /* :226-230.  An entry the provider cannot serve: in memory (ByteBufferDataProvider.read,
+   * :323-330) a slice beyond the buffer; from a store a negative position or length, or a
+   * length beyond a Java buffer (the (int) allocation).  The reference throws
+   * IllegalArgumentException there; the oracle (like the device) reports "Could not load
+   * byte data" (DESIGN.md quirk Q14).  A store range past the end of the file is no error: it
+   * reads zero-padded (file_range_read). */
+  if (off < 0 || len < 0 ||
+      (J->path ? (len > 2147483647LL || off > INT64_MAX - len) : off + len > J->nbytes)) {
     char cs[256];
     fmt_coords(cs, sizeof cs, c, n);
     set_err(err, errlen, "Could not load byte data for chunk %s", cs);
@@ -418,8 +434,7 @@ static int decode_one_inner(inner_job_t* J, int64_t k, char* err, size_t errlen)
   const uint8_t* bytes = J->shard ? J->shard + off : NULL;
   uint8_t* fbuf = NULL;
   if (J->path) { /* dataProvider.read(off, len) → storeHandle.read(off, off + len) :354-356 */
-    fbuf = file_range_read(J->path, off, len, NULL);
-    if (!fbuf) {
+    if (file_range_read(J->path, off, len, &fbuf, NULL) != FR_OK) { /* null → :227-229 */
       char cs[256];
       fmt_coords(cs, sizeof cs, c, n);
       set_err(err, errlen, "Could not load byte data for chunk %s", cs);
@@ -487,14 +502,21 @@ static int sharding_decode_internal(const zh_array_meta* m, const uint8_t* shard
   int64_t isz = shard_index_size(m);                                  /* :190 */
   uint8_t* fidx = NULL;
   if (path) { /* StoreHandleDataProvider.readPrefix / readSuffix :340-352 */
-    fidx = file_range_read(path, m->chain.index_location == ZH_INDEX_START ? 0 : -isz, isz,
-                           &nbytes);
-    if (!fidx) { /* a null index buffer → fill_value (:199-204) */
+    int rc = file_range_read(path, m->chain.index_location == ZH_INDEX_START ? 0 : -isz, isz,
+                             &fidx, &nbytes);
+    if (rc == FR_MISSING) { /* a null index buffer → fill_value (:199-204) */
       fill_elems(out, nel, ds, m->fill_value);
       return ZH_OK;
     }
-  }
-  if (nbytes < isz) {
+    if (rc == FR_NEGATIVE) { /* a suffix longer than the file: position(< 0) throws
+                              * IllegalArgumentException; reported as the device does (Q14) */
+      set_err(err, errlen, "Shard of %lld bytes is smaller than its index (%lld bytes).",
+              (long long)nbytes, (long long)isz);
+      return ZH_EDATA;
+    }
+    /* a prefix read is zero-padded like any range: a file shorter than the index gives an
+     * index of isz bytes (whose crc32c, if any, then fails) */
+  } else if (nbytes < isz) {
     set_err(err, errlen, "Shard of %lld bytes is smaller than its index (%lld bytes).",
             (long long)nbytes, (long long)isz);
     free(fidx);
@@ -625,7 +647,7 @@ static int array_read_impl(const zh_array_meta* m, const zh_chunk_src* chunks,
         struct stat sb;
         if (stat(paths[i], &sb) == 0) {
           fsz = (int64_t)sb.st_size;
-          whole = file_range_read(paths[i], 0, fsz, NULL);
+          (void)file_range_read(paths[i], 0, fsz, &whole, NULL);
         }
         fsrc.data = whole;
         fsrc.nbytes = fsz;

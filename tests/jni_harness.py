@@ -282,29 +282,32 @@ class FakeJVM:
         """A java.lang.String (None: a null reference)."""
         return None if text is None else self.L.fj_new_string(os.fsencode(text))
 
-    def array_read_files(self, ctxs, meta, paths, offset, shape):
+    def array_read_files(self, ctxs, meta, paths, offset, shape, store=(None, None)):
         """arrayReadFiles: HipArray.read over a FilesystemStore — the chunk keys' paths
         (StoreHandle.toPath()) in computeChunkCoords order, None = no path; ctxs: one context
-        or a list (ZH_DEVICES)."""
+        or a list (ZH_DEVICES); store: (storeRoot, storeName) strings (None: null)."""
         nel = int(np.prod(shape))
         out = self.output(meta.dtype_size, nel)
         jp = self.objs([self.string(p) for p in paths], b"java/lang/String")
         cl = ctxs if isinstance(ctxs, (list, tuple)) else [ctxs or 0]
         args = (self.longs([int(c) for c in cl]),) + self.meta_args(meta) + \
-            (jp, self.longs(offset), self.longs(shape), out)
+            (self.string(store[0]), self.string(store[1]), jp, self.longs(offset),
+             self.longs(shape), out)
         rc = self._done(self._fn("arrayReadFiles")(P(self.env), None, *map(P, args)))
         dt = {1: np.uint8, 2: np.uint16, 4: np.uint32, 8: np.uint64}[meta.dtype_size]
         return rc, (self.array_of(out, dt).reshape(shape) if rc == 0 else None)
 
-    def array_write_files(self, ctx, meta, arr, offset, paths):
+    def array_write_files(self, ctx, meta, arr, offset, paths, store=(None, None)):
         """arrayWriteFiles: HipArray.write over a FilesystemStore — the region's primitive
-        array and the chunk keys' paths; returns the status (0, or 3: the caller writes)."""
+        array, the store (storeRoot, storeName) and the chunk keys' paths; returns the status
+        (0, or 3: the caller writes)."""
         kind = KIND[meta.dtype_size]
         data = self.prim(kind, np.ascontiguousarray(arr).view(
             {1: np.int8, 2: np.int16, 4: np.int32, 8: np.int64}[meta.dtype_size]).ravel())
         self.sources.append(data)
         jp = self.objs([self.string(p) for p in paths], b"java/lang/String")
-        args = self.meta_args(meta) + (self.longs(offset), self.longs(list(arr.shape)), data, jp)
+        args = self.meta_args(meta) + (self.longs(offset), self.longs(list(arr.shape)), data,
+                                       self.string(store[0]), self.string(store[1]), jp)
         fn = self._fn("arrayWriteFiles")
         fn.restype = C.c_int32
         return self._done(fn(P(self.env), None, C.c_int64(int(ctx or 0)), *map(P, args)))

@@ -3,7 +3,9 @@ device): FilesystemStore semantics (M/store/FilesystemStore.java:43-102) — a m
 non-regular file is a missing key, a whole chunk is one read, a shard is its index read (a
 prefix with index_location start, else the last 16·n + 4 bytes: get(keys, -isz)) followed by the
 referenced inner chunks' ranges (StoreHandleDataProvider, ShardingIndexedCodec.java:333-357),
-adjacent ones merged, entries beyond the file left out."""
+adjacent ones merged.  A part's ranges are read like get(keys, start, end) (zero-padded past the
+end of the file), so no entry is dropped for its offset; a whole shard is sliced out of the
+file as it is (ShardingIndexedCodec.java:246-251), so entries beyond the file are left out."""
 import os
 import struct
 
@@ -77,7 +79,8 @@ def test_shard_reads_are_index_then_referenced_ranges(tmp_path, loc):
                   for d in range(3)]
             hi = [min(off[d] + shp[d], (c[d] + 1) * meta.chunk_shape[d]) -
                   c[d] * meta.chunk_shape[d] for d in range(3)]
-            rs = shard_ranges(meta, index, size, lo, hi, 1 << 30)
+            whole = all(lo[d] == 0 and hi[d] == meta.chunk_shape[d] for d in range(3))
+            rs = shard_ranges(meta, index, size if whole else -1, lo, hi, 1 << 30)
             want += [(i, o, nb) for o, nb in rs]
             # every referenced present entry lies inside exactly one read range
             mine = [(o, nb) for j, o, nb in got if j == i][1:]
@@ -106,7 +109,7 @@ def test_missing_directories_and_short_files(tmp_path):
     assert all(k in by for k in range(5, len(paths)))
 
 
-def test_truncated_shard_drops_entries_beyond_the_file(tmp_path):
+def test_truncated_whole_shard_drops_entries_beyond_the_file(tmp_path):
     shape = [8, 16, 24]
     meta = A.make_meta(shape, [8, 16, 24], 4, sharded=True, inner_chunk_shape=[4, 8, 8],
                        index_location=A.ZH_INDEX_START)
@@ -118,6 +121,31 @@ def test_truncated_shard_drops_entries_beyond_the_file(tmp_path):
     assert cut[0] == full[0]  # the index read
     assert sum(n for _, _, n in cut[1:]) < sum(n for _, _, n in full[1:])
     assert all(o + n <= len(s) - 100 for _, o, n in cut)
+
+
+@pytest.mark.parametrize("loc", [A.ZH_INDEX_END, A.ZH_INDEX_START])
+def test_truncated_part_reads_every_entry(tmp_path, loc):
+    """A part of a truncated shard reads the same ranges as of the intact one (the store read
+    returns zeros past the end), and a file shorter than a prefix index still reads an index of
+    the full length (zero-padded; a suffix index of such a file is reported short)."""
+    shape = [8, 16, 24]
+    meta = A.make_meta(shape, [8, 16, 24], 4, sharded=True, inner_chunk_shape=[4, 8, 8],
+                       index_location=loc, index_crc32c=True)
+    s = encode_oracle(meta, rand_array(shape, 4, seed=9, fill_frac=0.0))[0]
+    paths = _write(tmp_path, [s])
+    off, shp = [0, 0, 0], [8, 16, 23]
+    full = file_reads(meta, paths, off, shp)
+    isz = 16 * (2 * 2 * 3) + 4
+    with open(paths[0], "wb") as f:  # the payload loses its last 3000 bytes, the index stays
+        f.write(s[:-3000 - isz] + s[-isz:] if loc == A.ZH_INDEX_END else s[:-3000])
+    cut = file_reads(meta, paths, off, shp)
+    assert cut[0][2] == full[0][2] == isz and cut[1:] == full[1:]
+    os.truncate(paths[0], 20)
+    got = file_reads(meta, paths, off, shp)
+    if loc == A.ZH_INDEX_START:
+        assert got[0] == (0, 0, isz)
+    else:
+        assert got == [(0, 0, 20)]  # what the file holds: the planner reports it short
 
 
 def test_unsharded_whole_objects_and_errors(tmp_path):
@@ -133,11 +161,35 @@ def test_unsharded_whole_objects_and_errors(tmp_path):
     with pytest.raises(ZhError) as e:
         file_reads(meta, paths[:-1], [0, 0, 0], shape)
     assert e.value.status == A.ZH_EINVAL
-    if os.geteuid() != 0:
+    if os.geteuid() != 0:  # unreadable: exists (a regular file), the read itself fails
         os.chmod(paths[0], 0)
         try:
-            with pytest.raises(ZhError) as e:
-                file_reads(meta, paths, [0, 0, 0], shape)
-            assert e.value.status == A.ZH_EIO
+            assert file_reads(meta, paths, [0, 0, 0], shape)[0] == (0, 0, len(chunks[0]))
         finally:
             os.chmod(paths[0], 0o600)
+
+
+def test_shard_unreadable_index_is_store_exception(tmp_path):
+    """A shard file that exists but cannot be opened: the index read fails with
+    StoreException.readFailed's text (StoreException.java:17-21), naming the store and the key
+    below its directory.  (Root reads files regardless of their mode: a directory entry that
+    cannot be opened for reading stands in — a FIFO would block, so a dangling permission
+    is simulated with a file in a directory without search permission only for non-root.)"""
+    shape = [8, 16, 24]
+    meta = A.make_meta(shape, [8, 16, 24], 4, sharded=True, inner_chunk_shape=[4, 8, 8])
+    s = encode_oracle(meta, rand_array(shape, 4, seed=13))[0]
+    d = tmp_path / "store" / "c" / "0"
+    d.mkdir(parents=True)
+    p = d / "0"
+    p.write_bytes(s)
+    if os.geteuid() == 0:
+        pytest.skip("root reads files regardless of their mode")
+    os.chmod(p, 0)
+    try:
+        with pytest.raises(ZhError) as e:
+            file_reads(meta, [str(p)], [0, 0, 0], shape, store=str(tmp_path / "store"))
+        assert e.value.status == A.ZH_EIO
+        assert str(e.value) == (f"Failed to read from store 'file://{tmp_path}/store' at key "
+                                f"'c/0/0/0': {p}")
+    finally:
+        os.chmod(p, 0o600)

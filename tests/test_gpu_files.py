@@ -1,11 +1,14 @@
 """Region reads straight from a FilesystemStore's files (zh_array_read_files).
 
 Reference: core.Array.read over a FilesystemStore (M/core/Array.java:378-441) —
-`exists` per chunk key (a regular file, FilesystemStore.java:43-46), `get(keys)` for a whole
-chunk (:49-58), and for a shard the StoreHandleDataProvider reads (ShardingIndexedCodec.java:
-333-357): the index by a prefix / suffix read, one range per referenced inner chunk.  Here the
-library does those reads (pread straight into the pipelined read's page-locked ring); every case
-is compared bit-exactly with the oracle (oracle/zh_oracle.c) on the same stored bytes."""
+`exists` per chunk key (a regular file, FilesystemStore.java:42-45), `get(keys)` for a whole
+chunk (:47-57), and for a part of a shard the StoreHandleDataProvider reads
+(ShardingIndexedCodec.java:333-357): the index by a prefix / suffix read, one range per
+referenced inner chunk, each a get(keys, start, end) that returns end - start bytes, zeros past
+the end of the file (:84-102).  Here the library does those reads (pread straight into the
+pipelined read's page-locked ring); every case is compared bit-exactly with the oracle
+(oracle/zh_oracle.c) on the same stored bytes, read from the same files
+(oracle.array_read_store) where the store semantics matter."""
 import os
 import stat
 
@@ -36,10 +39,16 @@ def mode(request, monkeypatch):
     return request.param
 
 
-def files_read(dev, meta, paths, off, shp, flags=0):
+def files_read(dev, meta, paths, off, shp, flags=0, store=None):
     out = np.empty(shp, NP_DT[meta.dtype_size])
-    dev.array_read_files(meta, paths, off, shp, out.ctypes.data, flags)
+    dev.array_read_files(meta, paths, off, shp, out.ctypes.data, flags, store=store)
     return out
+
+
+def store_read(meta, paths, off, shp):
+    """The oracle's core.Array.read over the same files (zo_array_read_store)."""
+    return np.frombuffer(O.array_read_store(meta, paths, off, shp),
+                         NP_DT[meta.dtype_size]).reshape(shp)
 
 
 @pytest.mark.parametrize("chain", list(CHAINS))
@@ -130,11 +139,13 @@ def test_files_one_plan_batches(dev, tmp_path, monkeypatch, pin):
 
 
 def test_files_shrinking_file_mid_read(dev, tmp_path, monkeypatch):
-    """A shard file cut short by someone else while the pipelined read is under way: the read
-    either completes (the cut came after the last pread), reports what the reference reports
-    for the shorter file (the cut came before the file's size was taken), or fails with the store
-    error of a pread that hit the end (ZH_EIO, "unexpected end of file") — never a hang or a
-    crash — and the context reads correctly afterwards (the aborted lanes left it clean)."""
+    """A whole-shard read whose file is cut short by someone else while the pipelined read is
+    under way (the reference would read the file in one readAllBytes): the read either
+    completes (the cut came after the last pread), reports what the reference reports for the
+    shorter file (the cut came before the file's size was taken), or fails with the store
+    error of a pread that hit the end (ZH_EIO, readFailed "unexpected end of file") — never a
+    hang, a crash or a silently zero-padded whole shard — and the context reads correctly
+    afterwards (the aborted lanes left it clean)."""
     import threading
     import time
     monkeypatch.setenv("ZH_PIPE_MIN_KB", "1")
@@ -153,13 +164,14 @@ def test_files_shrinking_file_mid_read(dev, tmp_path, monkeypatch):
         cut = threading.Timer(delay, lambda: os.truncate(p, len(shard) // 2))
         cut.start()
         try:
-            got = files_read(dev, meta, [str(p)], [0] * 4, shape)
+            got = files_read(dev, meta, [str(p)], [0] * 4, shape, store=tmp_path)
             np.testing.assert_array_equal(got, arr)
             seen.add("complete")
         except ZhError as e:
             msg = str(e)
             if e.status == A.ZH_EIO:
-                assert msg == f"Failed to read from store at '{p}': unexpected end of file", msg
+                assert msg == (f"Failed to read from store 'file://{tmp_path}' at key 's': "
+                               "unexpected end of file"), msg
                 seen.add("eio")
             else:  # the size was taken after the cut: entries past the end, or the index
                 # read from the middle of the old payload
@@ -208,22 +220,77 @@ def test_files_corrupt_index_reports_device_crc(dev, tmp_path, mode, where):
         assert str(ed.value).startswith("The checksum of the sharding index is invalid.")
 
 
-def test_files_truncated_shard(dev, tmp_path):
-    """A shard file cut short: entries beyond its end are never read and report the
-    reference's "Could not load byte data for chunk [...]" (ShardingIndexedCodec.java:
-    226-230); a file shorter than its index reports that."""
+def test_files_truncated_whole_shard(dev, tmp_path):
+    """A whole shard read from a file cut short: the reference reads the file in one piece and
+    slices it (decodePartial → chunkHandle.read(), ShardingIndexedCodec.java:246-251), which
+    throws for an entry beyond its bytes (IllegalArgumentException).  Here that is the
+    oracle's and the device's "Could not load byte data for chunk [...]", and a file shorter
+    than its index "... is smaller than its index" (the error's class and
+    text differ from the reference's, that it is an error does not)."""
     meta, arr, shards = make_case("start_beindex", seed=61, fill_frac=0.0)
     paths = write_store(tmp_path, meta, shards)
     full = os.path.getsize(paths[0])
     os.truncate(paths[0], full - 100)  # the last inner chunk's payload loses 100 bytes
     off, shp = [0, 0, 0], [8, 16, 24]
+    with pytest.raises(O.OracleError) as eo:
+        store_read(meta, region_paths(meta, paths, off, shp), off, shp)
     with pytest.raises(ZhError) as ed:
         files_read(dev, meta, region_paths(meta, paths, off, shp), off, shp)
+    assert str(ed.value) == str(eo.value)
     assert str(ed.value).startswith("Could not load byte data for chunk [")
     os.truncate(paths[0], 10)
     with pytest.raises(ZhError) as ed:
         files_read(dev, meta, region_paths(meta, paths, off, shp), off, shp)
     assert "is smaller than its index" in str(ed.value)
+
+
+@pytest.mark.parametrize("chain", ["sharded", "start_beindex", "transpose_be", "chunk_crc"])
+def test_files_truncated_part_reads_zeros(dev, tmp_path, mode, chain):
+    """A part of a shard whose file was cut short: each range read is
+    FilesystemStore.get(keys, start, end) (FilesystemStore.java:84-102), a buffer of the
+    entry's length holding what the file has and zeros after its end, so the part decodes
+    (where the chunk codecs accept those bytes) — equal to the oracle reading the same files.
+    With a chunk crc32c the zeros fail the chunk's check with the reference's message."""
+    meta, arr, shards = make_case(chain, seed=163, fill_frac=0.0)
+    paths = write_store(tmp_path, meta, shards)
+    p = paths[0]
+    whole = open(p, "rb").read()
+    isz = 16 * (2 * 2 * 3) + 4
+    end_idx = meta.chain.index_location == A.ZH_INDEX_END
+    for cut in (100, 3000):
+        open(p, "wb").write(whole[:-cut - isz] + whole[-isz:] if end_idx else whole[:-cut])
+        for off, shp in (([0, 0, 0], [8, 16, 23]), ([4, 8, 16], [4, 8, 8]), ([1, 3, 5], [6, 9, 17])):
+            rp = region_paths(meta, paths, off, shp)
+            try:
+                want = store_read(meta, rp, off, shp)
+            except O.OracleError as eo:
+                with pytest.raises(ZhError) as ed:
+                    files_read(dev, meta, rp, off, shp)
+                if chain == "chunk_crc":  # several chunks fail: the device names any of them
+                    pre = "The checksum of the sharding index is invalid. Stored: "
+                    assert str(ed.value).startswith(pre) and str(eo.value).startswith(pre)
+                else:
+                    assert str(ed.value) == str(eo.value), (cut, off)
+                continue
+            np.testing.assert_array_equal(files_read(dev, meta, rp, off, shp), want,
+                                          err_msg=f"cut {cut} region {off} {shp}")
+
+
+def test_files_short_prefix_index_of_a_part(dev, tmp_path):
+    """index_location start, a part of a file shorter than its index: the prefix read returns
+    the file's bytes zero-padded to the index's length (get(keys, 0, n)), whose crc32c fails
+    with the reference's message — the oracle's text, read from the same file."""
+    meta, arr, shards = make_case("start_beindex", seed=167, fill_frac=0.0)
+    paths = write_store(tmp_path, meta, shards)
+    os.truncate(paths[0], 37)
+    off, shp = [1, 3, 5], [6, 9, 17]
+    rp = region_paths(meta, paths, off, shp)
+    with pytest.raises(O.OracleError) as eo:
+        store_read(meta, rp, off, shp)
+    with pytest.raises(ZhError) as ed:
+        files_read(dev, meta, rp, off, shp)
+    assert str(ed.value) == str(eo.value)
+    assert str(ed.value).startswith("The checksum of the sharding index is invalid. Stored: 0 ")
 
 
 @pytest.mark.skipif(os.geteuid() == 0, reason="root reads files regardless of their mode")
@@ -235,9 +302,14 @@ def test_files_unreadable_is_store_exception(dev, tmp_path):
     try:
         off, shp = [0, 0, 0], [8, 16, 24]
         with pytest.raises(ZhError) as ed:
-            files_read(dev, meta, region_paths(meta, paths, off, shp), off, shp)
+            files_read(dev, meta, region_paths(meta, paths, off, shp), off, shp,
+                       store=tmp_path)
         assert ed.value.status == A.ZH_EIO
-        assert str(ed.value).startswith(f"Failed to read from store at '{paths[0]}': ")
+        # StoreException.readFailed (StoreException.java:17-21): the store, the key below it,
+        # and the cause's text (an AccessDeniedException carries the file)
+        key = os.path.relpath(paths[0], tmp_path)
+        assert str(ed.value) == (f"Failed to read from store 'file://{tmp_path}' at key "
+                                 f"'{key}': {paths[0]}")
     finally:
         os.chmod(paths[0], stat.S_IRUSR | stat.S_IWUSR)
 
@@ -569,9 +641,53 @@ def test_write_files_device_source_and_errors(dev, tmp_path):
     blocker.write_bytes(b"x")
     bad = [str(blocker / "c" / str(i)) for i in range(len(paths))]
     with pytest.raises(ZhError) as ed:
-        dev.array_write_files(meta, arr.ctypes.data, [0, 0, 0], shape, bad)
+        dev.array_write_files(meta, arr.ctypes.data, [0, 0, 0], shape, bad, store=tmp_path)
     assert ed.value.status == A.ZH_EIO
-    assert str(ed.value).startswith(f"Failed to write to store at '{bad[0]}': ")
+    # StoreException.writeFailed with FilesystemStore.set's cause (FilesystemStore.java:107-115)
+    assert str(ed.value) == (f"Failed to write to store 'file://{tmp_path}' at key "
+                             f"'blocker/c/0': Failed to create parent directories for path: "
+                             f"{blocker}/c")
+
+
+def _nofile_headroom(extra):
+    """Lower this process's RLIMIT_NOFILE soft limit to the descriptors open now + extra; returns
+    the old limits (restore them with resource.setrlimit)."""
+    import resource
+    old = resource.getrlimit(resource.RLIMIT_NOFILE)
+    used = len(os.listdir("/proc/self/fd"))
+    resource.setrlimit(resource.RLIMIT_NOFILE, (used + extra, old[1]))
+    return old
+
+
+def test_files_read_more_chunks_than_descriptors(dev, tmp_path, mode):
+    """A region of more chunk files than the process may open at once (RLIMIT_NOFILE lowered
+    to 24 beyond what is open): the reference opens one file per get(); the library keeps at
+    most a bounded number of descriptors (closing idle ones, reopening by path), so the read
+    completes and equals the oracle's."""
+    import resource
+    shape = [40, 40, 40]
+    meta = A.make_meta(shape, [4, 4, 8], 4, endian=A.ZH_ENDIAN_BIG)  # 10*10*5 = 500 files
+    arr = rand_array(shape, 4, seed=171)
+    chunks = encode_oracle(meta, arr)
+    paths = write_store(tmp_path, meta, chunks)
+    off, shp = [0, 0, 0], shape
+    old = _nofile_headroom(24)
+    try:
+        got = files_read(dev, meta, region_paths(meta, paths, off, shp), off, shp)
+    finally:
+        resource.setrlimit(resource.RLIMIT_NOFILE, old)
+    np.testing.assert_array_equal(got, arr)
+    # sharded parts too: 500 shards, each read as index + ranges
+    meta = A.make_meta(shape, [4, 4, 8], 4, sharded=True, inner_chunk_shape=[2, 2, 4])
+    shards = encode_oracle(meta, arr)
+    paths = write_store(tmp_path, meta, shards, tag="s")
+    off, shp = [1, 1, 1], [38, 38, 38]
+    old = _nofile_headroom(24)
+    try:
+        got = files_read(dev, meta, region_paths(meta, paths, off, shp), off, shp)
+    finally:
+        resource.setrlimit(resource.RLIMIT_NOFILE, old)
+    np.testing.assert_array_equal(got, arr[1:39, 1:39, 1:39])
 
 
 def test_array_write_goes_through_files(dev, tmp_path, monkeypatch):
@@ -601,3 +717,62 @@ def test_array_write_goes_through_files(dev, tmp_path, monkeypatch):
     assert n_lib == n_mir
     np.testing.assert_array_equal(z.Array.open(z.FilesystemStore(tmp_path / "lib").resolve("a"))
                                   .read(), data)
+
+
+def _tmp_leftovers(root):
+    return [os.path.join(d, f) for d, _, fs in os.walk(root) for f in fs if ".zhtmp" in f]
+
+
+def test_write_files_more_chunks_than_descriptors(dev, tmp_path, wmode):
+    """More chunk files than the process may open at once (RLIMIT_NOFILE lowered to 24 beyond
+    what is open): the reference opens, writes and closes one file per set(); the library keeps
+    at most 3 files per lane open, so the write completes with the oracle's bytes and leaves
+    no temporary files."""
+    import resource
+    shape = [40, 40, 48]
+    meta = A.make_meta(shape, [4, 4, 8], 4, **WCHAINS["sharded_t"] | dict(
+        inner_chunk_shape=[2, 2, 4]))  # 10*10*6 = 600 chunk files
+    arr = rand_array(shape, 4, seed=173, fill_frac=0.0)
+    want = encode_oracle(meta, arr)
+    coords = chunk_coords(meta, [0, 0, 0], shape)
+    paths = [str(tmp_path / "n" / "c" / "/".join(map(str, c))) for c in coords]
+    old = _nofile_headroom(24)
+    try:
+        dev.array_write_files(meta, arr.ctypes.data, [0, 0, 0], shape, paths)
+    finally:
+        resource.setrlimit(resource.RLIMIT_NOFILE, old)
+    assert [open(p, "rb").read() for p in paths] == want
+    assert not _tmp_leftovers(tmp_path)
+
+
+def test_write_files_failure_leaves_unfinished_chunks_intact(dev, tmp_path, wmode):
+    """A write that fails part-way (one chunk's path is a directory, so its file cannot be put
+    in place): the call raises StoreException.writeFailed's text for that chunk; every other
+    chunk file holds either its old bytes or its new bytes, whole — a chunk the failure did not
+    let finish is never truncated or half-written (each chunk goes to a temporary file renamed
+    over the old one once complete) — and no temporary file is left behind."""
+    shape = [24, 32, 48]
+    meta = A.make_meta(shape, [8, 16, 24], 4, **WCHAINS["sharded_t"])
+    old_arr = rand_array(shape, 4, seed=179, fill_frac=0.0)
+    new_arr = rand_array(shape, 4, seed=181, fill_frac=0.0)
+    old_enc, new_enc = encode_oracle(meta, old_arr), encode_oracle(meta, new_arr)
+    coords = chunk_coords(meta, [0, 0, 0], shape)
+    paths = [str(tmp_path / "f" / "c" / "/".join(map(str, c))) for c in coords]
+    dev.array_write_files(meta, old_arr.ctypes.data, [0, 0, 0], shape, paths)
+    k = len(paths) // 2
+    os.remove(paths[k])
+    os.makedirs(os.path.join(paths[k], "x"))  # a non-empty directory at the chunk's key
+    with pytest.raises(ZhError) as ed:
+        dev.array_write_files(meta, new_arr.ctypes.data, [0, 0, 0], shape, paths,
+                              store=tmp_path / "f")
+    assert ed.value.status == A.ZH_EIO
+    key = "c/" + "/".join(map(str, coords[k]))
+    assert str(ed.value) == (f"Failed to write to store 'file://{tmp_path}/f' at key '{key}': "
+                             f"Failed to write {len(new_enc[k])} bytes to file: {paths[k]}")
+    for i, p in enumerate(paths):
+        if i == k:
+            assert os.path.isdir(p)
+            continue
+        b = open(p, "rb").read()
+        assert b in (old_enc[i], new_enc[i]), (i, len(b))
+    assert not _tmp_leftovers(tmp_path)

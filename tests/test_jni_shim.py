@@ -314,9 +314,13 @@ def test_array_read_files_errors_via_shim(dev, tmp_path):
         os.chmod(paths[0], 0)
         try:
             with pytest.raises(JavaException) as ej:
-                jvm.array_read_files(dev.h.value, meta, [paths[0]], off, shp)
+                jvm.array_read_files(dev.h.value, meta, [paths[0]], off, shp,
+                                     store=(str(tmp_path), f"file://{tmp_path}"))
             assert ej.value.cls == "dev/zarr/zarrjava/store/StoreException"
-            assert ej.value.msg.startswith("Failed to read from store at ")
+            key = os.path.relpath(paths[0], tmp_path)
+            # StoreException.readFailed (StoreException.java:17-21): store, key, cause
+            assert ej.value.msg == (f"Failed to read from store 'file://{tmp_path}' at key "
+                                    f"'{key}': {paths[0]}")
         finally:
             os.chmod(paths[0], 0o600)
     jvm.check_rules()
@@ -463,9 +467,15 @@ def test_array_write_files_store_error_via_shim(dev, tmp_path):
     paths = [str(blocker / "c" / "/".join(map(str, c))) for c in coords]
     jvm = FakeJVM()
     with pytest.raises(JavaException) as ej:
-        jvm.array_write_files(dev.h.value, meta, arr, [0, 0, 0], paths)
+        jvm.array_write_files(dev.h.value, meta, arr, [0, 0, 0], paths,
+                              store=(str(tmp_path), "file://" + str(tmp_path)))
     assert ej.value.cls == "dev/zarr/zarrjava/store/StoreException"
-    assert ej.value.msg.startswith(f"Failed to write to store at '{paths[0]}': ")
+    # StoreException.writeFailed with FilesystemStore.set's cause (FilesystemStore.java:
+    # 107-115): the parent directory that could not be created
+    key = os.path.relpath(paths[0], tmp_path)
+    assert ej.value.msg == (f"Failed to write to store 'file://{tmp_path}' at key '{key}': "
+                            "Failed to create parent directories for path: "
+                            f"{os.path.dirname(paths[0])}")
     jvm.check_rules()
 
 

@@ -53,17 +53,64 @@ def test_store_read_equals_memory_read(tmp_path, sharded, order, loc):
     np.testing.assert_array_equal(full[keep], arr[keep])
 
 
-def test_store_read_truncated_shard_raises(tmp_path):
+def _one_shard(tmp_path, loc, crc=True, seed=3):
     shape = [1, 16, 16, 16]
     meta = A.make_meta(shape, [1, 16, 16, 16], 4, endian=A.ZH_ENDIAN_LITTLE, sharded=True,
-                       inner_chunk_shape=[1, 8, 8, 8], index_location=A.ZH_INDEX_START)
-    shards = encode_oracle(meta, rand_array(shape, 4, seed=3))
-    _, paths = _store(tmp_path, meta, shards)
-    p = paths[(0, 0, 0, 0)]
-    b = open(p, "rb").read()
-    # cut 10 bytes off the last inner chunk's payload (index at the start stays intact), so
-    # that chunk's range ends past the file → "Could not load byte data" (an
-    # out-of-range entry raises the reference's chunk message)
-    open(p, "wb").write(b[:-10])
+                       inner_chunk_shape=[1, 8, 8, 8], index_location=loc, index_crc32c=crc)
+    shard = encode_oracle(meta, rand_array(shape, 4, seed=seed))[0]
+    _, paths = _store(tmp_path, meta, [shard])
+    return meta, shard, paths[(0, 0, 0, 0)]
+
+
+@pytest.mark.parametrize("loc", [A.ZH_INDEX_START, A.ZH_INDEX_END])
+def test_store_part_of_truncated_shard_reads_zeros(tmp_path, loc):
+    """FilesystemStore.get(keys, start, end) (FilesystemStore.java:84-102) allocates end - start
+    bytes and reads what the file holds: a part whose inner chunk lost its tail decodes what
+    the file has at the entry's offsets and zeros past its end — the in-memory read of a shard
+    whose payload region holds exactly that — and a range entirely past the end reads all
+    zeros."""
+    meta, shard, p = _one_shard(tmp_path, loc)
+    isz = 16 * 8 + 4
+    payload_end = len(shard) if loc == A.ZH_INDEX_START else len(shard) - isz
+    for cut in (10, 2048 + 100):  # into the last chunk; the last chunk gone and more
+        keep = payload_end - cut
+        stored = shard[:keep] + (shard[payload_end:] if loc == A.ZH_INDEX_END else b"")
+        open(p, "wb").write(stored)
+        # what each range read returns: the file's bytes at the entry's offsets (with the
+        # index at the end, the moved index where the payload was), zeros past the end
+        padded = (stored + bytes(payload_end))[:payload_end] + \
+            (shard[payload_end:] if loc == A.ZH_INDEX_END else b"")
+        for off, shp in (([0, 0, 0, 0], [1, 16, 16, 15]), ([0, 8, 8, 8], [1, 8, 8, 8]),
+                         ([0, 3, 9, 9], [1, 13, 7, 6])):
+            want = O.array_read(meta, [padded], off, shp)
+            assert O.array_read_store(meta, [p], off, shp) == want, (cut, off)
+
+
+def test_store_whole_truncated_shard_raises(tmp_path):
+    """The whole shard is read in one piece (decodePartial → chunkHandle.read(),
+    ShardingIndexedCodec.java:246-251) and sliced: an entry beyond the bytes cannot be served
+    (the reference's ByteBuffer slice throws IllegalArgumentException; reported as "Could not
+    load byte data")."""
+    meta, shard, p = _one_shard(tmp_path, A.ZH_INDEX_START)
+    open(p, "wb").write(shard[:-10])
     with pytest.raises(O.OracleError, match=r"Could not load byte data for chunk \[0, 1, 1, 1\]"):
-        O.array_read_store(meta, [p], [0, 0, 0, 0], [1, 16, 16, 15])
+        O.array_read_store(meta, [p], [0, 0, 0, 0], [1, 16, 16, 16])
+
+
+def test_store_short_index_reads(tmp_path):
+    """A file shorter than its index: a suffix read (index_location end, get(keys, -n)) resolves
+    to a negative position, which the reference's channel rejects — an error; a prefix read
+    (start, get(keys, 0, n)) returns the file's bytes zero-padded to the index's length, whose
+    crc32c then fails with the reference's message (stored 0)."""
+    meta, shard, p = _one_shard(tmp_path, A.ZH_INDEX_END)
+    open(p, "wb").write(shard[:50])
+    with pytest.raises(O.OracleError, match="is smaller than its index"):
+        O.array_read_store(meta, [p], [0, 0, 0, 0], [1, 8, 8, 8])
+    meta, shard, p = _one_shard(tmp_path, A.ZH_INDEX_START)
+    open(p, "wb").write(shard[:50])
+    want_crc = O.crc32c(shard[:50] + bytes(16 * 8 - 50))
+    want_crc = want_crc - (1 << 32) if want_crc >= 1 << 31 else want_crc
+    with pytest.raises(O.OracleError) as e:
+        O.array_read_store(meta, [p], [0, 0, 0, 0], [1, 8, 8, 8])
+    assert str(e.value) == ("The checksum of the sharding index is invalid. Stored: 0 "
+                            f"Computed: {want_crc}")

@@ -67,16 +67,74 @@ constexpr size_t kUploadSlotBytes = 64 << 10;
 
 namespace zh {
 
+[[noreturn]] void src_ref_misuse(const char* what);
+
+// Where the bytes of a source range are: memory (a host address, or a device address under
+// ZH_SRC_DEVICE), or byte `offset` of a store file open for the read (zh_array_read_files:
+// `slot` in zh_files.cpp's file table).  The planner lays both out alike (offsets add,
+// adjacent ranges merge); only memory can be dereferenced or DMA'd, and mem() is the one way
+// to the address: it refuses a file source, so no host-pointer use can receive one.
+class SrcRef {
+ public:
+  SrcRef() = default;
+  static SrcRef memory(const void* p) {
+    SrcRef r;
+    r.p_ = (const uint8_t*)p;
+    return r;
+  }
+  static SrcRef file(int32_t slot, int64_t offset) {
+    SrcRef r;
+    r.slot_ = slot;
+    r.off_ = offset;
+    return r;
+  }
+  bool is_file() const { return slot_ >= 0; }
+  bool empty() const { return slot_ < 0 && p_ == nullptr; }
+  const uint8_t* mem() const {
+    if (slot_ >= 0) src_ref_misuse("a store file range used as memory");
+    return p_;
+  }
+  int32_t slot() const {
+    if (slot_ < 0) src_ref_misuse("memory used as a store file range");
+    return slot_;
+  }
+  int64_t file_offset() const { return off_; }
+  SrcRef operator+(int64_t d) const {
+    SrcRef r = *this;
+    if (slot_ >= 0) r.off_ += d;
+    else r.p_ += d;
+    return r;
+  }
+  // this range starts where `prev` (prev_len bytes) ends, in the same memory or file
+  bool follows(const SrcRef& prev, int64_t prev_len) const {
+    if (slot_ != prev.slot_) return false;
+    return slot_ >= 0 ? off_ == prev.off_ + prev_len : p_ == prev.p_ + prev_len;
+  }
+
+ private:
+  const uint8_t* p_ = nullptr;
+  int32_t slot_ = -1;
+  int64_t off_ = 0;
+};
+
+// One held byte range of a stored shard (zh_shard_piece with a typed source).
+struct Piece {
+  int64_t offset = 0, nbytes = 0;
+  SrcRef data;
+  int64_t data_nbytes = 0;
+};
+
 // One stored chunk / shard as the planner takes it: a whole object (data, nbytes), or a
-// sub-shard form (the stored index + the byte ranges held, zh_shard_src); data == nullptr and
-// index == nullptr: the key is missing.
+// sub-shard form (the stored index + the byte ranges held, zh_shard_src); data empty and
+// index == nullptr: the key is missing.  The index is always memory; pieces point into
+// storage the entry point owns for the call.
 struct SrcDesc {
-  const uint8_t* data = nullptr;
+  SrcRef data;
   int64_t nbytes = 0;
   const uint8_t* index = nullptr;
   int64_t index_nbytes = 0;
   int64_t shard_nbytes = -1;
-  const zh_shard_piece* pieces = nullptr;
+  const Piece* pieces = nullptr;
   int64_t npieces = 0;
 };
 
@@ -105,7 +163,7 @@ struct zh_plan {
   int64_t n_crc_jobs = 0, n_crc_spans = 0;
   int crc_shift = 0;            // index-CRC span = kIdxSpan << crc_shift
   uint8_t* d_input = nullptr;   // staged host sources
-  std::vector<std::pair<int64_t, const void*>> h2d;  // (offset in d_input, host ptr)
+  std::vector<std::pair<int64_t, zh::SrcRef>> h2d;  // (offset in d_input, host source)
   std::vector<int64_t> h2d_len;
   std::vector<std::unique_ptr<uint8_t[]>> h2d_keep;  // file bytes read for its own h2d copies
   bool external_h2d = false;    // the pipelined read does the h2d copies (plan_enqueue skips)
@@ -158,10 +216,11 @@ int plan_create(zh_ctx* ctx, const zh_array_meta* m, const SrcDesc* srcs, int64_
 void plan_free(zh_plan* p);
 
 // The byte ranges of one stored shard a part [part_lo, part_hi) needs (zh_shard_ranges):
-// (offset, nbytes) pairs sorted by offset, adjacent runs merged up to max_run bytes.
+// (offset, nbytes) pairs sorted by offset, adjacent runs merged up to max_run bytes; entries
+// longer than max_entry bytes are left out.
 int shard_ranges(const zh_array_meta* m, const uint8_t* index, int64_t shard_nbytes,
                  const int64_t* part_lo, const int64_t* part_hi, int64_t max_run,
-                 std::vector<std::pair<int64_t, int64_t>>& out);
+                 std::vector<std::pair<int64_t, int64_t>>& out, int64_t max_entry = INT64_MAX);
 
 // Region read over generic sources: the pipelined path for large host reads (zh_pipeline.cpp),
 // else one plan.  Caller holds ctx->mu.
@@ -194,35 +253,26 @@ int plan_mark_done_impl(zh_plan* p, hipStream_t s);
 int projection(int n, const int64_t* cc, const int64_t* ashape, const int32_t* chunk,
                const int64_t* soff, const int64_t* sshape, int32_t* co, int32_t* oo, int32_t* ps);
 
-// File addresses (zh_array_read_files): a source byte that lives at byte `off` of the store
-// file registered in `slot` of the process-wide file table (zh_files.cpp) is named by
-// kFileTag | slot << kFileOffBits | off, a value no host pointer takes (bit 62 set: not a
-// canonical x86-64 user address).  The planner treats it as an opaque host pointer (offsets
-// add, adjacent ranges merge); the pipelined read's in lanes read it with pread straight into
-// their ring slots, and plan_create reads the file bytes of a plan that stages its own copies
-// (not pipelined) into host buffers the plan keeps.  off < 2^40, slot < 2^22.
-constexpr uint64_t kFileTag = 1ull << 62;
-constexpr int kFileOffBits = 40;
-constexpr int64_t kFileMaxBytes = (int64_t)1 << kFileOffBits;
-constexpr int64_t kFileMaxSlots = (int64_t)1 << (62 - kFileOffBits);
+// Store files of a read (zh_array_read_files, zh_files.cpp).  A process-wide table holds, per
+// file of the reads in flight, its path, the store and key its errors name, and — while a read
+// needs it — an open descriptor: at most kFileMaxOpen are open at once (a read of thousands of
+// chunk files stays under the process's descriptor limit; a closed one is reopened by path when
+// its next range is read).  Sources name file bytes as SrcRef::file(slot, offset).
+constexpr int kFileMaxOpen = 64;
 // the largest extent a one-plan file read stages in zh_ctx::file_pin
 constexpr int64_t kFilePinMax = (int64_t)256 << 20;
-inline bool is_file_addr(const void* p) { return ((uint64_t)(uintptr_t)p & kFileTag) != 0; }
-inline const uint8_t* file_addr(int64_t slot, int64_t off) {
-  return (const uint8_t*)(uintptr_t)(kFileTag | ((uint64_t)slot << kFileOffBits) | (uint64_t)off);
-}
-// Reads n bytes named by the file address src into dst (pread, retried on EINTR / short
-// reads).  Returns "" or the failure's message (the path and the reason).
-std::string file_fetch(void* dst, const void* src, int64_t n);
-// file_fetch of every (dst, src, n) in `reads`: the small reads a plan stages itself (a 64^3
-// region's index + 27 inner chunks) and the shards' indexes.  ZH_FILE_THREADS > 1 spreads them
-// in pieces of 512 KiB over a small pool of reader threads (default 1: on the GPU box 8 readers
-// made a 64^3 store read 2.2x slower, profiles/r04/q).  "" or the first failure's message.
+// Reads the n bytes at `src` (a file SrcRef) into dst: pread, retried on EINTR and short reads.
+// Bytes past the end of the file read as zeros, as FilesystemStore.get(keys, start, end)
+// returns a buffer of end - start bytes holding what the file has (M/store/FilesystemStore.java:
+// 84-102).  Returns "" or StoreException.readFailed's text (StoreException.java:17-21).
+std::string file_fetch(void* dst, const SrcRef& src, int64_t n);
 struct FileRead {
   void* dst;
-  const void* src;
+  SrcRef src;
   int64_t n;
 };
+// file_fetch of every read in order: the small reads a plan stages itself and the shards'
+// indexes.  "" or the first failure's message.
 std::string file_fetch_all(const std::vector<FileRead>& reads);
 
 }  // namespace zh

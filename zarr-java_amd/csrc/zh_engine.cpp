@@ -45,6 +45,13 @@ void set_err(char* err, size_t errlen, const char* fmt, ...) {
   va_end(ap);
 }
 
+// A SrcRef used as the wrong kind is a planner bug: stop before a store file offset is
+// dereferenced as an address (or an address read as a file).
+void src_ref_misuse(const char* what) {
+  fprintf(stderr, "zarrhip: internal error: %s\n", what);
+  abort();
+}
+
 #define ZH_HIP(call)                                                                       \
   do {                                                                                     \
     hipError_t e_ = (call);                                                                \
@@ -677,7 +684,7 @@ uint64_t ld_u64_host(const uint8_t* p, bool be) {
 // of the shard it needs (sub-shard reads), or the whole object.
 struct HeldPieces {
   const uint8_t* index = nullptr;       // the stored index (isz bytes), host or device
-  std::vector<zh_shard_piece> pieces;   // sorted, disjoint
+  std::vector<Piece> pieces;            // sorted, disjoint
 };
 
 // Host whole-shard sources, single-level sharding: StoreHandleDataProvider semantics
@@ -703,7 +710,8 @@ bool compact_pieces(const zh_array_meta* m, const DevShard& S, int64_t isz, Held
   if (10 * ref > 9 * S.nbytes) return false;
   hp.index = S.data + S.index_off;
   hp.pieces.clear();
-  for (auto& r : rs) hp.pieces.push_back({r.first, r.second, S.data + r.first, r.second});
+  for (auto& r : rs)
+    hp.pieces.push_back({r.first, r.second, SrcRef::memory(S.data + r.first), r.second});
   return true;
 }
 
@@ -726,9 +734,9 @@ int caller_pieces(const zh_array_meta* m, const SrcDesc& src, int64_t isz, const
   }
   std::vector<std::pair<int64_t, int64_t>> need;
   if (shard_ranges(m, hp.index, src.shard_nbytes, lo, hi, INT64_MAX, need) != ZH_OK) return ZH_OK;
-  std::vector<zh_shard_piece> kept;
+  std::vector<Piece> kept;
   size_t r = 0;
-  for (const zh_shard_piece& q : hp.pieces) {
+  for (const Piece& q : hp.pieces) {
     const int64_t qe = q.offset + q.nbytes;
     while (r < need.size() && need[r].first + need[r].second <= q.offset) r++;
     for (size_t k = r; k < need.size() && need[k].first < qe; k++) {
@@ -739,7 +747,7 @@ int caller_pieces(const zh_array_meta* m, const SrcDesc& src, int64_t isz, const
         kept.push_back(q);
         break;
       }
-      kept.push_back({a, b - a, (const uint8_t*)q.data + (a - q.offset), b - a});
+      kept.push_back({a, b - a, q.data + (a - q.offset), b - a});
     }
   }
   hp.pieces.swap(kept);
@@ -761,7 +769,7 @@ int caller_pieces_all(const zh_array_meta* m, const SrcDesc& src, int64_t isz, c
   hp.index = src.index + (m->chain.index_location == ZH_INDEX_START ? 0 : src.index_nbytes - isz);
   hp.pieces.assign(src.pieces, src.pieces + std::max<int64_t>(0, src.npieces));
   for (size_t k = 0; k < hp.pieces.size(); k++) {
-    const zh_shard_piece& q = hp.pieces[k];
+    const Piece& q = hp.pieces[k];
     // disjoint, except host-decoded pieces among themselves at distinct offsets: each serves
     // exactly the entry it was read for (piece_src), as the reference decodes each entry
     const bool dec = q.data_nbytes != q.nbytes;
@@ -770,7 +778,7 @@ int caller_pieces_all(const zh_array_meta* m, const SrcDesc& src, int64_t isz, c
         !(dec && hp.pieces[k - 1].data_nbytes != hp.pieces[k - 1].nbytes &&
           q.offset > hp.pieces[k - 1].offset);
     const bool bad = q.offset < 0 || q.nbytes < 0 || q.data_nbytes < 0 ||
-                     (q.data_nbytes > 0 && !q.data) || overlap ||
+                     (q.data_nbytes > 0 && q.data.empty()) || overlap ||
                      (k > 0 && q.offset < hp.pieces[k - 1].offset) || (dec && m->chain.nested);
     if (bad) {
       set_err(err, errlen,
@@ -956,7 +964,10 @@ int plan_create(zh_ctx* ctx, const zh_array_meta* m, const SrcDesc* srcs, int64_
               fmt_ints(cc, n).c_str());
       return fail(ZH_EINVAL);
     }
-    S.data = pieced ? src.index : src.data;
+    // a whole object in a store file has no address until it is staged (its bytes are read
+    // into host memory or the pipelined read's ring first)
+    const bool present = pieced || !src.data.empty();
+    S.data = pieced ? src.index : src.data.is_file() ? nullptr : src.data.mem();
     S.nbytes = pieced ? (src.shard_nbytes >= 0 ? src.shard_nbytes : INT64_MAX) : src.nbytes;
     S.item_begin = items;
     int64_t ob = 0, nit = 1;
@@ -977,7 +988,7 @@ int plan_create(zh_ctx* ctx, const zh_array_meta* m, const SrcDesc* srcs, int64_
     S.out_base = ob;
     S.l1_begin = l1_items;
     items += nit;
-    if (!S.data) continue;
+    if (!present) continue;
     if (pieced) {
       if ((st = caller_pieces(m, src, isz, cc, S, src_dev, held[i], err, errlen)) != ZH_OK) return fail(st);
       is_held[i] = 1;
@@ -1023,7 +1034,8 @@ int plan_create(zh_ctx* ctx, const zh_array_meta* m, const SrcDesc* srcs, int64_
     if (src_dev) continue;  // device sources are read where they are
     // host sources: a whole object is staged as it is, unless the part references little
     // of a single-level shard (then its index + the referenced ranges, as a caller's pieces)
-    if (!is_held[i] && c.sharded && !nested && compact_pieces(m, S, isz, held[i])) {
+    if (!is_held[i] && c.sharded && !nested && !src.data.is_file() &&
+        compact_pieces(m, S, isz, held[i])) {
       is_held[i] = 1;
       S.index_off = 0;  // the staging block starts with the stored index
     }
@@ -1035,7 +1047,7 @@ int plan_create(zh_ctx* ctx, const zh_array_meta* m, const SrcDesc* srcs, int64_
     // staging block: [index][pieces], each raw piece at its shard offset's residue mod 256
     // (the payload alignment the fast kernels see is the stored one)
     int64_t pos = isz;
-    for (const zh_shard_piece& q : held[i].pieces) {
+    for (const Piece& q : held[i].pieces) {
       pos = ((pos + 255) & ~(int64_t)255) + (q.data_nbytes == q.nbytes ? (q.offset & 255) : 0);
       piece_dst[i].push_back(pos);
       pos += q.data_nbytes;
@@ -1053,7 +1065,7 @@ int plan_create(zh_ctx* ctx, const zh_array_meta* m, const SrcDesc* srcs, int64_
     for (int64_t i = 0; i < ncoords; i++) {
       if (stage_off[i] < 0) continue;
       if (is_held[i]) {
-        p->h2d.push_back({stage_off[i], held[i].index});
+        p->h2d.push_back({stage_off[i], SrcRef::memory(held[i].index)});
         p->h2d_len.push_back(isz);
         const auto& pv = held[i].pieces;
         for (size_t k = 0; k < pv.size(); k++) {
@@ -1062,7 +1074,7 @@ int plan_create(zh_ctx* ctx, const zh_array_meta* m, const SrcDesc* srcs, int64_
           p->h2d_len.push_back(pv[k].data_nbytes);
         }
       } else {
-        p->h2d.push_back({stage_off[i], hs[i].data});
+        p->h2d.push_back({stage_off[i], srcs[i].data});
         p->h2d_len.push_back(hs[i].nbytes);
       }
       hs[i].data = p->d_input + stage_off[i];
@@ -1073,8 +1085,7 @@ int plan_create(zh_ctx* ctx, const zh_array_meta* m, const SrcDesc* srcs, int64_
     size_t w = 0;
     for (size_t k = 0; k < p->h2d.size(); k++) {
       if (w > 0 && p->h2d[w - 1].first + p->h2d_len[w - 1] == p->h2d[k].first &&
-          (const uint8_t*)p->h2d[w - 1].second + p->h2d_len[w - 1] ==
-              (const uint8_t*)p->h2d[k].second) {
+          p->h2d[k].second.follows(p->h2d[w - 1].second, p->h2d_len[w - 1])) {
         p->h2d_len[w - 1] += p->h2d_len[k];
         continue;
       }
@@ -1094,7 +1105,7 @@ int plan_create(zh_ctx* ctx, const zh_array_meta* m, const SrcDesc* srcs, int64_
     bool files = false;
     int64_t lo = INT64_MAX, hi = 0, sum = 0;
     for (size_t k = 0; !external_h2d && k < p->h2d.size(); k++) {
-      files = files || is_file_addr(p->h2d[k].second);
+      files = files || p->h2d[k].second.is_file();
       lo = std::min(lo, p->h2d[k].first);
       hi = std::max(hi, p->h2d[k].first + p->h2d_len[k]);
       sum += p->h2d_len[k];
@@ -1127,13 +1138,13 @@ int plan_create(zh_ctx* ctx, const zh_array_meta* m, const SrcDesc* srcs, int64_
       return ZH_OK;
     };
     for (size_t k = 0; files && k < p->h2d.size(); k++) {
-      const bool f = is_file_addr(p->h2d[k].second);
+      const bool f = p->h2d[k].second.is_file();
       if (pin) {
         uint8_t* dst = pin + (p->h2d[k].first - lo);
         if (f)
           freads.push_back({dst, p->h2d[k].second, p->h2d_len[k]});
         else
-          std::memcpy(dst, p->h2d[k].second, (size_t)p->h2d_len[k]);
+          std::memcpy(dst, p->h2d[k].second.mem(), (size_t)p->h2d_len[k]);
         b_lo = std::min(b_lo, p->h2d[k].first);
         b_hi = std::max(b_hi, p->h2d[k].first + p->h2d_len[k]);
         if (b_hi - b_lo >= ((int64_t)1 << 20)) {
@@ -1146,7 +1157,7 @@ int plan_create(zh_ctx* ctx, const zh_array_meta* m, const SrcDesc* srcs, int64_
       // uninitialised: the read fills every byte
       p->h2d_keep.emplace_back(new uint8_t[(size_t)std::max<int64_t>(1, p->h2d_len[k])]);
       freads.push_back({p->h2d_keep.back().get(), p->h2d[k].second, p->h2d_len[k]});
-      p->h2d[k].second = p->h2d_keep.back().get();
+      p->h2d[k].second = SrcRef::memory(p->h2d_keep.back().get());
     }
     if (pin) {
       const int rc = flush();
@@ -1170,7 +1181,7 @@ int plan_create(zh_ctx* ctx, const zh_array_meta* m, const SrcDesc* srcs, int64_
     piece_first[i] = (int64_t)dpieces.size();
     const auto& pv = held[i].pieces;
     for (size_t k = 0; k < pv.size(); k++) {
-      const uint8_t* dsrc = src_dev ? (const uint8_t*)pv[k].data : hs[i].data + piece_dst[i][k];
+      const uint8_t* dsrc = src_dev ? pv[k].data.mem() : hs[i].data + piece_dst[i][k];
       dpieces.push_back({(uint64_t)pv[k].offset, (uint64_t)pv[k].nbytes, dsrc,
                          (uint64_t)pv[k].data_nbytes});
     }
@@ -1466,7 +1477,7 @@ int plan_enqueue_impl(zh_plan* p, void* out, hipStream_t s) {
     if (!ok) return ZH_EHIP;
   }
   for (size_t k = 0; !p->external_h2d && k < p->h2d.size(); k++)
-    ZH_HIP(hipMemcpyAsync(p->d_input + p->h2d[k].first, p->h2d[k].second, (size_t)p->h2d_len[k],
+    ZH_HIP(hipMemcpyAsync(p->d_input + p->h2d[k].first, p->h2d[k].second.mem(), (size_t)p->h2d_len[k],
                           hipMemcpyHostToDevice, s));
   if (p->upload_slot >= 0 && (p->upload_pending || p->use_graph)) {
     // the tables with zeroed status words and slow-list count (a graph replays the copy)
@@ -1539,7 +1550,7 @@ int zh_plan_create(zh_ctx* ctx, const zh_array_meta* m, const zh_chunk_src* chun
                    zh_plan** out, char* err, size_t errlen) {
   std::vector<SrcDesc> srcs((size_t)std::max<int64_t>(0, nchunks));
   for (int64_t i = 0; chunks && i < nchunks; i++) {
-    srcs[(size_t)i].data = (const uint8_t*)chunks[i].data;
+    srcs[(size_t)i].data = SrcRef::memory(chunks[i].data);
     srcs[(size_t)i].nbytes = chunks[i].nbytes;
   }
   return plan_create(ctx, m, chunks ? srcs.data() : nullptr, nchunks, offset, shape, flags,
@@ -1747,7 +1758,7 @@ int zh_array_read(zh_ctx* ctx, const zh_array_meta* meta, const zh_chunk_src* ch
   std::lock_guard<std::mutex> lk(ctx->mu);
   std::vector<SrcDesc> srcs((size_t)std::max<int64_t>(0, nchunks));
   for (int64_t i = 0; chunks && i < nchunks; i++) {
-    srcs[(size_t)i].data = (const uint8_t*)chunks[i].data;
+    srcs[(size_t)i].data = SrcRef::memory(chunks[i].data);
     srcs[(size_t)i].nbytes = chunks[i].nbytes;
   }
   return read_region(ctx, meta, chunks ? srcs.data() : nullptr, nchunks, offset, shape, out,
@@ -1961,7 +1972,7 @@ int read_multi_impl(zh_ctx* const* ctxs, int ndev, int root, const zh_array_meta
     int64_t st0[kMaxDims], cnt[kMaxDims];
     const int64_t m = chunk_coords(n, meta->chunk_shape, o, s, st0, cnt);
     std::vector<SrcDesc> sub((size_t)m);
-    std::vector<std::vector<zh_shard_piece>> moved;  // pieces restaged on this device
+    std::vector<std::vector<Piece>> moved;  // pieces restaged on this device
     int64_t cur[kMaxDims] = {0};
     for (int64_t i = 0; i < m; i++) {
       int64_t lin = 0;
@@ -2014,9 +2025,9 @@ int read_multi_impl(zh_ctx* const* ctxs, int ndev, int root, const zh_array_meta
         return true;
       };
       for (auto& c : sub) {
-        const void* p = c.data;
-        if (!localize(c.data, c.nbytes, &p)) break;
-        c.data = (const uint8_t*)p;
+        const void* p = c.data.mem();
+        if (!localize(p, c.nbytes, &p)) break;
+        c.data = SrcRef::memory(p);
         p = c.index;
         if (!localize(c.index, c.index_nbytes, &p)) break;
         c.index = (const uint8_t*)p;
@@ -2024,9 +2035,9 @@ int read_multi_impl(zh_ctx* const* ctxs, int ndev, int root, const zh_array_meta
           moved.emplace_back(c.pieces, c.pieces + c.npieces);
           bool ok = true;
           for (auto& q : moved.back()) {
-            const void* qp = q.data;
-            if (!(ok = localize(q.data, q.data_nbytes, &qp))) break;
-            q.data = qp;
+            const void* qp = q.data.mem();
+            if (!(ok = localize(qp, q.data_nbytes, &qp))) break;
+            q.data = SrcRef::memory(qp);
           }
           if (!ok) break;
           c.pieces = moved.back().data();
@@ -2097,7 +2108,7 @@ int zh_array_read_multi_routed(zh_ctx* const* ctxs, int ndev, int root,
                                size_t errlen) {
   std::vector<SrcDesc> srcs((size_t)std::max<int64_t>(0, nchunks));
   for (int64_t i = 0; chunks && i < nchunks; i++) {
-    srcs[(size_t)i].data = (const uint8_t*)chunks[i].data;
+    srcs[(size_t)i].data = SrcRef::memory(chunks[i].data);
     srcs[(size_t)i].nbytes = chunks[i].nbytes;
   }
   return read_multi_impl(ctxs, ndev, root, meta, chunks ? srcs.data() : nullptr, nchunks, offset,

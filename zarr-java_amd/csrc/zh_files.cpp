@@ -1,22 +1,25 @@
-// zh_files.cpp — region reads whose chunks are files of a FilesystemStore.
+// zh_files.cpp — region reads and writes whose chunks are files of a FilesystemStore.
 //
 // core.Array.read over a FilesystemStore (M/core/Array.java:378-441) reads every chunk key
-// through FilesystemStore (M/store/FilesystemStore.java:43-102): `exists` (a regular file),
-// then for a whole chunk `get(keys)`, and for a shard the StoreHandleDataProvider reads of
-// decodeInternal (ShardingIndexedCodec.java:190-230, 333-357) — the index by a prefix or suffix
-// read, then one range read per referenced inner chunk.  zh_array_read_files takes the files'
-// paths and does those reads itself: the index on the calling thread (it decides the ranges),
-// the ranges inside the pipelined read's in lanes, each pread landing in a page-locked ring slot
-// that is DMA'd to the device (zh_pipeline.cpp).  The bytes are copied once on the host, not
-// read into a store buffer first and copied into the ring after, and the reads of slab r + 1
-// overlap the decode and D2H of slab r.  Sources name the file bytes by file addresses
-// (zh_ctx.h) into a process-wide table of open files, so one read may span several contexts
-// (zh_array_read_files_multi); the planner lays file bytes out like any host bytes and reads
-// them itself only for a plan that stages its own copies (not pipelined).
+// through FilesystemStore (M/store/FilesystemStore.java:42-102): `exists` (a regular file),
+// then for a whole chunk `get(keys)`, and for a part of a shard the StoreHandleDataProvider
+// reads of decodeInternal (ShardingIndexedCodec.java:190-230, 333-357) — the index by a prefix
+// or suffix read, then one range read per referenced inner chunk.  zh_array_read_files takes
+// the files' paths and does those reads itself: the indexes on the calling thread (they decide
+// the ranges), the ranges inside the pipelined read's in lanes, each pread landing in a
+// page-locked ring slot that is DMA'd to the device (zh_pipeline.cpp).  Sources name file
+// bytes as SrcRef::file(slot, offset) into a process-wide table of the files of the reads in
+// flight, so one read may span several contexts (zh_array_read_files_multi).
+//
+// Range semantics follow get(keys, start, end) (:84-102): a buffer of end - start bytes holding
+// what the file has, zeros after its end (file_fetch).  A whole-shard part is the reference's
+// chunkHandle.read() + ByteBufferDataProvider (ShardingIndexedCodec.java:246-251, 301-331):
+// slices of the file as it is, where an index or entry beyond the file is an error.
 //
 // zh_array_write_files is the write side: the device encode, then writeChunk's store calls
 // (FilesystemStore.set / delete) here, the encoded bytes D2H'd through the page-locked ring in
-// windows that the copy lanes pwrite straight into the chunk files.
+// windows that the copy lanes pwrite into a temporary file per chunk, renamed over the chunk's
+// file once all its bytes are in.
 #include <errno.h>
 #include <fcntl.h>
 #include <sys/stat.h>
@@ -24,8 +27,8 @@
 
 #include <algorithm>
 #include <atomic>
-#include <condition_variable>
 #include <cstring>
+#include <memory>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -35,152 +38,231 @@
 
 namespace {
 
-// The process-wide table of the store files open for reads in flight: slot → (fd, path).
-// Slots are taken and given back per read; file addresses name a slot.
-struct FileSlots {
-  std::mutex mu;
-  std::vector<int> fd;
-  std::vector<std::string> path;
-  std::vector<int64_t> free;
-};
+using zh::SrcRef;
 
-FileSlots& slots() {
-  static FileSlots s;
-  return s;
+// ---- store names (StoreException's text) ----------------------------------------------
+
+// FilesystemStore.toString() of a store (its file: URI without the trailing '/'), or the
+// caller's name for it; the filesystem root when no store is given.
+std::string store_name(const zh_file_store* st) {
+  if (st && st->name) return st->name;
+  std::string r = st && st->root ? st->root : "/";
+  while (r.size() > 1 && r.back() == '/') r.pop_back();
+  if (r == "/") r.clear();
+  return "file://" + r;
 }
 
-int64_t slot_take(int fd, const char* path) {
-  FileSlots& s = slots();
-  std::lock_guard<std::mutex> lk(s.mu);
-  int64_t k;
-  if (!s.free.empty()) {
-    k = s.free.back();
-    s.free.pop_back();
-    s.fd[(size_t)k] = fd;
-    s.path[(size_t)k] = path;
+// The key of `path` in the store: the path below the store's directory ('/'-joined keys,
+// String.join("/", keys) in StoreException), or the path itself outside it.
+std::string store_key(const zh_file_store* st, const char* path) {
+  std::string root = st && st->root ? st->root : "/";
+  while (root.size() > 1 && root.back() == '/') root.pop_back();
+  const std::string p(path);
+  size_t k = 0;
+  if (root == "/") {
+    if (p.empty() || p[0] != '/') return p;
   } else {
-    if ((int64_t)s.fd.size() >= zh::kFileMaxSlots) return -1;
-    k = (int64_t)s.fd.size();
-    s.fd.push_back(fd);
-    s.path.push_back(path);
+    if (p.compare(0, root.size(), root) != 0 || p.size() <= root.size() || p[root.size()] != '/')
+      return p;
+    k = root.size();
   }
+  while (k < p.size() && p[k] == '/') k++;
+  return p.substr(k);
+}
+
+std::string failed(const char* what, const std::string& store, const std::string& key,
+                   const std::string& cause) {
+  return std::string("Failed to ") + what + " store '" + store + "' at key '" + key + "': " + cause;
+}
+
+// IOException.getMessage() of a failed open of `path` as the JDK words it (UnixException:
+// AccessDeniedException carries just the file; other errors "file: reason").
+std::string open_cause(const std::string& path, int e) {
+  if (e == EACCES || e == EPERM) return path;
+  return path + ": " + strerror(e);
+}
+
+// ---- the file table --------------------------------------------------------------------
+
+struct FileEnt {
+  std::string path, store, key;
+  int fd = -1;
+  int pins = 0;       // file_fetch calls reading it now (its descriptor stays open)
+  uint64_t used = 0;  // last use, for closing the least recently used descriptor
+  bool live = false;
+  // range reads past the end read as zeros (a part's reads, get(keys, start, end)); otherwise
+  // the file is read as it was when its size was taken (a whole object or shard), and a read
+  // that meets the end (the file shrank meanwhile) fails
+  bool pad = false;
+};
+
+struct FileTable {
+  std::mutex mu;
+  std::vector<FileEnt> ent;
+  std::vector<int32_t> free;
+  int open = 0;  // descriptors open (and slots reserved for an open in progress)
+  uint64_t tick = 0;
+};
+
+FileTable& table() {
+  static FileTable t;
+  return t;
+}
+
+int32_t slot_take(const std::string& path, const std::string& store, const std::string& key,
+                  bool pad) {
+  FileTable& t = table();
+  std::lock_guard<std::mutex> lk(t.mu);
+  int32_t k;
+  if (!t.free.empty()) {
+    k = t.free.back();
+    t.free.pop_back();
+  } else {
+    k = (int32_t)t.ent.size();
+    t.ent.emplace_back();
+  }
+  FileEnt& e = t.ent[(size_t)k];
+  e.path = path;
+  e.store = store;
+  e.key = key;
+  e.fd = -1;
+  e.pins = 0;
+  e.live = true;
+  e.pad = pad;
   return k;
 }
 
-void slot_give(int64_t k) {
-  FileSlots& s = slots();
-  std::lock_guard<std::mutex> lk(s.mu);
-  if (s.fd[(size_t)k] >= 0) close(s.fd[(size_t)k]);
-  s.fd[(size_t)k] = -1;
-  s.path[(size_t)k].clear();
-  s.free.push_back(k);
+void slot_give(int32_t k) {
+  FileTable& t = table();
+  std::lock_guard<std::mutex> lk(t.mu);
+  FileEnt& e = t.ent[(size_t)k];
+  if (e.fd >= 0) {
+    close(e.fd);
+    t.open--;
+  }
+  e = FileEnt();
+  t.free.push_back(k);
+}
+
+// Closes the least recently used descriptor nobody is reading (caller holds t.mu); false when
+// every open descriptor is in use.
+bool close_lru(FileTable& t) {
+  FileEnt* v = nullptr;
+  for (FileEnt& e : t.ent)
+    if (e.live && e.fd >= 0 && e.pins == 0 && (!v || e.used < v->used)) v = &e;
+  if (!v) return false;
+  close(v->fd);
+  v->fd = -1;
+  t.open--;
+  return true;
+}
+
+// The open descriptor of slot k, pinned until file_unpin (opened by path when closed), or -1
+// with *msg set.  At most kFileMaxOpen descriptors are open: beyond that the least recently
+// used idle one is closed first.  The open itself runs outside the table's lock.
+int file_pin(int32_t k, std::string* msg) {
+  FileTable& t = table();
+  std::string path;
+  {
+    std::lock_guard<std::mutex> lk(t.mu);
+    FileEnt& e = t.ent[(size_t)k];
+    if (!e.live) {
+      *msg = "a store file that no read has open";
+      return -1;
+    }
+    e.used = ++t.tick;
+    if (e.fd >= 0) {
+      e.pins++;
+      return e.fd;
+    }
+    while (t.open >= zh::kFileMaxOpen && close_lru(t)) {
+    }
+    t.open++;  // reserved for this open
+    path = e.path;
+  }
+  int fd = open(path.c_str(), O_RDONLY | O_CLOEXEC);
+  if (fd < 0 && (errno == EMFILE || errno == ENFILE)) {  // other descriptors of the process
+    {
+      std::lock_guard<std::mutex> lk(t.mu);
+      while (close_lru(t)) {
+      }
+    }
+    fd = open(path.c_str(), O_RDONLY | O_CLOEXEC);
+  }
+  const int oe = errno;
+  std::lock_guard<std::mutex> lk(t.mu);
+  FileEnt& e = t.ent[(size_t)k];
+  if (fd < 0) {
+    t.open--;
+    *msg = failed("read from", e.store, e.key, open_cause(e.path, oe));
+    return -1;
+  }
+  if (e.fd >= 0) {  // another lane opened it meanwhile
+    close(fd);
+    t.open--;
+  } else {
+    e.fd = fd;
+  }
+  e.pins++;
+  return e.fd;
+}
+
+void file_unpin(int32_t k) {
+  FileTable& t = table();
+  std::lock_guard<std::mutex> lk(t.mu);
+  t.ent[(size_t)k].pins--;
+}
+
+bool slot_pads(int32_t k) {
+  FileTable& t = table();
+  std::lock_guard<std::mutex> lk(t.mu);
+  return t.ent[(size_t)k].pad;
+}
+
+std::string slot_read_failed(int32_t k, const std::string& cause) {
+  FileTable& t = table();
+  std::lock_guard<std::mutex> lk(t.mu);
+  const FileEnt& e = t.ent[(size_t)k];
+  return failed("read from", e.store, e.key, cause);
 }
 
 }  // namespace
 
 namespace zh {
 
-std::string file_fetch(void* dst, const void* src, int64_t n) {
-  const uint64_t a = (uint64_t)(uintptr_t)src & ~kFileTag;
-  const size_t k = (size_t)(a >> kFileOffBits);
-  int64_t off = (int64_t)(a & ((1ull << kFileOffBits) - 1));
-  int fd = -1;
-  {
-    FileSlots& s = slots();
-    std::lock_guard<std::mutex> lk(s.mu);
-    if (k < s.fd.size()) fd = s.fd[k];
-  }
-  if (fd < 0) return "a file source that no read has open";
+std::string file_fetch(void* dst, const SrcRef& src, int64_t n) {
+  const int32_t k = src.slot();
+  int64_t off = src.file_offset();
+  std::string msg;
+  const int fd = file_pin(k, &msg);
+  if (fd < 0) return msg;
   uint8_t* d = (uint8_t*)dst;
   while (n > 0) {
     const ssize_t r = pread(fd, d, (size_t)std::min<int64_t>(n, (int64_t)1 << 30), (off_t)off);
     if (r < 0 && errno == EINTR) continue;
-    if (r <= 0) {  // an error, or the file ended (it shrank after its size was taken)
-      const std::string why = r < 0 ? strerror(errno) : "unexpected end of file";
-      FileSlots& s = slots();
-      std::lock_guard<std::mutex> lk(s.mu);
-      return "Failed to read from store at '" + s.path[k] + "': " + why;
+    if (r < 0) {
+      msg = slot_read_failed(k, strerror(errno));
+      break;
+    }
+    if (r == 0) {  // the end of the file: the rest of a part's range reads as zeros
+      if (slot_pads(k)) memset(d, 0, (size_t)n);
+      else msg = slot_read_failed(k, "unexpected end of file");
+      break;
     }
     d += r;
     off += r;
     n -= r;
   }
-  return "";
+  file_unpin(k);
+  return msg;
 }
-
-namespace {
-
-// A small pool of reader threads for file_fetch_all, created on first use and kept: a read
-// below the pipeline threshold would otherwise pay a thread start per call.
-struct ReadPool {
-  std::mutex mu;
-  std::condition_variable cv, done_cv;
-  std::vector<std::thread> th;
-  std::vector<FileRead> q;
-  size_t next = 0, finished = 0, total = 0;
-  std::string fail;
-  bool stop = false;
-  ~ReadPool() {
-    {
-      std::lock_guard<std::mutex> lk(mu);
-      stop = true;
-    }
-    cv.notify_all();
-    for (auto& t : th) t.join();
-  }
-  void worker() {
-    std::unique_lock<std::mutex> lk(mu);
-    for (;;) {
-      cv.wait(lk, [&] { return stop || next < q.size(); });
-      if (stop) return;
-      const FileRead r = q[next++];
-      lk.unlock();
-      const std::string m = file_fetch(r.dst, r.src, r.n);
-      lk.lock();
-      if (!m.empty() && fail.empty()) fail = m;
-      if (++finished == total) done_cv.notify_all();
-    }
-  }
-};
-
-ReadPool& read_pool(int want) {
-  static ReadPool p;
-  std::lock_guard<std::mutex> lk(p.mu);
-  while ((int)p.th.size() < want) p.th.emplace_back([] { read_pool(0).worker(); });
-  return p;
-}
-
-std::mutex g_pool_call;  // one batch at a time
-
-}  // namespace
 
 std::string file_fetch_all(const std::vector<FileRead>& reads) {
-  constexpr int64_t kPiece = 512 << 10;
-  std::vector<FileRead> pieces;
-  for (const FileRead& r : reads)
-    for (int64_t o = 0; o < r.n; o += kPiece)
-      pieces.push_back({(uint8_t*)r.dst + o, (const uint8_t*)r.src + o, std::min(kPiece, r.n - o)});
-  const int threads = std::min(32, std::max(1, env_int("ZH_FILE_THREADS", 1)));
-  if (pieces.size() <= 1 || threads <= 1) {
-    for (const FileRead& r : pieces) {
-      const std::string m = file_fetch(r.dst, r.src, r.n);
-      if (!m.empty()) return m;
-    }
-    return "";
+  for (const FileRead& r : reads) {
+    const std::string m = file_fetch(r.dst, r.src, r.n);
+    if (!m.empty()) return m;
   }
-  std::lock_guard<std::mutex> call(g_pool_call);
-  ReadPool& p = read_pool(threads);
-  std::unique_lock<std::mutex> lk(p.mu);
-  p.q = std::move(pieces);
-  p.next = p.finished = 0;
-  p.total = p.q.size();
-  p.fail.clear();
-  p.cv.notify_all();
-  p.done_cv.wait(lk, [&] { return p.finished == p.total; });
-  std::string m = p.fail;
-  p.q.clear();
-  p.next = p.total = p.finished = 0;
-  return m;
+  return "";
 }
 
 }  // namespace zh
@@ -189,22 +271,28 @@ using namespace zh;
 
 namespace {
 
-// The files of one read, open for its duration: their slots go back (and the files are closed)
-// on every exit.
+// The files of one read: their slots go back (and their descriptors are closed) on every exit.
 struct FileSet {
-  std::vector<int64_t> taken;
+  std::vector<int32_t> taken;
   ~FileSet() {
-    for (int64_t k : taken) slot_give(k);
+    for (int32_t k : taken) slot_give(k);
   }
 };
 
+// What one read of files holds for the planner: the sources and the memory they point into.
+struct FileSources {
+  FileSet set;
+  std::vector<SrcDesc> srcs;
+  std::vector<std::vector<uint8_t>> index;
+  std::vector<std::vector<Piece>> pieces;
+};
+
 // Sources for a read of the files `paths` (computeChunkCoords order of [offset, offset+shape)):
-// per file the reference's store reads up to the ranges (open / exists, the stored index), the
-// ranges as file addresses.  index / pieces hold what the sources point into.
-int file_sources(const zh_array_meta* meta, const char* const* paths, int64_t npaths,
-                 const int64_t* offset, const int64_t* shape, FileSet& set,
-                 std::vector<SrcDesc>& srcs, std::vector<std::vector<uint8_t>>& index,
-                 std::vector<std::vector<zh_shard_piece>>& pieces, char* err, size_t errlen) {
+// per file the reference's store reads up to the ranges (exists, the stored index), the ranges
+// as file sources.
+int file_sources(const zh_array_meta* meta, const zh_file_store* store, const char* const* paths,
+                 int64_t npaths, const int64_t* offset, const int64_t* shape, FileSources& fs,
+                 char* err, size_t errlen) {
   const int n = meta->ndim;
   for (int d = 0; d < n; d++) {  // M/core/Array.java:386-390 (the planner's check, early)
     if (offset[d] < 0 || offset[d] + shape[d] > meta->shape[d]) {
@@ -229,141 +317,141 @@ int file_sources(const zh_array_meta* meta, const char* const* paths, int64_t np
   }
   const zh_codec_chain& c = meta->chain;
   const int64_t isz = c.sharded ? zh_shard_index_size(meta) : 0;
-  srcs.assign((size_t)npaths, SrcDesc());
-  index.assign((size_t)npaths, {});
-  pieces.assign((size_t)npaths, {});
-  int64_t cur[kMaxDims] = {0};
+  const std::string sname = store_name(store);
+  fs.srcs.assign((size_t)npaths, SrcDesc());
+  fs.index.assign((size_t)npaths, {});
+  fs.pieces.assign((size_t)npaths, {});
   std::vector<FileRead> ireads;
-  std::vector<int64_t> slot_of((size_t)npaths, -1);  // the file's slot in the table
+  std::vector<int32_t> slot_of((size_t)npaths, -1);
+  std::vector<std::array<int64_t, kMaxDims>> lo((size_t)npaths), hi((size_t)npaths);
+  int64_t cur[kMaxDims] = {0};
   for (int64_t i = 0; i < npaths; i++) {
-    const char* path = paths[i];
-    if (!path) continue;  // missing key
-    const int fd = open(path, O_RDONLY | O_CLOEXEC);
-    if (fd < 0) {
-      const int oe = errno;
-      // FilesystemStore.exists is Files.isRegularFile (false when the file is absent, is no
-      // regular file, or cannot be stat'ed); an existing regular file that cannot be opened is
-      // a failed read (readAllBytes / newByteChannel → StoreException.readFailed)
-      struct stat sb;
-      if (oe == ENOENT || oe == ENOTDIR || stat(path, &sb) != 0 || !S_ISREG(sb.st_mode)) continue;
-      set_err(err, errlen, "Failed to read from store at '%s': %s", path, strerror(oe));
-      return ZH_EIO;
-    }
-    struct stat sb;
-    if (fstat(fd, &sb) != 0) {
-      const int fe = errno;
-      close(fd);
-      set_err(err, errlen, "Failed to read from store at '%s': %s", path, strerror(fe));
-      return ZH_EIO;
-    }
-    if (!S_ISREG(sb.st_mode)) {  // Files.isRegularFile (FilesystemStore.java:44-46)
-      close(fd);
-      continue;
-    }
-    const int64_t size = (int64_t)sb.st_size;
-    const int64_t k = size < kFileMaxBytes ? slot_take(fd, path) : -1;
-    if (k < 0) {
-      close(fd);
-      set_err(err, errlen, "'%s': %s", path,
-              size < kFileMaxBytes ? "too many store files open for reads at once"
-                                   : "file larger than a file address can name");
-      return ZH_EUNSUPPORTED;
-    }
-    set.taken.push_back(k);
-    slot_of[(size_t)i] = k;
-    SrcDesc& s = srcs[(size_t)i];
-    if (!c.sharded) {  // get(keys): the whole object
-      s.data = file_addr(k, 0);
-      s.nbytes = size;
-      continue;
-    }
-    // the stored index: a prefix read (index_location start) or a suffix read of isz bytes
-    // (get(keys, -isz)); a file shorter than the index gives what it holds, and the planner
-    // reports "Shard [...] is smaller than its index"
-    const int64_t ilen = std::min(size, isz);
-    auto& ib = index[(size_t)i];
-    ib.resize((size_t)std::max<int64_t>(ilen, 1));
-    const int64_t ioff = c.index_location == ZH_INDEX_START ? 0 : size - ilen;
-    ireads.push_back({ib.data(), file_addr(k, ioff), ilen});
-    s.index = ib.data();
-    s.index_nbytes = ilen;
-    s.shard_nbytes = size;
-  }
-  // every shard's index in one batch (file_fetch_all), then the ranges from each
-  const std::string m = file_fetch_all(ireads);
-  if (!m.empty()) {
-    set_err(err, errlen, "%s", m.c_str());
-    return ZH_EIO;
-  }
-  std::fill(cur, cur + kMaxDims, 0);
-  for (int64_t i = 0; c.sharded && i < npaths; i++) {
     int64_t cc[kMaxDims];
     for (int d = 0; d < n; d++) cc[d] = cstart[d] + cur[d];
     for (int d = n - 1; d >= 0; d--) {
       if (++cur[d] < ccount[d]) break;
       cur[d] = 0;
     }
-    SrcDesc& s = srcs[(size_t)i];
-    if (!s.index || s.index_nbytes < isz) continue;  // missing, or the planner reports it short
-    const int64_t k = slot_of[(size_t)i];
+    const char* path = paths[i];
+    if (!path) continue;  // missing key
+    // FilesystemStore.exists is Files.isRegularFile (:42-45): false when the file is absent,
+    // is no regular file, or cannot be stat'ed
+    struct stat sb;
+    if (stat(path, &sb) != 0 || !S_ISREG(sb.st_mode)) continue;
+    const int64_t size = (int64_t)sb.st_size;
+    SrcDesc& s = fs.srcs[(size_t)i];
+    if (!c.sharded) {  // get(keys): the whole object
+      const int32_t k = slot_take(path, sname, store_key(store, path), false);
+      fs.set.taken.push_back(k);
+      s.data = SrcRef::file(k, 0);
+      s.nbytes = size;
+      continue;
+    }
     int32_t co[kMaxDims], oo[kMaxDims], ps[kMaxDims];
     if (projection(n, cc, meta->shape, meta->chunk_shape, offset, shape, co, oo, ps) != ZH_OK) {
       set_err(err, errlen, "projection exceeds Integer.MAX_VALUE");
       return ZH_EARITH;
     }
-    int64_t lo[kMaxDims], hi[kMaxDims];
+    bool full = true;  // decodePartial: Arrays.equals(shape, chunkShape) (:246)
     for (int d = 0; d < n; d++) {
-      lo[d] = co[d];
-      hi[d] = (int64_t)co[d] + ps[d];
+      full = full && ps[d] == meta->chunk_shape[d];
+      lo[(size_t)i][(size_t)d] = co[d];
+      hi[(size_t)i][(size_t)d] = (int64_t)co[d] + ps[d];
     }
-    // the referenced inner chunks' ranges, adjacent ones merged (one pread per run); entries
-    // beyond the file are left out and read as "Could not load byte data" on the device
+    const int32_t k = slot_take(path, sname, store_key(store, path), !full);
+    fs.set.taken.push_back(k);
+    slot_of[(size_t)i] = k;
+    // the stored index: a suffix read (get(keys, -isz)) or a prefix read (get(keys, 0, isz)).
+    // A suffix of a file shorter than the index, or any index past the end of a whole shard's
+    // bytes, is short: the planner reports "Shard [...] of N bytes is smaller than its index".
+    // A part's prefix read is zero-padded like any range (get(keys, start, end)).
+    const bool start = c.index_location == ZH_INDEX_START;
+    const int64_t ilen = start && !full ? isz : std::min(size, isz);
+    auto& ib = fs.index[(size_t)i];
+    ib.resize((size_t)std::max<int64_t>(ilen, 1));
+    ireads.push_back({ib.data(), SrcRef::file(k, start ? 0 : size - ilen), ilen});
+    s.index = ib.data();
+    s.index_nbytes = ilen;
+    // a whole shard resolves its entries against the file's size; a part's range reads are
+    // zero-padded, so no entry is out of reach by its offset (shard size unknown)
+    s.shard_nbytes = full ? size : -1;
+  }
+  // every shard's index, then the ranges from each
+  const std::string m = file_fetch_all(ireads);
+  if (!m.empty()) {
+    set_err(err, errlen, "%s", m.c_str());
+    return ZH_EIO;
+  }
+  for (int64_t i = 0; c.sharded && i < npaths; i++) {
+    SrcDesc& s = fs.srcs[(size_t)i];
+    if (!s.index || s.index_nbytes < isz) continue;  // missing, or the planner reports it short
+    const int32_t k = slot_of[(size_t)i];
+    const uint8_t* ib = s.index + (c.index_location == ZH_INDEX_START ? 0 : s.index_nbytes - isz);
+    // the referenced inner chunks' ranges, adjacent ones merged (one pread per run).  Entries
+    // beyond a whole shard's file, or longer than a Java buffer (2^31 - 1 bytes: the
+    // reference's (int) allocation fails) are left out and read as "Could not load byte data"
+    // on the device.
     std::vector<std::pair<int64_t, int64_t>> rs;
-    if (shard_ranges(meta, s.index, s.shard_nbytes, lo, hi, INT64_MAX, rs) != ZH_OK) continue;
-    for (auto& r : rs) pieces[(size_t)i].push_back({r.first, r.second, file_addr(k, r.first), r.second});
-    s.pieces = pieces[(size_t)i].data();
-    s.npieces = (int64_t)pieces[(size_t)i].size();
+    if (shard_ranges(meta, ib, s.shard_nbytes, lo[(size_t)i].data(), hi[(size_t)i].data(),
+                     INT64_MAX, rs, kIntMax) != ZH_OK)
+      continue;
+    auto& pv = fs.pieces[(size_t)i];
+    for (auto& r : rs) {
+      if (r.first > INT64_MAX - r.second) continue;  // the range's end is not a file offset
+      pv.push_back({r.first, r.second, SrcRef::file(k, r.first), r.second});
+    }
+    s.pieces = pv.data();
+    s.npieces = (int64_t)pv.size();
   }
   return ZH_OK;
 }
 
-// Files.createDirectories(parent) (FilesystemStore.set, M/store/FilesystemStore.java:106-115):
-// every missing directory above `path`.  "" or the failure's message.
-std::string make_parents(const char* path) {
-  std::string p(path);
-  for (size_t k = 1; k < p.size(); k++) {
-    if (p[k] != '/') continue;
-    const std::string dir = p.substr(0, k);
+// Files.createDirectories(parent) (FilesystemStore.set, M/store/FilesystemStore.java:107-115):
+// every missing directory above `path`.  "" or the failing directory.
+std::string make_parents(const std::string& path, int* why) {
+  for (size_t k = 1; k < path.size(); k++) {
+    if (path[k] != '/') continue;
+    const std::string dir = path.substr(0, k);
     if (mkdir(dir.c_str(), 0777) != 0 && errno != EEXIST) {
+      const int me = errno;  // mkdir's reason, before stat can change errno
       struct stat sb;
       if (stat(dir.c_str(), &sb) == 0 && S_ISDIR(sb.st_mode)) continue;
-      return "Failed to create parent directories for path: " + dir + ": " + strerror(errno);
+      *why = me;
+      return dir;
     }
   }
   return "";
 }
 
-// pwrite of n bytes at off, retried on EINTR / short writes; "" or strerror.
-std::string write_all(int fd, const uint8_t* p, int64_t n, int64_t off) {
+std::string parent_of(const std::string& path) {
+  const size_t k = path.find_last_of('/');
+  return k == std::string::npos || k == 0 ? std::string(k == 0 ? "/" : "") : path.substr(0, k);
+}
+
+// pwrite of n bytes at off, retried on EINTR / short writes; 0 or the errno.
+int write_all(int fd, const uint8_t* p, int64_t n, int64_t off) {
   while (n > 0) {
     const ssize_t w = pwrite(fd, p, (size_t)std::min<int64_t>(n, (int64_t)1 << 30), (off_t)off);
     if (w < 0 && errno == EINTR) continue;
-    if (w <= 0) return w < 0 ? strerror(errno) : "no progress";
+    if (w < 0) return errno;
+    if (w == 0) return EIO;
     p += w;
     off += w;
     n -= w;
   }
-  return "";
+  return 0;
 }
+
+std::atomic<uint64_t> g_tmp_seq{0};
 
 }  // namespace
 
 extern "C" {
 
 int zh_array_write_files(zh_ctx* ctx, const zh_array_meta* m, const void* src,
-                         const int64_t* offset, const int64_t* shape, const char* const* paths,
-                         int64_t npaths, uint32_t flags, int64_t* nbytes, char* err,
-                         size_t errlen) {
+                         const int64_t* offset, const int64_t* shape, const zh_file_store* store,
+                         const char* const* paths, int64_t npaths, uint32_t flags,
+                         int64_t* nbytes, char* err, size_t errlen) {
   if (!ctx || !m || !src || !offset || !shape || (npaths > 0 && !paths)) return ZH_EINVAL;
   int st = zh_validate_meta(m, err, errlen);
   if (st != ZH_OK) return st;
@@ -373,6 +461,7 @@ int zh_array_write_files(zh_ctx* ctx, const zh_array_meta* m, const void* src,
       return ZH_EINVAL;
     }
   (void)hipSetDevice(ctx->device);
+  const std::string sname = store_name(store);
   int64_t rbytes = m->dtype_size;
   for (int d = 0; d < m->ndim; d++) rbytes *= std::max<int64_t>(0, shape[d]);
   const int64_t bound = zh_array_encoded_bound(m);
@@ -397,35 +486,35 @@ int zh_array_write_files(zh_ctx* ctx, const zh_array_meta* m, const void* src,
     st = zh_array_write(ctx, m, dsrc ? dsrc : src, offset, shape, dsts.data(), npaths, nullptr,
                         err, errlen);
   }
-  std::vector<int> fds((size_t)std::max<int64_t>(1, npaths), -1);
   if (e == hipSuccess && st == ZH_OK) {
     std::lock_guard<std::mutex> lk(ctx->mu);
     // writeChunk per chunk (M/core/Array.java:143-156): all fill → delete the key
-    // (FilesystemStore.delete: a missing file is fine), else set: the parent directories, then
-    // the file created or truncated and written
+    // (FilesystemStore.delete, :130-143: a missing file is fine); otherwise set (:105-128):
+    // the parent directories first (here, for every chunk, before any byte is written)
+    std::string last_parent;
     for (int64_t i = 0; st == ZH_OK && i < npaths; i++) {
       const int64_t nb = dsts[(size_t)i].nbytes;
       if (nbytes) nbytes[i] = nb;
+      const std::string key = store_key(store, paths[i]);
       if (nb == 0) {
         if (unlink(paths[i]) != 0 && errno != ENOENT) {
-          set_err(err, errlen, "Failed to delete from store at '%s': %s", paths[i],
-                  strerror(errno));
+          const std::string cause = std::string("Failed to delete file: ") + paths[i];
+          set_err(err, errlen, "%s", failed("delete from", sname, key, cause).c_str());
           st = ZH_EIO;
         }
         continue;
       }
-      std::string msg = make_parents(paths[i]);
-      int fd = -1;
-      if (msg.empty()) {
-        fd = open(paths[i], O_WRONLY | O_CREAT | O_TRUNC | O_CLOEXEC, 0666);
-        if (fd < 0) msg = strerror(errno);
-      }
-      if (!msg.empty()) {
-        set_err(err, errlen, "Failed to write to store at '%s': %s", paths[i], msg.c_str());
+      const std::string parent = parent_of(paths[i]);
+      if (parent == last_parent) continue;
+      int why = 0;
+      if (!make_parents(paths[i], &why).empty()) {
+        (void)why;
+        const std::string cause = "Failed to create parent directories for path: " + parent;
+        set_err(err, errlen, "%s", failed("write to", sname, key, cause).c_str());
         st = ZH_EIO;
         break;
       }
-      fds[(size_t)i] = fd;
+      last_parent = parent;
     }
     // the encoded bytes out: windows of the ring size, the copy lanes each D2H'ing one window
     // into a page-locked slot of their own while pwrite-ing the previous one
@@ -436,17 +525,31 @@ int zh_array_write_files(zh_ctx* ctx, const zh_array_meta* m, const void* src,
     struct Job {
       int64_t chunk, off, len;
     };
-    // windows taken round-robin over the chunks: buffered writes to one file serialize on its
-    // inode lock, so the lanes spread over as many files as the write has
+    // windows taken round-robin over groups of `lanes` chunks: buffered writes to one file
+    // serialize on its inode lock, so the lanes spread over the files of a group; a chunk's
+    // file is open from its first window's write to its last, so at most 3 * lanes files are
+    // open (two undrained windows per lane, plus the group being taken)
     std::vector<Job> jobs;
-    int64_t most = 0;
-    for (int64_t i = 0; st == ZH_OK && i < npaths; i++)
-      most = std::max(most, dsts[(size_t)i].nbytes);
-    for (int64_t o = 0; st == ZH_OK && o < most; o += win)
-      for (int64_t i = 0; i < npaths; i++)
-        if (o < dsts[(size_t)i].nbytes)
-          jobs.push_back({i, o, std::min(win, dsts[(size_t)i].nbytes - o)});
+    for (int64_t g0 = 0; st == ZH_OK && g0 < npaths; g0 += lanes) {
+      const int64_t g1 = std::min<int64_t>(npaths, g0 + lanes);
+      int64_t most = 0;
+      for (int64_t i = g0; i < g1; i++) most = std::max(most, dsts[(size_t)i].nbytes);
+      for (int64_t o = 0; o < most; o += win)
+        for (int64_t i = g0; i < g1; i++)
+          if (o < dsts[(size_t)i].nbytes)
+            jobs.push_back({i, o, std::min(win, dsts[(size_t)i].nbytes - o)});
+    }
     lanes = (int)std::max<int64_t>(1, std::min<int64_t>(lanes, (int64_t)jobs.size()));
+    // per chunk: its temporary file (created by its first write) and the windows still due
+    struct Out {
+      std::mutex mu;
+      int fd = -1;
+      std::string tmp;
+      int64_t left = 0;
+      bool done = false;
+    };
+    std::unique_ptr<Out[]> outs(new Out[(size_t)std::max<int64_t>(1, npaths)]);
+    for (const Job& J : jobs) outs[(size_t)J.chunk].left++;
     std::atomic<size_t> next{0};
     std::atomic<int> fail{ZH_OK};
     std::mutex fmu;
@@ -457,6 +560,46 @@ int zh_array_write_files(zh_ctx* ctx, const zh_array_meta* m, const void* src,
         fail = code;
         fmsg = m2;
       }
+    };
+    auto write_failed = [&](int64_t i, int eno) {
+      (void)eno;
+      const std::string cause = "Failed to write " + std::to_string(dsts[(size_t)i].nbytes) +
+                                " bytes to file: " + paths[i];
+      lane_fail(ZH_EIO, failed("write to", sname, store_key(store, paths[i]), cause));
+    };
+    // one window into chunk J.chunk's temporary file; the chunk's last window renames it over
+    // the chunk's file
+    auto put = [&](const Job& J, const uint8_t* bytes) {
+      Out& O = outs[(size_t)J.chunk];
+      int fd;
+      {
+        std::lock_guard<std::mutex> g(O.mu);
+        if (O.fd < 0) {
+          O.tmp = std::string(paths[J.chunk]) + ".zhtmp" + std::to_string(getpid()) + "." +
+                  std::to_string(g_tmp_seq.fetch_add(1));
+          O.fd = open(O.tmp.c_str(), O_WRONLY | O_CREAT | O_TRUNC | O_CLOEXEC, 0666);
+          if (O.fd < 0) {
+            write_failed(J.chunk, errno);
+            return;
+          }
+        }
+        fd = O.fd;
+      }
+      const int we = write_all(fd, bytes, J.len, J.off);
+      if (we != 0) {
+        write_failed(J.chunk, we);
+        return;
+      }
+      std::lock_guard<std::mutex> g(O.mu);
+      if (--O.left > 0) return;
+      const int ce = close(O.fd) != 0 ? errno : 0;
+      O.fd = -1;
+      if (ce != 0 || rename(O.tmp.c_str(), paths[J.chunk]) != 0) {
+        write_failed(J.chunk, ce ? ce : errno);
+        unlink(O.tmp.c_str());
+        return;
+      }
+      O.done = true;
     };
     auto lane = [&](int L) {
       (void)hipSetDevice(ctx->device);
@@ -470,16 +613,10 @@ int zh_array_write_files(zh_ctx* ctx, const zh_array_meta* m, const void* src,
       int pslot = 0, flip = 0;
       auto drain = [&]() {
         if (!pend) return;
-        if (hipEventSynchronize(ev[pslot]) != hipSuccess) {
+        if (hipEventSynchronize(ev[pslot]) != hipSuccess)
           lane_fail(ZH_EHIP, "device-to-host copy of an encoded chunk failed");
-        } else {
-          const std::string w = write_all(fds[(size_t)pend->chunk],
-                                          (const uint8_t*)ctx->ring_out[(size_t)(2 * L + pslot)],
-                                          pend->len, pend->off);
-          if (!w.empty())
-            lane_fail(ZH_EIO, std::string("Failed to write to store at '") + paths[pend->chunk] +
-                                  "': " + w);
-        }
+        else if (fail.load() == ZH_OK)
+          put(*pend, (const uint8_t*)ctx->ring_out[(size_t)(2 * L + pslot)]);
         pend = nullptr;
       };
       for (;;) {
@@ -512,12 +649,11 @@ int zh_array_write_files(zh_ctx* ctx, const zh_array_meta* m, const void* src,
         set_err(err, errlen, "%s", fmsg.c_str());
       }
     }
-    for (size_t i = 0; i < fds.size(); i++) {
-      if (fds[i] < 0) continue;
-      if (close(fds[i]) != 0 && st == ZH_OK) {
-        set_err(err, errlen, "Failed to write to store at '%s': %s", paths[i], strerror(errno));
-        st = ZH_EIO;
-      }
+    // chunks a failure left unfinished: their temporary files go, their files stay as they were
+    for (int64_t i = 0; i < npaths; i++) {
+      Out& O = outs[(size_t)i];
+      if (O.fd >= 0) close(O.fd);
+      if (!O.tmp.empty() && !O.done) unlink(O.tmp.c_str());
     }
   }
   if (dsrc) ctx_release(ctx, dsrc, gsrc);
@@ -530,17 +666,15 @@ int zh_array_write_files(zh_ctx* ctx, const zh_array_meta* m, const void* src,
   return st;
 }
 
-int64_t zh_debug_file_reads(const zh_array_meta* meta, const char* const* paths, int64_t npaths,
-                            const int64_t* offset, const int64_t* shape, int64_t* reads,
-                            int64_t cap, char* err, size_t errlen) {
+int64_t zh_debug_file_reads(const zh_array_meta* meta, const zh_file_store* store,
+                            const char* const* paths, int64_t npaths, const int64_t* offset,
+                            const int64_t* shape, int64_t* reads, int64_t cap, char* err,
+                            size_t errlen) {
   if (!meta || !offset || !shape || (npaths > 0 && !paths)) return -ZH_EINVAL;
   int st = zh_validate_meta(meta, err, errlen);
   if (st != ZH_OK) return -st;
-  FileSet set;
-  std::vector<SrcDesc> srcs;
-  std::vector<std::vector<uint8_t>> index;
-  std::vector<std::vector<zh_shard_piece>> pieces;
-  st = file_sources(meta, paths, npaths, offset, shape, set, srcs, index, pieces, err, errlen);
+  FileSources fs;
+  st = file_sources(meta, store, paths, npaths, offset, shape, fs, err, errlen);
   if (st != ZH_OK) return -st;
   int64_t k = 0;
   auto put = [&](int64_t i, int64_t off, int64_t n) {
@@ -552,19 +686,23 @@ int64_t zh_debug_file_reads(const zh_array_meta* meta, const char* const* paths,
     k++;
   };
   for (int64_t i = 0; i < npaths; i++) {
-    const SrcDesc& s = srcs[(size_t)i];
-    if (s.data) put(i, 0, s.nbytes);  // a whole object
-    if (s.index)  // the index read: a prefix, or the last index_nbytes bytes
-      put(i, meta->chain.index_location == ZH_INDEX_START ? 0 : s.shard_nbytes - s.index_nbytes,
+    const SrcDesc& s = fs.srcs[(size_t)i];
+    if (s.data.is_file()) put(i, 0, s.nbytes);  // a whole object
+    if (s.index) {  // the index read: a prefix, or a suffix of the file
+      struct stat sb;
+      const int64_t size = stat(paths[i], &sb) == 0 ? (int64_t)sb.st_size : 0;
+      put(i, meta->chain.index_location == ZH_INDEX_START ? 0 : size - s.index_nbytes,
           s.index_nbytes);
+    }
     for (int64_t q = 0; q < s.npieces; q++) put(i, s.pieces[q].offset, s.pieces[q].nbytes);
   }
   return k;
 }
 
-int zh_array_read_files(zh_ctx* ctx, const zh_array_meta* meta, const char* const* paths,
-                        int64_t npaths, const int64_t* offset, const int64_t* shape, void* out,
-                        uint32_t flags, char* err, size_t errlen) {
+int zh_array_read_files(zh_ctx* ctx, const zh_array_meta* meta, const zh_file_store* store,
+                        const char* const* paths, int64_t npaths, const int64_t* offset,
+                        const int64_t* shape, void* out, uint32_t flags, char* err,
+                        size_t errlen) {
   if (!ctx || !meta || !offset || !shape || !out || (npaths > 0 && !paths)) return ZH_EINVAL;
   if (flags & ZH_SRC_DEVICE) {
     set_err(err, errlen, "zh_array_read_files reads host files: ZH_SRC_DEVICE is not allowed");
@@ -572,23 +710,21 @@ int zh_array_read_files(zh_ctx* ctx, const zh_array_meta* meta, const char* cons
   }
   int st = zh_validate_meta(meta, err, errlen);
   if (st != ZH_OK) return st;
-  FileSet set;
-  std::vector<SrcDesc> srcs;
-  std::vector<std::vector<uint8_t>> index;
-  std::vector<std::vector<zh_shard_piece>> pieces;
-  st = file_sources(meta, paths, npaths, offset, shape, set, srcs, index, pieces, err, errlen);
+  FileSources fs;
+  st = file_sources(meta, store, paths, npaths, offset, shape, fs, err, errlen);
   if (st != ZH_OK) return st;
   std::lock_guard<std::mutex> lk(ctx->mu);
   // large reads pipelined (the in lanes pread the ranges into the ring); otherwise one plan,
   // which reads the file bytes into host buffers first
-  return read_region(ctx, meta, srcs.data(), npaths, offset, shape, out, flags & ZH_OUT_DEVICE,
+  return read_region(ctx, meta, fs.srcs.data(), npaths, offset, shape, out, flags & ZH_OUT_DEVICE,
                      nullptr, err, errlen);
 }
 
 int zh_array_read_files_multi(zh_ctx* const* ctxs, int ndev, int root, const zh_array_meta* meta,
-                              const char* const* paths, int64_t npaths, const int64_t* offset,
-                              const int64_t* shape, void* out, uint32_t flags,
-                              int32_t* slab_route, char* err, size_t errlen) {
+                              const zh_file_store* store, const char* const* paths,
+                              int64_t npaths, const int64_t* offset, const int64_t* shape,
+                              void* out, uint32_t flags, int32_t* slab_route, char* err,
+                              size_t errlen) {
   if (!ctxs || ndev <= 0 || !meta || !offset || !shape || !out || (npaths > 0 && !paths))
     return ZH_EINVAL;
   if (flags & ZH_SRC_DEVICE) {
@@ -597,13 +733,10 @@ int zh_array_read_files_multi(zh_ctx* const* ctxs, int ndev, int root, const zh_
   }
   int st = zh_validate_meta(meta, err, errlen);
   if (st != ZH_OK) return st;
-  FileSet set;
-  std::vector<SrcDesc> srcs;
-  std::vector<std::vector<uint8_t>> index;
-  std::vector<std::vector<zh_shard_piece>> pieces;
-  st = file_sources(meta, paths, npaths, offset, shape, set, srcs, index, pieces, err, errlen);
+  FileSources fs;
+  st = file_sources(meta, store, paths, npaths, offset, shape, fs, err, errlen);
   if (st != ZH_OK) return st;
-  return read_multi_impl(ctxs, ndev, root, meta, srcs.data(), npaths, offset, shape, out,
+  return read_multi_impl(ctxs, ndev, root, meta, fs.srcs.data(), npaths, offset, shape, out,
                          flags & ZH_OUT_DEVICE, slab_route, err, errlen);
 }
 

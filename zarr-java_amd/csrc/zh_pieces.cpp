@@ -98,16 +98,18 @@ static int shard_ranges_impl(const zh_array_meta* m, const uint8_t* index, int64
 
 int shard_ranges(const zh_array_meta* m, const uint8_t* index, int64_t shard_nbytes,
                  const int64_t* part_lo, const int64_t* part_hi, int64_t max_run,
-                 std::vector<std::pair<int64_t, int64_t>>& out) {
-  return shard_ranges_impl(m, index, shard_nbytes, part_lo, part_hi, max_run, INT64_MAX, out);
+                 std::vector<std::pair<int64_t, int64_t>>& out, int64_t max_entry) {
+  return shard_ranges_impl(m, index, shard_nbytes, part_lo, part_hi, max_run, max_entry, out);
 }
 
 }  // namespace zh
 
 namespace {
 
-// zh_shard_src → planner source: missing, whole object (one piece at 0), or index + pieces.
-int to_src(const zh_shard_src& s, int64_t i, SrcDesc& d, char* err, size_t errlen) {
+// zh_shard_src → planner source: missing, whole object (one piece at 0), or index + pieces
+// (copied into `held`, which the call keeps until it returns).
+int to_src(const zh_shard_src& s, int64_t i, SrcDesc& d, std::vector<Piece>& held, char* err,
+           size_t errlen) {
   d = SrcDesc();
   if (s.npieces < 0 || (s.npieces > 0 && !s.pieces)) {
     set_err(err, errlen, "shard source %lld: invalid piece list", (long long)i);
@@ -122,14 +124,19 @@ int to_src(const zh_shard_src& s, int64_t i, SrcDesc& d, char* err, size_t errle
               (long long)i);
       return ZH_EINVAL;
     }
-    d.data = (const uint8_t*)q.data;
+    d.data = SrcRef::memory(q.data);
     d.nbytes = q.nbytes;
     return ZH_OK;
   }
   d.index = (const uint8_t*)s.index;
   d.index_nbytes = s.index_nbytes;
   d.shard_nbytes = s.shard_nbytes;
-  d.pieces = s.pieces;
+  held.resize((size_t)s.npieces);
+  for (int64_t k = 0; k < s.npieces; k++) {
+    const zh_shard_piece& q = s.pieces[k];
+    held[(size_t)k] = Piece{q.offset, q.nbytes, SrcRef::memory(q.data), q.data_nbytes};
+  }
+  d.pieces = held.data();
   d.npieces = s.npieces;
   return ZH_OK;
 }
@@ -169,8 +176,9 @@ int zh_array_read_pieces(zh_ctx* ctx, const zh_array_meta* meta, const zh_shard_
   }
   if (nshards > 0 && !shards) return ZH_EINVAL;
   std::vector<SrcDesc> srcs((size_t)std::max<int64_t>(0, nshards));
+  std::vector<std::vector<Piece>> held((size_t)std::max<int64_t>(0, nshards));
   for (int64_t i = 0; i < nshards; i++) {
-    const int st = to_src(shards[i], i, srcs[(size_t)i], err, errlen);
+    const int st = to_src(shards[i], i, srcs[(size_t)i], held[(size_t)i], err, errlen);
     if (st != ZH_OK) return st;
   }
   std::lock_guard<std::mutex> lk(ctx->mu);
@@ -189,8 +197,9 @@ int zh_array_read_pieces_multi(zh_ctx* const* ctxs, int ndev, int root,
     return ZH_EINVAL;
   }
   std::vector<SrcDesc> srcs((size_t)std::max<int64_t>(0, nshards));
+  std::vector<std::vector<Piece>> held((size_t)std::max<int64_t>(0, nshards));
   for (int64_t i = 0; i < nshards; i++) {
-    const int st = to_src(shards[i], i, srcs[(size_t)i], err, errlen);
+    const int st = to_src(shards[i], i, srcs[(size_t)i], held[(size_t)i], err, errlen);
     if (st != ZH_OK) return st;
   }
   return read_multi_impl(ctxs, ndev, root, meta, srcs.data(), nshards, offset, shape, out, flags,

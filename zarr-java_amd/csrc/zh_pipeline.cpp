@@ -98,7 +98,7 @@ struct InJob {
   uint8_t* dst;
   int64_t len;
   const void* direct;  // non-null: DMA from here
-  std::vector<std::pair<int64_t, std::pair<const void*, int64_t>>> parts;
+  std::vector<std::pair<int64_t, std::pair<SrcRef, int64_t>>> parts;
 };
 
 // One device → host copy job of a decoded slab.
@@ -130,11 +130,11 @@ void in_jobs(zh_plan* p, int64_t slab, int64_t chunk, std::vector<InJob>& jobs,
   };
   for (size_t k = 0; k < p->h2d.size(); k++) {
     const int64_t off = p->h2d[k].first, len = p->h2d_len[k];
-    const uint8_t* src = (const uint8_t*)p->h2d[k].second;
+    const SrcRef& src = p->h2d[k].second;
     if (len <= 0) continue;
-    if (len >= kDirectMin && !is_file_addr(src) && host_pinned(src)) {
+    if (len >= kDirectMin && !src.is_file() && host_pinned(src.mem())) {
       flush();  // a window must not span (and overwrite) a directly copied range
-      jobs.push_back(InJob{slab, p->d_input + off, len, src, {}});
+      jobs.push_back(InJob{slab, p->d_input + off, len, src.mem(), {}});
       continue;
     }
     *any_pageable = true;
@@ -439,8 +439,8 @@ int read_pipelined(zh_ctx* ctx, const zh_array_meta* meta, const SrcDesc* srcs, 
             uint8_t* slot = (uint8_t*)ctx->ring_in[(size_t)k];
             std::string io;
             for (auto& part : J.parts) {
-              if (!is_file_addr(part.second.first)) {
-                copy_bytes(slot + part.first, part.second.first, part.second.second);
+              if (!part.second.first.is_file()) {
+                copy_bytes(slot + part.first, part.second.first.mem(), part.second.second);
                 continue;
               }
               // a store file's range (zh_array_read_files): read straight into the slot

@@ -249,7 +249,7 @@ static jint array_read_common(JNIEnv* env, zh_ctx* const* ctxs, int nctx, jintAr
     return throw_status(env, ZH_EINVAL, "output array size does not match the region");
   const jsize nchunks = (*env)->GetArrayLength(env, jchunks);
   units_of(&m, 0, u);
-  const SlabPlan SP = slab_plan(&m, r64, u, slab_cap_bytes() * (nctx > 1 ? nctx : 1));
+  const SlabPlan SP = slab_plan(&m, r64, u, slab_cap_bytes());
   const int a = SP.axis;
   for (int64_t s = o64[a]; st == ZH_OK && s < o64[a] + r64[a];) {
     const int64_t e = slab_end(&SP, s, o64[a] + r64[a]);
@@ -261,6 +261,13 @@ static jint array_read_common(JNIEnv* env, zh_ctx* const* ctxs, int nctx, jintAr
       break;
     }
     Pinned P;
+    /* the slab's chunk arrays stay referenced until pin_release: room for all of them (the
+     * JNI spec guarantees 16 local references) */
+    if ((*env)->EnsureLocalCapacity(env, cnt + 16) != 0) {
+      st = ZH_ENOMEM;
+      snprintf(err, sizeof err, "out of local references for %d chunk arrays", (int)cnt);
+      break;
+    }
     zh_chunk_src* srcs = (zh_chunk_src*)calloc((size_t)(cnt > 0 ? cnt : 1), sizeof(zh_chunk_src));
     if (!srcs || pin_alloc(&P, cnt + 1, 0) != ZH_OK) {
       free(srcs);
@@ -330,8 +337,44 @@ JNIEXPORT jint JNICALL Java_dev_zarr_zarrjava_hip_ZarrHip_arrayReadMulti(
                            jchunks, joffset, jregion, out);
 }
 
+/* Copies a Java string into malloc'd UTF-8 (NULL for a null string); *st = ZH_ENOMEM when the
+ * copy fails.  (GetStringUTFChars' modified UTF-8 equals UTF-8 for every path without NUL or
+ * supplementary characters.) */
+static char* dup_string(JNIEnv* env, jstring js, int* st) {
+  if (!js) return NULL;
+  const char* c = (*env)->GetStringUTFChars(env, js, NULL);
+  char* r = c ? strdup(c) : NULL;
+  if (c) (*env)->ReleaseStringUTFChars(env, js, c);
+  if (!r) *st = ZH_ENOMEM;
+  return r;
+}
+
+/* The chunk paths of a files call, each copied (null stays NULL). */
+static char** dup_paths(JNIEnv* env, jobjectArray jpaths, jsize n, int* st) {
+  char** paths = (char**)calloc((size_t)(n > 0 ? n : 1), sizeof(char*));
+  if (!paths) {
+    *st = ZH_ENOMEM;
+    return NULL;
+  }
+  for (jsize i = 0; *st == ZH_OK && i < n; i++) {
+    jstring js = (jstring)(*env)->GetObjectArrayElement(env, jpaths, i);
+    paths[i] = dup_string(env, js, st);
+    if (js) (*env)->DeleteLocalRef(env, js);
+  }
+  return paths;
+}
+
+static void free_paths(char** paths, jsize n, zh_file_store* store) {
+  for (jsize i = 0; paths && i < n; i++) free(paths[i]);
+  free(paths);
+  free((char*)store->root);
+  free((char*)store->name);
+}
+
 /* core.Array.read over a FilesystemStore (HipArray.read): paths[i] = StoreHandle.toPath() of the
- * i-th chunk of computeChunkCoords(shape, chunkShape, offset, regionShape), or null.  The library
+ * i-th chunk of computeChunkCoords(shape, chunkShape, offset, regionShape), or null; storeRoot =
+ * the store's directory and storeName = FilesystemStore.toString(), which StoreException's
+ * messages name (zh_file_store).  The library
  * reads the files itself (zh_array_read_files; with several contexts zh_array_read_files_multi,
  * one slab per device): no source array crosses the boundary, so per slab only the result is
  * held critical.  The paths are converted before any critical section
@@ -339,8 +382,8 @@ JNIEXPORT jint JNICALL Java_dev_zarr_zarrjava_hip_ZarrHip_arrayReadMulti(
  * NUL or supplementary characters). */
 JNIEXPORT jint JNICALL Java_dev_zarr_zarrjava_hip_ZarrHip_arrayReadFiles(
     JNIEnv* env, jclass cls, jlongArray jctxs, jintArray jm, jlongArray jshape, jintArray jchunk,
-    jintArray jinner, jintArray jorder, jbyteArray jfill, jobjectArray jpaths,
-    jlongArray joffset, jlongArray jregion, jobject out) {
+    jintArray jinner, jintArray jorder, jbyteArray jfill, jstring jroot, jstring jname,
+    jobjectArray jpaths, jlongArray joffset, jlongArray jregion, jobject out) {
   (void)cls;
   zh_array_meta m;
   int st = build_meta(env, jm, jshape, jchunk, jinner, jorder, jfill, &m);
@@ -361,24 +404,11 @@ JNIEXPORT jint JNICALL Java_dev_zarr_zarrjava_hip_ZarrHip_arrayReadFiles(
   if ((int64_t)(*env)->GetArrayLength(env, (jarray)out) != nel)
     return throw_status(env, ZH_EINVAL, "output array size does not match the region");
   const jsize n = (*env)->GetArrayLength(env, jpaths);
-  char** paths = (char**)calloc((size_t)(n > 0 ? n : 1), sizeof(char*));
-  if (!paths) return throw_status(env, ZH_ENOMEM, "out of host memory");
-  for (jsize i = 0; st == ZH_OK && i < n; i++) {
-    jstring js = (jstring)(*env)->GetObjectArrayElement(env, jpaths, i);
-    if (!js) continue;
-    const char* c = (*env)->GetStringUTFChars(env, js, NULL);
-    if (c) {
-      paths[i] = strdup(c);
-      (*env)->ReleaseStringUTFChars(env, js, c);
-    }
-    (*env)->DeleteLocalRef(env, js);
-    if (!c || !paths[i]) {
-      st = ZH_ENOMEM;
-      snprintf(err, sizeof err, "out of host memory");
-    }
-  }
+  zh_file_store store = {dup_string(env, jroot, &st), dup_string(env, jname, &st)};
+  char** paths = dup_paths(env, jpaths, n, &st);
+  if (st != ZH_OK) snprintf(err, sizeof err, "out of host memory");
   units_of(&m, 0, u);
-  const SlabPlan SP = slab_plan(&m, r64, u, slab_cap_bytes() * k);
+  const SlabPlan SP = slab_plan(&m, r64, u, slab_cap_bytes());
   const int a = SP.axis;
   for (int64_t s = o64[a]; st == ZH_OK && s < o64[a] + r64[a];) {
     const int64_t e = slab_end(&SP, s, o64[a] + r64[a]);
@@ -399,9 +429,9 @@ JNIEXPORT jint JNICALL Java_dev_zarr_zarrjava_hip_ZarrHip_arrayReadFiles(
     void* pin = (*env)->GetPrimitiveArrayCritical(env, (jarray)out, NULL);
     if (pin) {
       uint8_t* dst = (uint8_t*)pin + (size_t)((s - o64[a]) * SP.row);
-      st = k == 1 ? zh_array_read_files(ctxs[0], &m, (const char* const*)(paths + first), cnt,
-                                        so, ss, dst, 0, err, sizeof err)
-                  : zh_array_read_files_multi(ctxs, (int)k, 0, &m,
+      st = k == 1 ? zh_array_read_files(ctxs[0], &m, &store, (const char* const*)(paths + first),
+                                        cnt, so, ss, dst, 0, err, sizeof err)
+                  : zh_array_read_files_multi(ctxs, (int)k, 0, &m, &store,
                                               (const char* const*)(paths + first), cnt, so, ss,
                                               dst, 0, NULL, err, sizeof err);
       (*env)->ReleasePrimitiveArrayCritical(env, (jarray)out, pin, 0);
@@ -411,8 +441,7 @@ JNIEXPORT jint JNICALL Java_dev_zarr_zarrjava_hip_ZarrHip_arrayReadFiles(
     }
     s = e;
   }
-  for (jsize i = 0; i < n; i++) free(paths[i]);
-  free(paths);
+  free_paths(paths, n, &store);
   if (st == ZH_EUNSUPPORTED) return st;
   if (st != ZH_OK) return throw_status(env, st, err);
   return 0;
@@ -635,7 +664,7 @@ JNIEXPORT jint JNICALL Java_dev_zarr_zarrjava_hip_ZarrHip_arrayReadPieces(
     return throw_status(env, ZH_EINVAL, "output array size does not match the region");
   const jsize n = (*env)->GetArrayLength(env, jidx);
   units_of(&m, 1, u);
-  const SlabPlan SP = slab_plan(&m, r64, u, slab_cap_bytes() * k);
+  const SlabPlan SP = slab_plan(&m, r64, u, slab_cap_bytes());
   const int a = SP.axis;
   for (int64_t s = o64[a]; st == ZH_OK && s < o64[a] + r64[a];) {
     const int64_t e = slab_end(&SP, s, o64[a] + r64[a]);
@@ -780,7 +809,7 @@ static uint8_t* copy_region_out(JNIEnv* env, jobject data, size_t rbytes) {
 JNIEXPORT jint JNICALL Java_dev_zarr_zarrjava_hip_ZarrHip_arrayWriteFiles(
     JNIEnv* env, jclass cls, jlong ctx, jintArray jm, jlongArray jshape, jintArray jchunk,
     jintArray jinner, jintArray jorder, jbyteArray jfill, jlongArray joffset,
-    jlongArray jregion, jobject data, jobjectArray jpaths) {
+    jlongArray jregion, jobject data, jstring jroot, jstring jname, jobjectArray jpaths) {
   (void)cls;
   zh_array_meta m;
   int st = build_meta(env, jm, jshape, jchunk, jinner, jorder, jfill, &m);
@@ -795,22 +824,9 @@ JNIEXPORT jint JNICALL Java_dev_zarr_zarrjava_hip_ZarrHip_arrayWriteFiles(
   /* a Java array of another length than the region: never read past its end */
   if ((int64_t)(*env)->GetArrayLength(env, (jarray)data) != want) return ZH_EUNSUPPORTED;
   const jsize n = (*env)->GetArrayLength(env, jpaths);
-  char** paths = (char**)calloc((size_t)(n > 0 ? n : 1), sizeof(char*));
-  if (!paths) return throw_status(env, ZH_ENOMEM, "out of host memory");
-  for (jsize i = 0; st == ZH_OK && i < n; i++) {
-    jstring js = (jstring)(*env)->GetObjectArrayElement(env, jpaths, i);
-    if (!js) continue;
-    const char* c = (*env)->GetStringUTFChars(env, js, NULL);
-    if (c) {
-      paths[i] = strdup(c);
-      (*env)->ReleaseStringUTFChars(env, js, c);
-    }
-    (*env)->DeleteLocalRef(env, js);
-    if (!c || !paths[i]) {
-      st = ZH_ENOMEM;
-      snprintf(err, sizeof err, "out of host memory");
-    }
-  }
+  zh_file_store store = {dup_string(env, jroot, &st), dup_string(env, jname, &st)};
+  char** paths = dup_paths(env, jpaths, n, &st);
+  if (st != ZH_OK) snprintf(err, sizeof err, "out of host memory");
   uint8_t* src = NULL;
   if (st == ZH_OK) {
     src = copy_region_out(env, data, (size_t)want * (size_t)m.dtype_size);
@@ -820,11 +836,10 @@ JNIEXPORT jint JNICALL Java_dev_zarr_zarrjava_hip_ZarrHip_arrayWriteFiles(
     }
   }
   if (st == ZH_OK)
-    st = zh_array_write_files((zh_ctx*)(intptr_t)ctx, &m, src, o64, r64,
+    st = zh_array_write_files((zh_ctx*)(intptr_t)ctx, &m, src, o64, r64, &store,
                               (const char* const*)paths, n, 0, NULL, err, sizeof err);
   free(src);
-  for (jsize i = 0; i < n; i++) free(paths[i]);
-  free(paths);
+  free_paths(paths, n, &store);
   if (st == ZH_EUNSUPPORTED) return st;
   if (st != ZH_OK) return throw_status(env, st, err);
   return 0;

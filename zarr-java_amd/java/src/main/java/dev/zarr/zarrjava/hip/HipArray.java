@@ -75,8 +75,9 @@ public class HipArray extends Array {
             ucar.ma2.Array out = ucar.ma2.Array.factory(md.dataType().getMA2DataType(),
                     Utils.toIntArray(shape));
             int st = ZarrHip.arrayReadFiles(ctxs, chain.meta, chain.shape, chain.chunkShape,
-                    chain.innerShape, chain.order, chain.fill, paths, offset, shape,
-                    out.getStorage());
+                    chain.innerShape, chain.order, chain.fill,
+                    ZarrHip.storeRoot(storeHandle.store), storeHandle.store.toString(), paths,
+                    offset, shape, out.getStorage());
             return st == 0 ? out : super.read(offset, shape, parallel);
         }
         final ShardPieces[] shards = new ShardPieces[coords.length];
@@ -173,7 +174,8 @@ public class HipArray extends Array {
             }
             if (ZarrHip.arrayWriteFiles(ZarrHip.ctx(), chain.meta, chain.shape, chain.chunkShape,
                     chain.innerShape, chain.order, chain.fill, offset, shape,
-                    array.copyTo1DJavaArray(), paths) == 0) {
+                    array.copyTo1DJavaArray(), ZarrHip.storeRoot(storeHandle.store),
+                    storeHandle.store.toString(), paths) == 0) {
                 return;
             }
         }

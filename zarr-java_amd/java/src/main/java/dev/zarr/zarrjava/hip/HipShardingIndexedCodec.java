@@ -74,6 +74,7 @@ public class HipShardingIndexedCodec extends ShardingIndexedCodec {
                 int st = ZarrHip.arrayReadFiles(new long[]{ZarrHip.codecCtx()}, chain.meta,
                         shardShape,
                         chain.chunkShape, chain.innerShape, chain.order, chain.fill,
+                        ZarrHip.storeRoot(chunkHandle.store), chunkHandle.store.toString(),
                         new String[]{path.toString()}, offset, part, out.getStorage());
                 if (st == 0) return out;
             }

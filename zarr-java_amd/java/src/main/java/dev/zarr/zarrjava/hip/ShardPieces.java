@@ -74,8 +74,11 @@ final class ShardPieces {
         if (ib == null) return null;
         byte[] index = bytes(ib);
         // StoreHandle.getSize() is -1 when the store cannot tell (an HTTP HEAD without
-        // Content-Length, a failed HEAD): the ranges are then bounded by the reads themselves
-        long size = h.getSize();
+        // Content-Length, a failed HEAD): the ranges are then bounded by the reads themselves.
+        // A FilesystemStore range read past the end of the file returns zeros
+        // (FilesystemStore.get(keys, start, end), M/store/FilesystemStore.java:84-102), so no
+        // entry is out of its reach by offset: the size bounds nothing there either.
+        long size = h.store instanceof dev.zarr.zarrjava.store.FilesystemStore ? -1 : h.getSize();
         if (size < 0) size = -1;
         if (index.length < isz) {  // the device reports "Shard ... is smaller than its index"
             return new ShardPieces(index, size, new long[0], new long[0], new byte[0][]);

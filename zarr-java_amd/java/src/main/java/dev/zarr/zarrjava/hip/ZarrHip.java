@@ -123,12 +123,15 @@ public final class ZarrHip {
     /**
      * core.Array.write of a region of whole chunks into a FilesystemStore
      * (zh_array_write_files): paths[i] is StoreHandle.toPath() of the i-th chunk of
-     * computeChunkCoords; the library encodes on the device and writes (all fill_value:
-     * deletes) the chunk files.  Returns 0, or UNSUPPORTED when the caller must write itself.
+     * computeChunkCoords, storeRoot / storeName the store's directory and toString() (the
+     * StoreException text names them); the library encodes on the device and writes (all
+     * fill_value: deletes) the chunk files.  Returns 0, or UNSUPPORTED when the caller must
+     * write itself.
      */
     static native int arrayWriteFiles(long ctx, int[] meta, long[] shape, int[] chunkShape,
                                       int[] innerShape, int[] order, byte[] fill, long[] offset,
-                                      long[] regionShape, Object data, String[] paths);
+                                      long[] regionShape, Object data, String storeRoot,
+                                      String storeName, String[] paths);
 
     /** ShardingIndexedCodec.decodePartial over one shard's bytes. */
     static native int shardDecodePartial(long ctx, int[] meta, long[] shape, int[] chunkShape,
@@ -163,11 +166,18 @@ public final class ZarrHip {
      * StoreHandle.toPath() of the i-th chunk of computeChunkCoords (null: no key); the library
      * reads the files (exists, the index and the referenced ranges, or whole chunks) with the
      * pipelined read, so no chunk bytes cross into the Java heap.  An unreadable file throws
-     * dev.zarr.zarrjava.store.StoreException.
+     * dev.zarr.zarrjava.store.StoreException naming storeName (FilesystemStore.toString())
+     * and the key below storeRoot (the store's directory).
      */
     static native int arrayReadFiles(long[] ctxs, int[] meta, long[] shape, int[] chunkShape,
-                                     int[] innerShape, int[] order, byte[] fill, String[] paths,
+                                     int[] innerShape, int[] order, byte[] fill,
+                                     String storeRoot, String storeName, String[] paths,
                                      long[] offset, long[] regionShape, Object out);
+
+    /** The directory of a FilesystemStore (its keys resolve below it). */
+    static String storeRoot(dev.zarr.zarrjava.store.Store store) {
+        return new dev.zarr.zarrjava.store.StoreHandle(store).toPath().toString();
+    }
 
     /** ShardingIndexedCodec.decodePartial over one shard as index + pieces. */
     static native int shardDecodePieces(long ctx, int[] meta, long[] shape, int[] chunkShape,

@@ -85,6 +85,11 @@ class zh_shard_src(C.Structure):
                 ("npieces", C.c_int64)]
 
 
+class zh_file_store(C.Structure):
+    """A FilesystemStore as the file reads name it (zarrhip.h zh_file_store)."""
+    _fields_ = [("root", C.c_char_p), ("name", C.c_char_p)]
+
+
 def make_meta(shape, chunk_shape, dtype_size, *, fill=b"\0" * 8, is_bool=False, sharded=False,
               inner_chunk_shape=None, transpose_order=None, endian=ZH_ENDIAN_LITTLE,
               index_endian=ZH_ENDIAN_LITTLE, index_crc32c=True, index_location=ZH_INDEX_END,

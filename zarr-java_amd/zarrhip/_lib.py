@@ -21,6 +21,7 @@ CH = C.c_char_p
 PI64 = C.POINTER(C.c_int64)
 PI32 = C.POINTER(C.c_int32)
 PMETA = C.POINTER(A.zh_array_meta)
+PSTORE = C.POINTER(A.zh_file_store)
 
 _SIGS = {
     "zh_version": (CH, []),
@@ -67,13 +68,13 @@ _SIGS = {
     "zh_sharding_decode_pieces": (C.c_int, [P, PMETA, C.POINTER(A.zh_shard_src), PI64, PI32, P,
                                             U32, P, CH, SZ]),
     "zh_host_staging": (C.c_int, [P, SZ, C.POINTER(P)]),
-    "zh_array_read_files": (C.c_int, [P, PMETA, C.POINTER(C.c_char_p), I64, PI64, PI64, P, U32,
-                                      CH, SZ]),
-    "zh_debug_file_reads": (I64, [PMETA, C.POINTER(C.c_char_p), I64, PI64, PI64, PI64, I64, CH,
-                                  SZ]),
-    "zh_array_write_files": (C.c_int, [P, PMETA, P, PI64, PI64, C.POINTER(C.c_char_p), I64, U32,
-                                       PI64, CH, SZ]),
-    "zh_array_read_files_multi": (C.c_int, [C.POINTER(P), C.c_int, C.c_int, PMETA,
+    "zh_array_read_files": (C.c_int, [P, PMETA, PSTORE, C.POINTER(C.c_char_p), I64, PI64, PI64,
+                                      P, U32, CH, SZ]),
+    "zh_debug_file_reads": (I64, [PMETA, PSTORE, C.POINTER(C.c_char_p), I64, PI64, PI64, PI64,
+                                  I64, CH, SZ]),
+    "zh_array_write_files": (C.c_int, [P, PMETA, P, PI64, PI64, PSTORE, C.POINTER(C.c_char_p),
+                                       I64, U32, PI64, CH, SZ]),
+    "zh_array_read_files_multi": (C.c_int, [C.POINTER(P), C.c_int, C.c_int, PMETA, PSTORE,
                                             C.POINTER(C.c_char_p), I64, PI64, PI64, P, U32, PI32,
                                             CH, SZ]),
     "zh_array_encoded_bound": (I64, [PMETA]),
@@ -355,24 +356,28 @@ class DeviceContext:
         del keep
         check(st, err)
 
-    def array_read_files(self, meta, paths, offset, shape, out, flags=0):
+    def array_read_files(self, meta, paths, offset, shape, out, flags=0, store=None):
         """zh_array_read_files: the chunks as files of a FilesystemStore (None or a path that
-        is not a regular file = missing key); the library does the store reads."""
+        is not a regular file = missing key); the library does the store reads.  `store`: the
+        store the paths belong to (file_store), for StoreException's text."""
         arr = path_array(paths)
         err = C.create_string_buffer(1024)
-        st = self.L.zh_array_read_files(self.h, C.byref(meta), arr, len(paths), i64arr(offset),
-                                        i64arr(shape), P(out), int(flags), err, 1024)
+        fs = file_store(store)
+        st = self.L.zh_array_read_files(self.h, C.byref(meta), fs, arr, len(paths),
+                                        i64arr(offset), i64arr(shape), P(out), int(flags), err,
+                                        1024)
         check(st, err)
 
-    def array_write_files(self, meta, src, offset, shape, paths, flags=0):
+    def array_write_files(self, meta, src, offset, shape, paths, flags=0, store=None):
         """zh_array_write_files: encode the region (host pointer, or device with ZH_SRC_DEVICE)
         and write / delete the chunk files; returns the bytes written per chunk (0: deleted)."""
         n = len(paths)
         sizes = (C.c_int64 * max(1, n))()
         err = C.create_string_buffer(1024)
+        fs = file_store(store)
         st = self.L.zh_array_write_files(self.h, C.byref(meta), P(src), i64arr(offset),
-                                         i64arr(shape), path_array(paths), n, int(flags), sizes,
-                                         err, 1024)
+                                         i64arr(shape), fs, path_array(paths), n, int(flags),
+                                         sizes, err, 1024)
         check(st, err)
         return [int(sizes[i]) for i in range(n)]
 
@@ -511,31 +516,47 @@ def path_array(paths):
         *[None if p is None else os.fsencode(p) for p in paths])
 
 
-def file_reads(meta, paths, offset, shape):
+def file_store(store):
+    """zh_file_store* for a store argument: None (the filesystem root), a directory (str or
+    path-like: name "file://<dir>") or a (root, name) pair; the struct keeps its strings."""
+    if store is None:
+        return None
+    if isinstance(store, tuple):
+        root, name = store
+    else:
+        root, name = os.fspath(store), None
+    fs = A.zh_file_store(os.fsencode(root), None if name is None else name.encode())
+    return C.pointer(fs)
+
+
+def file_reads(meta, paths, offset, shape, store=None):
     """zh_debug_file_reads: [(chunk index, file offset, bytes)] the files read would make
     (raises ZhError with the read's status and message)."""
     L = lib()
     arr = path_array(paths)
     err = C.create_string_buffer(1024)
-    n = L.zh_debug_file_reads(C.byref(meta), arr, len(paths), i64arr(offset), i64arr(shape),
-                              None, 0, err, 1024)
+    fs = file_store(store)
+    n = L.zh_debug_file_reads(C.byref(meta), fs, arr, len(paths), i64arr(offset),
+                              i64arr(shape), None, 0, err, 1024)
     if n < 0:
         check(-n, err)
     buf = (C.c_int64 * max(1, 3 * n))()
-    L.zh_debug_file_reads(C.byref(meta), arr, len(paths), i64arr(offset), i64arr(shape), buf, n,
-                          err, 1024)
+    L.zh_debug_file_reads(C.byref(meta), fs, arr, len(paths), i64arr(offset), i64arr(shape),
+                          buf, n, err, 1024)
     return [tuple(buf[3 * k:3 * k + 3]) for k in range(n)]
 
 
-def array_read_files_multi(ctxs, meta, paths, offset, shape, out, flags=0, root=0):
+def array_read_files_multi(ctxs, meta, paths, offset, shape, out, flags=0, root=0,
+                           store=None):
     """zh_array_read_files_multi: the files form of array_read_multi; returns the routes."""
     L = lib()
     hs = (P * len(ctxs))(*[c.h for c in ctxs])
     routes = (C.c_int32 * len(ctxs))()
     err = C.create_string_buffer(1024)
-    st = L.zh_array_read_files_multi(hs, len(ctxs), int(root), C.byref(meta), path_array(paths),
-                                     len(paths), i64arr(offset), i64arr(shape), P(out),
-                                     int(flags), routes, err, 1024)
+    fs = file_store(store)
+    st = L.zh_array_read_files_multi(hs, len(ctxs), int(root), C.byref(meta), fs,
+                                     path_array(paths), len(paths), i64arr(offset),
+                                     i64arr(shape), P(out), int(flags), routes, err, 1024)
     check(st, err)
     return list(routes)
 

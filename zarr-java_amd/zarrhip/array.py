@@ -297,12 +297,19 @@ class Array:
             return None
         isz = _lib.lib().zh_shard_index_size(C.byref(self.zmeta))
         start = self.chain.chain["index_location"] == A.ZH_INDEX_START
-        idx = h.read(0, isz) if start else h.read(-isz)
+        try:
+            idx = h.read(0, isz) if start else h.read(-isz)
+        except ValueError:  # a suffix longer than the file (the reference's position(< 0))
+            idx = h.read()  # what it holds: the device reports "Shard [...] smaller than its index"
         if idx is None:
             return None
         idx = bytes(idx)
+        from .store import FilesystemStore
         size = h.size() if hasattr(h, "size") else None
-        size = -1 if size is None else int(size)
+        # a FilesystemStore range read past the end of the file returns zeros
+        # (FilesystemStore.get(keys, start, end), FilesystemStore.java:84-102): no entry is out
+        # of reach by its offset, so the shard size bounds nothing
+        size = -1 if size is None or isinstance(h.store, FilesystemStore) else int(size)
         ibuf = np.frombuffer(idx if idx else b"\0", np.uint8)
         keep = [ibuf]
         self._count_staged(len(idx))
@@ -386,6 +393,12 @@ class Array:
             return None
         return [st._p(self._handle(c).keys) for c in coords]
 
+    def _file_store(self):
+        """The FilesystemStore the chunk files belong to, as (root, FilesystemStore.toString())
+        for StoreException's text."""
+        st = self.storeHandle.store
+        return (st.path, repr(st))
+
     # ---------------------------------------------------------------- read
     def read(self, offset=None, shape=None, parallel=True):
         """core.Array.read → numpy array (C order, the array's dtype)."""
@@ -407,10 +420,10 @@ class Array:
             try:
                 if len(devs) > 1:  # one slab per device, each over its own PCIe link
                     _lib.array_read_files_multi(devs, self.zmeta, paths, offset, shape,
-                                                out.ctypes.data, 0)
+                                                out.ctypes.data, 0, store=self._file_store())
                 else:
                     devs[0].array_read_files(self.zmeta, paths, offset, shape, out.ctypes.data,
-                                             0)
+                                             0, store=self._file_store())
             except _lib.ZhError as e:
                 raise_for(e)
             self.last_read_timing = {"prep_s": t0 - t_enter, "stage_s": t1 - t0,
@@ -493,7 +506,8 @@ class Array:
             for d in range(self.ndim):
                 m.shape[d] = cs[d]
             try:
-                device().array_read_files(m, paths, [0] * self.ndim, cs, out.ctypes.data, 0)
+                device().array_read_files(m, paths, [0] * self.ndim, cs, out.ctypes.data, 0,
+                                          store=self._file_store())
             except _lib.ZhError as e:
                 raise_for(e)
             return out
@@ -543,7 +557,8 @@ class Array:
         paths = None if keep_fill else self._file_paths(coords, [dev])
         if paths is not None:  # the library writes (and deletes) the chunk files itself
             try:
-                dev.array_write_files(self.zmeta, data.ctypes.data, offset, shape, paths)
+                dev.array_write_files(self.zmeta, data.ctypes.data, offset, shape, paths,
+                                      store=self._file_store())
             except _lib.ZhError as e:
                 raise_for(e)
             return

@@ -66,6 +66,11 @@ class FilesystemStore(Store):
         return os.path.isfile(self._p(keys))
 
     def get(self, keys, start=None, end=None):
+        """get(keys) / get(keys, start) / get(keys, start, end) (FilesystemStore.java:47-102):
+        a negative start counts from the end (a resolved start below 0 raises, as the
+        channel's position(< 0) does); a [start, end) read returns end - start bytes, zeros
+        past the end of the file (the reference allocates the buffer and reads what the file
+        has)."""
         p = self._p(keys)
         try:
             with open(p, "rb") as f:
@@ -73,9 +78,12 @@ class FilesystemStore(Store):
                     return f.read()
                 size = os.fstat(f.fileno()).st_size
                 s = start if start >= 0 else size + start
+                if s < 0:
+                    raise ValueError("newPosition < 0: (%d < 0)" % s)
                 e = size if end is None else end
                 f.seek(s)
-                return f.read(e - s)
+                b = f.read(max(0, e - s))
+                return b + bytes(max(0, e - s - len(b))) if end is not None else b
         except FileNotFoundError:
             return None
 
@@ -92,10 +100,11 @@ class FilesystemStore(Store):
                 got = 0
                 while got < len(view):
                     r = f.readinto(view[got:])
-                    if not r:
+                    if not r:  # the end of the file: the rest of [start, end) reads as zeros
+                        view[got:] = bytes(len(view) - got)
                         break
                     got += r
-                return got
+                return len(view)
         except FileNotFoundError:
             return None
 
