@@ -1,6 +1,8 @@
-"""Multi-process (world_size 2, gloo on CPU) coverage of the N>1 paths: bench.py's
-barrier / max-over-ranks harness and zarrhip.parallel's slab partition + gather.  The
-per-rank decode here is the oracle (test infrastructure); on GPUs it is the HIP path."""
+"""Multi-process (world_size 2 and 3, gloo on CPU) coverage of the N>1 paths: bench.py's
+barrier / max-over-ranks harness and zarrhip.parallel's slab partition and region gather
+(RegionGather / distributed_read, the same code that runs over RCCL on GPUs).  The per-rank
+decode here is the oracle (test infrastructure); on GPUs it is the HIP path (PlanDecoder /
+array_decoder)."""
 import os
 import socket
 
@@ -71,28 +73,58 @@ def _worker(rank, world, port, tmp):
     shards = encode_oracle(meta, arr)
     allc = O.compute_chunk_coords(shape, [1, 8, 8, 8], [0] * 4, shape)
     pos = {c: i for i, c in enumerate(allc)}
+    calls = []
 
-    def decode(off, shp):
-        sel = O.compute_chunk_coords(shape, [1, 8, 8, 8], off, shp)
-        raw = O.array_read(meta, [shards[pos[c]] for c in sel], off, shp)
-        return np.frombuffer(raw, np.uint32).reshape(shp)
+    def decode(po, ps, dst):  # the oracle stands in for the device decode (CPU test)
+        calls.append((list(po), list(ps)))
+        sel = O.compute_chunk_coords(shape, [1, 8, 8, 8], po, ps)
+        raw = O.array_read(meta, [shards[pos[c]] for c in sel], po, ps)
+        dst.numpy()[:] = np.frombuffer(raw, np.uint8)
 
-    full = PP.distributed_read(decode, [0] * 4, shape, dist, root=0, align=4)
+    # the product's distributed read: slabs on the inner-chunk grid, pieces of 2 rows
+    full = PP.distributed_read(decode, [0] * 4, shape, np.uint32, align=4,
+                               piece_bytes=2 * 20 * 12 * 4)
+    # an unaligned region at an offset: the same gather, region-relative placement
+    off2, shp2 = [0, 3, 2, 1], [1, 19, 15, 9]
+    part = PP.distributed_read(decode, off2, shp2, np.uint32, align=1,
+                               piece_bytes=3 * 15 * 9 * 4)
     if rank == 0:
         np.save(os.path.join(tmp, "full.npy"), full)
+        np.save(os.path.join(tmp, "part.npy"), part)
         np.save(os.path.join(tmp, "want.npy"), arr)
     with open(os.path.join(tmp, f"max{rank}.txt"), "w") as f:
         f.write(str(mx))
+    with open(os.path.join(tmp, f"calls{rank}.txt"), "w") as f:
+        f.write(repr(calls))
     d.close()
 
 
-def test_two_rank_gloo_partition_gather_and_bench_harness(tmp_path):
+@pytest.mark.parametrize("world", [2, 3])
+def test_gloo_distributed_read_and_bench_harness(tmp_path, world):
+    """zarrhip.parallel.distributed_read (RegionGather: bounded pieces, decode(k) before
+    send(k), the root's own slab decoded into place) with gloo at world sizes 2 and 3: the
+    assembled region equals the array for the whole region and for an unaligned part at an
+    offset; each rank decoded exactly its own pieces, in order; bench.Dist's max over ranks."""
+    import ast
     import torch.multiprocessing as mp
-    world = 2
     mp.spawn(_worker, args=(world, free_port(), str(tmp_path)), nprocs=world, join=True)
-    np.testing.assert_array_equal(np.load(tmp_path / "full.npy"), np.load(tmp_path / "want.npy"))
+    want = np.load(tmp_path / "want.npy")
+    np.testing.assert_array_equal(np.load(tmp_path / "full.npy"), want)
+    np.testing.assert_array_equal(np.load(tmp_path / "part.npy"), want[:, 3:22, 2:17, 1:10])
     for r in range(world):
-        assert float(open(tmp_path / f"max{r}.txt").read()) == 2.0
+        assert float(open(tmp_path / f"max{r}.txt").read()) == float(world)
+    shape = [1, 24, 20, 12]
+    for (off, shp, align, cap) in (([0] * 4, shape, 4, 2 * 20 * 12 * 4),
+                                   ([0, 3, 2, 1], [1, 19, 15, 9], 1, 3 * 15 * 9 * 4)):
+        parts = P.slab_partition(off, shp, world, align)
+        rel = [([o - b for o, b in zip(po, off)], ps) for po, ps in parts]
+        sched = P.gather_pieces(shp, rel, 4, cap, align)
+        for r in range(world):
+            calls = ast.literal_eval(open(tmp_path / f"calls{r}.txt").read())
+            mine = [([a + b for a, b in zip(po, off)], ps) for po, ps, _, _ in sched[r]]
+            assert all(c in calls for c in mine)
+            idx = [calls.index(c) for c in mine]
+            assert idx == sorted(idx) and len(mine) > 1  # in order, several pieces
 
 
 @pytest.mark.parametrize("seed", range(12))

@@ -410,25 +410,45 @@ class Array:
         dt = self.metadata.data_type.numpy
         if any(s == 0 for s in shape):
             return np.zeros(shape, dtype=dt)
+        out = np.empty(shape, dtype=dt)
+        self._read_into(offset, shape, out.ctypes.data, 0, devices(), parallel, t_enter)
+        return out
+
+    def read_device(self, offset, shape, out_ptr, dev=None, parallel=True):
+        """core.Array.read delivered to device memory: the C-order region is written to
+        `out_ptr` on `dev`'s device (a DeviceContext; default the first context) and nothing
+        is copied back to the host (ZH_OUT_DEVICE).  The store I/O is the same as read()'s
+        (for a FilesystemStore the library's own file reads).  The per-rank decode of
+        zarrhip.parallel.array_decoder."""
+        t_enter = time.perf_counter()
+        offset = [int(o) for o in offset]
+        shape = [int(s) for s in shape]
+        self._check_region(offset, shape)
+        if any(s == 0 for s in shape):
+            return
+        self._read_into(offset, shape, int(out_ptr), A.ZH_OUT_DEVICE,
+                        [dev if dev is not None else device()], parallel, t_enter)
+
+    def _read_into(self, offset, shape, out_addr, flags, devs, parallel, t_enter):
+        """The device read of a checked, non-empty region into out_addr (host memory, or
+        device memory with flags ZH_OUT_DEVICE and one context)."""
         coords = self._chunk_coords(offset, shape)
         t0 = time.perf_counter()
-        out = np.empty(shape, dtype=dt)
-        devs = devices()
         paths = self._file_paths(coords, devs)
         if paths is not None:  # the library reads the store's files itself
             t1 = time.perf_counter()
             try:
                 if len(devs) > 1:  # one slab per device, each over its own PCIe link
                     _lib.array_read_files_multi(devs, self.zmeta, paths, offset, shape,
-                                                out.ctypes.data, 0, store=self._file_store())
+                                                out_addr, flags, store=self._file_store())
                 else:
-                    devs[0].array_read_files(self.zmeta, paths, offset, shape, out.ctypes.data,
-                                             0, store=self._file_store())
+                    devs[0].array_read_files(self.zmeta, paths, offset, shape, out_addr,
+                                             flags, store=self._file_store())
             except _lib.ZhError as e:
                 raise_for(e)
             self.last_read_timing = {"prep_s": t0 - t_enter, "stage_s": t1 - t0,
                                      "device_s": time.perf_counter() - t1, "files": True}
-            return out
+            return
         lease = []  # staging buffers of this read, back to the pool after the device read
         sharded = self.chain.chain["sharded"]
         try:
@@ -465,10 +485,10 @@ class Array:
                                                              len(s[1]))]))
                     if len(devs) > 1:
                         _lib.array_read_pieces_multi(devs, self.zmeta, shards, offset, shape,
-                                                     out.ctypes.data, 0)
+                                                     out_addr, flags)
                     else:
                         devs[0].array_read_pieces(self.zmeta, shards, offset, shape,
-                                                  out.ctypes.data, 0)
+                                                  out_addr, flags)
                 else:
                     # views of the staged bytes (the library only reads them); an empty but
                     # present chunk keeps a non-null pointer (null = missing key → fill)
@@ -480,9 +500,9 @@ class Array:
                             for b, s in zip(bufs, sources)]
                     if len(devs) > 1:  # one slab per device, each D2H'd into its slice of `out`
                         _lib.array_read_multi(devs, self.zmeta, srcs, offset, shape,
-                                              out.ctypes.data, 0)
+                                              out_addr, flags)
                     else:
-                        devs[0].array_read(self.zmeta, srcs, offset, shape, out.ctypes.data, 0)
+                        devs[0].array_read(self.zmeta, srcs, offset, shape, out_addr, flags)
             except _lib.ZhError as e:
                 raise_for(e)
             finally:  # the call has consumed the staged bytes (it returns after its copies)
@@ -491,7 +511,6 @@ class Array:
             staging_pool.give(lease)
         self.last_read_timing = {"prep_s": t0 - t_enter, "stage_s": t1 - t0,
                                  "device_s": time.perf_counter() - t1}
-        return out
 
     def readChunk(self, coords):
         """core.Array.readChunk (M/core/Array.java:167-182)."""

@@ -121,38 +121,181 @@ def gather_pieces_p2p(tdist, grp, rank, world, sched, send_buf, region, decode=N
     return works
 
 
-def assemble(slabs, shape, axis):
-    """Concatenate per-rank slabs (in rank order) into the full region."""
-    parts = [np.asarray(s) for s in slabs if np.asarray(s).size]
-    full = np.concatenate(parts, axis=axis) if parts else np.zeros(shape)
-    assert list(full.shape) == list(shape)
-    return full
+class PlanDecoder:
+    """decode(piece_offset, piece_shape, dst) for RegionGather over device-resident chunk
+    sources: one zh plan per piece (created on its first use and kept, so a repeated read plans
+    nothing), executed asynchronously on torch's current stream into `dst` (a CUDA byte
+    tensor): a send that follows on that stream waits for exactly this piece's decode.
+    `sources(piece_offset, piece_shape)` gives the piece's chunk sources in computeChunkCoords
+    order ((device pointer, nbytes) or (None, 0)).  wait() reports the plans' deferred device
+    errors (the reference's messages); close() frees them."""
+
+    def __init__(self, dev, meta, sources, flags=None):
+        from . import _abi as A
+        self.dev, self.meta, self.sources = dev, meta, sources
+        self.flags = (A.ZH_SRC_DEVICE | A.ZH_OUT_DEVICE) if flags is None else flags
+        self.plans = {}
+
+    def plan(self, po, ps):
+        key = (tuple(po), tuple(ps))
+        p = self.plans.get(key)
+        if p is None:
+            p = self.dev.plan(self.meta, self.sources(po, ps), list(po), list(ps), self.flags)
+            self.plans[key] = p
+        return p
+
+    def __call__(self, po, ps, dst):
+        import torch
+        self.plan(po, ps).execute(dst.data_ptr(), torch.cuda.current_stream(dst.device).cuda_stream)
+
+    def wait(self):
+        for p in self.plans.values():
+            p.wait()
+
+    def close(self):
+        for p in self.plans.values():
+            p.close()
+        self.plans.clear()
 
 
-def distributed_read(decode, offset, shape, dist, root=0, align=1):
-    """Each rank decodes its slab with `decode(offset, shape) -> np.ndarray` (the device
-    read, e.g. zarrhip.Array.read); the root gathers and returns the full region (other
-    ranks return their slab).  `dist` is an initialised torch.distributed module."""
-    import torch
-    world, rank = dist.get_world_size(), dist.get_rank()
-    parts = slab_partition(offset, shape, world, align)
-    ax = slab_axis(shape, world)
-    so, ss = parts[rank]
-    mine = decode(so, ss) if all(s > 0 for s in ss) else None
-    # gather as flat byte tensors of the largest slab (gather needs equal sizes)
-    sizes = [int(np.prod(s)) for _, s in parts]
-    dts = [None] * world
-    dist.all_gather_object(dts, None if mine is None else np.dtype(mine.dtype).str)
-    dt = np.dtype(next(d for d in dts if d is not None))
-    itemsize = dt.itemsize
-    nmax = max(sizes) * itemsize
-    buf = torch.zeros(nmax, dtype=torch.uint8)
-    if mine is not None:
-        buf[: mine.nbytes] = torch.from_numpy(np.ascontiguousarray(mine).view(np.uint8).ravel())
-    gl = [torch.zeros(nmax, dtype=torch.uint8) for _ in range(world)] if rank == root else None
-    dist.gather(buf, gl, dst=root)
-    if rank != root:
-        return mine
-    slabs = [gl[r][: sizes[r] * itemsize].numpy().view(dt).reshape(parts[r][1])
-             for r in range(world)]
-    return assemble(slabs, shape, ax)
+def array_decoder(array, dev=None):
+    """decode(piece_offset, piece_shape, dst) for RegionGather over a zarrhip.Array: the piece
+    is core.Array.read from the array's store (for a FilesystemStore the library's own file
+    reads) straight into `dst` — device memory (Array.read_device, ZH_OUT_DEVICE) for a CUDA
+    tensor, host memory for a CPU tensor (the gloo form).  Synchronous: the call returns after
+    the piece is in `dst`."""
+    import numpy as _np
+
+    def decode(po, ps, dst):
+        if dst.is_cuda:
+            array.read_device(po, ps, dst.data_ptr(), dev)
+        else:
+            got = array.read(po, ps)
+            dst.numpy()[:] = _np.ascontiguousarray(got).view(_np.uint8).ravel()
+    return decode
+
+
+class RegionGather:
+    """One region read spread over the ranks of a process group and assembled on the root
+    (the reference's ForkJoin loop over chunks, M/core/Array.java:403-407, becomes
+    one slab per rank).  The region splits into contiguous C-order slabs (slab_partition, on the
+    inner-chunk grid `align`); every slab is cut into pieces of at most `piece_bytes`
+    (gather_pieces).  run(decode) decodes each piece and sends it point-to-point into its place
+    in the root's region buffer as soon as its own decode is done, so the decode of piece k+1
+    overlaps the transfer of piece k, and the root receives round k of every peer as one batch
+    (the peers' links in parallel).  The root decodes its own slab straight into the region, on
+    a side stream (device) so that its receives never wait for it.
+
+    Backends: an NCCL (= RCCL on ROCm) group moves CUDA byte tensors over xGMI (device-resident
+    read: no host memory on the data path); a gloo group moves CPU tensors (the host form, and
+    the form the CPU tests drive).  `decode(piece_offset, piece_shape, dst)` writes the piece's
+    C-order bytes into `dst` (a byte tensor on the group's side: enqueued on torch's current
+    stream for CUDA, or synchronously); PlanDecoder and array_decoder are the two product ones.
+    With decode=None the buffers already hold the slabs (send() only).  The buffers (the send
+    slab on peers, the region on the root) are allocated once and reused by every run()."""
+
+    def __init__(self, offset, shape, itemsize, group=None, root=0, align=1,
+                 piece_bytes=1 << 30, device=None, region=None, send=None):
+        import torch
+        import torch.distributed as tdist
+        self.torch, self.tdist = torch, tdist
+        self.group = group if group is not None else tdist.group.WORLD
+        self.rank = tdist.get_rank(self.group)
+        self.world = tdist.get_world_size(self.group)
+        if root != 0:
+            raise ValueError("RegionGather assembles on rank 0 of the group")
+        self.root = root
+        self.offset = [int(o) for o in offset]
+        self.shape = [int(s) for s in shape]
+        self.itemsize = int(itemsize)
+        self.on_device = tdist.get_backend(self.group) == "nccl"
+        if self.on_device:
+            self.device = torch.device("cuda", torch.cuda.current_device() if device is None
+                                       else int(device))
+        else:
+            self.device = torch.device("cpu")
+        self.parts = slab_partition(self.offset, self.shape, self.world, align)
+        rel = [([o - b for o, b in zip(po, self.offset)], ps) for po, ps in self.parts]
+        self.sched = gather_pieces(self.shape, rel, self.itemsize, piece_bytes, align)
+        nel = 1
+        for s in self.shape:
+            nel *= s
+        self.nbytes = nel * self.itemsize
+        so, ss = rel[self.rank]
+        self.base = slab_byte_offset(self.shape, so, self.itemsize)
+        n = 1
+        for s in ss:
+            n *= s
+        self.slab_bytes = n * self.itemsize
+        if self.rank == self.root:
+            self.region = region if region is not None else torch.empty(
+                self.nbytes, dtype=torch.uint8, device=self.device)
+            self.send_buf = self.region[self.base:self.base + self.slab_bytes]
+        else:
+            self.region = None
+            self.send_buf = send if send is not None else torch.empty(
+                max(1, self.slab_bytes), dtype=torch.uint8, device=self.device)
+        self._side = torch.cuda.Stream(self.device) if self.on_device else None
+        if self.on_device:  # every rank creates the communicator together, before any P2P op
+            tdist.all_reduce(torch.zeros(1, device=self.device), group=self.group)
+            torch.cuda.synchronize(self.device)
+
+    def pieces(self, rank=None):
+        """This rank's (or `rank`'s) pieces: [(absolute piece_offset, piece_shape,
+        region byte offset, nbytes)]."""
+        r = self.rank if rank is None else rank
+        return [([o + b for o, b in zip(po, self.offset)], ps, b, nb)
+                for po, ps, b, nb in self.sched[r]]
+
+    def _dst(self, b, nb):
+        return self.send_buf[b - self.base:b - self.base + nb]
+
+    def run(self, decode=None):
+        """Decode (unless None) and gather; returns the region byte tensor on the root and this
+        rank's slab byte tensor elsewhere, complete (device work synchronised)."""
+        torch = self.torch
+        mine = self.pieces()
+        if self.rank == self.root:
+            works = gather_pieces_p2p(self.tdist, self.group, self.rank, self.world, self.sched,
+                                      None, self.region)
+            if decode is not None:
+                if self.on_device:
+                    with torch.cuda.stream(self._side):
+                        for po, ps, b, nb in mine:
+                            decode(po, ps, self._dst(b, nb))
+                else:
+                    for po, ps, b, nb in mine:
+                        decode(po, ps, self._dst(b, nb))
+            for w in works:
+                w.wait()
+        else:
+            def dec(k):
+                po, ps, b, nb = mine[k]
+                decode(po, ps, self._dst(b, nb))
+            for w in gather_pieces_p2p(self.tdist, self.group, self.rank, self.world, self.sched,
+                                       self.send_buf[:self.slab_bytes] if self.slab_bytes
+                                       else self.send_buf[:0], None,
+                                       dec if decode is not None else None):
+                w.wait()
+        if self.on_device:
+            torch.cuda.current_stream(self.device).wait_stream(self._side)
+            torch.cuda.synchronize(self.device)
+        if decode is not None and hasattr(decode, "wait"):
+            decode.wait()
+        return self.region if self.rank == self.root else self.send_buf[:self.slab_bytes]
+
+
+def distributed_read(decode, offset, shape, dtype, group=None, root=0, align=1,
+                     piece_bytes=1 << 30, device=None):
+    """One region read over the ranks of `group` (RegionGather): on the root the assembled
+    region, elsewhere this rank's slab.  NCCL groups return CUDA byte tensors (view them as the
+    dtype), gloo groups numpy arrays of `dtype` in the region's / slab's shape."""
+    import numpy as _np
+    dt = _np.dtype(dtype)
+    g = RegionGather(offset, shape, dt.itemsize, group=group, root=root, align=align,
+                     piece_bytes=piece_bytes, device=device)
+    out = g.run(decode)
+    if g.on_device:
+        return out
+    shp = g.shape if g.rank == root else g.parts[g.rank][1]
+    return out.numpy().view(dt).reshape(shp)
