@@ -1,0 +1,139 @@
+"""The product's multi-GPU read on one GPU (zarrhip.parallel).
+
+- `Array.read_device` (ZH_OUT_DEVICE) through each store form — the library's own file reads,
+  the mirror's store reads, a MemoryStore — equals `Array.read` and the written array;
+- `RegionGather` over an NCCL (= RCCL) group of one rank: the device-tensor branch — the root's
+  pieces decoded on the side stream by `PlanDecoder` (one plan per piece over device-resident
+  shards, on torch's current stream) or `array_decoder` (store reads into device memory),
+  assembled in a CUDA byte tensor, and a second run reusing the same plans and buffers.
+The point-to-point exchange itself runs on gloo at world sizes 2 and 3 in
+tests/test_distributed.py (the same code), and over RCCL in the driver's 8-GPU bench; RCCL
+cannot put two ranks on one card."""
+import socket
+
+import numpy as np
+import pytest
+
+import oracle as O
+import zarrhip as z
+from helpers import chunk_coords, encode_oracle, rand_array, shape_of
+from zarrhip import _abi as A
+from zarrhip import parallel as P
+
+pytestmark = pytest.mark.gpu
+
+SHAPE = [1, 48, 40, 56]
+
+
+def _metadata():
+    return (z.ArrayMetadataBuilder().withShape(*SHAPE).withDataType(z.DataType.UINT32)
+            .withChunkShape(1, 16, 40, 32).withFillValue(0)
+            .withCodecs(lambda c: c.withSharding(
+                [1, 8, 8, 16], lambda c1: c1.withTranspose([0, 3, 2, 1]).withBytes("BIG")))
+            .build())
+
+
+@pytest.fixture
+def written(tmp_path):
+    data = np.random.default_rng(191).integers(0, 2 ** 32, SHAPE, dtype=np.uint32)
+    data[0, 16:32, :, 32:] = 0  # an all-fill shard (deleted on write): reads fill_value
+    stores = {"files": z.FilesystemStore(tmp_path / "f"), "mirror": z.FilesystemStore(tmp_path / "m"),
+              "memory": z.MemoryStore()}
+    for st in stores.values():
+        z.Array.create(st.resolve("a"), _metadata()).write(None, data)
+    return data, stores
+
+
+REGIONS = [([0, 0, 0, 0], SHAPE), ([0, 3, 5, 7], [1, 41, 30, 45]), ([0, 20, 1, 33], [1, 1, 1, 1])]
+
+
+@pytest.mark.parametrize("kind", ["files", "mirror", "memory"])
+def test_read_device_matches_read(dev, written, monkeypatch, kind):
+    data, stores = written
+    if kind == "mirror":
+        monkeypatch.setenv("ZH_FILES", "0")
+    a = z.Array.open(stores[kind].resolve("a"))
+    for off, shp in REGIONS:
+        nb = int(np.prod(shp)) * 4
+        d = dev.malloc(nb)
+        try:
+            a.read_device(off, shp, d, dev)
+            got = np.frombuffer(dev.d2h(d, nb), np.uint32).reshape(shp)
+        finally:
+            dev.free(d)
+        want = data[tuple(slice(o, o + s) for o, s in zip(off, shp))]
+        np.testing.assert_array_equal(got, want)
+        np.testing.assert_array_equal(got, a.read(off, shp))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+@pytest.fixture
+def nccl_group():
+    import torch
+    import torch.distributed as dist
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{_free_port()}", rank=0,
+                            world_size=1)
+    yield dist.group.WORLD
+    dist.destroy_process_group()
+
+
+def test_region_gather_nccl_one_rank(dev, written, nccl_group):
+    """RegionGather's device branch: the region in pieces of 8 rows, each decoded by its own
+    plan (PlanDecoder over device-resident shards) into its place of the root's CUDA region on
+    the side stream; equal to the oracle's read; a second run reuses plans and buffers; the
+    same region through array_decoder (the files read straight into device memory)."""
+    import torch
+    data, stores = written
+    meta = A.make_meta(SHAPE, [1, 16, 40, 32], 4, sharded=True, inner_chunk_shape=[1, 8, 8, 16],
+                       transpose_order=[0, 3, 2, 1], endian=A.ZH_ENDIAN_BIG)
+    shards = encode_oracle(meta, data)
+    allc = chunk_coords(meta, [0] * 4, shape_of(meta))
+    bufs = {}
+    for c, s in zip(allc, shards):
+        if s is not None:
+            p = dev.malloc(len(s))
+            dev.h2d(p, s)
+            bufs[c] = (p, len(s))
+    try:
+        def sources(po, ps):
+            return [bufs.get(c, (None, 0)) for c in chunk_coords(meta, po, ps)]
+        for off, shp in REGIONS[:2]:
+            g = P.RegionGather(off, shp, 4, group=nccl_group, align=8,
+                               piece_bytes=8 * shp[2] * shp[3] * 4, device=0)
+            assert g.on_device and g.region.is_cuda and len(g.pieces()) > 1
+            dec = P.PlanDecoder(dev, meta, sources)
+            try:
+                for _ in range(2):
+                    g.region.zero_()
+                    out = g.run(dec)
+                    got = out.cpu().numpy().view(np.uint32).reshape(shp)
+                    want = np.frombuffer(O.array_read(meta, sources_host(meta, shards, allc, off, shp),
+                                                      off, shp), np.uint32).reshape(shp)
+                    np.testing.assert_array_equal(got, want)
+                assert len(dec.plans) == len(g.pieces())  # one plan per piece, reused
+            finally:
+                dec.close()
+        a = z.Array.open(stores["files"].resolve("a"))
+        off, shp = REGIONS[1]
+        out = P.distributed_read(P.array_decoder(a, dev), off, shp, np.uint32,
+                                 group=nccl_group, align=8, piece_bytes=8 * 30 * 45 * 4,
+                                 device=0)
+        assert isinstance(out, torch.Tensor) and out.is_cuda
+        np.testing.assert_array_equal(out.cpu().numpy().view(np.uint32).reshape(shp),
+                                      data[tuple(slice(o, o + s) for o, s in zip(off, shp))])
+    finally:
+        for p, _ in bufs.values():
+            dev.free(p)
+
+
+def sources_host(meta, shards, allc, off, shp):
+    pos = {c: i for i, c in enumerate(allc)}
+    return [shards[pos[c]] for c in chunk_coords(meta, off, shp)]

@@ -28,6 +28,7 @@
 #include <algorithm>
 #include <atomic>
 #include <cstring>
+#include <deque>
 #include <memory>
 #include <mutex>
 #include <string>
@@ -88,7 +89,6 @@ struct FileEnt {
   std::string path, store, key;
   int fd = -1;
   int pins = 0;       // file_fetch calls reading it now (its descriptor stays open)
-  uint64_t used = 0;  // last use, for closing the least recently used descriptor
   bool live = false;
   // range reads past the end read as zeros (a part's reads, get(keys, start, end)); otherwise
   // the file is read as it was when its size was taken (a whole object or shard), and a read
@@ -100,8 +100,8 @@ struct FileTable {
   std::mutex mu;
   std::vector<FileEnt> ent;
   std::vector<int32_t> free;
+  std::deque<int32_t> opened;  // slots in the order their descriptors were opened (may be stale)
   int open = 0;  // descriptors open (and slots reserved for an open in progress)
-  uint64_t tick = 0;
 };
 
 FileTable& table() {
@@ -144,22 +144,31 @@ void slot_give(int32_t k) {
   t.free.push_back(k);
 }
 
-// Closes the least recently used descriptor nobody is reading (caller holds t.mu); false when
-// every open descriptor is in use.
+// Closes the oldest open descriptor nobody is reading (caller holds t.mu): the queue of opens
+// in order, stale entries (closed since, or a slot given back) dropped, pinned ones moved to
+// the back; false when every open descriptor is being read.  O(1) per close but for the few
+// pinned ones (at most one per lane), so a read of many files costs no scan of the table.
 bool close_lru(FileTable& t) {
-  FileEnt* v = nullptr;
-  for (FileEnt& e : t.ent)
-    if (e.live && e.fd >= 0 && e.pins == 0 && (!v || e.used < v->used)) v = &e;
-  if (!v) return false;
-  close(v->fd);
-  v->fd = -1;
-  t.open--;
-  return true;
+  for (size_t tries = t.opened.size(); tries > 0; tries--) {
+    const int32_t k = t.opened.front();
+    t.opened.pop_front();
+    FileEnt& e = t.ent[(size_t)k];
+    if (!e.live || e.fd < 0) continue;
+    if (e.pins > 0) {
+      t.opened.push_back(k);
+      continue;
+    }
+    close(e.fd);
+    e.fd = -1;
+    t.open--;
+    return true;
+  }
+  return false;
 }
 
 // The open descriptor of slot k, pinned until file_unpin (opened by path when closed), or -1
-// with *msg set.  At most kFileMaxOpen descriptors are open: beyond that the least recently
-// used idle one is closed first.  The open itself runs outside the table's lock.
+// with *msg set.  At most kFileMaxOpen descriptors are open: beyond that the oldest idle one is
+// closed first.  The open itself runs outside the table's lock.
 int file_pin(int32_t k, std::string* msg) {
   FileTable& t = table();
   std::string path;
@@ -170,7 +179,6 @@ int file_pin(int32_t k, std::string* msg) {
       *msg = "a store file that no read has open";
       return -1;
     }
-    e.used = ++t.tick;
     if (e.fd >= 0) {
       e.pins++;
       return e.fd;
@@ -202,6 +210,7 @@ int file_pin(int32_t k, std::string* msg) {
     t.open--;
   } else {
     e.fd = fd;
+    t.opened.push_back(k);
   }
   e.pins++;
   return e.fd;
