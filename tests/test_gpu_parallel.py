@@ -9,7 +9,16 @@
 The point-to-point exchange itself runs on gloo at world sizes 2 and 3 in
 tests/test_distributed.py (the same code), and over RCCL in the driver's 8-GPU bench; RCCL
 cannot put two ranks on one card."""
+import os
 import socket
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if __name__ == "__main__":  # the child process: the paths conftest.py sets for pytest
+    for _p in (os.path.join(ROOT, "zarr-java_amd"), os.path.join(ROOT, "oracle"), ROOT,
+               os.path.join(ROOT, "tests")):
+        sys.path.insert(0, _p)
+    import torch  # noqa: F401  before zarrhip loads its library (one HIP runtime)
 
 import numpy as np
 import pytest
@@ -74,66 +83,99 @@ def _free_port():
     return p
 
 
-@pytest.fixture
-def nccl_group():
+def test_region_gather_nccl_one_rank(written, tmp_path):
+    """RegionGather's device branch over an RCCL group of one rank, in a child process that
+    imports torch before zarrhip loads its library (one shared HIP runtime, INTEGRATION.md §4;
+    this test process loaded the library first): the region in pieces of 8 rows, each decoded
+    by its own plan (PlanDecoder over device-resident shards) into its place of the root's CUDA
+    region on the side stream, equal to the oracle's read, twice with the same plans and
+    buffers; the same region through array_decoder (the files read straight into device
+    memory).  In this process (library first): the gloo form, and RegionGather's refusal of a
+    device group with a clear message instead of torch's failing CUDA init."""
+    import subprocess
+    import sys
+    import torch.distributed as dist
+    data, stores = written
+    np.save(tmp_path / "data.npy", data)
+    r = subprocess.run([sys.executable, os.path.abspath(__file__), "child", str(tmp_path),
+                        str(stores["files"].path), str(_free_port())],
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, (r.stdout[-3000:], r.stderr[-3000:])
+    assert r.stdout.strip().endswith("child ok"), r.stdout[-2000:]
+    from zarrhip import _lib
+    _lib.lib()  # loaded by this process's earlier device tests, before torch
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{_free_port()}", rank=0,
+                            world_size=1)
+    try:
+        g = P.RegionGather([0] * 4, SHAPE, 4, align=8)  # gloo: host tensors, no torch HIP
+        assert not g.on_device
+        if not _lib.LOADED_AFTER_TORCH:  # a device group here would meet a second HIP runtime
+            real = dist.get_backend
+            dist.get_backend = lambda group=None: "nccl"
+            try:
+                with pytest.raises(RuntimeError, match="loaded before torch"):
+                    P.RegionGather([0] * 4, SHAPE, 4, align=8)
+            finally:
+                dist.get_backend = real
+    finally:
+        dist.destroy_process_group()
+
+
+def _child(tmp, files_root, port):
+    """The child of test_region_gather_nccl_one_rank (torch first)."""
     import torch
     import torch.distributed as dist
+    torch.cuda.init()
     torch.cuda.set_device(0)
-    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{_free_port()}", rank=0,
-                            world_size=1)
-    yield dist.group.WORLD
-    dist.destroy_process_group()
-
-
-def test_region_gather_nccl_one_rank(dev, written, nccl_group):
-    """RegionGather's device branch: the region in pieces of 8 rows, each decoded by its own
-    plan (PlanDecoder over device-resident shards) into its place of the root's CUDA region on
-    the side stream; equal to the oracle's read; a second run reuses plans and buffers; the
-    same region through array_decoder (the files read straight into device memory)."""
-    import torch
-    data, stores = written
+    from zarrhip import _lib
+    from zarrhip._lib import DeviceContext
+    data = np.load(os.path.join(tmp, "data.npy"))
+    dev = DeviceContext(0)
+    assert _lib.LOADED_AFTER_TORCH
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1)
+    group = dist.group.WORLD
     meta = A.make_meta(SHAPE, [1, 16, 40, 32], 4, sharded=True, inner_chunk_shape=[1, 8, 8, 16],
                        transpose_order=[0, 3, 2, 1], endian=A.ZH_ENDIAN_BIG)
     shards = encode_oracle(meta, data)
     allc = chunk_coords(meta, [0] * 4, shape_of(meta))
+    pos = {c: i for i, c in enumerate(allc)}
     bufs = {}
     for c, s in zip(allc, shards):
         if s is not None:
             p = dev.malloc(len(s))
             dev.h2d(p, s)
             bufs[c] = (p, len(s))
-    try:
-        def sources(po, ps):
-            return [bufs.get(c, (None, 0)) for c in chunk_coords(meta, po, ps)]
-        for off, shp in REGIONS[:2]:
-            g = P.RegionGather(off, shp, 4, group=nccl_group, align=8,
-                               piece_bytes=8 * shp[2] * shp[3] * 4, device=0)
-            assert g.on_device and g.region.is_cuda and len(g.pieces()) > 1
-            dec = P.PlanDecoder(dev, meta, sources)
-            try:
-                for _ in range(2):
-                    g.region.zero_()
-                    out = g.run(dec)
-                    got = out.cpu().numpy().view(np.uint32).reshape(shp)
-                    want = np.frombuffer(O.array_read(meta, sources_host(meta, shards, allc, off, shp),
-                                                      off, shp), np.uint32).reshape(shp)
-                    np.testing.assert_array_equal(got, want)
-                assert len(dec.plans) == len(g.pieces())  # one plan per piece, reused
-            finally:
-                dec.close()
-        a = z.Array.open(stores["files"].resolve("a"))
-        off, shp = REGIONS[1]
-        out = P.distributed_read(P.array_decoder(a, dev), off, shp, np.uint32,
-                                 group=nccl_group, align=8, piece_bytes=8 * 30 * 45 * 4,
-                                 device=0)
-        assert isinstance(out, torch.Tensor) and out.is_cuda
-        np.testing.assert_array_equal(out.cpu().numpy().view(np.uint32).reshape(shp),
-                                      data[tuple(slice(o, o + s) for o, s in zip(off, shp))])
-    finally:
-        for p, _ in bufs.values():
-            dev.free(p)
+
+    def sources(po, ps):
+        return [bufs.get(c, (None, 0)) for c in chunk_coords(meta, po, ps)]
+    for off, shp in REGIONS[:2]:
+        g = P.RegionGather(off, shp, 4, group=group, align=8,
+                           piece_bytes=8 * shp[2] * shp[3] * 4, device=0)
+        assert g.on_device and g.region.is_cuda and len(g.pieces()) > 1
+        dec = P.PlanDecoder(dev, meta, sources)
+        want = np.frombuffer(O.array_read(meta, [shards[pos[c]] for c in
+                                                 chunk_coords(meta, off, shp)], off, shp),
+                             np.uint32).reshape(shp)
+        for _ in range(2):
+            g.region.zero_()
+            got = g.run(dec).cpu().numpy().view(np.uint32).reshape(shp)
+            np.testing.assert_array_equal(got, want)
+        assert len(dec.plans) == len(g.pieces())  # one plan per piece, reused
+        dec.close()
+    a = z.Array.open(z.FilesystemStore(files_root).resolve("a"))
+    off, shp = REGIONS[1]
+    out = P.distributed_read(P.array_decoder(a, dev), off, shp, np.uint32, group=group, align=8,
+                             piece_bytes=8 * 30 * 45 * 4, device=0)
+    assert isinstance(out, torch.Tensor) and out.is_cuda
+    np.testing.assert_array_equal(out.cpu().numpy().view(np.uint32).reshape(shp),
+                                  data[tuple(slice(o, o + s) for o, s in zip(off, shp))])
+    for p, _ in bufs.values():
+        dev.free(p)
+    dist.destroy_process_group()
+    print("child ok", flush=True)
 
 
-def sources_host(meta, shards, allc, off, shp):
-    pos = {c: i for i, c in enumerate(allc)}
-    return [shards[pos[c]] for c in chunk_coords(meta, off, shp)]
+if __name__ == "__main__" and len(__import__("sys").argv) > 1 and \
+        __import__("sys").argv[1] == "child":
+    import sys
+    _child(sys.argv[2], sys.argv[3], int(sys.argv[4]))

@@ -10,6 +10,12 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("ZH_LIB_PATH") or os.path.join(_HERE, "libzarrhip.so")
 
 _lib = None
+# Whether torch was imported before the library was loaded.  torch's ROCm wheel bundles its own
+# HIP runtime with the same SONAME (libamdhip64.so.7) as the system's: loaded first, torch's
+# runtime is the one libzarrhip.so binds to and both share it; loaded after ours, torch gets a
+# second copy and its CUDA init fails ("No HIP GPUs are available").  zarrhip.parallel, which
+# moves torch tensors, checks this.
+LOADED_AFTER_TORCH = None
 
 P = C.c_void_p
 I32 = C.c_int32
@@ -121,8 +127,10 @@ _SIGS = {
 
 def lib():
     """The loaded libzarrhip.so (raises ImportError when it has not been built)."""
-    global _lib
+    global _lib, LOADED_AFTER_TORCH
     if _lib is None:
+        import sys
+        LOADED_AFTER_TORCH = "torch" in sys.modules
         if not os.path.exists(LIB_PATH):
             raise ImportError(
                 f"libzarrhip.so not found at {LIB_PATH}: build it with "

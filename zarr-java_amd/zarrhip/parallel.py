@@ -209,6 +209,12 @@ class RegionGather:
         self.shape = [int(s) for s in shape]
         self.itemsize = int(itemsize)
         self.on_device = tdist.get_backend(self.group) == "nccl"
+        from . import _lib
+        if self.on_device and _lib._lib is not None and not _lib.LOADED_AFTER_TORCH:
+            raise RuntimeError(
+                "zarrhip's library was loaded before torch: import torch (and initialise "
+                "torch.cuda) before the first zarrhip call, so that both use torch's HIP "
+                "runtime (INTEGRATION.md §4)")
         if self.on_device:
             self.device = torch.device("cuda", torch.cuda.current_device() if device is None
                                        else int(device))
