@@ -776,3 +776,45 @@ def test_write_files_failure_leaves_unfinished_chunks_intact(dev, tmp_path, wmod
         b = open(p, "rb").read()
         assert b in (old_enc[i], new_enc[i]), (i, len(b))
     assert not _tmp_leftovers(tmp_path)
+
+
+@pytest.mark.parametrize("loc", ["end", "start"])
+def test_mirror_and_library_store_reads_agree_on_truncated_shards(dev, tmp_path, monkeypatch,
+                                                                   loc):
+    """zarrhip.Array.read over a FilesystemStore whose shard file lost its tail, through the
+    library's own file reads (ZH_FILES=1) and through the mirror's store reads (ZH_FILES=0:
+    FilesystemStore.get(keys, start, end) zero-padded in store.py, the shard size bounding
+    nothing in Array._stage_shard, as ShardPieces.part does in Java): both equal the oracle's
+    read of the same files — a part decodes, a whole shard fails with the same message."""
+    shape = [1, 32, 32, 48]
+    m = (z.ArrayMetadataBuilder().withShape(*shape).withDataType(z.DataType.UINT32)
+         .withChunkShape(1, 16, 32, 48).withFillValue(0)
+         .withCodecs(lambda c: c.withSharding([1, 8, 8, 16], lambda c1: c1.withTranspose(
+             [0, 3, 2, 1]).withBytes("BIG"), loc)).build())
+    data = np.random.default_rng(193).integers(0, 2 ** 32, shape, dtype=np.uint32)
+    a = z.Array.create(z.FilesystemStore(tmp_path).resolve("t"), m)
+    a.write(None, data)
+    f = tmp_path / "t" / "c" / "0" / "0" / "0" / "0"
+    whole = f.read_bytes()
+    isz = 16 * (2 * 4 * 3) + 4
+    f.write_bytes(whole[:-3000 - isz] + whole[-isz:] if loc == "end" else whole[:-3000])
+    p1 = str(tmp_path / "t" / "c" / "0" / "1" / "0" / "0")
+    for off, shp, whole_shard in (([0, 1, 2, 3], [1, 14, 29, 40], False),
+                                  ([0, 0, 0, 0], [1, 16, 32, 48], True)):
+        b = z.Array.open(z.FilesystemStore(tmp_path).resolve("t"))
+        paths = [str(f)] + ([p1] if off[1] + shp[1] > 16 else [])
+        try:
+            want = store_read(b.zmeta, paths, off, shp)
+        except O.OracleError as eo:
+            assert whole_shard
+            for files in ("1", "0"):
+                monkeypatch.setenv("ZH_FILES", files)
+                with pytest.raises(z.ZarrException) as ez:
+                    z.Array.open(z.FilesystemStore(tmp_path).resolve("t")).read(off, shp)
+                assert str(ez.value) == str(eo), files
+            continue
+        assert not whole_shard
+        for files in ("1", "0"):
+            monkeypatch.setenv("ZH_FILES", files)
+            got = z.Array.open(z.FilesystemStore(tmp_path).resolve("t")).read(off, shp)
+            np.testing.assert_array_equal(got, want, err_msg=f"ZH_FILES={files}")
