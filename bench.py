@@ -478,49 +478,44 @@ def _mem_available():
     return avail
 
 
-def host_terminated(args, dist, dev, plan, out, out_bytes, shape, so, ss, rank, ws):
-    """Host-terminated read (no gather): each rank decodes its slab and copies it
-    D2H into ITS slice of one host buffer that holds the whole region (POSIX shared memory
-    mapped by every rank; the slabs are contiguous in C order), so N GPUs drive N PCIe links
-    at once.  Each rank page-locks only its own slice (zh_host_register).  When the host
-    cannot hold the region (tmpfs or MemAvailable short by the region + 32 GiB), each rank
-    streams its slab through a private 2 GiB pinned ring instead (same links, nothing kept),
-    and says so.  Timed: barrier, reps x (decode + D2H), sync, max over ranks."""
-    import mmap
-    from zarrhip.parallel import slab_byte_offset
+def host_terminated(args, dist, dev, plan, out, out_bytes, shape, so, ss, rank, ws, align):
+    """Host-terminated read (no gather) through the product's
+    zarrhip.parallel.SharedHostRegion: one host buffer holding the whole region in /dev/shm,
+    mapped by every rank, each rank page-locking only its own slice and decoding its slab
+    straight into it (here: its plan into device memory, then one D2H into the slice), so N
+    GPUs drive N PCIe links at once.  When the host cannot hold the region (tmpfs or
+    MemAvailable short by the region + 32 GiB), each rank streams its slab through a private
+    2 GiB pinned ring instead (same links, nothing kept), and says so.  Timed: barrier, reps x
+    (decode + D2H), sync, max over ranks; then the slices are verified against the generator."""
+    from zarrhip.parallel import SharedHostRegion
     full = 4
     for s in shape:
         full *= s
-    off = slab_byte_offset(shape, so, 4)
-    name = f"/dev/shm/zh_region_{os.environ.get('MASTER_PORT', 'solo')}_{os.getuid()}"
-    try:
-        vfs = os.statvfs("/dev/shm")
-        room = vfs.f_bavail * vfs.f_frsize >= full + (1 << 30)
-    except OSError:
-        room = False
-    shared = int(dist.max(0 if (room and _mem_available() >= full + (32 << 30)) else 1)) == 0
     reps = max(1, min(args.steps, 3))
-    mm = cbuf = None
-    reg = 0
     ring = 2 << 30
-    if shared:
-        if rank == 0:
-            fd = os.open(name, os.O_RDWR | os.O_CREAT | os.O_TRUNC, 0o600)
-            os.ftruncate(fd, full)
-            os.close(fd)
-        dist.barrier()
-        fd = os.open(name, os.O_RDWR)
-        mm = mmap.mmap(fd, full, mmap.MAP_SHARED, mmap.PROT_READ | mmap.PROT_WRITE)
-        os.close(fd)
-        cbuf = C.c_char.from_buffer(mm)
-        base = C.addressof(cbuf)
-        dst = base + off
-        reg = dst & ~4095
-        dev.host_register(reg, ((dst + out_bytes + 4095) & ~4095) - reg)
-        kind = "one region buffer in /dev/shm shared by the ranks; each pins its slice"
+    region = None
+    if int(dist.max(0 if _mem_available() >= full + (32 << 30) else 1)) == 0:
+        try:
+            region = SharedHostRegion(
+                [0] * len(shape), shape, 4, dev=dev, align=align,
+                name=f"/dev/shm/zh_region_{os.environ.get('MASTER_PORT', 'solo')}_{os.getuid()}")
+        except MemoryError:
+            region = None
+    if region is not None:
+        assert region.slab_offset == list(so) and region.slab_shape == list(ss)
+        dst = region.slice_addr()
+        kind = ("zarrhip.parallel.SharedHostRegion: one region buffer in /dev/shm shared by the "
+                "ranks; each pins its slice")
 
         def copy_out():
             dev.memcpy(dst, out, out_bytes, 1, None, False)
+
+        def decode(po, ps, addr):  # the slab's plan, then its D2H into the slice
+            plan.execute(out)
+            dev.memcpy(addr, out, out_bytes, 1, None, False)
+            plan.wait()
+            dev.sync()
+        region.read(decode)
     else:
         dst = dev.malloc_pinned(min(ring, out_bytes))
         kind = "bounded: each rank streams its slab through a private 2 GiB pinned ring"
@@ -528,9 +523,9 @@ def host_terminated(args, dist, dev, plan, out, out_bytes, shape, so, ss, rank, 
         def copy_out():
             for o in range(0, out_bytes, ring):
                 dev.memcpy(dst, out + o, min(ring, out_bytes - o), 1, None, False)
-    plan.execute(out)
-    copy_out()
-    plan.wait()
+        plan.execute(out)
+        copy_out()
+        plan.wait()
     dev.sync()
     dist.barrier()
     t0 = time.perf_counter()
@@ -547,16 +542,11 @@ def host_terminated(args, dist, dev, plan, out, out_bytes, shape, so, ss, rank, 
     dev.sync()
     t_copy = dist.max(time.perf_counter() - t1)
     bad = 0
-    if shared:  # the host slice must hold this rank's slab of the generator's array
+    if region is not None:  # the host slice must hold this rank's slab of the generator's array
         dev.memset(out, 0, out_bytes)
         dev.memcpy(out, dst, out_bytes, 0, None, True)
         bad = dist.max(dev.synth_verify(out, shape, so, ss, 4, SEED))
-        dev.host_unregister(reg)
-        del cbuf
-        mm.close()
-        dist.barrier()
-        if rank == 0:
-            os.unlink(name)
+        region.close()
     else:
         dev.free_pinned(dst)
     if bad:
@@ -565,7 +555,7 @@ def host_terminated(args, dist, dev, plan, out, out_bytes, shape, so, ss, rank, 
             "value": round(full * reps / t / GiB, 2), "unit": "GiB/s",
             "d2h_only_ms_per_step": round(t_copy * 1e3 / reps, 3),
             "d2h_GBps_per_rank": round(out_bytes * reps / t_copy / 1e9, 2),
-            "region_bytes": full, "verified": shared}
+            "region_bytes": full, "verified": region is not None}
 
 
 def gpus_shared(dist, device, ndev, ws):
@@ -710,7 +700,7 @@ def run_strong(args, dist, A, meta, rank, ws, local):
     host_out = None
     if not args.no_host_out:
         host_out = host_terminated(args, dist, dev, plan, out, out_bytes, shape, so, ss, rank,
-                                   ws)
+                                   ws, inner_y)
     res = {"slab_offset": so, "slab_shape": ss, "device": device, "shared_gpu": shared_gpu,
            "decode_ms_per_step": round(t_dec * 1e3 / args.steps, 3),
            "rank_ms_per_step": round(t_rank * 1e3 / args.steps, 3),

@@ -127,6 +127,72 @@ def test_gloo_distributed_read_and_bench_harness(tmp_path, world):
             assert idx == sorted(idx) and len(mine) > 1  # in order, several pieces
 
 
+def _host_worker(rank, world, port, tmp):
+    import ctypes
+    import sys
+    for p in (os.path.join(ROOT, "zarr-java_amd"), os.path.join(ROOT, "oracle"), ROOT,
+              os.path.join(ROOT, "tests")):
+        sys.path.insert(0, p)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world))
+    import torch.distributed as dist
+    import oracle as O
+    from helpers import encode_oracle, rand_array
+    from zarrhip import _abi as A
+    from zarrhip import parallel as PP
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    shape = [1, 24, 20, 12]
+    meta = A.make_meta(shape, [1, 8, 8, 8], 4, endian=A.ZH_ENDIAN_BIG, sharded=True,
+                       inner_chunk_shape=[1, 4, 4, 4], transpose_order=[0, 3, 2, 1])
+    arr = rand_array(shape, 4, seed=97)
+    shards = encode_oracle(meta, arr)
+    allc = O.compute_chunk_coords(shape, [1, 8, 8, 8], [0] * 4, shape)
+    pos = {c: i for i, c in enumerate(allc)}
+    seen = []
+
+    def decode(po, ps, addr):  # the oracle stands in for the device read (CPU test)
+        seen.append((list(po), list(ps)))
+        sel = O.compute_chunk_coords(shape, [1, 8, 8, 8], po, ps)
+        raw = O.array_read(meta, [shards[pos[c]] for c in sel], po, ps)
+        ctypes.memmove(addr, raw, len(raw))
+
+    for off, shp in (([0] * 4, shape), ([0, 3, 2, 1], [1, 19, 15, 9])):
+        h = PP.SharedHostRegion(off, shp, 4, group=None, align=4 if off == [0] * 4 else 1,
+                                name=os.path.join(tmp, f"region_{port}"))
+        h.read(decode)
+        got = h.array(np.uint32).copy()  # every rank sees the whole region
+        h.close()
+        want = arr[tuple(slice(o, o + s) for o, s in zip(off, shp))]
+        np.save(os.path.join(tmp, f"host{rank}_{off[1]}.npy"), got)
+        np.save(os.path.join(tmp, f"want_{off[1]}.npy"), want)
+        assert not os.path.exists(os.path.join(tmp, f"region_{port}")) or rank != 0
+    with open(os.path.join(tmp, f"seen{rank}.txt"), "w") as f:
+        f.write(repr(seen))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_gloo_shared_host_region(tmp_path, world):
+    """zarrhip.parallel.SharedHostRegion (the host-terminated multi-GPU read, no gather): every
+    rank decodes exactly its slab into its slice of one shared buffer, and every rank then sees
+    the whole region — for the whole array and an unaligned part at an offset; rank 0 removes
+    the buffer on close."""
+    import ast
+    import torch.multiprocessing as mp
+    mp.spawn(_host_worker, args=(world, free_port(), str(tmp_path)), nprocs=world, join=True)
+    for y in (0, 3):
+        want = np.load(tmp_path / f"want_{y}.npy")
+        for r in range(world):
+            np.testing.assert_array_equal(np.load(tmp_path / f"host{r}_{y}.npy"), want)
+    shape = [1, 24, 20, 12]
+    for r in range(world):
+        seen = [tuple(map(list, c)) for c in
+                ast.literal_eval(open(tmp_path / f"seen{r}.txt").read())]
+        assert seen == [tuple(P.slab_partition([0] * 4, shape, world, 4)[r]),
+                        tuple(P.slab_partition([0, 3, 2, 1], [1, 19, 15, 9], world, 1)[r])]
+    assert not [f for f in os.listdir(tmp_path) if f.startswith("region_")]
+
+
 @pytest.mark.parametrize("seed", range(12))
 def test_c_slab_partition_matches_python(seed):
     """zh_slab_partition (the C-ABI multi-GPU read's split) == zarrhip.parallel.slab_partition."""

@@ -179,3 +179,28 @@ if __name__ == "__main__" and len(__import__("sys").argv) > 1 and \
         __import__("sys").argv[1] == "child":
     import sys
     _child(sys.argv[2], sys.argv[3], int(sys.argv[4]))
+
+
+def test_shared_host_region_one_rank(dev, written, tmp_path):
+    """SharedHostRegion on the GPU (a gloo group of one rank: no torch HIP involved): the slice
+    page-locked with zh_host_register, the slab read by array_host_decoder (Array.read_into: the
+    library's pipelined read DMA-ing straight into the pinned slice), equal to the array; the
+    buffer removed on close."""
+    import torch.distributed as dist
+    data, stores = written
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{_free_port()}", rank=0,
+                            world_size=1)
+    try:
+        a = z.Array.open(stores["files"].resolve("a"))
+        for off, shp in REGIONS[:2]:
+            name = str(tmp_path / "region")
+            h = P.SharedHostRegion(off, shp, 4, dev=dev, align=8, name=name)
+            try:
+                h.read(P.array_host_decoder(a, dev))
+                np.testing.assert_array_equal(
+                    h.array(np.uint32), data[tuple(slice(o, o + s) for o, s in zip(off, shp))])
+            finally:
+                h.close()
+            assert not os.path.exists(name)
+    finally:
+        dist.destroy_process_group()

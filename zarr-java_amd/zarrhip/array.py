@@ -414,6 +414,20 @@ class Array:
         self._read_into(offset, shape, out.ctypes.data, 0, devices(), parallel, t_enter)
         return out
 
+    def read_into(self, offset, shape, out_addr, dev=None, parallel=True):
+        """core.Array.read into caller-owned HOST memory at out_addr (C order, the array's
+        dtype; page-locked memory is DMA'd straight into): the per-rank decode of
+        zarrhip.parallel.SharedHostRegion.  `dev`: the DeviceContext to read with (default: the
+        process's contexts, as read())."""
+        t_enter = time.perf_counter()
+        offset = [int(o) for o in offset]
+        shape = [int(s) for s in shape]
+        self._check_region(offset, shape)
+        if any(s == 0 for s in shape):
+            return
+        self._read_into(offset, shape, int(out_addr), 0,
+                        [dev] if dev is not None else devices(), parallel, t_enter)
+
     def read_device(self, offset, shape, out_ptr, dev=None, parallel=True):
         """core.Array.read delivered to device memory: the C-order region is written to
         `out_ptr` on `dev`'s device (a DeviceContext; default the first context) and nothing

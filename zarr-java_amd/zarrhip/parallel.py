@@ -291,6 +291,117 @@ class RegionGather:
         return self.region if self.rank == self.root else self.send_buf[:self.slab_bytes]
 
 
+class SharedHostRegion:
+    """One region read over the ranks of a group, delivered to HOST memory with no gather
+    (SURVEY §8(e)'s host-terminated form; the reference's read ends in a host array): the
+    region's buffer lives in POSIX shared memory (/dev/shm), mapped by every rank; each rank
+    page-locks only its own slab's slice (`dev.host_register`) and decodes its slab straight
+    into it, so N GPUs drive N PCIe links at once and every rank sees the whole region when
+    read() returns.  The slabs are slab_partition's (contiguous in C order, on the inner-chunk
+    grid `align`).  `decode(slab_offset, slab_shape, dst_addr)` writes the slab's C-order bytes
+    to host address dst_addr: `array_host_decoder(array)` (a zarrhip.Array read, the library's
+    pipelined read DMA-ing into the page-locked slice), or a caller's own (a device plan plus a
+    D2H copy, as bench.py does).  The buffer needs room in /dev/shm (MemoryError otherwise:
+    the caller streams its slab through a smaller buffer instead).  close() unpins, unmaps, and
+    rank 0 removes the file; the numpy view (array()) is invalid after it."""
+
+    def __init__(self, offset, shape, itemsize, dev=None, group=None, align=1, name=None):
+        import mmap
+        import os
+        import torch.distributed as tdist
+        self.tdist = tdist
+        self.group = group if group is not None else tdist.group.WORLD
+        self.rank = tdist.get_rank(self.group)
+        self.world = tdist.get_world_size(self.group)
+        self.offset = [int(o) for o in offset]
+        self.shape = [int(s) for s in shape]
+        self.itemsize = int(itemsize)
+        self.dev = dev
+        self.parts = slab_partition(self.offset, self.shape, self.world, align)
+        n = self.itemsize
+        for v in self.shape:
+            n *= v
+        self.nbytes = n
+        so, ss = self.parts[self.rank]
+        self.slab_offset, self.slab_shape = so, ss
+        self.base = slab_byte_offset(self.shape, [o - b for o, b in zip(so, self.offset)],
+                                     self.itemsize)
+        sb = self.itemsize
+        for v in ss:
+            sb *= v
+        self.slab_bytes = sb
+        # one name for the group: rank 0's choice, broadcast
+        names = [name or f"/dev/shm/zh_region_{os.getpid()}_{os.getuid()}"]
+        tdist.broadcast_object_list(names, src=0, group=self.group)
+        self.name = names[0]
+        try:
+            vfs = os.statvfs(os.path.dirname(self.name))
+            room = vfs.f_bavail * vfs.f_frsize >= n + (1 << 30)
+        except OSError:
+            room = False
+        ok = [room]
+        tdist.broadcast_object_list(ok, src=0, group=self.group)
+        if not ok[0]:
+            raise MemoryError(f"{os.path.dirname(self.name)} cannot hold the {n}-byte region")
+        if self.rank == 0:
+            fd = os.open(self.name, os.O_RDWR | os.O_CREAT | os.O_TRUNC, 0o600)
+            os.ftruncate(fd, max(1, n))
+            os.close(fd)
+        tdist.barrier(group=self.group)
+        fd = os.open(self.name, os.O_RDWR)
+        self._mm = mmap.mmap(fd, max(1, n), mmap.MAP_SHARED, mmap.PROT_READ | mmap.PROT_WRITE)
+        os.close(fd)
+        import ctypes
+        self._cbuf = ctypes.c_char.from_buffer(self._mm)
+        self.addr = ctypes.addressof(self._cbuf)
+        self._reg = None
+        if dev is not None and self.slab_bytes > 0:  # page-lock this rank's slice only
+            dst = self.addr + self.base
+            lo = dst & ~4095
+            hi = (dst + self.slab_bytes + 4095) & ~4095
+            dev.host_register(lo, hi - lo)
+            self._reg = lo
+
+    def slice_addr(self):
+        """Host address of this rank's slice (its slab's bytes in the region)."""
+        return self.addr + self.base
+
+    def read(self, decode):
+        """Every rank decodes its slab into its slice; returns after all ranks are done."""
+        if self.slab_bytes > 0:
+            decode(self.slab_offset, self.slab_shape, self.slice_addr())
+        self.tdist.barrier(group=self.group)
+
+    def array(self, dtype):
+        """The whole region as a numpy array over the shared buffer (valid until close())."""
+        import numpy as _np
+        return _np.frombuffer(self._mm, dtype=_np.dtype(dtype), count=self.nbytes //
+                              _np.dtype(dtype).itemsize).reshape(self.shape)
+
+    def close(self):
+        import os
+        if self._reg is not None:
+            self.dev.host_unregister(self._reg)
+            self._reg = None
+        del self._cbuf
+        self._mm.close()
+        self.tdist.barrier(group=self.group)
+        if self.rank == 0:
+            try:
+                os.unlink(self.name)
+            except FileNotFoundError:
+                pass
+
+
+def array_host_decoder(array, dev=None):
+    """decode(slab_offset, slab_shape, dst_addr) for SharedHostRegion over a zarrhip.Array:
+    core.Array.read of the slab straight into host memory at dst_addr (the library's pipelined
+    read DMAs into page-locked memory directly)."""
+    def decode(po, ps, addr):
+        array.read_into(po, ps, addr, dev)
+    return decode
+
+
 def distributed_read(decode, offset, shape, dtype, group=None, root=0, align=1,
                      piece_bytes=1 << 30, device=None):
     """One region read over the ranks of `group` (RegionGather): on the root the assembled
