@@ -5,7 +5,7 @@
 # the gather rehearses through gloo, labelled).
 set -u
 R=${GRAFT_REPO_ROOT:-$(pwd)}
-OUT=$R/gpurun_out/r05c
+OUT=$R/gpurun_out/${R05_TAG:-r05c}
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 step() {
