@@ -193,3 +193,33 @@ def test_shard_unreadable_index_is_store_exception(tmp_path):
                                 f"'c/0/0/0': {p}")
     finally:
         os.chmod(p, 0o600)
+
+
+def test_mirror_filesystem_store_exceptions(tmp_path):
+    """The Python mirror's FilesystemStore raises StoreException with the reference's texts
+    (StoreException.java:17-43 around FilesystemStore's causes, FilesystemStore.java:105-143),
+    the same the library's file calls use; and get(keys, start, end) zero-pads past the end."""
+    import zarrhip as z
+    st = z.FilesystemStore(tmp_path)
+    name = f"file://{tmp_path}"
+    (tmp_path / "blocker").write_bytes(b"x")
+    with pytest.raises(z.StoreException) as e:
+        st.set(["blocker", "c", "0"], b"abc")
+    assert str(e.value) == (f"Failed to write to store '{name}' at key 'blocker/c/0': "
+                            f"Failed to create parent directories for path: {tmp_path}/blocker/c")
+    (tmp_path / "d" / "x").mkdir(parents=True)
+    with pytest.raises(z.StoreException) as e:
+        st.delete(["d"])
+    assert str(e.value) == (f"Failed to delete from store '{name}' at key 'd': "
+                            f"Failed to delete file: {tmp_path}/d")
+    with pytest.raises(z.StoreException) as e:
+        st.get(["d"])
+    assert str(e.value).startswith(f"Failed to read from store '{name}' at key 'd': {tmp_path}/d: ")
+    st.set(["k"], b"0123456789")
+    assert st.get(["k"], 2, 6) == b"2345"
+    assert st.get(["k"], 8, 14) == b"89" + bytes(4)  # get(keys, start, end): zero-padded
+    assert st.get(["k"], 20, 22) == bytes(2)
+    assert st.get(["k"], -4) == b"6789"
+    with pytest.raises(ValueError):  # a resolved negative position (position(< 0))
+        st.get(["k"], -11)
+    assert st.get(["nope"], 0, 4) is None

@@ -14,12 +14,33 @@ import urllib.request
 
 
 class StoreException(RuntimeError):
-    """M/store/StoreException.java: `readFailed` wraps the cause's message."""
+    """M/store/StoreException.java:17-43: `readFailed` / `writeFailed` / `deleteFailed` wrap the
+    cause's message with the store and the '/'-joined key (the library's zh_array_read_files /
+    zh_array_write_files raise the same text)."""
 
     @staticmethod
     def read_failed(store_path, keys, cause):
         return StoreException("Failed to read from store '%s' at key '%s': %s"
                               % (store_path, "/".join(keys), cause))
+
+    @staticmethod
+    def write_failed(store_path, keys, cause):
+        return StoreException("Failed to write to store '%s' at key '%s': %s"
+                              % (store_path, "/".join(keys), cause))
+
+    @staticmethod
+    def delete_failed(store_path, keys, cause):
+        return StoreException("Failed to delete from store '%s' at key '%s': %s"
+                              % (store_path, "/".join(keys), cause))
+
+
+def _io_cause(path, e):
+    """IOException.getMessage() of a failed file operation as the JDK words it (UnixException:
+    AccessDeniedException carries just the file; other errors "file: reason")."""
+    import errno
+    if e.errno in (errno.EACCES, errno.EPERM):
+        return path
+    return "%s: %s" % (path, e.strerror or e)
 
 
 class Store:
@@ -86,6 +107,10 @@ class FilesystemStore(Store):
                 return b + bytes(max(0, e - s - len(b))) if end is not None else b
         except FileNotFoundError:
             return None
+        except IsADirectoryError as err:  # exists() is false for it: read as a failed read
+            raise StoreException.read_failed(repr(self), keys, _io_cause(p, err)) from None
+        except PermissionError as err:
+            raise StoreException.read_failed(repr(self), keys, _io_cause(p, err)) from None
 
     def size(self, keys):
         try:
@@ -107,20 +132,44 @@ class FilesystemStore(Store):
                 return len(view)
         except FileNotFoundError:
             return None
+        except PermissionError as err:
+            raise StoreException.read_failed(repr(self), keys,
+                                             _io_cause(self._p(keys), err)) from None
 
     def set(self, keys, data):
+        """FilesystemStore.set (:105-128): the parent directories, then the bytes — through a
+        temporary file renamed into place, as the library writes."""
         p = self._p(keys)
-        os.makedirs(os.path.dirname(p), exist_ok=True)
+        parent = os.path.dirname(p)
+        try:
+            os.makedirs(parent, exist_ok=True)
+        except OSError:
+            raise StoreException.write_failed(
+                repr(self), keys, "Failed to create parent directories for path: " + parent) \
+                from None
         tmp = p + ".tmp%d" % threading.get_ident()
-        with open(tmp, "wb") as f:
-            f.write(bytes(data))
-        os.replace(tmp, p)
+        b = bytes(data)
+        try:
+            with open(tmp, "wb") as f:
+                f.write(b)
+            os.replace(tmp, p)
+        except OSError:
+            try:
+                os.remove(tmp)
+            except OSError:
+                pass
+            raise StoreException.write_failed(
+                repr(self), keys, "Failed to write %d bytes to file: %s" % (len(b), p)) from None
 
     def delete(self, keys):
+        p = self._p(keys)
         try:
-            os.remove(self._p(keys))
+            os.remove(p)
         except FileNotFoundError:
             pass
+        except OSError:
+            raise StoreException.delete_failed(repr(self), keys,
+                                               "Failed to delete file: " + p) from None
 
     def __repr__(self):
         return f"file://{self.path}"
