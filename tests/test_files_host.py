@@ -223,3 +223,39 @@ def test_mirror_filesystem_store_exceptions(tmp_path):
     with pytest.raises(ValueError):  # a resolved negative position (position(< 0))
         st.get(["k"], -11)
     assert st.get(["nope"], 0, 4) is None
+
+
+@pytest.mark.parametrize("chain", ["sharded", "start_beindex", "nested"])
+def test_corrupt_index_entries_plan_sane_reads(tmp_path, chain):
+    """The host planner over the corrupt indexes of test_gpu_fuzz_index (huge, negative,
+    wrapping, straddling, colliding entries; index crc32c off): every planned read lies inside
+    [0, 2^63) with a length a Java buffer holds (≤ Integer.MAX_VALUE, the reference's (int)
+    allocation), or the plan fails with a message — never a crash (this test also runs under
+    the host sanitizer build).  What the device then makes of the ranges is the GPU test."""
+    from test_gpu_fuzz_index import corrupt
+    from test_gpu_pieces import make_case
+    meta, arr, _ = make_case(chain, seed=211)
+    meta.chain.index_has_crc32c = 0
+    shards = encode_oracle(meta, arr)
+    shape = [meta.shape[d] for d in range(meta.ndim)]
+    rng = np.random.default_rng(223)
+    for t in range(40):
+        bad = list(shards)
+        for i in rng.choice(len(bad), size=2, replace=False):
+            if bad[i] is not None:
+                bad[i], _ = corrupt(rng, meta, bad[i], int(rng.integers(1, 5)))
+        d = tmp_path / f"t{t}"
+        d.mkdir()
+        paths = _write(d, bad)
+        full = rng.random() < 0.5
+        off = [0, 0, 0] if full else [int(rng.integers(0, s)) for s in shape]
+        shp = shape if full else [int(rng.integers(1, s - o + 1)) for s, o in zip(shape, off)]
+        allc = chunk_coords(meta, [0, 0, 0], shape)
+        rp = [paths[allc.index(c)] for c in chunk_coords(meta, off, shp)]
+        try:
+            reads = file_reads(meta, rp, off, shp)
+        except ZhError:
+            continue
+        for k, o, nb in reads:
+            assert 0 <= k < len(rp) and o >= 0 and nb >= 0, (t, k, o, nb)
+            assert o <= 2 ** 63 - 1 - nb and nb <= 2 ** 31 - 1, (t, k, o, nb)

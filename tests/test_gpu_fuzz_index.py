@@ -1,0 +1,150 @@
+"""Seeded corrupt shard indexes on the HIP path vs the oracle (SURVEY §8(c) edge cases:
+erasures, collisions, out-of-range and wrapping entries).
+
+The shard index is read without its crc32c here, so every corrupt entry reaches the code that
+interprets it: the device's resolve kernel (memory shards: ByteBufferDataProvider slices,
+ShardingIndexedCodec.java:215-231, 323-330) and the library's host planner over files
+(sub-shard reads: StoreHandleDataProvider.read → FilesystemStore.get, zero-padded past the end
+of the file, ShardingIndexedCodec.java:340-356; whole-shard reads slice the file's bytes).
+Each trial corrupts a few entries of one or two shards with one of the mutations below and
+reads a random region (or the whole array) both ways:
+- both succeed → the outputs are equal, bit for bit;
+- both fail → "Could not load byte data for chunk [...]" and index-checksum texts are equal;
+  a wrong inner-chunk length is the documented Q12 divergence (same first words, the device
+  names the chunk instead of the two lengths).
+The nested chain keeps its sub-shard index crc32c, so an outer entry that moves a sub-shard
+fails that checksum with the same Stored/Computed values on both sides."""
+import struct
+
+import numpy as np
+import pytest
+
+import oracle as O
+from helpers import NP_DT, chunk_coords, device_read, encode_oracle
+from test_gpu_files import files_read, store_read
+from test_gpu_pieces import CHAINS, make_case, region_paths, write_store
+from zarrhip import _abi as A
+from zarrhip._lib import ZhError
+
+pytestmark = pytest.mark.gpu
+
+U64 = (1 << 64) - 1
+MUTATIONS = ["missing_off", "missing_nb", "huge_off", "negative_off", "straddle_end", "nb_off_by",
+             "nb_zero", "nb_huge", "wrap", "collide", "into_index"]
+
+
+def _layout(meta):
+    ch = meta.chain
+    cps = 1
+    for d in range(meta.ndim):
+        cps *= meta.chunk_shape[d] // ch.inner_chunk_shape[d]
+    isz = 16 * cps + (4 if ch.index_has_crc32c else 0)
+    fmt = ">QQ" if ch.index_endian == A.ZH_ENDIAN_BIG else "<QQ"
+    return cps, isz, ch.index_location == A.ZH_INDEX_START, fmt
+
+
+def corrupt(rng, meta, shard, nbad):
+    """`shard` with `nbad` index entries mutated; returns (bytes, [mutation names])."""
+    cps, isz, start, fmt = _layout(meta)
+    total = len(shard)
+    ib = 0 if start else total - isz
+    ents = [list(struct.unpack(fmt, shard[ib + 16 * k:ib + 16 * k + 16])) for k in range(cps)]
+    live = [k for k in range(cps) if ents[k][0] != U64]
+    names = []
+    for k in rng.choice(cps, size=min(nbad, cps), replace=False):
+        off, nb = ents[k]
+        want = nb if off != U64 else int(np.prod(meta.chain.inner_chunk_shape[:meta.ndim])) * \
+            meta.dtype_size
+        mu = MUTATIONS[int(rng.integers(len(MUTATIONS)))]
+        names.append(mu)
+        if mu == "missing_off":
+            ents[k] = [U64, int(rng.integers(0, 1 << 40))]
+        elif mu == "missing_nb":
+            ents[k] = [int(rng.integers(0, 1 << 40)), U64]
+        elif mu == "huge_off":
+            ents[k] = [int(rng.integers(total + 1, 1 << 62)), want]
+        elif mu == "negative_off":
+            ents[k] = [(1 << 63) + int(rng.integers(0, 1 << 40)), want]
+        elif mu == "straddle_end":
+            ents[k] = [max(0, total - want + int(rng.integers(1, 9))), want]
+        elif mu == "nb_off_by":
+            ents[k] = [off if off != U64 else 0, max(0, want + int(rng.choice([-5, -1, 1, 3])))]
+        elif mu == "nb_zero":
+            ents[k] = [off if off != U64 else 0, 0]
+        elif mu == "nb_huge":
+            ents[k] = [0, (1 << 63) + int(rng.integers(0, 1 << 20))]
+        elif mu == "wrap":  # off + nb overflows 64 bits
+            ents[k] = [U64 - want // 2, want]
+        elif mu == "collide" and live:  # another chunk's payload: read twice, no error
+            ents[k] = list(ents[int(rng.choice(live))])
+        else:  # into_index (or collide with nothing live): the index bytes read as data
+            ents[k] = [ib, want]
+    idx = b"".join(struct.pack(fmt, *e) for e in ents)
+    if meta.chain.index_has_crc32c:
+        idx += struct.pack("<I", O.crc32c(idx))
+    out = shard[:ib] + idx + shard[ib + isz:]
+    assert len(out) == total
+    return out, names
+
+
+def _outcome(fn):
+    try:
+        return "ok", fn()
+    except (ZhError, O.OracleError) as e:
+        return "err", str(e)
+
+
+def _same(got, want, ctx):
+    assert got[0] == want[0], (ctx, got if got[0] == "err" else "ok",
+                               want if want[0] == "err" else "ok")
+    if got[0] == "ok":
+        np.testing.assert_array_equal(got[1], want[1], err_msg=str(ctx))
+        return
+    g, w = got[1], want[1]
+    if w.startswith("unexpected inner chunk byte length"):  # Q12
+        assert g.startswith("unexpected inner chunk byte length"), (ctx, g, w)
+    else:
+        assert g == w, ctx
+
+
+def _region(rng, shape):
+    if rng.random() < 0.4:
+        return [0] * len(shape), list(shape)
+    off = [int(rng.integers(0, s)) for s in shape]
+    return off, [int(rng.integers(1, s - o + 1)) for s, o in zip(shape, off)]
+
+
+@pytest.mark.parametrize("form", ["memory", "files"])
+@pytest.mark.parametrize("chain", list(CHAINS))
+def test_corrupt_index_entries_match_oracle(dev, tmp_path, chain, form):
+    meta, arr, shards = make_case(chain, seed=211)
+    meta.chain.index_has_crc32c = 0
+    shards = encode_oracle(meta, arr)
+    shape = [meta.shape[d] for d in range(meta.ndim)]
+    allc = chunk_coords(meta, [0] * meta.ndim, shape)
+    pos = {c: i for i, c in enumerate(allc)}
+    rng = np.random.default_rng(sum(map(ord, chain + form)))
+    kinds = {"ok": 0, "err": 0}
+    for t in range(24):
+        bad = list(shards)
+        muts = []
+        for i in rng.choice(len(bad), size=int(rng.integers(1, 3)), replace=False):
+            if bad[i] is not None:
+                bad[i], m = corrupt(rng, meta, bad[i], int(rng.integers(1, 4)))
+                muts += m
+        off, shp = _region(rng, shape)
+        sel = chunk_coords(meta, off, shp)
+        ctx = (chain, form, t, muts, off, shp)
+        if form == "memory":
+            src = [bad[pos[c]] for c in sel]
+            want = _outcome(lambda: np.frombuffer(O.array_read(meta, src, off, shp),
+                                                  NP_DT[meta.dtype_size]).reshape(shp))
+            got = _outcome(lambda: device_read(dev, meta, src, off, shp))
+        else:
+            paths = write_store(tmp_path, meta, bad, tag=f"t{t}")
+            rp = region_paths(meta, paths, off, shp)
+            want = _outcome(lambda: store_read(meta, rp, off, shp))
+            got = _outcome(lambda: files_read(dev, meta, rp, off, shp))
+        _same(got, want, ctx)
+        kinds[want[0]] += 1
+    assert kinds["ok"] and kinds["err"], kinds  # both outcomes exercised
