@@ -225,17 +225,15 @@ def test_mirror_filesystem_store_exceptions(tmp_path):
     assert st.get(["nope"], 0, 4) is None
 
 
-@pytest.mark.parametrize("chain", ["sharded", "start_beindex", "nested"])
+@pytest.mark.parametrize("chain", ["sharded", "start_beindex", "nested", "nested_crc"])
 def test_corrupt_index_entries_plan_sane_reads(tmp_path, chain):
     """The host planner over the corrupt indexes of test_gpu_fuzz_index (huge, negative,
     wrapping, straddling, colliding entries; index crc32c off): every planned read lies inside
     [0, 2^63) with a length a Java buffer holds (≤ Integer.MAX_VALUE, the reference's (int)
     allocation), or the plan fails with a message — never a crash (this test also runs under
     the host sanitizer build).  What the device then makes of the ranges is the GPU test."""
-    from test_gpu_fuzz_index import corrupt
-    from test_gpu_pieces import make_case
-    meta, arr, _ = make_case(chain, seed=211)
-    meta.chain.index_has_crc32c = 0
+    from test_gpu_fuzz_index import corrupt, make_case
+    meta, arr = make_case(chain, seed=211)
     shards = encode_oracle(meta, arr)
     shape = [meta.shape[d] for d in range(meta.ndim)]
     rng = np.random.default_rng(223)

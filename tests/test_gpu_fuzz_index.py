@@ -22,7 +22,8 @@ import pytest
 import oracle as O
 from helpers import NP_DT, chunk_coords, device_read, encode_oracle
 from test_gpu_files import files_read, store_read
-from test_gpu_pieces import CHAINS, make_case, region_paths, write_store
+from helpers import rand_array
+from test_gpu_pieces import CHAINS, region_paths, write_store
 from zarrhip import _abi as A
 from zarrhip._lib import ZhError
 
@@ -82,9 +83,28 @@ def corrupt(rng, meta, shard, nbad):
     idx = b"".join(struct.pack(fmt, *e) for e in ents)
     if meta.chain.index_has_crc32c:
         idx += struct.pack("<I", O.crc32c(idx))
-    out = shard[:ib] + idx + shard[ib + isz:]
+    out = bytearray(shard[:ib] + idx + shard[ib + isz:])
     assert len(out) == total
-    return out, names
+    if total > isz and rng.random() < 0.4:  # one payload byte flipped (a chunk crc32c, a
+        names.append("flip")                 # sub-shard index, or data both sides read alike)
+        k = int(rng.integers(0, total - isz)) + (isz if start else 0)
+        out[k] ^= 1 << int(rng.integers(8))
+    return bytes(out), names
+
+
+# test_gpu_pieces' chains, plus leaves with a crc32c under nested sharding (the sub-shard
+# decode checks every leaf of a referenced cell, inside the requested part or not)
+FUZZ_CHAINS = dict(CHAINS, nested_crc=dict(sharded=True, inner_chunk_shape=[8, 8, 8],
+                                           nested_chunk_shape=[4, 4, 8], inner_crc32c=True))
+
+
+def make_case(chain, seed):
+    shape = [24, 32, 48]
+    meta = A.make_meta(shape, [8, 16, 24], 4, fill=(7).to_bytes(4, "little"),
+                       index_crc32c=False, **FUZZ_CHAINS[chain])
+    arr = rand_array(shape, 4, seed=seed, fill_frac=0.2, fill=0)
+    arr[:4, :8, :8] = 0  # an inner chunk of zeros: a missing entry
+    return meta, arr
 
 
 def _outcome(fn):
@@ -115,17 +135,16 @@ def _region(rng, shape):
 
 
 @pytest.mark.parametrize("form", ["memory", "files"])
-@pytest.mark.parametrize("chain", list(CHAINS))
+@pytest.mark.parametrize("chain", list(FUZZ_CHAINS))
 def test_corrupt_index_entries_match_oracle(dev, tmp_path, chain, form):
-    meta, arr, shards = make_case(chain, seed=211)
-    meta.chain.index_has_crc32c = 0
+    meta, arr = make_case(chain, seed=211)
     shards = encode_oracle(meta, arr)
     shape = [meta.shape[d] for d in range(meta.ndim)]
     allc = chunk_coords(meta, [0] * meta.ndim, shape)
     pos = {c: i for i, c in enumerate(allc)}
     rng = np.random.default_rng(sum(map(ord, chain + form)))
     kinds = {"ok": 0, "err": 0}
-    for t in range(24):
+    for t in range(32):
         bad = list(shards)
         muts = []
         for i in rng.choice(len(bad), size=int(rng.integers(1, 3)), replace=False):

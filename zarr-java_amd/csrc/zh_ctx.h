@@ -60,7 +60,7 @@ struct zh_ctx {
 
 namespace zh {
 constexpr int kStatusSlots = 64;
-constexpr int kStatusSlotWords = 128;  // 32 shards × kStWords
+constexpr int kStatusSlotWords = 192;  // 32 shards × kStWords
 constexpr int kUploadSlots = 16;
 constexpr size_t kUploadSlotBytes = 64 << 10;
 }  // namespace zh

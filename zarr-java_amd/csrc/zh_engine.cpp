@@ -472,8 +472,10 @@ void fill_common_args(const zh_array_meta* m, const int64_t* region_shape, bool 
   st = 1;
   for (int d = n - 1; d >= 0; d--) {
     a.cps_stride[d] = st;
+    a.rank.cps_stride[d] = st;
     st *= c.sharded ? (m->chunk_shape[d] / inner[d]) : 1;
   }
+  a.rank.ndim = n;  // single level; plan creation adds the nested geometry
   int64_t nel = 1;
   for (int d = 0; d < n; d++) {
     a.inner[d] = inner[d];
@@ -1202,13 +1204,21 @@ int plan_create(zh_ctx* ctx, const zh_array_meta* m, const SrcDesc* srcs, int64_
     N.sub_isz = sub_isz;
     N.cps2 = cps2;
     N.leaf_nbytes = p->args.inner_nbytes + p->args.crc_extra;
-    int64_t s1 = 1, sf = 1;
+    N.leaf_crc = c.inner_crc32c ? 1 : 0;
+    RankGeom& R = p->args.rank;
+    R.r2 = cps2 + 1;
+    int64_t s1 = 1, sf = 1, s2 = 1;
     for (int d = n - 1; d >= 0; d--) {
       N.cps1_stride[d] = s1;
+      R.cps1_stride[d] = s1;
       s1 *= m->chunk_shape[d] / c.inner_chunk_shape[d];
       N.flat_stride[d] = sf;
       sf *= m->chunk_shape[d] / inner[d];
       N.r[d] = c.inner_chunk_shape[d] / inner[d];
+      R.r[d] = N.r[d];
+      R.k2_stride[d] = s2;
+      s2 *= N.r[d];
+      N.leaf[d] = inner[d];
     }
     p->nest_grid = (int)std::min<int64_t>(l1_items, (int64_t)ctx->cu_count * 16);
   }
@@ -1363,6 +1373,8 @@ int plan_create(zh_ctx* ctx, const zh_array_meta* m, const SrcDesc* srcs, int64_
     D.skip_fast = fuse ? 1 : 0;
     D.partials = p->d_dcrc;
     D.status = p->d_status;
+    D.shards = p->d_shards;
+    D.rank = p->args.rank;
     g.crc_fused = fuse ? 1 : 0;
     g.crc_partials = p->d_dcrc;
     p->dcrc_grid = (int)std::min<int64_t>(items * nspan, (int64_t)ctx->cu_count * 32);
@@ -1633,21 +1645,36 @@ int zh_plan_wait(zh_plan* p, char* err, size_t errlen) {
               (int32_t)(uint32_t)w[kStCrcStored], (int32_t)(uint32_t)w[kStCrcComputed]);
       return ZH_EDATA;
     }
+    // the first chunk-level error in the oracle's order (RankGeom)
     const uint64_t key = w[kStBadChunk];
-    const uint32_t lin = 0xFFFFFFFFu - (uint32_t)(key >> 8);
+    const uint32_t rank = 0xFFFFFFFFu - (uint32_t)(key >> 8);
     const uint32_t level = (uint32_t)(key & (kFlagL1 | kFlagLeaf));
-    const uint32_t kind = (uint32_t)(key & (kFlagRange | kFlagLength));
-    // chunk coordinates in the grid of the codec that read the entry: the outer shard's
-    // inner-chunk grid, or (nested, kFlagLeaf) the sub-shard's leaf grid
+    const uint32_t kind = (uint32_t)(key & (kFlagRange | kFlagLength | kFlagChunkCrc | kFlagShort));
     const zh_codec_chain& ch = p->meta.chain;
+    if (kind == kFlagChunkCrc) {  // a chunk's (or sub-shard index's) Crc32cCodec.decode :39-44
+      set_err(err, errlen, "The checksum of the sharding index is invalid. Stored: %d Computed: %d",
+              (int32_t)(uint32_t)w[kStDetailA], (int32_t)(uint32_t)w[kStDetailB]);
+      return ZH_EDATA;
+    }
+    if (kind == kFlagShort) {  // the level-2 decode of a sub-shard shorter than its index
+      const int64_t cps2 = (int64_t)p->args.rank.r2 - 1;
+      set_err(err, errlen, "Shard of %lld bytes is smaller than its index (%lld bytes).",
+              (long long)(uint32_t)w[kStDetailA],
+              (long long)(16 * cps2 + (ch.nested_index_has_crc32c ? 4 : 0)));
+      return ZH_EDATA;
+    }
+    // chunk coordinates in the grid of the codec that read the entry: the shard's inner-chunk
+    // grid, (nested, kFlagL1) its level-1 cell grid, or (kFlagLeaf) the sub-shard's leaf grid
+    uint64_t r = rank;
+    if (level & kFlagL1) r = rank / (uint64_t)p->args.rank.r2;
+    if (level & kFlagLeaf) r = rank % (uint64_t)p->args.rank.r2 - 1;
     int64_t ic[kMaxDims];
-    uint32_t r = lin;
     for (int d = n - 1; d >= 0; d--) {
       int32_t cps = p->meta.chunk_shape[d] / leaf_shape(&p->meta)[d];
       if (level & kFlagL1) cps = p->meta.chunk_shape[d] / ch.inner_chunk_shape[d];
       if (level & kFlagLeaf) cps = ch.inner_chunk_shape[d] / ch.nested_chunk_shape[d];
-      ic[d] = r % cps;
-      r /= cps;
+      ic[d] = (int64_t)(r % (uint64_t)cps);
+      r /= (uint64_t)cps;
     }
     if (kind == kFlagRange)  // ShardingIndexedCodec.java:227-230
       set_err(err, errlen, "Could not load byte data for chunk %s", fmt_ints(ic, n).c_str());

@@ -19,10 +19,35 @@ constexpr int kIdxSpan = 4096;         // index bytes per index-CRC workgroup (o
                                        // per lane: a 512 KiB index is 128 workgroups)
 constexpr int kCrcLane = kCrcSpan / kBlock;  // 256 bytes per lane
 
-// Per-shard status words (device, uint64 each), read back by zh_plan_wait.
+// Per-shard status words (device, uint64 each), read back by zh_plan_wait: the flags, the
+// shard index's crc32c pair (kFlagCrc: checked before any inner chunk, Crc32cCodec.java:24-48),
+// and the first chunk-level error in the oracle's sequential order (chunk_error below): its
+// key ((0xFFFFFFFF − rank) << 8 | kind, atomicMax) and two detail words keyed by the same rank.
 enum : uint32_t { kStFlags = 0, kStCrcStored = 1, kStCrcComputed = 2, kStBadChunk = 3,
-                  kStWords = 4 };
-enum : uint32_t { kFlagCrc = 1u, kFlagRange = 2u, kFlagLength = 4u };
+                  kStDetailA = 4, kStDetailB = 5, kStWords = 6 };
+// kinds: kFlagCrc is the shard index's own checksum; the others are chunk-level (with kFlagL1
+// / kFlagLeaf, below, on nested chains): an unreadable range, a wrong length, a failed chunk
+// or sub-shard index crc32c (details: stored, computed), a sub-shard shorter than its index
+// (detail A: its length)
+enum : uint32_t { kFlagCrc = 1u, kFlagRange = 2u, kFlagLength = 4u, kFlagChunkCrc = 32u,
+                  kFlagShort = 64u };
+
+// The rank of a chunk-level error: its place in the sequential order in which the oracle
+// decodes a shard (the reference decodes the inner chunks in a parallel stream,
+// ShardingIndexedCodec.java:210-212, so any failing chunk's error may surface there; the
+// device and the oracle both report the first in C order).  Single level: the
+// inner chunk's C-order index in the shard grid.  Nested: level-1 cell lin1 ranks
+// lin1·(cps2 + 1) (its entry, its sub-shard's length and index crc32c), its leaf k2
+// lin1·(cps2 + 1) + 1 + k2 (the sub-shard decode visits every leaf, :97-103).
+struct RankGeom {
+  int64_t cps_stride[ZH_MAX_DIMS];   // single level: inner-grid C-order strides
+  int64_t cps1_stride[ZH_MAX_DIMS];  // nested: level-1 cell grid strides
+  int64_t k2_stride[ZH_MAX_DIMS];    // nested: leaf-in-cell C-order strides
+  int64_t r2;                        // nested: cps2 + 1 (0: single level)
+  int32_t r[ZH_MAX_DIMS];            // nested: leaves per cell per dim
+  int32_t ndim;
+  int32_t pad;
+};
 
 // Exact floor(n / d) for 0 <= n < 2^31, 1 <= d < 2^31 (Granlund–Montgomery round-up
 // method with N = 31): q = (n * m) >> s.
@@ -162,6 +187,7 @@ struct ScatterArgs {
                                 // and the tile rows follow each other (host-checked), so the
                                 // movers load 128-B aligned lines (tiles_rowcrc_aln_kernel)
   int64_t tile_ystride;         // tile_align: unit u's region offset is u · tile_ystride
+  RankGeom rank;                // chunk-level error order (decode)
 };
 
 // Chunk-payload CRC-32C pass (inner crc32c codec): one workgroup per (item, 64 KiB span) of
@@ -178,6 +204,8 @@ struct DataCrcArgs {
   int32_t pad;
   uint32_t* partials;           // n_items * nspan
   uint64_t* status;             // decode: kStWords per shard
+  const DevShard* shards;       // decode: the items' shards (a mismatch's rank)
+  RankGeom rank;
 };
 
 // Nested sharding pre-pass (nested_index_kernel): one workgroup per referenced level-1 cell
@@ -198,7 +226,10 @@ struct NestArgs {
   int32_t pad;
   int64_t sub_isz;                // encoded sub-shard index size (16 * cps2 [+ 4])
   int64_t cps2;                   // leaves per level-1 cell
-  int64_t leaf_nbytes;
+  int64_t leaf_nbytes;            // stored leaf bytes (+ 4 with the leaf crc32c)
+  int32_t leaf_crc;               // leaves carry a crc32c: the cell's leaves outside the part
+  int32_t pad2;                   //   are checked here (the data-CRC pass checks the rest)
+  int32_t leaf[kMaxDims];         // leaf chunk shape
   int64_t cps1_stride[kMaxDims];  // outer index entry stride per level-1 coordinate
   int64_t flat_stride[kMaxDims];  // flat index entry stride per leaf coordinate
   int32_t r[kMaxDims];            // leaves per level-1 cell along each dim

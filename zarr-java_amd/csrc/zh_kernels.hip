@@ -218,6 +218,42 @@ __device__ __forceinline__ void index_entry(const ScatterArgs& a, const DevShard
   nb = ld_u64_unaligned(ent + 8, a.index_be);
 }
 
+__device__ __forceinline__ uint32_t rank_clamp(uint64_t r) {
+  return r > 0xFFFFFFFEull ? 0xFFFFFFFEu : (uint32_t)r;
+}
+
+// The rank (RankGeom) of the inner chunk — the leaf, nested — at shard-grid coordinates ic.
+__device__ __forceinline__ uint32_t chunk_rank(const RankGeom& g, const int32_t* ic) {
+  uint64_t l1 = 0, k2 = 0;
+#pragma unroll
+  for (int d = 0; d < kMaxDims; d++) {
+    if (d >= g.ndim) continue;
+    if (g.r2 == 0) {
+      l1 += (uint64_t)ic[d] * (uint64_t)g.cps_stride[d];
+      continue;
+    }
+    const int32_t c1 = ic[d] / g.r[d];
+    l1 += (uint64_t)c1 * (uint64_t)g.cps1_stride[d];
+    k2 += (uint64_t)(ic[d] - c1 * g.r[d]) * (uint64_t)g.k2_stride[d];
+  }
+  return rank_clamp(g.r2 == 0 ? l1 : l1 * (uint64_t)g.r2 + 1 + k2);
+}
+
+// Records a chunk-level decode error in the shard's status words st: the lowest rank wins the
+// key, and its details (a failed crc32c's stored and computed values, a short sub-shard's
+// length) win the detail words, which are keyed by the same rank.
+__device__ __forceinline__ void chunk_error(uint64_t* st, uint32_t rank, uint32_t kind,
+                                            uint32_t da = 0, uint32_t db = 0) {
+  const uint64_t hi = (uint64_t)(0xFFFFFFFFu - rank);
+  atomicOr((unsigned long long*)(st + kStFlags),
+           (unsigned long long)(kind & (kFlagRange | kFlagLength | kFlagChunkCrc | kFlagShort)));
+  atomicMax((unsigned long long*)(st + kStBadChunk), (unsigned long long)((hi << 8) | kind));
+  if (kind & (kFlagChunkCrc | kFlagShort)) {
+    atomicMax((unsigned long long*)(st + kStDetailA), (unsigned long long)((hi << 32) | da));
+    atomicMax((unsigned long long*)(st + kStDetailB), (unsigned long long)((hi << 32) | db));
+  }
+}
+
 // Device address of the stored range [off, off + nb) of shard S (range-checked against the
 // object size by the caller).  Without a piece table the object is whole at S.data.  With
 // one (sub-shard reads: StoreHandleDataProvider.read(off, nb), ShardingIndexedCodec.java:
@@ -687,11 +723,8 @@ __device__ __forceinline__ ItemDesc resolve_one(const ScatterArgs& a, int64_t ci
     bool range_ok = off <= total && nb <= total - off;
     if (range_ok) range_ok = piece_src(S, off, nb, src);  // sub-shard reads: the held pieces
     if (!range_ok || nb != (uint64_t)(a.inner_nbytes + a.crc_extra)) {
-      const uint32_t kind = range_ok ? kFlagLength : kFlagRange;
-      const uint64_t key = ((uint64_t)(0xFFFFFFFFu - (uint32_t)lin) << 8) | kind;
-      atomicOr((unsigned long long*)(a.status + s * kStWords + kStFlags), (unsigned long long)kind);
-      atomicMax((unsigned long long*)(a.status + s * kStWords + kStBadChunk),
-                (unsigned long long)key);
+      const uint32_t kind = (range_ok ? kFlagLength : kFlagRange) | (a.rank.r2 ? kFlagLeaf : 0u);
+      chunk_error(a.status + s * kStWords, chunk_rank(a.rank, ic), kind);
       D.kind = kDescSkip;
       return D;
     }
@@ -2721,12 +2754,22 @@ __global__ void data_crc_finalize_kernel(DataCrcArgs a) {
   }
   const uint32_t stored =
       (uint32_t)s[0] | ((uint32_t)s[1] << 8) | ((uint32_t)s[2] << 16) | ((uint32_t)s[3] << 24);
-  if (c != stored) {
-    uint64_t* st = a.status + (int64_t)D.shard * kStWords;
-    if (atomicCAS((unsigned long long*)(st + kStCrcStored), 0ull,
-                  (unsigned long long)((1ull << 32) | stored)) == 0ull)
-      st[kStCrcComputed] = c;
-    atomicOr((unsigned long long*)(st + kStFlags), (unsigned long long)kFlagCrc);
+  if (c != stored) {  // the chunk's shard-grid coordinates (the resolve kernel's unravel)
+    const DevShard& S = a.shards[D.shard];
+    uint32_t j = (uint32_t)(item - S.item_begin);
+    int32_t ic[kMaxDims];
+#pragma unroll
+    for (int d = kMaxDims - 1; d >= 0; --d) {
+      ic[d] = 0;
+      if (d < a.rank.ndim) {
+        const uint32_t cnt = (uint32_t)S.box_count[d];
+        const uint32_t q = j / cnt;
+        ic[d] = S.box_start[d] + (int32_t)(j - q * cnt);
+        j = q;
+      }
+    }
+    chunk_error(a.status + (int64_t)D.shard * kStWords, chunk_rank(a.rank, ic),
+                kFlagChunkCrc | (a.rank.r2 ? kFlagLeaf : 0u), stored, c);
   }
 }
 
@@ -2736,12 +2779,9 @@ __global__ void data_crc_finalize_kernel(DataCrcArgs a) {
 // applied twice — the outer codec's inner pipeline is the level-2 sharding codec, whose
 // decode(ByteBuffer) :97-103 reads its own index from the sub-shard bytes)
 // ---------------------------------------------------------------------------------
-__device__ __forceinline__ void nest_error(const NestArgs& a, int64_t s, uint32_t lin,
-                                           uint32_t kind) {
-  const uint64_t key = ((uint64_t)(0xFFFFFFFFu - lin) << 8) | kind;
-  atomicOr((unsigned long long*)(a.status + s * kStWords + kStFlags),
-           (unsigned long long)(kind & (kFlagRange | kFlagLength)));
-  atomicMax((unsigned long long*)(a.status + s * kStWords + kStBadChunk), (unsigned long long)key);
+// rank of level-1 cell lin1 (k2 < 0) or of its leaf k2 (RankGeom)
+__device__ __forceinline__ uint32_t nest_rank(const NestArgs& a, int64_t lin1, int64_t k2) {
+  return rank_clamp((uint64_t)lin1 * (uint64_t)(a.cps2 + 1) + (uint64_t)(k2 + 1));
 }
 
 // CRC-32C of p[0, len) by the whole workgroup (kBlock lanes, kCrcLane-byte segments per
@@ -2803,9 +2843,13 @@ __global__ __launch_bounds__(kBlock) void nested_index_kernel(NestArgs a) {
     bool ok = !(off1 == ~0ull || nb1 == ~0ull);  // missing sub-shard: zeros (Q1)
     const uint8_t* sub = nullptr;
     uint64_t held = nb1;  // the sub-shard must be held whole (sub-shard reads: one piece)
-    if (ok && !(off1 <= total && nb1 <= total - off1 && nb1 >= (uint64_t)a.sub_isz &&
-                piece_src(S, off1, held, sub) && held == nb1)) {
-      if (tid == 0) nest_error(a, lo, (uint32_t)lin1, kFlagRange | kFlagL1);
+    uint64_t* st = a.status + lo * kStWords;
+    if (ok && !(off1 <= total && nb1 <= total - off1 && piece_src(S, off1, held, sub) &&
+                held == nb1)) {
+      if (tid == 0) chunk_error(st, nest_rank(a, lin1, -1), kFlagRange | kFlagL1);
+      ok = false;
+    } else if (ok && nb1 < (uint64_t)a.sub_isz) {  // the level-2 decode's index read fails
+      if (tid == 0) chunk_error(st, nest_rank(a, lin1, -1), kFlagShort | kFlagL1, (uint32_t)nb1);
       ok = false;
     }
     const uint8_t* ib = ok ? (a.sub_start ? sub : sub + nb1 - a.sub_isz) : nullptr;
@@ -2815,14 +2859,9 @@ __global__ __launch_bounds__(kBlock) void nested_index_kernel(NestArgs a) {
       const uint8_t* s = ib + len;
       const uint32_t stored =
           (uint32_t)s[0] | ((uint32_t)s[1] << 8) | ((uint32_t)s[2] << 16) | ((uint32_t)s[3] << 24);
-      if (c != stored && tid == 0) {
-        uint64_t* st = a.status + lo * kStWords;
-        // first reporter wins the (stored, computed) pair; bit 32 marks the word as set
-        if (atomicCAS((unsigned long long*)(st + kStCrcStored), 0ull,
-                      (unsigned long long)((1ull << 32) | stored)) == 0ull)
-          st[kStCrcComputed] = c;
-        atomicOr((unsigned long long*)(st + kStFlags), (unsigned long long)kFlagCrc);
-      }
+      if (c != stored && tid == 0)
+        chunk_error(st, nest_rank(a, lin1, -1), kFlagChunkCrc | kFlagL1, stored, c);
+      ok = ok && c == stored;
     }
     uint64_t* flat = reinterpret_cast<uint64_t*>(S.flat);
     for (int64_t k2 = tid; k2 < a.cps2; k2 += kBlock) {
@@ -2839,9 +2878,9 @@ __global__ __launch_bounds__(kBlock) void nested_index_kernel(NestArgs a) {
         const uint64_t nb2 = ld_u64_unaligned(ib + 16 * k2 + 8, a.sub_be);
         if (!(off2 == ~0ull || nb2 == ~0ull)) {
           if (!(off2 <= nb1 && nb2 <= nb1 - off2)) {
-            nest_error(a, lo, (uint32_t)k2, kFlagRange | kFlagLeaf);
+            chunk_error(st, nest_rank(a, lin1, k2), kFlagRange | kFlagLeaf);
           } else if (nb2 != (uint64_t)a.leaf_nbytes) {
-            nest_error(a, lo, (uint32_t)k2, kFlagLength | kFlagLeaf);
+            chunk_error(st, nest_rank(a, lin1, k2), kFlagLength | kFlagLeaf);
           } else {
             eo = off1 + off2;
             en = nb2;
@@ -2850,6 +2889,34 @@ __global__ __launch_bounds__(kBlock) void nested_index_kernel(NestArgs a) {
       }
       flat[2 * f] = eo;
       flat[2 * f + 1] = en;
+    }
+    if (!ok || !a.leaf_crc) continue;
+    // Crc32cCodec.decode (:24-48) of the cell's leaves outside the requested part: the level-2
+    // decode reads every leaf of the sub-shard (:97-103); the data-CRC pass checks the leaves
+    // inside the part.  Uniform over the workgroup (block_crc).
+    for (int64_t k2 = 0; k2 < a.cps2; k2++) {
+      int64_t q = k2;
+      bool inside = true;
+#pragma unroll
+      for (int d = kMaxDims - 1; d >= 0; --d)
+        if (d < n) {
+          const int64_t lo_e = ((int64_t)c1[d] * a.r[d] + q % a.r[d]) * a.leaf[d];
+          q /= a.r[d];
+          inside = inside && lo_e < S.part_hi[d] && lo_e + a.leaf[d] > S.part_lo[d];
+        }
+      if (inside) continue;
+      const uint64_t off2 = ld_u64_unaligned(ib + 16 * k2, a.sub_be);
+      const uint64_t nb2 = ld_u64_unaligned(ib + 16 * k2 + 8, a.sub_be);
+      if (off2 == ~0ull || nb2 == ~0ull || !(off2 <= nb1 && nb2 <= nb1 - off2) ||
+          nb2 != (uint64_t)a.leaf_nbytes)
+        continue;  // missing, or reported above
+      const uint8_t* lp = sub + off2;
+      const uint32_t c = block_crc(lp, (int64_t)nb2 - 4, T, red);
+      const uint8_t* sp = lp + nb2 - 4;
+      const uint32_t stored = (uint32_t)sp[0] | ((uint32_t)sp[1] << 8) |
+                              ((uint32_t)sp[2] << 16) | ((uint32_t)sp[3] << 24);
+      if (c != stored && tid == 0)
+        chunk_error(st, nest_rank(a, lin1, k2), kFlagChunkCrc | kFlagLeaf, stored, c);
     }
   }
 }
