@@ -127,12 +127,15 @@ def shard_part(meta, coords, offset, shape):
     return lo, hi
 
 
-def jni_fetch(meta, paths, offset, shape, max_run=64 << 20, size_known=True, drop=None):
+def jni_fetch(meta, paths, offset, shape, max_run=64 << 20, size_known=True, drop=None,
+              pad=False):
     """HipArray.read's store I/O (FilesystemStore): per shard of the region either the whole
     object (part == shard) or the stored index by one prefix/suffix read, zh_shard_ranges, and
     one range read per returned range.  Returns [(index bytes|None, shard size, [(offset,
     bytes)])] in computeChunkCoords order (None = missing key).  `drop`: (shard, range) pairs
-    whose store read "fails" (returns null: the piece is not passed on)."""
+    whose store read "fails" (returns null: the piece is not passed on).  `pad`: a range
+    past the end of the file reads zero-padded, as FilesystemStore.get(keys, start, end) does
+    (M/store/FilesystemStore.java:43-75)."""
     from zarrhip._lib import shard_ranges
     n = meta.ndim
     isz = lib().zh_shard_index_size(C.byref(meta))
@@ -154,6 +157,10 @@ def jni_fetch(meta, paths, offset, shape, max_run=64 << 20, size_known=True, dro
             pieces = []
             for k, (o, nb) in enumerate(rs):
                 if drop and (si, k) in drop:
+                    continue
+                if pad:  # pread: no seek (an offset beyond the file system's largest file)
+                    b = os.pread(f.fileno(), nb, o)
+                    pieces.append((o, b + bytes(nb - len(b))))
                     continue
                 f.seek(o)
                 pieces.append((o, f.read(nb)))

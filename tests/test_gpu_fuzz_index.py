@@ -6,6 +6,8 @@ interprets it: the device's resolve kernel (memory shards: ByteBufferDataProvide
 ShardingIndexedCodec.java:215-231, 323-330) and the library's host planner over files
 (sub-shard reads: StoreHandleDataProvider.read → FilesystemStore.get, zero-padded past the end
 of the file, ShardingIndexedCodec.java:340-356; whole-shard reads slice the file's bytes).
+The third form is the Java drop-in's: HipArray.read's store reads (the stored index, then
+zh_shard_ranges' ranges, zero-padded past the end of the file) handed to zh_array_read_pieces.
 Each trial corrupts a few entries of one or two shards with one of the mutations below and
 reads a random region (or the whole array) both ways:
 - both succeed → the outputs are equal, bit for bit;
@@ -20,9 +22,9 @@ import numpy as np
 import pytest
 
 import oracle as O
-from helpers import NP_DT, chunk_coords, device_read, encode_oracle
+from helpers import (NP_DT, chunk_coords, device_read, encode_oracle, jni_fetch, jni_read,
+                     rand_array)
 from test_gpu_files import files_read, store_read
-from helpers import rand_array
 from test_gpu_pieces import CHAINS, region_paths, write_store
 from zarrhip import _abi as A
 from zarrhip._lib import ZhError
@@ -134,7 +136,7 @@ def _region(rng, shape):
     return off, [int(rng.integers(1, s - o + 1)) for s, o in zip(shape, off)]
 
 
-@pytest.mark.parametrize("form", ["memory", "files"])
+@pytest.mark.parametrize("form", ["memory", "files", "pieces"])
 @pytest.mark.parametrize("chain", list(FUZZ_CHAINS))
 def test_corrupt_index_entries_match_oracle(dev, tmp_path, chain, form):
     meta, arr = make_case(chain, seed=211)
@@ -163,7 +165,12 @@ def test_corrupt_index_entries_match_oracle(dev, tmp_path, chain, form):
             paths = write_store(tmp_path, meta, bad, tag=f"t{t}")
             rp = region_paths(meta, paths, off, shp)
             want = _outcome(lambda: store_read(meta, rp, off, shp))
-            got = _outcome(lambda: files_read(dev, meta, rp, off, shp))
+            if form == "files":
+                got = _outcome(lambda: files_read(dev, meta, rp, off, shp))
+            else:  # HipArray.read's pieces over a FilesystemStore (size unknown: -1)
+                got = _outcome(lambda: jni_read(
+                    dev, meta, jni_fetch(meta, rp, off, shp, size_known=False, pad=True),
+                    off, shp))
         _same(got, want, ctx)
         kinds[want[0]] += 1
     assert kinds["ok"] and kinds["err"], kinds  # both outcomes exercised
