@@ -266,6 +266,10 @@ __device__ __forceinline__ bool piece_src(const DevShard& S, uint64_t off, uint6
     src = S.data + off;
     return true;
   }
+  if (nb == 0) {  // an empty range is an empty buffer wherever it points (get(k, o, o)); the
+    src = S.data;  // caller's length check then rejects it as the oracle does
+    return true;
+  }
   int64_t lo = 0, hi = S.npieces - 1;
   if (hi < 0 || S.pieces[0].off > off) return false;
   while (lo < hi) {  // last piece with p.off <= off
