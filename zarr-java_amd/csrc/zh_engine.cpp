@@ -1656,6 +1656,22 @@ int zh_plan_wait(zh_plan* p, char* err, size_t errlen) {
               (int32_t)(uint32_t)w[kStDetailA], (int32_t)(uint32_t)w[kStDetailB]);
       return ZH_EDATA;
     }
+    if (kind == kFlagLength && level == 0 && p->args.crc_extra) {
+      // The reference's pipeline runs the crc32c stage before the bytes codec: the checksum over
+      // the chunk's stored bytes decides first (error path only: one workgroup on the device).
+      uint64_t o[3] = {0, 0, 0};
+      uint64_t* dw = p->d_status + (size_t)i * kStWords;
+      hipStream_t s = p->last_stream ? p->last_stream : p->ctx->stream;
+      ZH_HIP(launch_chunk_crc_detail(p->args, i, (int64_t)rank, dw, s));
+      ZH_HIP(hipMemcpyAsync(o, dw, sizeof o, hipMemcpyDeviceToHost, s));
+      ZH_HIP(hipStreamSynchronize(s));
+      if (o[0] & 2) {
+        set_err(err, errlen,
+                "The checksum of the sharding index is invalid. Stored: %d Computed: %d",
+                (int32_t)(uint32_t)o[1], (int32_t)(uint32_t)o[2]);
+        return ZH_EDATA;
+      }
+    }
     if (kind == kFlagShort) {  // the level-2 decode of a sub-shard shorter than its index
       const int64_t cps2 = (int64_t)p->args.rank.r2 - 1;
       set_err(err, errlen, "Shard of %lld bytes is smaller than its index (%lld bytes).",

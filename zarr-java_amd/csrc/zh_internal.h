@@ -254,6 +254,9 @@ hipError_t launch_nested_index(const NestArgs& a, int grid, hipStream_t stream);
 hipError_t launch_data_crc(const DataCrcArgs& a, int grid, hipStream_t stream);
 hipError_t launch_data_crc_partial(const DataCrcArgs& a, int grid, hipStream_t stream);
 hipError_t launch_data_crc_finalize(const DataCrcArgs& a, hipStream_t stream);
+// error path: the crc32c of a single-level chunk rejected for its length (out: 3 words)
+hipError_t launch_chunk_crc_detail(const ScatterArgs& a, int64_t shard, int64_t lin,
+                                   uint64_t* out, hipStream_t stream);
 extern std::atomic<int64_t> g_last_fast_path;  // diagnostic, zh_debug_last_fast_path
 extern std::atomic<int64_t> g_last_encode_path;
 bool rowcrc_lds_at_zero();  // the row-CRC tile kernels have no static LDS

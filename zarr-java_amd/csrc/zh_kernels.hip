@@ -2884,7 +2884,8 @@ __global__ __launch_bounds__(kBlock) void nested_index_kernel(NestArgs a) {
           if (!(off2 <= nb1 && nb2 <= nb1 - off2)) {
             chunk_error(st, nest_rank(a, lin1, k2), kFlagRange | kFlagLeaf);
           } else if (nb2 != (uint64_t)a.leaf_nbytes) {
-            chunk_error(st, nest_rank(a, lin1, k2), kFlagLength | kFlagLeaf);
+            // with a leaf crc32c the checksum comes first (below)
+            if (!a.leaf_crc) chunk_error(st, nest_rank(a, lin1, k2), kFlagLength | kFlagLeaf);
           } else {
             eo = off1 + off2;
             en = nb2;
@@ -2895,9 +2896,11 @@ __global__ __launch_bounds__(kBlock) void nested_index_kernel(NestArgs a) {
       flat[2 * f + 1] = en;
     }
     if (!ok || !a.leaf_crc) continue;
-    // Crc32cCodec.decode (:24-48) of the cell's leaves outside the requested part: the level-2
-    // decode reads every leaf of the sub-shard (:97-103); the data-CRC pass checks the leaves
-    // inside the part.  Uniform over the workgroup (block_crc).
+    // Crc32cCodec.decode (:24-48) of the cell's leaves outside the requested part, and of every
+    // leaf whose stored length is wrong: the level-2 decode reads every leaf of the sub-shard
+    // (:97-103), the crc32c stage before the bytes codec (so a wrong length fails the checksum
+    // unless it happens to match, then the length, Q12).  The data-CRC pass checks the
+    // well-formed leaves inside the part.  Uniform over the workgroup (block_crc).
     for (int64_t k2 = 0; k2 < a.cps2; k2++) {
       int64_t q = k2;
       bool inside = true;
@@ -2908,21 +2911,70 @@ __global__ __launch_bounds__(kBlock) void nested_index_kernel(NestArgs a) {
           q /= a.r[d];
           inside = inside && lo_e < S.part_hi[d] && lo_e + a.leaf[d] > S.part_lo[d];
         }
-      if (inside) continue;
       const uint64_t off2 = ld_u64_unaligned(ib + 16 * k2, a.sub_be);
       const uint64_t nb2 = ld_u64_unaligned(ib + 16 * k2 + 8, a.sub_be);
-      if (off2 == ~0ull || nb2 == ~0ull || !(off2 <= nb1 && nb2 <= nb1 - off2) ||
-          nb2 != (uint64_t)a.leaf_nbytes)
-        continue;  // missing, or reported above
+      const bool len_ok = nb2 == (uint64_t)a.leaf_nbytes;
+      if ((inside && len_ok) || off2 == ~0ull || nb2 == ~0ull ||
+          !(off2 <= nb1 && nb2 <= nb1 - off2))
+        continue;  // the data-CRC pass's, missing, or reported above
+      const uint32_t rk = nest_rank(a, lin1, k2);
+      if (nb2 < 4) {  // no room for the checksum
+        if (tid == 0) chunk_error(st, rk, kFlagLength | kFlagLeaf);
+        continue;
+      }
       const uint8_t* lp = sub + off2;
       const uint32_t c = block_crc(lp, (int64_t)nb2 - 4, T, red);
       const uint8_t* sp = lp + nb2 - 4;
       const uint32_t stored = (uint32_t)sp[0] | ((uint32_t)sp[1] << 8) |
                               ((uint32_t)sp[2] << 16) | ((uint32_t)sp[3] << 24);
       if (c != stored && tid == 0)
-        chunk_error(st, nest_rank(a, lin1, k2), kFlagChunkCrc | kFlagLeaf, stored, c);
+        chunk_error(st, rk, kFlagChunkCrc | kFlagLeaf, stored, c);
+      else if (!len_ok && tid == 0)
+        chunk_error(st, rk, kFlagLength | kFlagLeaf);
     }
   }
+}
+
+// Error path of a single-level chain with a chunk crc32c (zh_plan_wait): the chunk of shard
+// `shard`, index entry `lin`, was rejected for its length.  The reference's pipeline runs the
+// crc32c stage before the bytes codec, so the checksum over its stored bytes decides first:
+// out = {1 + (mismatch ? 2 : 0), stored, computed} (out[0] = 0: under 4 bytes).  One workgroup.
+__global__ __launch_bounds__(kBlock) void chunk_crc_detail_kernel(ScatterArgs a, int64_t shard,
+                                                                  int64_t lin, uint64_t* out) {
+  __shared__ uint32_t T[1][256];
+  __shared__ uint32_t red[kBlock];
+  const int tid = threadIdx.x;
+  {
+    uint32_t c = (uint32_t)tid;
+#pragma unroll
+    for (int k = 0; k < 8; k++) c = (c & 1) ? (c >> 1) ^ kPoly : c >> 1;
+    T[0][tid] = c;
+  }
+  __syncthreads();
+  const DevShard& S = a.shards[shard];
+  uint64_t off, nb;
+  index_entry(a, S, lin, off, nb);
+  const uint8_t* src = nullptr;
+  const uint64_t total = (uint64_t)S.nbytes;
+  if (!(off <= total && nb <= total - off) || nb < 4 || !piece_src(S, off, nb, src)) {
+    if (tid == 0) out[0] = 0;
+    return;
+  }
+  const uint32_t c = block_crc(src, (int64_t)nb - 4, T, red);
+  if (tid != 0) return;
+  const uint8_t* sp = src + nb - 4;
+  const uint32_t stored = (uint32_t)sp[0] | ((uint32_t)sp[1] << 8) | ((uint32_t)sp[2] << 16) |
+                          ((uint32_t)sp[3] << 24);
+  out[0] = 1 | (c != stored ? 2 : 0);
+  out[1] = stored;
+  out[2] = c;
+}
+
+hipError_t launch_chunk_crc_detail(const ScatterArgs& a, int64_t shard, int64_t lin,
+                                   uint64_t* out, hipStream_t stream) {
+  hipLaunchKernelGGL(chunk_crc_detail_kernel, dim3(1), dim3(kBlock), 0, stream, a, shard, lin,
+                     out);
+  return hipGetLastError();
 }
 
 // ---------------------------------------------------------------------------------
