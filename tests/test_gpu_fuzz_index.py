@@ -8,6 +8,7 @@ ShardingIndexedCodec.java:215-231, 323-330) and the library's host planner over 
 of the file, ShardingIndexedCodec.java:340-356; whole-shard reads slice the file's bytes).
 The third form is the Java drop-in's: HipArray.read's store reads (the stored index, then
 zh_shard_ranges' ranges, zero-padded past the end of the file) handed to zh_array_read_pieces.
+ZH_FUZZ_TRIALS / ZH_FUZZ_SEED widen the search (default 48 trials, seed 0).
 Each trial corrupts a few entries of one or two shards with one of the mutations below and
 reads a random region (or the whole array) both ways:
 - both succeed → the outputs are equal, bit for bit;
@@ -16,6 +17,7 @@ reads a random region (or the whole array) both ways:
   names the chunk instead of the two lengths).
 The nested chain keeps its sub-shard index crc32c, so an outer entry that moves a sub-shard
 fails that checksum with the same Stored/Computed values on both sides."""
+import os
 import struct
 
 import numpy as np
@@ -144,9 +146,10 @@ def test_corrupt_index_entries_match_oracle(dev, tmp_path, chain, form):
     shape = [meta.shape[d] for d in range(meta.ndim)]
     allc = chunk_coords(meta, [0] * meta.ndim, shape)
     pos = {c: i for i, c in enumerate(allc)}
-    rng = np.random.default_rng(sum(map(ord, chain + form)))
+    seed = int(os.environ.get("ZH_FUZZ_SEED", "0"))
+    rng = np.random.default_rng(sum(map(ord, chain + form)) + 7919 * seed)
     kinds = {"ok": 0, "err": 0}
-    for t in range(32):
+    for t in range(int(os.environ.get("ZH_FUZZ_TRIALS", "48"))):
         bad = list(shards)
         muts = []
         for i in rng.choice(len(bad), size=int(rng.integers(1, 3)), replace=False):
