@@ -1,8 +1,8 @@
 """Seeded corrupt shard indexes on the HIP path vs the oracle (SURVEY §8(c) edge cases:
 erasures, collisions, out-of-range and wrapping entries).
 
-The shard index is read without its crc32c here, so every corrupt entry reaches the code that
-interprets it: the device's resolve kernel (memory shards: ByteBufferDataProvider slices,
+The shard index carries no crc32c here (one chain: a recomputed, valid one), so every corrupt
+entry reaches the code that interprets it: the device's resolve kernel (memory shards: ByteBufferDataProvider slices,
 ShardingIndexedCodec.java:215-231, 323-330) and the library's host planner over files
 (sub-shard reads: StoreHandleDataProvider.read → FilesystemStore.get, zero-padded past the end
 of the file, ShardingIndexedCodec.java:340-356; whole-shard reads slice the file's bytes).
@@ -86,7 +86,11 @@ def corrupt(rng, meta, shard, nbad):
             ents[k] = [ib, want]
     idx = b"".join(struct.pack(fmt, *e) for e in ents)
     if meta.chain.index_has_crc32c:
-        idx += struct.pack("<I", O.crc32c(idx))
+        c = O.crc32c(idx)
+        if rng.random() < 0.15:
+            names.append("index_crc")
+            c ^= 1 << int(rng.integers(32))
+        idx += struct.pack("<I", c)
     out = bytearray(shard[:ib] + idx + shard[ib + isz:])
     assert len(out) == total
     if total > isz and rng.random() < 0.4:  # one payload byte flipped (a chunk crc32c, a
@@ -97,15 +101,20 @@ def corrupt(rng, meta, shard, nbad):
 
 
 # test_gpu_pieces' chains, plus leaves with a crc32c under nested sharding (the sub-shard
-# decode checks every leaf of a referenced cell, inside the requested part or not)
+# decode checks every leaf of a referenced cell, inside the requested part or not), plus the
+# shard index with its crc32c (corrupt entries under a recomputed, valid crc; sometimes the
+# crc itself broken: the index checksum is then reported first)
 FUZZ_CHAINS = dict(CHAINS, nested_crc=dict(sharded=True, inner_chunk_shape=[8, 8, 8],
-                                           nested_chunk_shape=[4, 4, 8], inner_crc32c=True))
+                                           nested_chunk_shape=[4, 4, 8], inner_crc32c=True),
+                   index_crc=dict(sharded=True, inner_chunk_shape=[4, 8, 8], index_crc32c=True,
+                                  inner_crc32c=True, index_location=A.ZH_INDEX_START))
 
 
 def make_case(chain, seed):
     shape = [24, 32, 48]
-    meta = A.make_meta(shape, [8, 16, 24], 4, fill=(7).to_bytes(4, "little"),
-                       index_crc32c=False, **FUZZ_CHAINS[chain])
+    kw = dict(index_crc32c=False)
+    kw.update(FUZZ_CHAINS[chain])
+    meta = A.make_meta(shape, [8, 16, 24], 4, fill=(7).to_bytes(4, "little"), **kw)
     arr = rand_array(shape, 4, seed=seed, fill_frac=0.2, fill=0)
     arr[:4, :8, :8] = 0  # an inner chunk of zeros: a missing entry
     return meta, arr
