@@ -56,11 +56,6 @@ struct zh_ctx {
   // created, run and freed while mu is held (read_region, read_multi_impl)
   uint8_t* file_pin = nullptr;
   size_t file_pin_cap = 0;
-  // the index crc32c's stream: plans run the index check beside their resolve/scatter kernels
-  // (it only writes status words) and join it before the status read-back; created on first use
-  std::mutex side_mu;
-  hipStream_t side = nullptr;
-  bool side_failed = false;
 };
 
 namespace zh {
@@ -156,7 +151,6 @@ struct zh_plan {
   // device state
   std::vector<std::pair<void*, size_t>> blocks;  // context-cache blocks owned by the plan
   hipEvent_t done_ev = nullptr;  // recorded after every execute (plan_free waits on it)
-  hipEvent_t crc_fork = nullptr, crc_join = nullptr;  // the index check on ctx->side
   uint8_t* d_tables = nullptr;   // one allocation holding the tables below
   zh::DevShard* d_shards = nullptr;
   uint64_t* d_status = nullptr;

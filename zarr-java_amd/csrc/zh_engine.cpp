@@ -291,7 +291,6 @@ void zh_ctx_destroy(zh_ctx* c) {
   if (!c) return;
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamDestroy(c->stream);
-  if (c->side) (void)hipStreamDestroy(c->side);
   if (c->status_pin) (void)hipHostFree(c->status_pin);
   if (c->upload_pin) (void)hipHostFree(c->upload_pin);
   if (c->file_pin) (void)hipHostFree(c->file_pin);
@@ -844,9 +843,6 @@ void plan_free(zh_plan* p) {
     (void)hipEventSynchronize(p->done_ev);
     (void)hipEventDestroy(p->done_ev);
   }
-  if (p->crc_join) (void)hipEventSynchronize(p->crc_join);  // joined before done_ev anyway
-  if (p->crc_fork) (void)hipEventDestroy(p->crc_fork);
-  if (p->crc_join) (void)hipEventDestroy(p->crc_join);
   if (p->status_slot >= 0 || p->upload_slot >= 0) {  // after done_ev: copies may be queued
     std::lock_guard<std::mutex> lk(p->ctx->status_mu);
     if (p->status_slot >= 0) p->ctx->status_free.push_back(p->status_slot);
@@ -1480,22 +1476,6 @@ int plan_create(zh_ctx* ctx, const zh_array_meta* m, const SrcDesc* srcs, int64_
   return ZH_OK;
 }
 
-// The context's side stream (created on first use; null when creation failed).
-static hipStream_t ctx_side_stream(zh_ctx* c) {
-  std::lock_guard<std::mutex> lk(c->side_mu);
-  if (!c->side && !c->side_failed) {
-    int cur = 0;
-    (void)hipGetDevice(&cur);
-    (void)hipSetDevice(c->device);
-    if (hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking) != hipSuccess) {
-      c->side = nullptr;
-      c->side_failed = true;
-    }
-    (void)hipSetDevice(cur);
-  }
-  return c->side;
-}
-
 // Enqueues one execution of the plan on stream s (also the body a hipGraph captures).
 int plan_enqueue_impl(zh_plan* p, void* out, hipStream_t s) {
   char* err = nullptr;
@@ -1534,23 +1514,8 @@ int plan_enqueue_impl(zh_plan* p, void* out, hipStream_t s) {
     }
     ZH_HIP(hipEventRecord(ev[0], s));
   }
-  // The index crc32c only writes the status words, which zh_plan_wait reads after the join:
-  // it runs on the context's side stream beside resolve/scatter (a small read's chain of
-  // dependent kernels loses the 12.7 µs check, §4 "Small reads"); ZH_CRC_SIDE=0 keeps it first
-  // on s.  Not under graph capture.
-  hipStream_t cs = s;
-  if (p->n_crc_jobs > 0 && !p->use_graph && env_int("ZH_CRC_SIDE", 1) != 0) {
-    hipStream_t side = ctx_side_stream(p->ctx);
-    if (side && (p->crc_fork || hipEventCreateWithFlags(&p->crc_fork, hipEventDisableTiming) == hipSuccess) &&
-        (p->crc_join || hipEventCreateWithFlags(&p->crc_join, hipEventDisableTiming) == hipSuccess)) {
-      ZH_HIP(hipEventRecord(p->crc_fork, s));
-      ZH_HIP(hipStreamWaitEvent(side, p->crc_fork, 0));
-      cs = side;
-    }
-  }
   ZH_HIP(launch_crc(p->d_crc_jobs, p->n_crc_jobs, p->n_crc_spans, p->crc_shift, p->d_crc_partials,
-                    p->d_status, cs));
-  if (cs != s) ZH_HIP(hipEventRecord(p->crc_join, cs));
+                    p->d_status, s));
   if (p->d_flat) ZH_HIP(launch_nested_index(p->nest, p->nest_grid, s));
   ScatterArgs a = p->args;
   a.region = (p->flags & ZH_OUT_DEVICE) ? (uint8_t*)out : p->d_out;
@@ -1566,7 +1531,6 @@ int plan_enqueue_impl(zh_plan* p, void* out, hipStream_t s) {
     ZH_HIP(hipEventRecord(ev[2], s));
     p->ev_pending.push_back(ev);
   }
-  if (cs != s) ZH_HIP(hipStreamWaitEvent(s, p->crc_join, 0));  // before the status read-back
   if (!(p->flags & ZH_OUT_DEVICE))
     ZH_HIP(hipMemcpyAsync(out, p->d_out, (size_t)p->out_bytes, hipMemcpyDeviceToHost, s));
   return ZH_OK;
