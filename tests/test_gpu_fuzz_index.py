@@ -186,3 +186,40 @@ def test_corrupt_index_entries_match_oracle(dev, tmp_path, chain, form):
         _same(got, want, ctx)
         kinds[want[0]] += 1
     assert kinds["ok"] and kinds["err"], kinds  # both outcomes exercised
+
+
+@pytest.mark.parametrize("form", ["memory", "files"])
+def test_unsharded_crc_chunk_of_wrong_length(dev, tmp_path, form):
+    """A whole chunk with a crc32c whose stored length is wrong: the reference's pipeline checks
+    the checksum first (so the checksum fails, with its stored and computed values) unless the
+    stored crc happens to match the bytes, then the length (Q12).  Device and oracle agree on
+    which error and on its text, in chunk order."""
+    shape = [16, 24]
+    meta = A.make_meta(shape, [8, 8], 4, transpose_order=[1, 0], inner_crc32c=True)
+    arr = rand_array(shape, 4, seed=227)
+    chunks = encode_oracle(meta, arr)
+    rng = np.random.default_rng(229)
+    cases = []
+    # appended bytes (checksum over the longer body fails), a truncated chunk, a chunk whose
+    # longer body carries a matching crc (then the length is reported)
+    longer = bytearray(chunks[1]) + bytes(8)
+    cases.append({1: bytes(longer)})
+    cases.append({4: chunks[4][:-12]})
+    body = bytes(rng.integers(0, 256, 8 * 8 * 4 + 16, dtype=np.uint8))
+    cases.append({2: body + struct.pack("<I", O.crc32c(body)), 5: chunks[5][:-1]})
+    for k, mod in enumerate(cases):
+        bad = [mod.get(i, c) for i, c in enumerate(chunks)]
+        off, shp = [0, 0], shape
+        if form == "memory":
+            want = _outcome(lambda: O.array_read(meta, bad, off, shp))
+            got = _outcome(lambda: device_read(dev, meta, bad, off, shp))
+        else:
+            paths = write_store(tmp_path, meta, bad, tag=f"u{k}")
+            want = _outcome(lambda: store_read(meta, paths, off, shp))
+            got = _outcome(lambda: files_read(dev, meta, paths, off, shp))
+        assert want[0] == got[0] == "err", (k, want, got)
+        if want[1].startswith("unexpected inner chunk byte length"):
+            assert got[1].startswith("unexpected inner chunk byte length"), (k, got, want)
+            assert k == 2 and got[1].endswith("for chunk [0, 2]"), got
+        else:
+            assert got[1] == want[1], (k, got, want)

@@ -1002,7 +1002,10 @@ int plan_create(zh_ctx* ctx, const zh_array_meta* m, const SrcDesc* srcs, int64_
         return fail(ZH_EDATA);
       }
       S.index_off = c.index_location == ZH_INDEX_START ? 0 : S.nbytes - isz;
-    } else if (S.nbytes != p->args.inner_nbytes + p->args.crc_extra) {  // Q12 (knowing divergence)
+    } else if (S.nbytes != p->args.inner_nbytes + p->args.crc_extra &&
+               !(p->args.crc_extra && S.nbytes >= 4)) {  // Q12 (knowing divergence); with a
+      // crc32c the checksum decides first: the resolve kernel flags the chunk, zh_plan_wait
+      // checks its crc on the device (chunk_crc_detail_kernel)
       set_err(err, errlen,
               "unexpected inner chunk byte length: %lld (expected %lld) for chunk %s",
               (long long)S.nbytes, (long long)(p->args.inner_nbytes + p->args.crc_extra),
@@ -1659,7 +1662,7 @@ int zh_plan_wait(zh_plan* p, char* err, size_t errlen) {
     if (kind == kFlagLength && level == 0 && p->args.crc_extra) {
       // The reference's pipeline runs the crc32c stage before the bytes codec: the checksum over
       // the chunk's stored bytes decides first (error path only: one workgroup on the device).
-      uint64_t o[3] = {0, 0, 0};
+      uint64_t o[4] = {0, 0, 0, 0};
       uint64_t* dw = p->d_status + (size_t)i * kStWords;
       hipStream_t s = p->last_stream ? p->last_stream : p->ctx->stream;
       ZH_HIP(launch_chunk_crc_detail(p->args, i, (int64_t)rank, dw, s));
@@ -1669,6 +1672,12 @@ int zh_plan_wait(zh_plan* p, char* err, size_t errlen) {
         set_err(err, errlen,
                 "The checksum of the sharding index is invalid. Stored: %d Computed: %d",
                 (int32_t)(uint32_t)o[1], (int32_t)(uint32_t)o[2]);
+        return ZH_EDATA;
+      }
+      if (!ch.sharded) {  // the planner's Q12 text for a whole chunk
+        set_err(err, errlen, "unexpected inner chunk byte length: %lld (expected %lld) for chunk %s",
+                (long long)o[3], (long long)(p->args.inner_nbytes + p->args.crc_extra),
+                fmt_ints(p->coords.data() + i * n, n).c_str());
         return ZH_EDATA;
       }
     }

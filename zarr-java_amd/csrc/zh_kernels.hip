@@ -733,6 +733,13 @@ __device__ __forceinline__ ItemDesc resolve_one(const ScatterArgs& a, int64_t ci
       return D;
     }
   }
+  if (!a.sharded && (uint64_t)S.nbytes != (uint64_t)(a.inner_nbytes + a.crc_extra)) {
+    // a whole chunk of the wrong length with a crc32c (the planner rejects the others): its
+    // checksum decides first (zh_plan_wait, chunk_crc_detail_kernel)
+    chunk_error(a.status + s * kStWords, 0, kFlagLength);
+    D.kind = kDescSkip;
+    return D;
+  }
   D.src = (uint64_t)(uintptr_t)src;
   D.kind = full ? kDescFullCopy : kDescClip;
   if (!full && row_clip && !a.tile && a.crc_extra == 0 &&
@@ -2938,7 +2945,8 @@ __global__ __launch_bounds__(kBlock) void nested_index_kernel(NestArgs a) {
 // Error path of a single-level chain with a chunk crc32c (zh_plan_wait): the chunk of shard
 // `shard`, index entry `lin`, was rejected for its length.  The reference's pipeline runs the
 // crc32c stage before the bytes codec, so the checksum over its stored bytes decides first:
-// out = {1 + (mismatch ? 2 : 0), stored, computed} (out[0] = 0: under 4 bytes).  One workgroup.
+// out = {1 + (mismatch ? 2 : 0), stored, computed, stored length} (out[0] = 0: under 4 bytes).
+// Unsharded chains: the whole chunk object.  One workgroup.
 __global__ __launch_bounds__(kBlock) void chunk_crc_detail_kernel(ScatterArgs a, int64_t shard,
                                                                   int64_t lin, uint64_t* out) {
   __shared__ uint32_t T[1][256];
@@ -2952,12 +2960,15 @@ __global__ __launch_bounds__(kBlock) void chunk_crc_detail_kernel(ScatterArgs a,
   }
   __syncthreads();
   const DevShard& S = a.shards[shard];
-  uint64_t off, nb;
-  index_entry(a, S, lin, off, nb);
+  uint64_t off = 0, nb = (uint64_t)S.nbytes;
+  if (a.sharded) index_entry(a, S, lin, off, nb);
   const uint8_t* src = nullptr;
   const uint64_t total = (uint64_t)S.nbytes;
   if (!(off <= total && nb <= total - off) || nb < 4 || !piece_src(S, off, nb, src)) {
-    if (tid == 0) out[0] = 0;
+    if (tid == 0) {
+      out[0] = 0;
+      out[3] = nb;
+    }
     return;
   }
   const uint32_t c = block_crc(src, (int64_t)nb - 4, T, red);
@@ -2968,6 +2979,7 @@ __global__ __launch_bounds__(kBlock) void chunk_crc_detail_kernel(ScatterArgs a,
   out[0] = 1 | (c != stored ? 2 : 0);
   out[1] = stored;
   out[2] = c;
+  out[3] = nb;
 }
 
 hipError_t launch_chunk_crc_detail(const ScatterArgs& a, int64_t shard, int64_t lin,
