@@ -106,7 +106,10 @@ typedef struct zh_array_meta {
   int32_t ndim;
   int32_t dtype_size;                 /* DataType.getByteCount(): 1, 2, 4 or 8             */
   int32_t dtype_is_bool;              /* bool decodes as b != 0 (core BytesCodec.java:24-33) */
-  int32_t reserved0;
+  int32_t dtype_is_float;             /* float32 / float64: the write path's all-fill test
+                                       * compares as Java's == (MultiArrayUtils.allValuesEqual,
+                                       * MultiArrayUtils.java:69-80), so a ±0 fill matches
+                                       * both zeros; other types compare bits */
   int64_t shape[ZH_MAX_DIMS];         /* array shape                                       */
   int32_t chunk_shape[ZH_MAX_DIMS];   /* regular chunk grid shape (= shard shape)          */
   uint8_t fill_value[8];              /* parsed fill value, element bytes little-endian     */

@@ -718,15 +718,35 @@ int zo_array_read_store(const zh_array_meta* m, const char* const* paths, int64_
 /* ---------------------------------------------------------------------------------
  * Write path
  * ------------------------------------------------------------------------------- */
-/* MultiArrayUtils.allValuesEqual — M/utils/MultiArrayUtils.java:69-102 (bitwise here) */
-static int all_equal(const nd_t* a, const int64_t* off, const int64_t* shape, const uint8_t* fill) {
+/* One element against the fill value as ValueAccessor.isEqual compares them
+ * (M/utils/MultiArrayUtils.java:104-280): Java's == on float / double (NaN equals nothing,
+ * +0.0 == -0.0), the integer value otherwise (= the bits). */
+static int elem_equal(const uint8_t* e, const uint8_t* fill, int ds, int is_float) {
+  if (is_float && ds == 4) {
+    float x, y;
+    memcpy(&x, e, 4);
+    memcpy(&y, fill, 4);
+    return x == y;
+  }
+  if (is_float && ds == 8) {
+    double x, y;
+    memcpy(&x, e, 8);
+    memcpy(&y, fill, 8);
+    return x == y;
+  }
+  return memcmp(e, fill, ds) == 0;
+}
+
+/* MultiArrayUtils.allValuesEqual — M/utils/MultiArrayUtils.java:69-80 */
+static int all_equal(const nd_t* a, const int64_t* off, const int64_t* shape, const uint8_t* fill,
+                     int is_float) {
   int n = a->ndim, ds = a->dsize;
   int64_t total = prod64(shape, n);
   int64_t idx[ZH_MAX_DIMS] = {0};
   for (int64_t t = 0; t < total; t++) {
     int64_t o = 0;
     for (int d = 0; d < n; d++) o += (off[d] + idx[d]) * a->stride[d];
-    if (memcmp(a->data + o * ds, fill, ds) != 0) return 0;
+    if (!elem_equal(a->data + o * ds, fill, ds, is_float)) return 0;
     for (int d = n - 1; d >= 0; d--) {
       if (++idx[d] < shape[d]) break;
       idx[d] = 0;
@@ -794,7 +814,7 @@ static int sharding_encode(const zh_array_meta* m, const nd_t* chunk, uint8_t** 
       o[d] = coords[k * n + d] * inner[d];
       sh[d] = inner[d];
     }
-    if (all_equal(chunk, o, sh, m->fill_value)) {                    /* :129-133 */
+    if (all_equal(chunk, o, sh, m->fill_value, m->dtype_is_float)) { /* :129-133 */
       offs[k] = -1;
       lens[k] = 0;
     } else {
@@ -904,7 +924,7 @@ int zo_array_write(const zh_array_meta* m, const void* src_v, const int64_t* off
     copy_region(&src, so, &ch, dof, sh);
     int64_t full[ZH_MAX_DIMS];
     for (int d = 0; d < n; d++) full[d] = m->chunk_shape[d];
-    if (all_equal(&ch, zero, full, m->fill_value)) {                 /* writeChunk :150-151 */
+    if (all_equal(&ch, zero, full, m->fill_value, m->dtype_is_float)) { /* writeChunk :150-151 */
       out_bufs[i] = NULL;
       out_sizes[i] = 0;
       continue;

@@ -131,13 +131,13 @@ class FakeJVM:
         return a.copy() if copy else a
 
     def meta_args(self, meta):
-        """DeviceChain's packing: int[14] meta, long[] shape, int[] chunkShape, int[] innerShape
+        """DeviceChain's packing: int[15] meta, long[] shape, int[] chunkShape, int[] innerShape
         (nested: inner then leaf shape), int[] order, byte[] fill."""
         n, ch = meta.ndim, meta.chain
         mi = [n, meta.dtype_size, meta.dtype_is_bool, ch.sharded, ch.has_transpose, ch.endian,
               ch.index_endian, ch.index_has_crc32c, ch.index_location, ch.nested,
               ch.nested_index_endian, ch.nested_index_has_crc32c, ch.nested_index_location,
-              ch.inner_crc32c]
+              ch.inner_crc32c, meta.dtype_is_float]
         inner = [ch.inner_chunk_shape[d] for d in range(n)]
         if ch.nested:
             inner += [ch.nested_chunk_shape[d] for d in range(n)]

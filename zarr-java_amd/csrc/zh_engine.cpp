@@ -492,6 +492,14 @@ void fill_common_args(const zh_array_meta* m, const int64_t* region_shape, bool 
   uint64_t f = 0;
   for (int i = 0; i < 8; i++) f |= (uint64_t)m->fill_value[i] << (8 * i);
   a.fill = f;
+  // the write path's all-fill test compares as Java's == (MultiArrayUtils.allValuesEqual,
+  // M/utils/MultiArrayUtils.java:69-80, 104-150): for a float ±0 fill, +0.0 == -0.0
+  a.fill_mask = ~0ull;
+  if (m->dtype_is_float && (m->dtype_size == 4 || m->dtype_size == 8)) {
+    const uint64_t sign = 1ull << (8 * m->dtype_size - 1);
+    const uint64_t elem = m->dtype_size == 8 ? ~0ull : 0xFFFFFFFFull;
+    if ((f & elem & ~sign) == 0) a.fill_mask = ~sign;
+  }
   if (encode) {
     a.fs = n - 1;
     a.fd = order[n - 1];

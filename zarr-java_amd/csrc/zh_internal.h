@@ -147,6 +147,8 @@ struct ScatterArgs {
   int64_t cps_stride[kMaxDims]; // index entry stride of each inner-chunk coordinate
   int64_t inner_nbytes;
   uint64_t fill;                // fill_value bytes (little-endian), replicated as needed
+  uint64_t fill_mask;           // write path's all-fill test: element bits compared (a float
+                                // ±0 fill drops the sign bit; else all ones), low dsize bytes
   FastDiv inner_div[kMaxDims];  // divisors for unclipped extents
   // decode fast path for unclipped inner chunks
   ItemDesc* desc;               // per inner chunk (resolve kernel output)

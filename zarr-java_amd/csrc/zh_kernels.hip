@@ -381,6 +381,18 @@ __device__ __forceinline__ int64_t make_item(const ScatterArgs& a, int64_t item,
   return s;
 }
 
+// The write path's all-fill test (MultiArrayUtils.allValuesEqual, Java's ==): does an
+// element differ from fill_value?  Bits compared under a.fill_mask, which drops the sign bit
+// for a float ±0 fill (+0.0 == -0.0); every other fill compares every bit (a NaN fill: DESIGN
+// §3 Q19).
+__device__ __forceinline__ bool ne16(const uint4& v, const uint4& f, const uint4& m) {
+  return (((v.x ^ f.x) & m.x) | ((v.y ^ f.y) & m.y) | ((v.z ^ f.z) & m.z) |
+          ((v.w ^ f.w) & m.w)) != 0;
+}
+__device__ __forceinline__ bool ne4x4(const uint4& v, uint32_t f, uint32_t m) {
+  return (((v.x ^ f) | (v.y ^ f) | (v.z ^ f) | (v.w ^ f)) & m) != 0;
+}
+
 // ---------------------------------------------------------------------------------
 // row pass: rows along dim F, unit-stride on both sides (on the destination only for
 // constant fills).  VEC: 16-byte granules; otherwise single elements with
@@ -412,6 +424,7 @@ __device__ __forceinline__ bool row_pass(const ScatterArgs& a, const Item& it, i
   const uint32_t total = (r1 - r0) * gpr;
   const uint4 fv = fill16<DS>(CHECK ? a.fill : it.fill);
   const uint4 pad = fill16<DS>(a.fill);  // CLIP: raw fill_value granule (encoded on store)
+  const uint4 fm = fill16<DS>(a.fill_mask);
   int64_t sF = 1, dF = 1;
   uint32_t vgF = 0;  // CLIP: loadable granules along F
 #pragma unroll
@@ -473,17 +486,16 @@ __device__ __forceinline__ bool row_pass(const ScatterArgs& a, const Item& it, i
       if (!ok[u]) continue;
       if constexpr (CHECK) {
         if constexpr (VEC) {
-          diff |= (vv[u].x != fv.x) | (vv[u].y != fv.y) | (vv[u].z != fv.z) | (vv[u].w != fv.w);
+          diff |= ne16(vv[u], fv, fm);
         } else {
-          diff |= sv[u] != (T)a.fill;
+          diff |= ((sv[u] ^ (T)a.fill) & (T)a.fill_mask) != 0;
         }
       } else if constexpr (VEC) {
         st16(it.dbase + doff[u], fill ? fv : xform16<DS>(vv[u], a.swap, a.is_bool));
-        if constexpr (FLAG)
-          diff |= (vv[u].x != pad.x) | (vv[u].y != pad.y) | (vv[u].z != pad.z) | (vv[u].w != pad.w);
+        if constexpr (FLAG) diff |= ne16(vv[u], pad, fm);
       } else {
         st1<DS>(it.dbase + doff[u], fill ? (T)it.fill : xform1<DS>(sv[u], a.swap, a.is_bool));
-        if constexpr (FLAG) diff |= sv[u] != (T)a.fill;
+        if constexpr (FLAG) diff |= ((sv[u] ^ (T)a.fill) & (T)a.fill_mask) != 0;
       }
     }
   }
@@ -1143,6 +1155,7 @@ __global__ __launch_bounds__(kBlock) void decode_rows_kernel(ScatterArgs a) {
   uint64_t da[U];
   bool differs = false;
   const uint4 ffill = fill16<DS>(a.fill);
+  const uint4 fmask = fill16<DS>(a.fill_mask);
   auto load_step = [&](uint4* v, uint64_t* dd) {
 #pragma unroll
     for (int u = 0; u < U; u++) {
@@ -1186,8 +1199,7 @@ __global__ __launch_bounds__(kBlock) void decode_rows_kernel(ScatterArgs a) {
 #pragma unroll
       for (int u = 0; u < U; u++)
         if (da[u] != ~0ull)
-          differs |= (va[u].x != ffill.x) | (va[u].y != ffill.y) | (va[u].z != ffill.z) |
-                      (va[u].w != ffill.w);
+          differs |= ne16(va[u], ffill, fmask);
       if (piece_end) {  // uniform: one flag byte per piece, set by any wave that saw data
         if (__ballot(differs) != 0 && (threadIdx.x & 63) == 0)
           a.flags[pitem(a, item_a) >> a.piece_shift] = 1;
@@ -1327,6 +1339,7 @@ __global__ __launch_bounds__(kBlock) void rows_group_kernel(ScatterArgs a) {
   for (int o = 0; o < 64; o += GL) qmask |= (((1ull << (1 << vs)) - 1) << (q << vs)) << o;
   const bool leader = lane == (q << vs);
   const uint4 ffill = fill16<DS>(a.fill);
+  const uint4 fmask = fill16<DS>(a.fill_mask);
   for (int64_t g = blockIdx.x; g < ngroups; g += gridDim.x) {
     const int64_t pg = a.item_mul ? (int64_t)(((uint64_t)g * a.item_mul) % (uint64_t)ngroups) : g;
     const int64_t c = pg * G + q;
@@ -1372,8 +1385,7 @@ __global__ __launch_bounds__(kBlock) void rows_group_kernel(ScatterArgs a) {
           const uint4 w = fill ? fv : xform16<DS>(v[u], a.swap, a.is_bool);
           st16s<(NT & 2) != 0>(dst + dd[u], w);
           if (FLAGS)
-            differs |= (v[u].x != ffill.x) | (v[u].y != ffill.y) | (v[u].z != ffill.z) |
-                       (v[u].w != ffill.w);
+            differs |= ne16(v[u], ffill, fmask);
           if constexpr (CRC) {  // the payload vector: stored (encode) or loaded (decode)
             const uint4 pv = FLAGS ? w : v[u];
             const v4u wv = {pv.x, pv.y, pv.z, pv.w};
@@ -1523,10 +1535,9 @@ __device__ __forceinline__ uint32_t fast_tiles_rows(const ScatterArgs& a, const 
     const bool live = ub + t < u1;
     if constexpr (FLAGS) {  // write path: any element != fill_value (uint32 tiles)
       if (live) {
-        const uint32_t f = (uint32_t)a.fill;
+        const uint32_t f = (uint32_t)a.fill, fm = (uint32_t)a.fill_mask;
 #pragma unroll
-        for (int k = 0; k < 8; k++)
-          differs |= (x[k].x != f) | (x[k].y != f) | (x[k].z != f) | (x[k].w != f);
+        for (int k = 0; k < 8; k++) differs |= ne4x4(x[k], f, fm);
       }
     }
     if (live) {
@@ -1744,7 +1755,7 @@ __global__ __launch_bounds__(kBlock) void tiles_group_kernel(ScatterArgs a) {
   const int64_t ngroups = (a.n_citems + G - 1) / G;
   const uint64_t qmask = (TG * 8 == 64 ? ~0ull : ((1ull << (TG * 8)) - 1)) << (q * TG * 8);
   const bool leader = lane == q * TG * 8;
-  const uint32_t f = (uint32_t)a.fill;
+  const uint32_t f = (uint32_t)a.fill, fm = (uint32_t)a.fill_mask;
   uint32_t* mine = lds + t * kTilePitch;
   for (int64_t gi = blockIdx.x; gi < ngroups; gi += gridDim.x) {
     const int64_t pg = a.item_mul ? (int64_t)(((uint64_t)gi * a.item_mul) % (uint64_t)ngroups) : gi;
@@ -1781,7 +1792,7 @@ __global__ __launch_bounds__(kBlock) void tiles_group_kernel(ScatterArgs a) {
         if (!PF) load(ub);  // inside the live branch: 46.3 → 42.3 ms on the c4crc encode
 #pragma unroll
         for (int k = 0; k < 8; k++) {
-          if (FLAGS) differs |= (x[k].x != f) | (x[k].y != f) | (x[k].z != f) | (x[k].w != f);
+          if (FLAGS) differs |= ne4x4(x[k], f, fm);
           uint32_t* row = mine + (wave * 8 + k) * 33 + g * 4;
           row[0] = xform1<4>(x[k].x, a.swap, 0);
           row[1] = xform1<4>(x[k].y, a.swap, 0);

@@ -64,15 +64,15 @@ JNIEXPORT void JNICALL Java_dev_zarr_zarrjava_hip_ZarrHip_ctxDestroy(JNIEnv* env
 
 /* meta: int[] {ndim, dtypeSize, isBool, sharded, hasTranspose, endian, indexEndian,
  *              indexCrc32c, indexLocation[, nested, nestedIndexEndian, nestedIndexCrc32c,
- *              nestedIndexLocation, innerCrc32c]}; shape long[ndim]; chunkShape/order int[ndim];
+ *              nestedIndexLocation, innerCrc32c[, isFloat]]}; shape long[ndim]; chunkShape/order int[ndim];
  *              innerShape int[ndim] (nested: int[2*ndim], inner then leaf shape);
  *              fill byte[dtypeSize] (little-endian element bytes). */
 static int build_meta(JNIEnv* env, jintArray jm, jlongArray jshape, jintArray jchunk,
                       jintArray jinner, jintArray jorder, jbyteArray jfill, zh_array_meta* m) {
   memset(m, 0, sizeof(*m));
-  jint mi[14] = {0};
+  jint mi[15] = {0};
   jsize nm = (*env)->GetArrayLength(env, jm);
-  (*env)->GetIntArrayRegion(env, jm, 0, nm < 14 ? nm : 14, mi);
+  (*env)->GetIntArrayRegion(env, jm, 0, nm < 15 ? nm : 15, mi);
   m->ndim = mi[0];
   if (m->ndim <= 0 || m->ndim > ZH_MAX_DIMS) return ZH_EUNSUPPORTED;
   m->dtype_size = mi[1];
@@ -88,6 +88,7 @@ static int build_meta(JNIEnv* env, jintArray jm, jlongArray jshape, jintArray jc
   m->chain.nested_index_has_crc32c = mi[11];
   m->chain.nested_index_location = mi[12];
   m->chain.inner_crc32c = mi[13];
+  m->dtype_is_float = mi[14];
   jlong sh[ZH_MAX_DIMS];
   jint ch[ZH_MAX_DIMS];
   (*env)->GetLongArrayRegion(env, jshape, 0, m->ndim, sh);

@@ -17,10 +17,10 @@ import java.nio.ByteOrder;
  * zh_array_meta fields the JNI shim expects.  Anything else → null (use the reference).
  */
 final class DeviceChain {
-    final int[] meta = new int[14]; // ndim, dtypeSize, isBool, sharded, hasTranspose, endian,
+    final int[] meta = new int[15]; // ndim, dtypeSize, isBool, sharded, hasTranspose, endian,
                                     // indexEndian, indexCrc32c, indexLocation, nested,
                                     // nestedIndexEndian, nestedIndexCrc32c,
-                                    // nestedIndexLocation, innerCrc32c
+                                    // nestedIndexLocation, innerCrc32c, isFloat
     // sharded: the inner chunk shape; nested: inner chunk shape followed by the leaf shape
     final long[] shape;
     final int[] chunkShape;
@@ -38,6 +38,9 @@ final class DeviceChain {
         meta[0] = m.ndim();
         meta[1] = m.dataType.getByteCount();
         meta[2] = "bool".equals(m.dataType.toString().toLowerCase()) ? 1 : 0;
+        // float32 / float64: the write path's all-fill test compares as == (a ±0 fill)
+        String dt = m.dataType.toString().toLowerCase();
+        meta[14] = "float32".equals(dt) || "float64".equals(dt) ? 1 : 0;
         fill = fillBytes(m);
     }
 

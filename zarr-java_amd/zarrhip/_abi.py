@@ -56,7 +56,7 @@ class zh_array_meta(C.Structure):
         ("ndim", C.c_int32),
         ("dtype_size", C.c_int32),
         ("dtype_is_bool", C.c_int32),
-        ("reserved0", C.c_int32),
+        ("dtype_is_float", C.c_int32),
         ("shape", C.c_int64 * ZH_MAX_DIMS),
         ("chunk_shape", C.c_int32 * ZH_MAX_DIMS),
         ("fill_value", C.c_uint8 * 8),
@@ -90,7 +90,8 @@ class zh_file_store(C.Structure):
     _fields_ = [("root", C.c_char_p), ("name", C.c_char_p)]
 
 
-def make_meta(shape, chunk_shape, dtype_size, *, fill=b"\0" * 8, is_bool=False, sharded=False,
+def make_meta(shape, chunk_shape, dtype_size, *, fill=b"\0" * 8, is_bool=False, is_float=False,
+              sharded=False,
               inner_chunk_shape=None, transpose_order=None, endian=ZH_ENDIAN_LITTLE,
               index_endian=ZH_ENDIAN_LITTLE, index_crc32c=True, index_location=ZH_INDEX_END,
               nested_chunk_shape=None, nested_index_endian=ZH_ENDIAN_LITTLE,
@@ -102,6 +103,7 @@ def make_meta(shape, chunk_shape, dtype_size, *, fill=b"\0" * 8, is_bool=False, 
     m.ndim = n
     m.dtype_size = dtype_size
     m.dtype_is_bool = 1 if is_bool else 0
+    m.dtype_is_float = 1 if is_float else 0
     for d in range(n):
         m.shape[d] = int(shape[d])
         m.chunk_shape[d] = int(chunk_shape[d])

@@ -156,8 +156,10 @@ class ArrayMetadata:
 def zh_meta_for(md, device_chain, is_bool):
     """zh_array_meta of an array's metadata (v3 or v2) and its device chain."""
     ch = device_chain.chain
+    core = getattr(md.data_type, "core", md.data_type)  # v2: its v3 core type
     return A.make_meta(md.shape, md.chunk_shape, md.data_type.getByteCount(),
                        fill=md.fill_bytes, is_bool=is_bool,
+                       is_float=core in (DataType.FLOAT32, DataType.FLOAT64),
                        sharded=ch["sharded"], inner_chunk_shape=ch.get("inner_chunk_shape"),
                        transpose_order=ch["transpose_order"], endian=ch["endian"],
                        index_endian=ch.get("index_endian", A.ZH_ENDIAN_LITTLE),
