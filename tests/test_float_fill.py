@@ -5,9 +5,8 @@ and an inner chunk of a shard (ShardingIndexedCodec.encode :129-133).
 
 - fill ±0.0: a chunk of zeros of either sign is all fill (+0.0 == -0.0): elided, so it reads
   back as the fill's zero — the oracle and the device agree byte for byte;
-- fill NaN: NaN == NaN is false, so the reference (and the oracle) never elides; the device
-  compares bits and elides a chunk whose elements all carry the fill's NaN bits, which reads
-  back the same bits: the stored chunks differ, the decoded array does not."""
+- fill NaN: NaN == NaN is false, so nothing is elided — every chunk and inner chunk is
+  written, boundary padding included (an elided inner chunk would read back as 0, Q1)."""
 import numpy as np
 import pytest
 
@@ -77,19 +76,15 @@ def test_device_zero_fill_matches_oracle_bytes(dev, dt, sharded):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("sharded", [False, True])
-def test_device_nan_fill_reads_back_the_same(dev, sharded):
-    """Q19: the device elides the chunks that hold only the fill's NaN bits, the oracle keeps
-    them; every other chunk is byte-identical and both stores decode to the same bits."""
-    dt = "<f4"
+@pytest.mark.parametrize("dt", ["<f4", "<f8"])
+def test_device_nan_fill_matches_oracle_bytes(dev, dt, sharded):
+    """A NaN fill equals nothing: every chunk and inner chunk is written, the boundary shard's
+    pure-padding inner chunks included (rows 12-15 of the second shard), byte for byte as the
+    oracle; an elided inner chunk would read back as 0, not NaN (Q1)."""
     meta = _meta(dt, np.nan, sharded)
     a = _array(dt, np.nan)
-    dev_chunks = device_write(dev, meta, a)
-    ora_chunks = encode_oracle(meta, a)
-    for dc, oc in zip(dev_chunks, ora_chunks):
-        assert oc is not None
-        if dc != oc:
-            assert sharded or dc is None  # an unsharded chunk: deleted instead of written
-    want = a.view(np.uint32)
-    for chunks in (dev_chunks, ora_chunks):
-        np.testing.assert_array_equal(
-            device_read(dev, meta, chunks, [0, 0], SHAPE).view(np.uint32), want)
+    got = device_write(dev, meta, a)
+    assert got == encode_oracle(meta, a)
+    assert all(c is not None for c in got)
+    np.testing.assert_array_equal(device_read(dev, meta, got, [0, 0], SHAPE).view(np.uint8),
+                                  a.view(np.uint8))

@@ -494,11 +494,16 @@ void fill_common_args(const zh_array_meta* m, const int64_t* region_shape, bool 
   a.fill = f;
   // the write path's all-fill test compares as Java's == (MultiArrayUtils.allValuesEqual,
   // M/utils/MultiArrayUtils.java:69-80, 104-150): for a float ±0 fill, +0.0 == -0.0
+  // (a NaN fill equals nothing: every chunk is kept, fill_never)
   a.fill_mask = ~0ull;
+  a.fill_never = 0;
   if (m->dtype_is_float && (m->dtype_size == 4 || m->dtype_size == 8)) {
+    const bool d8 = m->dtype_size == 8;
     const uint64_t sign = 1ull << (8 * m->dtype_size - 1);
-    const uint64_t elem = m->dtype_size == 8 ? ~0ull : 0xFFFFFFFFull;
-    if ((f & elem & ~sign) == 0) a.fill_mask = ~sign;
+    const uint64_t mag = f & (d8 ? ~0ull : 0xFFFFFFFFull) & ~sign;
+    const uint64_t inf = d8 ? 0x7FF0000000000000ull : 0x7F800000ull;
+    if (mag == 0) a.fill_mask = ~sign;
+    if (mag > inf) a.fill_never = 1;
   }
   if (encode) {
     a.fs = n - 1;
@@ -2358,8 +2363,9 @@ static int array_write_fast(zh_ctx* ctx, const zh_array_meta* m, ScatterArgs a,
           q /= nz.g1[d];
           c1v[d] = c1;
           const int64_t lo = c1 * c.inner_chunk_shape[d];
-          nk *= std::max<int64_t>(0, std::min<int64_t>(nz.r[d], (S.part_hi[d] - lo + inner[d] - 1) /
-                                                                     inner[d]));
+          nk *= a.fill_never ? nz.r[d]  // a NaN fill: every leaf kept (padding included)
+                             : std::max<int64_t>(0, std::min<int64_t>(
+                                   nz.r[d], (S.part_hi[d] - lo + inner[d] - 1) / inner[d]));
         }
         if (keep) {  // the cell's kept leaves, C order over its leaf grid
           nk = 0;
@@ -2405,7 +2411,8 @@ static int array_write_fast(zh_ctx* ctx, const zh_array_meta* m, ScatterArgs a,
       payload = kept * cn;
     } else {
       int64_t kept = 1;  // in-bounds inner chunks of the shard (all kept under this layout)
-      for (int d = 0; d < n; d++) kept *= (S.part_hi[d] + inner[d] - 1) / inner[d];
+      for (int d = 0; d < n; d++)
+        kept *= a.fill_never ? S.box_count[d] : (S.part_hi[d] + inner[d] - 1) / inner[d];
       payload = kept * cn;
     }
     if (keep && payload == 0) {  // all fill: writeChunk deletes the key (Array.java:150-151)
@@ -2529,7 +2536,8 @@ static int array_write_fast(zh_ctx* ctx, const zh_array_meta* m, ScatterArgs a,
   if (!jobs.empty())
     ZH_HIPF(hipMemcpyAsync(W + o_jobs, jobs.data(), jobs.size() * sizeof(CrcJob),
                            hipMemcpyHostToDevice, s));
-  ZH_HIPF(hipMemsetAsync(d_flags, 0, (size_t)items, s));
+  // a NaN fill equals nothing (Java's ==): every chunk holds a non-fill element
+  ZH_HIPF(hipMemsetAsync(d_flags, a.fill_never ? 1 : 0, (size_t)items, s));
   ZH_HIPF(hipMemsetAsync(d_slow, 0, sizeof(uint32_t), s));
   ZH_HIPF(hipMemsetAsync(d_cnt, 0, sizeof(uint32_t), s));
   if (c.nested) {
@@ -2781,6 +2789,7 @@ int zh_array_write(zh_ctx* ctx, const zh_array_meta* m, const void* src, const i
   std::vector<uint8_t> hflags((size_t)pitems);
   ZH_HIPC(hipMemcpyAsync(hflags.data(), d_flags, (size_t)pitems, hipMemcpyDeviceToHost, s));
   ZH_HIPC(hipStreamSynchronize(s));
+  if (a.fill_never) std::fill(hflags.begin(), hflags.end(), (uint8_t)1);  // a NaN fill
   // layout: C-order over the non-fill inner chunks (deterministic)
   const int64_t isz = c.sharded ? zh_shard_index_size(m) : 0;
   const int start = c.sharded && c.index_location == ZH_INDEX_START;

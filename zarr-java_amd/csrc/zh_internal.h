@@ -149,6 +149,9 @@ struct ScatterArgs {
   uint64_t fill;                // fill_value bytes (little-endian), replicated as needed
   uint64_t fill_mask;           // write path's all-fill test: element bits compared (a float
                                 // ±0 fill drops the sign bit; else all ones), low dsize bytes
+  int32_t fill_never;           // write path, a float NaN fill: no element equals it, so every
+                                // chunk and inner chunk is kept, boundary padding included
+  int32_t pad_fill;
   FastDiv inner_div[kMaxDims];  // divisors for unclipped extents
   // decode fast path for unclipped inner chunks
   ItemDesc* desc;               // per inner chunk (resolve kernel output)

@@ -367,7 +367,7 @@ __device__ __forceinline__ int64_t make_item(const ScatterArgs& a, int64_t item,
         const int32_t io = ic[d] * a.inner[d];
         const int32_t vhi = min(io + a.inner[d], S.part_hi[d]) - io;
         it.e[d] = a.inner[d];
-        it.v[d] = vhi;
+        it.v[d] = max(vhi, 0);
         empty |= vhi <= 0;
         s0 += (int64_t)(io - S.part_lo[d]) * a.rstride[d];
         it.ediv[d] = a.inner_div[d];
@@ -375,16 +375,17 @@ __device__ __forceinline__ int64_t make_item(const ScatterArgs& a, int64_t item,
     }
     it.s0 = s0;
     it.d0 = 0;
-    // an inner chunk entirely in the boundary padding is all fill: never encoded
-    if (empty) it.mode = kSkip;
+    // an inner chunk entirely in the boundary padding is all fill: never encoded, unless no
+    // element equals the fill (a NaN fill): then it is stored as padding like any other
+    if (empty && !a.fill_never) it.mode = kSkip;
   }
   return s;
 }
 
 // The write path's all-fill test (MultiArrayUtils.allValuesEqual, Java's ==): does an
 // element differ from fill_value?  Bits compared under a.fill_mask, which drops the sign bit
-// for a float ±0 fill (+0.0 == -0.0); every other fill compares every bit (a NaN fill: DESIGN
-// §3 Q19).
+// for a float ±0 fill (+0.0 == -0.0); every other fill compares every bit.  A NaN fill equals
+// nothing: a.fill_never, the flags then start at 1 and every chunk is kept (engine.cpp).
 __device__ __forceinline__ bool ne16(const uint4& v, const uint4& f, const uint4& m) {
   return (((v.x ^ f.x) & m.x) | ((v.y ^ f.y) & m.y) | ((v.z ^ f.z) & m.z) |
           ((v.w ^ f.w) & m.w)) != 0;
@@ -2359,8 +2360,9 @@ __device__ __forceinline__ void nest_coords(const ScatterArgs& a, const EncNest&
     const int32_t lc = (int32_t)(j - q * bc);
     j = q;
     const int32_t c1 = lc / nz.r[d], w = lc - c1 * nz.r[d];
-    const int32_t cnt = min(nz.r[d], (S.part_hi[d] - c1 * nz.r[d] * a.inner[d] + a.inner[d] - 1) /
-                                         a.inner[d]);
+    const int32_t cnt = a.fill_never ? nz.r[d]
+                                     : min(nz.r[d], (S.part_hi[d] - c1 * nz.r[d] * a.inner[d] +
+                                                     a.inner[d] - 1) / a.inner[d]);
     in &= w < cnt;
     cell += c1 * mc;
     mc *= nz.g1[d];
@@ -2398,7 +2400,7 @@ __global__ __launch_bounds__(kBlock) void encode_resolve_kernel(ScatterArgs a, E
         const uint32_t q = j / bc;
         const int64_t icd = (int64_t)(j - q * bc);
         j = q;
-        const int64_t cnt = (S.part_hi[d] + a.inner[d] - 1) / a.inner[d];
+        const int64_t cnt = a.fill_never ? (int64_t)bc : (S.part_hi[d] + a.inner[d] - 1) / a.inner[d];
         in &= icd < cnt;
         rank += icd * mul;
         mul *= cnt;
