@@ -1704,7 +1704,11 @@ __global__ __launch_bounds__(kBlock) void decode_tiles_kernel(ScatterArgs a) {
 // CRC tables: T[8][256], S[4][256], SD[4][256] (16 KiB; 50.5 KB per workgroup with the
 // tiles, 3 per CU).  Compact slicing-by-4 tables (4 per CU) and conflict-free field tables
 // measured slower or equal (round 3, profiles/r03/g, profiles/r03/l) and were removed.
-template <int NT, int G, bool CRC, bool PF, bool FLAGS>
+//
+// FLAGS (write path): 0 none, 1 the all-fill test by exact compares, 2 under a.fill_mask (a
+// float ±0 fill); the masked form costs the CRC encode 2 % (42.1 vs 43.0 ms, c4crc,
+// profiles/r05/wab/), so it gets kernels of its own.
+template <int NT, int G, bool CRC, bool PF, int FLAGS>
 __global__ __launch_bounds__(kBlock) void tiles_group_kernel(ScatterArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   // CRC: the tables first (T, S, SD: a constant LDS position for crc_upd16_k / crc_shift_k),
@@ -1793,7 +1797,9 @@ __global__ __launch_bounds__(kBlock) void tiles_group_kernel(ScatterArgs a) {
         if (!PF) load(ub);  // inside the live branch: 46.3 → 42.3 ms on the c4crc encode
 #pragma unroll
         for (int k = 0; k < 8; k++) {
-          if (FLAGS) differs |= ne4x4(x[k], f, fm);
+          if constexpr (FLAGS == 2) differs |= ne4x4(x[k], f, fm);
+          if constexpr (FLAGS == 1)
+            differs |= (x[k].x != f) | (x[k].y != f) | (x[k].z != f) | (x[k].w != f);
           uint32_t* row = mine + (wave * 8 + k) * 33 + g * 4;
           row[0] = xform1<4>(x[k].x, a.swap, 0);
           row[1] = xform1<4>(x[k].y, a.swap, 0);
@@ -3150,10 +3156,10 @@ static void launch_scatter_ds(const ScatterArgs& a, int tile, int enc, int grid,
       }
       if (v > 20 && !a.crc_fused) {  // G chunks per work item, next step's loads prefetched
         switch (v - 20) {
-          case 1: hipLaunchKernelGGL((tiles_group_kernel<3, 1, false, true, false>), dim3(grid), dim3(kBlock), lds, s, a); return;
-          case 2: hipLaunchKernelGGL((tiles_group_kernel<3, 2, false, true, false>), dim3(grid), dim3(kBlock), lds, s, a); return;
-          case 4: hipLaunchKernelGGL((tiles_group_kernel<3, 4, false, true, false>), dim3(grid), dim3(kBlock), lds, s, a); return;
-          case 8: hipLaunchKernelGGL((tiles_group_kernel<3, 8, false, true, false>), dim3(grid), dim3(kBlock), lds, s, a); return;
+          case 1: hipLaunchKernelGGL((tiles_group_kernel<3, 1, false, true, 0>), dim3(grid), dim3(kBlock), lds, s, a); return;
+          case 2: hipLaunchKernelGGL((tiles_group_kernel<3, 2, false, true, 0>), dim3(grid), dim3(kBlock), lds, s, a); return;
+          case 4: hipLaunchKernelGGL((tiles_group_kernel<3, 4, false, true, 0>), dim3(grid), dim3(kBlock), lds, s, a); return;
+          case 8: hipLaunchKernelGGL((tiles_group_kernel<3, 8, false, true, 0>), dim3(grid), dim3(kBlock), lds, s, a); return;
           default: return;
         }
       }
@@ -3293,18 +3299,22 @@ static bool launch_encode_fast_ds(const ScatterArgs& v, int grid, int group, hip
     const size_t l = lds + (size_t)kTG * kTilePitch * 4;
     if (group > 0 && v.crc_fused) {  // host: crc_tile_step for 8/G units
       const size_t lc = l + 16 * 256 * 4 + (size_t)v.fast_n * 4 + 64;  // + alignment
-      switch (group) {
-        case 1: hipLaunchKernelGGL((tiles_group_kernel<3, 1, true, false, true>), dim3(grid), dim3(kBlock), lc, s, v); return true;
-        case 2: hipLaunchKernelGGL((tiles_group_kernel<3, 2, true, false, true>), dim3(grid), dim3(kBlock), lc, s, v); return true;
-        case 4: hipLaunchKernelGGL((tiles_group_kernel<3, 4, true, false, true>), dim3(grid), dim3(kBlock), lc, s, v); return true;
+      const bool m = v.fill_mask != ~0ull;  // a float ±0 fill: the masked all-fill test
+      switch (group * 2 + (m ? 1 : 0)) {
+        case 2: hipLaunchKernelGGL((tiles_group_kernel<3, 1, true, false, 1>), dim3(grid), dim3(kBlock), lc, s, v); return true;
+        case 3: hipLaunchKernelGGL((tiles_group_kernel<3, 1, true, false, 2>), dim3(grid), dim3(kBlock), lc, s, v); return true;
+        case 4: hipLaunchKernelGGL((tiles_group_kernel<3, 2, true, false, 1>), dim3(grid), dim3(kBlock), lc, s, v); return true;
+        case 5: hipLaunchKernelGGL((tiles_group_kernel<3, 2, true, false, 2>), dim3(grid), dim3(kBlock), lc, s, v); return true;
+        case 8: hipLaunchKernelGGL((tiles_group_kernel<3, 4, true, false, 1>), dim3(grid), dim3(kBlock), lc, s, v); return true;
+        case 9: hipLaunchKernelGGL((tiles_group_kernel<3, 4, true, false, 2>), dim3(grid), dim3(kBlock), lc, s, v); return true;
         default: return false;
       }
     }
     if (group > 0) {  // host: piece_shift == 0, item_mul
       switch (group) {
-        case 1: hipLaunchKernelGGL((tiles_group_kernel<3, 1, false, false, true>), dim3(grid), dim3(kBlock), l, s, v); return true;
-        case 2: hipLaunchKernelGGL((tiles_group_kernel<3, 2, false, false, true>), dim3(grid), dim3(kBlock), l, s, v); return true;
-        case 4: hipLaunchKernelGGL((tiles_group_kernel<3, 4, false, false, true>), dim3(grid), dim3(kBlock), l, s, v); return true;
+        case 1: hipLaunchKernelGGL((tiles_group_kernel<3, 1, false, false, 2>), dim3(grid), dim3(kBlock), l, s, v); return true;
+        case 2: hipLaunchKernelGGL((tiles_group_kernel<3, 2, false, false, 2>), dim3(grid), dim3(kBlock), l, s, v); return true;
+        case 4: hipLaunchKernelGGL((tiles_group_kernel<3, 4, false, false, 2>), dim3(grid), dim3(kBlock), l, s, v); return true;
         default: return false;
       }
     }
