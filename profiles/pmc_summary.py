@@ -21,6 +21,12 @@ def flags_arg(n):
     return args[4] if "tiles_group_kernel" in n and len(args) > 5 else args[-1]
 
 
+def is_encode_flags(a):
+    """FLAGS of an encode-view kernel: `true`, or (round 5, tiles_group_kernel's int FLAGS)
+    1 (exact all-fill compares) / 2 (masked)."""
+    return a in ("true", "1", "2")
+
+
 def kernel_rows(path, match):
     rows = []
     for r in csv.DictReader(open(path)):
@@ -38,7 +44,7 @@ DECODE_ONLY = ("tiles_rowcrc_kernel", "tiles_crcw_kernel", "tiles_rowcrc_aln_ker
 def main(src, config, out):
     def encode_view(n):  # the bench's setup encode runs the fast kernels with FLAGS = true
         return any(k in n for k in FAST) and not any(k in n for k in DECODE_ONLY) and \
-            flags_arg(n) == "true"
+            is_encode_flags(flags_arg(n))
 
     def decode(n):  # every decode kernel of one step: fast rows/tiles + the generic list
         return any(k in n for k in FAST + ("decode_slow_kernel",)) and not encode_view(n)

@@ -13,14 +13,14 @@ import os
 import sys
 
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
-from pmc_summary import FAST, DECODE_ONLY, flags_arg, kernel_rows  # noqa: E402
+from pmc_summary import FAST, DECODE_ONLY, flags_arg, is_encode_flags, kernel_rows  # noqa: E402
 
 
 def encode_view(n):
     if "tiles_rowcrc_enc_aln_kernel" in n:
         return True
     return any(k in n for k in FAST) and not any(k in n for k in DECODE_ONLY) and \
-        flags_arg(n) == "true"
+        is_encode_flags(flags_arg(n))
 
 
 def main(src, config, out, alg):
