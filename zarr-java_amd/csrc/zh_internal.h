@@ -248,6 +248,8 @@ struct CrcJob {
   int32_t pad;
 };
 
+int env_int(const char* name, int def);  // zh_engine.cpp: an integer switch from the environment
+
 // Kernel launchers (zh_kernels.hip).
 // index crc32c of every job in one launch, spans of kIdxSpan << span_shift bytes (job
 // span_begin set by assign_crc_spans); partials holds nspans span registers followed by njobs

@@ -1419,7 +1419,7 @@ __global__ __launch_bounds__(kBlock) void rows_group_kernel(ScatterArgs a) {
 // 9.71 ms, and was removed in round 4.)
 constexpr int kXRow = 72;  // 16-B vectors per exchange row (64 + 8)
 
-template <int DS>
+template <int DS, bool PF>
 __global__ __launch_bounds__(kBlock) void rows_xpose_kernel(ScatterArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   uint2* tab = reinterpret_cast<uint2*>(smem);
@@ -1450,23 +1450,25 @@ __global__ __launch_bounds__(kBlock) void rows_xpose_kernel(ScatterArgs a) {
     }
     if (__syncthreads_or(on) == 0) continue;  // block-uniform: no fast chunk in the group
     const uint64_t onm = __ballot(on), fillm = __ballot(on && fill);
+    uint4 v[8];
+    auto load = [&](uint32_t rb) {  // layout B loads: row rb + hi of chunk k
+      uint64_t so, dof;
+      row_offsets(a, tab, rb + hi, so, dof);
+#pragma unroll
+      for (int k = 0; k < 8; k++) {
+        const uint64_t s = ((uint64_t)__builtin_amdgcn_readlane((int)(sb >> 32), k * 8) << 32) |
+                           (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)sb, k * 8);
+        v[k] = make_uint4(0, 0, 0, 0);
+        if (((onm & ~fillm) >> (k * 8)) & 1 && rb + hi < nrows)
+          v[k] = ld16s<true>((const uint8_t*)s + so * DS + col * 16);
+      }
+    };
+    if (PF) load(wave * 8);
 #pragma unroll 1
     for (uint32_t rb = wave * 8; rb < nrows; rb += 32) {
-      uint4 v[8];
-      {  // layout B loads: row rb + hi of chunk k
-        uint64_t so, dof;
-        row_offsets(a, tab, rb + hi, so, dof);
+      if (!PF) load(rb);
 #pragma unroll
-        for (int k = 0; k < 8; k++) {
-          const uint64_t s = ((uint64_t)__builtin_amdgcn_readlane((int)(sb >> 32), k * 8) << 32) |
-                             (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)sb, k * 8);
-          v[k] = make_uint4(0, 0, 0, 0);
-          if (((onm & ~fillm) >> (k * 8)) & 1 && rb + hi < nrows)
-            v[k] = ld16s<true>((const uint8_t*)s + so * DS + col * 16);
-        }
-#pragma unroll
-        for (int k = 0; k < 8; k++) xw[hi * kXRow + k * 8 + col] = v[k];
-      }
+      for (int k = 0; k < 8; k++) xw[hi * kXRow + k * 8 + col] = v[k];
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -1476,6 +1478,7 @@ __global__ __launch_bounds__(kBlock) void rows_xpose_kernel(ScatterArgs a) {
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      if (PF && rb + 32 < nrows) load(rb + 32);  // the next step's loads before these stores
 #pragma unroll
       for (int r = 0; r < 8; r++) {  // layout A stores into chunk hi's region rows
         uint64_t so, dof;
@@ -3173,8 +3176,12 @@ static void launch_scatter_ds(const ScatterArgs& a, int tile, int enc, int grid,
       }
     }
   } else if (a.fast_mode != kFastNone && a.row_group == 8) {  // host: 128-B rows, no CRC
-    hipLaunchKernelGGL((rows_xpose_kernel<DS>), dim3(grid), dim3(kBlock), lds + 4 * 8 * kXRow * 16,
-                       s, a);
+    if (env_int("ZH_XPOSE_PF", 1) != 0)  // the next step's loads before this step's stores
+      hipLaunchKernelGGL((rows_xpose_kernel<DS, true>), dim3(grid), dim3(kBlock),
+                         lds + 4 * 8 * kXRow * 16, s, a);
+    else
+      hipLaunchKernelGGL((rows_xpose_kernel<DS, false>), dim3(grid), dim3(kBlock),
+                         lds + 4 * 8 * kXRow * 16, s, a);
   } else if (a.fast_mode != kFastNone && a.row_group > 0) {  // host: piece_shift 0
     // with the chunk CRC the payload loads go through the cache (NT = 2): a payload after a
     // 4-byte crc32c sits at 4 mod 16 and the line two wave loads share then hits in L2
