@@ -1,0 +1,128 @@
+"""Seeded random codec chains through the write path: the device encode against the oracle's
+bytes (ShardingIndexedCodec.encode :105-168, BytesCodec.encode, Crc32cCodec.encode :50-60,
+TransposeCodec.encode, Array.writeChunk's all-fill elision :148-151), then the stored chunks
+read back (device and oracle) against the array.
+
+Each case draws: rank 1-4, array / chunk / inner / leaf shapes (boundary chunks included),
+dtype 1/2/4/8 bytes (float32/float64 with a 0, -0, NaN or ordinary fill among them), transpose
+order, bytes and index endianness, index at start or end, index crc32c, chunk crc32c, nested
+sharding; the data holds blocks of fill so that chunks, inner chunks and leaves are elided.
+The CPU test holds the oracle to its own round trip; the GPU test compares the device's bytes
+with it."""
+import numpy as np
+import pytest
+
+import oracle as O
+from helpers import NP_DT, device_read, device_write, encode_oracle
+from zarrhip import _abi as A
+
+FLOATS = {4: "<f4", 8: "<f8"}
+
+
+def _divisors(n):
+    return [d for d in range(1, n + 1) if n % d == 0]
+
+
+def random_case(seed):
+    """(meta, array, numpy dtype) of one random case."""
+    rng = np.random.default_rng(seed)
+    n = int(rng.integers(1, 5))
+    sharded = rng.random() < 0.75
+    nested = sharded and rng.random() < 0.3
+    chunk, inner, leaf, shape = [], [], [], []
+    for _ in range(n):
+        c = int(rng.choice([2, 4, 6, 8, 12, 16]))
+        i = int(rng.choice(_divisors(c))) if sharded else c
+        lf = int(rng.choice(_divisors(i))) if nested else i
+        chunk.append(c)
+        inner.append(i)
+        leaf.append(lf)
+        shape.append(int(rng.integers(1, 2 * c + 3)))
+    # keep the element count small (the oracle is a C loop, the cases many)
+    while int(np.prod(shape)) > 6000:
+        d = int(np.argmax(shape))
+        shape[d] = max(1, shape[d] // 2)
+    ds = int(rng.choice([1, 2, 4, 8]))
+    is_float = ds in FLOATS and rng.random() < 0.5
+    dt = np.dtype(FLOATS[ds]) if is_float else NP_DT[ds]
+    if is_float:
+        fill = float(rng.choice([0.0, -0.0, np.nan, 1.5]))
+    else:
+        fill = int(rng.integers(0, 4))
+    fill_bytes = np.array([fill], dt).tobytes()
+    order = [int(x) for x in rng.permutation(n)] if rng.random() < 0.5 else None
+    kw = dict(fill=fill_bytes, is_float=is_float, is_bool=False,
+              transpose_order=order,
+              endian=A.ZH_ENDIAN_BIG if rng.random() < 0.5 else A.ZH_ENDIAN_LITTLE,
+              inner_crc32c=bool(rng.random() < 0.3))
+    if sharded:
+        kw.update(sharded=True, inner_chunk_shape=inner,
+                  index_endian=A.ZH_ENDIAN_BIG if rng.random() < 0.3 else A.ZH_ENDIAN_LITTLE,
+                  index_crc32c=bool(rng.random() < 0.6),
+                  index_location=A.ZH_INDEX_START if rng.random() < 0.4 else A.ZH_INDEX_END)
+        if nested:
+            kw.update(nested_chunk_shape=leaf,
+                      nested_index_crc32c=bool(rng.random() < 0.6),
+                      nested_index_location=(A.ZH_INDEX_START if rng.random() < 0.4
+                                             else A.ZH_INDEX_END))
+    meta = A.make_meta(shape, chunk, ds, **kw)
+    if is_float:
+        a = rng.standard_normal(shape).astype(dt)
+        a[rng.random(shape) < 0.1] = -0.0
+    else:
+        a = rng.integers(0, 2 ** (8 * ds) - 1, size=shape, dtype=np.uint64).astype(dt)
+    # blocks of fill (whole chunks, inner chunks or leaves where they line up)
+    blk = leaf if nested else inner
+    for _ in range(int(rng.integers(0, 4))):
+        lo = [int(rng.integers(0, max(1, s))) // b * b for s, b in zip(shape, blk)]
+        sl = tuple(slice(lo_, lo_ + b * int(rng.integers(1, 3))) for lo_, b in zip(lo, blk))
+        a[sl] = fill
+    return meta, a, dt
+
+
+CASES = list(range(40))
+
+
+def _bits(a):
+    return np.ascontiguousarray(a).view(np.uint8)
+
+
+def _decode(meta, chunks, dt, shape):
+    return np.frombuffer(O.array_read(meta, chunks, [0] * len(shape), shape), dt).reshape(shape)
+
+
+@pytest.mark.parametrize("seed", CASES)
+def test_oracle_write_read_round_trip(seed):
+    """The oracle's write then read: every element equal to the array, except the values the
+    reference's elision rewrites (an elided inner chunk reads 0 — Q1 — and an elided chunk the
+    fill value; under Java's == a -0.0 chunk with a 0.0 fill reads +0.0)."""
+    meta, a, dt = random_case(seed)
+    shape = list(a.shape)
+    chunks = encode_oracle(meta, a)
+    got = _decode(meta, chunks, dt, shape)
+    fill = np.frombuffer(bytes(meta.fill_value)[:meta.dtype_size], dt)[0]
+    same = _bits(got).reshape(shape + [-1]).tolist() == _bits(a).reshape(shape + [-1]).tolist()
+    if not same:  # only elided blocks may differ: they read 0 or the fill, and held fill
+        g, x = got.reshape(-1), a.reshape(-1)
+        diff = g.view(np.uint8).reshape(len(g), -1) != x.view(np.uint8).reshape(len(x), -1)
+        bad = np.nonzero(diff.any(axis=1))[0]
+        for i in bad:
+            if np.dtype(dt).kind == "f":
+                assert x[i] == fill or (np.isnan(fill) and np.isnan(x[i])), (seed, i)
+                assert g[i] == 0 or g[i] == fill, (seed, i)
+            else:
+                assert x[i] == fill and g[i] == 0, (seed, i)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", CASES)
+def test_device_write_matches_oracle_bytes(dev, seed):
+    meta, a, dt = random_case(seed)
+    shape = list(a.shape)
+    got = device_write(dev, meta, a)
+    want = encode_oracle(meta, a)
+    assert len(got) == len(want)
+    for k, (g, w) in enumerate(zip(got, want)):
+        assert g == w, (seed, k, None if g is None else len(g), None if w is None else len(w))
+    np.testing.assert_array_equal(_bits(device_read(dev, meta, got, [0] * len(shape), shape)),
+                                  _bits(_decode(meta, want, dt, shape)))
