@@ -9,6 +9,8 @@ order, bytes and index endianness, index at start or end, index crc32c, chunk cr
 sharding; the data holds blocks of fill so that chunks, inner chunks and leaves are elided.
 The CPU test holds the oracle to its own round trip; the GPU test compares the device's bytes
 with it."""
+import os
+
 import numpy as np
 import pytest
 
@@ -80,7 +82,8 @@ def random_case(seed):
     return meta, a, dt
 
 
-CASES = list(range(40))
+# ZH_FUZZ_WCASES widens the search (default 40 cases; the round-5 search ran 1000 on the GPU)
+CASES = list(range(int(os.environ.get("ZH_FUZZ_WCASES", "40"))))
 
 
 def _bits(a):
