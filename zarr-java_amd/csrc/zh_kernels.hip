@@ -456,7 +456,11 @@ __device__ __forceinline__ bool row_pass(const ScatterArgs& a, const Item& it, i
       bool valid = true;
 #pragma unroll
       for (int d = kMaxDims - 1; d >= 0; --d) {
-        if (d >= n || d == F || ext[d] <= 1) continue;
+        if (d >= n || d == F) continue;
+        if (ext[d] <= 1) {  // one element along d: loadable unless the item lies beyond the
+          valid &= it.v[d] > 0;  // array there (a padding-only item, kept for a NaN fill)
+          continue;
+        }
         const uint32_t q = fdiv(r, ediv[d]);
         const uint32_t m = r - q * (uint32_t)ext[d];
         so += (int64_t)m * sstr[d];
@@ -611,7 +615,11 @@ __device__ __forceinline__ void tile_pass(const ScatterArgs& a, const Item& it,
       bool bv = true;
 #pragma unroll
       for (int d = kMaxDims - 1; d >= 0; --d) {
-        if (d >= n || d == fs || d == fd || it.e[d] <= 1) continue;
+        if (d >= n || d == fs || d == fd) continue;
+        if (it.e[d] <= 1) {  // see row_pass: a padding-only item loads nothing
+          bv &= it.v[d] > 0;
+          continue;
+        }
         const uint32_t q = fdiv(b, it.ediv[d]);
         const uint32_t m = b - q * (uint32_t)it.e[d];
         so += (int64_t)m * sstr[d];
@@ -2314,7 +2322,7 @@ __device__ __forceinline__ bool flag_item(const ScatterArgs& a, const Item& it) 
     ext[d] = it.v[d];
     ediv[d] = it.ediv[d];
     if (d >= n) continue;
-    if (ext[d] != a.inner[d]) ediv[d] = make_fastdiv((uint32_t)ext[d]);
+    if (ext[d] != a.inner[d] && ext[d] > 0) ediv[d] = make_fastdiv((uint32_t)ext[d]);
     if (d != F) {
       nrows *= (uint32_t)ext[d];
       if (ext[d] > 1 && ((sstr[d] * DS) & 15)) vec = false;
