@@ -129,3 +129,33 @@ def test_device_write_matches_oracle_bytes(dev, seed):
         assert g == w, (seed, k, None if g is None else len(g), None if w is None else len(w))
     np.testing.assert_array_equal(_bits(device_read(dev, meta, got, [0] * len(shape), shape)),
                                   _bits(_decode(meta, want, dt, shape)))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", CASES)
+def test_device_read_random_regions_match_oracle(dev, tmp_path, seed):
+    """The same random chains read back: three random regions per case (any offset and
+    extent inside the array), from memory and from the chunk files through the library's own
+    store reads, against the oracle's read of the same stored chunks."""
+    from helpers import chunk_coords
+    from test_gpu_files import files_read, store_read
+    from test_gpu_pieces import region_paths, write_store
+    meta, a, dt = random_case(seed)
+    shape = list(a.shape)
+    chunks = encode_oracle(meta, a)
+    rng = np.random.default_rng(10_000 + seed)
+    allc = chunk_coords(meta, [0] * len(shape), shape)
+    pos = {c: i for i, c in enumerate(allc)}
+    paths = write_store(tmp_path, meta, chunks) if seed % 2 == 0 else None
+    for _ in range(3):
+        off = [int(rng.integers(0, s)) for s in shape]
+        shp = [int(rng.integers(1, s - o + 1)) for s, o in zip(shape, off)]
+        src = [chunks[pos[c]] for c in chunk_coords(meta, off, shp)]
+        want = np.frombuffer(O.array_read(meta, src, off, shp), dt).reshape(shp)
+        got = device_read(dev, meta, src, off, shp)
+        np.testing.assert_array_equal(_bits(got), _bits(want), err_msg=f"{seed} {off} {shp}")
+        if paths is not None:
+            rp = region_paths(meta, paths, off, shp)
+            np.testing.assert_array_equal(_bits(files_read(dev, meta, rp, off, shp).view(dt)),
+                                          _bits(store_read(meta, rp, off, shp).view(dt)),
+                                          err_msg=f"files {seed} {off} {shp}")
