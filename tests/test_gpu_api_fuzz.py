@@ -1,11 +1,12 @@
 """Seeded random arrays through the Python mirror's Array API (Array.create / write / read,
 M/v3/Array.java, M/core/Array.java:83-156, 378-441): random data types, shapes, chunk
 grids and codec chains — transpose, bytes endianness, sharding with the index at either end,
-and the host byte-to-byte stages (gzip, zstd, blosc, crc32c: SURVEY §8(f) rank 3) inside or
-outside the shard — written to a FilesystemStore and read back, whole and in random regions,
+and the host byte-to-byte stages (gzip, zstd, blosc, crc32c: SURVEY §8(f) rank 3) on whole
+chunks or on a shard's inner chunks — written to a FilesystemStore and read back, whole and in random regions,
 through the library's own file reads (ZH_FILES=1, the default) and through the mirror's
 store reads (ZH_FILES=0).  No oracle runs the compressors, so the check is the round trip:
-the read equals the written array (fill 0, so an elided inner chunk reads the same, Q1)."""
+the read equals the written array (fill 0, so an elided inner chunk reads the same, Q1).
+ZH_FUZZ_APICASES widens the search (default 24; the round-5 search ran 300 on the GPU)."""
 import os
 
 import numpy as np
