@@ -147,9 +147,14 @@ def _region(rng, shape):
     return off, [int(rng.integers(1, s - o + 1)) for s, o in zip(shape, off)]
 
 
+@pytest.mark.parametrize("pipelined", [False, True])
 @pytest.mark.parametrize("form", ["memory", "files", "pieces"])
 @pytest.mark.parametrize("chain", list(FUZZ_CHAINS))
-def test_corrupt_index_entries_match_oracle(dev, tmp_path, chain, form):
+def test_corrupt_index_entries_match_oracle(dev, tmp_path, monkeypatch, chain, form, pipelined):
+    if pipelined:  # the reads in slabs through the page-locked rings (test_gpu_files' mode)
+        for k, v in (("ZH_PIPE_MIN_KB", "1"), ("ZH_PIPE_SLAB_KB", "4"),
+                     ("ZH_PIPE_CHUNK_KB", "64"), ("ZH_PIPE_THREADS", "3")):
+            monkeypatch.setenv(k, v)
     meta, arr = make_case(chain, seed=211)
     shards = encode_oracle(meta, arr)
     shape = [meta.shape[d] for d in range(meta.ndim)]
