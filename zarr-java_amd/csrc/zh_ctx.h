@@ -183,6 +183,10 @@ struct zh_plan {
   int grid = 0;
   int slow_grid = 0;
   hipStream_t last_stream = nullptr;
+  // zh_plan_wait's device-detected data error: its shard (index into coords) and the key
+  // that orders it within the shard (~0: the shard index crc32c; else the kStBadChunk key)
+  int64_t err_shard = -1;
+  uint64_t err_key = 0;
   // hipGraph replay of execute (zh_plan_set_graph)
   bool use_graph = false;
   hipGraphExec_t graph_exec = nullptr;

@@ -1636,6 +1636,7 @@ int zh_plan_set_graph(zh_plan* p, int enable) {
 int zh_plan_wait(zh_plan* p, char* err, size_t errlen) {
   if (!p) return ZH_EINVAL;
   (void)hipSetDevice(p->ctx->device);
+  p->err_shard = -1;
   std::vector<uint64_t> stv((size_t)p->nshards * kStWords);
   if (p->status_slot < 0 && p->last_stream && !stv.empty())
     p->status_slot = status_slot_take(p->ctx, p->nshards);
@@ -1656,6 +1657,8 @@ int zh_plan_wait(zh_plan* p, char* err, size_t errlen) {
   for (int64_t i = 0; i < p->nshards; i++) {
     const uint64_t* w = &stv[i * kStWords];
     if (!w[kStFlags]) continue;
+    p->err_shard = i;  // where the error sits in the oracle's order (the pipelined read's pick)
+    p->err_key = (w[kStFlags] & kFlagCrc) ? ~0ull : w[kStBadChunk];
     if (w[kStFlags] & kFlagCrc) {  // Crc32cCodec.java:39-44 (signed ints)
       set_err(err, errlen, "The checksum of the sharding index is invalid. Stored: %d Computed: %d",
               (int32_t)(uint32_t)w[kStCrcStored], (int32_t)(uint32_t)w[kStCrcComputed]);

@@ -19,9 +19,12 @@
 // so both PCIe directions, the host copies and the kernels overlap.  Each slab is planned
 // over only the chunks it touches, and a sub-shard part stages only the ranges it references
 // (zh_engine.cpp caller_pieces / compact_pieces).  At most ZH_PIPE_PLANS (4) slab plans are
-// alive, so their device staging cycles through the context's block cache.  Errors: the first
-// failing slab in C order (a planning failure at slab r runs slabs < r and reports a device
-// error among them first, as the one-plan read would; a device error stops the read).
+// alive, so their device staging cycles through the context's block cache.  Errors: a data
+// error the device finds (a checksum, an index entry) does not stop the read; of all of them
+// the one reported is the first in the oracle's order — the chunk first in C order, then the
+// error the one-plan read would report in it — since slabs can cut a shard
+// into parts.  A planning failure at slab r runs slabs < r and reports a data error among
+// them first, as the one-plan read would; HIP and store-read failures stop the read.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -412,6 +415,11 @@ int read_pipelined(zh_ctx* ctx, const zh_array_meta* meta, const SrcDesc* srcs, 
   // status of the slabs, in C order: planning failure (from slab plan_fail on), device errors
   int plan_st = ZH_OK, dev_st = ZH_OK;
   std::string plan_msg, dev_msg;
+  // the data error first in the oracle's order: its chunk coords, its key in the shard
+  bool data_err = false;
+  std::vector<int64_t> data_cc;
+  uint64_t data_key = 0;
+  std::string data_msg;
   int64_t nplan = nslab;  // slabs that got a plan
   const bool go = st == ZH_OK && he == hipSuccess;
   if (go) {
@@ -569,7 +577,17 @@ int read_pipelined(zh_ctx* ctx, const zh_array_meta* meta, const SrcDesc* srcs, 
       p->last_stream = nullptr;
       if (dev_st == ZH_OK && lane_err.load() == ZH_OK) {
         const int rc = zh_plan_wait(p, e, sizeof e);
-        if (rc != ZH_OK) {
+        if (rc == ZH_EDATA && p->err_shard >= 0) {
+          const int n = p->meta.ndim;
+          std::vector<int64_t> cc(p->coords.begin() + p->err_shard * n,
+                                  p->coords.begin() + (p->err_shard + 1) * n);
+          if (!data_err || cc < data_cc || (cc == data_cc && p->err_key > data_key)) {
+            data_cc = cc;
+            data_key = p->err_key;
+            data_msg = e;
+          }
+          data_err = true;
+        } else if (rc != ZH_OK) {
           dev_st = rc;
           dev_msg = e;
         }
@@ -646,6 +664,10 @@ int read_pipelined(zh_ctx* ctx, const zh_array_meta* meta, const SrcDesc* srcs, 
   if (st == ZH_OK && dev_st != ZH_OK) {
     set_err(err, errlen, "%s", dev_msg.c_str());
     st = dev_st;
+  }
+  if (st == ZH_OK && data_err) {
+    set_err(err, errlen, "%s", data_msg.c_str());
+    st = ZH_EDATA;
   }
   if (st == ZH_OK && plan_st != ZH_OK) {
     set_err(err, errlen, "%s", plan_msg.c_str());
