@@ -6,6 +6,7 @@ entry reaches the code that interprets it: the device's resolve kernel (memory s
 ShardingIndexedCodec.java:215-231, 323-330) and the library's host planner over files
 (sub-shard reads: StoreHandleDataProvider.read → FilesystemStore.get, zero-padded past the end
 of the file, ShardingIndexedCodec.java:340-356; whole-shard reads slice the file's bytes).
+A fourth form reads the region in slabs over three contexts (zh_array_read_multi).
 The third form is the Java drop-in's: HipArray.read's store reads (the stored index, then
 zh_shard_ranges' ranges, zero-padded past the end of the file) handed to zh_array_read_pieces.
 ZH_FUZZ_TRIALS / ZH_FUZZ_SEED widen the search (default 48 trials, seed 0).
@@ -26,7 +27,7 @@ import pytest
 import oracle as O
 from helpers import (NP_DT, chunk_coords, device_read, encode_oracle, jni_fetch, jni_read,
                      rand_array)
-from test_gpu_files import files_read, store_read
+from test_gpu_files import files_read, store_read, three_ctxs  # noqa: F401 (fixture)
 from test_gpu_pieces import CHAINS, region_paths, write_store
 from zarrhip import _abi as A
 from zarrhip._lib import ZhError
@@ -120,6 +121,17 @@ def make_case(chain, seed):
     return meta, arr
 
 
+def _multi_read(ctxs, meta, src, off, shp):
+    import ctypes as C
+    from zarrhip import _lib
+    keep = [None if b is None else (C.c_char * max(1, len(b))).from_buffer_copy(b or b"\0")
+            for b in src]
+    sources = [(None, 0) if k is None else (C.addressof(k), len(b)) for k, b in zip(keep, src)]
+    out = np.zeros(shp, NP_DT[meta.dtype_size])
+    _lib.array_read_multi(ctxs, meta, sources, off, shp, out.ctypes.data, 0)
+    return out
+
+
 def _outcome(fn):
     try:
         return "ok", fn()
@@ -148,9 +160,10 @@ def _region(rng, shape):
 
 
 @pytest.mark.parametrize("pipelined", [False, True])
-@pytest.mark.parametrize("form", ["memory", "files", "pieces"])
+@pytest.mark.parametrize("form", ["memory", "files", "pieces", "multi"])
 @pytest.mark.parametrize("chain", list(FUZZ_CHAINS))
-def test_corrupt_index_entries_match_oracle(dev, tmp_path, monkeypatch, chain, form, pipelined):
+def test_corrupt_index_entries_match_oracle(dev, three_ctxs, tmp_path, monkeypatch, chain, form,
+                                            pipelined):
     if pipelined:  # the reads in slabs through the page-locked rings (test_gpu_files' mode)
         for k, v in (("ZH_PIPE_MIN_KB", "1"), ("ZH_PIPE_SLAB_KB", "4"),
                      ("ZH_PIPE_CHUNK_KB", "64"), ("ZH_PIPE_THREADS", "3")):
@@ -173,11 +186,14 @@ def test_corrupt_index_entries_match_oracle(dev, tmp_path, monkeypatch, chain, f
         off, shp = _region(rng, shape)
         sel = chunk_coords(meta, off, shp)
         ctx = (chain, form, t, muts, off, shp)
-        if form == "memory":
+        if form in ("memory", "multi"):
             src = [bad[pos[c]] for c in sel]
             want = _outcome(lambda: np.frombuffer(O.array_read(meta, src, off, shp),
                                                   NP_DT[meta.dtype_size]).reshape(shp))
-            got = _outcome(lambda: device_read(dev, meta, src, off, shp))
+            if form == "memory":
+                got = _outcome(lambda: device_read(dev, meta, src, off, shp))
+            else:  # zh_array_read_multi: the region in slabs over three contexts
+                got = _outcome(lambda: _multi_read(three_ctxs, meta, src, off, shp))
         else:
             paths = write_store(tmp_path, meta, bad, tag=f"t{t}")
             rp = region_paths(meta, paths, off, shp)

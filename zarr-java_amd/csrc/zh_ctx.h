@@ -228,6 +228,22 @@ int shard_ranges(const zh_array_meta* m, const uint8_t* index, int64_t shard_nby
 
 // Region read over generic sources: the pipelined path for large host reads (zh_pipeline.cpp),
 // else one plan.  Caller holds ctx->mu.
+// Where the last data error reported on this thread sits in the oracle's order (DESIGN §3
+// Q17): the failing chunk's coords and its key in the shard (zh_plan::err_key).  Set by
+// zh_plan_wait and by the pipelined read's pick, cleared by read_region; the multi-device
+// read orders its slabs' data errors by it.
+struct DataErrPos {
+  bool set = false;
+  std::vector<int64_t> cc;
+  uint64_t key = 0;
+};
+extern thread_local DataErrPos g_data_err;
+// is (a, ka) before (b, kb) in that order?
+inline bool data_err_before(const std::vector<int64_t>& a, uint64_t ka,
+                            const std::vector<int64_t>& b, uint64_t kb) {
+  return a < b || (a == b && ka > kb);
+}
+
 int read_region(zh_ctx* ctx, const zh_array_meta* meta, const SrcDesc* srcs, int64_t nsrc,
                 const int64_t* offset, const int64_t* shape, void* out, uint32_t flags,
                 void* stream, char* err, size_t errlen);

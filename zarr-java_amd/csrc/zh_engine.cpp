@@ -1637,6 +1637,7 @@ int zh_plan_wait(zh_plan* p, char* err, size_t errlen) {
   if (!p) return ZH_EINVAL;
   (void)hipSetDevice(p->ctx->device);
   p->err_shard = -1;
+  g_data_err.set = false;
   std::vector<uint64_t> stv((size_t)p->nshards * kStWords);
   if (p->status_slot < 0 && p->last_stream && !stv.empty())
     p->status_slot = status_slot_take(p->ctx, p->nshards);
@@ -1659,6 +1660,9 @@ int zh_plan_wait(zh_plan* p, char* err, size_t errlen) {
     if (!w[kStFlags]) continue;
     p->err_shard = i;  // where the error sits in the oracle's order (the pipelined read's pick)
     p->err_key = (w[kStFlags] & kFlagCrc) ? ~0ull : w[kStBadChunk];
+    g_data_err.set = true;
+    g_data_err.cc.assign(p->coords.begin() + i * n, p->coords.begin() + (i + 1) * n);
+    g_data_err.key = p->err_key;
     if (w[kStFlags] & kFlagCrc) {  // Crc32cCodec.java:39-44 (signed ints)
       set_err(err, errlen, "The checksum of the sharding index is invalid. Stored: %d Computed: %d",
               (int32_t)(uint32_t)w[kStCrcStored], (int32_t)(uint32_t)w[kStCrcComputed]);
@@ -1804,9 +1808,12 @@ int read_one_plan(zh_ctx* ctx, const zh_array_meta* meta, const SrcDesc* srcs, i
 // A region read: large reads with a host side (host sources or a host output) go through the
 // pipelined path (H2D | decode | D2H per slab, zh_pipeline.cpp); everything else, and regions
 // that do not split, as one plan.
+thread_local DataErrPos g_data_err;
+
 int read_region(zh_ctx* ctx, const zh_array_meta* meta, const SrcDesc* srcs, int64_t nsrc,
                 const int64_t* offset, const int64_t* shape, void* out, uint32_t flags,
                 void* stream, char* err, size_t errlen) {
+  g_data_err.set = false;
   if (meta && offset && shape && out && env_int("ZH_PIPE", 1) != 0) {
     const int st = read_pipelined(ctx, meta, srcs, nsrc, offset, shape, out, flags, stream, err,
                                   errlen);
@@ -2024,6 +2031,7 @@ int read_multi_impl(zh_ctx* const* ctxs, int ndev, int root, const zh_array_meta
   }
   std::vector<int> status(nslab, ZH_OK);
   std::vector<std::string> msgs(nslab);
+  std::vector<DataErrPos> where(nslab);  // a data error's place in the oracle's order
   auto work = [&](int r) {
     const int64_t* o = &so[(size_t)r * n];
     const int64_t* s = &ss[(size_t)r * n];
@@ -2153,16 +2161,29 @@ int read_multi_impl(zh_ctx* const* ctxs, int ndev, int root, const zh_array_meta
     if (slab_route) slab_route[r] = route;
     status[r] = rc;
     msgs[r] = e;
+    if (rc == ZH_EDATA && g_data_err.set) where[r] = g_data_err;
   };
   std::vector<std::thread> th;
   for (int r = 0; r < nslab; r++) th.emplace_back(work, r);
   for (auto& t : th) t.join();
-  for (int r = 0; r < nslab; r++)  // first failing slab in C order
-    if (status[r] != ZH_OK) {
-      set_err(err, errlen, "%s", msgs[r].c_str());
-      return status[r];
+  // the first failing slab in C order; when every failure is a data error the device placed,
+  // the first of those in the oracle's order (slabs can cut a shard)
+  int first = -1, best = -1;
+  bool placed = true;
+  for (int r = 0; r < nslab; r++) {
+    if (status[r] == ZH_OK) continue;
+    if (first < 0) first = r;
+    if (status[r] != ZH_EDATA || !where[r].set) {
+      placed = false;
+      continue;
     }
-  return ZH_OK;
+    if (best < 0 || data_err_before(where[r].cc, where[r].key, where[best].cc, where[best].key))
+      best = r;
+  }
+  if (first < 0) return ZH_OK;
+  const int r = placed && best >= 0 ? best : first;
+  set_err(err, errlen, "%s", msgs[r].c_str());
+  return status[r];
 }
 
 }  // namespace zh

@@ -581,7 +581,7 @@ int read_pipelined(zh_ctx* ctx, const zh_array_meta* meta, const SrcDesc* srcs, 
           const int n = p->meta.ndim;
           std::vector<int64_t> cc(p->coords.begin() + p->err_shard * n,
                                   p->coords.begin() + (p->err_shard + 1) * n);
-          if (!data_err || cc < data_cc || (cc == data_cc && p->err_key > data_key)) {
+          if (!data_err || data_err_before(cc, p->err_key, data_cc, data_key)) {
             data_cc = cc;
             data_key = p->err_key;
             data_msg = e;
@@ -665,9 +665,13 @@ int read_pipelined(zh_ctx* ctx, const zh_array_meta* meta, const SrcDesc* srcs, 
     set_err(err, errlen, "%s", dev_msg.c_str());
     st = dev_st;
   }
+  g_data_err.set = false;
   if (st == ZH_OK && data_err) {
     set_err(err, errlen, "%s", data_msg.c_str());
     st = ZH_EDATA;
+    g_data_err.set = true;
+    g_data_err.cc = data_cc;
+    g_data_err.key = data_key;
   }
   if (st == ZH_OK && plan_st != ZH_OK) {
     set_err(err, errlen, "%s", plan_msg.c_str());
