@@ -49,8 +49,9 @@ def _layout(meta):
     return cps, isz, ch.index_location == A.ZH_INDEX_START, fmt
 
 
-def corrupt(rng, meta, shard, nbad):
-    """`shard` with `nbad` index entries mutated; returns (bytes, [mutation names])."""
+def corrupt(rng, meta, shard, nbad, huge=1 << 62):
+    """`shard` with `nbad` index entries mutated; returns (bytes, [mutation names]).  `huge`
+    bounds the far-out offsets of huge_off."""
     cps, isz, start, fmt = _layout(meta)
     total = len(shard)
     ib = 0 if start else total - isz
@@ -68,7 +69,7 @@ def corrupt(rng, meta, shard, nbad):
         elif mu == "missing_nb":
             ents[k] = [int(rng.integers(0, 1 << 40)), U64]
         elif mu == "huge_off":
-            ents[k] = [int(rng.integers(total + 1, 1 << 62)), want]
+            ents[k] = [int(rng.integers(total + 1, huge)), want]
         elif mu == "negative_off":
             ents[k] = [(1 << 63) + int(rng.integers(0, 1 << 40)), want]
         elif mu == "straddle_end":
@@ -244,3 +245,49 @@ def test_unsharded_crc_chunk_of_wrong_length(dev, tmp_path, form):
             assert k == 2 and got[1].endswith("for chunk [0, 2]"), got
         else:
             assert got[1] == want[1], (k, got, want)
+
+
+@pytest.mark.parametrize("loc", ["end", "start"])
+def test_corrupt_shard_files_through_the_array_api(dev, tmp_path, monkeypatch, loc):
+    """The same corrupt entries in the shard files of an array written through the Array API
+    (index [bytes, crc32c], recomputed valid over the corrupt entries), read through
+    Array.read with the library's file reads (ZH_FILES=1) and with the mirror's store reads
+    (ZH_FILES=0): both equal the oracle's store read — the same array or the same message.
+    Huge offsets stay below 2^40 here, under every file system's largest file (Q18)."""
+    import os
+    import zarrhip as z
+    shape = [24, 32, 48]
+    data = np.random.default_rng(233).integers(0, 2 ** 32, shape, dtype=np.uint32)
+    data[:8, :16, :24] = 0
+    m = (z.ArrayMetadataBuilder().withShape(*shape).withDataType(z.DataType.UINT32)
+         .withChunkShape(8, 16, 24).withFillValue(0)
+         .withCodecs(lambda c: c.withSharding([4, 8, 8], lambda c1: c1.withTranspose([2, 0, 1])
+                                              .withBytes("BIG"), loc)).build())
+    z.Array.create(z.FilesystemStore(tmp_path).resolve("a"), m).write(None, data)
+    a = z.Array.open(z.FilesystemStore(tmp_path).resolve("a"))
+    meta = a.zmeta
+    allc = chunk_coords(meta, [0, 0, 0], shape)
+    path = {c: os.path.join(tmp_path, "a", "c", *map(str, c)) for c in allc}
+    originals = {c: open(p, "rb").read() for c, p in path.items() if os.path.exists(p)}
+    rng = np.random.default_rng(239 if loc == "end" else 241)
+    for t in range(40):
+        for c, b in originals.items():  # fresh files, then corrupt one or two
+            with open(path[c], "wb") as f:
+                f.write(b)
+        for c in [list(originals)[int(i)] for i in
+                  rng.choice(len(originals), size=int(rng.integers(1, 3)), replace=False)]:
+            bad, _ = corrupt(rng, meta, originals[c], int(rng.integers(1, 4)), huge=1 << 40)
+            with open(path[c], "wb") as f:
+                f.write(bad)
+        off = [int(rng.integers(0, s)) for s in shape]
+        shp = [int(rng.integers(1, s - o + 1)) for s, o in zip(shape, off)]
+        rp = [path[c] if os.path.exists(path[c]) else None for c in chunk_coords(meta, off, shp)]
+        want = _outcome(lambda: store_read(meta, rp, off, shp))
+        for files in ("1", "0"):
+            monkeypatch.setenv("ZH_FILES", files)
+            b = z.Array.open(z.FilesystemStore(tmp_path).resolve("a"))
+            try:
+                got = ("ok", b.read(off, shp))
+            except z.ZarrException as e:
+                got = ("err", str(e))
+            _same(got, want, (loc, t, files, off, shp))
