@@ -231,7 +231,10 @@ int zh_array_read(zh_ctx* ctx, const zh_array_meta* meta, const zh_chunk_src* ch
  *                        into their own HBM and copy their slab to the root's slice over
  *                        xGMI (hipMemcpyPeerAsync), or through pinned host memory when the
  *                        pair has no peer access (see zh_array_read_multi_routed).
- *   Errors: the first failing slab in C order, with zh_array_read's messages.
+ *   Errors: zh_array_read's messages; when the slabs' failures are all data errors the
+ *   device placed (checksums, index entries), the first of them in zh_array_read's order (the
+ *   chunk first in C order, then the error within it; slabs may cut a shard), else the first
+ *   failing slab in C order.
  * zh_slab_partition writes nslabs rows of ndim int64 offsets / shapes (ZH_EINVAL when the
  * region cannot be split into nslabs contiguous slabs).
  */
