@@ -4,7 +4,8 @@ TransposeCodec.encode, Array.writeChunk's all-fill elision :148-151), then the s
 read back (device and oracle) against the array.
 
 Each case draws: rank 1-4, array / chunk / inner / leaf shapes (boundary chunks included),
-dtype 1/2/4/8 bytes (float32/float64 with a 0, -0, NaN or ordinary fill among them), transpose
+dtype 1/2/4/8 bytes (bool among the 1-byte ones; float32/float64 with a 0, -0, NaN or ordinary
+fill among them), transpose
 order, bytes and index endianness, index at start or end, index crc32c, chunk crc32c, nested
 sharding; the data holds blocks of fill so that chunks, inner chunks and leaves are elided.
 The CPU test holds the oracle to its own round trip; the GPU test compares the device's bytes
@@ -46,14 +47,15 @@ def random_case(seed):
         shape[d] = max(1, shape[d] // 2)
     ds = int(rng.choice([1, 2, 4, 8]))
     is_float = ds in FLOATS and rng.random() < 0.5
+    is_bool = ds == 1 and rng.random() < 0.3
     dt = np.dtype(FLOATS[ds]) if is_float else NP_DT[ds]
     if is_float:
         fill = float(rng.choice([0.0, -0.0, np.nan, 1.5]))
     else:
-        fill = int(rng.integers(0, 4))
+        fill = int(rng.integers(0, 2 if is_bool else 4))
     fill_bytes = np.array([fill], dt).tobytes()
     order = [int(x) for x in rng.permutation(n)] if rng.random() < 0.5 else None
-    kw = dict(fill=fill_bytes, is_float=is_float, is_bool=False,
+    kw = dict(fill=fill_bytes, is_float=is_float, is_bool=is_bool,
               transpose_order=order,
               endian=A.ZH_ENDIAN_BIG if rng.random() < 0.5 else A.ZH_ENDIAN_LITTLE,
               inner_crc32c=bool(rng.random() < 0.3))
@@ -71,6 +73,8 @@ def random_case(seed):
     if is_float:
         a = rng.standard_normal(shape).astype(dt)
         a[rng.random(shape) < 0.1] = -0.0
+    elif is_bool:
+        a = (rng.random(shape) < 0.5).astype(dt)
     else:
         a = rng.integers(0, 2 ** (8 * ds) - 1, size=shape, dtype=np.uint64).astype(dt)
     # blocks of fill (whole chunks, inner chunks or leaves where they line up)
