@@ -317,3 +317,24 @@ def test_read_spread_over_devices(tmp_path, monkeypatch, spec):
     monkeypatch.setenv("ZH_DEVICES", spec)
     np.testing.assert_array_equal(arr.read(), content)
     np.testing.assert_array_equal(arr.read([1, 2, 3], [14, 13, 12]), one)
+
+
+def test_large_array_with_offset_beyond_max_int(tmp_path):
+    """testLargeArrayWithOffsetBeyondMaxInt (ZarrV3Test.java:994-1036): a 3e9 x 3e9 int32
+    array of 1000² chunks, fill 42; a [1, 1000] row written at [0, 0] and at
+    [1, Integer.MAX_VALUE + 1] (each a read-modify-write of one chunk) reads back, and a
+    chunk nobody wrote reads the fill value."""
+    big = 3_000_000_000
+    m = (z.ArrayMetadataBuilder().withShape(big, big).withDataType(z.DataType.INT32)
+         .withChunkShape(1000, 1000).withFillValue(42).build())
+    a = z.Array.create(z.FilesystemStore(tmp_path).resolve("large_array_beyond_int"), m)
+    a.write([0, 0], np.full((1, 1000), 100, np.int32))
+    far = [1, 2 ** 31]
+    a.write(far, np.full((1, 1000), 200, np.int32))
+    b = z.Array.open(z.FilesystemStore(tmp_path).resolve("large_array_beyond_int"))
+    assert b.read([0, 0], [1, 100])[0, 0] == 100
+    got = b.read(far, [1, 100])
+    assert (got == 200).all()
+    assert (b.read([0, 2 ** 31], [1, 100]) == 42).all()  # the same chunk's row 0: fill
+    assert (b.read([5000, 5000], [3, 3]) == 42).all()    # a chunk never written
+    assert b.metadata.shape == [big, big]
