@@ -566,9 +566,12 @@ class Array:
         return out
 
     # ---------------------------------------------------------------- write
-    def write(self, offset, data):
-        """core.Array.write: whole-chunk regions are encoded on the device in one call;
-        partial chunks are read-modify-written (decode → patch → encode)."""
+    def write(self, offset, data, parallel=True):
+        """core.Array.write(offset, array, parallel) (M/core/Array.java:83-156): whole-chunk
+        regions are encoded on the device in one call; partial chunks are read-modify-written
+        (decode → patch → encode).  `parallel` is the reference's switch between a serial and a
+        parallel chunk stream; the device encodes every chunk of a call in one launch either
+        way, so it only reaches the read of a read-modify-write."""
         data = np.ascontiguousarray(data, dtype=self.metadata.data_type.numpy)
         n = self.ndim
         offset = [0] * n if offset is None else [int(o) for o in offset]
@@ -579,7 +582,7 @@ class Array:
         hi = [min(-(-(o + s) // c) * c, a) for o, s, c, a in zip(offset, shape, cs, ash)]
         if lo != offset or hi != [o + s for o, s in zip(offset, shape)]:
             ext = [h - l for l, h in zip(lo, hi)]
-            region = self.read(lo, ext)
+            region = self.read(lo, ext, parallel)
             sl = tuple(slice(o - l, o - l + s) for o, l, s in zip(offset, lo, shape))
             region[sl] = data
             data, offset, shape = region, lo, ext
