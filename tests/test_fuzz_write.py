@@ -169,3 +169,30 @@ def test_device_read_random_regions_match_oracle(dev, tmp_path, monkeypatch, see
             np.testing.assert_array_equal(_bits(files_read(dev, meta, rp, off, shp).view(dt)),
                                           _bits(store_read(meta, rp, off, shp).view(dt)),
                                           err_msg=f"files {seed} {off} {shp}")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", CASES[:max(1, len(CASES) // 2)])
+def test_jni_shim_random_chains(dev, seed):
+    """The same random chains through the JNI shim under the fake JVM (HipArray.write's
+    arrayWrite and HipArray.read's arrayRead: zh_array_meta packed from Java primitives, the
+    float flag included): the encoded chunk objects equal the oracle's (null where all fill),
+    and a random region reads back as the oracle reads it; the JNI rules hold."""
+    from helpers import chunk_coords
+    from jni_harness import FakeJVM
+    meta, a, dt = random_case(seed)
+    shape = list(a.shape)
+    want = encode_oracle(meta, a)
+    jvm = FakeJVM()
+    got = jvm.array_write(dev.h.value, meta, a, [0] * len(shape))
+    assert got == want, seed
+    rng = np.random.default_rng(20_000 + seed)
+    off = [int(rng.integers(0, s)) for s in shape]
+    shp = [int(rng.integers(1, s - o + 1)) for s, o in zip(shape, off)]
+    allc = chunk_coords(meta, [0] * len(shape), shape)
+    pos = {c: i for i, c in enumerate(allc)}
+    src = [want[pos[c]] for c in chunk_coords(meta, off, shp)]
+    rc, out = jvm.array_read(dev.h.value, meta, src, off, shp)
+    assert rc == 0, seed
+    np.testing.assert_array_equal(_bits(out), _bits(_decode(meta, src, dt, shp)))
+    jvm.check_rules()
