@@ -17,6 +17,7 @@ import pytest
 
 import oracle as O
 from helpers import NP_DT, device_read, device_write, encode_oracle
+from test_gpu_files import three_ctxs  # noqa: F401 (fixture)
 from zarrhip import _abi as A
 
 FLOATS = {4: "<f4", 8: "<f8"}
@@ -138,7 +139,8 @@ def test_device_write_matches_oracle_bytes(dev, seed):
 @pytest.mark.gpu
 @pytest.mark.parametrize("pipelined", [False, True])
 @pytest.mark.parametrize("seed", CASES)
-def test_device_read_random_regions_match_oracle(dev, tmp_path, monkeypatch, seed, pipelined):
+def test_device_read_random_regions_match_oracle(dev, three_ctxs, tmp_path, monkeypatch, seed,
+                                                 pipelined):
     """The same random chains read back: three random regions per case (any offset and
     extent inside the array), from memory and from the chunk files through the library's own
     store reads, against the oracle's read of the same stored chunks.  pipelined: thresholds
@@ -164,6 +166,11 @@ def test_device_read_random_regions_match_oracle(dev, tmp_path, monkeypatch, see
         want = np.frombuffer(O.array_read(meta, src, off, shp), dt).reshape(shp)
         got = device_read(dev, meta, src, off, shp)
         np.testing.assert_array_equal(_bits(got), _bits(want), err_msg=f"{seed} {off} {shp}")
+        if seed % 3 == 0:  # the region in slabs over three contexts (zh_array_read_multi)
+            from test_gpu_fuzz_index import _multi_read
+            got = _multi_read(three_ctxs, meta, src, off, shp).view(dt)
+            np.testing.assert_array_equal(_bits(got), _bits(want),
+                                          err_msg=f"multi {seed} {off} {shp}")
         if paths is not None:
             rp = region_paths(meta, paths, off, shp)
             np.testing.assert_array_equal(_bits(files_read(dev, meta, rp, off, shp).view(dt)),
