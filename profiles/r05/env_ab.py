@@ -1,0 +1,76 @@
+"""Round 5 lab: interleaved A/B of decode plan variants selected by environment switches (read
+at plan creation), one process, plain hipMalloc buffers (the headline's allocation), the full
+array.  Each variant has its own plan over the same shards; per round every variant runs
+`steps` launches, HIP-event kernel time of the scatter launch; the output is verified after
+each variant's launches.
+usage: python3 profiles/r05/env_ab.py OUT.json CONFIG ROUNDS STEPS VAR=VAL[,VAR=VAL] ...
+("-" = no switches)"""
+import json
+import os
+import statistics
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "zarr-java_amd")]
+import bench  # noqa: E402
+
+
+def main():
+    out_path, cfg = sys.argv[1], sys.argv[2]
+    rounds, steps = int(sys.argv[3]), int(sys.argv[4])
+    variants = sys.argv[5:]
+    from zarrhip import _abi as A
+    from zarrhip._lib import DeviceContext, lib
+    dev = DeviceContext(0)
+    meta = bench.build_meta(A, cfg, 1)
+    L = lib()
+    n = meta.ndim
+    shape = [meta.shape[d] for d in range(n)]
+    coords = bench.all_coords(L, meta)
+    caps = bench.chunk_capacities(meta, coords)
+    offs, tot = bench.slab_layout(caps)
+    nel = 1
+    for s in shape:
+        nel *= s
+    out = dev.malloc(max(nel * 4, tot))
+    slab = dev.malloc(max(nel * 4, tot))
+    dev.synth_fill(out, nel, 4, 0, bench.SEED)
+    sizes = dev.array_write(meta, out, [0] * n, shape,
+                            [(slab + o, c) for o, c in zip(offs, caps)])
+    sources = [(slab + o, s) for o, s in zip(offs, sizes)]
+    flags = A.ZH_SRC_DEVICE | A.ZH_OUT_DEVICE
+    plans = {}
+    for v in variants:
+        saved = {}
+        for kv in ([] if v == "-" else v.split(",")):
+            k, val = kv.split("=")
+            saved[k] = os.environ.get(k)
+            os.environ[k] = val
+        plans[v] = dev.plan(meta, sources, [0] * n, shape, flags)
+        plans[v].set_timing(True)
+        for k, old in saved.items():
+            if old is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = old
+    res = {"config": cfg, "steps": steps, "variants": variants, "kernel_ms": {v: [] for v in variants}}
+    for r in range(rounds):
+        for v in variants:
+            p = plans[v]
+            p.kernel_time()  # drain earlier timings
+            for _ in range(steps):
+                p.execute(out)
+            p.wait()
+            kt = p.kernel_time()
+            res["kernel_ms"][v].append(round(kt["scatter_ms"] / max(1, kt["launches"]), 3))
+            bad = int(dev.synth_verify(out, shape, [0] * n, shape, 4, bench.SEED))
+            assert bad == 0, (v, bad)
+        print(json.dumps({v: res["kernel_ms"][v][-1] for v in variants}), flush=True)
+    res["median_ms"] = {v: statistics.median(x) for v, x in res["kernel_ms"].items()}
+    with open(out_path, "w") as f:
+        json.dump(res, f, indent=1)
+    print(json.dumps(res["median_ms"]), flush=True)
+
+
+if __name__ == "__main__":
+    main()
