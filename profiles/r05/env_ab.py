@@ -4,7 +4,9 @@ array.  Each variant has its own plan over the same shards; per round every vari
 `steps` launches, HIP-event kernel time of the scatter launch; the output is verified after
 each variant's launches.
 usage: python3 profiles/r05/env_ab.py OUT.json CONFIG ROUNDS STEPS VAR=VAL[,VAR=VAL] ...
-("-" = no switches)"""
+("-" = no switches).  AB_YDIV divides the array's y extent; AB_OUTS > 1 allocates that many
+output buffers (each held while the next is allocated, so each gets other memory) and runs
+every variant into each: a switch's effect per placement of the output."""
 import json
 import os
 import statistics
@@ -22,7 +24,9 @@ def main():
     from zarrhip import _abi as A
     from zarrhip._lib import DeviceContext, lib
     dev = DeviceContext(0)
-    meta = bench.build_meta(A, cfg, 1)
+    ydiv = int(os.environ.get("AB_YDIV", "1"))
+    nouts = int(os.environ.get("AB_OUTS", "1"))
+    meta = bench.build_meta(A, cfg, ydiv)
     L = lib()
     n = meta.ndim
     shape = [meta.shape[d] for d in range(n)]
@@ -32,8 +36,9 @@ def main():
     nel = 1
     for s in shape:
         nel *= s
-    out = dev.malloc(max(nel * 4, tot))
     slab = dev.malloc(max(nel * 4, tot))
+    outs = [dev.malloc(nel * 4) for _ in range(nouts)]
+    out = outs[0]
     dev.synth_fill(out, nel, 4, 0, bench.SEED)
     sizes = dev.array_write(meta, out, [0] * n, shape,
                             [(slab + o, c) for o, c in zip(offs, caps)])
@@ -53,19 +58,25 @@ def main():
                 os.environ.pop(k, None)
             else:
                 os.environ[k] = old
-    res = {"config": cfg, "steps": steps, "variants": variants, "kernel_ms": {v: [] for v in variants}}
+    keys = [f"out{k}:{v}" if nouts > 1 else v for k in range(nouts) for v in variants]
+    res = {"config": cfg, "ydiv": ydiv, "outputs": nouts, "steps": steps, "variants": variants,
+           "kernel_ms": {key: [] for key in keys}}
     for r in range(rounds):
-        for v in variants:
-            p = plans[v]
-            p.kernel_time()  # drain earlier timings
-            for _ in range(steps):
-                p.execute(out)
-            p.wait()
-            kt = p.kernel_time()
-            res["kernel_ms"][v].append(round(kt["scatter_ms"] / max(1, kt["launches"]), 3))
-            bad = int(dev.synth_verify(out, shape, [0] * n, shape, 4, bench.SEED))
-            assert bad == 0, (v, bad)
-        print(json.dumps({v: res["kernel_ms"][v][-1] for v in variants}), flush=True)
+        row = {}
+        for k, o in enumerate(outs):
+            for v in variants:
+                key = f"out{k}:{v}" if nouts > 1 else v
+                p = plans[v]
+                p.kernel_time()  # drain earlier timings
+                for _ in range(steps):
+                    p.execute(o)
+                p.wait()
+                kt = p.kernel_time()
+                res["kernel_ms"][key].append(round(kt["scatter_ms"] / max(1, kt["launches"]), 3))
+                row[key] = res["kernel_ms"][key][-1]
+                bad = int(dev.synth_verify(o, shape, [0] * n, shape, 4, bench.SEED))
+                assert bad == 0, (key, bad)
+        print(json.dumps(row), flush=True)
     res["median_ms"] = {v: statistics.median(x) for v, x in res["kernel_ms"].items()}
     with open(out_path, "w") as f:
         json.dump(res, f, indent=1)
