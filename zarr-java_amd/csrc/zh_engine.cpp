@@ -1412,10 +1412,12 @@ int plan_create(zh_ctx* ctx, const zh_array_meta* m, const SrcDesc* srcs, int64_
   // streams (the grouped row-CRC decode loads its payloads through the cache, launcher)
   p->args.nt = 3;
   // Visit items in a golden-ratio stride order: +3.6 % on the tile path (c4) on every normal
-  // allocation, neutral on the row path (interleaved A/B, profiles/placement_perm.py), so
-  // on by default for tiles.  ZH_ITEM_PERM=0/1 overrides.
-  p->args.item_mul =
-      env_int("ZH_ITEM_PERM", p->tile_mode ? 1 : 0) ? golden_item_mul(p->args.total_items) : 0;
+  // allocation (profiles/placement_perm.py); on the row paths it evens out where the output
+  // lands — half-array c2 into three hipMalloc outputs: 18.10 / 16.14 / 16.13 → 16.45 / 16.03 /
+  // 16.03 ms, c3 19.16 / 18.42 / 17.33 → 19.62 / 16.87 / 16.52 ms (round 5,
+  // profiles/r05/perm/) — so on by default for every decode fast path.  ZH_ITEM_PERM=0 turns
+  // it off.
+  p->args.item_mul = env_int("ZH_ITEM_PERM", 1) ? golden_item_mul(p->args.total_items) : 0;
   p->slow_grid = p->grid;
   // The tile decode over G consecutive (z-adjacent) chunks per work item, the next step's
   // loads issued before this step's stores (tiles_group_kernel; tile_variant 20 + G): c4
@@ -1483,7 +1485,7 @@ int plan_create(zh_ctx* ctx, const zh_array_meta* m, const SrcDesc* srcs, int64_
       if (G >= 1 && (xpose || (G << g.fast_vpr_shift) <= 64)) {
         const int64_t groups = (items + G - 1) / G;
         p->args.row_group = G;
-        p->args.item_mul = env_int("ZH_ITEM_PERM", 0) ? golden_item_mul(groups) : 0;
+        p->args.item_mul = env_int("ZH_ITEM_PERM", 1) ? golden_item_mul(groups) : 0;
         p->grid = grid_for(ctx, groups);
       }
     }
