@@ -38,7 +38,8 @@ def kernel_rows(path, match):
 FAST = ("decode_rows_kernel", "decode_tiles_kernel", "tiles_group_kernel", "rows_group_kernel",
         "rows_xpose_kernel", "tiles_rowcrc_kernel", "tiles_crcw_kernel",
         "tiles_rowcrc_aln_kernel")
-DECODE_ONLY = ("tiles_rowcrc_kernel", "tiles_crcw_kernel", "tiles_rowcrc_aln_kernel")  # last template argument is not FLAGS
+DECODE_ONLY = ("tiles_rowcrc_kernel", "tiles_crcw_kernel", "tiles_rowcrc_aln_kernel",
+               "rows_xpose_kernel")  # last template argument is not FLAGS (xpose: PF)
 
 
 def main(src, config, out):
