@@ -1,8 +1,10 @@
-"""Round 5 lab: the small read (BASELINE configs[0]'s call shape, bench.small_read) with the
-index crc32c on the context's side stream (ZH_CRC_SIDE=1, default) or first on the plan's
-stream (0), interleaved in one process over one c4-format array (y/4: the region's shard is
-the same 4 GiB c4 shard).  Median of `reps` one-shot reads per setting and round.
-usage: python3 profiles/r05/small_ab.py OUT.json [rounds] [reps]"""
+"""Round 5 lab: the small read (BASELINE configs[0]'s call shape, bench.small_read) under two
+settings of one switch read at plan creation, interleaved in one process over one c4-format
+array (y/4: the region's shard is the same 4 GiB c4 shard).  Median of `reps` one-shot reads
+per setting and round.  First use: the index crc32c on a side stream (ZH_CRC_SIDE, since
+removed); then the index crc32c inside the slow kernel's launch (ZH_CRC_FUSE=1) or on its own
+ahead of the resolve kernel (0).
+usage: python3 profiles/r05/small_ab.py OUT.json [rounds] [reps] [VAR]"""
 import json
 import os
 import statistics
@@ -19,6 +21,7 @@ def main():
     out_path = sys.argv[1]
     rounds = int(sys.argv[2]) if len(sys.argv) > 2 else 5
     reps = int(sys.argv[3]) if len(sys.argv) > 3 else 200
+    var = sys.argv[4] if len(sys.argv) > 4 else "ZH_CRC_FUSE"
     from zarrhip import _abi as A
     from zarrhip._lib import DeviceContext, lib
     dev = DeviceContext(0)
@@ -43,11 +46,11 @@ def main():
     nb = 4 * 64 ** 3
     dout = dev.malloc(nb)
     host = (C.c_char * nb)()
-    res = {"region_offset": off, "region_shape": shp, "reps": reps, "rounds": []}
+    res = {"region_offset": off, "region_shape": shp, "reps": reps, "switch": var, "rounds": []}
     for r in range(rounds):
         row = {}
         for side in ("1", "0"):
-            os.environ["ZH_CRC_SIDE"] = side
+            os.environ[var] = side
             for tag, dst, flags in (("device_out_us", dout, A.ZH_SRC_DEVICE | A.ZH_OUT_DEVICE),
                                     ("host_out_us", C.addressof(host), A.ZH_SRC_DEVICE)):
                 ts = []
@@ -56,7 +59,7 @@ def main():
                     dev.array_read(meta, src, off, shp, dst, flags)
                     if i >= 20:
                         ts.append(time.perf_counter() - t0)
-                row[f"side{side}_{tag}"] = round(statistics.median(ts) * 1e6, 1)
+                row[f"{var}={side}:{tag}"] = round(statistics.median(ts) * 1e6, 1)
                 if dst != dout:
                     dev.memcpy(dout, dst, nb, 0, None, True)
                 bad = int(dev.synth_verify(dout, shape, off, shp, 4, bench.SEED))

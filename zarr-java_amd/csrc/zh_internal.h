@@ -248,6 +248,19 @@ struct CrcJob {
   int32_t pad;
 };
 
+// one index-CRC launch: the jobs, their span count, the span registers + completion counters
+// (launch_crc below), the status words (nullptr: store the CRC, the write path)
+struct CrcIdxArgs {
+  const CrcJob* jobs;
+  int64_t njobs;
+  int64_t nspans;
+  uint32_t* partials;
+  uint64_t* status;
+  int32_t sshift;
+  int32_t pad;
+};
+constexpr int kCrcLdsWords = 12 * 256 + kBlock + 1;  // tables, wave reduction, last flag
+
 int env_int(const char* name, int def);  // zh_engine.cpp: an integer switch from the environment
 
 // Kernel launchers (zh_kernels.hip).
@@ -270,7 +283,10 @@ bool rowcrc_lds_at_zero();  // the row-CRC tile kernels have no static LDS
 constexpr int kAlnUnitsMax = 32;  // tiles_rowcrc_aln_kernel: units per chunk (its K capacity)
 hipError_t launch_scatter(const ScatterArgs& a, int dsize, int tile_mode, int encode, int grid,
                           hipStream_t stream);
-hipError_t launch_decode_slow(const ScatterArgs& a, int grid, hipStream_t stream);
+// the slow list; with crc.nspans > 0 the index crc32c runs in the same launch (first
+// crc.nspans workgroups) instead of launch_crc ahead of the resolve kernel
+hipError_t launch_decode_slow(const ScatterArgs& a, int grid, const CrcIdxArgs& crc,
+                              hipStream_t stream);
 hipError_t launch_flags(const ScatterArgs& a, int dsize, int grid, hipStream_t stream);
 // write path, one pass: payload offsets + encode-view descriptors + slow list, the fast
 // kernels with the all-fill test, the slow list through the generic encode, then the finish

@@ -2246,13 +2246,24 @@ void decode_tiles_crc_w3_kernel(ScatterArgs a) {
 
 // decode, slow kernel: the items the resolve kernel listed (clipped by the region,
 // misaligned, or without a fast table), through the generic strided paths
+__device__ void crc_index_block(const CrcIdxArgs& c, int64_t span, uint32_t* lds);  // below
+
+// The first c.nspans workgroups run the index crc32c instead (crc_index_block; c.nspans = 0
+// when the plan launched it on its own), in the same LDS.
 template <int DS, bool TILE>
-__global__ __launch_bounds__(kBlock) void decode_slow_kernel(ScatterArgs a) {
+__global__ __launch_bounds__(kBlock) void decode_slow_kernel(ScatterArgs a, CrcIdxArgs c) {
   using T = typename ElemT<DS>::T;
-  __shared__ T tile[TILE ? kTileTPB : 1][32][33];
+  constexpr int kTileWords = ((TILE ? kTileTPB : 1) * 32 * 33 * DS + 7) / 8 * 2;
+  __shared__ uint64_t sm[(kTileWords > kCrcLdsWords ? kTileWords : kCrcLdsWords) / 2 + 1];
+  if (blockIdx.x < c.nspans) {  // uniform per workgroup
+    crc_index_block(c, blockIdx.x, reinterpret_cast<uint32_t*>(sm));
+    return;
+  }
+  T (*tile)[32][33] = reinterpret_cast<T (*)[32][33]>(sm);
   const int64_t total = (int64_t)(*a.slow_count) << a.piece_shift;
   const uint32_t pmask = (1u << a.piece_shift) - 1;
-  for (int64_t k = blockIdx.x; k < total; k += gridDim.x) {
+  const int64_t nb = (int64_t)gridDim.x - c.nspans;
+  for (int64_t k = (int64_t)blockIdx.x - c.nspans; k < total; k += nb) {
     const uint32_t citem = a.slow_list[k >> a.piece_shift];
     const uint32_t piece = (uint32_t)k & pmask;
     const ItemDesc D = ld_desc(a.desc + citem);
@@ -2613,41 +2624,52 @@ __device__ __forceinline__ void crc_index_finish(const CrcJob& J, const uint32_t
   }
 }
 
-__global__ __launch_bounds__(kBlock) void crc_index_kernel(const CrcJob* jobs, int64_t njobs,
-                                                           int64_t nspans, int sshift,
-                                                           uint32_t* partials,
-                                                           uint64_t* status) {
+// One workgroup's share of the index CRC launch: span `span` of the jobs, in LDS scratch of
+// kCrcLdsWords words (the tables, the wave reduction, the last-workgroup flag).  Its own
+// launch (crc_index_kernel, the write path) or the first c.nspans workgroups of the decode's
+// slow kernel (decode_slow_kernel): the index check then runs beside the clipped chunks'
+// decode instead of ahead of the resolve kernel — it only writes status words.
+__device__ void crc_index_block(const CrcIdxArgs& c, int64_t span, uint32_t* lds) {
+  uint32_t (*T)[256] = reinterpret_cast<uint32_t (*)[256]>(lds);
+  uint32_t (*S)[256] = reinterpret_cast<uint32_t (*)[256]>(lds + 8 * 256);
+  uint32_t* red = lds + 12 * 256;
+  uint32_t* last = red + kBlock;
+  const int sshift = c.sshift;
   const int64_t SPAN = (int64_t)kIdxSpan << sshift;
-  __shared__ uint32_t T[8][256];
-  __shared__ uint32_t S[4][256];
-  __shared__ uint32_t red[kBlock];
-  __shared__ int last;
   const int tid = threadIdx.x;
-#pragma unroll
-  for (int b = 0; b < 4; b++) S[b][tid] = g_crc.S[b][tid];
-  init_crc_tables(T);
-  const int64_t span = blockIdx.x;
-  int64_t lo = 0, hi = njobs - 1;
+  int64_t lo = 0, hi = c.njobs - 1;
   while (lo < hi) {
     int64_t mid = (lo + hi + 1) >> 1;
-    if (jobs[mid].span_begin <= span) lo = mid;
+    if (c.jobs[mid].span_begin <= span) lo = mid;
     else hi = mid - 1;
   }
-  const CrcJob J = jobs[lo];
+  const CrcJob J = c.jobs[lo];
   const int64_t sb = (span - J.span_begin) * SPAN;
   const int64_t slen = min(SPAN, J.len - sb);
   const uint8_t* base = J.base + sb;
+  const bool aligned = (((uintptr_t)base) & 3) == 0;
+  const int nblk = (int)(slen >> 4);
+  // the span's first vectors are in flight while the tables are copied into LDS
+  v4u v[4];
+#pragma unroll
+  for (int u = 0; u < 4; u++) {
+    const int j = tid + u * kBlock;
+    if (aligned && j < nblk) v[u] = *reinterpret_cast<const v4u*>(base + 16 * (int64_t)j);
+  }
+#pragma unroll
+  for (int b = 0; b < 4; b++) S[b][tid] = g_crc.S[b][tid];
+  init_crc_tables(T);
   uint32_t raw;
-  if ((((uintptr_t)base) & 3) == 0) {
-    const int nblk = (int)(slen >> 4);
+  if (aligned) {
     uint32_t acc = 0;
     int nb = 0;
     for (int j0 = 0; j0 < nblk; j0 += kBlock * 4) {
-      v4u v[4];
+      if (j0 > 0) {
 #pragma unroll
-      for (int u = 0; u < 4; u++) {
-        const int j = j0 + tid + u * kBlock;
-        if (j < nblk) v[u] = *reinterpret_cast<const v4u*>(base + 16 * (int64_t)j);
+        for (int u = 0; u < 4; u++) {
+          const int j = j0 + tid + u * kBlock;
+          if (j < nblk) v[u] = *reinterpret_cast<const v4u*>(base + 16 * (int64_t)j);
+        }
       }
 #pragma unroll
       for (int u = 0; u < 4; u++)
@@ -2676,32 +2698,37 @@ __global__ __launch_bounds__(kBlock) void crc_index_kernel(const CrcJob* jobs, i
     const int64_t kLane = SPAN / kBlock;  // bytes per lane
     const int64_t lb = (int64_t)tid * kLane;
     const int64_t llen = max((int64_t)0, min((int64_t)kLane, slen - lb));
-    uint32_t c = 0;
-    for (int64_t i = 0; i < llen; i++) c = T[0][(c ^ base[lb + i]) & 0xFFu] ^ (c >> 8);
-    uint32_t v = llen > 0 ? multmodp(x2nmodp((uint64_t)(slen - lb - llen), 3), c) : 0u;
+    uint32_t cr = 0;
+    for (int64_t i = 0; i < llen; i++) cr = T[0][(cr ^ base[lb + i]) & 0xFFu] ^ (cr >> 8);
+    uint32_t w = llen > 0 ? multmodp(x2nmodp((uint64_t)(slen - lb - llen), 3), cr) : 0u;
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v ^= (uint32_t)__shfl_xor((int)v, o, 64);
-    if ((tid & 63) == 0) red[tid >> 6] = v;
+    for (int o = 32; o > 0; o >>= 1) w ^= (uint32_t)__shfl_xor((int)w, o, 64);
+    if ((tid & 63) == 0) red[tid >> 6] = w;
     __syncthreads();
     raw = red[0] ^ red[1] ^ red[2] ^ red[3];
   }
-  uint32_t* counter = partials + nspans + lo;
+  uint32_t* counter = c.partials + c.nspans + lo;
   const int64_t njs = (J.len + SPAN - 1) / SPAN;
   // Publish the span's register write-through (an agent-scope store: sc1, past this XCD's L2)
   // and wait for it before the ticket; the last workgroup reads every partial with agent-scope
   // loads.  No release / acquire fence: __threadfence() here wrote back the whole XCD L2 in
   // every workgroup (MI355X_MICROARCH.md "Workgroup dispatch ... inter-workgroup visibility").
   if (tid == 0) {
-    __hip_atomic_store(partials + span, raw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(c.partials + span, raw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    last = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
-           (uint32_t)(njs - 1);
+    *last = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+            (uint32_t)(njs - 1);
   }
   __syncthreads();
-  if (!last) return;  // uniform
+  if (!*last) return;  // uniform
   // ready for the next launch (every other workgroup has counted)
   if (tid == 0) __hip_atomic_store(counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  crc_index_finish(J, partials, sshift, status, red);
+  crc_index_finish(J, c.partials, sshift, c.status, red);
+}
+
+__global__ __launch_bounds__(kBlock) void crc_index_kernel(CrcIdxArgs c) {
+  __shared__ uint32_t lds[kCrcLdsWords];
+  crc_index_block(c, blockIdx.x, lds);
 }
 
 // (crc_upd16 / crc_shift_tab: see "CRC-32C helpers" above the row kernel)
@@ -3123,8 +3150,8 @@ hipError_t launch_data_crc(const DataCrcArgs& a, int grid, hipStream_t stream) {
 hipError_t launch_crc(const CrcJob* jobs, int64_t njobs, int64_t nspans, int span_shift,
                       uint32_t* partials, uint64_t* status, hipStream_t stream) {
   if (njobs == 0) return hipSuccess;
-  hipLaunchKernelGGL(crc_index_kernel, dim3((unsigned)nspans), dim3(kBlock), 0, stream, jobs,
-                     njobs, nspans, span_shift, partials, status);
+  const CrcIdxArgs c{jobs, njobs, nspans, partials, status, span_shift, 0};
+  hipLaunchKernelGGL(crc_index_kernel, dim3((unsigned)nspans), dim3(kBlock), 0, stream, c);
   return hipGetLastError();
 }
 
@@ -3251,19 +3278,22 @@ hipError_t launch_scatter(const ScatterArgs& a, int dsize, int tile_mode, int en
 }
 
 template <int DS>
-static void launch_slow_ds(const ScatterArgs& a, int grid, hipStream_t s) {
+static void launch_slow_ds(const ScatterArgs& a, int grid, const CrcIdxArgs& c, hipStream_t s) {
   if (a.tile)
-    hipLaunchKernelGGL((decode_slow_kernel<DS, true>), dim3(grid), dim3(kBlock), 0, s, a);
+    hipLaunchKernelGGL((decode_slow_kernel<DS, true>), dim3(grid), dim3(kBlock), 0, s, a, c);
   else
-    hipLaunchKernelGGL((decode_slow_kernel<DS, false>), dim3(grid), dim3(kBlock), 0, s, a);
+    hipLaunchKernelGGL((decode_slow_kernel<DS, false>), dim3(grid), dim3(kBlock), 0, s, a, c);
 }
 
-hipError_t launch_decode_slow(const ScatterArgs& a, int grid, hipStream_t stream) {
+hipError_t launch_decode_slow(const ScatterArgs& a, int grid, const CrcIdxArgs& crc,
+                              hipStream_t stream) {
+  const CrcIdxArgs c = crc.njobs > 0 ? crc : CrcIdxArgs{};
+  grid = std::max(grid, 1) + (int)c.nspans;
   switch (a.dsize) {
-    case 1: launch_slow_ds<1>(a, grid, stream); break;
-    case 2: launch_slow_ds<2>(a, grid, stream); break;
-    case 4: launch_slow_ds<4>(a, grid, stream); break;
-    case 8: launch_slow_ds<8>(a, grid, stream); break;
+    case 1: launch_slow_ds<1>(a, grid, c, stream); break;
+    case 2: launch_slow_ds<2>(a, grid, c, stream); break;
+    case 4: launch_slow_ds<4>(a, grid, c, stream); break;
+    case 8: launch_slow_ds<8>(a, grid, c, stream); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();
