@@ -2,7 +2,7 @@
 at plan creation), one process, plain hipMalloc buffers (the headline's allocation), the full
 array.  Each variant has its own plan over the same shards; per round every variant runs
 `steps` launches, HIP-event kernel time of the scatter launch; the output is verified after
-each variant's launches.
+each variant's launches; the wall time per launch (execute × steps + wait) beside it.
 usage: python3 profiles/r05/env_ab.py OUT.json CONFIG ROUNDS STEPS VAR=VAL[,VAR=VAL] ...
 ("-" = no switches).  AB_YDIV divides the array's y extent; AB_OUTS > 1 allocates that many
 output buffers (each held while the next is allocated, so each gets other memory) and runs
@@ -11,6 +11,7 @@ import json
 import os
 import statistics
 import sys
+import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path[:0] = [ROOT, os.path.join(ROOT, "zarr-java_amd")]
@@ -60,7 +61,7 @@ def main():
                 os.environ[k] = old
     keys = [f"out{k}:{v}" if nouts > 1 else v for k in range(nouts) for v in variants]
     res = {"config": cfg, "ydiv": ydiv, "outputs": nouts, "steps": steps, "variants": variants,
-           "kernel_ms": {key: [] for key in keys}}
+           "kernel_ms": {key: [] for key in keys}, "step_ms": {key: [] for key in keys}}
     for r in range(rounds):
         row = {}
         for k, o in enumerate(outs):
@@ -68,19 +69,24 @@ def main():
                 key = f"out{k}:{v}" if nouts > 1 else v
                 p = plans[v]
                 p.kernel_time()  # drain earlier timings
+                t0 = time.perf_counter()
                 for _ in range(steps):
                     p.execute(o)
                 p.wait()
+                t1 = time.perf_counter()
                 kt = p.kernel_time()
                 res["kernel_ms"][key].append(round(kt["scatter_ms"] / max(1, kt["launches"]), 3))
-                row[key] = res["kernel_ms"][key][-1]
+                res["step_ms"][key].append(round((t1 - t0) * 1e3 / steps, 3))
+                row[key] = [res["kernel_ms"][key][-1], res["step_ms"][key][-1]]
                 bad = int(dev.synth_verify(o, shape, [0] * n, shape, 4, bench.SEED))
                 assert bad == 0, (key, bad)
         print(json.dumps(row), flush=True)
     res["median_ms"] = {v: statistics.median(x) for v, x in res["kernel_ms"].items()}
+    res["median_step_ms"] = {v: statistics.median(x) for v, x in res["step_ms"].items()}
     with open(out_path, "w") as f:
         json.dump(res, f, indent=1)
     print(json.dumps(res["median_ms"]), flush=True)
+    print(json.dumps(res["median_step_ms"]), flush=True)
 
 
 if __name__ == "__main__":
