@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round 5: the index crc32c inside the slow kernel's launch (ZH_CRC_FUSE, default 1): the GPU
+# Round 5: the index crc32c inside the slow kernel's launch (then named ZH_CRC_FUSE, which also switches the chunk-CRC fusion c4 does not use; now ZH_IDX_CRC_FUSE): the GPU
 # suite, the small-read A/B in one process, the default bench line.  Records → gpurun_out/r05fuse.
 set -u
 R=${GRAFT_REPO_ROOT:-$(pwd)}

@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round 5: ZH_CRC_FUSE at full size, interleaved in one process (kernel window and wall time
+# Round 5: ZH_IDX_CRC_FUSE at full size, interleaved in one process (kernel window and wall time
 # per step), c4 at half y over three output placements, c3 full.  Records → gpurun_out/r05fuse2.
 set -u
 R=${GRAFT_REPO_ROOT:-$(pwd)}
@@ -16,7 +16,7 @@ step() {  # name, timeout, cmd...
 }
 cd "$R" || exit 1
 export AB_OUTS=3 AB_YDIV=2
-step ab_c4 400 python3 profiles/r05/env_ab.py "$OUT/fuse_c4.json" c4 5 10 ZH_CRC_FUSE=1 ZH_CRC_FUSE=0
+step ab_c4 400 python3 profiles/r05/env_ab.py "$OUT/fuse_c4.json" c4 5 10 ZH_IDX_CRC_FUSE=1 ZH_IDX_CRC_FUSE=0
 export AB_OUTS=1 AB_YDIV=1
-step ab_c3 300 python3 profiles/r05/env_ab.py "$OUT/fuse_c3.json" c3 5 10 ZH_CRC_FUSE=1 ZH_CRC_FUSE=0
+step ab_c3 300 python3 profiles/r05/env_ab.py "$OUT/fuse_c3.json" c3 5 10 ZH_IDX_CRC_FUSE=1 ZH_IDX_CRC_FUSE=0
 echo done >&2

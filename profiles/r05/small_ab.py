@@ -2,7 +2,7 @@
 settings of one switch read at plan creation, interleaved in one process over one c4-format
 array (y/4: the region's shard is the same 4 GiB c4 shard).  Median of `reps` one-shot reads
 per setting and round.  First use: the index crc32c on a side stream (ZH_CRC_SIDE, since
-removed); then the index crc32c inside the slow kernel's launch (ZH_CRC_FUSE=1) or on its own
+removed); then the index crc32c inside the slow kernel's launch (ZH_IDX_CRC_FUSE=1; the first run named it ZH_CRC_FUSE) or on its own
 ahead of the resolve kernel (0).
 usage: python3 profiles/r05/small_ab.py OUT.json [rounds] [reps] [VAR]"""
 import json
@@ -21,7 +21,7 @@ def main():
     out_path = sys.argv[1]
     rounds = int(sys.argv[2]) if len(sys.argv) > 2 else 5
     reps = int(sys.argv[3]) if len(sys.argv) > 3 else 200
-    var = sys.argv[4] if len(sys.argv) > 4 else "ZH_CRC_FUSE"
+    var = sys.argv[4] if len(sys.argv) > 4 else "ZH_IDX_CRC_FUSE"
     from zarrhip import _abi as A
     from zarrhip._lib import DeviceContext, lib
     dev = DeviceContext(0)

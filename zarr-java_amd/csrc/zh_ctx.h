@@ -162,7 +162,7 @@ struct zh_plan {
   uint32_t* d_crc_partials = nullptr;
   int64_t n_crc_jobs = 0, n_crc_spans = 0;
   int crc_shift = 0;            // index-CRC span = kIdxSpan << crc_shift
-  bool crc_fused = true;        // the index CRC runs in the slow kernel's launch (ZH_CRC_FUSE)
+  bool idx_crc_fused = true;    // the index CRC runs in the slow kernel's launch (ZH_IDX_CRC_FUSE)
   uint8_t* d_input = nullptr;   // staged host sources
   std::vector<std::pair<int64_t, zh::SrcRef>> h2d;  // (offset in d_input, host source)
   std::vector<int64_t> h2d_len;

@@ -1253,7 +1253,7 @@ int plan_create(zh_ctx* ctx, const zh_array_meta* m, const SrcDesc* srcs, int64_
     }
     p->n_crc_jobs = (int64_t)jobs.size();
     p->n_crc_spans = assign_crc_spans(jobs, ctx->cu_count, &p->crc_shift);
-    p->crc_fused = env_int("ZH_CRC_FUSE", 1) != 0;
+    p->idx_crc_fused = env_int("ZH_IDX_CRC_FUSE", 1) != 0;
   }
   if (!(flags & ZH_OUT_DEVICE)) {
     if ((st = plan_alloc(p, &p->d_out, (size_t)p->out_bytes, err, errlen)) != ZH_OK) {
@@ -1537,7 +1537,7 @@ int plan_enqueue_impl(zh_plan* p, void* out, hipStream_t s) {
   // kernel's launch, beside the clipped chunks' decode, instead of ahead of the resolve kernel
   const CrcIdxArgs crc{p->d_crc_jobs, p->n_crc_jobs, p->n_crc_spans, p->d_crc_partials,
                        p->d_status, p->crc_shift, 0};
-  if (!p->crc_fused)
+  if (!p->idx_crc_fused)
     ZH_HIP(launch_crc(p->d_crc_jobs, p->n_crc_jobs, p->n_crc_spans, p->crc_shift, p->d_crc_partials,
                       p->d_status, s));
   if (p->d_flat) ZH_HIP(launch_nested_index(p->nest, p->nest_grid, s));
@@ -1549,7 +1549,7 @@ int plan_enqueue_impl(zh_plan* p, void* out, hipStream_t s) {
   if (p->d_dcrc) ZH_HIP(launch_data_crc_partial(p->dcrc, p->dcrc_grid, s));
   if (p->timing) ZH_HIP(hipEventRecord(ev[1], s));
   ZH_HIP(launch_scatter(a, p->meta.dtype_size, p->tile_mode, 0, p->grid, s));
-  ZH_HIP(launch_decode_slow(a, p->slow_grid, p->crc_fused ? crc : CrcIdxArgs{}, s));
+  ZH_HIP(launch_decode_slow(a, p->slow_grid, p->idx_crc_fused ? crc : CrcIdxArgs{}, s));
   if (p->d_dcrc) ZH_HIP(launch_data_crc_finalize(p->dcrc, s));
   if (p->timing) {
     ZH_HIP(hipEventRecord(ev[2], s));
