@@ -15,6 +15,7 @@ step() {  # name, timeout, cmd...
   if [ $rc -ne 0 ]; then tail -n 60 "$OUT/$name.out" "$OUT/$name.err" >&2; exit $rc; fi
 }
 cd "$R" || exit 1
+step tests 300 python3 -u -m pytest tests/test_gpu_parity.py -m gpu -x -q --timeout 120 --timeout-method thread
 export AB_OUTS=3 AB_YDIV=2
 step ab_c4 400 python3 profiles/r05/env_ab.py "$OUT/fuse_c4.json" c4 5 10 ZH_IDX_CRC_FUSE=1 ZH_IDX_CRC_FUSE=0
 export AB_OUTS=1 AB_YDIV=1

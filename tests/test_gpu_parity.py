@@ -44,13 +44,17 @@ def test_reference_fixtures_decode_to_arange(dev):
                                       np.arange(4096).reshape(16, 16, 16)[3:12, 5:12, 1:15])
 
 
+@pytest.mark.parametrize("fuse", ["1", "0"])
 @pytest.mark.parametrize("loc,stored_crc", [("end", 0xB756D1D4), ("start", 0x56F05363)])
-def test_device_crc_on_reference_index_bytes(dev, loc, stored_crc):
+def test_device_crc_on_reference_index_bytes(dev, monkeypatch, loc, stored_crc, fuse):
     """The device index-CRC kernel on the reference fixture's own, untouched 68-byte index
     (testdata/sharding_index_location, Crc32cCodec.decode, Crc32cCodec.java:24-48).  With
     only the stored crc zeroed, the device must report Computed = the crc the reference
     stored; with the index intact the CRC passes and the read stops at the next stage (the
-    blosc-framed inner chunks are not raw `bytes`), exactly as the oracle does."""
+    blosc-framed inner chunks are not raw `bytes`), exactly as the oracle does.  Both forms
+    of the index check: inside the slow kernel's launch (ZH_IDX_CRC_FUSE=1, the default) and
+    its own launch ahead of the resolve kernel (0)."""
+    monkeypatch.setenv("ZH_IDX_CRC_FUSE", fuse)
     import os
     import struct
     from helpers import GOLDEN
@@ -75,6 +79,44 @@ def test_device_crc_on_reference_index_bytes(dev, loc, stored_crc):
     # Q12: both reject the 1040-byte framed chunk (the texts differ in detail)
     for e in (ed2.value, eo2.value):
         assert str(e).startswith("unexpected inner chunk byte length")
+
+
+@pytest.mark.parametrize("fuse", ["1", "0"])
+@pytest.mark.parametrize("loc", ["end", "start"])
+def test_index_crc_multi_span_jobs(dev, monkeypatch, loc, fuse):
+    """Index crc32c over jobs of several spans each (64 KiB indexes: 16 workgroups of 4 KiB per
+    shard, combined by the job's last workgroup), in both launch forms (ZH_IDX_CRC_FUSE):
+    intact indexes read equal to the data for an aligned region (no slow items: the fused
+    launch is CRC workgroups only) and a clipped one (CRC beside the slow list); one shard's
+    stored crc flipped fails with the oracle's message, whichever region touches it, and a
+    region that avoids that shard reads."""
+    monkeypatch.setenv("ZH_IDX_CRC_FUSE", fuse)
+    meta = A.make_meta([128, 64, 64], [64, 64, 64], 4, sharded=True, inner_chunk_shape=[4, 4, 4],
+                       index_location=A.ZH_INDEX_START if loc == "start" else A.ZH_INDEX_END)
+    data = np.arange(128 * 64 * 64, dtype=np.uint32).reshape(128, 64, 64) * np.uint32(2654435761)
+    shards = device_write(dev, meta, data)
+    assert [bytes(x) for x in shards] == [bytes(x) for x in encode_oracle(meta, data)]
+    regions = [([0, 0, 0], [128, 64, 64]), ([3, 5, 1], [67, 55, 62]), ([70, 0, 0], [10, 64, 64])]
+
+    def pick(srcs, off, shp):  # the shards a region references, in chunk-coordinate order
+        return [srcs[c[0]] for c in chunk_coords(meta, off, shp)]
+    for off, shp in regions:
+        want = data[tuple(slice(o, o + n) for o, n in zip(off, shp))]
+        np.testing.assert_array_equal(device_read(dev, meta, pick(shards, off, shp), off, shp),
+                                      want)
+    cpos = 64 * 1024 if loc == "start" else len(shards[1]) - 4
+    bad = bytearray(shards[1])
+    bad[cpos] ^= 0x5A
+    srcs = [shards[0], bytes(bad)]
+    for off, shp in regions:
+        with pytest.raises(ZhError) as ed:
+            device_read(dev, meta, pick(srcs, off, shp), off, shp)
+        with pytest.raises(O.OracleError) as eo:
+            O.array_read(meta, pick(srcs, off, shp), off, shp)
+        assert str(ed.value) == str(eo.value)
+        assert str(ed.value).startswith("The checksum of the sharding index is invalid. Stored: ")
+    np.testing.assert_array_equal(device_read(dev, meta, srcs[:1], [0, 0, 0], [64, 64, 64]),
+                                  data[:64])
 
 
 @pytest.mark.parametrize("loc,stored_crc", [("end", 0xB756D1D4), ("start", 0x56F05363)])
