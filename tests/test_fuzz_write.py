@@ -137,14 +137,17 @@ def test_device_write_matches_oracle_bytes(dev, seed):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("small_one", ["0", "1"])
 @pytest.mark.parametrize("pipelined", [False, True])
 @pytest.mark.parametrize("seed", CASES)
 def test_device_read_random_regions_match_oracle(dev, three_ctxs, tmp_path, monkeypatch, seed,
-                                                 pipelined):
+                                                 pipelined, small_one):
     """The same random chains read back: three random regions per case (any offset and
     extent inside the array), from memory and from the chunk files through the library's own
     store reads, against the oracle's read of the same stored chunks.  pipelined: thresholds
-    shrunk so that the reads run in slabs through the page-locked rings (test_gpu_files)."""
+    shrunk so that the reads run in slabs through the page-locked rings (test_gpu_files).
+    small_one: plans of at most 64 inner chunks in one launch (the library's default, conftest)."""
+    monkeypatch.setenv("ZH_SMALL_ONE", small_one)
     if pipelined:
         for k, v in (("ZH_PIPE_MIN_KB", "1"), ("ZH_PIPE_SLAB_KB", "4"),
                      ("ZH_PIPE_CHUNK_KB", "64"), ("ZH_PIPE_THREADS", "3")):

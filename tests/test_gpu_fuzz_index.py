@@ -160,11 +160,13 @@ def _region(rng, shape):
     return off, [int(rng.integers(1, s - o + 1)) for s, o in zip(shape, off)]
 
 
+@pytest.mark.parametrize("small_one", ["0", "1"])
 @pytest.mark.parametrize("pipelined", [False, True])
 @pytest.mark.parametrize("form", ["memory", "files", "pieces", "multi"])
 @pytest.mark.parametrize("chain", list(FUZZ_CHAINS))
 def test_corrupt_index_entries_match_oracle(dev, three_ctxs, tmp_path, monkeypatch, chain, form,
-                                            pipelined):
+                                            pipelined, small_one):
+    monkeypatch.setenv("ZH_SMALL_ONE", small_one)  # small plans in one launch (conftest)
     if pipelined:  # the reads in slabs through the page-locked rings (test_gpu_files' mode)
         for k, v in (("ZH_PIPE_MIN_KB", "1"), ("ZH_PIPE_SLAB_KB", "4"),
                      ("ZH_PIPE_CHUNK_KB", "64"), ("ZH_PIPE_THREADS", "3")):

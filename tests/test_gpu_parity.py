@@ -119,6 +119,26 @@ def test_index_crc_multi_span_jobs(dev, monkeypatch, loc, fuse):
                                   data[:64])
 
 
+@pytest.mark.parametrize("fuse", ["1", "0"])
+@pytest.mark.parametrize("dsize", [1, 2, 4, 8])
+def test_small_read_one_launch(dev, monkeypatch, dsize, fuse):
+    """BASELINE configs[0]'s call shape in the library's default small-plan form
+    (ZH_SMALL_ONE=1: resolve + decode of every item in one launch, the index CRC in the same
+    launch or, ZH_IDX_CRC_FUSE=0, its own): c4's chain (transpose [0,3,2,1], bytes(big), 32³
+    inner chunks) at 64³ regions of 27 inner chunks, 26 of them clipped, one aligned region,
+    a missing inner chunk (Q1: zero) and the plan size at the one-launch limit (64 chunks)."""
+    monkeypatch.setenv("ZH_SMALL_ONE", "1")
+    monkeypatch.setenv("ZH_IDX_CRC_FUSE", fuse)
+    shape = [1, 128, 128, 128]
+    meta = A.make_meta(shape, [1, 64, 128, 64], dsize, endian=A.ZH_ENDIAN_BIG, sharded=True,
+                       inner_chunk_shape=[1, 32, 32, 32], transpose_order=[0, 3, 2, 1])
+    arr = rand_array(shape, dsize, seed=31 + dsize)
+    arr[0, 32:64, 32:64, 64:96] = 0  # an all-fill inner chunk: elided, read back as 0 (Q1)
+    roundtrip(dev, meta, arr, [([0, 3, 17, 21], [1, 64, 64, 64]), ([0, 0, 0, 0], shape),
+                               ([0, 33, 1, 40], [1, 64, 64, 64]), ([0, 0, 0, 0], [1, 128, 64, 128]),
+                               ([0, 5, 5, 5], [1, 1, 1, 1])])
+
+
 @pytest.mark.parametrize("loc,stored_crc", [("end", 0xB756D1D4), ("start", 0x56F05363)])
 def test_device_chunk_crc_on_reference_bytes(dev, loc, stored_crc):
     """The inner-chunk crc32c path (Crc32cCodec.encode/decode, Crc32cCodec.java:24-60, run as

@@ -163,6 +163,8 @@ struct zh_plan {
   int64_t n_crc_jobs = 0, n_crc_spans = 0;
   int crc_shift = 0;            // index-CRC span = kIdxSpan << crc_shift
   bool idx_crc_fused = true;    // the index CRC runs in the slow kernel's launch (ZH_IDX_CRC_FUSE)
+  bool small_one = false;       // resolve + decode in one launch (ZH_SMALL_ONE, small plans)
+  int small_grid = 0;
   uint8_t* d_input = nullptr;   // staged host sources
   std::vector<std::pair<int64_t, zh::SrcRef>> h2d;  // (offset in d_input, host source)
   std::vector<int64_t> h2d_len;

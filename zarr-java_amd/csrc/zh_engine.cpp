@@ -1491,6 +1491,14 @@ int plan_create(zh_ctx* ctx, const zh_array_meta* m, const SrcDesc* srcs, int64_
       }
     }
   }
+  // small plans (at most kSmallOneItems inner chunks, no chunk crc32c, no nested index): the
+  // resolve and the decode of every item in one launch beside the index CRC
+  // (decode_small_kernel): a 64³ region of a c4 shard took four dependent launches
+  if (env_int("ZH_SMALL_ONE", 1) != 0 && items > 0 && items <= kSmallOneItems && !p->d_flat &&
+      !p->d_dcrc && !p->args.crc_fused) {
+    p->small_one = true;
+    p->small_grid = (int)std::min<int64_t>(p->args.total_items, std::max(p->grid, 1));
+  }
   *out = p;
   return ZH_OK;
 }
@@ -1545,11 +1553,16 @@ int plan_enqueue_impl(zh_plan* p, void* out, hipStream_t s) {
   a.region = (p->flags & ZH_OUT_DEVICE) ? (uint8_t*)out : p->d_out;
   if (p->d_dcrc && p->args.crc_fused)  // the row kernel XOR-accumulates per-piece partials
     ZH_HIP(hipMemsetAsync(p->d_dcrc, 0, (size_t)p->dcrc.n_items * p->dcrc.nspan * 4, s));
-  ZH_HIP(launch_resolve(a, s));
-  if (p->d_dcrc) ZH_HIP(launch_data_crc_partial(p->dcrc, p->dcrc_grid, s));
-  if (p->timing) ZH_HIP(hipEventRecord(ev[1], s));
-  ZH_HIP(launch_scatter(a, p->meta.dtype_size, p->tile_mode, 0, p->grid, s));
-  ZH_HIP(launch_decode_slow(a, p->slow_grid, p->idx_crc_fused ? crc : CrcIdxArgs{}, s));
+  if (p->small_one) {
+    if (p->timing) ZH_HIP(hipEventRecord(ev[1], s));
+    ZH_HIP(launch_decode_small(a, p->small_grid, p->idx_crc_fused ? crc : CrcIdxArgs{}, s));
+  } else {
+    ZH_HIP(launch_resolve(a, s));
+    if (p->d_dcrc) ZH_HIP(launch_data_crc_partial(p->dcrc, p->dcrc_grid, s));
+    if (p->timing) ZH_HIP(hipEventRecord(ev[1], s));
+    ZH_HIP(launch_scatter(a, p->meta.dtype_size, p->tile_mode, 0, p->grid, s));
+    ZH_HIP(launch_decode_slow(a, p->slow_grid, p->idx_crc_fused ? crc : CrcIdxArgs{}, s));
+  }
   if (p->d_dcrc) ZH_HIP(launch_data_crc_finalize(p->dcrc, s));
   if (p->timing) {
     ZH_HIP(hipEventRecord(ev[2], s));

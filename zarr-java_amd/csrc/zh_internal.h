@@ -260,6 +260,7 @@ struct CrcIdxArgs {
   int32_t pad;
 };
 constexpr int kCrcLdsWords = 12 * 256 + kBlock + 1;  // tables, wave reduction, last flag
+constexpr int64_t kSmallOneItems = 64;  // plans of at most this many inner chunks: one launch
 
 int env_int(const char* name, int def);  // zh_engine.cpp: an integer switch from the environment
 
@@ -287,6 +288,9 @@ hipError_t launch_scatter(const ScatterArgs& a, int dsize, int tile_mode, int en
 // crc.nspans workgroups) instead of launch_crc ahead of the resolve kernel
 hipError_t launch_decode_slow(const ScatterArgs& a, int grid, const CrcIdxArgs& crc,
                               hipStream_t stream);
+// small plans: resolve + decode of every item in one launch (with the index CRC as above)
+hipError_t launch_decode_small(const ScatterArgs& a, int grid, const CrcIdxArgs& crc,
+                               hipStream_t stream);
 hipError_t launch_flags(const ScatterArgs& a, int dsize, int grid, hipStream_t stream);
 // write path, one pass: payload offsets + encode-view descriptors + slow list, the fast
 // kernels with the all-fill test, the slow list through the generic encode, then the finish

@@ -2277,6 +2277,44 @@ __global__ __launch_bounds__(kBlock) void decode_slow_kernel(ScatterArgs a, CrcI
   }
 }
 
+// decode, small plans in one launch (zh_plan::small_one): the index crc32c workgroups first
+// (c.nspans, as in the slow kernel), then one workgroup per item piece resolves its item's
+// index entry (resolve_one, the resolve kernel's per-item body, on one lane; its status writes
+// are idempotent across an item's pieces) and moves it through the generic paths the slow
+// kernel uses.  A 64³ region of a c4 shard (27 inner chunks, 26 clipped) took four dependent
+// launches: the index CRC, resolve, the fast kernel for its one whole chunk, the slow list.
+template <int DS, bool TILE>
+__global__ __launch_bounds__(kBlock) void decode_small_kernel(ScatterArgs a, CrcIdxArgs c) {
+  using T = typename ElemT<DS>::T;
+  constexpr int kTileWords = ((TILE ? kTileTPB : 1) * 32 * 33 * DS + 7) / 8 * 2;
+  __shared__ uint64_t sm[(kTileWords > kCrcLdsWords ? kTileWords : kCrcLdsWords) / 2 + 1];
+  __shared__ ItemDesc sd;
+  if (blockIdx.x < c.nspans) {  // uniform per workgroup
+    crc_index_block(c, blockIdx.x, reinterpret_cast<uint32_t*>(sm));
+    return;
+  }
+  T (*tile)[32][33] = reinterpret_cast<T (*)[32][33]>(sm);
+  const int64_t total = a.total_items;
+  const uint32_t pmask = (1u << a.piece_shift) - 1;
+  const int64_t nb = (int64_t)gridDim.x - c.nspans;
+  for (int64_t k = (int64_t)blockIdx.x - c.nspans; k < total; k += nb) {
+    const int64_t citem = k >> a.piece_shift;
+    if (threadIdx.x == 0) sd = resolve_one(a, citem);
+    __syncthreads();
+    const ItemDesc D = sd;
+    __syncthreads();
+    const uint32_t mode = D.kind & kDescModeMask;
+    if (mode == kDescSkip) continue;  // uniform
+    Item it;
+    if (mode == kDescClip) {
+      make_item<false>(a, k, it, &D);
+    } else {
+      full_item(a, D, (uint32_t)k & pmask, it);
+    }
+    generic_item<DS, TILE>(a, it, tile);
+  }
+}
+
 // encode one (piece of an) item through the generic paths: source = region, destination =
 // shard payload, boundary padding written as fill_value.  FLAG (row paths): returns this
 // thread's share of the all-fill test from the same loads.
@@ -3283,6 +3321,28 @@ static void launch_slow_ds(const ScatterArgs& a, int grid, const CrcIdxArgs& c, 
     hipLaunchKernelGGL((decode_slow_kernel<DS, true>), dim3(grid), dim3(kBlock), 0, s, a, c);
   else
     hipLaunchKernelGGL((decode_slow_kernel<DS, false>), dim3(grid), dim3(kBlock), 0, s, a, c);
+}
+
+template <int DS>
+static void launch_small_ds(const ScatterArgs& a, int grid, const CrcIdxArgs& c, hipStream_t s) {
+  if (a.tile)
+    hipLaunchKernelGGL((decode_small_kernel<DS, true>), dim3(grid), dim3(kBlock), 0, s, a, c);
+  else
+    hipLaunchKernelGGL((decode_small_kernel<DS, false>), dim3(grid), dim3(kBlock), 0, s, a, c);
+}
+
+hipError_t launch_decode_small(const ScatterArgs& a, int grid, const CrcIdxArgs& crc,
+                               hipStream_t stream) {
+  const CrcIdxArgs c = crc.njobs > 0 ? crc : CrcIdxArgs{};
+  grid = std::max(grid, 1) + (int)c.nspans;
+  switch (a.dsize) {
+    case 1: launch_small_ds<1>(a, grid, c, stream); break;
+    case 2: launch_small_ds<2>(a, grid, c, stream); break;
+    case 4: launch_small_ds<4>(a, grid, c, stream); break;
+    case 8: launch_small_ds<8>(a, grid, c, stream); break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
 }
 
 hipError_t launch_decode_slow(const ScatterArgs& a, int grid, const CrcIdxArgs& crc,
