@@ -48,7 +48,8 @@ def main(src, config, out):
             is_encode_flags(flags_arg(n))
 
     def decode(n):  # every decode kernel of one step: fast rows/tiles + the generic list
-        return any(k in n for k in FAST + ("decode_slow_kernel",)) and not encode_view(n)
+        return any(k in n for k in FAST + ("decode_slow_kernel", "decode_small_kernel")) and \
+            not encode_view(n)
 
     def fast(n):
         return any(k in n for k in FAST) and not encode_view(n)

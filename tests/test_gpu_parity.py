@@ -137,6 +137,20 @@ def test_small_read_one_launch(dev, monkeypatch, dsize, fuse):
     roundtrip(dev, meta, arr, [([0, 3, 17, 21], [1, 64, 64, 64]), ([0, 0, 0, 0], shape),
                                ([0, 33, 1, 40], [1, 64, 64, 64]), ([0, 0, 0, 0], [1, 128, 64, 128]),
                                ([0, 5, 5, 5], [1, 1, 1, 1])])
+    assert lib().zh_debug_last_fast_path(0) == -1  # the one-launch kernel ran
+
+
+def test_small_one_byte_bound(dev, monkeypatch):
+    """Few but large chunks stay on the fast kernels (kSmallOneBytes = 16 MiB): 3 unsharded
+    chunks of 8 MiB take the row kernel, 2 of them (16 MiB) the one launch."""
+    monkeypatch.setenv("ZH_SMALL_ONE", "1")
+    shape = [3, 1024, 2048]
+    meta = A.make_meta(shape, [1, 1024, 2048], 4, endian=A.ZH_ENDIAN_BIG)
+    arr = rand_array(shape, 4, seed=5)
+    roundtrip(dev, meta, arr, [([0, 0, 0], shape)])
+    assert lib().zh_debug_last_fast_path(0) != -1
+    roundtrip(dev, meta, arr, [([1, 0, 0], [2, 1024, 2048])])
+    assert lib().zh_debug_last_fast_path(0) == -1
 
 
 @pytest.mark.parametrize("loc,stored_crc", [("end", 0xB756D1D4), ("start", 0x56F05363)])

@@ -1491,11 +1491,14 @@ int plan_create(zh_ctx* ctx, const zh_array_meta* m, const SrcDesc* srcs, int64_
       }
     }
   }
-  // small plans (at most kSmallOneItems inner chunks, no chunk crc32c, no nested index): the
-  // resolve and the decode of every item in one launch beside the index CRC
-  // (decode_small_kernel): a 64³ region of a c4 shard took four dependent launches
-  if (env_int("ZH_SMALL_ONE", 1) != 0 && items > 0 && items <= kSmallOneItems && !p->d_flat &&
-      !p->d_dcrc && !p->args.crc_fused) {
+  // small plans (at most kSmallOneItems inner chunks of at most kSmallOneBytes together, no
+  // chunk crc32c, no nested index): the resolve and the decode of every item in one launch
+  // beside the index CRC (decode_small_kernel): a 64³ region of a c4 shard took four dependent
+  // launches.  The byte bound keeps few large chunks (c2: 24 chunks of 4 GiB) on the fast
+  // kernels.
+  if (env_int("ZH_SMALL_ONE", 1) != 0 && items > 0 && items <= kSmallOneItems &&
+      items * p->args.inner_nbytes <= kSmallOneBytes && !p->d_flat && !p->d_dcrc &&
+      !p->args.crc_fused) {
     p->small_one = true;
     p->small_grid = (int)std::min<int64_t>(p->args.total_items, std::max(p->grid, 1));
   }

@@ -3333,6 +3333,7 @@ static void launch_small_ds(const ScatterArgs& a, int grid, const CrcIdxArgs& c,
 
 hipError_t launch_decode_small(const ScatterArgs& a, int grid, const CrcIdxArgs& crc,
                                hipStream_t stream) {
+  g_last_fast_path.store(-1);  // zh_debug_last_fast_path: the one-launch small decode
   const CrcIdxArgs c = crc.njobs > 0 ? crc : CrcIdxArgs{};
   grid = std::max(grid, 1) + (int)c.nspans;
   switch (a.dsize) {
