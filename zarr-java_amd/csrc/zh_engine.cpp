@@ -294,6 +294,7 @@ void zh_ctx_destroy(zh_ctx* c) {
   if (c->status_pin) (void)hipHostFree(c->status_pin);
   if (c->upload_pin) (void)hipHostFree(c->upload_pin);
   if (c->file_pin) (void)hipHostFree(c->file_pin);
+  if (c->hout_pin) (void)hipHostFree(c->hout_pin);
   if (c->wscratch) (void)hipFree(c->wscratch);
   for (auto& kv : c->cache) (void)hipFree(kv.second);
   pipeline_release(c);
@@ -1811,6 +1812,28 @@ int zh_plan_kernel_time(zh_plan* p, double* scatter_ms, int64_t* launches, doubl
 
 namespace zh {
 
+// A small output in pageable host memory (a Java array, a fresh numpy array) lands in the
+// context's page-locked buffer as one DMA and leaves it by one memcpy after the wait, instead
+// of the runtime's staged pageable copy.  Null: write to `out` directly.
+static uint8_t* hout_stage(zh_ctx* ctx, const void* out, int64_t nbytes, uint32_t flags) {
+  if ((flags & ZH_OUT_DEVICE) || nbytes <= 0 || nbytes > kHoutPinBytes || ctx->hout_pin_failed ||
+      env_int("ZH_HOUT_PIN", 1) == 0)
+    return nullptr;
+  unsigned int hf = 0;
+  if (hipHostGetFlags(&hf, const_cast<void*>(out)) == hipSuccess) return nullptr;  // pinned
+  (void)hipGetLastError();
+  if (!ctx->hout_pin) {
+    void* q = nullptr;
+    if (hipHostMalloc(&q, (size_t)kHoutPinBytes, hipHostMallocDefault) != hipSuccess) {
+      (void)hipGetLastError();
+      ctx->hout_pin_failed = true;
+      return nullptr;
+    }
+    ctx->hout_pin = (uint8_t*)q;
+  }
+  return ctx->hout_pin;
+}
+
 int read_one_plan(zh_ctx* ctx, const zh_array_meta* meta, const SrcDesc* srcs, int64_t nsrc,
                   const int64_t* offset, const int64_t* shape, void* out, uint32_t flags,
                   void* stream, char* err, size_t errlen) {
@@ -1818,13 +1841,15 @@ int read_one_plan(zh_ctx* ctx, const zh_array_meta* meta, const SrcDesc* srcs, i
   int st = plan_create(ctx, meta, srcs, nsrc, offset, shape, flags, false, &p, err, errlen);
   if (st != ZH_OK) return st;
   g_quiet_err[0] = 0;
-  st = zh_plan_execute(p, out, stream);
+  uint8_t* stage = hout_stage(ctx, out, p->out_bytes, flags);
+  st = zh_plan_execute(p, stage ? (void*)stage : out, stream);
   if (st != ZH_OK) {
     set_err(err, errlen, "kernel launch failed%s%s", g_quiet_err[0] ? ": " : "", g_quiet_err);
     plan_free(p);
     return st;
   }
   st = zh_plan_wait(p, err, errlen);
+  if (st == ZH_OK && stage) std::memcpy(out, stage, (size_t)p->out_bytes);
   plan_free(p);
   return st;
 }

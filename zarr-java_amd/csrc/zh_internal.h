@@ -262,6 +262,7 @@ struct CrcIdxArgs {
 constexpr int kCrcLdsWords = 12 * 256 + kBlock + 1;  // tables, wave reduction, last flag
 constexpr int64_t kSmallOneItems = 64;  // plans of at most this many inner chunks: one launch
 constexpr int64_t kSmallOneBytes = 16ll << 20;  // ... of at most this many payload bytes
+constexpr int64_t kHoutPinBytes = 4ll << 20;  // one-plan reads into pageable memory up to this: staged
 
 int env_int(const char* name, int def);  // zh_engine.cpp: an integer switch from the environment
 
