@@ -16,6 +16,13 @@ from zarrhip._lib import lib
 
 pytestmark = pytest.mark.gpu
 
+
+@pytest.fixture(autouse=True)
+def _multi_launch(monkeypatch):
+    """These tests assert which fast kernel ran (zh_debug_last_fast_path): keep small plans on
+    the multi-launch kernels whatever the environment says (ZH_SMALL_ONE, conftest)."""
+    monkeypatch.setenv("ZH_SMALL_ONE", "0")
+
 SHAPE = [1, 32, 64, 1536]
 CHUNK = [1, 16, 32, 1024]
 

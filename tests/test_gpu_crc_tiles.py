@@ -13,6 +13,13 @@ from zarrhip._lib import ZhError, lib
 
 pytestmark = pytest.mark.gpu
 
+
+@pytest.fixture(autouse=True)
+def _multi_launch(monkeypatch):
+    """These tests assert which fast kernel ran (zh_debug_last_fast_path): keep small plans on
+    the multi-launch kernels whatever the environment says (ZH_SMALL_ONE, conftest)."""
+    monkeypatch.setenv("ZH_SMALL_ONE", "0")
+
 SHAPE = [64, 64, 96]
 CHUNK = 32 * 32 * 32 * 4 + 4  # stored inner chunk: payload + crc32c
 
