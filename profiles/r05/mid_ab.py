@@ -1,0 +1,73 @@
+"""Round 5 lab: mid-size reads into pageable host memory (a Java array's case between the
+small-output landing buffer, <= 4 MiB, and the pipelined host read, >= ZH_PIPE_MIN_KB = 64 MiB
+by default): one c4-format shard on the device, regions of 8-48 MiB, settings of
+ZH_PIPE_MIN_KB interleaved in one process; median wall time of `reps` one-shot reads each.
+usage: python3 profiles/r05/mid_ab.py OUT.json [rounds] [reps]"""
+import ctypes as C
+import json
+import os
+import statistics
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "zarr-java_amd")]
+import bench  # noqa: E402
+
+
+def main():
+    out_path = sys.argv[1]
+    rounds = int(sys.argv[2]) if len(sys.argv) > 2 else 3
+    reps = int(sys.argv[3]) if len(sys.argv) > 3 else 20
+    from zarrhip import _abi as A
+    from zarrhip._lib import DeviceContext, lib
+    dev = DeviceContext(0)
+    meta = bench.build_meta(A, "c4", 4)  # y/4: the region's shard is one 4 GiB c4 shard
+    L = lib()
+    shape = [meta.shape[d] for d in range(meta.ndim)]
+    coords = bench.all_coords(L, meta)
+    caps = bench.chunk_capacities(meta, coords)
+    offs, tot = bench.slab_layout(caps)
+    nel = 1
+    for s in shape:
+        nel *= s
+    region = dev.malloc(nel * 4)
+    slab = dev.malloc(tot)
+    dev.synth_fill(region, nel, 4, 0, bench.SEED)
+    sizes = dev.array_write(meta, region, [0] * len(shape), shape,
+                            [(slab + o, c) for o, c in zip(offs, caps)])
+    sources = [(slab + o, s) for o, s in zip(offs, sizes)]
+    pos = {c: i for i, c in enumerate(coords)}
+    src = [sources[pos[(0, 0, 0, 0)]]]
+    shapes = {"8MiB": [1, 64, 128, 256], "16MiB": [1, 128, 128, 256], "32MiB": [1, 128, 256, 256],
+              "48MiB": [1, 192, 256, 256]}
+    settings = ["65536", "16384", "4096"]
+    host = (C.c_char * (48 << 20))()
+    dout = dev.malloc(48 << 20)
+    res = {"reps": reps, "settings": settings, "rounds": []}
+    for r in range(rounds):
+        row = {}
+        for name, shp in shapes.items():
+            nb = 4 * shp[1] * shp[2] * shp[3]
+            off = [0, 1, 3, 5]
+            for st in settings:
+                os.environ["ZH_PIPE_MIN_KB"] = st
+                ts = []
+                for i in range(reps + 3):
+                    t0 = time.perf_counter()
+                    dev.array_read(meta, src, off, shp, C.addressof(host), A.ZH_SRC_DEVICE)
+                    if i >= 3:
+                        ts.append(time.perf_counter() - t0)
+                ms = statistics.median(ts) * 1e3
+                row[f"{name}:min_kb={st}"] = [round(ms, 3), round(nb / 2**30 / (ms / 1e3), 2)]
+                dev.memcpy(dout, C.addressof(host), nb, 0, None, True)
+                bad = int(dev.synth_verify(dout, shape, off, shp, 4, bench.SEED))
+                assert bad == 0, (name, st, bad)
+        res["rounds"].append(row)
+        print(json.dumps(row), flush=True)
+    with open(out_path, "w") as f:
+        json.dump(res, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()
