@@ -2,6 +2,7 @@
 small-output landing buffer, <= 4 MiB, and the pipelined host read, >= ZH_PIPE_MIN_KB = 64 MiB
 by default): one c4-format shard on the device, regions of 8-48 MiB, settings of
 ZH_PIPE_MIN_KB interleaved in one process; median wall time of `reps` one-shot reads each.
+MID_BIG=1: regions of 64-512 MiB, the pipelined read (64 MiB) against one plan (1 GiB).
 usage: python3 profiles/r05/mid_ab.py OUT.json [rounds] [reps]"""
 import ctypes as C
 import json
@@ -39,11 +40,17 @@ def main():
     sources = [(slab + o, s) for o, s in zip(offs, sizes)]
     pos = {c: i for i, c in enumerate(coords)}
     src = [sources[pos[(0, 0, 0, 0)]]]
+    big = os.environ.get("MID_BIG") == "1"  # 64-512 MiB: pipelined (64 MiB) vs one plan
     shapes = {"8MiB": [1, 64, 128, 256], "16MiB": [1, 128, 128, 256], "32MiB": [1, 128, 256, 256],
               "48MiB": [1, 192, 256, 256]}
     settings = ["65536", "16384", "4096"]
-    host = (C.c_char * (48 << 20))()
-    dout = dev.malloc(48 << 20)
+    if big:
+        shapes = {"64MiB": [1, 256, 256, 256], "128MiB": [1, 256, 512, 256],
+                  "256MiB": [1, 512, 512, 256], "512MiB": [1, 512, 512, 512]}
+        settings = ["65536", "1048576"]
+    cap = max(4 * s[1] * s[2] * s[3] for s in shapes.values())
+    host = (C.c_char * cap)()
+    dout = dev.malloc(cap)
     res = {"reps": reps, "settings": settings, "rounds": []}
     for r in range(rounds):
         row = {}
