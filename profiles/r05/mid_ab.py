@@ -2,7 +2,9 @@
 small-output landing buffer, <= 4 MiB, and the pipelined host read, >= ZH_PIPE_MIN_KB = 64 MiB
 by default): one c4-format shard on the device, regions of 8-48 MiB, settings of
 ZH_PIPE_MIN_KB interleaved in one process; median wall time of `reps` one-shot reads each.
-MID_BIG=1: regions of 64-512 MiB, the pipelined read (64 MiB) against one plan (1 GiB).
+MID_BIG=1: regions of 64-512 MiB, the pipelined read (64 MiB) against one plan (1 GiB);
+MID_HUGE=1: 1 and 2 GiB against 4 GiB; MID_VAR: the switch (ZH_PIPE_DOUT_MIN_KB since it
+exists: device sources with a host output).
 usage: python3 profiles/r05/mid_ab.py OUT.json [rounds] [reps]"""
 import ctypes as C
 import json
@@ -44,10 +46,14 @@ def main():
     shapes = {"8MiB": [1, 64, 128, 256], "16MiB": [1, 128, 128, 256], "32MiB": [1, 128, 256, 256],
               "48MiB": [1, 192, 256, 256]}
     settings = ["65536", "16384", "4096"]
+    var = os.environ.get("MID_VAR", "ZH_PIPE_MIN_KB")
     if big:
         shapes = {"64MiB": [1, 256, 256, 256], "128MiB": [1, 256, 512, 256],
                   "256MiB": [1, 512, 512, 256], "512MiB": [1, 512, 512, 512]}
         settings = ["65536", "1048576"]
+    if os.environ.get("MID_HUGE") == "1":  # 1-2 GiB: pipelined (64 MiB) vs one plan (4 GiB)
+        shapes = {"1GiB": [1, 512, 1024, 512], "2GiB": [1, 1024, 1024, 512]}
+        settings = ["65536", "4194304"]
     cap = max(4 * s[1] * s[2] * s[3] for s in shapes.values())
     host = (C.c_char * cap)()
     dout = dev.malloc(cap)
@@ -58,7 +64,7 @@ def main():
             nb = 4 * shp[1] * shp[2] * shp[3]
             off = [0, 1, 3, 5]
             for st in settings:
-                os.environ["ZH_PIPE_MIN_KB"] = st
+                os.environ[var] = st
                 ts = []
                 for i in range(reps + 3):
                     t0 = time.perf_counter()

@@ -44,6 +44,7 @@ namespace {
 
 struct PipeCfg {
   int64_t min_bytes;   // host bytes (sources + output) below which one plan is used
+  int64_t dout_min_bytes;  // the same for device sources and a host output
   int64_t slab_bytes;  // output (or input) bytes per slab
   int64_t chunk;       // bytes per ring slot / DMA window
   int threads;         // memcpy lanes per direction
@@ -52,7 +53,12 @@ struct PipeCfg {
 
 PipeCfg pipe_cfg() {
   PipeCfg c;
-  c.min_bytes = (int64_t)std::max(0, env_int("ZH_PIPE_MIN_KB", 64 << 10)) << 10;
+  const int min_kb = std::max(0, env_int("ZH_PIPE_MIN_KB", 64 << 10));
+  c.min_bytes = (int64_t)min_kb << 10;
+  // device sources, host output: only the D2H has anything to overlap with, and one plan (its
+  // D2H a DMA into pinned memory or the runtime's pageable copy, ~49 GiB/s) measured faster up
+  // to 512 MiB (46.6 vs 30.7 GiB/s at 64 MiB, 49.1 vs 43.9 at 512 MiB, profiles/r05/mid/)
+  c.dout_min_bytes = (int64_t)std::max(0, env_int("ZH_PIPE_DOUT_MIN_KB", min_kb * 16)) << 10;
   c.slab_bytes = (int64_t)std::max(4, env_int("ZH_PIPE_SLAB_KB", 128 << 10)) << 10;
   c.chunk = (int64_t)std::max(64, env_int("ZH_PIPE_CHUNK_KB", 16 << 10)) << 10;
   c.threads = std::min(16, std::max(1, env_int("ZH_PIPE_THREADS", 6)));
@@ -233,7 +239,7 @@ int read_pipelined(zh_ctx* ctx, const zh_array_meta* meta, const SrcDesc* srcs, 
     }
   const PipeCfg cfg = pipe_cfg();
   const int64_t host_bytes = (host_out ? obytes : 0) + ibytes;
-  if (host_bytes < cfg.min_bytes) return ZH_EUNSUPPORTED;
+  if (host_bytes < (host_in ? cfg.min_bytes : cfg.dout_min_bytes)) return ZH_EUNSUPPORTED;
   {
     int64_t cs[kMaxDims], cc[kMaxDims];  // the caller's list must match the whole region
     if (chunk_coords(n, meta->chunk_shape, offset, shape, cs, cc) != nsrc || !srcs)
