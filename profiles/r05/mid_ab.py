@@ -51,7 +51,8 @@ def main():
         shapes = {"64MiB": [1, 256, 256, 256], "128MiB": [1, 256, 512, 256],
                   "256MiB": [1, 512, 512, 256], "512MiB": [1, 512, 512, 512]}
         settings = ["65536", "1048576"]
-    if os.environ.get("MID_HUGE") == "1":  # 1-2 GiB: pipelined (64 MiB) vs one plan (4 GiB)
+    huge = os.environ.get("MID_HUGE") == "1"
+    if huge:  # 1-2 GiB: pipelined (64 MiB) vs one plan (4 GiB)
         shapes = {"1GiB": [1, 512, 1024, 512], "2GiB": [1, 1024, 1024, 512]}
         settings = ["65536", "4194304"]
     cap = max(4 * s[1] * s[2] * s[3] for s in shapes.values())
@@ -62,7 +63,7 @@ def main():
         row = {}
         for name, shp in shapes.items():
             nb = 4 * shp[1] * shp[2] * shp[3]
-            off = [0, 1, 3, 5]
+            off = [0, 0, 0, 0] if huge else [0, 1, 3, 5]  # inside the first shard
             for st in settings:
                 os.environ[var] = st
                 ts = []
