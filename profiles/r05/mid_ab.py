@@ -3,7 +3,7 @@ small-output landing buffer, <= 4 MiB, and the pipelined host read, >= ZH_PIPE_M
 by default): one c4-format shard on the device, regions of 8-48 MiB, settings of
 ZH_PIPE_MIN_KB interleaved in one process; median wall time of `reps` one-shot reads each.
 MID_BIG=1: regions of 64-512 MiB, the pipelined read (64 MiB) against one plan (1 GiB);
-MID_HUGE=1: 1 and 2 GiB against 4 GiB; MID_VAR: the switch (ZH_PIPE_DOUT_MIN_KB since it
+MID_HUGE=1: 1 and 2 GiB against 4 GiB; MID_SMALL=1: 0.5-4 MiB with ZH_HOUT_PIN 1 / 0; MID_VAR: the switch (ZH_PIPE_DOUT_MIN_KB since it
 exists: device sources with a host output).
 usage: python3 profiles/r05/mid_ab.py OUT.json [rounds] [reps]"""
 import ctypes as C
@@ -51,6 +51,11 @@ def main():
         shapes = {"64MiB": [1, 256, 256, 256], "128MiB": [1, 256, 512, 256],
                   "256MiB": [1, 512, 512, 256], "512MiB": [1, 512, 512, 512]}
         settings = ["65536", "1048576"]
+    if os.environ.get("MID_SMALL") == "1":  # 0.5-4 MiB: the pinned landing buffer on / off
+        shapes = {"512KiB": [1, 32, 64, 64], "1MiB": [1, 64, 64, 64], "2MiB": [1, 64, 64, 128],
+                  "4MiB": [1, 64, 128, 128]}
+        settings = ["1", "0"]
+        var = "ZH_HOUT_PIN"
     huge = os.environ.get("MID_HUGE") == "1"
     if huge:  # 1-2 GiB: pipelined (64 MiB) vs one plan (4 GiB)
         shapes = {"1GiB": [1, 512, 1024, 512], "2GiB": [1, 1024, 1024, 512]}
