@@ -262,7 +262,9 @@ struct CrcIdxArgs {
 constexpr int kCrcLdsWords = 12 * 256 + kBlock + 1;  // tables, wave reduction, last flag
 constexpr int64_t kSmallOneItems = 64;  // plans of at most this many inner chunks: one launch
 constexpr int64_t kSmallOneBytes = 16ll << 20;  // ... of at most this many payload bytes
-constexpr int64_t kHoutPinBytes = 4ll << 20;  // one-plan reads into pageable memory up to this: staged
+// one-plan reads into pageable memory up to this: staged (above it the runtime's own pageable
+// copy is faster: 2 MiB 0.10 vs 0.17 ms, 4 MiB 0.15 vs 0.29 ms, profiles/r05/hout/small_hout.json)
+constexpr int64_t kHoutPinBytes = 1ll << 20;
 
 int env_int(const char* name, int def);  // zh_engine.cpp: an integer switch from the environment
 
