@@ -54,7 +54,7 @@ def main():
     if os.environ.get("MID_SMALL") == "1":  # 0.5-4 MiB: the pinned landing buffer on / off
         shapes = {"512KiB": [1, 32, 64, 64], "1MiB": [1, 64, 64, 64], "2MiB": [1, 64, 64, 128],
                   "4MiB": [1, 64, 128, 128]}
-        settings = ["1", "0", "2"]  # 2: page-lock the caller's pages (lab form)
+        settings = ["1", "0"]  # (a third form, 2, page-locked the caller's pages; removed)
         var = "ZH_HOUT_PIN"
     huge = os.environ.get("MID_HUGE") == "1"
     if huge:  # 1-2 GiB: pipelined (64 MiB) vs one plan (4 GiB)

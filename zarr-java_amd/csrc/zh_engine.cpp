@@ -1842,23 +1842,14 @@ int read_one_plan(zh_ctx* ctx, const zh_array_meta* meta, const SrcDesc* srcs, i
   if (st != ZH_OK) return st;
   g_quiet_err[0] = 0;
   uint8_t* stage = hout_stage(ctx, out, p->out_bytes, flags);
-  // lab form (ZH_HOUT_PIN=2): page-lock the caller's pages for the one DMA instead
-  bool registered = false;
-  if (stage && env_int("ZH_HOUT_PIN", 1) == 2) {
-    registered = hipHostRegister(out, (size_t)p->out_bytes, hipHostRegisterDefault) == hipSuccess;
-    if (!registered) (void)hipGetLastError();
-    if (registered) stage = nullptr;
-  }
   st = zh_plan_execute(p, stage ? (void*)stage : out, stream);
   if (st != ZH_OK) {
     set_err(err, errlen, "kernel launch failed%s%s", g_quiet_err[0] ? ": " : "", g_quiet_err);
-    if (registered) (void)hipHostUnregister(out);
     plan_free(p);
     return st;
   }
   st = zh_plan_wait(p, err, errlen);
   if (st == ZH_OK && stage) std::memcpy(out, stage, (size_t)p->out_bytes);
-  if (registered) (void)hipHostUnregister(out);
   plan_free(p);
   return st;
 }
