@@ -185,6 +185,16 @@ int zh_plan_create(zh_ctx* ctx, const zh_array_meta* meta, const zh_chunk_src* c
                    zh_plan** out, char* err, size_t errlen);
 int zh_plan_execute(zh_plan* plan, void* out, void* stream);
 int zh_plan_wait(zh_plan* plan, char* err, size_t errlen);
+/* Where the data error (ZH_EDATA) that the last read call on this thread reported sits in the
+ * reference's sequential order: the failing chunk's grid coordinates (ndim
+ * values into coords[0..cap)) and *key, its place inside that chunk (larger = earlier: the
+ * index crc32c is ~0, else the failing inner chunk's C-order rank, complemented).  Returns
+ * ndim, or 0 when that call placed no data error; the position is cleared once reported.
+ * Multi-rank callers order the ranks' errors
+ * by (coords, -key) so every rank reports the one a sequential read would have
+ * (zarrhip.parallel.pick_error; the reference throws from its parallel chunk loop,
+ * M/core/Array.java:403-407, 436-438). */
+int zh_last_data_error(int64_t* coords, int cap, uint64_t* key);
 void zh_plan_destroy(zh_plan* plan);
 /* Plan statistics: bytes of encoded input read, output bytes written, number of
  * inner-chunk work items, shards touched. */
@@ -524,6 +534,13 @@ int zh_device_scatter_view(zh_ctx* ctx, void* ptr, uint64_t order, void** out);
  * the buffer. */
 int zh_device_write_rate(zh_ctx* ctx, void* ptr, size_t bytes, int pattern, int reps,
                          double* gbps);
+/* Copy ceiling of a buffer pair: one untimed and `reps` timed launches of a streaming
+ * byte-swapping copy src -> dst over the first bytes rounded down to 128 KiB (non-temporal
+ * 16-B loads and stores, 128 KiB per workgroup step: the fastest stream of
+ * tools/copy_lab.hip).  *gbps = (bytes read + bytes written) / median time, in 1e9 B/s, the
+ * decode's own traffic count.  Overwrites dst.  ZH_EINVAL below 128 KiB. */
+int zh_device_copy_rate(zh_ctx* ctx, void* dst, const void* src, size_t bytes, int reps,
+                        double* gbps);
 int zh_device_free(zh_ctx* ctx, void* ptr);
 int zh_host_malloc_pinned(zh_ctx* ctx, size_t bytes, void** out);
 int zh_host_free_pinned(zh_ctx* ctx, void* ptr);

@@ -111,6 +111,41 @@ def test_multi_error_is_first_failing_slab(ctxs):
     with pytest.raises(ZhError) as ed:
         array_read_multi(ctxs, meta, hs, off, shp, C.addressof(out), 0)
     assert str(ed.value) == str(eo.value)
+    # zh_last_data_error: the failing shard's grid coords, the index crc32c's key (~0)
+    last = chunk_coords(meta, off, shp)[-1]
+    assert ed.value.position == (tuple(last), 2 ** 64 - 1)
+
+
+def test_data_error_position_is_the_sequential_first(ctxs):
+    """Two corrupt shards, one plan and one multi-context read: the error raised and its
+    position (zh_last_data_error: what the multi-rank API orders ranks by) are the first
+    corrupt shard's in C order, as the oracle's sequential read reports."""
+    meta = _meta()
+    arr = rand_array(shape_of(meta), 4, seed=83)
+    shards = encode_oracle(meta, arr)
+    off, shp = [0, 0, 0, 0], [1, 96, 64, 80]
+    cc = chunk_coords(meta, off, shp)
+    srcs = _sources(meta, shards, off, shp)
+    for k in (4, 2):
+        bad = bytearray(srcs[k])
+        bad[-10] ^= 0x40
+        srcs[k] = bytes(bad)
+    with pytest.raises(O.OracleError) as eo:
+        O.array_read(meta, srcs, off, shp)
+    keep, hs = _host_srcs(srcs)
+    nb = int(np.prod(shp)) * 4
+    out = (C.c_char * nb)()
+    dev = ctxs[0]
+    with pytest.raises(ZhError) as e1:
+        dev.array_read(meta, hs, off, shp, C.addressof(out), 0)
+    with pytest.raises(ZhError) as e3:
+        array_read_multi(ctxs, meta, hs, off, shp, C.addressof(out), 0)
+    for e in (e1, e3):
+        assert str(e.value) == str(eo.value)
+        assert e.value.position == (tuple(cc[2]), 2 ** 64 - 1)
+    # reported once: a later error without a position does not inherit this one
+    from zarrhip._lib import last_data_error
+    assert last_data_error() is None
 
 
 @pytest.mark.parametrize("src_device", [False, True])

@@ -169,6 +169,42 @@ def _child(tmp, files_root, port):
     assert isinstance(out, torch.Tensor) and out.is_cuda
     np.testing.assert_array_equal(out.cpu().numpy().view(np.uint32).reshape(shp),
                                   data[tuple(slice(o, o + s) for o, s in zip(off, shp))])
+    # error parity: two shards with a corrupt index crc32c.  Every piece's
+    # plan defers its device error to wait(); RegionGather collects them all and raises the one
+    # a sequential read meets first — the oracle's text, placed by zh_last_data_error
+    corrupt = [c for c in allc if c in bufs][1:3]
+    bad_shards = list(shards)
+    cbufs = dict(bufs)
+    for c in corrupt:
+        b = bytearray(shards[pos[c]])
+        b[-2] ^= 0x77
+        bad_shards[pos[c]] = bytes(b)
+        p = dev.malloc(len(b))
+        dev.h2d(p, bytes(b))
+        cbufs[c] = (p, len(b))
+    try:
+        O.array_read(meta, [bad_shards[pos[c]] for c in allc], [0] * 4, SHAPE)
+        raise AssertionError("the oracle read a corrupt index")
+    except O.OracleError as e:
+        want_msg = str(e)
+    assert want_msg.startswith("The checksum of the sharding index is invalid.")
+    g = P.RegionGather([0] * 4, SHAPE, 4, group=group, align=8,
+                       piece_bytes=8 * SHAPE[2] * SHAPE[3] * 4, device=0)
+    bad_dec = P.PlanDecoder(dev, meta, lambda po, ps: [cbufs.get(c, (None, 0))
+                                                       for c in chunk_coords(meta, po, ps)])
+    try:
+        g.run(bad_dec)
+        raise AssertionError("RegionGather returned a region with corrupt shards")
+    except _lib.ZhError as e:
+        assert str(e) == want_msg, (str(e), want_msg)
+        assert e.position == (tuple(corrupt[0]), 2 ** 64 - 1), e.position
+    bad_dec.close()
+    dec = P.PlanDecoder(dev, meta, sources)  # the group and buffers serve the next read
+    got = g.run(dec).cpu().numpy().view(np.uint32).reshape(SHAPE)
+    np.testing.assert_array_equal(got, data)
+    dec.close()
+    for c in corrupt:
+        dev.free(cbufs[c][0])
     for p, _ in bufs.values():
         dev.free(p)
     dist.destroy_process_group()

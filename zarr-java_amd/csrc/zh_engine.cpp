@@ -2229,8 +2229,10 @@ int read_multi_impl(zh_ctx* const* ctxs, int ndev, int root, const zh_array_meta
     if (best < 0 || data_err_before(where[r].cc, where[r].key, where[best].cc, where[best].key))
       best = r;
   }
+  g_data_err = DataErrPos{};
   if (first < 0) return ZH_OK;
   const int r = placed && best >= 0 ? best : first;
+  if (r == best) g_data_err = where[r];  // zh_last_data_error on the calling thread
   set_err(err, errlen, "%s", msgs[r].c_str());
   return status[r];
 }
@@ -3316,7 +3318,9 @@ bool scatter_free(void* ptr) {
   return true;
 }
 
-int write_rate(hipStream_t s, void* ptr, size_t bytes, int pattern, int reps, double* gbps) {
+// median rate (GB/s of `bytes`) of `reps` timed launches after one untimed one
+template <typename Launch>
+int stream_rate(hipStream_t s, size_t bytes, int reps, double* gbps, Launch launch) {
   hipEvent_t e0, e1;
   if (hipEventCreate(&e0) != hipSuccess) return ZH_EHIP;
   if (hipEventCreate(&e1) != hipSuccess) {
@@ -3325,11 +3329,10 @@ int write_rate(hipStream_t s, void* ptr, size_t bytes, int pattern, int reps, do
   }
   int rc = ZH_OK;
   std::vector<float> ms;
-  if (launch_write_probe(ptr, (int64_t)bytes, pattern, s) != hipSuccess) rc = ZH_EHIP;
+  if (launch() != hipSuccess) rc = ZH_EHIP;
   for (int r = 0; rc == ZH_OK && r < reps; r++) {
     float t = 0;
-    if (hipEventRecord(e0, s) != hipSuccess ||
-        launch_write_probe(ptr, (int64_t)bytes, pattern, s) != hipSuccess ||
+    if (hipEventRecord(e0, s) != hipSuccess || launch() != hipSuccess ||
         hipEventRecord(e1, s) != hipSuccess || hipEventSynchronize(e1) != hipSuccess ||
         hipEventElapsedTime(&t, e0, e1) != hipSuccess)
       rc = ZH_EHIP;
@@ -3346,6 +3349,12 @@ int write_rate(hipStream_t s, void* ptr, size_t bytes, int pattern, int reps, do
   const double med = ms[ms.size() / 2];
   *gbps = med > 0 ? (double)bytes / (med * 1e-3) / 1e9 : 0.0;
   return ZH_OK;
+}
+
+int write_rate(hipStream_t s, void* ptr, size_t bytes, int pattern, int reps, double* gbps) {
+  return stream_rate(s, bytes, reps, gbps, [&] {
+    return launch_write_probe(ptr, (int64_t)bytes, pattern, s);
+  });
 }
 
 // ZH_MALLOC_CALIBRATE: the write rate of a large scatter arena is set by which physical chunks
@@ -3433,6 +3442,27 @@ int zh_device_write_rate(zh_ctx* ctx, void* ptr, size_t bytes, int pattern, int 
     return ZH_EINVAL;
   (void)hipSetDevice(ctx->device);
   return write_rate(ctx->stream, ptr, bytes, pattern, reps, gbps);
+}
+int zh_last_data_error(int64_t* coords, int cap, uint64_t* key) {
+  if (!g_data_err.set) return 0;
+  const int n = (int)g_data_err.cc.size();
+  for (int d = 0; coords && d < n && d < cap; d++) coords[d] = g_data_err.cc[(size_t)d];
+  if (key) *key = g_data_err.key;
+  g_data_err.set = false;  // reported once
+  return n;
+}
+int zh_device_copy_rate(zh_ctx* ctx, void* dst, const void* src, size_t bytes, int reps,
+                        double* gbps) {
+  if (!ctx || !dst || !src || !gbps || bytes < ((size_t)128 << 10) || reps <= 0)
+    return ZH_EINVAL;
+  (void)hipSetDevice(ctx->device);
+  const size_t n = bytes / ((size_t)128 << 10) * ((size_t)128 << 10);
+  double g = 0;
+  const int rc = stream_rate(ctx->stream, n, reps, &g, [&] {
+    return launch_copy_probe(dst, src, (int64_t)n, ctx->stream);
+  });
+  *gbps = 2.0 * g;  // bytes read + bytes written
+  return rc;
 }
 int zh_device_free(zh_ctx* ctx, void* ptr) {
   if (!ctx) return ZH_EINVAL;

@@ -323,6 +323,7 @@ hipError_t launch_encode_finish(const ScatterArgs& a, const EncNest& nz, int64_t
 hipError_t launch_gather_blocks(void* dst, const void* src, const int64_t* d_idx, int64_t n,
                                 int64_t bb, hipStream_t stream);
 hipError_t launch_write_probe(void* dst, int64_t bytes, int pattern, hipStream_t stream);
+hipError_t launch_copy_probe(void* dst, const void* src, int64_t bytes, hipStream_t stream);
 hipError_t launch_synth_fill(void* dst, int64_t n, int dsize, int64_t first, uint64_t seed,
                              hipStream_t stream);
 hipError_t launch_synth_verify(const void* region, int ndim, const int64_t* array_shape,

@@ -3557,6 +3557,43 @@ hipError_t launch_write_probe(void* dst, int64_t bytes, int pattern, hipStream_t
   return hipGetLastError();
 }
 
+// Copy ceiling of a (source, destination) pair (bench evidence, DESIGN §4 "Ceilings"): the
+// fastest plain stream measured in tools/copy_lab.hip — a 32-bit byte-swapping copy, each
+// workgroup owning 128 KiB spans, 4 non-temporal 16-B loads in flight per lane, then their
+// non-temporal stores.  Same bytes moved per output byte as the decode (one read, one write).
+__global__ __launch_bounds__(kBlock) void copy_probe_kernel(const uint8_t* __restrict__ src,
+                                                             uint8_t* __restrict__ dst,
+                                                             int64_t bytes) {
+  constexpr int64_t kSpan = 128 << 10, kU = 4;
+  const int64_t spans = bytes / kSpan;
+  for (int64_t sp = blockIdx.x; sp < spans; sp += gridDim.x) {
+    const uint8_t* s = src + sp * kSpan;
+    uint8_t* d = dst + sp * kSpan;
+    for (int64_t i = threadIdx.x * 16; i < kSpan; i += kBlock * 16 * kU) {
+      uint4 v[kU];
+#pragma unroll
+      for (int u = 0; u < kU; u++) v[u] = ld16s<true>(s + i + u * kBlock * 16);
+#pragma unroll
+      for (int u = 0; u < kU; u++)
+        st16s<true>(d + i + u * kBlock * 16,
+                    make_uint4(__builtin_bswap32(v[u].x), __builtin_bswap32(v[u].y),
+                               __builtin_bswap32(v[u].z), __builtin_bswap32(v[u].w)));
+    }
+  }
+}
+
+hipError_t launch_copy_probe(void* dst, const void* src, int64_t bytes, hipStream_t stream) {
+  bytes = bytes / (128 << 10) * (128 << 10);
+  if (bytes <= 0) return hipSuccess;
+  int dev = 0, cus = 256;
+  (void)hipGetDevice(&dev);
+  (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  const int grid = (int)std::min<int64_t>(bytes / (128 << 10), (int64_t)cus * 32);
+  hipLaunchKernelGGL(copy_probe_kernel, dim3(grid), dim3(kBlock), 0, stream,
+                     (const uint8_t*)src, (uint8_t*)dst, bytes);
+  return hipGetLastError();
+}
+
 hipError_t launch_synth_fill(void* dst, int64_t n, int dsize, int64_t first, uint64_t seed,
                              hipStream_t stream) {
   if (n <= 0) return hipSuccess;

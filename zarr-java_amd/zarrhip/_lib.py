@@ -47,6 +47,7 @@ _SIGS = {
                                  C.POINTER(P), CH, SZ]),
     "zh_plan_execute": (C.c_int, [P, P, P]),
     "zh_plan_wait": (C.c_int, [P, CH, SZ]),
+    "zh_last_data_error": (C.c_int, [PI64, C.c_int, C.POINTER(U64)]),
     "zh_plan_destroy": (None, [P]),
     "zh_plan_stats": (C.c_int, [P, PI64, PI64, PI64, PI64]),
     "zh_plan_set_timing": (C.c_int, [P, C.c_int]),
@@ -101,6 +102,7 @@ _SIGS = {
     "zh_device_alloc_probes": (C.c_int, [P, P, C.POINTER(C.c_double), C.c_int,
                                          C.POINTER(C.c_int)]),
     "zh_device_write_rate": (C.c_int, [P, P, SZ, C.c_int, C.c_int, C.POINTER(C.c_double)]),
+    "zh_device_copy_rate": (C.c_int, [P, P, P, SZ, C.c_int, C.POINTER(C.c_double)]),
     "zh_host_malloc_pinned": (C.c_int, [P, SZ, C.POINTER(P)]),
     "zh_host_free_pinned": (C.c_int, [P, P]),
     "zh_host_register": (C.c_int, [P, P, SZ]),
@@ -159,15 +161,27 @@ def i32arr(vals):
 
 
 class ZhError(RuntimeError):
-    def __init__(self, status, message):
+    def __init__(self, status, message, position=None):
         super().__init__(message)
         self.status = status
+        # ZH_EDATA: (chunk grid coords, key) of the failing chunk in a sequential read's order
+        # (zh_last_data_error), or None
+        self.position = position
+
+
+def last_data_error():
+    """zh_last_data_error for this thread's last read call: (coords tuple, key) or None."""
+    cc = (C.c_int64 * 32)()
+    key = C.c_uint64()
+    n = lib().zh_last_data_error(cc, 32, C.byref(key))
+    return (tuple(cc[i] for i in range(n)), key.value) if n > 0 else None
 
 
 def check(status, err=None):
     if status != A.ZH_OK:
         msg = err.value.decode(errors="replace") if err is not None else ""
-        raise ZhError(status, msg or f"zarrhip status {status}")
+        pos = last_data_error() if status == A.ZH_EDATA else None
+        raise ZhError(status, msg or f"zarrhip status {status}", pos)
 
 
 class DeviceContext:
@@ -235,6 +249,14 @@ class DeviceContext:
         g = C.c_double()
         check(self.L.zh_device_write_rate(self.h, P(ptr), int(nbytes), int(pattern), int(reps),
                                           C.byref(g)))
+        return g.value
+
+    def copy_rate(self, dst, src, nbytes, reps=3):
+        """Copy ceiling of a buffer pair by a streaming byte-swapping copy src -> dst,
+        GB/s of bytes read + written (overwrites dst)."""
+        g = C.c_double()
+        check(self.L.zh_device_copy_rate(self.h, P(dst), P(src), int(nbytes), int(reps),
+                                         C.byref(g)))
         return g.value
 
     def malloc_pinned(self, nbytes):

@@ -16,7 +16,11 @@ def raise_for(err):
     st = getattr(err, "status", None)
     msg = str(err)
     if st == A.ZH_EDATA:
-        raise ZarrException(msg) from None
+        e = ZarrException(msg)
+        # where the failing chunk sits in a sequential read (zh_last_data_error): the
+        # multi-rank read orders the ranks' errors by it (zarrhip.parallel.pick_error)
+        e.position = getattr(err, "position", None)
+        raise e from None
     if st == A.ZH_EUNSUPPORTED:
         raise UnsupportedChainError(msg) from None
     if st == A.ZH_EINVAL:

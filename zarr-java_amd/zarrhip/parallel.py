@@ -121,6 +121,90 @@ def gather_pieces_p2p(tdist, grp, rank, world, sched, send_buf, region, decode=N
     return works
 
 
+def error_record(exc):
+    """What the other ranks of a group need to raise `exc` again: its class, message, C-ABI
+    status and, for a data error, where the failing chunk sits in a sequential read
+    (ZarrException.position / ZhError.position: (chunk grid coords, key), zh_last_data_error)."""
+    pos = getattr(exc, "position", None)
+    return {"cls": type(exc).__name__, "module": type(exc).__module__, "msg": str(exc),
+            "status": getattr(exc, "status", None),
+            "pos": (tuple(int(c) for c in pos[0]), int(pos[1])) if pos else None}
+
+
+def pick_error(records):
+    """The error one sequential core.Array.read would have thrown, out of every rank's errors
+    (`records[r]`: rank r's error_records, in its own order).  When every error is a placed data
+    error, the first in the reference's sequential order — chunk grid coords in C order, then
+    the larger key (the index crc32c before the inner chunks, lower C-order rank first: DESIGN
+    §3 Q17, the rule zh_array_read_multi applies to its slabs); otherwise the first error of the
+    first failing rank (the slabs are contiguous in C order).  Returns (rank, index) or None."""
+    failing = [(r, i, e) for r, errs in enumerate(records) for i, e in enumerate(errs or [])]
+    if not failing:
+        return None
+    if all(e["pos"] is not None for _, _, e in failing):
+        r, i, _ = min(failing, key=lambda t: (tuple(t[2]["pos"][0]), -t[2]["pos"][1], t[0], t[1]))
+        return r, i
+    return min(failing, key=lambda t: (t[0], t[1]))[:2]
+
+
+def rebuild_error(rec):
+    """An exception equal in class and message to the one error_record described."""
+    import builtins
+    from . import _lib, errors
+    from .store import StoreException
+    known = {("zarrhip.errors", "ZarrException"): errors.ZarrException,
+             ("zarrhip.errors", "UnsupportedChainError"): errors.UnsupportedChainError,
+             ("zarrhip.store", "StoreException"): StoreException}
+    if (rec["module"], rec["cls"]) == ("zarrhip._lib", "ZhError"):
+        e = _lib.ZhError(rec["status"], rec["msg"], rec["pos"])
+    else:
+        cls = known.get((rec["module"], rec["cls"]))
+        if cls is None and rec["module"] == "builtins":
+            b = getattr(builtins, rec["cls"], None)
+            cls = b if isinstance(b, type) and issubclass(b, Exception) else None
+        try:
+            e = (cls or RuntimeError)(rec["msg"])
+        except Exception:
+            e = RuntimeError(rec["msg"])
+    if rec["pos"] is not None:
+        e.position = rec["pos"]
+    return e
+
+
+def raise_group_error(tdist, group, rank, world, errs):
+    """Collective over `group` (every rank calls it, also as the read's closing barrier): each
+    rank contributes the errors its part of a read met, and if any rank met one, EVERY rank
+    raises the same pick_error choice — the rank that met it its own exception object, the others
+    an equal one (rebuild_error).  The reference throws out of read() when any chunk fails
+    (M/core/Array.java:403-407, 436-438); no rank may return a region with a failed slab, and no
+    rank waits for a peer that gave up."""
+    mine = [error_record(e) for e in errs]
+    every = [None] * world
+    tdist.all_gather_object(every, mine, group=group)
+    pick = pick_error(every)
+    if pick is None:
+        return
+    r, i = pick
+    if r == rank:
+        raise errs[i]
+    raise rebuild_error(every[r][i])
+
+
+def deferred_errors(decode):
+    """The errors a decoder reports only when waited on: decode.wait_errors() (PlanDecoder: one
+    per failed plan), else whatever decode.wait() raises."""
+    if decode is None:
+        return []
+    if hasattr(decode, "wait_errors"):
+        return list(decode.wait_errors())
+    if hasattr(decode, "wait"):
+        try:
+            decode.wait()
+        except Exception as e:  # reported through raise_group_error
+            return [e]
+    return []
+
+
 class PlanDecoder:
     """decode(piece_offset, piece_shape, dst) for RegionGather over device-resident chunk
     sources: one zh plan per piece (created on its first use and kept, so a repeated read plans
@@ -148,9 +232,23 @@ class PlanDecoder:
         import torch
         self.plan(po, ps).execute(dst.data_ptr(), torch.cuda.current_stream(dst.device).cuda_stream)
 
-    def wait(self):
+    def wait_errors(self):
+        """Wait for every plan; the deferred device errors, one per failed plan (ZhError with
+        the reference's message and the failing chunk's position)."""
+        errs = []
         for p in self.plans.values():
-            p.wait()
+            try:
+                p.wait()
+            except Exception as e:  # every plan is waited on; the caller picks
+                errs.append(e)
+        return errs
+
+    def wait(self):
+        """Wait for every plan; raise the error a sequential read would have met first."""
+        errs = self.wait_errors()
+        pick = pick_error([[error_record(e) for e in errs]])
+        if pick is not None:
+            raise errs[pick[1]]
 
     def close(self):
         for p in self.plans.values():
@@ -258,9 +356,22 @@ class RegionGather:
 
     def run(self, decode=None):
         """Decode (unless None) and gather; returns the region byte tensor on the root and this
-        rank's slab byte tensor elsewhere, complete (device work synchronised)."""
+        rank's slab byte tensor elsewhere, complete (device work synchronised).
+
+        Errors: a piece whose decode raises is still sent (its bytes are never handed out), so
+        no peer or root waits for a send that never comes; after the gather, deferred device
+        errors (decode.wait_errors / wait) are collected and raise_group_error makes EVERY rank
+        raise the error a sequential read would have met first (the reference's message)."""
         torch = self.torch
         mine = self.pieces()
+        errs = []
+
+        def safe(po, ps, dst):
+            try:
+                decode(po, ps, dst)
+            except Exception as e:  # raised on every rank by raise_group_error below
+                errs.append(e)
+
         if self.rank == self.root:
             works = gather_pieces_p2p(self.tdist, self.group, self.rank, self.world, self.sched,
                                       None, self.region)
@@ -268,16 +379,16 @@ class RegionGather:
                 if self.on_device:
                     with torch.cuda.stream(self._side):
                         for po, ps, b, nb in mine:
-                            decode(po, ps, self._dst(b, nb))
+                            safe(po, ps, self._dst(b, nb))
                 else:
                     for po, ps, b, nb in mine:
-                        decode(po, ps, self._dst(b, nb))
+                        safe(po, ps, self._dst(b, nb))
             for w in works:
                 w.wait()
         else:
             def dec(k):
                 po, ps, b, nb = mine[k]
-                decode(po, ps, self._dst(b, nb))
+                safe(po, ps, self._dst(b, nb))
             for w in gather_pieces_p2p(self.tdist, self.group, self.rank, self.world, self.sched,
                                        self.send_buf[:self.slab_bytes] if self.slab_bytes
                                        else self.send_buf[:0], None,
@@ -286,9 +397,12 @@ class RegionGather:
         if self.on_device:
             torch.cuda.current_stream(self.device).wait_stream(self._side)
             torch.cuda.synchronize(self.device)
-        if decode is not None and hasattr(decode, "wait"):
-            decode.wait()
+        errs += deferred_errors(decode)
+        raise_group_error(self.tdist, self.group, self.rank, self.world, errs)
         return self.region if self.rank == self.root else self.send_buf[:self.slab_bytes]
+
+
+_REGION_SEQ = 0  # SharedHostRegion names: regions created by this process
 
 
 class SharedHostRegion:
@@ -330,24 +444,37 @@ class SharedHostRegion:
         for v in ss:
             sb *= v
         self.slab_bytes = sb
-        # one name for the group: rank 0's choice, broadcast
-        names = [name or f"/dev/shm/zh_region_{os.getpid()}_{os.getuid()}"]
-        tdist.broadcast_object_list(names, src=0, group=self.group)
-        self.name = names[0]
-        try:
-            vfs = os.statvfs(os.path.dirname(self.name))
-            room = vfs.f_bavail * vfs.f_frsize >= n + (1 << 30)
-        except OSError:
-            room = False
-        ok = [room]
-        tdist.broadcast_object_list(ok, src=0, group=self.group)
-        if not ok[0]:
-            raise MemoryError(f"{os.path.dirname(self.name)} cannot hold the {n}-byte region")
+        # one file per region: rank 0 picks a fresh name (pid, uid, a per-process counter and
+        # random bits, unless the caller names it), creates it exclusively (never another live
+        # region's file) and broadcasts the name with the outcome, so every rank raises together
+        res = [None, None]
         if self.rank == 0:
-            fd = os.open(self.name, os.O_RDWR | os.O_CREAT | os.O_TRUNC, 0o600)
-            os.ftruncate(fd, max(1, n))
-            os.close(fd)
-        tdist.barrier(group=self.group)
+            import uuid
+            global _REGION_SEQ
+            _REGION_SEQ += 1
+            path = name or (f"/dev/shm/zh_region_{os.getpid()}_{os.getuid()}_{_REGION_SEQ}_"
+                            f"{uuid.uuid4().hex[:12]}")
+            res[0] = path
+            try:
+                vfs = os.statvfs(os.path.dirname(path))
+                if vfs.f_bavail * vfs.f_frsize < n + (1 << 30):
+                    res[1] = ("MemoryError",
+                              f"{os.path.dirname(path)} cannot hold the {n}-byte region")
+                else:
+                    fd = os.open(path, os.O_RDWR | os.O_CREAT | os.O_EXCL, 0o600)
+                    try:
+                        os.ftruncate(fd, max(1, n))
+                    finally:
+                        os.close(fd)
+            except FileExistsError:
+                res[1] = ("FileExistsError", f"shared region file {path} already exists")
+            except OSError as e:
+                res[1] = ("OSError", f"shared region file {path}: {e}")
+        tdist.broadcast_object_list(res, src=0, group=self.group)
+        self.name = res[0]
+        if res[1] is not None:
+            import builtins
+            raise getattr(builtins, res[1][0])(res[1][1])
         fd = os.open(self.name, os.O_RDWR)
         self._mm = mmap.mmap(fd, max(1, n), mmap.MAP_SHARED, mmap.PROT_READ | mmap.PROT_WRITE)
         os.close(fd)
@@ -367,10 +494,17 @@ class SharedHostRegion:
         return self.addr + self.base
 
     def read(self, decode):
-        """Every rank decodes its slab into its slice; returns after all ranks are done."""
+        """Every rank decodes its slab into its slice; returns after all ranks are done.  If any
+        rank's decode failed, every rank raises the same error (raise_group_error, which is also
+        the closing barrier), so none returns a region holding a failed slab and none hangs."""
+        errs = []
         if self.slab_bytes > 0:
-            decode(self.slab_offset, self.slab_shape, self.slice_addr())
-        self.tdist.barrier(group=self.group)
+            try:
+                decode(self.slab_offset, self.slab_shape, self.slice_addr())
+            except Exception as e:  # raised on every rank below
+                errs.append(e)
+        errs += deferred_errors(decode)
+        raise_group_error(self.tdist, self.group, self.rank, self.world, errs)
 
     def array(self, dtype):
         """The whole region as a numpy array over the shared buffer (valid until close())."""
@@ -379,18 +513,25 @@ class SharedHostRegion:
                               _np.dtype(dtype).itemsize).reshape(self.shape)
 
     def close(self):
+        """Unpin and unmap this rank's view, then (every rank, even when unmapping failed — a
+        caller still holding array()'s view makes mmap.close raise BufferError) the barrier;
+        rank 0 removes the file; a local failure is raised after the barrier."""
         import os
-        if self._reg is not None:
-            self.dev.host_unregister(self._reg)
-            self._reg = None
-        del self._cbuf
-        self._mm.close()
-        self.tdist.barrier(group=self.group)
-        if self.rank == 0:
-            try:
-                os.unlink(self.name)
-            except FileNotFoundError:
-                pass
+        try:
+            if self._reg is not None:
+                self._reg, reg = None, self._reg
+                self.dev.host_unregister(reg)
+            if getattr(self, "_cbuf", None) is not None:
+                del self._cbuf
+                self._cbuf = None
+            self._mm.close()
+        finally:
+            self.tdist.barrier(group=self.group)
+            if self.rank == 0:
+                try:
+                    os.unlink(self.name)
+                except FileNotFoundError:
+                    pass
 
 
 def array_host_decoder(array, dev=None):
