@@ -220,24 +220,17 @@ def pmc_traffic(config):
 
 
 def kernel_name(meta):
-    # tile chains: tiles_group_kernel (ZH_DEC_TGROUP=0: decode_tiles_kernel); with the chunk
-    # crc32c the row-CRC tile kernel
+    # tile chains: tiles_group_kernel; with the chunk crc32c the row-CRC tile kernel over
+    # 128-B aligned payload windows (c4crc's layout)
     if meta.chain.has_transpose:
-        if os.environ.get("ZH_DEC_TGROUP") == "0":
-            return "decode_tiles_kernel"
-        if meta.chain.inner_crc32c:
-            # 128-B aligned payload windows unless ZH_DEC_ALIGN=0 (round 3)
-            return ("tiles_rowcrc_kernel" if os.environ.get("ZH_DEC_ALIGN") == "0"
-                    else "tiles_rowcrc_aln_kernel")
-        return "tiles_group_kernel"
-    # row chains with 128-B rows and no chunk CRC: the lane-exchange kernel (ZH_DEC_RGROUP=8)
+        return "tiles_rowcrc_aln_kernel" if meta.chain.inner_crc32c else "tiles_group_kernel"
+    # row chains with 128-B rows and no chunk CRC: the lane-exchange kernel
     c = meta.chain
-    rg = os.environ.get("ZH_DEC_RGROUP")
-    if c.sharded and not c.inner_crc32c and rg in (None, "8") and \
+    if c.sharded and not c.inner_crc32c and \
             c.inner_chunk_shape[meta.ndim - 1] * meta.dtype_size == 128:
         return "rows_xpose_kernel"
-    # with the chunk crc32c: the grouped row-CRC kernel (ZH_DEC_RGROUP=-1 picks its group)
-    if c.sharded and c.inner_crc32c and rg in (None, "-1", "1", "2", "4"):
+    # with the chunk crc32c: the grouped row-CRC kernel
+    if c.sharded and c.inner_crc32c:
         return "rows_group_kernel"
     return "decode_rows_kernel<4,4>"
 
@@ -668,6 +661,52 @@ def visible_devices():
     return torch.cuda.device_count()
 
 
+def strong_slab(L, meta, ws, rank):
+    """Rank `rank`'s part of the strong-scaling read: the region's y-slabs on the
+    inner-chunk grid (slab_partition; 512 rows at N=8 on the full array), this rank's slab, and
+    the shard-aligned box `lo`/`ext` whose shards it must hold (`cover`, computeChunkCoords
+    order).  Pure geometry: tests/test_multigpu_plan.py runs it at full size and at world 8 on
+    a scaled array."""
+    from zarrhip.parallel import slab_partition
+    n = meta.ndim
+    shape = [meta.shape[d] for d in range(n)]
+    cs = [meta.chunk_shape[d] for d in range(n)]
+    inner_y = meta.chain.inner_chunk_shape[1] if meta.chain.sharded else 1
+    parts = slab_partition([0] * n, shape, ws, align=inner_y)
+    so, ss = parts[rank]
+    lo = [(so[d] // cs[d]) * cs[d] for d in range(n)]
+    hi = [min(-(-(so[d] + ss[d]) // cs[d]) * cs[d], shape[d]) for d in range(n)]
+    ext = [h - l for l, h in zip(lo, hi)]
+    for d in range(2, n):
+        assert lo[d] == 0 and ext[d] == shape[d]
+    nel_cover = 1
+    for e in ext:
+        nel_cover *= e
+    full_bytes = meta.dtype_size
+    for s_ in shape:
+        full_bytes *= s_
+    slab_bytes = meta.dtype_size
+    for s_ in ss:
+        slab_bytes *= s_
+    return {"parts": parts, "so": so, "ss": ss, "lo": lo, "ext": ext, "align": inner_y,
+            "cover": all_coords(L, meta, lo, ext), "nel_cover": nel_cover,
+            "cover_bytes": nel_cover * meta.dtype_size, "slab_bytes": slab_bytes,
+            "full_bytes": full_bytes}
+
+
+def strong_memory_plan(geo, shard_bytes, rank, backend, headroom=4 << 30):
+    """Device memory one rank of the strong-scaling read holds at once, checked before anything
+    is allocated: the decode's output (the shard-aligned cover box, also the encode source of
+    the rank's shards), its shards, on the root with RCCL the assembled region (torch), on a
+    peer with RCCL its send buffer, and headroom for plan tables and staging."""
+    region = geo["full_bytes"] if rank == 0 and backend == "nccl" else 0
+    send = geo["slab_bytes"] if rank != 0 and backend == "nccl" else 0
+    out = {"output": geo["cover_bytes"], "shards": int(shard_bytes), "region": region,
+           "send_buffer": send, "headroom": headroom}
+    out["total"] = sum(out.values())
+    return out
+
+
 def run_strong(args, dist, A, meta, rank, ws, local):
     """Strong scaling: ONE full array split into per-rank y-slabs (512 rows at
     N=8, aligned to inner chunks); each rank holds only the shards its slab touches (encoded
@@ -675,7 +714,7 @@ def run_strong(args, dist, A, meta, rank, ws, local):
     rank copies its slab to its slice of one host buffer."""
     import torch
     from zarrhip._lib import DeviceContext, lib
-    from zarrhip.parallel import slab_byte_offset, slab_partition
+    from zarrhip.parallel import slab_byte_offset
     L = lib()
     ndev = visible_devices()
     device = local % max(1, ndev)
@@ -689,36 +728,21 @@ def run_strong(args, dist, A, meta, rank, ws, local):
     info = dev.info()
     n = meta.ndim
     shape = [meta.shape[d] for d in range(n)]
-    cs = [meta.chunk_shape[d] for d in range(n)]
-    inner_y = meta.chain.inner_chunk_shape[1] if meta.chain.sharded else 1
-    parts = slab_partition([0] * n, shape, ws, align=inner_y)
-    so, ss = parts[rank]
-    lo = [(so[d] // cs[d]) * cs[d] for d in range(n)]
-    hi = [min(-(-(so[d] + ss[d]) // cs[d]) * cs[d], shape[d]) for d in range(n)]
-    ext = [h - l for l, h in zip(lo, hi)]
-    for d in range(2, n):
-        assert lo[d] == 0 and ext[d] == shape[d]
-    cover = all_coords(L, meta, lo, ext)
+    geo = strong_slab(L, meta, ws, rank)
+    parts, so, ss, lo, ext, cover = (geo[k] for k in ("parts", "so", "ss", "lo", "ext", "cover"))
+    inner_y = geo["align"]
     caps = chunk_capacities(meta, cover)
-    nel_cover = 1
-    for e in ext:
-        nel_cover *= e
+    nel_cover = geo["nel_cover"]
     first = lo[1] * shape[2] * shape[3] if n == 4 else 0
     t0 = time.perf_counter()
     offs, tot = slab_layout(caps)
-    full_bytes = 4
-    for s_ in shape:
-        full_bytes *= s_
-    # memory plan, checked before anything is allocated: the decode's output (also the encode
-    # source of this rank's shards), the shards, on the root the assembled region (RCCL), and
-    # tables/staging headroom
-    need = nel_cover * 4 + tot + (full_bytes if rank == 0 and backend == "nccl" else 0) + \
-        (4 << 30)
+    full_bytes = geo["full_bytes"]
+    plan_mem = strong_memory_plan(geo, tot, rank, backend)
+    need = plan_mem["total"]
     if need > info["total_mem"]:
-        raise SystemExit(f"[rank {rank}] memory plan: {need / GiB:.1f} GiB needed (output "
-                         f"{nel_cover * 4 / GiB:.1f} + shards {tot / GiB:.1f} GiB"
-                         f"{' + the region' if rank == 0 and backend == 'nccl' else ''} + 4 GiB) > "
-                         f"{info['total_mem'] / GiB:.1f} GiB on device {device}; use more ranks")
+        raise SystemExit(f"[rank {rank}] memory plan: {need / GiB:.1f} GiB needed "
+                         f"({json.dumps(plan_mem)}) > {info['total_mem'] / GiB:.1f} GiB on "
+                         f"device {device}; use more ranks")
     log(f"[rank {rank}] memory plan: {need / GiB:.1f} of {info['total_mem'] / GiB:.1f} GiB")
     # plain device allocations (hipMalloc), as the library's own reads use
     src = dev.malloc(nel_cover * 4, 0)

@@ -508,8 +508,8 @@ int zh_device_malloc(zh_ctx* ctx, size_t bytes, void** out);
  * hipMalloc on 18 buffers, 3 boxes).  The rest beyond the last whole chunk gets one smaller
  * chunk (rounded up to the allocation granularity), mapped last.  Freed by zh_device_free. */
 #define ZH_MALLOC_SCATTER 0x4u
-/* With ZH_MALLOC_SCATTER: allocate up to ZH_CALIB_TRIES candidate arenas (default 2, each
- * held while the next is allocated, so each gets other physical chunks), time a contiguous
+/* With ZH_MALLOC_SCATTER: allocate two candidate arenas (the first held while the second is
+ * allocated, so each gets other physical chunks), time a contiguous
  * store probe over each (zh_device_write_rate pattern 0) and keep the fastest.  A large
  * arena's write rate is set by its physical chunks (not their order or its address) and the
  * probe predicts the decode's rate into it (DESIGN.md §4 "Placement").  Needs the memory of

@@ -42,7 +42,7 @@ def test_c2_geometry_decode_and_encode(dev, monkeypatch, small_split):
     """small_split "0": whole 2 MiB chunks are the work items, as at full size (32 chunks ×
     2048 pieces there, so the small-read split never applies); None: the default knobs at
     this size, which split the 8 chunks further for the launch width."""
-    for k in ("ZH_PIECE_KB", "ZH_DEC_RGROUP", "ZH_ENC_GROUP", "ZH_PIPE"):
+    for k in ("ZH_PIECE_KB", "ZH_PIPE"):
         monkeypatch.delenv(k, raising=False)
     if small_split is None:
         monkeypatch.delenv("ZH_SMALL_SPLIT", raising=False)

@@ -76,8 +76,6 @@ def test_row_crc_tile_kernel_is_the_default(dev, monkeypatch, order):
     """Without switches a whole-chunk [transpose, bytes(big), crc32c] read runs
     tiles_rowcrc_kernel at G = 1 (variant 51) and matches the oracle; a flipped payload byte
     in the middle of a chunk is reported with the oracle's message."""
-    for k in ("ZH_DEC_TGROUP",):
-        monkeypatch.delenv(k, raising=False)
     monkeypatch.setenv("ZH_SMALL_SPLIT", "0")
     meta = _meta(order)
     arr = rand_array(SHAPE, 4, seed=57)
@@ -88,14 +86,13 @@ def test_row_crc_tile_kernel_is_the_default(dev, monkeypatch, order):
     _corrupt_matches_oracle(dev, meta, shards, 0, CHUNK + 65536 + 77)
 
 
-@pytest.mark.parametrize("variant", ["0", "1"])
-@pytest.mark.parametrize("perm", ["0", "1"])
-def test_tile_crc_variants_and_item_order(dev, monkeypatch, variant, perm):
-    """Row-per-tile variant (ZH_TILE_VARIANT=0: the CRC stays a separate pass) and the
-    golden-ratio item order on/off give the same bytes; corruption of the last payload byte
-    of a shard's last inner chunk is caught."""
-    monkeypatch.setenv("ZH_TILE_VARIANT", variant)
-    monkeypatch.setenv("ZH_ITEM_PERM", perm)
+@pytest.mark.parametrize("split", ["0", "1"])
+def test_tile_crc_pieces_item_order(dev, monkeypatch, split):
+    """Chunks cut into 32 KiB pieces (the per-chunk row-interleaved tile kernel with the chunk
+    CRC fused, walked in the golden-ratio item order) give the same bytes, with and without the
+    small-plan split; corruption of the last payload byte of a shard's last inner chunk is
+    caught."""
+    monkeypatch.setenv("ZH_SMALL_SPLIT", split)
     monkeypatch.setenv("ZH_PIECE_KB", "32")
     meta = _meta([2, 1, 0])
     arr = rand_array(SHAPE, 4, seed=43)
@@ -108,24 +105,23 @@ def test_tile_crc_variants_and_item_order(dev, monkeypatch, variant, perm):
 
 
 @pytest.mark.parametrize("order", [[0, 2, 1], [2, 1, 0], [1, 2, 0]])
-@pytest.mark.parametrize("group", ["0", "1", "2", "4", "8"])
+@pytest.mark.parametrize("split", ["0", "1"])
 @pytest.mark.parametrize("crc", [True, False])
-def test_grouped_tile_decode(dev, monkeypatch, order, group, crc):
-    """tiles_group_kernel in the decode direction (ZH_DEC_TGROUP chunks per work item, 8/G
-    tiles of each per step, the next step's loads before this step's stores); with the chunk
-    CRC the row-CRC tile kernel at one chunk per work item whatever G (ZH_DEC_TGROUP=0: the
-    per-chunk row-interleaved kernels, CRC fused).  An elided inner chunk, a missing shard, a
-    clipped region; a corrupt byte of a fast chunk is caught."""
-    monkeypatch.setenv("ZH_DEC_TGROUP", group)
-    monkeypatch.setenv("ZH_SMALL_SPLIT", "0")  # whole chunks: the grouped kernels need them
+def test_grouped_tile_decode(dev, monkeypatch, order, split, crc):
+    """tiles_group_kernel in the decode direction (4 chunks per work item, 2 tiles of each per
+    step, the next step's loads before this step's stores); with the chunk CRC the row-CRC tile
+    kernel at one chunk per work item.  With the small-plan split (ZH_SMALL_SPLIT=1: this
+    8-chunk read is cut into pieces) the per-chunk row-interleaved kernels run instead, CRC
+    fused.  An elided inner chunk, a missing shard, a clipped region; a corrupt byte of a fast
+    chunk is caught."""
+    monkeypatch.setenv("ZH_SMALL_SPLIT", split)
     meta = A.make_meta(SHAPE, [32, 64, 64], 4, endian=A.ZH_ENDIAN_BIG, sharded=True,
                        inner_chunk_shape=[32, 32, 32], transpose_order=order, inner_crc32c=crc)
     arr = rand_array(SHAPE, 4, seed=47)
     arr[32:64, 0:32, 32:64] = 0
     shards = encode_oracle(meta, arr)
     shards[2] = None
-    G = int(group)
-    want_variant = 1 if G == 0 else 51 if crc else 20 + G
+    want_variant = 1 if split == "1" else 51 if crc else 24
     for off, shp in [([0, 0, 0], SHAPE), ([5, 3, 7], [50, 60, 80])]:
         got, want = _read_both(dev, meta, shards, off, shp)
         np.testing.assert_array_equal(got, want)
@@ -142,8 +138,6 @@ def test_row_crc_tile_decode_endian(dev, monkeypatch, order, endian):
     carried swapped): same bytes as the oracle with an elided chunk, a missing shard and a
     clipped region; corruption in a chunk's first payload row, in a middle row and in its last
     byte is reported with the oracle's message."""
-    for k in ("ZH_DEC_TGROUP", "ZH_DEC_ALIGN"):
-        monkeypatch.delenv(k, raising=False)
     monkeypatch.setenv("ZH_SMALL_SPLIT", "0")
     meta = A.make_meta(SHAPE, [32, 64, 64], 4, endian=endian, sharded=True,
                        inner_chunk_shape=[32, 32, 32], transpose_order=order, inner_crc32c=True)
@@ -166,8 +160,7 @@ def test_row_crc_tile_kernel_many_groups(dev, monkeypatch):
     64 MiB: 512 inner chunks over 8 shards, the golden-ratio group order and the default
     row-CRC tile kernel; equals the oracle, and a flipped byte deep inside the last shard is
     reported with the oracle's message."""
-    for k in ("ZH_DEC_TGROUP", "ZH_SMALL_SPLIT"):
-        monkeypatch.delenv(k, raising=False)
+    monkeypatch.delenv("ZH_SMALL_SPLIT", raising=False)
     shape = [1, 256, 256, 256]
     meta = A.make_meta(shape, [1, 128, 128, 128], 4, endian=A.ZH_ENDIAN_BIG, sharded=True,
                        inner_chunk_shape=[1, 32, 32, 32], transpose_order=[0, 3, 2, 1],
@@ -175,8 +168,7 @@ def test_row_crc_tile_kernel_many_groups(dev, monkeypatch):
     arr = rand_array(shape, 4, seed=59)
     arr[arr == 0] = 1
     shards = encode_oracle(meta, arr)
-    # the default tile encode with the fused chunk CRC (2 chunks per work item) at this size
-    monkeypatch.delenv("ZH_ENC_TGROUP", raising=False)
+    # the tile encode with the fused chunk CRC (2 chunks per work item) at this size
     assert device_write(dev, meta, arr) == shards
     assert (lib().zh_debug_last_fast_path(1) % 1000000) // 1000 == 2
     want = np.frombuffer(O.array_read(meta, shards, [0, 0, 0, 0], shape), np.uint32).reshape(shape)
@@ -204,8 +196,6 @@ def test_row_crc_tile_kernel_unit_layouts(dev, monkeypatch, units, order):
     per-unit K multiply (no regular fold step: crc_tile_step 0), 12 units the regular fold
     over a partly filled last step.  Equals the oracle; a flipped byte in the last unit of a
     chunk is caught with the oracle's message."""
-    for k in ("ZH_DEC_TGROUP",):
-        monkeypatch.delenv(k, raising=False)
     monkeypatch.setenv("ZH_SMALL_SPLIT", "0")
     shape = [units * 2, 64, 96]
     meta = A.make_meta(shape, [units * 2, 64, 64], 4, endian=A.ZH_ENDIAN_BIG, sharded=True,
@@ -248,13 +238,11 @@ def test_row_crc_aligned_windows(dev, monkeypatch, nb, endian):
     carry each step's last line into the next step's tile through a ring of 9 LDS slots.  One
     shard of 36 inner chunks puts the payloads at every offset 4i mod 128 (the head lines, the
     carried line ends and the row tails of every δ, and δ = 0; 2, 3 and 4 steps per chunk).  Equals the oracle over the
-    whole array and a ragged region, with an elided chunk; ZH_DEC_ALIGN=0 gives the same bytes
-    through the unaligned loads; flipped bytes in a row tail (read at the last step from the
-    box), in a carried line end and in a head line are reported with the oracle's message."""
-    for k in ("ZH_DEC_TGROUP",):
-        monkeypatch.delenv(k, raising=False)
+    whole array and a ragged region, with an elided chunk (the unaligned row-CRC kernel keeps
+    the layouts this one does not take: test_row_crc_tile_kernel_unit_layouts and the other
+    transpose orders); flipped bytes in a row tail (read at the last step from the box), in a
+    carried line end and in a head line are reported with the oracle's message."""
     monkeypatch.setenv("ZH_SMALL_SPLIT", "0")
-    monkeypatch.setenv("ZH_DEC_ALIGN", "1")
     shape = [64, 6 * nb, 96]
     meta = A.make_meta(shape, shape, 4, endian=endian, sharded=True,
                        inner_chunk_shape=[32, nb, 32], transpose_order=[2, 1, 0],
@@ -270,10 +258,6 @@ def test_row_crc_aligned_windows(dev, monkeypatch, nb, endian):
     off, shp = [3, 5, 7], [58, 6 * nb - 9, 80]
     sel = np.frombuffer(O.array_read(meta, shards, off, shp), np.uint32).reshape(shp)
     np.testing.assert_array_equal(device_read(dev, meta, shards, off, shp), sel)
-    monkeypatch.setenv("ZH_DEC_ALIGN", "0")
-    np.testing.assert_array_equal(device_read(dev, meta, shards, [0, 0, 0], shape), arr)
-    assert _variant() == 51 and _aligned() == 0
-    monkeypatch.setenv("ZH_DEC_ALIGN", "1")
     chunk = 32 * nb * 32 * 4 + 4
     row = nb * 128  # bytes of one payload row (all units)
     for i in (5, 31):  # δ = 20 and 124
@@ -302,7 +286,7 @@ def test_row_crc_chain_64mib_defaults(dev, monkeypatch):
     item, payloads stored through the cache since round 3) gives the oracle's shard bytes, and
     the grouped row-CRC decode (cached payload loads) gives the array back; a flipped byte deep
     inside the last shard is reported with the oracle's message."""
-    for k in ("ZH_ENC_GROUP", "ZH_DEC_RGROUP", "ZH_SMALL_SPLIT", "ZH_PIPE"):
+    for k in ("ZH_SMALL_SPLIT", "ZH_PIPE"):
         monkeypatch.delenv(k, raising=False)
     shape = [1, 256, 256, 256]
     meta = A.make_meta(shape, [1, 128, 128, 128], 4, endian=A.ZH_ENDIAN_BIG, sharded=True,
@@ -334,8 +318,7 @@ def test_plain_chains_64mib_defaults(dev, monkeypatch, order):
     inner chunks) at 64 MiB through the default kernels: the grouped encodes give the oracle's
     shard bytes, and the decode (lane exchange for c3, tile groups for c4) gives the array
     back, also for a region that cuts every shard."""
-    for k in ("ZH_ENC_GROUP", "ZH_ENC_TGROUP", "ZH_DEC_RGROUP", "ZH_DEC_TGROUP",
-              "ZH_SMALL_SPLIT", "ZH_PIPE"):
+    for k in ("ZH_SMALL_SPLIT", "ZH_PIPE"):
         monkeypatch.delenv(k, raising=False)
     shape = [1, 256, 256, 256]
     meta = A.make_meta(shape, [1, 128, 128, 128], 4, endian=A.ZH_ENDIAN_BIG, sharded=True,
@@ -354,33 +337,32 @@ def test_plain_chains_64mib_defaults(dev, monkeypatch, order):
 
 
 @pytest.mark.parametrize("order", [[0, 2, 1], [2, 1, 0], [1, 2, 0]])
-@pytest.mark.parametrize("group", ["1", "2", "4"])
-def test_tile_crc_encode_groups(dev, monkeypatch, order, group):
-    """The tile encode with the fused chunk CRC over 1, 2 and 4 chunks per work item:
-    byte-identical to the oracle's shards (an all-fill chunk elided, so the later payloads
-    shift), and the kernel that ran is that group size."""
-    monkeypatch.setenv("ZH_ENC_TGROUP", group)
+def test_tile_crc_encode_groups(dev, monkeypatch, order):
+    """The tile encode with the fused chunk CRC over 2 chunks per work item: byte-identical to
+    the oracle's shards (an all-fill chunk elided, so the later payloads shift), and the kernel
+    that ran is that group size."""
     meta = _meta(order)
     arr = rand_array(SHAPE, 4, seed=97)
     arr[0:32, 32:64, 0:32] = 0
     want = encode_oracle(meta, arr)
     got = device_write(dev, meta, arr)
     assert got == want
-    assert (lib().zh_debug_last_fast_path(1) % 1000000) // 1000 == int(group)
+    assert (lib().zh_debug_last_fast_path(1) % 1000000) // 1000 == 2
 
 
-@pytest.mark.parametrize("group", ["1", "2", "4"])
-def test_row_crc_encode_groups(dev, monkeypatch, group):
-    """The row encode with the fused chunk CRC ([bytes(big), crc32c], no transpose) over 1, 2
-    and 4 chunks per work item, payloads stored through the cache: byte-identical to the
-    oracle's shards (an all-fill chunk elided, so later payloads shift)."""
-    monkeypatch.setenv("ZH_ENC_GROUP", group)
-    meta = _meta(None)
+@pytest.mark.parametrize("row,group", [(64, 1), (32, 2), (16, 4)])
+def test_row_crc_encode_groups(dev, monkeypatch, row, group):
+    """The row encode with the fused chunk CRC ([bytes(big), crc32c], no transpose) groups
+    256 B of region row per wave: 1, 2 and 4 chunks per work item for 256-, 128- and 64-B
+    inner chunk rows, payloads stored through the cache: byte-identical to the oracle's
+    shards (an all-fill chunk elided, so later payloads shift)."""
+    meta = A.make_meta(SHAPE, [32, 64, 64], 4, endian=A.ZH_ENDIAN_BIG, sharded=True,
+                       inner_chunk_shape=[32, 32, row], inner_crc32c=True)
     arr = rand_array(SHAPE, 4, seed=101)
-    arr[32:64, 0:32, 32:64] = 0
+    arr[32:64, 0:32, 0:64] = 0  # whole inner chunks for every row length
     want = encode_oracle(meta, arr)
     assert device_write(dev, meta, arr) == want
-    assert (lib().zh_debug_last_fast_path(1) % 1000000) // 1000 == int(group)
+    assert (lib().zh_debug_last_fast_path(1) % 1000000) // 1000 == group
 
 
 @pytest.mark.parametrize("start", [False, True])

@@ -188,8 +188,9 @@ def test_multi_forced_staged_route(ctxs, src_device, monkeypatch):
 def test_multi_distinct_devices(peer, monkeypatch):
     """One context per visible GPU (up to 8): root gather of a region read with device
     sources on the root, vs the oracle; the non-root slabs must report the xGMI route when
-    the pair has peer access (peer=1) and the staged route when peer access is disabled."""
-    monkeypatch.setenv("ZH_MULTI_PEER", peer)
+    the pair has peer access (peer=1) and the staged route when it is forced off
+    (ZH_MULTI_FORCE_STAGED=1)."""
+    monkeypatch.setenv("ZH_MULTI_FORCE_STAGED", "0" if peer == "1" else "1")
     nd = min(8, device_count())
     cs = [DeviceContext(d) for d in range(nd)]
     try:

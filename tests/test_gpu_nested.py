@@ -94,7 +94,7 @@ def test_nested_encode_one_pass(dev, monkeypatch, case, variant):
     """The one-pass write on nested chains (no leaf is all fill_value, so the speculative
     layout holds): cell table, outer index and its crc32c on the host; leaf offsets, sub-index
     entries and sub-index crc32c on the device.  Boundary shards elide padding-only cells and
-    leaves.  Bytes equal the oracle's and the flags → layout → encode fallback's."""
+    leaves.  Bytes equal the oracle's."""
     m = _meta(case, order=[1, 0] + list(range(2, len(case["shape"])))
               if variant == "transpose" else None)
     if variant == "crc32c":
@@ -103,8 +103,6 @@ def test_nested_encode_one_pass(dev, monkeypatch, case, variant):
     arr = rand_array(shape, 4, seed=13)
     arr[arr == 0] = 1
     want = encode_oracle(m, arr)
-    assert device_write(dev, m, arr) == want
-    monkeypatch.setenv("ZH_ENC_FAST", "0")
     assert device_write(dev, m, arr) == want
 
 

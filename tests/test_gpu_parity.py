@@ -436,7 +436,7 @@ def test_device_encode_matches_oracle_bytes(dev, sharded, order, loc):
 def test_device_encode_one_pass(dev, monkeypatch, dsize, mode, loc):
     """The one-pass write path (no all-fill chunk, so the speculative C-order layout holds):
     fast kernels on the encode view + the generic kernel for clipped chunks + device index and
-    index crc32c.  Bytes equal the oracle's and the flags → layout → encode path's."""
+    index crc32c.  Bytes equal the oracle's."""
     if mode == "unsharded" and loc == A.ZH_INDEX_START:
         pytest.skip("no index")
     shape = [40, 48, 72]          # boundary chunks on every axis
@@ -457,8 +457,6 @@ def test_device_encode_one_pass(dev, monkeypatch, dsize, mode, loc):
     got = device_write(dev, meta, arr)
     assert [len(g) if g else 0 for g in got] == [len(w) if w else 0 for w in want]
     assert got == want
-    monkeypatch.setenv("ZH_ENC_FAST", "0")
-    assert device_write(dev, meta, arr) == want
 
 
 @pytest.mark.parametrize("dsize", [1, 2, 4, 8])
@@ -480,16 +478,16 @@ def test_device_encode_grouped_rows(dev, dsize, order):
 
 @pytest.mark.parametrize("crc", [False, True])
 @pytest.mark.parametrize("dsize", [1, 4, 8])
-@pytest.mark.parametrize("group", ["0", "1", "2", "4", "8", "-1"])
-def test_device_encode_chunk_groups(dev, monkeypatch, dsize, group, crc):
-    """rows_group_kernel on the encode view (G consecutive inner chunks per work item,
-    ZH_ENC_GROUP; 4 rows in flight per lane): an odd number of inner chunks along each shard row (groups straddle
-    shard rows and the item list's end), all-fill chunks beside data chunks in one group
-    (per-chunk flags from one ballot), clipped boundary chunks on the slow list.  crc: inner
-    [bytes(big), crc32c] with 4 KiB chunk payloads, the chunk CRC fused into the grouped
-    kernel (256/G lanes per chunk)."""
-    monkeypatch.setenv("ZH_ENC_GROUP", group)
-    inner_last = 128 // dsize
+@pytest.mark.parametrize("row", [32, 64, 128, 256])
+def test_device_encode_chunk_groups(dev, monkeypatch, dsize, row, crc):
+    """rows_group_kernel on the encode view (G consecutive inner chunks per work item so a wave
+    covers 256 B of a region row: G = 8, 4, 2, 1 for 32-, 64-, 128- and 256-B inner chunk rows,
+    at most 4 with the chunk CRC; 4 rows in flight per lane): an odd number of inner chunks along
+    each shard row (groups straddle shard rows and the item list's end), all-fill chunks beside
+    data chunks in one group (per-chunk flags from one ballot), clipped boundary chunks on the
+    slow list.  crc: inner [bytes(big), crc32c], the chunk CRC fused into the grouped kernel
+    where whole 4 KiB rounds allow (256/G lanes per chunk), else the CRC pass."""
+    inner_last = row // dsize
     shape = [13, 24, inner_last * 7 + inner_last // 2]
     meta = A.make_meta(shape, [8, 8, inner_last * 5], dsize, endian=A.ZH_ENDIAN_BIG,
                        sharded=True, inner_chunk_shape=[4, 8, inner_last],
@@ -506,13 +504,11 @@ def test_device_encode_chunk_groups(dev, monkeypatch, dsize, group, crc):
     assert got == want
 
 
-@pytest.mark.parametrize("group", ["0", "1", "2", "4", "-1"])
 @pytest.mark.parametrize("loc", [A.ZH_INDEX_END, A.ZH_INDEX_START])
-def test_device_encode_tile_groups(dev, monkeypatch, group, loc):
-    """encode_tiles_group_kernel (ZH_ENC_TGROUP chunks per work item, 8/G tiles of each per
+def test_device_encode_tile_groups(dev, monkeypatch, loc):
+    """The grouped tile encode (tiles_group_kernel, 2 chunks per work item, 4 tiles of each per
     step): uint32 inner chunks transposed through 32x32 tiles, an odd number of chunks along
     each shard row, all-fill chunks inside groups, clipped boundary chunks."""
-    monkeypatch.setenv("ZH_ENC_TGROUP", group)
     shape = [40, 7, 32 * 7 + 16]
     meta = A.make_meta(shape, [32, 4, 32 * 5], 4, endian=A.ZH_ENDIAN_BIG, sharded=True,
                        inner_chunk_shape=[32, 2, 32], transpose_order=[2, 1, 0],
@@ -531,15 +527,15 @@ def test_device_encode_tile_groups(dev, monkeypatch, group, loc):
 
 @pytest.mark.parametrize("crc", [False, True])
 @pytest.mark.parametrize("dsize", [1, 4, 8])
-@pytest.mark.parametrize("group", ["0", "-1", "1", "2", "4"])
-def test_grouped_row_decode(dev, monkeypatch, crc, dsize, group):
-    """rows_group_kernel in the decode direction (ZH_DEC_RGROUP): G consecutive inner chunks
-    per work item with per-lane-group descriptors — copies beside Q1 zero-fill items (elided
-    chunks) and a missing shard's fill, an odd chunk count per shard row, row-clipped boundary
-    chunks sent to the generic kernel, the fused chunk CRC over 256/G lanes per chunk (and a
-    corrupt payload byte caught with the oracle's message)."""
-    monkeypatch.setenv("ZH_DEC_RGROUP", group)
-    inner_last = 128 // dsize
+@pytest.mark.parametrize("row", [64, 128, 256])
+def test_grouped_row_decode(dev, monkeypatch, crc, dsize, row):
+    """The row decode kernels: with the chunk CRC rows_group_kernel (G = 4, 2, 1 consecutive
+    inner chunks per work item for 64-, 128- and 256-B rows, per-lane-group descriptors, the
+    fused chunk CRC over 256/G lanes per chunk), without it the lane exchange for 128-B rows and
+    the per-chunk row kernel otherwise — copies beside Q1 zero-fill items (elided chunks) and a
+    missing shard's fill, an odd chunk count per shard row, row-clipped boundary chunks sent to
+    the generic kernel, a corrupt payload byte caught with the oracle's message."""
+    inner_last = row // dsize
     shape = [13, 24, inner_last * 7 + inner_last // 2]
     meta = A.make_meta(shape, [8, 8, inner_last * 5], dsize, endian=A.ZH_ENDIAN_BIG,
                        sharded=True, inner_chunk_shape=[4, 8, inner_last],
@@ -571,10 +567,10 @@ def test_grouped_row_decode(dev, monkeypatch, crc, dsize, group):
 @pytest.mark.parametrize("dsize", [1, 4, 8])
 @pytest.mark.parametrize("crc", [False, True])
 def test_lane_exchange_row_decode(dev, monkeypatch, dsize, inner_rows, crc):
-    """rows_xpose_kernel in the decode direction (ZH_DEC_RGROUP=8): copies beside Q1 zero-fill
-    items and a missing shard's fill inside one group of 8 chunks, row-clipped boundary chunks
-    on the generic kernel, partial regions; the fused-CRC and 15-row chains fall back."""
-    monkeypatch.setenv("ZH_DEC_RGROUP", "8")
+    """rows_xpose_kernel in the decode direction (128-B rows without the chunk CRC): copies
+    beside Q1 zero-fill items and a missing shard's fill inside one group of 8 chunks,
+    row-clipped boundary chunks on the generic kernel, partial regions; the fused-CRC and
+    15-row chains fall back."""
     L = 128 // dsize
     a, b = inner_rows
     shape = [a * 3 + 1, b * 3, L * 9 + L // 2]
@@ -596,14 +592,12 @@ def test_lane_exchange_row_decode(dev, monkeypatch, dsize, inner_rows, crc):
 
 
 @pytest.mark.parametrize("order", [[0, 3, 2, 1], [0, 1, 3, 2]])
-@pytest.mark.parametrize("group", ["-1", "0", "1", "2", "4"])
-def test_tile_encode_chunk_crc_fused(dev, monkeypatch, order, group):
+def test_tile_encode_chunk_crc_fused(dev, monkeypatch, order):
     """c4crc-shaped chain at small extent: [transpose, bytes(big), crc32c] with 32x32 tiles,
     the chunk CRC fused into the tile encode (stored vectors, per-unit end shifts from the
     payload side of the table), boundary chunks through the slow list + CRC pass; equals the
-    oracle and the unfused pass, and decodes back.  ZH_ENC_TGROUP: the grouped tile encode
-    (the unit fold step for 8/G units), or the ungrouped kernel (0)."""
-    monkeypatch.setenv("ZH_ENC_TGROUP", group)
+    oracle and the unfused pass, and decodes back (the grouped tile encode: the unit fold step
+    for 4 units)."""
     shape = [1, 64, 80, 96]
     meta = A.make_meta(shape, [1, 64, 64, 64], 4, endian=A.ZH_ENDIAN_BIG, sharded=True,
                        inner_chunk_shape=[1, 32, 32, 32], transpose_order=order,
@@ -746,8 +740,8 @@ def test_chunk_crc32c_fused_row_kernel(dev, monkeypatch, piece_kb, fuse):
 
 @pytest.mark.parametrize("mode", ["rows", "tiles", "rows_crc"])
 def test_item_permutation_order(dev, monkeypatch, mode):
-    """ZH_ITEM_PERM=1 (fast kernels walk items in a coprime-stride order): same bytes."""
-    monkeypatch.setenv("ZH_ITEM_PERM", "1")
+    """Chunks cut into 16 KiB pieces, walked in the golden-ratio item order by the fast
+    kernels: same bytes."""
     monkeypatch.setenv("ZH_PIECE_KB", "16")
     shape = [64, 64, 96]
     kw = dict(endian=A.ZH_ENDIAN_BIG, sharded=True, inner_chunk_shape=[16, 32, 32])
@@ -1014,7 +1008,6 @@ def test_grouped_row_crc_decode_misaligned(dev, monkeypatch):
     payloads after each 4-byte crc32c, the same bytes as the oracle and a corrupt payload byte
     reported alike."""
     monkeypatch.setenv("ZH_SMALL_SPLIT", "0")  # whole chunks: the grouped kernel needs them
-    monkeypatch.delenv("ZH_DEC_RGROUP", raising=False)
     shape = [64, 64, 96]
     meta = A.make_meta(shape, [32, 64, 64], 4, endian=A.ZH_ENDIAN_BIG, sharded=True,
                        inner_chunk_shape=[32, 32, 32], inner_crc32c=True)

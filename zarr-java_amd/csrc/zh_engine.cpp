@@ -642,8 +642,6 @@ int64_t assign_crc_spans(std::vector<CrcJob>& jobs, int cu_count, int* shift) {
   int64_t small = 0;
   for (const CrcJob& J : jobs) small += (J.len + kIdxSpan - 1) / kIdxSpan;
   *shift = small >= 4 * (int64_t)cu_count ? 4 : 0;
-  const int force = env_int("ZH_CRC_SHIFT", -1);  // A/B: 4 KiB << force per workgroup (0-4)
-  if (force >= 0 && force <= 4) *shift = force;
   const int64_t span = (int64_t)kIdxSpan << *shift;
   int64_t spans = 0;
   for (CrcJob& J : jobs) {
@@ -654,8 +652,7 @@ int64_t assign_crc_spans(std::vector<CrcJob>& jobs, int cu_count, int* shift) {
 }
 
 int grid_for(const zh_ctx* ctx, int64_t total_items) {
-  const int per_cu = std::max(1, env_int("ZH_BLOCKS_PER_CU", 256));
-  int64_t g = (int64_t)ctx->cu_count * per_cu;
+  int64_t g = (int64_t)ctx->cu_count * 256;  // grid-stride kernels: 256 workgroups per CU
   return (int)std::max<int64_t>(1, std::min<int64_t>(g, total_items));
 }
 
@@ -711,7 +708,6 @@ struct HeldPieces {
 // "Could not load byte data").  Returns false when the part references over 90 % of the
 // shard: the whole object is copied then.
 bool compact_pieces(const zh_array_meta* m, const DevShard& S, int64_t isz, HeldPieces& hp) {
-  if (!env_int("ZH_COMPACT", 1)) return false;  // A/B switch: whole-shard staging
   int64_t lo[kMaxDims], hi[kMaxDims];
   for (int d = 0; d < m->ndim; d++) {
     lo[d] = S.part_lo[d];
@@ -1271,7 +1267,7 @@ int plan_create(zh_ctx* ctx, const zh_array_meta* m, const SrcDesc* srcs, int64_
            (p->args.inner_nbytes >> (p->args.piece_shift + 1)) % 4096 == 0)
       p->args.piece_shift++;
   std::vector<uint32_t> tab = setup_fast(m, p->args, p->tile_mode);
-  p->args.tile_variant = std::min(1, std::max(0, env_int("ZH_TILE_VARIANT", 1)));
+  p->args.tile_variant = 1;  // the row-interleaved per-chunk tile kernel unless grouped below
   // Chunk CRC fused into the row-interleaved tile kernel: every payload byte of a fast item
   // is loaded exactly once by some lane, and each lane's share is shifted to the payload end
   // by K[u] = x^(8(L − E_u)) (E_u = end of unit u's last row, appended to the table) and a
@@ -1417,14 +1413,14 @@ int plan_create(zh_ctx* ctx, const zh_array_meta* m, const SrcDesc* srcs, int64_
   // allocation (profiles/placement_perm.py); on the row paths it evens out where the output
   // lands — half-array c2 into three hipMalloc outputs: 18.10 / 16.14 / 16.13 → 16.45 / 16.03 /
   // 16.03 ms, c3 19.16 / 18.42 / 17.33 → 19.62 / 16.87 / 16.52 ms (round 5,
-  // profiles/r05/perm/) — so on by default for every decode fast path.  ZH_ITEM_PERM=0 turns
-  // it off.
-  p->args.item_mul = env_int("ZH_ITEM_PERM", 1) ? golden_item_mul(p->args.total_items) : 0;
+  // profiles/r05/perm/) — so every decode fast path uses it (the switch that turned it off
+  // was removed in round 6).
+  p->args.item_mul = golden_item_mul(p->args.total_items);
   p->slow_grid = p->grid;
   // The tile decode over G consecutive (z-adjacent) chunks per work item, the next step's
   // loads issued before this step's stores (tiles_group_kernel; tile_variant 20 + G): c4
   // 33.4 → 32.9 ms (G = 4), interleaved A/B in profiles/r02/experiments/ab_r02abdtgpf*.txt.
-  // ZH_DEC_TGROUP = G (0: the row-interleaved per-chunk tile kernel; 1, 2, 4, 8).
+  // G = 4 (round 6 removed the switch and the other group sizes of this direction).
   //
   // With the fused chunk CRC: tiles_rowcrc_kernel, one chunk per work item (tile_variant 51:
   // every lane also CRCs one payload row from the LDS tiles, 16 lookups per 16-B vector):
@@ -1433,20 +1429,18 @@ int plan_create(zh_ctx* ctx, const zh_array_meta* m, const SrcDesc* srcs, int64_
   // tables); their A/B records stay under profiles/.
   {
     const bool crc = p->args.crc_fused != 0;
-    const int G = crc ? 1 : env_int("ZH_DEC_TGROUP", 4);
+    const int G = crc ? 1 : 4;
     const bool rowcrc_ok = !crc || zh::rowcrc_lds_at_zero();
-    if ((G == 1 || G == 2 || G == 4 || G == 8) && rowcrc_ok && p->tile_mode &&
-        p->args.fast_mode == kFastTileTable && p->args.tile_variant == 1 &&
-        (!crc || tile_crc) && p->args.piece_shift == 0 && items > 0 &&
-        (!crc || env_int("ZH_DEC_TGROUP", 1) != 0)) {
+    if (rowcrc_ok && p->tile_mode && p->args.fast_mode == kFastTileTable &&
+        (!crc || tile_crc) && p->args.piece_shift == 0 && items > 0) {
       const int64_t groups = (items + G - 1) / G;
       p->args.tile_variant = crc ? 51 : 20 + G;
       // Aligned windows for the row-CRC kernel: every payload after a 4-byte crc32c starts at
       // 4·i mod 128, so a 1 KiB wave load of it touched 9 lines and the shared line was
       // fetched twice.  When unit u's rows start at 32u elements and row r + 1 follows row r
       // (the payload is [32 rows][units][32 words], c4's layout), the movers load 128-B aligned
-      // lines and route each word to its tile in LDS (ZH_DEC_ALIGN=0: off).
-      if (crc && env_int("ZH_DEC_ALIGN", 1) != 0) {
+      // lines and route each word to its tile in LDS; other layouts keep the unaligned loads.
+      if (crc) {
         const ScatterArgs& g = p->args;
         const int64_t nu = g.fast_n;
         // [32 rows][nu units][32 words], 2-4 steps of 8 units (K fits the kernel's K area),
@@ -1462,21 +1456,19 @@ int plan_create(zh_ctx* ctx, const zh_array_meta* m, const SrcDesc* srcs, int64_
         p->args.tile_ystride = al ? (int64_t)ys : 0;
       }
       if (crc) p->args.crc_tile_step = tile_crc_step(ends, (size_t)(8 / G));
-      p->args.item_mul = env_int("ZH_ITEM_PERM", 1) ? golden_item_mul(groups) : 0;
+      p->args.item_mul = golden_item_mul(groups);
       p->grid = grid_for(ctx, groups);
     }
   }
   // The row decode over G consecutive chunks per work item (rows_group_kernel, narrow rows:
-  // G·row bytes of a region row per wave store).  ZH_DEC_RGROUP: 0 off, -1 G·row = 256 B,
-  // or G (1, 2, 4; 8 = rows_xpose_kernel: 128-B rows, 8 chunks, 1 KiB contiguous on both
-  // sides through an LDS lane exchange).  Row-clipped items then take the generic kernel
-  // (is_fast).  Default: with the fused chunk CRC -1 (c3crc 37.2 → 35.9 ms); without it, 8 for
-  // 128-B rows (c3, quarter array: 8.71 → 8.49 ms, profiles/r02/experiments/ab_xpose_c3.json)
-  // and off otherwise (plain c3 with G = 2: 33.2 → 33.5 ms, profiles/r02/experiments/
-  // ab_r02drg_*.txt).
+  // G·row bytes of a region row per wave store).  With the fused chunk CRC, G·row = 256 B
+  // (c3crc 37.2 → 35.9 ms); without it, 128-B rows take rows_xpose_kernel (8 chunks, 1 KiB
+  // contiguous on both sides through an LDS lane exchange; c3, quarter array: 8.71 → 8.49 ms,
+  // profiles/r02/experiments/ab_xpose_c3.json) and other rows the per-chunk row kernel (plain
+  // c3 with G = 2: 33.2 → 33.5 ms, profiles/r02/experiments/ab_r02drg_*.txt).  Row-clipped
+  // items then take the generic kernel (is_fast).
   {
-    const int want = env_int("ZH_DEC_RGROUP", p->args.crc_fused ? -1
-                                              : p->args.fast_vpr_shift == 3 ? 8 : 0);
+    const int want = p->args.crc_fused ? -1 : p->args.fast_vpr_shift == 3 ? 8 : 0;
     const ScatterArgs& g = p->args;
     if (want != 0 && !p->tile_mode && (g.fast_mode == kFastRowArith || g.fast_mode == kFastRowTable) &&
         g.piece_shift == 0 && items > 0) {
@@ -1487,7 +1479,7 @@ int plan_create(zh_ctx* ctx, const zh_array_meta* m, const SrcDesc* srcs, int64_
       if (G >= 1 && (xpose || (G << g.fast_vpr_shift) <= 64)) {
         const int64_t groups = (items + G - 1) / G;
         p->args.row_group = G;
-        p->args.item_mul = env_int("ZH_ITEM_PERM", 1) ? golden_item_mul(groups) : 0;
+        p->args.item_mul = golden_item_mul(groups);
         p->grid = grid_for(ctx, groups);
       }
     }
@@ -1564,7 +1556,7 @@ int plan_enqueue_impl(zh_plan* p, void* out, hipStream_t s) {
     ZH_HIP(launch_resolve(a, s));
     if (p->d_dcrc) ZH_HIP(launch_data_crc_partial(p->dcrc, p->dcrc_grid, s));
     if (p->timing) ZH_HIP(hipEventRecord(ev[1], s));
-    ZH_HIP(launch_scatter(a, p->meta.dtype_size, p->tile_mode, 0, p->grid, s));
+    ZH_HIP(launch_scatter(a, p->meta.dtype_size, p->grid, s));
     ZH_HIP(launch_decode_slow(a, p->slow_grid, p->idx_crc_fused ? crc : CrcIdxArgs{}, s));
   }
   if (p->d_dcrc) ZH_HIP(launch_data_crc_finalize(p->dcrc, s));
@@ -1816,8 +1808,7 @@ namespace zh {
 // context's page-locked buffer as one DMA and leaves it by one memcpy after the wait, instead
 // of the runtime's staged pageable copy.  Null: write to `out` directly.
 static uint8_t* hout_stage(zh_ctx* ctx, const void* out, int64_t nbytes, uint32_t flags) {
-  if ((flags & ZH_OUT_DEVICE) || nbytes <= 0 || nbytes > kHoutPinBytes || ctx->hout_pin_failed ||
-      env_int("ZH_HOUT_PIN", 1) == 0)
+  if ((flags & ZH_OUT_DEVICE) || nbytes <= 0 || nbytes > kHoutPinBytes || ctx->hout_pin_failed)
     return nullptr;
   unsigned int hf = 0;
   if (hipHostGetFlags(&hf, const_cast<void*>(out)) == hipSuccess) return nullptr;  // pinned
@@ -1894,12 +1885,10 @@ int zh_array_read(zh_ctx* ctx, const zh_array_meta* meta, const zh_chunk_src* ch
 namespace {
 // Peer access from device `from` to device `to` (once per pair per process), so that the
 // slab copies to the root device go device to device over xGMI and kernels on `from` may
-// read `to`'s memory.  Returns false when the pair has no peer access (or ZH_MULTI_PEER=0):
-// the caller then stages through host memory.
+// read `to`'s memory.  Returns false when the pair has no peer access: the caller then stages
+// through host memory (ZH_MULTI_FORCE_STAGED=1 takes that route for every pair).
 bool enable_peer(int from, int to) {
   if (from == to) return true;
-  const char* env = getenv("ZH_MULTI_PEER");
-  if (env && env[0] == '0') return false;
   static std::mutex mu;
   static std::vector<std::pair<std::pair<int, int>, bool>> done;
   std::lock_guard<std::mutex> lk(mu);
@@ -2306,56 +2295,6 @@ int64_t zh_array_encoded_bound(const zh_array_meta* m) {
   return bound;
 }
 
-// Crc32cCodec.encode (:50-60) of every written chunk payload (inner crc32c), on the device:
-// the data-CRC pass in store mode over descriptors of the kept chunks.
-static int store_chunk_crcs(zh_ctx* ctx, const ScatterArgs& a, const std::vector<DevShard>& hs,
-                            const std::vector<int64_t>& hoff, const zh_chunk_dst* dsts,
-                            int64_t ncoords, int64_t nit, int64_t items, hipStream_t s,
-                            char* err, size_t errlen) {
-  std::vector<ItemDesc> wd((size_t)items);
-  for (int64_t i = 0; i < ncoords; i++) {
-    for (int64_t k = 0; k < nit; k++) {
-      ItemDesc& D = wd[(size_t)(hs[i].item_begin + k)];
-      memset(&D, 0, sizeof(D));
-      D.kind = kDescSkip;
-      const int64_t o = hoff[(size_t)(hs[i].item_begin + k)];
-      if (o < 0 || dsts[i].nbytes == 0) continue;
-      D.kind = kDescFullCopy;
-      D.src = (uint64_t)(uintptr_t)((uint8_t*)dsts[i].data + o);
-      D.shard = (uint32_t)i;
-    }
-  }
-  const int64_t nspan = (a.inner_nbytes + kCrcSpan - 1) / kCrcSpan;
-  ItemDesc* d_wd = nullptr;
-  uint32_t* d_part = nullptr;
-  int st;
-  if ((st = dev_alloc(&d_wd, wd.size(), err, errlen)) != ZH_OK ||
-      (st = dev_alloc(&d_part, (size_t)(items * nspan), err, errlen)) != ZH_OK) {
-    (void)hipFree(d_wd);
-    return st;
-  }
-  DataCrcArgs D{};
-  D.desc = d_wd;
-  D.n_items = items;
-  D.len = a.inner_nbytes;
-  D.span = kCrcSpan;
-  D.nspan = (int32_t)nspan;
-  D.store = 1;
-  D.partials = d_part;
-  hipError_t e1 = hipMemcpyAsync(d_wd, wd.data(), wd.size() * sizeof(ItemDesc),
-                                 hipMemcpyHostToDevice, s);
-  if (e1 == hipSuccess)
-    e1 = launch_data_crc(D, (int)std::min<int64_t>(items * nspan, (int64_t)ctx->cu_count * 32), s);
-  if (e1 == hipSuccess) e1 = hipStreamSynchronize(s);
-  (void)hipFree(d_wd);
-  (void)hipFree(d_part);
-  if (e1 != hipSuccess) {
-    set_err(err, errlen, "HIP error %s (%s)", hipGetErrorName(e1), hipGetErrorString(e1));
-    return ZH_EHIP;
-  }
-  return ZH_OK;
-}
-
 constexpr int kWriteFallback = -1;
 
 // zh_array_write in one pass over the region (single-level chains): the layout assumes every
@@ -2648,38 +2587,34 @@ static int array_write_fast(zh_ctx* ctx, const zh_array_meta* m, ScatterArgs a,
   v.fast_tab = (uint32_t*)(W + o_tab);
   // golden-ratio visit order and (uint32 rows) 8 rows in flight per lane: +2.4 % on c3, the
   // order +4 % on c4 (interleaved A/B, profiles/tune_write.py → profiles/r01/experiments/)
-  v.item_mul = env_int("ZH_ITEM_PERM", 1) ? golden_item_mul(pitems) : 0;
+  v.item_mul = golden_item_mul(pitems);
   v.crc_fused = crc_fuse ? 1 : 0;
   v.crc_partials = (uint32_t*)(W + o_cpart);
   if (crc_fuse)
     ZH_HIPF(hipMemsetAsync(W + o_cpart, 0, (size_t)(items * nspan) * sizeof(uint32_t), s));
   v.nt = 3;  // non-temporal region loads and payload stores (launch_encode_fast_ds)
   // narrow rows: G consecutive chunks per work item so a wave load covers G·row bytes of a
-  // region row (ZH_ENC_GROUP: 0 off, default G·row = 256 B; rows_group_kernel, 4 rows in
-  // flight per lane; c3 write G × U grid in profiles/r02/write/ab_enc3.txt: G = 2, U = 4 best,
-  // 40.1 → 36.2 ms)
+  // region row (G·row = 256 B; rows_group_kernel, 4 rows in flight per lane; c3 write G × U
+  // grid in profiles/r02/write/ab_enc3.txt: G = 2, U = 4 best, 40.1 → 36.2 ms)
   int group = 0;
   // (not nested: c3nest measured 42 → 48 ms grouped, profiles/r02/write/ab_enc.txt)
   // (with the chunk CRC fused: rows sequential in the payload, checked above; whole chunks)
   if ((v.fast_mode == kFastRowArith || v.fast_mode == kFastRowTable) && a.piece_shift == 0 &&
-      (!nz.cell || env_int("ZH_ENC_GROUP", -1) > 0)) {
-    const int want = env_int("ZH_ENC_GROUP", -1);
-    int G = want >= 0 ? want : (16 >> std::min(v.fast_vpr_shift, 5));
+      !nz.cell) {
+    int G = 16 >> std::min(v.fast_vpr_shift, 5);
     G = G >= 8 ? 8 : G >= 4 ? 4 : G >= 2 ? 2 : G;
     if (crc_fuse && G > 4) G = 4;  // the CRC variants: G 1, 2, 4
     if (G && (G << v.fast_vpr_shift) <= 64) group = G;
   }
-  // tiles (uint32 transposed chunks): G chunks per work item, 8/G tiles of each per step
-  // (ZH_ENC_TGROUP: 0 off; tiles_group_kernel).  With the tile CRC fused, the kernel folds
-  // each lane's units (8/G apart) with the step for that stride.
+  // tiles (uint32 transposed chunks): 2 chunks per work item, 4 tiles of each per step
+  // (tiles_group_kernel; 1 and 4 measured slower, profiles/r02/write/ab_tenc.txt).  With the
+  // tile CRC fused, the kernel folds each lane's units (4 apart) with the step for that stride.
   if (v.fast_mode == kFastTileTable && (!crc_fuse || tile_crc) && a.piece_shift == 0 &&
-      (!nz.cell || env_int("ZH_ENC_TGROUP", -1) > 0)) {
-    const int want = env_int("ZH_ENC_TGROUP", -1);
-    const int G = want < 0 ? 2 : want;
-    if (G == 1 || G == 2 || G == 4) group = G;
-    if (group && tile_crc) v.crc_tile_step = tile_crc_step(tile_ends, (size_t)(8 / group));
+      !nz.cell) {
+    group = 2;
+    if (tile_crc) v.crc_tile_step = tile_crc_step(tile_ends, (size_t)(8 / group));
   }
-  if (group) v.item_mul = env_int("ZH_ITEM_PERM", 1) ? golden_item_mul((items + group - 1) / group) : 0;
+  if (group) v.item_mul = golden_item_mul((items + group - 1) / group);
   const int grid = grid_for(ctx, group ? (items + group - 1) / group : pitems);
   ZH_HIPF(launch_encode_fast(v, grid, group, s));
   ZH_HIPF(launch_encode_slow(a, grid, s));
@@ -2784,7 +2719,7 @@ int zh_array_write(zh_ctx* ctx, const zh_array_meta* m, const void* src, const i
     S.out_base = ob;
     items += c.sharded ? cps_total : 1;
   }
-  if (env_int("ZH_ENC_FAST", 1) != 0) {
+  {
     a.region = (uint8_t*)src;
     std::vector<uint8_t> flags;
     st = array_write_fast(ctx, m, a, hs, items, tile_mode, dsts, nullptr, &flags, s, err, errlen);
@@ -2827,205 +2762,6 @@ int zh_array_write(zh_ctx* ctx, const zh_array_meta* m, const void* src, const i
     for (size_t j = 0; j < which.size(); j++) dsts[which[j]].nbytes = d2[j].nbytes;
     return st;
   }
-  // ZH_ENC_FAST=0: the independent flags → host layout → encode path (kept as a cross-check)
-  const int64_t pitems = items << a.piece_shift;
-  DevShard* d_shards = nullptr;
-  uint8_t* d_flags = nullptr;
-  int64_t* d_off = nullptr;
-  auto cleanup = [&]() {
-    (void)hipFree(d_shards);
-    (void)hipFree(d_flags);
-    (void)hipFree(d_off);
-  };
-  if ((st = dev_alloc(&d_shards, hs.size(), err, errlen)) != ZH_OK ||
-      (st = dev_alloc(&d_flags, (size_t)pitems, err, errlen)) != ZH_OK ||
-      (st = dev_alloc(&d_off, (size_t)items, err, errlen)) != ZH_OK) {
-    cleanup();
-    return st;
-  }
-#define ZH_HIPC(call)                                                                      \
-  do {                                                                                     \
-    hipError_t e_ = (call);                                                                \
-    if (e_ != hipSuccess) {                                                                \
-      set_err(err, errlen, "HIP error %s (%s)", hipGetErrorName(e_), hipGetErrorString(e_)); \
-      cleanup();                                                                           \
-      return ZH_EHIP;                                                                      \
-    }                                                                                      \
-  } while (0)
-  ZH_HIPC(hipMemcpy(d_shards, hs.data(), hs.size() * sizeof(DevShard), hipMemcpyHostToDevice));
-  a.shards = d_shards;
-  a.nshards = ncoords;
-  a.total_items = pitems;
-  a.region = (uint8_t*)src;
-  a.flags = d_flags;
-  a.item_off = nullptr;
-  const int grid = grid_for(ctx, pitems);
-  ZH_HIPC(launch_flags(a, m->dtype_size, grid, s));
-  std::vector<uint8_t> hflags((size_t)pitems);
-  ZH_HIPC(hipMemcpyAsync(hflags.data(), d_flags, (size_t)pitems, hipMemcpyDeviceToHost, s));
-  ZH_HIPC(hipStreamSynchronize(s));
-  if (a.fill_never) std::fill(hflags.begin(), hflags.end(), (uint8_t)1);  // a NaN fill
-  // layout: C-order over the non-fill inner chunks (deterministic)
-  const int64_t isz = c.sharded ? zh_shard_index_size(m) : 0;
-  const int start = c.sharded && c.index_location == ZH_INDEX_START;
-  const int big = c.index_endian == ZH_ENDIAN_BIG;
-  std::vector<int64_t> hoff((size_t)items, -1);
-  std::vector<std::vector<uint8_t>> indexes(ncoords);
-  struct SubIndex {  // nested: a sub-shard index, kept alive until the stream syncs
-    int64_t shard, pos;
-    std::vector<uint8_t> bytes;
-  };
-  std::vector<SubIndex> sub_indexes;
-  const int64_t np = 1ll << a.piece_shift;
-  auto put_entry = [](uint8_t* e, uint64_t eo, uint64_t en, bool be) {
-    for (int byte = 0; byte < 8; byte++) {
-      const int sh = be ? 56 - 8 * byte : 8 * byte;
-      e[byte] = (uint8_t)(eo >> sh);
-      e[8 + byte] = (uint8_t)(en >> sh);
-    }
-  };
-  for (int64_t i = 0; i < ncoords; i++) {
-    const int64_t nit = c.sharded ? cps_total : 1;
-    const int64_t b = hs[i].item_begin;
-    int64_t payload = 0, nonfill = 0;
-    std::vector<uint8_t>& idx = indexes[i];
-    if (c.sharded) idx.assign((size_t)isz, 0);
-    auto leaf_any = [&](int64_t k) {
-      bool any = false;
-      for (int64_t q = 0; q < np; q++) any |= hflags[(size_t)(((b + k) << a.piece_shift) + q)] != 0;
-      return any;
-    };
-    if (c.sharded && c.nested) {
-      // level-1 cells in C order, each a sub-shard (ShardingIndexedCodec.encode of the level-2
-      // codec, :105-168): its non-fill leaves in C order + its own index (+crc32c); an
-      // all-fill cell is elided at level 1 (-1, -1)
-      int64_t g1[kMaxDims], r[kMaxDims], fstr[kMaxDims], ncell = 1, cps2 = 1;
-      for (int d = 0; d < n; d++) {
-        g1[d] = m->chunk_shape[d] / c.inner_chunk_shape[d];
-        r[d] = c.inner_chunk_shape[d] / inner[d];
-        ncell *= g1[d];
-        cps2 *= r[d];
-      }
-      int64_t sf = 1;
-      for (int d = n - 1; d >= 0; d--) {
-        fstr[d] = sf;
-        sf *= m->chunk_shape[d] / inner[d];
-      }
-      const int64_t sub_isz = 16 * cps2 + (c.nested_index_has_crc32c ? 4 : 0);
-      const bool sub_start = c.nested_index_location == ZH_INDEX_START;
-      const bool sub_be = c.nested_index_endian == ZH_ENDIAN_BIG;
-      int64_t pos = start ? isz : 0;
-      std::vector<int64_t> ks((size_t)cps2);
-      for (int64_t cell = 0; cell < ncell; cell++) {
-        int64_t c1[kMaxDims], q = cell;
-        for (int d = n - 1; d >= 0; d--) {
-          c1[d] = q % g1[d];
-          q /= g1[d];
-        }
-        bool any_cell = false;
-        for (int64_t k2 = 0; k2 < cps2; k2++) {
-          int64_t f = 0, t = k2;
-          for (int d = n - 1; d >= 0; d--) {
-            f += (c1[d] * r[d] + t % r[d]) * fstr[d];
-            t /= r[d];
-          }
-          ks[(size_t)k2] = f;
-          any_cell |= leaf_any(f);
-        }
-        if (!any_cell) {
-          put_entry(&idx[16 * cell], ~0ull, ~0ull, big);
-          continue;
-        }
-        const int64_t sub_pos = pos;
-        int64_t leaf_pos = pos + (sub_start ? sub_isz : 0);
-        std::vector<uint8_t> sidx((size_t)sub_isz, 0);
-        for (int64_t k2 = 0; k2 < cps2; k2++) {
-          const int64_t f = ks[(size_t)k2];
-          if (leaf_any(f)) {
-            hoff[b + f] = leaf_pos;
-            put_entry(&sidx[16 * k2], (uint64_t)(leaf_pos - sub_pos),
-                      (uint64_t)(a.inner_nbytes + a.crc_extra), sub_be);
-            leaf_pos += a.inner_nbytes + a.crc_extra;
-            nonfill++;
-          } else {
-            put_entry(&sidx[16 * k2], ~0ull, ~0ull, sub_be);
-          }
-        }
-        if (c.nested_index_has_crc32c) {
-          const uint32_t crc = crc32c_host(0, sidx.data(), (size_t)(sub_isz - 4));
-          for (int byte = 0; byte < 4; byte++) sidx[sub_isz - 4 + byte] = (uint8_t)(crc >> (8 * byte));
-        }
-        const int64_t sidx_pos = sub_start ? sub_pos : leaf_pos;
-        const int64_t sub_len = leaf_pos - sub_pos + (sub_start ? 0 : sub_isz);
-        put_entry(&idx[16 * cell], (uint64_t)sub_pos, (uint64_t)sub_len, big);
-        sub_indexes.push_back({i, sidx_pos, std::move(sidx)});
-        pos = sub_pos + sub_len;
-      }
-      payload = pos - (start ? isz : 0);
-    }
-    for (int64_t k = 0; k < nit && !(c.sharded && c.nested); k++) {
-      bool any = false;
-      for (int64_t q = 0; q < np; q++) any |= hflags[(size_t)(((b + k) << a.piece_shift) + q)] != 0;
-      uint64_t eo = ~0ull, en = ~0ull;
-      if (any) {
-        hoff[b + k] = (start ? isz : 0) + payload;
-        eo = (uint64_t)hoff[b + k];
-        en = (uint64_t)(a.inner_nbytes + a.crc_extra);
-        payload += a.inner_nbytes + a.crc_extra;
-        nonfill++;
-      }
-      if (c.sharded) {
-        for (int byte = 0; byte < 8; byte++) {
-          const int sh = big ? 56 - 8 * byte : 8 * byte;
-          idx[16 * k + byte] = (uint8_t)(eo >> sh);
-          idx[16 * k + 8 + byte] = (uint8_t)(en >> sh);
-        }
-      }
-    }
-    if (nonfill == 0) {  // all fill → writeChunk deletes the key (M/core/Array.java:150-151)
-      dsts[i].nbytes = 0;
-      continue;
-    }
-    const int64_t total = payload + isz;
-    if (total > dsts[i].capacity || !dsts[i].data) {
-      set_err(err, errlen, "chunk destination %lld too small: need %lld bytes, have %lld",
-              (long long)i, (long long)total, (long long)dsts[i].capacity);
-      cleanup();
-      return ZH_EINVAL;
-    }
-    dsts[i].nbytes = total;
-    if (c.sharded && c.nested) {
-      for (auto& si : sub_indexes)
-        if (si.shard == i)
-          ZH_HIPC(hipMemcpyAsync((uint8_t*)dsts[i].data + si.pos, si.bytes.data(), si.bytes.size(),
-                                 hipMemcpyHostToDevice, s));
-    }
-    if (c.sharded) {
-      if (c.index_has_crc32c) {  // Crc32cCodec.encode :50-60
-        const uint32_t crc = crc32c_host(0, idx.data(), (size_t)(isz - 4));
-        for (int byte = 0; byte < 4; byte++) idx[isz - 4 + byte] = (uint8_t)(crc >> (8 * byte));
-      }
-      uint8_t* dst = (uint8_t*)dsts[i].data + (start ? 0 : payload);
-      ZH_HIPC(hipMemcpyAsync(dst, idx.data(), (size_t)isz, hipMemcpyHostToDevice, s));
-    }
-  }
-  ZH_HIPC(hipMemcpyAsync(d_off, hoff.data(), (size_t)items * sizeof(int64_t),
-                         hipMemcpyHostToDevice, s));
-  a.item_off = d_off;
-  a.flags = nullptr;
-  ZH_HIPC(launch_scatter(a, m->dtype_size, tile_mode, 1, grid, s));
-  if (c.inner_crc32c) {  // Crc32cCodec.encode (:50-60) of every written payload, on the device
-    st = store_chunk_crcs(ctx, a, hs, hoff, dsts, ncoords, c.sharded ? cps_total : 1, items, s,
-                          err, errlen);
-    if (st != ZH_OK) {
-      cleanup();
-      return st;
-    }
-  }
-  ZH_HIPC(hipStreamSynchronize(s));
-  cleanup();
-#undef ZH_HIPC
-  return ZH_OK;
 }
 
 int zh_array_write_host(zh_ctx* ctx, const zh_array_meta* m, const void* src_host,
@@ -3097,7 +2833,6 @@ struct ScatterAlloc {
 };
 std::mutex g_scatter_mu;
 std::map<void*, ScatterAlloc> g_scatter;
-std::vector<std::pair<void*, size_t>> g_va_retired;  // lab switch ZH_SCATTER_RETIRE only
 // Every virtual range a scatter allocation or view ever used, [begin, end), and reservations
 // set aside because they overlapped one.  ROCm 7.2 did not drop the device's translations of a
 // freed range: a later range reserved over it and mapped to other chunks was partly written
@@ -3308,11 +3043,6 @@ bool scatter_free(void* ptr) {
   scatter_unmap(ptr, A);
   if (!A.view)
     for (auto h : A.handles) (void)hipMemRelease(h);
-  if (env_int("ZH_SCATTER_RETIRE", 0)) {  // lab switch: keep the range reserved
-    std::lock_guard<std::mutex> lk(g_scatter_mu);
-    g_va_retired.emplace_back(ptr, A.size);
-    return true;
-  }
   (void)hipMemAddressFree(ptr, A.size);
   (void)hipGetLastError();
   return true;
@@ -3360,11 +3090,11 @@ int write_rate(hipStream_t s, void* ptr, size_t bytes, int pattern, int reps, do
 // ZH_MALLOC_CALIBRATE: the write rate of a large scatter arena is set by which physical chunks
 // it got (not their order, not its virtual address), and a contiguous store probe predicts
 // the decode's rate into it (profiles/r02/placement/calib*.jsonl).  Allocate up to
-// ZH_CALIB_TRIES candidates (default 2) while holding the earlier ones, so the driver hands out
+// two candidates, holding the first while allocating the second, so the driver hands out
 // different chunks, probe each, keep the fastest.  A candidate that does not fit ends the
 // search.  On return *out is the kept allocation, with every probe recorded on it.
 void scatter_calibrate(zh_ctx* ctx, size_t bytes, void** out) {
-  const int tries = std::max(1, env_int("ZH_CALIB_TRIES", 2));
+  const int tries = 2;
   std::vector<void*> cand{*out};
   std::vector<double> rate;
   for (int k = 0;; k++) {

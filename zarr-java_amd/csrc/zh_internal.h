@@ -286,8 +286,7 @@ extern std::atomic<int64_t> g_last_fast_path;  // diagnostic, zh_debug_last_fast
 extern std::atomic<int64_t> g_last_encode_path;
 bool rowcrc_lds_at_zero();  // the row-CRC tile kernels have no static LDS
 constexpr int kAlnUnitsMax = 32;  // tiles_rowcrc_aln_kernel: units per chunk (its K capacity)
-hipError_t launch_scatter(const ScatterArgs& a, int dsize, int tile_mode, int encode, int grid,
-                          hipStream_t stream);
+hipError_t launch_scatter(const ScatterArgs& a, int dsize, int grid, hipStream_t stream);
 // the slow list; with crc.nspans > 0 the index crc32c runs in the same launch (first
 // crc.nspans workgroups) instead of launch_crc ahead of the resolve kernel
 hipError_t launch_decode_slow(const ScatterArgs& a, int grid, const CrcIdxArgs& crc,
@@ -295,7 +294,6 @@ hipError_t launch_decode_slow(const ScatterArgs& a, int grid, const CrcIdxArgs& 
 // small plans: resolve + decode of every item in one launch (with the index CRC as above)
 hipError_t launch_decode_small(const ScatterArgs& a, int grid, const CrcIdxArgs& crc,
                                hipStream_t stream);
-hipError_t launch_flags(const ScatterArgs& a, int dsize, int grid, hipStream_t stream);
 // write path, one pass: payload offsets + encode-view descriptors + slow list, the fast
 // kernels with the all-fill test, the slow list through the generic encode, then the finish
 // kernel (all-fill count, index entries, chunk-CRC descriptors); launch_crc with

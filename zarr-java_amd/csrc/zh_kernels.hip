@@ -845,56 +845,6 @@ __device__ __forceinline__ void full_item(const ScatterArgs& a, const ItemDesc& 
   }
 }
 
-// Fast tile path (uint32): full 32x32 tiles whose origins come from the LDS table; the next
-// group's global loads are issued before the current group's LDS reads and stores.
-template <int TPB, int NT>
-__device__ __forceinline__ void fast_tiles(const ScatterArgs& a, const uint2* tab,
-                                           const uint8_t* src, uint8_t* dst, uint32_t piece,
-                                           uint32_t (*tile)[32][33]) {
-  const int tid = threadIdx.x, l = tid >> 3, g = tid & 7;
-  const int64_t s_fd = a.pstride[a.fd], d_fs = a.rstride[a.fs];
-  const uint32_t units = (uint32_t)a.fast_n, pieces = 1u << a.piece_shift;
-  const uint32_t u0 = (uint32_t)(((uint64_t)units * piece) / pieces);
-  const uint32_t u1 = (uint32_t)(((uint64_t)units * (piece + 1)) / pieces);
-  uint4 x[TPB];
-#pragma unroll
-  for (int t = 0; t < TPB; t++)
-    if (u0 + t < u1)
-      x[t] = ld16s<(NT & 1) != 0>(src + ((size_t)tab[u0 + t].x + (size_t)l * s_fd + g * 4) * 4);
-  for (uint32_t ub = u0; ub < u1; ub += TPB) {
-#pragma unroll
-    for (int t = 0; t < TPB; t++) {
-      if (ub + t < u1) {
-        uint32_t* row = &tile[t][l][g * 4];
-        row[0] = xform1<4>(x[t].x, a.swap, 0);
-        row[1] = xform1<4>(x[t].y, a.swap, 0);
-        row[2] = xform1<4>(x[t].z, a.swap, 0);
-        row[3] = xform1<4>(x[t].w, a.swap, 0);
-      }
-    }
-    __syncthreads();
-    const uint32_t nb = ub + TPB;
-#pragma unroll
-    for (int t = 0; t < TPB; t++)
-      if (nb + t < u1)
-        x[t] = ld16s<(NT & 1) != 0>(src + ((size_t)tab[nb + t].x + (size_t)l * s_fd + g * 4) * 4);
-#pragma unroll
-    for (int t = 0; t < TPB; t++) {
-      if (ub + t < u1) {
-        uint4 y;
-        y.x = tile[t][g * 4 + 0][l];
-        y.y = tile[t][g * 4 + 1][l];
-        y.z = tile[t][g * 4 + 2][l];
-        y.w = tile[t][g * 4 + 3][l];
-        st16s<(NT & 2) != 0>(dst + ((size_t)tab[ub + t].y + (size_t)l * d_fs + g * 4) * 4, y);
-      }
-    }
-    __syncthreads();
-  }
-}
-
-constexpr int kFastTPB = 4;
-
 // Row-interleaved tile path: a group of 8 tile units whose source rows are adjacent (the
 // table's unit order puts batch-adjacent tiles next to each other, e.g. C4's x-neighbours)
 // is moved so that one wave instruction covers the SAME row of all 8 tiles: lane (t, g)
@@ -1427,7 +1377,7 @@ __global__ __launch_bounds__(kBlock) void rows_group_kernel(ScatterArgs a) {
 // 9.71 ms, and was removed in round 4.)
 constexpr int kXRow = 72;  // 16-B vectors per exchange row (64 + 8)
 
-template <int DS, bool PF>
+template <int DS>
 __global__ __launch_bounds__(kBlock) void rows_xpose_kernel(ScatterArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   uint2* tab = reinterpret_cast<uint2*>(smem);
@@ -1471,10 +1421,9 @@ __global__ __launch_bounds__(kBlock) void rows_xpose_kernel(ScatterArgs a) {
           v[k] = ld16s<true>((const uint8_t*)s + so * DS + col * 16);
       }
     };
-    if (PF) load(wave * 8);
+    load(wave * 8);
 #pragma unroll 1
     for (uint32_t rb = wave * 8; rb < nrows; rb += 32) {
-      if (!PF) load(rb);
 #pragma unroll
       for (int k = 0; k < 8; k++) xw[hi * kXRow + k * 8 + col] = v[k];
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -1486,7 +1435,7 @@ __global__ __launch_bounds__(kBlock) void rows_xpose_kernel(ScatterArgs a) {
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      if (PF && rb + 32 < nrows) load(rb + 32);  // the next step's loads before these stores
+      if (rb + 32 < nrows) load(rb + 32);  // the next step's loads before these stores
 #pragma unroll
       for (int r = 0; r < 8; r++) {  // layout A stores into chunk hi's region rows
         uint64_t so, dof;
@@ -1617,7 +1566,7 @@ __device__ __forceinline__ uint32_t fast_tiles_rows(const ScatterArgs& a, const 
 // origins come from the LDS table.  CRC: the chunk CRC is fused (row-interleaved variant);
 // each wave XORs its lanes' shares, already shifted to the payload end, into the chunk's
 // partial, which data_crc_finalize_kernel compares with the stored value.
-template <int NT, int VARIANT, bool CRC, bool FLAGS>
+template <int NT, bool CRC, bool FLAGS>
 __device__ __forceinline__ void decode_tiles_body(const ScatterArgs& a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   uint2* tab = reinterpret_cast<uint2*>(smem);
@@ -1665,32 +1614,28 @@ __device__ __forceinline__ void decode_tiles_body(const ScatterArgs& a) {
     if (D.kind & kDescFast) {
       const uint8_t* src = (const uint8_t*)(uintptr_t)D.src;
       uint8_t* dst = a.region + D.d0 * 4;
-      if constexpr (VARIANT == 0) {
-        fast_tiles<kFastTPB, NT>(a, tab, src, dst, (uint32_t)pitem(a, item) & pmask, tile);
-      } else {
-        const int64_t pi = pitem(a, item);
-        bool differs = false;
-        const uint32_t share = fast_tiles_rows<NT, CRC, FLAGS>(
-            a, tab, src, dst, (uint32_t)pi & pmask, reinterpret_cast<uint32_t*>(tile), T, S, SD,
-            K, differs);
-        if constexpr (FLAGS) {
-          if (__ballot(differs) != 0 && (threadIdx.x & 63) == 0) a.flags[pi >> a.piece_shift] = 1;
-        }
-        if constexpr (CRC) {
-          uint32_t c = multmodp(kb, share);
+      const int64_t pi = pitem(a, item);
+      bool differs = false;
+      const uint32_t share = fast_tiles_rows<NT, CRC, FLAGS>(
+          a, tab, src, dst, (uint32_t)pi & pmask, reinterpret_cast<uint32_t*>(tile), T, S, SD,
+          K, differs);
+      if constexpr (FLAGS) {
+        if (__ballot(differs) != 0 && (threadIdx.x & 63) == 0) a.flags[pi >> a.piece_shift] = 1;
+      }
+      if constexpr (CRC) {
+        uint32_t c = multmodp(kb, share);
 #pragma unroll
-          for (int o = 32; o > 0; o >>= 1) c ^= (uint32_t)__shfl_xor((int)c, o, 64);
-          if ((threadIdx.x & 63) == 0) atomicXor(a.crc_partials + (pi >> a.piece_shift), c);
-        }
+        for (int o = 32; o > 0; o >>= 1) c ^= (uint32_t)__shfl_xor((int)c, o, 64);
+        if ((threadIdx.x & 63) == 0) atomicXor(a.crc_partials + (pi >> a.piece_shift), c);
       }
     }
     D = Dn;
   }
 }
 
-template <int NT, int VARIANT, bool CRC = false, bool FLAGS = false>
+template <int NT, bool CRC = false, bool FLAGS = false>
 __global__ __launch_bounds__(kBlock) void decode_tiles_kernel(ScatterArgs a) {
-  decode_tiles_body<NT, VARIANT, CRC, FLAGS>(a);
+  decode_tiles_body<NT, CRC, FLAGS>(a);
 }
 
 // encode, grouped tile kernel (write path, uint32, transposed inner chunks): the tile path of
@@ -2241,7 +2186,7 @@ void tiles_rowcrc_aln_kernel(ScatterArgs a) {
 template <int NT, bool FLAGS>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3)))
 void decode_tiles_crc_w3_kernel(ScatterArgs a) {
-  decode_tiles_body<NT, 1, true, FLAGS>(a);
+  decode_tiles_body<NT, true, FLAGS>(a);
 }
 
 // decode, slow kernel: the items the resolve kernel listed (clipped by the region,
@@ -2344,19 +2289,6 @@ __device__ __forceinline__ bool encode_item(const ScatterArgs& a, Item& it,
   }
 }
 
-// encode: the same geometry with source = region and destination = shard payload
-template <int DS, bool TILE>
-__global__ __launch_bounds__(kBlock) void encode_kernel(ScatterArgs a) {
-  using T = typename ElemT<DS>::T;
-  __shared__ T tile[TILE ? kTileTPB : 1][32][33];
-  for (int64_t item = blockIdx.x; item < a.total_items; item += gridDim.x) {
-    Item it;
-    make_item<true>(a, item, it);
-    if (it.mode == kSkip) continue;
-    encode_item<DS, TILE>(a, it, tile);
-  }
-}
-
 // Does this thread's share of the loadable part of an (encode) item differ from fill_value?
 template <int DS>
 __device__ __forceinline__ bool flag_item(const ScatterArgs& a, const Item& it) {
@@ -2383,24 +2315,11 @@ __device__ __forceinline__ bool flag_item(const ScatterArgs& a, const Item& it) 
   return row_pass<DS, false, true>(a, it, F, sstr, sstr, nrows, ext, ediv);
 }
 
-// encode pre-pass: does the loadable part of an inner chunk differ from fill_value?
-// (ShardingIndexedCodec.encode :129-133 / writeChunk M/core/Array.java:150-151)
-template <int DS>
-__global__ __launch_bounds__(kBlock) void flags_kernel(ScatterArgs a) {
-  for (int64_t item = blockIdx.x; item < a.total_items; item += gridDim.x) {
-    Item it;
-    make_item<true>(a, item, it);
-    const bool diff = it.mode == kCopy && flag_item<DS>(a, it);
-    const int any = __syncthreads_or(diff ? 1 : 0);
-    if (threadIdx.x == 0) a.flags[item] = any ? 1 : 0;
-  }
-}
-
 // ---------------------------------------------------------------------------------
 // write path, one pass (zh_array_write fast path): the layout assumes every in-bounds
 // inner chunk is kept, the fast decode kernels run on an "encode view" (source = region,
-// destination = payloads) and record the all-fill test per piece; the host falls back to
-// flags → layout → encode when some chunk turns out to be all fill_value.
+// destination = payloads) and record the all-fill test per piece; when some chunk turns out
+// to be all fill_value, the host runs a second pass with the true layout over those shards.
 // ---------------------------------------------------------------------------------
 // per inner chunk: its payload offset under the one-pass layout (every in-bounds inner chunk
 // kept, C order: the chunk's rank in the shard's in-bounds box × stored chunk bytes, after the
@@ -3201,15 +3120,7 @@ hipError_t launch_resolve(const ScatterArgs& a, hipStream_t stream) {
 }
 
 template <int DS>
-static void launch_scatter_ds(const ScatterArgs& a, int tile, int enc, int grid,
-                              hipStream_t s) {
-  if (enc) {
-    if (tile)
-      hipLaunchKernelGGL((encode_kernel<DS, true>), dim3(grid), dim3(kBlock), 0, s, a);
-    else
-      hipLaunchKernelGGL((encode_kernel<DS, false>), dim3(grid), dim3(kBlock), 0, s, a);
-    return;
-  }
+static void launch_scatter_ds(const ScatterArgs& a, int grid, hipStream_t s) {
   // Every decode fast kernel streams non-temporal loads and stores (host: nt & 3 == 3); the
   // host picks the kernel (tile_variant, row_group, crc_fused, tile_align) and checks the LDS
   // layout each one assumes (check_lds_layouts).
@@ -3217,7 +3128,7 @@ static void launch_scatter_ds(const ScatterArgs& a, int tile, int enc, int grid,
   if (a.fast_mode == kFastTileTable) {
     if constexpr (DS == 4) {
       const int v = a.tile_variant;
-      lds += v == 0 ? (size_t)kFastTPB * 32 * 33 * 4 : (size_t)kTG * kTilePitch * 4;
+      lds += (size_t)kTG * kTilePitch * 4;
       if (v == 51 && a.crc_fused) {  // the row-CRC tile kernel, one chunk per work item
         if (a.tile_align) {  // LDS: tables 12.5 KiB + 9 slots (the host checked the rest)
           const size_t la = kAlnSlotsAt + (size_t)9 * kTilePitch * 4;
@@ -3230,44 +3141,33 @@ static void launch_scatter_ds(const ScatterArgs& a, int tile, int enc, int grid,
         else hipLaunchKernelGGL((tiles_rowcrc_kernel<1, false>), dim3(grid), dim3(kBlock), lc, s, a);
         return;
       }
-      if (v > 20 && !a.crc_fused) {  // G chunks per work item, next step's loads prefetched
-        switch (v - 20) {
-          case 1: hipLaunchKernelGGL((tiles_group_kernel<3, 1, false, true, 0>), dim3(grid), dim3(kBlock), lds, s, a); return;
-          case 2: hipLaunchKernelGGL((tiles_group_kernel<3, 2, false, true, 0>), dim3(grid), dim3(kBlock), lds, s, a); return;
-          case 4: hipLaunchKernelGGL((tiles_group_kernel<3, 4, false, true, 0>), dim3(grid), dim3(kBlock), lds, s, a); return;
-          case 8: hipLaunchKernelGGL((tiles_group_kernel<3, 8, false, true, 0>), dim3(grid), dim3(kBlock), lds, s, a); return;
-          default: return;
-        }
+      if (v == 24 && !a.crc_fused) {  // 4 chunks per work item, next step's loads prefetched
+        hipLaunchKernelGGL((tiles_group_kernel<3, 4, false, true, 0>), dim3(grid), dim3(kBlock), lds, s, a);
+        return;
       }
-      if (v == 1 && a.crc_fused) {
+      if (a.crc_fused) {
         lds += 16 * 256 * 4 + (size_t)a.fast_n * 4;  // T[8][256] + S, SD[4][256] + K[fast_n]
         hipLaunchKernelGGL((decode_tiles_crc_w3_kernel<3, false>), dim3(grid), dim3(kBlock), lds, s, a);
-      } else if (v == 1) {
-        hipLaunchKernelGGL((decode_tiles_kernel<3, 1>), dim3(grid), dim3(kBlock), lds, s, a);
       } else {
-        hipLaunchKernelGGL((decode_tiles_kernel<3, 0>), dim3(grid), dim3(kBlock), lds, s, a);
+        hipLaunchKernelGGL((decode_tiles_kernel<3>), dim3(grid), dim3(kBlock), lds, s, a);
       }
     }
   } else if (a.fast_mode != kFastNone && a.row_group == 8) {  // host: 128-B rows, no CRC
-    if (env_int("ZH_XPOSE_PF", 1) != 0)  // the next step's loads before this step's stores
-      hipLaunchKernelGGL((rows_xpose_kernel<DS, true>), dim3(grid), dim3(kBlock),
-                         lds + 4 * 8 * kXRow * 16, s, a);
-    else
-      hipLaunchKernelGGL((rows_xpose_kernel<DS, false>), dim3(grid), dim3(kBlock),
-                         lds + 4 * 8 * kXRow * 16, s, a);
+    hipLaunchKernelGGL((rows_xpose_kernel<DS>), dim3(grid), dim3(kBlock),
+                       lds + 4 * 8 * kXRow * 16, s, a);
   } else if (a.fast_mode != kFastNone && a.row_group > 0) {  // host: piece_shift 0
     // with the chunk CRC the payload loads go through the cache (NT = 2): a payload after a
     // 4-byte crc32c sits at 4 mod 16 and the line two wave loads share then hits in L2
     // (c3crc reads 1.085× → 1.0016× algorithmic, profiles/r03/c3crc_summary.json)
     const size_t lc = lds + (a.crc_fused ? 12 * 256 * 4 : 0);
+    // host: with the fused chunk CRC G·row = 256 B (G = 1, 2, 4); without it G = 4 for 128-B
+    // rows whose row count is not a multiple of 8 (the lane exchange needs that)
     switch (a.row_group * 2 + (a.crc_fused ? 1 : 0)) {
-      case 2: hipLaunchKernelGGL((rows_group_kernel<DS, 1, 4, 3, false, false>), dim3(grid), dim3(kBlock), lc, s, a); break;
       case 3: hipLaunchKernelGGL((rows_group_kernel<DS, 1, 4, 2, true, false>), dim3(grid), dim3(kBlock), lc, s, a); break;
-      case 4: hipLaunchKernelGGL((rows_group_kernel<DS, 2, 4, 3, false, false>), dim3(grid), dim3(kBlock), lc, s, a); break;
       case 5: hipLaunchKernelGGL((rows_group_kernel<DS, 2, 4, 2, true, false>), dim3(grid), dim3(kBlock), lc, s, a); break;
       case 8: hipLaunchKernelGGL((rows_group_kernel<DS, 4, 4, 3, false, false>), dim3(grid), dim3(kBlock), lc, s, a); break;
       case 9: hipLaunchKernelGGL((rows_group_kernel<DS, 4, 4, 2, true, false>), dim3(grid), dim3(kBlock), lc, s, a); break;
-      default: break;  // host only sets 1, 2, 4
+      default: break;  // no other combination is planned
     }
   } else if (a.fast_mode != kFastNone && a.crc_fused) {
     lds += 12 * 256 * 4;  // slicing tables T[8][256] + zero-shift tables S[4][256]
@@ -3298,18 +3198,16 @@ std::atomic<int64_t> g_last_fast_path{-1};
 // the encode view's fast-path selection of the last write: fast_mode·10⁶ + group·10³ + deep
 std::atomic<int64_t> g_last_encode_path{-1};
 
-hipError_t launch_scatter(const ScatterArgs& a, int dsize, int tile_mode, int encode, int grid,
-                          hipStream_t stream) {
+hipError_t launch_scatter(const ScatterArgs& a, int dsize, int grid, hipStream_t stream) {
   if (a.total_items == 0) return hipSuccess;
-  if (!encode)
-    g_last_fast_path.store((int64_t)a.tile_align * 1000000000 + (int64_t)a.fast_mode * 1000000 +
-                           (int64_t)a.tile_variant * 1000 +
-                           (int64_t)(a.row_group & 0xFF) * 4 + (a.piece_shift ? 1 : 0));
+  g_last_fast_path.store((int64_t)a.tile_align * 1000000000 + (int64_t)a.fast_mode * 1000000 +
+                         (int64_t)a.tile_variant * 1000 +
+                         (int64_t)(a.row_group & 0xFF) * 4 + (a.piece_shift ? 1 : 0));
   switch (dsize) {
-    case 1: launch_scatter_ds<1>(a, tile_mode, encode, grid, stream); break;
-    case 2: launch_scatter_ds<2>(a, tile_mode, encode, grid, stream); break;
-    case 4: launch_scatter_ds<4>(a, tile_mode, encode, grid, stream); break;
-    case 8: launch_scatter_ds<8>(a, tile_mode, encode, grid, stream); break;
+    case 1: launch_scatter_ds<1>(a, grid, stream); break;
+    case 2: launch_scatter_ds<2>(a, grid, stream); break;
+    case 4: launch_scatter_ds<4>(a, grid, stream); break;
+    case 8: launch_scatter_ds<8>(a, grid, stream); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();
@@ -3406,29 +3304,23 @@ static bool launch_encode_fast_ds(const ScatterArgs& v, int grid, int group, hip
     if (group > 0 && v.crc_fused) {  // host: crc_tile_step for 8/G units
       const size_t lc = l + 16 * 256 * 4 + (size_t)v.fast_n * 4 + 64;  // + alignment
       const bool m = v.fill_mask != ~0ull;  // a float ±0 fill: the masked all-fill test
-      switch (group * 2 + (m ? 1 : 0)) {
-        case 2: hipLaunchKernelGGL((tiles_group_kernel<3, 1, true, false, 1>), dim3(grid), dim3(kBlock), lc, s, v); return true;
-        case 3: hipLaunchKernelGGL((tiles_group_kernel<3, 1, true, false, 2>), dim3(grid), dim3(kBlock), lc, s, v); return true;
-        case 4: hipLaunchKernelGGL((tiles_group_kernel<3, 2, true, false, 1>), dim3(grid), dim3(kBlock), lc, s, v); return true;
-        case 5: hipLaunchKernelGGL((tiles_group_kernel<3, 2, true, false, 2>), dim3(grid), dim3(kBlock), lc, s, v); return true;
-        case 8: hipLaunchKernelGGL((tiles_group_kernel<3, 4, true, false, 1>), dim3(grid), dim3(kBlock), lc, s, v); return true;
-        case 9: hipLaunchKernelGGL((tiles_group_kernel<3, 4, true, false, 2>), dim3(grid), dim3(kBlock), lc, s, v); return true;
-        default: return false;
-      }
+      if (group != 2) return false;  // host: 2 chunks per work item
+      if (m)
+        hipLaunchKernelGGL((tiles_group_kernel<3, 2, true, false, 2>), dim3(grid), dim3(kBlock), lc, s, v);
+      else
+        hipLaunchKernelGGL((tiles_group_kernel<3, 2, true, false, 1>), dim3(grid), dim3(kBlock), lc, s, v);
+      return true;
     }
     if (group > 0) {  // host: piece_shift == 0, item_mul
-      switch (group) {
-        case 1: hipLaunchKernelGGL((tiles_group_kernel<3, 1, false, false, 2>), dim3(grid), dim3(kBlock), l, s, v); return true;
-        case 2: hipLaunchKernelGGL((tiles_group_kernel<3, 2, false, false, 2>), dim3(grid), dim3(kBlock), l, s, v); return true;
-        case 4: hipLaunchKernelGGL((tiles_group_kernel<3, 4, false, false, 2>), dim3(grid), dim3(kBlock), l, s, v); return true;
-        default: return false;
-      }
+      if (group != 2) return false;  // host: 2 chunks per work item
+      hipLaunchKernelGGL((tiles_group_kernel<3, 2, false, false, 2>), dim3(grid), dim3(kBlock), l, s, v);
+      return true;
     }
     if (v.crc_fused)  // chunk crc32c of the stored payload: tables + per-unit shifts
       hipLaunchKernelGGL((decode_tiles_crc_w3_kernel<3, true>), dim3(grid), dim3(kBlock),
                          l + 16 * 256 * 4 + (size_t)v.fast_n * 4, s, v);
     else
-      hipLaunchKernelGGL((decode_tiles_kernel<3, 1, false, true>), dim3(grid), dim3(kBlock), l, s, v);
+      hipLaunchKernelGGL((decode_tiles_kernel<3, false, true>), dim3(grid), dim3(kBlock), l, s, v);
     return true;
   }
   return group == 0;
@@ -3484,18 +3376,6 @@ hipError_t launch_encode_finish(const ScatterArgs& a, const EncNest& nz, int64_t
   const int grid = (int)std::min<int64_t>((a.n_citems + kBlock - 1) / kBlock, 8192);
   hipLaunchKernelGGL(encode_finish_kernel, dim3(grid), dim3(kBlock), 0, stream, a, nz,
                      chunk_nbytes, bad, crc_desc);
-  return hipGetLastError();
-}
-
-hipError_t launch_flags(const ScatterArgs& a, int dsize, int grid, hipStream_t stream) {
-  if (a.total_items == 0) return hipSuccess;
-  switch (dsize) {
-    case 1: hipLaunchKernelGGL(flags_kernel<1>, dim3(grid), dim3(kBlock), 0, stream, a); break;
-    case 2: hipLaunchKernelGGL(flags_kernel<2>, dim3(grid), dim3(kBlock), 0, stream, a); break;
-    case 4: hipLaunchKernelGGL(flags_kernel<4>, dim3(grid), dim3(kBlock), 0, stream, a); break;
-    case 8: hipLaunchKernelGGL(flags_kernel<8>, dim3(grid), dim3(kBlock), 0, stream, a); break;
-    default: return hipErrorInvalidValue;
-  }
   return hipGetLastError();
 }
 

@@ -244,7 +244,7 @@ int zh_host_staging(zh_ctx* ctx, size_t bytes, void** out) {
   // freed or replaced under its DMA
   std::lock_guard<std::mutex> lk(ctx->mu);
   (void)hipSetDevice(ctx->device);
-  const size_t cap = (size_t)std::max(64, env_int("ZH_STAGING_MAX_MB", 8192)) << 20;
+  const size_t cap = (size_t)8192 << 20;  // at most 8 GiB of page-locked staging
   const size_t want = std::max<size_t>(bytes, 1);
   if (ctx->staging && (ctx->staging_oneoff || want > ctx->staging_cap)) {
     (void)hipHostFree(ctx->staging);

@@ -18,7 +18,7 @@
 //
 // so both PCIe directions, the host copies and the kernels overlap.  Each slab is planned
 // over only the chunks it touches, and a sub-shard part stages only the ranges it references
-// (zh_engine.cpp caller_pieces / compact_pieces).  At most ZH_PIPE_PLANS (4) slab plans are
+// (zh_engine.cpp caller_pieces / compact_pieces).  At most 4 slab plans are
 // alive, so their device staging cycles through the context's block cache.  Errors: a data
 // error the device finds (a checksum, an index entry) does not stop the read; of all of them
 // the one reported is the first in the oracle's order — the chunk first in C order, then the
@@ -58,11 +58,11 @@ PipeCfg pipe_cfg() {
   // device sources, host output: only the D2H has anything to overlap with, and one plan (its
   // D2H a DMA into pinned memory or the runtime's pageable copy, ~49 GiB/s) measured faster up
   // to 512 MiB (46.6 vs 30.7 GiB/s at 64 MiB, 49.1 vs 43.9 at 512 MiB, profiles/r05/mid/)
-  c.dout_min_bytes = (int64_t)std::max(0, env_int("ZH_PIPE_DOUT_MIN_KB", min_kb * 16)) << 10;
+  c.dout_min_bytes = c.min_bytes * 16;
   c.slab_bytes = (int64_t)std::max(4, env_int("ZH_PIPE_SLAB_KB", 128 << 10)) << 10;
   c.chunk = (int64_t)std::max(64, env_int("ZH_PIPE_CHUNK_KB", 16 << 10)) << 10;
   c.threads = std::min(16, std::max(1, env_int("ZH_PIPE_THREADS", 6)));
-  c.dslots = std::min(8, std::max(2, env_int("ZH_PIPE_DSLOTS", 3)));
+  c.dslots = 3;
   return c;
 }
 
@@ -324,7 +324,7 @@ int read_pipelined(zh_ctx* ctx, const zh_array_meta* meta, const SrcDesc* srcs, 
   // At most `W` slab plans are alive: each holds its device staging, which then comes back
   // from the context's block cache for the next slab and the next call (fresh device memory
   // pays for its first touch: all slabs' staging at once cost ~15 ms per GiB on every call).
-  const int W = std::max(2, std::min(16, env_int("ZH_PIPE_PLANS", 4)));
+  const int W = 4;
   std::vector<zh_plan*> plans((size_t)nslab, nullptr);
   int st = ZH_OK;
   hipError_t he = hipSuccess;
