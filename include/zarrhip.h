@@ -455,6 +455,10 @@ int64_t zh_debug_file_reads(const zh_array_meta* meta, const zh_file_store* stor
                             const char* const* paths, int64_t npaths, const int64_t* offset,
                             const int64_t* shape, int64_t* reads, int64_t cap, char* err,
                             size_t errlen);
+/* Diagnostic (no device needed): the process-wide file table of the file reads —
+ * out[0] = slots in use, out[1] = descriptors open, out[2] = entries in the queue of opens
+ * (bounded: stale entries are dropped as files are given back).  Returns ZH_OK. */
+int zh_debug_file_table(int64_t* out);
 
 /* ShardingIndexedCodec.decode: whole shard → chunk_shape elements. */
 int zh_sharding_decode(zh_ctx* ctx, const zh_array_meta* meta, const void* shard, int64_t nbytes,

@@ -257,3 +257,20 @@ def test_corrupt_index_entries_plan_sane_reads(tmp_path, chain):
         for k, o, nb in reads:
             assert 0 <= k < len(rp) and o >= 0 and nb >= 0, (t, k, o, nb)
             assert o <= 2 ** 63 - 1 - nb and nb <= 2 ** 31 - 1, (t, k, o, nb)
+
+
+def test_file_table_queue_stays_bounded(tmp_path):
+    """the file table's queue of opens drops its stale entries as files are given
+    back, so a long-running process doing many reads of few files keeps it bounded (it grew
+    by one entry per descriptor opened until 64 were open at once)."""
+    import ctypes as C
+    from zarrhip._lib import lib
+    shape = [16, 16]
+    meta = A.make_meta(shape, [8, 8], 4, sharded=True, inner_chunk_shape=[4, 4])
+    arr = rand_array(shape, 4, seed=9)
+    paths = _write(tmp_path, encode_oracle(meta, arr))
+    st = (C.c_int64 * 3)()
+    for _ in range(300):  # each read opens, pins and gives back the 4 shard files
+        assert len(file_reads(meta, paths, [0, 0], shape)) > 0
+        assert lib().zh_debug_file_table(st) == 0
+        assert list(st) == [0, 0, 0]

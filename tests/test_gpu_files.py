@@ -818,3 +818,66 @@ def test_mirror_and_library_store_reads_agree_on_truncated_shards(dev, tmp_path,
             monkeypatch.setenv("ZH_FILES", files)
             got = z.Array.open(z.FilesystemStore(tmp_path).resolve("t")).read(off, shp)
             np.testing.assert_array_equal(got, want, err_msg=f"ZH_FILES={files}")
+
+
+def test_truncated_whole_shard_with_host_codec(dev, tmp_path):
+    """a whole shard with an inner host codec (zstd) whose file was cut short is
+    the file as it is (decodePartial → chunkHandle.read() → ByteBufferDataProvider,
+    ShardingIndexedCodec.java:246-251, 301-331): the entry beyond its bytes is an error — the
+    device's "Could not load byte data for chunk [..]" (DESIGN quirk Q14) — never a
+    zero-padded range decoded on the host.  A part of the same shard still reads its other
+    inner chunks."""
+    import zarrhip as z
+    data = np.arange(16 * 16 * 16, dtype=np.uint32).reshape(16, 16, 16) + 1
+    m = (z.ArrayMetadataBuilder().withShape(16, 16, 16).withDataType(z.DataType.UINT32)
+         .withChunkShape(8, 8, 8).withFillValue(0)
+         .withCodecs(lambda c: c.withSharding([4, 8, 8], lambda c1: c1.withZstd(),
+                                              index_location="start")).build())
+    h = z.FilesystemStore(tmp_path).resolve("a")
+    z.Array.create(h, m).write(None, data)
+    a = z.Array.open(h)
+    p = tmp_path / "a" / "c" / "0" / "0" / "0"
+    assert p.exists()
+    os.truncate(p, os.path.getsize(p) - 3)  # the last inner chunk's zstd frame loses 3 bytes
+    with pytest.raises(z.ZarrException) as e:
+        a.read([0, 0, 0], [8, 8, 8])
+    assert str(e.value).startswith("Could not load byte data for chunk [")
+    np.testing.assert_array_equal(a.read([0, 0, 0], [4, 8, 8]), data[0:4, 0:8, 0:8])
+
+
+def test_write_files_symlink_mode_and_stale_temporaries(dev, tmp_path, wmode):
+    """ADVICE r05 / DESIGN Q15: FilesystemStore.set opens the chunk's path and writes it in place
+    (FilesystemStore.java:116-121); the library writes a temporary file and renames it, and so
+    (a) a chunk path that is a symlink is written through — the link stays, its target gets the
+    bytes; (b) an existing chunk file keeps its permission bits; (c) a temporary file a dead
+    writer left beside a chunk is removed when that chunk is written next (it would otherwise
+    show up in FilesystemStore.list), while one of a live process is left alone."""
+    import subprocess
+    shape = [16, 16, 24]
+    meta = A.make_meta(shape, [8, 16, 24], 4, **WCHAINS["sharded_t"])
+    arr = rand_array(shape, 4, seed=191, fill_frac=0.0)
+    want = encode_oracle(meta, arr)
+    coords = chunk_coords(meta, [0, 0, 0], shape)
+    paths = [str(tmp_path / "s" / "c" / "/".join(map(str, c))) for c in coords]
+    for p in paths:
+        os.makedirs(os.path.dirname(p), exist_ok=True)
+    real = tmp_path / "elsewhere"
+    real.write_bytes(b"old")
+    os.symlink(real, paths[0])                      # (a)
+    with open(paths[1], "wb") as f:                 # (b)
+        f.write(b"old")
+    os.chmod(paths[1], 0o640)
+    dead = subprocess.Popen(["true"])
+    dead.wait()
+    stale = paths[1] + f".zhtmp{dead.pid}.0"        # (c) a dead writer's leftover
+    live = paths[1] + f".zhtmp{os.getppid()}.0"     # a live process's: not ours to remove
+    for q in (stale, live):
+        with open(q, "wb") as f:
+            f.write(b"partial")
+    dev.array_write_files(meta, arr.ctypes.data, [0, 0, 0], shape, paths)
+    assert os.path.islink(paths[0]) and real.read_bytes() == want[0]
+    assert open(paths[1], "rb").read() == want[1]
+    assert (os.stat(paths[1]).st_mode & 0o777) == 0o640
+    assert not os.path.exists(stale) and os.path.exists(live)
+    os.unlink(live)
+    assert not _tmp_leftovers(tmp_path)

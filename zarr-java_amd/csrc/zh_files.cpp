@@ -20,8 +20,12 @@
 // (FilesystemStore.set / delete) here, the encoded bytes D2H'd through the page-locked ring in
 // windows that the copy lanes pwrite into a temporary file per chunk, renamed over the chunk's
 // file once all its bytes are in.
+#include <dirent.h>
 #include <errno.h>
 #include <fcntl.h>
+#include <limits.h>
+#include <signal.h>
+#include <stdlib.h>
 #include <sys/stat.h>
 #include <unistd.h>
 
@@ -142,6 +146,18 @@ void slot_give(int32_t k) {
   }
   e = FileEnt();
   t.free.push_back(k);
+  // the queue of opens keeps an entry per open until close_lru meets it: drop the stale ones
+  // at its front now (all of them once nothing is open), so a long-running process doing
+  // reads of few files keeps it bounded
+  if (t.open == 0) {
+    t.opened.clear();
+  } else {
+    while (!t.opened.empty()) {
+      const FileEnt& f = t.ent[(size_t)t.opened.front()];
+      if (f.live && f.fd >= 0) break;
+      t.opened.pop_front();
+    }
+  }
 }
 
 // Closes the oldest open descriptor nobody is reading (caller holds t.mu): the queue of opens
@@ -453,6 +469,38 @@ int write_all(int fd, const uint8_t* p, int64_t n, int64_t off) {
 
 std::atomic<uint64_t> g_tmp_seq{0};
 
+// Where a chunk's bytes go: the chunk's path, or a symlink's target, so that
+// the rename replaces the file the link names and not the link (FilesystemStore.set writes
+// through it).
+std::string write_target(const std::string& path) {
+  struct stat sb;
+  if (lstat(path.c_str(), &sb) == 0 && S_ISLNK(sb.st_mode)) {
+    char buf[PATH_MAX];
+    if (realpath(path.c_str(), buf)) return buf;
+  }
+  return path;
+}
+
+// Temporary files "<target>.zhtmp<pid>.<n>" left by a writer process that died part-way: a
+// crash would otherwise leave them for FilesystemStore.list to report as keys.  Removed when
+// the next write of the same chunk starts (the name's pid no longer runs).
+void sweep_stale_tmp(const std::string& target) {
+  const size_t slash = target.find_last_of('/');
+  const std::string dir = slash == std::string::npos ? "." : target.substr(0, slash);
+  const std::string pre =
+      (slash == std::string::npos ? target : target.substr(slash + 1)) + ".zhtmp";
+  DIR* d = opendir(dir.c_str());
+  if (!d) return;
+  while (dirent* e = readdir(d)) {
+    const std::string name = e->d_name;
+    if (name.compare(0, pre.size(), pre) != 0) continue;
+    const long pid = strtol(name.c_str() + pre.size(), nullptr, 10);
+    if (pid <= 0 || pid == (long)getpid()) continue;
+    if (kill((pid_t)pid, 0) != 0 && errno == ESRCH) (void)unlink((dir + "/" + name).c_str());
+  }
+  closedir(d);
+}
+
 }  // namespace
 
 extern "C" {
@@ -553,7 +601,7 @@ int zh_array_write_files(zh_ctx* ctx, const zh_array_meta* m, const void* src,
     struct Out {
       std::mutex mu;
       int fd = -1;
-      std::string tmp;
+      std::string tmp, target;  // the temporary file; the file it is renamed over
       int64_t left = 0;
       bool done = false;
     };
@@ -584,13 +632,17 @@ int zh_array_write_files(zh_ctx* ctx, const zh_array_meta* m, const void* src,
       {
         std::lock_guard<std::mutex> g(O.mu);
         if (O.fd < 0) {
-          O.tmp = std::string(paths[J.chunk]) + ".zhtmp" + std::to_string(getpid()) + "." +
+          O.target = write_target(paths[J.chunk]);
+          sweep_stale_tmp(O.target);
+          O.tmp = O.target + ".zhtmp" + std::to_string(getpid()) + "." +
                   std::to_string(g_tmp_seq.fetch_add(1));
           O.fd = open(O.tmp.c_str(), O_WRONLY | O_CREAT | O_TRUNC | O_CLOEXEC, 0666);
           if (O.fd < 0) {
             write_failed(J.chunk, errno);
             return;
           }
+          struct stat old;  // an existing chunk file keeps its permission bits
+          if (stat(O.target.c_str(), &old) == 0) (void)fchmod(O.fd, old.st_mode & 07777);
         }
         fd = O.fd;
       }
@@ -603,7 +655,7 @@ int zh_array_write_files(zh_ctx* ctx, const zh_array_meta* m, const void* src,
       if (--O.left > 0) return;
       const int ce = close(O.fd) != 0 ? errno : 0;
       O.fd = -1;
-      if (ce != 0 || rename(O.tmp.c_str(), paths[J.chunk]) != 0) {
+      if (ce != 0 || rename(O.tmp.c_str(), O.target.c_str()) != 0) {
         write_failed(J.chunk, ce ? ce : errno);
         unlink(O.tmp.c_str());
         return;
@@ -673,6 +725,16 @@ int zh_array_write_files(zh_ctx* ctx, const zh_array_meta* m, const void* src,
     return e == hipErrorOutOfMemory ? ZH_ENOMEM : ZH_EHIP;
   }
   return st;
+}
+
+int zh_debug_file_table(int64_t* out) {
+  if (!out) return ZH_EINVAL;
+  FileTable& t = table();
+  std::lock_guard<std::mutex> lk(t.mu);
+  out[0] = (int64_t)(t.ent.size() - t.free.size());
+  out[1] = t.open;
+  out[2] = (int64_t)t.opened.size();
+  return ZH_OK;
 }
 
 int64_t zh_debug_file_reads(const zh_array_meta* meta, const zh_file_store* store,

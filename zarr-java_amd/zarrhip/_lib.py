@@ -79,6 +79,7 @@ _SIGS = {
                                       P, U32, CH, SZ]),
     "zh_debug_file_reads": (I64, [PMETA, PSTORE, C.POINTER(C.c_char_p), I64, PI64, PI64, PI64,
                                   I64, CH, SZ]),
+    "zh_debug_file_table": (C.c_int, [PI64]),
     "zh_array_write_files": (C.c_int, [P, PMETA, P, PI64, PI64, PSTORE, C.POINTER(C.c_char_p),
                                        I64, U32, PI64, CH, SZ]),
     "zh_array_read_files_multi": (C.c_int, [C.POINTER(P), C.c_int, C.c_int, PMETA, PSTORE,

@@ -283,7 +283,7 @@ class Array:
         pb = b"".join(payload)
         return ib + pb if start else pb + ib
 
-    def _stage_shard(self, h, part_lo, part_hi, lease):
+    def _stage_shard(self, h, part_lo, part_hi, lease, full=False):
         """StoreHandleDataProvider semantics (ShardingIndexedCodec.java:190-230, 333-357): one
         range read for the index, zh_shard_ranges for the inner chunks the part references,
         one store read per range (in parallel, straight into one pooled buffer).  The stored
@@ -291,8 +291,11 @@ class Array:
         here — so a corrupt entry cannot size a host allocation.  Inner host byte-to-byte
         stages (zstd, gzip, blosc) are undone per inner chunk: those pieces hold the raw
         payload.  A range the store cannot deliver is left out (the device then reports the
-        reference's "Could not load byte data for chunk").  Returns a ShardSource plus the
-        buffers it points into, or None for a missing shard."""
+        reference's "Could not load byte data for chunk").  `full`: the part is the whole shard
+        (decodePartial → chunkHandle.read() → ByteBufferDataProvider, :246-251, 301-331), so
+        the shard is the file as it is — an entry beyond its bytes is an error (Q14), not a
+        zero-padded range.  Returns a ShardSource plus the buffers it points into, or None for
+        a missing shard."""
         if not h.exists():
             return None
         isz = _lib.lib().zh_shard_index_size(C.byref(self.zmeta))
@@ -309,7 +312,10 @@ class Array:
         # a FilesystemStore range read past the end of the file returns zeros
         # (FilesystemStore.get(keys, start, end), FilesystemStore.java:84-102): no entry is out
         # of reach by its offset, so the shard size bounds nothing
-        size = -1 if size is None or isinstance(h.store, FilesystemStore) else int(size)
+        if full and size is not None:
+            size = int(size)  # the whole object: sliced, never padded (zh_files.cpp file_sources)
+        else:
+            size = -1 if size is None or isinstance(h.store, FilesystemStore) else int(size)
         ibuf = np.frombuffer(idx if idx else b"\0", np.uint8)
         keep = [ibuf]
         self._count_staged(len(idx))
@@ -329,6 +335,8 @@ class Array:
         pieces = []
         if host:  # per inner chunk: undo the host codecs
             for o, nb in rs:
+                if full and o + nb > size:  # beyond the object: left out, the device reports it
+                    continue
                 blob = h.read(o, o + nb)
                 if blob is None or len(blob) < nb:
                     continue
@@ -369,7 +377,7 @@ class Array:
             full = all(lo == 0 and hi == c for lo, hi, c in
                        zip(part_lo, part_hi, self.metadata.chunk_shape))
             if not full or self.chain.inner_host_bb:  # the index + the referenced ranges
-                st = self._stage_shard(h, part_lo, part_hi, lease)
+                st = self._stage_shard(h, part_lo, part_hi, lease, full)
                 return None if st is None else ("pieces",) + st
         # raw payloads go to the device as they are: parallel reads into one buffer; host
         # byte-to-byte stages take the store's bytes
