@@ -1449,14 +1449,15 @@ def main():
         nel *= s
     out_bytes = nel * 4
 
-    # device buffers: decoded region (also the encode source) + one slab for all shards, plain
-    # hipMalloc allocations (zh_device_malloc), as the library's own reads allocate (ZH_MALLOC
-    # picks another kind for labs)
+    # device buffers: decoded region (also the encode source) + one slab for all shards, the
+    # library's default kind (zh_device_malloc: 1 GiB physical chunks at this size, the highest
+    # floor of the round-6 allocation A/B, DESIGN §4 "Placement"; ZH_MALLOC picks another kind)
     t0 = time.perf_counter()
     offs, tot = slab_layout(caps)
     out = dev.malloc(max(out_bytes, tot))
     shard_slab = dev.malloc(max(out_bytes, tot))
-    alloc_kind = ("hipMalloc" if int(os.environ.get("ZH_MALLOC", "0"), 0) == 0
+    alloc_kind = ("zh_device_malloc's default: 1 GiB physical chunks (ZH_MALLOC_SCATTER) for "
+                  "buffers of 1 GiB or more" if int(os.environ.get("ZH_MALLOC", "0"), 0) == 0
                   else f"zh_device_malloc_ex flags {os.environ['ZH_MALLOC']}")
     dev.synth_fill(out, nel, 4, 0, SEED)
     dev.sync()

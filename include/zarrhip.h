@@ -498,6 +498,12 @@ int zh_array_write_host(zh_ctx* ctx, const zh_array_meta* meta, const void* src_
 /* sizeof of the public structs, for binding-side layout checks (ctypes / JNI mirrors):
  * out[0..3] = zh_codec_chain, zh_array_meta, zh_chunk_src, zh_chunk_dst.  Returns 4. */
 int zh_abi_sizes(int64_t* out, int n);
+/* Device memory for regions and shards, the library's default kind (zh_device_malloc_ex with
+ * flags 0): a buffer of at least 1 GiB is built from 1 GiB physical chunks (ZH_MALLOC_SCATTER,
+ * falling back to hipMalloc), a smaller one is hipMalloc'd.  Round 6 timed the full c4 decode
+ * into 3 fresh outputs of each kind on two boxes (DESIGN.md §4 "Placement"): 1 GiB chunks had
+ * the highest floor on both (2871 / 2869 GiB/s against hipMalloc's 2841 / 2844 and 16 MiB
+ * chunks' 2803 / 2830). */
 int zh_device_malloc(zh_ctx* ctx, size_t bytes, void** out);
 /* Allocation flags for zh_device_malloc_ex.  The write bandwidth a large buffer gets depends
  * on where its physical memory lands (DESIGN.md §4 "Placement": writes only, any access
@@ -520,6 +526,8 @@ int zh_device_malloc(zh_ctx* ctx, size_t bytes, void** out);
  * two arenas while it runs; a candidate that does not fit ends the search.  The buffer's
  * contents are undefined.  zh_device_alloc_probes reports the probes. */
 #define ZH_MALLOC_CALIBRATE 0x8u
+/* hipMalloc whatever the size (the default kind's small-buffer form for every size). */
+#define ZH_MALLOC_PLAIN 0x10u
 int zh_device_malloc_ex(zh_ctx* ctx, size_t bytes, unsigned flags, void** out);
 /* Map a ZH_MALLOC_SCATTER allocation's physical chunks a second time, at a fresh virtual
  * range, in chunk order `order` (0 = the allocation's order: slot i <- chunk (i*m) mod n;

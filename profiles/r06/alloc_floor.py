@@ -35,8 +35,9 @@ L = lib()
 coords = bench.all_coords(L, meta)
 caps = bench.chunk_capacities(meta, coords)
 offs, tot = bench.slab_layout(caps)
-slab = dev.malloc(tot, 0)
-gen = dev.malloc(nb, 0)
+PLAIN = getattr(A, "ZH_MALLOC_PLAIN", 0)  # hipMalloc (flags 0 before round 6's default change)
+slab = dev.malloc(tot, PLAIN)
+gen = dev.malloc(nb, PLAIN)
 dev.synth_fill(gen, nel, 4, 0, bench.SEED)
 sizes = dev.array_write(meta, gen, [0] * n, shape, [(slab + o, c) for o, c in zip(offs, caps)])
 plan = dev.plan(meta, [(slab + o, s) for o, s in zip(offs, sizes)], [0] * n, shape,
@@ -81,10 +82,11 @@ def measure(kind, out, rnd):
 
 measure("hipMalloc(first, gen buffer)", gen, -1)
 dev.free(gen)
-kinds = [("hipMalloc", 0, None), ("vmm1g", A.ZH_MALLOC_SCATTER, "1024"),
+kinds = [("hipMalloc", getattr(A, "ZH_MALLOC_PLAIN", 0), None),
+         ("vmm1g", A.ZH_MALLOC_SCATTER, "1024"),
          ("vmm16m", A.ZH_MALLOC_SCATTER, "16")]
 for r in range(rounds):
-    spacer = dev.malloc(r * 20 * GiB, 0) if r else None
+    spacer = dev.malloc(r * 20 * GiB, PLAIN) if r else None
     for name, flags, mb in kinds:
         if mb:
             os.environ["ZH_SCATTER_MB"] = mb

@@ -129,3 +129,25 @@ def test_calibrated_arena(dev, monkeypatch):
         assert dev.alloc_probes(q) == ([], -1)
     finally:
         dev.free(q)
+
+
+def test_default_kind_by_size(dev):
+    """zh_device_malloc's default kind (flags 0): a buffer of 1 GiB or more is built from 1 GiB
+    physical chunks (a scatter allocation: scatter_view accepts it), a smaller one and
+    ZH_MALLOC_PLAIN are hipMalloc'd (scatter_view refuses them); data round-trips in each."""
+    big = dev.malloc((1 << 30) + 4096, 0)
+    small = dev.malloc(64 << 20, 0)
+    plain = dev.malloc(1 << 30, A.ZH_MALLOC_PLAIN)
+    try:
+        v = dev.scatter_view(big, 0)
+        dev.free(v)
+        for p in (small, plain):
+            with pytest.raises(ZhError):
+                dev.scatter_view(p, 0)
+        for p, nb in ((big, (1 << 30) + 4096), (small, 64 << 20), (plain, 1 << 30)):
+            nel = nb // 4
+            dev.synth_fill(p, nel, 4, 0, 77)
+            assert dev.synth_verify(p, [nel], [0], [nel], 4, 77) == 0
+    finally:
+        for p in (big, small, plain):
+            dev.free(p)

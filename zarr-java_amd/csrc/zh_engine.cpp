@@ -2613,6 +2613,15 @@ static int array_write_fast(zh_ctx* ctx, const zh_array_meta* m, ScatterArgs a,
       !nz.cell) {
     group = 2;
     if (tile_crc) v.crc_tile_step = tile_crc_step(tile_ends, (size_t)(8 / group));
+    // sector-aligned payload stores for c4crc's layout (tiles_group_kernel<…, ALN>): the
+    // payload [32 rows][units][32 words], unit u at 32u words, rows contiguous, ≥ 2 steps of 4
+    // units; the boxes keep 3 workgroups per CU up to 32 units (kAlnUnitsMax)
+    const int64_t nu = v.fast_n;
+    bool al = tile_crc && nu >= 8 && nu % 4 == 0 && nu <= zh::kAlnUnitsMax &&
+              v.rstride[v.fs] == 32 * nu && a.inner_nbytes == 4096 * nu &&
+              (int64_t)tab.size() >= 2 * nu;
+    for (int64_t u = 0; al && u < nu; u++) al = tab[2 * (size_t)u + 1] == (uint32_t)(32 * u);
+    v.tile_align = al ? 1 : 0;
   }
   if (group) v.item_mul = golden_item_mul((items + group - 1) / group);
   const int grid = grid_for(ctx, group ? (items + group - 1) / group : pitems);
@@ -3130,14 +3139,14 @@ int zh_abi_sizes(int64_t* out, int n) {
   return 4;
 }
 int zh_device_malloc(zh_ctx* ctx, size_t bytes, void** out) {
-  if (!ctx || !out) return ZH_EINVAL;
-  (void)hipSetDevice(ctx->device);
-  hipError_t e = hipMalloc(out, bytes);
-  return e == hipSuccess ? ZH_OK : (e == hipErrorOutOfMemory ? ZH_ENOMEM : ZH_EHIP);
+  return zh_device_malloc_ex(ctx, bytes, 0, out);
 }
 int zh_device_malloc_ex(zh_ctx* ctx, size_t bytes, unsigned flags, void** out) {
   if (!ctx || !out) return ZH_EINVAL;
   (void)hipSetDevice(ctx->device);
+  // the default kind: large buffers from 1 GiB physical chunks (the highest floor of the
+  // round-6 allocation A/B, DESIGN §4 "Placement"), hipMalloc below 1 GiB or when that fails
+  if (flags == 0 && bytes >= ((size_t)1 << 30)) flags = ZH_MALLOC_SCATTER;
   hipError_t e = hipErrorOutOfMemory;
   if (flags & ZH_MALLOC_SCATTER) {
     const int st = scatter_malloc(ctx->device, bytes, out);

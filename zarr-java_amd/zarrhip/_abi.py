@@ -22,6 +22,7 @@ ZH_MALLOC_CONTIGUOUS = 0x1
 ZH_MALLOC_REQUIRE = 0x2
 ZH_MALLOC_SCATTER = 0x4
 ZH_MALLOC_CALIBRATE = 0x8
+ZH_MALLOC_PLAIN = 0x10
 ZH_OUT_DEVICE = 0x2
 # zh_array_read_multi_routed per-slab routes (include/zarrhip.h)
 ZH_ROUTE_DIRECT = 0
