@@ -744,7 +744,7 @@ def run_strong(args, dist, A, meta, rank, ws, local):
                          f"({json.dumps(plan_mem)}) > {info['total_mem'] / GiB:.1f} GiB on "
                          f"device {device}; use more ranks")
     log(f"[rank {rank}] memory plan: {need / GiB:.1f} of {info['total_mem'] / GiB:.1f} GiB")
-    # plain device allocations (hipMalloc), as the library's own reads use
+    # zh_device_malloc's default (1 GiB VMM chunks at these sizes), as at N = 1
     src = dev.malloc(nel_cover * 4, 0)
     dev.synth_fill(src, nel_cover, 4, first, SEED)
     slab_buf = dev.malloc(tot, 0)
@@ -777,6 +777,8 @@ def run_strong(args, dist, A, meta, rank, ws, local):
     bad = dev.synth_verify(out, shape, so, ss, 4, SEED)
     if bad:
         raise SystemExit(f"[rank {rank}] slab verification FAILED: {bad} mismatches")
+    # this rank's box: the copy ceiling of its own buffers (shards -> output), as at N = 1
+    ceil = ceiling_probe(dev, out, slab_buf, min(out_bytes, tot))
     plan.set_timing(True)
     dist.barrier()
     dev.sync()
@@ -789,6 +791,12 @@ def run_strong(args, dist, A, meta, rank, ws, local):
     t_dec = dist.max(t_rank)
     dist.barrier()
     roof = roofline_of(plan, st)
+    # each rank's decode against its own copy ceiling (collectives on every rank)
+    own = (roof.get("achieved") or 0.0) / max(ceil["copy_ceiling_GBps"], 1e-9)
+    roof["frac_of_copy_ceiling_min_over_ranks"] = round(-dist.max(-own), 4)
+    roof["frac_of_copy_ceiling_max_over_ranks"] = round(dist.max(own), 4)
+    roof["copy_ceiling_GBps_min_over_ranks"] = round(-dist.max(-ceil["copy_ceiling_GBps"]), 1)
+    roof["copy_ceiling_GBps_max_over_ranks"] = round(dist.max(ceil["copy_ceiling_GBps"]), 1)
     kern_max = dist.max(roof["kernel_ms"])
     if roof.get("kernel_ms"):  # the line's roofline: the slowest rank's kernel time
         roof["kernel_ms_rank0"] = roof["kernel_ms"]
