@@ -906,10 +906,15 @@ def gather_to_root(args, dist, dev, backend, plan, out, out_t, region_t, out_byt
     # gloo (ranks sharing one GPU): a rehearsal through host tensors
     if backend != "nccl":
         world = ws
+        mx = max(sizes)
+        # host memory on this one box: every rank's slab copy plus the root's receive buffers
+        if int(dist.max(0 if _mem_available() >= 2 * ws * mx + (8 << 30) else 1)):
+            return {"backend": backend, "world_size": world,
+                    "skipped": f"gloo rehearsal gather needs {2 * ws * mx / GiB:.0f} GiB of host "
+                               "memory beyond what this box has free (use --ydiv)"}
         host = (C.c_char * out_bytes)()
         dev.memcpy(C.addressof(host), out, out_bytes, 1, None, True)
         send = torch.frombuffer(host, dtype=torch.uint8)
-        mx = max(sizes)
         if out_bytes < mx:
             send = torch.cat([send, torch.zeros(mx - out_bytes, dtype=torch.uint8)])
         recv = [torch.empty(mx, dtype=torch.uint8) for _ in range(ws)] if rank == 0 else None
