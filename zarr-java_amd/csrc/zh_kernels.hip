@@ -3416,6 +3416,14 @@ hipError_t launch_decode_slow(const ScatterArgs& a, int grid, const CrcIdxArgs& 
 // payload stores (3).  Its payloads after each 4-byte crc32c sit at 4 mod 16, so the stores
 // split 32-B sectors; the lab build `make lab_enc_cached` stores through the cache (1), which
 // lets L2 merge them, to measure what the split sectors cost (profiles/r06/enc/).
+// lab builds only (make lab_pad PAD=…, never the product): extra LDS per workgroup of the CRC
+// tile encode, to measure its sensitivity to workgroups per CU (profiles/r06/occ/: padded to 2
+// per CU 47.8 vs 42.2 ms at 3).  Two 4-wave sub-groups per 512-thread workgroup sharing one
+// set of tables (4 waves per SIMD in 2 barrier domains per CU instead of 3 per SIMD in 3) were
+// built and measured slower still: 48.2-49.9 vs 41.7 ms (profiles/r06/occ/, removed).
+#ifndef ZH_LAB_ENC_LDS_PAD
+#define ZH_LAB_ENC_LDS_PAD 0
+#endif
 #ifndef ZH_ENC_CRC_TILE_NT
 #define ZH_ENC_CRC_TILE_NT 3
 #endif
@@ -3472,9 +3480,9 @@ static bool launch_encode_fast_ds(const ScatterArgs& v, int grid, int group, hip
         }
       }
       if (m)
-        hipLaunchKernelGGL((tiles_group_kernel<kNT, 2, true, false, 2>), dim3(grid), dim3(kBlock), lc, s, v);
+        hipLaunchKernelGGL((tiles_group_kernel<kNT, 2, true, false, 2>), dim3(grid), dim3(kBlock), lc + ZH_LAB_ENC_LDS_PAD, s, v);
       else
-        hipLaunchKernelGGL((tiles_group_kernel<kNT, 2, true, false, 1>), dim3(grid), dim3(kBlock), lc, s, v);
+        hipLaunchKernelGGL((tiles_group_kernel<kNT, 2, true, false, 1>), dim3(grid), dim3(kBlock), lc + ZH_LAB_ENC_LDS_PAD, s, v);
       return true;
     }
     if (group > 0) {  // host: piece_shift == 0, item_mul
