@@ -569,12 +569,20 @@ def host_terminated(args, dist, dev, plan, out, out_bytes, shape, so, ss, rank, 
     reps = max(1, min(args.steps, 3))
     ring = 2 << 30
     region = None
+    # this job's region file (SharedHostRegion creates it exclusively): one a killed earlier run
+    # on the same port left behind is removed first, so it neither blocks the name nor holds
+    # the host memory the check below counts
+    name = f"/dev/shm/zh_region_{os.environ.get('MASTER_PORT', 'solo')}_{os.getuid()}"
+    if rank == 0:
+        try:
+            os.unlink(name)
+        except OSError:
+            pass
+    dist.barrier()
     if int(dist.max(0 if _mem_available() >= full + (32 << 30) else 1)) == 0:
         try:
-            region = SharedHostRegion(
-                [0] * len(shape), shape, 4, dev=dev, align=align,
-                name=f"/dev/shm/zh_region_{os.environ.get('MASTER_PORT', 'solo')}_{os.getuid()}")
-        except MemoryError:
+            region = SharedHostRegion([0] * len(shape), shape, 4, dev=dev, align=align, name=name)
+        except (MemoryError, OSError):  # no room, or the file cannot be made: the bounded form
             region = None
     if region is not None:
         assert region.slab_offset == list(so) and region.slab_shape == list(ss)
