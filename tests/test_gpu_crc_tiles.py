@@ -3,8 +3,6 @@
 LDS-tile fast path.  Bit-exact against the oracle (decoded values, mismatch message) across
 piece splits and transpose orders, with an elided inner chunk, a missing shard and a clipped
 region (slow items keep the standalone CRC pass)."""
-import os
-
 import numpy as np
 import pytest
 
@@ -12,9 +10,6 @@ import oracle as O
 from helpers import chunk_coords, device_read, device_write, encode_oracle, rand_array
 from zarrhip import _abi as A
 from zarrhip._lib import ZhError, lib
-
-# 1 when the loaded library is the aligned-store lab build (make lab LAB=1), 0 for the product
-ALN_BUILD = int(os.environ.get("ZH_LIB_PATH", "").endswith("libzarrhip_lab_aln1.so"))
 
 pytestmark = pytest.mark.gpu
 
@@ -176,7 +171,6 @@ def test_row_crc_tile_kernel_many_groups(dev, monkeypatch):
     # the tile encode with the fused chunk CRC (2 chunks per work item) at this size
     assert device_write(dev, meta, arr) == shards
     assert (lib().zh_debug_last_fast_path(1) % 1000000) // 1000 == 2
-    assert lib().zh_debug_last_fast_path(1) // 10 ** 9 == ALN_BUILD
     want = np.frombuffer(O.array_read(meta, shards, [0, 0, 0, 0], shape), np.uint32).reshape(shape)
     got = device_read(dev, meta, shards, [0, 0, 0, 0], shape)  # pipelined (128 MiB host side)
     np.testing.assert_array_equal(got, want)
@@ -400,16 +394,14 @@ def test_index_crc_span_combine(dev, monkeypatch, start):
 
 @pytest.mark.parametrize("loc", [A.ZH_INDEX_END, A.ZH_INDEX_START])
 @pytest.mark.parametrize("elide", [False, True])
-def test_aligned_crc_tile_encode(dev, loc, elide):
+def test_crc_tile_encode_every_word_offset(dev, loc, elide):
     """The chunk-CRC tile encode at every payload word offset: c4crc's payload layout ([32
     rows][32 units][32 words] under transpose [2, 1, 0]) with 9 inner chunks per shard, so the
     payloads after each 4-byte crc32c start at every word offset mod 8 (index at the end; at
     the start the index shifts them again); an elided all-fill chunk sends its shard through
     the second pass with the host's layout.  Every byte of every shard (the buffers are
-    poisoned first) equals the oracle's and the shards decode back.  The product runs the
-    unaligned kernel; the lab build with sector-aligned stores (tiles_group_kernel<…, ALN>,
-    `make lab LAB=1`, loaded by ZH_LIB_PATH) runs the same test and reports the aligned form
-    (round 6: 368 passed with it, profiles/r06/aln/)."""
+    poisoned first) equals the oracle's and the shards decode back (round 6 ran it against the
+    sector-aligned store variant too before removing it, profiles/r06/aln/)."""
     shape = [64, 32 * 9, 32]
     meta = A.make_meta(shape, [32, 32 * 9, 32], 4, endian=A.ZH_ENDIAN_BIG, sharded=True,
                        inner_chunk_shape=[32, 32, 32], transpose_order=[2, 1, 0],
@@ -422,6 +414,6 @@ def test_aligned_crc_tile_encode(dev, loc, elide):
     got = device_write(dev, meta, arr)
     assert [len(g) if g else 0 for g in got] == [len(w) if w else 0 for w in want]
     assert got == want
-    assert lib().zh_debug_last_fast_path(1) // 10 ** 9 == ALN_BUILD
+    assert (lib().zh_debug_last_fast_path(1) % 1000000) // 1000 == 2  # the CRC tile encode
     np.testing.assert_array_equal(
         device_read(dev, meta, got, [0, 0, 0], shape), arr)

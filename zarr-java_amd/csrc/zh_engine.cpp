@@ -2613,15 +2613,6 @@ static int array_write_fast(zh_ctx* ctx, const zh_array_meta* m, ScatterArgs a,
       !nz.cell) {
     group = 2;
     if (tile_crc) v.crc_tile_step = tile_crc_step(tile_ends, (size_t)(8 / group));
-    // sector-aligned payload stores for c4crc's layout (tiles_group_kernel<…, ALN>): the
-    // payload [32 rows][units][32 words], unit u at 32u words, rows contiguous, ≥ 2 steps of 4
-    // units; the boxes keep 3 workgroups per CU up to 32 units (kAlnUnitsMax)
-    const int64_t nu = v.fast_n;
-    bool al = tile_crc && nu >= 8 && nu % 4 == 0 && nu <= zh::kAlnUnitsMax &&
-              v.rstride[v.fs] == 32 * nu && a.inner_nbytes == 4096 * nu &&
-              (int64_t)tab.size() >= 2 * nu;
-    for (int64_t u = 0; al && u < nu; u++) al = tab[2 * (size_t)u + 1] == (uint32_t)(32 * u);
-    v.tile_align = al ? 1 : 0;
   }
   if (group) v.item_mul = golden_item_mul((items + group - 1) / group);
   const int grid = grid_for(ctx, group ? (items + group - 1) / group : pitems);

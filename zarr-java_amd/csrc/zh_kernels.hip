@@ -1638,102 +1638,6 @@ __global__ __launch_bounds__(kBlock) void decode_tiles_kernel(ScatterArgs a) {
   decode_tiles_body<NT, CRC, FLAGS>(a);
 }
 
-// The aligned stores of tiles_group_kernel<…, ALN> for one lane and payload row r of one step
-// (see there).  Chunk q's tiles are slots q·4 … q·4 + 3 of `lds` (pitch kTilePitch, [column][row]
-// with row pitch 33); the boxes follow the 8 tiles.  `dst`: the chunk's payload (its first
-// word at dst); `u0`: the step's first unit's payload offset in words (32·ub); `d_fs`: the
-// payload row pitch in words (32·units).
-constexpr int kAlnEncBox = 2 * 32 * 7;  // words of the head box: [2 chunks][32 rows][7 words]
-// Run words 4i − m … 4i − m + 3 of slot i from the lanes' own vectors y (lane i holds run words
-// 4i … 4i + 3): words of lane i − 1 by a DPP wave shift right by one lane (wave_shr:1), of lane
-// i − 2 by two, no LDS access.  m is uniform per chunk (per 32-lane half); every lane of the half
-// takes part, and slots 0-1 (whose sources lie before the run) are not stored from it.
-__device__ __forceinline__ uint32_t dpp_shr1(uint32_t v) {
-  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x138 /* wave_shr:1 */, 0xF, 0xF,
-                                               false);
-}
-__device__ __forceinline__ uint4 aln_shift(uint4 y, int m) {
-  const uint32_t a[4] = {y.x, y.y, y.z, y.w};
-  uint32_t p1[4], p2[4];
-#pragma unroll
-  for (int c = 0; c < 4; c++) p1[c] = dpp_shr1(a[c]);
-  uint32_t z[4];
-  switch (m) {
-#define ZH_ALN_CASE(M)                                                   \
-  case M:                                                                \
-    _Pragma("unroll") for (int j = 0; j < 4; j++) z[j] = j >= M ? a[j - M] : p1[4 + j - M]; \
-    break;
-    ZH_ALN_CASE(1)
-    ZH_ALN_CASE(2)
-    ZH_ALN_CASE(3)
-    ZH_ALN_CASE(4)
-#undef ZH_ALN_CASE
-#define ZH_ALN_CASE(M)                                                   \
-  case M:                                                                \
-    _Pragma("unroll") for (int c = 0; c < 4; c++) p2[c] = dpp_shr1(p1[c]); \
-    _Pragma("unroll") for (int j = 0; j < 4; j++) z[j] = j >= M - 4 ? p1[j - M + 4] : p2[8 + j - M]; \
-    break;
-    ZH_ALN_CASE(5)
-    ZH_ALN_CASE(6)
-    ZH_ALN_CASE(7)
-#undef ZH_ALN_CASE
-    default:
-      return y;
-  }
-  return make_uint4(z[0], z[1], z[2], z[3]);
-}
-// Slots 0-1 of a misaligned run (m > 0) of row r, after the step's other stores, one lane per
-// (row, slot): the run's first words with the previous step's tail (`tail`: this lane's words
-// 4i … 4i + 3 of it, kept in registers across steps), the head box (LDS, row r's entry at
-// `headb`, row r + 1's at headb + 7) and the sector at the row's end (see tiles_group_kernel).
-// `rs`: the run's first byte.
-template <int NT>
-__device__ __forceinline__ void aln_store_edge(const uint32_t* tq, uint32_t* headb, uint8_t* rs,
-                                               int m, int i, int r, bool first, bool last,
-                                               uint32_t (&tail)[4]) {
-  constexpr bool kNTS = (NT & 2) != 0;
-  auto tw = [&](int w) { return tq[(w >> 5) * kTilePitch + (w & 31) * 33 + r]; };
-  uint8_t* wa = rs - 4 * m + 16 * i;
-  uint32_t z[4];
-#pragma unroll
-  for (int j = 0; j < 4; j++) {
-    const int w = 4 * i + j - m;
-    z[j] = w >= 0 ? tw(w) : tail[j];
-  }
-  if (!first) {
-    st16s<kNTS>(wa, make_uint4(z[0], z[1], z[2], z[3]));
-  } else if (r > 0) {  // the sector is completed by row r − 1's last step
-#pragma unroll
-    for (int j = 0; j < 4; j++)
-      if (4 * i + j - m >= 0) headb[4 * i + j - m] = z[j];
-  } else {  // row 0: the sector holds the previous chunk's crc32c too, word by word
-#pragma unroll
-    for (int j = 0; j < 4; j++)
-      if (4 * i + j - m >= 0) __builtin_nontemporal_store(z[j], (uint32_t*)(wa + 4 * j));
-  }
-  if (!last) {  // this step's last m words, for this lane at the next step
-#pragma unroll
-    for (int j = 0; j < 4; j++)
-      if (4 * i + j < m) tail[j] = tw(128 - m + 4 * i + j);
-    return;
-  }
-  // the sector at the row's end: its last m words + row r + 1's head (row 31: the m words)
-  uint8_t* ea = rs + 512 - 4 * m + 16 * i;
-  uint32_t e[4];
-#pragma unroll
-  for (int j = 0; j < 4; j++) {
-    const int b = 4 * i + j;
-    e[j] = b < m ? tw(128 - m + b) : (r < 31 ? headb[7 + (b - m)] : 0u);  // row r + 1's box
-  }
-  if (r < 31) {
-    st16s<kNTS>(ea, make_uint4(e[0], e[1], e[2], e[3]));
-  } else {
-#pragma unroll
-    for (int j = 0; j < 4; j++)
-      if (4 * i + j < m) __builtin_nontemporal_store(e[j], (uint32_t*)(ea + 4 * j));
-  }
-}
-
 // encode, grouped tile kernel (write path, uint32, transposed inner chunks): the tile path of
 // the encode view reads region rows of 128 B, one per tile (the 8 tiles of a step are
 // x-neighbours, a region row pitch apart), where the decode mirror reads 1 KiB of payload.
@@ -1761,36 +1665,8 @@ __device__ __forceinline__ void aln_store_edge(const uint32_t* tq, uint32_t* hea
 // float ±0 fill); the masked form costs the CRC encode 2 % (42.1 vs 43.0 ms, c4crc,
 // profiles/r05/wab/), so it gets kernels of its own.
 //
-// ALN (lab builds only, ZH_LAB_ALN below; encode with the chunk CRC, G = 2, round 6; host:
-// a.tile_align on the encode view, the payload [32 rows][units][32 words] with units % 4 == 0
-// and ≥ 8): each payload after a 4-byte crc32c starts m = (address / 4) mod 8 words into a 32-B
-// sector, so the 512-B run a chunk's 32 lanes store per row and step split a sector at each
-// end, written twice as partial sectors (PMC writes 1.059× the payload).  Here the lanes store
-// the run's sector-aligned window instead: slot i holds run words 4i − m … 4i − m + 3, taken
-// from the lanes' own vectors by DPP lane shifts (aln_shift; reading them from the LDS tiles
-// measured the same).  Slots 0-1 (the m words before the run belong to the previous step) go
-// after the step's other stores, one lane per (row, slot): the previous step's last m words
-// come from that lane's registers (it saved them there); at the first step the slots keep their
-// run words in the head box (row 0: stored word by word, the sector is shared with the previous
-// chunk's crc32c), and at the last step they store the sector at the row's end: its last m
-// words + the next row's head box (row 31: its m words only, the crc32c follows).  Every
-// payload word is written once, whole sectors but 8 words per chunk
-// (profiles/r06/enc/aln_store_sim.py replays the stores on the host).  The CRC still folds the
-// lanes' own vectors (y), unchanged.  The head box, [2 chunks][32 rows][7 words] after the
-// tiles (1.75 KiB), keeps 3 workgroups per CU.  Measured on c4crc (profiles/r06/aln/): byte-
-// identical, writes 1.024× the payload, but 47.7 ms against the unaligned kernel's 41.9 ms —
-// and 45.6 ms with the slot 0-1 work left out, so the aligned stores alone do not pay: the
-// product keeps the unaligned kernel.
-// ZH_LAB_ALN (compile time; make lab LAB=…, loaded with ZH_LIB_PATH): 0 the product — the
-// unaligned kernel (ALN measured slower, DESIGN §4 "The chunk-CRC encode"); 1 the aligned
-// stores; 2 aligned without the slot 0-1 stores, 3 unshifted stores plus the slot 0-1 work (2
-// and 3 write wrong payloads: timing labs only)
-#ifndef ZH_LAB_ALN
-#define ZH_LAB_ALN 0
-#endif
-template <int NT, int G, bool CRC, bool PF, int FLAGS, bool ALN = false>
+template <int NT, int G, bool CRC, bool PF, int FLAGS>
 __global__ __launch_bounds__(kBlock) void tiles_group_kernel(ScatterArgs a) {
-  static_assert(!ALN || (G == 2 && CRC && FLAGS != 0), "aligned stores: the CRC tile encode");
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   // CRC: the tables first (T, S, SD: a constant LDS position for crc_upd16_k / crc_shift_k),
   // then K, the unit table and the tiles
@@ -1857,10 +1733,6 @@ __global__ __launch_bounds__(kBlock) void tiles_group_kernel(ScatterArgs a) {
       dst = a.region + (int64_t)(((uint64_t)x.w << 32) | x.z) * 4;
     }
     if (__syncthreads_or(on) == 0) continue;  // block-uniform
-    // ALN: this chunk's payload misalignment in words (32-B sectors) and the lane's slot
-    const int am = ALN ? (int)(((uintptr_t)dst >> 2) & 7) : 0;
-    const int ai = ti * 8 + g;
-    uint32_t atail[4] = {0u, 0u, 0u, 0u};  // ALN edge lanes: the previous step's tail words
     bool differs = false;
     uint32_t share = 0, run = 0, ulast = ~0u;
     uint4 x[8];
@@ -1910,16 +1782,7 @@ __global__ __launch_bounds__(kBlock) void tiles_group_kernel(ScatterArgs a) {
           y.y = mine[(g * 4 + 1) * 33 + r];
           y.z = mine[(g * 4 + 2) * 33 + r];
           y.w = mine[(g * 4 + 3) * 33 + r];
-          if constexpr (ALN) {  // slots 2-31 (all slots of an aligned run): the window slot
-            if (ZH_LAB_ALN == 3) {
-              st16s<(NT & 2) != 0>(base + (size_t)r * d_fs * 4, y);
-            } else {
-              const uint4 z = aln_shift(y, am);
-              if (am == 0 || ai >= 2) st16s<(NT & 2) != 0>(base + (size_t)r * d_fs * 4 - 4 * am, z);
-            }
-          } else {
-            st16s<(NT & 2) != 0>(base + (size_t)r * d_fs * 4, y);
-          }
+          st16s<(NT & 2) != 0>(base + (size_t)r * d_fs * 4, y);
           if constexpr (CRC && FLAGS) {  // encode: the stored vectors
             const v4u w = {y.x, y.y, y.z, y.w};
             const uint32_t ck = crc_upd16_k(0u, w, T);
@@ -1940,14 +1803,6 @@ __global__ __launch_bounds__(kBlock) void tiles_group_kernel(ScatterArgs a) {
             ulast = u;
           } else {
             share ^= multmodp(K[u], eacc);
-          }
-        }
-        if constexpr (ALN) {  // slots 0-1 of a misaligned run: one lane per (row, slot)
-          if (am != 0 && ai < 16 && ZH_LAB_ALN != 2) {
-            const int r = wave * 8 + (ai >> 1);
-            aln_store_edge<NT>(lds + q * 4 * kTilePitch, lds + kTG * kTilePitch + (q * 32 + r) * 7,
-                               dst + ((size_t)tab[ub].y + (size_t)r * d_fs) * 4, am, ai & 1, r,
-                               ub == 0, ub + TG >= units, atail);
           }
         }
       }
@@ -3341,8 +3196,7 @@ bool rowcrc_lds_at_zero() {
 
 // the fast-path selection of the last decode scatter launch (diagnostic: zh_debug_last_fast_path)
 std::atomic<int64_t> g_last_fast_path{-1};
-// the encode view's fast-path selection of the last write: tile_align·10⁹ (the sector-aligned
-// CRC tile encode) + fast_mode·10⁶ + group·10³
+// the encode view's fast-path selection of the last write: fast_mode·10⁶ + group·10³
 std::atomic<int64_t> g_last_encode_path{-1};
 
 hipError_t launch_scatter(const ScatterArgs& a, int dsize, int grid, hipStream_t stream) {
@@ -3412,21 +3266,13 @@ hipError_t launch_decode_slow(const ScatterArgs& a, int grid, const CrcIdxArgs& 
 // through the cache: a payload after a 4-byte crc32c sits at 4 mod 16, and L2 merges the line two
 // stores share (c3crc write 41.04 → 39.77 ms, writes 1.079× → 1.007×; the tile encode measured
 // 43.28 → 43.66 ms that way and keeps non-temporal stores).
-// Cache policy of the chunk-CRC tile encode (c4crc write): non-temporal region loads and
-// payload stores (3).  Its payloads after each 4-byte crc32c sit at 4 mod 16, so the stores
-// split 32-B sectors; the lab build `make lab_enc_cached` stores through the cache (1), which
-// lets L2 merge them, to measure what the split sectors cost (profiles/r06/enc/).
-// lab builds only (make lab_pad PAD=…, never the product): extra LDS per workgroup of the CRC
-// tile encode, to measure its sensitivity to workgroups per CU (profiles/r06/occ/: padded to 2
-// per CU 47.8 vs 42.2 ms at 3).  Two 4-wave sub-groups per 512-thread workgroup sharing one
-// set of tables (4 waves per SIMD in 2 barrier domains per CU instead of 3 per SIMD in 3) were
-// built and measured slower still: 48.2-49.9 vs 41.7 ms (profiles/r06/occ/, removed).
-#ifndef ZH_LAB_ENC_LDS_PAD
-#define ZH_LAB_ENC_LDS_PAD 0
-#endif
-#ifndef ZH_ENC_CRC_TILE_NT
-#define ZH_ENC_CRC_TILE_NT 3
-#endif
+// The chunk-CRC tile encode (c4crc write) stores its payloads non-temporally too.  Its
+// payloads after each 4-byte crc32c sit at 4 mod 16 and split 32-B sectors (writes 1.059× the
+// payload); round 6 measured the alternatives on the GPU and removed them (DESIGN §4 "The
+// chunk-CRC encode", profiles/r06/{enc,aln,occ}/; the code is in git history, commit 7ab15c4):
+// stores through the cache (writes 1.089×, 42.6 vs 41.8 ms), sector-aligned stores (writes
+// 1.024×, 47.7 ms), 2 workgroups per CU (47.8 vs 42.2 ms at 3) and two sub-groups per workgroup
+// sharing one table set (48.2–49.9 vs 41.7 ms).
 
 template <int DS>
 static bool launch_encode_fast_ds(const ScatterArgs& v, int grid, int group, hipStream_t s) {
@@ -3468,21 +3314,10 @@ static bool launch_encode_fast_ds(const ScatterArgs& v, int grid, int group, hip
       const size_t lc = l + 16 * 256 * 4 + (size_t)v.fast_n * 4 + 64;  // + alignment
       const bool m = v.fill_mask != ~0ull;  // a float ±0 fill: the masked all-fill test
       if (group != 2) return false;  // host: 2 chunks per work item
-      constexpr int kNT = ZH_ENC_CRC_TILE_NT;
-      if constexpr (ZH_LAB_ALN != 0) {  // lab: sector-aligned payload stores (host: c4crc)
-        if (v.tile_align) {
-          const size_t la = lc + kAlnEncBox * 4;  // + the head box
-          if (m)
-            hipLaunchKernelGGL((tiles_group_kernel<kNT, 2, true, false, 2, true>), dim3(grid), dim3(kBlock), la, s, v);
-          else
-            hipLaunchKernelGGL((tiles_group_kernel<kNT, 2, true, false, 1, true>), dim3(grid), dim3(kBlock), la, s, v);
-          return true;
-        }
-      }
       if (m)
-        hipLaunchKernelGGL((tiles_group_kernel<kNT, 2, true, false, 2>), dim3(grid), dim3(kBlock), lc + ZH_LAB_ENC_LDS_PAD, s, v);
+        hipLaunchKernelGGL((tiles_group_kernel<3, 2, true, false, 2>), dim3(grid), dim3(kBlock), lc, s, v);
       else
-        hipLaunchKernelGGL((tiles_group_kernel<kNT, 2, true, false, 1>), dim3(grid), dim3(kBlock), lc + ZH_LAB_ENC_LDS_PAD, s, v);
+        hipLaunchKernelGGL((tiles_group_kernel<3, 2, true, false, 1>), dim3(grid), dim3(kBlock), lc, s, v);
       return true;
     }
     if (group > 0) {  // host: piece_shift == 0, item_mul
@@ -3502,8 +3337,7 @@ static bool launch_encode_fast_ds(const ScatterArgs& v, int grid, int group, hip
 
 hipError_t launch_encode_fast(const ScatterArgs& view, int grid, int group, hipStream_t stream) {
   if (view.total_items == 0 || view.fast_mode == kFastNone) return hipSuccess;
-  g_last_encode_path.store((int64_t)(view.tile_align && ZH_LAB_ALN != 0) * 1000000000 +
-                           (int64_t)view.fast_mode * 1000000 + (int64_t)group * 1000);
+  g_last_encode_path.store((int64_t)view.fast_mode * 1000000 + (int64_t)group * 1000);
   bool ok = false;
   switch (view.dsize) {
     case 1: ok = launch_encode_fast_ds<1>(view, grid, group, stream); break;
