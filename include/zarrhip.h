@@ -262,7 +262,6 @@ int zh_array_read_multi(zh_ctx* const* ctxs, int ndev, int root, const zh_array_
  *   sources (ZH_SRC_DEVICE chunks on another device than the slab's), OR-ed in:
  *           ZH_ROUTE_SRC_PEER    the kernels read them over xGMI (peer access on)
  *           ZH_ROUTE_SRC_STAGED  copied to the slab's device first (no peer access)
- *   ZH_MULTI_PEER=0 in the environment disables peer access (forces the staged routes);
  *   ZH_MULTI_FORCE_STAGED=1 stages every non-root slab even on one device (tests).
  */
 #define ZH_ROUTE_DIRECT 0

@@ -56,7 +56,7 @@ struct zh_ctx {
   // created, run and freed while mu is held (read_region, read_multi_impl)
   uint8_t* file_pin = nullptr;
   size_t file_pin_cap = 0;
-  // page-locked landing buffer of a small one-plan read into pageable host memory (ZH_HOUT_PIN):
+  // page-locked landing buffer of a small one-plan read into pageable host memory:
   // the D2H goes here as a DMA and one memcpy moves it out; used under mu, created on first use
   uint8_t* hout_pin = nullptr;
   bool hout_pin_failed = false;

@@ -1261,7 +1261,9 @@ __device__ __forceinline__ uint32_t crc_shift_k(uint32_t c, const uint32_t (*S)[
 // shifted to the payload end by x^(8·16·(Lc − 1 − j)); the chunk's lanes XOR their shares
 // (CRC is linear over GF(2)) into its partial, one atomic per wave.
 //
-// FLAGS = false: the decode direction (payload rows → region rows; ZH_DEC_RGROUP): full-fill
+// FLAGS = false: the decode direction (payload rows → region rows; the planner's groups: with
+// the fused chunk CRC by row length, without it 128-B rows whose row count is not a multiple
+// of 8, rows_xpose_kernel taking the rest): full-fill
 // items store their fill value, the CRC runs over the loaded payload vectors.
 template <int DS, int G, int U, int NT, bool CRC, bool FLAGS>
 __global__ __launch_bounds__(kBlock) void rows_group_kernel(ScatterArgs a) {
@@ -1648,7 +1650,7 @@ __global__ __launch_bounds__(kBlock) void decode_tiles_kernel(ScatterArgs a) {
 // lanes and stay on the slow list).  No CRC, piece_shift == 0 (host-checked).
 //
 // FLAGS = false: the decode direction (payload → region; every fast tile item is a full copy),
-// ZH_DEC_TGROUP.  CRC: the chunk crc32c of the payload (encode: the stored vectors, which
+// the decode's tile groups (G = 4).  CRC: the chunk crc32c of the payload (encode: the stored vectors, which
 // have the decode loads' geometry; decode: the loaded ones), fused as in fast_tiles_rows: a
 // lane's 8 vectors
 // fold with S, its units (u, u + 8/G, …) with SD = x^(8Δ) for that unit stride (host:
@@ -1999,7 +2001,7 @@ static_assert(kAlnSDnAt % 16 == 0 && kAlnSlotsAt % 16 == 0, "aligned row-CRC LDS
 static_assert(kAlnSlotsAt + 9 * kTilePitch * 4 <= 160 * 1024 / 3,
               "aligned row-CRC LDS: 3 workgroups per CU (160 KiB)");
 
-// decode, the row-CRC tile kernel over 128-B aligned lines (ZH_DEC_ALIGN; host: a.tile_align,
+// decode, the row-CRC tile kernel over 128-B aligned lines (the default; host: a.tile_align,
 // one chunk per work item, 16 ≤ fast_n ≤ 32 units, fast_n % 8 == 0, tab[u] = (32u, u·ystride)).
 // The payload is then [32 rows][fast_n units][32 words]: step s of row r is the contiguous 1 KiB
 // L(r, s) at 4096r·(fast_n/32) + 1024s.  A payload after a 4-byte crc32c starts δ = 4i mod 128
