@@ -500,9 +500,9 @@ int zh_abi_sizes(int64_t* out, int n);
 /* Device memory for regions and shards, the library's default kind (zh_device_malloc_ex with
  * flags 0): a buffer of at least 1 GiB is built from 1 GiB physical chunks (ZH_MALLOC_SCATTER,
  * falling back to hipMalloc), a smaller one is hipMalloc'd.  Round 6 timed the full c4 decode
- * into 3 fresh outputs of each kind on two boxes (DESIGN.md §4 "Placement"): 1 GiB chunks had
- * the highest floor on both (2871 / 2869 GiB/s against hipMalloc's 2841 / 2844 and 16 MiB
- * chunks' 2803 / 2830). */
+ * into 3 fresh outputs of each kind on three boxes (DESIGN.md §4 "Placement"): 1 GiB chunks had
+ * the highest floor on each (2871 / 2869 / 2927 GiB/s against hipMalloc's 2841 / 2844 / 2913
+ * and 16 MiB chunks' 2803 / 2830 / 2900). */
 int zh_device_malloc(zh_ctx* ctx, size_t bytes, void** out);
 /* Allocation flags for zh_device_malloc_ex.  The write bandwidth a large buffer gets depends
  * on where its physical memory lands (DESIGN.md §4 "Placement": writes only, any access
