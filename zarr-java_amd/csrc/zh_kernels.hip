@@ -1747,13 +1747,41 @@ __global__ __launch_bounds__(kBlock) void tiles_group_kernel(ScatterArgs a) {
           x[k] = ld16s<(NT & 1) != 0>(base + (size_t)(wave * 8 + k) * s_fd * 4);
       }
     };
+    // DEFER (encode CRC): step s's stored vectors stay in registers (yp) and fold into the CRC
+    // after step s + 1 has issued its loads, so the lookups run under the load latency (c4crc
+    // encode 41.80–42.04 → 41.51–41.58 ms, profiles/r06/defer/; the same deferral in the grouped
+    // row kernels cost them 2 waves per SIMD of registers and measured 13 % slower)
+    constexpr bool DEFER = CRC && FLAGS && !PF;
+    uint4 yp[8];
+    bool lp = false;
+    uint32_t up = 0;
+    auto fold = [&]() {
+      if constexpr (DEFER) {
+        if (lp) {
+          uint32_t eacc = 0;
+#pragma unroll
+          for (int k = 0; k < 8; k++) {
+            const v4u w = {yp[k].x, yp[k].y, yp[k].z, yp[k].w};
+            const uint32_t ck = crc_upd16_k(0u, w, T);
+            eacc = k ? crc_shift_k(eacc, S) ^ ck : ck;
+          }
+          if (regular) {
+            run = (ulast != ~0u ? crc_shift_k(run, SD) : 0u) ^ eacc;
+            ulast = up;
+          } else {
+            share ^= multmodp(K[up], eacc);
+          }
+        }
+      }
+    };
     if (PF) load(0);
 #pragma unroll 1
     for (uint32_t ub = 0; ub < units; ub += TG) {
       const uint32_t u = ub + ti;
       const bool live = on && u < units;
+      if (live && !PF) load(ub);  // inside the live branch: 46.3 → 42.3 ms on the c4crc encode
+      fold();                     // DEFER: the previous step's CRC, under these loads
       if (live) {
-        if (!PF) load(ub);  // inside the live branch: 46.3 → 42.3 ms on the c4crc encode
 #pragma unroll
         for (int k = 0; k < 8; k++) {
           if constexpr (FLAGS == 2) differs |= ne4x4(x[k], f, fm);
@@ -1785,7 +1813,9 @@ __global__ __launch_bounds__(kBlock) void tiles_group_kernel(ScatterArgs a) {
           y.z = mine[(g * 4 + 2) * 33 + r];
           y.w = mine[(g * 4 + 3) * 33 + r];
           st16s<(NT & 2) != 0>(base + (size_t)r * d_fs * 4, y);
-          if constexpr (CRC && FLAGS) {  // encode: the stored vectors
+          if constexpr (DEFER) {
+            yp[k] = y;
+          } else if constexpr (CRC && FLAGS) {  // encode: the stored vectors
             const v4u w = {y.x, y.y, y.z, y.w};
             const uint32_t ck = crc_upd16_k(0u, w, T);
             eacc = k ? crc_shift_k(eacc, S) ^ ck : ck;
@@ -1799,7 +1829,7 @@ __global__ __launch_bounds__(kBlock) void tiles_group_kernel(ScatterArgs a) {
             eacc = k ? crc_shift_k(eacc, S) ^ ck : ck;
           }
         }
-        if constexpr (CRC) {
+        if constexpr (CRC && !DEFER) {
           if (regular) {
             run = (ulast != ~0u ? crc_shift_k(run, SD) : 0u) ^ eacc;
             ulast = u;
@@ -1808,8 +1838,11 @@ __global__ __launch_bounds__(kBlock) void tiles_group_kernel(ScatterArgs a) {
           }
         }
       }
+      lp = live;
+      up = u;
       __syncthreads();
     }
+    fold();  // DEFER: the last step's CRC
     if (FLAGS && (__ballot(differs) & qmask) != 0 && leader && on) a.flags[c] = 1;
     if constexpr (CRC) {
       uint32_t cr = regular ? (ulast != ~0u ? multmodp(kq, run) : 0u) : multmodp(kb, share);
