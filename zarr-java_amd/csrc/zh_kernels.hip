@@ -1749,8 +1749,9 @@ __global__ __launch_bounds__(kBlock) void tiles_group_kernel(ScatterArgs a) {
     };
     // DEFER (encode CRC): step s's stored vectors stay in registers (yp) and fold into the CRC
     // after step s + 1 has issued its loads, so the lookups run under the load latency (c4crc
-    // encode 41.80–42.04 → 41.51–41.58 ms, profiles/r06/defer/; the same deferral in the grouped
-    // row kernels cost them 2 waves per SIMD of registers and measured 13 % slower)
+    // encode 41.87–41.93 → 41.54–41.84 ms in this form, 41.80–42.04 → 41.51–41.58 with the load
+    // outside the live branch, profiles/r06/defer/; the same deferral in the grouped row kernels
+    // cost them 2 waves per SIMD of registers and measured 13 % slower)
     constexpr bool DEFER = CRC && FLAGS && !PF;
     uint4 yp[8];
     bool lp = false;
@@ -1779,9 +1780,10 @@ __global__ __launch_bounds__(kBlock) void tiles_group_kernel(ScatterArgs a) {
     for (uint32_t ub = 0; ub < units; ub += TG) {
       const uint32_t u = ub + ti;
       const bool live = on && u < units;
-      if (live && !PF) load(ub);  // inside the live branch: 46.3 → 42.3 ms on the c4crc encode
-      fold();                     // DEFER: the previous step's CRC, under these loads
+      if (!live) fold();  // DEFER: the previous step's CRC (no loads to hide it under)
       if (live) {
+        if (!PF) load(ub);  // inside the live branch: 46.3 → 42.3 ms on the c4crc encode
+        fold();             // DEFER: the previous step's CRC, under these loads
 #pragma unroll
         for (int k = 0; k < 8; k++) {
           if constexpr (FLAGS == 2) differs |= ne4x4(x[k], f, fm);
